@@ -1,0 +1,81 @@
+/*
+ * openr_decision.h — C ABI of libopenr_decision, the host-side mirror of
+ * OpenR's LinkState (openr/decision/LinkState.{h,cpp}) whose SPF runs on the
+ * MI355X engine (include/openr_spf.h).
+ *
+ * The C++ class (openr_amd/csrc/decision/link_state.h, namespace odl) keeps
+ * the reference's public surface and semantics:
+ *   updateAdjacencyDatabase  LinkState.cpp:584-726 -> odl_apply
+ *   deleteAdjacencyDatabase  LinkState.cpp:728-746 -> odl_apply (db_delete=1)
+ *   linksFromNode            LinkState.cpp:477-485 -> odl_links_text
+ *   isNodeOverloaded         LinkState.cpp:515-518 -> odl_is_overloaded
+ *   getSpfResult             LinkState.cpp:821-831 -> odl_spf_text
+ *   getKthPaths              LinkState.cpp:790-819 -> odl_kth_paths_text
+ *   getMetricFromAToB        LinkState.cpp:777-788 -> odl_metric_a_to_b
+ *   decision.spf_runs        LinkState.cpp:843     -> odl_spf_runs
+ * plus batched entry points the reference lacks (all-sources digests, KSP2
+ * masked reruns for many destinations, per-neighbour reruns).
+ *
+ * This ABI exists for tests, benches and non-C++ callers; a C++ Decision
+ * module links the class directly. Text results use the format documented
+ * in DESIGN.md §Result text (same as the oracle's). Returned strings are
+ * malloc'd; free them with odl_free(). NULL / negative return = error, see
+ * odl_last_error().
+ */
+#ifndef OPENR_DECISION_H
+#define OPENR_DECISION_H
+
+#include <stdint.h>
+
+#include "openr_adjdb.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct odl_ls odl_ls;
+
+/* New LinkState for `area` whose SPF engine runs on HIP device `device`. */
+int odl_create(const char* area, int device, odl_ls** out);
+void odl_destroy(odl_ls* ls);
+const char* odl_last_error(const odl_ls* ls);
+void odl_free(char* p);
+
+/* Apply stream records [first, first+count) in order; changes[count] out. */
+int odl_apply(odl_ls* ls, const oadj_stream* s, uint32_t first, uint32_t count,
+              oadj_change* changes);
+
+char* odl_spf_text(odl_ls* ls, const char* root, int use_link_metric);
+char* odl_kth_paths_text(odl_ls* ls, const char* src, const char* dst, int k);
+char* odl_links_text(odl_ls* ls, const char* node);
+int64_t odl_metric_a_to_b(odl_ls* ls, const char* a, const char* b, int use_link_metric);
+int odl_is_overloaded(odl_ls* ls, const char* node);
+uint64_t odl_spf_runs(const odl_ls* ls);
+uint32_t odl_num_nodes(const odl_ls* ls);
+uint32_t odl_num_links(const odl_ls* ls);
+
+/* Batched runs. roots / dsts are '\n'-separated node names.
+ * odl_spf_digests: one engine batch, out[3*i] = {reached, sum_dist, hash}. */
+int odl_spf_digests(odl_ls* ls, const char* roots_nl, uint32_t n, int use_link_metric,
+                    uint64_t* out);
+/* Fill the getSpfResult memo for many roots with one engine batch. */
+int odl_spf_prefetch(odl_ls* ls, const char* roots_nl, uint32_t n, int use_link_metric);
+/* getKthPaths(src, d, 2) for every d, masked reruns batched on the engine;
+ * text = paths of each d, then a line "=". */
+char* odl_ksp2_text(odl_ls* ls, const char* src, const char* dsts_nl, uint32_t n);
+
+/* CSR snapshot the engine sees (node ids = rank of name, byte order).
+ * Copies into caller arrays sized by odl_csr_size(); any pointer may be NULL. */
+int odl_csr_size(odl_ls* ls, uint32_t* n_nodes, uint32_t* n_edges);
+int odl_csr_export(odl_ls* ls, uint32_t* row_ptr, uint32_t* col, uint32_t* metric,
+                   uint32_t* link_id, uint32_t* twin, uint8_t* edge_up, uint8_t* no_transit,
+                   uint32_t* link_rank);
+/* Node name of id (pointer valid until the next apply). */
+const char* odl_node_name(odl_ls* ls, uint32_t id);
+int64_t odl_node_id(odl_ls* ls, const char* name);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OPENR_DECISION_H */

@@ -1,0 +1,163 @@
+/*
+ * openr_spf.h — C ABI of libopenr_spf_hip, the MI355X batched SPF engine.
+ *
+ * Drop-in boundary for OpenR's Decision SPF hot path. The reference has no
+ * FFI or plugin hook for SPF (openr/plugin/Plugin.h:19-42 is queue-level), so
+ * the surface this ABI replaces is the body of one private C++ method:
+ *
+ *   LinkState::runSpf(src, useLinkMetric, linksToIgnore)
+ *                                  openr/decision/LinkState.cpp:836-911
+ *                                  (declared openr/decision/LinkState.h:518-525)
+ *
+ * batched over many roots, plus the graph those calls read
+ * (linkMap_/allLinks_/nodeOverloads_, LinkState.h:538-549). The C++ caller (our
+ * LinkState mirror, include/openr_decision.h, or the reference's own LinkState
+ * after the patch in INTEGRATION.md) keeps the memo, SpfResult reconstruction
+ * and route building; this library only computes, per root:
+ *   dist[v]   u32, LinkState metric (UINT32_MAX = not reached)
+ *   nh[v][w]  next-hop set of v as a bitset over the root's distinct
+ *             neighbours in ascending node-id order (bit i = i-th neighbour)
+ *   digest    {reached, sum dist, 64-bit hash} (definition: DESIGN.md §Digest)
+ *
+ * Semantics = the reference's runSpf: edges usable iff
+ * Link::isUp (LinkState.cpp:242-245) and not ignored; weight = metric
+ * advertised by the relaxing node (Link::getMetricFromNode, LinkState.cpp:193)
+ * or 1 in hop-count mode; overloaded nodes other than the root never relax
+ * (LinkState.cpp:859-866); nextHops(v) = union over tight transit predecessors
+ * u of (u == root ? {v} : nextHops(u)) (LinkState.cpp:885-901).
+ *
+ * Conventions: every function returns OSPF_OK (0) or a negative OSPF_E_*
+ * code; nothing throws or aborts across the ABI; ospf_last_error() explains
+ * the last failure. One context per LinkState (area); a context is not
+ * thread-safe (the reference calls SPF from the single Decision thread,
+ * openr/Main.cpp:515-527). Out-of-contract inputs (metric 0, possible u32
+ * distance overflow, > OSPF_MAX_ROOT_NEIGHBORS distinct root neighbours)
+ * return OSPF_E_RANGE; there is no CPU fallback.
+ */
+#ifndef OPENR_SPF_H
+#define OPENR_SPF_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OSPF_OK 0
+#define OSPF_E_INVAL (-1)   /* bad argument */
+#define OSPF_E_NOGRAPH (-2) /* no graph loaded */
+#define OSPF_E_DEVICE (-3)  /* HIP runtime / device error */
+#define OSPF_E_RANGE (-4)   /* input outside the engine's contract */
+#define OSPF_E_NOMEM (-5)   /* device allocation failed */
+
+#define OSPF_DIST_INF 0xFFFFFFFFu
+#define OSPF_MAX_ROOT_NEIGHBORS 8192u /* nh words <= 256 */
+#define OSPF_MAX_IGNORED_PER_RUN 2048u
+
+/* flags for ospf_sssp_batch* */
+#define OSPF_HOP_COUNT 0x1u   /* useLinkMetric = false (LinkState.cpp:878) */
+#define OSPF_WANT_DIST 0x2u
+#define OSPF_WANT_NH 0x4u
+#define OSPF_WANT_DIGEST 0x8u
+
+typedef struct ospf_ctx ospf_ctx;
+
+/* Link-state graph snapshot in CSR form (caller-owned, copied on load).
+ * Node ids are 0..n_nodes-1; each row lists the directed edges u->col[e] of
+ * node u sorted by col ascending (parallel links adjacent). Every undirected
+ * link appears twice (once per endpoint); twin[e] is the other entry. */
+typedef struct ospf_csr {
+  uint32_t n_nodes;
+  uint32_t n_edges;            /* directed entries = 2 x links */
+  const uint32_t* row_ptr;     /* [n_nodes + 1] */
+  const uint32_t* col;         /* [n_edges] neighbour id */
+  const uint32_t* metric;      /* [n_edges] metric advertised by the row node, >= 1 */
+  const uint32_t* link_id;     /* [n_edges] undirected link id (same for twins) */
+  const uint32_t* twin;        /* [n_edges] index of the reverse entry */
+  const uint8_t* edge_up;      /* [n_edges] Link::isUp() */
+  const uint8_t* no_transit;   /* [n_nodes] LinkState::isNodeOverloaded() */
+} ospf_csr;
+
+/* Per-run ignored links (LinkState::runSpf linksToIgnore). Run i ignores
+ * link_ids[offsets[i] .. offsets[i+1]) (sorted ascending). */
+typedef struct ospf_ignore {
+  const uint32_t* offsets;  /* [n_roots + 1] */
+  const uint32_t* link_ids;
+} ospf_ignore;
+
+typedef struct ospf_digest {
+  uint64_t reached;
+  uint64_t sum_dist;
+  uint64_t hash;
+} ospf_digest;
+
+typedef struct ospf_graph_info {
+  uint32_t n_nodes;
+  uint32_t n_edges;
+  uint32_t n_links;
+  uint32_t max_degree;
+  uint32_t max_metric;
+  uint32_t unit_metric;        /* every usable edge has metric 1 */
+  uint64_t version;
+  uint64_t device_bytes;       /* resident graph bytes on the device */
+} ospf_graph_info;
+
+/* Open a context on HIP device `device` (ordinal). */
+int ospf_open(int device, ospf_ctx** out);
+int ospf_close(ospf_ctx* ctx);
+const char* ospf_last_error(const ospf_ctx* ctx);
+
+/* Upload (replace) the graph. `version` is the caller's topology version;
+ * it is echoed by ospf_graph_info. */
+int ospf_load_graph(ospf_ctx* ctx, const ospf_csr* csr, uint64_t version);
+int ospf_graph_info_get(const ospf_ctx* ctx, ospf_graph_info* info);
+
+/* Distinct neighbours of `root` in ascending id order = the nh bit order.
+ * Writes min(n, cap) ids; *n = total. nh words for root = ceil(n / 32). */
+int ospf_root_neighbors(const ospf_ctx* ctx, uint32_t root, uint32_t* ids,
+                        uint32_t cap, uint32_t* n);
+
+/* Batched SPF, host buffers, synchronous.
+ *   roots[n_roots]; ignore may be NULL (no run ignores anything);
+ *   dist_out: [n_roots][n_nodes] when OSPF_WANT_DIST;
+ *   nh_out:   [n_roots][n_nodes][nh_words] when OSPF_WANT_NH; nh_words must be
+ *             >= ceil(distinct neighbours / 32) of every root in the batch;
+ *   digest_out: [n_roots] when OSPF_WANT_DIGEST. */
+int ospf_sssp_batch(ospf_ctx* ctx, const uint32_t* roots, uint32_t n_roots,
+                    const ospf_ignore* ignore, uint32_t flags, uint32_t nh_words,
+                    uint32_t* dist_out, uint32_t* nh_out, ospf_digest* digest_out);
+
+/* Same, device-resident: every pointer is device memory, the work is queued
+ * on `stream` (hipStream_t, NULL = default stream) and NOT synchronised.
+ * d_dist / d_nh may be NULL when not wanted (the engine then uses its own
+ * scratch). d_ign_offsets / d_ign_ids may be NULL; otherwise max_ignored
+ * bounds every run's ignore-list length. A run whose root has more than
+ * 32 * nh_words distinct neighbours, or whose ignore list exceeds
+ * max_ignored, raises the context's device error word: check it with
+ * ospf_sync(). */
+int ospf_sssp_batch_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n_roots,
+                        const uint32_t* d_ign_offsets, const uint32_t* d_ign_ids,
+                        uint32_t max_ignored, uint32_t flags, uint32_t nh_words,
+                        uint32_t* d_dist, uint32_t* d_nh, ospf_digest* d_digest,
+                        void* stream);
+
+/* Wait for `stream`, then report (and clear) the device error word:
+ * OSPF_OK or OSPF_E_RANGE. */
+int ospf_sync(ospf_ctx* ctx, void* stream);
+
+/* Kernel variant the engine would use for a batch (for reporting):
+ * 0 = LDS-resident (dist+nh in LDS), 1 = LDS dist + HBM next-hops,
+ * 2 = HBM frontier (dist+nh in HBM). */
+int ospf_plan_variant(const ospf_ctx* ctx, uint32_t flags, uint32_t nh_words,
+                      int* variant);
+
+/* Runtime statistics. spf_runs counts logical runSpf executions (one per
+ * root per batch), matching the reference's decision.spf_runs counter
+ * (LinkState.cpp:843). */
+uint64_t ospf_spf_runs(const ospf_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OPENR_SPF_H */

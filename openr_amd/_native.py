@@ -1,0 +1,127 @@
+"""ctypes bindings for the in-tree native libraries.
+
+Loading fails loudly (ImportError) when a library is missing: there is no
+Python or CPU fallback for the SPF path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from .build import DECISION_SO, ENGINE_SO
+
+vp, cp, u32, i32, u64, i64 = C.c_void_p, C.c_char_p, C.c_uint32, C.c_int, C.c_uint64, C.c_int64
+
+OSPF_OK = 0
+OSPF_E_INVAL = -1
+OSPF_E_NOGRAPH = -2
+OSPF_E_DEVICE = -3
+OSPF_E_RANGE = -4
+OSPF_E_NOMEM = -5
+OSPF_DIST_INF = 0xFFFFFFFF
+OSPF_HOP_COUNT = 0x1
+OSPF_WANT_DIST = 0x2
+OSPF_WANT_NH = 0x4
+OSPF_WANT_DIGEST = 0x8
+
+ENGINE_SYMBOLS = [
+    "ospf_open", "ospf_close", "ospf_last_error", "ospf_load_graph", "ospf_graph_info_get",
+    "ospf_root_neighbors", "ospf_sssp_batch", "ospf_sssp_batch_dev", "ospf_sync",
+    "ospf_plan_variant", "ospf_spf_runs",
+]
+DECISION_SYMBOLS = [
+    "odl_create", "odl_destroy", "odl_last_error", "odl_free", "odl_apply", "odl_spf_text",
+    "odl_kth_paths_text", "odl_links_text", "odl_metric_a_to_b", "odl_is_overloaded",
+    "odl_spf_runs", "odl_num_nodes", "odl_num_links", "odl_spf_digests", "odl_spf_prefetch",
+    "odl_ksp2_text", "odl_csr_size", "odl_csr_export", "odl_node_name", "odl_node_id",
+]
+
+
+class ospf_csr(C.Structure):  # noqa: N801
+    _fields_ = [("n_nodes", u32), ("n_edges", u32), ("row_ptr", vp), ("col", vp),
+                ("metric", vp), ("link_id", vp), ("twin", vp), ("edge_up", vp),
+                ("no_transit", vp)]
+
+
+class ospf_ignore(C.Structure):  # noqa: N801
+    _fields_ = [("offsets", vp), ("link_ids", vp)]
+
+
+class ospf_digest(C.Structure):  # noqa: N801
+    _fields_ = [("reached", u64), ("sum_dist", u64), ("hash", u64)]
+
+
+class ospf_graph_info(C.Structure):  # noqa: N801
+    _fields_ = [("n_nodes", u32), ("n_edges", u32), ("n_links", u32), ("max_degree", u32),
+                ("max_metric", u32), ("unit_metric", u32), ("version", u64),
+                ("device_bytes", u64)]
+
+
+_engine = None
+_decision = None
+
+
+def _load(path: str) -> C.CDLL:
+    if not os.path.exists(path):
+        raise ImportError(f"{path} is not built; run `python -m openr_amd.build` "
+                          "(there is no CPU fallback for the SPF engine)")
+    return C.CDLL(path, mode=C.RTLD_GLOBAL)
+
+
+def engine() -> C.CDLL:
+    global _engine
+    if _engine is None:
+        L = _load(ENGINE_SO)
+        L.ospf_open.argtypes = [i32, C.POINTER(vp)]
+        L.ospf_close.argtypes = [vp]
+        L.ospf_last_error.argtypes = [vp]
+        L.ospf_last_error.restype = cp
+        L.ospf_load_graph.argtypes = [vp, C.POINTER(ospf_csr), u64]
+        L.ospf_graph_info_get.argtypes = [vp, C.POINTER(ospf_graph_info)]
+        L.ospf_root_neighbors.argtypes = [vp, u32, vp, u32, C.POINTER(u32)]
+        L.ospf_sssp_batch.argtypes = [vp, vp, u32, C.POINTER(ospf_ignore), u32, u32, vp, vp, vp]
+        L.ospf_sssp_batch_dev.argtypes = [vp, vp, u32, vp, vp, u32, u32, u32, vp, vp, vp, vp]
+        L.ospf_sync.argtypes = [vp, vp]
+        L.ospf_plan_variant.argtypes = [vp, u32, u32, C.POINTER(C.c_int)]
+        L.ospf_spf_runs.argtypes = [vp]
+        L.ospf_spf_runs.restype = u64
+        _engine = L
+    return _engine
+
+
+def decision() -> C.CDLL:
+    global _decision
+    if _decision is None:
+        engine()
+        L = _load(DECISION_SO)
+        L.odl_create.argtypes = [cp, i32, C.POINTER(vp)]
+        L.odl_destroy.argtypes = [vp]
+        L.odl_last_error.argtypes = [vp]
+        L.odl_last_error.restype = cp
+        L.odl_free.argtypes = [vp]
+        L.odl_apply.argtypes = [vp, vp, u32, u32, vp]
+        for f in ("odl_spf_text", "odl_kth_paths_text", "odl_links_text", "odl_ksp2_text"):
+            getattr(L, f).restype = C.POINTER(C.c_char)
+        L.odl_spf_text.argtypes = [vp, cp, i32]
+        L.odl_kth_paths_text.argtypes = [vp, cp, cp, i32]
+        L.odl_links_text.argtypes = [vp, cp]
+        L.odl_ksp2_text.argtypes = [vp, cp, cp, u32]
+        L.odl_metric_a_to_b.argtypes = [vp, cp, cp, i32]
+        L.odl_metric_a_to_b.restype = i64
+        L.odl_is_overloaded.argtypes = [vp, cp]
+        L.odl_spf_runs.argtypes = [vp]
+        L.odl_spf_runs.restype = u64
+        L.odl_num_nodes.argtypes = [vp]
+        L.odl_num_nodes.restype = u32
+        L.odl_num_links.argtypes = [vp]
+        L.odl_num_links.restype = u32
+        L.odl_spf_digests.argtypes = [vp, cp, u32, i32, vp]
+        L.odl_spf_prefetch.argtypes = [vp, cp, u32, i32]
+        L.odl_csr_size.argtypes = [vp, C.POINTER(u32), C.POINTER(u32)]
+        L.odl_csr_export.argtypes = [vp] + [vp] * 8
+        L.odl_node_name.argtypes = [vp, u32]
+        L.odl_node_name.restype = cp
+        L.odl_node_id.argtypes = [vp, cp]
+        L.odl_node_id.restype = i64
+        _decision = L
+    return _decision

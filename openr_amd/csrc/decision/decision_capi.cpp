@@ -1,0 +1,257 @@
+// decision_capi.cpp — C ABI over odl::LinkState (include/openr_decision.h).
+// Exceptions never cross the ABI: they become an error code + odl_last_error.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../../include/openr_decision.h"
+#include "link_state.h"
+
+struct odl_ls {
+  odl::LinkState ls;
+  std::string err;
+  odl_ls(const char* area, int device) : ls(area ? area : "0", device) {}
+};
+
+namespace {
+
+char* dup(const std::string& s) {
+  char* p = (char*)std::malloc(s.size() + 1);
+  if (p) std::memcpy(p, s.c_str(), s.size() + 1);
+  return p;
+}
+
+std::string at(const oadj_stream* s, uint32_t i) {
+  return std::string(s->str_data + s->str_off[i], s->str_data + s->str_off[i + 1]);
+}
+
+std::vector<std::string> splitNl(const char* p, uint32_t n) {
+  std::vector<std::string> out;
+  out.reserve(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    const char* q = std::strchr(p, '\n');
+    if (!q) q = p + std::strlen(p);
+    out.emplace_back(p, q);
+    p = *q ? q + 1 : q;
+  }
+  return out;
+}
+
+// DESIGN.md §Result text: one line per reached node, sorted by name:
+// name \t metric \t nexthops(sorted, ',') \t pathLinks(key@prev, ';')
+std::string spfText(const odl::SpfResult& r) {
+  std::vector<const std::string*> names;
+  names.reserve(r.size());
+  for (const auto& kv : r) names.push_back(&kv.first);
+  std::sort(names.begin(), names.end(),
+            [](const std::string* a, const std::string* b) { return *a < *b; });
+  std::ostringstream os;
+  for (const std::string* n : names) {
+    const auto& nr = r.at(*n);
+    std::vector<std::string> nh(nr.nextHops().begin(), nr.nextHops().end());
+    std::sort(nh.begin(), nh.end());
+    os << *n << '\t' << nr.metric() << '\t';
+    for (size_t i = 0; i < nh.size(); ++i) os << (i ? "," : "") << nh[i];
+    os << '\t';
+    const auto& pl = nr.pathLinks();
+    for (size_t i = 0; i < pl.size(); ++i)
+      os << (i ? ";" : "") << pl[i].link->key() << '@' << pl[i].prevNode;
+    os << '\n';
+  }
+  return os.str();
+}
+
+void pathsText(std::ostringstream& os, const std::vector<odl::Path>& paths) {
+  for (const auto& p : paths) {
+    for (size_t i = 0; i < p.size(); ++i) os << (i ? "," : "") << p[i]->key();
+    os << '\n';
+  }
+}
+
+template <class F>
+auto guard(odl_ls* h, F&& f, decltype(f()) bad) -> decltype(f()) {
+  if (!h) return bad;
+  try {
+    return f();
+  } catch (const odl::EngineError& e) {
+    h->err = std::string("engine: ") + e.what();
+  } catch (const std::exception& e) {
+    h->err = e.what();
+  }
+  return bad;
+}
+
+}  // namespace
+
+extern "C" {
+
+int odl_create(const char* area, int device, odl_ls** out) {
+  if (!out) return -1;
+  try {
+    *out = new odl_ls(area, device);
+    return 0;
+  } catch (...) {
+    *out = nullptr;
+    return -1;
+  }
+}
+
+void odl_destroy(odl_ls* h) { delete h; }
+const char* odl_last_error(const odl_ls* h) { return h ? h->err.c_str() : "null handle"; }
+void odl_free(char* p) { std::free(p); }
+
+int odl_apply(odl_ls* h, const oadj_stream* s, uint32_t first, uint32_t count,
+              oadj_change* changes) {
+  return guard(h, [&]() -> int {
+    if (!s) throw std::invalid_argument("null stream");
+    for (uint32_t k = 0; k < count; ++k) {
+      const uint32_t i = first + k;
+      if (i >= s->n_dbs) throw std::out_of_range("stream index");
+      const std::string name = at(s, s->db_name[i]);
+      odl::LinkStateChange ch;
+      if (s->db_delete && s->db_delete[i]) {
+        ch = h->ls.deleteAdjacencyDatabase(name);
+      } else {
+        odl::AdjacencyDatabase db;
+        db.thisNodeName = name;
+        db.isOverloaded = s->db_overloaded[i] != 0;
+        db.nodeLabel = s->db_node_label[i];
+        for (uint64_t a = s->db_adj_off[i]; a < s->db_adj_off[i + 1]; ++a) {
+          odl::Adjacency x;
+          x.otherNodeName = at(s, s->adj_other[a]);
+          x.ifName = at(s, s->adj_if[a]);
+          x.otherIfName = at(s, s->adj_other_if[a]);
+          x.metric = s->adj_metric[a];
+          x.adjLabel = s->adj_label[a];
+          x.isOverloaded = s->adj_overloaded[a] != 0;
+          x.weight = s->adj_weight[a];
+          db.adjacencies.push_back(std::move(x));
+        }
+        ch = h->ls.updateAdjacencyDatabase(db);
+      }
+      if (changes)
+        changes[k] = oadj_change{ch.topologyChanged, ch.linkAttributesChanged,
+                                 ch.nodeLabelChanged, (int32_t)ch.addedLinks.size()};
+    }
+    return 0;
+  }, -1);
+}
+
+char* odl_spf_text(odl_ls* h, const char* root, int use_link_metric) {
+  return guard(h, [&]() -> char* {
+    return dup(spfText(h->ls.getSpfResult(root, use_link_metric != 0)));
+  }, (char*)nullptr);
+}
+
+char* odl_kth_paths_text(odl_ls* h, const char* src, const char* dst, int k) {
+  return guard(h, [&]() -> char* {
+    std::ostringstream os;
+    pathsText(os, h->ls.getKthPaths(src, dst, (size_t)k));
+    return dup(os.str());
+  }, (char*)nullptr);
+}
+
+char* odl_links_text(odl_ls* h, const char* node) {
+  return guard(h, [&]() -> char* {
+    std::ostringstream os;
+    for (const auto& l : h->ls.linksFromNode(node))
+      os << l->key() << '\t' << l->metricFrom(node) << '\t' << (l->isUp() ? 1 : 0) << '\n';
+    return dup(os.str());
+  }, (char*)nullptr);
+}
+
+int64_t odl_metric_a_to_b(odl_ls* h, const char* a, const char* b, int use_link_metric) {
+  return guard(h, [&]() -> int64_t {
+    auto m = h->ls.getMetricFromAToB(a, b, use_link_metric != 0);
+    return m ? (int64_t)*m : -1;
+  }, (int64_t)-2);
+}
+
+int odl_is_overloaded(odl_ls* h, const char* node) {
+  return h ? (h->ls.isNodeOverloaded(node) ? 1 : 0) : -1;
+}
+uint64_t odl_spf_runs(const odl_ls* h) { return h ? h->ls.spfRuns() : 0; }
+uint32_t odl_num_nodes(const odl_ls* h) { return h ? (uint32_t)h->ls.numNodes() : 0; }
+uint32_t odl_num_links(const odl_ls* h) { return h ? (uint32_t)h->ls.numLinks() : 0; }
+
+int odl_spf_digests(odl_ls* h, const char* roots_nl, uint32_t n, int use_link_metric,
+                    uint64_t* out) {
+  return guard(h, [&]() -> int {
+    auto d = h->ls.spfDigests(splitNl(roots_nl, n), use_link_metric != 0);
+    for (uint32_t i = 0; i < n; ++i) {
+      out[3 * i] = d[i].reached;
+      out[3 * i + 1] = d[i].sum_dist;
+      out[3 * i + 2] = d[i].hash;
+    }
+    return 0;
+  }, -1);
+}
+
+int odl_spf_prefetch(odl_ls* h, const char* roots_nl, uint32_t n, int use_link_metric) {
+  return guard(h, [&]() -> int {
+    h->ls.prefetchSpf(splitNl(roots_nl, n), use_link_metric != 0);
+    return 0;
+  }, -1);
+}
+
+char* odl_ksp2_text(odl_ls* h, const char* src, const char* dsts_nl, uint32_t n) {
+  return guard(h, [&]() -> char* {
+    auto dsts = splitNl(dsts_nl, n);
+    h->ls.prefetchKsp2(src, dsts);
+    std::ostringstream os;
+    for (const auto& d : dsts) {
+      pathsText(os, h->ls.getKthPaths(src, d, 2));
+      os << "=\n";
+    }
+    return dup(os.str());
+  }, (char*)nullptr);
+}
+
+int odl_csr_size(odl_ls* h, uint32_t* n_nodes, uint32_t* n_edges) {
+  return guard(h, [&]() -> int {
+    const auto& c = h->ls.snapshot();
+    if (n_nodes) *n_nodes = (uint32_t)c.names.size();
+    if (n_edges) *n_edges = (uint32_t)c.col.size();
+    return 0;
+  }, -1);
+}
+
+int odl_csr_export(odl_ls* h, uint32_t* row_ptr, uint32_t* col, uint32_t* metric,
+                   uint32_t* link_id, uint32_t* twin, uint8_t* edge_up, uint8_t* no_transit,
+                   uint32_t* link_rank) {
+  return guard(h, [&]() -> int {
+    const auto& c = h->ls.snapshot();
+    auto cp = [](auto* dst, const auto& v) {
+      if (dst && !v.empty()) std::memcpy(dst, v.data(), v.size() * sizeof(v[0]));
+    };
+    cp(row_ptr, c.rowPtr);
+    cp(col, c.col);
+    cp(metric, c.metric);
+    cp(link_id, c.linkId);
+    cp(twin, c.twin);
+    cp(edge_up, c.edgeUp);
+    cp(no_transit, c.noTransit);
+    cp(link_rank, c.linkRank);
+    return 0;
+  }, -1);
+}
+
+const char* odl_node_name(odl_ls* h, uint32_t id) {
+  return guard(h, [&]() -> const char* {
+    const auto& c = h->ls.snapshot();
+    return id < c.names.size() ? c.names[id].c_str() : nullptr;
+  }, (const char*)nullptr);
+}
+
+int64_t odl_node_id(odl_ls* h, const char* name) {
+  return guard(h, [&]() -> int64_t {
+    const auto& c = h->ls.snapshot();
+    auto it = c.ids.find(name);
+    return it == c.ids.end() ? -1 : (int64_t)it->second;
+  }, (int64_t)-2);
+}
+
+}  // extern "C"

@@ -1,0 +1,699 @@
+// link_state.cpp — LinkState mirror (see link_state.h); SPF on the engine.
+#include "link_state.h"
+
+#include <algorithm>
+#include <functional>
+#include <stdexcept>
+#include <tuple>
+
+namespace odl {
+
+namespace {
+
+// folly::hash::hash_128_to_64 (folly rev 04c2275157a3e44c1d1fa1df75835fe4ec8a7b1e,
+// folly/hash/Hash.h), used by folly's std::hash<std::pair> specialisation that
+// the reference's Link hash relies on (LinkState.cpp:134-138).
+inline uint64_t fold(uint64_t hi, uint64_t lo) {
+  constexpr uint64_t kMul = 0x9ddfea08eb382d69ULL;
+  uint64_t a = (lo ^ hi) * kMul;
+  a ^= a >> 47;
+  uint64_t b = (hi ^ a) * kMul;
+  b ^= b >> 47;
+  return b * kMul;
+}
+
+inline uint64_t hashPair(const std::pair<std::string, std::string>& p) {
+  const std::hash<std::string> h;
+  return fold(h(p.first), h(p.second));
+}
+
+inline std::string tripleKey(const std::string& a, const std::string& b, const std::string& c) {
+  std::string k;
+  k.reserve(a.size() + b.size() + c.size() + 2);
+  k += a;
+  k += '\0';
+  k += b;
+  k += '\0';
+  k += c;
+  return k;
+}
+
+constexpr uint32_t kInf = OSPF_DIST_INF;
+
+}  // namespace
+
+// ---------------------------------------------------------------- Link
+size_t Link::hashOf(const std::pair<std::string, std::string>& a,
+                    const std::pair<std::string, std::string>& b) {
+  return fold(hashPair(a), hashPair(b));
+}
+
+static std::pair<std::pair<std::string, std::string>, std::pair<std::string, std::string>>
+orderedEnds(const std::string& n1, const std::string& i1, const std::string& n2,
+            const std::string& i2) {
+  auto x = std::make_pair(n1, i1), y = std::make_pair(n2, i2);
+  if (y < x) std::swap(x, y);
+  return {x, y};
+}
+
+Link::Link(const std::string& n1, const Adjacency& a1, const std::string& n2, const Adjacency& a2)
+    : hash([&] {
+        auto o = orderedEnds(n1, a1.ifName, n2, a2.ifName);
+        return hashOf(o.first, o.second);
+      }()) {
+  auto o = orderedEnds(n1, a1.ifName, n2, a2.ifName);
+  low_ = o.first;
+  high_ = o.second;
+  const Adjacency* adj[2] = {&a1, &a2};
+  const std::string* nn[2] = {&n1, &n2};
+  for (int i = 0; i < 2; ++i) {
+    end_[i].node = *nn[i];
+    end_[i].iface = adj[i]->ifName;
+    end_[i].metric = (Metric)(int64_t)adj[i]->metric;  // i32 -> u64 as the reference
+    end_[i].overload = adj[i]->isOverloaded;
+    end_[i].adjLabel = adj[i]->adjLabel;
+    end_[i].weight = adj[i]->weight;
+  }
+}
+
+Link::End& Link::endOf(const std::string& n) {
+  if (end_[0].node == n) return end_[0];
+  if (end_[1].node == n) return end_[1];
+  throw std::invalid_argument(n);
+}
+const Link::End& Link::endOf(const std::string& n) const {
+  return const_cast<Link*>(this)->endOf(n);
+}
+const std::string& Link::otherNode(const std::string& n) const {
+  if (end_[0].node == n) return end_[1].node;
+  if (end_[1].node == n) return end_[0].node;
+  throw std::invalid_argument(n);
+}
+const std::string& Link::ifaceFrom(const std::string& n) const { return endOf(n).iface; }
+Metric Link::metricFrom(const std::string& n) const { return endOf(n).metric; }
+bool Link::overloadFrom(const std::string& n) const { return endOf(n).overload; }
+int32_t Link::adjLabelFrom(const std::string& n) const { return endOf(n).adjLabel; }
+int64_t Link::weightFrom(const std::string& n) const { return endOf(n).weight; }
+
+bool Link::setMetricFrom(const std::string& n, Metric m) {
+  End& e = endOf(n);
+  if (e.metric == m) return false;
+  e.metric = m;
+  return true;
+}
+bool Link::setOverloadFrom(const std::string& n, bool ov) {
+  const bool wasUp = isUp();
+  endOf(n).overload = ov;
+  return wasUp != isUp();
+}
+void Link::setAdjLabelFrom(const std::string& n, int32_t l) { endOf(n).adjLabel = l; }
+void Link::setWeightFrom(const std::string& n, int64_t w) { endOf(n).weight = w; }
+
+bool Link::sameLink(const Link& o) const {
+  return hash == o.hash && low_ == o.low_ && high_ == o.high_;
+}
+bool Link::orderedBefore(const Link& o) const {
+  if (hash != o.hash) return hash < o.hash;
+  return std::tie(low_, high_) < std::tie(o.low_, o.high_);
+}
+std::string Link::key() const {
+  return low_.first + "%" + low_.second + "|" + high_.first + "%" + high_.second;
+}
+
+// ---------------------------------------------------------------- LinkState
+LinkState::LinkState(std::string area, int device) : area_(std::move(area)), device_(device) {}
+
+LinkState::~LinkState() {
+  if (engine_) ospf_close(engine_);
+}
+
+const LinkSet& LinkState::linksFromNode(const std::string& node) const {
+  static const LinkSet kEmpty;
+  auto it = linkMap_.find(node);
+  return it == linkMap_.end() ? kEmpty : it->second;
+}
+
+bool LinkState::isNodeOverloaded(const std::string& node) const {
+  auto it = nodeOverloads_.find(node);
+  return it != nodeOverloads_.end() && it->second;
+}
+
+LinkPtr LinkState::makeLink(const std::string& node, const Adjacency& adj) const {
+  auto other = adjDbs_.find(adj.otherNodeName);
+  if (other == adjDbs_.end()) return nullptr;
+  auto idx = adjIndex_.find(adj.otherNodeName);
+  if (idx == adjIndex_.end()) return nullptr;
+  auto hit = idx->second.find(tripleKey(node, adj.otherIfName, adj.ifName));
+  if (hit == idx->second.end()) return nullptr;
+  return std::make_shared<Link>(node, adj, adj.otherNodeName,
+                                other->second.adjacencies[hit->second]);
+}
+
+void LinkState::addLink(const LinkPtr& l) {
+  if (!linkMap_[l->lowNode()].insert(l).second || !linkMap_[l->highNode()].insert(l).second ||
+      !allLinks_.insert(l).second)
+    throw std::logic_error("duplicate link " + l->key());
+}
+
+void LinkState::removeLink(const LinkPtr& l) {
+  if (!linkMap_.at(l->lowNode()).erase(l) || !linkMap_.at(l->highNode()).erase(l) ||
+      !allLinks_.erase(l))
+    throw std::logic_error("missing link " + l->key());
+}
+
+std::vector<LinkPtr> LinkState::sortedLinksOf(const std::string& node) const {
+  const LinkSet& s = linksFromNode(node);
+  std::vector<LinkPtr> v(s.begin(), s.end());
+  std::sort(v.begin(), v.end(), [](const LinkPtr& a, const LinkPtr& b) {
+    return a->orderedBefore(*b);
+  });
+  return v;
+}
+
+void LinkState::invalidate() {
+  ++version_;
+  memoMetric_.clear();
+  memoHops_.clear();
+  rawMetric_.clear();
+  memoKsp_.clear();
+}
+
+LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db) {
+  LinkStateChange ch;
+  const std::string me = db.thisNodeName;
+  const int32_t priorLabel = adjDbs_.count(me) ? adjDbs_.at(me).nodeLabel : 0;
+  adjDbs_[me] = db;
+  auto& idx = adjIndex_[me];
+  idx.clear();
+  for (uint32_t i = 0; i < db.adjacencies.size(); ++i) {
+    const auto& a = db.adjacencies[i];
+    idx.emplace(tripleKey(a.otherNodeName, a.ifName, a.otherIfName), i);
+  }
+
+  std::vector<LinkPtr> before = sortedLinksOf(me);
+  std::vector<LinkPtr> after;
+  after.reserve(db.adjacencies.size());
+  for (const auto& a : db.adjacencies)
+    if (LinkPtr l = makeLink(me, a)) after.push_back(std::move(l));
+  std::sort(after.begin(), after.end(),
+            [](const LinkPtr& a, const LinkPtr& b) { return a->orderedBefore(*b); });
+
+  auto ov = nodeOverloads_.find(me);
+  if (ov == nodeOverloads_.end()) {
+    nodeOverloads_.emplace(me, db.isOverloaded);  // a new node is not a change
+  } else if (ov->second != db.isOverloaded) {
+    ov->second = db.isOverloaded;
+    ch.topologyChanged = true;
+  }
+  ch.nodeLabelChanged = priorLabel != db.nodeLabel;
+
+  // two-pointer merge of old vs new link sets (both in Link::operator< order)
+  size_t i = 0, j = 0;
+  while (i < after.size() || j < before.size()) {
+    const bool takeNew = i < after.size() && (j == before.size() || after[i]->orderedBefore(*before[j]));
+    const bool takeOld = !takeNew && j < before.size() &&
+                         (i == after.size() || before[j]->orderedBefore(*after[i]));
+    if (takeNew) {
+      ch.topologyChanged |= after[i]->isUp();
+      addLink(after[i]);
+      ch.addedLinks.push_back(after[i]);
+      ++i;
+    } else if (takeOld) {
+      ch.topologyChanged |= before[j]->isUp();
+      removeLink(before[j]);
+      ++j;
+    } else {
+      const Link& fresh = *after[i];
+      Link& kept = *before[j];
+      if (fresh.metricFrom(me) != kept.metricFrom(me))
+        ch.topologyChanged |= kept.setMetricFrom(me, fresh.metricFrom(me));
+      if (fresh.overloadFrom(me) != kept.overloadFrom(me))
+        ch.topologyChanged |= kept.setOverloadFrom(me, fresh.overloadFrom(me));
+      if (fresh.adjLabelFrom(me) != kept.adjLabelFrom(me)) {
+        kept.setAdjLabelFrom(me, fresh.adjLabelFrom(me));
+        ch.linkAttributesChanged = true;
+      }
+      if (fresh.weightFrom(me) != kept.weightFrom(me)) {
+        kept.setWeightFrom(me, fresh.weightFrom(me));
+        ch.linkAttributesChanged = true;
+      }
+      ++i;
+      ++j;
+    }
+  }
+  // Memo survives non-topology updates exactly as in the reference
+  // (LinkState.cpp:721-724); the CSR is re-snapshotted on any update because
+  // node ids (name ranks) may have changed.
+  if (ch.topologyChanged) {
+    invalidate();
+  } else {
+    ++version_;
+  }
+  return ch;
+}
+
+LinkStateChange LinkState::deleteAdjacencyDatabase(const std::string& node) {
+  LinkStateChange ch;
+  auto db = adjDbs_.find(node);
+  if (db == adjDbs_.end()) return ch;
+  auto lm = linkMap_.find(node);
+  if (lm != linkMap_.end()) {
+    for (const auto& l : lm->second) {
+      if (!linkMap_.at(l->otherNode(node)).erase(l) || !allLinks_.erase(l))
+        throw std::logic_error("inconsistent link map");
+    }
+    linkMap_.erase(lm);
+    nodeOverloads_.erase(node);
+  }
+  adjDbs_.erase(db);
+  adjIndex_.erase(node);
+  invalidate();
+  ch.topologyChanged = true;
+  return ch;
+}
+
+// ---------------------------------------------------------------- snapshot
+const LinkState::Csr& LinkState::snapshot() {
+  if (snapVersion_ == version_) return csr_;
+  rawMetric_.clear();  // dist rows are indexed by the old node ids
+  Csr c;
+  c.names.reserve(adjDbs_.size());
+  for (const auto& kv : adjDbs_) c.names.push_back(kv.first);
+  std::sort(c.names.begin(), c.names.end());
+  c.ids.reserve(c.names.size() * 2);
+  for (uint32_t i = 0; i < c.names.size(); ++i) c.ids.emplace(c.names[i], i);
+  const uint32_t V = (uint32_t)c.names.size();
+  c.rowPtr.assign(V + 1, 0);
+  c.noTransit.assign(V, 0);
+  struct Ent {
+    uint32_t v, rank, lid, metric;
+    uint8_t up;
+    bool low;
+  };
+  std::vector<Ent> ents;
+  ents.reserve(allLinks_.size() * 2);
+  for (uint32_t u = 0; u < V; ++u) {
+    const std::string& un = c.names[u];
+    c.noTransit[u] = isNodeOverloaded(un) ? 1 : 0;
+    const size_t first = ents.size();
+    uint32_t rank = 0;
+    for (const auto& l : linksFromNode(un)) {
+      auto it = c.linkIds.find(l.get());
+      uint32_t lid;
+      if (it == c.linkIds.end()) {
+        lid = (uint32_t)c.links.size();
+        c.linkIds.emplace(l.get(), lid);
+        c.links.push_back(l);
+      } else {
+        lid = it->second;
+      }
+      const Metric m = l->metricFrom(un);
+      Ent e;
+      e.v = c.ids.at(l->otherNode(un));
+      e.rank = rank++;
+      e.lid = lid;
+      // metric outside u32 (negative i32 wrapped to u64) is out of the engine
+      // contract; mark it with 0 so ospf_load_graph rejects it if usable.
+      e.metric = (m >= 1 && m <= 0xFFFFFFFFull) ? (uint32_t)m : 0u;
+      e.up = l->isUp() ? 1 : 0;
+      e.low = (l->lowNode() == un);
+      ents.push_back(e);
+    }
+    std::sort(ents.begin() + first, ents.end(), [](const Ent& a, const Ent& b) {
+      return a.v != b.v ? a.v < b.v : a.rank < b.rank;
+    });
+    c.rowPtr[u + 1] = (uint32_t)ents.size();
+  }
+  const size_t E = ents.size();
+  c.col.resize(E);
+  c.metric.resize(E);
+  c.linkId.resize(E);
+  c.twin.resize(E);
+  c.linkRank.resize(E);
+  c.edgeUp.resize(E);
+  std::vector<uint32_t> side(c.links.size() * 2, kInf);
+  for (size_t e = 0; e < E; ++e) {
+    c.col[e] = ents[e].v;
+    c.metric[e] = ents[e].metric;
+    c.linkId[e] = ents[e].lid;
+    c.linkRank[e] = ents[e].rank;
+    c.edgeUp[e] = ents[e].up;
+    side[ents[e].lid * 2 + (ents[e].low ? 0 : 1)] = (uint32_t)e;
+  }
+  for (size_t e = 0; e < E; ++e) c.twin[e] = side[ents[e].lid * 2 + (ents[e].low ? 1 : 0)];
+  csr_ = std::move(c);
+  snapVersion_ = version_;
+  return csr_;
+}
+
+void LinkState::ensureEngine() {
+  snapshot();
+  if (!engine_) {
+    int rc = ospf_open(device_, &engine_);
+    if (rc != OSPF_OK) {
+      engine_ = nullptr;
+      throw EngineError(rc, "ospf_open failed (no MI355X device / HIP runtime?)");
+    }
+  }
+  if (engineVersion_ != snapVersion_) {
+    ospf_csr g{};
+    g.n_nodes = (uint32_t)csr_.names.size();
+    g.n_edges = (uint32_t)csr_.col.size();
+    g.row_ptr = csr_.rowPtr.data();
+    g.col = csr_.col.data();
+    g.metric = csr_.metric.data();
+    g.link_id = csr_.linkId.data();
+    g.twin = csr_.twin.data();
+    g.edge_up = csr_.edgeUp.data();
+    g.no_transit = csr_.noTransit.data();
+    int rc = ospf_load_graph(engine_, &g, snapVersion_);
+    if (rc != OSPF_OK) throw EngineError(rc, ospf_last_error(engine_));
+    engineVersion_ = snapVersion_;
+  }
+}
+
+uint32_t LinkState::nhWordsFor(uint32_t root) const {
+  uint32_t n = 0;
+  for (uint32_t e = csr_.rowPtr[root]; e < csr_.rowPtr[root + 1]; ++e)
+    if (csr_.col[e] != root && (e == csr_.rowPtr[root] || csr_.col[e - 1] != csr_.col[e])) ++n;
+  return std::max<uint32_t>(1, (n + 31) / 32);
+}
+
+void LinkState::runBatch(const std::vector<uint32_t>& roots,
+                         const std::vector<std::vector<uint32_t>>* ign, bool useLinkMetric,
+                         uint32_t flags, uint32_t W, std::vector<uint32_t>* dist,
+                         std::vector<uint32_t>* nh, std::vector<ospf_digest>* dig) {
+  ensureEngine();
+  const size_t V = csr_.names.size(), n = roots.size();
+  if (!useLinkMetric) flags |= OSPF_HOP_COUNT;
+  if (dist) dist->assign(n * V, kInf);
+  if (nh) nh->assign(n * V * W, 0);
+  if (dig) dig->assign(n, ospf_digest{0, 0, 0});
+  std::vector<uint32_t> off, ids;
+  ospf_ignore ig{};
+  if (ign) {
+    off.reserve(n + 1);
+    off.push_back(0);
+    for (const auto& l : *ign) {
+      ids.insert(ids.end(), l.begin(), l.end());
+      off.push_back((uint32_t)ids.size());
+    }
+    ig.offsets = off.data();
+    ig.link_ids = ids.data();
+  }
+  int rc = ospf_sssp_batch(engine_, roots.data(), (uint32_t)n, ign ? &ig : nullptr, flags, W,
+                           dist ? dist->data() : nullptr, nh ? nh->data() : nullptr,
+                           dig ? dig->data() : nullptr);
+  if (rc != OSPF_OK) throw EngineError(rc, ospf_last_error(engine_));
+}
+
+std::vector<PathLink> LinkState::pathLinksOf(const RawRun& run, uint32_t v,
+                                             bool useLinkMetric) const {
+  std::vector<PathLink> out;
+  const uint32_t dv = run.dist[v];
+  if (v == run.root || dv == kInf) return out;
+  struct Cand {
+    uint32_t du, u, rank, lid;
+  };
+  std::vector<Cand> cands;
+  for (uint32_t e = csr_.rowPtr[v]; e < csr_.rowPtr[v + 1]; ++e) {
+    if (!csr_.edgeUp[e]) continue;
+    const uint32_t lid = csr_.linkId[e];
+    if (!run.ignored.empty() && std::binary_search(run.ignored.begin(), run.ignored.end(), lid))
+      continue;
+    const uint32_t u = csr_.col[e];
+    const uint32_t du = run.dist[u];
+    if (du == kInf) continue;
+    const uint32_t t = csr_.twin[e];  // entry u -> v: metric advertised by u
+    const uint64_t w = useLinkMetric ? csr_.metric[t] : 1u;
+    if ((uint64_t)du + w != dv) continue;
+    if (u != run.root && csr_.noTransit[u]) continue;
+    cands.push_back({du, u, csr_.linkRank[t], lid});
+  }
+  // reference order: predecessor pop order (dist, name) then the link's
+  // position in linksFromNode(predecessor)
+  std::sort(cands.begin(), cands.end(), [](const Cand& a, const Cand& b) {
+    return std::tie(a.du, a.u, a.rank) < std::tie(b.du, b.u, b.rank);
+  });
+  out.reserve(cands.size());
+  for (const auto& c : cands) out.push_back(PathLink{csr_.links[c.lid], csr_.names[c.u]});
+  return out;
+}
+
+SpfResult LinkState::buildResult(const RawRun& run, const uint32_t* nh, uint32_t W,
+                                 bool useLinkMetric) {
+  SpfResult res;
+  const uint32_t V = (uint32_t)csr_.names.size();
+  std::vector<uint32_t> nbrs;
+  for (uint32_t e = csr_.rowPtr[run.root]; e < csr_.rowPtr[run.root + 1]; ++e) {
+    const uint32_t v = csr_.col[e];
+    if (v != run.root && (nbrs.empty() || nbrs.back() != v)) nbrs.push_back(v);
+  }
+  res.reserve(V);
+  for (uint32_t v = 0; v < V; ++v) {
+    if (run.dist[v] == kInf) continue;
+    NodeSpfResult r(run.dist[v]);
+    const uint32_t* bits = nh + (size_t)v * W;
+    for (uint32_t w = 0; w < W; ++w) {
+      uint32_t b = bits[w];
+      while (b) {
+        const uint32_t i = w * 32 + (uint32_t)__builtin_ctz(b);
+        b &= b - 1;
+        r.nextHops_.insert(csr_.names[nbrs.at(i)]);
+      }
+    }
+    r.pathLinks_ = pathLinksOf(run, v, useLinkMetric);
+    res.emplace(csr_.names[v], std::move(r));
+  }
+  return res;
+}
+
+const SpfResult& LinkState::getSpfResult(const std::string& node, bool useLinkMetric) {
+  auto& memo = useLinkMetric ? memoMetric_ : memoHops_;
+  auto it = memo.find(node);
+  if (it != memo.end()) return it->second;
+  prefetchSpf({node}, useLinkMetric);
+  return memo.at(node);
+}
+
+void LinkState::prefetchSpf(const std::vector<std::string>& roots, bool useLinkMetric) {
+  auto& memo = useLinkMetric ? memoMetric_ : memoHops_;
+  snapshot();
+  std::unordered_map<uint32_t, std::vector<uint32_t>> byW;  // W -> roots
+  std::unordered_set<std::string> queued;
+  for (const auto& r : roots) {
+    if (memo.count(r) || !queued.insert(r).second) continue;
+    ++spfRuns_;
+    auto id = csr_.ids.find(r);
+    if (id == csr_.ids.end()) {  // no adjacency DB: only the root itself
+      SpfResult res;
+      res.emplace(r, NodeSpfResult(0));
+      memo.emplace(r, std::move(res));
+      continue;
+    }
+    byW[nhWordsFor(id->second)].push_back(id->second);
+  }
+  const size_t V = csr_.names.size();
+  for (auto& [W, ids] : byW) {
+    const size_t chunk = std::max<size_t>(1, std::min<size_t>(ids.size(), (256ull << 20) / (V * 4 * (1 + W))));
+    for (size_t c0 = 0; c0 < ids.size(); c0 += chunk) {
+      std::vector<uint32_t> part(ids.begin() + c0, ids.begin() + std::min(ids.size(), c0 + chunk));
+      std::vector<uint32_t> dist, nh;
+      runBatch(part, nullptr, useLinkMetric, OSPF_WANT_DIST | OSPF_WANT_NH, W, &dist, &nh, nullptr);
+      for (size_t i = 0; i < part.size(); ++i) {
+        RawRun run{part[i], std::vector<uint32_t>(dist.begin() + i * V, dist.begin() + (i + 1) * V), {}};
+        SpfResult res = buildResult(run, nh.data() + i * V * W, W, useLinkMetric);
+        const std::string& name = csr_.names[part[i]];
+        memo.emplace(name, std::move(res));
+        if (useLinkMetric) rawMetric_.emplace(name, std::move(run));
+      }
+    }
+  }
+}
+
+std::vector<ospf_digest> LinkState::spfDigests(const std::vector<std::string>& roots,
+                                               bool useLinkMetric) {
+  snapshot();
+  std::vector<ospf_digest> out(roots.size(), ospf_digest{0, 0, 0});
+  std::vector<uint32_t> ids;
+  std::vector<size_t> pos;
+  uint32_t W = 1;
+  for (size_t i = 0; i < roots.size(); ++i) {
+    ++spfRuns_;
+    auto id = csr_.ids.find(roots[i]);
+    if (id == csr_.ids.end()) {
+      // root without a database: result {root: 0}; digest as the oracle's
+      uint64_t x = (0xFFFFFFFFull << 32);
+      x ^= x >> 30;
+      x *= 0xbf58476d1ce4e5b9ULL;
+      x ^= x >> 27;
+      x *= 0x94d049bb133111ebULL;
+      x ^= x >> 31;
+      out[i] = ospf_digest{1, 0, x};
+      continue;
+    }
+    ids.push_back(id->second);
+    pos.push_back(i);
+    W = std::max(W, nhWordsFor(id->second));
+  }
+  if (!ids.empty()) {
+    std::vector<ospf_digest> d;
+    runBatch(ids, nullptr, useLinkMetric, OSPF_WANT_DIGEST, W, nullptr, nullptr, &d);
+    for (size_t k = 0; k < ids.size(); ++k) out[pos[k]] = d[k];
+  }
+  return out;
+}
+
+std::optional<Metric> LinkState::getMetricFromAToB(const std::string& a, const std::string& b,
+                                                   bool useLinkMetric) {
+  if (a == b) return 0;
+  const SpfResult& r = getSpfResult(a, useLinkMetric);
+  auto it = r.find(b);
+  if (it == r.end()) return std::nullopt;
+  return it->second.metric();
+}
+
+const LinkState::RawRun& LinkState::rawSpf(const std::string& node) {
+  getSpfResult(node, true);
+  snapshot();
+  auto it = rawMetric_.find(node);
+  if (it == rawMetric_.end()) {
+    // node ids moved under a memoised result (a non-topology update added or
+    // removed a node): re-derive the arrays; not a new logical runSpf.
+    const uint32_t s = csr_.ids.at(node);
+    std::vector<uint32_t> dist;
+    runBatch({s}, nullptr, true, OSPF_WANT_DIST, nhWordsFor(s), &dist, nullptr, nullptr);
+    it = rawMetric_.emplace(node, RawRun{s, std::move(dist), {}}).first;
+  }
+  return it->second;
+}
+
+std::optional<Path> LinkState::trace(const RawRun& run, uint32_t src, uint32_t x,
+                                     std::unordered_set<const Link*>& seen) const {
+  if (x == src) return Path{};
+  for (const auto& pl : pathLinksOf(run, x, true)) {
+    if (!seen.insert(pl.link.get()).second) continue;
+    auto p = trace(run, src, csr_.ids.at(pl.prevNode), seen);
+    if (p) {
+      p->push_back(pl.link);
+      return p;
+    }
+  }
+  return std::nullopt;
+}
+
+std::vector<Path> LinkState::tracePaths(const RawRun& run, uint32_t src, uint32_t dst) const {
+  std::vector<Path> out;
+  if (run.dist[dst] == kInf) return out;
+  std::unordered_set<const Link*> seen;
+  for (auto p = trace(run, src, dst, seen); p && !p->empty(); p = trace(run, src, dst, seen))
+    out.push_back(std::move(*p));
+  return out;
+}
+
+static std::string kspKey(const std::string& s, const std::string& d, size_t k) {
+  std::string key = s;
+  key += '\x01';
+  key += d;
+  key += '\x01';
+  key += std::to_string(k);
+  return key;
+}
+
+const std::vector<Path>& LinkState::getKthPaths(const std::string& src, const std::string& dst,
+                                                size_t k) {
+  if (k < 1) throw std::invalid_argument("k must be >= 1");
+  const std::string key = kspKey(src, dst, k);
+  auto it = memoKsp_.find(key);
+  if (it != memoKsp_.end()) return it->second;
+  std::unordered_set<const Link*> skipSet;
+  std::vector<LinkPtr> skip;
+  for (size_t i = 1; i < k; ++i)
+    for (const auto& p : getKthPaths(src, dst, i))
+      for (const auto& l : p)
+        if (skipSet.insert(l.get()).second) skip.push_back(l);
+  std::vector<Path> paths;
+  if (skip.empty()) {
+    const SpfResult& r = getSpfResult(src, true);
+    if (r.count(dst) && csr_.ids.count(src)) {
+      const RawRun& run = rawSpf(src);
+      paths = tracePaths(run, csr_.ids.at(src), csr_.ids.at(dst));
+    }
+  } else {
+    ++spfRuns_;
+    snapshot();
+    const uint32_t s = csr_.ids.at(src);
+    std::vector<uint32_t> ign;
+    for (const auto& l : skip) ign.push_back(csr_.linkIds.at(l.get()));
+    std::sort(ign.begin(), ign.end());
+    std::vector<std::vector<uint32_t>> igns{ign};
+    std::vector<uint32_t> dist;
+    runBatch({s}, &igns, true, OSPF_WANT_DIST, nhWordsFor(s), &dist, nullptr, nullptr);
+    RawRun run{s, std::move(dist), std::move(ign)};
+    auto d = csr_.ids.find(dst);
+    if (d != csr_.ids.end()) paths = tracePaths(run, s, d->second);
+  }
+  return memoKsp_.emplace(key, std::move(paths)).first->second;
+}
+
+void LinkState::prefetchKsp2(const std::string& src, const std::vector<std::string>& dsts) {
+  snapshot();
+  auto sid = csr_.ids.find(src);
+  if (sid == csr_.ids.end()) {
+    for (const auto& d : dsts) getKthPaths(src, d, 2);
+    return;
+  }
+  const uint32_t s = sid->second;
+  struct Job {
+    std::string dst;
+    std::vector<uint32_t> ign;
+  };
+  std::vector<Job> jobs;
+  for (const auto& d : dsts) {
+    if (memoKsp_.count(kspKey(src, d, 2))) continue;
+    const auto& first = getKthPaths(src, d, 1);
+    std::vector<uint32_t> ign;
+    for (const auto& p : first)
+      for (const auto& l : p) ign.push_back(csr_.linkIds.at(l.get()));
+    std::sort(ign.begin(), ign.end());
+    ign.erase(std::unique(ign.begin(), ign.end()), ign.end());
+    if (ign.empty()) {
+      getKthPaths(src, d, 2);  // no masked rerun: reference reuses getSpfResult
+      continue;
+    }
+    jobs.push_back(Job{d, std::move(ign)});
+  }
+  const size_t V = csr_.names.size();
+  const uint32_t W = nhWordsFor(s);
+  const size_t chunk = std::max<size_t>(1, std::min<size_t>(jobs.size(), (512ull << 20) / (V * 4)));
+  for (size_t c0 = 0; c0 < jobs.size(); c0 += chunk) {
+    const size_t n = std::min(chunk, jobs.size() - c0);
+    std::vector<uint32_t> roots(n, s);
+    std::vector<std::vector<uint32_t>> igns(n);
+    for (size_t i = 0; i < n; ++i) igns[i] = jobs[c0 + i].ign;
+    std::vector<uint32_t> dist;
+    runBatch(roots, &igns, true, OSPF_WANT_DIST, W, &dist, nullptr, nullptr);
+    spfRuns_ += n;
+    for (size_t i = 0; i < n; ++i) {
+      RawRun run{s, std::vector<uint32_t>(dist.begin() + i * V, dist.begin() + (i + 1) * V),
+                 std::move(igns[i])};
+      const std::string& d = jobs[c0 + i].dst;
+      auto did = csr_.ids.find(d);
+      std::vector<Path> paths;
+      if (did != csr_.ids.end()) paths = tracePaths(run, s, did->second);
+      memoKsp_.emplace(kspKey(src, d, 2), std::move(paths));
+    }
+  }
+}
+
+bool LinkState::pathAInPathB(const Path& a, const Path& b) {
+  if (a.size() > b.size()) return false;
+  for (size_t i = 0; i + a.size() <= b.size(); ++i) {
+    size_t k = 0;
+    while (k < a.size() && a[k]->sameLink(*b[i + k])) ++k;
+    if (k == a.size()) return true;
+  }
+  return false;
+}
+
+}  // namespace odl

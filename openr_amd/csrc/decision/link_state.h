@@ -1,0 +1,225 @@
+// link_state.h — host-side mirror of OpenR's LinkState whose SPF runs on the
+// MI355X engine (libopenr_spf_hip, include/openr_spf.h).
+//
+// Public surface and semantics follow openr/decision/LinkState.h:339-452:
+// links exist only when both ends advertise each other with matching
+// interface names, are kept once per undirected link in per-node hash sets
+// keyed by the folly hash of the ordered (node, ifName) pairs (so iteration
+// order — which fixes pathLinks and KSP2 order — matches the reference), and
+// SPF / KSP results are memoised until a topology change.
+//
+// What differs is where runSpf happens: the graph is snapshotted into a CSR
+// (node id = rank of the node name in byte order, rows sorted by neighbour
+// id, link_rank = position in linksFromNode iteration) and handed to the
+// engine, which returns per-root distances and next-hop bitsets. SpfResult
+// objects (names, next-hop name sets, ordered pathLinks) are rebuilt from
+// those arrays on demand.
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "../../../include/openr_adjdb.h"
+#include "../../../include/openr_spf.h"
+
+namespace odl {
+
+using Metric = uint64_t;
+
+struct Adjacency {
+  std::string otherNodeName, ifName, otherIfName;
+  int32_t metric = 1;
+  int32_t adjLabel = 0;
+  bool isOverloaded = false;
+  int64_t weight = 1;
+};
+
+struct AdjacencyDatabase {
+  std::string thisNodeName;
+  bool isOverloaded = false;
+  int32_t nodeLabel = 0;
+  std::vector<Adjacency> adjacencies;
+};
+
+// One undirected link (LinkState.h:80-182).
+class Link {
+ public:
+  Link(const std::string& n1, const Adjacency& a1, const std::string& n2, const Adjacency& a2);
+
+  const std::string& otherNode(const std::string& n) const;
+  const std::string& ifaceFrom(const std::string& n) const;
+  Metric metricFrom(const std::string& n) const;
+  bool overloadFrom(const std::string& n) const;
+  int32_t adjLabelFrom(const std::string& n) const;
+  int64_t weightFrom(const std::string& n) const;
+  bool isUp() const { return !end_[0].overload && !end_[1].overload; }
+
+  // attribute updates from node n; return value per LinkState.cpp:284-330
+  bool setMetricFrom(const std::string& n, Metric m);
+  bool setOverloadFrom(const std::string& n, bool ov);  // true iff isUp() flipped
+  void setAdjLabelFrom(const std::string& n, int32_t l);
+  void setWeightFrom(const std::string& n, int64_t w);
+
+  const std::string& lowNode() const { return low_.first; }
+  const std::string& highNode() const { return high_.first; }
+  bool sameLink(const Link& o) const;
+  bool orderedBefore(const Link& o) const;  // Link::operator< (hash, names)
+  std::string key() const;                  // "n1%if1|n2%if2" (ordered)
+
+  const size_t hash;
+
+ private:
+  struct End {
+    std::string node, iface;
+    Metric metric = 1;
+    bool overload = false;
+    int32_t adjLabel = 0;
+    int64_t weight = 0;
+  };
+  End& endOf(const std::string& n);
+  const End& endOf(const std::string& n) const;
+  End end_[2];
+  std::pair<std::string, std::string> low_, high_;
+  static size_t hashOf(const std::pair<std::string, std::string>& a,
+                       const std::pair<std::string, std::string>& b);
+};
+
+using LinkPtr = std::shared_ptr<Link>;
+struct LinkPtrHash {
+  size_t operator()(const LinkPtr& l) const { return l->hash; }
+};
+struct LinkPtrEq {
+  bool operator()(const LinkPtr& a, const LinkPtr& b) const { return a->sameLink(*b); }
+};
+using LinkSet = std::unordered_set<LinkPtr, LinkPtrHash, LinkPtrEq>;
+
+struct PathLink {
+  LinkPtr link;
+  std::string prevNode;
+};
+
+class NodeSpfResult {
+ public:
+  explicit NodeSpfResult(Metric m) : metric_(m) {}
+  Metric metric() const { return metric_; }
+  const std::vector<PathLink>& pathLinks() const { return pathLinks_; }
+  const std::unordered_set<std::string>& nextHops() const { return nextHops_; }
+
+ private:
+  friend class LinkState;
+  Metric metric_;
+  std::vector<PathLink> pathLinks_;
+  std::unordered_set<std::string> nextHops_;
+};
+
+using SpfResult = std::unordered_map<std::string, NodeSpfResult>;
+using Path = std::vector<LinkPtr>;
+
+struct LinkStateChange {
+  bool topologyChanged = false;
+  bool linkAttributesChanged = false;
+  bool nodeLabelChanged = false;
+  std::vector<LinkPtr> addedLinks;
+};
+
+// Raised for engine failures (no device, out-of-contract graph). There is no
+// CPU fallback; the Decision caller decides what to do.
+struct EngineError : std::runtime_error {
+  int code;
+  EngineError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+class LinkState {
+ public:
+  LinkState(std::string area, int device);
+  ~LinkState();
+  LinkState(const LinkState&) = delete;
+  LinkState& operator=(const LinkState&) = delete;
+
+  LinkStateChange updateAdjacencyDatabase(const AdjacencyDatabase& db);
+  LinkStateChange deleteAdjacencyDatabase(const std::string& node);
+
+  const LinkSet& linksFromNode(const std::string& node) const;
+  bool isNodeOverloaded(const std::string& node) const;
+  size_t numLinks() const { return allLinks_.size(); }
+  size_t numNodes() const { return adjDbs_.size(); }
+  const std::unordered_map<std::string, AdjacencyDatabase>& getAdjacencyDatabases() const {
+    return adjDbs_;
+  }
+
+  const SpfResult& getSpfResult(const std::string& node, bool useLinkMetric = true);
+  std::optional<Metric> getMetricFromAToB(const std::string& a, const std::string& b,
+                                          bool useLinkMetric = true);
+  const std::vector<Path>& getKthPaths(const std::string& src, const std::string& dst, size_t k);
+  static bool pathAInPathB(const Path& a, const Path& b);
+
+  // ---- batched entry points (no reference counterpart) ----
+  void prefetchSpf(const std::vector<std::string>& roots, bool useLinkMetric);
+  std::vector<ospf_digest> spfDigests(const std::vector<std::string>& roots, bool useLinkMetric);
+  void prefetchKsp2(const std::string& src, const std::vector<std::string>& dsts);
+
+  uint64_t spfRuns() const { return spfRuns_; }
+
+  // ---- CSR snapshot (what the engine sees) ----
+  struct Csr {
+    std::vector<std::string> names;                 // id -> name (sorted)
+    std::unordered_map<std::string, uint32_t> ids;  // name -> id
+    std::vector<uint32_t> rowPtr, col, metric, linkId, twin, linkRank;
+    std::vector<uint8_t> edgeUp, noTransit;
+    std::vector<LinkPtr> links;                     // link id -> link
+    std::unordered_map<const Link*, uint32_t> linkIds;
+  };
+  const Csr& snapshot();
+
+ private:
+  struct RawRun {  // one engine run kept for pathLinks / trace reconstruction
+    uint32_t root;
+    std::vector<uint32_t> dist;
+    std::vector<uint32_t> ignored;  // sorted link ids
+  };
+
+  LinkPtr makeLink(const std::string& node, const Adjacency& adj) const;
+  void addLink(const LinkPtr& l);
+  void removeLink(const LinkPtr& l);
+  std::vector<LinkPtr> sortedLinksOf(const std::string& node) const;
+  void invalidate();
+  void ensureEngine();
+  uint32_t nhWordsFor(uint32_t root) const;
+  void runBatch(const std::vector<uint32_t>& roots, const std::vector<std::vector<uint32_t>>* ign,
+                bool useLinkMetric, uint32_t flags, uint32_t W, std::vector<uint32_t>* dist,
+                std::vector<uint32_t>* nh, std::vector<ospf_digest>* dig);
+  SpfResult buildResult(const RawRun& run, const uint32_t* nh, uint32_t W, bool useLinkMetric);
+  std::vector<PathLink> pathLinksOf(const RawRun& run, uint32_t v, bool useLinkMetric) const;
+  std::optional<Path> trace(const RawRun& run, uint32_t src, uint32_t x,
+                            std::unordered_set<const Link*>& seen) const;
+  std::vector<Path> tracePaths(const RawRun& run, uint32_t src, uint32_t dst) const;
+  const RawRun& rawSpf(const std::string& node);
+
+  std::string area_;
+  int device_;
+  ospf_ctx* engine_ = nullptr;
+  uint64_t engineVersion_ = 0;  // snapshot version loaded into the engine
+  uint64_t version_ = 1;        // bumped on every ingest call
+  uint64_t snapVersion_ = 0;
+  Csr csr_;
+  uint64_t spfRuns_ = 0;
+
+  std::unordered_map<std::string, LinkSet> linkMap_;
+  LinkSet allLinks_;
+  std::unordered_map<std::string, bool> nodeOverloads_;
+  std::unordered_map<std::string, AdjacencyDatabase> adjDbs_;
+  // (otherNodeName \0 ifName \0 otherIfName) -> first adjacency index, per node
+  std::unordered_map<std::string, std::unordered_map<std::string, uint32_t>> adjIndex_;
+
+  std::unordered_map<std::string, SpfResult> memoMetric_, memoHops_;
+  std::unordered_map<std::string, RawRun> rawMetric_;  // unmasked runs (useLinkMetric)
+  std::unordered_map<std::string, std::vector<Path>> memoKsp_;
+};
+
+}  // namespace odl

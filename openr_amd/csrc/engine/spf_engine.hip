@@ -1,0 +1,434 @@
+// spf_engine.hip — C ABI of libopenr_spf_hip (include/openr_spf.h).
+//
+// Owns the device-resident CSR snapshot of one LinkState (area), picks the
+// kernel variant for a batch (LDS-resident vs HBM-streamed state) and launches
+// one workgroup per SPF run. No CPU fallback: a missing device or an
+// out-of-contract graph is an error code.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "spf_kernels.h"
+
+struct ospf_ctx {
+  int device = 0;
+  size_t lds_limit = 64 * 1024;
+  int n_cu = 256;
+  std::string err;
+  uint64_t spf_runs = 0;
+  // graph
+  bool loaded = false;
+  ospf_graph_info info{};
+  std::vector<uint32_t> h_row_ptr, h_dn_off, h_dn;  // host copies for root queries
+  void* d_graph = nullptr;
+  ospf::DevGraph g{};
+  uint32_t max_dn = 0;
+  // scratch
+  void* d_scratch = nullptr;
+  size_t scratch_bytes = 0;
+  void* d_stage = nullptr;
+  size_t stage_bytes = 0;
+  uint32_t* d_err = nullptr;
+};
+
+namespace {
+
+int fail(ospf_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+int hip_fail(ospf_ctx* c, hipError_t e, const char* what) {
+  return fail(c, OSPF_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIPCHK(ctx, call)                                  \
+  do {                                                     \
+    hipError_t e_ = (call);                                \
+    if (e_ != hipSuccess) return hip_fail(ctx, e_, #call); \
+  } while (0)
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+int ensure(ospf_ctx* c, void** p, size_t* have, size_t need) {
+  if (*have >= need) return OSPF_OK;
+  const size_t want = std::max(need, *have * 3 / 2);
+  if (*p) hipFree(*p);
+  *p = nullptr;
+  *have = 0;
+  hipError_t e = hipMalloc(p, want);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return fail(c, OSPF_E_NOMEM, std::string("hipMalloc scratch: ") + hipGetErrorString(e));
+  }
+  *have = want;
+  return OSPF_OK;
+}
+
+struct Plan {
+  int variant;
+  uint32_t block;
+  size_t lds;
+  uint32_t nbr_cap, ign_cap;
+};
+
+Plan make_plan(const ospf_ctx* c, uint32_t W, uint32_t ign_cap) {
+  Plan p{};
+  const size_t V = c->info.n_nodes;
+  p.nbr_cap = (uint32_t)align_up(std::max<uint32_t>(c->max_dn, 1), 4);
+  p.ign_cap = (uint32_t)align_up(ign_cap, 4);
+  const size_t head = (32 + p.nbr_cap + p.ign_cap) * 4;
+  const size_t full = head + V * 4 + V * W * 4;
+  const size_t half = head + V * 4;
+  if (full <= c->lds_limit) {
+    p.variant = 0;
+    p.lds = full;
+  } else if (half <= c->lds_limit) {
+    p.variant = 1;
+    p.lds = half;
+  } else {
+    p.variant = 2;
+    p.lds = head;
+  }
+  // test/benchmark knob: OSPF_FORCE_VARIANT=1|2 forces the HBM-state
+  // variants on graphs that would fit in LDS (never a smaller variant than
+  // what fits).
+  if (const char* f = getenv("OSPF_FORCE_VARIANT")) {
+    const int want = atoi(f);
+    if (want > p.variant && want <= 2) {
+      p.variant = want;
+      p.lds = want == 1 ? half : head;
+    }
+  }
+  p.block = V >= 4096 ? 512 : 256;
+  return p;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ospf_open(int device, ospf_ctx** out) {
+  if (!out) return OSPF_E_INVAL;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return OSPF_E_DEVICE;
+  if (device < 0 || device >= n) return OSPF_E_INVAL;
+  ospf_ctx* c = new (std::nothrow) ospf_ctx();
+  if (!c) return OSPF_E_NOMEM;
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess) {
+    delete c;
+    return OSPF_E_DEVICE;
+  }
+  int lds = 0, cu = 0;
+  hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device);
+  hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device);
+  // keep 1 KiB for the kernel's static LDS (digest reduction)
+  if (lds > 2048) c->lds_limit = (size_t)lds - 1024;
+  if (cu > 0) c->n_cu = cu;
+  if (hipMalloc((void**)&c->d_err, sizeof(uint32_t)) != hipSuccess ||
+      hipMemset(c->d_err, 0, sizeof(uint32_t)) != hipSuccess) {
+    delete c;
+    return OSPF_E_DEVICE;
+  }
+  *out = c;
+  return OSPF_OK;
+}
+
+int ospf_close(ospf_ctx* c) {
+  if (!c) return OSPF_E_INVAL;
+  hipSetDevice(c->device);
+  if (c->d_graph) hipFree(c->d_graph);
+  if (c->d_scratch) hipFree(c->d_scratch);
+  if (c->d_stage) hipFree(c->d_stage);
+  if (c->d_err) hipFree(c->d_err);
+  delete c;
+  return OSPF_OK;
+}
+
+const char* ospf_last_error(const ospf_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+uint64_t ospf_spf_runs(const ospf_ctx* c) { return c ? c->spf_runs : 0; }
+
+int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
+  if (!c || !csr) return OSPF_E_INVAL;
+  const uint32_t V = csr->n_nodes, E = csr->n_edges;
+  if (V == 0 || V >= 0x80000000u) return fail(c, OSPF_E_INVAL, "n_nodes out of range");
+  if (!csr->row_ptr || (E && (!csr->col || !csr->metric || !csr->link_id || !csr->twin ||
+                              !csr->edge_up)))
+    return fail(c, OSPF_E_INVAL, "null CSR array");
+  if (csr->row_ptr[0] != 0 || csr->row_ptr[V] != E)
+    return fail(c, OSPF_E_INVAL, "row_ptr must start at 0 and end at n_edges");
+
+  std::vector<uint32_t> colx(E), rw(E), nt((V + 31) / 32, 0u), dn_off(V + 1, 0u);
+  std::vector<uint32_t> dn;
+  dn.reserve(E);
+  uint32_t max_deg = 0, max_metric = 0, max_dn = 0, n_links = 0;
+  bool unit = true;
+  for (uint32_t u = 0; u < V; ++u) {
+    const uint32_t b = csr->row_ptr[u], e1 = csr->row_ptr[u + 1];
+    if (e1 < b || e1 > E) return fail(c, OSPF_E_INVAL, "row_ptr not monotone");
+    max_deg = std::max(max_deg, e1 - b);
+    dn_off[u] = (uint32_t)dn.size();
+    for (uint32_t e = b; e < e1; ++e) {
+      const uint32_t v = csr->col[e];
+      if (v >= V) return fail(c, OSPF_E_INVAL, "col out of range");
+      if (e > b && csr->col[e - 1] > v) return fail(c, OSPF_E_INVAL, "rows must be sorted by col");
+      const uint32_t t = csr->twin[e];
+      if (t >= E || csr->twin[t] != e || csr->col[t] != u || t < csr->row_ptr[v] ||
+          t >= csr->row_ptr[v + 1] || csr->link_id[t] != csr->link_id[e])
+        return fail(c, OSPF_E_INVAL, "twin/link_id inconsistent");
+      if (csr->edge_up[e] != csr->edge_up[t])
+        return fail(c, OSPF_E_INVAL, "edge_up must match on both directions of a link");
+      const bool up = csr->edge_up[e] != 0;
+      colx[e] = v | (up ? 0u : 0x80000000u);
+      rw[e] = csr->metric[t];
+      if (up) {
+        if (csr->metric[e] == 0)
+          return fail(c, OSPF_E_RANGE, "metric 0 on a usable link is outside the engine contract");
+        max_metric = std::max(max_metric, csr->metric[e]);
+        unit &= csr->metric[e] == 1;
+      }
+      if (e < t) ++n_links;
+      if (v != u && (e == b || csr->col[e - 1] != v)) dn.push_back(v);
+    }
+    max_dn = std::max<uint32_t>(max_dn, (uint32_t)dn.size() - dn_off[u]);
+    if (csr->no_transit && csr->no_transit[u]) nt[u >> 5] |= 1u << (u & 31);
+  }
+  dn_off[V] = (uint32_t)dn.size();
+  if (max_dn > OSPF_MAX_ROOT_NEIGHBORS)
+    return fail(c, OSPF_E_RANGE, "a node has more distinct neighbours than OSPF_MAX_ROOT_NEIGHBORS");
+
+  // device layout: one allocation, 256-B aligned sub-buffers
+  const size_t sz_row = (V + 1) * 4ull, sz_e = (size_t)E * 4ull, sz_nt = nt.size() * 4ull,
+               sz_dnoff = (V + 1) * 4ull, sz_dn = std::max<size_t>(dn.size(), 1) * 4ull;
+  size_t off[8], tot = 0;
+  const size_t szs[8] = {sz_row, sz_e, sz_e, sz_e, sz_e, sz_nt, sz_dnoff, sz_dn};
+  for (int i = 0; i < 8; ++i) {
+    off[i] = tot;
+    tot += align_up(std::max<size_t>(szs[i], 4), 256);
+  }
+  HIPCHK(c, hipSetDevice(c->device));
+  if (c->d_graph) {
+    hipFree(c->d_graph);
+    c->d_graph = nullptr;
+    c->loaded = false;
+  }
+  hipError_t he = hipMalloc(&c->d_graph, tot);
+  if (he != hipSuccess) {
+    c->d_graph = nullptr;
+    return fail(c, OSPF_E_NOMEM, std::string("hipMalloc graph: ") + hipGetErrorString(he));
+  }
+  char* base = (char*)c->d_graph;
+  const void* srcs[8] = {csr->row_ptr, colx.data(), csr->metric, rw.data(), csr->link_id,
+                         nt.data(), dn_off.data(), dn.data()};
+  for (int i = 0; i < 8; ++i)
+    if (szs[i] && srcs[i]) HIPCHK(c, hipMemcpy(base + off[i], srcs[i], szs[i], hipMemcpyHostToDevice));
+  c->g.V = V;
+  c->g.E = E;
+  c->g.row_ptr = (const uint32_t*)(base + off[0]);
+  c->g.colx = (const uint32_t*)(base + off[1]);
+  c->g.w = (const uint32_t*)(base + off[2]);
+  c->g.rw = (const uint32_t*)(base + off[3]);
+  c->g.link_id = (const uint32_t*)(base + off[4]);
+  c->g.nt_bits = (const uint32_t*)(base + off[5]);
+  c->g.dn_off = (const uint32_t*)(base + off[6]);
+  c->g.dn = (const uint32_t*)(base + off[7]);
+  c->h_row_ptr.assign(csr->row_ptr, csr->row_ptr + V + 1);
+  c->h_dn_off = std::move(dn_off);
+  c->h_dn = std::move(dn);
+  c->max_dn = max_dn;
+  c->info.n_nodes = V;
+  c->info.n_edges = E;
+  c->info.n_links = n_links;
+  c->info.max_degree = max_deg;
+  c->info.max_metric = max_metric;
+  c->info.unit_metric = unit ? 1u : 0u;
+  c->info.version = version;
+  c->info.device_bytes = tot;
+  c->loaded = true;
+  return OSPF_OK;
+}
+
+int ospf_graph_info_get(const ospf_ctx* c, ospf_graph_info* info) {
+  if (!c || !info) return OSPF_E_INVAL;
+  if (!c->loaded) return OSPF_E_NOGRAPH;
+  *info = c->info;
+  return OSPF_OK;
+}
+
+int ospf_root_neighbors(const ospf_ctx* c, uint32_t root, uint32_t* ids, uint32_t cap,
+                        uint32_t* n) {
+  if (!c || !n) return OSPF_E_INVAL;
+  if (!c->loaded) return OSPF_E_NOGRAPH;
+  if (root >= c->info.n_nodes) return OSPF_E_INVAL;
+  const uint32_t b = c->h_dn_off[root], e = c->h_dn_off[root + 1];
+  *n = e - b;
+  if (ids)
+    for (uint32_t i = 0; i < std::min(cap, e - b); ++i) ids[i] = c->h_dn[b + i];
+  return OSPF_OK;
+}
+
+int ospf_plan_variant(const ospf_ctx* c, uint32_t flags, uint32_t nh_words, int* variant) {
+  if (!c || !variant) return OSPF_E_INVAL;
+  if (!c->loaded) return OSPF_E_NOGRAPH;
+  (void)flags;
+  *variant = make_plan(c, std::max<uint32_t>(nh_words, 1), 0).variant;
+  return OSPF_OK;
+}
+
+int ospf_sssp_batch_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n_roots,
+                        const uint32_t* d_ign_off, const uint32_t* d_ign_ids,
+                        uint32_t max_ignored, uint32_t flags, uint32_t nh_words,
+                        uint32_t* d_dist, uint32_t* d_nh, ospf_digest* d_digest,
+                        void* stream) {
+  if (!c) return OSPF_E_INVAL;
+  if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  if (n_roots == 0) return OSPF_OK;
+  if (!d_roots) return fail(c, OSPF_E_INVAL, "null roots");
+  if (nh_words == 0 || nh_words > OSPF_MAX_ROOT_NEIGHBORS / 32)
+    return fail(c, OSPF_E_INVAL, "nh_words out of range");
+  if ((flags & OSPF_WANT_DIST) && !d_dist) return fail(c, OSPF_E_INVAL, "WANT_DIST without buffer");
+  if ((flags & OSPF_WANT_NH) && !d_nh) return fail(c, OSPF_E_INVAL, "WANT_NH without buffer");
+  if ((flags & OSPF_WANT_DIGEST) && !d_digest)
+    return fail(c, OSPF_E_INVAL, "WANT_DIGEST without buffer");
+  const bool hop = flags & OSPF_HOP_COUNT;
+  const bool ign = d_ign_off != nullptr;
+  if (ign && (!d_ign_ids && max_ignored)) return fail(c, OSPF_E_INVAL, "null ignore ids");
+  if (ign && max_ignored > OSPF_MAX_IGNORED_PER_RUN)
+    return fail(c, OSPF_E_RANGE, "max_ignored above OSPF_MAX_IGNORED_PER_RUN");
+  const uint64_t V = c->info.n_nodes;
+  if (!hop && (uint64_t)c->info.max_metric * (V - 1) >= 0xFFFFFFFFull)
+    return fail(c, OSPF_E_RANGE, "u32 distance overflow possible (max_metric * (V-1))");
+  const bool unit = hop || c->info.unit_metric;
+
+  const Plan p = make_plan(c, nh_words, ign ? std::max<uint32_t>(max_ignored, 1) : 0);
+  // scratch for state the caller does not want back
+  size_t need = 0;
+  const bool dist_scratch = (p.variant == 2) && !(flags & OSPF_WANT_DIST);
+  const bool nh_scratch = (p.variant >= 1) && !(flags & OSPF_WANT_NH);
+  if (dist_scratch) need += align_up(n_roots * V * 4, 256);
+  if (nh_scratch) need += align_up(n_roots * V * nh_words * 4ull, 256);
+  if (need) {
+    int rc = ensure(c, &c->d_scratch, &c->scratch_bytes, need);
+    if (rc) return rc;
+  }
+  char* sp = (char*)c->d_scratch;
+  ospf::RunArgs a{};
+  a.roots = d_roots;
+  a.ign_off = ign ? d_ign_off : nullptr;
+  a.ign_ids = d_ign_ids;
+  a.flags = flags;
+  a.W = nh_words;
+  a.nbr_cap = p.nbr_cap;
+  a.ign_cap = p.ign_cap;
+  a.dist = d_dist;
+  a.nh = d_nh;
+  a.digest = d_digest;
+  a.err = c->d_err;
+  if (dist_scratch) {
+    a.dist = (uint32_t*)sp;
+    sp += align_up(n_roots * V * 4, 256);
+  }
+  if (nh_scratch) a.nh = (uint32_t*)sp;
+  if (!(flags & OSPF_WANT_DIST) && p.variant != 2) a.dist = nullptr;
+  if (!(flags & OSPF_WANT_NH) && p.variant == 0) a.nh = nullptr;
+
+  HIPCHK(c, hipSetDevice(c->device));
+  hipError_t e = ospf::launch_spf(p.variant, unit, ign, c->g, a, n_roots, p.block, p.lds,
+                                  (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(c, e, "launch_spf");
+  c->spf_runs += n_roots;
+  return OSPF_OK;
+}
+
+int ospf_sync(ospf_ctx* c, void* stream) {
+  if (!c) return OSPF_E_INVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
+  uint32_t err = 0;
+  HIPCHK(c, hipMemcpy(&err, c->d_err, 4, hipMemcpyDeviceToHost));
+  if (err) {
+    HIPCHK(c, hipMemset(c->d_err, 0, 4));
+    return fail(c, OSPF_E_RANGE,
+                (err & 1u) ? "a root has more distinct neighbours than 32*nh_words"
+                           : "a run's ignore list exceeds max_ignored");
+  }
+  return OSPF_OK;
+}
+
+int ospf_sssp_batch(ospf_ctx* c, const uint32_t* roots, uint32_t n_roots, const ospf_ignore* ig,
+                    uint32_t flags, uint32_t nh_words, uint32_t* dist_out, uint32_t* nh_out,
+                    ospf_digest* digest_out) {
+  if (!c) return OSPF_E_INVAL;
+  if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  if (n_roots == 0) return OSPF_OK;
+  if (!roots) return fail(c, OSPF_E_INVAL, "null roots");
+  const uint64_t V = c->info.n_nodes;
+  uint32_t max_ign = 0;
+  for (uint32_t i = 0; i < n_roots; ++i) {
+    if (roots[i] >= V) return fail(c, OSPF_E_INVAL, "root out of range");
+    const uint32_t need = (c->h_dn_off[roots[i] + 1] - c->h_dn_off[roots[i]] + 31) / 32;
+    if (need > nh_words) return fail(c, OSPF_E_INVAL, "nh_words smaller than a root needs");
+    if (ig) {
+      if (ig->offsets[i + 1] < ig->offsets[i]) return fail(c, OSPF_E_INVAL, "ignore offsets");
+      max_ign = std::max(max_ign, ig->offsets[i + 1] - ig->offsets[i]);
+    }
+  }
+  if (max_ign > OSPF_MAX_IGNORED_PER_RUN)
+    return fail(c, OSPF_E_RANGE, "ignore list above OSPF_MAX_IGNORED_PER_RUN");
+  const uint32_t n_ign = ig ? ig->offsets[n_roots] : 0;
+  HIPCHK(c, hipSetDevice(c->device));
+
+  // chunk so one chunk's device outputs stay under ~2 GiB
+  const uint64_t per_root = V * 4ull * (1 + nh_words) + sizeof(ospf_digest);
+  uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_roots, (2ull << 30) / per_root));
+  const size_t sz_roots = align_up(chunk * 4ull, 256), sz_off = align_up((chunk + 1) * 4ull, 256),
+               sz_ids = align_up(std::max<uint32_t>(n_ign, 1) * 4ull, 256),
+               sz_dist = align_up(chunk * V * 4, 256), sz_nh = align_up(chunk * V * nh_words * 4, 256),
+               sz_dig = align_up(chunk * sizeof(ospf_digest), 256);
+  int rc = ensure(c, &c->d_stage, &c->stage_bytes, sz_roots + sz_off + sz_ids + sz_dist + sz_nh + sz_dig);
+  if (rc) return rc;
+  char* s = (char*)c->d_stage;
+  uint32_t* d_roots = (uint32_t*)s;
+  uint32_t* d_off = (uint32_t*)(s + sz_roots);
+  uint32_t* d_ids = (uint32_t*)(s + sz_roots + sz_off);
+  uint32_t* d_dist = (uint32_t*)(s + sz_roots + sz_off + sz_ids);
+  uint32_t* d_nh = (uint32_t*)(s + sz_roots + sz_off + sz_ids + sz_dist);
+  ospf_digest* d_dig = (ospf_digest*)(s + sz_roots + sz_off + sz_ids + sz_dist + sz_nh);
+  if (ig && n_ign) HIPCHK(c, hipMemcpy(d_ids, ig->link_ids, n_ign * 4ull, hipMemcpyHostToDevice));
+  std::vector<uint32_t> off(chunk + 1);
+  const uint32_t want = flags & (OSPF_WANT_DIST | OSPF_WANT_NH | OSPF_WANT_DIGEST);
+  for (uint32_t r0 = 0; r0 < n_roots; r0 += chunk) {
+    const uint32_t n = std::min(chunk, n_roots - r0);
+    HIPCHK(c, hipMemcpy(d_roots, roots + r0, n * 4ull, hipMemcpyHostToDevice));
+    if (ig) {
+      for (uint32_t i = 0; i <= n; ++i) off[i] = ig->offsets[r0 + i];
+      HIPCHK(c, hipMemcpy(d_off, off.data(), (n + 1) * 4ull, hipMemcpyHostToDevice));
+    }
+    rc = ospf_sssp_batch_dev(c, d_roots, n, ig ? d_off : nullptr, d_ids, max_ign, flags, nh_words,
+                             (want & OSPF_WANT_DIST) ? d_dist : nullptr,
+                             (want & OSPF_WANT_NH) ? d_nh : nullptr,
+                             (want & OSPF_WANT_DIGEST) ? d_dig : nullptr, nullptr);
+    if (rc) return rc;
+    rc = ospf_sync(c, nullptr);
+    if (rc) return rc;
+    if (want & OSPF_WANT_DIST)
+      HIPCHK(c, hipMemcpy(dist_out + (size_t)r0 * V, d_dist, n * V * 4, hipMemcpyDeviceToHost));
+    if (want & OSPF_WANT_NH)
+      HIPCHK(c, hipMemcpy(nh_out + (size_t)r0 * V * nh_words, d_nh, n * V * nh_words * 4ull,
+                          hipMemcpyDeviceToHost));
+    if (want & OSPF_WANT_DIGEST)
+      HIPCHK(c, hipMemcpy(digest_out + r0, d_dig, n * sizeof(ospf_digest), hipMemcpyDeviceToHost));
+  }
+  return OSPF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,130 @@
+"""Python face of libopenr_spf_hip (include/openr_spf.h).
+
+``Engine`` owns one ospf_ctx on a HIP device. ``run`` is the synchronous
+host-buffer batch (the drop-in ``ospf_sssp_batch``); ``run_dev`` queues a
+device-resident batch on a stream (raw device pointers, e.g. from torch
+tensors' ``data_ptr()``) — that is what bench.py times.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Optional, Sequence
+
+import numpy as np
+
+from . import _native as N
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"ospf error {code}: {msg}")
+        self.code = code
+
+
+def csr_struct(csr: Dict[str, np.ndarray]):
+    keep = {k: np.ascontiguousarray(v) for k, v in csr.items()}
+    s = N.ospf_csr(int(keep["row_ptr"].size - 1), int(keep["col"].size),
+                   keep["row_ptr"].ctypes.data, keep["col"].ctypes.data,
+                   keep["metric"].ctypes.data, keep["link_id"].ctypes.data,
+                   keep["twin"].ctypes.data, keep["edge_up"].ctypes.data,
+                   keep["no_transit"].ctypes.data)
+    return s, keep
+
+
+class Engine:
+    def __init__(self, device: int = 0):
+        self._L = N.engine()
+        h = C.c_void_p()
+        rc = self._L.ospf_open(device, C.byref(h))
+        if rc != 0:
+            raise EngineError(rc, f"ospf_open(device={device}) failed: no usable HIP device")
+        self._h = h
+        self.V = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.ospf_close(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def _check(self, rc: int):
+        if rc != 0:
+            raise EngineError(rc, self._L.ospf_last_error(self._h).decode())
+
+    def load(self, csr: Dict[str, np.ndarray], version: int = 1) -> None:
+        s, keep = csr_struct(csr)
+        self._check(self._L.ospf_load_graph(self._h, C.byref(s), version))
+        self.V = int(s.n_nodes)
+
+    def info(self) -> N.ospf_graph_info:
+        gi = N.ospf_graph_info()
+        self._check(self._L.ospf_graph_info_get(self._h, C.byref(gi)))
+        return gi
+
+    def root_neighbors(self, root: int) -> np.ndarray:
+        n = C.c_uint32()
+        self._check(self._L.ospf_root_neighbors(self._h, root, None, 0, C.byref(n)))
+        ids = np.zeros(max(n.value, 1), np.uint32)
+        self._check(self._L.ospf_root_neighbors(self._h, root, ids.ctypes.data, n.value,
+                                                C.byref(n)))
+        return ids[: n.value]
+
+    def nh_words(self, root: int) -> int:
+        return max(1, (len(self.root_neighbors(root)) + 31) // 32)
+
+    def plan_variant(self, nh_words: int, flags: int = 0) -> int:
+        v = C.c_int()
+        self._check(self._L.ospf_plan_variant(self._h, flags, nh_words, C.byref(v)))
+        return v.value
+
+    @property
+    def spf_runs(self) -> int:
+        return int(self._L.ospf_spf_runs(self._h))
+
+    def run(self, roots: Sequence[int], nh_words: int, *, hop_count: bool = False,
+            want_dist: bool = True, want_nh: bool = True, want_digest: bool = False,
+            ignore: Optional[Sequence[Sequence[int]]] = None):
+        """Synchronous batch. Returns dict with dist [n,V] u32, nh [n,V,W] u32,
+        digest [n,3] u64 (only the requested ones)."""
+        roots = np.ascontiguousarray(roots, np.uint32)
+        n, V, W = roots.size, self.V, nh_words
+        flags = (N.OSPF_HOP_COUNT if hop_count else 0) | \
+            (N.OSPF_WANT_DIST if want_dist else 0) | (N.OSPF_WANT_NH if want_nh else 0) | \
+            (N.OSPF_WANT_DIGEST if want_digest else 0)
+        dist = np.zeros((n, V), np.uint32) if want_dist else None
+        nh = np.zeros((n, V, W), np.uint32) if want_nh else None
+        dig = np.zeros((n, 3), np.uint64) if want_digest else None
+        ig_ref = None
+        if ignore is not None:
+            off = np.zeros(n + 1, np.uint32)
+            off[1:] = np.cumsum([len(x) for x in ignore])
+            ids = np.ascontiguousarray(np.concatenate(
+                [np.sort(np.asarray(x, np.uint32)) for x in ignore]) if off[-1] else
+                np.zeros(1, np.uint32), np.uint32)
+            ig = N.ospf_ignore(off.ctypes.data, ids.ctypes.data)
+            ig_ref = (C.byref(ig), off, ids)
+        self._check(self._L.ospf_sssp_batch(
+            self._h, roots.ctypes.data, n, ig_ref[0] if ig_ref else None, flags, W,
+            dist.ctypes.data if dist is not None else None,
+            nh.ctypes.data if nh is not None else None,
+            dig.ctypes.data if dig is not None else None))
+        out = {}
+        if want_dist:
+            out["dist"] = dist
+        if want_nh:
+            out["nh"] = nh
+        if want_digest:
+            out["digest"] = dig
+        return out
+
+    def run_dev(self, d_roots: int, n_roots: int, nh_words: int, *, flags: int,
+                d_dist: int = 0, d_nh: int = 0, d_digest: int = 0, stream: int = 0,
+                d_ign_off: int = 0, d_ign_ids: int = 0, max_ignored: int = 0) -> None:
+        """Queue a device-resident batch (raw device pointers) on `stream`."""
+        self._check(self._L.ospf_sssp_batch_dev(
+            self._h, d_roots, n_roots, d_ign_off or None, d_ign_ids or None, max_ignored,
+            flags, nh_words, d_dist or None, d_nh or None, d_digest or None, stream or None))
+
+    def sync(self, stream: int = 0) -> None:
+        self._check(self._L.ospf_sync(self._h, stream or None))

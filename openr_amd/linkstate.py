@@ -1,0 +1,157 @@
+"""Python face of the GPU-backed LinkState mirror (libopenr_decision).
+
+Method names follow openr/decision/LinkState.h (getSpfResult, getKthPaths,
+getMetricFromAToB, linksFromNode, isNodeOverloaded, updateAdjacencyDatabase,
+deleteAdjacencyDatabase); the snake_case helpers below are what the parity
+tests drive.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _native as N
+from .adjdb import AdjDbStream, change_array, changes_to_list
+
+
+class LinkStateError(RuntimeError):
+    pass
+
+
+def _parse_spf(t: str) -> Dict[str, Tuple[int, tuple, tuple]]:
+    out = {}
+    for ln in t.splitlines():
+        name, metric, nh, pl = ln.split("\t")
+        out[name] = (int(metric), tuple(x for x in nh.split(",") if x),
+                     tuple(x for x in pl.split(";") if x))
+    return out
+
+
+class LinkState:
+    """odl::LinkState over the MI355X SPF engine (device `device`)."""
+
+    def __init__(self, area: str = "0", device: int = 0, stream: Optional[AdjDbStream] = None):
+        self._L = N.decision()
+        h = C.c_void_p()
+        if self._L.odl_create(area.encode(), device, C.byref(h)) != 0:
+            raise LinkStateError("odl_create failed")
+        self._h = h
+        if stream is not None:
+            self.apply(stream)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._L.odl_destroy(self._h)
+            self._h = None
+
+    # ------------------------------------------------------------ plumbing
+    def _err(self) -> str:
+        return self._L.odl_last_error(self._h).decode()
+
+    def _take(self, p) -> str:
+        if not p:
+            raise LinkStateError(self._err())
+        s = C.cast(p, C.c_char_p).value.decode()
+        self._L.odl_free(p)
+        return s
+
+    # ------------------------------------------------------------ ingest
+    def apply(self, stream: AdjDbStream, first: int = 0, count: Optional[int] = None):
+        count = stream.n_dbs - first if count is None else count
+        ch = change_array(count)
+        if self._L.odl_apply(self._h, C.addressof(stream.struct), first, count,
+                             C.addressof(ch)) != 0:
+            raise LinkStateError(self._err())
+        return changes_to_list(ch, count)
+
+    updateAdjacencyDatabases = apply
+
+    # ------------------------------------------------------------ queries
+    def spf_text(self, root: str, use_link_metric: bool = True) -> str:
+        return self._take(self._L.odl_spf_text(self._h, root.encode(), int(use_link_metric)))
+
+    def spf(self, root: str, use_link_metric: bool = True):
+        return _parse_spf(self.spf_text(root, use_link_metric))
+
+    getSpfResult = spf
+
+    def kth_paths(self, src: str, dst: str, k: int) -> List[List[str]]:
+        t = self._take(self._L.odl_kth_paths_text(self._h, src.encode(), dst.encode(), k))
+        return [ln.split(",") for ln in t.splitlines()]
+
+    getKthPaths = kth_paths
+
+    def ksp2_text(self, src: str, dsts: Sequence[str]) -> str:
+        return self._take(self._L.odl_ksp2_text(self._h, src.encode(),
+                                                "\n".join(dsts).encode(), len(dsts)))
+
+    def links(self, node: str):
+        out = []
+        for ln in self._take(self._L.odl_links_text(self._h, node.encode())).splitlines():
+            key, m, up = ln.split("\t")
+            out.append((key, int(m), up == "1"))
+        return out
+
+    linksFromNode = links
+
+    def metric(self, a: str, b: str, use_link_metric: bool = True) -> Optional[int]:
+        v = self._L.odl_metric_a_to_b(self._h, a.encode(), b.encode(), int(use_link_metric))
+        if v == -2:
+            raise LinkStateError(self._err())
+        return None if v < 0 else v
+
+    getMetricFromAToB = metric
+
+    def is_overloaded(self, node: str) -> bool:
+        return bool(self._L.odl_is_overloaded(self._h, node.encode()))
+
+    isNodeOverloaded = is_overloaded
+
+    @property
+    def spf_runs(self) -> int:
+        return int(self._L.odl_spf_runs(self._h))
+
+    def num_nodes(self) -> int:
+        return int(self._L.odl_num_nodes(self._h))
+
+    def num_links(self) -> int:
+        return int(self._L.odl_num_links(self._h))
+
+    # ------------------------------------------------------------ batches
+    def digests(self, roots: Sequence[str], use_link_metric: bool = True) -> np.ndarray:
+        out = np.zeros((len(roots), 3), np.uint64)
+        if self._L.odl_spf_digests(self._h, "\n".join(roots).encode(), len(roots),
+                                   int(use_link_metric), out.ctypes.data) != 0:
+            raise LinkStateError(self._err())
+        return out
+
+    def prefetch(self, roots: Sequence[str], use_link_metric: bool = True) -> None:
+        if self._L.odl_spf_prefetch(self._h, "\n".join(roots).encode(), len(roots),
+                                    int(use_link_metric)) != 0:
+            raise LinkStateError(self._err())
+
+    # ------------------------------------------------------------ snapshot
+    def csr(self) -> Dict[str, np.ndarray]:
+        V, E = C.c_uint32(), C.c_uint32()
+        if self._L.odl_csr_size(self._h, C.byref(V), C.byref(E)) != 0:
+            raise LinkStateError(self._err())
+        V, E = V.value, E.value
+        a = dict(row_ptr=np.zeros(V + 1, np.uint32), col=np.zeros(E, np.uint32),
+                 metric=np.zeros(E, np.uint32), link_id=np.zeros(E, np.uint32),
+                 twin=np.zeros(E, np.uint32), edge_up=np.zeros(E, np.uint8),
+                 no_transit=np.zeros(V, np.uint8), link_rank=np.zeros(E, np.uint32))
+        ptrs = [a[k].ctypes.data if a[k].size else None for k in
+                ("row_ptr", "col", "metric", "link_id", "twin", "edge_up", "no_transit",
+                 "link_rank")]
+        if self._L.odl_csr_export(self._h, *ptrs) != 0:
+            raise LinkStateError(self._err())
+        return a
+
+    def node_names(self) -> List[str]:
+        n = self.num_nodes()
+        return [self._L.odl_node_name(self._h, i).decode() for i in range(n)]
+
+    def node_id(self, name: str) -> int:
+        return int(self._L.odl_node_id(self._h, name.encode()))

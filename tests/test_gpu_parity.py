@@ -1,0 +1,230 @@
+"""GPU parity: the MI355X engine (through the C ABI) vs the CPU oracle and the
+reference's own fixtures. Bit-exact: integer distances, next-hop name sets,
+pathLinks order, KSP2 paths, digests. Run with ``-m gpu`` on an MI355X."""
+import os
+
+import numpy as np
+import pytest
+
+from golden_eval import ProductLS, load_fixtures, run_fixture
+from oracle import Oracle
+from openr_amd import topology as T
+from openr_amd.adjdb import AdjDb, AdjDbStream, create_adjacency
+from openr_amd.engine import Engine, EngineError
+from openr_amd.linkstate import LinkState
+
+pytestmark = pytest.mark.gpu
+
+FIXTURES = load_fixtures()
+
+
+@pytest.fixture(params=["auto", "1", "2"])
+def variant(request, monkeypatch):
+    """Run each parity test with the planner's choice and with the HBM-state
+    kernel variants forced (OSPF_FORCE_VARIANT)."""
+    if request.param == "auto":
+        monkeypatch.delenv("OSPF_FORCE_VARIANT", raising=False)
+    else:
+        monkeypatch.setenv("OSPF_FORCE_VARIANT", request.param)
+    return request.param
+
+
+@pytest.mark.parametrize("fx", FIXTURES, ids=[f["name"] for f in FIXTURES])
+def test_reference_fixture_on_gpu(fx, variant):
+    assert run_fixture(fx, ProductLS) > 0
+
+
+def random_stream(seed, n=40, p=0.15, parallel=0.2, overload=0.1, down=0.1, wmax=20,
+                  unit=False):
+    rng = np.random.default_rng(seed)
+    names = [f"r{int(x)}" for x in rng.permutation(10 * n)[:n]]
+    adjs = {nm: [] for nm in names}
+    k = 0
+    for i in range(n):
+        for j in range(i + 1, n):
+            if rng.random() > p:
+                continue
+            for _ in range(2 if rng.random() < parallel else 1):
+                a, b = names[i], names[j]
+                ia, ib = f"{a}-{b}-{k}", f"{b}-{a}-{k}"
+                k += 1
+                m1 = 1 if unit else int(rng.integers(1, wmax + 1))
+                m2 = 1 if unit else int(rng.integers(1, wmax + 1))
+                adjs[a].append(create_adjacency(b, ia, ib, m1, overloaded=bool(rng.random() < down)))
+                adjs[b].append(create_adjacency(a, ib, ia, m2))
+    dbs = [AdjDb(nm, adjs[nm], i + 1, overloaded=bool(rng.random() < overload))
+           for i, nm in enumerate(names)]
+    return AdjDbStream.from_dbs([dbs[i] for i in rng.permutation(n)]), names
+
+
+def both(stream):
+    o, p = Oracle(), LinkState()
+    assert o.apply(stream) == p.apply(stream)
+    return o, p
+
+
+@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("unit", [False, True])
+def test_random_graph_all_roots_spf_text(seed, unit, variant):
+    st, names = random_stream(seed, unit=unit)
+    o, p = both(st)
+    p.prefetch(names)  # one batched engine launch for every root
+    for r in names:
+        assert p.spf_text(r) == o.spf_text(r), r
+        assert p.spf_text(r, False) == o.spf_text(r, False), r
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_graph_ksp2_batch(seed, variant):
+    st, names = random_stream(100 + seed, n=30, p=0.25)
+    o, p = both(st)
+    for src in names[:5]:
+        assert p.ksp2_text(src, names) == o.ksp2_text(src, names), src
+
+
+def test_unknown_and_isolated_roots():
+    st, names = random_stream(7)
+    extra = AdjDbStream.from_dbs([AdjDb("zz-isolated", [], 99)])
+    o, p = both(st)
+    assert o.apply(extra) == p.apply(extra)
+    for r in ("zz-isolated", "not-a-node"):
+        assert p.spf_text(r) == o.spf_text(r)
+        assert p.kth_paths(r, names[0], 2) == o.kth_paths(r, names[0], 2)
+
+
+def test_incremental_updates_keep_parity():
+    """Topology changes invalidate the memo and the device snapshot
+    (LinkState.cpp:721-724); non-topology updates keep the memo."""
+    st, names = random_stream(21, n=30)
+    o, p = both(st)
+    rng = np.random.default_rng(5)
+    dbs = st.to_dbs()
+    for step in range(6):
+        db = dbs[int(rng.integers(len(dbs)))]
+        if step % 3 == 0:
+            db.overloaded = not db.overloaded
+        elif step % 3 == 1 and db.adjs:
+            a = db.adjs[int(rng.integers(len(db.adjs)))]
+            a.metric = int(rng.integers(1, 30))
+        else:
+            db.node_label += 1000
+        upd = AdjDbStream.from_dbs([db])
+        assert o.apply(upd) == p.apply(upd)
+        for r in names[:8]:
+            assert p.spf_text(r) == o.spf_text(r)
+    assert p.spf_runs == o.spf_runs
+
+
+def test_grid31_all_sources_digests():
+    st = T.grid(31)
+    o, p = both(st)
+    roots = [str(i) for i in range(31 * 31)]
+    assert np.array_equal(p.digests(roots), o.digests(roots, threads=8))
+    # Manhattan distance sum check from the reference grid fixture semantics
+    d = p.digests(["0"])[0]
+    assert int(d[0]) == 961 and int(d[1]) == sum(r + c for r in range(31) for c in range(31))
+
+
+def test_grid31_hop_count_and_weighted():
+    st = T.grid(31, weighted_seed=3)
+    o, p = both(st)
+    roots = [str(i) for i in range(0, 961, 7)]
+    assert np.array_equal(p.digests(roots), o.digests(roots, threads=8))
+    assert np.array_equal(p.digests(roots, False), o.digests(roots, False, threads=8))
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+def test_fabric_sampled_digests(weighted, variant):
+    st = T.fabric(pods=12, planes=8, weighted_seed=7 if weighted else None)
+    o, p = both(st)
+    names = p.node_names()
+    rng = np.random.default_rng(0x5eed)
+    roots = [names[i] for i in rng.choice(len(names), 24, replace=False)]
+    roots += ["1-0-0", "2-0-0", "3-0-0"]  # one SSW, FSW, RSW
+    assert np.array_equal(p.digests(roots), o.digests(roots, threads=8))
+    for r in roots[-3:]:
+        assert p.spf_text(r) == o.spf_text(r)
+
+
+def test_fabric_reference_quirk():
+    st = T.fabric(pods=6, planes=4, reference_quirk=True)
+    o, p = both(st)
+    for r in ("1-0-0", "2-3-1", "3-5-7"):
+        assert p.spf_text(r) == o.spf_text(r)
+
+
+def test_mesh_sampled_digests():
+    st = T.mesh(3000, seed=42)
+    o, p = both(st)
+    names = p.node_names()
+    rng = np.random.default_rng(0x5eed)
+    roots = [names[i] for i in rng.choice(len(names), 16, replace=False)]
+    assert np.array_equal(p.digests(roots), o.digests(roots, threads=8))
+
+
+def test_fabric_ksp2_batch_from_rsw():
+    st = T.fabric(pods=6, planes=4)
+    o, p = both(st)
+    dsts = p.node_names()[::7]
+    assert p.ksp2_text("3-0-0", dsts) == o.ksp2_text("3-0-0", dsts)
+    assert p.spf_runs == o.spf_runs
+
+
+# ------------------------------------------------------------ engine ABI
+def _csr_of(stream):
+    p = LinkState(stream=stream)
+    return p, p.csr()
+
+
+def test_engine_direct_batch_matches_linkstate():
+    p, csr = _csr_of(T.grid(12))
+    eng = Engine(0)
+    eng.load(csr)
+    roots = np.arange(144, dtype=np.uint32)
+    out = eng.run(roots, 1, want_digest=True)
+    names = p.node_names()
+    assert np.array_equal(out["digest"], p.digests(names))
+    # dist of root 0 in a 12x12 grid is the Manhattan distance
+    r, c = np.divmod(np.arange(144), 12)
+    assert np.array_equal(out["dist"][0], (r + c).astype(np.uint32))
+    assert eng.spf_runs == 144
+
+
+def test_engine_rejects_out_of_contract():
+    p, csr = _csr_of(T.grid(4))
+    eng = Engine(0)
+    bad = dict(csr)
+    bad["metric"] = csr["metric"].copy()
+    bad["metric"][0] = 0
+    with pytest.raises(EngineError) as ei:
+        eng.load(bad)
+    assert ei.value.code == -4
+    eng.load(csr)
+    p2, csr2 = _csr_of(T.fabric(pods=2, planes=4))
+    eng.load(csr2)
+    ssw = p2.node_id("1-0-0")
+    with pytest.raises(EngineError):  # nh_words too small for a root
+        eng.run([ssw], 0)
+
+
+def test_engine_device_api_and_error_word():
+    torch = pytest.importorskip("torch")
+    p, csr = _csr_of(T.fabric(pods=40, planes=8))
+    eng = Engine(0)
+    eng.load(csr)
+    V = eng.V
+    names = p.node_names()
+    rsw = [p.node_id(f"3-{i}-0") for i in range(16)]
+    d_roots = torch.tensor(rsw, dtype=torch.int32, device="cuda")
+    d_dig = torch.zeros((16, 3), dtype=torch.int64, device="cuda")
+    d_dist = torch.zeros((16, V), dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    eng.run_dev(d_roots.data_ptr(), 16, 1, flags=0x2 | 0x8, d_dist=d_dist.data_ptr(),
+                d_digest=d_dig.data_ptr(), stream=s)
+    eng.sync(s)
+    want = p.digests([names[i] for i in rsw])
+    assert np.array_equal(d_dig.cpu().numpy().view(np.uint64), want)
+    ssw = torch.tensor([p.node_id("1-0-0")], dtype=torch.int32, device="cuda")
+    eng.run_dev(ssw.data_ptr(), 1, 1, flags=0x8, d_digest=d_dig.data_ptr(), stream=s)
+    with pytest.raises(EngineError):
+        eng.sync(s)
