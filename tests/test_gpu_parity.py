@@ -184,9 +184,11 @@ def test_engine_direct_batch_matches_linkstate():
     out = eng.run(roots, 1, want_digest=True)
     names = p.node_names()
     assert np.array_equal(out["digest"], p.digests(names))
-    # dist of root 0 in a 12x12 grid is the Manhattan distance
-    r, c = np.divmod(np.arange(144), 12)
-    assert np.array_equal(out["dist"][0], (r + c).astype(np.uint32))
+    # dist from node "0" in a 12x12 grid is the Manhattan distance (ids are
+    # name ranks: "0" < "1" < "10" < ...)
+    root0 = names.index("0")
+    r, c = np.divmod(np.array([int(n) for n in names]), 12)
+    assert np.array_equal(out["dist"][root0], (r + c).astype(np.uint32))
     assert eng.spf_runs == 144
 
 
