@@ -103,6 +103,10 @@ def main():
     eng = Engine(local)
     eng.load(csr)
     V, E = eng.V, int(csr["col"].size)
+    props = torch.cuda.get_device_properties(local)
+    log(f"[rank {rank}] {props.name} CUs={props.multi_processor_count} "
+        f"lds/block={getattr(props, 'shared_memory_per_block', '?')} "
+        f"lds/cu={getattr(props, 'shared_memory_per_multiprocessor', '?')}")
     log(f"[rank {rank}] {desc}: V={V} E_dir={E} setup {time.time() - t0:.1f}s")
 
     # all-sources root permutation, grouped by next-hop width class

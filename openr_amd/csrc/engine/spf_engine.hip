@@ -19,6 +19,7 @@
 struct ospf_ctx {
   int device = 0;
   size_t lds_limit = 64 * 1024;
+  int lds_attr = 0;
   int n_cu = 256;
   std::string err;
   uint64_t spf_runs = 0;
@@ -78,35 +79,45 @@ struct Plan {
   uint32_t nbr_cap, ign_cap;
 };
 
-Plan make_plan(const ospf_ctx* c, uint32_t W, uint32_t ign_cap) {
+Plan make_plan(const ospf_ctx* c, uint32_t W, uint32_t ign_cap, bool unit) {
   Plan p{};
   const size_t V = c->info.n_nodes;
   p.nbr_cap = (uint32_t)align_up(std::max<uint32_t>(c->max_dn, 1), 4);
   p.ign_cap = (uint32_t)align_up(ign_cap, 4);
   const size_t head = (32 + p.nbr_cap + p.ign_cap) * 4;
-  const size_t full = head + V * 4 + V * W * 4;
-  const size_t half = head + V * 4;
-  if (full <= c->lds_limit) {
-    p.variant = 0;
-    p.lds = full;
-  } else if (half <= c->lds_limit) {
-    p.variant = 1;
-    p.lds = half;
+  const size_t full = head + V * 4 + V * W * 4;   // variant 0
+  const size_t half = head + V * 4;               // variant 1
+  const size_t bw = (((V + 31) / 32) + 1) & ~(size_t)1;
+  const size_t bfs = head + 3 * bw * 4;            // variant 4
+  const size_t bfs_nh = bfs + ((V + 3) / 4) * 4;   // variant 3
+  const size_t lim = c->lds_limit;
+  auto fits = [&](int v) {
+    switch (v) {
+      case 0: return full <= lim;
+      case 1: return half <= lim;
+      case 2: return true;
+      case 3: return unit && bfs_nh <= lim;
+      case 4: return unit && bfs <= lim;
+    }
+    return false;
+  };
+  if (unit) {
+    p.variant = (W == 1 && fits(3)) ? 3 : fits(4) ? 4 : 2;
   } else {
-    p.variant = 2;
-    p.lds = head;
+    p.variant = fits(0) ? 0 : fits(1) ? 1 : 2;
   }
-  // test/benchmark knob: OSPF_FORCE_VARIANT=1|2 forces the HBM-state
-  // variants on graphs that would fit in LDS (never a smaller variant than
-  // what fits).
+  // test/benchmark knob: OSPF_FORCE_VARIANT=0..4 forces a kernel variant when
+  // its state fits (e.g. the HBM-state Dial kernel on a small graph).
   if (const char* f = getenv("OSPF_FORCE_VARIANT")) {
     const int want = atoi(f);
-    if (want > p.variant && want <= 2) {
-      p.variant = want;
-      p.lds = want == 1 ? half : head;
-    }
+    if (want >= 0 && want <= 4 && fits(want)) p.variant = want;
   }
-  p.block = V >= 4096 ? 512 : 256;
+  const size_t ldsz[5] = {full, half, head, bfs_nh, bfs};
+  p.lds = ldsz[p.variant];
+  if (p.variant >= 3)
+    p.block = p.lds > 80 * 1024 ? 1024 : (V >= 4096 ? 512 : 256);
+  else
+    p.block = V >= 4096 ? 512 : 256;
   return p;
 }
 
@@ -130,8 +141,9 @@ int ospf_open(int device, ospf_ctx** out) {
   int lds = 0, cu = 0;
   hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device);
   hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device);
-  // keep 1 KiB for the kernel's static LDS (digest reduction)
+  // keep 1 KiB for the kernels' static LDS (digest reduction)
   if (lds > 2048) c->lds_limit = (size_t)lds - 1024;
+  c->lds_attr = lds;
   if (cu > 0) c->n_cu = cu;
   if (hipMalloc((void**)&c->d_err, sizeof(uint32_t)) != hipSuccess ||
       hipMemset(c->d_err, 0, sizeof(uint32_t)) != hipSuccess) {
@@ -279,8 +291,8 @@ int ospf_root_neighbors(const ospf_ctx* c, uint32_t root, uint32_t* ids, uint32_
 int ospf_plan_variant(const ospf_ctx* c, uint32_t flags, uint32_t nh_words, int* variant) {
   if (!c || !variant) return OSPF_E_INVAL;
   if (!c->loaded) return OSPF_E_NOGRAPH;
-  (void)flags;
-  *variant = make_plan(c, std::max<uint32_t>(nh_words, 1), 0).variant;
+  const bool unit = (flags & OSPF_HOP_COUNT) || c->info.unit_metric;
+  *variant = make_plan(c, std::max<uint32_t>(nh_words, 1), 0, unit).variant;
   return OSPF_OK;
 }
 
@@ -309,10 +321,11 @@ int ospf_sssp_batch_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n_roots,
     return fail(c, OSPF_E_RANGE, "u32 distance overflow possible (max_metric * (V-1))");
   const bool unit = hop || c->info.unit_metric;
 
-  const Plan p = make_plan(c, nh_words, ign ? std::max<uint32_t>(max_ignored, 1) : 0);
-  // scratch for state the caller does not want back
+  const Plan p = make_plan(c, nh_words, ign ? std::max<uint32_t>(max_ignored, 1) : 0, unit);
+  // scratch for state the caller does not want back (HBM-state variants
+  // keep dist / next-hops in the output rows while they run)
   size_t need = 0;
-  const bool dist_scratch = (p.variant == 2) && !(flags & OSPF_WANT_DIST);
+  const bool dist_scratch = (p.variant >= 2) && !(flags & OSPF_WANT_DIST);
   const bool nh_scratch = (p.variant >= 1) && !(flags & OSPF_WANT_NH);
   if (dist_scratch) need += align_up(n_roots * V * 4, 256);
   if (nh_scratch) need += align_up(n_roots * V * nh_words * 4ull, 256);
@@ -338,12 +351,14 @@ int ospf_sssp_batch_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n_roots,
     sp += align_up(n_roots * V * 4, 256);
   }
   if (nh_scratch) a.nh = (uint32_t*)sp;
-  if (!(flags & OSPF_WANT_DIST) && p.variant != 2) a.dist = nullptr;
+  if (!(flags & OSPF_WANT_DIST) && p.variant < 2) a.dist = nullptr;
   if (!(flags & OSPF_WANT_NH) && p.variant == 0) a.nh = nullptr;
 
   HIPCHK(c, hipSetDevice(c->device));
-  hipError_t e = ospf::launch_spf(p.variant, unit, ign, c->g, a, n_roots, p.block, p.lds,
-                                  (hipStream_t)stream);
+  hipError_t e = p.variant >= 3
+      ? ospf::launch_bfs(p.variant == 3, ign, c->g, a, n_roots, p.block, p.lds, (hipStream_t)stream)
+      : ospf::launch_spf(p.variant, unit, ign, c->g, a, n_roots, p.block, p.lds,
+                         (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(c, e, "launch_spf");
   c->spf_runs += n_roots;
   return OSPF_OK;

@@ -41,8 +41,15 @@ struct RunArgs {
   uint32_t* err;            // device error word (bit0: nh words, bit1: ignore cap)
 };
 
-// variant: 0 = LDS dist + LDS nh, 1 = LDS dist + HBM nh, 2 = HBM dist + HBM nh
+// Dial kernels (spf_kernels.hip), any metric:
+//   variant 0 = LDS dist + LDS nh, 1 = LDS dist + HBM nh, 2 = HBM dist + HBM nh
 hipError_t launch_spf(int variant, bool unit, bool ign, const DevGraph& g, const RunArgs& a,
                       uint32_t n_roots, uint32_t block, size_t lds_bytes, hipStream_t s);
+
+// BFS kernel (spf_bfs.hip), unit metric / hop count, LDS bitmaps:
+//   nh_lds = variant 3 (byte next-hops in LDS for roots with <= 8 neighbours),
+//   otherwise variant 4 (next-hops in HBM).
+hipError_t launch_bfs(bool nh_lds, bool ign, const DevGraph& g, const RunArgs& a, uint32_t n,
+                      uint32_t block, size_t lds, hipStream_t s);
 
 }  // namespace ospf

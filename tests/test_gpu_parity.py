@@ -18,10 +18,12 @@ pytestmark = pytest.mark.gpu
 FIXTURES = load_fixtures()
 
 
-@pytest.fixture(params=["auto", "1", "2"])
+@pytest.fixture(params=["auto", "0", "1", "2", "4"])
 def variant(request, monkeypatch):
-    """Run each parity test with the planner's choice and with the HBM-state
-    kernel variants forced (OSPF_FORCE_VARIANT)."""
+    """Run each parity test with the planner's choice and with every other
+    kernel variant forced where its state fits (OSPF_FORCE_VARIANT): 0/1/2 =
+    Dial kernel (LDS / mixed / HBM state), 3/4 = BFS kernel (LDS bitmaps,
+    byte next-hops in LDS / next-hops in HBM; unit metric only)."""
     if request.param == "auto":
         monkeypatch.delenv("OSPF_FORCE_VARIANT", raising=False)
     else:
