@@ -522,7 +522,7 @@ std::vector<ospf_digest> LinkState::spfDigests(const std::vector<std::string>& r
     ++spfRuns_;
     auto id = csr_.ids.find(roots[i]);
     if (id == csr_.ids.end()) {
-      // root without a database: result {root: 0}; digest as the oracle's
+      // root without a database: result {root: 0}; node_term(0xFFFFFFFF, 0)
       uint64_t x = (0xFFFFFFFFull << 32);
       x ^= x >> 30;
       x *= 0xbf58476d1ce4e5b9ULL;

@@ -1,25 +1,30 @@
 // spf_bfs.hip — unit-metric / hop-count SPF for large graphs (gfx950).
 //
-// One workgroup per SPF run. Same result as LinkState::runSpf
-// (openr/decision/LinkState.cpp:836-911) when every usable weight is 1
-// (fabric and grid topologies, or useLinkMetric=false): Dijkstra's settle
-// order by (dist, name) degenerates to BFS levels, and the ECMP next-hop set of
-// a node at level d+1 is the OR over its usable in-edges from transit nodes
-// of level d (LinkState.cpp:885-901).
+// One workgroup per (SPF run, next-hop slice). Same result as
+// LinkState::runSpf (openr/decision/LinkState.cpp:836-911) when every usable
+// weight is 1 (fabric and grid topologies, or useLinkMetric=false): the
+// (dist, name) settle order degenerates to BFS levels, and the ECMP next-hop
+// set of a node at level d+1 is the OR over its usable in-edges from transit
+// nodes of level d (LinkState.cpp:885-901).
 //
 // State lives in LDS as three V-bit bitmaps (visited, current level, next
 // level) — 37.5 KB at V = 100k — so the per-edge random accesses of the BFS
-// hit LDS, not HBM. Each level picks its direction (Beamer-style):
+// hit LDS, not HBM. Each level picks its direction (Beamer-style) from exact
+// edge masses:
 //   push  (top-down):  frontier nodes scan out-edges, mark unvisited heads;
 //   pull  (bottom-up): unvisited nodes scan in-edges for frontier tails.
 // Next-hop sets:
 //   NH_LDS (root has <= 8 distinct neighbours, e.g. every rack switch): one
-//     byte per node in LDS; push ORs it forward with 32-bit LDS atomics, pull
-//     ORs it in registers — one pass per level either way.
-//   otherwise: next-hops live in the HBM output row; push only marks the next
-//     level and a pull over the new level ORs the tails' words.
-// dist / nh rows are written once per node (masked coalesced stores), the
-// digest is accumulated in the same pass.
+//     byte per node in LDS (100 KB at V = 100k); push ORs it forward with
+//     32-bit LDS atomics, pull ORs it in registers: one pass per level.
+//   otherwise next-hops live in the HBM output row: push marks the next level
+//     and a pull over it ORs the tails' words in registers. Rows wider than 4
+//     words (a 1,781-port spine has 56) are cut into 4-word slices, one
+//     workgroup each: OR is bitwise, so slices are independent runs that share
+//     only the (recomputed) traversal. Slice 0 writes dist.
+// dist / next-hop rows are written once per node (masked coalesced stores);
+// the digest (a sum of per-node and per-(node, next-hop) terms, so slices add
+// up) is folded into the same pass.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -32,15 +37,7 @@ constexpr uint32_t kInf = 0xFFFFFFFFu;
 constexpr uint32_t kDown = 0x80000000u;
 constexpr int kWave = 64;
 constexpr uint32_t kCoopDeg = 32;
-
-__device__ __forceinline__ uint64_t mix(uint64_t x) {
-  x ^= x >> 30;
-  x *= 0xbf58476d1ce4e5b9ULL;
-  x ^= x >> 27;
-  x *= 0x94d049bb133111ebULL;
-  x ^= x >> 31;
-  return x;
-}
+constexpr uint32_t kSliceWords = 4;
 
 __device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* a, uint32_t n, uint32_t key) {
   uint32_t lo = 0, hi = n;
@@ -61,25 +58,25 @@ __device__ __forceinline__ uint64_t wsum(uint64_t x) {
   for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, kWave);
   return x;
 }
-
 __device__ __forceinline__ bool bit(const uint32_t* bm, uint32_t v) {
   return (bm[v >> 5] >> (v & 31)) & 1u;
 }
 
-template <bool NH_LDS, bool IGN, int WF>
+template <bool NH_LDS, bool IGN>
 struct Bfs {
   const DevGraph& g;
   const RunArgs& a;
   uint32_t root, V, W, nwords;
-  uint32_t *vis, *cur, *nxt;   // LDS bitmaps
-  uint32_t* nhb;               // NH_LDS: one byte per node, packed in words
-  uint32_t* nh_out;            // HBM next-hop row (W words per node)
-  uint32_t* dist_out;          // HBM dist row
+  uint32_t w0, ws;              // slice: words [w0, w0 + ws) of each row
+  bool slice0;
+  uint32_t *vis, *cur, *nxt;    // LDS bitmaps
+  uint32_t* nhb;                // NH_LDS: one byte per node, packed in words
+  uint32_t* nh_out;             // HBM next-hop row base (W words per node)
+  uint32_t* dist_out;           // HBM dist row
   const uint32_t* nbr;
   uint32_t nbr_n;
   const uint32_t* ign;
   uint32_t ign_n;
-  uint32_t* cnt;               // LDS counters
 
   __device__ Bfs(const DevGraph& g_, const RunArgs& a_) : g(g_), a(a_) {}
 
@@ -100,11 +97,14 @@ struct Bfs {
   __device__ __forceinline__ uint32_t nh_byte(uint32_t v) const {
     return (nhb[v >> 2] >> (8 * (v & 3))) & 0xFFu;
   }
-  __device__ __forceinline__ uint32_t root_bit(uint32_t v) const {
-    return lower_bound_u32(nbr, nbr_n, v);
+  __device__ __forceinline__ uint32_t* row(uint32_t v) const {
+    return nh_out + (size_t)v * W + w0;
+  }
+  // bit of root-neighbour v inside this slice (>= 32*ws: not in slice)
+  __device__ __forceinline__ uint32_t slice_bit(uint32_t v) const {
+    return lower_bound_u32(nbr, nbr_n, v) - 32u * w0;
   }
 
-  // ---------------- push: u (level d, transit) -> mark unvisited heads
   __device__ __forceinline__ void push_edge(uint32_t u, uint32_t e, uint32_t nbu) {
     const uint32_t cx = g.colx[e];
     if (!usable(e, cx)) return;
@@ -112,55 +112,38 @@ struct Bfs {
     if (bit(vis, x)) return;
     atomicOr(&nxt[x >> 5], 1u << (x & 31));
     if constexpr (NH_LDS) {
-      const uint32_t val = (u == root) ? (1u << root_bit(x)) : nbu;
+      const uint32_t val = (u == root) ? (1u << slice_bit(x)) : nbu;
       atomicOr(&nhb[x >> 2], val << (8 * (x & 3)));
     }
   }
 
-  // ---------------- pull: v collects next-hops from level-d tails
-  // returns true when v has at least one tight transit tail
+  // v collects next-hops from level-d tails; true when it has a tight tail
   template <bool COOP>
   __device__ __forceinline__ bool pull_node(uint32_t v, uint32_t beg, uint32_t end, int lane,
                                             uint32_t* acc) {
     bool any = false;
-    bool zeroed = COOP;  // the cooperative path zeroes before calling
-    const uint32_t step = COOP ? kWave : 1;
-    for (uint32_t e = beg + (COOP ? lane : 0); e < end; e += step) {
+    for (uint32_t e = beg + (COOP ? lane : 0); e < end; e += (COOP ? kWave : 1)) {
       const uint32_t cx = g.colx[e];
       if (!usable(e, cx)) continue;
       const uint32_t u = cx;
       if (!bit(cur, u) || !transit(u)) continue;
       any = true;
-      if constexpr (!NH_LDS && WF == 0 && !COOP) {
-        if (!zeroed) {
-          for (uint32_t w = 0; w < W; ++w) nh_out[(size_t)v * W + w] = 0;
-          zeroed = true;
-        }
-      }
       if (u == root) {
-        const uint32_t b = root_bit(v);
+        const uint32_t b = slice_bit(v);
         if constexpr (NH_LDS) {
           acc[0] |= 1u << b;
-        } else if constexpr (WF > 0) {
-#pragma unroll
-          for (int w = 0; w < WF; ++w) acc[w] |= ((b >> 5) == (uint32_t)w) ? (1u << (b & 31)) : 0u;
         } else {
-          atomicOr(&nh_out[(size_t)v * W + (b >> 5)], 1u << (b & 31));
+#pragma unroll
+          for (uint32_t w = 0; w < kSliceWords; ++w)
+            acc[w] |= ((b >> 5) == w) ? (1u << (b & 31)) : 0u;
         }
+      } else if constexpr (NH_LDS) {
+        acc[0] |= nh_byte(u);
       } else {
-        if constexpr (NH_LDS) {
-          acc[0] |= nh_byte(u);
-        } else if constexpr (WF > 0) {
-          const uint32_t* s = nh_out + (size_t)u * W;
+        const uint32_t* s = row(u);
 #pragma unroll
-          for (int w = 0; w < WF; ++w) if ((uint32_t)w < W) acc[w] |= s[w];
-        } else {
-          const uint32_t* s = nh_out + (size_t)u * W;
-          for (uint32_t w = 0; w < W; ++w) {
-            const uint32_t x = s[w];
-            if (x) atomicOr(&nh_out[(size_t)v * W + w], x);
-          }
-        }
+        for (uint32_t w = 0; w < kSliceWords; ++w)
+          if (w < ws) acc[w] |= s[w];
       }
     }
     return any;
@@ -169,9 +152,11 @@ struct Bfs {
   __device__ __forceinline__ void store_nh(uint32_t v, const uint32_t* acc) {
     if constexpr (NH_LDS) {
       atomicOr(&nhb[v >> 2], acc[0] << (8 * (v & 3)));
-    } else if constexpr (WF > 0) {
+    } else {
+      uint32_t* r = row(v);
 #pragma unroll
-      for (int w = 0; w < WF; ++w) if ((uint32_t)w < W) nh_out[(size_t)v * W + w] = acc[w];
+      for (uint32_t w = 0; w < kSliceWords; ++w)
+        if (w < ws) r[w] = acc[w];
     }
   }
 
@@ -180,6 +165,10 @@ struct Bfs {
   __device__ void pull_level(int lane, int wave, int nwaves) {
     const uint32_t nchunks = (V + 63) / 64;
     for (uint32_t c = wave; c < nchunks; c += nwaves) {
+      if (!PULL_ALL) {
+        const uint32_t w1 = (c * 2 + 1 < nwords) ? nxt[c * 2 + 1] : 0u;
+        if ((nxt[c * 2] | w1) == 0) continue;
+      }
       const uint32_t v = c * 64 + lane;
       bool act = v < V;
       if (act) act = PULL_ALL ? !bit(vis, v) : bit(nxt, v);
@@ -190,9 +179,8 @@ struct Bfs {
       }
       const bool big = act && (end - beg) > kCoopDeg;
       if (act && !big) {
-        uint32_t acc[WF > 0 ? WF : 1] = {};
-        const bool any = pull_node<false>(v, beg, end, lane, acc);
-        if (any) {
+        uint32_t acc[kSliceWords] = {0u, 0u, 0u, 0u};
+        if (pull_node<false>(v, beg, end, lane, acc)) {
           store_nh(v, acc);
           if (PULL_ALL) atomicOr(&nxt[v >> 5], 1u << (v & 31));
         }
@@ -203,26 +191,10 @@ struct Bfs {
         bm &= bm - 1;
         const uint32_t bv = __shfl(v, l, kWave), bb = __shfl(beg, l, kWave),
                        be = __shfl(end, l, kWave);
-        uint32_t acc[WF > 0 ? WF : 1] = {};
-        if constexpr (!NH_LDS && WF == 0) {
-          // wide rows: only zero (then OR into HBM) when the node has a tail
-          bool has = false;
-          for (uint32_t e = bb + lane; e < be && !has; e += kWave) {
-            const uint32_t cx = g.colx[e];
-            has = usable(e, cx) && bit(cur, cx) && transit(cx);
-          }
-          if (__ballot(has) == 0) continue;
-          for (uint32_t w = lane; w < W; w += kWave) nh_out[(size_t)bv * W + w] = 0;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        }
-        const bool any_l = pull_node<true>(bv, bb, be, lane, acc);
-        const bool any = __ballot(any_l) != 0;
-        if constexpr (NH_LDS || WF > 0) {
+        uint32_t acc[kSliceWords] = {0u, 0u, 0u, 0u};
+        const bool any = __ballot(pull_node<true>(bv, bb, be, lane, acc)) != 0;
 #pragma unroll
-          for (int w = 0; w < (WF > 0 ? WF : 1); ++w) acc[w] = wor(acc[w]);
-        }
+        for (uint32_t w = 0; w < kSliceWords; ++w) acc[w] = wor(acc[w]);
         if (any && lane == 0) {
           store_nh(bv, acc);
           if (PULL_ALL) atomicOr(&nxt[bv >> 5], 1u << (bv & 31));
@@ -235,11 +207,10 @@ struct Bfs {
   __device__ void push_level(int lane, int wave, int nwaves) {
     const uint32_t nchunks = (V + 63) / 64;
     for (uint32_t c = wave; c < nchunks; c += nwaves) {
-      // skip empty chunks cheaply (two bitmap words)
-      const uint32_t w0 = cur[c * 2], w1 = (c * 2 + 1 < nwords) ? cur[c * 2 + 1] : 0u;
-      if ((w0 | w1) == 0) continue;
+      const uint32_t w1 = (c * 2 + 1 < nwords) ? cur[c * 2 + 1] : 0u;
+      if ((cur[c * 2] | w1) == 0) continue;
       const uint32_t v = c * 64 + lane;
-      bool act = v < V && bit(cur, v) && transit(v);
+      const bool act = v < V && bit(cur, v) && transit(v);
       uint32_t beg = 0, end = 0, nbv = 0;
       if (act) {
         beg = g.row_ptr[v];
@@ -259,27 +230,51 @@ struct Bfs {
       }
     }
   }
+
+  // digest terms of the next-hop bits of v held by this slice
+  __device__ __forceinline__ uint64_t pair_terms(uint32_t v) const {
+    uint64_t h = 0;
+    if constexpr (NH_LDS) {
+      uint32_t bits = nh_byte(v);
+      while (bits) {
+        h += digest_pair_term(v, nbr[__ffs(bits) - 1]);
+        bits &= bits - 1;
+      }
+    } else {
+      const uint32_t* r = row(v);
+      for (uint32_t w = 0; w < ws; ++w) {
+        uint32_t bits = r[w];
+        while (bits) {
+          h += digest_pair_term(v, nbr[32 * (w0 + w) + __ffs(bits) - 1]);
+          bits &= bits - 1;
+        }
+      }
+    }
+    return h;
+  }
 };
 
-template <bool NH_LDS, bool IGN, int WF>
-__device__ void bfs_run(const DevGraph& g, const RunArgs& a, uint32_t* lds) {
+template <bool NH_LDS, bool IGN>
+__device__ void bfs_run(const DevGraph& g, const RunArgs& a, uint32_t* lds, uint32_t rix,
+                        uint32_t slice) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
-  const uint32_t rix = blockIdx.x;
-  Bfs<NH_LDS, IGN, WF> b(g, a);
+  Bfs<NH_LDS, IGN> b(g, a);
   const uint32_t V = g.V, W = a.W;
   b.root = a.roots[rix];
   b.V = V;
   b.W = W;
   b.nwords = (V + 31) / 32;
+  b.w0 = slice * kSliceWords;
+  b.ws = min(kSliceWords, W - b.w0);
+  b.slice0 = slice == 0;
   const uint32_t bw = (b.nwords + 1) & ~1u;  // even: chunks of two words
-  uint32_t* cnt = lds;                        // [0,32) counters / reductions
+  uint32_t* cnt = lds;                        // [0,32) counters
   uint32_t* s_nbr = lds + 32;
   uint32_t* s_ign = s_nbr + a.nbr_cap;
   b.vis = s_ign + a.ign_cap;
   b.cur = b.vis + bw;
   b.nxt = b.cur + bw;
   b.nhb = b.nxt + bw;  // NH_LDS: (V+3)/4 words
-  b.cnt = cnt;
   b.nbr = s_nbr;
   b.ign = s_ign;
   b.dist_out = a.dist + (size_t)rix * V;
@@ -289,6 +284,12 @@ __device__ void bfs_run(const DevGraph& g, const RunArgs& a, uint32_t* lds) {
   b.nbr_n = g.dn_off[b.root + 1] - nb0;
   if (b.nbr_n > 32u * W || b.nbr_n > a.nbr_cap) {
     if (tid == 0) atomicOr(a.err, 1u);
+    return;
+  }
+  if (!b.slice0 && 32u * b.w0 >= b.nbr_n) {
+    // slice past the root's last neighbour: its words are all zero
+    for (uint32_t v = tid; v < V; v += blockDim.x)
+      for (uint32_t w = 0; w < b.ws; ++w) b.row(v)[w] = 0u;
     return;
   }
   for (uint32_t i = tid; i < b.nbr_n; i += blockDim.x) s_nbr[i] = g.dn[nb0 + i];
@@ -310,72 +311,65 @@ __device__ void bfs_run(const DevGraph& g, const RunArgs& a, uint32_t* lds) {
   }
   if constexpr (NH_LDS) {
     for (uint32_t i = tid; i < (V + 3) / 4; i += blockDim.x) b.nhb[i] = 0u;
+  } else {
+    for (uint32_t w = tid; w < b.ws; w += blockDim.x) b.row(b.root)[w] = 0u;
   }
   if (tid < 32) cnt[tid] = 0u;
   if (tid == 0) {
-    b.dist_out[b.root] = 0u;
-    cnt[4] = g.row_ptr[b.root + 1] - g.row_ptr[b.root];  // frontier edge mass
+    if (b.slice0) b.dist_out[b.root] = 0u;
+    cnt[4] = g.row_ptr[b.root + 1] - g.row_ptr[b.root];  // level-0 edge mass
   }
-  for (uint32_t w = tid; w < W; w += blockDim.x) b.nh_out[(size_t)b.root * W + w] = 0u;
   __syncthreads();
 
   const bool want_dig = a.flags & 8u;
   uint64_t reached = 0, sumd = 0, hsum = 0;
-  if (want_dig && tid == 0) {  // the root itself: dist 0, no next-hops
+  if (want_dig && tid == 0 && b.slice0) {  // the root itself: dist 0, no next-hops
     reached = 1;
-    hsum = mix((uint64_t)b.root << 32);
+    hsum = digest_node_term(b.root, 0);
   }
-  const uint32_t E = g.E;
-  uint32_t unvisited_mass = E - cnt[4];
+  // cnt[1..3]: "level found" ring; cnt[4], cnt[6]: edge mass of levels d, d+1
+  uint32_t unvisited_mass = g.E - cnt[4];
   for (uint32_t d = 0;; ++d) {
     const uint32_t front_mass = cnt[4 + (d & 1) * 2];
-    // direction: pull when the unvisited edge mass is not larger than what a
-    // push + follow-up pull would scan
+    // pull when the unvisited edge mass is below what push (+ the follow-up
+    // pull when next-hops live in HBM) would scan
     const bool pull_all = NH_LDS ? (unvisited_mass < front_mass)
                                  : (unvisited_mass < 2u * front_mass);
-    if (pull_all) b.template pull_level<true>(lane, wave, nwaves);
-    else b.push_level(lane, wave, nwaves);
-    __syncthreads();
-    if (!NH_LDS && !pull_all) {
-      b.template pull_level<false>(lane, wave, nwaves);
+    if (pull_all) {
+      b.template pull_level<true>(lane, wave, nwaves);
       __syncthreads();
+    } else {
+      b.push_level(lane, wave, nwaves);
+      __syncthreads();
+      if constexpr (!NH_LDS) {
+        b.template pull_level<false>(lane, wave, nwaves);
+        __syncthreads();
+      }
     }
-    // new level: write dist (+ digest), count its edge mass, roll bitmaps
-    uint32_t mass = 0, found = 0;
+    // new level: write dist (+ digest), count its edge mass
+    uint32_t mass = 0;
+    bool found = false;
     const uint32_t nchunks = (V + 63) / 64;
     for (uint32_t c = wave; c < nchunks; c += nwaves) {
+      const uint32_t w1 = (c * 2 + 1 < b.nwords) ? b.nxt[c * 2 + 1] : 0u;
+      if ((b.nxt[c * 2] | w1) == 0) continue;
       const uint32_t v = c * 64 + lane;
-      const bool in = v < V && bit(b.nxt, v);
-      if (in) {
-        b.dist_out[v] = d + 1;
+      if (v < V && bit(b.nxt, v)) {
+        found = true;
         mass += g.row_ptr[v + 1] - g.row_ptr[v];
-        found = 1;
+        if (b.slice0) b.dist_out[v] = d + 1;
         if (want_dig) {
-          uint64_t s = 0;
-          if constexpr (NH_LDS) {
-            uint32_t bits = b.nh_byte(v);
-            while (bits) {
-              s += mix((uint64_t)s_nbr[__ffs(bits) - 1] + 1ull);
-              bits &= bits - 1;
-            }
-          } else {
-            for (uint32_t w = 0; w < W; ++w) {
-              uint32_t bits = b.nh_out[(size_t)v * W + w];
-              while (bits) {
-                s += mix((uint64_t)s_nbr[w * 32 + __ffs(bits) - 1] + 1ull);
-                bits &= bits - 1;
-              }
-            }
+          if (b.slice0) {
+            reached += 1;
+            sumd += d + 1;
+            hsum += digest_node_term(v, d + 1);
           }
-          reached += 1;
-          sumd += d + 1;
-          hsum += mix(((uint64_t)v << 32) ^ (uint64_t)(d + 1) ^ (s * 0x9E3779B97F4A7C15ULL));
+          hsum += b.pair_terms(v);
         }
       }
     }
-    // reduce mass/found per wave, then into LDS
-    uint64_t m64 = wsum((uint64_t)mass);
-    const bool any = __ballot(found != 0) != 0;
+    const uint64_t m64 = wsum((uint64_t)mass);
+    const bool any = __ballot(found) != 0;
     if (lane == 0 && m64) atomicAdd(&cnt[4 + ((d + 1) & 1) * 2], (uint32_t)m64);
     if (lane == 0 && any) cnt[1 + (d % 3)] = 1u;
     __syncthreads();
@@ -386,27 +380,28 @@ __device__ void bfs_run(const DevGraph& g, const RunArgs& a, uint32_t* lds) {
       b.nxt[i] = 0u;
     }
     const bool more = cnt[1 + (d % 3)] != 0;
-    const uint32_t nm = cnt[4 + ((d + 1) & 1) * 2];
+    const uint32_t next_mass = cnt[4 + ((d + 1) & 1) * 2];
     __syncthreads();
     if (tid == 0) {
       cnt[1 + ((d + 1) % 3)] = 0u;
-      cnt[4 + (d & 1) * 2] = 0u;  // this level's mass slot is reused two levels on
+      cnt[4 + (d & 1) * 2] = 0u;  // level d's mass slot is reused by level d+2
     }
     if (!more) break;
-    unvisited_mass -= nm;
+    unvisited_mass -= next_mass;
   }
-  // epilogue: unreached nodes (dist INF, nh 0); NH_LDS next-hop row
+  // epilogue: unreached nodes (dist INF, zero next-hops); NH_LDS row write-out
+  const bool want_nh = a.flags & 4u;
   for (uint32_t v = tid; v < V; v += blockDim.x) {
     const bool seen = bit(b.vis, v);
-    if (!seen) b.dist_out[v] = kInf;
+    if (!seen && b.slice0) b.dist_out[v] = kInf;
     if constexpr (NH_LDS) {
-      if (a.flags & 4u) {
-        b.nh_out[(size_t)v * W] = seen ? b.nh_byte(v) : 0u;
-        for (uint32_t w = 1; w < W; ++w) b.nh_out[(size_t)v * W + w] = 0u;
+      if (want_nh) {
+        uint32_t* r = b.row(v);
+        r[0] = seen ? b.nh_byte(v) : 0u;
+        for (uint32_t w = 1; w < b.ws; ++w) r[w] = 0u;
       }
-    } else {
-      if (!seen)
-        for (uint32_t w = 0; w < W; ++w) b.nh_out[(size_t)v * W + w] = 0u;
+    } else if (!seen) {
+      for (uint32_t w = 0; w < b.ws; ++w) b.row(v)[w] = 0u;
     }
   }
   if (want_dig) {
@@ -427,57 +422,65 @@ __device__ void bfs_run(const DevGraph& g, const RunArgs& a, uint32_t* lds) {
         dg.sum_dist += s_dig[16 + i];
         dg.hash += s_dig[32 + i];
       }
-      a.digest[rix] = dg;
+      if (a.slices == 1) {
+        a.digest[rix] = dg;
+      } else {  // slices add into a zeroed record
+        atomicAdd((unsigned long long*)&a.digest[rix].reached, (unsigned long long)dg.reached);
+        atomicAdd((unsigned long long*)&a.digest[rix].sum_dist, (unsigned long long)dg.sum_dist);
+        atomicAdd((unsigned long long*)&a.digest[rix].hash, (unsigned long long)dg.hash);
+      }
     }
   }
 }
 
-// NHL: LDS holds the byte next-hop array; a block uses it when its root has
-// <= 8 distinct neighbours, the HBM next-hop path otherwise.
-template <bool NHL, bool IGN, int WF>
+// NHL: LDS holds the byte next-hop array; a run uses it when its root has
+// <= 8 distinct neighbours (then it is its own single slice).
+template <bool NHL, bool IGN>
 __global__ void __launch_bounds__(1024) spf_bfs_kernel(DevGraph g, RunArgs a) {
   extern __shared__ uint32_t lds[];
+  const uint32_t rix = blockIdx.x / a.slices, slice = blockIdx.x % a.slices;
   if constexpr (NHL) {
-    const uint32_t root = a.roots[blockIdx.x];
+    const uint32_t root = a.roots[rix];
     if (g.dn_off[root + 1] - g.dn_off[root] <= 8) {
-      bfs_run<true, IGN, 1>(g, a, lds);
+      if (slice == 0) {
+        bfs_run<true, IGN>(g, a, lds, rix, 0);
+      } else {  // words beyond the first slice are zero for such a root
+        uint32_t* base = a.nh + (size_t)rix * g.V * a.W;
+        const uint32_t w0 = slice * kSliceWords, ws = min(kSliceWords, a.W - w0);
+        for (uint32_t v = threadIdx.x; v < g.V; v += blockDim.x)
+          for (uint32_t w = 0; w < ws; ++w) base[(size_t)v * a.W + w0 + w] = 0u;
+      }
       return;
     }
   }
-  bfs_run<false, IGN, WF>(g, a, lds);
+  bfs_run<false, IGN>(g, a, lds, rix, slice);
 }
 
-template <bool NH_LDS, bool IGN, int WF>
+template <bool NHL, bool IGN>
 hipError_t launch_bfs_one(const DevGraph& g, const RunArgs& a, uint32_t n, uint32_t block,
                           size_t lds, hipStream_t s) {
-  auto k = spf_bfs_kernel<NH_LDS, IGN, WF>;
+  auto k = spf_bfs_kernel<NHL, IGN>;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k, dim3(n), dim3(block), lds, s, g, a);
+  hipLaunchKernelGGL(k, dim3(n * a.slices), dim3(block), lds, s, g, a);
   return hipGetLastError();
-}
-
-template <bool NH_LDS, bool IGN>
-hipError_t launch_bfs_wf(const DevGraph& g, const RunArgs& a, uint32_t n, uint32_t block,
-                         size_t lds, hipStream_t s) {
-  if (NH_LDS || a.W == 1) return launch_bfs_one<NH_LDS, IGN, 1>(g, a, n, block, lds, s);
-  if (a.W <= 4) return launch_bfs_one<NH_LDS, IGN, 4>(g, a, n, block, lds, s);
-  return launch_bfs_one<NH_LDS, IGN, 0>(g, a, n, block, lds, s);
 }
 
 }  // namespace
 
+uint32_t bfs_slices(uint32_t W) { return (W + kSliceWords - 1) / kSliceWords; }
+
 hipError_t launch_bfs(bool nh_lds, bool ign, const DevGraph& g, const RunArgs& a, uint32_t n,
                       uint32_t block, size_t lds, hipStream_t s) {
   if (nh_lds) {
-    return ign ? launch_bfs_wf<true, true>(g, a, n, block, lds, s)
-               : launch_bfs_wf<true, false>(g, a, n, block, lds, s);
+    return ign ? launch_bfs_one<true, true>(g, a, n, block, lds, s)
+               : launch_bfs_one<true, false>(g, a, n, block, lds, s);
   }
-  return ign ? launch_bfs_wf<false, true>(g, a, n, block, lds, s)
-             : launch_bfs_wf<false, false>(g, a, n, block, lds, s);
+  return ign ? launch_bfs_one<false, true>(g, a, n, block, lds, s)
+             : launch_bfs_one<false, false>(g, a, n, block, lds, s);
 }
 
 }  // namespace ospf

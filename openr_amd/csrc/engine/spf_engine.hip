@@ -346,6 +346,7 @@ int ospf_sssp_batch_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n_roots,
   a.nh = d_nh;
   a.digest = d_digest;
   a.err = c->d_err;
+  a.slices = p.variant >= 3 ? ospf::bfs_slices(nh_words) : 1u;
   if (dist_scratch) {
     a.dist = (uint32_t*)sp;
     sp += align_up(n_roots * V * 4, 256);
@@ -355,6 +356,8 @@ int ospf_sssp_batch_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n_roots,
   if (!(flags & OSPF_WANT_NH) && p.variant == 0) a.nh = nullptr;
 
   HIPCHK(c, hipSetDevice(c->device));
+  if (a.slices > 1 && (flags & OSPF_WANT_DIGEST))  // slices add into the records
+    HIPCHK(c, hipMemsetAsync(d_digest, 0, n_roots * sizeof(ospf_digest), (hipStream_t)stream));
   hipError_t e = p.variant >= 3
       ? ospf::launch_bfs(p.variant == 3, ign, c->g, a, n_roots, p.block, p.lds, (hipStream_t)stream)
       : ospf::launch_spf(p.variant, unit, ign, c->g, a, n_roots, p.block, p.lds,

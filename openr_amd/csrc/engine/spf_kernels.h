@@ -39,7 +39,26 @@ struct RunArgs {
   uint32_t* nh;             // [n_roots][V][W]
   ospf_digest* digest;      // [n_roots] when OSPF_WANT_DIGEST
   uint32_t* err;            // device error word (bit0: nh words, bit1: ignore cap)
+  uint32_t slices;          // BFS kernel: workgroups per run (4-word next-hop slices)
 };
+
+// Digest: sum over reached nodes of node_term(v, dist) plus,
+// for every next-hop n of v, pair_term(v, n) (mod 2^64). A sum of independent
+// terms, so next-hop slices of one run add up.
+__host__ __device__ inline uint64_t digest_mix(uint64_t x) {
+  x ^= x >> 30;
+  x *= 0xbf58476d1ce4e5b9ULL;
+  x ^= x >> 27;
+  x *= 0x94d049bb133111ebULL;
+  x ^= x >> 31;
+  return x;
+}
+__host__ __device__ inline uint64_t digest_node_term(uint32_t v, uint32_t dist) {
+  return digest_mix(((uint64_t)v << 32) | dist);
+}
+__host__ __device__ inline uint64_t digest_pair_term(uint32_t v, uint32_t nh) {
+  return digest_mix((((uint64_t)nh + 1) << 32) ^ (uint64_t)v ^ 0xD6E8FEB86659FD93ULL);
+}
 
 // Dial kernels (spf_kernels.hip), any metric:
 //   variant 0 = LDS dist + LDS nh, 1 = LDS dist + HBM nh, 2 = HBM dist + HBM nh
@@ -49,6 +68,7 @@ hipError_t launch_spf(int variant, bool unit, bool ign, const DevGraph& g, const
 // BFS kernel (spf_bfs.hip), unit metric / hop count, LDS bitmaps:
 //   nh_lds = variant 3 (byte next-hops in LDS for roots with <= 8 neighbours),
 //   otherwise variant 4 (next-hops in HBM).
+uint32_t bfs_slices(uint32_t W);
 hipError_t launch_bfs(bool nh_lds, bool ign, const DevGraph& g, const RunArgs& a, uint32_t n,
                       uint32_t block, size_t lds, hipStream_t s);
 

@@ -39,15 +39,6 @@ constexpr uint32_t DOWN = 0x80000000u;
 constexpr int WAVE = 64;
 constexpr uint32_t HYB_DEG = 32;
 
-__device__ __forceinline__ uint64_t mix64(uint64_t x) {
-  x ^= x >> 30;
-  x *= 0xbf58476d1ce4e5b9ULL;
-  x ^= x >> 27;
-  x *= 0x94d049bb133111ebULL;
-  x ^= x >> 31;
-  return x;
-}
-
 // lower_bound over a sorted LDS array
 __device__ __forceinline__ uint32_t lbound(const uint32_t* a, uint32_t n, uint32_t key) {
   uint32_t lo = 0, hi = n;
@@ -370,19 +361,18 @@ __global__ void __launch_bounds__(512) spf_run_kernel(DevGraph g, RunArgs a) {
       continue;
     }
     if (want_dig) {
-      uint64_t s = 0;
       const uint32_t* hv = r.nh_of(v);
       for (uint32_t w = 0; w < W; ++w) {
         uint32_t bits = hv[w];
         while (bits) {
           uint32_t b = __ffs(bits) - 1;
           bits &= bits - 1;
-          s += mix64((uint64_t)s_nbr[w * 32 + b] + 1ull);
+          hsum += digest_pair_term(v, s_nbr[w * 32 + b]);
         }
       }
       reached += 1;
       sumd += dv;
-      hsum += mix64(((uint64_t)v << 32) ^ (uint64_t)dv ^ (s * 0x9E3779B97F4A7C15ULL));
+      hsum += digest_node_term(v, dv);
     }
   }
   if constexpr (LDS_NH) {

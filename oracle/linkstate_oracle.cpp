@@ -474,20 +474,27 @@ struct Digest {
   uint64_t reached = 0, sumDist = 0, hash = 0;
 };
 
+// sum over reached nodes of node_term(v, dist) plus, for
+// every next-hop n of v, pair_term(v, n) (mod 2^64). Unknown names get id
+// 0xFFFFFFFF.
+static inline uint64_t nodeTerm(uint64_t v, uint64_t dist) { return mix64((v << 32) | dist); }
+static inline uint64_t pairTerm(uint64_t v, uint64_t n) {
+  return mix64(((n + 1) << 32) ^ v ^ 0xD6E8FEB86659FD93ULL);
+}
+
 static Digest digestOf(const SpfResult& r,
                        const std::unordered_map<std::string, uint32_t>& ids) {
   Digest d;
+  auto idOf = [&](const std::string& n) -> uint64_t {
+    auto it = ids.find(n);
+    return it == ids.end() ? 0xFFFFFFFFull : it->second;
+  };
   for (const auto& [name, nr] : r) {
-    auto it = ids.find(name);
-    uint64_t id = it == ids.end() ? 0xFFFFFFFFu : it->second;
-    uint64_t nhs = 0;
-    for (const auto& nh : nr.nextHops) {
-      auto jt = ids.find(nh);
-      nhs += mix64((jt == ids.end() ? 0xFFFFFFFFull : jt->second) + 1);
-    }
+    const uint64_t id = idOf(name);
     d.reached++;
     d.sumDist += nr.metric;
-    d.hash += mix64((id << 32) ^ nr.metric ^ (nhs * 0x9E3779B97F4A7C15ULL));
+    d.hash += nodeTerm(id, nr.metric);
+    for (const auto& nh : nr.nextHops) d.hash += pairTerm(id, idOf(nh));
   }
   return d;
 }

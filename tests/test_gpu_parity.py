@@ -148,6 +148,21 @@ def test_fabric_sampled_digests(weighted, variant):
         assert p.spf_text(r) == o.spf_text(r)
 
 
+@pytest.mark.parametrize("variant_env", [None, "2"])
+def test_wide_root_nexthop_slices(variant_env, monkeypatch):
+    """A spine with 140 distinct neighbours needs 5 next-hop words: the BFS
+    kernel splits the row into 4-word slices run by separate workgroups."""
+    if variant_env:
+        monkeypatch.setenv("OSPF_FORCE_VARIANT", variant_env)
+    st = T.fabric(pods=140, planes=2)
+    o, p = both(st)
+    roots = ["1-0-0", "1-1-35", "2-7-1", "3-139-47"]
+    assert np.array_equal(p.digests(roots), o.digests(roots, threads=8))
+    for r in roots:
+        assert p.spf_text(r) == o.spf_text(r)
+        assert p.spf_text(r, False) == o.spf_text(r, False)
+
+
 def test_fabric_reference_quirk():
     st = T.fabric(pods=6, planes=4, reference_quirk=True)
     o, p = both(st)
