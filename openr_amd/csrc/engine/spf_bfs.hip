@@ -38,6 +38,7 @@ constexpr uint32_t kDown = 0x80000000u;
 constexpr int kWave = 64;
 constexpr uint32_t kCoopDeg = 32;
 constexpr uint32_t kSliceWords = 4;
+constexpr uint32_t kUnroll = 8;
 
 __device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* a, uint32_t n, uint32_t key) {
   uint32_t lo = 0, hi = n;
@@ -105,8 +106,7 @@ struct Bfs {
     return lower_bound_u32(nbr, nbr_n, v) - 32u * w0;
   }
 
-  __device__ __forceinline__ void push_edge(uint32_t u, uint32_t e, uint32_t nbu) {
-    const uint32_t cx = g.colx[e];
+  __device__ __forceinline__ void push_one(uint32_t u, uint32_t e, uint32_t cx, uint32_t nbu) {
     if (!usable(e, cx)) return;
     const uint32_t x = cx;
     if (bit(vis, x)) return;
@@ -117,34 +117,61 @@ struct Bfs {
     }
   }
 
-  // v collects next-hops from level-d tails; true when it has a tight tail
-  template <bool COOP>
-  __device__ __forceinline__ bool pull_node(uint32_t v, uint32_t beg, uint32_t end, int lane,
-                                            uint32_t* acc) {
-    bool any = false;
-    for (uint32_t e = beg + (COOP ? lane : 0); e < end; e += (COOP ? kWave : 1)) {
-      const uint32_t cx = g.colx[e];
-      if (!usable(e, cx)) continue;
-      const uint32_t u = cx;
-      if (!bit(cur, u) || !transit(u)) continue;
-      any = true;
-      if (u == root) {
-        const uint32_t b = slice_bit(v);
-        if constexpr (NH_LDS) {
-          acc[0] |= 1u << b;
-        } else {
+  // edges [beg, end) of u, one lane (STEP 1) or the whole wave (STEP 64),
+  // CSR loads issued kUnroll at a time so each lane keeps several in flight
+  template <uint32_t STEP>
+  __device__ __forceinline__ void push_edges(uint32_t u, uint32_t beg, uint32_t end,
+                                             uint32_t nbu) {
+    for (uint32_t e = beg; e < end; e += kUnroll * STEP) {
+      uint32_t cx[kUnroll];
 #pragma unroll
-          for (uint32_t w = 0; w < kSliceWords; ++w)
-            acc[w] |= ((b >> 5) == w) ? (1u << (b & 31)) : 0u;
-        }
-      } else if constexpr (NH_LDS) {
-        acc[0] |= nh_byte(u);
+      for (uint32_t k = 0; k < kUnroll; ++k)
+        cx[k] = (e + k * STEP < end) ? g.colx[e + k * STEP] : kDown;
+#pragma unroll
+      for (uint32_t k = 0; k < kUnroll; ++k)
+        if (e + k * STEP < end) push_one(u, e + k * STEP, cx[k], nbu);
+    }
+  }
+
+  // v collects next-hops from level-d tails (cur holds only transit nodes);
+  // true when it has a tight tail
+  __device__ __forceinline__ void pull_one(uint32_t v, uint32_t e, uint32_t cx, uint32_t* acc,
+                                           bool& any) const {
+    if (!usable(e, cx)) return;
+    const uint32_t u = cx;
+    if (!bit(cur, u)) return;
+    any = true;
+    if (u == root) {
+      const uint32_t b = slice_bit(v);
+      if constexpr (NH_LDS) {
+        acc[0] |= 1u << b;
       } else {
-        const uint32_t* s = row(u);
 #pragma unroll
         for (uint32_t w = 0; w < kSliceWords; ++w)
-          if (w < ws) acc[w] |= s[w];
+          acc[w] |= ((b >> 5) == w) ? (1u << (b & 31)) : 0u;
       }
+    } else if constexpr (NH_LDS) {
+      acc[0] |= nh_byte(u);
+    } else {
+      const uint32_t* s = row(u);
+#pragma unroll
+      for (uint32_t w = 0; w < kSliceWords; ++w)
+        if (w < ws) acc[w] |= s[w];
+    }
+  }
+
+  template <uint32_t STEP>
+  __device__ __forceinline__ bool pull_edges(uint32_t v, uint32_t beg, uint32_t end,
+                                             uint32_t* acc) const {
+    bool any = false;
+    for (uint32_t e = beg; e < end; e += kUnroll * STEP) {
+      uint32_t cx[kUnroll];
+#pragma unroll
+      for (uint32_t k = 0; k < kUnroll; ++k)
+        cx[k] = (e + k * STEP < end) ? g.colx[e + k * STEP] : kDown;
+#pragma unroll
+      for (uint32_t k = 0; k < kUnroll; ++k)
+        if (e + k * STEP < end) pull_one(v, e + k * STEP, cx[k], acc, any);
     }
     return any;
   }
@@ -165,7 +192,10 @@ struct Bfs {
   __device__ void pull_level(int lane, int wave, int nwaves) {
     const uint32_t nchunks = (V + 63) / 64;
     for (uint32_t c = wave; c < nchunks; c += nwaves) {
-      if (!PULL_ALL) {
+      if (PULL_ALL) {  // skip chunks with every node already visited
+        const uint32_t w1 = (c * 2 + 1 < nwords) ? vis[c * 2 + 1] : 0xFFFFFFFFu;
+        if ((vis[c * 2] & w1) == 0xFFFFFFFFu) continue;
+      } else {
         const uint32_t w1 = (c * 2 + 1 < nwords) ? nxt[c * 2 + 1] : 0u;
         if ((nxt[c * 2] | w1) == 0) continue;
       }
@@ -180,7 +210,7 @@ struct Bfs {
       const bool big = act && (end - beg) > kCoopDeg;
       if (act && !big) {
         uint32_t acc[kSliceWords] = {0u, 0u, 0u, 0u};
-        if (pull_node<false>(v, beg, end, lane, acc)) {
+        if (pull_edges<1>(v, beg, end, acc)) {
           store_nh(v, acc);
           if (PULL_ALL) atomicOr(&nxt[v >> 5], 1u << (v & 31));
         }
@@ -192,7 +222,7 @@ struct Bfs {
         const uint32_t bv = __shfl(v, l, kWave), bb = __shfl(beg, l, kWave),
                        be = __shfl(end, l, kWave);
         uint32_t acc[kSliceWords] = {0u, 0u, 0u, 0u};
-        const bool any = __ballot(pull_node<true>(bv, bb, be, lane, acc)) != 0;
+        const bool any = __ballot(pull_edges<kWave>(bv, bb + lane, be, acc)) != 0;
 #pragma unroll
         for (uint32_t w = 0; w < kSliceWords; ++w) acc[w] = wor(acc[w]);
         if (any && lane == 0) {
@@ -210,7 +240,7 @@ struct Bfs {
       const uint32_t w1 = (c * 2 + 1 < nwords) ? cur[c * 2 + 1] : 0u;
       if ((cur[c * 2] | w1) == 0) continue;
       const uint32_t v = c * 64 + lane;
-      const bool act = v < V && bit(cur, v) && transit(v);
+      const bool act = v < V && bit(cur, v);
       uint32_t beg = 0, end = 0, nbv = 0;
       if (act) {
         beg = g.row_ptr[v];
@@ -218,15 +248,14 @@ struct Bfs {
         if constexpr (NH_LDS) nbv = nh_byte(v);
       }
       const bool big = act && (end - beg) > kCoopDeg;
-      if (act && !big)
-        for (uint32_t e = beg; e < end; ++e) push_edge(v, e, nbv);
+      if (act && !big) push_edges<1>(v, beg, end, nbv);
       uint64_t bm = __ballot(big);
       while (bm) {
         const int l = __ffsll((unsigned long long)bm) - 1;
         bm &= bm - 1;
         const uint32_t bv = __shfl(v, l, kWave), bb = __shfl(beg, l, kWave),
                        be = __shfl(end, l, kWave), bn = __shfl(nbv, l, kWave);
-        for (uint32_t e = bb + lane; e < be; e += kWave) push_edge(bv, e, bn);
+        push_edges<kWave>(bv, bb + lane, be, bn);
       }
     }
   }
@@ -373,10 +402,12 @@ __device__ void bfs_run(const DevGraph& g, const RunArgs& a, uint32_t* lds, uint
     if (lane == 0 && m64) atomicAdd(&cnt[4 + ((d + 1) & 1) * 2], (uint32_t)m64);
     if (lane == 0 && any) cnt[1 + (d % 3)] = 1u;
     __syncthreads();
+    // roll bitmaps; the next frontier keeps only nodes that may transit
+    // (overloaded nodes are reached but never relax, LinkState.cpp:859-866)
     for (uint32_t i = tid; i < bw; i += blockDim.x) {
       const uint32_t n = b.nxt[i];
       b.vis[i] |= n;
-      b.cur[i] = n;
+      b.cur[i] = (i < b.nwords) ? (n & ~g.nt_bits[i]) : 0u;
       b.nxt[i] = 0u;
     }
     const bool more = cnt[1 + (d % 3)] != 0;

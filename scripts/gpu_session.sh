@@ -17,9 +17,14 @@ rc=$?; echo "pytest rc=$rc" | tee -a "$OUT/session.log"; tail -5 "$OUT/pytest_gp
 if fatal $rc; then echo "fatal pytest exit; stopping"; exit $rc; fi
 
 echo "== bench" | tee -a "$OUT/session.log"
-timeout -k 10 400 python -u bench.py --steps 5 --warmup 1 > "$OUT/bench.json" 2> "$OUT/bench.err"
+timeout -k 10 400 python -u bench.py --steps 5 --warmup 1 ${BENCH_ARGS:-} > "$OUT/bench.json" 2> "$OUT/bench.err"
 rc=$?; echo "bench rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/bench.json"; tail -3 "$OUT/bench.err"
 if fatal $rc; then exit $rc; fi
+if [ -n "${BENCH2_ARGS:-}" ]; then
+  timeout -k 10 400 python -u bench.py --no-cpu $BENCH2_ARGS > "$OUT/bench2.json" 2> "$OUT/bench2.err"
+  rc=$?; echo "bench2 rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/bench2.json"
+  if fatal $rc; then exit $rc; fi
+fi
 
 echo "== rocprofv3 kernel trace" | tee -a "$OUT/session.log"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
