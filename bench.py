@@ -3,14 +3,16 @@
 
 BASELINE.json metric: "all-sources SPF/sec + GTEPS on 100k-node fabric
 topology at 1/2/4/8 GPUs". A *step* = one batch of roots per GPU run through
-the engine (ospf_sssp_batch_dev): per-root distances, next-hop bitsets and
-digests written to HBM, then (N > 1) the 24-B per-root digest records
-all-gathered over RCCL. Roots sweep a fixed permutation of every node (all
-sources), grouped per launch by next-hop width class (RSW / FSW / SSW).
-Roots are sharded across ranks with no data-path collective: scaling "weak".
+the engine's device API (ospf_sssp_batch_dev): per-root distance rows,
+next-hop bitset rows and digests written to HBM, then (N > 1) the 24-B
+per-root digest records all-gathered over RCCL. Roots sweep a fixed
+permutation of every node (all sources); each step launches one kernel per
+next-hop width class (rack / fabric / spine switches), each on its own HIP
+stream. Ranks shard the roots with no data-path collective: scaling "weak".
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
-       torchrun --nproc-per-node N bench.py --gpus N ...
+       torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+                --master-port P bench.py --gpus N ...
 """
 from __future__ import annotations
 
@@ -28,6 +30,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from openr_amd import _native as N  # noqa: E402
+from openr_amd import shard  # noqa: E402
 from openr_amd import topology as T  # noqa: E402
 from openr_amd.engine import Engine  # noqa: E402
 from openr_amd.linkstate import LinkState  # noqa: E402
@@ -45,6 +48,9 @@ def build_topology(name: str):
         return T.fabric(pods=1781, planes=8), "F100k fabric pods=1781 planes=8 (unit metric)"
     if name == "fabric10k":
         return T.fabric(pods=173, planes=8), "F10k fabric pods=173 planes=8 (unit metric)"
+    if name == "fabric100k-w":
+        return (T.fabric(pods=1781, planes=8, weighted_seed=7),
+                "F100k fabric pods=1781 planes=8 (metric 1..64, seed 7)")
     if name == "grid31":
         return T.grid(31), "G31 grid 31x31 (unit metric)"
     if name == "mesh1m":
@@ -53,22 +59,22 @@ def build_topology(name: str):
 
 
 def bytes_per_root(V: int, E: int, W: int) -> int:
-    """CSR neighbour+weight reads, offsets, dist write,
-    next-hop bitset write."""
+    """SURVEY.md §8(d) algorithmic bytes of one SPF run: CSR neighbour + weight
+    reads, row offsets, dist write, next-hop bitset write."""
     return 8 * E + 4 * (V + 1) + 4 * V + 4 * V * W
 
 
-def pmc_traffic(profile_dir: str, kernel_substr: str):
-    """Per-launch HBM bytes from committed rocprofv3 --pmc summaries
-    (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE, KiB units)."""
+def pmc_traffic(profile_dir: str, key: str):
+    """Per-launch HBM bytes of the kernel `key` from the committed rocprofv3
+    --pmc summary (profiles/<round>/pmc_traffic.json, written by
+    scripts/pmc_traffic.py: FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE)."""
     path = os.path.join(profile_dir, "pmc_traffic.json")
     if not os.path.exists(path):
         return None
     try:
         with open(path) as f:
-            d = json.load(f)
-        return d.get(kernel_substr)
-    except Exception:
+            return json.load(f).get(key, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
         return None
 
 
@@ -77,12 +83,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=1024, help="roots per GPU per step")
+    ap.add_argument("--batch", type=int, default=4096, help="roots per GPU per step")
     ap.add_argument("--topology", default="fabric100k")
     ap.add_argument("--cpu-sample", type=int, default=32)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-nh", action="store_true", help="skip next-hop output (diagnostic)")
+    ap.add_argument("--serial-streams", action="store_true", help="one stream for all classes")
     ap.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles", "r01"))
     args = ap.parse_args()
 
@@ -90,10 +97,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     dist_on = world > 1
     if dist_on:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.distributed.init_process_group("nccl", device_id=dev)
 
     t0 = time.time()
     stream, desc = build_topology(args.topology)
@@ -105,80 +112,65 @@ def main():
     V, E = eng.V, int(csr["col"].size)
     props = torch.cuda.get_device_properties(local)
     log(f"[rank {rank}] {props.name} CUs={props.multi_processor_count} "
-        f"lds/block={getattr(props, 'shared_memory_per_block', '?')} "
-        f"lds/cu={getattr(props, 'shared_memory_per_multiprocessor', '?')}")
-    log(f"[rank {rank}] {desc}: V={V} E_dir={E} setup {time.time() - t0:.1f}s")
+        f"{desc}: V={V} E_dir={E} setup {time.time() - t0:.1f}s")
 
-    # all-sources root permutation, grouped by next-hop width class
-    rng = np.random.default_rng(0x5EED)
-    perm = rng.permutation(V).astype(np.uint32)
-    rp, col = csr["row_ptr"], csr["col"]
-    deg_distinct = np.array([len(np.unique(col[rp[u]:rp[u + 1]])) for u in range(V)])
-    words = np.maximum(1, (deg_distinct + 31) // 32)
-    classes = []
-    for W in sorted(set(words.tolist())):
-        members = perm[words[perm] == W]
-        share = max(1, int(round(args.batch * members.size / V)))
-        classes.append(dict(W=W, roots=members, per_step=share))
-    B = sum(c["per_step"] for c in classes)
     flags = N.OSPF_WANT_DIST | N.OSPF_WANT_DIGEST | (0 if args.no_nh else N.OSPF_WANT_NH)
-    dev = torch.device("cuda", local)
+    perm = np.random.default_rng(0x5EED).permutation(V).astype(np.uint32)
+    words = shard.nh_words_of(csr["row_ptr"], csr["col"])
+    classes = shard.make_classes(perm, words, args.batch)
+    B = sum(c.per_step for c in classes)
     for c in classes:
-        n = c["per_step"]
-        c["d_all"] = torch.from_numpy(c["roots"].astype(np.int32)).to(dev)
-        c["dist"] = torch.empty((n, V), dtype=torch.int32, device=dev)
-        c["nh"] = None if args.no_nh else torch.empty((n, V, c["W"]), dtype=torch.int32, device=dev)
-        c["dig"] = torch.empty((n, 3), dtype=torch.int64, device=dev)
-        c["ms"] = []
-        c["variant"] = eng.plan_variant(c["W"], flags)
+        n = c.per_step
+        x = c.extra
+        x["plan"] = eng.plan(c.nh_words, flags)
+        x["d_all"] = torch.from_numpy(c.roots.astype(np.int32)).to(dev)
+        x["roots"] = torch.empty(n, dtype=torch.int32, device=dev)
+        x["dist"] = torch.empty((n, V), dtype=torch.int32, device=dev)
+        x["nh"] = None if args.no_nh else torch.empty((n, V, c.nh_words), dtype=torch.int32,
+                                                      device=dev)
+        x["dig"] = torch.empty((n, 3), dtype=torch.int64, device=dev)
+        x["stream"] = torch.cuda.current_stream() if args.serial_streams else \
+            torch.cuda.Stream(device=dev)
+        x["ev"] = []
     dig_all = torch.empty((B, 3), dtype=torch.int64, device=dev)
-    gathered = torch.empty((world * B, 3), dtype=torch.int64, device=dev) if dist_on else None
-    s = torch.cuda.current_stream()
-    sh = s.cuda_stream
-    # one HIP stream per root class so the classes' workgroups share the GPU
-    # (the 3 spine roots are long single-root runs); heaviest class first
-    for c in classes:
-        c["stream"] = torch.cuda.Stream(device=dev)
-        c["roots_i32"] = torch.empty(c["per_step"], dtype=torch.int32, device=dev)
-    launch_order = sorted(classes, key=lambda c: -c["W"])
+    main_s = torch.cuda.current_stream()
+    order = sorted(classes, key=lambda c: -c.nh_words)  # longest runs first
 
     def step(i: int, timed: bool):
-        done_prev = torch.cuda.Event()
-        done_prev.record(s)  # previous step's digest copies are queued on s
-        for c in launch_order:
-            n, m = c["per_step"], c["roots"].size
-            start = ((i * world + rank) * n) % m
-            cs = c["stream"]
+        ready = torch.cuda.Event()
+        ready.record(main_s)  # the previous step's digest copies are queued on main_s
+        done = []
+        for c in order:
+            x, n, m = c.extra, c.per_step, c.roots.size
+            cs = x["stream"]
             with torch.cuda.stream(cs):
-                cs.wait_event(done_prev)
+                cs.wait_event(ready)
+                start = ((i * world + rank) * n) % m  # == shard.step_roots on the device
                 idx = (torch.arange(n, device=dev) + start) % m
-                torch.index_select(c["d_all"], 0, idx, out=c["roots_i32"])
+                torch.index_select(x["d_all"], 0, idx, out=x["roots"])
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record(cs)
-                eng.run_dev(c["roots_i32"].data_ptr(), n, c["W"], flags=flags,
-                            d_dist=c["dist"].data_ptr(),
-                            d_nh=c["nh"].data_ptr() if c["nh"] is not None else 0,
-                            d_digest=c["dig"].data_ptr(), stream=cs.cuda_stream)
+                eng.run_dev(x["roots"].data_ptr(), n, c.nh_words, flags=flags,
+                            d_dist=x["dist"].data_ptr(),
+                            d_nh=x["nh"].data_ptr() if x["nh"] is not None else 0,
+                            d_digest=x["dig"].data_ptr(), stream=cs.cuda_stream)
                 ev[1].record(cs)
+            done.append(ev[1])
             if timed:
-                c["ms"].append(ev)
+                x["ev"].append(ev)
+        for e in done:
+            main_s.wait_event(e)
         off = 0
         for c in classes:
-            s.wait_event(c["ms"][-1][1] if timed else ev_record(c["stream"]))
-            dig_all[off:off + c["per_step"]].copy_(c["dig"])
-            off += c["per_step"]
+            dig_all[off:off + c.per_step].copy_(c.extra["dig"])
+            off += c.per_step
         if dist_on:
-            torch.distributed.all_gather_into_tensor(gathered, dig_all)
-
-    def ev_record(cs):
-        e = torch.cuda.Event()
-        e.record(cs)
-        return e
+            shard.gather_digests(dig_all)
 
     for i in range(args.warmup):
         step(i, False)
     torch.cuda.synchronize()
-    eng.sync(sh)
+    eng.sync(main_s.cuda_stream)
     if dist_on:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -189,7 +181,7 @@ def main():
     if dist_on:
         torch.distributed.barrier()
     dt = time.perf_counter() - t_start
-    eng.sync(sh)  # raises if the device error word was set
+    eng.sync(main_s.cuda_stream)  # raises if the device error word was set
     if dist_on:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -199,26 +191,29 @@ def main():
     spf_s = roots_total / dt
     gteps = roots_total * E / dt / 1e9
 
-    # roofline for the dominant kernel (largest total device time)
+    # roofline of the dominant kernel (largest total device time), from the
+    # HIP events bracketing its launches on its own stream
     for c in classes:
-        c["kernel_ms"] = [a.elapsed_time(b) for a, b in c["ms"]]
-    dom = max(classes, key=lambda c: sum(c["kernel_ms"]))
-    avg_ms = float(np.mean(dom["kernel_ms"]))
-    alg_bytes = dom["per_step"] * bytes_per_root(V, E, dom["W"])
-    achieved = alg_bytes / (avg_ms / 1e3) / 1e9
-    kname = f"spf_run_kernel variant={dom['variant']} W={dom['W']}"
+        c.extra["ms"] = [a.elapsed_time(b) for a, b in c.extra["ev"]]
+    dom = max(classes, key=lambda c: sum(c.extra["ms"]))
+    avg_ms = float(np.mean(dom.extra["ms"]))
+    alg = dom.per_step * bytes_per_root(V, E, dom.nh_words)
+    achieved = alg / (avg_ms / 1e3) / 1e9
+    p = dom.extra["plan"]
+    key = f"variant{p['variant']}_W{dom.nh_words}"
+    traffic = pmc_traffic(args.profile_dir, key)
     roofline = {
         "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 4),
-        "traffic": pmc_traffic(args.profile_dir, f"W{dom['W']}"),
-        "kernel": kname, "roots_per_launch": dom["per_step"],
-        "bytes_per_root": bytes_per_root(V, E, dom["W"]),
+        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+        "kernel": f"spf_bfs_kernel (variant {p['variant']}, nh_words {dom.nh_words})"
+        if p["variant"] >= 3 else f"spf_run_kernel (variant {p['variant']})",
+        "grid": dom.per_step * p["slices"], "block": p["block"], "lds_bytes": p["lds_bytes"],
+        "roots_per_launch": dom.per_step, "bytes_per_root": bytes_per_root(V, E, dom.nh_words),
         "avg_launch_ms": round(avg_ms, 3),
-        "teps_per_launch": round(dom["per_step"] * E / (avg_ms / 1e3) / 1e9, 3),
+        "edges_per_s_per_launch": round(dom.per_step * E / (avg_ms / 1e3), 1),
     }
 
-    cpu = None
-    parity = None
+    cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu:
         from oracle import Oracle  # CPU baseline leg only (reference-shaped restatement)
         sample_ids = perm[: args.cpu_sample]
@@ -232,23 +227,28 @@ def main():
                "sample": f"{len(sample)} roots (permutation seed 0x5eed) of the same topology, "
                          f"reference-shaped runSpf restatement (oracle/), {args.cpu_threads} "
                          f"threads, {ct:.2f}s"}
-        W = int(words[sample_ids].max())
-        gd = eng.run(sample_ids, W, want_dist=False, want_nh=False, want_digest=True)["digest"]
+        gd = eng.run(sample_ids, int(words[sample_ids].max()), want_dist=False, want_nh=False,
+                     want_digest=True)["digest"]
         parity = bool(np.array_equal(gd, cd))
 
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(spf_s, 2), "unit": "SPF/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic", "gteps": round(gteps, 3),
-            "config": {"workload": desc + " all-sources SPF + ECMP next-hop bitsets (dist+nh "
-                                          "rows to HBM, per-root digests)",
-                       "n_nodes": V, "n_directed_edges": E, "roots_per_step_per_gpu": B,
-                       "root_classes": [{"nh_words": c["W"], "roots_per_step": c["per_step"],
-                                         "variant": c["variant"]} for c in classes],
-                       "parallelism": f"root-sharded x{world}" + (", RCCL all_gather of "
-                                                                  "24-B digests" if dist_on else "")},
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "gteps": round(gteps, 3),
+            "config": {
+                "workload": desc + " all-sources SPF + ECMP next-hop bitsets (dist + next-hop "
+                                   "rows written to HBM, per-root digests)",
+                "n_nodes": V, "n_directed_edges": E, "roots_per_step_per_gpu": B,
+                "root_classes": [{"nh_words": c.nh_words, "roots_per_step": c.per_step,
+                                  **{k: c.extra["plan"][k] for k in ("variant", "slices",
+                                                                     "block")},
+                                  "avg_launch_ms": round(float(np.mean(c.extra["ms"])), 3)}
+                                 for c in classes],
+                "parallelism": f"root-sharded x{world}" +
+                               (", RCCL all_gather of 24-B digests" if dist_on else "")},
             "roofline": roofline, "cpu_baseline": cpu, "parity_vs_cpu_sample": parity,
         }
         print(json.dumps(line), flush=True)

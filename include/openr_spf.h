@@ -151,6 +151,16 @@ int ospf_sync(ospf_ctx* ctx, void* stream);
 int ospf_plan_variant(const ospf_ctx* ctx, uint32_t flags, uint32_t nh_words,
                       int* variant);
 
+/* Full launch plan the engine would use for a batch (reporting / profiling). */
+typedef struct ospf_plan_info {
+  int32_t variant;       /* as ospf_plan_variant */
+  uint32_t block;        /* threads per workgroup */
+  uint32_t lds_bytes;    /* dynamic LDS per workgroup */
+  uint32_t slices;       /* workgroups per SPF run (next-hop slices) */
+} ospf_plan_info;
+int ospf_plan(const ospf_ctx* ctx, uint32_t flags, uint32_t nh_words, uint32_t max_ignored,
+              ospf_plan_info* out);
+
 /* Runtime statistics. spf_runs counts logical runSpf executions (one per
  * root per batch), matching the reference's decision.spf_runs counter
  * (LinkState.cpp:843). */

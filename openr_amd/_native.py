@@ -27,7 +27,7 @@ OSPF_WANT_DIGEST = 0x8
 ENGINE_SYMBOLS = [
     "ospf_open", "ospf_close", "ospf_last_error", "ospf_load_graph", "ospf_graph_info_get",
     "ospf_root_neighbors", "ospf_sssp_batch", "ospf_sssp_batch_dev", "ospf_sync",
-    "ospf_plan_variant", "ospf_spf_runs",
+    "ospf_plan_variant", "ospf_plan", "ospf_spf_runs",
 ]
 DECISION_SYMBOLS = [
     "odl_create", "odl_destroy", "odl_last_error", "odl_free", "odl_apply", "odl_spf_text",
@@ -49,6 +49,10 @@ class ospf_ignore(C.Structure):  # noqa: N801
 
 class ospf_digest(C.Structure):  # noqa: N801
     _fields_ = [("reached", u64), ("sum_dist", u64), ("hash", u64)]
+
+
+class ospf_plan_info(C.Structure):  # noqa: N801
+    _fields_ = [("variant", C.c_int32), ("block", u32), ("lds_bytes", u32), ("slices", u32)]
 
 
 class ospf_graph_info(C.Structure):  # noqa: N801
@@ -83,6 +87,7 @@ def engine() -> C.CDLL:
         L.ospf_sssp_batch_dev.argtypes = [vp, vp, u32, vp, vp, u32, u32, u32, vp, vp, vp, vp]
         L.ospf_sync.argtypes = [vp, vp]
         L.ospf_plan_variant.argtypes = [vp, u32, u32, C.POINTER(C.c_int)]
+        L.ospf_plan.argtypes = [vp, u32, u32, u32, C.POINTER(ospf_plan_info)]
         L.ospf_spf_runs.argtypes = [vp]
         L.ospf_spf_runs.restype = u64
         _engine = L

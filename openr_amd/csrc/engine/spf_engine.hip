@@ -296,6 +296,20 @@ int ospf_plan_variant(const ospf_ctx* c, uint32_t flags, uint32_t nh_words, int*
   return OSPF_OK;
 }
 
+int ospf_plan(const ospf_ctx* c, uint32_t flags, uint32_t nh_words, uint32_t max_ignored,
+              ospf_plan_info* out) {
+  if (!c || !out) return OSPF_E_INVAL;
+  if (!c->loaded) return OSPF_E_NOGRAPH;
+  const bool unit = (flags & OSPF_HOP_COUNT) || c->info.unit_metric;
+  const uint32_t W = std::max<uint32_t>(nh_words, 1);
+  const Plan p = make_plan(c, W, max_ignored, unit);
+  out->variant = p.variant;
+  out->block = p.block;
+  out->lds_bytes = (uint32_t)p.lds;
+  out->slices = p.variant >= 3 ? ospf::bfs_slices(W) : 1u;
+  return OSPF_OK;
+}
+
 int ospf_sssp_batch_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n_roots,
                         const uint32_t* d_ign_off, const uint32_t* d_ign_ids,
                         uint32_t max_ignored, uint32_t flags, uint32_t nh_words,

@@ -78,6 +78,11 @@ class Engine:
         self._check(self._L.ospf_plan_variant(self._h, flags, nh_words, C.byref(v)))
         return v.value
 
+    def plan(self, nh_words: int, flags: int = 0, max_ignored: int = 0) -> dict:
+        p = N.ospf_plan_info()
+        self._check(self._L.ospf_plan(self._h, flags, nh_words, max_ignored, C.byref(p)))
+        return dict(variant=p.variant, block=p.block, lds_bytes=p.lds_bytes, slices=p.slices)
+
     @property
     def spf_runs(self) -> int:
         return int(self._L.ospf_spf_runs(self._h))

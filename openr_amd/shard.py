@@ -1,0 +1,74 @@
+"""Root sharding for multi-GPU all-sources runs.
+
+Every SPF run is independent, so ranks split the roots with no data-path
+collective; the only exchange is an all-gather of the fixed 24-byte per-root
+digest records {reached, sum_dist, hash} (RCCL over xGMI on MI355X, gloo in
+the CPU tests). Roots are grouped in next-hop width classes (one kernel launch
+per class per step), and every class is swept round-robin over ranks.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Sequence
+
+import numpy as np
+
+
+@dataclass
+class RootClass:
+    nh_words: int
+    roots: np.ndarray          # this class's roots in sweep order (u32 node ids)
+    per_step: int              # roots of this class each rank runs per step
+    extra: dict = field(default_factory=dict)
+
+
+def nh_words_of(row_ptr: np.ndarray, col: np.ndarray) -> np.ndarray:
+    """ceil(distinct neighbours / 32) per node (>= 1) from a CSR whose rows
+    are sorted by neighbour id (what the engine uses for the bit order)."""
+    V = row_ptr.size - 1
+    deg = np.diff(row_ptr.astype(np.int64))
+    owner = np.repeat(np.arange(V), deg)
+    new = np.ones(col.size, bool)
+    if col.size:
+        new[1:] = (col[1:] != col[:-1]) | (owner[1:] != owner[:-1])
+        new &= col != owner  # self-loops are not next hops
+    distinct = np.bincount(owner[new], minlength=V) if col.size else np.zeros(V, np.int64)
+    return np.maximum(1, (distinct + 31) // 32)
+
+
+def make_classes(perm: np.ndarray, words: np.ndarray, batch: int) -> List[RootClass]:
+    """Split a root permutation into width classes; each class's share of a
+    `batch`-root step is proportional to its size (at least 1)."""
+    V = perm.size
+    out = []
+    for W in sorted(set(words[perm].tolist())):
+        members = perm[words[perm] == W]
+        share = max(1, int(round(batch * members.size / V)))
+        out.append(RootClass(int(W), members.astype(np.uint32), share))
+    return out
+
+
+def step_roots(cls: RootClass, step: int, world: int, rank: int) -> np.ndarray:
+    """Roots of `cls` that `rank` runs in `step` (cyclic sweep, disjoint across
+    ranks within a step)."""
+    n, m = cls.per_step, cls.roots.size
+    start = ((step * world + rank) * n) % m
+    return cls.roots[(np.arange(n) + start) % m]
+
+
+def gather_digests(local, group=None):
+    """all_gather of per-rank [n, 3] int64 digest tensors -> [world*n, 3]."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    if dist.get_backend(group) == "nccl":  # RCCL on ROCm
+        out = torch.empty((world * local.shape[0], 3), dtype=local.dtype, device=local.device)
+        dist.all_gather_into_tensor(out, local, group=group)
+        return out
+    parts = [torch.empty_like(local) for _ in range(world)]
+    dist.all_gather(parts, local, group=group)
+    return torch.cat(parts)
+
+
+def digests_as_u64(t) -> np.ndarray:
+    return t.cpu().numpy().view(np.uint64)

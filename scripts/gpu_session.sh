@@ -31,4 +31,14 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --outpu
   -- python3 bench.py --steps 3 --warmup 1 --no-cpu > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
 rc=$?; echo "rocprof rc=$rc" | tee -a "$OUT/session.log"
 find "$OUT/prof" -name "*kernel_stats.csv" -exec cat {} \; | head -20
+if [ -n "${PMC:-}" ]; then
+  echo "== rocprofv3 PMC passes" | tee -a "$OUT/session.log"
+  timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv \
+    -- python3 bench.py --steps 2 --warmup 1 --no-cpu > "$OUT/pmc_fetch.json" 2> "$OUT/pmc_fetch.err"
+  rc=$?; echo "pmc fetch rc=$rc" | tee -a "$OUT/session.log"; if fatal $rc; then exit $rc; fi
+  timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv \
+    -- python3 bench.py --steps 2 --warmup 1 --no-cpu > "$OUT/pmc_write.json" 2> "$OUT/pmc_write.err"
+  rc=$?; echo "pmc write rc=$rc" | tee -a "$OUT/session.log"; if fatal $rc; then exit $rc; fi
+  python3 scripts/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_fetch.json" "$OUT/pmc_traffic.json" || true
+fi
 exit 0
