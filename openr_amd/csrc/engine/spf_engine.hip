@@ -118,6 +118,10 @@ Plan make_plan(const ospf_ctx* c, uint32_t W, uint32_t ign_cap, bool unit) {
     p.block = p.lds > 80 * 1024 ? 1024 : (V >= 4096 ? 512 : 256);
   else
     p.block = V >= 4096 ? 512 : 256;
+  if (const char* b = getenv("OSPF_BLOCK")) {  // experiment knob: 256/512/1024
+    const int want = atoi(b);
+    if (want == 256 || want == 512 || want == 1024) p.block = (uint32_t)want;
+  }
   return p;
 }
 

@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Time one root class of the F100k all-sources sweep in isolation (one
+stream, back-to-back launches, HIP events). Experiment harness for kernel
+knobs (OSPF_BLOCK, OSPF_FORCE_VARIANT). Prints one JSON line per config."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from openr_amd import _native as N  # noqa: E402
+from openr_amd import shard, topology as T  # noqa: E402
+from openr_amd.engine import Engine  # noqa: E402
+from openr_amd.linkstate import LinkState  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--pods", type=int, default=1781)
+ap.add_argument("--planes", type=int, default=8)
+ap.add_argument("--W", type=int, nargs="+", default=[1, 3, 56])
+ap.add_argument("--n", type=int, nargs="+", default=[256, 1024, 4096])
+ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--blocks", type=int, nargs="+", default=[0])
+args = ap.parse_args()
+
+torch.cuda.set_device(0)
+st = T.fabric(pods=args.pods, planes=args.planes)
+ls = LinkState(stream=st)
+csr = ls.csr()
+eng = Engine(0)
+eng.load(csr)
+V, E = eng.V, csr["col"].size
+words = shard.nh_words_of(csr["row_ptr"], csr["col"])
+perm = np.random.default_rng(1).permutation(V).astype(np.uint32)
+flags = N.OSPF_WANT_DIST | N.OSPF_WANT_NH | N.OSPF_WANT_DIGEST
+s = torch.cuda.current_stream()
+for W in args.W:
+    members = perm[words[perm] == W]
+    if members.size == 0:
+        continue
+    for n in args.n:
+        roots = torch.from_numpy(np.resize(members, n).astype(np.int32)).cuda()
+        dist = torch.empty((n, V), dtype=torch.int32, device="cuda")
+        nh = torch.empty((n, V, W), dtype=torch.int32, device="cuda")
+        dig = torch.empty((n, 3), dtype=torch.int64, device="cuda")
+        for blk in args.blocks:
+            if blk:
+                os.environ["OSPF_BLOCK"] = str(blk)
+            else:
+                os.environ.pop("OSPF_BLOCK", None)
+            plan = eng.plan(W, flags)
+            ts = []
+            for r in range(args.reps + 1):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(s)
+                eng.run_dev(roots.data_ptr(), n, W, flags=flags, d_dist=dist.data_ptr(),
+                            d_nh=nh.data_ptr(), d_digest=dig.data_ptr(), stream=s.cuda_stream)
+                b.record(s)
+                b.synchronize()
+                if r:
+                    ts.append(a.elapsed_time(b))
+            eng.sync(s.cuda_stream)
+            ms = float(np.median(ts))
+            print(json.dumps(dict(W=W, n=n, plan=plan, ms=round(ms, 3),
+                                  spf_s=round(n / ms * 1e3, 1),
+                                  us_per_root=round(ms * 1e3 / n, 2),
+                                  gteps=round(n * E / ms / 1e6, 2))), flush=True)
