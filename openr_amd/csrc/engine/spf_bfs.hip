@@ -73,6 +73,7 @@ struct Bfs {
   uint32_t *vis, *cur, *nxt;    // LDS bitmaps
   uint32_t* nhb;                // NH_LDS: one byte per node, packed in words
   uint32_t* nh_out;             // HBM next-hop row base (W words per node)
+  uint32_t* plane;              // sliced runs: this slice's [V][4] scratch plane
   uint32_t* dist_out;           // HBM dist row
   const uint32_t* nbr;
   uint32_t nbr_n;
@@ -98,7 +99,13 @@ struct Bfs {
   __device__ __forceinline__ uint32_t nh_byte(uint32_t v) const {
     return (nhb[v >> 2] >> (8 * (v & 3))) & 0xFFu;
   }
+  // where the propagation keeps v's next-hop words: the output row (W <= 4)
+  // or, for sliced wide rows, a compact 16-B-per-node scratch plane so pulls
+  // read whole lines of useful words (copied to the output rows at the end)
   __device__ __forceinline__ uint32_t* row(uint32_t v) const {
+    return plane ? plane + (size_t)v * kSliceWords : nh_out + (size_t)v * W + w0;
+  }
+  __device__ __forceinline__ uint32_t* out_row(uint32_t v) const {
     return nh_out + (size_t)v * W + w0;
   }
   // bit of root-neighbour v inside this slice (>= 32*ws: not in slice)
@@ -110,10 +117,15 @@ struct Bfs {
     if (!usable(e, cx)) return;
     const uint32_t x = cx;
     if (bit(vis, x)) return;
-    atomicOr(&nxt[x >> 5], 1u << (x & 31));
+    // plain LDS reads first: most pushes re-mark a head another tail already
+    // marked with the same next-hops (36 spines -> one fabric switch), and a
+    // no-op atomic still costs an LDS atomic slot. ORs are monotone, so a
+    // stale read only costs an extra atomic.
+    const uint32_t m = 1u << (x & 31);
+    if (!(nxt[x >> 5] & m)) atomicOr(&nxt[x >> 5], m);
     if constexpr (NH_LDS) {
-      const uint32_t val = (u == root) ? (1u << slice_bit(x)) : nbu;
-      atomicOr(&nhb[x >> 2], val << (8 * (x & 3)));
+      const uint32_t val = ((u == root) ? (1u << slice_bit(x)) : nbu) << (8 * (x & 3));
+      if ((nhb[x >> 2] & val) != val) atomicOr(&nhb[x >> 2], val);
     }
   }
 
@@ -208,12 +220,22 @@ struct Bfs {
         end = g.row_ptr[v + 1];
       }
       const bool big = act && (end - beg) > kCoopDeg;
-      if (act && !big) {
-        uint32_t acc[kSliceWords] = {0u, 0u, 0u, 0u};
-        if (pull_edges<1>(v, beg, end, acc)) {
-          store_nh(v, acc);
-          if (PULL_ALL) atomicOr(&nxt[v >> 5], 1u << (v & 31));
-        }
+      uint32_t acc[kSliceWords] = {0u, 0u, 0u, 0u};
+      bool got = false;
+      if (act && !big) got = pull_edges<1>(v, beg, end, acc);
+      if constexpr (NH_LDS && PULL_ALL) {
+        // this wave owns chunk c in this pass: fold the 64 lanes' results
+        // into 2 bitmap words and 16 next-hop words with plain stores
+        const uint64_t gm = __ballot(got);
+        uint32_t byte = got ? (acc[0] << (8 * (lane & 3))) : 0u;
+        byte |= __shfl_xor(byte, 1, kWave);
+        byte |= __shfl_xor(byte, 2, kWave);
+        if ((lane & 3) == 0 && byte) nhb[(c * 64 + lane) >> 2] |= byte;
+        if (lane == 0 && (uint32_t)gm) nxt[c * 2] |= (uint32_t)gm;
+        if (lane == 32 && (uint32_t)(gm >> 32)) nxt[c * 2 + 1] |= (uint32_t)(gm >> 32);
+      } else if (got) {
+        store_nh(v, acc);
+        if (PULL_ALL) atomicOr(&nxt[v >> 5], 1u << (v & 31));
       }
       uint64_t bm = __ballot(big);
       while (bm) {
@@ -308,6 +330,9 @@ __device__ void bfs_run(const DevGraph& g, const RunArgs& a, uint32_t* lds, uint
   b.ign = s_ign;
   b.dist_out = a.dist + (size_t)rix * V;
   b.nh_out = a.nh + (size_t)rix * V * W;
+  b.plane = (!NH_LDS && a.slices > 1 && a.planes)
+                ? a.planes + ((size_t)rix * a.slices + slice) * V * kSliceWords
+                : nullptr;
 
   const uint32_t nb0 = g.dn_off[b.root];
   b.nbr_n = g.dn_off[b.root + 1] - nb0;
@@ -318,7 +343,7 @@ __device__ void bfs_run(const DevGraph& g, const RunArgs& a, uint32_t* lds, uint
   if (!b.slice0 && 32u * b.w0 >= b.nbr_n) {
     // slice past the root's last neighbour: its words are all zero
     for (uint32_t v = tid; v < V; v += blockDim.x)
-      for (uint32_t w = 0; w < b.ws; ++w) b.row(v)[w] = 0u;
+      for (uint32_t w = 0; w < b.ws; ++w) b.out_row(v)[w] = 0u;
     return;
   }
   for (uint32_t i = tid; i < b.nbr_n; i += blockDim.x) s_nbr[i] = g.dn[nb0 + i];
@@ -431,6 +456,11 @@ __device__ void bfs_run(const DevGraph& g, const RunArgs& a, uint32_t* lds, uint
         r[0] = seen ? b.nh_byte(v) : 0u;
         for (uint32_t w = 1; w < b.ws; ++w) r[w] = 0u;
       }
+    } else if (b.plane) {  // copy the compact plane into the output rows
+      const uint4 q = seen ? *reinterpret_cast<const uint4*>(b.row(v)) : make_uint4(0, 0, 0, 0);
+      uint32_t* r = b.out_row(v);
+      const uint32_t qq[4] = {q.x, q.y, q.z, q.w};
+      for (uint32_t w = 0; w < b.ws; ++w) r[w] = qq[w];
     } else if (!seen) {
       for (uint32_t w = 0; w < b.ws; ++w) b.row(v)[w] = 0u;
     }

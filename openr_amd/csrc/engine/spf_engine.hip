@@ -345,8 +345,11 @@ int ospf_sssp_batch_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n_roots,
   size_t need = 0;
   const bool dist_scratch = (p.variant >= 2) && !(flags & OSPF_WANT_DIST);
   const bool nh_scratch = (p.variant >= 1) && !(flags & OSPF_WANT_NH);
+  const uint32_t slices = p.variant >= 3 ? ospf::bfs_slices(nh_words) : 1u;
+  const size_t planes_bytes = slices > 1 ? align_up((size_t)n_roots * slices * V * 16ull, 256) : 0;
   if (dist_scratch) need += align_up(n_roots * V * 4, 256);
   if (nh_scratch) need += align_up(n_roots * V * nh_words * 4ull, 256);
+  need += planes_bytes;
   if (need) {
     int rc = ensure(c, &c->d_scratch, &c->scratch_bytes, need);
     if (rc) return rc;
@@ -364,7 +367,12 @@ int ospf_sssp_batch_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n_roots,
   a.nh = d_nh;
   a.digest = d_digest;
   a.err = c->d_err;
-  a.slices = p.variant >= 3 ? ospf::bfs_slices(nh_words) : 1u;
+  a.slices = slices;
+  a.planes = nullptr;
+  if (planes_bytes) {
+    a.planes = (uint32_t*)sp;
+    sp += planes_bytes;
+  }
   if (dist_scratch) {
     a.dist = (uint32_t*)sp;
     sp += align_up(n_roots * V * 4, 256);

@@ -40,6 +40,7 @@ struct RunArgs {
   ospf_digest* digest;      // [n_roots] when OSPF_WANT_DIGEST
   uint32_t* err;            // device error word (bit0: nh words, bit1: ignore cap)
   uint32_t slices;          // BFS kernel: workgroups per run (4-word next-hop slices)
+  uint32_t* planes;         // BFS kernel, slices > 1: [n_roots][slices][V][4] scratch
 };
 
 // Digest: sum over reached nodes of node_term(v, dist) plus,
