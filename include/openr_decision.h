@@ -64,6 +64,17 @@ int odl_spf_prefetch(odl_ls* ls, const char* roots_nl, uint32_t n, int use_link_
  * text = paths of each d, then a line "=". */
 char* odl_ksp2_text(odl_ls* ls, const char* src, const char* dsts_nl, uint32_t n);
 
+/* Route building over the GPU SPF results (SpfSolver consumers, SURVEY.md §8
+ * a8-a10) for a prefix announced by `announcers` ('\n'-separated):
+ *   algo 0 = SP_ECMP unicast (getNextHopsWithMetric + getNextHopsThrift,
+ *            SpfSolver.cpp:1043-1285), 1 = KSP2_ED_ECMP (selectBestPathsKsp2,
+ *            SpfSolver.cpp:847-973), 2 = MPLS node-label route of the single
+ *            announcer (PHP / SWAP, SpfSolver.cpp:501-598).
+ * Text: one next-hop per line, sorted: ifName \t neighbor \t metric \t
+ * mpls-op (0 none, 1 PHP, 2 SWAP, 3 PUSH) \t labels (',' separated). */
+char* odl_route_text(odl_ls* ls, const char* me, const char* announcers_nl, uint32_t n,
+                     int algo);
+
 /* CSR snapshot the engine sees (node ids = rank of name, byte order).
  * Copies into caller arrays sized by odl_csr_size(); any pointer may be NULL. */
 int odl_csr_size(odl_ls* ls, uint32_t* n_nodes, uint32_t* n_edges);

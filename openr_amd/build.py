@@ -16,13 +16,14 @@ ROOT = os.path.dirname(PKG)
 LIB = os.path.join(PKG, "lib")
 ENGINE_SRC = [os.path.join(PKG, "csrc", "engine", f) for f in ("spf_kernels.hip", "spf_bfs.hip", "spf_engine.hip")]
 DECISION_SRC = [os.path.join(PKG, "csrc", "decision", f)
-                for f in ("link_state.cpp", "decision_capi.cpp")]
+                for f in ("link_state.cpp", "spf_solver.cpp", "decision_capi.cpp")]
 ENGINE_SO = os.path.join(LIB, "libopenr_spf_hip.so")
 DECISION_SO = os.path.join(LIB, "libopenr_decision.so")
 HEADERS = [os.path.join(ROOT, "include", h)
            for h in ("openr_spf.h", "openr_decision.h", "openr_adjdb.h")] + \
     [os.path.join(PKG, "csrc", "engine", "spf_kernels.h"),
-     os.path.join(PKG, "csrc", "decision", "link_state.h")]
+     os.path.join(PKG, "csrc", "decision", "link_state.h"),
+     os.path.join(PKG, "csrc", "decision", "spf_solver.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"

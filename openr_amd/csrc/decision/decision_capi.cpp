@@ -9,6 +9,7 @@
 
 #include "../../../include/openr_decision.h"
 #include "link_state.h"
+#include "spf_solver.h"
 
 struct odl_ls {
   odl::LinkState ls;
@@ -205,6 +206,26 @@ char* odl_ksp2_text(odl_ls* h, const char* src, const char* dsts_nl, uint32_t n)
     for (const auto& d : dsts) {
       pathsText(os, h->ls.getKthPaths(src, d, 2));
       os << "=\n";
+    }
+    return dup(os.str());
+  }, (char*)nullptr);
+}
+
+char* odl_route_text(odl_ls* h, const char* me, const char* announcers_nl, uint32_t n,
+                     int algo) {
+  return guard(h, [&]() -> char* {
+    odl::SpfSolver solver(h->ls);
+    const auto ann = splitNl(announcers_nl, n);
+    std::vector<odl::NextHop> nhs;
+    if (algo == 0) nhs = solver.ecmpRoute(me, ann);
+    else if (algo == 1) nhs = solver.ksp2Route(me, ann);
+    else if (algo == 2 && n == 1) nhs = solver.nodeLabelRoute(me, ann[0]);
+    else throw std::invalid_argument("algo must be 0, 1 or 2 (2 needs one announcer)");
+    std::ostringstream os;
+    for (const auto& x : nhs) {
+      os << x.ifName << '\t' << x.neighbor << '\t' << x.metric << '\t' << (int)x.op << '\t';
+      for (size_t i = 0; i < x.labels.size(); ++i) os << (i ? "," : "") << x.labels[i];
+      os << '\n';
     }
     return dup(os.str());
   }, (char*)nullptr);

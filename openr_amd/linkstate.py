@@ -87,6 +87,19 @@ class LinkState:
         return self._take(self._L.odl_ksp2_text(self._h, src.encode(),
                                                 "\n".join(dsts).encode(), len(dsts)))
 
+    def route(self, me: str, announcers: Sequence[str], algo: str = "ecmp"):
+        """Route next-hops built in C++ (odl::SpfSolver): algo 'ecmp',
+        'ksp2' or 'label'. Returns a set of (ifName, metric, labels)."""
+        code = {"ecmp": 0, "ksp2": 1, "label": 2}[algo]
+        t = self._take(self._L.odl_route_text(self._h, me.encode(),
+                                              "\n".join(announcers).encode(),
+                                              len(announcers), code))
+        out = set()
+        for ln in t.splitlines():
+            ifn, nbr, metric, op, labels = ln.split("\t")
+            out.add((ifn, int(metric), tuple(int(x) for x in labels.split(",") if x)))
+        return out or None
+
     def links(self, node: str):
         out = []
         for ln in self._take(self._L.odl_links_text(self._h, node.encode())).splitlines():

@@ -157,6 +157,9 @@ def run_fixture(fx: dict, make_ls, check_changes: bool = True, spf: bool = True)
             elif k == "ecmp":
                 assert ecmp_routes(ls, c["src"], c["dst"]) == _as_set(c["expect"]), \
                     f"{where}: {ecmp_routes(ls, c['src'], c['dst'])}"
+                if hasattr(ls, "route"):  # the product's C++ SpfSolver port
+                    got = ls.route(c["src"], [c["dst"]], "ecmp")
+                    assert got == _as_set(c["expect"]), f"{where}: C++ {got}"
             elif k == "ecmp_all":
                 for a in c["nodes"]:
                     for b in c["nodes"]:
@@ -164,6 +167,9 @@ def run_fixture(fx: dict, make_ls, check_changes: bool = True, spf: bool = True)
             elif k == "ksp2":
                 got = ksp2_routes(ls, c["src"], c["dst"], labels, metrics)
                 assert got == _as_set(c["expect"]), f"{where}: {got}"
+                if hasattr(ls, "route"):  # the product's C++ SpfSolver port
+                    got = ls.route(c["src"], [c["dst"]], "ksp2")
+                    assert got == _as_set(c["expect"]), f"{where}: C++ {got}"
             elif k == "ksp2_all":
                 for a in c["nodes"]:
                     for b in c["nodes"]:
