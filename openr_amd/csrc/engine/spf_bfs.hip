@@ -38,7 +38,6 @@ constexpr uint32_t kDown = 0x80000000u;
 constexpr int kWave = 64;
 constexpr uint32_t kCoopDeg = 32;
 constexpr uint32_t kSliceWords = 4;
-constexpr uint32_t kUnroll = 8;
 
 __device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* a, uint32_t n, uint32_t key) {
   uint32_t lo = 0, hi = n;
@@ -126,19 +125,28 @@ struct Bfs {
     }
   }
 
-  // edges [beg, end) of u, one lane (STEP 1) or the whole wave (STEP 64),
-  // CSR loads issued kUnroll at a time so each lane keeps several in flight
-  template <uint32_t STEP>
+  // edges [beg, end) of u (a padded row: beg, end multiples of 4), one lane
+  // (LANES 1) or the whole wave (LANES 64, lane offset folded into beg),
+  // read as uint4 so one load instruction fetches 4 CSR entries
+  template <uint32_t LANES>
   __device__ __forceinline__ void push_edges(uint32_t u, uint32_t beg, uint32_t end,
                                              uint32_t nbu) {
-    for (uint32_t e = beg; e < end; e += kUnroll * STEP) {
-      uint32_t cx[kUnroll];
-#pragma unroll
-      for (uint32_t k = 0; k < kUnroll; ++k)
-        cx[k] = (e + k * STEP < end) ? g.colx[e + k * STEP] : kDown;
-#pragma unroll
-      for (uint32_t k = 0; k < kUnroll; ++k)
-        if (e + k * STEP < end) push_one(u, e + k * STEP, cx[k], nbu);
+    const uint4* q = reinterpret_cast<const uint4*>(g.colx);
+    for (uint32_t e = beg; e < end; e += 4 * LANES * 2) {
+      const uint4 a = q[e >> 2];
+      const bool two = e + 4 * LANES < end;
+      const uint4 b = two ? q[(e + 4 * LANES) >> 2] : make_uint4(kDown, kDown, kDown, kDown);
+      push_one(u, e, a.x, nbu);
+      push_one(u, e + 1, a.y, nbu);
+      push_one(u, e + 2, a.z, nbu);
+      push_one(u, e + 3, a.w, nbu);
+      if (two) {
+        const uint32_t f = e + 4 * LANES;
+        push_one(u, f, b.x, nbu);
+        push_one(u, f + 1, b.y, nbu);
+        push_one(u, f + 2, b.z, nbu);
+        push_one(u, f + 3, b.w, nbu);
+      }
     }
   }
 
@@ -169,18 +177,26 @@ struct Bfs {
     }
   }
 
-  template <uint32_t STEP>
+  template <uint32_t LANES>
   __device__ __forceinline__ bool pull_edges(uint32_t v, uint32_t beg, uint32_t end,
                                              uint32_t* acc) const {
     bool any = false;
-    for (uint32_t e = beg; e < end; e += kUnroll * STEP) {
-      uint32_t cx[kUnroll];
-#pragma unroll
-      for (uint32_t k = 0; k < kUnroll; ++k)
-        cx[k] = (e + k * STEP < end) ? g.colx[e + k * STEP] : kDown;
-#pragma unroll
-      for (uint32_t k = 0; k < kUnroll; ++k)
-        if (e + k * STEP < end) pull_one(v, e + k * STEP, cx[k], acc, any);
+    const uint4* q = reinterpret_cast<const uint4*>(g.colx);
+    for (uint32_t e = beg; e < end; e += 4 * LANES * 2) {
+      const uint4 a = q[e >> 2];
+      const bool two = e + 4 * LANES < end;
+      const uint4 b = two ? q[(e + 4 * LANES) >> 2] : make_uint4(kDown, kDown, kDown, kDown);
+      pull_one(v, e, a.x, acc, any);
+      pull_one(v, e + 1, a.y, acc, any);
+      pull_one(v, e + 2, a.z, acc, any);
+      pull_one(v, e + 3, a.w, acc, any);
+      if (two) {
+        const uint32_t f = e + 4 * LANES;
+        pull_one(v, f, b.x, acc, any);
+        pull_one(v, f + 1, b.y, acc, any);
+        pull_one(v, f + 2, b.z, acc, any);
+        pull_one(v, f + 3, b.w, acc, any);
+      }
     }
     return any;
   }
@@ -231,7 +247,7 @@ struct Bfs {
         const uint32_t bv = __shfl(v, l, kWave), bb = __shfl(beg, l, kWave),
                        be = __shfl(end, l, kWave);
         uint32_t acc[kSliceWords] = {0u, 0u, 0u, 0u};
-        const bool any = __ballot(pull_edges<kWave>(bv, bb + lane, be, acc)) != 0;
+        const bool any = __ballot(pull_edges<kWave>(bv, bb + 4 * lane, be, acc)) != 0;
 #pragma unroll
         for (uint32_t w = 0; w < kSliceWords; ++w) acc[w] = wor(acc[w]);
         if (any && lane == 0) {
@@ -264,7 +280,7 @@ struct Bfs {
         bm &= bm - 1;
         const uint32_t bv = __shfl(v, l, kWave), bb = __shfl(beg, l, kWave),
                        be = __shfl(end, l, kWave), bn = __shfl(nbv, l, kWave);
-        push_edges<kWave>(bv, bb + lane, be, bn);
+        push_edges<kWave>(bv, bb + 4 * lane, be, bn);
       }
     }
   }

@@ -222,8 +222,26 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   if (max_dn > OSPF_MAX_ROOT_NEIGHBORS)
     return fail(c, OSPF_E_RANGE, "a node has more distinct neighbours than OSPF_MAX_ROOT_NEIGHBORS");
 
+  // Device rows are padded to a multiple of 4 entries with down-marked
+  // fillers (colx = 0x80000000, link id UINT32_MAX) so every row starts on a
+  // 16-B boundary and the kernels read the CSR with uint4 loads.
+  std::vector<uint32_t> prow(V + 1, 0u);
+  for (uint32_t u = 0; u < V; ++u)
+    prow[u + 1] = prow[u] + ((csr->row_ptr[u + 1] - csr->row_ptr[u] + 3u) & ~3u);
+  const uint32_t Ep = prow[V];
+  std::vector<uint32_t> pcolx(Ep, 0x80000000u), pw(Ep, 0u), prw(Ep, 0u), plink(Ep, 0xFFFFFFFFu);
+  for (uint32_t u = 0; u < V; ++u) {
+    const uint32_t b = csr->row_ptr[u], n = csr->row_ptr[u + 1] - b, pb = prow[u];
+    for (uint32_t k = 0; k < n; ++k) {
+      pcolx[pb + k] = colx[b + k];
+      pw[pb + k] = csr->metric[b + k];
+      prw[pb + k] = rw[b + k];
+      plink[pb + k] = csr->link_id[b + k];
+    }
+  }
+
   // device layout: one allocation, 256-B aligned sub-buffers
-  const size_t sz_row = (V + 1) * 4ull, sz_e = (size_t)E * 4ull, sz_nt = nt.size() * 4ull,
+  const size_t sz_row = (V + 1) * 4ull, sz_e = (size_t)Ep * 4ull, sz_nt = nt.size() * 4ull,
                sz_dnoff = (V + 1) * 4ull, sz_dn = std::max<size_t>(dn.size(), 1) * 4ull;
   size_t off[8], tot = 0;
   const size_t szs[8] = {sz_row, sz_e, sz_e, sz_e, sz_e, sz_nt, sz_dnoff, sz_dn};
@@ -243,12 +261,12 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
     return fail(c, OSPF_E_NOMEM, std::string("hipMalloc graph: ") + hipGetErrorString(he));
   }
   char* base = (char*)c->d_graph;
-  const void* srcs[8] = {csr->row_ptr, colx.data(), csr->metric, rw.data(), csr->link_id,
+  const void* srcs[8] = {prow.data(), pcolx.data(), pw.data(), prw.data(), plink.data(),
                          nt.data(), dn_off.data(), dn.data()};
   for (int i = 0; i < 8; ++i)
     if (szs[i] && srcs[i]) HIPCHK(c, hipMemcpy(base + off[i], srcs[i], szs[i], hipMemcpyHostToDevice));
   c->g.V = V;
-  c->g.E = E;
+  c->g.E = Ep;
   c->g.row_ptr = (const uint32_t*)(base + off[0]);
   c->g.colx = (const uint32_t*)(base + off[1]);
   c->g.w = (const uint32_t*)(base + off[2]);

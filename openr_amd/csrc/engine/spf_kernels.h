@@ -7,7 +7,9 @@
 
 namespace ospf {
 
-// Device-resident CSR snapshot (built once per ospf_load_graph).
+// Device-resident CSR snapshot (built once per ospf_load_graph). Rows are
+// padded to a multiple of 4 entries (row_ptr[v] % 4 == 0) with down-marked
+// fillers, so rows can be read as uint4; E counts the padded entries.
 //   colx[e]    = neighbour id | 0x80000000 when the link is down (!isUp)
 //   w[e]       = metric advertised by the row node (u -> colx[e])
 //   rw[e]      = w[twin[e]]: metric of the reverse direction, i.e. of the
