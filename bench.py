@@ -116,13 +116,15 @@ def main():
 
     flags = N.OSPF_WANT_DIST | N.OSPF_WANT_DIGEST | (0 if args.no_nh else N.OSPF_WANT_NH)
     perm = np.random.default_rng(0x5EED).permutation(V).astype(np.uint32)
-    words = shard.nh_words_of(csr["row_ptr"], csr["col"])
+    nbrs = shard.distinct_neighbors(csr["row_ptr"], csr["col"])
+    words = np.maximum(1, (nbrs + 31) // 32)
     classes = shard.make_classes(perm, words, args.batch)
     B = sum(c.per_step for c in classes)
     for c in classes:
         n = c.per_step
         x = c.extra
-        x["plan"] = eng.plan(c.nh_words, flags)
+        x["max_nbrs"] = int(max(1, nbrs[c.roots].max()))  # engine hint: sizes bit-planes
+        x["plan"] = eng.plan(c.nh_words, flags, n_roots=n, max_root_neighbors=x["max_nbrs"])
         x["d_all"] = torch.from_numpy(c.roots.astype(np.int32)).to(dev)
         x["roots"] = torch.empty(n, dtype=torch.int32, device=dev)
         x["dist"] = torch.empty((n, V), dtype=torch.int32, device=dev)
@@ -153,7 +155,8 @@ def main():
                 eng.run_dev(x["roots"].data_ptr(), n, c.nh_words, flags=flags,
                             d_dist=x["dist"].data_ptr(),
                             d_nh=x["nh"].data_ptr() if x["nh"] is not None else 0,
-                            d_digest=x["dig"].data_ptr(), stream=cs.cuda_stream)
+                            d_digest=x["dig"].data_ptr(), stream=cs.cuda_stream,
+                            max_root_neighbors=x["max_nbrs"])
                 ev[1].record(cs)
             done.append(ev[1])
             if timed:
@@ -205,7 +208,10 @@ def main():
     roofline = {
         "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-        "kernel": f"spf_bfs_kernel (variant {p['variant']}, nh_words {dom.nh_words})"
+        "kernel": (f"msbfs_level_kernel + init/final/row_digest (variant 5, nh_words "
+                   f"{dom.nh_words}; one 'launch' = the class's kernel sequence)")
+        if p["variant"] == 5 else
+        f"spf_bfs_kernel (variant {p['variant']}, nh_words {dom.nh_words})"
         if p["variant"] >= 3 else f"spf_run_kernel (variant {p['variant']})",
         "grid": dom.per_step * p["slices"], "block": p["block"], "lds_bytes": p["lds_bytes"],
         "roots_per_launch": dom.per_step, "bytes_per_root": bytes_per_root(V, E, dom.nh_words),

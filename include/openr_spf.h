@@ -141,13 +141,35 @@ int ospf_sssp_batch_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n_roots
                         uint32_t* d_dist, uint32_t* d_nh, ospf_digest* d_digest,
                         void* stream);
 
+/* Device-resident batch with every option in one descriptor. Same contract
+ * as ospf_sssp_batch_dev, plus a hint: max_root_neighbors >= the distinct
+ * neighbour count of every root in the batch (0 = unknown, 32 * nh_words).
+ * It sizes the multi-source BFS (next-hop passes and planes); a root above
+ * it raises the device error word like a too-small nh_words. */
+typedef struct ospf_batch {
+  const uint32_t* d_roots;
+  uint32_t n_roots;
+  const uint32_t* d_ign_offsets; /* NULL = no run ignores links */
+  const uint32_t* d_ign_ids;
+  uint32_t max_ignored;
+  uint32_t flags;
+  uint32_t nh_words;
+  uint32_t max_root_neighbors;
+  uint32_t* d_dist;
+  uint32_t* d_nh;
+  ospf_digest* d_digest;
+} ospf_batch;
+int ospf_run_batch_dev(ospf_ctx* ctx, const ospf_batch* batch, void* stream);
+
 /* Wait for `stream`, then report (and clear) the device error word:
  * OSPF_OK or OSPF_E_RANGE. */
 int ospf_sync(ospf_ctx* ctx, void* stream);
 
-/* Kernel variant the engine would use for a batch (for reporting):
- * 0 = LDS-resident (dist+nh in LDS), 1 = LDS dist + HBM next-hops,
- * 2 = HBM frontier (dist+nh in HBM). */
+/* Kernel variant the engine would use for a large batch (for reporting):
+ * 0 = Dial, LDS-resident (dist+nh in LDS), 1 = Dial, LDS dist + HBM
+ * next-hops, 2 = Dial, HBM state, 3 = per-root BFS with LDS bitmaps and LDS
+ * byte next-hops, 4 = per-root BFS with HBM next-hops, 5 = multi-source
+ * bit-parallel BFS (64 roots per traversal; unit metric, no ignored links). */
 int ospf_plan_variant(const ospf_ctx* ctx, uint32_t flags, uint32_t nh_words,
                       int* variant);
 
@@ -156,10 +178,15 @@ typedef struct ospf_plan_info {
   int32_t variant;       /* as ospf_plan_variant */
   uint32_t block;        /* threads per workgroup */
   uint32_t lds_bytes;    /* dynamic LDS per workgroup */
-  uint32_t slices;       /* workgroups per SPF run (next-hop slices) */
+  uint32_t slices;       /* workgroups per SPF run (next-hop slices); variant 5:
+                            passes per 64-root batch */
 } ospf_plan_info;
 int ospf_plan(const ospf_ctx* ctx, uint32_t flags, uint32_t nh_words, uint32_t max_ignored,
               ospf_plan_info* out);
+/* Same for a batch of n_roots roots with the given neighbour hint (variant 5:
+ * slices = next-hop passes per 64-root batch). */
+int ospf_plan_n(const ospf_ctx* ctx, uint32_t flags, uint32_t nh_words, uint32_t max_ignored,
+                uint32_t n_roots, uint32_t max_root_neighbors, ospf_plan_info* out);
 
 /* Runtime statistics. spf_runs counts logical runSpf executions (one per
  * root per batch), matching the reference's decision.spf_runs counter

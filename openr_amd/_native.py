@@ -27,7 +27,7 @@ OSPF_WANT_DIGEST = 0x8
 ENGINE_SYMBOLS = [
     "ospf_open", "ospf_close", "ospf_last_error", "ospf_load_graph", "ospf_graph_info_get",
     "ospf_root_neighbors", "ospf_sssp_batch", "ospf_sssp_batch_dev", "ospf_sync",
-    "ospf_plan_variant", "ospf_plan", "ospf_spf_runs",
+    "ospf_plan_variant", "ospf_plan", "ospf_plan_n", "ospf_spf_runs", "ospf_run_batch_dev",
 ]
 DECISION_SYMBOLS = [
     "odl_create", "odl_destroy", "odl_last_error", "odl_free", "odl_apply", "odl_spf_text",
@@ -49,6 +49,12 @@ class ospf_ignore(C.Structure):  # noqa: N801
 
 class ospf_digest(C.Structure):  # noqa: N801
     _fields_ = [("reached", u64), ("sum_dist", u64), ("hash", u64)]
+
+
+class ospf_batch(C.Structure):  # noqa: N801
+    _fields_ = [("d_roots", vp), ("n_roots", u32), ("d_ign_offsets", vp), ("d_ign_ids", vp),
+                ("max_ignored", u32), ("flags", u32), ("nh_words", u32),
+                ("max_root_neighbors", u32), ("d_dist", vp), ("d_nh", vp), ("d_digest", vp)]
 
 
 class ospf_plan_info(C.Structure):  # noqa: N801
@@ -88,6 +94,8 @@ def engine() -> C.CDLL:
         L.ospf_sync.argtypes = [vp, vp]
         L.ospf_plan_variant.argtypes = [vp, u32, u32, C.POINTER(C.c_int)]
         L.ospf_plan.argtypes = [vp, u32, u32, u32, C.POINTER(ospf_plan_info)]
+        L.ospf_plan_n.argtypes = [vp, u32, u32, u32, u32, u32, C.POINTER(ospf_plan_info)]
+        L.ospf_run_batch_dev.argtypes = [vp, C.POINTER(ospf_batch), vp]
         L.ospf_spf_runs.argtypes = [vp]
         L.ospf_spf_runs.restype = u64
         _engine = L

@@ -30,6 +30,7 @@ struct ospf_ctx {
   void* d_graph = nullptr;
   ospf::DevGraph g{};
   uint32_t max_dn = 0;
+  uint32_t depth_bound = 2;  // BFS levels any root can reach (unit metric / hop count)
   // scratch
   void* d_scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -79,7 +80,11 @@ struct Plan {
   uint32_t nbr_cap, ign_cap;
 };
 
-Plan make_plan(const ospf_ctx* c, uint32_t W, uint32_t ign_cap, bool unit) {
+// multi-source BFS (variant 5) pays a fixed per-level cost for a whole
+// 64-root batch; below this many roots the per-root kernels win
+constexpr uint32_t kMsMinRoots = 32;
+
+Plan make_plan(const ospf_ctx* c, uint32_t W, uint32_t ign_cap, bool unit, uint32_t n_roots) {
   Plan p{};
   const size_t V = c->info.n_nodes;
   p.nbr_cap = (uint32_t)align_up(std::max<uint32_t>(c->max_dn, 1), 4);
@@ -98,10 +103,13 @@ Plan make_plan(const ospf_ctx* c, uint32_t W, uint32_t ign_cap, bool unit) {
       case 2: return true;
       case 3: return unit && bfs_nh <= lim;
       case 4: return unit && bfs <= lim;
+      case 5: return unit && ign_cap == 0;
     }
     return false;
   };
-  if (unit) {
+  if (unit && fits(5) && n_roots >= kMsMinRoots) {
+    p.variant = 5;
+  } else if (unit) {
     p.variant = (W == 1 && fits(3)) ? 3 : fits(4) ? 4 : 2;
   } else {
     p.variant = fits(0) ? 0 : fits(1) ? 1 : 2;
@@ -110,11 +118,13 @@ Plan make_plan(const ospf_ctx* c, uint32_t W, uint32_t ign_cap, bool unit) {
   // its state fits (e.g. the HBM-state Dial kernel on a small graph).
   if (const char* f = getenv("OSPF_FORCE_VARIANT")) {
     const int want = atoi(f);
-    if (want >= 0 && want <= 4 && fits(want)) p.variant = want;
+    if (want >= 0 && want <= 5 && fits(want)) p.variant = want;
   }
-  const size_t ldsz[5] = {full, half, head, bfs_nh, bfs};
+  const size_t ldsz[6] = {full, half, head, bfs_nh, bfs, 0};
   p.lds = ldsz[p.variant];
-  if (p.variant >= 3)
+  if (p.variant == 5)
+    p.block = 256;
+  else if (p.variant >= 3)
     p.block = p.lds > 80 * 1024 ? 1024 : (V >= 4096 ? 512 : 256);
   else
     p.block = V >= 4096 ? 512 : 256;
@@ -123,6 +133,113 @@ Plan make_plan(const ospf_ctx* c, uint32_t W, uint32_t ign_cap, bool unit) {
     if (want == 256 || want == 512 || want == 1024) p.block = (uint32_t)want;
   }
   return p;
+}
+
+// Upper bound on the number of BFS levels (max hop distance) from any root.
+// A shortest path r = x0, x1, ..., xk = v has transit interior nodes
+// x1..x(k-1) (overloaded nodes never relax, LinkState.cpp:859-866), and its
+// interior is a shortest path of the transit subgraph G' (usable links
+// between transit nodes), so k <= diam(component) + 2 <= 2 * ecc(seed) + 2.
+// O(V + E) on the host at load time; lets the multi-source BFS launch a
+// fixed number of level kernels with no device -> host round trip.
+uint32_t transit_depth_bound(uint32_t V, const uint32_t* row_ptr, const uint32_t* colx,
+                             const std::vector<uint32_t>& nt) {
+  auto transit = [&](uint32_t u) { return !((nt[u >> 5] >> (u & 31)) & 1u); };
+  std::vector<uint32_t> lvl(V, 0xFFFFFFFFu), q;
+  q.reserve(V);
+  uint32_t ecc_max = 0;
+  for (uint32_t s = 0; s < V; ++s) {
+    if (!transit(s) || lvl[s] != 0xFFFFFFFFu) continue;
+    q.clear();
+    q.push_back(s);
+    lvl[s] = 0;
+    uint32_t ecc = 0;
+    for (size_t i = 0; i < q.size(); ++i) {
+      const uint32_t u = q[i];
+      for (uint32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e) {
+        const uint32_t cx = colx[e];
+        if (cx & 0x80000000u) continue;
+        if (!transit(cx) || lvl[cx] != 0xFFFFFFFFu) continue;
+        lvl[cx] = lvl[u] + 1;
+        ecc = std::max(ecc, lvl[cx]);
+        q.push_back(cx);
+      }
+    }
+    ecc_max = std::max(ecc_max, ecc);
+  }
+  return 2u * ecc_max + 2u;
+}
+
+// Variant 5: multi-source bit-parallel BFS (spf_msbfs.hip). Roots go in
+// 64-root batches; each batch runs one pass per computed next-hop word; a
+// round runs up to `nb` (batch, word) pairs side by side. All launches are
+// queued on `s`; nothing waits on the host.
+int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
+  const uint32_t V = c->info.n_nodes, W = b->nh_words, flags = b->flags;
+  const uint32_t kcap = b->max_root_neighbors ? std::min(b->max_root_neighbors, 32u * W) : 32u * W;
+  const uint32_t npass = std::max<uint32_t>(1, (kcap + 31) / 32);
+  const uint32_t kneed = std::min<uint32_t>(32, kcap);
+  const int kp = kneed <= 8 ? 8 : kneed <= 16 ? 16 : 32;
+  const bool dig = flags & OSPF_WANT_DIGEST;
+  const bool dist_scr = dig && !(flags & OSPF_WANT_DIST);
+  const bool nh_scr = dig && !(flags & OSPF_WANT_NH);
+  const uint32_t lmax = c->depth_bound + 2;
+  // seen, front x2, accb, planes (u64 per node each) + found, mass
+  const size_t per_vb = align_up((size_t)V * 8ull * (4 + kp) + lmax * 8ull, 256);
+  uint32_t push_div = 8;  // push a level when its frontier's edge mass * push_div < E
+  if (const char* e = getenv("OSPF_MS_PUSH_DIV")) push_div = (uint32_t)std::max(0, atoi(e));
+  uint32_t nb_cap = 32;
+  if (const char* e = getenv("OSPF_MS_NB")) nb_cap = std::max(1, atoi(e));
+  nb_cap = (uint32_t)std::max<size_t>(1, std::min<size_t>(nb_cap, (4ull << 30) / per_vb));
+  // roots per chunk: bounded when digest rows live in scratch
+  const size_t row_bytes = (dist_scr ? V * 4ull : 0) + (nh_scr ? (size_t)V * W * 4ull : 0);
+  uint32_t chunk = b->n_roots;
+  if (row_bytes)
+    chunk = (uint32_t)std::max<size_t>(64, std::min<size_t>(chunk, (2ull << 30) / row_bytes) / 64 * 64);
+  const uint32_t nb_max = std::min<uint32_t>(nb_cap, ((std::min(chunk, b->n_roots) + 63) / 64) * npass);
+  const size_t state_bytes = per_vb * nb_max;
+  const size_t dist_bytes = dist_scr ? align_up((size_t)chunk * V * 4ull, 256) : 0;
+  const size_t nh_bytes = nh_scr ? align_up((size_t)chunk * V * W * 4ull, 256) : 0;
+  int rc = ensure(c, &c->d_scratch, &c->scratch_bytes, state_bytes + dist_bytes + nh_bytes);
+  if (rc) return rc;
+  char* sp = (char*)c->d_scratch;
+  HIPCHK(c, hipSetDevice(c->device));
+  for (uint32_t r0 = 0; r0 < b->n_roots; r0 += chunk) {
+    const uint32_t n = std::min(chunk, b->n_roots - r0);
+    ospf::MsArgs a{};
+    a.roots = b->d_roots + r0;
+    a.n = n;
+    a.W = W;
+    a.npass = npass;
+    a.lmax = lmax;
+    a.kcap = kcap;
+    a.push_div = push_div;
+    a.err = c->d_err;
+    a.dist = dist_scr ? (uint32_t*)(sp + state_bytes)
+                      : ((flags & OSPF_WANT_DIST) ? b->d_dist + (size_t)r0 * V : nullptr);
+    a.nh = nh_scr ? (uint32_t*)(sp + state_bytes + dist_bytes)
+                  : ((flags & OSPF_WANT_NH) ? b->d_nh + (size_t)r0 * V * W : nullptr);
+    const uint32_t total_vb = ((n + 63) / 64) * npass;
+    for (uint32_t vb0 = 0; vb0 < total_vb; vb0 += nb_max) {
+      a.vb0 = vb0;
+      a.nb = std::min(nb_max, total_vb - vb0);
+      a.seen = (uint64_t*)sp;
+      a.front = a.seen + (size_t)a.nb * V;
+      a.accb = a.front + 2ull * a.nb * V;
+      a.planes = a.accb + (size_t)a.nb * V;
+      a.found = (uint32_t*)(a.planes + (size_t)a.nb * V * kp);
+      a.mass = a.found + (size_t)a.nb * lmax;
+      HIPCHK(c, hipMemsetAsync(sp, 0, (size_t)a.nb * V * 8ull * (4 + kp) + (size_t)a.nb * lmax * 8ull, s));
+      hipError_t e = ospf::launch_msbfs_round(kp, c->g, a, c->depth_bound, s);
+      if (e != hipSuccess) return hip_fail(c, e, "launch_msbfs_round");
+    }
+    if (dig) {
+      hipError_t e = ospf::launch_row_digest(c->g, a.roots, n, a.dist, a.nh, W, kcap, b->d_digest + r0, s);
+      if (e != hipSuccess) return hip_fail(c, e, "launch_row_digest");
+    }
+  }
+  c->spf_runs += b->n_roots;
+  return OSPF_OK;
 }
 
 }  // namespace
@@ -241,11 +358,15 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   }
 
   // device layout: one allocation, 256-B aligned sub-buffers
+  std::vector<uint32_t> big;  // rows the multi-source BFS scans with a whole wave
+  for (uint32_t u = 0; u < V; ++u)
+    if (prow[u + 1] - prow[u] > ospf::kMsBigDeg) big.push_back(u);
   const size_t sz_row = (V + 1) * 4ull, sz_e = (size_t)Ep * 4ull, sz_nt = nt.size() * 4ull,
-               sz_dnoff = (V + 1) * 4ull, sz_dn = std::max<size_t>(dn.size(), 1) * 4ull;
-  size_t off[8], tot = 0;
-  const size_t szs[8] = {sz_row, sz_e, sz_e, sz_e, sz_e, sz_nt, sz_dnoff, sz_dn};
-  for (int i = 0; i < 8; ++i) {
+               sz_dnoff = (V + 1) * 4ull, sz_dn = std::max<size_t>(dn.size(), 1) * 4ull,
+               sz_big = std::max<size_t>(big.size(), 1) * 4ull;
+  size_t off[9], tot = 0;
+  const size_t szs[9] = {sz_row, sz_e, sz_e, sz_e, sz_e, sz_nt, sz_dnoff, sz_dn, sz_big};
+  for (int i = 0; i < 9; ++i) {
     off[i] = tot;
     tot += align_up(std::max<size_t>(szs[i], 4), 256);
   }
@@ -261,9 +382,9 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
     return fail(c, OSPF_E_NOMEM, std::string("hipMalloc graph: ") + hipGetErrorString(he));
   }
   char* base = (char*)c->d_graph;
-  const void* srcs[8] = {prow.data(), pcolx.data(), pw.data(), prw.data(), plink.data(),
-                         nt.data(), dn_off.data(), dn.data()};
-  for (int i = 0; i < 8; ++i)
+  const void* srcs[9] = {prow.data(), pcolx.data(), pw.data(), prw.data(), plink.data(),
+                         nt.data(), dn_off.data(), dn.data(), big.data()};
+  for (int i = 0; i < 9; ++i)
     if (szs[i] && srcs[i]) HIPCHK(c, hipMemcpy(base + off[i], srcs[i], szs[i], hipMemcpyHostToDevice));
   c->g.V = V;
   c->g.E = Ep;
@@ -275,10 +396,13 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   c->g.nt_bits = (const uint32_t*)(base + off[5]);
   c->g.dn_off = (const uint32_t*)(base + off[6]);
   c->g.dn = (const uint32_t*)(base + off[7]);
+  c->g.nbig = (uint32_t)big.size();
+  c->g.big = (const uint32_t*)(base + off[8]);
   c->h_row_ptr.assign(csr->row_ptr, csr->row_ptr + V + 1);
   c->h_dn_off = std::move(dn_off);
   c->h_dn = std::move(dn);
   c->max_dn = max_dn;
+  c->depth_bound = transit_depth_bound(V, csr->row_ptr, colx.data(), nt);
   c->info.n_nodes = V;
   c->info.n_edges = E;
   c->info.n_links = n_links;
@@ -314,30 +438,43 @@ int ospf_plan_variant(const ospf_ctx* c, uint32_t flags, uint32_t nh_words, int*
   if (!c || !variant) return OSPF_E_INVAL;
   if (!c->loaded) return OSPF_E_NOGRAPH;
   const bool unit = (flags & OSPF_HOP_COUNT) || c->info.unit_metric;
-  *variant = make_plan(c, std::max<uint32_t>(nh_words, 1), 0, unit).variant;
+  *variant = make_plan(c, std::max<uint32_t>(nh_words, 1), 0, unit, 0xFFFFFFFFu).variant;
+  return OSPF_OK;
+}
+
+int ospf_plan_n(const ospf_ctx* c, uint32_t flags, uint32_t nh_words, uint32_t max_ignored,
+                uint32_t n_roots, uint32_t max_root_neighbors, ospf_plan_info* out) {
+  if (!c || !out) return OSPF_E_INVAL;
+  if (!c->loaded) return OSPF_E_NOGRAPH;
+  const bool unit = (flags & OSPF_HOP_COUNT) || c->info.unit_metric;
+  const uint32_t W = std::max<uint32_t>(nh_words, 1);
+  const Plan p = make_plan(c, W, max_ignored, unit, n_roots);
+  out->variant = p.variant;
+  out->block = p.block;
+  out->lds_bytes = (uint32_t)p.lds;
+  if (p.variant == 5) {
+    const uint32_t kcap = max_root_neighbors ? std::min(max_root_neighbors, 32u * W) : 32u * W;
+    out->slices = std::max<uint32_t>(1, (kcap + 31) / 32);
+  } else {
+    out->slices = p.variant >= 3 ? ospf::bfs_slices(W) : 1u;
+  }
   return OSPF_OK;
 }
 
 int ospf_plan(const ospf_ctx* c, uint32_t flags, uint32_t nh_words, uint32_t max_ignored,
               ospf_plan_info* out) {
-  if (!c || !out) return OSPF_E_INVAL;
-  if (!c->loaded) return OSPF_E_NOGRAPH;
-  const bool unit = (flags & OSPF_HOP_COUNT) || c->info.unit_metric;
-  const uint32_t W = std::max<uint32_t>(nh_words, 1);
-  const Plan p = make_plan(c, W, max_ignored, unit);
-  out->variant = p.variant;
-  out->block = p.block;
-  out->lds_bytes = (uint32_t)p.lds;
-  out->slices = p.variant >= 3 ? ospf::bfs_slices(W) : 1u;
-  return OSPF_OK;
+  return ospf_plan_n(c, flags, nh_words, max_ignored, 0xFFFFFFFFu, 0, out);
 }
 
-int ospf_sssp_batch_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n_roots,
-                        const uint32_t* d_ign_off, const uint32_t* d_ign_ids,
-                        uint32_t max_ignored, uint32_t flags, uint32_t nh_words,
-                        uint32_t* d_dist, uint32_t* d_nh, ospf_digest* d_digest,
-                        void* stream) {
-  if (!c) return OSPF_E_INVAL;
+int ospf_run_batch_dev(ospf_ctx* c, const ospf_batch* b, void* stream) {
+  if (!c || !b) return OSPF_E_INVAL;
+  const uint32_t* d_roots = b->d_roots;
+  const uint32_t n_roots = b->n_roots;
+  const uint32_t *d_ign_off = b->d_ign_offsets, *d_ign_ids = b->d_ign_ids;
+  const uint32_t max_ignored = b->max_ignored, flags = b->flags, nh_words = b->nh_words;
+  uint32_t* d_dist = b->d_dist;
+  uint32_t* d_nh = b->d_nh;
+  ospf_digest* d_digest = b->d_digest;
   if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
   if (n_roots == 0) return OSPF_OK;
   if (!d_roots) return fail(c, OSPF_E_INVAL, "null roots");
@@ -357,7 +494,8 @@ int ospf_sssp_batch_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n_roots,
     return fail(c, OSPF_E_RANGE, "u32 distance overflow possible (max_metric * (V-1))");
   const bool unit = hop || c->info.unit_metric;
 
-  const Plan p = make_plan(c, nh_words, ign ? std::max<uint32_t>(max_ignored, 1) : 0, unit);
+  const Plan p = make_plan(c, nh_words, ign ? std::max<uint32_t>(max_ignored, 1) : 0, unit, n_roots);
+  if (p.variant == 5) return run_msbfs(c, b, (hipStream_t)stream);
   // scratch for state the caller does not want back (HBM-state variants
   // keep dist / next-hops in the output rows while they run)
   size_t need = 0;
@@ -411,6 +549,26 @@ int ospf_sssp_batch_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n_roots,
   return OSPF_OK;
 }
 
+int ospf_sssp_batch_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n_roots,
+                        const uint32_t* d_ign_off, const uint32_t* d_ign_ids,
+                        uint32_t max_ignored, uint32_t flags, uint32_t nh_words,
+                        uint32_t* d_dist, uint32_t* d_nh, ospf_digest* d_digest,
+                        void* stream) {
+  ospf_batch b{};
+  b.d_roots = d_roots;
+  b.n_roots = n_roots;
+  b.d_ign_offsets = d_ign_off;
+  b.d_ign_ids = d_ign_ids;
+  b.max_ignored = max_ignored;
+  b.flags = flags;
+  b.nh_words = nh_words;
+  b.max_root_neighbors = 0;
+  b.d_dist = d_dist;
+  b.d_nh = d_nh;
+  b.d_digest = d_digest;
+  return ospf_run_batch_dev(c, &b, stream);
+}
+
 int ospf_sync(ospf_ctx* c, void* stream) {
   if (!c) return OSPF_E_INVAL;
   HIPCHK(c, hipSetDevice(c->device));
@@ -434,10 +592,12 @@ int ospf_sssp_batch(ospf_ctx* c, const uint32_t* roots, uint32_t n_roots, const 
   if (n_roots == 0) return OSPF_OK;
   if (!roots) return fail(c, OSPF_E_INVAL, "null roots");
   const uint64_t V = c->info.n_nodes;
-  uint32_t max_ign = 0;
+  uint32_t max_ign = 0, max_nn = 1;
   for (uint32_t i = 0; i < n_roots; ++i) {
     if (roots[i] >= V) return fail(c, OSPF_E_INVAL, "root out of range");
-    const uint32_t need = (c->h_dn_off[roots[i] + 1] - c->h_dn_off[roots[i]] + 31) / 32;
+    const uint32_t nn = c->h_dn_off[roots[i] + 1] - c->h_dn_off[roots[i]];
+    max_nn = std::max(max_nn, nn);
+    const uint32_t need = (nn + 31) / 32;
     if (need > nh_words) return fail(c, OSPF_E_INVAL, "nh_words smaller than a root needs");
     if (ig) {
       if (ig->offsets[i + 1] < ig->offsets[i]) return fail(c, OSPF_E_INVAL, "ignore offsets");
@@ -475,10 +635,19 @@ int ospf_sssp_batch(ospf_ctx* c, const uint32_t* roots, uint32_t n_roots, const 
       for (uint32_t i = 0; i <= n; ++i) off[i] = ig->offsets[r0 + i];
       HIPCHK(c, hipMemcpy(d_off, off.data(), (n + 1) * 4ull, hipMemcpyHostToDevice));
     }
-    rc = ospf_sssp_batch_dev(c, d_roots, n, ig ? d_off : nullptr, d_ids, max_ign, flags, nh_words,
-                             (want & OSPF_WANT_DIST) ? d_dist : nullptr,
-                             (want & OSPF_WANT_NH) ? d_nh : nullptr,
-                             (want & OSPF_WANT_DIGEST) ? d_dig : nullptr, nullptr);
+    ospf_batch bt{};
+    bt.d_roots = d_roots;
+    bt.n_roots = n;
+    bt.d_ign_offsets = ig ? d_off : nullptr;
+    bt.d_ign_ids = d_ids;
+    bt.max_ignored = max_ign;
+    bt.flags = flags;
+    bt.nh_words = nh_words;
+    bt.max_root_neighbors = max_nn;
+    bt.d_dist = (want & OSPF_WANT_DIST) ? d_dist : nullptr;
+    bt.d_nh = (want & OSPF_WANT_NH) ? d_nh : nullptr;
+    bt.d_digest = (want & OSPF_WANT_DIGEST) ? d_dig : nullptr;
+    rc = ospf_run_batch_dev(c, &bt, nullptr);
     if (rc) return rc;
     rc = ospf_sync(c, nullptr);
     if (rc) return rc;

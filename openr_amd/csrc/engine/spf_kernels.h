@@ -17,8 +17,13 @@ namespace ospf {
 //   link_id[e] = undirected link id (ignore sets)
 //   nt_bits    = no-transit (overloaded) bitmap, 1 bit per node
 //   dn_off/dn  = distinct neighbours per node, ascending (next-hop bit order)
+//   big        = nodes whose padded row is longer than kMsBigDeg (scanned by a
+//                whole wave in the multi-source BFS)
+constexpr uint32_t kMsBigDeg = 256;
 struct DevGraph {
   uint32_t V, E;
+  uint32_t nbig;
+  const uint32_t* big;
   const uint32_t* row_ptr;
   const uint32_t* colx;
   const uint32_t* w;
@@ -46,8 +51,10 @@ struct RunArgs {
 };
 
 // Digest: sum over reached nodes of node_term(v, dist) plus,
-// for every next-hop n of v, pair_term(v, n) (mod 2^64). A sum of independent
-// terms, so next-hop slices of one run add up.
+// for every next-hop n of v, pair_term(v, n) = node_key(v) * nh_key(n)
+// (mod 2^64). A sum of independent terms, so next-hop slices of one run add
+// up, and the pair terms of one node factor: node_key(v) * sum of nh_key over
+// its next hops (one multiply per node, one add per next hop).
 __host__ __device__ inline uint64_t digest_mix(uint64_t x) {
   x ^= x >> 30;
   x *= 0xbf58476d1ce4e5b9ULL;
@@ -59,8 +66,14 @@ __host__ __device__ inline uint64_t digest_mix(uint64_t x) {
 __host__ __device__ inline uint64_t digest_node_term(uint32_t v, uint32_t dist) {
   return digest_mix(((uint64_t)v << 32) | dist);
 }
+__host__ __device__ inline uint64_t digest_node_key(uint32_t v) {
+  return digest_mix((uint64_t)v ^ 0xD6E8FEB86659FD93ULL) | 1ull;
+}
+__host__ __device__ inline uint64_t digest_nh_key(uint32_t nh) {
+  return digest_mix((((uint64_t)nh + 1) << 32) ^ 0x9E3779B97F4A7C15ULL);
+}
 __host__ __device__ inline uint64_t digest_pair_term(uint32_t v, uint32_t nh) {
-  return digest_mix((((uint64_t)nh + 1) << 32) ^ (uint64_t)v ^ 0xD6E8FEB86659FD93ULL);
+  return digest_node_key(v) * digest_nh_key(nh);
 }
 
 // Dial kernels (spf_kernels.hip), any metric:
@@ -74,5 +87,36 @@ hipError_t launch_spf(int variant, bool unit, bool ign, const DevGraph& g, const
 uint32_t bfs_slices(uint32_t W);
 hipError_t launch_bfs(bool nh_lds, bool ign, const DevGraph& g, const RunArgs& a, uint32_t n,
                       uint32_t block, size_t lds, hipStream_t s);
+
+// Multi-source bit-parallel BFS (spf_msbfs.hip), variant 5: unit metric / hop
+// count, no ignored links. One round = up to nb "virtual batches"
+// (64-root batch, next-hop word g) sharing the launches.
+struct MsArgs {
+  const uint32_t* roots;  // every root of the call
+  uint32_t n;             // roots in the call
+  uint32_t W;             // nh words per node of the output rows
+  uint32_t npass;         // next-hop words computed (passes per 64-root batch)
+  uint32_t vb0;           // first virtual batch of this round (vb = batch*npass + g)
+  uint32_t nb;            // virtual batches in this round
+  uint32_t lmax;          // stride of found[]
+  uint32_t kcap;          // max distinct neighbours of a root (caller's bound)
+  uint32_t push_div;      // level d pushes when frontier edge mass * push_div < E
+  uint32_t* dist;         // [n][V] or null
+  uint32_t* nh;           // [n][V][W] or null
+  uint64_t* seen;         // [nb][V]
+  uint64_t* front;        // [2][nb][V]   frontier of level d in front[d & 1]
+  uint64_t* accb;         // [nb][V]      push accumulator (zero between levels)
+  uint64_t* planes;       // [nb][V][KP]
+  uint32_t* found;        // [nb][lmax]   level d non-empty
+  uint32_t* mass;         // [nb][lmax]   out-edge mass of level d's frontier
+  uint32_t* err;
+};
+// kp = 8, 16 or 32 planes per node; depth_bound bounds the BFS level count
+hipError_t launch_msbfs_round(int kp, const DevGraph& g, const MsArgs& a, uint32_t depth_bound,
+                              hipStream_t s);
+// digests of finished rows, one workgroup per root
+hipError_t launch_row_digest(const DevGraph& g, const uint32_t* roots, uint32_t n,
+                             const uint32_t* dist, const uint32_t* nh, uint32_t W, uint32_t kcap,
+                             ospf_digest* out, hipStream_t s);
 
 }  // namespace ospf

@@ -1,0 +1,503 @@
+// spf_msbfs.hip — multi-source bit-parallel BFS (gfx950), unit metric /
+// hop count, no ignored links: the all-sources path.
+//
+// Same result as LinkState::runSpf (openr/decision/LinkState.cpp:836-911) for
+// every root of a batch when every usable weight is 1: levels are BFS levels
+// and the ECMP next-hop set of a node at level d+1 is the OR over its usable
+// in-edges from transit level-d nodes (LinkState.cpp:885-901).
+//
+// 64 roots share one traversal: per node, one 64-bit word holds a bit per
+// root ("seen", "frontier"), so one CSR scan serves 64 SPF runs and the
+// per-edge work is a 64-bit AND/OR instead of 64 bitmap probes. Next-hop sets
+// are bit-sliced the same way: plane k of node v (one u64) has bit r set when
+// the k-th distinct neighbour of root r is a next hop of v. A pass computes
+// one 32-bit next-hop word g (planes for neighbour indices [32g, 32g+32)); a
+// root with K distinct neighbours needs ceil(K/32) passes, each re-running the
+// traversal. A "virtual batch" = (64-root batch, word g); a round runs up to
+// NB virtual batches side by side, and virtual batch i of a round is served by
+// workgroups i, i+NB, ... so with NB a multiple of 8 its workgroups land on one
+// XCD and its state stays in that XCD's L2.
+//
+// Level d -> d+1, chosen per virtual batch from the frontier's out-edge mass:
+//  * pull (bottom-up): node v with unseen roots m scans its in-edges u:
+//    f = frontier[u] & m; next |= f; plane_k(v) |= plane_k(u) & f. The owner
+//    lane of v is the only writer of v's state: no atomics.
+//  * push (top-down, small frontiers): frontier node u ORs f = frontier[u] &
+//    ~seen[v] into an accumulator and planes of each head v (64-bit atomics);
+//    a finalize pass then folds the accumulator into seen / next frontier.
+// Rows longer than kMsBigDeg (spines) are scanned by a whole wave each, in
+// extra workgroups after the per-node ones, so they never serialise a wave.
+// dist / next-hop rows of newly reached (root, node) pairs are written when
+// the level is settled (coalesced across the wave's 64 nodes, one store per
+// root). Level 1 (the root's own neighbours) is expanded by the init kernel.
+// The level count is bounded on the host (spf_engine.hip: 2 * eccentricity of
+// the transit subgraph + 2), so the launches need no host round trip; a level
+// whose predecessor found nothing returns at once.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "spf_kernels.h"
+
+namespace ospf {
+namespace {
+
+constexpr uint32_t kInf = 0xFFFFFFFFu;
+constexpr uint32_t kDown = 0x80000000u;
+constexpr int kWave = 64;
+constexpr uint32_t kBlock = 256;
+constexpr uint32_t kWavesPerBlock = kBlock / kWave;
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t x, int o) {
+  const uint32_t lo = __shfl_xor((uint32_t)x, o, kWave);
+  const uint32_t hi = __shfl_xor((uint32_t)(x >> 32), o, kWave);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x |= shfl_xor64(x, o);
+  return x;
+}
+__device__ __forceinline__ uint32_t wave_add32(uint32_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, kWave);
+  return x;
+}
+__device__ __forceinline__ bool transit(const DevGraph& g, uint32_t v) {
+  return !((g.nt_bits[v >> 5] >> (v & 31)) & 1u);
+}
+__device__ __forceinline__ void or64(uint64_t* p, uint64_t x) {
+  atomicOr((unsigned long long*)p, (unsigned long long)x);
+}
+
+// one (64-root batch, next-hop word) of the round, and its state arrays
+struct VB {
+  uint32_t vbl, g, rix0, V;
+  uint64_t valid;  // bits of roots present
+  uint64_t* seen;
+  uint64_t* accb;
+  uint64_t* P;
+  __device__ VB(const MsArgs& a, uint32_t vbl_, uint32_t V_, int kp) : vbl(vbl_), V(V_) {
+    const uint32_t vb = a.vb0 + vbl;
+    g = vb % a.npass;
+    rix0 = (vb / a.npass) * 64u;
+    const uint32_t nv = min(64u, a.n - rix0);
+    valid = nv == 64u ? ~0ull : ((1ull << nv) - 1ull);
+    seen = a.seen + (size_t)vbl * V;
+    accb = a.accb + (size_t)vbl * V;
+    P = a.planes + (size_t)vbl * V * kp;
+  }
+  __device__ uint64_t* front(const MsArgs& a, uint32_t d) const {
+    return a.front + ((size_t)(d & 1u) * a.nb + vbl) * V;
+  }
+};
+
+// next-hop word of root r from the KP planes (bit k = plane k, bit r)
+template <int KP>
+__device__ __forceinline__ uint32_t gather_word(const uint64_t* p, uint32_t r) {
+  uint32_t w = 0;
+#pragma unroll
+  for (int k = 0; k < KP; ++k) w |= (uint32_t)((p[k] >> r) & 1ull) << k;
+  return w;
+}
+
+// dist / next-hop rows of the (root, v) pairs in `acc` (lane = node v): one
+// coalesced store per root present anywhere in the wave
+template <int KP>
+__device__ __forceinline__ void emit_rows(const MsArgs& a, const VB& b, uint32_t v, uint64_t acc,
+                                          const uint64_t* pacc, uint32_t dist) {
+  uint64_t un = wave_or64(acc);
+  while (un) {
+    const uint32_t r = (uint32_t)(__ffsll((unsigned long long)un) - 1);
+    un &= un - 1;
+    if ((acc >> r) & 1ull) {
+      const size_t row = (size_t)(b.rix0 + r) * b.V + v;
+      if (a.dist && b.g == 0) a.dist[row] = dist;
+      if (a.nh) a.nh[row * a.W + b.g] = gather_word<KP>(pacc, r);
+    }
+  }
+}
+
+template <int KP>
+__device__ __forceinline__ void load_planes(const uint64_t* P, uint32_t u, uint64_t* pu) {
+  const uint4* q = reinterpret_cast<const uint4*>(P + (size_t)u * KP);
+#pragma unroll
+  for (int k = 0; k < KP / 2; ++k) {
+    const uint4 w = q[k];
+    pu[2 * k] = ((uint64_t)w.y << 32) | w.x;
+    pu[2 * k + 1] = ((uint64_t)w.w << 32) | w.z;
+  }
+}
+
+// ---------------------------------------------------------------- init
+// One wave per root: level 0 (the root) and level 1 (its usable neighbours,
+// next hop = themselves). Atomics: several roots of a batch may share nodes.
+template <int KP>
+__global__ void __launch_bounds__(256) msbfs_init_kernel(DevGraph g, MsArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t slot = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const uint32_t vbl = slot / 64u, bit = slot % 64u;
+  if (vbl >= a.nb) return;
+  const VB b(a, vbl, g.V, KP);
+  const uint32_t rix = b.rix0 + bit;
+  if (rix >= a.n) return;
+  const uint32_t V = g.V;
+  const uint32_t s = a.roots[rix];
+  const uint32_t nb0 = g.dn_off[s], nn = g.dn_off[s + 1] - nb0;
+  if (nn > a.kcap || nn > 32u * a.W) {
+    if (lane == 0) atomicOr(a.err, 1u);
+    return;
+  }
+  const uint64_t bm = 1ull << bit;
+  uint64_t* f1 = b.front(a, 1);
+  const size_t row = (size_t)rix * V;
+  if (lane == 0) {
+    or64(&b.seen[s], bm);
+    if (a.dist && b.g == 0) a.dist[row + s] = 0u;
+    if (a.nh) a.nh[(row + s) * a.W + b.g] = 0u;
+  }
+  const uint32_t e0 = g.row_ptr[s], e1 = g.row_ptr[s + 1];
+  bool any = false;
+  uint32_t mass = 0;
+  for (uint32_t e = e0 + lane; e < e1; e += kWave) {
+    const uint32_t cx = g.colx[e];
+    if ((cx & kDown) || cx == s) continue;
+    const uint32_t v = cx;
+    // index of v among s's distinct neighbours (ascending ids)
+    uint32_t lo = 0, hi = nn;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (g.dn[nb0 + mid] < v) lo = mid + 1; else hi = mid;
+    }
+    const uint32_t k = lo - 32u * b.g;  // >= 32 (wrapped) when outside this word
+    or64(&b.seen[v], bm);
+    if (transit(g, v)) {
+      const unsigned long long old = atomicOr((unsigned long long*)&f1[v], (unsigned long long)bm);
+      if (!old) mass += g.row_ptr[v + 1] - g.row_ptr[v];  // first root to reach v
+    }
+    if (k < (uint32_t)KP) or64(&b.P[(size_t)v * KP + k], bm);
+    if (a.dist && b.g == 0) a.dist[row + v] = 1u;
+    if (a.nh) a.nh[(row + v) * a.W + b.g] = (k < 32u) ? (1u << k) : 0u;
+    any = true;
+  }
+  mass = wave_add32(mass);
+  if (lane == 0 && mass) atomicAdd(&a.mass[vbl * a.lmax + 1], mass);
+  if (__ballot(any) && lane == 0) a.found[vbl * a.lmax + 1] = 1u;
+}
+
+// ---------------------------------------------------------------- pull
+// in-edges [beg, end) of a node with unseen roots m, one lane (STEP 4) or the
+// wave (lane offset folded into beg, STEP 256); rows are padded to 4 entries
+template <int KP, uint32_t STEP>
+__device__ __forceinline__ void pull_scan(const DevGraph& g, const uint64_t* fcur, const uint64_t* P,
+                                          uint32_t beg, uint32_t end, uint64_t m, uint64_t& acc,
+                                          uint64_t* pacc) {
+  const uint4* q = reinterpret_cast<const uint4*>(g.colx);
+  for (uint32_t e = beg; e < end; e += STEP) {
+    const uint4 c = q[e >> 2];
+    const uint32_t cs[4] = {c.x, c.y, c.z, c.w};
+    uint64_t fs[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fs[i] = (cs[i] & kDown) ? 0ull : fcur[cs[i]];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint64_t f = fs[i] & m;
+      if (!f) continue;
+      acc |= f;
+      uint64_t pu[KP];
+      load_planes<KP>(P, cs[i], pu);
+#pragma unroll
+      for (int k = 0; k < KP; ++k) pacc[k] |= pu[k] & f;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- push
+// out-edges [beg, end) of frontier node u (roots fu, planes pu)
+template <int KP, uint32_t STEP>
+__device__ __forceinline__ void push_scan(const DevGraph& g, const VB& b, uint32_t beg,
+                                          uint32_t end, uint64_t fu, const uint64_t* pu) {
+  const uint4* q = reinterpret_cast<const uint4*>(g.colx);
+  for (uint32_t e = beg; e < end; e += STEP) {
+    const uint4 c = q[e >> 2];
+    const uint32_t cs[4] = {c.x, c.y, c.z, c.w};
+    uint64_t ss[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ss[i] = (cs[i] & kDown) ? ~0ull : b.seen[cs[i]];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint64_t f = fu & ~ss[i];
+      if (!f) continue;
+      const uint32_t v = cs[i];
+      or64(&b.accb[v], f);
+#pragma unroll
+      for (int k = 0; k < KP; ++k) {
+        const uint64_t x = pu[k] & f;
+        if (x) or64(&b.P[(size_t)v * KP + k], x);
+      }
+    }
+  }
+}
+
+template <int KP>
+__global__ void __launch_bounds__(256) msbfs_level_kernel(DevGraph g, MsArgs a, uint32_t d) {
+  const uint32_t vbl = blockIdx.x % a.nb;
+  if (!a.found[vbl * a.lmax + d]) return;  // level d is empty: this batch is done
+  const bool push = (uint64_t)a.mass[vbl * a.lmax + d] * a.push_div < g.E;
+  const VB b(a, vbl, g.V, KP);
+  const uint32_t V = g.V;
+  const int lane = threadIdx.x & 63;
+  const uint64_t* fcur = b.front(a, d);
+  uint64_t* fnext = b.front(a, d + 1);
+  const uint32_t blk = blockIdx.x / a.nb, chunks = (V + kBlock - 1) / kBlock;
+
+  if (blk >= chunks) {  // ------------------------- one long row per wave
+    const uint32_t bi = (blk - chunks) * kWavesPerBlock + (threadIdx.x >> 6);
+    if (bi >= g.nbig) return;
+    const uint32_t u = g.big[bi];
+    const uint32_t beg = g.row_ptr[u], end = g.row_ptr[u + 1];
+    if (push) {
+      const uint64_t fu = fcur[u];
+      if (!fu) return;
+      uint64_t pu[KP];
+      load_planes<KP>(b.P, u, pu);
+      push_scan<KP, 4u * kWave>(g, b, beg + 4u * lane, end, fu, pu);
+      return;
+    }
+    const uint64_t m = ~b.seen[u] & b.valid;
+    if (!m) return;  // the node's own lane writes fnext[u] = 0
+    uint64_t acc = 0, pacc[KP];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) pacc[k] = 0;
+    pull_scan<KP, 4u * kWave>(g, fcur, b.P, beg + 4u * lane, end, m, acc, pacc);
+    acc = wave_or64(acc);
+#pragma unroll
+    for (int k = 0; k < KP; ++k) pacc[k] = wave_or64(pacc[k]);
+    const bool tr = transit(g, u);
+    if (lane == 0) {
+      fnext[u] = tr ? acc : 0ull;
+      if (acc) {
+        b.seen[u] = (~m & b.valid) | acc;
+#pragma unroll
+        for (int k = 0; k < KP; ++k) b.P[(size_t)u * KP + k] |= pacc[k];
+        a.found[vbl * a.lmax + d + 1] = 1u;
+        if (tr) atomicAdd(&a.mass[vbl * a.lmax + d + 1], end - beg);
+      }
+    }
+    if ((acc >> lane) & 1ull) {  // lane r writes root r's entries
+      const size_t row = (size_t)(b.rix0 + lane) * V + u;
+      if (a.dist && b.g == 0) a.dist[row] = d + 1;
+      if (a.nh) a.nh[row * a.W + b.g] = gather_word<KP>(pacc, lane);
+    }
+    return;
+  }
+
+  // ------------------------------------------------ one node per lane
+  const uint32_t v = blk * kBlock + threadIdx.x;
+  if (push) {
+    if (v >= V) return;
+    const uint64_t fu = fcur[v];
+    if (!fu) return;
+    const uint32_t beg = g.row_ptr[v], end = g.row_ptr[v + 1];
+    if (end - beg > kMsBigDeg) return;
+    uint64_t pu[KP];
+    load_planes<KP>(b.P, v, pu);
+    push_scan<KP, 4u>(g, b, beg, end, fu, pu);
+    return;
+  }
+  uint64_t s0 = 0, m = 0;
+  uint32_t beg = 0, end = 0;
+  if (v < V) {
+    s0 = b.seen[v];
+    m = ~s0 & b.valid;
+    if (m) {
+      beg = g.row_ptr[v];
+      end = g.row_ptr[v + 1];
+    }
+  }
+  const bool big = m && (end - beg) > kMsBigDeg;
+  uint64_t acc = 0, pacc[KP];
+#pragma unroll
+  for (int k = 0; k < KP; ++k) pacc[k] = 0;
+  if (m && !big) pull_scan<KP, 4u>(g, fcur, b.P, beg, end, m, acc, pacc);
+  uint32_t mass = 0;
+  if (v < V && !big) {
+    const bool tr = acc && transit(g, v);
+    if (acc) {
+      b.seen[v] = s0 | acc;
+#pragma unroll
+      for (int k = 0; k < KP; ++k)
+        if (pacc[k]) b.P[(size_t)v * KP + k] |= pacc[k];
+    }
+    fnext[v] = tr ? acc : 0ull;
+    if (tr) mass = end - beg;
+  }
+  emit_rows<KP>(a, b, v, acc, pacc, d + 1);
+  mass = wave_add32(mass);
+  if (lane == 0 && mass) atomicAdd(&a.mass[vbl * a.lmax + d + 1], mass);
+  if (__ballot(acc != 0) && lane == 0) a.found[vbl * a.lmax + d + 1] = 1u;
+}
+
+// settle a pushed level: fold the accumulator into seen / next frontier and
+// write the rows (pull levels return at once)
+template <int KP>
+__global__ void __launch_bounds__(256) msbfs_settle_kernel(DevGraph g, MsArgs a, uint32_t d) {
+  const uint32_t vbl = blockIdx.x % a.nb;
+  if (!a.found[vbl * a.lmax + d]) return;
+  if (!((uint64_t)a.mass[vbl * a.lmax + d] * a.push_div < g.E)) return;
+  const VB b(a, vbl, g.V, KP);
+  const uint32_t V = g.V;
+  const int lane = threadIdx.x & 63;
+  uint64_t* fnext = b.front(a, d + 1);
+  const uint32_t v = (blockIdx.x / a.nb) * kBlock + threadIdx.x;
+  uint64_t acc = 0, pacc[KP];
+#pragma unroll
+  for (int k = 0; k < KP; ++k) pacc[k] = 0;
+  uint32_t mass = 0;
+  if (v < V) {
+    acc = b.accb[v];
+    const bool tr = acc && transit(g, v);
+    if (acc) {
+      b.accb[v] = 0ull;
+      b.seen[v] |= acc;
+      load_planes<KP>(b.P, v, pacc);
+      if (tr) mass = g.row_ptr[v + 1] - g.row_ptr[v];
+    }
+    fnext[v] = tr ? acc : 0ull;
+  }
+  emit_rows<KP>(a, b, v, acc, pacc, d + 1);
+  mass = wave_add32(mass);
+  if (lane == 0 && mass) atomicAdd(&a.mass[vbl * a.lmax + d + 1], mass);
+  if (__ballot(acc != 0) && lane == 0) a.found[vbl * a.lmax + d + 1] = 1u;
+}
+
+// ---------------------------------------------------------------- final
+// Unreached (root, node) pairs: dist INF, next-hop word 0; words past the
+// computed passes (nh_words > passes needed) are zero for every node.
+__global__ void __launch_bounds__(256) msbfs_final_kernel(DevGraph g, MsArgs a) {
+  const uint32_t vbl = blockIdx.x % a.nb;
+  const VB b(a, vbl, g.V, 0);
+  const uint32_t V = g.V;
+  const uint32_t v = (blockIdx.x / a.nb) * kBlock + threadIdx.x;
+  const uint64_t un = v < V ? (~b.seen[v] & b.valid) : 0ull;
+  uint64_t w = wave_or64(un);
+  while (w) {
+    const uint32_t r = (uint32_t)(__ffsll((unsigned long long)w) - 1);
+    w &= w - 1;
+    if ((un >> r) & 1ull) {
+      const size_t row = (size_t)(b.rix0 + r) * V + v;
+      if (a.dist && b.g == 0) a.dist[row] = kInf;
+      if (a.nh) a.nh[row * a.W + b.g] = 0u;
+    }
+  }
+  if (a.nh && b.g == a.npass - 1 && a.npass < a.W && v < V) {
+    for (uint64_t x = b.valid; x; x &= x - 1) {
+      const uint32_t r = (uint32_t)(__ffsll((unsigned long long)x) - 1);
+      uint32_t* p = a.nh + ((size_t)(b.rix0 + r) * V + v) * a.W;
+      for (uint32_t k = a.npass; k < a.W; ++k) p[k] = 0u;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- digest
+// Digest of finished rows: `segs` workgroups per root, each over a node
+// range, adding into a zeroed record. The root's next-hop keys sit in LDS, so
+// a next-hop bit costs one LDS read and one add.
+__global__ void __launch_bounds__(256) row_digest_kernel(DevGraph g, const uint32_t* roots,
+                                                         const uint32_t* dist, const uint32_t* nh,
+                                                         uint32_t W, uint32_t kcap, uint32_t segs,
+                                                         ospf_digest* out) {
+  extern __shared__ uint64_t keys[];
+  const uint32_t rix = blockIdx.x / segs, seg = blockIdx.x % segs, V = g.V;
+  const uint32_t s = roots[rix];
+  const uint32_t nb0 = g.dn_off[s];
+  const uint32_t nn = min(g.dn_off[s + 1] - nb0, kcap);  // > kcap: error word already set
+  for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) keys[i] = digest_nh_key(g.dn[nb0 + i]);
+  __syncthreads();
+  const uint32_t* drow = dist + (size_t)rix * V;
+  const uint32_t* nrow = nh + (size_t)rix * V * W;
+  const uint32_t v0 = (uint32_t)((uint64_t)V * seg / segs), v1 = (uint32_t)((uint64_t)V * (seg + 1) / segs);
+  uint64_t reached = 0, sumd = 0, h = 0;
+  for (uint32_t v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
+    const uint32_t d = drow[v];
+    if (d == kInf) continue;
+    reached += 1;
+    sumd += d;
+    h += digest_node_term(v, d);
+    uint64_t ks = 0;
+    for (uint32_t w = 0; w < W; ++w) {
+      uint32_t bits = nrow[(size_t)v * W + w];
+      while (bits) {
+        const uint32_t i = 32u * w + __ffs(bits) - 1;
+        bits &= bits - 1;
+        if (i < nn) ks += keys[i];
+      }
+    }
+    if (ks) h += digest_node_key(v) * ks;
+  }
+  __shared__ uint64_t s_r[kWavesPerBlock], s_s[kWavesPerBlock], s_h[kWavesPerBlock];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    reached += shfl_xor64(reached, o);
+    sumd += shfl_xor64(sumd, o);
+    h += shfl_xor64(h, o);
+  }
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s_r[wave] = reached;
+    s_s[wave] = sumd;
+    s_h[wave] = h;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t r = 0, sd = 0, hh = 0;
+    for (uint32_t i = 0; i < kWavesPerBlock; ++i) {
+      r += s_r[i];
+      sd += s_s[i];
+      hh += s_h[i];
+    }
+    atomicAdd((unsigned long long*)&out[rix].reached, (unsigned long long)r);
+    atomicAdd((unsigned long long*)&out[rix].sum_dist, (unsigned long long)sd);
+    atomicAdd((unsigned long long*)&out[rix].hash, (unsigned long long)hh);
+  }
+}
+
+template <int KP>
+hipError_t launch_round_kp(const DevGraph& g, const MsArgs& a, uint32_t depth_bound,
+                           hipStream_t s) {
+  const uint32_t init_blocks = (a.nb * 64u + kWavesPerBlock - 1) / kWavesPerBlock;
+  hipLaunchKernelGGL(msbfs_init_kernel<KP>, dim3(init_blocks), dim3(kBlock), 0, s, g, a);
+  const uint32_t chunks = (g.V + kBlock - 1) / kBlock;
+  const uint32_t bigblocks = (g.nbig + kWavesPerBlock - 1) / kWavesPerBlock;
+  for (uint32_t d = 1; d < depth_bound; ++d) {
+    hipLaunchKernelGGL(msbfs_level_kernel<KP>, dim3(a.nb * (chunks + bigblocks)), dim3(kBlock), 0,
+                       s, g, a, d);
+    hipLaunchKernelGGL(msbfs_settle_kernel<KP>, dim3(a.nb * chunks), dim3(kBlock), 0, s, g, a, d);
+  }
+  hipLaunchKernelGGL(msbfs_final_kernel, dim3(a.nb * chunks), dim3(kBlock), 0, s, g, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_msbfs_round(int kp, const DevGraph& g, const MsArgs& a, uint32_t depth_bound,
+                              hipStream_t s) {
+  switch (kp) {
+    case 8: return launch_round_kp<8>(g, a, depth_bound, s);
+    case 16: return launch_round_kp<16>(g, a, depth_bound, s);
+    default: return launch_round_kp<32>(g, a, depth_bound, s);
+  }
+}
+
+hipError_t launch_row_digest(const DevGraph& g, const uint32_t* roots, uint32_t n,
+                             const uint32_t* dist, const uint32_t* nh, uint32_t W, uint32_t kcap,
+                             ospf_digest* out, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(out, 0, (size_t)n * sizeof(ospf_digest), s);
+  if (e != hipSuccess) return e;
+  const uint32_t cap = min(kcap, 32u * W);
+  const uint32_t segs = max(1u, min((2048u + n - 1) / n, max(1u, g.V / 2048u)));
+  hipLaunchKernelGGL(row_digest_kernel, dim3(n * segs), dim3(kBlock), (size_t)cap * 8u, s, g, roots,
+                     dist, nh, W, cap, segs, out);
+  return hipGetLastError();
+}
+
+}  // namespace ospf

@@ -78,9 +78,11 @@ class Engine:
         self._check(self._L.ospf_plan_variant(self._h, flags, nh_words, C.byref(v)))
         return v.value
 
-    def plan(self, nh_words: int, flags: int = 0, max_ignored: int = 0) -> dict:
+    def plan(self, nh_words: int, flags: int = 0, max_ignored: int = 0,
+             n_roots: int = 0xFFFFFFFF, max_root_neighbors: int = 0) -> dict:
         p = N.ospf_plan_info()
-        self._check(self._L.ospf_plan(self._h, flags, nh_words, max_ignored, C.byref(p)))
+        self._check(self._L.ospf_plan_n(self._h, flags, nh_words, max_ignored, n_roots,
+                                        max_root_neighbors, C.byref(p)))
         return dict(variant=p.variant, block=p.block, lds_bytes=p.lds_bytes, slices=p.slices)
 
     @property
@@ -125,11 +127,15 @@ class Engine:
 
     def run_dev(self, d_roots: int, n_roots: int, nh_words: int, *, flags: int,
                 d_dist: int = 0, d_nh: int = 0, d_digest: int = 0, stream: int = 0,
-                d_ign_off: int = 0, d_ign_ids: int = 0, max_ignored: int = 0) -> None:
-        """Queue a device-resident batch (raw device pointers) on `stream`."""
-        self._check(self._L.ospf_sssp_batch_dev(
-            self._h, d_roots, n_roots, d_ign_off or None, d_ign_ids or None, max_ignored,
-            flags, nh_words, d_dist or None, d_nh or None, d_digest or None, stream or None))
+                d_ign_off: int = 0, d_ign_ids: int = 0, max_ignored: int = 0,
+                max_root_neighbors: int = 0) -> None:
+        """Queue a device-resident batch (raw device pointers) on `stream`.
+        max_root_neighbors: optional bound on the roots' distinct neighbour
+        counts (sizes the multi-source BFS; 0 = 32 * nh_words)."""
+        b = N.ospf_batch(d_roots, n_roots, d_ign_off or None, d_ign_ids or None, max_ignored,
+                         flags, nh_words, max_root_neighbors, d_dist or None, d_nh or None,
+                         d_digest or None)
+        self._check(self._L.ospf_run_batch_dev(self._h, C.byref(b), stream or None))
 
     def sync(self, stream: int = 0) -> None:
         self._check(self._L.ospf_sync(self._h, stream or None))

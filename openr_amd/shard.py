@@ -25,6 +25,12 @@ class RootClass:
 def nh_words_of(row_ptr: np.ndarray, col: np.ndarray) -> np.ndarray:
     """ceil(distinct neighbours / 32) per node (>= 1) from a CSR whose rows
     are sorted by neighbour id (what the engine uses for the bit order)."""
+    return np.maximum(1, (distinct_neighbors(row_ptr, col) + 31) // 32)
+
+
+def distinct_neighbors(row_ptr: np.ndarray, col: np.ndarray) -> np.ndarray:
+    """Distinct neighbours per node (self-loops excluded) = next-hop bits a
+    root needs (the engine's max_root_neighbors hint)."""
     V = row_ptr.size - 1
     deg = np.diff(row_ptr.astype(np.int64))
     owner = np.repeat(np.arange(V), deg)
@@ -32,8 +38,7 @@ def nh_words_of(row_ptr: np.ndarray, col: np.ndarray) -> np.ndarray:
     if col.size:
         new[1:] = (col[1:] != col[:-1]) | (owner[1:] != owner[:-1])
         new &= col != owner  # self-loops are not next hops
-    distinct = np.bincount(owner[new], minlength=V) if col.size else np.zeros(V, np.int64)
-    return np.maximum(1, (distinct + 31) // 32)
+    return np.bincount(owner[new], minlength=V) if col.size else np.zeros(V, np.int64)
 
 
 def make_classes(perm: np.ndarray, words: np.ndarray, batch: int) -> List[RootClass]:

@@ -475,11 +475,13 @@ struct Digest {
 };
 
 // sum over reached nodes of node_term(v, dist) plus, for
-// every next-hop n of v, pair_term(v, n) (mod 2^64). Unknown names get id
-// 0xFFFFFFFF.
+// every next-hop n of v, pair_term(v, n) = node_key(v) * nh_key(n)
+// (mod 2^64). Unknown names get id 0xFFFFFFFF.
 static inline uint64_t nodeTerm(uint64_t v, uint64_t dist) { return mix64((v << 32) | dist); }
 static inline uint64_t pairTerm(uint64_t v, uint64_t n) {
-  return mix64(((n + 1) << 32) ^ v ^ 0xD6E8FEB86659FD93ULL);
+  const uint64_t nodeKey = mix64((v & 0xFFFFFFFFull) ^ 0xD6E8FEB86659FD93ULL) | 1ull;
+  const uint64_t nhKey = mix64((((n & 0xFFFFFFFFull) + 1) << 32) ^ 0x9E3779B97F4A7C15ULL);
+  return nodeKey * nhKey;
 }
 
 static Digest digestOf(const SpfResult& r,

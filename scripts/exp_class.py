@@ -33,7 +33,8 @@ csr = ls.csr()
 eng = Engine(0)
 eng.load(csr)
 V, E = eng.V, csr["col"].size
-words = shard.nh_words_of(csr["row_ptr"], csr["col"])
+nbrs = shard.distinct_neighbors(csr["row_ptr"], csr["col"])
+words = np.maximum(1, (nbrs + 31) // 32)
 perm = np.random.default_rng(1).permutation(V).astype(np.uint32)
 flags = N.OSPF_WANT_DIST | N.OSPF_WANT_NH | N.OSPF_WANT_DIGEST
 s = torch.cuda.current_stream()
@@ -51,13 +52,15 @@ for W in args.W:
                 os.environ["OSPF_BLOCK"] = str(blk)
             else:
                 os.environ.pop("OSPF_BLOCK", None)
-            plan = eng.plan(W, flags)
+            hint = int(nbrs[members].max())
+            plan = eng.plan(W, flags, n_roots=n, max_root_neighbors=hint)
             ts = []
             for r in range(args.reps + 1):
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record(s)
                 eng.run_dev(roots.data_ptr(), n, W, flags=flags, d_dist=dist.data_ptr(),
-                            d_nh=nh.data_ptr(), d_digest=dig.data_ptr(), stream=s.cuda_stream)
+                            d_nh=nh.data_ptr(), d_digest=dig.data_ptr(), stream=s.cuda_stream,
+                            max_root_neighbors=hint)
                 b.record(s)
                 b.synchronize()
                 if r:

@@ -18,12 +18,13 @@ pytestmark = pytest.mark.gpu
 FIXTURES = load_fixtures()
 
 
-@pytest.fixture(params=["auto", "0", "1", "2", "4"])
+@pytest.fixture(params=["auto", "0", "1", "2", "4", "5"])
 def variant(request, monkeypatch):
     """Run each parity test with the planner's choice and with every other
     kernel variant forced where its state fits (OSPF_FORCE_VARIANT): 0/1/2 =
     Dial kernel (LDS / mixed / HBM state), 3/4 = BFS kernel (LDS bitmaps,
-    byte next-hops in LDS / next-hops in HBM; unit metric only)."""
+    byte next-hops in LDS / next-hops in HBM; unit metric only), 5 =
+    multi-source bit-parallel BFS (unit metric, no ignored links)."""
     if request.param == "auto":
         monkeypatch.delenv("OSPF_FORCE_VARIANT", raising=False)
     else:
@@ -245,5 +246,89 @@ def test_engine_device_api_and_error_word():
     assert np.array_equal(d_dig.cpu().numpy().view(np.uint64), want)
     ssw = torch.tensor([p.node_id("1-0-0")], dtype=torch.int32, device="cuda")
     eng.run_dev(ssw.data_ptr(), 1, 1, flags=0x8, d_digest=d_dig.data_ptr(), stream=s)
+    with pytest.raises(EngineError):
+        eng.sync(s)
+
+
+# ------------------------------------------------ multi-source BFS (variant 5)
+def _engine_for(stream):
+    p = LinkState(stream=stream)
+    eng = Engine(0)
+    eng.load(p.csr())
+    return p, eng
+
+
+def _run_forced(eng, monkeypatch, variant, roots, W, **kw):
+    monkeypatch.setenv("OSPF_FORCE_VARIANT", variant)
+    return eng.run(roots, W, want_digest=True, **kw)
+
+
+@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("hop", [False, True])
+def test_msbfs_matches_per_root_bfs(seed, hop, monkeypatch):
+    """Variant 5 (64 roots per traversal) vs variant 4 (one root per
+    workgroup) on random unit graphs with parallel links, down links and
+    overloaded nodes; 150 roots = two full 64-root batches + a ragged one."""
+    st, names = random_stream(300 + seed, n=150, p=0.05, unit=not hop)
+    p, eng = _engine_for(st)
+    roots = np.arange(eng.V, dtype=np.uint32)
+    W = int(max(eng.nh_words(int(r)) for r in roots))
+    a = _run_forced(eng, monkeypatch, "5", roots, W, hop_count=hop)
+    b = _run_forced(eng, monkeypatch, "4", roots, W, hop_count=hop)
+    assert np.array_equal(a["dist"], b["dist"])
+    assert np.array_equal(a["nh"], b["nh"])
+    assert np.array_equal(a["digest"], b["digest"])
+    o = Oracle(st)
+    assert np.array_equal(a["digest"], o.digests([p.node_names()[i] for i in roots],
+                                                 not hop, threads=8))
+
+
+@pytest.mark.parametrize("nb", ["1", "3", "8"])
+def test_msbfs_wide_roots_and_rounds(nb, monkeypatch):
+    """Spines with 140 distinct neighbours need 5 next-hop words = 5 passes
+    per batch; OSPF_MS_NB bounds the (batch, word) pairs per round so the
+    sweep spans several rounds; nh_words above the need is zero-filled."""
+    monkeypatch.setenv("OSPF_MS_NB", nb)
+    st = T.fabric(pods=140, planes=2)
+    p, eng = _engine_for(st)
+    names = p.node_names()
+    rng = np.random.default_rng(1)
+    roots = np.concatenate([[p.node_id(n) for n in ("1-0-0", "1-1-35", "2-7-1", "3-139-47")],
+                            rng.choice(eng.V, 90, replace=False)]).astype(np.uint32)
+    a = _run_forced(eng, monkeypatch, "5", roots, 6)
+    b = _run_forced(eng, monkeypatch, "4", roots, 6)
+    assert np.array_equal(a["dist"], b["dist"])
+    assert np.array_equal(a["nh"], b["nh"])
+    o = Oracle(st)
+    assert np.array_equal(a["digest"], o.digests([names[i] for i in roots], threads=8))
+
+
+def test_msbfs_device_api_hint_and_error_word():
+    """ospf_run_batch_dev with max_root_neighbors: rack switches (8
+    neighbours) run with 8 bit-planes; a spine under the same hint raises the
+    device error word."""
+    torch = pytest.importorskip("torch")
+    p, eng = _engine_for(T.fabric(pods=40, planes=8))
+    V = eng.V
+    names = p.node_names()
+    rsw = [p.node_id(f"3-{i}-{j}") for i in range(40) for j in range(2)]
+    n = len(rsw)
+    assert eng.plan(1, 0x2 | 0x4, n_roots=n, max_root_neighbors=8)["variant"] == 5
+    d_roots = torch.tensor(rsw, dtype=torch.int32, device="cuda")
+    d_dig = torch.zeros((n, 3), dtype=torch.int64, device="cuda")
+    d_dist = torch.zeros((n, V), dtype=torch.int32, device="cuda")
+    d_nh = torch.zeros((n, V, 1), dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    eng.run_dev(d_roots.data_ptr(), n, 1, flags=0x2 | 0x4 | 0x8, d_dist=d_dist.data_ptr(),
+                d_nh=d_nh.data_ptr(), d_digest=d_dig.data_ptr(), stream=s, max_root_neighbors=8)
+    eng.sync(s)
+    want = p.digests([names[i] for i in rsw])
+    assert np.array_equal(d_dig.cpu().numpy().view(np.uint64), want)
+    ref = eng.run(np.array(rsw, np.uint32), 1)
+    assert np.array_equal(d_dist.cpu().numpy().view(np.uint32), ref["dist"])
+    assert np.array_equal(d_nh.cpu().numpy().view(np.uint32), ref["nh"])
+    bad = torch.tensor(rsw[:40] + [p.node_id("2-0-0")], dtype=torch.int32, device="cuda")
+    eng.run_dev(bad.data_ptr(), 41, 4, flags=0x8, d_digest=d_dig.data_ptr(), stream=s,
+                max_root_neighbors=8)
     with pytest.raises(EngineError):
         eng.sync(s)
