@@ -285,26 +285,16 @@ struct Bfs {
     }
   }
 
-  // digest terms of the next-hop bits of v held by this slice
+  // digest terms of the next-hop words of v held by this slice
   __device__ __forceinline__ uint64_t pair_terms(uint32_t v) const {
-    uint64_t h = 0;
     if constexpr (NH_LDS) {
-      uint32_t bits = nh_byte(v);
-      while (bits) {
-        h += digest_pair_term(v, nbr[__ffs(bits) - 1]);
-        bits &= bits - 1;
-      }
+      return digest_word_term(v, 0, nh_byte(v));
     } else {
       const uint32_t* r = row(v);
-      for (uint32_t w = 0; w < ws; ++w) {
-        uint32_t bits = r[w];
-        while (bits) {
-          h += digest_pair_term(v, nbr[32 * (w0 + w) + __ffs(bits) - 1]);
-          bits &= bits - 1;
-        }
-      }
+      uint64_t h = 0;
+      for (uint32_t w = 0; w < ws; ++w) h += digest_word_term(v, w0 + w, r[w]);
+      return h;
     }
-    return h;
   }
 };
 

@@ -181,11 +181,16 @@ int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
   const uint32_t kneed = std::min<uint32_t>(32, kcap);
   const int kp = kneed <= 8 ? 8 : kneed <= 16 ? 16 : 32;
   const bool dig = flags & OSPF_WANT_DIGEST;
-  const bool dist_scr = dig && !(flags & OSPF_WANT_DIST);
-  const bool nh_scr = dig && !(flags & OSPF_WANT_NH);
   const uint32_t lmax = c->depth_bound + 2;
-  // seen, front x2, accb, planes (u64 per node each) + found, mass
-  const size_t per_vb = align_up((size_t)V * 8ull * (4 + kp) + lmax * 8ull, 256);
+  // levels are recorded as dist + 1 in a byte per (node, root): rows are then
+  // written once, whole, by msbfs_rows (needs depth <= 254), which also folds
+  // the digest in (no row re-read, no row scratch)
+  const bool defer = c->depth_bound <= 254 && !getenv("OSPF_MS_NODEFER");
+  const bool dist_scr = dig && !defer && !(flags & OSPF_WANT_DIST);
+  const bool nh_scr = dig && !defer && !(flags & OSPF_WANT_NH);
+  // seen, front x2, accb, planes (u64 per node each) + lev (64 B per node) +
+  // found, mass
+  const size_t per_vb = align_up((size_t)V * 8ull * (4 + kp) + (defer ? V * 64ull : 0) + lmax * 8ull, 256);
   uint32_t push_div = 8;  // push a level when its frontier's edge mass * push_div < E
   if (const char* e = getenv("OSPF_MS_PUSH_DIV")) push_div = (uint32_t)std::max(0, atoi(e));
   uint32_t nb_cap = 32;
@@ -214,6 +219,9 @@ int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
     a.lmax = lmax;
     a.kcap = kcap;
     a.push_div = push_div;
+    a.defer = defer ? 1u : 0u;
+    a.digest = (defer && dig) ? b->d_digest + r0 : nullptr;
+    if (a.digest) HIPCHK(c, hipMemsetAsync(a.digest, 0, (size_t)n * sizeof(ospf_digest), s));
     a.err = c->d_err;
     a.dist = dist_scr ? (uint32_t*)(sp + state_bytes)
                       : ((flags & OSPF_WANT_DIST) ? b->d_dist + (size_t)r0 * V : nullptr);
@@ -223,18 +231,22 @@ int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
     for (uint32_t vb0 = 0; vb0 < total_vb; vb0 += nb_max) {
       a.vb0 = vb0;
       a.nb = std::min(nb_max, total_vb - vb0);
+
       a.seen = (uint64_t*)sp;
       a.front = a.seen + (size_t)a.nb * V;
       a.accb = a.front + 2ull * a.nb * V;
       a.planes = a.accb + (size_t)a.nb * V;
-      a.found = (uint32_t*)(a.planes + (size_t)a.nb * V * kp);
+      a.lev = (uint8_t*)(a.planes + (size_t)a.nb * V * kp);  // 16-B aligned (uint4 access)
+      a.found = (uint32_t*)(a.lev + (defer ? (size_t)a.nb * V * 64ull : 0));
       a.mass = a.found + (size_t)a.nb * lmax;
-      HIPCHK(c, hipMemsetAsync(sp, 0, (size_t)a.nb * V * 8ull * (4 + kp) + (size_t)a.nb * lmax * 8ull, s));
+      HIPCHK(c, hipMemsetAsync(sp, 0, (size_t)a.nb * V * 8ull * (4 + kp) +
+                                          (defer ? (size_t)a.nb * V * 64ull : 0) +
+                                          (size_t)a.nb * lmax * 8ull, s));
       hipError_t e = ospf::launch_msbfs_round(kp, c->g, a, c->depth_bound, s);
       if (e != hipSuccess) return hip_fail(c, e, "launch_msbfs_round");
     }
-    if (dig) {
-      hipError_t e = ospf::launch_row_digest(c->g, a.roots, n, a.dist, a.nh, W, kcap, b->d_digest + r0, s);
+    if (dig && !defer) {
+      hipError_t e = ospf::launch_row_digest(c->g, n, a.dist, a.nh, W, b->d_digest + r0, s);
       if (e != hipSuccess) return hip_fail(c, e, "launch_row_digest");
     }
   }
@@ -363,10 +375,15 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
     if (prow[u + 1] - prow[u] > ospf::kMsBigDeg) big.push_back(u);
   const size_t sz_row = (V + 1) * 4ull, sz_e = (size_t)Ep * 4ull, sz_nt = nt.size() * 4ull,
                sz_dnoff = (V + 1) * 4ull, sz_dn = std::max<size_t>(dn.size(), 1) * 4ull,
-               sz_big = std::max<size_t>(big.size(), 1) * 4ull;
-  size_t off[9], tot = 0;
-  const size_t szs[9] = {sz_row, sz_e, sz_e, sz_e, sz_e, sz_nt, sz_dnoff, sz_dn, sz_big};
-  for (int i = 0; i < 9; ++i) {
+               sz_big = std::max<size_t>(big.size(), 1) * 4ull, sz_key = V * 16ull;
+  std::vector<uint64_t> dkey(2ull * V);  // digest key tables (row digest kernel)
+  for (uint32_t u = 0; u < V; ++u) {
+    dkey[2ull * u] = ospf::digest_dist_key(u);
+    dkey[2ull * u + 1] = ospf::digest_node_key(u);
+  }
+  size_t off[10], tot = 0;
+  const size_t szs[10] = {sz_row, sz_e, sz_e, sz_e, sz_e, sz_nt, sz_dnoff, sz_dn, sz_big, sz_key};
+  for (int i = 0; i < 10; ++i) {
     off[i] = tot;
     tot += align_up(std::max<size_t>(szs[i], 4), 256);
   }
@@ -382,9 +399,9 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
     return fail(c, OSPF_E_NOMEM, std::string("hipMalloc graph: ") + hipGetErrorString(he));
   }
   char* base = (char*)c->d_graph;
-  const void* srcs[9] = {prow.data(), pcolx.data(), pw.data(), prw.data(), plink.data(),
-                         nt.data(), dn_off.data(), dn.data(), big.data()};
-  for (int i = 0; i < 9; ++i)
+  const void* srcs[10] = {prow.data(), pcolx.data(), pw.data(), prw.data(), plink.data(),
+                          nt.data(), dn_off.data(), dn.data(), big.data(), dkey.data()};
+  for (int i = 0; i < 10; ++i)
     if (szs[i] && srcs[i]) HIPCHK(c, hipMemcpy(base + off[i], srcs[i], szs[i], hipMemcpyHostToDevice));
   c->g.V = V;
   c->g.E = Ep;
@@ -398,6 +415,7 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   c->g.dn = (const uint32_t*)(base + off[7]);
   c->g.nbig = (uint32_t)big.size();
   c->g.big = (const uint32_t*)(base + off[8]);
+  c->g.dkey = (const uint64_t*)(base + off[9]);
   c->h_row_ptr.assign(csr->row_ptr, csr->row_ptr + V + 1);
   c->h_dn_off = std::move(dn_off);
   c->h_dn = std::move(dn);

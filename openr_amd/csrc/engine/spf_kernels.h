@@ -24,6 +24,7 @@ struct DevGraph {
   uint32_t V, E;
   uint32_t nbig;
   const uint32_t* big;
+  const uint64_t* dkey;  // [V][2] = {digest_dist_key(v), digest_node_key(v)}
   const uint32_t* row_ptr;
   const uint32_t* colx;
   const uint32_t* w;
@@ -50,11 +51,13 @@ struct RunArgs {
   uint32_t* planes;         // BFS kernel, slices > 1: [n_roots][slices][V][4] scratch
 };
 
-// Digest: sum over reached nodes of node_term(v, dist) plus,
-// for every next-hop n of v, pair_term(v, n) = node_key(v) * nh_key(n)
-// (mod 2^64). A sum of independent terms, so next-hop slices of one run add
-// up, and the pair terms of one node factor: node_key(v) * sum of nh_key over
-// its next hops (one multiply per node, one add per next hop).
+// Digest, mod 2^64, a sum of independent terms:
+//   sum over reached v of  dist_key(v) * (dist + 1)
+//                        + sum over next-hop words g != 0 of v of
+//                          node_key(v) * word_key(g, word)
+// where word g holds the next-hop bits of the root's distinct neighbours
+// 32g .. 32g+31 (ascending node id). Words and slices of one run add up, and
+// a node costs one multiply plus one hash per non-zero next-hop word.
 __host__ __device__ inline uint64_t digest_mix(uint64_t x) {
   x ^= x >> 30;
   x *= 0xbf58476d1ce4e5b9ULL;
@@ -63,17 +66,20 @@ __host__ __device__ inline uint64_t digest_mix(uint64_t x) {
   x ^= x >> 31;
   return x;
 }
-__host__ __device__ inline uint64_t digest_node_term(uint32_t v, uint32_t dist) {
-  return digest_mix(((uint64_t)v << 32) | dist);
+__host__ __device__ inline uint64_t digest_dist_key(uint32_t v) {
+  return digest_mix((uint64_t)v ^ 0x2545F4914F6CDD1DULL) | 1ull;
 }
 __host__ __device__ inline uint64_t digest_node_key(uint32_t v) {
   return digest_mix((uint64_t)v ^ 0xD6E8FEB86659FD93ULL) | 1ull;
 }
-__host__ __device__ inline uint64_t digest_nh_key(uint32_t nh) {
-  return digest_mix((((uint64_t)nh + 1) << 32) ^ 0x9E3779B97F4A7C15ULL);
+__host__ __device__ inline uint64_t digest_node_term(uint32_t v, uint32_t dist) {
+  return digest_dist_key(v) * ((uint64_t)dist + 1);
 }
-__host__ __device__ inline uint64_t digest_pair_term(uint32_t v, uint32_t nh) {
-  return digest_node_key(v) * digest_nh_key(nh);
+__host__ __device__ inline uint64_t digest_word_key(uint32_t g, uint32_t word) {
+  return digest_mix((((uint64_t)g << 32) | word) ^ 0x9E3779B97F4A7C15ULL);
+}
+__host__ __device__ inline uint64_t digest_word_term(uint32_t v, uint32_t g, uint32_t word) {
+  return word ? digest_node_key(v) * digest_word_key(g, word) : 0ull;
 }
 
 // Dial kernels (spf_kernels.hip), any metric:
@@ -109,14 +115,17 @@ struct MsArgs {
   uint64_t* planes;       // [nb][V][KP]
   uint32_t* found;        // [nb][lmax]   level d non-empty
   uint32_t* mass;         // [nb][lmax]   out-edge mass of level d's frontier
+  uint8_t* lev;           // [nb][V][64]  dist + 1 per (node, root), 0 = unreached
+                          //              (defer: rows are written once, at the end)
+  uint32_t defer;         // 1: levels fill lev, msbfs_rows writes the rows
+  ospf_digest* digest;    // [n] (defer: msbfs_rows adds each pass's terms; zeroed first)
   uint32_t* err;
 };
 // kp = 8, 16 or 32 planes per node; depth_bound bounds the BFS level count
 hipError_t launch_msbfs_round(int kp, const DevGraph& g, const MsArgs& a, uint32_t depth_bound,
                               hipStream_t s);
 // digests of finished rows, one workgroup per root
-hipError_t launch_row_digest(const DevGraph& g, const uint32_t* roots, uint32_t n,
-                             const uint32_t* dist, const uint32_t* nh, uint32_t W, uint32_t kcap,
-                             ospf_digest* out, hipStream_t s);
+hipError_t launch_row_digest(const DevGraph& g, uint32_t n, const uint32_t* dist,
+                             const uint32_t* nh, uint32_t W, ospf_digest* out, hipStream_t s);
 
 }  // namespace ospf

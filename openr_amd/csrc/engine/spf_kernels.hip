@@ -362,14 +362,7 @@ __global__ void __launch_bounds__(512) spf_run_kernel(DevGraph g, RunArgs a) {
     }
     if (want_dig) {
       const uint32_t* hv = r.nh_of(v);
-      for (uint32_t w = 0; w < W; ++w) {
-        uint32_t bits = hv[w];
-        while (bits) {
-          uint32_t b = __ffs(bits) - 1;
-          bits &= bits - 1;
-          hsum += digest_pair_term(v, s_nbr[w * 32 + b]);
-        }
-      }
+      for (uint32_t w = 0; w < W; ++w) hsum += digest_word_term(v, w, hv[w]);
       reached += 1;
       sumd += dv;
       hsum += digest_node_term(v, dv);

@@ -100,11 +100,36 @@ __device__ __forceinline__ uint32_t gather_word(const uint64_t* p, uint32_t r) {
   return w;
 }
 
+// lev bytes of node v for the roots in `acc` := val (they are 0 before: a
+// (node, root) pair is reached once). Byte r of the 64-B record is root r.
+__device__ __forceinline__ void set_lev(const MsArgs& a, const VB& b, uint32_t v, uint64_t acc,
+                                        uint32_t val) {
+  uint4* rec = reinterpret_cast<uint4*>(a.lev + ((size_t)b.vbl * b.V + v) * 64u);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const uint32_t bits = (uint32_t)(acc >> (16 * c)) & 0xFFFFu;
+    if (!bits) continue;
+    // nibble -> one 0x01 byte per set bit (bit i -> byte i), times val
+    auto spread = [&](uint32_t nib) { return ((nib * 0x00204081u) & 0x01010101u) * val; };
+    uint4 w = rec[c];
+    w.x |= spread(bits & 0xFu);
+    w.y |= spread((bits >> 4) & 0xFu);
+    w.z |= spread((bits >> 8) & 0xFu);
+    w.w |= spread((bits >> 12) & 0xFu);
+    rec[c] = w;
+  }
+}
+
 // dist / next-hop rows of the (root, v) pairs in `acc` (lane = node v): one
-// coalesced store per root present anywhere in the wave
+// coalesced store per root present anywhere in the wave; deferred runs only
+// record dist + 1 in lev (msbfs_rows writes whole rows at the end)
 template <int KP>
 __device__ __forceinline__ void emit_rows(const MsArgs& a, const VB& b, uint32_t v, uint64_t acc,
                                           const uint64_t* pacc, uint32_t dist) {
+  if (a.defer) {
+    if (acc) set_lev(a, b, v, acc, dist + 1u);
+    return;
+  }
   uint64_t un = wave_or64(acc);
   while (un) {
     const uint32_t r = (uint32_t)(__ffsll((unsigned long long)un) - 1);
@@ -150,10 +175,18 @@ __global__ void __launch_bounds__(256) msbfs_init_kernel(DevGraph g, MsArgs a) {
   const uint64_t bm = 1ull << bit;
   uint64_t* f1 = b.front(a, 1);
   const size_t row = (size_t)rix * V;
+  uint32_t* lev32 = reinterpret_cast<uint32_t*>(a.lev);
+  auto lev_or = [&](uint32_t v, uint32_t val) {  // byte `bit` of node v's record
+    atomicOr(&lev32[(((size_t)vbl * V + v) * 64u + bit) / 4u], val << (8u * (bit & 3u)));
+  };
   if (lane == 0) {
     or64(&b.seen[s], bm);
-    if (a.dist && b.g == 0) a.dist[row + s] = 0u;
-    if (a.nh) a.nh[(row + s) * a.W + b.g] = 0u;
+    if (a.defer) {
+      lev_or(s, 1u);
+    } else {
+      if (a.dist && b.g == 0) a.dist[row + s] = 0u;
+      if (a.nh) a.nh[(row + s) * a.W + b.g] = 0u;
+    }
   }
   const uint32_t e0 = g.row_ptr[s], e1 = g.row_ptr[s + 1];
   bool any = false;
@@ -175,8 +208,13 @@ __global__ void __launch_bounds__(256) msbfs_init_kernel(DevGraph g, MsArgs a) {
       if (!old) mass += g.row_ptr[v + 1] - g.row_ptr[v];  // first root to reach v
     }
     if (k < (uint32_t)KP) or64(&b.P[(size_t)v * KP + k], bm);
-    if (a.dist && b.g == 0) a.dist[row + v] = 1u;
-    if (a.nh) a.nh[(row + v) * a.W + b.g] = (k < 32u) ? (1u << k) : 0u;
+    if (a.defer) {
+      // parallel links: the same byte again, same value (an OR of 2 | 2 = 2)
+      lev_or(v, 2u);
+    } else {
+      if (a.dist && b.g == 0) a.dist[row + v] = 1u;
+      if (a.nh) a.nh[(row + v) * a.W + b.g] = (k < 32u) ? (1u << k) : 0u;
+    }
     any = true;
   }
   mass = wave_add32(mass);
@@ -283,7 +321,9 @@ __global__ void __launch_bounds__(256) msbfs_level_kernel(DevGraph g, MsArgs a, 
         if (tr) atomicAdd(&a.mass[vbl * a.lmax + d + 1], end - beg);
       }
     }
-    if ((acc >> lane) & 1ull) {  // lane r writes root r's entries
+    if (a.defer) {
+      if (lane == 0 && acc) set_lev(a, b, u, acc, d + 2u);
+    } else if ((acc >> lane) & 1ull) {  // lane r writes root r's entries
       const size_t row = (size_t)(b.rix0 + lane) * V + u;
       if (a.dist && b.g == 0) a.dist[row] = d + 1;
       if (a.nh) a.nh[row * a.W + b.g] = gather_word<KP>(pacc, lane);
@@ -398,41 +438,165 @@ __global__ void __launch_bounds__(256) msbfs_final_kernel(DevGraph g, MsArgs a) 
   }
 }
 
-// ---------------------------------------------------------------- digest
-// Digest of finished rows: `segs` workgroups per root, each over a node
-// range, adding into a zeroed record. The root's next-hop keys sit in LDS, so
-// a next-hop bit costs one LDS read and one add.
-__global__ void __launch_bounds__(256) row_digest_kernel(DevGraph g, const uint32_t* roots,
-                                                         const uint32_t* dist, const uint32_t* nh,
-                                                         uint32_t W, uint32_t kcap, uint32_t segs,
-                                                         ospf_digest* out) {
-  extern __shared__ uint64_t keys[];
-  const uint32_t rix = blockIdx.x / segs, seg = blockIdx.x % segs, V = g.V;
-  const uint32_t s = roots[rix];
-  const uint32_t nb0 = g.dn_off[s];
-  const uint32_t nn = min(g.dn_off[s + 1] - nb0, kcap);  // > kcap: error word already set
-  for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) keys[i] = digest_nh_key(g.dn[nb0 + i]);
+// ---------------------------------------------------------------- rows
+// Deferred output: one workgroup writes the whole rows of 64 nodes x 64 roots.
+// lev (dist + 1) and the next-hop words (bit-planes transposed per root) are
+// staged in LDS, then stored root by root: 16 lanes x 16 B cover one root's
+// 64 consecutive dist values, so the dist rows (and nh rows when W == 1) go
+// out as whole 16-B stores; wider nh rows store word g of each node.
+template <int KP>
+__global__ void __launch_bounds__(256) msbfs_rows_kernel(DevGraph g, MsArgs a) {
+  __shared__ uint8_t s_lev[64 * 64];   // [node][root]
+  __shared__ uint32_t s_nh[64 * 65];   // [root][node] (+1 pad: conflict-free columns)
+  __shared__ uint64_t s_dk[64 * 2];    // [node] {dist_key, node_key}
+  const uint32_t vbl = blockIdx.x % a.nb;
+  const VB b(a, vbl, g.V, KP);
+  const uint32_t V = g.V, tid = threadIdx.x;
+  const uint32_t v0 = (blockIdx.x / a.nb) * 64u, nv = min(64u, V - v0);
+  // stage lev: 64 nodes x 64 B contiguous
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(a.lev + ((size_t)vbl * V + v0) * 64u);
+    if (tid < nv * 4u) reinterpret_cast<uint4*>(s_lev)[tid] = src[tid];
+  }
+  // next-hop word g of (node n, roots 16q..16q+15) from n's planes
+  {
+    const uint32_t n = tid >> 2, q = tid & 3u;
+    uint64_t p[KP];
+    if (n < nv) {
+      load_planes<KP>(b.P, v0 + n, p);
+    } else {
+#pragma unroll
+      for (int k = 0; k < KP; ++k) p[k] = 0;
+    }
+#pragma unroll 4
+    for (uint32_t i = 0; i < 16u; ++i) {
+      const uint32_t r = 16u * q + i;
+      s_nh[r * 65u + n] = gather_word<KP>(p, r);
+    }
+  }
+  if (a.digest && tid < 128u) s_dk[tid] = (v0 + tid / 2u < V) ? g.dkey[2ull * v0 + tid] : 0ull;
   __syncthreads();
-  const uint32_t* drow = dist + (size_t)rix * V;
-  const uint32_t* nrow = nh + (size_t)rix * V * W;
-  const uint32_t v0 = (uint32_t)((uint64_t)V * seg / segs), v1 = (uint32_t)((uint64_t)V * (seg + 1) / segs);
-  uint64_t reached = 0, sumd = 0, h = 0;
-  for (uint32_t v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
-    const uint32_t d = drow[v];
-    if (d == kInf) continue;
-    reached += 1;
-    sumd += d;
-    h += digest_node_term(v, d);
-    uint64_t ks = 0;
-    for (uint32_t w = 0; w < W; ++w) {
-      uint32_t bits = nrow[(size_t)v * W + w];
-      while (bits) {
-        const uint32_t i = 32u * w + __ffs(bits) - 1;
-        bits &= bits - 1;
-        if (i < nn) ks += keys[i];
+  const uint32_t nr = min(64u, a.n - b.rix0);
+  const bool vec = (V & 3u) == 0 && nv == 64u;
+  if (a.digest) {
+    // root r = tid / 4 over nodes 16 * (tid % 4) .. + 15; the 4 lanes of a
+    // root then add up and one of them adds into the record (passes add up)
+    const uint32_t r = tid >> 2, n0 = 16u * (tid & 3u);
+    uint64_t reached = 0, sumd = 0, h = 0;
+    if (r < nr) {
+      for (uint32_t n = n0; n < n0 + 16u && n < nv; ++n) {
+        const uint32_t l = s_lev[n * 64u + r];
+        if (!l) continue;
+        if (b.g == 0) {
+          reached += 1;
+          sumd += l - 1u;
+          h += s_dk[2u * n] * (uint64_t)l;
+        }
+        const uint32_t word = s_nh[r * 65u + n];
+        if (word) h += s_dk[2u * n + 1u] * digest_word_key(b.g, word);
       }
     }
-    if (ks) h += digest_node_key(v) * ks;
+#pragma unroll
+    for (int o = 1; o < 4; o <<= 1) {
+      reached += shfl_xor64(reached, o);
+      sumd += shfl_xor64(sumd, o);
+      h += shfl_xor64(h, o);
+    }
+    if ((tid & 3u) == 0 && r < nr) {
+      ospf_digest* dg = a.digest + b.rix0 + r;
+      if (reached) {
+        atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)reached);
+        atomicAdd((unsigned long long*)&dg->sum_dist, (unsigned long long)sumd);
+      }
+      if (h) atomicAdd((unsigned long long*)&dg->hash, (unsigned long long)h);
+    }
+  }
+  if (a.dist && b.g == 0) {
+    for (uint32_t i = tid; i < 64u * 16u; i += kBlock) {  // (root, node quad)
+      const uint32_t r = i >> 4, q = i & 15u;
+      if (r >= nr) break;
+      uint32_t dv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t l = s_lev[(4u * q + j) * 64u + r];
+        dv[j] = l ? l - 1u : kInf;
+      }
+      uint32_t* row = a.dist + (size_t)(b.rix0 + r) * V + v0 + 4u * q;
+      if (vec) {
+        *reinterpret_cast<uint4*>(row) = make_uint4(dv[0], dv[1], dv[2], dv[3]);
+      } else {
+        for (uint32_t j = 0; j < 4u; ++j)
+          if (4u * q + j < nv) row[j] = dv[j];
+      }
+    }
+  }
+  if (a.nh) {
+    if (a.W == 1) {
+      for (uint32_t i = tid; i < 64u * 16u; i += kBlock) {
+        const uint32_t r = i >> 4, q = i & 15u;
+        if (r >= nr) break;
+        const uint32_t* src = &s_nh[r * 65u + 4u * q];
+        uint32_t* row = a.nh + (size_t)(b.rix0 + r) * V + v0 + 4u * q;
+        if (vec) {
+          *reinterpret_cast<uint4*>(row) = make_uint4(src[0], src[1], src[2], src[3]);
+        } else {
+          for (uint32_t j = 0; j < 4u; ++j)
+            if (4u * q + j < nv) row[j] = src[j];
+        }
+      }
+    } else {
+      const bool last = b.g == a.npass - 1 && a.npass < a.W;
+      for (uint32_t i = tid; i < 64u * 64u; i += kBlock) {  // (root, node)
+        const uint32_t r = i >> 6, n = i & 63u;
+        if (r >= nr) break;
+        if (n >= nv) continue;
+        uint32_t* p = a.nh + ((size_t)(b.rix0 + r) * V + v0 + n) * a.W;
+        p[b.g] = s_nh[r * 65u + n];
+        if (last)  // words past the computed passes
+          for (uint32_t k = a.npass; k < a.W; ++k) p[k] = 0u;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- digest
+// Digest of finished rows (runs whose rows are written per level): `segs`
+// workgroups per root, each over a node range, adding into a zeroed record.
+__global__ void __launch_bounds__(256) row_digest_kernel(DevGraph g, const uint32_t* dist,
+                                                         const uint32_t* nh, uint32_t W,
+                                                         uint32_t segs, ospf_digest* out) {
+  const uint32_t rix = blockIdx.x / segs, seg = blockIdx.x % segs, V = g.V;
+  const uint32_t* drow = dist + (size_t)rix * V;
+  const uint32_t* nrow = nh + (size_t)rix * V * W;
+  const uint32_t v0 = (uint32_t)((uint64_t)V / 4u * seg / segs) * 4u,
+                 v1 = seg + 1 == segs ? V : (uint32_t)((uint64_t)V / 4u * (seg + 1) / segs) * 4u;
+  uint64_t reached = 0, sumd = 0, h = 0;
+  auto node = [&](uint32_t v, uint32_t d, uint64_t wsum) {
+    if (d == kInf) return;
+    const uint4 kk = reinterpret_cast<const uint4*>(g.dkey)[v];
+    const uint64_t kd = ((uint64_t)kk.y << 32) | kk.x, kn = ((uint64_t)kk.w << 32) | kk.z;
+    reached += 1;
+    sumd += d;
+    h += kd * ((uint64_t)d + 1) + kn * wsum;
+  };
+  auto wk = [](uint32_t w, uint32_t word) { return word ? digest_word_key(w, word) : 0ull; };
+  if (W == 1 && (V & 3u) == 0) {
+    // 4 nodes per lane per step (segment bounds are multiples of 4): one
+    // 16-B load each of dist and next hops
+    for (uint32_t v = v0 + threadIdx.x * 4u; v < v1; v += blockDim.x * 4u) {
+      const uint4 d4 = *reinterpret_cast<const uint4*>(drow + v);
+      const uint4 n4 = *reinterpret_cast<const uint4*>(nrow + v);
+      node(v, d4.x, wk(0, n4.x));
+      node(v + 1, d4.y, wk(0, n4.y));
+      node(v + 2, d4.z, wk(0, n4.z));
+      node(v + 3, d4.w, wk(0, n4.w));
+    }
+  } else {
+    for (uint32_t v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
+      uint64_t ws = 0;
+      for (uint32_t w = 0; w < W; ++w) ws += wk(w, nrow[(size_t)v * W + w]);
+      node(v, drow[v], ws);
+    }
   }
   __shared__ uint64_t s_r[kWavesPerBlock], s_s[kWavesPerBlock], s_h[kWavesPerBlock];
 #pragma unroll
@@ -473,7 +637,11 @@ hipError_t launch_round_kp(const DevGraph& g, const MsArgs& a, uint32_t depth_bo
                        s, g, a, d);
     hipLaunchKernelGGL(msbfs_settle_kernel<KP>, dim3(a.nb * chunks), dim3(kBlock), 0, s, g, a, d);
   }
-  hipLaunchKernelGGL(msbfs_final_kernel, dim3(a.nb * chunks), dim3(kBlock), 0, s, g, a);
+  if (a.defer)
+    hipLaunchKernelGGL(msbfs_rows_kernel<KP>, dim3(a.nb * ((g.V + 63u) / 64u)), dim3(kBlock), 0, s,
+                       g, a);
+  else
+    hipLaunchKernelGGL(msbfs_final_kernel, dim3(a.nb * chunks), dim3(kBlock), 0, s, g, a);
   return hipGetLastError();
 }
 
@@ -488,15 +656,15 @@ hipError_t launch_msbfs_round(int kp, const DevGraph& g, const MsArgs& a, uint32
   }
 }
 
-hipError_t launch_row_digest(const DevGraph& g, const uint32_t* roots, uint32_t n,
-                             const uint32_t* dist, const uint32_t* nh, uint32_t W, uint32_t kcap,
-                             ospf_digest* out, hipStream_t s) {
+hipError_t launch_row_digest(const DevGraph& g, uint32_t n, const uint32_t* dist,
+                             const uint32_t* nh, uint32_t W, ospf_digest* out, hipStream_t s) {
   hipError_t e = hipMemsetAsync(out, 0, (size_t)n * sizeof(ospf_digest), s);
   if (e != hipSuccess) return e;
-  const uint32_t cap = min(kcap, 32u * W);
-  const uint32_t segs = max(1u, min((2048u + n - 1) / n, max(1u, g.V / 2048u)));
-  hipLaunchKernelGGL(row_digest_kernel, dim3(n * segs), dim3(kBlock), (size_t)cap * 8u, s, g, roots,
-                     dist, nh, W, cap, segs, out);
+  // enough workgroups to fill the chip; segment bounds are multiples of 4
+  // nodes so the 16-B loads stay aligned
+  const uint32_t segs = max(1u, min((16384u + n - 1) / n, max(1u, g.V / 1024u)));
+  hipLaunchKernelGGL(row_digest_kernel, dim3(n * segs), dim3(kBlock), 0, s, g, dist, nh, W, segs,
+                     out);
   return hipGetLastError();
 }
 

@@ -46,6 +46,7 @@
 #include <string>
 #include <thread>
 #include <tuple>
+#include <map>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -474,29 +475,48 @@ struct Digest {
   uint64_t reached = 0, sumDist = 0, hash = 0;
 };
 
-// sum over reached nodes of node_term(v, dist) plus, for
-// every next-hop n of v, pair_term(v, n) = node_key(v) * nh_key(n)
-// (mod 2^64). Unknown names get id 0xFFFFFFFF.
-static inline uint64_t nodeTerm(uint64_t v, uint64_t dist) { return mix64((v << 32) | dist); }
-static inline uint64_t pairTerm(uint64_t v, uint64_t n) {
+// sum over reached nodes v of dist_key(v) * (dist + 1) plus,
+// for every non-zero next-hop word g of v, node_key(v) * word_key(g, word)
+// (mod 2^64). Word g holds the bits of the root's distinct neighbours
+// 32g .. 32g+31 in ascending id order (ids = name ranks; neighbours over
+// every link of the root, up or down). Unknown names get id 0xFFFFFFFF.
+static inline uint64_t nodeTerm(uint64_t v, uint64_t dist) {
+  const uint64_t distKey = mix64((v & 0xFFFFFFFFull) ^ 0x2545F4914F6CDD1DULL) | 1ull;
+  return distKey * (dist + 1);
+}
+static inline uint64_t wordTerm(uint64_t v, uint64_t g, uint32_t word) {
+  if (!word) return 0;
   const uint64_t nodeKey = mix64((v & 0xFFFFFFFFull) ^ 0xD6E8FEB86659FD93ULL) | 1ull;
-  const uint64_t nhKey = mix64((((n & 0xFFFFFFFFull) + 1) << 32) ^ 0x9E3779B97F4A7C15ULL);
-  return nodeKey * nhKey;
+  const uint64_t wordKey = mix64(((g << 32) | word) ^ 0x9E3779B97F4A7C15ULL);
+  return nodeKey * wordKey;
 }
 
-static Digest digestOf(const SpfResult& r,
+static Digest digestOf(const Graph& g, const std::string& root, const SpfResult& r,
                        const std::unordered_map<std::string, uint32_t>& ids) {
   Digest d;
   auto idOf = [&](const std::string& n) -> uint64_t {
     auto it = ids.find(n);
     return it == ids.end() ? 0xFFFFFFFFull : it->second;
   };
+  std::vector<uint64_t> nbr;  // the root's distinct neighbours, ascending id
+  for (const auto& e : g.linksOf(root)) {
+    const std::string& p = e->peer(root);
+    if (p != root) nbr.push_back(idOf(p));
+  }
+  std::sort(nbr.begin(), nbr.end());
+  nbr.erase(std::unique(nbr.begin(), nbr.end()), nbr.end());
+  std::map<uint64_t, uint32_t> words;
   for (const auto& [name, nr] : r) {
     const uint64_t id = idOf(name);
     d.reached++;
     d.sumDist += nr.metric;
     d.hash += nodeTerm(id, nr.metric);
-    for (const auto& nh : nr.nextHops) d.hash += pairTerm(id, idOf(nh));
+    words.clear();
+    for (const auto& nh : nr.nextHops) {
+      const uint64_t i = std::lower_bound(nbr.begin(), nbr.end(), idOf(nh)) - nbr.begin();
+      words[i / 32] |= 1u << (i % 32);
+    }
+    for (const auto& [w, bits] : words) d.hash += wordTerm(id, w, bits);
   }
   return d;
 }
@@ -654,7 +674,7 @@ int orc_digest_roots(void* h, const char* rootsNl, uint32_t n, int useMetric,
   auto work = [&]() {
     for (uint32_t i; (i = next.fetch_add(1)) < n;) {
       SpfResult r = o->g.dijkstra(roots[i], useMetric != 0, nullptr);
-      Digest d = digestOf(r, o->ids);
+      Digest d = digestOf(o->g, roots[i], r, o->ids);
       out[3 * i] = d.reached;
       out[3 * i + 1] = d.sumDist;
       out[3 * i + 2] = d.hash;

@@ -10,7 +10,7 @@ n = int(sys.argv[2]) if len(sys.argv) > 2 else 60
 tot = {}
 for r in rows:
     k = r["Kernel_Name"]
-    short = next((s for s in ("init", "level", "settle", "final", "digest", "fill", "spf_bfs")
+    short = next((s for s in ("init", "level", "settle", "final", "rows", "digest", "fill", "spf_bfs")
                   if s in k.lower()), k[:24])
     dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     tot[short] = tot.get(short, 0) + dur

@@ -265,10 +265,15 @@ def _run_forced(eng, monkeypatch, variant, roots, W, **kw):
 
 @pytest.mark.parametrize("seed", range(3))
 @pytest.mark.parametrize("hop", [False, True])
-def test_msbfs_matches_per_root_bfs(seed, hop, monkeypatch):
+@pytest.mark.parametrize("defer", [True, False])
+def test_msbfs_matches_per_root_bfs(seed, hop, defer, monkeypatch):
     """Variant 5 (64 roots per traversal) vs variant 4 (one root per
     workgroup) on random unit graphs with parallel links, down links and
-    overloaded nodes; 150 roots = two full 64-root batches + a ragged one."""
+    overloaded nodes; 150 roots = two full 64-root batches + a ragged one.
+    defer: rows written once at the end from per-(node, root) level bytes
+    (default) or per level (OSPF_MS_NODEFER)."""
+    if not defer:
+        monkeypatch.setenv("OSPF_MS_NODEFER", "1")
     st, names = random_stream(300 + seed, n=150, p=0.05, unit=not hop)
     p, eng = _engine_for(st)
     roots = np.arange(eng.V, dtype=np.uint32)
