@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <map>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -32,8 +33,12 @@ struct ospf_ctx {
   uint32_t max_dn = 0;
   uint32_t depth_bound = 2;  // BFS levels any root can reach (unit metric / hop count)
   // scratch
-  void* d_scratch = nullptr;
-  size_t scratch_bytes = 0;
+  // scratch per stream: batches queued on different streams run concurrently
+  struct Scratch {
+    void* p = nullptr;
+    size_t bytes = 0;
+  };
+  std::map<void*, Scratch> scratch;
   void* d_stage = nullptr;
   size_t stage_bytes = 0;
   uint32_t* d_err = nullptr;
@@ -73,6 +78,17 @@ int ensure(ospf_ctx* c, void** p, size_t* have, size_t need) {
   return OSPF_OK;
 }
 
+// the scratch of `stream`, grown to `need` bytes (a grown buffer replaces the
+// old one only after the stream's queued work is done with it)
+char* stream_scratch(ospf_ctx* c, void* stream, size_t need, int* rc) {
+  ospf_ctx::Scratch& sc = c->scratch[stream];
+  *rc = OSPF_OK;
+  if (sc.bytes >= need) return (char*)sc.p;
+  if (sc.p) hipStreamSynchronize((hipStream_t)stream);
+  *rc = ensure(c, &sc.p, &sc.bytes, need);
+  return (char*)sc.p;
+}
+
 struct Plan {
   int variant;
   uint32_t block;
@@ -107,7 +123,9 @@ Plan make_plan(const ospf_ctx* c, uint32_t W, uint32_t ign_cap, bool unit, uint3
     }
     return false;
   };
-  if (unit && fits(5) && n_roots >= kMsMinRoots) {
+  // wide roots (many next-hop words) go multi-source even in small batches:
+  // the per-root kernel re-runs the traversal per 4-word slice
+  if (unit && fits(5) && (n_roots >= kMsMinRoots || (W >= 8 && n_roots >= 4))) {
     p.variant = 5;
   } else if (unit) {
     p.variant = (W == 1 && fits(3)) ? 3 : fits(4) ? 4 : 2;
@@ -188,9 +206,9 @@ int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
   const bool defer = c->depth_bound <= 254 && !getenv("OSPF_MS_NODEFER");
   const bool dist_scr = dig && !defer && !(flags & OSPF_WANT_DIST);
   const bool nh_scr = dig && !defer && !(flags & OSPF_WANT_NH);
-  // seen, front x2, accb, planes (u64 per node each) + lev (64 B per node) +
-  // found, mass
-  const size_t per_vb = align_up((size_t)V * 8ull * (4 + kp) + (defer ? V * 64ull : 0) + lmax * 8ull, 256);
+  // seen, accb, 2 frontier records (16 B), planes (u64 per node each) + lev
+  // (64 B per node) + found, mass
+  const size_t per_vb = align_up((size_t)V * 8ull * (6 + kp) + (defer ? V * 64ull : 0) + lmax * 8ull, 256);
   uint32_t push_div = 8;  // push a level when its frontier's edge mass * push_div < E
   if (const char* e = getenv("OSPF_MS_PUSH_DIV")) push_div = (uint32_t)std::max(0, atoi(e));
   uint32_t nb_cap = 32;
@@ -205,9 +223,9 @@ int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
   const size_t state_bytes = per_vb * nb_max;
   const size_t dist_bytes = dist_scr ? align_up((size_t)chunk * V * 4ull, 256) : 0;
   const size_t nh_bytes = nh_scr ? align_up((size_t)chunk * V * W * 4ull, 256) : 0;
-  int rc = ensure(c, &c->d_scratch, &c->scratch_bytes, state_bytes + dist_bytes + nh_bytes);
+  int rc = OSPF_OK;
+  char* sp = stream_scratch(c, s, state_bytes + dist_bytes + nh_bytes, &rc);
   if (rc) return rc;
-  char* sp = (char*)c->d_scratch;
   HIPCHK(c, hipSetDevice(c->device));
   for (uint32_t r0 = 0; r0 < b->n_roots; r0 += chunk) {
     const uint32_t n = std::min(chunk, b->n_roots - r0);
@@ -232,14 +250,14 @@ int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
       a.vb0 = vb0;
       a.nb = std::min(nb_max, total_vb - vb0);
 
-      a.seen = (uint64_t*)sp;
-      a.front = a.seen + (size_t)a.nb * V;
-      a.accb = a.front + 2ull * a.nb * V;
+      a.front = (uint64_t*)sp;  // 16-B records: first, for alignment
+      a.seen = a.front + 4ull * a.nb * V;
+      a.accb = a.seen + (size_t)a.nb * V;
       a.planes = a.accb + (size_t)a.nb * V;
       a.lev = (uint8_t*)(a.planes + (size_t)a.nb * V * kp);  // 16-B aligned (uint4 access)
       a.found = (uint32_t*)(a.lev + (defer ? (size_t)a.nb * V * 64ull : 0));
       a.mass = a.found + (size_t)a.nb * lmax;
-      HIPCHK(c, hipMemsetAsync(sp, 0, (size_t)a.nb * V * 8ull * (4 + kp) +
+      HIPCHK(c, hipMemsetAsync(sp, 0, (size_t)a.nb * V * 8ull * (6 + kp) +
                                           (defer ? (size_t)a.nb * V * 64ull : 0) +
                                           (size_t)a.nb * lmax * 8ull, s));
       hipError_t e = ospf::launch_msbfs_round(kp, c->g, a, c->depth_bound, s);
@@ -291,7 +309,8 @@ int ospf_close(ospf_ctx* c) {
   if (!c) return OSPF_E_INVAL;
   hipSetDevice(c->device);
   if (c->d_graph) hipFree(c->d_graph);
-  if (c->d_scratch) hipFree(c->d_scratch);
+  for (auto& kv : c->scratch)
+    if (kv.second.p) hipFree(kv.second.p);
   if (c->d_stage) hipFree(c->d_stage);
   if (c->d_err) hipFree(c->d_err);
   delete c;
@@ -524,11 +543,9 @@ int ospf_run_batch_dev(ospf_ctx* c, const ospf_batch* b, void* stream) {
   if (dist_scratch) need += align_up(n_roots * V * 4, 256);
   if (nh_scratch) need += align_up(n_roots * V * nh_words * 4ull, 256);
   need += planes_bytes;
-  if (need) {
-    int rc = ensure(c, &c->d_scratch, &c->scratch_bytes, need);
-    if (rc) return rc;
-  }
-  char* sp = (char*)c->d_scratch;
+  int src = OSPF_OK;
+  char* sp = need ? stream_scratch(c, stream, need, &src) : nullptr;
+  if (src) return src;
   ospf::RunArgs a{};
   a.roots = d_roots;
   a.ign_off = ign ? d_ign_off : nullptr;

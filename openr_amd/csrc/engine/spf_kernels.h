@@ -110,7 +110,7 @@ struct MsArgs {
   uint32_t* dist;         // [n][V] or null
   uint32_t* nh;           // [n][V][W] or null
   uint64_t* seen;         // [nb][V]
-  uint64_t* front;        // [2][nb][V]   frontier of level d in front[d & 1]
+  uint64_t* front;        // [2][nb][V][2] {frontier, with-planes} of level d in front[d & 1]
   uint64_t* accb;         // [nb][V]      push accumulator (zero between levels)
   uint64_t* planes;       // [nb][V][KP]
   uint32_t* found;        // [nb][lmax]   level d non-empty

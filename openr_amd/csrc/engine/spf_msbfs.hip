@@ -86,8 +86,10 @@ struct VB {
     accb = a.accb + (size_t)vbl * V;
     P = a.planes + (size_t)vbl * V * kp;
   }
+  // frontier record of level d: {roots with v in the frontier, those of them
+  // with a non-zero plane in this pass} (16 B per node)
   __device__ uint64_t* front(const MsArgs& a, uint32_t d) const {
-    return a.front + ((size_t)(d & 1u) * a.nb + vbl) * V;
+    return a.front + ((size_t)(d & 1u) * a.nb + vbl) * V * 2u;
   }
 };
 
@@ -204,8 +206,10 @@ __global__ void __launch_bounds__(256) msbfs_init_kernel(DevGraph g, MsArgs a) {
     const uint32_t k = lo - 32u * b.g;  // >= 32 (wrapped) when outside this word
     or64(&b.seen[v], bm);
     if (transit(g, v)) {
-      const unsigned long long old = atomicOr((unsigned long long*)&f1[v], (unsigned long long)bm);
+      const unsigned long long old =
+          atomicOr((unsigned long long*)&f1[2u * v], (unsigned long long)bm);
       if (!old) mass += g.row_ptr[v + 1] - g.row_ptr[v];  // first root to reach v
+      if (k < (uint32_t)KP) or64(&f1[2u * v + 1u], bm);
     }
     if (k < (uint32_t)KP) or64(&b.P[(size_t)v * KP + k], bm);
     if (a.defer) {
@@ -230,21 +234,25 @@ __device__ __forceinline__ void pull_scan(const DevGraph& g, const uint64_t* fcu
                                           uint32_t beg, uint32_t end, uint64_t m, uint64_t& acc,
                                           uint64_t* pacc) {
   const uint4* q = reinterpret_cast<const uint4*>(g.colx);
+  const uint4* fr = reinterpret_cast<const uint4*>(fcur);
   for (uint32_t e = beg; e < end; e += STEP) {
     const uint4 c = q[e >> 2];
     const uint32_t cs[4] = {c.x, c.y, c.z, c.w};
-    uint64_t fs[4];
+    uint4 fs[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) fs[i] = (cs[i] & kDown) ? 0ull : fcur[cs[i]];
+    for (int i = 0; i < 4; ++i) fs[i] = (cs[i] & kDown) ? make_uint4(0, 0, 0, 0) : fr[cs[i]];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const uint64_t f = fs[i] & m;
+      const uint64_t f = (((uint64_t)fs[i].y << 32) | fs[i].x) & m;
       if (!f) continue;
       acc |= f;
+      // roots whose tail has no plane bit in this pass add nothing to them
+      const uint64_t fz = (((uint64_t)fs[i].w << 32) | fs[i].z) & f;
+      if (!fz) continue;
       uint64_t pu[KP];
       load_planes<KP>(P, cs[i], pu);
 #pragma unroll
-      for (int k = 0; k < KP; ++k) pacc[k] |= pu[k] & f;
+      for (int k = 0; k < KP; ++k) pacc[k] |= pu[k] & fz;
     }
   }
 }
@@ -277,6 +285,14 @@ __device__ __forceinline__ void push_scan(const DevGraph& g, const VB& b, uint32
 }
 
 template <int KP>
+__device__ __forceinline__ uint64_t planes_or(const uint64_t* p) {
+  uint64_t z = 0;
+#pragma unroll
+  for (int k = 0; k < KP; ++k) z |= p[k];
+  return z;
+}
+
+template <int KP>
 __global__ void __launch_bounds__(256) msbfs_level_kernel(DevGraph g, MsArgs a, uint32_t d) {
   const uint32_t vbl = blockIdx.x % a.nb;
   if (!a.found[vbl * a.lmax + d]) return;  // level d is empty: this batch is done
@@ -294,7 +310,7 @@ __global__ void __launch_bounds__(256) msbfs_level_kernel(DevGraph g, MsArgs a, 
     const uint32_t u = g.big[bi];
     const uint32_t beg = g.row_ptr[u], end = g.row_ptr[u + 1];
     if (push) {
-      const uint64_t fu = fcur[u];
+      const uint64_t fu = fcur[2u * u];
       if (!fu) return;
       uint64_t pu[KP];
       load_planes<KP>(b.P, u, pu);
@@ -312,7 +328,8 @@ __global__ void __launch_bounds__(256) msbfs_level_kernel(DevGraph g, MsArgs a, 
     for (int k = 0; k < KP; ++k) pacc[k] = wave_or64(pacc[k]);
     const bool tr = transit(g, u);
     if (lane == 0) {
-      fnext[u] = tr ? acc : 0ull;
+      fnext[2u * u] = tr ? acc : 0ull;
+      fnext[2u * u + 1u] = tr ? planes_or<KP>(pacc) & acc : 0ull;
       if (acc) {
         b.seen[u] = (~m & b.valid) | acc;
 #pragma unroll
@@ -335,7 +352,7 @@ __global__ void __launch_bounds__(256) msbfs_level_kernel(DevGraph g, MsArgs a, 
   const uint32_t v = blk * kBlock + threadIdx.x;
   if (push) {
     if (v >= V) return;
-    const uint64_t fu = fcur[v];
+    const uint64_t fu = fcur[2u * v];
     if (!fu) return;
     const uint32_t beg = g.row_ptr[v], end = g.row_ptr[v + 1];
     if (end - beg > kMsBigDeg) return;
@@ -368,7 +385,8 @@ __global__ void __launch_bounds__(256) msbfs_level_kernel(DevGraph g, MsArgs a, 
       for (int k = 0; k < KP; ++k)
         if (pacc[k]) b.P[(size_t)v * KP + k] |= pacc[k];
     }
-    fnext[v] = tr ? acc : 0ull;
+    fnext[2u * v] = tr ? acc : 0ull;
+    fnext[2u * v + 1u] = tr ? planes_or<KP>(pacc) & acc : 0ull;
     if (tr) mass = end - beg;
   }
   emit_rows<KP>(a, b, v, acc, pacc, d + 1);
@@ -402,7 +420,8 @@ __global__ void __launch_bounds__(256) msbfs_settle_kernel(DevGraph g, MsArgs a,
       load_planes<KP>(b.P, v, pacc);
       if (tr) mass = g.row_ptr[v + 1] - g.row_ptr[v];
     }
-    fnext[v] = tr ? acc : 0ull;
+    fnext[2u * v] = tr ? acc : 0ull;
+    fnext[2u * v + 1u] = tr ? planes_or<KP>(pacc) & acc : 0ull;
   }
   emit_rows<KP>(a, b, v, acc, pacc, d + 1);
   mass = wave_add32(mass);
