@@ -90,6 +90,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-nh", action="store_true", help="skip next-hop output (diagnostic)")
     ap.add_argument("--serial-streams", action="store_true", help="one stream for all classes")
+    ap.add_argument("--root-order", choices=["auto", "locality", "random"], default="auto",
+                    help="sweep order within a width class: grouped by smallest neighbour "
+                         "(multi-source batches share frontiers), the random permutation, or "
+                         "auto = grouped for single-word classes only (measured: grouping "
+                         "wide roots makes their per-pass next-hop planes denser and slower)")
     ap.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles", "r01"))
     args = ap.parse_args()
 
@@ -118,7 +123,10 @@ def main():
     perm = np.random.default_rng(0x5EED).permutation(V).astype(np.uint32)
     nbrs = shard.distinct_neighbors(csr["row_ptr"], csr["col"])
     words = np.maximum(1, (nbrs + 31) // 32)
-    classes = shard.make_classes(perm, words, args.batch)
+    key = shard.first_neighbor(csr["row_ptr"], csr["col"]) if args.root_order != "random" \
+        else None
+    classes = shard.make_classes(perm, words, args.batch, key,
+                                 max_grouped_words=1 if args.root_order == "auto" else None)
     B = sum(c.per_step for c in classes)
     for c in classes:
         n = c.per_step

@@ -188,22 +188,74 @@ uint32_t transit_depth_bound(uint32_t V, const uint32_t* row_ptr, const uint32_t
   return 2u * ecc_max + 2u;
 }
 
+// Batch shape of the multi-source BFS for n roots with at most kcap distinct
+// neighbours: R roots per traversal, PP planes per 64-bit plane word, KP
+// plane words per node, OW next-hop words per pass, npass passes per batch.
+struct MsShape {
+  uint32_t R = 64, PP = 1, KP = 32, OW = 1, npass = 1;
+};
+
+// Packing (R < 64) trades launch parallelism for fewer traversals: measured
+// slower for a 12-spine batch on F100k (fewer, denser passes; the plane-presence
+// skip is per root), so it is opt-in (OSPF_MS_PACK=1 or OSPF_MS_R) for now.
+MsShape ms_shape(uint32_t n, uint32_t kcap, bool pack) {
+  MsShape m;
+  if (kcap <= 32) {  // one pass, one word: 64 roots, as few planes as will do
+    m.KP = kcap <= 8 ? 8 : kcap <= 16 ? 16 : 32;
+    return m;
+  }
+  // wide roots: KP = 32 words; pick R minimising the traversals
+  // ceil(n / R) * ceil(kcap / (32 * PP)) (ties: more roots per traversal)
+  m.KP = 32;
+  m.npass = (kcap + 31) / 32;
+  if (!pack) return m;
+  const uint64_t t64 = (uint64_t)((n + 63) / 64) * m.npass;
+  uint64_t best = ~0ull;
+  for (uint32_t R = 64; R >= 1; --R) {
+    const uint32_t PP = 64 / R;
+    const uint64_t t = (uint64_t)((n + R - 1) / R) * ((kcap + 32 * PP - 1) / (32 * PP));
+    if (t < best) {
+      best = t;
+      m.R = R;
+      m.PP = PP;
+    }
+  }
+  if (4 * best > 3 * t64) {  // packing must save a quarter of the traversals
+    m.R = 64;
+    m.PP = 1;
+    return m;
+  }
+  m.OW = m.PP;
+  m.npass = (kcap + 32 * m.OW - 1) / (32 * m.OW);
+  return m;
+}
+
 // Variant 5: multi-source bit-parallel BFS (spf_msbfs.hip). Roots go in
-// 64-root batches; each batch runs one pass per computed next-hop word; a
-// round runs up to `nb` (batch, word) pairs side by side. All launches are
+// R-root batches; each batch runs npass passes (OW next-hop words each); a
+// round runs up to `nb` (batch, pass) pairs side by side. All launches are
 // queued on `s`; nothing waits on the host.
 int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
   const uint32_t V = c->info.n_nodes, W = b->nh_words, flags = b->flags;
   const uint32_t kcap = b->max_root_neighbors ? std::min(b->max_root_neighbors, 32u * W) : 32u * W;
-  const uint32_t npass = std::max<uint32_t>(1, (kcap + 31) / 32);
-  const uint32_t kneed = std::min<uint32_t>(32, kcap);
-  const int kp = kneed <= 8 ? 8 : kneed <= 16 ? 16 : 32;
   const bool dig = flags & OSPF_WANT_DIGEST;
   const uint32_t lmax = c->depth_bound + 2;
   // levels are recorded as dist + 1 in a byte per (node, root): rows are then
   // written once, whole, by msbfs_rows (needs depth <= 254), which also folds
-  // the digest in (no row re-read, no row scratch)
+  // the digest in (no row re-read, no row scratch); packed planes need it
   const bool defer = c->depth_bound <= 254 && !getenv("OSPF_MS_NODEFER");
+  MsShape sh = ms_shape(b->n_roots, kcap, defer && getenv("OSPF_MS_PACK"));
+  if (const char* e = getenv("OSPF_MS_R")) {  // test knob: force R (packs when defer)
+    const uint32_t R = std::min(64, std::max(1, atoi(e)));
+    if (defer && kcap > 32) {
+      sh.R = R;
+      sh.PP = sh.OW = 64 / R;
+      sh.npass = (kcap + 32 * sh.OW - 1) / (32 * sh.OW);
+    }
+  }
+  const int kp = (int)sh.KP;
+  const uint32_t npass = sh.npass;
+  uint64_t rep = 0;
+  for (uint32_t j = 0; j < sh.PP; ++j) rep |= 1ull << (j * sh.R);
   const bool dist_scr = dig && !defer && !(flags & OSPF_WANT_DIST);
   const bool nh_scr = dig && !defer && !(flags & OSPF_WANT_NH);
   // seen, accb, 2 frontier records (16 B), planes (u64 per node each) + lev
@@ -211,15 +263,16 @@ int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
   const size_t per_vb = align_up((size_t)V * 8ull * (6 + kp) + (defer ? V * 64ull : 0) + lmax * 8ull, 256);
   uint32_t push_div = 8;  // push a level when its frontier's edge mass * push_div < E
   if (const char* e = getenv("OSPF_MS_PUSH_DIV")) push_div = (uint32_t)std::max(0, atoi(e));
-  uint32_t nb_cap = 32;
+  uint32_t nb_cap = 96;
   if (const char* e = getenv("OSPF_MS_NB")) nb_cap = std::max(1, atoi(e));
-  nb_cap = (uint32_t)std::max<size_t>(1, std::min<size_t>(nb_cap, (4ull << 30) / per_vb));
+  nb_cap = (uint32_t)std::max<size_t>(1, std::min<size_t>(nb_cap, (6ull << 30) / per_vb));
   // roots per chunk: bounded when digest rows live in scratch
   const size_t row_bytes = (dist_scr ? V * 4ull : 0) + (nh_scr ? (size_t)V * W * 4ull : 0);
   uint32_t chunk = b->n_roots;
   if (row_bytes)
     chunk = (uint32_t)std::max<size_t>(64, std::min<size_t>(chunk, (2ull << 30) / row_bytes) / 64 * 64);
-  const uint32_t nb_max = std::min<uint32_t>(nb_cap, ((std::min(chunk, b->n_roots) + 63) / 64) * npass);
+  const uint32_t nb_max =
+      std::min<uint32_t>(nb_cap, ((std::min(chunk, b->n_roots) + sh.R - 1) / sh.R) * npass);
   const size_t state_bytes = per_vb * nb_max;
   const size_t dist_bytes = dist_scr ? align_up((size_t)chunk * V * 4ull, 256) : 0;
   const size_t nh_bytes = nh_scr ? align_up((size_t)chunk * V * W * 4ull, 256) : 0;
@@ -234,6 +287,10 @@ int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
     a.n = n;
     a.W = W;
     a.npass = npass;
+    a.R = sh.R;
+    a.PP = sh.PP;
+    a.OW = sh.OW;
+    a.rep = rep;
     a.lmax = lmax;
     a.kcap = kcap;
     a.push_div = push_div;
@@ -245,7 +302,7 @@ int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
                       : ((flags & OSPF_WANT_DIST) ? b->d_dist + (size_t)r0 * V : nullptr);
     a.nh = nh_scr ? (uint32_t*)(sp + state_bytes + dist_bytes)
                   : ((flags & OSPF_WANT_NH) ? b->d_nh + (size_t)r0 * V * W : nullptr);
-    const uint32_t total_vb = ((n + 63) / 64) * npass;
+    const uint32_t total_vb = ((n + sh.R - 1) / sh.R) * npass;
     for (uint32_t vb0 = 0; vb0 < total_vb; vb0 += nb_max) {
       a.vb0 = vb0;
       a.nb = std::min(nb_max, total_vb - vb0);
@@ -491,7 +548,7 @@ int ospf_plan_n(const ospf_ctx* c, uint32_t flags, uint32_t nh_words, uint32_t m
   out->lds_bytes = (uint32_t)p.lds;
   if (p.variant == 5) {
     const uint32_t kcap = max_root_neighbors ? std::min(max_root_neighbors, 32u * W) : 32u * W;
-    out->slices = std::max<uint32_t>(1, (kcap + 31) / 32);
+    out->slices = ms_shape(n_roots, kcap, c->depth_bound <= 254 && getenv("OSPF_MS_PACK")).npass;
   } else {
     out->slices = p.variant >= 3 ? ospf::bfs_slices(W) : 1u;
   }

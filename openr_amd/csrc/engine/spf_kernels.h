@@ -101,7 +101,11 @@ struct MsArgs {
   const uint32_t* roots;  // every root of the call
   uint32_t n;             // roots in the call
   uint32_t W;             // nh words per node of the output rows
-  uint32_t npass;         // next-hop words computed (passes per 64-root batch)
+  uint32_t npass;         // passes per R-root batch (each computes OW next-hop words)
+  uint32_t R;             // roots per batch (<= 64)
+  uint32_t PP;            // planes per 64-bit plane word (PP * R <= 64)
+  uint32_t OW;            // next-hop words per pass (32 * OW planes)
+  uint64_t rep;           // sum over j < PP of 1 << (j * R): root bits -> every plane slot
   uint32_t vb0;           // first virtual batch of this round (vb = batch*npass + g)
   uint32_t nb;            // virtual batches in this round
   uint32_t lmax;          // stride of found[]

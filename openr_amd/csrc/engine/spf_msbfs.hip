@@ -13,7 +13,11 @@
 // the k-th distinct neighbour of root r is a next hop of v. A pass computes
 // one 32-bit next-hop word g (planes for neighbour indices [32g, 32g+32)); a
 // root with K distinct neighbours needs ceil(K/32) passes, each re-running the
-// traversal. A "virtual batch" = (64-root batch, word g); a round runs up to
+// traversal. Small batches of wide roots pack planes: a batch of R <= 64
+// roots keeps PP = 64/R planes per word (bit j*R + r = plane j of root r), so
+// a pass covers 32*PP neighbours (PP next-hop words) and a 12-root batch of
+// 1,781-port spines needs 12 passes instead of 56 (the host picks R, PP).
+// A "virtual batch" = (R-root batch, pass g); a round runs up to
 // NB virtual batches side by side, and virtual batch i of a round is served by
 // workgroups i, i+NB, ... so with NB a multiple of 8 its workgroups land on one
 // XCD and its state stays in that XCD's L2.
@@ -72,15 +76,15 @@ __device__ __forceinline__ void or64(uint64_t* p, uint64_t x) {
 // one (64-root batch, next-hop word) of the round, and its state arrays
 struct VB {
   uint32_t vbl, g, rix0, V;
-  uint64_t valid;  // bits of roots present
+  uint64_t valid;  // bits of roots present (R bits at most)
   uint64_t* seen;
   uint64_t* accb;
   uint64_t* P;
   __device__ VB(const MsArgs& a, uint32_t vbl_, uint32_t V_, int kp) : vbl(vbl_), V(V_) {
     const uint32_t vb = a.vb0 + vbl;
     g = vb % a.npass;
-    rix0 = (vb / a.npass) * 64u;
-    const uint32_t nv = min(64u, a.n - rix0);
+    rix0 = (vb / a.npass) * a.R;
+    const uint32_t nv = min(a.R, a.n - rix0);
     valid = nv == 64u ? ~0ull : ((1ull << nv) - 1ull);
     seen = a.seen + (size_t)vbl * V;
     accb = a.accb + (size_t)vbl * V;
@@ -155,6 +159,38 @@ __device__ __forceinline__ void load_planes(const uint64_t* P, uint32_t u, uint6
   }
 }
 
+// roots with a set bit in any of the KP packed plane words
+template <int KP>
+__device__ __forceinline__ uint64_t planes_roots(const MsArgs& a, const uint64_t* p) {
+  uint64_t z = 0;
+#pragma unroll
+  for (int k = 0; k < KP; ++k) z |= p[k];
+  uint64_t zz = z;
+  for (uint32_t j = 1; j < a.PP; ++j) zz |= z >> (j * a.R);
+  return a.PP == 1 ? zz : zz & ((1ull << a.R) - 1ull);
+}
+
+// next-hop word w (0 .. OW-1) of this pass for root r: planes 32w .. 32w+31
+// of the pass (plane li = k * PP + j sits in word k, bit j * R + r)
+template <int KP>
+__device__ __forceinline__ uint32_t pass_word(const MsArgs& a, const uint64_t* p, uint32_t r,
+                                              uint32_t w) {
+  if (a.PP == 1) return gather_word<KP>(p, r);
+  const uint32_t lo = 32u * w, hi = lo + 32u;
+  uint32_t word = 0;
+#pragma unroll
+  for (int k = 0; k < KP; ++k) {
+    const uint32_t l0 = (uint32_t)k * a.PP;
+    if (l0 + a.PP <= lo || l0 >= hi) continue;
+    const uint64_t x = p[k] >> r;
+    for (uint32_t j = 0; j < a.PP; ++j) {
+      const uint32_t li = l0 + j;
+      if (li >= lo && li < hi) word |= (uint32_t)((x >> (j * a.R)) & 1ull) << (li - lo);
+    }
+  }
+  return word;
+}
+
 // ---------------------------------------------------------------- init
 // One wave per root: level 0 (the root) and level 1 (its usable neighbours,
 // next hop = themselves). Atomics: several roots of a batch may share nodes.
@@ -162,7 +198,7 @@ template <int KP>
 __global__ void __launch_bounds__(256) msbfs_init_kernel(DevGraph g, MsArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t slot = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  const uint32_t vbl = slot / 64u, bit = slot % 64u;
+  const uint32_t vbl = slot / a.R, bit = slot % a.R;
   if (vbl >= a.nb) return;
   const VB b(a, vbl, g.V, KP);
   const uint32_t rix = b.rix0 + bit;
@@ -203,21 +239,25 @@ __global__ void __launch_bounds__(256) msbfs_init_kernel(DevGraph g, MsArgs a) {
       const uint32_t mid = (lo + hi) >> 1;
       if (g.dn[nb0 + mid] < v) lo = mid + 1; else hi = mid;
     }
-    const uint32_t k = lo - 32u * b.g;  // >= 32 (wrapped) when outside this word
+    // plane of v in this pass (>= KP * PP, wrapped, when outside it)
+    const uint32_t li = lo - 32u * a.OW * b.g;
+    const bool in = li < (uint32_t)KP * a.PP;
+    const uint32_t k = li / a.PP, pb = (li % a.PP) * a.R + bit;  // plane word, bit
+    const uint32_t kw = lo - 32u * b.g;  // unpacked (PP == 1) next-hop word bit
     or64(&b.seen[v], bm);
     if (transit(g, v)) {
       const unsigned long long old =
           atomicOr((unsigned long long*)&f1[2u * v], (unsigned long long)bm);
       if (!old) mass += g.row_ptr[v + 1] - g.row_ptr[v];  // first root to reach v
-      if (k < (uint32_t)KP) or64(&f1[2u * v + 1u], bm);
+      if (in) or64(&f1[2u * v + 1u], bm);
     }
-    if (k < (uint32_t)KP) or64(&b.P[(size_t)v * KP + k], bm);
+    if (in) or64(&b.P[(size_t)v * KP + k], 1ull << pb);
     if (a.defer) {
       // parallel links: the same byte again, same value (an OR of 2 | 2 = 2)
       lev_or(v, 2u);
     } else {
       if (a.dist && b.g == 0) a.dist[row + v] = 1u;
-      if (a.nh) a.nh[(row + v) * a.W + b.g] = (k < 32u) ? (1u << k) : 0u;
+      if (a.nh) a.nh[(row + v) * a.W + b.g] = (kw < 32u) ? (1u << kw) : 0u;
     }
     any = true;
   }
@@ -231,8 +271,8 @@ __global__ void __launch_bounds__(256) msbfs_init_kernel(DevGraph g, MsArgs a) {
 // wave (lane offset folded into beg, STEP 256); rows are padded to 4 entries
 template <int KP, uint32_t STEP>
 __device__ __forceinline__ void pull_scan(const DevGraph& g, const uint64_t* fcur, const uint64_t* P,
-                                          uint32_t beg, uint32_t end, uint64_t m, uint64_t& acc,
-                                          uint64_t* pacc) {
+                                          uint32_t beg, uint32_t end, uint64_t m, uint64_t rep,
+                                          uint64_t& acc, uint64_t* pacc) {
   const uint4* q = reinterpret_cast<const uint4*>(g.colx);
   const uint4* fr = reinterpret_cast<const uint4*>(fcur);
   for (uint32_t e = beg; e < end; e += STEP) {
@@ -249,10 +289,11 @@ __device__ __forceinline__ void pull_scan(const DevGraph& g, const uint64_t* fcu
       // roots whose tail has no plane bit in this pass add nothing to them
       const uint64_t fz = (((uint64_t)fs[i].w << 32) | fs[i].z) & f;
       if (!fz) continue;
+      const uint64_t fx = fz * rep;  // the roots' bits in every packed plane slot
       uint64_t pu[KP];
       load_planes<KP>(P, cs[i], pu);
 #pragma unroll
-      for (int k = 0; k < KP; ++k) pacc[k] |= pu[k] & fz;
+      for (int k = 0; k < KP; ++k) pacc[k] |= pu[k] & fx;
     }
   }
 }
@@ -261,7 +302,8 @@ __device__ __forceinline__ void pull_scan(const DevGraph& g, const uint64_t* fcu
 // out-edges [beg, end) of frontier node u (roots fu, planes pu)
 template <int KP, uint32_t STEP>
 __device__ __forceinline__ void push_scan(const DevGraph& g, const VB& b, uint32_t beg,
-                                          uint32_t end, uint64_t fu, const uint64_t* pu) {
+                                          uint32_t end, uint64_t fu, uint64_t rep,
+                                          const uint64_t* pu) {
   const uint4* q = reinterpret_cast<const uint4*>(g.colx);
   for (uint32_t e = beg; e < end; e += STEP) {
     const uint4 c = q[e >> 2];
@@ -275,9 +317,10 @@ __device__ __forceinline__ void push_scan(const DevGraph& g, const VB& b, uint32
       if (!f) continue;
       const uint32_t v = cs[i];
       or64(&b.accb[v], f);
+      const uint64_t fx = f * rep;
 #pragma unroll
       for (int k = 0; k < KP; ++k) {
-        const uint64_t x = pu[k] & f;
+        const uint64_t x = pu[k] & fx;
         if (x) or64(&b.P[(size_t)v * KP + k], x);
       }
     }
@@ -314,7 +357,7 @@ __global__ void __launch_bounds__(256) msbfs_level_kernel(DevGraph g, MsArgs a, 
       if (!fu) return;
       uint64_t pu[KP];
       load_planes<KP>(b.P, u, pu);
-      push_scan<KP, 4u * kWave>(g, b, beg + 4u * lane, end, fu, pu);
+      push_scan<KP, 4u * kWave>(g, b, beg + 4u * lane, end, fu, a.rep, pu);
       return;
     }
     const uint64_t m = ~b.seen[u] & b.valid;
@@ -322,14 +365,14 @@ __global__ void __launch_bounds__(256) msbfs_level_kernel(DevGraph g, MsArgs a, 
     uint64_t acc = 0, pacc[KP];
 #pragma unroll
     for (int k = 0; k < KP; ++k) pacc[k] = 0;
-    pull_scan<KP, 4u * kWave>(g, fcur, b.P, beg + 4u * lane, end, m, acc, pacc);
+    pull_scan<KP, 4u * kWave>(g, fcur, b.P, beg + 4u * lane, end, m, a.rep, acc, pacc);
     acc = wave_or64(acc);
 #pragma unroll
     for (int k = 0; k < KP; ++k) pacc[k] = wave_or64(pacc[k]);
     const bool tr = transit(g, u);
     if (lane == 0) {
       fnext[2u * u] = tr ? acc : 0ull;
-      fnext[2u * u + 1u] = tr ? planes_or<KP>(pacc) & acc : 0ull;
+      fnext[2u * u + 1u] = tr ? planes_roots<KP>(a, pacc) & acc : 0ull;
       if (acc) {
         b.seen[u] = (~m & b.valid) | acc;
 #pragma unroll
@@ -358,7 +401,7 @@ __global__ void __launch_bounds__(256) msbfs_level_kernel(DevGraph g, MsArgs a, 
     if (end - beg > kMsBigDeg) return;
     uint64_t pu[KP];
     load_planes<KP>(b.P, v, pu);
-    push_scan<KP, 4u>(g, b, beg, end, fu, pu);
+    push_scan<KP, 4u>(g, b, beg, end, fu, a.rep, pu);
     return;
   }
   uint64_t s0 = 0, m = 0;
@@ -375,7 +418,7 @@ __global__ void __launch_bounds__(256) msbfs_level_kernel(DevGraph g, MsArgs a, 
   uint64_t acc = 0, pacc[KP];
 #pragma unroll
   for (int k = 0; k < KP; ++k) pacc[k] = 0;
-  if (m && !big) pull_scan<KP, 4u>(g, fcur, b.P, beg, end, m, acc, pacc);
+  if (m && !big) pull_scan<KP, 4u>(g, fcur, b.P, beg, end, m, a.rep, acc, pacc);
   uint32_t mass = 0;
   if (v < V && !big) {
     const bool tr = acc && transit(g, v);
@@ -386,7 +429,7 @@ __global__ void __launch_bounds__(256) msbfs_level_kernel(DevGraph g, MsArgs a, 
         if (pacc[k]) b.P[(size_t)v * KP + k] |= pacc[k];
     }
     fnext[2u * v] = tr ? acc : 0ull;
-    fnext[2u * v + 1u] = tr ? planes_or<KP>(pacc) & acc : 0ull;
+    fnext[2u * v + 1u] = tr ? planes_roots<KP>(a, pacc) & acc : 0ull;
     if (tr) mass = end - beg;
   }
   emit_rows<KP>(a, b, v, acc, pacc, d + 1);
@@ -421,7 +464,7 @@ __global__ void __launch_bounds__(256) msbfs_settle_kernel(DevGraph g, MsArgs a,
       if (tr) mass = g.row_ptr[v + 1] - g.row_ptr[v];
     }
     fnext[2u * v] = tr ? acc : 0ull;
-    fnext[2u * v + 1u] = tr ? planes_or<KP>(pacc) & acc : 0ull;
+    fnext[2u * v + 1u] = tr ? planes_roots<KP>(a, pacc) & acc : 0ull;
   }
   emit_rows<KP>(a, b, v, acc, pacc, d + 1);
   mass = wave_add32(mass);
@@ -458,11 +501,13 @@ __global__ void __launch_bounds__(256) msbfs_final_kernel(DevGraph g, MsArgs a) 
 }
 
 // ---------------------------------------------------------------- rows
-// Deferred output: one workgroup writes the whole rows of 64 nodes x 64 roots.
-// lev (dist + 1) and the next-hop words (bit-planes transposed per root) are
-// staged in LDS, then stored root by root: 16 lanes x 16 B cover one root's
-// 64 consecutive dist values, so the dist rows (and nh rows when W == 1) go
-// out as whole 16-B stores; wider nh rows store word g of each node.
+// Deferred output: one workgroup writes the rows of 64 nodes x the batch's
+// roots for this pass. lev (dist + 1) and, word by word, the pass's next-hop
+// words (bit-planes transposed per root) are staged in LDS and stored root by
+// root: 16 lanes x 16 B cover one root's 64 consecutive dist values, so the
+// dist rows (and nh rows when W == 1) go out as whole 16-B stores; wider nh
+// rows store word g*OW + w of each node. The digest terms of the same values
+// are added into the roots' records (passes add up).
 template <int KP>
 __global__ void __launch_bounds__(256) msbfs_rows_kernel(DevGraph g, MsArgs a) {
   __shared__ uint8_t s_lev[64 * 64];   // [node][root]
@@ -472,108 +517,118 @@ __global__ void __launch_bounds__(256) msbfs_rows_kernel(DevGraph g, MsArgs a) {
   const VB b(a, vbl, g.V, KP);
   const uint32_t V = g.V, tid = threadIdx.x;
   const uint32_t v0 = (blockIdx.x / a.nb) * 64u, nv = min(64u, V - v0);
-  // stage lev: 64 nodes x 64 B contiguous
+  const uint32_t nr = min(a.R, a.n - b.rix0);
   {
     const uint4* src = reinterpret_cast<const uint4*>(a.lev + ((size_t)vbl * V + v0) * 64u);
     if (tid < nv * 4u) reinterpret_cast<uint4*>(s_lev)[tid] = src[tid];
   }
-  // next-hop word g of (node n, roots 16q..16q+15) from n's planes
-  {
-    const uint32_t n = tid >> 2, q = tid & 3u;
-    uint64_t p[KP];
-    if (n < nv) {
-      load_planes<KP>(b.P, v0 + n, p);
-    } else {
-#pragma unroll
-      for (int k = 0; k < KP; ++k) p[k] = 0;
-    }
-#pragma unroll 4
-    for (uint32_t i = 0; i < 16u; ++i) {
-      const uint32_t r = 16u * q + i;
-      s_nh[r * 65u + n] = gather_word<KP>(p, r);
-    }
-  }
   if (a.digest && tid < 128u) s_dk[tid] = (v0 + tid / 2u < V) ? g.dkey[2ull * v0 + tid] : 0ull;
-  __syncthreads();
-  const uint32_t nr = min(64u, a.n - b.rix0);
+  // node n = tid / 4 computes the words of roots 16q .. 16q+15 (q = tid % 4)
+  const uint32_t pn = tid >> 2, pq = tid & 3u;
+  uint64_t p[KP];
+  if (pn < nv) {
+    load_planes<KP>(b.P, v0 + pn, p);
+  } else {
+#pragma unroll
+    for (int k = 0; k < KP; ++k) p[k] = 0;
+  }
+  // digest: root dr = tid / 4 over nodes 16 * (tid % 4) .. + 15
+  const uint32_t dr = tid >> 2, dn0 = 16u * (tid & 3u);
+  uint64_t reached = 0, sumd = 0, h = 0;
   const bool vec = (V & 3u) == 0 && nv == 64u;
-  if (a.digest) {
-    // root r = tid / 4 over nodes 16 * (tid % 4) .. + 15; the 4 lanes of a
-    // root then add up and one of them adds into the record (passes add up)
-    const uint32_t r = tid >> 2, n0 = 16u * (tid & 3u);
-    uint64_t reached = 0, sumd = 0, h = 0;
-    if (r < nr) {
-      for (uint32_t n = n0; n < n0 + 16u && n < nv; ++n) {
-        const uint32_t l = s_lev[n * 64u + r];
+  __syncthreads();
+  if (b.g == 0) {
+    if (a.digest && dr < nr) {
+      for (uint32_t n = dn0; n < dn0 + 16u && n < nv; ++n) {
+        const uint32_t l = s_lev[n * 64u + dr];
         if (!l) continue;
-        if (b.g == 0) {
-          reached += 1;
-          sumd += l - 1u;
-          h += s_dk[2u * n] * (uint64_t)l;
-        }
-        const uint32_t word = s_nh[r * 65u + n];
-        if (word) h += s_dk[2u * n + 1u] * digest_word_key(b.g, word);
+        reached += 1;
+        sumd += l - 1u;
+        h += s_dk[2u * n] * (uint64_t)l;
       }
     }
+    if (a.dist) {
+      for (uint32_t i = tid; i < 64u * 16u; i += kBlock) {  // (root, node quad)
+        const uint32_t r = i >> 4, q = i & 15u;
+        if (r >= nr) break;
+        uint32_t dv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t l = s_lev[(4u * q + j) * 64u + r];
+          dv[j] = l ? l - 1u : kInf;
+        }
+        uint32_t* row = a.dist + (size_t)(b.rix0 + r) * V + v0 + 4u * q;
+        if (vec) {
+          *reinterpret_cast<uint4*>(row) = make_uint4(dv[0], dv[1], dv[2], dv[3]);
+        } else {
+          for (uint32_t j = 0; j < 4u; ++j)
+            if (4u * q + j < nv) row[j] = dv[j];
+        }
+      }
+    }
+  }
+  for (uint32_t w = 0; w < a.OW; ++w) {
+    const uint32_t wg = b.g * a.OW + w;  // next-hop word of the output row
+    if (wg >= a.W) break;
+    for (uint32_t i = 0; i < 16u; ++i) {
+      const uint32_t r = 16u * pq + i;
+      if (r < nr) s_nh[r * 65u + pn] = pass_word<KP>(a, p, r, w);
+    }
+    __syncthreads();
+    if (a.digest && dr < nr) {
+      for (uint32_t n = dn0; n < dn0 + 16u && n < nv; ++n) {
+        const uint32_t word = s_nh[dr * 65u + n];
+        if (word && s_lev[n * 64u + dr]) h += s_dk[2u * n + 1u] * digest_word_key(wg, word);
+      }
+    }
+    if (a.nh) {
+      if (a.W == 1) {
+        for (uint32_t i = tid; i < 64u * 16u; i += kBlock) {
+          const uint32_t r = i >> 4, q = i & 15u;
+          if (r >= nr) break;
+          const uint32_t* src = &s_nh[r * 65u + 4u * q];
+          uint32_t* row = a.nh + (size_t)(b.rix0 + r) * V + v0 + 4u * q;
+          if (vec) {
+            *reinterpret_cast<uint4*>(row) = make_uint4(src[0], src[1], src[2], src[3]);
+          } else {
+            for (uint32_t j = 0; j < 4u; ++j)
+              if (4u * q + j < nv) row[j] = src[j];
+          }
+        }
+      } else {
+        for (uint32_t i = tid; i < 64u * 64u; i += kBlock) {  // (root, node)
+          const uint32_t r = i >> 6, n = i & 63u;
+          if (r >= nr) break;
+          if (n < nv) a.nh[((size_t)(b.rix0 + r) * V + v0 + n) * a.W + wg] = s_nh[r * 65u + n];
+        }
+      }
+    }
+    __syncthreads();  // s_nh is rewritten for the next word
+  }
+  // words past the computed passes are zero for every node
+  if (a.nh && b.g == a.npass - 1 && a.npass * a.OW < a.W) {
+    for (uint32_t i = tid; i < 64u * 64u; i += kBlock) {
+      const uint32_t r = i >> 6, n = i & 63u;
+      if (r >= nr) break;
+      if (n >= nv) continue;
+      uint32_t* row = a.nh + ((size_t)(b.rix0 + r) * V + v0 + n) * a.W;
+      for (uint32_t k = a.npass * a.OW; k < a.W; ++k) row[k] = 0u;
+    }
+  }
+  if (a.digest) {
 #pragma unroll
     for (int o = 1; o < 4; o <<= 1) {
       reached += shfl_xor64(reached, o);
       sumd += shfl_xor64(sumd, o);
       h += shfl_xor64(h, o);
     }
-    if ((tid & 3u) == 0 && r < nr) {
-      ospf_digest* dg = a.digest + b.rix0 + r;
+    if ((tid & 3u) == 0 && dr < nr) {
+      ospf_digest* dg = a.digest + b.rix0 + dr;
       if (reached) {
         atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)reached);
         atomicAdd((unsigned long long*)&dg->sum_dist, (unsigned long long)sumd);
       }
       if (h) atomicAdd((unsigned long long*)&dg->hash, (unsigned long long)h);
-    }
-  }
-  if (a.dist && b.g == 0) {
-    for (uint32_t i = tid; i < 64u * 16u; i += kBlock) {  // (root, node quad)
-      const uint32_t r = i >> 4, q = i & 15u;
-      if (r >= nr) break;
-      uint32_t dv[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t l = s_lev[(4u * q + j) * 64u + r];
-        dv[j] = l ? l - 1u : kInf;
-      }
-      uint32_t* row = a.dist + (size_t)(b.rix0 + r) * V + v0 + 4u * q;
-      if (vec) {
-        *reinterpret_cast<uint4*>(row) = make_uint4(dv[0], dv[1], dv[2], dv[3]);
-      } else {
-        for (uint32_t j = 0; j < 4u; ++j)
-          if (4u * q + j < nv) row[j] = dv[j];
-      }
-    }
-  }
-  if (a.nh) {
-    if (a.W == 1) {
-      for (uint32_t i = tid; i < 64u * 16u; i += kBlock) {
-        const uint32_t r = i >> 4, q = i & 15u;
-        if (r >= nr) break;
-        const uint32_t* src = &s_nh[r * 65u + 4u * q];
-        uint32_t* row = a.nh + (size_t)(b.rix0 + r) * V + v0 + 4u * q;
-        if (vec) {
-          *reinterpret_cast<uint4*>(row) = make_uint4(src[0], src[1], src[2], src[3]);
-        } else {
-          for (uint32_t j = 0; j < 4u; ++j)
-            if (4u * q + j < nv) row[j] = src[j];
-        }
-      }
-    } else {
-      const bool last = b.g == a.npass - 1 && a.npass < a.W;
-      for (uint32_t i = tid; i < 64u * 64u; i += kBlock) {  // (root, node)
-        const uint32_t r = i >> 6, n = i & 63u;
-        if (r >= nr) break;
-        if (n >= nv) continue;
-        uint32_t* p = a.nh + ((size_t)(b.rix0 + r) * V + v0 + n) * a.W;
-        p[b.g] = s_nh[r * 65u + n];
-        if (last)  // words past the computed passes
-          for (uint32_t k = a.npass; k < a.W; ++k) p[k] = 0u;
-      }
     }
   }
 }
@@ -647,7 +702,7 @@ __global__ void __launch_bounds__(256) row_digest_kernel(DevGraph g, const uint3
 template <int KP>
 hipError_t launch_round_kp(const DevGraph& g, const MsArgs& a, uint32_t depth_bound,
                            hipStream_t s) {
-  const uint32_t init_blocks = (a.nb * 64u + kWavesPerBlock - 1) / kWavesPerBlock;
+  const uint32_t init_blocks = (a.nb * a.R + kWavesPerBlock - 1) / kWavesPerBlock;
   hipLaunchKernelGGL(msbfs_init_kernel<KP>, dim3(init_blocks), dim3(kBlock), 0, s, g, a);
   const uint32_t chunks = (g.V + kBlock - 1) / kBlock;
   const uint32_t bigblocks = (g.nbig + kWavesPerBlock - 1) / kWavesPerBlock;

@@ -41,13 +41,37 @@ def distinct_neighbors(row_ptr: np.ndarray, col: np.ndarray) -> np.ndarray:
     return np.bincount(owner[new], minlength=V) if col.size else np.zeros(V, np.int64)
 
 
-def make_classes(perm: np.ndarray, words: np.ndarray, batch: int) -> List[RootClass]:
+def first_neighbor(row_ptr: np.ndarray, col: np.ndarray) -> np.ndarray:
+    """Smallest neighbour id per node (V for an isolated node)."""
+    V = row_ptr.size - 1
+    deg = np.diff(row_ptr.astype(np.int64))
+    owner = np.repeat(np.arange(V), deg)
+    key = np.full(V, V, np.int64)
+    ok = col != owner
+    np.minimum.at(key, owner[ok], col[ok].astype(np.int64))
+    return key
+
+
+def locality_order(roots: np.ndarray, key: np.ndarray) -> np.ndarray:
+    """Roots grouped by their smallest neighbour (stable): roots hanging off
+    the same hub share frontiers and next-hop planes in a multi-source batch,
+    so one 64-root traversal does more useful work per edge it scans. Any
+    order is valid for an all-sources sweep; this one is topology-agnostic."""
+    return roots[np.argsort(key[roots], kind="stable")]
+
+
+def make_classes(perm: np.ndarray, words: np.ndarray, batch: int,
+                 key: np.ndarray = None, max_grouped_words: int = None) -> List[RootClass]:
     """Split a root permutation into width classes; each class's share of a
-    `batch`-root step is proportional to its size (at least 1)."""
+    `batch`-root step is proportional to its size (at least 1). With `key`
+    (first_neighbor) the sweep of each class with at most `max_grouped_words`
+    next-hop words (all classes when None) is locality-ordered."""
     V = perm.size
     out = []
     for W in sorted(set(words[perm].tolist())):
         members = perm[words[perm] == W]
+        if key is not None and (max_grouped_words is None or W <= max_grouped_words):
+            members = locality_order(members, key)
         share = max(1, int(round(batch * members.size / V)))
         out.append(RootClass(int(W), members.astype(np.uint32), share))
     return out

@@ -24,6 +24,8 @@ ap.add_argument("--W", type=int, nargs="+", default=[1, 3, 56])
 ap.add_argument("--n", type=int, nargs="+", default=[256, 1024, 4096])
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--blocks", type=int, nargs="+", default=[0])
+ap.add_argument("--order", choices=["auto", "random", "locality"], default="auto",
+                help="auto = locality for single-word classes (as bench.py)")
 args = ap.parse_args()
 
 torch.cuda.set_device(0)
@@ -40,6 +42,8 @@ flags = N.OSPF_WANT_DIST | N.OSPF_WANT_NH | N.OSPF_WANT_DIGEST
 s = torch.cuda.current_stream()
 for W in args.W:
     members = perm[words[perm] == W]
+    if args.order == "locality" or (args.order == "auto" and W == 1):
+        members = shard.locality_order(members, shard.first_neighbor(csr["row_ptr"], csr["col"]))
     if members.size == 0:
         continue
     for n in args.n:

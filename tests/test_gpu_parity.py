@@ -288,12 +288,17 @@ def test_msbfs_matches_per_root_bfs(seed, hop, defer, monkeypatch):
                                                  not hop, threads=8))
 
 
-@pytest.mark.parametrize("nb", ["1", "3", "8"])
-def test_msbfs_wide_roots_and_rounds(nb, monkeypatch):
+@pytest.mark.parametrize("nb,R", [("1", None), ("3", None), ("8", None), ("32", "3"),
+                                  ("4", "7"), ("32", "20"), ("2", "1")])
+def test_msbfs_wide_roots_and_rounds(nb, R, monkeypatch):
     """Spines with 140 distinct neighbours need 5 next-hop words = 5 passes
-    per batch; OSPF_MS_NB bounds the (batch, word) pairs per round so the
-    sweep spans several rounds; nh_words above the need is zero-filled."""
+    per 64-root batch; OSPF_MS_NB bounds the (batch, pass) pairs per round so
+    the sweep spans several rounds; nh_words above the need is zero-filled.
+    OSPF_MS_R packs the bit-planes: R roots per batch, 64/R planes per word,
+    64/R next-hop words per pass."""
     monkeypatch.setenv("OSPF_MS_NB", nb)
+    if R:
+        monkeypatch.setenv("OSPF_MS_R", R)
     st = T.fabric(pods=140, planes=2)
     p, eng = _engine_for(st)
     names = p.node_names()
