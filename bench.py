@@ -64,18 +64,21 @@ def bytes_per_root(V: int, E: int, W: int) -> int:
     return 8 * E + 4 * (V + 1) + 4 * V + 4 * V * W
 
 
-def pmc_traffic(profile_dir: str, key: str):
-    """Per-launch HBM bytes of the kernel `key` from the committed rocprofv3
-    --pmc summary (profiles/<round>/pmc_traffic.json, written by
-    scripts/pmc_traffic.py: FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE)."""
+def pmc_traffic(profile_dir: str, key: str, roots: int):
+    """Measured HBM bytes per launch of the class `key` with `roots` roots from
+    the committed per-class rocprofv3 --pmc summary (profiles/<round>/
+    pmc_traffic.json, written by scripts/pmc_class_traffic.py: FETCH_SIZE x 2
+    (gfx950 correction) + WRITE_SIZE, summed over the class's kernels); None
+    when absent or measured at another batch size."""
     path = os.path.join(profile_dir, "pmc_traffic.json")
     if not os.path.exists(path):
         return None
     try:
         with open(path) as f:
-            return json.load(f).get(key, {}).get("hbm_bytes_per_launch")
+            e = json.load(f).get(key, {})
     except (OSError, ValueError):
         return None
+    return e.get("hbm_bytes_per_launch") if e.get("roots_per_launch") == roots else None
 
 
 def main():
@@ -83,7 +86,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=4096, help="roots per GPU per step")
+    ap.add_argument("--batch", type=int, default=16384,
+                    help="roots per GPU per step (6 steps sweep all 100k sources of F100k)")
     ap.add_argument("--topology", default="fabric100k")
     ap.add_argument("--cpu-sample", type=int, default=32)
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -96,6 +100,8 @@ def main():
                          "auto = grouped for single-word classes only (measured: grouping "
                          "wide roots makes their per-pass next-hop planes denser and slower)")
     ap.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles", "r01"))
+    ap.add_argument("--iso-reps", type=int, default=3,
+                    help="isolated launches per class for the roofline (after the timed steps)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -202,29 +208,65 @@ def main():
     spf_s = roots_total / dt
     gteps = roots_total * E / dt / 1e9
 
-    # roofline of the dominant kernel (largest total device time), from the
-    # HIP events bracketing its launches on its own stream
+    # roofline. The classes overlap on their streams inside the timed steps,
+    # so each class is then timed ALONE (not part of `value`): R launches on
+    # one stream bracketed by HIP events on that stream. The dominant class is
+    # the one with the largest share of a step's device time. A multi-source
+    # class launch is a sequence of kernels (init, level/settle pairs, rows);
+    # its events bracket the whole sequence, and profiles/<round>/ holds the
+    # rocprofv3 per-kernel summary whose per-class sums it matches.
+    iso_s = torch.cuda.Stream(device=dev)
     for c in classes:
-        c.extra["ms"] = [a.elapsed_time(b) for a, b in c.extra["ev"]]
-    dom = max(classes, key=lambda c: sum(c.extra["ms"]))
-    avg_ms = float(np.mean(dom.extra["ms"]))
-    alg = dom.per_step * bytes_per_root(V, E, dom.nh_words)
-    achieved = alg / (avg_ms / 1e3) / 1e9
+        x = c.extra
+        ms = []
+        with torch.cuda.stream(iso_s):
+            for _ in range(args.iso_reps + 1):
+                a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a_.record(iso_s)
+                eng.run_dev(x["roots"].data_ptr(), c.per_step, c.nh_words, flags=flags,
+                            d_dist=x["dist"].data_ptr(),
+                            d_nh=x["nh"].data_ptr() if x["nh"] is not None else 0,
+                            d_digest=x["dig"].data_ptr(), stream=iso_s.cuda_stream,
+                            max_root_neighbors=x["max_nbrs"])
+                b_.record(iso_s)
+                b_.synchronize()
+                ms.append(a_.elapsed_time(b_))
+        x["iso_ms"] = float(np.median(ms[1:]))
+        x["ms"] = [a_.elapsed_time(b_) for a_, b_ in x["ev"]]
+    eng.sync(iso_s.cuda_stream)
+
+    def class_roofline(c):
+        x, p = c.extra, c.extra["plan"]
+        alg = c.per_step * bytes_per_root(V, E, c.nh_words)
+        ach = alg / (x["iso_ms"] / 1e3) / 1e9
+        tr = pmc_traffic(args.profile_dir, f"variant{p['variant']}_W{c.nh_words}", c.per_step)
+        return {"nh_words": c.nh_words, "roots_per_launch": c.per_step,
+                "isolated_launch_ms": round(x["iso_ms"], 3),
+                "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                "traffic": tr,
+                "traffic_GBs": round(tr / (x["iso_ms"] / 1e3) / 1e9, 1) if tr else None}
+
+    dom = max(classes, key=lambda c: c.extra["iso_ms"])
+    dr = class_roofline(dom)
     p = dom.extra["plan"]
-    key = f"variant{p['variant']}_W{dom.nh_words}"
-    traffic = pmc_traffic(args.profile_dir, key)
     roofline = {
-        "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-        "kernel": (f"msbfs_level_kernel + init/final/row_digest (variant 5, nh_words "
-                   f"{dom.nh_words}; one 'launch' = the class's kernel sequence)")
+        "bound": "hbm", "achieved": dr["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": dr["frac"], "traffic": dr["traffic"],
+        "kernel": (f"multi-source BFS class launch (variant 5, nh_words {dom.nh_words}: "
+                   f"msbfs init + level/settle pairs + rows kernels)")
         if p["variant"] == 5 else
         f"spf_bfs_kernel (variant {p['variant']}, nh_words {dom.nh_words})"
         if p["variant"] >= 3 else f"spf_run_kernel (variant {p['variant']})",
-        "grid": dom.per_step * p["slices"], "block": p["block"], "lds_bytes": p["lds_bytes"],
-        "roots_per_launch": dom.per_step, "bytes_per_root": bytes_per_root(V, E, dom.nh_words),
-        "avg_launch_ms": round(avg_ms, 3),
-        "edges_per_s_per_launch": round(dom.per_step * E / (avg_ms / 1e3), 1),
+        "block": p["block"], "roots_per_launch": dom.per_step,
+        "bytes_per_root": bytes_per_root(V, E, dom.nh_words),
+        "avg_launch_ms": dr["isolated_launch_ms"],
+        "traffic_GBs": dr["traffic_GBs"],
+        "edges_per_s_per_launch": round(dom.per_step * E / (dom.extra["iso_ms"] / 1e3), 1),
+        "classes": [class_roofline(c) for c in classes],
+        "note": "achieved = roots x SURVEY 8(d) bytes_root (8E + 8V + 4VW: every root scanning "
+                "the CSR) / isolated launch time; 64 roots share each CSR scan, so achieved "
+                "can exceed the HBM peak; traffic = measured HBM bytes per launch (rocprofv3 "
+                "FETCH_SIZE x2 + WRITE_SIZE, profiles/<round>/pmc_traffic.json)",
     }
 
     cpu = parity = None
@@ -259,7 +301,8 @@ def main():
                 "root_classes": [{"nh_words": c.nh_words, "roots_per_step": c.per_step,
                                   **{k: c.extra["plan"][k] for k in ("variant", "slices",
                                                                      "block")},
-                                  "avg_launch_ms": round(float(np.mean(c.extra["ms"])), 3)}
+                                  "avg_launch_ms": round(float(np.mean(c.extra["ms"])), 3),
+                                  "isolated_launch_ms": round(c.extra["iso_ms"], 3)}
                                  for c in classes],
                 "parallelism": f"root-sharded x{world}" +
                                (", RCCL all_gather of 24-B digests" if dist_on else "")},
