@@ -13,6 +13,7 @@
  *   getKthPaths              LinkState.cpp:790-819 -> odl_kth_paths_text
  *   getMetricFromAToB        LinkState.cpp:777-788 -> odl_metric_a_to_b
  *   decision.spf_runs        LinkState.cpp:843     -> odl_spf_runs
+ *   resolveUcmpWeights       LinkState.cpp:913-1033 -> odl_ucmp_text
  * plus batched entry points the reference lacks (all-sources digests, KSP2
  * masked reruns for many destinations, per-neighbour reruns).
  *
@@ -74,6 +75,14 @@ char* odl_ksp2_text(odl_ls* ls, const char* src, const char* dsts_nl, uint32_t n
  * mpls-op (0 none, 1 PHP, 2 SWAP, 3 PUSH) \t labels (',' separated). */
 char* odl_route_text(odl_ls* ls, const char* me, const char* announcers_nl, uint32_t n,
                      int algo);
+
+/* LinkState::resolveUcmpWeights (LinkState.cpp:913-1033) over
+ * getSpfResult(root): leaves_nl = n lines "name\tweight"; algo 2 =
+ * SP_UCMP_ADJ_WEIGHT_PROPAGATION, 3 = SP_UCMP_PREFIX_WEIGHT_PROPAGATION.
+ * Text: one line per node of the result, sorted by name:
+ *   node \t advertised weight \t iface=nextHopNode:weight,... (sorted by iface) */
+char* odl_ucmp_text(odl_ls* ls, const char* root, const char* leaves_nl, uint32_t n, int algo,
+                    int use_link_metric);
 
 /* CSR snapshot the engine sees (node ids = rank of name, byte order).
  * Copies into caller arrays sized by odl_csr_size(); any pointer may be NULL. */

@@ -5,6 +5,7 @@
 #include <cstring>
 #include <sstream>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../../include/openr_decision.h"
@@ -225,6 +226,39 @@ char* odl_route_text(odl_ls* h, const char* me, const char* announcers_nl, uint3
     for (const auto& x : nhs) {
       os << x.ifName << '\t' << x.neighbor << '\t' << x.metric << '\t' << (int)x.op << '\t';
       for (size_t i = 0; i < x.labels.size(); ++i) os << (i ? "," : "") << x.labels[i];
+      os << '\n';
+    }
+    return dup(os.str());
+  }, (char*)nullptr);
+}
+
+char* odl_ucmp_text(odl_ls* h, const char* root, const char* leaves_nl, uint32_t n, int algo,
+                    int use_link_metric) {
+  return guard(h, [&]() -> char* {
+    if (algo != 2 && algo != 3) throw std::invalid_argument("algo must be 2 or 3");
+    std::unordered_map<std::string, int64_t> leaves;
+    for (const auto& ln : splitNl(leaves_nl, n)) {
+      const size_t t = ln.find('\t');
+      if (t == std::string::npos) throw std::invalid_argument("leaf line needs name\tweight");
+      leaves.emplace(ln.substr(0, t), std::stoll(ln.substr(t + 1)));
+    }
+    const bool um = use_link_metric != 0;
+    const auto res = h->ls.resolveUcmpWeights(h->ls.getSpfResult(root, um), leaves,
+                                              (odl::UcmpAlgo)algo, um);
+    std::vector<std::string> names;
+    for (const auto& kv : res) names.push_back(kv.first);
+    std::sort(names.begin(), names.end());
+    std::ostringstream os;
+    for (const auto& nm : names) {
+      const auto& u = res.at(nm);
+      os << nm << '\t' << (u.weight() ? *u.weight() : 0) << '\t';
+      std::vector<std::string> ifs;
+      for (const auto& kv : u.nextHopLinks()) ifs.push_back(kv.first);
+      std::sort(ifs.begin(), ifs.end());
+      for (size_t i = 0; i < ifs.size(); ++i) {
+        const auto& hop = u.nextHopLinks().at(ifs[i]);
+        os << (i ? "," : "") << ifs[i] << '=' << hop.nextHopNode << ':' << hop.weight;
+      }
       os << '\n';
     }
     return dup(os.str());

@@ -1,6 +1,8 @@
 // link_state.cpp — LinkState mirror (see link_state.h); SPF on the engine.
 #include "link_state.h"
 
+#include <numeric>
+#include <set>
 #include <algorithm>
 #include <functional>
 #include <stdexcept>
@@ -684,6 +686,76 @@ void LinkState::prefetchKsp2(const std::string& src, const std::vector<std::stri
       memoKsp_.emplace(kspKey(src, d, 2), std::move(paths));
     }
   }
+}
+
+void NodeUcmpResult::normalizeNextHopWeights() {
+  int64_t g = 0;
+  for (const auto& kv : nextHopLinks_) g = std::gcd(g, kv.second.weight);
+  if (g > 1)
+    for (auto& kv : nextHopLinks_) kv.second.weight /= g;
+}
+
+UcmpResult LinkState::resolveUcmpWeights(
+    const SpfResult& spfGraph, const std::unordered_map<std::string, int64_t>& leafNodeToWeights,
+    UcmpAlgo algo, bool useLinkMetric) const {
+  UcmpResult out;
+  // DijkstraQ<DijkstraQUcmpNode> (LinkState.h:573-645): entries still queued,
+  // by name; pop order (metric, name). A popped node leaves the map, so a later
+  // path link to it queues it again, as in the reference.
+  struct Item {
+    Metric metric;
+    NodeUcmpResult result;
+  };
+  std::unordered_map<std::string, Item> queued;
+  std::set<std::pair<Metric, std::string>> order;
+  auto insert = [&](const std::string& n, Metric m) {
+    queued[n] = Item{m, NodeUcmpResult{}};
+    order.emplace(m, n);
+  };
+  // leaves present in the SPF graph, all at the same distance from the root
+  // (LinkState.cpp:937-959)
+  std::optional<Metric> spfMetric;
+  for (const auto& [leaf, weight] : leafNodeToWeights) {
+    auto it = spfGraph.find(leaf);
+    if (it == spfGraph.end()) continue;
+    const Metric m = it->second.metric();
+    if (!spfMetric) {
+      spfMetric = m;
+    } else if (*spfMetric != m) {
+      return UcmpResult{};  // "Skipping resolveUcmpWeights"
+    }
+    insert(leaf, 0);
+    queued.at(leaf).result.setWeight(weight);
+  }
+  // walk from the leaves towards the root (LinkState.cpp:961-1023)
+  while (!order.empty()) {
+    const auto [metric, name] = *order.begin();
+    order.erase(order.begin());
+    NodeUcmpResult cur = std::move(queued.at(name).result);
+    queued.erase(name);
+    if (!cur.weight()) {
+      int64_t advertised = 0;
+      for (const auto& [iface, nh] : cur.nextHopLinks())
+        advertised += algo == UcmpAlgo::kAdjWeightPropagation ? nh.link->weightFrom(name)
+                                                              : nh.weight;
+      cur.setWeight(advertised);
+    }
+    auto sit = spfGraph.find(name);
+    if (sit == spfGraph.end()) throw std::logic_error("UCMP node not in the SPF graph");
+    for (const auto& pl : sit->second.pathLinks()) {
+      const Metric lm = useLinkMetric ? pl.link->metricFrom(pl.prevNode) : 1;
+      auto q = queued.find(pl.prevNode);
+      if (q == queued.end()) {
+        insert(pl.prevNode, metric + lm);
+        q = queued.find(pl.prevNode);
+      }
+      q->second.result.addNextHopLink(pl.link->ifaceFrom(pl.prevNode), pl.link, name,
+                                      *cur.weight());
+    }
+    cur.normalizeNextHopWeights();
+    out.emplace(name, std::move(cur));
+  }
+  return out;
 }
 
 bool LinkState::pathAInPathB(const Path& a, const Path& b) {

@@ -121,6 +121,34 @@ class NodeSpfResult {
 using SpfResult = std::unordered_map<std::string, NodeSpfResult>;
 using Path = std::vector<LinkPtr>;
 
+// thrift::PrefixForwardingAlgorithm values of the two UCMP algorithms
+enum class UcmpAlgo : int { kAdjWeightPropagation = 2, kPrefixWeightPropagation = 3 };
+
+// LinkState::NodeUcmpResult (LinkState.h:275-333)
+class NodeUcmpResult {
+ public:
+  struct NextHopLink {
+    LinkPtr link;
+    std::string nextHopNode;
+    int64_t weight = 0;
+  };
+  const std::unordered_map<std::string, NextHopLink>& nextHopLinks() const {
+    return nextHopLinks_;
+  }
+  std::optional<int64_t> weight() const { return weight_; }
+  void setWeight(int64_t w) { weight_ = w; }
+  void addNextHopLink(const std::string& localIface, const LinkPtr& link,
+                      const std::string& nextHopNode, int64_t weight) {
+    nextHopLinks_.emplace(localIface, NextHopLink{link, nextHopNode, weight});
+  }
+  void normalizeNextHopWeights();
+
+ private:
+  std::unordered_map<std::string, NextHopLink> nextHopLinks_;
+  std::optional<int64_t> weight_;
+};
+using UcmpResult = std::unordered_map<std::string, NodeUcmpResult>;
+
 struct LinkStateChange {
   bool topologyChanged = false;
   bool linkAttributesChanged = false;
@@ -158,6 +186,11 @@ class LinkState {
                                           bool useLinkMetric = true);
   const std::vector<Path>& getKthPaths(const std::string& src, const std::string& dst, size_t k);
   static bool pathAInPathB(const Path& a, const Path& b);
+  // LinkState::resolveUcmpWeights (LinkState.cpp:913-1033): host walk of the
+  // SPF DAG (computed on the engine) from equally distant weighted leaves.
+  UcmpResult resolveUcmpWeights(const SpfResult& spfGraph,
+                                const std::unordered_map<std::string, int64_t>& leafNodeToWeights,
+                                UcmpAlgo algo, bool useLinkMetric = true) const;
 
   // ---- batched entry points (no reference counterpart) ----
   void prefetchSpf(const std::vector<std::string>& roots, bool useLinkMetric);

@@ -20,6 +20,23 @@ class LinkStateError(RuntimeError):
     pass
 
 
+def parse_ucmp_text(t: str) -> Dict[str, Tuple[int, Dict[str, Tuple[str, int]]]]:
+    """odl/orc UCMP text -> {node: (advertised weight, {iface: (next hop, weight)})}."""
+    out = {}
+    for ln in t.splitlines():
+        node, w, hops = ln.split("\t")
+        hp = {}
+        for h in filter(None, hops.split(",")):
+            iface, rest = h.split("=", 1)
+            nh, hw = rest.rsplit(":", 1)
+            hp[iface] = (nh, int(hw))
+        out[node] = (int(w), hp)
+    return out
+
+
+UCMP_ALGOS = {"adj": 2, "prefix": 3}  # SP_UCMP_{ADJ,PREFIX}_WEIGHT_PROPAGATION
+
+
 def _parse_spf(t: str) -> Dict[str, Tuple[int, tuple, tuple]]:
     out = {}
     for ln in t.splitlines():
@@ -99,6 +116,16 @@ class LinkState:
             ifn, nbr, metric, op, labels = ln.split("\t")
             out.add((ifn, int(metric), tuple(int(x) for x in labels.split(",") if x)))
         return out or None
+
+    def ucmp(self, root: str, leaves: Dict[str, int], algo: str = "adj",
+             use_link_metric: bool = True):
+        """resolveUcmpWeights(getSpfResult(root), leaves, algo) (C++ over the
+        GPU SPF result) -> {node: (weight, {iface: (next hop, weight)})}."""
+        items = "\n".join(f"{k}\t{v}" for k, v in leaves.items())
+        t = self._take(self._L.odl_ucmp_text(self._h, root.encode(), items.encode(),
+                                             len(leaves), UCMP_ALGOS[algo],
+                                             int(use_link_metric)))
+        return parse_ucmp_text(t)
 
     def links(self, node: str):
         out = []

@@ -37,12 +37,14 @@ def lib():
         L.orc_destroy.argtypes = [vp]
         L.orc_free.argtypes = [vp]
         L.orc_apply.argtypes = [vp, vp, u32, u32, vp]
-        for f in ("orc_spf_text", "orc_kth_paths_text", "orc_links_text", "orc_ksp2_text"):
+        for f in ("orc_spf_text", "orc_kth_paths_text", "orc_links_text", "orc_ksp2_text",
+                  "orc_ucmp_text"):
             getattr(L, f).restype = C.POINTER(C.c_char)
         L.orc_spf_text.argtypes = [vp, cp, i32]
         L.orc_kth_paths_text.argtypes = [vp, cp, cp, i32]
         L.orc_links_text.argtypes = [vp, cp]
         L.orc_ksp2_text.argtypes = [vp, cp, cp, u32]
+        L.orc_ucmp_text.argtypes = [vp, cp, cp, u32, i32, i32]
         L.orc_metric_a_to_b.argtypes = [vp, cp, cp, i32]
         L.orc_metric_a_to_b.restype = C.c_int64
         L.orc_spf_runs.argtypes = [vp]
@@ -103,6 +105,14 @@ class Oracle:
     def ksp2_text(self, src: str, dsts: Sequence[str]) -> str:
         return _take(lib().orc_ksp2_text(self._h, src.encode(),
                                          "\n".join(dsts).encode(), len(dsts)))
+
+    def ucmp(self, root: str, leaves, algo: str = "adj", use_link_metric: bool = True):
+        """resolveUcmpWeights restated -> {node: (weight, {iface: (next hop, weight)})}."""
+        from openr_amd.linkstate import UCMP_ALGOS, parse_ucmp_text  # text format only
+        items = "\n".join(f"{k}\t{v}" for k, v in leaves.items())
+        return parse_ucmp_text(_take(lib().orc_ucmp_text(
+            self._h, root.encode(), items.encode(), len(leaves), UCMP_ALGOS[algo],
+            int(use_link_metric))))
 
     def links_text(self, node: str) -> str:
         return _take(lib().orc_links_text(self._h, node.encode()))

@@ -21,6 +21,8 @@
 //   * getSpfResult / memo        LinkState.cpp:821-831
 //   * getKthPaths/traceOnePath   LinkState.cpp:418-439, 790-819
 //   * getMetricFromAToB          LinkState.cpp:777-788
+//   * resolveUcmpWeights         LinkState.cpp:913-1033 (+ NodeUcmpResult,
+//                                LinkState.h:275-333; DijkstraQUcmpNode :573-586)
 // It keeps the reference's data-structure style (string keys, hash sets of
 // shared_ptr<Link>, heap + reMake) on purpose: that cost shape is what the
 // bench's cpu_baseline measures.
@@ -47,6 +49,8 @@
 #include <thread>
 #include <tuple>
 #include <map>
+#include <numeric>
+#include <set>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -107,6 +111,11 @@ struct Edge {  // one undirected Link of the reference
   const std::string& ifFrom(const std::string& n) const {
     if (nA == n) return ifA;
     if (nB == n) return ifB;
+    throw std::invalid_argument(n);
+  }
+  int64_t weightFrom(const std::string& n) const {  // Link::getWeightFromNode
+    if (nA == n) return wA;
+    if (nB == n) return wB;
     throw std::invalid_argument(n);
   }
   bool sameAs(const Edge& o) const {
@@ -461,6 +470,78 @@ class Graph {
 };
 
 // ---------------------------------------------------------------------------
+// resolveUcmpWeights (LinkState.cpp:913-1033): walk the SPF DAG from equally
+// distant weighted leaves towards the root in (metric, name) order; a node's
+// advertised weight is the sum over its next-hop links of the link weight
+// (ADJ propagation, algo 2) or of the next hop's advertised weight (PREFIX
+// propagation, algo 3); next-hop weights are then divided by their gcd.
+struct UcmpHop {
+  EdgeP link;
+  std::string nextHopNode;
+  int64_t weight;
+};
+struct NodeUcmp {
+  std::optional<int64_t> weight;
+  std::unordered_map<std::string, UcmpHop> hops;  // local interface -> hop
+};
+using UcmpResult = std::unordered_map<std::string, NodeUcmp>;
+
+static UcmpResult resolveUcmp(const SpfResult& spf,
+                              const std::vector<std::pair<std::string, int64_t>>& leaves,
+                              int algo, bool useMetric) {
+  UcmpResult out;
+  // DijkstraQ<DijkstraQUcmpNode>: live entries by name, pop order (metric, name)
+  struct Item {
+    Metric metric;
+    NodeUcmp res;
+  };
+  std::unordered_map<std::string, Item> live;
+  std::set<std::pair<Metric, std::string>> order;
+  auto insert = [&](const std::string& n, Metric m) {
+    live[n] = Item{m, NodeUcmp{}};
+    order.emplace(m, n);
+  };
+  std::optional<Metric> spfMetric;
+  for (const auto& [leaf, w] : leaves) {
+    auto it = spf.find(leaf);
+    if (it == spf.end()) continue;
+    const Metric m = it->second.metric;
+    if (!spfMetric) {
+      spfMetric = m;
+    } else if (*spfMetric != m) {
+      return UcmpResult{};  // leaves at different distances: skipped
+    }
+    insert(leaf, 0);
+    live[leaf].res.weight = w;
+  }
+  while (!order.empty()) {
+    const auto [m, name] = *order.begin();
+    order.erase(order.begin());
+    NodeUcmp cur = std::move(live.at(name).res);
+    live.erase(name);
+    if (!cur.weight) {
+      int64_t w = 0;
+      for (const auto& [iface, hop] : cur.hops)
+        w += algo == 2 ? hop.link->weightFrom(name) : hop.weight;
+      cur.weight = w;
+    }
+    auto sit = spf.find(name);
+    if (sit == spf.end()) abort();  // CHECK in the reference
+    for (const auto& [link, prev] : sit->second.pathLinks) {
+      const Metric lm = useMetric ? link->metricFrom(prev) : 1;
+      if (!live.count(prev)) insert(prev, m + lm);
+      live.at(prev).res.hops.emplace(link->ifFrom(prev), UcmpHop{link, name, *cur.weight});
+    }
+    int64_t g = 0;  // normalizeNextHopWeights
+    for (const auto& [iface, hop] : cur.hops) g = std::gcd(g, hop.weight);
+    if (g > 1)
+      for (auto& [iface, hop] : cur.hops) hop.weight /= g;
+    out.emplace(name, std::move(cur));
+  }
+  return out;
+}
+
+// ---------------------------------------------------------------------------
 // digest (layout-independent; identical definition in DESIGN.md §Digest)
 static inline uint64_t mix64(uint64_t x) {
   x ^= x >> 30;
@@ -555,6 +636,26 @@ char* dupString(const std::string& s) {
   return p;
 }
 
+std::string ucmpText(const UcmpResult& r) {
+  std::vector<std::string> names;
+  for (const auto& kv : r) names.push_back(kv.first);
+  std::sort(names.begin(), names.end());
+  std::ostringstream os;
+  for (const auto& n : names) {
+    const NodeUcmp& u = r.at(n);
+    os << n << '\t' << (u.weight ? *u.weight : 0) << '\t';
+    std::vector<std::string> ifs;
+    for (const auto& kv : u.hops) ifs.push_back(kv.first);
+    std::sort(ifs.begin(), ifs.end());
+    for (size_t i = 0; i < ifs.size(); ++i) {
+      const UcmpHop& hp = u.hops.at(ifs[i]);
+      os << (i ? "," : "") << ifs[i] << '=' << hp.nextHopNode << ':' << hp.weight;
+    }
+    os << '\n';
+  }
+  return os.str();
+}
+
 std::string spfText(const SpfResult& r) {
   std::vector<const std::string*> names;
   for (const auto& kv : r) names.push_back(&kv.first);
@@ -631,6 +732,26 @@ char* orc_kth_paths_text(void* h, const char* src, const char* dst, int k) {
     os << '\n';
   }
   return dupString(os.str());
+}
+
+// resolveUcmpWeights over getSpfResult(root): leaves = "name\tweight\n"...,
+// algo 2 (ADJ weight propagation) or 3 (PREFIX weight propagation). Text: one
+// line per node, sorted: node \t weight \t iface=nextHop:weight,... (sorted)
+char* orc_ucmp_text(void* h, const char* root, const char* leavesNl, uint32_t n, int algo,
+                    int useMetric) {
+  Oracle* o = (Oracle*)h;
+  std::vector<std::pair<std::string, int64_t>> leaves;
+  const char* p = leavesNl;
+  for (uint32_t i = 0; i < n; ++i) {
+    const char* q = strchr(p, '\n');
+    if (!q) q = p + strlen(p);
+    const std::string ln(p, q);
+    const size_t t = ln.find('\t');
+    leaves.emplace_back(ln.substr(0, t), std::stoll(ln.substr(t + 1)));
+    p = *q ? q + 1 : q;
+  }
+  return dupString(ucmpText(resolveUcmp(o->g.spf(root, useMetric != 0), leaves, algo,
+                                        useMetric != 0)));
 }
 
 char* orc_links_text(void* h, const char* node) {

@@ -100,6 +100,45 @@ fixtures.append(dict(
     ]))
 
 # ---------------------------------------------------------------------------
+# LinkStateTest.UcmpTest — openr/decision/tests/LinkStateTest.cpp:330-483
+# (kDefaultAdjWeight = 1, openr/common/Constants.h:238; adjacency weights
+# default to it, LsdbUtil.h:143-152)
+_ucmp_tree = [(1, [2, 3]), (2, [1, 4, 5, 6]), (3, [1, 6]), (4, [2]), (5, [2]), (6, [2, 3])]
+fixtures.append(dict(
+    name="linkstate_ucmp",
+    source="openr/decision/tests/LinkStateTest.cpp:330-483",
+    steps=[
+        dict(dbs=adjmap_dbs(_ucmp_tree), checks=[
+            # LWP (SP_UCMP_ADJ_WEIGHT_PROPAGATION), :341-383
+            dict(kind="ucmp", root="1", leaves={"4": 2, "5": 1, "6": 1}, algo="adj",
+                 expect_size=6, expect={
+                     "2": {"weight": 3, "hops": {"2/4/0": 2, "2/5/0": 1, "2/6/0": 1}},
+                     "3": {"weight": 1, "hops": {"3/6/0": 1}},
+                     "1": {"weight": 2, "hops": {"1/2/0": 3, "1/3/0": 1}}}),
+            # AWP (SP_UCMP_PREFIX_WEIGHT_PROPAGATION), :395-438
+            dict(kind="ucmp", root="1", leaves={"4": 2, "5": 1, "6": 1}, algo="prefix",
+                 expect_size=6, expect={
+                     "2": {"weight": 4, "hops": {"2/4/0": 2, "2/5/0": 1, "2/6/0": 1}},
+                     "3": {"weight": 1, "hops": {"3/6/0": 1}},
+                     "1": {"weight": 5, "hops": {"1/2/0": 4, "1/3/0": 1}}}),
+        ]),
+    ]))
+fixtures.append(dict(
+    name="linkstate_ucmp_parallel_cost",
+    source="openr/decision/tests/LinkStateTest.cpp:440-482",
+    steps=[
+        dict(dbs=adjmap_dbs([(1, [(2, 1), (5, 2), (5, 2)]), (2, [(1, 1), (3, 1), (4, 1)]),
+                             (3, [(2, 1)]), (4, [(2, 1)]), (5, [(1, 2), (1, 2)])]),
+             checks=[
+                 dict(kind="ucmp", root="1", leaves={"3": 4, "4": 2, "5": 1}, algo="prefix",
+                      expect={
+                          "2": {"weight": 6, "hops": {"2/3/0": 2, "2/4/0": 1}},
+                          "1": {"weight": 8,
+                                "hops": {"1/2/0": 6, "1/5/0": 1, "1/5/1": 1}}}),
+             ]),
+    ]))
+
+# ---------------------------------------------------------------------------
 # LinkStateTest.getKthPaths — LinkStateTest.cpp:256-328
 fixtures.append(dict(
     name="linkstate_kth_paths_box",

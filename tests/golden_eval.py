@@ -117,7 +117,7 @@ def _as_set(expect):
 
 
 SPF_KINDS = {"spf_runs", "ecmp", "ecmp_all", "ksp2", "ksp2_all", "kth_paths",
-             "kth_paths_edge_disjoint", "reachable", "grid_manhattan"}
+             "kth_paths_edge_disjoint", "reachable", "grid_manhattan", "ucmp"}
 
 
 def run_fixture(fx: dict, make_ls, check_changes: bool = True, spf: bool = True) -> int:
@@ -198,6 +198,15 @@ def run_fixture(fx: dict, make_ls, check_changes: bool = True, spf: bool = True)
                             seen.add(key)
             elif k == "reachable":
                 assert (c["dst"] in ls.spf(c["src"])) == c["expect"], where
+            elif k == "ucmp":
+                got = ls.ucmp(c["root"], c["leaves"], c["algo"])
+                if "expect_size" in c:
+                    assert len(got) == c["expect_size"], f"{where}: {sorted(got)}"
+                for node, e in c["expect"].items():
+                    w, hops = got[node]
+                    assert w == e["weight"], f"{where}: {node} weight {w}"
+                    assert {i: hw for i, (_, hw) in hops.items()} == e["hops"], \
+                        f"{where}: {node} hops {hops}"
             elif k == "grid_manhattan":
                 n = c["n"]
                 for s in range(n * n):
@@ -246,6 +255,9 @@ class OracleLS:
 
     def is_overloaded(self, node):
         return self._o.is_overloaded(node)
+
+    def ucmp(self, root, leaves, algo):
+        return self._o.ucmp(root, leaves, algo)
 
     @property
     def spf_runs(self):

@@ -342,3 +342,29 @@ def test_msbfs_device_api_hint_and_error_word():
                 max_root_neighbors=8)
     with pytest.raises(EngineError):
         eng.sync(s)
+
+
+# ------------------------------------------------ UCMP
+@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("algo", ["adj", "prefix"])
+def test_ucmp_random_graphs_match_oracle(seed, algo):
+    """resolveUcmpWeights over the GPU SPF result vs the oracle's restatement
+    (LinkState.cpp:913-1033): leaves = every node at one distance from the
+    root, random weights; also a leaf set at mixed distances (skipped: empty)."""
+    st, names = random_stream(500 + seed, n=40, p=0.12)
+    o, p = both(st)
+    rng = np.random.default_rng(seed)
+    for root in names[:6]:
+        spf = p.spf(root)
+        by_d = {}
+        for n, (m, _, _) in spf.items():
+            if n != root:
+                by_d.setdefault(m, []).append(n)
+        if not by_d:
+            continue
+        d = sorted(by_d)[len(by_d) // 2]
+        leaves = {n: int(rng.integers(1, 9)) for n in by_d[d]}
+        assert p.ucmp(root, leaves, algo) == o.ucmp(root, leaves, algo)
+        if len(by_d) > 1:
+            mixed = {by_d[sorted(by_d)[0]][0]: 1, by_d[sorted(by_d)[-1]][0]: 1}
+            assert p.ucmp(root, mixed, algo) == o.ucmp(root, mixed, algo) == {}
