@@ -76,6 +76,13 @@ typedef struct ospf_csr {
   const uint32_t* twin;        /* [n_edges] index of the reverse entry */
   const uint8_t* edge_up;      /* [n_edges] Link::isUp() */
   const uint8_t* no_transit;   /* [n_nodes] LinkState::isNodeOverloaded() */
+  /* optional (NULL = keep the given order of parallel entries): position of
+   * the entry's link in linksFromNode(row node) iteration
+   * (LinkState.cpp:477-485). The engine orders each parallel group of a row
+   * by the rank of the twin entry, i.e. by the link's position in the
+   * neighbour's linksFromNode, which is the pathLinks order
+   * (LinkState.cpp:885-901) the KSP2 trace walks. */
+  const uint32_t* link_rank;   /* [n_edges] */
 } ospf_csr;
 
 /* Per-run ignored links (LinkState::runSpf linksToIgnore). Run i ignores
@@ -187,6 +194,39 @@ int ospf_plan(const ospf_ctx* ctx, uint32_t flags, uint32_t nh_words, uint32_t m
  * slices = next-hop passes per 64-root batch). */
 int ospf_plan_n(const ospf_ctx* ctx, uint32_t flags, uint32_t nh_words, uint32_t max_ignored,
                 uint32_t n_roots, uint32_t max_root_neighbors, ospf_plan_info* out);
+
+/* KSP2 edge-disjoint paths (LinkState::getKthPaths k = 1 and k = 2,
+ * LinkState.cpp:790-819, with traceOnePath :418-439) from one source to many
+ * destinations, computed on the device: the link-metric SPF of src; per
+ * destination the greedy edge-disjoint trace over its pathLinks (k = 1);
+ * the masked SPF rerun that ignores every link of the k = 1 paths and the
+ * trace over it (k = 2). Records (u32, per destination and k, path_cap words):
+ *   n_paths, then per path: len, link ids (ospf_csr link_id) from src to dst.
+ * status[i] bits: OSPF_KSP_RERUN = destination i's k = 2 needed a masked SPF
+ * (its k = 1 paths are not empty, LinkState.cpp:802-806); OSPF_KSP_OVF1 /
+ * OSPF_KSP_OVF2 = the k = 1 / k = 2 record was not computed (record or trace
+ * budget exceeded: path_cap, 256 links deep, 1536 links visited); the caller
+ * computes those destinations itself. src == dst and unreached destinations
+ * give empty records (no paths). The graph must be loaded with link_rank for
+ * the reference's parallel-link order. */
+#define OSPF_KSP_RERUN 0x1u
+#define OSPF_KSP_OVF1 0x2u
+#define OSPF_KSP_OVF2 0x4u
+typedef struct ospf_ksp2 {
+  uint32_t src;
+  const uint32_t* dsts;  /* [n] node ids */
+  uint32_t n;
+  uint32_t path_cap;     /* words per record, 2 .. OSPF_MAX_IGNORED_PER_RUN */
+  uint32_t* k1;          /* [n][path_cap] */
+  uint32_t* k2;          /* [n][path_cap] */
+  uint32_t* status;      /* [n] */
+} ospf_ksp2;
+/* host buffers, synchronous */
+int ospf_ksp2_run(ospf_ctx* ctx, const ospf_ksp2* args);
+/* device buffers, queued on `stream` (hipStream_t); the engine waits on the
+ * stream itself between rounds only when a masked run is deeper than the
+ * graph's static depth bound. */
+int ospf_ksp2_dev(ospf_ctx* ctx, const ospf_ksp2* args, void* stream);
 
 /* Runtime statistics. spf_runs counts logical runSpf executions (one per
  * root per batch), matching the reference's decision.spf_runs counter

@@ -28,6 +28,7 @@ ENGINE_SYMBOLS = [
     "ospf_open", "ospf_close", "ospf_last_error", "ospf_load_graph", "ospf_graph_info_get",
     "ospf_root_neighbors", "ospf_sssp_batch", "ospf_sssp_batch_dev", "ospf_sync",
     "ospf_plan_variant", "ospf_plan", "ospf_plan_n", "ospf_spf_runs", "ospf_run_batch_dev",
+    "ospf_ksp2_run", "ospf_ksp2_dev",
 ]
 DECISION_SYMBOLS = [
     "odl_create", "odl_destroy", "odl_last_error", "odl_free", "odl_apply", "odl_spf_text",
@@ -40,7 +41,7 @@ DECISION_SYMBOLS = [
 class ospf_csr(C.Structure):  # noqa: N801
     _fields_ = [("n_nodes", u32), ("n_edges", u32), ("row_ptr", vp), ("col", vp),
                 ("metric", vp), ("link_id", vp), ("twin", vp), ("edge_up", vp),
-                ("no_transit", vp)]
+                ("no_transit", vp), ("link_rank", vp)]
 
 
 class ospf_ignore(C.Structure):  # noqa: N801
@@ -55,6 +56,14 @@ class ospf_batch(C.Structure):  # noqa: N801
     _fields_ = [("d_roots", vp), ("n_roots", u32), ("d_ign_offsets", vp), ("d_ign_ids", vp),
                 ("max_ignored", u32), ("flags", u32), ("nh_words", u32),
                 ("max_root_neighbors", u32), ("d_dist", vp), ("d_nh", vp), ("d_digest", vp)]
+
+
+class ospf_ksp2(C.Structure):  # noqa: N801
+    _fields_ = [("src", u32), ("dsts", vp), ("n", u32), ("path_cap", u32), ("k1", vp),
+                ("k2", vp), ("status", vp)]
+
+
+OSPF_KSP_RERUN, OSPF_KSP_OVF1, OSPF_KSP_OVF2 = 0x1, 0x2, 0x4
 
 
 class ospf_plan_info(C.Structure):  # noqa: N801
@@ -96,6 +105,8 @@ def engine() -> C.CDLL:
         L.ospf_plan.argtypes = [vp, u32, u32, u32, C.POINTER(ospf_plan_info)]
         L.ospf_plan_n.argtypes = [vp, u32, u32, u32, u32, u32, C.POINTER(ospf_plan_info)]
         L.ospf_run_batch_dev.argtypes = [vp, C.POINTER(ospf_batch), vp]
+        L.ospf_ksp2_run.argtypes = [vp, C.POINTER(ospf_ksp2)]
+        L.ospf_ksp2_dev.argtypes = [vp, C.POINTER(ospf_ksp2), vp]
         L.ospf_spf_runs.argtypes = [vp]
         L.ospf_spf_runs.restype = u64
         _engine = L

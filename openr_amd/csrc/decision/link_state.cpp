@@ -1,6 +1,7 @@
 // link_state.cpp — LinkState mirror (see link_state.h); SPF on the engine.
 #include "link_state.h"
 
+#include <cstdlib>
 #include <numeric>
 #include <set>
 #include <algorithm>
@@ -368,6 +369,7 @@ void LinkState::ensureEngine() {
     g.twin = csr_.twin.data();
     g.edge_up = csr_.edgeUp.data();
     g.no_transit = csr_.noTransit.data();
+    g.link_rank = csr_.linkRank.data();
     int rc = ospf_load_graph(engine_, &g, snapVersion_);
     if (rc != OSPF_OK) throw EngineError(rc, ospf_last_error(engine_));
     engineVersion_ = snapVersion_;
@@ -641,50 +643,59 @@ const std::vector<Path>& LinkState::getKthPaths(const std::string& src, const st
 void LinkState::prefetchKsp2(const std::string& src, const std::vector<std::string>& dsts) {
   snapshot();
   auto sid = csr_.ids.find(src);
-  if (sid == csr_.ids.end()) {
-    for (const auto& d : dsts) getKthPaths(src, d, 2);
-    return;
-  }
-  const uint32_t s = sid->second;
-  struct Job {
-    std::string dst;
-    std::vector<uint32_t> ign;
-  };
-  std::vector<Job> jobs;
+  std::vector<uint32_t> ids;
+  std::vector<const std::string*> names;
+  std::unordered_set<std::string> queued;
   for (const auto& d : dsts) {
-    if (memoKsp_.count(kspKey(src, d, 2))) continue;
-    const auto& first = getKthPaths(src, d, 1);
-    std::vector<uint32_t> ign;
-    for (const auto& p : first)
-      for (const auto& l : p) ign.push_back(csr_.linkIds.at(l.get()));
-    std::sort(ign.begin(), ign.end());
-    ign.erase(std::unique(ign.begin(), ign.end()), ign.end());
-    if (ign.empty()) {
-      getKthPaths(src, d, 2);  // no masked rerun: reference reuses getSpfResult
+    if (memoKsp_.count(kspKey(src, d, 2)) || !queued.insert(d).second) continue;
+    auto did = csr_.ids.find(d);
+    if (sid == csr_.ids.end() || did == csr_.ids.end()) {
+      getKthPaths(src, d, 2);  // a side without an adjacency DB: no paths, host
       continue;
     }
-    jobs.push_back(Job{d, std::move(ign)});
+    ids.push_back(did->second);
+    names.push_back(&did->first);
   }
-  const size_t V = csr_.names.size();
-  const uint32_t W = nhWordsFor(s);
-  const size_t chunk = std::max<size_t>(1, std::min<size_t>(jobs.size(), (512ull << 20) / (V * 4)));
-  for (size_t c0 = 0; c0 < jobs.size(); c0 += chunk) {
-    const size_t n = std::min(chunk, jobs.size() - c0);
-    std::vector<uint32_t> roots(n, s);
-    std::vector<std::vector<uint32_t>> igns(n);
-    for (size_t i = 0; i < n; ++i) igns[i] = jobs[c0 + i].ign;
-    std::vector<uint32_t> dist;
-    runBatch(roots, &igns, true, OSPF_WANT_DIST, W, &dist, nullptr, nullptr);
-    spfRuns_ += n;
-    for (size_t i = 0; i < n; ++i) {
-      RawRun run{s, std::vector<uint32_t>(dist.begin() + i * V, dist.begin() + (i + 1) * V),
-                 std::move(igns[i])};
-      const std::string& d = jobs[c0 + i].dst;
-      auto did = csr_.ids.find(d);
-      std::vector<Path> paths;
-      if (did != csr_.ids.end()) paths = tracePaths(run, s, did->second);
-      memoKsp_.emplace(kspKey(src, d, 2), std::move(paths));
+  if (ids.empty()) return;
+  // k = 1 traces the memoised SPF of src (LinkState.cpp:804-805): one run
+  getSpfResult(src, true);
+  ensureEngine();
+  // Device KSP2: SPF of src, k = 1 traces, masked reruns and k = 2 traces all
+  // on the engine; records hold link ids. A destination over the engine's
+  // budgets is computed by the host path below (same results, slower).
+  uint32_t kCap = 512;  // record words per destination and k
+  if (const char* x = getenv("ODL_KSP_CAP")) kCap = std::max(2, std::min(2048, atoi(x)));
+  const size_t n = ids.size();
+  std::vector<uint32_t> k1(n * kCap), k2(n * kCap), status(n);
+  ospf_ksp2 a{};
+  a.src = sid->second;
+  a.dsts = ids.data();
+  a.n = (uint32_t)n;
+  a.path_cap = kCap;
+  a.k1 = k1.data();
+  a.k2 = k2.data();
+  a.status = status.data();
+  int rc = ospf_ksp2_run(engine_, &a);
+  if (rc != OSPF_OK) throw EngineError(rc, ospf_last_error(engine_));
+  auto decode = [&](const uint32_t* rec) {
+    std::vector<Path> paths(rec[0]);
+    for (uint32_t p = 0, q = 1; p < rec[0]; ++p) {
+      const uint32_t len = rec[q];
+      paths[p].reserve(len);
+      for (uint32_t j = 0; j < len; ++j) paths[p].push_back(csr_.links.at(rec[q + 1 + j]));
+      q += 1 + len;
     }
+    return paths;
+  };
+  for (size_t i = 0; i < n; ++i) {
+    const std::string& d = *names[i];
+    if (!(status[i] & OSPF_KSP_OVF1)) memoKsp_.emplace(kspKey(src, d, 1), decode(&k1[i * kCap]));
+    if (status[i] & (OSPF_KSP_OVF1 | OSPF_KSP_OVF2)) {
+      getKthPaths(src, d, 2);
+      continue;
+    }
+    if (status[i] & OSPF_KSP_RERUN) ++spfRuns_;  // runSpf(src, true, linksToIgnore)
+    memoKsp_.emplace(kspKey(src, d, 2), decode(&k2[i * kCap]));
   }
 }
 

@@ -79,9 +79,10 @@ int ensure(ospf_ctx* c, void** p, size_t* have, size_t need) {
 }
 
 // the scratch of `stream`, grown to `need` bytes (a grown buffer replaces the
-// old one only after the stream's queued work is done with it)
-char* stream_scratch(ospf_ctx* c, void* stream, size_t need, int* rc) {
-  ospf_ctx::Scratch& sc = c->scratch[stream];
+// old one only after the stream's queued work is done with it); `slot` 1 is a
+// second buffer of the same stream (KSP2 state around nested batch calls)
+char* stream_scratch(ospf_ctx* c, void* stream, size_t need, int* rc, int slot = 0) {
+  ospf_ctx::Scratch& sc = c->scratch[(char*)stream + slot];
   *rc = OSPF_OK;
   if (sc.bytes >= need) return (char*)sc.p;
   if (sc.p) hipStreamSynchronize((hipStream_t)stream);
@@ -329,6 +330,198 @@ int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
   return OSPF_OK;
 }
 
+
+// ---------------------------------------------------------------- KSP2
+// getKthPaths(src, dst, 1 and 2) for many destinations (LinkState.cpp:790-819):
+//  1. the link-metric SPF of src (one run, any variant) -> dist row;
+//  2. trace k = 1 per destination over that row -> records + sorted link sets;
+//  3. the masked reruns (run i ignores destination i's k = 1 links) and the
+//     k = 2 trace over each. Unit-metric graphs run the reruns as the
+//     multi-source BFS in distance-only mode (64 runs per traversal, per-run
+//     ignore masks) and trace straight from its level bytes; other graphs run
+//     per-run kernels into dist rows, in chunks.
+int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
+  const uint32_t V = c->info.n_nodes, n = k->n, cap = k->path_cap;
+  const uint32_t src = k->src;
+  const bool unit = c->info.unit_metric != 0;
+  const uint32_t nn = c->h_dn_off[src + 1] - c->h_dn_off[src];
+  const uint32_t W = std::max<uint32_t>(1, (nn + 31) / 32);
+  const bool ms = unit && c->g.n_lid && c->depth_bound <= 253 && !getenv("OSPF_KSP_ROWS");
+  constexpr uint32_t lmax = 256;
+  const size_t sz_ign = align_up((size_t)n * cap * 4ull, 256), sz_cnt = align_up(n * 4ull, 256),
+               sz_one = align_up(V * 4ull, 256) + 256;
+  // rerun state: multi-source rounds, or per-run rows in chunks
+  const size_t igw = ((size_t)c->g.E + 31) / 32;
+  const size_t per_vb = align_up((size_t)V * 8ull * 6 + V * 64ull + lmax * 8ull + igw * 4ull, 256) +
+                        align_up((size_t)c->g.E * 8ull, 256);
+  uint32_t nb_cap = 96;
+  if (const char* e = getenv("OSPF_MS_NB")) nb_cap = std::max(1, atoi(e));
+  nb_cap = (uint32_t)std::max<size_t>(1, std::min<size_t>(nb_cap, (6ull << 30) / per_vb));
+  const uint32_t total_vb = (n + 63) / 64, nb_max = std::min(nb_cap, total_vb);
+  uint32_t chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(n, (2ull << 30) / (V * 4ull)));
+  const size_t sz_roots = align_up((size_t)(ms ? n : chunk) * 4ull, 256);
+  const size_t sz_state = ms ? per_vb * nb_max
+                             : align_up((size_t)chunk * V * 4ull, 256) + align_up((chunk + 1) * 4ull, 256);
+  int rc = OSPF_OK;
+  char* sp = stream_scratch(c, s, sz_ign + sz_cnt + sz_one + sz_roots + sz_state, &rc, 1);
+  if (rc) return rc;
+  uint32_t* d_ign = (uint32_t*)sp;
+  uint32_t* d_cnt = (uint32_t*)(sp + sz_ign);
+  uint32_t* d_dist1 = (uint32_t*)(sp + sz_ign + sz_cnt);
+  uint32_t* d_src = (uint32_t*)(sp + sz_ign + sz_cnt + align_up(V * 4ull, 256));
+  uint32_t* d_roots = (uint32_t*)(sp + sz_ign + sz_cnt + sz_one);
+  char* st = sp + sz_ign + sz_cnt + sz_one + sz_roots;
+  HIPCHK(c, hipSetDevice(c->device));
+
+  // 1-2: SPF of src, k = 1
+  HIPCHK(c, hipMemsetD32Async(d_src, (int)src, 1, s));
+  ospf_batch b1{};
+  b1.d_roots = d_src;
+  b1.n_roots = 1;
+  b1.flags = OSPF_WANT_DIST;
+  b1.nh_words = W;
+  b1.max_root_neighbors = nn;
+  b1.d_dist = d_dist1;
+  rc = ospf_run_batch_dev(c, &b1, s);
+  if (rc) return rc;
+  ospf::TraceArgs t{};
+  t.src = src;
+  t.dsts = k->dsts;
+  t.n = n;
+  t.rows = d_dist1;
+  t.row_stride = 0;
+  t.stride = cap;
+  t.out = k->k1;
+  t.ign_out = d_ign;
+  t.cnt_out = d_cnt;
+  t.status = k->status;
+  t.k = 1;
+  t.unit = unit ? 1u : 0u;
+  hipError_t e = ospf::launch_ksp_trace(false, c->g, t, s);
+  if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_trace k1");
+
+  // 3: masked reruns + k = 2
+  HIPCHK(c, hipMemsetD32Async(d_roots, (int)src, ms ? n : chunk, s));
+  if (ms) {
+    std::vector<uint32_t> found;
+    for (uint32_t vb0 = 0; vb0 < total_vb; vb0 += nb_max) {
+      ospf::MsArgs a{};
+      a.roots = d_roots;
+      a.n = n;
+      a.W = W;
+      a.npass = 1;
+      a.R = 64;
+      a.PP = 1;
+      a.OW = 1;
+      a.rep = 1;
+      a.vb0 = vb0;
+      a.nb = std::min(nb_max, total_vb - vb0);
+      a.lmax = lmax;
+      a.kcap = nn;
+      a.push_div = 8;
+      if (const char* x = getenv("OSPF_MS_PUSH_DIV")) a.push_div = (uint32_t)std::max(0, atoi(x));
+      a.defer = 1;
+      a.err = c->d_err;
+      a.front = (uint64_t*)st;
+      a.seen = a.front + 4ull * a.nb * V;
+      a.accb = a.seen + (size_t)a.nb * V;
+      a.planes = a.accb + (size_t)a.nb * V;
+      a.lev = (uint8_t*)a.planes;
+      a.found = (uint32_t*)(a.lev + (size_t)a.nb * V * 64ull);
+      a.mass = a.found + (size_t)a.nb * lmax;
+      a.igw = (uint32_t)igw;
+      a.igb = a.mass + (size_t)a.nb * lmax;
+      const size_t zero = (char*)(a.igb + (size_t)a.nb * igw) - st;
+      a.igm = (uint64_t*)(st + align_up(zero, 256));
+      HIPCHK(c, hipMemsetAsync(st, 0, zero, s));
+      e = ospf::launch_ksp_masks(c->g, a, d_ign, d_cnt, cap, s);
+      if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_masks");
+      uint32_t d = std::max<uint32_t>(2, c->depth_bound);
+      // test knob: start with fewer levels (exercises the continuation below)
+      if (const char* x = getenv("OSPF_KSP_D0")) d = std::max(2, std::min((int)d, atoi(x)));
+      e = ospf::launch_msbfs_ksp(c->g, a, 1, d, s);
+      if (e != hipSuccess) return hip_fail(c, e, "launch_msbfs_ksp");
+      // masked runs may be deeper than the graph's bound: continue while any
+      // batch still has a frontier (levels up to 253: lev bytes hold dist + 1)
+      std::vector<uint32_t> deep;
+      for (;;) {
+        found.resize((size_t)a.nb * lmax);
+        HIPCHK(c, hipMemcpyAsync(found.data(), a.found, found.size() * 4ull, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        deep.clear();
+        for (uint32_t j = 0; j < a.nb; ++j)
+          if (found[(size_t)j * lmax + d]) deep.push_back(j);
+        if (deep.empty()) break;
+        if (d >= 254) {
+          for (uint32_t j : deep) {
+            const uint32_t r0 = (vb0 + j) * 64u;
+            e = ospf::launch_or_bits(k->status + r0, std::min(64u, n - r0), OSPF_KSP_OVF2, s);
+            if (e != hipSuccess) return hip_fail(c, e, "launch_or_bits");
+          }
+          break;
+        }
+        const uint32_t d1 = std::min<uint32_t>(d + 8, 254);
+        e = ospf::launch_msbfs_ksp(c->g, a, d, d1, s);
+        if (e != hipSuccess) return hip_fail(c, e, "launch_msbfs_ksp");
+        d = d1;
+      }
+      const uint32_t r0 = vb0 * 64u;
+      ospf::TraceArgs t2 = t;
+      t2.dsts = k->dsts + r0;
+      t2.n = std::min<uint32_t>(a.nb * 64u, n - r0);
+      t2.rows = nullptr;
+      t2.lev = a.lev;
+      t2.ign = d_ign + (size_t)r0 * cap;
+      t2.ign_cnt = d_cnt + r0;
+      t2.out = k->k2 + (size_t)r0 * cap;
+      t2.ign_out = nullptr;
+      t2.cnt_out = nullptr;
+      t2.status = k->status + r0;
+      t2.k = 2;
+      e = ospf::launch_ksp_trace(true, c->g, t2, s);
+      if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_trace k2");
+      // runs whose levels went past 253 keep OVF2 (the trace skips nothing
+      // else: their lev bytes stop at 254)
+    }
+    c->spf_runs += n;
+  } else {
+    uint32_t* d_rows = (uint32_t*)st;
+    uint32_t* d_off = (uint32_t*)(st + align_up((size_t)chunk * V * 4ull, 256));
+    e = ospf::launch_iota(d_off, chunk, cap, s);
+    if (e != hipSuccess) return hip_fail(c, e, "launch_iota");
+    for (uint32_t r0 = 0; r0 < n; r0 += chunk) {
+      const uint32_t nc = std::min(chunk, n - r0);
+      ospf_batch b{};
+      b.d_roots = d_roots;
+      b.n_roots = nc;
+      b.d_ign_offsets = d_off;
+      b.d_ign_ids = d_ign + (size_t)r0 * cap;
+      b.max_ignored = cap;
+      b.flags = OSPF_WANT_DIST;
+      b.nh_words = W;
+      b.max_root_neighbors = nn;
+      b.d_dist = d_rows;
+      rc = ospf_run_batch_dev(c, &b, s);
+      if (rc) return rc;
+      ospf::TraceArgs t2 = t;
+      t2.dsts = k->dsts + r0;
+      t2.n = nc;
+      t2.rows = d_rows;
+      t2.row_stride = V;
+      t2.ign = d_ign + (size_t)r0 * cap;
+      t2.ign_cnt = d_cnt + r0;
+      t2.out = k->k2 + (size_t)r0 * cap;
+      t2.ign_out = nullptr;
+      t2.cnt_out = nullptr;
+      t2.status = k->status + r0;
+      t2.k = 2;
+      e = ospf::launch_ksp_trace(false, c->g, t2, s);
+      if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_trace k2");
+    }
+  }
+  return OSPF_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -435,14 +628,36 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
     prow[u + 1] = prow[u] + ((csr->row_ptr[u + 1] - csr->row_ptr[u] + 3u) & ~3u);
   const uint32_t Ep = prow[V];
   std::vector<uint32_t> pcolx(Ep, 0x80000000u), pw(Ep, 0u), prw(Ep, 0u), plink(Ep, 0xFFFFFFFFu);
+  // link_rank given: a parallel group (same neighbour) is ordered by the
+  // twin entry's rank = the link's position in linksFromNode(neighbour), the
+  // order pathLinks lists links of one predecessor in (LinkState.cpp:885-901)
+  std::vector<uint32_t> ord;
+  uint32_t max_lid = 0;
   for (uint32_t u = 0; u < V; ++u) {
     const uint32_t b = csr->row_ptr[u], n = csr->row_ptr[u + 1] - b, pb = prow[u];
+    ord.resize(n);
+    for (uint32_t k = 0; k < n; ++k) ord[k] = b + k;
+    if (csr->link_rank)
+      std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
+        if (csr->col[x] != csr->col[y]) return csr->col[x] < csr->col[y];
+        return csr->link_rank[csr->twin[x]] < csr->link_rank[csr->twin[y]];
+      });
     for (uint32_t k = 0; k < n; ++k) {
-      pcolx[pb + k] = colx[b + k];
-      pw[pb + k] = csr->metric[b + k];
-      prw[pb + k] = rw[b + k];
-      plink[pb + k] = csr->link_id[b + k];
+      const uint32_t e = ord[k];
+      pcolx[pb + k] = colx[e];
+      pw[pb + k] = csr->metric[e];
+      prw[pb + k] = rw[e];
+      plink[pb + k] = csr->link_id[e];
+      max_lid = std::max(max_lid, csr->link_id[e]);
     }
+  }
+  // entries of each link id (KSP2 ignore masks); ids above 2^28 disable them
+  const uint32_t n_lid = (E && max_lid < (1u << 28)) ? max_lid + 1 : 0;
+  std::vector<uint32_t> link_e(std::max<size_t>(2ull * n_lid, 2), 0xFFFFFFFFu);
+  for (uint32_t e = 0; e < Ep && n_lid; ++e) {
+    if (plink[e] == 0xFFFFFFFFu) continue;
+    uint32_t* le = &link_e[2ull * plink[e]];
+    if (le[0] == 0xFFFFFFFFu) le[0] = e; else le[1] = e;
   }
 
   // device layout: one allocation, 256-B aligned sub-buffers
@@ -451,15 +666,16 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
     if (prow[u + 1] - prow[u] > ospf::kMsBigDeg) big.push_back(u);
   const size_t sz_row = (V + 1) * 4ull, sz_e = (size_t)Ep * 4ull, sz_nt = nt.size() * 4ull,
                sz_dnoff = (V + 1) * 4ull, sz_dn = std::max<size_t>(dn.size(), 1) * 4ull,
-               sz_big = std::max<size_t>(big.size(), 1) * 4ull, sz_key = V * 16ull;
+               sz_big = std::max<size_t>(big.size(), 1) * 4ull, sz_key = V * 16ull,
+               sz_le = link_e.size() * 4ull;
   std::vector<uint64_t> dkey(2ull * V);  // digest key tables (row digest kernel)
   for (uint32_t u = 0; u < V; ++u) {
     dkey[2ull * u] = ospf::digest_dist_key(u);
     dkey[2ull * u + 1] = ospf::digest_node_key(u);
   }
-  size_t off[10], tot = 0;
-  const size_t szs[10] = {sz_row, sz_e, sz_e, sz_e, sz_e, sz_nt, sz_dnoff, sz_dn, sz_big, sz_key};
-  for (int i = 0; i < 10; ++i) {
+  size_t off[11], tot = 0;
+  const size_t szs[11] = {sz_row, sz_e, sz_e, sz_e, sz_e, sz_nt, sz_dnoff, sz_dn, sz_big, sz_key, sz_le};
+  for (int i = 0; i < 11; ++i) {
     off[i] = tot;
     tot += align_up(std::max<size_t>(szs[i], 4), 256);
   }
@@ -475,9 +691,10 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
     return fail(c, OSPF_E_NOMEM, std::string("hipMalloc graph: ") + hipGetErrorString(he));
   }
   char* base = (char*)c->d_graph;
-  const void* srcs[10] = {prow.data(), pcolx.data(), pw.data(), prw.data(), plink.data(),
-                          nt.data(), dn_off.data(), dn.data(), big.data(), dkey.data()};
-  for (int i = 0; i < 10; ++i)
+  const void* srcs[11] = {prow.data(), pcolx.data(), pw.data(), prw.data(), plink.data(),
+                          nt.data(), dn_off.data(), dn.data(), big.data(), dkey.data(),
+                          link_e.data()};
+  for (int i = 0; i < 11; ++i)
     if (szs[i] && srcs[i]) HIPCHK(c, hipMemcpy(base + off[i], srcs[i], szs[i], hipMemcpyHostToDevice));
   c->g.V = V;
   c->g.E = Ep;
@@ -492,6 +709,8 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   c->g.nbig = (uint32_t)big.size();
   c->g.big = (const uint32_t*)(base + off[8]);
   c->g.dkey = (const uint64_t*)(base + off[9]);
+  c->g.n_lid = n_lid;
+  c->g.link_e = (const uint32_t*)(base + off[10]);
   c->h_row_ptr.assign(csr->row_ptr, csr->row_ptr + V + 1);
   c->h_dn_off = std::move(dn_off);
   c->h_dn = std::move(dn);
@@ -751,6 +970,49 @@ int ospf_sssp_batch(ospf_ctx* c, const uint32_t* roots, uint32_t n_roots, const 
     if (want & OSPF_WANT_DIGEST)
       HIPCHK(c, hipMemcpy(digest_out + r0, d_dig, n * sizeof(ospf_digest), hipMemcpyDeviceToHost));
   }
+  return OSPF_OK;
+}
+
+int ospf_ksp2_dev(ospf_ctx* c, const ospf_ksp2* k, void* stream) {
+  if (!c || !k) return OSPF_E_INVAL;
+  if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  if (k->n == 0) return OSPF_OK;
+  if (!k->dsts || !k->k1 || !k->k2 || !k->status) return fail(c, OSPF_E_INVAL, "null KSP2 buffer");
+  if (k->src >= c->info.n_nodes) return fail(c, OSPF_E_INVAL, "src out of range");
+  if (k->path_cap < 2 || k->path_cap > OSPF_MAX_IGNORED_PER_RUN)
+    return fail(c, OSPF_E_INVAL, "path_cap out of range");
+  const uint64_t V = c->info.n_nodes;
+  if ((uint64_t)c->info.max_metric * (V - 1) >= 0xFFFFFFFFull)
+    return fail(c, OSPF_E_RANGE, "u32 distance overflow possible (max_metric * (V-1))");
+  return run_ksp2(c, k, (hipStream_t)stream);
+}
+
+int ospf_ksp2_run(ospf_ctx* c, const ospf_ksp2* k) {
+  if (!c || !k) return OSPF_E_INVAL;
+  if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  if (k->n == 0) return OSPF_OK;
+  if (!k->dsts || !k->k1 || !k->k2 || !k->status) return fail(c, OSPF_E_INVAL, "null KSP2 buffer");
+  for (uint32_t i = 0; i < k->n; ++i)
+    if (k->dsts[i] >= c->info.n_nodes) return fail(c, OSPF_E_INVAL, "dst out of range");
+  const size_t n = k->n, rec = (size_t)k->path_cap * 4ull;
+  const size_t sz_d = align_up(n * 4, 256), sz_r = align_up(n * rec, 256);
+  int rc = ensure(c, &c->d_stage, &c->stage_bytes, 2 * sz_d + 2 * sz_r);
+  if (rc) return rc;
+  char* s = (char*)c->d_stage;
+  ospf_ksp2 d = *k;
+  d.dsts = (const uint32_t*)s;
+  d.status = (uint32_t*)(s + sz_d);
+  d.k1 = (uint32_t*)(s + 2 * sz_d);
+  d.k2 = (uint32_t*)(s + 2 * sz_d + sz_r);
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMemcpy((void*)d.dsts, k->dsts, n * 4, hipMemcpyHostToDevice));
+  rc = ospf_ksp2_dev(c, &d, nullptr);
+  if (rc) return rc;
+  rc = ospf_sync(c, nullptr);
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpy(k->status, d.status, n * 4, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(k->k1, d.k1, n * rec, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(k->k2, d.k2, n * rec, hipMemcpyDeviceToHost));
   return OSPF_OK;
 }
 

@@ -19,6 +19,11 @@ namespace ospf {
 //   dn_off/dn  = distinct neighbours per node, ascending (next-hop bit order)
 //   big        = nodes whose padded row is longer than kMsBigDeg (scanned by a
 //                whole wave in the multi-source BFS)
+//   link_e     = [n_lid][2] padded positions of the two entries of link id l
+//                (UINT32_MAX when absent): ignore masks of the KSP2 reruns
+// Parallel entries of a row (same neighbour) are ordered by the rank of the
+// twin entry in the neighbour's linksFromNode when the caller gives link_rank,
+// so row order = (neighbour id, rank) = the pathLinks order of a tight group.
 constexpr uint32_t kMsBigDeg = 256;
 struct DevGraph {
   uint32_t V, E;
@@ -33,6 +38,8 @@ struct DevGraph {
   const uint32_t* nt_bits;
   const uint32_t* dn_off;
   const uint32_t* dn;
+  uint32_t n_lid;
+  const uint32_t* link_e;
 };
 
 struct RunArgs {
@@ -124,10 +131,49 @@ struct MsArgs {
   uint32_t defer;         // 1: levels fill lev, msbfs_rows writes the rows
   ospf_digest* digest;    // [n] (defer: msbfs_rows adds each pass's terms; zeroed first)
   uint32_t* err;
+  // KSP2 reruns (kp = 0: distances only, every root of a batch is the same
+  // source, run r ignores its own links): edge e is ignored by the roots in
+  // igm[vb][e] when bit e of igb[vb] is set (both entries of a link marked)
+  uint32_t* igb;          // [nb][igw]
+  uint64_t* igm;          // [nb][E]
+  uint32_t igw;
 };
 // kp = 8, 16 or 32 planes per node; depth_bound bounds the BFS level count
 hipError_t launch_msbfs_round(int kp, const DevGraph& g, const MsArgs& a, uint32_t depth_bound,
                               hipStream_t s);
+// KSP2 mode (kp = 0): init + levels [d0, d1) only; lev holds the distances
+hipError_t launch_msbfs_ksp(const DevGraph& g, const MsArgs& a, uint32_t d0, uint32_t d1,
+                            hipStream_t s);
+// ignore masks of the runs of a round: run j of the round (root rix = vb0*64+j)
+// ignores ign[rix][0 .. cnt[rix]) (sorted)
+hipError_t launch_ksp_masks(const DevGraph& g, const MsArgs& a, const uint32_t* ign,
+                            const uint32_t* cnt, uint32_t stride, hipStream_t s);
+
+// KSP2 trace (spf_ksp2.hip): one wave per (source, destination) run walks
+// traceOnePath (LinkState.cpp:418-439) over the run's distances; see TraceArgs.
+struct TraceArgs {
+  uint32_t src;
+  const uint32_t* dsts;     // [n]
+  uint32_t n;
+  const uint32_t* rows;     // rows mode: dist of run i = rows + i * row_stride (0: shared)
+  uint64_t row_stride;
+  const uint8_t* lev;       // lev mode: [n/64][V][64] dist + 1 of run i at byte i % 64
+  const uint32_t* ign;      // [n][stride] run's ignored links, sorted (null: none)
+  const uint32_t* ign_cnt;  // [n]
+  uint32_t stride;          // words per record (= path_cap)
+  uint32_t* out;            // [n][stride] path record
+  uint32_t* ign_out;        // k = 1: [n][stride] links of the paths, sorted, UINT32_MAX padded
+  uint32_t* cnt_out;        // k = 1: [n]
+  uint32_t* status;         // [n]
+  uint32_t k;               // 1 or 2
+  uint32_t unit;            // every usable metric is 1
+};
+hipError_t launch_ksp_trace(bool lev, const DevGraph& g, const TraceArgs& t, hipStream_t s);
+// st[i] |= bits, i < n
+hipError_t launch_or_bits(uint32_t* st, uint32_t n, uint32_t bits, hipStream_t s);
+// out[i] = i * stride, i <= n
+hipError_t launch_iota(uint32_t* out, uint32_t n, uint32_t stride, hipStream_t s);
+
 // digests of finished rows, one workgroup per root
 hipError_t launch_row_digest(const DevGraph& g, uint32_t n, const uint32_t* dist,
                              const uint32_t* nh, uint32_t W, ospf_digest* out, hipStream_t s);

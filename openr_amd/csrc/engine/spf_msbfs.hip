@@ -40,6 +40,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "spf_kernels.h"
 
 namespace ospf {
@@ -72,6 +74,8 @@ __device__ __forceinline__ bool transit(const DevGraph& g, uint32_t v) {
 __device__ __forceinline__ void or64(uint64_t* p, uint64_t x) {
   atomicOr((unsigned long long*)p, (unsigned long long)x);
 }
+// register arrays of KP plane words (KP = 0: KSP2 distance-only mode)
+constexpr int kpa(int kp) { return kp > 0 ? kp : 1; }
 
 // one (64-root batch, next-hop word) of the round, and its state arrays
 struct VB {
@@ -80,7 +84,10 @@ struct VB {
   uint64_t* seen;
   uint64_t* accb;
   uint64_t* P;
-  __device__ VB(const MsArgs& a, uint32_t vbl_, uint32_t V_, int kp) : vbl(vbl_), V(V_) {
+  const uint32_t* igb;  // KSP2 mode: ignored-edge bitmap and root masks
+  const uint64_t* igm;
+  __device__ VB(const MsArgs& a, uint32_t vbl_, uint32_t V_, int kp, uint32_t E = 0)
+      : vbl(vbl_), V(V_) {
     const uint32_t vb = a.vb0 + vbl;
     g = vb % a.npass;
     rix0 = (vb / a.npass) * a.R;
@@ -89,6 +96,18 @@ struct VB {
     seen = a.seen + (size_t)vbl * V;
     accb = a.accb + (size_t)vbl * V;
     P = a.planes + (size_t)vbl * V * kp;
+    igb = kp == 0 ? a.igb + (size_t)vbl * a.igw : nullptr;
+    igm = kp == 0 ? a.igm + (size_t)vbl * E : nullptr;
+  }
+  // roots (of the batch) that ignore the link of entry e (KSP2 mode)
+  __device__ __forceinline__ uint64_t ignored(uint32_t e) const {
+    return ((igb[e >> 5] >> (e & 31u)) & 1u) ? igm[e] : 0ull;
+  }
+  // same for the 4 entries e .. e+3 (e % 4 == 0): ~mask per entry
+  __device__ __forceinline__ void keep4(uint32_t e, uint64_t* keep) const {
+    const uint32_t ib = (igb[e >> 5] >> (e & 31u)) & 0xFu;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) keep[i] = ((ib >> i) & 1u) ? ~igm[e + i] : ~0ull;
   }
   // frontier record of level d: {roots with v in the frontier, those of them
   // with a non-zero plane in this pass} (16 B per node)
@@ -200,7 +219,7 @@ __global__ void __launch_bounds__(256) msbfs_init_kernel(DevGraph g, MsArgs a) {
   const uint32_t slot = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   const uint32_t vbl = slot / a.R, bit = slot % a.R;
   if (vbl >= a.nb) return;
-  const VB b(a, vbl, g.V, KP);
+  const VB b(a, vbl, g.V, KP, g.E);
   const uint32_t rix = b.rix0 + bit;
   if (rix >= a.n) return;
   const uint32_t V = g.V;
@@ -232,6 +251,7 @@ __global__ void __launch_bounds__(256) msbfs_init_kernel(DevGraph g, MsArgs a) {
   for (uint32_t e = e0 + lane; e < e1; e += kWave) {
     const uint32_t cx = g.colx[e];
     if ((cx & kDown) || cx == s) continue;
+    if (KP == 0 && ((b.ignored(e) >> bit) & 1ull)) continue;
     const uint32_t v = cx;
     // index of v among s's distinct neighbours (ascending ids)
     uint32_t lo = 0, hi = nn;
@@ -270,9 +290,10 @@ __global__ void __launch_bounds__(256) msbfs_init_kernel(DevGraph g, MsArgs a) {
 // in-edges [beg, end) of a node with unseen roots m, one lane (STEP 4) or the
 // wave (lane offset folded into beg, STEP 256); rows are padded to 4 entries
 template <int KP, uint32_t STEP>
-__device__ __forceinline__ void pull_scan(const DevGraph& g, const uint64_t* fcur, const uint64_t* P,
-                                          uint32_t beg, uint32_t end, uint64_t m, uint64_t rep,
-                                          uint64_t& acc, uint64_t* pacc) {
+__device__ __forceinline__ void pull_scan(const DevGraph& g, const VB& b, const uint64_t* fcur,
+                                          const uint64_t* P, uint32_t beg, uint32_t end,
+                                          uint64_t m, uint64_t rep, uint64_t& acc,
+                                          uint64_t* pacc) {
   const uint4* q = reinterpret_cast<const uint4*>(g.colx);
   const uint4* fr = reinterpret_cast<const uint4*>(fcur);
   for (uint32_t e = beg; e < end; e += STEP) {
@@ -281,16 +302,19 @@ __device__ __forceinline__ void pull_scan(const DevGraph& g, const uint64_t* fcu
     uint4 fs[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) fs[i] = (cs[i] & kDown) ? make_uint4(0, 0, 0, 0) : fr[cs[i]];
+    uint64_t keep[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+    if (KP == 0) b.keep4(e, keep);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const uint64_t f = (((uint64_t)fs[i].y << 32) | fs[i].x) & m;
+      const uint64_t f = (((uint64_t)fs[i].y << 32) | fs[i].x) & m & keep[i];
       if (!f) continue;
       acc |= f;
+      if (KP == 0) continue;
       // roots whose tail has no plane bit in this pass add nothing to them
       const uint64_t fz = (((uint64_t)fs[i].w << 32) | fs[i].z) & f;
       if (!fz) continue;
       const uint64_t fx = fz * rep;  // the roots' bits in every packed plane slot
-      uint64_t pu[KP];
+      uint64_t pu[kpa(KP)];
       load_planes<KP>(P, cs[i], pu);
 #pragma unroll
       for (int k = 0; k < KP; ++k) pacc[k] |= pu[k] & fx;
@@ -311,9 +335,11 @@ __device__ __forceinline__ void push_scan(const DevGraph& g, const VB& b, uint32
     uint64_t ss[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) ss[i] = (cs[i] & kDown) ? ~0ull : b.seen[cs[i]];
+    uint64_t keep[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+    if (KP == 0) b.keep4(e, keep);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const uint64_t f = fu & ~ss[i];
+      const uint64_t f = fu & ~ss[i] & keep[i];
       if (!f) continue;
       const uint32_t v = cs[i];
       or64(&b.accb[v], f);
@@ -340,7 +366,7 @@ __global__ void __launch_bounds__(256) msbfs_level_kernel(DevGraph g, MsArgs a, 
   const uint32_t vbl = blockIdx.x % a.nb;
   if (!a.found[vbl * a.lmax + d]) return;  // level d is empty: this batch is done
   const bool push = (uint64_t)a.mass[vbl * a.lmax + d] * a.push_div < g.E;
-  const VB b(a, vbl, g.V, KP);
+  const VB b(a, vbl, g.V, KP, g.E);
   const uint32_t V = g.V;
   const int lane = threadIdx.x & 63;
   const uint64_t* fcur = b.front(a, d);
@@ -355,17 +381,17 @@ __global__ void __launch_bounds__(256) msbfs_level_kernel(DevGraph g, MsArgs a, 
     if (push) {
       const uint64_t fu = fcur[2u * u];
       if (!fu) return;
-      uint64_t pu[KP];
+      uint64_t pu[kpa(KP)];
       load_planes<KP>(b.P, u, pu);
       push_scan<KP, 4u * kWave>(g, b, beg + 4u * lane, end, fu, a.rep, pu);
       return;
     }
     const uint64_t m = ~b.seen[u] & b.valid;
     if (!m) return;  // the node's own lane writes fnext[u] = 0
-    uint64_t acc = 0, pacc[KP];
+    uint64_t acc = 0, pacc[kpa(KP)];
 #pragma unroll
-    for (int k = 0; k < KP; ++k) pacc[k] = 0;
-    pull_scan<KP, 4u * kWave>(g, fcur, b.P, beg + 4u * lane, end, m, a.rep, acc, pacc);
+    for (int k = 0; k < kpa(KP); ++k) pacc[k] = 0;
+    pull_scan<KP, 4u * kWave>(g, b, fcur, b.P, beg + 4u * lane, end, m, a.rep, acc, pacc);
     acc = wave_or64(acc);
 #pragma unroll
     for (int k = 0; k < KP; ++k) pacc[k] = wave_or64(pacc[k]);
@@ -399,7 +425,7 @@ __global__ void __launch_bounds__(256) msbfs_level_kernel(DevGraph g, MsArgs a, 
     if (!fu) return;
     const uint32_t beg = g.row_ptr[v], end = g.row_ptr[v + 1];
     if (end - beg > kMsBigDeg) return;
-    uint64_t pu[KP];
+    uint64_t pu[kpa(KP)];
     load_planes<KP>(b.P, v, pu);
     push_scan<KP, 4u>(g, b, beg, end, fu, a.rep, pu);
     return;
@@ -415,10 +441,10 @@ __global__ void __launch_bounds__(256) msbfs_level_kernel(DevGraph g, MsArgs a, 
     }
   }
   const bool big = m && (end - beg) > kMsBigDeg;
-  uint64_t acc = 0, pacc[KP];
+  uint64_t acc = 0, pacc[kpa(KP)];
 #pragma unroll
-  for (int k = 0; k < KP; ++k) pacc[k] = 0;
-  if (m && !big) pull_scan<KP, 4u>(g, fcur, b.P, beg, end, m, a.rep, acc, pacc);
+  for (int k = 0; k < kpa(KP); ++k) pacc[k] = 0;
+  if (m && !big) pull_scan<KP, 4u>(g, b, fcur, b.P, beg, end, m, a.rep, acc, pacc);
   uint32_t mass = 0;
   if (v < V && !big) {
     const bool tr = acc && transit(g, v);
@@ -450,9 +476,9 @@ __global__ void __launch_bounds__(256) msbfs_settle_kernel(DevGraph g, MsArgs a,
   const int lane = threadIdx.x & 63;
   uint64_t* fnext = b.front(a, d + 1);
   const uint32_t v = (blockIdx.x / a.nb) * kBlock + threadIdx.x;
-  uint64_t acc = 0, pacc[KP];
+  uint64_t acc = 0, pacc[kpa(KP)];
 #pragma unroll
-  for (int k = 0; k < KP; ++k) pacc[k] = 0;
+  for (int k = 0; k < kpa(KP); ++k) pacc[k] = 0;
   uint32_t mass = 0;
   if (v < V) {
     acc = b.accb[v];
@@ -719,7 +745,62 @@ hipError_t launch_round_kp(const DevGraph& g, const MsArgs& a, uint32_t depth_bo
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- KSP2
+// Ignore masks of a round's runs (every batch of 64 runs shares the source):
+// pass 0 clears the mask words of the entries listed in the round, pass 1 ORs
+// the run bits in and marks the entries in the batch's bitmap (the bitmap is
+// zeroed with the round's state, so stale mask words are never read).
+__global__ void __launch_bounds__(256) ksp_mask_kernel(DevGraph g, MsArgs a, const uint32_t* ign,
+                                                       const uint32_t* cnt, uint32_t stride,
+                                                       uint32_t pass) {
+  const uint32_t j = blockIdx.y;  // run of the round
+  const uint32_t vbl = j / 64u, r = j % 64u;
+  if (vbl >= a.nb) return;
+  const uint32_t rix = (a.vb0 + vbl) * 64u + r;
+  if (rix >= a.n) return;
+  const uint32_t n = min(cnt[rix], stride);
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < 2u * n; k += gridDim.x * blockDim.x) {
+    const uint32_t lid = ign[(size_t)rix * stride + k / 2u];
+    if (lid >= g.n_lid) continue;
+    const uint32_t e = g.link_e[2ull * lid + (k & 1u)];
+    if (e == kInf) continue;
+    uint64_t* m = a.igm + (size_t)vbl * g.E + e;
+    if (pass == 0) {
+      *m = 0ull;
+    } else {
+      or64(m, 1ull << r);
+      atomicOr(&a.igb[(size_t)vbl * a.igw + (e >> 5)], 1u << (e & 31u));
+    }
+  }
+}
+
 }  // namespace
+
+hipError_t launch_msbfs_ksp(const DevGraph& g, const MsArgs& a, uint32_t d0, uint32_t d1,
+                            hipStream_t s) {
+  if (d0 <= 1) {
+    const uint32_t init_blocks = (a.nb * a.R + kWavesPerBlock - 1) / kWavesPerBlock;
+    hipLaunchKernelGGL(msbfs_init_kernel<0>, dim3(init_blocks), dim3(kBlock), 0, s, g, a);
+    d0 = 1;
+  }
+  const uint32_t chunks = (g.V + kBlock - 1) / kBlock;
+  const uint32_t bigblocks = (g.nbig + kWavesPerBlock - 1) / kWavesPerBlock;
+  for (uint32_t d = d0; d < d1; ++d) {
+    hipLaunchKernelGGL(msbfs_level_kernel<0>, dim3(a.nb * (chunks + bigblocks)), dim3(kBlock), 0, s,
+                       g, a, d);
+    hipLaunchKernelGGL(msbfs_settle_kernel<0>, dim3(a.nb * chunks), dim3(kBlock), 0, s, g, a, d);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_ksp_masks(const DevGraph& g, const MsArgs& a, const uint32_t* ign,
+                            const uint32_t* cnt, uint32_t stride, hipStream_t s) {
+  const uint32_t bx = std::max(1u, std::min(8u, (2u * stride + kBlock - 1) / kBlock));
+  for (uint32_t pass = 0; pass < 2; ++pass)
+    hipLaunchKernelGGL(ksp_mask_kernel, dim3(bx, a.nb * 64u), dim3(kBlock), 0, s, g, a, ign, cnt,
+                       stride, pass);
+  return hipGetLastError();
+}
 
 hipError_t launch_msbfs_round(int kp, const DevGraph& g, const MsArgs& a, uint32_t depth_bound,
                               hipStream_t s) {

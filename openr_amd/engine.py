@@ -27,8 +27,26 @@ def csr_struct(csr: Dict[str, np.ndarray]):
                    keep["row_ptr"].ctypes.data, keep["col"].ctypes.data,
                    keep["metric"].ctypes.data, keep["link_id"].ctypes.data,
                    keep["twin"].ctypes.data, keep["edge_up"].ctypes.data,
-                   keep["no_transit"].ctypes.data)
+                   keep["no_transit"].ctypes.data,
+                   keep["link_rank"].ctypes.data if "link_rank" in keep else None)
     return s, keep
+
+
+def decode_paths(recs: np.ndarray, status: np.ndarray, bad: int):
+    """KSP2 records -> per row a list of paths (lists of link ids), None when
+    `status & bad`."""
+    out = []
+    for rec, st in zip(recs, status):
+        if int(st) & bad:
+            out.append(None)
+            continue
+        paths, q = [], 1
+        for _ in range(int(rec[0])):
+            ln = int(rec[q])
+            paths.append([int(x) for x in rec[q + 1:q + 1 + ln]])
+            q += 1 + ln
+        out.append(paths)
+    return out
 
 
 class Engine:
@@ -136,6 +154,27 @@ class Engine:
                          flags, nh_words, max_root_neighbors, d_dist or None, d_nh or None,
                          d_digest or None)
         self._check(self._L.ospf_run_batch_dev(self._h, C.byref(b), stream or None))
+
+    def ksp2(self, src: int, dsts: Sequence[int], path_cap: int = 512):
+        """getKthPaths(src, d, 1) and (src, d, 2) for every d (ospf_ksp2_run).
+        Returns (k1, k2, status): per destination a list of paths (lists of
+        link ids, src -> dst) or None where status says the engine's budget
+        was exceeded, and the status words."""
+        dsts = np.ascontiguousarray(dsts, np.uint32)
+        n = dsts.size
+        k1 = np.zeros((max(n, 1), path_cap), np.uint32)
+        k2 = np.zeros_like(k1)
+        st = np.zeros(max(n, 1), np.uint32)
+        a = N.ospf_ksp2(src, dsts.ctypes.data, n, path_cap, k1.ctypes.data, k2.ctypes.data,
+                        st.ctypes.data)
+        self._check(self._L.ospf_ksp2_run(self._h, C.byref(a)))
+        return (decode_paths(k1[:n], st[:n], N.OSPF_KSP_OVF1),
+                decode_paths(k2[:n], st[:n], N.OSPF_KSP_OVF2 | N.OSPF_KSP_OVF1), st[:n])
+
+    def ksp2_dev(self, src: int, d_dsts: int, n: int, path_cap: int, d_k1: int, d_k2: int,
+                 d_status: int, stream: int = 0) -> None:
+        a = N.ospf_ksp2(src, d_dsts, n, path_cap, d_k1, d_k2, d_status)
+        self._check(self._L.ospf_ksp2_dev(self._h, C.byref(a), stream or None))
 
     def sync(self, stream: int = 0) -> None:
         self._check(self._L.ospf_sync(self._h, stream or None))

@@ -78,11 +78,70 @@ def test_random_graph_all_roots_spf_text(seed, unit, variant):
 
 
 @pytest.mark.parametrize("seed", range(4))
-def test_random_graph_ksp2_batch(seed, variant):
-    st, names = random_stream(100 + seed, n=30, p=0.25)
+@pytest.mark.parametrize("unit", [False, True])
+def test_random_graph_ksp2_batch(seed, unit, variant):
+    st, names = random_stream(100 + seed, n=30, p=0.25, unit=unit)
     o, p = both(st)
     for src in names[:5]:
         assert p.ksp2_text(src, names) == o.ksp2_text(src, names), src
+    assert p.spf_runs == o.spf_runs
+
+
+KSP_KNOBS = {
+    "default": {},
+    "rows": {"OSPF_KSP_ROWS": "1"},          # per-run reruns + trace over dist rows
+    "deep": {"OSPF_KSP_D0": "2"},            # level continuation past the first launch
+    "one_batch_rounds": {"OSPF_MS_NB": "1"},  # one 64-run batch per round
+    "tiny_records": {"ODL_KSP_CAP": "6"},     # record overflow -> host path per destination
+}
+
+
+@pytest.mark.parametrize("knob", list(KSP_KNOBS), ids=list(KSP_KNOBS))
+@pytest.mark.parametrize("unit", [True, False])
+@pytest.mark.parametrize("seed", range(3))
+def test_ksp2_device_trace_matches_oracle(seed, unit, knob, monkeypatch):
+    """Device KSP2 (ospf_ksp2_run: k = 1 trace, masked reruns, k = 2 trace)
+    through LinkState.prefetchKsp2, every destination of 90-node graphs with
+    parallel links, down links and overloaded nodes (several 64-run batches)."""
+    for k, v in KSP_KNOBS[knob].items():
+        monkeypatch.setenv(k, v)
+    st, names = random_stream(300 + seed, n=90, p=0.06, unit=unit)
+    o, p = both(st)
+    for src in names[:3]:
+        assert p.ksp2_text(src, names) == o.ksp2_text(src, names), src
+    assert p.spf_runs == o.spf_runs
+
+
+def test_fabric_ksp2_from_fsw_all_destinations():
+    """BASELINE config 4 shape (KSP2 from FSW "2-0-0" to every node), small."""
+    st = T.fabric(pods=8, planes=4)
+    o, p = both(st)
+    dsts = p.node_names()
+    assert p.ksp2_text("2-0-0", dsts) == o.ksp2_text("2-0-0", dsts)
+    assert p.spf_runs == o.spf_runs
+
+
+def test_engine_ksp2_budget_status():
+    """Records that do not fit path_cap come back flagged, not truncated."""
+    p, csr = _csr_of(T.fabric(pods=3, planes=2))
+    eng = Engine(0)
+    eng.load(csr)
+    names = p.node_names()
+    src = names.index("2-0-0")
+    k1, k2, st = eng.ksp2(src, list(range(len(names))), path_cap=512)
+    assert all(x is not None for x in k1) and all(x is not None for x in k2)
+    assert k1[src] == [] and k2[src] == []
+    assert all(len(k1[d]) >= 1 for d in range(len(names)) if d != src)
+    # every k = 1 path starts at src's links and is edge-disjoint from the others
+    for d in range(len(names)):
+        flat = [l for path in k1[d] for l in path]
+        assert len(flat) == len(set(flat))
+    k1s, k2s, sts = eng.ksp2(src, list(range(len(names))), path_cap=2)
+    for d in range(len(names)):
+        if d == src:
+            assert k1s[d] == [] and sts[d] == 0
+        else:
+            assert k1s[d] is None and k2s[d] is None and sts[d] & 0x2
 
 
 def test_unknown_and_isolated_roots():
