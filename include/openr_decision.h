@@ -49,6 +49,9 @@ int odl_apply(odl_ls* ls, const oadj_stream* s, uint32_t first, uint32_t count,
 char* odl_spf_text(odl_ls* ls, const char* root, int use_link_metric);
 char* odl_kth_paths_text(odl_ls* ls, const char* src, const char* dst, int k);
 char* odl_links_text(odl_ls* ls, const char* node);
+/* Keys of the snapshot's links in link id order (the ids of odl_csr_export
+ * and of the engine's KSP2 records), one per line. */
+char* odl_link_keys_text(odl_ls* ls);
 int64_t odl_metric_a_to_b(odl_ls* ls, const char* a, const char* b, int use_link_metric);
 int odl_is_overloaded(odl_ls* ls, const char* node);
 uint64_t odl_spf_runs(const odl_ls* ls);

@@ -32,7 +32,7 @@ ENGINE_SYMBOLS = [
 ]
 DECISION_SYMBOLS = [
     "odl_create", "odl_destroy", "odl_last_error", "odl_free", "odl_apply", "odl_spf_text",
-    "odl_kth_paths_text", "odl_links_text", "odl_metric_a_to_b", "odl_is_overloaded",
+    "odl_kth_paths_text", "odl_links_text", "odl_link_keys_text", "odl_metric_a_to_b", "odl_is_overloaded",
     "odl_spf_runs", "odl_num_nodes", "odl_num_links", "odl_spf_digests", "odl_spf_prefetch",
     "odl_ksp2_text", "odl_route_text", "odl_ucmp_text", "odl_csr_size", "odl_csr_export", "odl_node_name", "odl_node_id",
 ]
@@ -125,11 +125,12 @@ def decision() -> C.CDLL:
         L.odl_free.argtypes = [vp]
         L.odl_apply.argtypes = [vp, vp, u32, u32, vp]
         for f in ("odl_spf_text", "odl_kth_paths_text", "odl_links_text", "odl_ksp2_text",
-                  "odl_route_text", "odl_ucmp_text"):
+                  "odl_route_text", "odl_ucmp_text", "odl_link_keys_text"):
             getattr(L, f).restype = C.POINTER(C.c_char)
         L.odl_spf_text.argtypes = [vp, cp, i32]
         L.odl_kth_paths_text.argtypes = [vp, cp, cp, i32]
         L.odl_links_text.argtypes = [vp, cp]
+        L.odl_link_keys_text.argtypes = [vp]
         L.odl_ksp2_text.argtypes = [vp, cp, cp, u32]
         L.odl_route_text.argtypes = [vp, cp, cp, u32, i32]
         L.odl_ucmp_text.argtypes = [vp, cp, cp, u32, i32, i32]

@@ -165,6 +165,14 @@ char* odl_links_text(odl_ls* h, const char* node) {
   }, (char*)nullptr);
 }
 
+char* odl_link_keys_text(odl_ls* h) {
+  return guard(h, [&]() -> char* {
+    std::ostringstream os;
+    for (const auto& l : h->ls.snapshot().links) os << l->key() << '\n';
+    return dup(os.str());
+  }, (char*)nullptr);
+}
+
 int64_t odl_metric_a_to_b(odl_ls* h, const char* a, const char* b, int use_link_metric) {
   return guard(h, [&]() -> int64_t {
     auto m = h->ls.getMetricFromAToB(a, b, use_link_metric != 0);

@@ -663,7 +663,7 @@ void LinkState::prefetchKsp2(const std::string& src, const std::vector<std::stri
   // Device KSP2: SPF of src, k = 1 traces, masked reruns and k = 2 traces all
   // on the engine; records hold link ids. A destination over the engine's
   // budgets is computed by the host path below (same results, slower).
-  uint32_t kCap = 512;  // record words per destination and k
+  uint32_t kCap = 1024;  // record words per destination and k
   if (const char* x = getenv("ODL_KSP_CAP")) kCap = std::max(2, std::min(2048, atoi(x)));
   const size_t n = ids.size();
   std::vector<uint32_t> k1(n * kCap), k2(n * kCap), status(n);

@@ -42,6 +42,9 @@ struct ospf_ctx {
   void* d_stage = nullptr;
   size_t stage_bytes = 0;
   uint32_t* d_err = nullptr;
+  // KSP2: traces run on an engine stream, overlapping later reruns
+  hipStream_t aux = nullptr;
+  std::vector<hipEvent_t> ev;  // [2 * slots]: rerun done / trace done per slot
 };
 
 namespace {
@@ -253,6 +256,11 @@ int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
       sh.npass = (kcap + 32 * sh.OW - 1) / (32 * sh.OW);
     }
   }
+  if (!(flags & (OSPF_WANT_NH | OSPF_WANT_DIGEST))) {  // distances only: one pass, no planes used
+    sh.R = 64;
+    sh.PP = sh.OW = sh.npass = 1;
+    sh.KP = 8;
+  }
   const int kp = (int)sh.KP;
   const uint32_t npass = sh.npass;
   uint64_t rep = 0;
@@ -348,32 +356,49 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
   const uint32_t W = std::max<uint32_t>(1, (nn + 31) / 32);
   const bool ms = unit && c->g.n_lid && c->depth_bound <= 253 && !getenv("OSPF_KSP_ROWS");
   constexpr uint32_t lmax = 256;
+  const uint32_t dw = (V + 31) / 32;
   const size_t sz_ign = align_up((size_t)n * cap * 4ull, 256), sz_cnt = align_up(n * 4ull, 256),
                sz_one = align_up(V * 4ull, 256) + 256;
-  // rerun state: multi-source rounds, or per-run rows in chunks
+  // multi-source reruns: shared traversal state + igm, and a ring of `slots`
+  // (lev bytes, dead bitmaps) so round r's trace (engine stream) overlaps
+  // the reruns of rounds r+1 .. r+slots-1
   const size_t igw = ((size_t)c->g.E + 31) / 32;
-  const size_t per_vb = align_up((size_t)V * 8ull * 6 + V * 64ull + lmax * 8ull + igw * 4ull, 256) +
-                        align_up((size_t)c->g.E * 8ull, 256);
+  const size_t st_zero = (size_t)V * 8ull * 6 + lmax * 8ull + igw * 4ull;
+  const size_t per_vb = align_up(st_zero, 256) + align_up((size_t)c->g.E * 8ull, 256);
+  const size_t per_vb_slot = (size_t)V * 64ull + 64ull * dw * 4ull;
   uint32_t nb_cap = 96;
   if (const char* e = getenv("OSPF_MS_NB")) nb_cap = std::max(1, atoi(e));
-  nb_cap = (uint32_t)std::max<size_t>(1, std::min<size_t>(nb_cap, (6ull << 30) / per_vb));
+  nb_cap = (uint32_t)std::max<size_t>(1, std::min<size_t>(nb_cap, (6ull << 30) / (per_vb + per_vb_slot)));
   const uint32_t total_vb = (n + 63) / 64, nb_max = std::min(nb_cap, total_vb);
+  const uint32_t rounds = (total_vb + nb_max - 1) / nb_max;
+  uint32_t slots = (uint32_t)std::max<size_t>(
+      1, std::min<size_t>({(size_t)16, (size_t)rounds, (12ull << 30) / (per_vb_slot * nb_max)}));
+  if (const char* e = getenv("OSPF_KSP_SLOTS")) slots = std::max(1, std::min((int)slots, atoi(e)));
+  const size_t sz_lev = align_up((size_t)nb_max * V * 64ull, 256),
+               sz_sdead = align_up((size_t)nb_max * 64ull * dw * 4ull, 256) +
+                          align_up((nb_max * 64ull + 2) * 4ull, 256);
+  // per-run rows path (and k = 1 traces): dead bitmaps per trace launch
   uint32_t chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(n, (2ull << 30) / (V * 4ull)));
+  uint32_t tchunk = (uint32_t)std::max<size_t>(64, std::min<size_t>(n, (1ull << 30) / (dw * 4ull)));
+  chunk = std::min(chunk, tchunk);
+  const size_t sz_dead = align_up((size_t)tchunk * dw * 4ull, 256) + align_up((tchunk + 2) * 4ull, 256);
   const size_t sz_roots = align_up((size_t)(ms ? n : chunk) * 4ull, 256);
-  const size_t sz_state = ms ? per_vb * nb_max
+  const size_t sz_state = ms ? per_vb * nb_max + slots * (sz_lev + sz_sdead)
                              : align_up((size_t)chunk * V * 4ull, 256) + align_up((chunk + 1) * 4ull, 256);
   int rc = OSPF_OK;
-  char* sp = stream_scratch(c, s, sz_ign + sz_cnt + sz_one + sz_roots + sz_state, &rc, 1);
+  char* sp = stream_scratch(c, s, sz_ign + sz_cnt + sz_one + sz_roots + sz_dead + sz_state, &rc, 1);
   if (rc) return rc;
   uint32_t* d_ign = (uint32_t*)sp;
   uint32_t* d_cnt = (uint32_t*)(sp + sz_ign);
   uint32_t* d_dist1 = (uint32_t*)(sp + sz_ign + sz_cnt);
   uint32_t* d_src = (uint32_t*)(sp + sz_ign + sz_cnt + align_up(V * 4ull, 256));
   uint32_t* d_roots = (uint32_t*)(sp + sz_ign + sz_cnt + sz_one);
-  char* st = sp + sz_ign + sz_cnt + sz_one + sz_roots;
+  uint32_t* d_dead = (uint32_t*)(sp + sz_ign + sz_cnt + sz_one + sz_roots);
+  char* st = sp + sz_ign + sz_cnt + sz_one + sz_roots + sz_dead;
   HIPCHK(c, hipSetDevice(c->device));
 
-  // 1-2: SPF of src, k = 1
+  // 1-2: SPF of src (the multi-source BFS for one root beats a one-workgroup
+  // BFS on a large graph), k = 1 traces
   HIPCHK(c, hipMemsetD32Async(d_src, (int)src, 1, s));
   ospf_batch b1{};
   b1.d_roots = d_src;
@@ -382,7 +407,8 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
   b1.nh_words = W;
   b1.max_root_neighbors = nn;
   b1.d_dist = d_dist1;
-  rc = ospf_run_batch_dev(c, &b1, s);
+  rc = (unit && c->depth_bound <= 254 && V >= 4096) ? run_msbfs(c, &b1, s)
+                                                     : ospf_run_batch_dev(c, &b1, s);
   if (rc) return rc;
   ospf::TraceArgs t{};
   t.src = src;
@@ -397,14 +423,48 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
   t.status = k->status;
   t.k = 1;
   t.unit = unit ? 1u : 0u;
-  hipError_t e = ospf::launch_ksp_trace(false, c->g, t, s);
-  if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_trace k1");
+  t.dead = d_dead;
+  t.dead_words = dw;
+  // unit metric: runs past kTraceBudget DFS steps finish on the 16-wave kernel
+  constexpr uint32_t kTraceBudget = 1024;
+  t.budget = unit && !getenv("OSPF_KSP_NOHEAVY") ? kTraceBudget : 0u;
+  if (const char* x = getenv("OSPF_KSP_BUDGET"))  // test knob: send runs to the heavy kernel
+    if (t.budget) t.budget = (uint32_t)std::max(1, atoi(x));
+  t.heavy = (uint32_t*)((char*)d_dead + align_up((size_t)tchunk * dw * 4ull, 256));
+  t.heavy_ctr = t.heavy + tchunk;
+  hipError_t e = hipSuccess;
+  for (uint32_t c0 = 0; c0 < n; c0 += tchunk) {
+    ospf::TraceArgs tc = t;
+    tc.n = std::min(tchunk, n - c0);
+    tc.dsts = k->dsts + c0;
+    tc.out = k->k1 + (size_t)c0 * cap;
+    tc.ign_out = d_ign + (size_t)c0 * cap;
+    tc.cnt_out = d_cnt + c0;
+    tc.status = k->status + c0;
+    HIPCHK(c, hipMemsetAsync(d_dead, 0, (size_t)tc.n * dw * 4ull, s));
+    HIPCHK(c, hipMemsetAsync(t.heavy_ctr, 0, 8, s));
+    e = ospf::launch_ksp_trace(false, c->g, tc, s);
+    if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_trace k1");
+  }
 
   // 3: masked reruns + k = 2
   HIPCHK(c, hipMemsetD32Async(d_roots, (int)src, ms ? n : chunk, s));
   if (ms) {
+    if (!c->aux) HIPCHK(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+    while (c->ev.size() < 2 * (size_t)slots + 1) {
+      hipEvent_t x;
+      HIPCHK(c, hipEventCreateWithFlags(&x, hipEventDisableTiming));
+      c->ev.push_back(x);
+    }
+    hipEvent_t* ev_bfs = c->ev.data();
+    hipEvent_t* ev_tr = c->ev.data() + slots;
+    hipEvent_t ev_end = c->ev[2 * slots];
+    char* ring = st + per_vb * nb_max;
     std::vector<uint32_t> found;
-    for (uint32_t vb0 = 0; vb0 < total_vb; vb0 += nb_max) {
+    for (uint32_t r = 0, vb0 = 0; vb0 < total_vb; ++r, vb0 += nb_max) {
+      const uint32_t slot = r % slots;
+      uint8_t* lev = (uint8_t*)(ring + (size_t)slot * (sz_lev + sz_sdead));
+      uint32_t* dead = (uint32_t*)(ring + (size_t)slot * (sz_lev + sz_sdead) + sz_lev);
       ospf::MsArgs a{};
       a.roots = d_roots;
       a.n = n;
@@ -426,14 +486,16 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
       a.seen = a.front + 4ull * a.nb * V;
       a.accb = a.seen + (size_t)a.nb * V;
       a.planes = a.accb + (size_t)a.nb * V;
-      a.lev = (uint8_t*)a.planes;
-      a.found = (uint32_t*)(a.lev + (size_t)a.nb * V * 64ull);
+      a.found = (uint32_t*)a.planes;
       a.mass = a.found + (size_t)a.nb * lmax;
       a.igw = (uint32_t)igw;
       a.igb = a.mass + (size_t)a.nb * lmax;
       const size_t zero = (char*)(a.igb + (size_t)a.nb * igw) - st;
       a.igm = (uint64_t*)(st + align_up(zero, 256));
+      a.lev = lev;
       HIPCHK(c, hipMemsetAsync(st, 0, zero, s));
+      if (r >= slots) HIPCHK(c, hipStreamWaitEvent(s, ev_tr[slot], 0));  // slot's trace done
+      HIPCHK(c, hipMemsetAsync(lev, 0, (size_t)a.nb * V * 64ull, s));
       e = ospf::launch_ksp_masks(c->g, a, d_ign, d_cnt, cap, s);
       if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_masks");
       uint32_t d = std::max<uint32_t>(2, c->depth_bound);
@@ -452,7 +514,7 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
         for (uint32_t j = 0; j < a.nb; ++j)
           if (found[(size_t)j * lmax + d]) deep.push_back(j);
         if (deep.empty()) break;
-        if (d >= 254) {
+        if (d >= 254) {  // these runs keep OVF2: their levels stop at 254
           for (uint32_t j : deep) {
             const uint32_t r0 = (vb0 + j) * 64u;
             e = ospf::launch_or_bits(k->status + r0, std::min(64u, n - r0), OSPF_KSP_OVF2, s);
@@ -465,12 +527,14 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
         if (e != hipSuccess) return hip_fail(c, e, "launch_msbfs_ksp");
         d = d1;
       }
+      HIPCHK(c, hipEventRecord(ev_bfs[slot], s));
+      HIPCHK(c, hipStreamWaitEvent(c->aux, ev_bfs[slot], 0));
       const uint32_t r0 = vb0 * 64u;
       ospf::TraceArgs t2 = t;
       t2.dsts = k->dsts + r0;
       t2.n = std::min<uint32_t>(a.nb * 64u, n - r0);
       t2.rows = nullptr;
-      t2.lev = a.lev;
+      t2.lev = lev;
       t2.ign = d_ign + (size_t)r0 * cap;
       t2.ign_cnt = d_cnt + r0;
       t2.out = k->k2 + (size_t)r0 * cap;
@@ -478,11 +542,17 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
       t2.cnt_out = nullptr;
       t2.status = k->status + r0;
       t2.k = 2;
-      e = ospf::launch_ksp_trace(true, c->g, t2, s);
+      t2.dead = dead;
+      t2.heavy = (uint32_t*)((char*)dead + align_up((size_t)nb_max * 64ull * dw * 4ull, 256));
+      t2.heavy_ctr = t2.heavy + nb_max * 64u;
+      HIPCHK(c, hipMemsetAsync(dead, 0, (size_t)t2.n * dw * 4ull, c->aux));
+      HIPCHK(c, hipMemsetAsync(t2.heavy_ctr, 0, 8, c->aux));
+      e = ospf::launch_ksp_trace(true, c->g, t2, c->aux);
       if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_trace k2");
-      // runs whose levels went past 253 keep OVF2 (the trace skips nothing
-      // else: their lev bytes stop at 254)
+      HIPCHK(c, hipEventRecord(ev_tr[slot], c->aux));
     }
+    HIPCHK(c, hipEventRecord(ev_end, c->aux));
+    HIPCHK(c, hipStreamWaitEvent(s, ev_end, 0));
     c->spf_runs += n;
   } else {
     uint32_t* d_rows = (uint32_t*)st;
@@ -515,6 +585,8 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
       t2.cnt_out = nullptr;
       t2.status = k->status + r0;
       t2.k = 2;
+      HIPCHK(c, hipMemsetAsync(d_dead, 0, (size_t)t2.n * dw * 4ull, s));
+      HIPCHK(c, hipMemsetAsync(t2.heavy_ctr, 0, 8, s));
       e = ospf::launch_ksp_trace(false, c->g, t2, s);
       if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_trace k2");
     }
@@ -563,6 +635,8 @@ int ospf_close(ospf_ctx* c) {
     if (kv.second.p) hipFree(kv.second.p);
   if (c->d_stage) hipFree(c->d_stage);
   if (c->d_err) hipFree(c->d_err);
+  for (hipEvent_t e : c->ev) hipEventDestroy(e);
+  if (c->aux) hipStreamDestroy(c->aux);
   delete c;
   return OSPF_OK;
 }

@@ -167,6 +167,11 @@ struct TraceArgs {
   uint32_t* status;         // [n]
   uint32_t k;               // 1 or 2
   uint32_t unit;            // every usable metric is 1
+  uint32_t* dead;           // [n][dead_words] dead-node bits, zeroed by the caller
+  uint32_t dead_words;      // (V + 31) / 32
+  uint32_t budget;          // DFS steps before a run goes to the heavy kernel (0 = none)
+  uint32_t* heavy;          // [n] queued run indices
+  uint32_t* heavy_ctr;      // [2] {queued, taken}, zeroed by the caller
 };
 hipError_t launch_ksp_trace(bool lev, const DevGraph& g, const TraceArgs& t, hipStream_t s);
 // st[i] |= bits, i < n

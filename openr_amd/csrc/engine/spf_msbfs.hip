@@ -753,13 +753,13 @@ hipError_t launch_round_kp(const DevGraph& g, const MsArgs& a, uint32_t depth_bo
 __global__ void __launch_bounds__(256) ksp_mask_kernel(DevGraph g, MsArgs a, const uint32_t* ign,
                                                        const uint32_t* cnt, uint32_t stride,
                                                        uint32_t pass) {
-  const uint32_t j = blockIdx.y;  // run of the round
+  const uint32_t j = blockIdx.x * (blockDim.x / 64u) + (threadIdx.x >> 6);  // run of the round
   const uint32_t vbl = j / 64u, r = j % 64u;
   if (vbl >= a.nb) return;
   const uint32_t rix = (a.vb0 + vbl) * 64u + r;
   if (rix >= a.n) return;
   const uint32_t n = min(cnt[rix], stride);
-  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < 2u * n; k += gridDim.x * blockDim.x) {
+  for (uint32_t k = threadIdx.x & 63u; k < 2u * n; k += 64u) {  // one wave per run
     const uint32_t lid = ign[(size_t)rix * stride + k / 2u];
     if (lid >= g.n_lid) continue;
     const uint32_t e = g.link_e[2ull * lid + (k & 1u)];
@@ -795,10 +795,9 @@ hipError_t launch_msbfs_ksp(const DevGraph& g, const MsArgs& a, uint32_t d0, uin
 
 hipError_t launch_ksp_masks(const DevGraph& g, const MsArgs& a, const uint32_t* ign,
                             const uint32_t* cnt, uint32_t stride, hipStream_t s) {
-  const uint32_t bx = std::max(1u, std::min(8u, (2u * stride + kBlock - 1) / kBlock));
   for (uint32_t pass = 0; pass < 2; ++pass)
-    hipLaunchKernelGGL(ksp_mask_kernel, dim3(bx, a.nb * 64u), dim3(kBlock), 0, s, g, a, ign, cnt,
-                       stride, pass);
+    hipLaunchKernelGGL(ksp_mask_kernel, dim3(a.nb * 64u / kWavesPerBlock), dim3(kBlock), 0, s, g,
+                       a, ign, cnt, stride, pass);
   return hipGetLastError();
 }
 

@@ -136,6 +136,11 @@ class LinkState:
 
     linksFromNode = links
 
+    def link_keys(self) -> List[str]:
+        """Link keys of the current snapshot in link id order (ids of csr()
+        and of the engine's KSP2 records)."""
+        return self._take(self._L.odl_link_keys_text(self._h)).splitlines()
+
     def metric(self, a: str, b: str, use_link_metric: bool = True) -> Optional[int]:
         v = self._L.odl_metric_a_to_b(self._h, a.encode(), b.encode(), int(use_link_metric))
         if v == -2:

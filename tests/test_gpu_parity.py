@@ -93,6 +93,8 @@ KSP_KNOBS = {
     "deep": {"OSPF_KSP_D0": "2"},            # level continuation past the first launch
     "one_batch_rounds": {"OSPF_MS_NB": "1"},  # one 64-run batch per round
     "tiny_records": {"ODL_KSP_CAP": "6"},     # record overflow -> host path per destination
+    "heavy": {"OSPF_KSP_BUDGET": "3"},        # most runs resumed by the 16-wave kernel
+    "no_heavy": {"OSPF_KSP_NOHEAVY": "1"},    # single-wave DFS only
 }
 
 
@@ -112,8 +114,12 @@ def test_ksp2_device_trace_matches_oracle(seed, unit, knob, monkeypatch):
     assert p.spf_runs == o.spf_runs
 
 
-def test_fabric_ksp2_from_fsw_all_destinations():
-    """BASELINE config 4 shape (KSP2 from FSW "2-0-0" to every node), small."""
+@pytest.mark.parametrize("budget", ["default", "3"])
+def test_fabric_ksp2_from_fsw_all_destinations(budget, monkeypatch):
+    """BASELINE config 4 shape (KSP2 from FSW "2-0-0" to every node), small;
+    budget 3 resumes nearly every trace on the 16-wave kernel."""
+    if budget != "default":
+        monkeypatch.setenv("OSPF_KSP_BUDGET", budget)
     st = T.fabric(pods=8, planes=4)
     o, p = both(st)
     dsts = p.node_names()
