@@ -426,7 +426,7 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
   t.dead = d_dead;
   t.dead_words = dw;
   // unit metric: runs past kTraceBudget DFS steps finish on the 16-wave kernel
-  constexpr uint32_t kTraceBudget = 1024;
+  constexpr uint32_t kTraceBudget = 256;
   t.budget = unit && !getenv("OSPF_KSP_NOHEAVY") ? kTraceBudget : 0u;
   if (const char* x = getenv("OSPF_KSP_BUDGET"))  // test knob: send runs to the heavy kernel
     if (t.budget) t.budget = (uint32_t)std::max(1, atoi(x));

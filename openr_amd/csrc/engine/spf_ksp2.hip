@@ -315,8 +315,9 @@ __device__ bool trace_setup(const DevGraph& g, const TraceArgs& t, uint32_t i, u
   return true;
 }
 
-// one wave per run; a run over the step budget (t.budget, unit metric) is
-// queued for ksp_heavy_kernel, which resumes it with 16 waves
+// one wave per run; a run that spends more than t.budget DFS steps (unit
+// metric) without finding a path -- a long failing search -- is queued for
+// ksp_heavy_kernel, which resumes it with 16 waves
 template <bool LEV>
 __global__ void __launch_bounds__(256) ksp_trace_kernel(DevGraph g, TraceArgs t) {
   __shared__ uint32_t s_stack[kWaves][kStack];
@@ -343,6 +344,7 @@ __global__ void __launch_bounds__(256) ksp_trace_kernel(DevGraph g, TraceArgs t)
       return;
     }
     if (r < 0 || !tr.emit(out, stk, depth, w, npaths, nclaim)) ovf = true;
+    if (t.budget) steps = 0;  // the budget bounds the steps between two paths
   }
   tr.finish(out, npaths, ovf, tr.hs);
 }
@@ -400,15 +402,30 @@ __global__ void __launch_bounds__(1024) ksp_heavy_kernel(DevGraph g, TraceArgs t
       int winner = -1;
       bool stop = false;
       for (;;) {  // dst's candidates, 16 at a time
-        if (wv == 0) {
+        if (wv == 0) {  // the next (up to) 16 candidates of dst in row order
           uint32_t m = 0;
           const uint32_t dv = tr.dist(tr.dst);
-          for (; m < kHeavyWaves; ++m) {
-            const uint64_t key = tr.next_cand(tr.dst, dv, lo);
-            if (key == ~0ull) break;
-            s_cand[m] = key;
-            lo = key + 1ull;
+          const uint32_t beg = g.row_ptr[tr.dst], end = g.row_ptr[tr.dst + 1];
+          uint32_t base = lo ? max(beg, (uint32_t)lo) : beg;
+          for (; base < end && m < kHeavyWaves; base += kWave) {
+            const uint32_t e = base + lane;
+            uint32_t du = 0;
+            const bool ok = e < end && tr.cand(tr.dst, dv, e, du);
+            const uint64_t bal = __ballot(ok);
+            const uint32_t rank = m + __popcll(bal & ((1ull << lane) - 1ull));
+            if (ok && rank < kHeavyWaves) s_cand[rank] = ((uint64_t)(dv - 1u) << 32) | e;
+            const uint32_t got = m + (uint32_t)__popcll(bal);
+            if (got >= kHeavyWaves) {  // resume after the 16th
+              uint64_t b2 = bal;
+              for (uint32_t k = m; k < kHeavyWaves - 1u; ++k) b2 &= b2 - 1ull;
+              base += (uint32_t)(__ffsll((unsigned long long)b2) - 1) + 1u - kWave;
+              m = kHeavyWaves;
+              base += kWave;
+              break;
+            }
+            m = got;
           }
+          lo = ((uint64_t)(dv - 1u) << 32) | min(base, end);
           s_ctl[2] = m;
         }
         __syncthreads();
@@ -432,7 +449,6 @@ __global__ void __launch_bounds__(1024) ksp_heavy_kernel(DevGraph g, TraceArgs t
           else winner = (int)k;
           break;
         }
-        if (wv == 0) lo = __shfl(lo, 0);  // (wave 0 owns the cursor)
       }
       __syncthreads();
       if (ovf || stop || winner < 0) break;
@@ -481,7 +497,7 @@ hipError_t launch_ksp_trace(bool lev, const DevGraph& g, const TraceArgs& t, hip
   else
     hipLaunchKernelGGL(ksp_trace_kernel<false>, grid, dim3(kBlock), 0, s, g, t);
   if (t.budget) {  // heavy runs queued by the pass above (counters zeroed by the caller)
-    const dim3 hg(std::min<uint32_t>(128u, t.n));
+    const dim3 hg(std::min<uint32_t>(512u, t.n));  // 2 per CU
     if (lev)
       hipLaunchKernelGGL(ksp_heavy_kernel<true>, hg, dim3(64 * kHeavyWaves), 0, s, g, t);
     else
