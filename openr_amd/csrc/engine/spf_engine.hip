@@ -124,6 +124,7 @@ Plan make_plan(const ospf_ctx* c, uint32_t W, uint32_t ign_cap, bool unit, uint3
       case 3: return unit && bfs_nh <= lim;
       case 4: return unit && bfs <= lim;
       case 5: return unit && ign_cap == 0;
+      case 6: return !unit && c->info.max_metric + 1 <= ospf::kMaxDialRing;
     }
     return false;
   };
@@ -134,17 +135,19 @@ Plan make_plan(const ospf_ctx* c, uint32_t W, uint32_t ign_cap, bool unit, uint3
   } else if (unit) {
     p.variant = (W == 1 && fits(3)) ? 3 : fits(4) ? 4 : 2;
   } else {
-    p.variant = fits(0) ? 0 : fits(1) ? 1 : 2;
+    // beyond LDS: frontier lists (variant 6) instead of a scan of every node
+    // per distance value (variant 2)
+    p.variant = fits(0) ? 0 : fits(1) ? 1 : fits(6) ? 6 : 2;
   }
   // test/benchmark knob: OSPF_FORCE_VARIANT=0..4 forces a kernel variant when
   // its state fits (e.g. the HBM-state Dial kernel on a small graph).
   if (const char* f = getenv("OSPF_FORCE_VARIANT")) {
     const int want = atoi(f);
-    if (want >= 0 && want <= 5 && fits(want)) p.variant = want;
+    if (want >= 0 && want <= 6 && fits(want)) p.variant = want;
   }
-  const size_t ldsz[6] = {full, half, head, bfs_nh, bfs, 0};
+  const size_t ldsz[7] = {full, half, head, bfs_nh, bfs, 0, head};
   p.lds = ldsz[p.variant];
-  if (p.variant == 5)
+  if (p.variant == 5 || p.variant == 6)
     p.block = 256;
   else if (p.variant >= 3)
     p.block = p.lds > 80 * 1024 ? 1024 : (V >= 4096 ? 512 : 256);
@@ -843,7 +846,7 @@ int ospf_plan_n(const ospf_ctx* c, uint32_t flags, uint32_t nh_words, uint32_t m
     const uint32_t kcap = max_root_neighbors ? std::min(max_root_neighbors, 32u * W) : 32u * W;
     out->slices = ms_shape(n_roots, kcap, c->depth_bound <= 254 && getenv("OSPF_MS_PACK")).npass;
   } else {
-    out->slices = p.variant >= 3 ? ospf::bfs_slices(W) : 1u;
+    out->slices = (p.variant == 3 || p.variant == 4) ? ospf::bfs_slices(W) : 1u;
   }
   return OSPF_OK;
 }
@@ -888,11 +891,16 @@ int ospf_run_batch_dev(ospf_ctx* c, const ospf_batch* b, void* stream) {
   size_t need = 0;
   const bool dist_scratch = (p.variant >= 2) && !(flags & OSPF_WANT_DIST);
   const bool nh_scratch = (p.variant >= 1) && !(flags & OSPF_WANT_NH);
-  const uint32_t slices = p.variant >= 3 ? ospf::bfs_slices(nh_words) : 1u;
+  const uint32_t slices = (p.variant == 3 || p.variant == 4) ? ospf::bfs_slices(nh_words) : 1u;
   const size_t planes_bytes = slices > 1 ? align_up((size_t)n_roots * slices * V * 16ull, 256) : 0;
   if (dist_scratch) need += align_up(n_roots * V * 4, 256);
   if (nh_scratch) need += align_up(n_roots * V * nh_words * 4ull, 256);
   need += planes_bytes;
+  // variant 6: per-root frontier lists
+  const uint32_t nbk = c->info.max_metric + 1;
+  const uint32_t bcap = (uint32_t)std::min<uint64_t>(V, 16384);
+  const size_t bkt_bytes = p.variant == 6 ? align_up((size_t)n_roots * nbk * bcap * 4ull, 256) : 0;
+  need += bkt_bytes;
   int src = OSPF_OK;
   char* sp = need ? stream_scratch(c, stream, need, &src) : nullptr;
   if (src) return src;
@@ -914,6 +922,12 @@ int ospf_run_batch_dev(ospf_ctx* c, const ospf_batch* b, void* stream) {
     a.planes = (uint32_t*)sp;
     sp += planes_bytes;
   }
+  if (bkt_bytes) {
+    a.bkt = (uint32_t*)sp;
+    a.bcap = bcap;
+    a.nbk = nbk;
+    sp += bkt_bytes;
+  }
   if (dist_scratch) {
     a.dist = (uint32_t*)sp;
     sp += align_up(n_roots * V * 4, 256);
@@ -925,7 +939,9 @@ int ospf_run_batch_dev(ospf_ctx* c, const ospf_batch* b, void* stream) {
   HIPCHK(c, hipSetDevice(c->device));
   if (a.slices > 1 && (flags & OSPF_WANT_DIGEST))  // slices add into the records
     HIPCHK(c, hipMemsetAsync(d_digest, 0, n_roots * sizeof(ospf_digest), (hipStream_t)stream));
-  hipError_t e = p.variant >= 3
+  hipError_t e = p.variant == 6
+      ? ospf::launch_dial(ign, c->g, a, n_roots, p.lds, (hipStream_t)stream)
+      : p.variant >= 3
       ? ospf::launch_bfs(p.variant == 3, ign, c->g, a, n_roots, p.block, p.lds, (hipStream_t)stream)
       : ospf::launch_spf(p.variant, unit, ign, c->g, a, n_roots, p.block, p.lds,
                          (hipStream_t)stream);

@@ -56,7 +56,10 @@ struct RunArgs {
   uint32_t* err;            // device error word (bit0: nh words, bit1: ignore cap)
   uint32_t slices;          // BFS kernel: workgroups per run (4-word next-hop slices)
   uint32_t* planes;         // BFS kernel, slices > 1: [n_roots][slices][V][4] scratch
+  uint32_t* bkt;            // bucketed Dial: [n_roots][nbk][bcap] frontier lists
+  uint32_t bcap, nbk;       //   list capacity, ring size (max_metric + 1)
 };
+constexpr uint32_t kMaxDialRing = 64;  // bucketed Dial: metrics up to 63
 
 // Digest, mod 2^64, a sum of independent terms:
 //   sum over reached v of  dist_key(v) * (dist + 1)
@@ -93,6 +96,11 @@ __host__ __device__ inline uint64_t digest_word_term(uint32_t v, uint32_t g, uin
 //   variant 0 = LDS dist + LDS nh, 1 = LDS dist + HBM nh, 2 = HBM dist + HBM nh
 hipError_t launch_spf(int variant, bool unit, bool ign, const DevGraph& g, const RunArgs& a,
                       uint32_t n_roots, uint32_t block, size_t lds_bytes, hipStream_t s);
+
+// Bucketed Dial (spf_dial.hip), variant 6: any metric <= 63, HBM state,
+// frontier lists instead of a per-distance scan of every node.
+hipError_t launch_dial(bool ign, const DevGraph& g, const RunArgs& a, uint32_t n_roots,
+                       size_t lds, hipStream_t s);
 
 // BFS kernel (spf_bfs.hip), unit metric / hop count, LDS bitmaps:
 //   nh_lds = variant 3 (byte next-hops in LDS for roots with <= 8 neighbours),

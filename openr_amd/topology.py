@@ -186,8 +186,31 @@ def _add_one_sided(st: AdjDbStream, names, src, dst) -> AdjDbStream:
     return AdjDbStream.from_dbs(dbs)
 
 
+def hilbert_index(x: np.ndarray, y: np.ndarray, order: int) -> np.ndarray:
+    """Position of integer points (0 <= x, y < 2**order) along a Hilbert curve."""
+    n = 1 << order
+    x = x.astype(np.int64).copy()
+    y = y.astype(np.int64).copy()
+    d = np.zeros_like(x)
+    s = n >> 1
+    while s > 0:
+        rx = (x & s) > 0
+        ry = (y & s) > 0
+        d += s * s * ((3 * rx.astype(np.int64)) ^ ry.astype(np.int64))
+        flip = ~ry & rx
+        x = np.where(flip, n - 1 - x, x)
+        y = np.where(flip, n - 1 - y, y)
+        x, y = np.where(~ry, y, x), np.where(~ry, x, y)
+        s >>= 1
+    return d
+
+
 def mesh(n_points: int, seed: int = 42, mean_degree: float = 8.0) -> AdjDbStream:
-    """Random geometric mesh (largest component), metric in [1, 16]."""
+    """Random geometric mesh (largest component), metric in [1, 16] (SURVEY.md
+    §8d M1M). Node names m%07d follow a Hilbert curve over the square, so
+    spatially near nodes get near names and near node ids (the engine's id =
+    name rank): a shortest-path wavefront then walks through nearby memory.
+    The reference leaves the naming of this synthetic topology open."""
     rng = np.random.default_rng(seed)
     pts = rng.random((n_points, 2))
     r = float(np.sqrt(mean_degree / (np.pi * n_points)))
@@ -233,7 +256,10 @@ def mesh(n_points: int, seed: int = 42, mean_degree: float = 8.0) -> AdjDbStream
     big = np.bincount(roots).argmax()
     alive = roots == big
     newid = -np.ones(n_points, np.int64)
-    newid[alive] = np.arange(alive.sum())
+    keep_idx = np.nonzero(alive)[0]
+    q = np.minimum((pts[keep_idx] * 1024).astype(np.int64), 1023)
+    newid[keep_idx[np.argsort(hilbert_index(q[:, 0], q[:, 1], 10), kind="stable")]] = \
+        np.arange(keep_idx.size)
     m = alive[a]
     a, b, d = newid[a[m]], newid[b[m]], d[m]
     rtt = 100.0 + 1500.0 * d / r

@@ -1,0 +1,5 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -m gpu -k "variant or mesh or ksp2" > gpurun_out/s22_pytest.log 2>&1 || { echo PYTEST_FAIL; tail -40 gpurun_out/s22_pytest.log; exit 1; }
+tail -2 gpurun_out/s22_pytest.log
+bash scripts/gpu_mesh_bench.sh

@@ -18,13 +18,14 @@ pytestmark = pytest.mark.gpu
 FIXTURES = load_fixtures()
 
 
-@pytest.fixture(params=["auto", "0", "1", "2", "4", "5"])
+@pytest.fixture(params=["auto", "0", "1", "2", "4", "5", "6"])
 def variant(request, monkeypatch):
     """Run each parity test with the planner's choice and with every other
     kernel variant forced where its state fits (OSPF_FORCE_VARIANT): 0/1/2 =
     Dial kernel (LDS / mixed / HBM state), 3/4 = BFS kernel (LDS bitmaps,
     byte next-hops in LDS / next-hops in HBM; unit metric only), 5 =
-    multi-source bit-parallel BFS (unit metric, no ignored links)."""
+    multi-source bit-parallel BFS (unit metric, no ignored links), 6 =
+    bucketed Dial (frontier lists; any metric <= 63)."""
     if request.param == "auto":
         monkeypatch.delenv("OSPF_FORCE_VARIANT", raising=False)
     else:
@@ -243,6 +244,22 @@ def test_mesh_sampled_digests():
     rng = np.random.default_rng(0x5eed)
     roots = [names[i] for i in rng.choice(len(names), 16, replace=False)]
     assert np.array_equal(p.digests(roots), o.digests(roots, threads=8))
+
+
+def test_mesh_60k_bucketed_dial_digests():
+    """Weighted mesh too large for LDS state: the planner's bucketed Dial
+    (variant 6) against the oracle, sampled roots, digests (dist + next hops)."""
+    st = T.mesh(60000, seed=7)
+    o, p = both(st)
+    names = p.node_names()
+    rng = np.random.default_rng(11)
+    roots = [names[i] for i in rng.choice(len(names), 12, replace=False)]
+    eng = Engine(0)
+    eng.load(p.csr())
+    assert eng.plan(1)["variant"] == 6
+    assert np.array_equal(p.digests(roots), o.digests(roots, threads=8))
+    for r in roots[:2]:
+        assert p.spf_text(r) == o.spf_text(r)
 
 
 def test_fabric_ksp2_batch_from_rsw():
