@@ -55,6 +55,11 @@ char* odl_link_keys_text(odl_ls* ls);
 int64_t odl_metric_a_to_b(odl_ls* ls, const char* a, const char* b, int use_link_metric);
 int odl_is_overloaded(odl_ls* ls, const char* node);
 uint64_t odl_spf_runs(const odl_ls* ls);
+/* Incremental mode (off by default; odl::LinkState::setIncremental): keep the
+ * memoised SPF of roots a metric / up / overload-only update cannot affect.
+ * Stats: {patches applied, results kept, results dropped}. */
+void odl_set_incremental(odl_ls* ls, int on);
+void odl_incremental_stats(const odl_ls* ls, uint64_t* out3);
 uint32_t odl_num_nodes(const odl_ls* ls);
 uint32_t odl_num_links(const odl_ls* ls);
 

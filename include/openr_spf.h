@@ -228,6 +228,54 @@ int ospf_ksp2_run(ospf_ctx* ctx, const ospf_ksp2* args);
  * graph's static depth bound. */
 int ospf_ksp2_dev(ospf_ctx* ctx, const ospf_ksp2* args, void* stream);
 
+/* Incremental updates (Decision.cpp:918-996 re-runs SPF after
+ * every debounced adjacency batch; LinkState clears every memoised result on
+ * a topology change, LinkState.cpp:751-754). When a batch changes only link
+ * metrics, link up/down state or node overload bits -- no link or node added
+ * or removed -- the resident device CSR is patched in place instead of
+ * reloaded, and ospf_affected_roots tells which of a set of finished runs can
+ * differ under the new state; the others are bit-identical and need no rerun.
+ *
+ * Link update: the two CSR entries of link_id get Link::isUp() = up and the
+ * metrics advertised by each endpoint (metric_lo: the endpoint with the lower
+ * node id). Node update: LinkState::isNodeOverloaded. `version` is the
+ * caller's new topology version. */
+typedef struct ospf_link_update {
+  uint32_t link_id;
+  uint32_t up;
+  uint32_t metric_lo;
+  uint32_t metric_hi;
+} ospf_link_update;
+int ospf_update_links(ospf_ctx* ctx, const ospf_link_update* updates, uint32_t n,
+                      uint64_t version);
+int ospf_update_nodes(ospf_ctx* ctx, const uint32_t* nodes, const uint8_t* no_transit,
+                      uint32_t n, uint64_t version);
+
+/* One change of a batch, for ospf_affected_roots. LINK: endpoints a, b;
+ * before / after: up, metric advertised by a (w_ab) and by b (w_ba). NODE:
+ * node a changed its overload bit (either way). */
+#define OSPF_CHANGE_LINK 0u
+#define OSPF_CHANGE_NODE 1u
+typedef struct ospf_change {
+  uint32_t kind;
+  uint32_t a, b;
+  uint32_t up0, w_ab0, w_ba0;
+  uint32_t up1, w_ab1, w_ba1;
+} ospf_change;
+/* Which finished runs can change: d_dist = their distance rows ([n_roots][V],
+ * device, computed before the batch), flags as the runs were made (only
+ * OSPF_HOP_COUNT is read); d_affected[i] = 1 if run i must be re-run, 0 if
+ * its dist / next hops / pathLinks are unchanged. Run i is unaffected when no
+ * changed link was tight for it before (dist(a) + w_ab0 == dist(b), or the
+ * reverse) nor reaches or ties a distance after (dist(a) + w_ab1 <= dist(b),
+ * or the reverse), and every re-flagged node either is unreached, is the root,
+ * or has no up link (x, y) with dist(x) + w(x -> y) <= dist(y) (transit
+ * conditions are ignored: the answer errs towards re-running). Graph state
+ * read for node changes: the current (patched) one. Queued on `stream`. */
+int ospf_affected_roots(ospf_ctx* ctx, const uint32_t* d_dist, uint32_t n_roots, uint32_t flags,
+                        const ospf_change* changes, uint32_t n_changes, uint8_t* d_affected,
+                        void* stream);
+
 /* Runtime statistics. spf_runs counts logical runSpf executions (one per
  * root per batch), matching the reference's decision.spf_runs counter
  * (LinkState.cpp:843). */

@@ -28,12 +28,13 @@ ENGINE_SYMBOLS = [
     "ospf_open", "ospf_close", "ospf_last_error", "ospf_load_graph", "ospf_graph_info_get",
     "ospf_root_neighbors", "ospf_sssp_batch", "ospf_sssp_batch_dev", "ospf_sync",
     "ospf_plan_variant", "ospf_plan", "ospf_plan_n", "ospf_spf_runs", "ospf_run_batch_dev",
-    "ospf_ksp2_run", "ospf_ksp2_dev",
+    "ospf_ksp2_run", "ospf_ksp2_dev", "ospf_update_links", "ospf_update_nodes",
+    "ospf_affected_roots",
 ]
 DECISION_SYMBOLS = [
     "odl_create", "odl_destroy", "odl_last_error", "odl_free", "odl_apply", "odl_spf_text",
     "odl_kth_paths_text", "odl_links_text", "odl_link_keys_text", "odl_metric_a_to_b", "odl_is_overloaded",
-    "odl_spf_runs", "odl_num_nodes", "odl_num_links", "odl_spf_digests", "odl_spf_prefetch",
+    "odl_spf_runs", "odl_set_incremental", "odl_incremental_stats", "odl_num_nodes", "odl_num_links", "odl_spf_digests", "odl_spf_prefetch",
     "odl_ksp2_text", "odl_route_text", "odl_ucmp_text", "odl_csr_size", "odl_csr_export", "odl_node_name", "odl_node_id",
 ]
 
@@ -64,6 +65,18 @@ class ospf_ksp2(C.Structure):  # noqa: N801
 
 
 OSPF_KSP_RERUN, OSPF_KSP_OVF1, OSPF_KSP_OVF2 = 0x1, 0x2, 0x4
+
+
+class ospf_link_update(C.Structure):  # noqa: N801
+    _fields_ = [("link_id", u32), ("up", u32), ("metric_lo", u32), ("metric_hi", u32)]
+
+
+OSPF_CHANGE_LINK, OSPF_CHANGE_NODE = 0, 1
+
+
+class ospf_change(C.Structure):  # noqa: N801
+    _fields_ = [("kind", u32), ("a", u32), ("b", u32), ("up0", u32), ("w_ab0", u32),
+                ("w_ba0", u32), ("up1", u32), ("w_ab1", u32), ("w_ba1", u32)]
 
 
 class ospf_plan_info(C.Structure):  # noqa: N801
@@ -107,6 +120,9 @@ def engine() -> C.CDLL:
         L.ospf_run_batch_dev.argtypes = [vp, C.POINTER(ospf_batch), vp]
         L.ospf_ksp2_run.argtypes = [vp, C.POINTER(ospf_ksp2)]
         L.ospf_ksp2_dev.argtypes = [vp, C.POINTER(ospf_ksp2), vp]
+        L.ospf_update_links.argtypes = [vp, vp, u32, u64]
+        L.ospf_update_nodes.argtypes = [vp, vp, vp, u32, u64]
+        L.ospf_affected_roots.argtypes = [vp, vp, u32, u32, vp, u32, vp, vp]
         L.ospf_spf_runs.argtypes = [vp]
         L.ospf_spf_runs.restype = u64
         _engine = L
@@ -139,6 +155,10 @@ def decision() -> C.CDLL:
         L.odl_is_overloaded.argtypes = [vp, cp]
         L.odl_spf_runs.argtypes = [vp]
         L.odl_spf_runs.restype = u64
+        L.odl_set_incremental.argtypes = [vp, i32]
+        L.odl_set_incremental.restype = None
+        L.odl_incremental_stats.argtypes = [vp, vp]
+        L.odl_incremental_stats.restype = None
         L.odl_num_nodes.argtypes = [vp]
         L.odl_num_nodes.restype = u32
         L.odl_num_links.argtypes = [vp]

@@ -184,6 +184,16 @@ int odl_is_overloaded(odl_ls* h, const char* node) {
   return h ? (h->ls.isNodeOverloaded(node) ? 1 : 0) : -1;
 }
 uint64_t odl_spf_runs(const odl_ls* h) { return h ? h->ls.spfRuns() : 0; }
+void odl_set_incremental(odl_ls* h, int on) {
+  if (h) h->ls.setIncremental(on != 0);
+}
+void odl_incremental_stats(const odl_ls* h, uint64_t* out) {
+  if (!h || !out) return;
+  const auto& st = h->ls.incrementalStats();
+  out[0] = st.patches;
+  out[1] = st.kept;
+  out[2] = st.dropped;
+}
 uint32_t odl_num_nodes(const odl_ls* h) { return h ? (uint32_t)h->ls.numNodes() : 0; }
 uint32_t odl_num_links(const odl_ls* h) { return h ? (uint32_t)h->ls.numLinks() : 0; }
 

@@ -184,7 +184,11 @@ void LinkState::invalidate() {
 LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db) {
   LinkStateChange ch;
   const std::string me = db.thisNodeName;
-  const int32_t priorLabel = adjDbs_.count(me) ? adjDbs_.at(me).nodeLabel : 0;
+  const bool known = adjDbs_.count(me) > 0;
+  const int32_t priorLabel = known ? adjDbs_.at(me).nodeLabel : 0;
+  bool structural = !known;  // a link or node added / removed (incremental mode)
+  std::vector<LinkDelta> deltas;
+  std::vector<std::string> nodeDeltas;
   adjDbs_[me] = db;
   auto& idx = adjIndex_[me];
   idx.clear();
@@ -207,6 +211,7 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db) 
   } else if (ov->second != db.isOverloaded) {
     ov->second = db.isOverloaded;
     ch.topologyChanged = true;
+    nodeDeltas.push_back(me);
   }
   ch.nodeLabelChanged = priorLabel != db.nodeLabel;
 
@@ -217,17 +222,23 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db) 
     const bool takeOld = !takeNew && j < before.size() &&
                          (i == after.size() || before[j]->orderedBefore(*after[i]));
     if (takeNew) {
+      structural = true;
       ch.topologyChanged |= after[i]->isUp();
       addLink(after[i]);
       ch.addedLinks.push_back(after[i]);
       ++i;
     } else if (takeOld) {
+      structural = true;
       ch.topologyChanged |= before[j]->isUp();
       removeLink(before[j]);
       ++j;
     } else {
       const Link& fresh = *after[i];
       Link& kept = *before[j];
+      if (fresh.metricFrom(me) != kept.metricFrom(me) ||
+          fresh.overloadFrom(me) != kept.overloadFrom(me))
+        deltas.push_back(LinkDelta{before[j], kept.isUp(), kept.metricFrom(kept.lowNode()),
+                                   kept.metricFrom(kept.highNode())});
       if (fresh.metricFrom(me) != kept.metricFrom(me))
         ch.topologyChanged |= kept.setMetricFrom(me, fresh.metricFrom(me));
       if (fresh.overloadFrom(me) != kept.overloadFrom(me))
@@ -243,6 +254,11 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db) 
       ++i;
       ++j;
     }
+  }
+  // Incremental mode: same nodes and links, CSR current -> patch in place
+  if (incremental_ && !structural && snapVersion_ == version_) {
+    if (ch.topologyChanged) applyIncremental(deltas, nodeDeltas);
+    return ch;
   }
   // Memo survives non-topology updates exactly as in the reference
   // (LinkState.cpp:721-724); the CSR is re-snapshotted on any update because
@@ -696,6 +712,90 @@ void LinkState::prefetchKsp2(const std::string& src, const std::vector<std::stri
     }
     if (status[i] & OSPF_KSP_RERUN) ++spfRuns_;  // runSpf(src, true, linksToIgnore)
     memoKsp_.emplace(kspKey(src, d, 2), decode(&k2[i * kCap]));
+  }
+}
+
+// ---------------------------------------------------------------- incremental
+void LinkState::applyIncremental(const std::vector<LinkDelta>& links,
+                                 const std::vector<std::string>& nodes) {
+  ++incStats_.patches;
+  constexpr uint64_t kInf64 = ~0ull;
+  auto distOf = [](const SpfResult& r, const std::string& n) -> uint64_t {
+    auto it = r.find(n);
+    return it == r.end() ? kInf64 : it->second.metric();
+  };
+  // the rule of ospf_affected_roots (include/openr_spf.h), on a memoised result
+  auto affected = [&](const std::string& root, const SpfResult& r, bool hop) {
+    for (const auto& d : links) {
+      const Link& l = *d.link;
+      const uint64_t da = distOf(r, l.lowNode()), db = distOf(r, l.highNode());
+      const uint64_t w0ab = hop ? 1 : d.mlo0, w0ba = hop ? 1 : d.mhi0;
+      const uint64_t w1ab = hop ? 1 : l.metricFrom(l.lowNode()),
+                     w1ba = hop ? 1 : l.metricFrom(l.highNode());
+      if (d.up0 && da != kInf64 && da + w0ab == db) return true;
+      if (d.up0 && db != kInf64 && db + w0ba == da) return true;
+      if (l.isUp() && da != kInf64 && da + w1ab <= db) return true;
+      if (l.isUp() && db != kInf64 && db + w1ba <= da) return true;
+    }
+    for (const auto& x : nodes) {
+      const uint64_t dx = distOf(r, x);
+      if (dx == kInf64 || x == root) continue;
+      for (const auto& l : linksFromNode(x)) {
+        if (!l->isUp()) continue;
+        if (dx + (hop ? 1 : l->metricFrom(x)) <= distOf(r, l->otherNode(x))) return true;
+      }
+    }
+    return false;
+  };
+  for (int mode = 0; mode < 2; ++mode) {
+    auto& memo = mode == 0 ? memoMetric_ : memoHops_;
+    for (auto it = memo.begin(); it != memo.end();) {
+      if (affected(it->first, it->second, mode == 1)) {
+        if (mode == 0) rawMetric_.erase(it->first);
+        it = memo.erase(it);
+        ++incStats_.dropped;
+      } else {
+        ++it;
+        ++incStats_.kept;
+      }
+    }
+  }
+  memoKsp_.clear();  // KSP2 masked reruns are not tracked
+  // CSR + device graph, in place (same ids, same links)
+  std::vector<ospf_link_update> ups;
+  for (const auto& d : links) {
+    const Link& l = *d.link;
+    const uint32_t lid = csr_.linkIds.at(&l);
+    const uint32_t lo = csr_.ids.at(l.lowNode());
+    auto clamp = [](Metric m) { return (m >= 1 && m <= 0xFFFFFFFFull) ? (uint32_t)m : 0u; };
+    const uint32_t mlo = clamp(l.metricFrom(l.lowNode())), mhi = clamp(l.metricFrom(l.highNode()));
+    for (uint32_t e = csr_.rowPtr[lo]; e < csr_.rowPtr[lo + 1]; ++e) {
+      if (csr_.linkId[e] != lid) continue;
+      const uint32_t t = csr_.twin[e];
+      csr_.metric[e] = mlo;
+      csr_.metric[t] = mhi;
+      csr_.edgeUp[e] = csr_.edgeUp[t] = l.isUp() ? 1 : 0;
+      break;
+    }
+    ups.push_back(ospf_link_update{lid, l.isUp() ? 1u : 0u, mlo, mhi});
+  }
+  std::vector<uint32_t> nids;
+  std::vector<uint8_t> nts;
+  for (const auto& x : nodes) {
+    const uint32_t id = csr_.ids.at(x);
+    csr_.noTransit[id] = isNodeOverloaded(x) ? 1 : 0;
+    nids.push_back(id);
+    nts.push_back(csr_.noTransit[id]);
+  }
+  const bool inSync = engine_ && engineVersion_ == snapVersion_;
+  ++version_;
+  snapVersion_ = version_;
+  if (inSync) {
+    int rc = ospf_update_links(engine_, ups.data(), (uint32_t)ups.size(), snapVersion_);
+    if (rc == OSPF_OK) rc = ospf_update_nodes(engine_, nids.data(), nts.data(), (uint32_t)nids.size(),
+                                              snapVersion_);
+    if (rc != OSPF_OK) throw EngineError(rc, ospf_last_error(engine_));
+    engineVersion_ = snapVersion_;
   }
 }
 

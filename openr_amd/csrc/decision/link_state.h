@@ -199,6 +199,22 @@ class LinkState {
 
   uint64_t spfRuns() const { return spfRuns_; }
 
+  // ---- incremental mode (off by default) ----
+  // The reference drops every memoised SPF on a topology change
+  // (LinkState.cpp:751-754). With incremental mode on, an update that only
+  // changes link metrics, link up state or node overload bits (no link or
+  // node added or removed) keeps the result of every root the change cannot
+  // affect -- no changed link was on its shortest-path DAG before, none
+  // reaches or ties a distance after, no re-flagged reached node can relax
+  // (the rule of ospf_affected_roots, on the memoised SpfResults) -- and
+  // patches the CSR and the device graph in place instead of re-snapshotting.
+  // Results are identical; decision.spf_runs then counts only the re-runs.
+  void setIncremental(bool on) { incremental_ = on; }
+  struct IncrementalStats {
+    uint64_t patches = 0, kept = 0, dropped = 0;
+  };
+  const IncrementalStats& incrementalStats() const { return incStats_; }
+
   // ---- CSR snapshot (what the engine sees) ----
   struct Csr {
     std::vector<std::string> names;                 // id -> name (sorted)
@@ -233,6 +249,13 @@ class LinkState {
                             std::unordered_set<const Link*>& seen) const;
   std::vector<Path> tracePaths(const RawRun& run, uint32_t src, uint32_t dst) const;
   const RawRun& rawSpf(const std::string& node);
+  struct LinkDelta {  // a kept link whose metric or up state changed
+    LinkPtr link;
+    bool up0;
+    Metric mlo0, mhi0;  // metric advertised by lowNode / highNode before
+  };
+  void applyIncremental(const std::vector<LinkDelta>& links,
+                        const std::vector<std::string>& nodes);
 
   std::string area_;
   int device_;
@@ -242,6 +265,8 @@ class LinkState {
   uint64_t snapVersion_ = 0;
   Csr csr_;
   uint64_t spfRuns_ = 0;
+  bool incremental_ = false;
+  IncrementalStats incStats_;
 
   std::unordered_map<std::string, LinkSet> linkMap_;
   LinkSet allLinks_;

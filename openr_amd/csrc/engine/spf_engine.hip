@@ -28,6 +28,8 @@ struct ospf_ctx {
   bool loaded = false;
   ospf_graph_info info{};
   std::vector<uint32_t> h_row_ptr, h_dn_off, h_dn;  // host copies for root queries
+  // host shadows of the padded device arrays patched by ospf_update_*
+  std::vector<uint32_t> h_prow, h_pcolx, h_pw, h_prw, h_nt, h_link_e;
   void* d_graph = nullptr;
   ospf::DevGraph g{};
   uint32_t max_dn = 0;
@@ -793,6 +795,12 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   c->h_dn = std::move(dn);
   c->max_dn = max_dn;
   c->depth_bound = transit_depth_bound(V, csr->row_ptr, colx.data(), nt);
+  c->h_prow = std::move(prow);
+  c->h_pcolx = std::move(pcolx);
+  c->h_pw = std::move(pw);
+  c->h_prw = std::move(prw);
+  c->h_nt = std::move(nt);
+  c->h_link_e = std::move(link_e);
   c->info.n_nodes = V;
   c->info.n_edges = E;
   c->info.n_links = n_links;
@@ -1103,6 +1111,116 @@ int ospf_ksp2_run(ospf_ctx* c, const ospf_ksp2* k) {
   HIPCHK(c, hipMemcpy(k->status, d.status, n * 4, hipMemcpyDeviceToHost));
   HIPCHK(c, hipMemcpy(k->k1, d.k1, n * rec, hipMemcpyDeviceToHost));
   HIPCHK(c, hipMemcpy(k->k2, d.k2, n * rec, hipMemcpyDeviceToHost));
+  return OSPF_OK;
+}
+
+// ---------------------------------------------------------------- incremental
+namespace {
+// graph-wide facts the planner uses, from the host shadows
+void refresh_graph_stats(ospf_ctx* c) {
+  uint32_t max_metric = 0;
+  bool unit = true;
+  for (size_t e = 0; e < c->h_pcolx.size(); ++e) {
+    if (c->h_pcolx[e] & 0x80000000u) continue;
+    max_metric = std::max(max_metric, c->h_pw[e]);
+    unit &= c->h_pw[e] == 1;
+  }
+  c->info.max_metric = max_metric;
+  c->info.unit_metric = unit ? 1u : 0u;
+  c->depth_bound = transit_depth_bound(c->info.n_nodes, c->h_prow.data(), c->h_pcolx.data(), c->h_nt);
+}
+}  // namespace
+
+int ospf_update_links(ospf_ctx* c, const ospf_link_update* u, uint32_t n, uint64_t version) {
+  if (!c || (n && !u)) return OSPF_E_INVAL;
+  if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  std::vector<uint32_t> idx, val;
+  idx.reserve(6ull * n);
+  val.reserve(6ull * n);
+  uint32_t* base = (uint32_t*)c->d_graph;
+  const size_t o_colx = c->g.colx - (const uint32_t*)base, o_w = c->g.w - (const uint32_t*)base,
+               o_rw = c->g.rw - (const uint32_t*)base;
+  auto owner = [&](uint32_t e) {
+    return (uint32_t)(std::upper_bound(c->h_prow.begin(), c->h_prow.end(), e) - c->h_prow.begin() - 1);
+  };
+  auto set = [&](std::vector<uint32_t>& shadow, size_t off, uint32_t e, uint32_t v) {
+    shadow[e] = v;
+    idx.push_back((uint32_t)(off + e));
+    val.push_back(v);
+  };
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t lid = u[i].link_id;
+    if (lid >= c->g.n_lid) return fail(c, OSPF_E_INVAL, "unknown link id");
+    const uint32_t e0 = c->h_link_e[2ull * lid], e1 = c->h_link_e[2ull * lid + 1];
+    if (e0 == 0xFFFFFFFFu || e1 == 0xFFFFFFFFu) return fail(c, OSPF_E_INVAL, "unknown link id");
+    if (u[i].up && (u[i].metric_lo == 0 || u[i].metric_hi == 0))
+      return fail(c, OSPF_E_RANGE, "metric 0 on a usable link is outside the engine contract");
+    const bool lo0 = owner(e0) <= owner(e1);
+    const uint32_t elo = lo0 ? e0 : e1, ehi = lo0 ? e1 : e0;
+    const uint32_t down = u[i].up ? 0u : 0x80000000u;
+    set(c->h_pcolx, o_colx, elo, (c->h_pcolx[elo] & 0x7FFFFFFFu) | down);
+    set(c->h_pcolx, o_colx, ehi, (c->h_pcolx[ehi] & 0x7FFFFFFFu) | down);
+    set(c->h_pw, o_w, elo, u[i].metric_lo);
+    set(c->h_pw, o_w, ehi, u[i].metric_hi);
+    set(c->h_prw, o_rw, elo, u[i].metric_hi);
+    set(c->h_prw, o_rw, ehi, u[i].metric_lo);
+  }
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipDeviceSynchronize());  // no batch may be reading the graph
+  if (!idx.empty()) {
+    int rc = ensure(c, &c->d_stage, &c->stage_bytes, idx.size() * 8ull + 256);
+    if (rc) return rc;
+    uint32_t* d_idx = (uint32_t*)c->d_stage;
+    uint32_t* d_val = d_idx + idx.size();
+    HIPCHK(c, hipMemcpy(d_idx, idx.data(), idx.size() * 4ull, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(d_val, val.data(), val.size() * 4ull, hipMemcpyHostToDevice));
+    hipError_t e = ospf::launch_scatter(base, d_idx, d_val, (uint32_t)idx.size(), nullptr);
+    if (e != hipSuccess) return hip_fail(c, e, "launch_scatter");
+    HIPCHK(c, hipDeviceSynchronize());
+  }
+  refresh_graph_stats(c);
+  c->info.version = version;
+  return OSPF_OK;
+}
+
+int ospf_update_nodes(ospf_ctx* c, const uint32_t* nodes, const uint8_t* no_transit, uint32_t n,
+                      uint64_t version) {
+  if (!c || (n && (!nodes || !no_transit))) return OSPF_E_INVAL;
+  if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t v = nodes[i];
+    if (v >= c->info.n_nodes) return fail(c, OSPF_E_INVAL, "node out of range");
+    if (no_transit[i]) c->h_nt[v >> 5] |= 1u << (v & 31u);
+    else c->h_nt[v >> 5] &= ~(1u << (v & 31u));
+  }
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipDeviceSynchronize());
+  HIPCHK(c, hipMemcpy((void*)c->g.nt_bits, c->h_nt.data(), c->h_nt.size() * 4ull,
+                      hipMemcpyHostToDevice));
+  refresh_graph_stats(c);
+  c->info.version = version;
+  return OSPF_OK;
+}
+
+int ospf_affected_roots(ospf_ctx* c, const uint32_t* d_dist, uint32_t n_roots, uint32_t flags,
+                        const ospf_change* ch, uint32_t n_ch, uint8_t* d_affected, void* stream) {
+  if (!c || (n_roots && (!d_dist || !d_affected)) || (n_ch && !ch)) return OSPF_E_INVAL;
+  if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  for (uint32_t k = 0; k < n_ch; ++k)
+    if (ch[k].a >= c->info.n_nodes || (ch[k].kind == OSPF_CHANGE_LINK && ch[k].b >= c->info.n_nodes))
+      return fail(c, OSPF_E_INVAL, "change names a node out of range");
+  if (n_roots == 0) return OSPF_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc = OSPF_OK;
+  ospf_change* d_ch =
+      (ospf_change*)stream_scratch(c, stream, std::max<size_t>(n_ch, 1) * sizeof(ospf_change), &rc, 2);
+  if (rc) return rc;
+  if (n_ch)
+    HIPCHK(c, hipMemcpyAsync(d_ch, ch, n_ch * sizeof(ospf_change), hipMemcpyHostToDevice,
+                             (hipStream_t)stream));
+  hipError_t e = ospf::launch_affected(c->g, d_dist, n_roots, (flags & OSPF_HOP_COUNT) != 0, d_ch,
+                                       n_ch, d_affected, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(c, e, "launch_affected");
   return OSPF_OK;
 }
 

@@ -184,6 +184,11 @@ struct TraceArgs {
 hipError_t launch_ksp_trace(bool lev, const DevGraph& g, const TraceArgs& t, hipStream_t s);
 // st[i] |= bits, i < n
 hipError_t launch_or_bits(uint32_t* st, uint32_t n, uint32_t bits, hipStream_t s);
+// incremental updates (spf_update.hip): base[idx[i]] = val[i]; affected runs
+hipError_t launch_scatter(uint32_t* base, const uint32_t* idx, const uint32_t* val, uint32_t n,
+                          hipStream_t s);
+hipError_t launch_affected(const DevGraph& g, const uint32_t* dist, uint32_t n_roots, bool hop,
+                           const ospf_change* ch, uint32_t n_ch, uint8_t* out, hipStream_t s);
 // out[i] = i * stride, i <= n
 hipError_t launch_iota(uint32_t* out, uint32_t n, uint32_t stride, hipStream_t s);
 

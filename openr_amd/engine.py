@@ -176,5 +176,26 @@ class Engine:
         a = N.ospf_ksp2(src, d_dsts, n, path_cap, d_k1, d_k2, d_status)
         self._check(self._L.ospf_ksp2_dev(self._h, C.byref(a), stream or None))
 
+    def update_links(self, updates, version: int) -> None:
+        """updates: iterable of (link_id, up, metric_lo, metric_hi)."""
+        ups = list(updates)
+        arr = (N.ospf_link_update * max(len(ups), 1))(*[N.ospf_link_update(*u) for u in ups])
+        self._check(self._L.ospf_update_links(self._h, arr, len(ups), version))
+
+    def update_nodes(self, nodes, no_transit, version: int) -> None:
+        n = np.ascontiguousarray(nodes, np.uint32)
+        t = np.ascontiguousarray(no_transit, np.uint8)
+        self._check(self._L.ospf_update_nodes(self._h, n.ctypes.data, t.ctypes.data, n.size,
+                                              version))
+
+    def affected(self, d_dist: int, n_roots: int, changes, d_out: int, flags: int = 0,
+                 stream: int = 0) -> None:
+        """changes: iterable of ospf_change field tuples
+        (kind, a, b, up0, w_ab0, w_ba0, up1, w_ab1, w_ba1)."""
+        ch = list(changes)
+        arr = (N.ospf_change * max(len(ch), 1))(*[N.ospf_change(*c) for c in ch])
+        self._check(self._L.ospf_affected_roots(self._h, d_dist, n_roots, flags, arr, len(ch),
+                                                d_out, stream or None))
+
     def sync(self, stream: int = 0) -> None:
         self._check(self._L.ospf_sync(self._h, stream or None))

@@ -158,6 +158,16 @@ class LinkState:
     def spf_runs(self) -> int:
         return int(self._L.odl_spf_runs(self._h))
 
+    def set_incremental(self, on: bool = True) -> None:
+        """Keep memoised SPF results a metric / up / overload-only update
+        cannot affect (odl_set_incremental; off = the reference's behaviour)."""
+        self._L.odl_set_incremental(self._h, int(on))
+
+    def incremental_stats(self) -> Dict[str, int]:
+        out = (C.c_uint64 * 3)()
+        self._L.odl_incremental_stats(self._h, out)
+        return {"patches": int(out[0]), "kept": int(out[1]), "dropped": int(out[2])}
+
     def num_nodes(self) -> int:
         return int(self._L.odl_num_nodes(self._h))
 

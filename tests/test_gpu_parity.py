@@ -246,6 +246,85 @@ def test_mesh_sampled_digests():
     assert np.array_equal(p.digests(roots), o.digests(roots, threads=8))
 
 
+@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("unit", [False, True])
+def test_incremental_linkstate_matches_full_recompute(seed, unit):
+    """Incremental mode: metric / link up-down / node overload updates keep the
+    memoised results of unaffected roots and patch the device graph in place;
+    every root's result must equal the oracle's full recompute."""
+    st, names = random_stream(500 + seed, n=40, unit=unit)
+    o, p = both(st)
+    p.set_incremental(True)
+    p.prefetch(names)
+    p.prefetch(names, False)
+    rng = np.random.default_rng(seed)
+    dbs = st.to_dbs()
+    for step in range(9):
+        db = dbs[int(rng.integers(len(dbs)))]
+        kind = step % 3
+        if kind == 0:
+            db.overloaded = not db.overloaded
+        elif db.adjs:
+            a = db.adjs[int(rng.integers(len(db.adjs)))]
+            if kind == 1 and not unit:
+                a.metric = int(rng.integers(1, 30))
+            else:
+                a.overloaded = not a.overloaded  # link down / up
+        upd = AdjDbStream.from_dbs([db])
+        assert o.apply(upd) == p.apply(upd)
+        for r in names:
+            assert p.spf_text(r) == o.spf_text(r), (step, r)
+            assert p.spf_text(r, False) == o.spf_text(r, False), (step, r)
+    stats = p.incremental_stats()
+    assert stats["patches"] > 0 and stats["kept"] > 0, stats
+
+
+def test_engine_affected_roots_and_patch():
+    """ospf_update_links patches the resident graph like a reload, and every
+    run ospf_affected_roots leaves unflagged is bit-identical after the change."""
+    import torch
+    st, names = random_stream(77, n=70, p=0.08)
+    p = LinkState(stream=st)
+    csr = p.csr()
+    V = len(names)
+    eng = Engine(0)
+    eng.load(csr)
+    W = int(max(eng.nh_words(r) for r in range(V)))
+    roots = np.arange(V, dtype=np.uint32)
+    before = eng.run(roots, W)
+    rp, col, lid = csr["row_ptr"], csr["col"], csr["link_id"]
+    owner = np.repeat(np.arange(V), np.diff(rp.astype(np.int64)))
+    rng = np.random.default_rng(3)
+    new = {k: v.copy() for k, v in csr.items()}
+    ups, changes = [], []
+    for l in rng.choice(int(lid.max()) + 1, 4, replace=False):
+        e = np.nonzero(lid == l)[0]
+        lo, hi = (e[0], e[1]) if owner[e[0]] <= owner[e[1]] else (e[1], e[0])
+        up0 = int(csr["edge_up"][lo])
+        up1 = 1 - up0 if rng.random() < 0.4 else 1
+        m_lo, m_hi = int(rng.integers(1, 21)), int(rng.integers(1, 21))
+        new["edge_up"][[lo, hi]] = up1
+        new["metric"][lo], new["metric"][hi] = m_lo, m_hi
+        ups.append((int(l), up1, m_lo, m_hi))
+        changes.append((0, int(owner[lo]), int(owner[hi]), up0, int(csr["metric"][lo]),
+                        int(csr["metric"][hi]), up1, m_lo, m_hi))
+    d_dist = torch.from_numpy(before["dist"].view(np.int32)).cuda()
+    flags = torch.zeros(V, dtype=torch.uint8, device="cuda")
+    eng.update_links(ups, version=2)
+    eng.affected(d_dist.data_ptr(), V, changes, flags.data_ptr())
+    eng.sync()
+    after = eng.run(roots, W)
+    fresh = Engine(0)
+    fresh.load(new)
+    ref = fresh.run(roots, W)
+    assert np.array_equal(after["dist"], ref["dist"]) and np.array_equal(after["nh"], ref["nh"])
+    f = flags.cpu().numpy().astype(bool)
+    keep = ~f
+    assert keep.any() and f.any()
+    assert np.array_equal(after["dist"][keep], before["dist"][keep])
+    assert np.array_equal(after["nh"][keep], before["nh"][keep])
+
+
 def test_mesh_60k_bucketed_dial_digests():
     """Weighted mesh too large for LDS state: the planner's bucketed Dial
     (variant 6) against the oracle, sampled roots, digests (dist + next hops)."""
