@@ -29,7 +29,7 @@ ENGINE_SYMBOLS = [
     "ospf_root_neighbors", "ospf_sssp_batch", "ospf_sssp_batch_dev", "ospf_sync",
     "ospf_plan_variant", "ospf_plan", "ospf_plan_n", "ospf_spf_runs", "ospf_run_batch_dev",
     "ospf_ksp2_run", "ospf_ksp2_dev", "ospf_update_links", "ospf_update_nodes",
-    "ospf_affected_roots",
+    "ospf_affected_roots", "ospf_repair_runs",
 ]
 DECISION_SYMBOLS = [
     "odl_create", "odl_destroy", "odl_last_error", "odl_free", "odl_apply", "odl_spf_text",
@@ -123,6 +123,7 @@ def engine() -> C.CDLL:
         L.ospf_update_links.argtypes = [vp, vp, u32, u64]
         L.ospf_update_nodes.argtypes = [vp, vp, vp, u32, u64]
         L.ospf_affected_roots.argtypes = [vp, vp, u32, u32, vp, u32, vp, vp]
+        L.ospf_repair_runs.argtypes = [vp, vp, u32, u32, u32, vp, vp, vp, u32, vp, vp]
         L.ospf_spf_runs.argtypes = [vp]
         L.ospf_spf_runs.restype = u64
         _engine = L

@@ -30,6 +30,7 @@ struct ospf_ctx {
   std::vector<uint32_t> h_row_ptr, h_dn_off, h_dn;  // host copies for root queries
   // host shadows of the padded device arrays patched by ospf_update_*
   std::vector<uint32_t> h_prow, h_pcolx, h_pw, h_prw, h_nt, h_link_e;
+  uint64_t non_unit = 0;  // usable entries with metric != 1 (exact unit_metric under patches)
   void* d_graph = nullptr;
   ospf::DevGraph g{};
   uint32_t max_dn = 0;
@@ -801,6 +802,9 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   c->h_prw = std::move(prw);
   c->h_nt = std::move(nt);
   c->h_link_e = std::move(link_e);
+  c->non_unit = 0;
+  for (uint32_t e = 0; e < Ep; ++e)
+    if (!(c->h_pcolx[e] & 0x80000000u) && c->h_pw[e] != 1) ++c->non_unit;
   c->info.n_nodes = V;
   c->info.n_edges = E;
   c->info.n_links = n_links;
@@ -1116,18 +1120,16 @@ int ospf_ksp2_run(ospf_ctx* c, const ospf_ksp2* k) {
 
 // ---------------------------------------------------------------- incremental
 namespace {
-// graph-wide facts the planner uses, from the host shadows
-void refresh_graph_stats(ospf_ctx* c) {
-  uint32_t max_metric = 0;
-  bool unit = true;
-  for (size_t e = 0; e < c->h_pcolx.size(); ++e) {
-    if (c->h_pcolx[e] & 0x80000000u) continue;
-    max_metric = std::max(max_metric, c->h_pw[e]);
-    unit &= c->h_pw[e] == 1;
-  }
-  c->info.max_metric = max_metric;
-  c->info.unit_metric = unit ? 1u : 0u;
-  c->depth_bound = transit_depth_bound(c->info.n_nodes, c->h_prow.data(), c->h_pcolx.data(), c->h_nt);
+// Planner facts after a patch. unit_metric is exact (a count of usable
+// entries with metric != 1); max_metric may stay conservative (a larger
+// ring / range check only); the BFS level bound is recomputed (O(V + E), host) only when a link
+// went down or a node stopped being transit, the changes that can deepen it.
+void refresh_graph_stats(ospf_ctx* c, uint32_t new_max, bool deeper) {
+  c->info.max_metric = std::max(c->info.max_metric, new_max);
+  c->info.unit_metric = c->non_unit == 0 ? 1u : 0u;
+  if (deeper)
+    c->depth_bound =
+        transit_depth_bound(c->info.n_nodes, c->h_prow.data(), c->h_pcolx.data(), c->h_nt);
 }
 }  // namespace
 
@@ -1148,6 +1150,8 @@ int ospf_update_links(ospf_ctx* c, const ospf_link_update* u, uint32_t n, uint64
     idx.push_back((uint32_t)(off + e));
     val.push_back(v);
   };
+  uint32_t new_max = 0;
+  bool deeper = false;
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t lid = u[i].link_id;
     if (lid >= c->g.n_lid) return fail(c, OSPF_E_INVAL, "unknown link id");
@@ -1158,6 +1162,13 @@ int ospf_update_links(ospf_ctx* c, const ospf_link_update* u, uint32_t n, uint64
     const bool lo0 = owner(e0) <= owner(e1);
     const uint32_t elo = lo0 ? e0 : e1, ehi = lo0 ? e1 : e0;
     const uint32_t down = u[i].up ? 0u : 0x80000000u;
+    if (!u[i].up && !(c->h_pcolx[elo] & 0x80000000u)) deeper = true;
+    if (u[i].up) new_max = std::max({new_max, u[i].metric_lo, u[i].metric_hi});
+    for (uint32_t e : {elo, ehi}) {  // usable non-unit entries, before -> after
+      if (!(c->h_pcolx[e] & 0x80000000u) && c->h_pw[e] != 1) --c->non_unit;
+      const uint32_t m = e == elo ? u[i].metric_lo : u[i].metric_hi;
+      if (u[i].up && m != 1) ++c->non_unit;
+    }
     set(c->h_pcolx, o_colx, elo, (c->h_pcolx[elo] & 0x7FFFFFFFu) | down);
     set(c->h_pcolx, o_colx, ehi, (c->h_pcolx[ehi] & 0x7FFFFFFFu) | down);
     set(c->h_pw, o_w, elo, u[i].metric_lo);
@@ -1178,7 +1189,7 @@ int ospf_update_links(ospf_ctx* c, const ospf_link_update* u, uint32_t n, uint64
     if (e != hipSuccess) return hip_fail(c, e, "launch_scatter");
     HIPCHK(c, hipDeviceSynchronize());
   }
-  refresh_graph_stats(c);
+  refresh_graph_stats(c, new_max, deeper);
   c->info.version = version;
   return OSPF_OK;
 }
@@ -1187,9 +1198,11 @@ int ospf_update_nodes(ospf_ctx* c, const uint32_t* nodes, const uint8_t* no_tran
                       uint64_t version) {
   if (!c || (n && (!nodes || !no_transit))) return OSPF_E_INVAL;
   if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  bool deeper = false;
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t v = nodes[i];
     if (v >= c->info.n_nodes) return fail(c, OSPF_E_INVAL, "node out of range");
+    if (no_transit[i] && !((c->h_nt[v >> 5] >> (v & 31u)) & 1u)) deeper = true;
     if (no_transit[i]) c->h_nt[v >> 5] |= 1u << (v & 31u);
     else c->h_nt[v >> 5] &= ~(1u << (v & 31u));
   }
@@ -1197,7 +1210,7 @@ int ospf_update_nodes(ospf_ctx* c, const uint32_t* nodes, const uint8_t* no_tran
   HIPCHK(c, hipDeviceSynchronize());
   HIPCHK(c, hipMemcpy((void*)c->g.nt_bits, c->h_nt.data(), c->h_nt.size() * 4ull,
                       hipMemcpyHostToDevice));
-  refresh_graph_stats(c);
+  refresh_graph_stats(c, 0, deeper);
   c->info.version = version;
   return OSPF_OK;
 }
@@ -1221,6 +1234,39 @@ int ospf_affected_roots(ospf_ctx* c, const uint32_t* d_dist, uint32_t n_roots, u
   hipError_t e = ospf::launch_affected(c->g, d_dist, n_roots, (flags & OSPF_HOP_COUNT) != 0, d_ch,
                                        n_ch, d_affected, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(c, e, "launch_affected");
+  return OSPF_OK;
+}
+
+int ospf_repair_runs(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t flags,
+                     uint32_t nh_words, uint32_t* d_dist, uint32_t* d_nh, const ospf_change* ch,
+                     uint32_t n_ch, uint32_t* d_status, void* stream) {
+  if (!c || (n && (!d_roots || !d_dist || !d_nh || !d_status)) || (n_ch && !ch) || !nh_words)
+    return OSPF_E_INVAL;
+  if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  for (uint32_t k = 0; k < n_ch; ++k)
+    if (ch[k].a >= c->info.n_nodes || (ch[k].kind == OSPF_CHANGE_LINK && ch[k].b >= c->info.n_nodes))
+      return fail(c, OSPF_E_INVAL, "change names a node out of range");
+  if (n == 0) return OSPF_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc = OSPF_OK;
+  ospf_change* d_ch =
+      (ospf_change*)stream_scratch(c, stream, std::max<size_t>(n_ch, 1) * sizeof(ospf_change), &rc, 2);
+  if (rc) return rc;
+  if (n_ch)
+    HIPCHK(c, hipMemcpyAsync(d_ch, ch, n_ch * sizeof(ospf_change), hipMemcpyHostToDevice,
+                             (hipStream_t)stream));
+  ospf::RepairArgs a{};
+  a.roots = d_roots;
+  a.n = n;
+  a.W = nh_words;
+  a.hop = (flags & OSPF_HOP_COUNT) ? 1u : 0u;
+  a.dist = d_dist;
+  a.nh = d_nh;
+  a.ch = d_ch;
+  a.n_ch = n_ch;
+  a.status = d_status;
+  hipError_t e = ospf::launch_repair(c->g, a, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(c, e, "launch_repair");
   return OSPF_OK;
 }
 

@@ -189,6 +189,16 @@ hipError_t launch_scatter(uint32_t* base, const uint32_t* idx, const uint32_t* v
                           hipStream_t s);
 hipError_t launch_affected(const DevGraph& g, const uint32_t* dist, uint32_t n_roots, bool hop,
                            const ospf_change* ch, uint32_t n_ch, uint8_t* out, hipStream_t s);
+struct RepairArgs {
+  const uint32_t* roots;
+  uint32_t n, W, hop;
+  uint32_t* dist;  // [n][V]
+  uint32_t* nh;    // [n][V][W]
+  const ospf_change* ch;
+  uint32_t n_ch;
+  uint32_t* status;  // [n] 0 repaired, 1 re-run
+};
+hipError_t launch_repair(const DevGraph& g, const RepairArgs& a, hipStream_t s);
 // out[i] = i * stride, i <= n
 hipError_t launch_iota(uint32_t* out, uint32_t n, uint32_t stride, hipStream_t s);
 

@@ -197,5 +197,14 @@ class Engine:
         self._check(self._L.ospf_affected_roots(self._h, d_dist, n_roots, flags, arr, len(ch),
                                                 d_out, stream or None))
 
+    def repair(self, d_roots: int, n: int, nh_words: int, d_dist: int, d_nh: int, changes,
+               d_status: int, flags: int = 0, stream: int = 0) -> None:
+        """ospf_repair_runs: fix finished rows in place after a patch; d_status
+        [n] u32 = 1 where the run must be re-run."""
+        ch = list(changes)
+        arr = (N.ospf_change * max(len(ch), 1))(*[N.ospf_change(*c) for c in ch])
+        self._check(self._L.ospf_repair_runs(self._h, d_roots, n, flags, nh_words, d_dist, d_nh,
+                                             arr, len(ch), d_status, stream or None))
+
     def sync(self, stream: int = 0) -> None:
         self._check(self._L.ospf_sync(self._h, stream or None))

@@ -323,6 +323,55 @@ def test_engine_affected_roots_and_patch():
     assert keep.any() and f.any()
     assert np.array_equal(after["dist"][keep], before["dist"][keep])
     assert np.array_equal(after["nh"][keep], before["nh"][keep])
+    # in-place repair: every run it keeps (status 0) equals the fresh run
+    d_nh = torch.from_numpy(before["nh"].view(np.int32)).cuda()
+    st = torch.zeros(V, dtype=torch.int32, device="cuda")
+    d_roots = torch.from_numpy(roots.view(np.int32)).cuda()
+    eng.repair(d_roots.data_ptr(), V, W, d_dist.data_ptr(), d_nh.data_ptr(), changes,
+               st.data_ptr())
+    eng.sync()
+    ok = st.cpu().numpy() == 0
+    assert ok.any()
+    rd = d_dist.cpu().numpy().view(np.uint32)
+    rn = d_nh.cpu().numpy().view(np.uint32)
+    assert np.array_equal(rd[ok], ref["dist"][ok]) and np.array_equal(rn[ok], ref["nh"][ok])
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_engine_repair_fabric_link_events(seed):
+    """Link events in an ECMP fabric (unit metric): uplink down / up, metric
+    change; repaired rows (status 0) equal fresh runs, most runs repair."""
+    import torch
+    p = LinkState(stream=T.fabric(pods=6, planes=4))
+    csr = p.csr()
+    V = p.num_nodes()
+    eng = Engine(0)
+    eng.load(csr)
+    W = int(max(eng.nh_words(r) for r in range(V)))
+    roots = np.arange(V, dtype=np.uint32)
+    before = eng.run(roots, W)
+    rp, lid = csr["row_ptr"], csr["link_id"]
+    owner = np.repeat(np.arange(V), np.diff(rp.astype(np.int64)))
+    rng = np.random.default_rng(seed)
+    l = int(rng.integers(int(lid.max()) + 1))
+    e = np.nonzero(lid == l)[0]
+    lo, hi = (e[0], e[1]) if owner[e[0]] <= owner[e[1]] else (e[1], e[0])
+    up1, m1 = (0, 1) if seed % 2 == 0 else (1, 3)
+    ch = [(0, int(owner[lo]), int(owner[hi]), 1, 1, 1, up1, m1, m1)]
+    eng.update_links([(l, up1, m1, m1)], version=2)
+    d_roots = torch.from_numpy(roots.view(np.int32)).cuda()
+    d_dist = torch.from_numpy(before["dist"].view(np.int32)).cuda()
+    d_nh = torch.from_numpy(before["nh"].view(np.int32)).cuda()
+    st = torch.zeros(V, dtype=torch.int32, device="cuda")
+    eng.repair(d_roots.data_ptr(), V, W, d_dist.data_ptr(), d_nh.data_ptr(), ch, st.data_ptr())
+    eng.sync()
+    ref = eng.run(roots, W)
+    ok = st.cpu().numpy() == 0
+    rd = d_dist.cpu().numpy().view(np.uint32)
+    rn = d_nh.cpu().numpy().view(np.uint32)
+    assert np.array_equal(rd[ok], ref["dist"][ok]) and np.array_equal(rn[ok], ref["nh"][ok])
+    if up1 == 0:
+        assert ok.mean() > 0.5, ok.mean()
 
 
 def test_mesh_60k_bucketed_dial_digests():
