@@ -282,10 +282,11 @@ int ospf_affected_roots(ospf_ctx* ctx, const uint32_t* d_dist, uint32_t n_roots,
  * (OSPF_HOP_COUNT read). A run none of whose shortest distances the batch
  * changes -- only next-hop sets and ties move, the usual effect of a link
  * event in an ECMP fabric -- gets its next-hop words re-derived where they
- * change (d_status[i] = 0: the rows now equal a fresh run's). A run whose
- * distances would change, with a re-flagged node that can relax, more than
- * 8 next-hop words, or beyond the repair budget gets d_status[i] = 1 and must
- * be re-run. Digests are not maintained. Queued on `stream`. */
+ * change (d_status[i] = 0: the rows now equal a fresh run's). Link changes
+ * and overload toggles (node changes: the current transit bit is read) are
+ * both repaired. A run whose distances would change, or beyond the repair
+ * budget (8192 re-derivations, 1024 queued nodes), gets d_status[i] = 1 and
+ * must be re-run. Digests are not maintained. Queued on `stream`. */
 int ospf_repair_runs(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n, uint32_t flags,
                      uint32_t nh_words, uint32_t* d_dist, uint32_t* d_nh,
                      const ospf_change* changes, uint32_t n_changes, uint32_t* d_status,

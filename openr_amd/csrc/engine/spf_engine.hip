@@ -35,6 +35,8 @@ struct ospf_ctx {
   ospf::DevGraph g{};
   uint32_t max_dn = 0;
   uint32_t depth_bound = 2;  // BFS levels any root can reach (unit metric / hop count)
+  uint32_t exact_bound = 2;  // depth_bound as last computed in full (patches may raise depth_bound)
+  std::vector<uint32_t> h_lvl;  // scratch of transit_detour (all UINT32_MAX between calls)
   // scratch
   // scratch per stream: batches queued on different streams run concurrently
   struct Scratch {
@@ -796,6 +798,7 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   c->h_dn = std::move(dn);
   c->max_dn = max_dn;
   c->depth_bound = transit_depth_bound(V, csr->row_ptr, colx.data(), nt);
+  c->exact_bound = c->depth_bound;
   c->h_prow = std::move(prow);
   c->h_pcolx = std::move(pcolx);
   c->h_pw = std::move(pw);
@@ -1127,9 +1130,38 @@ namespace {
 void refresh_graph_stats(ospf_ctx* c, uint32_t new_max, bool deeper) {
   c->info.max_metric = std::max(c->info.max_metric, new_max);
   c->info.unit_metric = c->non_unit == 0 ? 1u : 0u;
-  if (deeper)
+  if (deeper) {
     c->depth_bound =
         transit_depth_bound(c->info.n_nodes, c->h_prow.data(), c->h_pcolx.data(), c->h_nt);
+    c->exact_bound = c->depth_bound;
+  }
+}
+
+// Hops of a shortest a -> b path in the transit subgraph of the current
+// shadows, or UINT32_MAX when none is found within `budget` scanned entries.
+uint32_t transit_detour(ospf_ctx* c, uint32_t a, uint32_t b, size_t budget) {
+  auto transit = [&](uint32_t u) { return !((c->h_nt[u >> 5] >> (u & 31)) & 1u); };
+  std::vector<uint32_t>& lvl = c->h_lvl;
+  if (lvl.size() != c->info.n_nodes) lvl.assign(c->info.n_nodes, 0xFFFFFFFFu);
+  std::vector<uint32_t> q{a};
+  lvl[a] = 0;
+  uint32_t found = 0xFFFFFFFFu;
+  size_t scanned = 0;
+  for (size_t i = 0; i < q.size() && found == 0xFFFFFFFFu && scanned < budget; ++i) {
+    const uint32_t u = q[i];
+    for (uint32_t e = c->h_prow[u]; e < c->h_prow[u + 1]; ++e, ++scanned) {
+      const uint32_t x = c->h_pcolx[e];
+      if ((x & 0x80000000u) || !transit(x) || lvl[x] != 0xFFFFFFFFu) continue;
+      lvl[x] = lvl[u] + 1;
+      q.push_back(x);
+      if (x == b) {
+        found = lvl[x];
+        break;
+      }
+    }
+  }
+  for (uint32_t x : q) lvl[x] = 0xFFFFFFFFu;
+  return found;
 }
 }  // namespace
 
@@ -1151,7 +1183,7 @@ int ospf_update_links(ospf_ctx* c, const ospf_link_update* u, uint32_t n, uint64
     val.push_back(v);
   };
   uint32_t new_max = 0;
-  bool deeper = false;
+  std::vector<std::pair<uint32_t, uint32_t>> downs;  // links that went down (ends)
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t lid = u[i].link_id;
     if (lid >= c->g.n_lid) return fail(c, OSPF_E_INVAL, "unknown link id");
@@ -1162,7 +1194,7 @@ int ospf_update_links(ospf_ctx* c, const ospf_link_update* u, uint32_t n, uint64
     const bool lo0 = owner(e0) <= owner(e1);
     const uint32_t elo = lo0 ? e0 : e1, ehi = lo0 ? e1 : e0;
     const uint32_t down = u[i].up ? 0u : 0x80000000u;
-    if (!u[i].up && !(c->h_pcolx[elo] & 0x80000000u)) deeper = true;
+    if (!u[i].up && !(c->h_pcolx[elo] & 0x80000000u)) downs.push_back({owner(elo), owner(ehi)});
     if (u[i].up) new_max = std::max({new_max, u[i].metric_lo, u[i].metric_hi});
     for (uint32_t e : {elo, ehi}) {  // usable non-unit entries, before -> after
       if (!(c->h_pcolx[e] & 0x80000000u) && c->h_pw[e] != 1) --c->non_unit;
@@ -1188,6 +1220,29 @@ int ospf_update_links(ospf_ctx* c, const ospf_link_update* u, uint32_t n, uint64
     hipError_t e = ospf::launch_scatter(base, d_idx, d_val, (uint32_t)idx.size(), nullptr);
     if (e != hipSuccess) return hip_fail(c, e, "launch_scatter");
     HIPCHK(c, hipDeviceSynchronize());
+  }
+  // Level bound after links went down. A shortest path uses a removed link at
+  // most once, so replacing each removed link (a, b) of the transit subgraph
+  // by a shortest a -> b detour of k hops in the patched graph lengthens any
+  // distance by at most sum(k - 1): bound += sum(k - 1), found by a budgeted
+  // local BFS instead of the O(V + E) recomputation. A link with an
+  // overloaded end is not in the transit subgraph (only the first / last hop
+  // of a path, covered by the + 2 of the bound). No detour within the budget
+  // (a split component), or drift of more than 8 levels over the last exact
+  // bound, recomputes it.
+  bool deeper = false;
+  uint32_t grow = 0;
+  auto transit = [&](uint32_t x) { return !((c->h_nt[x >> 5] >> (x & 31)) & 1u); };
+  for (const auto& ab : downs) {
+    if (deeper) break;
+    if (!transit(ab.first) || !transit(ab.second)) continue;
+    const uint32_t k = transit_detour(c, ab.first, ab.second, 1u << 20);
+    if (k == 0xFFFFFFFFu) deeper = true;
+    else grow += k - 1;
+  }
+  if (!deeper && grow) {
+    if (c->depth_bound + grow > c->exact_bound + 8) deeper = true;
+    else c->depth_bound += grow;
   }
   refresh_graph_stats(c, new_max, deeper);
   c->info.version = version;

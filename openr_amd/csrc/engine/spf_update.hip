@@ -75,11 +75,13 @@ __global__ void affected_kernel(DevGraph g, const uint32_t* dist, uint32_t n_roo
 //     minimum over v's usable in-edges from reached transit nodes must still
 //     be dist(v) (else the run is flagged for a re-run), and v's next hops
 //     are pulled again (LinkState.cpp:885-901);
+//     an overload toggle of node x re-derives every tight successor of x;
 //  2. a node whose next hops changed re-derives its tight successors, in
 //     increasing distance order (an LDS min-heap), so every pull reads final
 //     predecessor words.
-// A dropped or shortened distance, a re-flagged node that can relax, more
-// than kPops re-derivations, or a full heap flag the run (status 1).
+// A dropped or shortened distance, more than kPops re-derivations, or a full
+// heap flag the run (status 1).
+// Any next-hop width: words are re-derived 8 at a time.
 constexpr uint32_t kRWaves = 4;
 constexpr uint32_t kHeapCap = 1024;
 constexpr uint32_t kPops = 8192;
@@ -108,42 +110,51 @@ __global__ void __launch_bounds__(256) repair_kernel(DevGraph g, RepairArgs a) {
   auto transit = [&](uint32_t x) {
     return x == root || !((g.nt_bits[x >> 5] >> (x & 31u)) & 1u);
   };
-  // re-derive y: 0 unchanged, 1 next hops changed, 2 its distance would change
+  // re-derive y: 0 unchanged, 1 next hops changed, 2 its distance would
+  // change. Words go 8 at a time (one in-edge scan per group of 8 words).
   auto rederive = [&](uint32_t y) -> int {
     if (y == root) return 0;
     const uint32_t dy = D[y];
-    uint32_t best = kInf, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (uint32_t e = g.row_ptr[y] + lane; e < g.row_ptr[y + 1]; e += 64) {
-      const uint32_t x = g.colx[e];
-      if ((x & kDown) || x == y) continue;
-      const uint32_t dx = D[x];
-      if (dx == kInf || !transit(x)) continue;
-      const uint64_t c = (uint64_t)dx + (a.hop ? 1u : g.rw[e]);
-      if (c < best) best = (uint32_t)min<uint64_t>(c, kInf - 1);
-      if (c != dy) continue;
-      if (x == root) {
-        uint32_t lo = 0, hi = nbn;
-        while (lo < hi) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (g.dn[nb0 + mid] < y) lo = mid + 1; else hi = mid;
-        }
-        acc[lo >> 5] |= 1u << (lo & 31u);
-      } else {
-        for (uint32_t w = 0; w < W; ++w) acc[w] |= H[(size_t)x * W + w];
-      }
-    }
-    if (wmin(best) != dy) return 2;
     bool changed = false;
-    for (uint32_t w = 0; w < W; ++w) {
-      const uint32_t v = wor(acc[w]);
-      changed |= v != H[(size_t)y * W + w];
-      if (lane == 0) H[(size_t)y * W + w] = v;
+    for (uint32_t w0 = 0; w0 < W; w0 += 8) {
+      uint32_t best = kInf, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (uint32_t e = g.row_ptr[y] + lane; e < g.row_ptr[y + 1]; e += 64) {
+        const uint32_t x = g.colx[e];
+        if ((x & kDown) || x == y) continue;
+        const uint32_t dx = D[x];
+        if (dx == kInf || !transit(x)) continue;
+        const uint64_t c = (uint64_t)dx + (a.hop ? 1u : g.rw[e]);
+        if (c < best) best = (uint32_t)min<uint64_t>(c, kInf - 1);
+        if (c != dy) continue;
+        if (x == root) {
+          uint32_t lo = 0, hi = nbn;
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (g.dn[nb0 + mid] < y) lo = mid + 1; else hi = mid;
+          }
+#pragma unroll
+          for (uint32_t j = 0; j < 8; ++j)
+            if ((lo >> 5) == w0 + j) acc[j] |= 1u << (lo & 31u);
+        } else {
+#pragma unroll
+          for (uint32_t j = 0; j < 8; ++j)
+            if (w0 + j < W) acc[j] |= H[(size_t)x * W + w0 + j];
+        }
+      }
+      if (w0 == 0 && wmin(best) != dy) return 2;
+#pragma unroll
+      for (uint32_t j = 0; j < 8; ++j) {
+        if (w0 + j >= W) break;
+        const uint32_t v = wor(acc[j]);
+        changed |= v != H[(size_t)y * W + w0 + j];
+        if (lane == 0) H[(size_t)y * W + w0 + j] = v;
+      }
     }
     __threadfence_block();
     return changed ? 1 : 0;
   };
   uint32_t hn = 0;
-  bool bail = W > 8;
+  bool bail = false;
   auto push = [&](uint32_t y) {  // lane 0 owns the heap; hn is wave-uniform
     if (hn == kHeapCap) {
       bail = true;
@@ -182,7 +193,40 @@ __global__ void __launch_bounds__(256) repair_kernel(DevGraph g, RepairArgs a) {
   for (uint32_t k = 0; k < a.n_ch && !bail; ++k) {
     const ospf_change c = a.ch[k];
     if (c.kind == OSPF_CHANGE_NODE) {
-      if (node_matters(g, D, c.a, a.hop != 0)) bail = true;
+      // an overload toggle of x changes the usable relaxations x -> y: a
+      // transit x may now shorten a distance (flag) or add a tight in-edge,
+      // a non-transit x may have dropped one; every tight successor of x is
+      // re-derived (from the current transit bits, whatever x's old state)
+      const uint32_t x = c.a;
+      const uint32_t dx = D[x];
+      if (x == root || dx == kInf) continue;
+      const bool tr = transit(x);
+      for (uint32_t e0 = g.row_ptr[x]; e0 < g.row_ptr[x + 1] && !bail; e0 += 64) {
+        const uint32_t e = e0 + lane;
+        bool tight = false, shorter = false;
+        uint32_t y = 0;
+        if (e < g.row_ptr[x + 1]) {
+          y = g.colx[e];
+          if (!(y & kDown) && y != x) {
+            const uint64_t nd = (uint64_t)dx + (a.hop ? 1u : g.w[e]);
+            shorter = tr && nd < D[y];
+            tight = D[y] != kInf && nd == D[y];
+          }
+        }
+        if (__ballot(shorter)) {
+          bail = true;
+          break;
+        }
+        uint64_t m = __ballot(tight);
+        while (m && !bail) {
+          const int l = __ffsll((unsigned long long)m) - 1;
+          m &= m - 1;
+          const uint32_t ys = __shfl((int)y, l, 64);
+          const int r = rederive(ys);
+          if (r == 2) bail = true;
+          else if (r == 1) push(ys);
+        }
+      }
       continue;
     }
     for (int dir = 0; dir < 2 && !bail; ++dir) {

@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--planes", type=int, default=8)
     ap.add_argument("--batch", type=int, default=16384)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--sample", type=int, default=256,
+                    help="roots per class recomputed (and checked) on a weighted patched graph")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     t0 = time.perf_counter()
@@ -67,7 +69,10 @@ def main():
             kmax=int(nbrs[r].max()),
             dist=torch.empty((r.size, V), dtype=torch.int32, device=dev),
             nh=torch.empty((r.size, V, c.nh_words), dtype=torch.int32, device=dev),
-            flag=torch.empty(r.size, dtype=torch.uint8, device=dev))
+            flag=torch.empty(r.size, dtype=torch.uint8, device=dev),
+            status=torch.empty(r.size, dtype=torch.int32, device=dev),
+            dist2=torch.empty((r.size, V), dtype=torch.int32, device=dev),
+            nh2=torch.empty((r.size, V, c.nh_words), dtype=torch.int32, device=dev))
 
     def run_all(dst="dist", nh="nh"):
         for c in classes:
@@ -112,7 +117,9 @@ def main():
         ("spine link metric 1 -> 10 (FSW-SSW)", "link", pick_link("2-", "1-", 2), 1, 10),
         ("fabric switch overloaded (FSW)", "node", names.index("2-7-3"), None, None),
     ]
-    for title, kind, obj, up1, m1 in scenarios:
+    # pass 0 warms every code path up (first launches load kernels and
+    # allocate); pass 1 is timed and printed
+    for title, kind, obj, up1, m1, rep in [sc + (r,) for r in range(2) for sc in scenarios]:
         changes, ups, nodes = [], [], []
         if kind == "link":
             lo, hi = link_state(obj)
@@ -147,56 +154,67 @@ def main():
                                              changes, c.extra["flag"].data_ptr(),
                                              stream=s.cuda_stream) for c in classes])
         n_aff = int(sum(int(c.extra["flag"].sum()) for c in classes))
-        for c in classes:
-            c.extra["status"] = torch.empty(c.extra["ids"].size, dtype=torch.int32, device=dev)
         t_repair = timed(lambda: [eng.repair(c.extra["roots"].data_ptr(), c.extra["ids"].size,
                                              c.nh_words, c.extra["dist"].data_ptr(),
                                              c.extra["nh"].data_ptr(), changes,
                                              c.extra["status"].data_ptr(), stream=s.cuda_stream)
                                   for c in classes])
-        sel = []
-        for c in classes:
-            f = c.extra["status"].cpu().numpy().astype(bool)
-            sel.append(np.nonzero(f)[0])
-        n_rerun = int(sum(x.size for x in sel))
+        n_rerun = [0]
 
         def rerun():
-            for c, idx in zip(classes, sel):
-                if idx.size == 0:
-                    continue
+            # the runs the repair flagged, into the front rows of the scratch
+            # buffers, then copied over their resident rows
+            for c in classes:
                 x = c.extra
-                sub = torch.from_numpy(idx).to(dev)
+                sub = torch.nonzero(x["status"]).flatten()
+                k = int(sub.numel())
+                n_rerun[0] += k
+                if k == 0:
+                    continue
                 r = x["roots"][sub]
-                d = torch.empty((idx.size, V), dtype=torch.int32, device=dev)
-                h = torch.empty((idx.size, V, c.nh_words), dtype=torch.int32, device=dev)
-                eng.run_dev(r.data_ptr(), idx.size, c.nh_words, flags=flags, d_dist=d.data_ptr(),
-                            d_nh=h.data_ptr(), stream=s.cuda_stream, max_root_neighbors=x["kmax"])
-                x["dist"][sub] = d
-                x["nh"][sub] = h
+                eng.run_dev(r.data_ptr(), k, c.nh_words, flags=flags, d_dist=x["dist2"].data_ptr(),
+                            d_nh=x["nh2"].data_ptr(), stream=s.cuda_stream, max_root_neighbors=x["kmax"])
+                x["dist"].index_copy_(0, sub, x["dist2"][:k])
+                x["nh"].index_copy_(0, sub, x["nh2"][:k])
         t_rerun = timed(rerun)
-        # check: a full re-run of every root under the new state
+        # the reference's behaviour: every result recomputed on the new graph.
+        # A weighted patched graph runs the per-root Dial kernels (~ms per
+        # root at F100k): there the recompute and the check cover the first
+        # `sample` roots of each class and the time is scaled to all roots.
+        weighted = m1 is not None and m1 != 1
+        lim = args.sample if weighted else None
+
+        def full_new():
+            for c in classes:
+                x = c.extra
+                k = x["ids"].size if lim is None else min(lim, x["ids"].size)
+                eng.run_dev(x["roots"].data_ptr(), k, c.nh_words, flags=flags,
+                            d_dist=x["dist2"].data_ptr(), d_nh=x["nh2"].data_ptr(),
+                            stream=s.cuda_stream, max_root_neighbors=x["kmax"])
+        t_full_new = timed(full_new)
+        done = sum(x.extra["ids"].size if lim is None else min(lim, x.extra["ids"].size)
+                   for x in classes)
+        t_full_new *= sum(c.extra["ids"].size for c in classes) / done
         ok = True
         for c in classes:
             x = c.extra
-            x["dist2"] = torch.empty_like(x["dist"])
-            x["nh2"] = torch.empty_like(x["nh"])
-        run_all("dist2", "nh2")
-        torch.cuda.synchronize()
-        for c in classes:
-            x = c.extra
-            ok &= bool(torch.equal(x["dist"], x["dist2"]) and torch.equal(x["nh"], x["nh2"]))
-            del x["dist2"], x["nh2"]
+            k = x["ids"].size if lim is None else min(lim, x["ids"].size)
+            ok &= bool(torch.equal(x["dist"][:k], x["dist2"][:k]) and torch.equal(x["nh"][:k], x["nh2"][:k]))
         unpatch()
         run_all()
         torch.cuda.synchronize()
-        inc = t_patch + t_repair + t_rerun
+        inc = t_patch + t_repair + t_rerun  # the affected check is informational
+        if rep == 0:
+            continue
         print(json.dumps({
             "scenario": title, "roots": int(sum(c.per_step for c in classes)),
-            "affected_roots": n_aff, "rerun_roots": n_rerun, "patch_ms": round(t_patch, 3),
+            "affected_roots": n_aff, "rerun_roots": n_rerun[0], "patch_ms": round(t_patch, 3),
             "affected_check_ms": round(t_flag, 3), "repair_ms": round(t_repair, 3),
             "rerun_ms": round(t_rerun, 3),
-            "incremental_ms": round(inc, 3), "full_recompute_ms": round(full_ms, 3),
-            "speedup": round(full_ms / inc, 2), "identical_to_full_rerun": ok}), flush=True)
+            "incremental_ms": round(inc, 3), "full_recompute_ms": round(t_full_new, 3),
+            "full_recompute_before_ms": round(full_ms, 3),
+            "full_recompute_scaled_from_sample": bool(lim),
+            "speedup": round(t_full_new / inc, 2), "identical_to_full_rerun": ok}), flush=True)
 
 
 if __name__ == "__main__":

@@ -71,7 +71,7 @@ for W in args.W:
                     ts.append(a.elapsed_time(b))
             eng.sync(s.cuda_stream)
             ms = float(np.median(ts))
-            print(json.dumps(dict(W=W, n=n, plan=plan, ms=round(ms, 3),
+            print(json.dumps(dict(W=W, n=n, order=args.order, pack=os.environ.get("OSPF_MS_PACK"), plan=plan, ms=round(ms, 3),
                                   spf_s=round(n / ms * 1e3, 1),
                                   us_per_root=round(ms * 1e3 / n, 2),
                                   gteps=round(n * E / ms / 1e6, 2))), flush=True)

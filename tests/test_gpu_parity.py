@@ -578,3 +578,51 @@ def test_ucmp_random_graphs_match_oracle(seed, algo):
         if len(by_d) > 1:
             mixed = {by_d[sorted(by_d)[0]][0]: 1, by_d[sorted(by_d)[-1]][0]: 1}
             assert p.ucmp(root, mixed, algo) == o.ucmp(root, mixed, algo) == {}
+
+
+@pytest.mark.parametrize("case", ["overload", "unoverload", "link_down", "metric"])
+def test_engine_repair_wide_and_node_events(case):
+    """Repair with spine roots wider than 8 next-hop words (300 pods: W = 10)
+    and with overload toggles; repaired rows (status 0) equal fresh runs."""
+    import torch
+    p = LinkState(stream=T.fabric(pods=300, planes=2, ssw_per_plane=4, rsw_per_pod=4))
+    csr = p.csr()
+    names = p.node_names()
+    V = p.num_nodes()
+    eng = Engine(0)
+    eng.load(csr)
+    W = int(max(eng.nh_words(r) for r in range(V)))
+    assert W >= 10
+    roots = np.arange(V, dtype=np.uint32)
+    rp, lid = csr["row_ptr"], csr["link_id"]
+    owner = np.repeat(np.arange(V), np.diff(rp.astype(np.int64)))
+    fsw = names.index("2-17-1")
+    if case == "unoverload":
+        eng.update_nodes([fsw], [1], version=2)
+    before = eng.run(roots, W)
+    if case in ("overload", "unoverload"):
+        eng.update_nodes([fsw], [1 if case == "overload" else 0], version=3)
+        ch = [(1, fsw, 0, 0, 0, 0, 0, 0, 0)]
+    else:
+        rsw = names.index("3-42-2")
+        e = next(int(e) for e in range(rp[rsw], rp[rsw + 1]) if csr["col"][e] == names.index("2-42-0"))
+        l = int(lid[e])
+        ee = np.nonzero(lid == l)[0]
+        lo, hi = (ee[0], ee[1]) if owner[ee[0]] <= owner[ee[1]] else (ee[1], ee[0])
+        up1, m1 = (0, 1) if case == "link_down" else (1, 2)
+        ch = [(0, int(owner[lo]), int(owner[hi]), 1, 1, 1, up1, m1, m1)]
+        eng.update_links([(l, up1, m1, m1)], version=3)
+    d_roots = torch.from_numpy(roots.view(np.int32)).cuda()
+    d_dist = torch.from_numpy(before["dist"].view(np.int32)).cuda()
+    d_nh = torch.from_numpy(before["nh"].view(np.int32)).cuda()
+    st = torch.zeros(V, dtype=torch.int32, device="cuda")
+    eng.repair(d_roots.data_ptr(), V, W, d_dist.data_ptr(), d_nh.data_ptr(), ch, st.data_ptr())
+    eng.sync()
+    ref = eng.run(roots, W)
+    ok = st.cpu().numpy() == 0
+    rd = d_dist.cpu().numpy().view(np.uint32)
+    rn = d_nh.cpu().numpy().view(np.uint32)
+    assert np.array_equal(rd[ok], ref["dist"][ok]) and np.array_equal(rn[ok], ref["nh"][ok])
+    spines = np.array([n.startswith("1-") for n in names])
+    assert ok.mean() > 0.3, ok.mean()
+    assert (ok & spines).any()  # wide rows repaired too
