@@ -7,6 +7,10 @@
 #include <algorithm>
 #include <functional>
 #include <stdexcept>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <thread>
 #include <tuple>
 
 namespace odl {
@@ -292,8 +296,52 @@ LinkStateChange LinkState::deleteAdjacencyDatabase(const std::string& node) {
 }
 
 // ---------------------------------------------------------------- snapshot
+namespace {
+// run f(lo, hi) over [0, n) in chunks of 512 handed out to up to 16 threads
+// (rows differ in length by 1000x: spines vs racks)
+template <class F>
+void parallelRows(uint32_t n, F&& f) {
+  constexpr uint32_t kChunk = 512;
+  const uint32_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const uint32_t nt = std::max(1u, std::min(hw, n / (4 * kChunk)));
+  if (nt == 1) {
+    f(0u, n);
+    return;
+  }
+  std::atomic<uint32_t> next{0};
+  auto work = [&] {
+    for (;;) {
+      const uint32_t lo = next.fetch_add(kChunk);
+      if (lo >= n) return;
+      f(lo, std::min(n, lo + kChunk));
+    }
+  };
+  std::vector<std::thread> th;
+  th.reserve(nt - 1);
+  for (uint32_t t = 1; t < nt; ++t) th.emplace_back(work);
+  work();
+  for (auto& x : th) x.join();
+}
+}  // namespace
+
+// Rows in parallel (threads over node ranges; the link sets are only read):
+// 1. each row gathers its links (neighbour id, linksFromNode position, metric
+//    from this end) and counts the links it sees first (smaller end id),
+//    recording its own id on its end of each Link;
+// 2. prefix sums give row offsets and link ids -- the same ids a sequential
+//    sweep in (node id, linksFromNode order) hands out on first sight;
+// 3. the lower end writes the link id into the Link, the upper end reads it;
+// 4. rows are sorted by (neighbour id, rank) and written, then twins.
 const LinkState::Csr& LinkState::snapshot() {
   if (snapVersion_ == version_) return csr_;
+  const bool tm = getenv("ODL_SNAP_TIMING") != nullptr;
+  auto t0 = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (!tm) return;
+    auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "snapshot %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(t - t0).count());
+    t0 = t;
+  };
   rawMetric_.clear();  // dist rows are indexed by the old node ids
   Csr c;
   c.names.reserve(adjDbs_.size());
@@ -305,45 +353,61 @@ const LinkState::Csr& LinkState::snapshot() {
   c.rowPtr.assign(V + 1, 0);
   c.noTransit.assign(V, 0);
   struct Ent {
-    uint32_t v, rank, lid, metric;
-    uint8_t up;
-    bool low;
+    uint32_t v, rank, metric;
+    uint8_t up, low, end;
+    const LinkPtr* link;
   };
-  std::vector<Ent> ents;
-  ents.reserve(allLinks_.size() * 2);
-  for (uint32_t u = 0; u < V; ++u) {
-    const std::string& un = c.names[u];
-    c.noTransit[u] = isNodeOverloaded(un) ? 1 : 0;
-    const size_t first = ents.size();
-    uint32_t rank = 0;
-    for (const auto& l : linksFromNode(un)) {
-      auto it = c.linkIds.find(l.get());
-      uint32_t lid;
-      if (it == c.linkIds.end()) {
-        lid = (uint32_t)c.links.size();
-        c.linkIds.emplace(l.get(), lid);
-        c.links.push_back(l);
-      } else {
-        lid = it->second;
+  std::vector<std::vector<Ent>> rows(V);
+  std::vector<uint32_t> nfirst(V + 1, 0);
+  parallelRows(V, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t u = lo; u < hi; ++u) {
+      const std::string& un = c.names[u];
+      c.noTransit[u] = isNodeOverloaded(un) ? 1 : 0;
+      const LinkSet& ls = linksFromNode(un);
+      auto& row = rows[u];
+      row.reserve(ls.size());
+      uint32_t rank = 0, nf = 0;
+      for (const auto& l : ls) {
+        Ent e;
+        e.end = (uint8_t)l->endIndex(un);
+        l->snapEnd[e.end] = u;
+        if (e.end == 0 && l->otherNode(un) == un) l->snapEnd[1] = u;  // a self-loop
+        const Metric m = l->metricOfEnd(e.end);
+        e.v = kInf;  // the other end's id: written by its own row
+        e.rank = rank++;
+        // metric outside u32 (negative i32 wrapped to u64) is out of the engine
+        // contract; mark it with 0 so ospf_load_graph rejects it if usable.
+        e.metric = (m >= 1 && m <= 0xFFFFFFFFull) ? (uint32_t)m : 0u;
+        e.up = l->isUp() ? 1 : 0;
+        // the lower end by name = by id sees the link first in id order
+        e.low = (l->lowNode() == un) ? 1 : 0;
+        e.link = &l;
+        nf += e.low;
+        row.push_back(e);
       }
-      const Metric m = l->metricFrom(un);
-      Ent e;
-      e.v = c.ids.at(l->otherNode(un));
-      e.rank = rank++;
-      e.lid = lid;
-      // metric outside u32 (negative i32 wrapped to u64) is out of the engine
-      // contract; mark it with 0 so ospf_load_graph rejects it if usable.
-      e.metric = (m >= 1 && m <= 0xFFFFFFFFull) ? (uint32_t)m : 0u;
-      e.up = l->isUp() ? 1 : 0;
-      e.low = (l->lowNode() == un);
-      ents.push_back(e);
+      nfirst[u + 1] = nf;
+      c.rowPtr[u + 1] = (uint32_t)row.size();
     }
-    std::sort(ents.begin() + first, ents.end(), [](const Ent& a, const Ent& b) {
-      return a.v != b.v ? a.v < b.v : a.rank < b.rank;
-    });
-    c.rowPtr[u + 1] = (uint32_t)ents.size();
+  });
+  for (uint32_t u = 0; u < V; ++u) {
+    nfirst[u + 1] += nfirst[u];
+    c.rowPtr[u + 1] += c.rowPtr[u];
   }
-  const size_t E = ents.size();
+  lap("gather");
+  const size_t E = c.rowPtr[V];
+  c.links.resize(nfirst[V]);
+  parallelRows(V, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t u = lo; u < hi; ++u) {
+      uint32_t lid = nfirst[u];
+      for (auto& e : rows[u]) {
+        e.v = (*e.link)->snapEnd[e.end ^ 1];
+        if (!e.low) continue;
+        (*e.link)->snapLid = lid;
+        c.links[lid++] = *e.link;
+      }
+    }
+  });
+  lap("link ids");
   c.col.resize(E);
   c.metric.resize(E);
   c.linkId.resize(E);
@@ -351,18 +415,44 @@ const LinkState::Csr& LinkState::snapshot() {
   c.linkRank.resize(E);
   c.edgeUp.resize(E);
   std::vector<uint32_t> side(c.links.size() * 2, kInf);
-  for (size_t e = 0; e < E; ++e) {
-    c.col[e] = ents[e].v;
-    c.metric[e] = ents[e].metric;
-    c.linkId[e] = ents[e].lid;
-    c.linkRank[e] = ents[e].rank;
-    c.edgeUp[e] = ents[e].up;
-    side[ents[e].lid * 2 + (ents[e].low ? 0 : 1)] = (uint32_t)e;
-  }
-  for (size_t e = 0; e < E; ++e) c.twin[e] = side[ents[e].lid * 2 + (ents[e].low ? 1 : 0)];
+  parallelRows(V, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t u = lo; u < hi; ++u) {
+      auto& row = rows[u];
+      std::sort(row.begin(), row.end(), [](const Ent& a, const Ent& b) {
+        return a.v != b.v ? a.v < b.v : a.rank < b.rank;
+      });
+      size_t e = c.rowPtr[u];
+      for (const auto& x : row) {
+        const uint32_t lid = (*x.link)->snapLid;
+        c.col[e] = x.v;
+        c.metric[e] = x.metric;
+        c.linkId[e] = lid;
+        c.linkRank[e] = x.rank;
+        c.edgeUp[e] = x.up;
+        side[lid * 2ull + (x.low ? 0 : 1)] = (uint32_t)e;  // each (link, end) once
+        ++e;
+      }
+    }
+  });
+  parallelRows(V, [&](uint32_t lo, uint32_t hi) {
+    for (size_t e = c.rowPtr[lo]; e < c.rowPtr[hi]; ++e) {
+      const uint32_t lid = c.linkId[e];
+      const uint32_t mine = side[lid * 2ull] == e ? 0u : 1u;
+      c.twin[e] = side[lid * 2ull + (1u - mine)];
+    }
+  });
+  lap("rows");
   csr_ = std::move(c);
+  lap("move");
   snapVersion_ = version_;
   return csr_;
+}
+
+uint32_t LinkState::linkIdOf(const Link& l) const {
+  const uint32_t lid = l.snapLid;
+  if (lid >= csr_.links.size() || csr_.links[lid].get() != &l)
+    throw std::out_of_range("link not in the CSR snapshot");
+  return lid;
 }
 
 void LinkState::ensureEngine() {
@@ -644,7 +734,7 @@ const std::vector<Path>& LinkState::getKthPaths(const std::string& src, const st
     snapshot();
     const uint32_t s = csr_.ids.at(src);
     std::vector<uint32_t> ign;
-    for (const auto& l : skip) ign.push_back(csr_.linkIds.at(l.get()));
+    for (const auto& l : skip) ign.push_back(linkIdOf(*l));
     std::sort(ign.begin(), ign.end());
     std::vector<std::vector<uint32_t>> igns{ign};
     std::vector<uint32_t> dist;
@@ -765,7 +855,7 @@ void LinkState::applyIncremental(const std::vector<LinkDelta>& links,
   std::vector<ospf_link_update> ups;
   for (const auto& d : links) {
     const Link& l = *d.link;
-    const uint32_t lid = csr_.linkIds.at(&l);
+    const uint32_t lid = linkIdOf(l);
     const uint32_t lo = csr_.ids.at(l.lowNode());
     auto clamp = [](Metric m) { return (m >= 1 && m <= 0xFFFFFFFFull) ? (uint32_t)m : 0u; };
     const uint32_t mlo = clamp(l.metricFrom(l.lowNode())), mhi = clamp(l.metricFrom(l.highNode()));

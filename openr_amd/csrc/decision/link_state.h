@@ -73,6 +73,12 @@ class Link {
   std::string key() const;                  // "n1%if1|n2%if2" (ordered)
 
   const size_t hash;
+  // id of this link in the CSR snapshot that last listed it (LinkState::linkIdOf
+  // checks it still does)
+  mutable uint32_t snapLid = 0xFFFFFFFFu;
+  mutable uint32_t snapEnd[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};  // snapshot node ids of the ends
+  int endIndex(const std::string& n) const { return end_[0].node == n ? 0 : 1; }
+  Metric metricOfEnd(int i) const { return end_[i].metric; }
 
  private:
   struct End {
@@ -222,9 +228,9 @@ class LinkState {
     std::vector<uint32_t> rowPtr, col, metric, linkId, twin, linkRank;
     std::vector<uint8_t> edgeUp, noTransit;
     std::vector<LinkPtr> links;                     // link id -> link
-    std::unordered_map<const Link*, uint32_t> linkIds;
   };
   const Csr& snapshot();
+  uint32_t linkIdOf(const Link& l) const;  // id in the current snapshot
 
  private:
   struct RawRun {  // one engine run kept for pathLinks / trace reconstruction
