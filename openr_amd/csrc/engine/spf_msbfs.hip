@@ -88,7 +88,15 @@ struct VB {
   const uint64_t* igm;
   __device__ VB(const MsArgs& a, uint32_t vbl_, uint32_t V_, int kp, uint32_t E = 0)
       : vbl(vbl_), V(V_) {
-    const uint32_t vb = a.vb0 + vbl;
+    // Multi-pass rounds: the passes of one batch write different next-hop
+    // words of the same row entries, so they go to one XCD (workgroup i of a
+    // launch runs on XCD i % 8 and serves state slot vbl = i % nb): slot vbl
+    // takes round position (vbl % 8) * nb / 8 + vbl / 8, and a batch's passes
+    // (consecutive positions) fill their lines in one L2 instead of writing
+    // back partial lines from several.
+    uint32_t t = vbl;
+    if (a.npass > 1 && (a.nb & 7u) == 0) t = (vbl & 7u) * (a.nb >> 3) + (vbl >> 3);
+    const uint32_t vb = a.vb0 + t;
     g = vb % a.npass;
     rix0 = (vb / a.npass) * a.R;
     const uint32_t nv = min(a.R, a.n - rix0);

@@ -24,6 +24,8 @@ ap.add_argument("--W", type=int, nargs="+", default=[1, 3, 56])
 ap.add_argument("--n", type=int, nargs="+", default=[256, 1024, 4096])
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--blocks", type=int, nargs="+", default=[0])
+ap.add_argument("--envs", nargs="+", default=[""],
+                help="engine env configs to sweep, each 'K=V,K=V' ('' = defaults)")
 ap.add_argument("--order", choices=["auto", "random", "locality"], default="auto",
                 help="auto = locality for single-word classes (as bench.py)")
 args = ap.parse_args()
@@ -51,7 +53,10 @@ for W in args.W:
         dist = torch.empty((n, V), dtype=torch.int32, device="cuda")
         nh = torch.empty((n, V, W), dtype=torch.int32, device="cuda")
         dig = torch.empty((n, 3), dtype=torch.int64, device="cuda")
-        for blk in args.blocks:
+        for blk, envc in [(b_, e_) for b_ in args.blocks for e_ in args.envs]:
+            for kv in [x for x in envc.split(",") if x]:
+                k_, v_ = kv.split("=")
+                os.environ[k_] = v_
             if blk:
                 os.environ["OSPF_BLOCK"] = str(blk)
             else:
@@ -70,8 +75,10 @@ for W in args.W:
                 if r:
                     ts.append(a.elapsed_time(b))
             eng.sync(s.cuda_stream)
+            for kv in [x for x in envc.split(",") if x]:
+                os.environ.pop(kv.split("=")[0], None)
             ms = float(np.median(ts))
-            print(json.dumps(dict(W=W, n=n, order=args.order, pack=os.environ.get("OSPF_MS_PACK"), plan=plan, ms=round(ms, 3),
+            print(json.dumps(dict(W=W, n=n, env=envc, order=args.order, pack=os.environ.get("OSPF_MS_PACK"), plan=plan, ms=round(ms, 3),
                                   spf_s=round(n / ms * 1e3, 1),
                                   us_per_root=round(ms * 1e3 / n, 2),
                                   gteps=round(n * E / ms / 1e6, 2))), flush=True)
