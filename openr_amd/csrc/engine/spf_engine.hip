@@ -288,11 +288,25 @@ int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
   uint32_t chunk = b->n_roots;
   if (row_bytes)
     chunk = (uint32_t)std::max<size_t>(64, std::min<size_t>(chunk, (2ull << 30) / row_bytes) / 64 * 64);
+  // wide rows: the rows kernels stage each pass's words word-major
+  // ([root][W][V], whole-line stores) and one interleave pass writes the
+  // [V][W] rows; the passes' scattered word stores otherwise write a 4-B word
+  // per W-word row entry. Measured on F100k: W = 56 class 4.55 -> 3.98 ms;
+  // W = 3 slower (11.1 -> 12.2 ms: the rows kernel there is not store-bound and
+  // the extra pass costs 1.3 ms), hence the threshold. OSPF_MS_ILV=0/1 forces.
+  bool ilv = defer && W >= 8 && W <= 64 && (flags & OSPF_WANT_NH) && !nh_scr;
+  if (const char* e = getenv("OSPF_MS_ILV"))
+    ilv = atoi(e) && defer && W > 1 && W <= 64 && (flags & OSPF_WANT_NH) && !nh_scr;
+  if (ilv) {
+    const size_t cap = 8ull << 30, per_root = (size_t)V * W * 4ull;
+    if ((size_t)chunk * per_root > cap)
+      chunk = (uint32_t)std::max<size_t>(64, cap / per_root / 64 * 64);
+  }
   const uint32_t nb_max =
       std::min<uint32_t>(nb_cap, ((std::min(chunk, b->n_roots) + sh.R - 1) / sh.R) * npass);
   const size_t state_bytes = per_vb * nb_max;
   const size_t dist_bytes = dist_scr ? align_up((size_t)chunk * V * 4ull, 256) : 0;
-  const size_t nh_bytes = nh_scr ? align_up((size_t)chunk * V * W * 4ull, 256) : 0;
+  const size_t nh_bytes = (nh_scr || ilv) ? align_up((size_t)chunk * V * W * 4ull, 256) : 0;
   int rc = OSPF_OK;
   char* sp = stream_scratch(c, s, state_bytes + dist_bytes + nh_bytes, &rc);
   if (rc) return rc;
@@ -319,6 +333,7 @@ int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
                       : ((flags & OSPF_WANT_DIST) ? b->d_dist + (size_t)r0 * V : nullptr);
     a.nh = nh_scr ? (uint32_t*)(sp + state_bytes + dist_bytes)
                   : ((flags & OSPF_WANT_NH) ? b->d_nh + (size_t)r0 * V * W : nullptr);
+    a.nhs = ilv ? (uint32_t*)(sp + state_bytes + dist_bytes) : nullptr;
     const uint32_t total_vb = ((n + sh.R - 1) / sh.R) * npass;
     for (uint32_t vb0 = 0; vb0 < total_vb; vb0 += nb_max) {
       a.vb0 = vb0;
@@ -336,6 +351,11 @@ int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
                                           (size_t)a.nb * lmax * 8ull, s));
       hipError_t e = ospf::launch_msbfs_round(kp, c->g, a, c->depth_bound, s);
       if (e != hipSuccess) return hip_fail(c, e, "launch_msbfs_round");
+    }
+    if (ilv) {
+      hipError_t e = ospf::launch_nh_interleave(a.nhs, a.nh, n, V, W,
+                                                std::min(W, npass * sh.OW), s);
+      if (e != hipSuccess) return hip_fail(c, e, "launch_nh_interleave");
     }
     if (dig && !defer) {
       hipError_t e = ospf::launch_row_digest(c->g, n, a.dist, a.nh, W, b->d_digest + r0, s);

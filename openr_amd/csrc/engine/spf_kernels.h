@@ -128,6 +128,9 @@ struct MsArgs {
   uint32_t push_div;      // level d pushes when frontier edge mass * push_div < E
   uint32_t* dist;         // [n][V] or null
   uint32_t* nh;           // [n][V][W] or null
+  uint32_t* nhs;          // [n][W][V] word-major staging (defer, W > 1) or null:
+                          //   msbfs_rows stores each pass's words as whole lines,
+                          //   launch_nh_interleave then writes the [V][W] rows
   uint64_t* seen;         // [nb][V]
   uint64_t* front;        // [2][nb][V][2] {frontier, with-planes} of level d in front[d & 1]
   uint64_t* accb;         // [nb][V]      push accumulator (zero between levels)
@@ -149,6 +152,9 @@ struct MsArgs {
 // kp = 8, 16 or 32 planes per node; depth_bound bounds the BFS level count
 hipError_t launch_msbfs_round(int kp, const DevGraph& g, const MsArgs& a, uint32_t depth_bound,
                               hipStream_t s);
+// nh[r][v][w] = w < wcomp ? nhs[r][w][v] : 0 for n rows (whole-line stores)
+hipError_t launch_nh_interleave(const uint32_t* nhs, uint32_t* nh, uint32_t n, uint32_t V,
+                                uint32_t W, uint32_t wcomp, hipStream_t s);
 // KSP2 mode (kp = 0): init + levels [d0, d1) only; lev holds the distances
 hipError_t launch_msbfs_ksp(const DevGraph& g, const MsArgs& a, uint32_t d0, uint32_t d1,
                             hipStream_t s);

@@ -616,12 +616,13 @@ __global__ void __launch_bounds__(256) msbfs_rows_kernel(DevGraph g, MsArgs a) {
       }
     }
     if (a.nh) {
-      if (a.W == 1) {
+      if (a.W == 1 || a.nhs) {  // word-major rows: 16 lanes x 16 B per root
         for (uint32_t i = tid; i < 64u * 16u; i += kBlock) {
           const uint32_t r = i >> 4, q = i & 15u;
           if (r >= nr) break;
           const uint32_t* src = &s_nh[r * 65u + 4u * q];
-          uint32_t* row = a.nh + (size_t)(b.rix0 + r) * V + v0 + 4u * q;
+          uint32_t* row = (a.nhs ? a.nhs + ((size_t)(b.rix0 + r) * a.W + wg) * V
+                                 : a.nh + (size_t)(b.rix0 + r) * V) + v0 + 4u * q;
           if (vec) {
             *reinterpret_cast<uint4*>(row) = make_uint4(src[0], src[1], src[2], src[3]);
           } else {
@@ -640,7 +641,7 @@ __global__ void __launch_bounds__(256) msbfs_rows_kernel(DevGraph g, MsArgs a) {
     __syncthreads();  // s_nh is rewritten for the next word
   }
   // words past the computed passes are zero for every node
-  if (a.nh && b.g == a.npass - 1 && a.npass * a.OW < a.W) {
+  if (a.nh && !a.nhs && b.g == a.npass - 1 && a.npass * a.OW < a.W) {
     for (uint32_t i = tid; i < 64u * 64u; i += kBlock) {
       const uint32_t r = i >> 6, n = i & 63u;
       if (r >= nr) break;
@@ -782,7 +783,38 @@ __global__ void __launch_bounds__(256) ksp_mask_kernel(DevGraph g, MsArgs a, con
   }
 }
 
+// Word-major staging -> [V][W] rows: block = (root, run of nodes); the
+// block's W words of each node are read word by word (coalesced along the
+// nodes), transposed through LDS and stored as one contiguous span, so every
+// row line is written whole, once.
+constexpr uint32_t kIlvWords = 4096;  // LDS words per block (16 KB)
+__global__ void __launch_bounds__(256) nh_interleave_kernel(const uint32_t* nhs, uint32_t* nh,
+                                                            uint32_t V, uint32_t W, uint32_t wcomp,
+                                                            uint32_t span, uint32_t runs) {
+  __shared__ uint32_t s[kIlvWords];
+  const uint32_t r = blockIdx.x / runs, v0 = (blockIdx.x % runs) * span;
+  const uint32_t nv = min(span, V - v0), tot = nv * W;
+  const uint32_t* src = nhs + (size_t)r * W * V + v0;
+  for (uint32_t i = threadIdx.x; i < tot; i += kBlock) {
+    const uint32_t w = i / nv, n = i - w * nv;
+    s[n * W + w] = w < wcomp ? src[(size_t)w * V + n] : 0u;
+  }
+  __syncthreads();
+  uint32_t* dst = nh + ((size_t)r * V + v0) * W;
+  for (uint32_t i = threadIdx.x; i < tot; i += kBlock) dst[i] = s[i];
+}
+
 }  // namespace
+
+hipError_t launch_nh_interleave(const uint32_t* nhs, uint32_t* nh, uint32_t n, uint32_t V,
+                                uint32_t W, uint32_t wcomp, hipStream_t s) {
+  if (W == 0 || W > kIlvWords / 64u) return hipErrorInvalidValue;
+  const uint32_t span = std::min<uint32_t>(1024u, (kIlvWords / W) / 64u * 64u);
+  const uint32_t runs = (V + span - 1) / span;
+  if (n) hipLaunchKernelGGL(nh_interleave_kernel, dim3(n * runs), dim3(kBlock), 0, s, nhs, nh, V, W,
+                            wcomp, span, runs);
+  return hipGetLastError();
+}
 
 hipError_t launch_msbfs_ksp(const DevGraph& g, const MsArgs& a, uint32_t d0, uint32_t d1,
                             hipStream_t s) {

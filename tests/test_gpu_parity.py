@@ -498,15 +498,19 @@ def test_msbfs_matches_per_root_bfs(seed, hop, defer, monkeypatch):
                                                  not hop, threads=8))
 
 
-@pytest.mark.parametrize("nb,R", [("1", None), ("3", None), ("8", None), ("32", "3"),
-                                  ("4", "7"), ("32", "20"), ("2", "1")])
-def test_msbfs_wide_roots_and_rounds(nb, R, monkeypatch):
+@pytest.mark.parametrize("nb,R,ilv", [("1", None, 1), ("3", None, 1), ("8", None, 1), ("32", "3", 1),
+                                      ("4", "7", 1), ("32", "20", 1), ("2", "1", 1),
+                                      ("8", None, 0), ("32", "20", 0)])
+def test_msbfs_wide_roots_and_rounds(nb, R, ilv, monkeypatch):
     """Spines with 140 distinct neighbours need 5 next-hop words = 5 passes
     per 64-root batch; OSPF_MS_NB bounds the (batch, pass) pairs per round so
     the sweep spans several rounds; nh_words above the need is zero-filled.
     OSPF_MS_R packs the bit-planes: R roots per batch, 64/R planes per word,
-    64/R next-hop words per pass."""
+    64/R next-hop words per pass. ilv: multi-word rows staged word-major and
+    interleaved (OSPF_MS_ILV=1) or stored word by word from each pass
+    (OSPF_MS_ILV=0; the default below 8 words)."""
     monkeypatch.setenv("OSPF_MS_NB", nb)
+    monkeypatch.setenv("OSPF_MS_ILV", str(ilv))
     if R:
         monkeypatch.setenv("OSPF_MS_R", R)
     st = T.fabric(pods=140, planes=2)
