@@ -74,12 +74,27 @@ def main():
             dist2=torch.empty((r.size, V), dtype=torch.int32, device=dev),
             nh2=torch.empty((r.size, V, c.nh_words), dtype=torch.int32, device=dev))
 
+    # width classes run side by side on their own streams (as bench.py does),
+    # for the full recompute and for every incremental step alike
+    streams = [torch.cuda.Stream(device=dev) for _ in classes]
+
+    def per_class(fn):
+        """fn(c, stream) for every class, each class on its own stream (torch
+        ops inside fn included), joined back into s"""
+        for c, cs in zip(classes, streams):
+            cs.wait_stream(s)
+            with torch.cuda.stream(cs):
+                fn(c, cs)
+        for cs in streams:
+            s.wait_stream(cs)
+
     def run_all(dst="dist", nh="nh"):
-        for c in classes:
+        def one(c, cs):
             x = c.extra
             eng.run_dev(x["roots"].data_ptr(), x["ids"].size, c.nh_words, flags=flags,
-                        d_dist=x[dst].data_ptr(), d_nh=x[nh].data_ptr(), stream=s.cuda_stream,
+                        d_dist=x[dst].data_ptr(), d_nh=x[nh].data_ptr(), stream=cs.cuda_stream,
                         max_root_neighbors=x["kmax"])
+        per_class(one)
 
     def timed(fn):
         torch.cuda.synchronize()
@@ -154,28 +169,32 @@ def main():
                                              changes, c.extra["flag"].data_ptr(),
                                              stream=s.cuda_stream) for c in classes])
         n_aff = int(sum(int(c.extra["flag"].sum()) for c in classes))
-        t_repair = timed(lambda: [eng.repair(c.extra["roots"].data_ptr(), c.extra["ids"].size,
-                                             c.nh_words, c.extra["dist"].data_ptr(),
-                                             c.extra["nh"].data_ptr(), changes,
-                                             c.extra["status"].data_ptr(), stream=s.cuda_stream)
-                                  for c in classes])
+        t_repair = timed(lambda: per_class(
+            lambda c, cs: eng.repair(c.extra["roots"].data_ptr(), c.extra["ids"].size,
+                                     c.nh_words, c.extra["dist"].data_ptr(),
+                                     c.extra["nh"].data_ptr(), changes,
+                                     c.extra["status"].data_ptr(), stream=cs.cuda_stream)))
         n_rerun = [0]
 
         def rerun():
-            # the runs the repair flagged, into the front rows of the scratch
+            # the runs the repair flagged (read back first: one host sync per
+            # class before any launch), into the front rows of the scratch
             # buffers, then copied over their resident rows
-            for c in classes:
-                x = c.extra
-                sub = torch.nonzero(x["status"]).flatten()
-                k = int(sub.numel())
-                n_rerun[0] += k
+            subs = [torch.nonzero(c.extra["status"]).flatten() for c in classes]
+            ks = [int(x.numel()) for x in subs]
+            n_rerun[0] += sum(ks)
+
+            def one(c, cs):
+                i = classes.index(c)
+                sub, k, x = subs[i], ks[i], c.extra
                 if k == 0:
-                    continue
+                    return
                 r = x["roots"][sub]
                 eng.run_dev(r.data_ptr(), k, c.nh_words, flags=flags, d_dist=x["dist2"].data_ptr(),
-                            d_nh=x["nh2"].data_ptr(), stream=s.cuda_stream, max_root_neighbors=x["kmax"])
+                            d_nh=x["nh2"].data_ptr(), stream=cs.cuda_stream, max_root_neighbors=x["kmax"])
                 x["dist"].index_copy_(0, sub, x["dist2"][:k])
                 x["nh"].index_copy_(0, sub, x["nh2"][:k])
+            per_class(one)
         t_rerun = timed(rerun)
         # the reference's behaviour: every result recomputed on the new graph.
         # A weighted patched graph runs the per-root Dial kernels (~ms per
@@ -185,12 +204,13 @@ def main():
         lim = args.sample if weighted else None
 
         def full_new():
-            for c in classes:
+            def one(c, cs):
                 x = c.extra
                 k = x["ids"].size if lim is None else min(lim, x["ids"].size)
                 eng.run_dev(x["roots"].data_ptr(), k, c.nh_words, flags=flags,
                             d_dist=x["dist2"].data_ptr(), d_nh=x["nh2"].data_ptr(),
-                            stream=s.cuda_stream, max_root_neighbors=x["kmax"])
+                            stream=cs.cuda_stream, max_root_neighbors=x["kmax"])
+            per_class(one)
         t_full_new = timed(full_new)
         done = sum(x.extra["ids"].size if lim is None else min(lim, x.extra["ids"].size)
                    for x in classes)
