@@ -570,17 +570,20 @@ __global__ void __launch_bounds__(256) msbfs_rows_kernel(DevGraph g, MsArgs a) {
   const uint32_t dr = tid >> 2, dn0 = 16u * (tid & 3u);
   uint64_t reached = 0, sumd = 0, h = 0;
   const bool vec = (V & 3u) == 0 && nv == 64u;
-  __syncthreads();
-  if (b.g == 0) {
-    if (a.digest && dr < nr) {
-      for (uint32_t n = dn0; n < dn0 + 16u && n < nv; ++n) {
-        const uint32_t l = s_lev[n * 64u + dr];
-        if (!l) continue;
-        reached += 1;
-        sumd += l - 1u;
-        h += s_dk[2u * n] * (uint64_t)l;
-      }
+  // the pass's words of root r (stage: s_nh[r][node]); the first word is
+  // staged before the barrier (nothing reads s_nh yet)
+  auto stage_words = [&](uint32_t w) {
+    for (uint32_t i = 0; i < 16u; ++i) {
+      const uint32_t r = 16u * pq + i;
+      if (r < nr) s_nh[r * 65u + pn] = pass_word<KP>(a, p, r, w);
     }
+  };
+  const uint32_t nw = b.g * a.OW < a.W ? min(a.OW, a.W - b.g * a.OW) : 0u;  // words of this pass
+  if (nw) stage_words(0);
+  __syncthreads();
+  // stores first, then the digest terms of the same LDS values: no barrier
+  // follows the last stores, so they drain under the digest work
+  if (b.g == 0) {
     if (a.dist) {
       for (uint32_t i = tid; i < 64u * 16u; i += kBlock) {  // (root, node quad)
         const uint32_t r = i >> 4, q = i & 15u;
@@ -600,20 +603,21 @@ __global__ void __launch_bounds__(256) msbfs_rows_kernel(DevGraph g, MsArgs a) {
         }
       }
     }
-  }
-  for (uint32_t w = 0; w < a.OW; ++w) {
-    const uint32_t wg = b.g * a.OW + w;  // next-hop word of the output row
-    if (wg >= a.W) break;
-    for (uint32_t i = 0; i < 16u; ++i) {
-      const uint32_t r = 16u * pq + i;
-      if (r < nr) s_nh[r * 65u + pn] = pass_word<KP>(a, p, r, w);
-    }
-    __syncthreads();
     if (a.digest && dr < nr) {
       for (uint32_t n = dn0; n < dn0 + 16u && n < nv; ++n) {
-        const uint32_t word = s_nh[dr * 65u + n];
-        if (word && s_lev[n * 64u + dr]) h += s_dk[2u * n + 1u] * digest_word_key(wg, word);
+        const uint32_t l = s_lev[n * 64u + dr];
+        if (!l) continue;
+        reached += 1;
+        sumd += l - 1u;
+        h += s_dk[2u * n] * (uint64_t)l;
       }
+    }
+  }
+  for (uint32_t w = 0; w < nw; ++w) {
+    const uint32_t wg = b.g * a.OW + w;  // next-hop word of the output row
+    if (w > 0) {
+      stage_words(w);
+      __syncthreads();
     }
     if (a.nh) {
       if (a.W == 1 || a.nhs) {  // word-major rows: 16 lanes x 16 B per root
@@ -638,7 +642,13 @@ __global__ void __launch_bounds__(256) msbfs_rows_kernel(DevGraph g, MsArgs a) {
         }
       }
     }
-    __syncthreads();  // s_nh is rewritten for the next word
+    if (a.digest && dr < nr) {
+      for (uint32_t n = dn0; n < dn0 + 16u && n < nv; ++n) {
+        const uint32_t word = s_nh[dr * 65u + n];
+        if (word && s_lev[n * 64u + dr]) h += s_dk[2u * n + 1u] * digest_word_key(wg, word);
+      }
+    }
+    if (w + 1 < nw) __syncthreads();  // s_nh is rewritten for the next word
   }
   // words past the computed passes are zero for every node
   if (a.nh && !a.nhs && b.g == a.npass - 1 && a.npass * a.OW < a.W) {
