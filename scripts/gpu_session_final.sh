@@ -1,11 +1,10 @@
-# Round-end confirmation: smoke(), incremental and KSP2 benches on the final build.
+# Round-end headline: the driver's default bench command, then a rocprofv3
+# kernel-trace summary of the same command.
 set -o pipefail
-T=${TAG:-s32}
+T=${TAG:-s37}
 mkdir -p gpurun_out/$T
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$T/smoke.log 2>&1 || { echo SMOKE_FAIL; tail -20 gpurun_out/$T/smoke.log; exit 1; }
-tail -1 gpurun_out/$T/smoke.log
-timeout -k 10 600 python -u scripts/bench_incremental.py > gpurun_out/$T/inc.jsonl 2> gpurun_out/$T/inc.err || { echo INC_FAIL; tail -20 gpurun_out/$T/inc.err; exit 1; }
-cut -c1-300 gpurun_out/$T/inc.jsonl
-timeout -k 10 400 python -u scripts/bench_ksp2.py --steps 3 > gpurun_out/$T/ksp.json 2> gpurun_out/$T/ksp.err || { echo KSP_FAIL; tail -20 gpurun_out/$T/ksp.err; exit 1; }
-cut -c1-300 gpurun_out/$T/ksp.json
+timeout -k 10 400 python -u bench.py > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err || { echo BENCH_FAIL; tail -20 gpurun_out/$T/bench.err; exit 1; }
+cut -c1-300 gpurun_out/$T/bench.json
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/$T/prof -o run --output-format csv -- python3 bench.py > gpurun_out/$T/prof_bench.json 2> gpurun_out/$T/prof.err || { echo PROF_FAIL; tail -20 gpurun_out/$T/prof.err; exit 1; }
+cut -d, -f1-4 gpurun_out/$T/prof/run_kernel_stats.csv | cut -c1-160 | head -12
