@@ -1,6 +1,6 @@
 # Parity, per-class timings (each class alone), the headline bench.
 set -o pipefail
-T=${TAG:-s36}
+T=${TAG:-s40}
 mkdir -p gpurun_out/$T
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/$T/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -40 gpurun_out/$T/pytest_gpu.log; exit 1; }
