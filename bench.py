@@ -1,18 +1,26 @@
 #!/usr/bin/env python3
-"""Benchmark: all-sources SPF + ECMP next-hops on the 100k-node fabric.
+"""Benchmark: all-sources SPF + ECMP next hops on the 100k-node fabric.
 
 BASELINE.json metric: "all-sources SPF/sec + GTEPS on 100k-node fabric
-topology at 1/2/4/8 GPUs". A *step* = one batch of roots per GPU run through
-the engine's device API (ospf_sssp_batch_dev): per-root distance rows,
-next-hop bitset rows and digests written to HBM, then (N > 1) the 24-B
-per-root digest records all-gathered over RCCL. Roots sweep a fixed
-permutation of every node (all sources); each step launches one kernel per
-next-hop width class (rack / fabric / spine switches), each on its own HIP
-stream. Ranks shard the roots with no data-path collective: scaling "weak".
+topology at 1/2/4/8 GPUs". A *step* = one all-sources sweep: every node of
+the topology is the root of one SPF run (LinkState::runSpf,
+openr/decision/LinkState.cpp:836-911) whose distance row and next-hop bitset
+row are written to HBM, plus a 24-B digest per run. The roots are split
+over the ranks (one process per GPU, contiguous slices of each next-hop width
+class), so the total work per step is fixed: scaling "strong". Each rank
+launches one engine call per width class (rack / fabric / spine switches),
+each on its own HIP stream; for N > 1 the digest records are all-gathered
+over RCCL. The timed steps' own digests of the CPU-sample roots are checked
+against the CPU restatement (`parity_vs_cpu_sample`).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
-       torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+Other topologies (parity / side benches, not the headline): fabric10k,
+fabric100k-w (metrics 1..64, seed 7), grid31, mesh1m (8,192 sampled roots).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--topology T]
+       torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
                 --master-port P bench.py --gpus N ...
+Profiling mode (one class alone, R launches on one stream, no JSON line):
+       python bench.py --class-only W --reps R
 """
 from __future__ import annotations
 
@@ -37,6 +45,7 @@ from openr_amd.linkstate import LinkState  # noqa: E402
 
 METRIC = "all-sources SPF/sec + GTEPS on 100k-node fabric topology at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+SEED = 0x5EED
 
 
 def log(*a):
@@ -44,32 +53,52 @@ def log(*a):
 
 
 def build_topology(name: str):
+    """-> (stream, description, weighted, default root count (0 = all))"""
     if name == "fabric100k":
-        return T.fabric(pods=1781, planes=8), "F100k fabric pods=1781 planes=8 (unit metric)"
+        return T.fabric(pods=1781, planes=8), "F100k fabric pods=1781 planes=8 (unit metric)", \
+            False, 0
     if name == "fabric10k":
-        return T.fabric(pods=173, planes=8), "F10k fabric pods=173 planes=8 (unit metric)"
+        return T.fabric(pods=173, planes=8), "F10k fabric pods=173 planes=8 (unit metric)", False, 0
     if name == "fabric100k-w":
         return (T.fabric(pods=1781, planes=8, weighted_seed=7),
-                "F100k fabric pods=1781 planes=8 (metric 1..64, seed 7)")
+                "F100k fabric pods=1781 planes=8 (metric 1..64, seed 7)", True, 0)
     if name == "grid31":
-        return T.grid(31), "G31 grid 31x31 (unit metric)"
+        return T.grid(31), "G31 grid 31x31 (unit metric)", False, 0
     if name == "mesh1m":
-        return T.mesh(1_000_000, seed=42), "M1M random-geometric mesh (metric 1..16)"
+        return T.mesh(1_000_000, seed=42), "M1M random-geometric mesh (metric 1..16)", True, 8192
     raise SystemExit(f"unknown topology {name}")
 
 
 def bytes_per_root(V: int, E: int, W: int) -> int:
-    """SURVEY.md §8(d) algorithmic bytes of one SPF run: CSR neighbour + weight
-    reads, row offsets, dist write, next-hop bitset write."""
+    """SURVEY.md §8(d) model of one SPF run: CSR neighbour + weight reads,
+    row offsets, dist write, next-hop bitset write. Every root is charged a
+    full CSR scan, which batched traversals do not make (alg_equiv only)."""
     return 8 * E + 4 * (V + 1) + 4 * V + 4 * V * W
 
 
+def compulsory_bytes(V: int, E: int, W: int, n: int, variant: int, npass: int,
+                     weighted: bool) -> int:
+    """Bytes a launch of n runs cannot avoid: the dist + next-hop rows it
+    writes (4V(1 + W) per run) plus the CSR reads its traversals need at
+    least once: the multi-source BFS (variant 5) scans neighbour ids + row
+    offsets once per 64-root pass (ceil(n / 64) * npass passes); a per-root
+    kernel scans them once per run, with both metric arrays when weighted."""
+    rows = n * 4 * V * (1 + W)
+    if variant == 5:
+        scans = -(-n // 64) * npass
+        per_scan = 4 * E + 4 * (V + 1)
+    else:
+        scans = n
+        per_scan = (12 if weighted else 4) * E + 4 * (V + 1)
+    return rows + scans * per_scan
+
+
 def pmc_traffic(profile_dir: str, key: str, roots: int):
-    """Measured HBM bytes per launch of the class `key` with `roots` roots from
+    """Measured HBM bytes per launch of class `key` with `roots` roots from
     the committed per-class rocprofv3 --pmc summary (profiles/<round>/
-    pmc_traffic.json, written by scripts/pmc_class_traffic.py: FETCH_SIZE x 2
-    (gfx950 correction) + WRITE_SIZE, summed over the class's kernels); None
-    when absent or measured at another batch size."""
+    pmc_traffic.json, scripts/pmc_class_traffic.py: FETCH_SIZE x 2 (gfx950
+    correction) + WRITE_SIZE, summed over the class's kernels); None when
+    absent or measured at another batch size."""
     path = os.path.join(profile_dir, "pmc_traffic.json")
     if not os.path.exists(path):
         return None
@@ -81,27 +110,53 @@ def pmc_traffic(profile_dir: str, key: str, roots: int):
     return e.get("hbm_bytes_per_launch") if e.get("roots_per_launch") == roots else None
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_threads() -> int:
+    """Host cores this process may use: the affinity mask, capped by
+    OMP_NUM_THREADS (the GPU box grants 16 and says so there)."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(omp))) if omp and omp.isdigit() else n
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=16384,
-                    help="roots per GPU per step (6 steps sweep all 100k sources of F100k)")
     ap.add_argument("--topology", default="fabric100k")
-    ap.add_argument("--cpu-sample", type=int, default=32)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--roots", type=int, default=-1,
+                    help="roots per step over all GPUs: 0 = every node (all-sources), k = a "
+                         "fixed sample of k nodes (seed 0x5eed); default per topology")
+    ap.add_argument("--roots-per-gpu", type=int, default=0,
+                    help="weak-scaling mode: each rank sweeps this many roots per step")
+    ap.add_argument("--cpu-sample", type=int, default=-1,
+                    help="roots of the reference-shaped CPU baseline (default 256; 16 on M1M)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the host cores granted")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-nh", action="store_true", help="skip next-hop output (diagnostic)")
     ap.add_argument("--serial-streams", action="store_true", help="one stream for all classes")
     ap.add_argument("--root-order", choices=["auto", "locality", "random"], default="auto",
                     help="sweep order within a width class: grouped by smallest neighbour "
                          "(multi-source batches share frontiers), the random permutation, or "
-                         "auto = grouped for single-word classes only (measured: grouping "
-                         "wide roots makes their per-pass next-hop planes denser and slower)")
-    ap.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles", "r01"))
+                         "auto = grouped for single-word classes only")
+    ap.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles", "r02"))
     ap.add_argument("--iso-reps", type=int, default=3,
                     help="isolated launches per class for the roofline (after the timed steps)")
+    ap.add_argument("--class-only", type=int, default=0,
+                    help="profiling mode: launch only the class with this neighbour capacity "
+                         "(8, 16, or 32 x next-hop words)")
+    ap.add_argument("--reps", type=int, default=3, help="launches in --class-only mode")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -114,7 +169,7 @@ def main():
         torch.distributed.init_process_group("nccl", device_id=dev)
 
     t0 = time.time()
-    stream, desc = build_topology(args.topology)
+    stream, desc, weighted, default_roots = build_topology(args.topology)
     ls = LinkState(device=local, stream=stream)
     csr = ls.csr()
     names = ls.node_names()
@@ -126,63 +181,89 @@ def main():
         f"{desc}: V={V} E_dir={E} setup {time.time() - t0:.1f}s")
 
     flags = N.OSPF_WANT_DIST | N.OSPF_WANT_DIGEST | (0 if args.no_nh else N.OSPF_WANT_NH)
-    perm = np.random.default_rng(0x5EED).permutation(V).astype(np.uint32)
+    perm = np.random.default_rng(SEED).permutation(V).astype(np.uint32)
+    n_roots = default_roots if args.roots < 0 else args.roots
+    pool = perm if n_roots <= 0 else perm[: min(n_roots, V)]
     nbrs = shard.distinct_neighbors(csr["row_ptr"], csr["col"])
-    words = np.maximum(1, (nbrs + 31) // 32)
     key = shard.first_neighbor(csr["row_ptr"], csr["col"]) if args.root_order != "random" \
         else None
-    classes = shard.make_classes(perm, words, args.batch, key,
+    weak = args.roots_per_gpu > 0
+    caps = shard.neighbor_caps(nbrs)
+    classes = shard.make_classes(pool, caps, args.roots_per_gpu if weak else pool.size, key,
                                  max_grouped_words=1 if args.root_order == "auto" else None)
-    B = sum(c.per_step for c in classes)
+    if args.class_only:
+        classes = [c for c in classes if c.cap == args.class_only]
+        if not classes:
+            raise SystemExit(f"no class with neighbour capacity {args.class_only}")
     for c in classes:
-        n = c.per_step
         x = c.extra
+        if weak:  # ranks' slices of one step must not overlap: <= m / world each
+            x["n"] = min(c.per_step, max(1, c.roots.size // world))
+        else:  # strong: this rank's contiguous slice of the class, every step
+            lo, hi = shard.rank_slice(c.roots.size, world, rank)
+            x["mine"] = c.roots[lo:hi]
+            x["n"] = hi - lo
+            x["slot"] = -(-c.roots.size // world)  # gather slot per rank (padded)
+    classes = [c for c in classes if c.extra["n"] > 0]
+    B = sum(c.extra["n"] for c in classes)
+    for c in classes:
+        n, x = c.extra["n"], c.extra
         x["max_nbrs"] = int(max(1, nbrs[c.roots].max()))  # engine hint: sizes bit-planes
         x["plan"] = eng.plan(c.nh_words, flags, n_roots=n, max_root_neighbors=x["max_nbrs"])
         x["d_all"] = torch.from_numpy(c.roots.astype(np.int32)).to(dev)
-        x["roots"] = torch.empty(n, dtype=torch.int32, device=dev)
+        x["roots"] = torch.from_numpy(x["mine"].astype(np.int32)).to(dev) if not weak else \
+            torch.empty(n, dtype=torch.int32, device=dev)
         x["dist"] = torch.empty((n, V), dtype=torch.int32, device=dev)
         x["nh"] = None if args.no_nh else torch.empty((n, V, c.nh_words), dtype=torch.int32,
                                                       device=dev)
-        x["dig"] = torch.empty((n, 3), dtype=torch.int64, device=dev)
+        x["dig"] = torch.zeros((x.get("slot", n), 3), dtype=torch.int64, device=dev)
         x["stream"] = torch.cuda.current_stream() if args.serial_streams else \
             torch.cuda.Stream(device=dev)
         x["ev"] = []
-    dig_all = torch.empty((B, 3), dtype=torch.int64, device=dev)
     main_s = torch.cuda.current_stream()
-    order = sorted(classes, key=lambda c: -c.nh_words)  # longest runs first
+    order = sorted(classes, key=lambda c: -c.cap)  # longest runs first
+
+    def launch(c, stream_):
+        x = c.extra
+        eng.run_dev(x["roots"].data_ptr(), x["n"], c.nh_words, flags=flags,
+                    d_dist=x["dist"].data_ptr(),
+                    d_nh=x["nh"].data_ptr() if x["nh"] is not None else 0,
+                    d_digest=x["dig"].data_ptr(), stream=stream_.cuda_stream,
+                    max_root_neighbors=x["max_nbrs"])
+
+    if args.class_only:  # profiling mode: the class alone, back to back
+        for _ in range(args.reps):
+            launch(classes[0], main_s)
+        eng.sync(main_s.cuda_stream)
+        log(f"class-only W={args.class_only}: {args.reps} launches of "
+            f"{classes[0].extra['n']} roots")
+        return
 
     def step(i: int, timed: bool):
         ready = torch.cuda.Event()
-        ready.record(main_s)  # the previous step's digest copies are queued on main_s
+        ready.record(main_s)  # the previous step's gathers are queued on main_s
         done = []
         for c in order:
-            x, n, m = c.extra, c.per_step, c.roots.size
+            x, n = c.extra, c.extra["n"]
             cs = x["stream"]
             with torch.cuda.stream(cs):
                 cs.wait_event(ready)
-                start = ((i * world + rank) * n) % m  # == shard.step_roots on the device
-                idx = (torch.arange(n, device=dev) + start) % m
-                torch.index_select(x["d_all"], 0, idx, out=x["roots"])
+                if weak:  # cyclic sweep of the class, disjoint slices per rank
+                    start = ((i * world + rank) * n) % c.roots.size
+                    idx = (torch.arange(n, device=dev) + start) % c.roots.size
+                    torch.index_select(x["d_all"], 0, idx, out=x["roots"])
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record(cs)
-                eng.run_dev(x["roots"].data_ptr(), n, c.nh_words, flags=flags,
-                            d_dist=x["dist"].data_ptr(),
-                            d_nh=x["nh"].data_ptr() if x["nh"] is not None else 0,
-                            d_digest=x["dig"].data_ptr(), stream=cs.cuda_stream,
-                            max_root_neighbors=x["max_nbrs"])
+                launch(c, cs)
                 ev[1].record(cs)
             done.append(ev[1])
             if timed:
                 x["ev"].append(ev)
         for e in done:
             main_s.wait_event(e)
-        off = 0
-        for c in classes:
-            dig_all[off:off + c.per_step].copy_(c.extra["dig"])
-            off += c.per_step
         if dist_on:
-            shard.gather_digests(dig_all)
+            for c in classes:
+                c.extra["gathered"] = shard.gather_digests(c.extra["dig"])
 
     for i in range(args.warmup):
         step(i, False)
@@ -204,17 +285,31 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
 
-    roots_total = world * B * args.steps
+    # digests of the LAST timed step, by root id (rank 0 sees every rank's)
+    step_digest = {}
+    if not weak:
+        for c in classes:
+            x = c.extra
+            if dist_on:
+                g = x["gathered"].cpu().numpy().view(np.uint64).reshape(world, x["slot"], 3)
+                for r in range(world):
+                    lo, hi = shard.rank_slice(c.roots.size, world, r)
+                    for j, root in enumerate(c.roots[lo:hi]):
+                        step_digest[int(root)] = g[r, j]
+            else:
+                d = x["dig"].cpu().numpy().view(np.uint64)
+                for j, root in enumerate(x["mine"]):
+                    step_digest[int(root)] = d[j]
+
+    roots_total = world * B * args.steps if weak else pool.size * args.steps
     spf_s = roots_total / dt
     gteps = roots_total * E / dt / 1e9
 
     # roofline. The classes overlap on their streams inside the timed steps,
     # so each class is then timed ALONE (not part of `value`): R launches on
-    # one stream bracketed by HIP events on that stream. The dominant class is
-    # the one with the largest share of a step's device time. A multi-source
-    # class launch is a sequence of kernels (init, level/settle pairs, rows);
-    # its events bracket the whole sequence, and profiles/<round>/ holds the
-    # rocprofv3 per-kernel summary whose per-class sums it matches.
+    # one stream bracketed by HIP events on that stream. A class launch is a
+    # sequence of kernels; profiles/<round>/ holds the single-stream rocprofv3
+    # per-kernel summary of each class alone, whose per-class sums match.
     iso_s = torch.cuda.Stream(device=dev)
     for c in classes:
         x = c.extra
@@ -223,84 +318,121 @@ def main():
             for _ in range(args.iso_reps + 1):
                 a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a_.record(iso_s)
-                eng.run_dev(x["roots"].data_ptr(), c.per_step, c.nh_words, flags=flags,
-                            d_dist=x["dist"].data_ptr(),
-                            d_nh=x["nh"].data_ptr() if x["nh"] is not None else 0,
-                            d_digest=x["dig"].data_ptr(), stream=iso_s.cuda_stream,
-                            max_root_neighbors=x["max_nbrs"])
+                launch(c, iso_s)
                 b_.record(iso_s)
                 b_.synchronize()
                 ms.append(a_.elapsed_time(b_))
-        x["iso_ms"] = float(np.median(ms[1:]))
+        x["iso_ms"] = float(np.median(ms[1:])) if len(ms) > 1 else float(ms[0])
         x["ms"] = [a_.elapsed_time(b_) for a_, b_ in x["ev"]]
     eng.sync(iso_s.cuda_stream)
 
     def class_roofline(c):
         x, p = c.extra, c.extra["plan"]
-        alg = c.per_step * bytes_per_root(V, E, c.nh_words)
-        ach = alg / (x["iso_ms"] / 1e3) / 1e9
-        tr = pmc_traffic(args.profile_dir, f"variant{p['variant']}_W{c.nh_words}", c.per_step)
-        return {"nh_words": c.nh_words, "roots_per_launch": c.per_step,
+        n = x["n"]
+        comp = compulsory_bytes(V, E, c.nh_words, n, p["variant"], p["slices"], weighted)
+        alg = n * bytes_per_root(V, E, c.nh_words)
+        sec = x["iso_ms"] / 1e3
+        tr = pmc_traffic(args.profile_dir, f"variant{p['variant']}_cap{c.cap}", n)
+        return {"cap": c.cap, "nh_words": c.nh_words, "variant": p["variant"],
+                "roots_per_launch": n,
                 "isolated_launch_ms": round(x["iso_ms"], 3),
-                "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
-                "traffic": tr,
-                "traffic_GBs": round(tr / (x["iso_ms"] / 1e3) / 1e9, 1) if tr else None}
+                "compulsory_bytes": comp, "achieved": round(comp / sec / 1e9, 1),
+                "frac": round(comp / sec / 1e9 / HBM_PEAK_GBS, 4),
+                "alg_equiv_GBs": round(alg / sec / 1e9, 1),
+                "traffic": tr, "traffic_GBs": round(tr / sec / 1e9, 1) if tr else None,
+                "traffic_over_compulsory": round(tr / comp, 2) if tr else None}
 
-    dom = max(classes, key=lambda c: c.extra["iso_ms"])
-    dr = class_roofline(dom)
-    p = dom.extra["plan"]
+    rl = [class_roofline(c) for c in classes]
+    dom = max(rl, key=lambda r: r["isolated_launch_ms"])
+    kname = {5: "multi-source BFS class launch (variant 5: msbfs init + level/settle pairs "
+                "+ rows kernels)",
+             7: "wave-per-root Dial class launch (variant 7: wdial_kernel + row digest)"}
     roofline = {
-        "bound": "hbm", "achieved": dr["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": dr["frac"], "traffic": dr["traffic"],
-        "kernel": (f"multi-source BFS class launch (variant 5, nh_words {dom.nh_words}: "
-                   f"msbfs init + level/settle pairs + rows kernels)")
-        if p["variant"] == 5 else
-        f"spf_bfs_kernel (variant {p['variant']}, nh_words {dom.nh_words})"
-        if p["variant"] >= 3 else f"spf_run_kernel (variant {p['variant']})",
-        "block": p["block"], "roots_per_launch": dom.per_step,
-        "bytes_per_root": bytes_per_root(V, E, dom.nh_words),
-        "avg_launch_ms": dr["isolated_launch_ms"],
-        "traffic_GBs": dr["traffic_GBs"],
-        "edges_per_s_per_launch": round(dom.per_step * E / (dom.extra["iso_ms"] / 1e3), 1),
-        "classes": [class_roofline(c) for c in classes],
-        "note": "achieved = roots x SURVEY 8(d) bytes_root (8E + 8V + 4VW: every root scanning "
-                "the CSR) / isolated launch time; 64 roots share each CSR scan, so achieved "
-                "can exceed the HBM peak; traffic = measured HBM bytes per launch (rocprofv3 "
-                "FETCH_SIZE x2 + WRITE_SIZE, profiles/<round>/pmc_traffic.json)",
+        "bound": "hbm", "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": dom["frac"], "traffic": dom["traffic"],
+        "kernel": kname.get(dom["variant"], f"variant {dom['variant']} class launch") +
+        f", neighbour capacity {dom['cap']} ({dom['nh_words']} next-hop words)",
+        "roots_per_launch": dom["roots_per_launch"], "avg_launch_ms": dom["isolated_launch_ms"],
+        "compulsory_bytes": dom["compulsory_bytes"], "alg_equiv_GBs": dom["alg_equiv_GBs"],
+        "traffic_GBs": dom["traffic_GBs"],
+        "traffic_over_compulsory": dom["traffic_over_compulsory"],
+        "classes": rl,
+        "note": "achieved = compulsory bytes of the dominant class launch (dist + next-hop rows "
+                "written, 4V(1+W) per run, plus the CSR reads its traversals need at least once: "
+                "variant 5 one neighbour-id + offset scan per 64-root pass; per-root kernels one "
+                "scan per run) / its isolated launch time (HIP events on its stream, alone); "
+                "alg_equiv_GBs = the SURVEY 8(d) per-root-scan model, which batched traversals "
+                "beat (not a roofline fraction); traffic = measured HBM bytes per launch "
+                "(rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/<round>/pmc_traffic.json)",
     }
 
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        from oracle import Oracle  # CPU baseline leg only (reference-shaped restatement)
-        sample_ids = perm[: args.cpu_sample]
+        from oracle import Oracle  # CPU baseline leg only (the restatements under oracle/)
+        threads = args.cpu_threads or host_threads()
+        k = args.cpu_sample if args.cpu_sample >= 0 else (16 if args.topology == "mesh1m" else 256)
+        sample_ids = [int(r) for r in pool[:k]]
         sample = [names[i] for i in sample_ids]
         o = Oracle(stream)
+        # reference-shaped restatement (string keys, hash sets, heap + make_heap
+        # per strict improvement): quadratic on weighted fabrics (~10 min per
+        # F100k root), so there the CSR-Dijkstra restatement is the baseline
+        ref_ok = args.topology != "fabric100k-w"
+        csr_k = max(k, 256)
+        csr_ids = [int(r) for r in pool[:csr_k]]
         t1 = time.perf_counter()
-        cd = o.digests(sample, threads=args.cpu_threads)
-        ct = time.perf_counter() - t1
-        cpu = {"value": round(len(sample) / ct, 4), "unit": "SPF/s", "cores": args.cpu_threads,
-               "kind": "port",
-               "sample": f"{len(sample)} roots (permutation seed 0x5eed) of the same topology, "
-                         f"reference-shaped runSpf restatement (oracle/), {args.cpu_threads} "
-                         f"threads, {ct:.2f}s"}
-        gd = eng.run(sample_ids, int(words[sample_ids].max()), want_dist=False, want_nh=False,
-                     want_digest=True)["digest"]
-        parity = bool(np.array_equal(gd, cd))
+        fd = o.fast_digests([names[i] for i in csr_ids], threads=threads)
+        ct_fast = time.perf_counter() - t1
+        csr_line = {"value": round(len(csr_ids) / ct_fast, 3), "unit": "SPF/s",
+                    "cores": threads, "kind": "port",
+                    "sample": f"{len(csr_ids)} roots (permutation seed 0x5eed), CSR-Dijkstra "
+                              f"restatement (oracle/, integer ids, binary heap), {threads} "
+                              f"threads, {ct_fast:.2f}s"}
+        checks = dict(zip(csr_ids, fd))
+        if ref_ok:
+            t1 = time.perf_counter()
+            one = o.digests(sample[:2], threads=1)
+            st_s = (time.perf_counter() - t1) / 2
+            t1 = time.perf_counter()
+            cd = o.digests(sample, threads=threads)
+            ct = time.perf_counter() - t1
+            assert np.array_equal(one, cd[:2])
+            cpu = {"value": round(len(sample) / ct, 4), "unit": "SPF/s", "cores": threads,
+                   "kind": "port",
+                   "sample": f"{len(sample)} roots (permutation seed 0x5eed) of the same "
+                             f"topology, reference-shaped runSpf restatement (oracle/: string "
+                             f"keys, hash sets, heap + make_heap), {threads} threads, {ct:.2f}s",
+                   "cpu_model": cpu_model(), "single_thread_s_per_root": round(st_s, 4),
+                   "csr_dijkstra": csr_line}
+            checks.update(zip(sample_ids, cd))
+        else:
+            cpu = dict(csr_line, cpu_model=cpu_model(),
+                       reference_shaped="not run: its make_heap per strict improvement "
+                                        "(LinkState.cpp:893) takes ~10 min per root here")
+        if step_digest:
+            parity = {"roots": len(checks),
+                      "equal": bool(all(np.array_equal(step_digest[r], d)
+                                        for r, d in checks.items())),
+                      "source": "digests of the last timed step vs the CPU restatement(s)"}
 
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(spf_s, 2), "unit": "SPF/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
-            "gteps": round(gteps, 3),
+            "scaling": "weak" if weak else "strong", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic", "gteps": round(gteps, 3),
             "config": {
-                "workload": desc + " all-sources SPF + ECMP next-hop bitsets (dist + next-hop "
-                                   "rows written to HBM, per-root digests)",
-                "n_nodes": V, "n_directed_edges": E, "roots_per_step_per_gpu": B,
-                "root_classes": [{"nh_words": c.nh_words, "roots_per_step": c.per_step,
-                                  **{k: c.extra["plan"][k] for k in ("variant", "slices",
-                                                                     "block")},
+                "workload": desc + (" all-sources" if n_roots <= 0 else
+                                    f" {pool.size} sampled roots") +
+                " SPF + ECMP next-hop bitsets (dist + next-hop rows written to HBM, per-root "
+                "digests)",
+                "n_nodes": V, "n_directed_edges": E,
+                "roots_per_step": int(world * B if weak else pool.size),
+                "root_classes": [{"cap": c.cap, "nh_words": c.nh_words,
+                                  "roots_this_rank": c.extra["n"],
+                                  **{kk: c.extra["plan"][kk] for kk in ("variant", "slices",
+                                                                        "block")},
                                   "avg_launch_ms": round(float(np.mean(c.extra["ms"])), 3),
                                   "isolated_launch_ms": round(c.extra["iso_ms"], 3)}
                                  for c in classes],

@@ -130,6 +130,7 @@ Plan make_plan(const ospf_ctx* c, uint32_t W, uint32_t ign_cap, bool unit, uint3
       case 4: return unit && bfs <= lim;
       case 5: return unit && ign_cap == 0;
       case 6: return !unit && c->info.max_metric + 1 <= ospf::kMaxDialRing;
+      case 7: return true;
     }
     return false;
   };
@@ -138,21 +139,20 @@ Plan make_plan(const ospf_ctx* c, uint32_t W, uint32_t ign_cap, bool unit, uint3
   if (unit && fits(5) && (n_roots >= kMsMinRoots || (W >= 8 && n_roots >= 4))) {
     p.variant = 5;
   } else if (unit) {
-    p.variant = (W == 1 && fits(3)) ? 3 : fits(4) ? 4 : 2;
+    p.variant = (W == 1 && fits(3)) ? 3 : fits(4) ? 4 : 7;
   } else {
-    // beyond LDS: frontier lists (variant 6) instead of a scan of every node
-    // per distance value (variant 2)
-    p.variant = fits(0) ? 0 : fits(1) ? 1 : fits(6) ? 6 : 2;
+    // beyond LDS: a wave per root over frontier lists (variant 7), any metric
+    p.variant = fits(0) ? 0 : fits(1) ? 1 : 7;
   }
   // test/benchmark knob: OSPF_FORCE_VARIANT=0..4 forces a kernel variant when
   // its state fits (e.g. the HBM-state Dial kernel on a small graph).
   if (const char* f = getenv("OSPF_FORCE_VARIANT")) {
     const int want = atoi(f);
-    if (want >= 0 && want <= 6 && fits(want)) p.variant = want;
+    if (want >= 0 && want <= 7 && fits(want)) p.variant = want;
   }
-  const size_t ldsz[7] = {full, half, head, bfs_nh, bfs, 0, head};
+  const size_t ldsz[8] = {full, half, head, bfs_nh, bfs, 0, head, 0};
   p.lds = ldsz[p.variant];
-  if (p.variant == 5 || p.variant == 6)
+  if (p.variant >= 5)
     p.block = 256;
   else if (p.variant >= 3)
     p.block = p.lds > 80 * 1024 ? 1024 : (V >= 4096 ? 512 : 256);
@@ -252,9 +252,10 @@ int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
   const bool dig = flags & OSPF_WANT_DIGEST;
   const uint32_t lmax = c->depth_bound + 2;
   // levels are recorded as dist + 1 in a byte per (node, root): rows are then
-  // written once, whole, by msbfs_rows (needs depth <= 254), which also folds
+  // written once, whole, by msbfs_rows (needs depth + 2 <= 255: the check
+  // level past the bound is recorded too), which also folds
   // the digest in (no row re-read, no row scratch); packed planes need it
-  const bool defer = c->depth_bound <= 254 && !getenv("OSPF_MS_NODEFER");
+  const bool defer = c->depth_bound <= 253 && !getenv("OSPF_MS_NODEFER");
   MsShape sh = ms_shape(b->n_roots, kcap, defer && getenv("OSPF_MS_PACK"));
   if (const char* e = getenv("OSPF_MS_R")) {  // test knob: force R (packs when defer)
     const uint32_t R = std::min(64, std::max(1, atoi(e)));
@@ -323,6 +324,7 @@ int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
     a.OW = sh.OW;
     a.rep = rep;
     a.lmax = lmax;
+    a.dbound = c->depth_bound;
     a.kcap = kcap;
     a.push_div = push_div;
     a.defer = defer ? 1u : 0u;
@@ -366,6 +368,94 @@ int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
   return OSPF_OK;
 }
 
+
+// Variant 7: group-per-root bucketed Dial (spf_wdial.hip). Persistent
+// workgroups of G waves (OSPF_WD_GROUP, default from the graph: see below),
+// 16 / G of them per CU, each own a ring of frontier lists; the ring covers
+// every tentative distance ahead of the current one: NB = max metric + 1
+// lists of one distance each, or, past kWDialMaxNB, buckets of delta
+// distances with tagged entries. List capacity comes from a memory budget
+// (OSPF_WD_LIST_MB, default 4096); an overflowing list falls back to node
+// scans for its rounds (correct, slower).
+int run_wdial(ospf_ctx* c, const ospf_batch* b, bool hop, hipStream_t s) {
+  const uint32_t V = c->info.n_nodes, W = b->nh_words, n = b->n_roots;
+  const uint32_t maxw = hop ? 1u : std::max<uint32_t>(c->info.max_metric, 1);
+  uint32_t NB, delta;
+  if (maxw + 1 <= ospf::kWDialMaxNB) {
+    NB = maxw + 1;
+    delta = 1;
+  } else {
+    NB = ospf::kWDialMaxNB;
+    delta = (maxw + NB - 2) / (NB - 1);
+  }
+  if (const char* e = getenv("OSPF_WD_DELTA")) {  // test knob: force tagged buckets
+    const uint32_t dl = (uint32_t)std::max(1, atoi(e));
+    if (dl > 1) {
+      delta = std::max(delta, dl);
+      NB = std::min<uint32_t>(ospf::kWDialMaxNB, (maxw + delta - 1) / delta + 1);
+      NB = std::max<uint32_t>(NB, 2);
+    }
+  }
+  // Waves per root: a round's work is about E / (distinct distances); graphs
+  // with many edges per distance value (low hop diameter, e.g. fabrics) get a
+  // whole CU per root, thin-frontier graphs (meshes) a wave per root.
+  const double rounds = (double)maxw * std::max<uint32_t>(2, c->depth_bound);
+  const double per_round = (double)c->info.n_edges / std::max(1.0, rounds);
+  uint32_t G = per_round > 2048 ? 4 : per_round > 128 ? 2 : 1;
+  // few roots: wider groups, so the groups that do run have several roots
+  // each (no one-root tail) and more lanes per round
+  while (G < 16 && n < 4ull * c->n_cu * (16 / G)) G *= 2;
+  if (const char* e = getenv("OSPF_WD_GROUP")) G = (uint32_t)std::max(1, std::min(16, atoi(e)));
+  while (16 % G) --G;
+  const uint32_t ngroups =
+      std::max<uint32_t>(1, std::min<uint32_t>(n, (uint32_t)c->n_cu * (16 / G)));
+  size_t budget = 4096ull << 20;
+  if (const char* e = getenv("OSPF_WD_LIST_MB")) budget = (size_t)std::max(1, atoi(e)) << 20;
+  const size_t eb = delta > 1 ? 8 : 4;
+  uint64_t bcap = budget / ((uint64_t)ngroups * NB * eb);
+  bcap = std::max<uint64_t>(64, std::min<uint64_t>(bcap, V));
+  if (const char* e = getenv("OSPF_WD_BCAP")) bcap = (uint64_t)std::max(1, atoi(e));  // test knob
+  // packed state (spf_wdial.hip PACK): one word per node for roots with at
+  // most 16 distinct neighbours (the caller's max_root_neighbors hint)
+  const uint32_t kcap = b->max_root_neighbors ? b->max_root_neighbors : 32u * W;
+  uint32_t pk_bits = (W == 1 && kcap <= 16) ? (kcap <= 8 ? 8u : 16u) : 0u;
+  if (const char* e = getenv("OSPF_WD_PACK")) {  // knob: 0 = off, 8 / 16 = field width
+    const int v = atoi(e);
+    pk_bits = (v == 0 || W != 1 || kcap > (uint32_t)v || (v != 8 && v != 16)) ? 0u : (uint32_t)v;
+  }
+  const bool want_dist = b->flags & OSPF_WANT_DIST, want_nh = b->flags & OSPF_WANT_NH;
+  const size_t sz_lists = align_up((size_t)ngroups * NB * bcap * eb, 256);
+  const size_t sz_dist = want_dist ? 0 : align_up((size_t)n * V * 4ull, 256);
+  const size_t sz_nh = want_nh ? 0 : align_up((size_t)n * V * W * 4ull, 256);
+  const size_t sz_pk = pk_bits ? align_up((size_t)ngroups * V * 4ull, 256) : 0;
+  int rc = OSPF_OK;
+  char* sp = stream_scratch(c, s, sz_lists + sz_dist + sz_nh + sz_pk, &rc);
+  if (rc) return rc;
+  ospf::WDialArgs a{};
+  a.roots = b->d_roots;
+  a.n = n;
+  a.ign_off = b->d_ign_offsets;
+  a.ign_ids = b->d_ign_ids;
+  a.hop = hop ? 1u : 0u;
+  a.W = W;
+  a.lists = (uint32_t*)sp;
+  a.dist = want_dist ? b->d_dist : (uint32_t*)(sp + sz_lists);
+  a.nh = want_nh ? b->d_nh : (uint32_t*)(sp + sz_lists + sz_dist);
+  a.digest = (b->flags & OSPF_WANT_DIGEST) ? b->d_digest : nullptr;
+  a.err = c->d_err;
+  a.NB = NB;
+  a.bcap = (uint32_t)bcap;
+  a.delta = delta;
+  a.group_waves = G;
+  a.ngroups = ngroups;
+  a.pk_bits = pk_bits;
+  a.pk = pk_bits ? (uint32_t*)(sp + sz_lists + sz_dist + sz_nh) : nullptr;
+  HIPCHK(c, hipSetDevice(c->device));
+  hipError_t e = ospf::launch_wdial(c->g, a, s);
+  if (e != hipSuccess) return hip_fail(c, e, "launch_wdial");
+  c->spf_runs += n;
+  return OSPF_OK;
+}
 
 // ---------------------------------------------------------------- KSP2
 // getKthPaths(src, dst, 1 and 2) for many destinations (LinkState.cpp:790-819):
@@ -435,7 +525,7 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
   b1.nh_words = W;
   b1.max_root_neighbors = nn;
   b1.d_dist = d_dist1;
-  rc = (unit && c->depth_bound <= 254 && V >= 4096) ? run_msbfs(c, &b1, s)
+  rc = (unit && c->depth_bound <= 253 && V >= 4096) ? run_msbfs(c, &b1, s)
                                                      : ospf_run_batch_dev(c, &b1, s);
   if (rc) return rc;
   ospf::TraceArgs t{};
@@ -879,7 +969,7 @@ int ospf_plan_n(const ospf_ctx* c, uint32_t flags, uint32_t nh_words, uint32_t m
   out->lds_bytes = (uint32_t)p.lds;
   if (p.variant == 5) {
     const uint32_t kcap = max_root_neighbors ? std::min(max_root_neighbors, 32u * W) : 32u * W;
-    out->slices = ms_shape(n_roots, kcap, c->depth_bound <= 254 && getenv("OSPF_MS_PACK")).npass;
+    out->slices = ms_shape(n_roots, kcap, c->depth_bound <= 253 && getenv("OSPF_MS_PACK")).npass;
   } else {
     out->slices = (p.variant == 3 || p.variant == 4) ? ospf::bfs_slices(W) : 1u;
   }
@@ -921,6 +1011,7 @@ int ospf_run_batch_dev(ospf_ctx* c, const ospf_batch* b, void* stream) {
 
   const Plan p = make_plan(c, nh_words, ign ? std::max<uint32_t>(max_ignored, 1) : 0, unit, n_roots);
   if (p.variant == 5) return run_msbfs(c, b, (hipStream_t)stream);
+  if (p.variant == 7) return run_wdial(c, b, hop, (hipStream_t)stream);
   // scratch for state the caller does not want back (HBM-state variants
   // keep dist / next-hops in the output rows while they run)
   size_t need = 0;
@@ -1015,7 +1106,9 @@ int ospf_sync(ospf_ctx* c, void* stream) {
     HIPCHK(c, hipMemset(c->d_err, 0, 4));
     return fail(c, OSPF_E_RANGE,
                 (err & 1u) ? "a root has more distinct neighbours than 32*nh_words"
-                           : "a run's ignore list exceeds max_ignored");
+                : (err & 2u) ? "a run's ignore list exceeds max_ignored"
+                : (err & 8u) ? "a BFS level past the graph's depth bound was reached"
+                             : "internal: a frontier entry out of range");
   }
   return OSPF_OK;
 }
@@ -1202,19 +1295,27 @@ int ospf_update_links(ospf_ctx* c, const ospf_link_update* u, uint32_t n, uint64
     idx.push_back((uint32_t)(off + e));
     val.push_back(v);
   };
-  uint32_t new_max = 0;
-  std::vector<std::pair<uint32_t, uint32_t>> downs;  // links that went down (ends)
+  // validate every update before touching any state: a rejected batch leaves
+  // the host shadows, the planner counters and the device graph as they were
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t lid = u[i].link_id;
     if (lid >= c->g.n_lid) return fail(c, OSPF_E_INVAL, "unknown link id");
-    const uint32_t e0 = c->h_link_e[2ull * lid], e1 = c->h_link_e[2ull * lid + 1];
-    if (e0 == 0xFFFFFFFFu || e1 == 0xFFFFFFFFu) return fail(c, OSPF_E_INVAL, "unknown link id");
+    if (c->h_link_e[2ull * lid] == 0xFFFFFFFFu || c->h_link_e[2ull * lid + 1] == 0xFFFFFFFFu)
+      return fail(c, OSPF_E_INVAL, "unknown link id");
     if (u[i].up && (u[i].metric_lo == 0 || u[i].metric_hi == 0))
       return fail(c, OSPF_E_RANGE, "metric 0 on a usable link is outside the engine contract");
+  }
+  uint32_t new_max = 0;
+  bool ups = false;  // a link came up: components may join, the level bound may grow
+  std::vector<std::pair<uint32_t, uint32_t>> downs;  // links that went down (ends)
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t lid = u[i].link_id;
+    const uint32_t e0 = c->h_link_e[2ull * lid], e1 = c->h_link_e[2ull * lid + 1];
     const bool lo0 = owner(e0) <= owner(e1);
     const uint32_t elo = lo0 ? e0 : e1, ehi = lo0 ? e1 : e0;
     const uint32_t down = u[i].up ? 0u : 0x80000000u;
     if (!u[i].up && !(c->h_pcolx[elo] & 0x80000000u)) downs.push_back({owner(elo), owner(ehi)});
+    if (u[i].up && (c->h_pcolx[elo] & 0x80000000u)) ups = true;
     if (u[i].up) new_max = std::max({new_max, u[i].metric_lo, u[i].metric_hi});
     for (uint32_t e : {elo, ehi}) {  // usable non-unit entries, before -> after
       if (!(c->h_pcolx[e] & 0x80000000u) && c->h_pw[e] != 1) --c->non_unit;
@@ -1249,8 +1350,9 @@ int ospf_update_links(ospf_ctx* c, const ospf_link_update* u, uint32_t n, uint64
   // overloaded end is not in the transit subgraph (only the first / last hop
   // of a path, covered by the + 2 of the bound). No detour within the budget
   // (a split component), or drift of more than 8 levels over the last exact
-  // bound, recomputes it.
-  bool deeper = false;
+  // bound, recomputes it. A link coming up can join two components of the
+  // transit subgraph (an eccentricity the old bound never saw): recompute.
+  bool deeper = ups;
   uint32_t grow = 0;
   auto transit = [&](uint32_t x) { return !((c->h_nt[x >> 5] >> (x & 31)) & 1u); };
   for (const auto& ab : downs) {
@@ -1273,11 +1375,14 @@ int ospf_update_nodes(ospf_ctx* c, const uint32_t* nodes, const uint8_t* no_tran
                       uint64_t version) {
   if (!c || (n && (!nodes || !no_transit))) return OSPF_E_INVAL;
   if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  for (uint32_t i = 0; i < n; ++i)
+    if (nodes[i] >= c->info.n_nodes) return fail(c, OSPF_E_INVAL, "node out of range");
   bool deeper = false;
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t v = nodes[i];
-    if (v >= c->info.n_nodes) return fail(c, OSPF_E_INVAL, "node out of range");
-    if (no_transit[i] && !((c->h_nt[v >> 5] >> (v & 31u)) & 1u)) deeper = true;
+    // either direction can deepen the level bound: an overloaded node splits
+    // transit paths, a node that becomes transit can join two components
+    if ((no_transit[i] != 0) != (((c->h_nt[v >> 5] >> (v & 31u)) & 1u) != 0)) deeper = true;
     if (no_transit[i]) c->h_nt[v >> 5] |= 1u << (v & 31u);
     else c->h_nt[v >> 5] &= ~(1u << (v & 31u));
   }

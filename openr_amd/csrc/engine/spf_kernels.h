@@ -102,6 +102,32 @@ hipError_t launch_spf(int variant, bool unit, bool ign, const DevGraph& g, const
 hipError_t launch_dial(bool ign, const DevGraph& g, const RunArgs& a, uint32_t n_roots,
                        size_t lds, hipStream_t s);
 
+// Group-per-root bucketed Dial (spf_wdial.hip), variant 7: any metric >= 1,
+// optional per-run ignored links; ngroups persistent workgroups of
+// group_waves waves, group i runs roots i, i + ngroups, ... with its own ring
+// of NB frontier lists of bcap entries (delta > 1: {node, dist} pairs).
+// dist / nh are the output rows (required).
+constexpr uint32_t kWDialMaxNB = 128;
+struct WDialArgs {
+  const uint32_t* roots;
+  uint32_t n;
+  const uint32_t* ign_off;  // [n + 1] or null
+  const uint32_t* ign_ids;
+  uint32_t hop;             // hop-count mode: every usable weight is 1
+  uint32_t W;               // next-hop words per node
+  uint32_t* dist;           // [n][V]
+  uint32_t* nh;             // [n][V][W]
+  ospf_digest* digest;      // [n] or null
+  uint32_t* err;
+  uint32_t* lists;          // [ngroups][NB][bcap][delta > 1 ? 2 : 1]
+  uint32_t NB, bcap, delta;
+  uint32_t group_waves;     // 1 .. 16 waves per root
+  uint32_t ngroups;
+  uint32_t pk_bits;         // 0, or 8 / 16: packed (dist << K | next hops) state
+  uint32_t* pk;             // [ngroups][V] packed words (pk_bits != 0)
+};
+hipError_t launch_wdial(const DevGraph& g, const WDialArgs& a, hipStream_t s);
+
 // BFS kernel (spf_bfs.hip), unit metric / hop count, LDS bitmaps:
 //   nh_lds = variant 3 (byte next-hops in LDS for roots with <= 8 neighbours),
 //   otherwise variant 4 (next-hops in HBM).
@@ -124,6 +150,8 @@ struct MsArgs {
   uint32_t vb0;           // first virtual batch of this round (vb = batch*npass + g)
   uint32_t nb;            // virtual batches in this round
   uint32_t lmax;          // stride of found[]
+  uint32_t dbound;        // levels launched: 1 .. dbound + 1 (found[dbound + 1] set =
+                          //   the host's depth bound was too small: error bit 8)
   uint32_t kcap;          // max distinct neighbours of a root (caller's bound)
   uint32_t push_div;      // level d pushes when frontier edge mass * push_div < E
   uint32_t* dist;         // [n][V] or null

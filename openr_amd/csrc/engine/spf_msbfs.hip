@@ -514,6 +514,7 @@ __global__ void __launch_bounds__(256) msbfs_final_kernel(DevGraph g, MsArgs a) 
   const VB b(a, vbl, g.V, 0);
   const uint32_t V = g.V;
   const uint32_t v = (blockIdx.x / a.nb) * kBlock + threadIdx.x;
+  if (v == 0 && a.found[vbl * a.lmax + a.dbound + 1]) atomicOr(a.err, 8u);
   const uint64_t un = v < V ? (~b.seen[v] & b.valid) : 0ull;
   uint64_t w = wave_or64(un);
   while (w) {
@@ -551,6 +552,7 @@ __global__ void __launch_bounds__(256) msbfs_rows_kernel(DevGraph g, MsArgs a) {
   const VB b(a, vbl, g.V, KP);
   const uint32_t V = g.V, tid = threadIdx.x;
   const uint32_t v0 = (blockIdx.x / a.nb) * 64u, nv = min(64u, V - v0);
+  if (v0 == 0 && tid == 0 && a.found[vbl * a.lmax + a.dbound + 1]) atomicOr(a.err, 8u);
   const uint32_t nr = min(a.R, a.n - b.rix0);
   {
     const uint4* src = reinterpret_cast<const uint4*>(a.lev + ((size_t)vbl * V + v0) * 64u);
@@ -751,7 +753,9 @@ hipError_t launch_round_kp(const DevGraph& g, const MsArgs& a, uint32_t depth_bo
   hipLaunchKernelGGL(msbfs_init_kernel<KP>, dim3(init_blocks), dim3(kBlock), 0, s, g, a);
   const uint32_t chunks = (g.V + kBlock - 1) / kBlock;
   const uint32_t bigblocks = (g.nbig + kWavesPerBlock - 1) / kWavesPerBlock;
-  for (uint32_t d = 1; d < depth_bound; ++d) {
+  // levels 2 .. depth_bound + 1: the last one must come out empty (a node
+  // there means the host's bound was stale; the rows kernel raises bit 8)
+  for (uint32_t d = 1; d <= depth_bound; ++d) {
     hipLaunchKernelGGL(msbfs_level_kernel<KP>, dim3(a.nb * (chunks + bigblocks)), dim3(kBlock), 0,
                        s, g, a, d);
     hipLaunchKernelGGL(msbfs_settle_kernel<KP>, dim3(a.nb * chunks), dim3(kBlock), 0, s, g, a, d);

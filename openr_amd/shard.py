@@ -20,6 +20,16 @@ class RootClass:
     roots: np.ndarray          # this class's roots in sweep order (u32 node ids)
     per_step: int              # roots of this class each rank runs per step
     extra: dict = field(default_factory=dict)
+    cap: int = 0               # distinct-neighbour capacity of the class (8, 16, 32 W)
+
+
+def neighbor_caps(nbrs: np.ndarray) -> np.ndarray:
+    """Launch class of each root by its distinct-neighbour count: 8, 16, or
+    32 x next-hop words. Classes of at most 8 / 16 neighbours let the engine
+    use 8 / 16 bit-planes (multi-source BFS) or packed 32-bit state
+    (weighted path) for the whole launch."""
+    words = np.maximum(1, (nbrs + 31) // 32)
+    return np.where(nbrs <= 8, 8, np.where(nbrs <= 16, 16, 32 * words)).astype(np.int64)
 
 
 def nh_words_of(row_ptr: np.ndarray, col: np.ndarray) -> np.ndarray:
@@ -60,27 +70,40 @@ def locality_order(roots: np.ndarray, key: np.ndarray) -> np.ndarray:
     return roots[np.argsort(key[roots], kind="stable")]
 
 
-def make_classes(perm: np.ndarray, words: np.ndarray, batch: int,
+def make_classes(perm: np.ndarray, caps: np.ndarray, batch: int,
                  key: np.ndarray = None, max_grouped_words: int = None) -> List[RootClass]:
-    """Split a root permutation into width classes; each class's share of a
-    `batch`-root step is proportional to its size (at least 1). With `key`
-    (first_neighbor) the sweep of each class with at most `max_grouped_words`
-    next-hop words (all classes when None) is locality-ordered."""
+    """Split a root permutation into launch classes by `caps` (per node: the
+    class's neighbour capacity, neighbor_caps, or 32 x next-hop words); each
+    class's share of a `batch`-root step is
+    proportional to its size (at least 1). With `key` (first_neighbor) the
+    sweep of each class with at most `max_grouped_words` next-hop words (all
+    classes when None) is locality-ordered."""
     V = perm.size
     out = []
-    for W in sorted(set(words[perm].tolist())):
-        members = perm[words[perm] == W]
+    for cap in sorted(set(caps[perm].tolist())):
+        members = perm[caps[perm] == cap]
+        W = max(1, (int(cap) + 31) // 32)
         if key is not None and (max_grouped_words is None or W <= max_grouped_words):
             members = locality_order(members, key)
         share = max(1, int(round(batch * members.size / V)))
-        out.append(RootClass(int(W), members.astype(np.uint32), share))
+        out.append(RootClass(W, members.astype(np.uint32), share, cap=int(cap)))
     return out
 
 
+def rank_slice(m: int, world: int, rank: int):
+    """[lo, hi) of rank's contiguous share of m items (sizes differ by <= 1):
+    the strong-scaling split of each width class over the ranks, so every
+    root of an all-sources step runs exactly once."""
+    q, r = divmod(m, world)
+    lo = rank * q + min(rank, r)
+    return lo, lo + q + (1 if rank < r else 0)
+
+
 def step_roots(cls: RootClass, step: int, world: int, rank: int) -> np.ndarray:
-    """Roots of `cls` that `rank` runs in `step` (cyclic sweep, disjoint across
-    ranks within a step)."""
-    n, m = cls.per_step, cls.roots.size
+    """Roots of `cls` that `rank` runs in `step` of a weak-scaling cyclic
+    sweep; disjoint across ranks within a step (n <= m / world per rank)."""
+    m = cls.roots.size
+    n = min(cls.per_step, max(1, m // world))
     start = ((step * world + rank) * n) % m
     return cls.roots[(np.arange(n) + start) % m]
 

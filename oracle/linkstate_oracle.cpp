@@ -44,6 +44,7 @@
 #include <functional>
 #include <memory>
 #include <optional>
+#include <queue>
 #include <sstream>
 #include <string>
 #include <thread>
@@ -614,10 +615,52 @@ static std::string str(const oadj_stream* s, uint32_t i) {
 using namespace orc;
 
 namespace {
+// CSR view of the oracle's own link sets (built from Graph, never from the
+// product's snapshot) for the CSR-Dijkstra restatement below.
+struct FastCsr {
+  uint32_t V = 0;
+  std::vector<uint32_t> rowPtr, col, wOut, wIn, nbrOff, nbr;
+  std::vector<uint8_t> up, noTransit;
+};
+
 struct Oracle {
   Graph g;
   std::unordered_map<std::string, uint32_t> ids;  // name -> rank (byte-lex)
   bool idsDirty = true;
+  FastCsr csr;
+  bool csrDirty = true;
+  void refreshCsr() {
+    refreshIds();
+    if (!csrDirty) return;
+    std::vector<std::string> names(ids.size());
+    for (const auto& kv : ids) names[kv.second] = kv.first;
+    FastCsr c;
+    c.V = (uint32_t)names.size();
+    c.rowPtr.assign(c.V + 1, 0);
+    c.nbrOff.assign(c.V + 1, 0);
+    c.noTransit.assign(c.V, 0);
+    for (uint32_t u = 0; u < c.V; ++u) {
+      c.noTransit[u] = g.overloaded(names[u]) ? 1 : 0;
+      std::vector<uint32_t> nb;
+      for (const auto& e : g.linksOf(names[u])) {
+        const std::string& p = e->peer(names[u]);
+        auto it = ids.find(p);
+        if (it == ids.end()) continue;
+        c.col.push_back(it->second);
+        c.wOut.push_back((uint32_t)e->metricFrom(names[u]));
+        c.wIn.push_back((uint32_t)e->metricFrom(p));
+        c.up.push_back(e->up() ? 1 : 0);
+        if (p != names[u]) nb.push_back(it->second);
+      }
+      std::sort(nb.begin(), nb.end());
+      nb.erase(std::unique(nb.begin(), nb.end()), nb.end());
+      c.nbr.insert(c.nbr.end(), nb.begin(), nb.end());
+      c.rowPtr[u + 1] = (uint32_t)c.col.size();
+      c.nbrOff[u + 1] = (uint32_t)c.nbr.size();
+    }
+    csr = std::move(c);
+    csrDirty = false;
+  }
   void refreshIds() {
     if (!idsDirty) return;
     std::vector<std::string> names;
@@ -714,6 +757,7 @@ int orc_apply(void* h, const oadj_stream* s, uint32_t first, uint32_t count,
       ch = o->g.update(db);
     }
     o->idsDirty = true;
+    o->csrDirty = true;
     if (changes) changes[k] = ch;
   }
   return 0;
@@ -799,6 +843,107 @@ int orc_digest_roots(void* h, const char* rootsNl, uint32_t n, int useMetric,
       out[3 * i] = d.reached;
       out[3 * i + 1] = d.sumDist;
       out[3 * i + 2] = d.hash;
+    }
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < threads; ++t) pool.emplace_back(work);
+  work();
+  for (auto& t : pool) t.join();
+  return 0;
+}
+
+// CSR-Dijkstra restatement of runSpf: the same
+// result as Graph::dijkstra -- distances, and next-hop sets as the OR over
+// tight usable in-links from settled transit tails (LinkState.cpp:869-901),
+// a directly connected node contributing itself -- on integer node ids with a
+// lazy-deletion binary heap, so weighted 100k..1M-node graphs take
+// milliseconds..seconds per root instead of the reference-shaped heap's
+// O(V) make_heap per strict improvement (LinkState.cpp:893). Metrics must be
+// >= 1 (then dist and next-hop sets do not depend on pop order within a
+// distance). Digests as orc_digest_roots. The test suite pins it against the
+// reference-shaped Graph::dijkstra on random graphs. Roots unknown to the
+// graph fall back to Graph::dijkstra.
+int orc_fast_digest_roots(void* h, const char* rootsNl, uint32_t n, int useMetric,
+                          int threads, uint64_t* out) {
+  Oracle* o = (Oracle*)h;
+  o->refreshCsr();
+  const FastCsr& c = o->csr;
+  std::vector<std::string> roots;
+  const char* p = rootsNl;
+  for (uint32_t i = 0; i < n; ++i) {
+    const char* q = strchr(p, '\n');
+    if (!q) q = p + strlen(p);
+    roots.emplace_back(p, q);
+    p = *q ? q + 1 : q;
+  }
+  if (threads < 1) threads = 1;
+  std::atomic<uint32_t> next{0};
+  const uint32_t INF = 0xFFFFFFFFu;
+  auto work = [&]() {
+    std::vector<uint32_t> dist(c.V), nh;
+    std::vector<uint8_t> done(c.V);
+    for (uint32_t i; (i = next.fetch_add(1)) < n;) {
+      auto it = o->ids.find(roots[i]);
+      if (it == o->ids.end()) {
+        SpfResult r = o->g.dijkstra(roots[i], useMetric != 0, nullptr);
+        Digest d = digestOf(o->g, roots[i], r, o->ids);
+        out[3 * i] = d.reached;
+        out[3 * i + 1] = d.sumDist;
+        out[3 * i + 2] = d.hash;
+        continue;
+      }
+      const uint32_t s = it->second;
+      const uint32_t nb0 = c.nbrOff[s], nnb = c.nbrOff[s + 1] - nb0;
+      const uint32_t W = std::max<uint32_t>(1, (nnb + 31) / 32);
+      std::fill(dist.begin(), dist.end(), INF);
+      std::fill(done.begin(), done.end(), 0);
+      nh.assign((size_t)c.V * W, 0u);
+      using QE = std::pair<uint64_t, uint32_t>;
+      std::priority_queue<QE, std::vector<QE>, std::greater<QE>> q;
+      dist[s] = 0;
+      q.push({0, s});
+      Digest dg;
+      while (!q.empty()) {
+        const auto [d, v] = q.top();
+        q.pop();
+        if (done[v] || d != dist[v]) continue;
+        done[v] = 1;
+        uint32_t* row = &nh[(size_t)v * W];
+        if (v != s) {
+          for (uint32_t e = c.rowPtr[v]; e < c.rowPtr[v + 1]; ++e) {
+            const uint32_t u = c.col[e];
+            if (!c.up[e] || u == v || !done[u]) continue;
+            const uint64_t w = useMetric ? c.wIn[e] : 1;
+            if ((uint64_t)dist[u] + w != d) continue;
+            if (u == s) {
+              const uint32_t b = (uint32_t)(std::lower_bound(c.nbr.begin() + nb0,
+                                                             c.nbr.begin() + nb0 + nnb, v) -
+                                            (c.nbr.begin() + nb0));
+              row[b / 32] |= 1u << (b % 32);
+            } else if (!c.noTransit[u]) {
+              const uint32_t* src = &nh[(size_t)u * W];
+              for (uint32_t k = 0; k < W; ++k) row[k] |= src[k];
+            }
+          }
+        }
+        dg.reached++;
+        dg.sumDist += d;
+        dg.hash += nodeTerm(v, d);
+        for (uint32_t k = 0; k < W; ++k) dg.hash += wordTerm(v, k, row[k]);
+        if (v != s && c.noTransit[v]) continue;
+        for (uint32_t e = c.rowPtr[v]; e < c.rowPtr[v + 1]; ++e) {
+          const uint32_t y = c.col[e];
+          if (!c.up[e] || y == v || done[y]) continue;
+          const uint64_t nd = d + (useMetric ? c.wOut[e] : 1);
+          if (nd < dist[y]) {
+            dist[y] = (uint32_t)nd;
+            q.push({nd, y});
+          }
+        }
+      }
+      out[3 * i] = dg.reached;
+      out[3 * i + 1] = dg.sumDist;
+      out[3 * i + 2] = dg.hash;
     }
   };
   std::vector<std::thread> pool;

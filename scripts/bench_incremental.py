@@ -59,7 +59,7 @@ def main():
     perm = np.random.default_rng(0x5EED).permutation(V).astype(np.uint32)
     nbrs = shard.distinct_neighbors(csr["row_ptr"], csr["col"])
     words = np.maximum(1, (nbrs + 31) // 32)
-    classes = shard.make_classes(perm, words, args.batch)
+    classes = shard.make_classes(perm, 32 * words, args.batch)
     flags = N.OSPF_WANT_DIST | N.OSPF_WANT_NH
     s = torch.cuda.current_stream()
     for c in classes:

@@ -1,0 +1,27 @@
+"""Random link-state graphs shared by the CPU and GPU parity tests."""
+import numpy as np
+
+from openr_amd.adjdb import AdjDb, AdjDbStream, create_adjacency
+
+
+def random_stream(seed, n=40, p=0.15, parallel=0.2, overload=0.1, down=0.1, wmax=20,
+                  unit=False):
+    rng = np.random.default_rng(seed)
+    names = [f"r{int(x)}" for x in rng.permutation(10 * n)[:n]]
+    adjs = {nm: [] for nm in names}
+    k = 0
+    for i in range(n):
+        for j in range(i + 1, n):
+            if rng.random() > p:
+                continue
+            for _ in range(2 if rng.random() < parallel else 1):
+                a, b = names[i], names[j]
+                ia, ib = f"{a}-{b}-{k}", f"{b}-{a}-{k}"
+                k += 1
+                m1 = 1 if unit else int(rng.integers(1, wmax + 1))
+                m2 = 1 if unit else int(rng.integers(1, wmax + 1))
+                adjs[a].append(create_adjacency(b, ia, ib, m1, overloaded=bool(rng.random() < down)))
+                adjs[b].append(create_adjacency(a, ib, ia, m2))
+    dbs = [AdjDb(nm, adjs[nm], i + 1, overloaded=bool(rng.random() < overload))
+           for i, nm in enumerate(names)]
+    return AdjDbStream.from_dbs([dbs[i] for i in rng.permutation(n)]), names

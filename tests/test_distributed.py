@@ -34,9 +34,9 @@ def _worker(rank, world, port, result_q):
     csr = ls.csr()
     names = ls.node_names()
     o = Oracle(st)
-    words = shard.nh_words_of(csr["row_ptr"], csr["col"])
+    caps = shard.neighbor_caps(shard.distinct_neighbors(csr["row_ptr"], csr["col"]))
     perm = np.random.default_rng(0x5EED).permutation(len(names)).astype(np.uint32)
-    classes = shard.make_classes(perm, words, batch=40)
+    classes = shard.make_classes(perm, caps, batch=40)
     ok = True
     for step in range(3):
         mine = np.concatenate([shard.step_roots(c, step, world, rank) for c in classes])

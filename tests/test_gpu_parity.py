@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 from golden_eval import ProductLS, load_fixtures, run_fixture
+from graphs import random_stream
 from oracle import Oracle
 from openr_amd import topology as T
 from openr_amd.adjdb import AdjDb, AdjDbStream, create_adjacency
@@ -18,14 +19,15 @@ pytestmark = pytest.mark.gpu
 FIXTURES = load_fixtures()
 
 
-@pytest.fixture(params=["auto", "0", "1", "2", "4", "5", "6"])
+@pytest.fixture(params=["auto", "0", "1", "2", "4", "5", "6", "7"])
 def variant(request, monkeypatch):
     """Run each parity test with the planner's choice and with every other
     kernel variant forced where its state fits (OSPF_FORCE_VARIANT): 0/1/2 =
     Dial kernel (LDS / mixed / HBM state), 3/4 = BFS kernel (LDS bitmaps,
     byte next-hops in LDS / next-hops in HBM; unit metric only), 5 =
     multi-source bit-parallel BFS (unit metric, no ignored links), 6 =
-    bucketed Dial (frontier lists; any metric <= 63)."""
+    bucketed Dial (frontier lists; any metric <= 63), 7 = wave-per-root
+    bucketed Dial (any metric, per-run ignored links)."""
     if request.param == "auto":
         monkeypatch.delenv("OSPF_FORCE_VARIANT", raising=False)
     else:
@@ -36,29 +38,6 @@ def variant(request, monkeypatch):
 @pytest.mark.parametrize("fx", FIXTURES, ids=[f["name"] for f in FIXTURES])
 def test_reference_fixture_on_gpu(fx, variant):
     assert run_fixture(fx, ProductLS) > 0
-
-
-def random_stream(seed, n=40, p=0.15, parallel=0.2, overload=0.1, down=0.1, wmax=20,
-                  unit=False):
-    rng = np.random.default_rng(seed)
-    names = [f"r{int(x)}" for x in rng.permutation(10 * n)[:n]]
-    adjs = {nm: [] for nm in names}
-    k = 0
-    for i in range(n):
-        for j in range(i + 1, n):
-            if rng.random() > p:
-                continue
-            for _ in range(2 if rng.random() < parallel else 1):
-                a, b = names[i], names[j]
-                ia, ib = f"{a}-{b}-{k}", f"{b}-{a}-{k}"
-                k += 1
-                m1 = 1 if unit else int(rng.integers(1, wmax + 1))
-                m2 = 1 if unit else int(rng.integers(1, wmax + 1))
-                adjs[a].append(create_adjacency(b, ia, ib, m1, overloaded=bool(rng.random() < down)))
-                adjs[b].append(create_adjacency(a, ib, ia, m2))
-    dbs = [AdjDb(nm, adjs[nm], i + 1, overloaded=bool(rng.random() < overload))
-           for i, nm in enumerate(names)]
-    return AdjDbStream.from_dbs([dbs[i] for i in rng.permutation(n)]), names
 
 
 def both(stream):
@@ -374,9 +353,13 @@ def test_engine_repair_fabric_link_events(seed):
         assert ok.mean() > 0.5, ok.mean()
 
 
-def test_mesh_60k_bucketed_dial_digests():
-    """Weighted mesh too large for LDS state: the planner's bucketed Dial
-    (variant 6) against the oracle, sampled roots, digests (dist + next hops)."""
+@pytest.mark.parametrize("forced", [None, "6"])
+def test_mesh_60k_bucketed_dial_digests(forced, monkeypatch):
+    """Weighted mesh too large for LDS state: the planner's wave-per-root Dial
+    (variant 7) and the workgroup-per-root bucketed Dial (variant 6) against
+    the oracle, sampled roots, digests (dist + next hops)."""
+    if forced:
+        monkeypatch.setenv("OSPF_FORCE_VARIANT", forced)
     st = T.mesh(60000, seed=7)
     o, p = both(st)
     names = p.node_names()
@@ -384,7 +367,7 @@ def test_mesh_60k_bucketed_dial_digests():
     roots = [names[i] for i in rng.choice(len(names), 12, replace=False)]
     eng = Engine(0)
     eng.load(p.csr())
-    assert eng.plan(1)["variant"] == 6
+    assert eng.plan(1)["variant"] == int(forced or 7)
     assert np.array_equal(p.digests(roots), o.digests(roots, threads=8))
     for r in roots[:2]:
         assert p.spf_text(r) == o.spf_text(r)
@@ -630,3 +613,175 @@ def test_engine_repair_wide_and_node_events(case):
     spines = np.array([n.startswith("1-") for n in names])
     assert ok.mean() > 0.3, ok.mean()
     assert (ok & spines).any()  # wide rows repaired too
+
+
+# ------------------------------------------ wave-per-root Dial (variant 7)
+WD_KNOBS = {
+    "default": {},
+    "tagged": {"OSPF_WD_DELTA": "3"},                      # buckets of 3 distances
+    "overflow": {"OSPF_WD_BCAP": "4"},                     # lists overflow -> node scans
+    "tagged_overflow": {"OSPF_WD_DELTA": "5", "OSPF_WD_BCAP": "3"},
+    "wave": {"OSPF_WD_GROUP": "1"},                        # a wave per root
+    "cu": {"OSPF_WD_GROUP": "16"},                         # a 16-wave group per root
+    "unpacked": {"OSPF_WD_PACK": "0"},                     # dist / next-hop rows as state
+    "pack16": {"OSPF_WD_PACK": "16"},                      # 16-bit next-hop field
+}
+
+
+@pytest.mark.parametrize("knob", list(WD_KNOBS), ids=list(WD_KNOBS))
+@pytest.mark.parametrize("wmax", [20, 200, 100000])
+@pytest.mark.parametrize("seed", range(3))
+def test_wdial_random_graphs_any_metric(seed, wmax, knob, monkeypatch):
+    """Variant 7 on random graphs with parallel, down and overloaded links and
+    metrics up to 200 (ring of one list per distance) and 100,000 (buckets of
+    several distances with tagged entries); full SPF text of every root, in
+    link-metric and hop-count mode, against the oracle."""
+    monkeypatch.setenv("OSPF_FORCE_VARIANT", "7")
+    for k, v in WD_KNOBS[knob].items():
+        monkeypatch.setenv(k, v)
+    st, names = random_stream(900 + seed, n=60, p=0.1, wmax=wmax)
+    o, p = both(st)
+    p.prefetch(names)
+    for r in names:
+        assert p.spf_text(r) == o.spf_text(r), r
+        assert p.spf_text(r, False) == o.spf_text(r, False), r
+
+
+@pytest.mark.parametrize("knob", ["default", "tagged", "overflow"])
+def test_wdial_ksp2_reruns_with_ignored_links(knob, monkeypatch):
+    """KSP2 masked reruns through variant 7 (per-run ignore lists read from
+    HBM) on a weighted graph with metrics above 63."""
+    monkeypatch.setenv("OSPF_FORCE_VARIANT", "7")
+    for k, v in WD_KNOBS[knob].items():
+        monkeypatch.setenv(k, v)
+    st, names = random_stream(950, n=40, p=0.15, wmax=500)
+    o, p = both(st)
+    for src in names[:4]:
+        assert p.ksp2_text(src, names) == o.ksp2_text(src, names), src
+    assert p.spf_runs == o.spf_runs
+
+
+@pytest.mark.parametrize("max_metric", [64, 1000, 70000])
+def test_weighted_fabric_metric_above_63(max_metric):
+    """Weighted fabric (pods = 800, 45k nodes) with metrics 1..max_metric: the
+    planner's large-graph weighted path (variant 7: state beyond LDS) vs the
+    oracle's CSR-Dijkstra restatement (the reference-shaped heap needs ~2 min
+    per root here), sampled roots of every switch class, in link-metric and
+    hop-count mode."""
+    st = T.fabric(pods=800, planes=8, weighted_seed=7, max_metric=max_metric)
+    o, p = both(st)
+    eng = Engine(0)
+    eng.load(p.csr())
+    assert eng.plan(1)["variant"] == 7
+    names = p.node_names()
+    rng = np.random.default_rng(0x5eed)
+    roots = [names[i] for i in rng.choice(len(names), 60, replace=False)]
+    roots += ["1-0-0", "1-7-35", "2-0-0", "3-0-0"]
+    assert np.array_equal(p.digests(roots), o.fast_digests(roots, threads=8))
+    assert np.array_equal(p.digests(roots, False), o.fast_digests(roots, False, threads=8))
+
+
+def _chain_dbs(names, down):
+    """A unit-metric chain; `down`: the middle link (19, 20) is drained."""
+    out = []
+    for i, nm in enumerate(names):
+        adjs = []
+        for j in (i - 1, i + 1):
+            if 0 <= j < len(names):
+                ov = down and i == 19 and j == 20
+                adjs.append(create_adjacency(names[j], f"{nm}-{names[j]}", f"{names[j]}-{nm}", 1,
+                                             overloaded=ov))
+        out.append(AdjDb(nm, adjs, i + 1))
+    return out
+
+
+def test_depth_bound_after_bridge_drain_and_undrain():
+    """draining a bridge recomputes the multi-source BFS
+    level bound on the two halves (ids chosen so each half's seed sits in its
+    middle: bound 22); undraining must recompute it again (the chain's hop
+    diameter is 39), or roots past level 22 come back unreached. Incremental
+    LinkState (the device graph patched in place), every root batched."""
+    names = [("a" if i in (10, 30) else "m") + f"{i:02d}" for i in range(40)]
+    o, p = Oracle(), LinkState()
+    st = AdjDbStream.from_dbs(_chain_dbs(names, False))
+    assert o.apply(st) == p.apply(st)
+    p.set_incremental(True)
+    for down in (True, False, True, False):
+        upd = AdjDbStream.from_dbs([d for d in _chain_dbs(names, down)
+                                    if d.name in (names[19], names[20])])
+        assert o.apply(upd) == p.apply(upd)
+        p.prefetch(names)
+        for r in names:
+            assert p.spf_text(r) == o.spf_text(r), (down, r)
+
+
+def test_engine_depth_bound_link_up_recomputes():
+    """Same at the C ABI: ospf_update_links down then up, the multi-source
+    BFS over every root equals a fresh load of the same graph."""
+    names = [("a" if i in (10, 30) else "m") + f"{i:02d}" for i in range(40)]
+    lsx = LinkState(stream=AdjDbStream.from_dbs(_chain_dbs(names, False)))
+    csr = lsx.csr()
+    eng = Engine(0)
+    eng.load(csr)
+    V = eng.V
+    i19, i20 = lsx.node_id(names[19]), lsx.node_id(names[20])
+    rp, col, lid = csr["row_ptr"], csr["col"], csr["link_id"]
+    e = next(e for e in range(rp[i19], rp[i19 + 1]) if col[e] == i20)
+    roots = np.arange(V, dtype=np.uint32)
+    for up in (0, 1):
+        eng.update_links([(int(lid[e]), up, 1, 1)], version=2 + up)
+        got = eng.run(roots, 1)
+        ref_csr = {k: v.copy() for k, v in csr.items()}
+        ref_csr["edge_up"][lid == lid[e]] = up
+        fresh = Engine(0)
+        fresh.load(ref_csr)
+        want = fresh.run(roots, 1)
+        assert np.array_equal(got["dist"], want["dist"]) and np.array_equal(got["nh"], want["nh"])
+    assert int(got["dist"][lsx.node_id(names[0]), lsx.node_id(names[39])]) == 39
+
+
+def test_engine_update_links_rejects_whole_batch():
+    """a batch with one bad entry (unknown link id, or
+    metric 0 on an up link) is rejected before any state changes: the graph,
+    its unit-metric flag and the results stay those of before the call."""
+    p, csr = _csr_of(T.fabric(pods=4, planes=2))
+    eng = Engine(0)
+    eng.load(csr)
+    V = eng.V
+    roots = np.arange(V, dtype=np.uint32)
+    W = int(max(eng.nh_words(r) for r in range(V)))
+    before = eng.run(roots, W)
+    l0 = int(csr["link_id"][0])
+    for bad in ([(l0, 1, 7, 7), (10 ** 6, 1, 1, 1)], [(l0, 0, 1, 1), (l0 + 1, 1, 0, 5)]):
+        with pytest.raises(EngineError):
+            eng.update_links(bad, version=9)
+        assert eng.info().unit_metric == 1
+        after = eng.run(roots, W)
+        assert np.array_equal(after["dist"], before["dist"])
+        assert np.array_equal(after["nh"], before["nh"])
+
+
+@pytest.mark.parametrize("pack", ["8", "16"])
+def test_wdial_packed_overflow_falls_back(pack, monkeypatch):
+    """Packed state (dist << K | next hops) with distances that outgrow the
+    field (metrics up to 100,000 on a long chain: > 2^24) aborts the packed
+    run and reruns the root unpacked: same rows as the unpacked kernel."""
+    monkeypatch.setenv("OSPF_FORCE_VARIANT", "7")
+    names = [f"c{i:03d}" for i in range(300)]
+    dbs = []
+    for i, nm in enumerate(names):
+        adjs = [create_adjacency(names[j], f"{nm}-{names[j]}", f"{names[j]}-{nm}", 90000 + j)
+                for j in (i - 1, i + 1) if 0 <= j < len(names)]
+        dbs.append(AdjDb(nm, adjs, i + 1))
+    st = AdjDbStream.from_dbs(dbs)
+    o, p = both(st)
+    eng = Engine(0)
+    eng.load(p.csr())
+    roots = np.arange(eng.V, dtype=np.uint32)
+    monkeypatch.setenv("OSPF_WD_PACK", pack)
+    a = eng.run(roots, 1, want_digest=True)
+    monkeypatch.setenv("OSPF_WD_PACK", "0")
+    b = eng.run(roots, 1, want_digest=True)
+    assert int(a["dist"].max()) > (1 << 24)
+    assert np.array_equal(a["dist"], b["dist"]) and np.array_equal(a["nh"], b["nh"])
+    assert np.array_equal(a["digest"], o.fast_digests(names, threads=8))
