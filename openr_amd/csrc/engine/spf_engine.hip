@@ -33,6 +33,7 @@ struct ospf_ctx {
   uint64_t non_unit = 0;  // usable entries with metric != 1 (exact unit_metric under patches)
   void* d_graph = nullptr;
   ospf::DevGraph g{};
+  const uint32_t* ew_base = nullptr;  // packed entries (g.ew) as words, for patches
   uint32_t max_dn = 0;
   uint32_t depth_bound = 2;  // BFS levels any root can reach (unit metric / hop count)
   uint32_t exact_bound = 2;  // depth_bound as last computed in full (patches may raise depth_bound)
@@ -401,10 +402,10 @@ int run_wdial(ospf_ctx* c, const ospf_batch* b, bool hop, hipStream_t s) {
   // whole CU per root, thin-frontier graphs (meshes) a wave per root.
   const double rounds = (double)maxw * std::max<uint32_t>(2, c->depth_bound);
   const double per_round = (double)c->info.n_edges / std::max(1.0, rounds);
-  uint32_t G = per_round > 2048 ? 4 : per_round > 128 ? 2 : 1;
-  // few roots: wider groups, so the groups that do run have several roots
-  // each (no one-root tail) and more lanes per round
-  while (G < 16 && n < 4ull * c->n_cu * (16 / G)) G *= 2;
+  uint32_t G = per_round > 2048 ? 8 : per_round > 128 ? 2 : 1;
+  // fewer roots than groups: wider groups (more lanes per round) until every
+  // group has a root
+  while (G < 16 && n < (uint64_t)c->n_cu * (16 / G)) G *= 2;
   if (const char* e = getenv("OSPF_WD_GROUP")) G = (uint32_t)std::max(1, std::min(16, atoi(e)));
   while (16 % G) --G;
   const uint32_t ngroups =
@@ -865,9 +866,19 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
     dkey[2ull * u] = ospf::digest_dist_key(u);
     dkey[2ull * u + 1] = ospf::digest_node_key(u);
   }
-  size_t off[11], tot = 0;
-  const size_t szs[11] = {sz_row, sz_e, sz_e, sz_e, sz_e, sz_nt, sz_dnoff, sz_dn, sz_big, sz_key, sz_le};
-  for (int i = 0; i < 11; ++i) {
+  // packed {colx, w | rw << 16} entries when every metric fits 16 bits
+  bool ew_ok = true;
+  for (uint32_t e = 0; e < Ep && ew_ok; ++e) ew_ok = pw[e] <= 0xFFFFu && prw[e] <= 0xFFFFu;
+  std::vector<uint32_t> pew(ew_ok ? 2ull * Ep : 2, 0u);
+  for (uint32_t e = 0; e < Ep && ew_ok; ++e) {
+    pew[2ull * e] = pcolx[e];
+    pew[2ull * e + 1] = pw[e] | (prw[e] << 16);
+  }
+  const size_t sz_ew = pew.size() * 4ull;
+  size_t off[12], tot = 0;
+  const size_t szs[12] = {sz_row, sz_e,     sz_e,  sz_e,   sz_e,  sz_nt,
+                          sz_dnoff, sz_dn, sz_big, sz_key, sz_le, sz_ew};
+  for (int i = 0; i < 12; ++i) {
     off[i] = tot;
     tot += align_up(std::max<size_t>(szs[i], 4), 256);
   }
@@ -883,10 +894,10 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
     return fail(c, OSPF_E_NOMEM, std::string("hipMalloc graph: ") + hipGetErrorString(he));
   }
   char* base = (char*)c->d_graph;
-  const void* srcs[11] = {prow.data(), pcolx.data(), pw.data(), prw.data(), plink.data(),
+  const void* srcs[12] = {prow.data(), pcolx.data(), pw.data(), prw.data(), plink.data(),
                           nt.data(), dn_off.data(), dn.data(), big.data(), dkey.data(),
-                          link_e.data()};
-  for (int i = 0; i < 11; ++i)
+                          link_e.data(), pew.data()};
+  for (int i = 0; i < 12; ++i)
     if (szs[i] && srcs[i]) HIPCHK(c, hipMemcpy(base + off[i], srcs[i], szs[i], hipMemcpyHostToDevice));
   c->g.V = V;
   c->g.E = Ep;
@@ -903,6 +914,8 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   c->g.dkey = (const uint64_t*)(base + off[9]);
   c->g.n_lid = n_lid;
   c->g.link_e = (const uint32_t*)(base + off[10]);
+  c->g.ew = ew_ok ? (const uint2*)(base + off[11]) : nullptr;
+  c->ew_base = ew_ok ? (const uint32_t*)(base + off[11]) : nullptr;
   c->h_row_ptr.assign(csr->row_ptr, csr->row_ptr + V + 1);
   c->h_dn_off = std::move(dn_off);
   c->h_dn = std::move(dn);
@@ -1328,6 +1341,19 @@ int ospf_update_links(ospf_ctx* c, const ospf_link_update* u, uint32_t n, uint64
     set(c->h_pw, o_w, ehi, u[i].metric_hi);
     set(c->h_prw, o_rw, elo, u[i].metric_hi);
     set(c->h_prw, o_rw, ehi, u[i].metric_lo);
+    if (c->g.ew) {  // packed entries: same change, or dropped past 16-bit metrics
+      if (u[i].metric_lo > 0xFFFFu || u[i].metric_hi > 0xFFFFu) {
+        c->g.ew = nullptr;
+      } else {
+        const size_t o_ew = c->ew_base - (const uint32_t*)base;
+        for (uint32_t e : {elo, ehi}) {
+          idx.push_back((uint32_t)(o_ew + 2ull * e));
+          val.push_back(c->h_pcolx[e]);
+          idx.push_back((uint32_t)(o_ew + 2ull * e + 1));
+          val.push_back(c->h_pw[e] | (c->h_prw[e] << 16));
+        }
+      }
+    }
   }
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipDeviceSynchronize());  // no batch may be reading the graph

@@ -40,6 +40,9 @@ struct DevGraph {
   const uint32_t* dn;
   uint32_t n_lid;
   const uint32_t* link_e;
+  // [E] {colx, w | rw << 16}: one 8-B load per entry for the weighted path
+  // (null when a metric exceeds 0xFFFF: the separate arrays are read instead)
+  const uint2* ew;
 };
 
 struct RunArgs {

@@ -207,14 +207,24 @@ struct GRun {
           e[u] = qb[lo] + (t - qp[lo]);
         }
       }
+      if (g.ew) {  // {colx, w | rw << 16}: one 8-B load per entry
 #pragma unroll
-      for (uint32_t u = 0; u < kUnroll; ++u) {
-        cx[u] = ok[u] ? g.colx[e[u]] : kDown;
-        w[u] = 1u;
-        rw[u] = 1u;
-        if (!a.hop && ok[u]) {
-          w[u] = g.w[e[u]];
-          rw[u] = g.rw[e[u]];
+        for (uint32_t u = 0; u < kUnroll; ++u) {
+          const uint2 ce = ok[u] ? g.ew[e[u]] : make_uint2(kDown, 0u);
+          cx[u] = ce.x;
+          w[u] = a.hop ? 1u : (ce.y & 0xFFFFu);
+          rw[u] = a.hop ? 1u : (ce.y >> 16);
+        }
+      } else {
+#pragma unroll
+        for (uint32_t u = 0; u < kUnroll; ++u) {
+          cx[u] = ok[u] ? g.colx[e[u]] : kDown;
+          w[u] = 1u;
+          rw[u] = 1u;
+          if (!a.hop && ok[u]) {
+            w[u] = g.w[e[u]];
+            rw[u] = g.rw[e[u]];
+          }
         }
       }
 #pragma unroll
@@ -520,10 +530,20 @@ __device__ bool run_root(const DevGraph& g, const WDialArgs& a, uint32_t* lds, u
   return r.run();
 }
 
+// Root order: callers sweep roots in locality order (roots hanging off the
+// same switches adjacent), and workgroup b runs on XCD b % 8. The k-th root
+// of group b is k * ngroups + (b % 8) * (ngroups / 8) + b / 8, so the groups
+// of one XCD run consecutive roots at once: they read the same graph rows
+// around the same rounds, and the XCD's L2 serves them to all of them.
+__device__ __forceinline__ uint32_t root_slot(uint32_t b, uint32_t ngroups) {
+  if (ngroups & 7u) return b;
+  return (b & 7u) * (ngroups >> 3) + (b >> 3);
+}
+
 template <bool IGN, bool TAG, bool PACK>
 __global__ void __launch_bounds__(1024) wdial_kernel(DevGraph g, WDialArgs a) {
   extern __shared__ uint32_t lds[];
-  for (uint32_t rix = blockIdx.x; rix < a.n; rix += gridDim.x) {
+  for (uint32_t rix = root_slot(blockIdx.x, gridDim.x); rix < a.n; rix += gridDim.x) {
     bool done = true;
     if (PACK) done = run_root<IGN, TAG, true>(g, a, lds, rix);
     __syncthreads();

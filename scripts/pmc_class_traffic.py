@@ -1,14 +1,13 @@
 #!/usr/bin/env python3
 """HBM traffic of one root class per launch: rocprofv3 --pmc FETCH_SIZE and
 WRITE_SIZE passes (separate: 3 + 2 > 4 TCC slots on gfx950) over
-scripts/exp_class.py running that class alone, summed over every engine
-kernel (the multi-source BFS runs a sequence of kernels per class launch) and
-divided by the launches exp_class made (reps + 1). MI355X_MICROARCH.md §HBM:
-FETCH_SIZE reads half the bytes of a wide coalesced stream on gfx950 -> x2;
-WRITE_SIZE as is.
+`bench.py --class-only CAP --reps R` (the class alone, R launches on one
+stream), summed over every engine kernel (a class launch is a sequence of
+kernels) and divided by R. MI355X_MICROARCH.md §HBM: FETCH_SIZE reads half
+the bytes of a wide coalesced stream on gfx950 -> x2; WRITE_SIZE as is.
 
 Usage: pmc_class_traffic.py FETCH_DIR WRITE_DIR LAUNCHES ROOTS KEY OUT_JSON
-(OUT_JSON is updated in place: one entry per KEY, e.g. variant5_W1)."""
+(OUT_JSON is updated in place: one entry per KEY, e.g. variant5_cap8)."""
 import csv
 import glob
 import json

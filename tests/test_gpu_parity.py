@@ -785,3 +785,41 @@ def test_wdial_packed_overflow_falls_back(pack, monkeypatch):
     assert int(a["dist"].max()) > (1 << 24)
     assert np.array_equal(a["dist"], b["dist"]) and np.array_equal(a["nh"], b["nh"])
     assert np.array_equal(a["digest"], o.fast_digests(names, threads=8))
+
+
+def test_wdial_packed_edges_follow_link_updates(monkeypatch):
+    """Variant 7 reads {colx, w | rw << 16} entries while every metric fits 16
+    bits: ospf_update_links patches them with the separate arrays, and a
+    metric above 0xFFFF drops them (the kernel reads the arrays). Each state
+    equals a fresh load of the same graph."""
+    monkeypatch.setenv("OSPF_FORCE_VARIANT", "7")
+    st, names = random_stream(61, n=60, p=0.1, wmax=30)
+    p = LinkState(stream=st)
+    csr = p.csr()
+    eng = Engine(0)
+    eng.load(csr)
+    V = eng.V
+    roots = np.arange(V, dtype=np.uint32)
+    W = int(max(eng.nh_words(r) for r in range(V)))
+    rp, lid = csr["row_ptr"], csr["link_id"]
+    owner = np.repeat(np.arange(V), np.diff(rp.astype(np.int64)))
+    rng = np.random.default_rng(4)
+    cur = {k: v.copy() for k, v in csr.items()}
+    for step, big in enumerate([False, False, True, False]):
+        ups = []
+        for l in rng.choice(int(lid.max()) + 1, 5, replace=False):
+            e = np.nonzero(lid == l)[0]
+            lo, hi = (e[0], e[1]) if owner[e[0]] <= owner[e[1]] else (e[1], e[0])
+            m_lo = int(rng.integers(1, 40)) + (100000 if big else 0)
+            m_hi = int(rng.integers(1, 40))
+            up = int(rng.random() > 0.2)
+            cur["edge_up"][[lo, hi]] = up
+            cur["metric"][lo], cur["metric"][hi] = m_lo, m_hi
+            ups.append((int(l), up, m_lo, m_hi))
+        eng.update_links(ups, version=2 + step)
+        got = eng.run(roots, W)
+        fresh = Engine(0)
+        fresh.load({k: v.copy() for k, v in cur.items()})
+        want = fresh.run(roots, W)
+        assert np.array_equal(got["dist"], want["dist"]), step
+        assert np.array_equal(got["nh"], want["nh"]), step
