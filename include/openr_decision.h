@@ -84,6 +84,28 @@ char* odl_ksp2_text(odl_ls* ls, const char* src, const char* dsts_nl, uint32_t n
 char* odl_route_text(odl_ls* ls, const char* me, const char* announcers_nl, uint32_t n,
                      int algo);
 
+/* LinkState::pathAInPathB (LinkState.h:477-492): 1 if path a (n links, keys
+ * "n1%if1|n2%if2" one per line) occurs contiguously in path b, else 0; -1 on
+ * a malformed key. */
+int odl_path_a_in_b(const char* a_nl, uint32_t na, const char* b_nl, uint32_t nb);
+
+/* SpfSolver::buildRouteDb (SpfSolver.cpp:460-646), one area, for each of the
+ * n_mes nodes in mes_nl (their SPF results come from one batched engine
+ * launch). prefixes_nl = n lines "prefix \t entry,entry,..." with
+ * entry = "node:fwd:algo:weight[:prepend]" (a thrift::PrefixEntry: fwd 0 IP /
+ * 1 SR_MPLS; algo 0 SP_ECMP, 1 KSP2_ED_ECMP, 2 SP_UCMP_ADJ_WEIGHT_PROPAGATION,
+ * 3 SP_UCMP_PREFIX_WEIGHT_PROPAGATION; weight 0 = unset; optional prepend
+ * label). flags: 1 node-segment labels, 2 adjacency labels, 4 UCMP (the
+ * SpfSolver constructor switches). Text, one line each, next hops sorted:
+ *   me \t NONE                       (`me` unknown: the reference's nullopt)
+ *   me \t R \t prefix \t igpCost(u32) \t ucmpWeight | -
+ *   me \t U \t prefix \t ifName \t neighbor \t metric(i32) \t op \t labels \t weight
+ *   me \t M \t label  \t ifName \t neighbor \t metric(i32) \t op \t labels \t weight
+ * op: 0 none, 1 PHP, 2 SWAP, 3 PUSH, 4 POP_AND_LOOKUP; labels comma-separated
+ * (SWAP: the swap label; PUSH: bottom of stack first). */
+char* odl_route_db_text(odl_ls* ls, const char* mes_nl, uint32_t n_mes, const char* prefixes_nl,
+                        uint32_t n, int flags);
+
 /* LinkState::resolveUcmpWeights (LinkState.cpp:913-1033) over
  * getSpfResult(root): leaves_nl = n lines "name\tweight"; algo 2 =
  * SP_UCMP_ADJ_WEIGHT_PROPAGATION, 3 = SP_UCMP_PREFIX_WEIGHT_PROPAGATION.

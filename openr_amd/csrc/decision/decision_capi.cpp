@@ -250,6 +250,101 @@ char* odl_route_text(odl_ls* h, const char* me, const char* announcers_nl, uint3
   }, (char*)nullptr);
 }
 
+int odl_path_a_in_b(const char* a_nl, uint32_t na, const char* b_nl, uint32_t nb) {
+  try {
+    auto parse = [](const char* nl, uint32_t n) {
+      odl::Path p;
+      for (const auto& key : splitNl(nl, n)) {
+        const size_t bar = key.find('|'), p1 = key.find('%'), p2 = key.find('%', bar);
+        if (bar == std::string::npos || p1 > bar || p2 == std::string::npos)
+          throw std::invalid_argument("link key must be n1%if1|n2%if2: " + key);
+        odl::Adjacency a1, a2;
+        const std::string n1 = key.substr(0, p1), n2 = key.substr(bar + 1, p2 - bar - 1);
+        a1.otherNodeName = n2;
+        a1.ifName = key.substr(p1 + 1, bar - p1 - 1);
+        a2.otherNodeName = n1;
+        a2.ifName = key.substr(p2 + 1);
+        a1.otherIfName = a2.ifName;
+        a2.otherIfName = a1.ifName;
+        p.push_back(std::make_shared<odl::Link>(n1, a1, n2, a2));
+      }
+      return p;
+    };
+    return odl::LinkState::pathAInPathB(parse(a_nl, na), parse(b_nl, nb)) ? 1 : 0;
+  } catch (...) {
+    return -1;
+  }
+}
+
+char* odl_route_db_text(odl_ls* h, const char* mes_nl, uint32_t n_mes, const char* prefixes_nl,
+                        uint32_t n, int flags) {
+  return guard(h, [&]() -> char* {
+    auto field = [](const std::string& s, size_t& pos, char sep) {
+      const size_t e = s.find(sep, pos);
+      std::string out = s.substr(pos, e == std::string::npos ? std::string::npos : e - pos);
+      pos = e == std::string::npos ? s.size() + 1 : e + 1;
+      return out;
+    };
+    std::vector<odl::PrefixRoute> prefixes;
+    for (const auto& ln : splitNl(prefixes_nl, n)) {
+      const size_t t = ln.find('\t');
+      if (t == std::string::npos) throw std::invalid_argument("prefix line needs prefix\\tentries");
+      odl::PrefixRoute pr;
+      pr.prefix = ln.substr(0, t);
+      std::stringstream es(ln.substr(t + 1));
+      for (std::string x; std::getline(es, x, ',');) {
+        if (x.empty()) continue;
+        size_t pos = 0;
+        odl::PrefixEntry e;
+        e.node = field(x, pos, ':');
+        const std::string fwd = field(x, pos, ':'), algo = field(x, pos, ':'),
+                          w = field(x, pos, ':'), pl = field(x, pos, ':');
+        if (e.node.empty() || fwd.empty() || algo.empty() || w.empty())
+          throw std::invalid_argument("prefix entry needs node:fwd:algo:weight[:prepend]");
+        e.fwdType = std::stoi(fwd);
+        e.algo = std::stoi(algo);
+        e.weight = std::stoll(w);
+        if (e.fwdType < 0 || e.fwdType > 1 || e.algo < 0 || e.algo > 3 || e.weight < 0)
+          throw std::invalid_argument("prefix entry out of range: " + x);
+        if (!pl.empty()) e.prependLabel = std::stoi(pl);
+        pr.entries.push_back(std::move(e));
+      }
+      prefixes.push_back(std::move(pr));
+    }
+    odl::RouteOptions opt;
+    opt.nodeSegmentLabels = flags & 1;
+    opt.adjacencyLabels = flags & 2;
+    opt.ucmp = flags & 4;
+    const auto mes = splitNl(mes_nl, n_mes);
+    odl::SpfSolver solver(h->ls);
+    const auto dbs = solver.buildRouteDbs(mes, prefixes, opt);
+    std::ostringstream os;
+    for (size_t i = 0; i < mes.size(); ++i) {
+      const auto& me = mes[i];
+      if (!dbs[i]) {
+        os << me << "\tNONE\n";
+        continue;
+      }
+      auto put = [&](const char* kind, const std::string& key, const std::vector<odl::NextHop>& nhs) {
+        for (const auto& x : nhs) {
+          os << me << '\t' << kind << '\t' << key << '\t' << x.ifName << '\t' << x.neighbor << '\t'
+             << x.metric << '\t' << (int)x.op << '\t';
+          for (size_t j = 0; j < x.labels.size(); ++j) os << (j ? "," : "") << x.labels[j];
+          os << '\t' << x.weight << '\n';
+        }
+      };
+      for (const auto& kv : dbs[i]->unicast) {
+        os << me << "\tR\t" << kv.first << '\t' << kv.second.igpCost << '\t';
+        if (kv.second.weight) os << *kv.second.weight; else os << '-';
+        os << '\n';
+        put("U", kv.first, kv.second.nextHops);
+      }
+      for (const auto& kv : dbs[i]->mpls) put("M", std::to_string(kv.first), kv.second);
+    }
+    return dup(os.str());
+  }, (char*)nullptr);
+}
+
 char* odl_ucmp_text(odl_ls* h, const char* root, const char* leaves_nl, uint32_t n, int algo,
                     int use_link_metric) {
   return guard(h, [&]() -> char* {

@@ -3,14 +3,16 @@
 // engine). Restates, for a prefix announced by a set of nodes in one area:
 //   getNextHopsWithMetric   openr/decision/SpfSolver.cpp:1043-1089
 //   getNextHopsThrift       openr/decision/SpfSolver.cpp:1163-1285
-//                           (perDestination = false: SP_ECMP unicast and
-//                            MPLS node-label routes)
+//   selectBestPathsSpf      openr/decision/SpfSolver.cpp:772-845 (UCMP too)
 //   selectBestPathsKsp2     openr/decision/SpfSolver.cpp:847-973
-// Prefix-state policy (RIB selection, BGP metrics, minNexthop, UCMP weights)
-// is outside the SPF path and not restated here.
+//   createRouteForPrefix / buildRouteDb  SpfSolver.cpp:197-646
+// RIB policy (BGP metric vectors, prefix-metric best-route selection,
+// minNexthop, static routes, multi-area merge) is outside the SPF path and
+// not restated here.
 #pragma once
 
 #include <cstdint>
+#include <map>
 #include <optional>
 #include <string>
 #include <unordered_map>
@@ -20,44 +22,116 @@
 
 namespace odl {
 
-enum class MplsOp : int { kNone = 0, kPhp = 1, kSwap = 2, kPush = 3 };
+enum class MplsOp : int { kNone = 0, kPhp = 1, kSwap = 2, kPush = 3, kPopAndLookup = 4 };
 
 // thrift::NextHopThrift (openr/if/Network.thrift:54-70), SPF-relevant fields.
-// `metric` is kept 64-bit; the reference stores it as i32.
+// `metric` is the thrift i32: createNextHop(..., int32_t metric, ...)
+// (openr/common/LsdbUtil.cpp:658-675) narrows the u64 LinkState metric, which
+// keeps its low 32 bits (two's complement), as toThriftMetric does.
 struct NextHop {
   std::string ifName;
   std::string neighbor;
-  Metric metric = 0;
+  int32_t metric = 0;
   MplsOp op = MplsOp::kNone;
   std::vector<int32_t> labels;  // SWAP: {label}; PUSH: stack, bottom first
+  int32_t weight = 0;           // UCMP next-hop weight, 0 = ECMP
   bool operator<(const NextHop& o) const;
   bool operator==(const NextHop& o) const;
+};
+inline int32_t toThriftMetric(Metric m) { return (int32_t)(uint32_t)m; }
+
+// isMplsLabelValid (openr/common/MplsUtil.h:19-22): 20-bit, non-zero
+inline bool isMplsLabelValid(int32_t l) { return (l & 0xfff00000) == 0 && l != 0; }
+
+// thrift::PrefixEntry (openr/if/Types.thrift), the fields the route build
+// reads: forwarding type (0 IP, 1 SR_MPLS) and algorithm (0 SP_ECMP,
+// 1 KSP2_ED_ECMP, 2 SP_UCMP_ADJ_WEIGHT_PROPAGATION, 3
+// SP_UCMP_PREFIX_WEIGHT_PROPAGATION; OpenrConfig.thrift:18-50), UCMP weight
+// (0 = unset) and prepend label. Prefix metrics / BGP metric vectors are RIB
+// policy outside the SPF path: every reachable announcer is a best route
+// (selectBestRoutes' non-BGP branch, SpfSolver.cpp:666-672).
+struct PrefixEntry {
+  std::string node;
+  int fwdType = 0;
+  int algo = 0;
+  int64_t weight = 0;
+  std::optional<int32_t> prependLabel;
+};
+struct PrefixRoute {
+  std::string prefix;
+  std::vector<PrefixEntry> entries;
+};
+
+// RibUnicastEntry (RibEntry.h:60-77): next hops, igpCost (unsigned int) and
+// the UCMP weight that replaces bestPrefixEntry.weight.
+struct UnicastRoute {
+  std::vector<NextHop> nextHops;
+  uint32_t igpCost = 0;
+  std::optional<int64_t> weight;
+};
+
+// DecisionRouteDb (SpfSolver.h:80-98): routes by prefix and by MPLS label,
+// next hops sorted
+struct RouteDb {
+  std::map<std::string, UnicastRoute> unicast;
+  std::map<int32_t, std::vector<NextHop>> mpls;
+};
+
+// SpfSolver constructor switches (SpfSolver.h:108-118) that shape the build
+struct RouteOptions {
+  bool nodeSegmentLabels = true;
+  bool adjacencyLabels = true;
+  bool ucmp = false;
 };
 
 struct MinCostNextHops {
   Metric shortest = 0;
-  // next-hop node -> distance from it to the closest announcer
-  std::unordered_map<std::string, Metric> viaNode;
+  // (next-hop node, destination or "" unless perDestination) -> distance
+  // from the next hop to the closest announcer
+  std::map<std::pair<std::string, std::string>, Metric> viaNode;
 };
 
 class SpfSolver {
  public:
   explicit SpfSolver(LinkState& ls) : ls_(ls) {}
 
-  // getNextHopsWithMetric(me, announcers, perDestination=false)
-  std::optional<MinCostNextHops> nextHopsWithMetric(const std::string& me,
-                                                    const std::vector<std::string>& announcers);
-  // SP_ECMP unicast route (empty: no route)
+  // getNextHopsWithMetric (SpfSolver.cpp:1043-1089)
+  MinCostNextHops nextHopsWithMetric(const std::string& me, const std::vector<std::string>& dsts,
+                                     bool perDestination);
+  // SP_ECMP unicast route from single-node IP announcers (empty: no route)
   std::vector<NextHop> ecmpRoute(const std::string& me, const std::vector<std::string>& announcers);
   // MPLS node-label route towards `dst` with its node label (PHP / SWAP)
   std::vector<NextHop> nodeLabelRoute(const std::string& me, const std::string& dst);
-  // KSP2_ED_ECMP route (SR-MPLS label stacks)
+  // KSP2_ED_ECMP route (SR-MPLS label stacks) over `announcers` (entries
+  // without prepend labels)
   std::vector<NextHop> ksp2Route(const std::string& me, const std::vector<std::string>& announcers);
+  // createRouteForPrefix (SpfSolver.cpp:197-458), one area, non-BGP
+  std::optional<UnicastRoute> prefixRoute(const std::string& me, const PrefixRoute& pr,
+                                          const RouteOptions& opt);
+  // SpfSolver::buildRouteDb (SpfSolver.cpp:460-646), one area: unicast routes
+  // of `prefixes`, MPLS node-label routes of every node (POP_AND_LOOKUP for
+  // our own label, PHP / SWAP towards the others, :501-598) and
+  // adjacency-label routes (PHP, :603-631). nullopt when `me` is not in the
+  // link state (:465-471). A duplicate MPLS label throws (the reference
+  // CHECK-fails, SpfSolver.h:92-97).
+  std::optional<RouteDb> buildRouteDb(const std::string& me, const std::vector<PrefixRoute>& prefixes,
+                                      const RouteOptions& opt = RouteOptions{});
+  // buildRouteDb for many nodes: one batched engine launch computes every
+  // SPF result the builds read (each `me` and, for node-label routes, the
+  // same roots), then the per-node builds run on the host.
+  std::vector<std::optional<RouteDb>> buildRouteDbs(const std::vector<std::string>& mes,
+                                                    const std::vector<PrefixRoute>& prefixes,
+                                                    const RouteOptions& opt = RouteOptions{});
 
  private:
-  std::vector<NextHop> expand(const std::string& me, const MinCostNextHops& m,
-                              const std::vector<std::string>& announcers,
-                              std::optional<int32_t> swapLabel);
+  // getNextHopsThrift (SpfSolver.cpp:1163-1285)
+  std::vector<NextHop> nextHopsThrift(const std::string& me, const std::vector<std::string>& dsts,
+                                      bool perDestination, const MinCostNextHops& m,
+                                      std::optional<int32_t> swapLabel,
+                                      const std::map<std::string, const PrefixEntry*>& entries,
+                                      const NodeUcmpResult* ucmp);
+  std::vector<NextHop> ksp2Paths(const std::string& me, const std::vector<std::string>& announcers,
+                                 const std::map<std::string, const PrefixEntry*>& entries);
   int32_t nodeLabel(const std::string& node) const;
   LinkState& ls_;
 };

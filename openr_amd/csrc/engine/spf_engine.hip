@@ -304,8 +304,17 @@ int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
     if ((size_t)chunk * per_root > cap)
       chunk = (uint32_t)std::max<size_t>(64, cap / per_root / 64 * 64);
   }
-  const uint32_t nb_max =
+  // merged rows (2..7 words, one per pass): every pass of a batch in the same
+  // round, all of a batch's passes on one XCD (nb a multiple of 8 * npass)
+  bool merged = defer && !ilv && npass > 1 && sh.PP == 1 && sh.OW == 1 && W <= 7 &&
+                (flags & (OSPF_WANT_NH | OSPF_WANT_DIGEST)) && !getenv("OSPF_MS_NOMERGE");
+  uint32_t nb_max =
       std::min<uint32_t>(nb_cap, ((std::min(chunk, b->n_roots) + sh.R - 1) / sh.R) * npass);
+  if (merged) {
+    const uint32_t unit = nb_max >= 8 * npass ? 8 * npass : npass;
+    nb_max = std::max(unit, nb_max / unit * unit);
+    merged = nb_max <= nb_cap || nb_max == npass;
+  }
   const size_t state_bytes = per_vb * nb_max;
   const size_t dist_bytes = dist_scr ? align_up((size_t)chunk * V * 4ull, 256) : 0;
   const size_t nh_bytes = (nh_scr || ilv) ? align_up((size_t)chunk * V * W * 4ull, 256) : 0;
@@ -329,6 +338,7 @@ int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
     a.kcap = kcap;
     a.push_div = push_div;
     a.defer = defer ? 1u : 0u;
+    a.merged = merged ? 1u : 0u;
     a.digest = (defer && dig) ? b->d_digest + r0 : nullptr;
     if (a.digest) HIPCHK(c, hipMemsetAsync(a.digest, 0, (size_t)n * sizeof(ospf_digest), s));
     a.err = c->d_err;
@@ -875,10 +885,23 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
     pew[2ull * e + 1] = pw[e] | (prw[e] << 16);
   }
   const size_t sz_ew = pew.size() * 4ull;
-  size_t off[12], tot = 0;
-  const size_t szs[12] = {sz_row, sz_e,     sz_e,  sz_e,   sz_e,  sz_nt,
-                          sz_dnoff, sz_dn, sz_big, sz_key, sz_le, sz_ew};
-  for (int i = 0; i < 12; ++i) {
+  // distinct-neighbour index per padded entry (rows are sorted by neighbour)
+  std::vector<uint16_t> didx(std::max<uint32_t>(Ep, 1), 0xFFFFu);
+  for (uint32_t u = 0; u < V; ++u) {
+    uint32_t k = 0, prev = 0xFFFFFFFFu;
+    for (uint32_t e = prow[u]; e < prow[u + 1]; ++e) {
+      const uint32_t v = pcolx[e] & 0x7FFFFFFFu;
+      if (plink[e] == 0xFFFFFFFFu || v == u) continue;  // padding, self-loop
+      if (prev != 0xFFFFFFFFu && v != prev) ++k;
+      prev = v;
+      didx[e] = (uint16_t)k;
+    }
+  }
+  const size_t sz_didx = didx.size() * 2ull;
+  size_t off[13], tot = 0;
+  const size_t szs[13] = {sz_row, sz_e,     sz_e,  sz_e,   sz_e,  sz_nt,  sz_dnoff,
+                          sz_dn,  sz_big,   sz_key, sz_le, sz_ew, sz_didx};
+  for (int i = 0; i < 13; ++i) {
     off[i] = tot;
     tot += align_up(std::max<size_t>(szs[i], 4), 256);
   }
@@ -894,10 +917,10 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
     return fail(c, OSPF_E_NOMEM, std::string("hipMalloc graph: ") + hipGetErrorString(he));
   }
   char* base = (char*)c->d_graph;
-  const void* srcs[12] = {prow.data(), pcolx.data(), pw.data(), prw.data(), plink.data(),
+  const void* srcs[13] = {prow.data(), pcolx.data(), pw.data(), prw.data(), plink.data(),
                           nt.data(), dn_off.data(), dn.data(), big.data(), dkey.data(),
-                          link_e.data(), pew.data()};
-  for (int i = 0; i < 12; ++i)
+                          link_e.data(), pew.data(), didx.data()};
+  for (int i = 0; i < 13; ++i)
     if (szs[i] && srcs[i]) HIPCHK(c, hipMemcpy(base + off[i], srcs[i], szs[i], hipMemcpyHostToDevice));
   c->g.V = V;
   c->g.E = Ep;
@@ -915,6 +938,7 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   c->g.n_lid = n_lid;
   c->g.link_e = (const uint32_t*)(base + off[10]);
   c->g.ew = ew_ok ? (const uint2*)(base + off[11]) : nullptr;
+  c->g.didx = (const uint16_t*)(base + off[12]);
   c->ew_base = ew_ok ? (const uint32_t*)(base + off[11]) : nullptr;
   c->h_row_ptr.assign(csr->row_ptr, csr->row_ptr + V + 1);
   c->h_dn_off = std::move(dn_off);

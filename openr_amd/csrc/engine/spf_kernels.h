@@ -43,6 +43,10 @@ struct DevGraph {
   // [E] {colx, w | rw << 16}: one 8-B load per entry for the weighted path
   // (null when a metric exceeds 0xFFFF: the separate arrays are read instead)
   const uint2* ew;
+  // [E] index of the entry's neighbour among the row node's distinct
+  // neighbours (= its next-hop bit when the row node is a root); 0xFFFF for
+  // self-loops and padding
+  const uint16_t* didx;
 };
 
 struct RunArgs {
@@ -171,6 +175,8 @@ struct MsArgs {
   uint8_t* lev;           // [nb][V][64]  dist + 1 per (node, root), 0 = unreached
                           //              (defer: rows are written once, at the end)
   uint32_t defer;         // 1: levels fill lev, msbfs_rows writes the rows
+  uint32_t merged;        // defer, 2..7 words, one per pass: one rows kernel for all
+                          //   passes of a batch (msbfs_rows_multi); pass 0 records lev
   ospf_digest* digest;    // [n] (defer: msbfs_rows adds each pass's terms; zeroed first)
   uint32_t* err;
   // KSP2 reruns (kp = 0: distances only, every root of a batch is the same

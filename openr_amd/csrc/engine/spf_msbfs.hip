@@ -159,8 +159,8 @@ __device__ __forceinline__ void set_lev(const MsArgs& a, const VB& b, uint32_t v
 template <int KP>
 __device__ __forceinline__ void emit_rows(const MsArgs& a, const VB& b, uint32_t v, uint64_t acc,
                                           const uint64_t* pacc, uint32_t dist) {
-  if (a.defer) {
-    if (acc) set_lev(a, b, v, acc, dist + 1u);
+  if (a.defer) {  // merged rows: the passes share the levels, pass 0 records them
+    if (acc && (!a.merged || b.g == 0)) set_lev(a, b, v, acc, dist + 1u);
     return;
   }
   uint64_t un = wave_or64(acc);
@@ -244,10 +244,11 @@ __global__ void __launch_bounds__(256) msbfs_init_kernel(DevGraph g, MsArgs a) {
   auto lev_or = [&](uint32_t v, uint32_t val) {  // byte `bit` of node v's record
     atomicOr(&lev32[(((size_t)vbl * V + v) * 64u + bit) / 4u], val << (8u * (bit & 3u)));
   };
+  const bool rec = !a.merged || b.g == 0;  // merged rows: pass 0 records the levels
   if (lane == 0) {
     or64(&b.seen[s], bm);
     if (a.defer) {
-      lev_or(s, 1u);
+      if (rec) lev_or(s, 1u);
     } else {
       if (a.dist && b.g == 0) a.dist[row + s] = 0u;
       if (a.nh) a.nh[(row + s) * a.W + b.g] = 0u;
@@ -261,12 +262,7 @@ __global__ void __launch_bounds__(256) msbfs_init_kernel(DevGraph g, MsArgs a) {
     if ((cx & kDown) || cx == s) continue;
     if (KP == 0 && ((b.ignored(e) >> bit) & 1ull)) continue;
     const uint32_t v = cx;
-    // index of v among s's distinct neighbours (ascending ids)
-    uint32_t lo = 0, hi = nn;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (g.dn[nb0 + mid] < v) lo = mid + 1; else hi = mid;
-    }
+    const uint32_t lo = g.didx[e];  // index of v among s's distinct neighbours
     // plane of v in this pass (>= KP * PP, wrapped, when outside it)
     const uint32_t li = lo - 32u * a.OW * b.g;
     const bool in = li < (uint32_t)KP * a.PP;
@@ -282,7 +278,7 @@ __global__ void __launch_bounds__(256) msbfs_init_kernel(DevGraph g, MsArgs a) {
     if (in) or64(&b.P[(size_t)v * KP + k], 1ull << pb);
     if (a.defer) {
       // parallel links: the same byte again, same value (an OR of 2 | 2 = 2)
-      lev_or(v, 2u);
+      if (rec) lev_or(v, 2u);
     } else {
       if (a.dist && b.g == 0) a.dist[row + v] = 1u;
       if (a.nh) a.nh[(row + v) * a.W + b.g] = (kw < 32u) ? (1u << kw) : 0u;
@@ -416,7 +412,7 @@ __global__ void __launch_bounds__(256) msbfs_level_kernel(DevGraph g, MsArgs a, 
       }
     }
     if (a.defer) {
-      if (lane == 0 && acc) set_lev(a, b, u, acc, d + 2u);
+      if (lane == 0 && acc && (!a.merged || b.g == 0)) set_lev(a, b, u, acc, d + 2u);
     } else if ((acc >> lane) & 1ull) {  // lane r writes root r's entries
       const size_t row = (size_t)(b.rix0 + lane) * V + u;
       if (a.dist && b.g == 0) a.dist[row] = d + 1;
@@ -680,6 +676,132 @@ __global__ void __launch_bounds__(256) msbfs_rows_kernel(DevGraph g, MsArgs a) {
   }
 }
 
+// Multi-pass batches (2..7 next-hop words, one word per pass): ONE rows
+// kernel per round for all passes of a batch, instead of one per pass that
+// writes its word into every W-word row entry (W partial writes per line,
+// each pass's lines written back separately). A block = (batch of the
+// round, 64 nodes): lev bytes once (the passes share the traversal; passes
+// g > 0 do not record them), then per half of the roots every pass's words
+// are assembled in LDS as [root][node][word] and each root's 64 x W words go
+// out as contiguous 16-B stores; dist rows and digests once.
+template <int KP>
+__global__ void __launch_bounds__(256) msbfs_rows_multi_kernel(DevGraph g, MsArgs a,
+                                                               uint32_t nbatch) {
+  __shared__ uint8_t s_lev[64 * 64];  // [node][root]
+  __shared__ uint64_t s_dk[64 * 2];
+  extern __shared__ uint32_t s_row[];  // [32 roots of the half][node][W words]
+  const uint32_t V = g.V, tid = threadIdx.x, W = a.W, np = a.npass;
+  const uint32_t bl = blockIdx.x % nbatch;
+  const uint32_t v0 = (blockIdx.x / nbatch) * 64u, nv = min(64u, V - v0);
+  const uint32_t nb8 = a.nb >> 3;
+  auto slot = [&](uint32_t t) {  // round position -> state slot (inverse of VB's map)
+    return (a.nb & 7u) == 0 ? (t % nb8) * 8u + t / nb8 : t;
+  };
+  const uint32_t vbl0 = slot(bl * np);
+  const uint32_t rix0 = (a.vb0 / np + bl) * a.R;
+  const uint32_t nr = min(a.R, a.n - rix0);
+  if (v0 == 0 && tid == 0 && a.found[vbl0 * a.lmax + a.dbound + 1]) atomicOr(a.err, 8u);
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(a.lev + ((size_t)vbl0 * V + v0) * 64u);
+    if (tid < nv * 4u) reinterpret_cast<uint4*>(s_lev)[tid] = src[tid];
+  }
+  if (a.digest && tid < 128u) s_dk[tid] = (v0 + tid / 2u < V) ? g.dkey[2ull * v0 + tid] : 0ull;
+  __syncthreads();
+  const bool vec = (V & 3u) == 0 && nv == 64u;
+  if (a.dist) {
+    for (uint32_t i = tid; i < 64u * 16u; i += kBlock) {  // (root, node quad)
+      const uint32_t r = i >> 4, q = i & 15u;
+      if (r >= nr) break;
+      uint32_t dv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t l = s_lev[(4u * q + j) * 64u + r];
+        dv[j] = l ? l - 1u : kInf;
+      }
+      uint32_t* row = a.dist + (size_t)(rix0 + r) * V + v0 + 4u * q;
+      if (vec) {
+        *reinterpret_cast<uint4*>(row) = make_uint4(dv[0], dv[1], dv[2], dv[3]);
+      } else {
+        for (uint32_t j = 0; j < 4u; ++j)
+          if (4u * q + j < nv) row[j] = dv[j];
+      }
+    }
+  }
+  // digest: root dr = tid / 4 over nodes 16 * (tid % 4) .. + 15
+  const uint32_t dr = tid >> 2, dn0 = 16u * (tid & 3u);
+  uint64_t reached = 0, sumd = 0, h = 0;
+  if (a.digest && dr < nr) {
+    for (uint32_t n = dn0; n < dn0 + 16u && n < nv; ++n) {
+      const uint32_t l = s_lev[n * 64u + dr];
+      if (!l) continue;
+      reached += 1;
+      sumd += l - 1u;
+      h += s_dk[2u * n] * (uint64_t)l;
+    }
+  }
+  const uint32_t pn = tid >> 2, pq = tid & 3u;  // node, 8-root group of the half
+  const uint32_t span = nv * W;                 // words of one root's slice
+  const bool vw = (((size_t)V * W) & 3u) == 0 && ((v0 * W) & 3u) == 0 && (span & 3u) == 0;
+  for (uint32_t h0 = 0; h0 < nr; h0 += 32u) {
+    for (uint32_t gp = 0; gp < W; ++gp) {
+      uint64_t p[KP];
+      const bool have = gp < np && pn < nv;
+      if (have) {
+        load_planes<KP>(a.planes + (size_t)slot(bl * np + gp) * V * KP, v0 + pn, p);
+      }
+#pragma unroll
+      for (uint32_t i = 0; i < 8u; ++i) {
+        const uint32_t rr = 8u * pq + i, r = h0 + rr;
+        if (pn >= nv || r >= nr) continue;
+        const uint32_t word = (have && s_lev[pn * 64u + r]) ? gather_word<KP>(p, r) : 0u;
+        s_row[(rr * 64u + pn) * W + gp] = word;
+      }
+    }
+    __syncthreads();
+    if (a.nh) {  // each root's nv * W words: contiguous in its row
+      const uint32_t nrh = min(32u, nr - h0);
+      if (vw) {
+        const uint32_t q4 = span / 4u;
+        for (uint32_t i = tid; i < nrh * q4; i += kBlock) {
+          const uint32_t rr = i / q4, k = i - rr * q4;
+          const uint32_t* src = &s_row[rr * 64u * W + 4u * k];
+          uint32_t* dst = a.nh + ((size_t)(rix0 + h0 + rr) * V + v0) * W + 4u * k;
+          *reinterpret_cast<uint4*>(dst) = make_uint4(src[0], src[1], src[2], src[3]);
+        }
+      } else {
+        for (uint32_t i = tid; i < nrh * span; i += kBlock) {
+          const uint32_t rr = i / span, k = i - rr * span;
+          a.nh[((size_t)(rix0 + h0 + rr) * V + v0) * W + k] = s_row[rr * 64u * W + k];
+        }
+      }
+    }
+    if (a.digest && dr >= h0 && dr < min(nr, h0 + 32u)) {
+      for (uint32_t n = dn0; n < dn0 + 16u && n < nv; ++n)
+        for (uint32_t gp = 0; gp < W; ++gp) {
+          const uint32_t word = s_row[((dr - h0) * 64u + n) * W + gp];
+          if (word) h += s_dk[2u * n + 1u] * digest_word_key(gp, word);
+        }
+    }
+    __syncthreads();
+  }
+  if (a.digest) {
+#pragma unroll
+    for (int o = 1; o < 4; o <<= 1) {
+      reached += shfl_xor64(reached, o);
+      sumd += shfl_xor64(sumd, o);
+      h += shfl_xor64(h, o);
+    }
+    if ((tid & 3u) == 0 && dr < nr) {
+      ospf_digest* dg = a.digest + rix0 + dr;
+      if (reached) {
+        atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)reached);
+        atomicAdd((unsigned long long*)&dg->sum_dist, (unsigned long long)sumd);
+      }
+      if (h) atomicAdd((unsigned long long*)&dg->hash, (unsigned long long)h);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- digest
 // Digest of finished rows (runs whose rows are written per level): `segs`
 // workgroups per root, each over a node range, adding into a zeroed record.
@@ -760,7 +882,10 @@ hipError_t launch_round_kp(const DevGraph& g, const MsArgs& a, uint32_t depth_bo
                        s, g, a, d);
     hipLaunchKernelGGL(msbfs_settle_kernel<KP>, dim3(a.nb * chunks), dim3(kBlock), 0, s, g, a, d);
   }
-  if (a.defer)
+  if (a.defer && a.merged)
+    hipLaunchKernelGGL(msbfs_rows_multi_kernel<KP>, dim3((a.nb / a.npass) * ((g.V + 63u) / 64u)),
+                       dim3(kBlock), 32u * 64u * a.W * 4u, s, g, a, a.nb / a.npass);
+  else if (a.defer)
     hipLaunchKernelGGL(msbfs_rows_kernel<KP>, dim3(a.nb * ((g.V + 63u) / 64u)), dim3(kBlock), 0, s,
                        g, a);
   else

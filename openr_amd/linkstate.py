@@ -117,6 +117,60 @@ class LinkState:
             out.add((ifn, int(metric), tuple(int(x) for x in labels.split(",") if x)))
         return out or None
 
+    def route_dbs(self, mes: Sequence[str], prefixes: Dict[str, Sequence],
+                  node_labels: bool = True, adj_labels: bool = True, ucmp: bool = False):
+        """SpfSolver::buildRouteDb (odl::SpfSolver, C++) for every node in
+        `mes`, over SPF results from one batched engine launch.
+
+        prefixes: {prefix: [entry, ...]}, entry = (node, fwd, algo, weight,
+        prepend) with fwd 'ip' | 'sr_mpls', algo 'ecmp' | 'ksp2' | 'ucmp_adj'
+        | 'ucmp_prefix', weight 0 = unset, prepend None or a label.
+        Returns {me: None | {"routes": {prefix: (igp_cost, weight|None)},
+        (kind, key): set of (ifName, neighbor, metric, op, labels, weight)}}
+        with kind 'U' (prefix) or 'M' (MPLS label) and op 'PHP' | 'SWAP' |
+        'PUSH' | 'POP' | ''."""
+        fwds = {"ip": 0, "sr_mpls": 1}
+        algos = {"ecmp": 0, "ksp2": 1, "ucmp_adj": 2, "ucmp_prefix": 3}
+        lines = []
+        for p, ents in prefixes.items():
+            es = []
+            for (node, fwd, algo, weight, prepend) in ents:
+                es.append(f"{node}:{fwds[fwd]}:{algos[algo]}:{int(weight)}:"
+                          f"{'' if prepend is None else int(prepend)}")
+            lines.append(f"{p}\t{','.join(es)}")
+        flags = int(node_labels) | (2 if adj_labels else 0) | (4 if ucmp else 0)
+        t = self._take(self._L.odl_route_db_text(
+            self._h, "\n".join(mes).encode(), len(mes), "\n".join(lines).encode(),
+            len(lines), flags))
+        ops = {"0": "", "1": "PHP", "2": "SWAP", "3": "PUSH", "4": "POP"}
+        out = {me: {"routes": {}} for me in mes}
+        for ln in t.splitlines():
+            f = ln.split("\t")
+            me, kind = f[0], f[1]
+            if kind == "NONE":
+                out[me] = None
+            elif kind == "R":
+                out[me]["routes"][f[2]] = (int(f[3]), None if f[4] == "-" else int(f[4]))
+            else:
+                key, ifn, nbr, metric, op, labels, w = f[2:]
+                out[me].setdefault((kind, key), set()).add(
+                    (ifn, nbr, int(metric), ops[op],
+                     tuple(int(x) for x in labels.split(",") if x), int(w)))
+        return out
+
+    @staticmethod
+    def path_a_in_b(a: Sequence[str], b: Sequence[str]) -> bool:
+        """LinkState::pathAInPathB (LinkState.h:477-492) in C++ over link keys."""
+        L = N.decision()
+        r = L.odl_path_a_in_b("\n".join(a).encode(), len(a), "\n".join(b).encode(), len(b))
+        if r < 0:
+            raise ValueError(f"malformed link key in {a} / {b}")
+        return bool(r)
+
+    def route_db(self, me: str, prefixes: Dict[str, Sequence], **kw):
+        """route_dbs for one node."""
+        return self.route_dbs([me], prefixes, **kw)[me]
+
     def ucmp(self, root: str, leaves: Dict[str, int], algo: str = "adj",
              use_link_metric: bool = True):
         """resolveUcmpWeights(getSpfResult(root), leaves, algo) (C++ over the

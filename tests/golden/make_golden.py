@@ -361,11 +361,293 @@ def grid_dbs(n):
     return out
 
 
+def grid_prefix(node):
+    """nodeToPrefixV6 (DecisionTest.cpp:4595-4598)."""
+    return f"::ffff:10.1.{node // 256}.{node % 256}/128"
+
+
 for n in range(2, 17, 2):
     fixtures.append(dict(
         name=f"decision_grid_{n}",
         source="openr/decision/tests/DecisionTest.cpp:4552-4713",
-        steps=[dict(dbs=grid_dbs(n), checks=[dict(kind="grid_manhattan", n=n)])]))
+        steps=[dict(dbs=grid_dbs(n), checks=[
+            dict(kind="grid_manhattan", n=n),
+            # ShortestPathTest (:4668-4713): 2n^4 + 3n^2 - 4n routes, corner
+            # to corner metrics = Manhattan distance
+            dict(kind="route_map", nodes=[str(i) for i in range(n * n)],
+                 prefixes={grid_prefix(i): [[str(i), "ip", "ecmp", 0, None]]
+                           for i in range(n * n)},
+                 expect_size=2 * n ** 4 + 3 * n ** 2 - 4 * n,
+                 expect_metric={f"0|U|{grid_prefix(n * n - 1)}": 2 * (n - 1),
+                                f"{n - 1}|U|{grid_prefix(n * (n - 1))}": 2 * (n - 1)}),
+        ])]))
+
+
+# ---------------------------------------------------------------------------
+# Route-DB fixtures: SpfSolver::buildRouteDb over the link state. A check
+# "route_map" lists the nodes whose route DBs the reference's getRouteMap
+# (DecisionTest.cpp:311-329) collects, the prefix entries, and the reference's
+# assertions: the map size (one key per (node, prefix | label)), exact next-hop
+# sets (validatePopLabelRoute / validateAdjLabelRoutes :363-386 included) and
+# per-node route counts. Next hop = [ifName, neighbor, metric, mpls action,
+# labels, ucmp weight] (createNextHopFromAdj :234-252; the address field is
+# the adjacency's, not modelled).
+def H(ifn, nbr, metric, op="", labels=(), w=0):
+    return [ifn, str(nbr), metric, op, list(labels), w]
+
+
+POP = ["", "", 0, "POP", [], 0]  # labelPopNextHop (DecisionTest.cpp:161-166)
+ADDR = {1: "::ffff:10.1.1.1/128", 2: "::ffff:10.2.2.2/128", 3: "::ffff:10.3.3.3/128",
+        4: "::ffff:10.4.4.4/128"}  # addr1..addr4 (DecisionTest.cpp:108-111)
+
+
+def loopbacks(nodes):
+    """prefixDb1..4 (DecisionTest.cpp:137-140): createPrefixEntry(addrN),
+    forwarding IP / SP_ECMP (the thrift defaults)."""
+    return {ADDR[n]: [[str(n), "ip", "ecmp", 0, None]] for n in nodes}
+
+
+def route_map(nodes, prefixes, **kw):
+    return dict(kind="route_map", nodes=[str(n) for n in nodes], prefixes=prefixes, **kw)
+
+
+def adj_routes(node, adjs):
+    """validateAdjLabelRoutes (DecisionTest.cpp:363-377)."""
+    return {f"{node}|M|{a['label']}": [H(a["if_name"], a["other"], a["metric"], "PHP")]
+            for a in adjs}
+
+
+# ShortestPathTest.* (DecisionTest.cpp:473-609)
+fixtures.append(dict(
+    name="decision_route_unreachable_nodes",
+    source="openr/decision/tests/DecisionTest.cpp:473-505",
+    steps=[dict(dbs=[db(1, [], 0), db(2, [], 0)],
+                expect_changes=[[False, None, None, None], [False, None, None, None]],
+                checks=[route_map([1, 2], loopbacks([1, 2]),
+                                  expect_counts={"1": [0, 0], "2": [0, 0]})])]))
+fixtures.append(dict(
+    name="decision_route_missing_neighbor_adjdb",
+    source="openr/decision/tests/DecisionTest.cpp:512-541",
+    steps=[dict(dbs=[db(1, [dadj(1, 2)], 0)], expect_changes=[[False, None, None, None]],
+                checks=[route_map([1], loopbacks([1, 2]), expect_counts={"1": [0, 0]})])]))
+fixtures.append(dict(
+    name="decision_route_empty_neighbor_adjdb",
+    source="openr/decision/tests/DecisionTest.cpp:549-586",
+    steps=[dict(dbs=[db(1, [dadj(1, 2)], 0), db(2, [], 0)],
+                expect_changes=[[False, None, None, None], [False, None, None, None]],
+                checks=[route_map([1, 2], loopbacks([1, 2]),
+                                  expect_counts={"1": [0, None], "2": [0, None]})])]))
+fixtures.append(dict(
+    name="decision_route_unknown_node",
+    source="openr/decision/tests/DecisionTest.cpp:591-609",
+    steps=[dict(dbs=[], checks=[route_map([1, 2], {}, expect_counts={"1": None, "2": None})])]))
+
+# SpfSolver.AdjacencyUpdate (DecisionTest.cpp:614-759). The next-hop address
+# updates (:664-718) change a field this path does not model and are left out.
+_au12 = adj("2", "1/2", "2/1", 10, 111)
+_au21 = adj("1", "2/1", "1/2", 10, 222)
+fixtures.append(dict(
+    name="decision_spf_solver_adjacency_update",
+    source="openr/decision/tests/DecisionTest.cpp:614-759",
+    steps=[
+        dict(dbs=[db(1, [dadj(1, 2)], 1)], expect_changes=[[False, None, True, None]]),
+        dict(dbs=[db(2, [dadj(2, 1)], 2)], expect_changes=[[True, None, True, None]],
+             checks=[route_map([1, 2], loopbacks([1, 2]),
+                               expect_counts={"1": [1, 3], "2": [1, 3]})]),
+        dict(dbs=[db(1, [_au12], 1)], expect_changes=[[False, True, None, None]]),
+        dict(dbs=[db(2, [_au21], 2)], expect_changes=[[False, True, None, None]]),
+        dict(dbs=[db(1, [_au12], 11)], expect_changes=[[False, False, True, None]]),
+        dict(dbs=[db(2, [_au21], 22)], expect_changes=[[False, False, True, None]]),
+    ]))
+
+# MplsRoutes.BasicTest (DecisionTest.cpp:765-812): 1 -> 2 not bidirectional,
+# 2 <-> 3; node 2 has no node label
+_m1 = db(1, [dadj(1, 2)], 1)
+fixtures.append(dict(
+    name="decision_mpls_routes_basic",
+    source="openr/decision/tests/DecisionTest.cpp:765-812",
+    steps=[dict(
+        dbs=[_m1, _m1, db(2, [dadj(2, 3)], 0), db(3, [dadj(3, 2)], 3)],
+        expect_changes=[[False, False, True, None], [False, False, False, None],
+                        [False, False, False, None], [True, False, True, None]],
+        checks=[route_map([1, 2, 3], {}, expect_size=5, expect={
+            "1|M|1": [POP],
+            "2|M|100003": [H("2/3", 3, 10, "PHP")],
+            "3|M|3": [POP],
+            "3|M|100002": [H("3/2", 2, 10, "PHP")]})])]))
+
+# SimpleRingTopologyFixture.OverloadNodeTest (DecisionTest.cpp:3115-3234)
+ring_pfx = loopbacks([1, 2, 3, 4])
+fixtures.append(dict(
+    name="decision_simple_ring_overload_node_routes",
+    source="openr/decision/tests/DecisionTest.cpp:3115-3234",
+    steps=[
+        dict(dbs=ring, expect_changes=ring_changes),
+        dict(dbs=[db(2, [dadj(2, 1), dadj(2, 4)], 2, overloaded=True),
+                  db(3, [dadj(3, 1), dadj(3, 4)], 3, overloaded=True)],
+             expect_changes=[[True, None, None, None], [True, None, None, None]],
+             checks=[route_map([1, 2, 3, 4], ring_pfx, expect_size=32, expect={
+                 f"1|U|{ADDR[3]}": [H("1/3", 3, 10)], "1|M|3": [H("1/3", 3, 10, "PHP")],
+                 f"1|U|{ADDR[2]}": [H("1/2", 2, 10)], "1|M|2": [H("1/2", 2, 10, "PHP")],
+                 "1|M|1": [POP], **adj_routes(1, ring[0]["adjs"]),
+                 f"2|U|{ADDR[4]}": [H("2/4", 4, 10)], "2|M|4": [H("2/4", 4, 10, "PHP")],
+                 f"2|U|{ADDR[3]}": [H("2/1", 1, 20), H("2/4", 4, 20)],
+                 "2|M|3": [H("2/1", 1, 20, "SWAP", [3]), H("2/4", 4, 20, "SWAP", [3])],
+                 f"2|U|{ADDR[1]}": [H("2/1", 1, 10)], "2|M|1": [H("2/1", 1, 10, "PHP")],
+                 "2|M|2": [POP], **adj_routes(2, ring[1]["adjs"]),
+                 f"3|U|{ADDR[4]}": [H("3/4", 4, 10)], "3|M|4": [H("3/4", 4, 10, "PHP")],
+                 f"3|U|{ADDR[2]}": [H("3/1", 1, 20), H("3/4", 4, 20)],
+                 "3|M|2": [H("3/1", 1, 20, "SWAP", [2]), H("3/4", 4, 20, "SWAP", [2])],
+                 f"3|U|{ADDR[1]}": [H("3/1", 1, 10)], "3|M|1": [H("3/1", 1, 10, "PHP")],
+                 "3|M|3": [POP], **adj_routes(3, ring[2]["adjs"]),
+                 f"4|U|{ADDR[3]}": [H("4/3", 3, 10)], "4|M|3": [H("4/3", 3, 10, "PHP")],
+                 f"4|U|{ADDR[2]}": [H("4/2", 2, 10)], "4|M|2": [H("4/2", 2, 10, "PHP")],
+                 "4|M|4": [POP], **adj_routes(4, ring[3]["adjs"])})]),
+    ]))
+
+# SimpleRingTopologyFixture.OverloadLinkTest (DecisionTest.cpp:3240-3427)
+_r3a = db(3, [dadj(3, 1, overloaded=True), dadj(3, 4)], 3)
+_r3b = db(3, [dadj(3, 1, overloaded=True), dadj(3, 4, overloaded=True)], 3)
+fixtures.append(dict(
+    name="decision_simple_ring_overload_link_routes",
+    source="openr/decision/tests/DecisionTest.cpp:3240-3427",
+    steps=[
+        dict(dbs=ring, expect_changes=ring_changes),
+        dict(dbs=[_r3a], expect_changes=[[True, None, None, None]],
+             checks=[route_map([1, 2, 3, 4], ring_pfx, expect_size=36, expect={
+                 f"1|U|{ADDR[4]}": [H("1/2", 2, 20)], "1|M|4": [H("1/2", 2, 20, "SWAP", [4])],
+                 f"1|U|{ADDR[3]}": [H("1/2", 2, 30)], "1|M|3": [H("1/2", 2, 30, "SWAP", [3])],
+                 f"1|U|{ADDR[2]}": [H("1/2", 2, 10)], "1|M|2": [H("1/2", 2, 10, "PHP")],
+                 "1|M|1": [POP], **adj_routes(1, ring[0]["adjs"]),
+                 f"2|U|{ADDR[4]}": [H("2/4", 4, 10)], "2|M|4": [H("2/4", 4, 10, "PHP")],
+                 f"2|U|{ADDR[3]}": [H("2/4", 4, 20)], "2|M|3": [H("2/4", 4, 20, "SWAP", [3])],
+                 f"2|U|{ADDR[1]}": [H("2/1", 1, 10)], "2|M|1": [H("2/1", 1, 10, "PHP")],
+                 "2|M|2": [POP], **adj_routes(2, ring[1]["adjs"]),
+                 f"3|U|{ADDR[4]}": [H("3/4", 4, 10)], "3|M|4": [H("3/4", 4, 10, "PHP")],
+                 f"3|U|{ADDR[2]}": [H("3/4", 4, 20)], "3|M|2": [H("3/4", 4, 20, "SWAP", [2])],
+                 f"3|U|{ADDR[1]}": [H("3/4", 4, 30)], "3|M|1": [H("3/4", 4, 30, "SWAP", [1])],
+                 "3|M|3": [POP], **adj_routes(3, _r3a["adjs"]),
+                 f"4|U|{ADDR[3]}": [H("4/3", 3, 10)], "4|M|3": [H("4/3", 3, 10, "PHP")],
+                 f"4|U|{ADDR[2]}": [H("4/2", 2, 10)], "4|M|2": [H("4/2", 2, 10, "PHP")],
+                 f"4|U|{ADDR[1]}": [H("4/2", 2, 20)], "4|M|1": [H("4/2", 2, 20, "SWAP", [1])],
+                 "4|M|4": [POP], **adj_routes(4, ring[3]["adjs"])})]),
+        dict(dbs=[_r3b], expect_changes=[[True, None, None, None]],
+             checks=[route_map([1, 2, 3, 4], ring_pfx, expect_size=24, expect={
+                 f"1|U|{ADDR[4]}": [H("1/2", 2, 20)], "1|M|4": [H("1/2", 2, 20, "SWAP", [4])],
+                 f"1|U|{ADDR[2]}": [H("1/2", 2, 10)], "1|M|2": [H("1/2", 2, 10, "PHP")],
+                 "1|M|1": [POP], **adj_routes(1, ring[0]["adjs"]),
+                 f"2|U|{ADDR[4]}": [H("2/4", 4, 10)], "2|M|4": [H("2/4", 4, 10, "PHP")],
+                 f"2|U|{ADDR[1]}": [H("2/1", 1, 10)], "2|M|1": [H("2/1", 1, 10, "PHP")],
+                 "2|M|2": [POP], **adj_routes(2, ring[1]["adjs"]),
+                 "3|M|3": [POP], **adj_routes(3, _r3b["adjs"]),
+                 f"4|U|{ADDR[2]}": [H("4/2", 2, 10)], "4|M|2": [H("4/2", 2, 10, "PHP")],
+                 f"4|U|{ADDR[1]}": [H("4/2", 2, 20)], "4|M|1": [H("4/2", 2, 20, "SWAP", [1])],
+                 "4|M|4": [POP], **adj_routes(4, ring[3]["adjs"])})]),
+    ]))
+
+# ParallelAdjRingTopologyFixture.ShortestPathTest (DecisionTest.cpp:3573-3706)
+def _sw(hops, lbl):
+    return [h[:3] + (["PHP", [], 0] if lbl is None else ["SWAP", [lbl], 0]) for h in hops]
+
+
+_p1_4 = [H("2/2", 2, 22), H("3/1", 3, 22), H("2/1", 2, 22)]
+_p2_3 = [H("1/2", 1, 22), H("1/1", 1, 22), H("4/1", 4, 22)]
+_p3_2 = [H("1/1", 1, 22), H("4/1", 4, 22)]
+_p4_1 = [H("2/1", 2, 22), H("3/1", 3, 22)]
+fixtures.append(dict(
+    name="decision_parallel_adj_ring_shortest_path_routes",
+    source="openr/decision/tests/DecisionTest.cpp:3573-3706",
+    steps=[dict(
+        dbs=pr, expect_changes=[[False, None, None, None], [True, None, None, None],
+                                [True, None, None, None], [True, None, None, None]],
+        checks=[route_map([1, 2, 3, 4], ring_pfx, expect_size=44, expect={
+            f"1|U|{ADDR[4]}": _p1_4, "1|M|4": _sw(_p1_4, 4),
+            f"1|U|{ADDR[3]}": [H("3/1", 3, 11)], "1|M|3": [H("3/1", 3, 11, "PHP")],
+            f"1|U|{ADDR[2]}": [H("2/2", 2, 11), H("2/1", 2, 11)],
+            "1|M|2": _sw([H("2/2", 2, 11), H("2/1", 2, 11)], None),
+            "1|M|1": [POP], **adj_routes(1, pr[0]["adjs"]),
+            f"2|U|{ADDR[4]}": [H("4/1", 4, 11)], "2|M|4": [H("4/1", 4, 11, "PHP")],
+            f"2|U|{ADDR[3]}": _p2_3, "2|M|3": _sw(_p2_3, 3),
+            f"2|U|{ADDR[1]}": [H("1/2", 1, 11), H("1/1", 1, 11)],
+            "2|M|1": _sw([H("1/2", 1, 11), H("1/1", 1, 11)], None),
+            "2|M|2": [POP], **adj_routes(2, pr[1]["adjs"]),
+            f"3|U|{ADDR[4]}": [H("4/1", 4, 11)], "3|M|4": [H("4/1", 4, 11, "PHP")],
+            f"3|U|{ADDR[2]}": _p3_2, "3|M|2": _sw(_p3_2, 2),
+            f"3|U|{ADDR[1]}": [H("1/1", 1, 11)], "3|M|1": [H("1/1", 1, 11, "PHP")],
+            "3|M|3": [POP], **adj_routes(3, pr[2]["adjs"]),
+            f"4|U|{ADDR[3]}": [H("3/1", 3, 11)], "4|M|3": [H("3/1", 3, 11, "PHP")],
+            f"4|U|{ADDR[2]}": [H("2/1", 2, 11)], "4|M|2": [H("2/1", 2, 11, "PHP")],
+            f"4|U|{ADDR[1]}": _p4_1, "4|M|1": _sw(_p4_1, 1),
+            "4|M|4": [POP], **adj_routes(4, pr[3]["adjs"])})])]))
+
+# DecisionTest.Ucmp (DecisionTest.cpp:7861-8130): UCMP on, node/adjacency
+# labels off; adjacencies metric 10, adj label 0, weight 100e9
+G = 10 ** 9
+
+
+def uadj(me, other):
+    return adj(str(other), f"{me}/{other}", f"{other}/{me}", 10, 0, weight=100 * G)
+
+
+_utree = {1: [2, 3], 2: [1, 4, 5], 3: [1, 6], 4: [2], 5: [2], 6: [3]}
+_udbs = [db(n, [uadj(n, o) for o in nb], n) for n, nb in _utree.items()]
+_dflt = "::/0"
+_uopts = dict(ucmp=True, node_labels=False, adj_labels=False)
+
+
+def _ue(node, algo, w):
+    return [str(node), "ip", algo, w, None]
+
+
+fixtures.append(dict(
+    name="decision_ucmp_routes",
+    source="openr/decision/tests/DecisionTest.cpp:7861-8130",
+    steps=[dict(dbs=_udbs, checks=[
+        # Test 1 (:7923-8013): all SP_UCMP_PREFIX_WEIGHT_PROPAGATION
+        route_map([1, 2, 3], {_dflt: [_ue(4, "ucmp_prefix", 200 * G),
+                                      _ue(5, "ucmp_prefix", 100 * G),
+                                      _ue(6, "ucmp_prefix", 100 * G)]}, opts=_uopts,
+                  expect_counts={"1": [1, 0], "2": [1, 0], "3": [1, 0]},
+                  expect_weight={f"1|{_dflt}": 400 * G, f"2|{_dflt}": 300 * G,
+                                 f"3|{_dflt}": 100 * G},
+                  expect={f"1|U|{_dflt}": [H("1/2", 2, 20, w=3), H("1/3", 3, 20, w=1)],
+                          f"2|U|{_dflt}": [H("2/4", 4, 10, w=2), H("2/5", 5, 10, w=1)],
+                          f"3|U|{_dflt}": [H("3/6", 6, 10, w=1)]}),
+        # Test 2 (:8015-8071): node 6 SP_UCMP_ADJ_WEIGHT_PROPAGATION
+        route_map([1, 2, 3], {_dflt: [_ue(4, "ucmp_prefix", 200 * G),
+                                      _ue(5, "ucmp_prefix", 100 * G),
+                                      _ue(6, "ucmp_adj", 100 * G)]}, opts=_uopts,
+                  expect_counts={"1": [1, 0], "2": [1, 0], "3": [1, 0]},
+                  expect_weight={f"1|{_dflt}": 200 * G, f"2|{_dflt}": 200 * G,
+                                 f"3|{_dflt}": 100 * G},
+                  expect={f"1|U|{_dflt}": [H("1/2", 2, 20, w=2), H("1/3", 3, 20, w=1)],
+                          f"2|U|{_dflt}": [H("2/4", 4, 10, w=2), H("2/5", 5, 10, w=1)],
+                          f"3|U|{_dflt}": [H("3/6", 6, 10, w=1)]}),
+        # Test 3 (:8073-8129): node 6 without a weight
+        route_map([1, 2, 3], {_dflt: [_ue(4, "ucmp_prefix", 200 * G),
+                                      _ue(5, "ucmp_prefix", 100 * G),
+                                      _ue(6, "ucmp_prefix", 0)]}, opts=_uopts,
+                  expect_counts={"1": [1, 0], "2": [1, 0], "3": [1, 0]},
+                  expect_weight={f"1|{_dflt}": None, f"2|{_dflt}": 300 * G,
+                                 f"3|{_dflt}": None},
+                  expect={f"1|U|{_dflt}": [H("1/2", 2, 20), H("1/3", 3, 20)],
+                          f"2|U|{_dflt}": [H("2/4", 4, 10, w=2), H("2/5", 5, 10, w=1)],
+                          f"3|U|{_dflt}": [H("3/6", 6, 10)]}),
+    ])]))
+
+# LinkStateTest.pathAInPathB (LinkStateTest.cpp:211-254)
+_l1, _l2, _l3 = "1%1/2|2%2/1", "2%2/3|3%3/2", "1%1/3|3%3/1"
+fixtures.append(dict(
+    name="linkstate_path_a_in_path_b",
+    source="openr/decision/tests/LinkStateTest.cpp:211-254",
+    steps=[dict(dbs=[], checks=[dict(kind="path_in", cases=[
+        [[], [], True], [[], [], True],
+        [[_l1], [], False], [[], [_l1], True],
+        [[_l1], [_l1], True], [[_l1], [_l1], True],
+        [[_l1, _l2], [_l1], False], [[_l1], [_l1, _l2], True],
+        [[_l1, _l2, _l3], [_l1, _l2], False], [[_l1, _l2], [_l1, _l2, _l3], True],
+        [[_l3, _l2], [_l1], False], [[_l1], [_l3, _l2], False],
+    ])])]))
 
 
 def main():

@@ -21,7 +21,7 @@ from __future__ import annotations
 import glob
 import json
 import os
-from typing import Dict, List, Optional
+from typing import Callable, Dict, List, Optional
 
 from openr_amd.adjdb import AdjDb, AdjDbStream, Adjacency
 
@@ -110,6 +110,253 @@ def ksp2_routes(ls, src: str, dst: str, labels: Dict[str, int],
     return out or None
 
 
+def i32(m: int) -> int:
+    """createNextHop's int32 metric (LsdbUtil.cpp:658-675): low 32 bits."""
+    return ((m + 2 ** 31) % 2 ** 32) - 2 ** 31
+
+
+def valid_label(lbl: int) -> bool:
+    """isMplsLabelValid (MplsUtil.h:19-22)."""
+    return (lbl & 0xfff00000) == 0 and lbl != 0
+
+
+class RouteBuilder:
+    """Test-side restatement of SpfSolver::buildRouteDb (SpfSolver.cpp:460-646)
+    for one area, over any LinkState-like object plus the current adjacency
+    databases (node labels, adjacency labels). Mirrors, line by line:
+    createRouteForPrefix :197-458 (reachable announcers, drained filter
+    :709-731, self-origination :333-337, forwarding type/algorithm = min over
+    best entries LsdbUtil.cpp:379-413), selectBestPathsSpf :772-845,
+    getNextHopsWithMetric :1043-1089, getNodeUcmpResult :1091-1161,
+    getNextHopsThrift :1163-1285, selectBestPathsKsp2 :847-973.
+    Next hop = (ifName, neighbor, metric i32, op, labels, weight)."""
+
+    def __init__(self, ls, dbs: Dict[str, dict], ucmp: bool = False,
+                 node_labels: bool = True, adj_labels: bool = True):
+        self.ls, self.dbs, self.ucmp = ls, dbs, ucmp
+        self.node_labels, self.adj_labels = node_labels, adj_labels
+        self._spf = {}
+
+    def spf(self, me):
+        if me not in self._spf:
+            self._spf[me] = self.ls.spf(me)
+        return self._spf[me]
+
+    def label(self, node) -> int:
+        return self.dbs[node]["node_label"] if node in self.dbs else 0
+
+    def adj_label(self, me, key) -> int:
+        ifn, other = if_from(key, me), other_of(key, me)
+        for a in self.dbs[me]["adjs"]:
+            if a["if_name"] == ifn and a["other"] == other:
+                return a["label"]
+        return 0
+
+    def with_metric(self, me, dsts, per_dst):
+        res = self.spf(me)
+        shortest, closest = None, []
+        for d in dsts:
+            if d not in res:
+                continue
+            m = res[d][0]
+            if shortest is None or m < shortest:
+                shortest, closest = m, []
+            if m == shortest:
+                closest.append(d)
+        via = {}
+        for d in closest:
+            for nh in res[d][1]:
+                via[(nh, d if per_dst else "")] = shortest - res[nh][0]
+        return shortest, via
+
+    def next_hops(self, me, dsts, per_dst, shortest, via, swap=None, entries=None,
+                  ucmp_hops=None):
+        out = set()
+        dset = set(dsts)
+        for key, metric, up in self.ls.links(me):
+            nbr = other_of(key, me)
+            for dst in (sorted(dset) if per_dst else [""]):
+                if (nbr, dst) not in via or not up:
+                    continue
+                if dst and nbr in dset and nbr != dst:
+                    continue
+                over = metric + via[(nbr, dst)]
+                if over != shortest:
+                    continue
+                op, labels = "", ()
+                if swap is not None:
+                    op, labels = ("PHP", ()) if nbr in dset else ("SWAP", (swap,))
+                if dst:
+                    push, ok = [], True
+                    pl = entries[dst][4]
+                    if pl is not None:
+                        push.append(pl)
+                        ok &= valid_label(pl)
+                    if dst != nbr:
+                        push.append(self.label(dst))
+                        ok &= valid_label(push[-1])
+                    if not ok:
+                        continue
+                    if push:
+                        op, labels = "PUSH", tuple(push)
+                ifn = if_from(key, me)
+                w = 0
+                if ucmp_hops is not None and ifn in ucmp_hops:
+                    w = ucmp_hops[ifn][1]
+                out.add((ifn, nbr, i32(over), op, labels, w))
+        return out
+
+    def ksp2(self, me, best, entries):
+        paths = []
+        for n in best:
+            if n != me:
+                paths += self.ls.kth_paths(me, n, 1)
+        first = len(paths)
+        for n in best:
+            for p in self.ls.kth_paths(me, n, 2):
+                if not any(path_in(paths[i], p) for i in range(first)):
+                    paths.append(p)
+        out = set()
+        for p in paths:
+            cost, node, lbl, ok = 0, me, [], True
+            for key in p:
+                cost += next(m for k, m, _ in self.ls.links(node) if k == key)
+                node = other_of(key, node)
+                lbl.insert(0, self.label(node))
+                ok &= valid_label(lbl[0])
+            if not ok:
+                continue
+            lbl.pop()
+            if node in entries and entries[node][4] is not None:
+                lbl.insert(0, entries[node][4])
+            out.add((if_from(p[0], me), other_of(p[0], me), i32(cost),
+                     "PUSH" if lbl else "", tuple(lbl), 0))
+        return out
+
+    def prefix_route(self, me, ents):
+        res = self.spf(me)
+        entries = {e[0]: e for e in ents if e[0] in res}
+        if not entries:
+            return None
+        self_prepend = entries[me][4] is not None if me in entries else True
+        best = sorted(n for n in entries if not self.ls.is_overloaded(n)) or sorted(entries)
+        if me in best and not self_prepend:
+            return None
+        fwd = min({"ip": 0, "sr_mpls": 1}[entries[n][1]] for n in best)
+        algo = min({"ecmp": 0, "ksp2": 1, "ucmp_adj": 2, "ucmp_prefix": 3}[entries[n][2]]
+                   for n in best)
+        shortest, weight = 2 ** 64 - 1, None
+        if algo == 1:
+            nhs = self.ksp2(me, best, entries) if fwd == 1 else set()
+        else:
+            per_dst = fwd == 1
+            filt = [n for n in best
+                    if not (n == me and per_dst and entries[me][4] is not None)]
+            shortest, via = self.with_metric(me, filt, per_dst)
+            if shortest is None:
+                shortest = 2 ** 64 - 1
+            nhs = set()
+            if via:
+                hops = None
+                if self.ucmp and algo in (2, 3):
+                    leaves, ok = {}, True
+                    for n in best:
+                        if n not in res or res[n][0] != shortest:
+                            continue
+                        if not entries[n][3]:
+                            ok = False
+                            break
+                        leaves[n] = entries[n][3]
+                    if ok:
+                        u = self.ls.ucmp(me, leaves, "adj" if algo == 2 else "prefix")
+                        if me in u:
+                            weight, hops = u[me]
+                nhs = self.next_hops(me, best, per_dst, shortest, via, entries=entries,
+                                     ucmp_hops=hops)
+        if not nhs:
+            return None
+        return (shortest % 2 ** 32, weight), nhs
+
+    def build(self, me, prefixes):
+        if me not in self.dbs:
+            return None
+        out = {"routes": {}}
+        for p, ents in prefixes.items():
+            r = self.prefix_route(me, ents)
+            if r is not None:
+                out["routes"][p] = r[0]
+                out[("U", p)] = r[1]
+        if self.node_labels:
+            label_to = {}
+            for node in sorted(self.dbs):
+                top = self.dbs[node]["node_label"]
+                if top == 0 or not valid_label(top):
+                    continue
+                if top in label_to and label_to[top][0] < node:
+                    continue
+                if node == me:
+                    label_to[top] = (me, {("", "", 0, "POP", (), 0)})
+                    continue
+                shortest, via = self.with_metric(me, [node], False)
+                if not via:
+                    continue
+                label_to[top] = (node, self.next_hops(me, [node], False, shortest, via,
+                                                      swap=top))
+            for top, (_, nhs) in label_to.items():
+                out[("M", str(top))] = nhs
+        if self.adj_labels:
+            for key, metric, _ in self.ls.links(me):
+                top = self.adj_label(me, key)
+                if top == 0 or not valid_label(top):
+                    continue
+                assert ("M", str(top)) not in out, f"duplicate MPLS label {top}"
+                out[("M", str(top))] = {(if_from(key, me), other_of(key, me), i32(metric),
+                                         "PHP", (), 0)}
+        return out
+
+
+def _hop_set(expect):
+    return {(h[0], h[1], h[2], h[3], tuple(h[4]), h[5]) for h in expect}
+
+
+def check_route_map(c, dbs_of: Callable[[str], dict], where: str):
+    """Assert one route_map check against {node: route db | None}."""
+    n_routes = 0
+    for node in c["nodes"]:
+        db = dbs_of(node)
+        exp = c.get("expect_counts", {}).get(node, "skip")
+        if exp is None:
+            assert db is None, f"{where}: {node} expected no route db"
+        if db is None:
+            assert exp in (None, "skip"), f"{where}: {node} has no route db"
+            continue
+        n_u = sum(1 for k in db if k[0] == "U")
+        n_m = sum(1 for k in db if k[0] == "M")
+        n_routes += n_u + n_m
+        if exp not in (None, "skip"):
+            if exp[0] is not None:
+                assert n_u == exp[0], f"{where}: {node} unicast {n_u} != {exp[0]}"
+            if exp[1] is not None:
+                assert n_m == exp[1], f"{where}: {node} mpls {n_m} != {exp[1]}"
+    if "expect_size" in c:
+        assert n_routes == c["expect_size"], f"{where}: route map size {n_routes}"
+    for k, hops in c.get("expect", {}).items():
+        node, kind, key = k.split("|", 2)
+        got = (dbs_of(node) or {}).get((kind, key))
+        assert got == _hop_set(hops), f"{where}: {k} {sorted(got or [])}"
+    for k in c.get("expect_absent", []):
+        node, kind, key = k.split("|", 2)
+        assert (kind, key) not in (dbs_of(node) or {}), f"{where}: {k} present"
+    for k, m in c.get("expect_metric", {}).items():
+        node, kind, key = k.split("|", 2)
+        got = dbs_of(node)[(kind, key)]
+        assert {h[2] for h in got} == {m}, f"{where}: {k} metrics {got}"
+    for k, w in c.get("expect_weight", {}).items():
+        node, key = k.split("|", 1)
+        assert dbs_of(node)["routes"][key][1] == w, \
+            f"{where}: {k} weight {dbs_of(node)['routes'][key]}"
+
+
 def _as_set(expect):
     if expect is None:
         return None
@@ -117,7 +364,7 @@ def _as_set(expect):
 
 
 SPF_KINDS = {"spf_runs", "ecmp", "ecmp_all", "ksp2", "ksp2_all", "kth_paths",
-             "kth_paths_edge_disjoint", "reachable", "grid_manhattan", "ucmp"}
+             "kth_paths_edge_disjoint", "reachable", "grid_manhattan", "ucmp", "route_map"}
 
 
 def run_fixture(fx: dict, make_ls, check_changes: bool = True, spf: bool = True) -> int:
@@ -125,12 +372,17 @@ def run_fixture(fx: dict, make_ls, check_changes: bool = True, spf: bool = True)
     spf=False evaluates only ingest-level checks (no SPF needed)."""
     ls = make_ls()
     labels: Dict[str, int] = {}
+    cur: Dict[str, dict] = {}  # the adjacency databases the link state holds
     n_checks = 0
     for si, step in enumerate(fx["steps"]):
         st = stream_of(step["dbs"])
         changes = ls.apply(st)
         for d in step["dbs"]:
             labels[d["name"]] = d["node_label"]
+            if d["delete"]:
+                cur.pop(d["name"], None)
+            else:
+                cur[d["name"]] = d
         if check_changes and "expect_changes" in step:
             for got, exp in zip(changes, step["expect_changes"]):
                 for g, e, what in zip(got, exp, ("topology", "attrs", "label", "added")):
@@ -207,6 +459,20 @@ def run_fixture(fx: dict, make_ls, check_changes: bool = True, spf: bool = True)
                     assert w == e["weight"], f"{where}: {node} weight {w}"
                     assert {i: hw for i, (_, hw) in hops.items()} == e["hops"], \
                         f"{where}: {node} hops {hops}"
+            elif k == "route_map":
+                opts = c.get("opts", {})
+                rb = RouteBuilder(ls, cur, **opts)
+                mine = {n: rb.build(n, c.get("prefixes", {})) for n in c["nodes"]}
+                check_route_map(c, mine.get, where)
+                if hasattr(ls, "route_dbs"):  # the product's C++ SpfSolver port
+                    prod = ls.route_dbs(c["nodes"], c.get("prefixes", {}), **opts)
+                    check_route_map(c, prod.get, where + " C++")
+                    assert prod == mine, f"{where}: C++ route dbs differ from restatement"
+            elif k == "path_in":
+                for a, b, want in c["cases"]:
+                    assert path_in(a, b) == want, f"{where}: {a} in {b}"
+                    if hasattr(ls, "path_a_in_b"):
+                        assert ls.path_a_in_b(a, b) == want, f"{where}: C++ {a} in {b}"
             elif k == "grid_manhattan":
                 n = c["n"]
                 for s in range(n * n):

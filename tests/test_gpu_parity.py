@@ -823,3 +823,29 @@ def test_wdial_packed_edges_follow_link_updates(monkeypatch):
         want = fresh.run(roots, W)
         assert np.array_equal(got["dist"], want["dist"]), step
         assert np.array_equal(got["nh"], want["nh"]), step
+
+
+@pytest.mark.parametrize("nb", [None, "1", "7", "24"])
+def test_msbfs_merged_rows_match_per_pass_rows(nb, monkeypatch):
+    """Multi-pass batches (fabric switches: 84 neighbours = 3 next-hop words)
+    write their rows with one kernel for all passes (msbfs_rows_multi) -- the
+    same dist / next-hop rows and digests as the per-pass rows kernels
+    (OSPF_MS_NOMERGE), at several round sizes (OSPF_MS_NB), and as the
+    oracle's digests; a ragged last batch and nh_words above the need
+    (zero-filled words) included."""
+    if nb:
+        monkeypatch.setenv("OSPF_MS_NB", nb)
+    monkeypatch.setenv("OSPF_FORCE_VARIANT", "5")
+    st = T.fabric(pods=40, planes=8)
+    p, eng = _engine_for(st)
+    names = p.node_names()
+    fsw = np.array([p.node_id(n) for n in names if n.startswith("2-")], np.uint32)[:150]
+    for W in (3, 5):
+        a = eng.run(fsw, W, want_digest=True)
+        monkeypatch.setenv("OSPF_MS_NOMERGE", "1")
+        b = eng.run(fsw, W, want_digest=True)
+        monkeypatch.delenv("OSPF_MS_NOMERGE")
+        assert np.array_equal(a["dist"], b["dist"]) and np.array_equal(a["nh"], b["nh"]), W
+        assert np.array_equal(a["digest"], b["digest"])
+    o = Oracle(st)
+    assert np.array_equal(a["digest"], o.digests([names[i] for i in fsw], threads=8))
