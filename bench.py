@@ -157,16 +157,28 @@ def main():
                     help="profiling mode: launch only the class with this neighbour capacity "
                          "(8, 16, or 32 x next-hop words)")
     ap.add_argument("--reps", type=int, default=3, help="launches in --class-only mode")
+    ap.add_argument("--dist-parity", type=int, default=0,
+                    help="N>1: rank 0 checks the gathered digests of the last timed step "
+                         "for this many roots against the CPU restatement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Multi-rank rehearsal on one GPU (tests/test_gpu_multirank.py): every rank
+    # on device 0, gloo for the collectives (RCCL refuses two ranks per GPU).
+    if os.environ.get("OPENR_BENCH_SHARE_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("OPENR_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist_on = world > 1
     if dist_on:
-        torch.distributed.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=dev)
+        else:
+            torch.distributed.init_process_group(backend)
+    coll_dev = dev if backend == "nccl" else torch.device("cpu")
 
     t0 = time.time()
     stream, desc, weighted, default_roots = build_topology(args.topology)
@@ -281,7 +293,7 @@ def main():
     dt = time.perf_counter() - t_start
     eng.sync(main_s.cuda_stream)  # raises if the device error word was set
     if dist_on:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
 
@@ -417,6 +429,15 @@ def main():
                                         for r, d in checks.items())),
                       "source": "digests of the last timed step vs the CPU restatement(s)"}
 
+    if rank == 0 and dist_on and args.dist_parity > 0 and step_digest:
+        from oracle import Oracle  # checker only, after the timed region
+        ids = [int(r) for r in pool[: args.dist_parity]]
+        want = Oracle(stream).fast_digests([names[i] for i in ids], threads=host_threads())
+        parity = {"roots": len(ids),
+                  "equal": bool(all(np.array_equal(step_digest[r], w) for r, w in zip(ids, want))),
+                  "source": "all-gathered digests of the last timed step (every rank's shard) "
+                            "vs the CSR-Dijkstra restatement"}
+
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(spf_s, 2), "unit": "SPF/s", "n_gpus": world,
@@ -442,6 +463,9 @@ def main():
                                (", RCCL all_gather of 24-B digests" if dist_on else "")},
             "roofline": roofline, "cpu_baseline": cpu, "parity_vs_cpu_sample": parity,
         }
+        if dist_on:
+            line["gathered_roots"] = len(step_digest)
+            line["dist_backend"] = backend
         print(json.dumps(line), flush=True)
     if dist_on:
         torch.distributed.destroy_process_group()

@@ -3,6 +3,9 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <sstream>
 #include <string>
 #include <unordered_map>
@@ -317,7 +320,12 @@ char* odl_route_db_text(odl_ls* h, const char* mes_nl, uint32_t n_mes, const cha
     opt.ucmp = flags & 4;
     const auto mes = splitNl(mes_nl, n_mes);
     odl::SpfSolver solver(h->ls);
+    const auto t0 = std::chrono::steady_clock::now();
     const auto dbs = solver.buildRouteDbs(mes, prefixes, opt);
+    if (getenv("ODL_SPF_TIMING"))
+      fprintf(stderr, "route_timing mes=%zu prefixes=%zu build_route_db_ms=%.3f\n", mes.size(),
+              prefixes.size(),
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     std::ostringstream os;
     for (size_t i = 0; i < mes.size(); ++i) {
       const auto& me = mes[i];

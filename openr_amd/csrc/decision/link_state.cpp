@@ -6,6 +6,7 @@
 #include <set>
 #include <algorithm>
 #include <functional>
+#include <map>
 #include <stdexcept>
 #include <atomic>
 #include <chrono>
@@ -177,6 +178,8 @@ std::vector<LinkPtr> LinkState::sortedLinksOf(const std::string& node) const {
   return v;
 }
 
+static size_t V_of(const LinkState::Csr& c) { return c.names.size(); }
+
 void LinkState::invalidate() {
   ++version_;
   memoMetric_.clear();
@@ -260,7 +263,20 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db) 
     }
   }
   // Incremental mode: same nodes and links, CSR current -> patch in place
-  if (incremental_ && !structural && snapVersion_ == version_) {
+  // (not in host-metric mode, and only while the patched metrics keep the
+  // engine contract: an in-range increase raises the distance bound by at
+  // most the new metric)
+  bool keepsContract = !hostMetric_;
+  uint64_t bound = distBound_;
+  for (const auto& d : deltas) {
+    for (const Metric m : {d.link->metricFrom(d.link->lowNode()), d.link->metricFrom(d.link->highNode())}) {
+      keepsContract &= m >= 1 && m <= 0xFFFFFFFFull;
+      bound += keepsContract ? m : 0;
+    }
+  }
+  keepsContract &= bound < 0xFFFFFFFFull;
+  if (incremental_ && !structural && snapVersion_ == version_ && keepsContract) {
+    distBound_ = bound;
     if (ch.topologyChanged) applyIncremental(deltas, nodeDeltas);
     return ch;
   }
@@ -359,6 +375,8 @@ const LinkState::Csr& LinkState::snapshot() {
   };
   std::vector<std::vector<Ent>> rows(V);
   std::vector<uint32_t> nfirst(V + 1, 0);
+  std::vector<uint8_t> rowBad(V, 0);
+  std::vector<uint64_t> rowMax(V, 0);
   parallelRows(V, [&](uint32_t lo, uint32_t hi) {
     for (uint32_t u = lo; u < hi; ++u) {
       const std::string& un = c.names[u];
@@ -375,9 +393,13 @@ const LinkState::Csr& LinkState::snapshot() {
         const Metric m = l->metricOfEnd(e.end);
         e.v = kInf;  // the other end's id: written by its own row
         e.rank = rank++;
-        // metric outside u32 (negative i32 wrapped to u64) is out of the engine
-        // contract; mark it with 0 so ospf_load_graph rejects it if usable.
-        e.metric = (m >= 1 && m <= 0xFFFFFFFFull) ? (uint32_t)m : 0u;
+        // a metric outside [1, 2^32) (0, or a negative i32 wrapped to u64) is
+        // outside the engine contract: the snapshot goes to host mode and the
+        // engine (hop-count runs only) sees 1
+        const bool inRange = m >= 1 && m <= 0xFFFFFFFFull;
+        e.metric = inRange ? (uint32_t)m : 1u;
+        if (!inRange) rowBad[u] = 1;
+        rowMax[u] = std::max<uint64_t>(rowMax[u], inRange ? m : 0);
         e.up = l->isUp() ? 1 : 0;
         // the lower end by name = by id sees the link first in id order
         e.low = (l->lowNode() == un) ? 1 : 0;
@@ -393,6 +415,17 @@ const LinkState::Csr& LinkState::snapshot() {
     nfirst[u + 1] += nfirst[u];
     c.rowPtr[u + 1] += c.rowPtr[u];
   }
+  // A simple path leaves each node at most once, so sum_u max_out(u) bounds
+  // every shortest distance: below 2^32 - 1 (the engine's unreached value)
+  // the engine's u32 distances cannot overflow.
+  uint64_t bound = 0;
+  bool bad = false;
+  for (uint32_t u = 0; u < V; ++u) {
+    bad |= rowBad[u] != 0;
+    bound = std::min<uint64_t>(bound + rowMax[u], ~0ull >> 1);
+  }
+  distBound_ = bound;
+  hostMetric_ = bad || bound >= 0xFFFFFFFFull;
   lap("gather");
   const size_t E = c.rowPtr[V];
   c.links.resize(nfirst[V]);
@@ -601,6 +634,10 @@ void LinkState::prefetchSpf(const std::vector<std::string>& roots, bool useLinkM
       memo.emplace(r, std::move(res));
       continue;
     }
+    if (useLinkMetric && hostMetric_) {
+      memo.emplace(r, runSpfHost(r, true, {}));
+      continue;
+    }
     byW[nhWordsFor(id->second)].push_back(id->second);
   }
   const size_t V = csr_.names.size();
@@ -609,13 +646,21 @@ void LinkState::prefetchSpf(const std::vector<std::string>& roots, bool useLinkM
     for (size_t c0 = 0; c0 < ids.size(); c0 += chunk) {
       std::vector<uint32_t> part(ids.begin() + c0, ids.begin() + std::min(ids.size(), c0 + chunk));
       std::vector<uint32_t> dist, nh;
+      const auto t0 = std::chrono::steady_clock::now();
       runBatch(part, nullptr, useLinkMetric, OSPF_WANT_DIST | OSPF_WANT_NH, W, &dist, &nh, nullptr);
+      const auto t1 = std::chrono::steady_clock::now();
       for (size_t i = 0; i < part.size(); ++i) {
         RawRun run{part[i], std::vector<uint32_t>(dist.begin() + i * V, dist.begin() + (i + 1) * V), {}};
         SpfResult res = buildResult(run, nh.data() + i * V * W, W, useLinkMetric);
         const std::string& name = csr_.names[part[i]];
         memo.emplace(name, std::move(res));
         if (useLinkMetric) rawMetric_.emplace(name, std::move(run));
+      }
+      if (getenv("ODL_SPF_TIMING")) {
+        const auto t2 = std::chrono::steady_clock::now();
+        fprintf(stderr, "spf_timing roots=%zu W=%u engine_ms=%.3f build_result_ms=%.3f\n",
+                part.size(), W, std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                std::chrono::duration<double, std::milli>(t2 - t1).count());
       }
     }
   }
@@ -640,6 +685,10 @@ std::vector<ospf_digest> LinkState::spfDigests(const std::vector<std::string>& r
       x *= 0x94d049bb133111ebULL;
       x ^= x >> 31;
       out[i] = ospf_digest{1, 0, x};
+      continue;
+    }
+    if (useLinkMetric && hostMetric_) {
+      out[i] = digestHost(roots[i], runSpfHost(roots[i], true, {}));
       continue;
     }
     ids.push_back(id->second);
@@ -723,7 +772,15 @@ const std::vector<Path>& LinkState::getKthPaths(const std::string& src, const st
       for (const auto& l : p)
         if (skipSet.insert(l.get()).second) skip.push_back(l);
   std::vector<Path> paths;
-  if (skip.empty()) {
+  snapshot();
+  if (hostMetric_) {
+    if (skip.empty()) {
+      paths = tracePathsHost(getSpfResult(src, true), src, dst);
+    } else {
+      ++spfRuns_;
+      paths = tracePathsHost(runSpfHost(src, true, skipSet), src, dst);
+    }
+  } else if (skip.empty()) {
     const SpfResult& r = getSpfResult(src, true);
     if (r.count(dst) && csr_.ids.count(src)) {
       const RawRun& run = rawSpf(src);
@@ -736,9 +793,38 @@ const std::vector<Path>& LinkState::getKthPaths(const std::string& src, const st
     std::vector<uint32_t> ign;
     for (const auto& l : skip) ign.push_back(linkIdOf(*l));
     std::sort(ign.begin(), ign.end());
-    std::vector<std::vector<uint32_t>> igns{ign};
     std::vector<uint32_t> dist;
-    runBatch({s}, &igns, true, OSPF_WANT_DIST, nhWordsFor(s), &dist, nullptr, nullptr);
+    if (ign.size() <= OSPF_MAX_IGNORED_PER_RUN) {
+      std::vector<std::vector<uint32_t>> igns{ign};
+      runBatch({s}, &igns, true, OSPF_WANT_DIST, nhWordsFor(s), &dist, nullptr, nullptr);
+    } else {
+      // more ignored links than a run's list holds (e.g. the host side of a
+      // KSP2 destination whose k = 1 paths overflowed the device record):
+      // take them down on the device graph for this one run, then restore
+      ensureEngine();
+      std::vector<ospf_link_update> down, back;
+      for (const uint32_t lid : ign) {
+        const Link& l = *csr_.links[lid];
+        const uint32_t lo = csr_.ids.at(l.lowNode());
+        for (uint32_t e = csr_.rowPtr[lo]; e < csr_.rowPtr[lo + 1]; ++e) {
+          if (csr_.linkId[e] != lid) continue;
+          const uint32_t mlo = csr_.metric[e], mhi = csr_.metric[csr_.twin[e]];
+          down.push_back(ospf_link_update{lid, 0u, mlo, mhi});
+          back.push_back(ospf_link_update{lid, csr_.edgeUp[e] ? 1u : 0u, mlo, mhi});
+          break;
+        }
+      }
+      int rc = ospf_update_links(engine_, down.data(), (uint32_t)down.size(), ~snapVersion_);
+      if (rc != OSPF_OK) throw EngineError(rc, ospf_last_error(engine_));
+      engineVersion_ = ~snapVersion_;
+      dist.assign(V_of(csr_), kInf);
+      rc = ospf_sssp_batch(engine_, &s, 1, nullptr, OSPF_WANT_DIST, nhWordsFor(s), dist.data(),
+                           nullptr, nullptr);
+      const int rc2 = ospf_update_links(engine_, back.data(), (uint32_t)back.size(), snapVersion_);
+      if (rc != OSPF_OK || rc2 != OSPF_OK)
+        throw EngineError(rc != OSPF_OK ? rc : rc2, ospf_last_error(engine_));
+      engineVersion_ = snapVersion_;
+    }
     RawRun run{s, std::move(dist), std::move(ign)};
     auto d = csr_.ids.find(dst);
     if (d != csr_.ids.end()) paths = tracePaths(run, s, d->second);
@@ -748,6 +834,10 @@ const std::vector<Path>& LinkState::getKthPaths(const std::string& src, const st
 
 void LinkState::prefetchKsp2(const std::string& src, const std::vector<std::string>& dsts) {
   snapshot();
+  if (hostMetric_) {
+    for (const auto& d : dsts) getKthPaths(src, d, 2);
+    return;
+  }
   auto sid = csr_.ids.find(src);
   std::vector<uint32_t> ids;
   std::vector<const std::string*> names;
@@ -957,6 +1047,110 @@ UcmpResult LinkState::resolveUcmpWeights(
     out.emplace(name, std::move(cur));
   }
   return out;
+}
+
+// ---------------------------------------------------------------- host path
+SpfResult LinkState::runSpfHost(const std::string& root, bool useLinkMetric,
+                                const std::unordered_set<const Link*>& ignore) const {
+  // Dijkstra with the reference's queue order -- (metric, name), keys only
+  // ever lowered by a strictly better path -- and its u64 arithmetic, so a
+  // wrapped negative metric behaves exactly as there.
+  SpfResult done;
+  std::unordered_map<std::string, NodeSpfResult> open;
+  std::set<std::pair<Metric, std::string>> order;
+  open.emplace(root, NodeSpfResult(0));
+  order.emplace(0, root);
+  while (!order.empty()) {
+    const std::string name = order.begin()->second;
+    order.erase(order.begin());
+    auto node = open.find(name);
+    auto& rec = done.emplace(name, std::move(node->second)).first->second;
+    open.erase(node);
+    if (name != root && isNodeOverloaded(name)) continue;  // no transit
+    for (const auto& link : linksFromNode(name)) {
+      const std::string& other = link->otherNode(name);
+      if (!link->isUp() || done.count(other) || ignore.count(link.get())) continue;
+      const Metric cand = rec.metric() + (useLinkMetric ? link->metricFrom(name) : 1);
+      auto it = open.find(other);
+      if (it == open.end()) {
+        it = open.emplace(other, NodeSpfResult(cand)).first;
+        order.emplace(cand, other);
+      }
+      NodeSpfResult& o = it->second;
+      if (o.metric() < cand) continue;
+      if (o.metric() > cand) {  // strictly better: forget the other paths
+        order.erase({o.metric(), other});
+        o = NodeSpfResult(cand);
+        order.emplace(cand, other);
+      }
+      o.pathLinks_.push_back(PathLink{link, name});
+      o.nextHops_.insert(rec.nextHops_.begin(), rec.nextHops_.end());
+      if (o.nextHops_.empty()) o.nextHops_.insert(other);  // a neighbour of the root
+    }
+  }
+  return done;
+}
+
+std::vector<Path> LinkState::tracePathsHost(const SpfResult& res, const std::string& src,
+                                            const std::string& dst) const {
+  std::vector<Path> out;
+  if (!res.count(dst)) return out;
+  std::unordered_set<const Link*> seen;
+  std::function<std::optional<Path>(const std::string&)> one =
+      [&](const std::string& x) -> std::optional<Path> {
+    if (x == src) return Path{};
+    for (const auto& pl : res.at(x).pathLinks()) {
+      if (!seen.insert(pl.link.get()).second) continue;
+      auto p = one(pl.prevNode);
+      if (p) {
+        p->push_back(pl.link);
+        return p;
+      }
+    }
+    return std::nullopt;
+  };
+  for (auto p = one(dst); p && !p->empty(); p = one(dst)) out.push_back(std::move(*p));
+  return out;
+}
+
+ospf_digest LinkState::digestHost(const std::string& root, const SpfResult& res) const {
+  // the engine's digest with u64 distances: node ids and the
+  // root's neighbour bit positions of the current snapshot
+  auto mix = [](uint64_t x) {
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ULL;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebULL;
+    x ^= x >> 31;
+    return x;
+  };
+  const uint32_t r = csr_.ids.at(root);
+  std::unordered_map<std::string, uint32_t> bit;
+  for (uint32_t e = csr_.rowPtr[r]; e < csr_.rowPtr[r + 1]; ++e) {
+    const uint32_t v = csr_.col[e];
+    if (v != r && !bit.count(csr_.names[v])) {
+      const uint32_t i = (uint32_t)bit.size();
+      bit.emplace(csr_.names[v], i);
+    }
+  }
+  ospf_digest d{0, 0, 0};
+  for (const auto& [name, nr] : res) {
+    const uint32_t v = csr_.ids.at(name);
+    const uint64_t kd = mix((uint64_t)v ^ 0x2545F4914F6CDD1DULL) | 1ull;
+    const uint64_t kn = mix((uint64_t)v ^ 0xD6E8FEB86659FD93ULL) | 1ull;
+    std::map<uint32_t, uint32_t> words;
+    for (const auto& h : nr.nextHops()) {
+      const uint32_t i = bit.at(h);
+      words[i / 32] |= 1u << (i % 32);
+    }
+    uint64_t ws = 0;
+    for (const auto& [w, word] : words)
+      if (word) ws += mix((((uint64_t)w << 32) | word) ^ 0x9E3779B97F4A7C15ULL);
+    d.reached += 1;
+    d.sum_dist += nr.metric();
+    d.hash += kd * (nr.metric() + 1) + kn * ws;
+  }
+  return d;
 }
 
 bool LinkState::pathAInPathB(const Path& a, const Path& b) {

@@ -162,8 +162,10 @@ struct LinkStateChange {
   std::vector<LinkPtr> addedLinks;
 };
 
-// Raised for engine failures (no device, out-of-contract graph). There is no
-// CPU fallback; the Decision caller decides what to do.
+// Raised for engine failures (no device, engine error). Graphs outside the
+// engine's metric contract (a metric 0 or negative i32 adjacency, or
+// distances that may not fit u32) are not an error: their link-metric runs
+// take LinkState's host path (runSpfHost), the reference's own algorithm.
 struct EngineError : std::runtime_error {
   int code;
   EngineError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
@@ -231,6 +233,13 @@ class LinkState {
   };
   const Csr& snapshot();
   uint32_t linkIdOf(const Link& l) const;  // id in the current snapshot
+  // true when the current snapshot is outside the engine's metric contract:
+  // link-metric SPF / KSP2 then run on the host (hop-count runs stay on the
+  // engine)
+  bool hostMetricMode() {
+    snapshot();
+    return hostMetric_;
+  }
 
  private:
   struct RawRun {  // one engine run kept for pathLinks / trace reconstruction
@@ -255,6 +264,14 @@ class LinkState {
                             std::unordered_set<const Link*>& seen) const;
   std::vector<Path> tracePaths(const RawRun& run, uint32_t src, uint32_t dst) const;
   const RawRun& rawSpf(const std::string& node);
+  // LinkState::runSpf (LinkState.cpp:836-911) on the host, u64 metrics with
+  // the reference's wrap-around, for graphs outside the engine contract
+  SpfResult runSpfHost(const std::string& root, bool useLinkMetric,
+                       const std::unordered_set<const Link*>& ignore) const;
+  // traceOnePath (LinkState.cpp:418-439) over a host result's pathLinks
+  std::vector<Path> tracePathsHost(const SpfResult& res, const std::string& src,
+                                   const std::string& dst) const;
+  ospf_digest digestHost(const std::string& root, const SpfResult& res) const;
   struct LinkDelta {  // a kept link whose metric or up state changed
     LinkPtr link;
     bool up0;
@@ -270,6 +287,8 @@ class LinkState {
   uint64_t version_ = 1;        // bumped on every ingest call
   uint64_t snapVersion_ = 0;
   Csr csr_;
+  bool hostMetric_ = false;   // snapshot outside the engine's metric contract
+  uint64_t distBound_ = 0;    // >= every simple-path metric sum of the snapshot
   uint64_t spfRuns_ = 0;
   bool incremental_ = false;
   IncrementalStats incStats_;

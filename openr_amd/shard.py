@@ -117,9 +117,32 @@ def gather_digests(local, group=None):
         out = torch.empty((world * local.shape[0], 3), dtype=local.dtype, device=local.device)
         dist.all_gather_into_tensor(out, local, group=group)
         return out
+    # gloo (CPU tests, or a multi-rank rehearsal sharing one GPU): host copies
+    local = local.detach().cpu()
     parts = [torch.empty_like(local) for _ in range(world)]
     dist.all_gather(parts, local, group=group)
     return torch.cat(parts)
+
+
+def ksp2_shards(V: int, neighbors: np.ndarray, world: int, rank: int):
+    """scripts/bench_ksp2.py's split of one KSP2 + LFA step over ranks: a
+    contiguous block of destination ids (np.array_split) and every world-th
+    neighbour of the source for the LFA reruns. Disjoint and covering; the
+    records need no collective (each rank holds its destinations' paths)."""
+    dsts = np.array_split(np.arange(V, dtype=np.uint32), world)[rank]
+    return dsts, np.asarray(neighbors)[rank::world]
+
+
+def reassemble_by_destination(parts):
+    """Merge per-rank {destination: record} maps (one per rank, disjoint) into
+    one ordered by destination id."""
+    out = {}
+    for part in parts:
+        for d, rec in part.items():
+            if d in out:
+                raise ValueError(f"destination {d} in two shards")
+            out[d] = rec
+    return dict(sorted(out.items()))
 
 
 def digests_as_u64(t) -> np.ndarray:

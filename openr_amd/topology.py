@@ -41,10 +41,8 @@ def _stream_from_edges(names: Sequence[str], labels: np.ndarray, src: np.ndarray
     V = len(names)
     E = src.size
     # strings: node names [0, V), then one ifName per directed edge [V, V+E)
-    nm = np.asarray(names, dtype=object)
-    ifn = np.char.add(np.char.add(np.char.add("if_", nm[src].astype(str)), "_"),
-                      nm[dst].astype(str))
-    strings = list(names) + ifn.tolist()
+    nl = list(names)
+    strings = nl + [f"if_{nl[a]}_{nl[b]}" for a, b in zip(src.tolist(), dst.tolist())]
     # reverse edge index: for edge (a->b) find (b->a); pair by sorted keys
     key_f = src.astype(np.int64) * V + dst
     key_r = dst.astype(np.int64) * V + src
@@ -61,8 +59,9 @@ def _stream_from_edges(names: Sequence[str], labels: np.ndarray, src: np.ndarray
     if order is None:
         order = np.arange(V)
     # adjacency columns in ingest order
-    sel = np.concatenate([by_src[starts[i]:starts[i + 1]] for i in order]) if E else \
-        np.zeros(0, np.int64)
+    rank = np.empty(V, np.int64)
+    rank[order] = np.arange(V)
+    sel = by_src[np.argsort(rank[src[by_src]], kind="stable")] if E else np.zeros(0, np.int64)
     db_off = np.zeros(V + 1, np.uint64)
     np.cumsum(counts[order], out=db_off[1:])
     cols = dict(
@@ -241,20 +240,12 @@ def mesh(n_points: int, seed: int = 42, mean_degree: float = 8.0) -> AdjDbStream
     keep = d <= r
     a, b, d = a[keep], b[keep], d[keep]
     # largest connected component (union-find)
-    parent = np.arange(n_points)
-
-    def find(x):
-        while parent[x] != x:
-            parent[x] = parent[parent[x]]
-            x = parent[x]
-        return x
-    for u, v in zip(a.tolist(), b.tolist()):
-        ru, rv = find(u), find(v)
-        if ru != rv:
-            parent[ru] = rv
-    roots = np.array([find(i) for i in range(n_points)])
-    big = np.bincount(roots).argmax()
-    alive = roots == big
+    from scipy.sparse import coo_matrix
+    from scipy.sparse.csgraph import connected_components
+    _, comp = connected_components(
+        coo_matrix((np.ones(a.size, np.int8), (a, b)), shape=(n_points, n_points)),
+        directed=False)
+    alive = comp == np.bincount(comp).argmax()
     newid = -np.ones(n_points, np.int64)
     keep_idx = np.nonzero(alive)[0]
     q = np.minimum((pts[keep_idx] * 1024).astype(np.int64), 1023)

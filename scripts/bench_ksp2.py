@@ -31,6 +31,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 from openr_amd import _native as N  # noqa: E402
+from openr_amd import shard  # noqa: E402
 from openr_amd import topology as T  # noqa: E402
 from openr_amd.engine import Engine, decode_paths  # noqa: E402
 from openr_amd.linkstate import LinkState  # noqa: E402
@@ -61,11 +62,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("OPENR_BENCH_SHARE_DEVICE") == "1":  # rehearsal: all ranks on GPU 0
+        local = 0
+    backend = os.environ.get("OPENR_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    coll_dev = dev if backend == "nccl" else torch.device("cpu")
     dist_on = world > 1
     if dist_on:
-        torch.distributed.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=dev)
+        else:
+            torch.distributed.init_process_group(backend)
 
     t0 = time.perf_counter()
     stream = T.fabric(pods=args.pods, planes=args.planes)
@@ -79,14 +87,13 @@ def main():
     log(f"[rank {rank}] topology V={V} E={E} src={args.src}({src}) in {time.perf_counter()-t0:.1f}s")
 
     # shards: destinations and LFA neighbours
-    dsts = np.array_split(np.arange(V, dtype=np.uint32), world)[rank]
+    nbrs = eng.root_neighbors(src)
+    dsts, mine = shard.ksp2_shards(V, nbrs, world, rank)
     n, cap = int(dsts.size), args.cap
     d_dsts = torch.from_numpy(dsts.view(np.int32)).to(dev)
     k1 = torch.empty((n, cap), dtype=torch.int32, device=dev)
     k2 = torch.empty_like(k1)
     st = torch.empty(n, dtype=torch.int32, device=dev)
-    nbrs = eng.root_neighbors(src)
-    mine = nbrs[rank::world]
     rp = csr["row_ptr"]
     cols = csr["col"]
     def nbr_count(u):
@@ -134,7 +141,7 @@ def main():
     dt = time.perf_counter() - t1
     eng.sync(s.cuda_stream)
     if dist_on:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
 
@@ -155,7 +162,7 @@ def main():
     reruns = int(np.count_nonzero(status & N.OSPF_KSP_RERUN))
     ovf = int(np.count_nonzero(status & (N.OSPF_KSP_OVF1 | N.OSPF_KSP_OVF2)))
     if dist_on:
-        t = torch.tensor([reruns, ovf], dtype=torch.int64, device=dev)
+        t = torch.tensor([reruns, ovf], dtype=torch.int64, device=coll_dev)
         torch.distributed.all_reduce(t)
         reruns, ovf = int(t[0]), int(t[1])
 

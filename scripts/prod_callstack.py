@@ -1,0 +1,123 @@
+#!/usr/bin/env python3
+"""Production call stack A at F100k:
+what Decision runs per route rebuild on one node --
+
+    getSpfResult(myNodeName)      (LinkState.cpp:821-831; engine SPF + host
+                                   SpfResult rebuild, link_state.cpp buildResult)
+    -> route build                (SpfSolver::buildRouteDb, SpfSolver.cpp:460-646:
+                                   every node's loopback prefix + MPLS node /
+                                   adjacency labels, odl::SpfSolver)
+
+timed through odl::LinkState on the MI355X, phase by phase (ODL_SPF_TIMING
+lines from libopenr_decision), cold (snapshot + device load) and warm, and
+after a link-metric event with incremental patching off / on; next to the
+CPU restatement of runSpf on the same root (oracle/, reference-shaped).
+
+Usage: python scripts/prod_callstack.py [--pods 1781] > out.json
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import re
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ["ODL_SPF_TIMING"] = "1"
+
+import torch  # noqa: E402,F401  (one HIP runtime for torch and the engine)
+
+from openr_amd import topology as T  # noqa: E402
+from openr_amd.adjdb import AdjDbStream  # noqa: E402
+from openr_amd.linkstate import LinkState  # noqa: E402
+
+
+class Stderr:
+    """Capture the C++ timing lines written to fd 2."""
+
+    def __enter__(self):
+        self.f = tempfile.TemporaryFile("w+")
+        sys.stderr.flush()
+        self.saved = os.dup(2)
+        os.dup2(self.f.fileno(), 2)
+        return self
+
+    def __exit__(self, *a):
+        sys.stderr.flush()
+        os.dup2(self.saved, 2)
+        os.close(self.saved)
+        self.f.seek(0)
+        self.text = self.f.read()
+        self.f.close()
+
+    def values(self, key):
+        return [float(x) for x in re.findall(key + r"=([0-9.]+)", self.text)]
+
+
+def timed(fn):
+    with Stderr() as cap:
+        t = time.perf_counter()
+        out = fn()
+        wall = (time.perf_counter() - t) * 1e3
+    return out, wall, cap
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pods", type=int, default=1781)
+    ap.add_argument("--me", default="3-0-0")
+    ap.add_argument("--other", default="3-17-5")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+    st = T.fabric(pods=args.pods, planes=8)
+    out = {"topology": f"fabric pods={args.pods} planes=8 (unit metric)", "me": args.me}
+
+    def stack(p, me, label):
+        _, wall, cap = timed(lambda: p.prefetch([me]))
+        rec = {"getSpfResult_wall_ms": round(wall, 3),
+               "engine_ms": sum(cap.values("engine_ms")),
+               "build_result_ms": sum(cap.values("build_result_ms"))}
+        names = p.node_names()
+        prefixes = {f"lo-{n}": [[n, "ip", "ecmp", 0, None]] for n in names}
+        _, wall_r, cap_r = timed(lambda: p.route_dbs([me], prefixes))
+        rec["route_build_ms"] = sum(cap_r.values("build_route_db_ms"))
+        rec["route_build_wall_ms_incl_text"] = round(wall_r, 3)
+        rec["total_ms"] = round(rec["getSpfResult_wall_ms"] + rec["route_build_ms"], 3)
+        out[label] = rec
+        print(f"{label}: {rec}", file=sys.stderr, flush=True)
+
+    for incremental in (False, True):
+        p = LinkState()
+        p.set_incremental(incremental)
+        t = time.perf_counter()
+        p.apply(st)
+        ingest = (time.perf_counter() - t) * 1e3
+        tag = "incremental" if incremental else "default"
+        out[f"{tag}_ingest_ms"] = round(ingest, 1)
+        stack(p, args.me, f"{tag}_cold")      # snapshot + engine open/load + run
+        stack(p, args.other, f"{tag}_warm")   # graph resident: run + rebuild
+        # a link-metric event on a far link, then the same node's rebuild
+        db = [d for d in st.to_dbs() if d.name == "3-900-0"][0]
+        db.adjs[0].metric = 3
+        ev = AdjDbStream.from_dbs([db])
+        _, wall, _ = timed(lambda: p.apply(ev))
+        out[f"{tag}_event_apply_ms"] = round(wall, 3)
+        stack(p, args.me, f"{tag}_after_event")
+        del p
+    if not args.no_cpu:
+        from oracle import Oracle  # CPU restatement, same root
+        o = Oracle(st)
+        t = time.perf_counter()
+        txt = o.spf_text(args.me, True)
+        out["cpu_runSpf_ms"] = round((time.perf_counter() - t) * 1e3, 3)
+        out["cpu_runSpf_note"] = ("reference-shaped runSpf restatement (oracle/), one thread, "
+                                  f"result text {len(txt)} bytes")
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -79,3 +79,61 @@ def test_nh_words_matches_engine_rule():
     assert w[names.index("1-0-0")] == 2      # spine: 40 pods -> 40 neighbours
     assert w[names.index("2-0-0")] == 3      # fabric sw: 36 + 48 = 84
     assert w[names.index("3-0-0")] == 1      # rack sw: 4 planes
+
+
+def _ksp2_worker(rank, world, port, result_q):
+    """One rank of scripts/bench_ksp2.py's split: its destination block's
+    k = 1 / k = 2 paths and its LFA neighbours' digests (the CPU restatement
+    stands in for ospf_ksp2_dev here), gathered to rank 0 and reassembled."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import Oracle
+    from openr_amd.linkstate import LinkState
+    st = T.fabric(pods=5, planes=4)
+    ls = LinkState(stream=st)
+    csr = ls.csr()
+    names = ls.node_names()
+    o = Oracle(st)
+    src = names.index("2-0-0")
+    rp, col = csr["row_ptr"], csr["col"]
+    nbrs = np.unique(col[rp[src]:rp[src + 1]])
+    dsts, lfa = shard.ksp2_shards(len(names), nbrs, world, rank)
+    mine = {int(d): (o.kth_paths("2-0-0", names[d], 1), o.kth_paths("2-0-0", names[d], 2))
+            for d in dsts}
+    lfa_dig = {int(u): o.digests([names[u]])[0].tolist() for u in lfa}
+    parts = [None] * world
+    dist.all_gather_object(parts, (mine, lfa_dig))
+    if rank == 0:
+        recs = shard.reassemble_by_destination([p[0] for p in parts])
+        lfas = shard.reassemble_by_destination([p[1] for p in parts])
+        want = {d: (o.kth_paths("2-0-0", names[d], 1), o.kth_paths("2-0-0", names[d], 2))
+                for d in range(len(names))}
+        ok = list(recs) == list(range(len(names))) and recs == want
+        ok &= sorted(lfas) == sorted(int(u) for u in nbrs)
+        ok &= all(lfas[int(u)] == o.digests([names[u]])[0].tolist() for u in nbrs)
+        result_q.put(bool(ok))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ksp2_destination_sharding_reassembles(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ksp2_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=5) is True
+
+
+def test_ksp2_shards_are_disjoint_and_cover():
+    nb = np.arange(84) * 7
+    for world in (1, 2, 4, 8):
+        ds, ls_ = zip(*(shard.ksp2_shards(1001, nb, world, r) for r in range(world)))
+        assert np.array_equal(np.sort(np.concatenate(ds)), np.arange(1001))
+        assert np.array_equal(np.sort(np.concatenate(ls_)), nb)
+    with pytest.raises(ValueError):
+        shard.reassemble_by_destination([{1: "a"}, {1: "b"}])

@@ -8,7 +8,7 @@ import pytest
 
 from golden_eval import ProductLS, load_fixtures, run_fixture
 from graphs import random_stream
-from oracle import Oracle
+from oracle import Oracle, parse_spf_text
 from openr_amd import topology as T
 from openr_amd.adjdb import AdjDb, AdjDbStream, create_adjacency
 from openr_amd.engine import Engine, EngineError
@@ -849,3 +849,63 @@ def test_msbfs_merged_rows_match_per_pass_rows(nb, monkeypatch):
         assert np.array_equal(a["digest"], b["digest"])
     o = Oracle(st)
     assert np.array_equal(a["digest"], o.digests([names[i] for i in fsw], threads=8))
+
+
+@pytest.mark.parametrize("incremental", [False, True])
+def test_out_of_contract_update_switches_to_host_and_back(incremental):
+    """An update that puts a metric-0 / negative adjacency on a live graph moves
+    its link-metric runs to the host path (incremental patching steps aside);
+    hop-count runs stay on the engine; restoring the metric returns to it."""
+    stream, names = random_stream(31, n=40)
+    o, p = Oracle(), LinkState()
+    p.set_incremental(incremental)
+    assert o.apply(stream) == p.apply(stream)
+
+    def check():
+        for r in names:
+            assert p.spf(r) == parse_spf_text(o.spf_text(r, True)), r
+            assert p.spf(r, False) == parse_spf_text(o.spf_text(r, False)), r
+
+    check()
+    db = next(d for d in stream.to_dbs() if len(d.adjs) >= 2)
+    orig = [a.metric for a in db.adjs]
+    for metric in (0, -3):
+        db.adjs[0].metric = metric
+        db.adjs[1].metric = 0
+        s = AdjDbStream.from_dbs([db])
+        assert o.apply(s) == p.apply(s)
+        check()
+    for a, m in zip(db.adjs, orig):
+        a.metric = m
+    s = AdjDbStream.from_dbs([db])
+    assert o.apply(s) == p.apply(s)
+    check()
+
+
+def test_ksp2_ignore_set_above_run_list_cap():
+    """k = 2 with more k = 1 path links than one run's ignore list holds
+    (OSPF_MAX_IGNORED_PER_RUN = 2048): 1,100 two-hop shortest paths s-m_i-d
+    (2,200 links) plus a 3-hop detour; device KSP2 records overflow too."""
+    n_mid = 1100
+    dbs = {"s": [], "d": [], "a": [], "b": []}
+    for i in range(n_mid):
+        m = f"m{i:04d}"
+        dbs[m] = [create_adjacency("s", f"{m}/s", f"s/{m}", 1),
+                  create_adjacency("d", f"{m}/d", f"d/{m}", 1)]
+        dbs["s"].append(create_adjacency(m, f"s/{m}", f"{m}/s", 1))
+        dbs["d"].append(create_adjacency(m, f"d/{m}", f"{m}/d", 1))
+    for x, y in (("s", "a"), ("a", "b"), ("b", "d")):
+        dbs[x].append(create_adjacency(y, f"{x}/{y}", f"{y}/{x}", 1))
+        dbs[y].append(create_adjacency(x, f"{y}/{x}", f"{x}/{y}", 1))
+    stream = AdjDbStream.from_dbs(AdjDb(n, a, i + 1) for i, (n, a) in enumerate(dbs.items()))
+    o, p = Oracle(), LinkState()
+    assert o.apply(stream) == p.apply(stream)
+    k1 = p.kth_paths("s", "d", 1)
+    assert len(k1) == n_mid and sum(len(x) for x in k1) > 2048
+    assert k1 == o.kth_paths("s", "d", 1)
+    k2 = p.kth_paths("s", "d", 2)
+    assert k2 == o.kth_paths("s", "d", 2) and len(k2) == 1 and len(k2[0]) == 3
+    assert p.spf("s") == parse_spf_text(o.spf_text("s", True))  # graph restored
+    q = LinkState()
+    q.apply(stream)
+    assert q.ksp2_text("s", ["d", "a"]) == o.ksp2_text("s", ["d", "a"])

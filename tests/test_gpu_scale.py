@@ -1,0 +1,129 @@
+"""Parity at BASELINE.json's full sizes: F10k all-sources,
+F100k KSP2 + per-neighbour LFA runs from "2-0-0", and M1M sampled roots, each
+against the CPU oracle, plus size-independent properties over every run the
+oracle cannot afford (reached counts, twin-run equality, edge-disjoint KSP2
+paths whose cost equals the SPF distance, and per-edge triangle / tight-
+predecessor checks on whole distance rows)."""
+import time
+
+import numpy as np
+import pytest
+
+from oracle import Oracle
+from openr_amd import topology as T
+from openr_amd.engine import Engine
+from openr_amd.linkstate import LinkState
+
+pytestmark = pytest.mark.gpu
+
+
+T0 = time.time()
+
+
+def note(msg):
+    """progress to stdout (run with -s): long CPU-side stages stay visible"""
+    print(f"[{time.time() - T0:7.1f}s] {msg}", flush=True)
+
+
+def both(stream):
+    o, p = Oracle(), LinkState()
+    assert o.apply(stream) == p.apply(stream)
+    note("ingested")
+    return o, p
+
+
+@pytest.mark.timeout(600)
+def test_f10k_all_sources_digests_and_properties():
+    st = T.fabric(pods=173, planes=8)
+    o, p = both(st)
+    names = p.node_names()
+    V = len(names)
+    got = p.digests(names)
+    note("F10k GPU digests")
+    # every root against the CPU restatement (CSR Dijkstra, unit metric)
+    assert np.array_equal(got, o.fast_digests(names, True, threads=16))
+    # properties: connected fabric, no drains -> every run reaches V; a twin
+    # run in reverse root order (different batches / classes) is identical
+    assert np.all(got[:, 0] == V)
+    assert np.array_equal(p.digests(names[::-1])[::-1], got)
+    # full SpfResult text (next hops + pathLinks) for one root of each role
+    for r in ("1-3-17", "2-100-5", "3-172-47"):
+        assert p.spf_text(r) == o.spf_text(r)
+
+
+def _path_cost(p, path, src):
+    cost, at = 0, src
+    for key in path:
+        a, b = key.split("|")
+        na, nb = a.split("%", 1)[0], b.split("%", 1)[0]
+        nxt = nb if na == at else na
+        cost += next(m for k, m, _ in p.links(at) if k == key)
+        at = nxt
+    return cost, at
+
+
+@pytest.mark.timeout(900)
+def test_f100k_ksp2_and_lfa_from_fsw():
+    st = T.fabric(pods=1781, planes=8)
+    o, p = both(st)
+    src = "2-0-0"
+    # spines of this and other planes, far pods' FSWs and RSWs, a local RSW
+    dsts = ["1-0-35", "1-3-17", "1-7-0", "2-1780-5", "2-900-0", "3-1780-0", "3-900-47", "3-0-0"]
+    assert p.ksp2_text(src, dsts) == o.ksp2_text(src, dsts)
+    note("F100k KSP2 text equal")
+    spf = p.spf(src)
+    for d in dsts:
+        k1, k2 = p.kth_paths(src, d, 1), p.kth_paths(src, d, 2)
+        assert k1, d
+        used = {key for path in k1 for key in path}
+        for path in k1:
+            cost, end = _path_cost(p, path, src)
+            assert end == d and cost == spf[d][0], (d, path)
+        for path in k2:
+            assert not used & set(path), (d, path)  # edge-disjoint from k = 1
+            cost, end = _path_cost(p, path, src)
+            assert end == d and cost >= spf[d][0]
+    # LFA: one SPF per neighbour of the source (its 48 RSWs and 36 spines)
+    nbrs = sorted({k.split("|")[0].split("%")[0] if not k.startswith(src + "%") else
+                   k.split("|")[1].split("%")[0] for k, _, _ in p.links(src)})
+    assert len(nbrs) == 48 + 36
+    assert np.array_equal(p.digests(nbrs), o.fast_digests(nbrs, True, threads=16))
+
+
+@pytest.mark.timeout(900)
+def test_m1m_sampled_roots_and_triangle_checks():
+    st = T.mesh(1_000_000, seed=42)
+    o, p = both(st)
+    names = p.node_names()
+    V = len(names)
+    rng = np.random.default_rng(0x5eed)
+    ids = rng.choice(V, 64, replace=False)
+    roots = [names[i] for i in ids]
+    dig = p.digests(roots)
+    note("M1M GPU digests")
+    assert np.array_equal(dig[:2], o.fast_digests(roots[:2], True, threads=2))
+    csr = p.csr()
+    e = Engine()
+    try:
+        e.load(csr)
+        rows = e.run(ids, max(e.nh_words(int(i)) for i in ids), want_nh=False)["dist"]
+    finally:
+        e.close()
+    rp = csr["row_ptr"].astype(np.int64)
+    src = np.repeat(np.arange(V), np.diff(rp))
+    col, met = csr["col"].astype(np.int64), csr["metric"].astype(np.int64)
+    up = csr["edge_up"].astype(bool)
+    nt = csr["no_transit"].astype(bool)
+    inf = np.uint32(0xFFFFFFFF)
+    for k, r in enumerate(ids):
+        d = rows[k].astype(np.int64)
+        reached = rows[k] != inf
+        assert reached.sum() == int(dig[k][0]) and d[reached].sum() == int(dig[k][1])
+        relax = up & reached[src] & ((src == r) | ~nt[src])
+        cand = d[src[relax]] + met[relax]
+        # triangle: no relaxable edge improves a distance
+        assert np.all(d[col[relax]] <= cand)
+        # every reached node but the root has a tight predecessor
+        tight = np.zeros(V, bool)
+        tight[col[relax][d[col[relax]] == cand]] = True
+        assert np.all(tight[reached] | (np.arange(V)[reached] == r))

@@ -1,0 +1,90 @@
+"""Graphs outside the engine's metric contract: a metric-0
+or negative i32 adjacency (the reference widens it to u64 and wraps,
+LinkState.cpp:878-893), or distances that may not fit the engine's u32. The
+product computes their link-metric SPF / KSP2 / routes on the host inside
+libopenr_decision (LinkState::runSpfHost), never through the oracle; these
+runs need no GPU, so the comparison with the oracle runs on the CPU. Hop-count
+runs on such graphs stay on the engine and are covered by the -m gpu test."""
+import dataclasses
+
+import numpy as np
+import pytest
+
+from golden_eval import OracleLS, RouteBuilder
+from oracle import Oracle, parse_spf_text
+from openr_amd.adjdb import AdjDb, AdjDbStream, create_adjacency
+from openr_amd.linkstate import LinkState
+
+POOLS = {
+    "zero": [0, 0, 1, 2, 3],
+    "negative": [-1, -7, 1, 2, 5, 9],
+    "huge": [2 ** 31 - 1, 2 ** 31 - 2, 2 ** 30, 1],
+}
+
+
+def contract_case(seed, pool, n=18, p=0.25):
+    rng = np.random.default_rng(seed)
+    names = [f"v{int(x)}" for x in rng.permutation(5 * n)[:n]]
+    adjs = {nm: [] for nm in names}
+    k = 0
+    for i in range(n):
+        for j in range(i + 1, n):
+            if rng.random() > p:
+                continue
+            for _ in range(2 if rng.random() < 0.2 else 1):
+                a, b = names[i], names[j]
+                ia, ib = f"{a}-{b}-{k}", f"{b}-{a}-{k}"
+                adjs[a].append(create_adjacency(b, ia, ib, int(rng.choice(pool)), 200000 + 2 * k,
+                                                overloaded=bool(rng.random() < 0.05)))
+                adjs[b].append(create_adjacency(a, ib, ia, int(rng.choice(pool)), 200001 + 2 * k))
+                k += 1
+    dbs = [AdjDb(nm, adjs[nm], i + 1, overloaded=bool(rng.random() < 0.1))
+           for i, nm in enumerate(names)]
+    return dbs, names
+
+
+@pytest.mark.parametrize("kind", sorted(POOLS))
+@pytest.mark.parametrize("seed", range(4))
+def test_spf_outside_contract_matches_oracle(kind, seed):
+    dbs, names = contract_case(seed, POOLS[kind])
+    stream = AdjDbStream.from_dbs(dbs)
+    o, p = Oracle(), LinkState()
+    assert o.apply(stream) == p.apply(stream)
+    for r in names:
+        assert p.spf(r) == parse_spf_text(o.spf_text(r, True)), r
+    rng = np.random.default_rng(seed)
+    for _ in range(12):
+        s, d = (str(x) for x in rng.choice(names, 2, replace=False))
+        for k in (1, 2):
+            assert p.kth_paths(s, d, k) == o.kth_paths(s, d, k), (s, d, k)
+
+
+@pytest.mark.parametrize("kind", sorted(POOLS))
+def test_routes_outside_contract_match_restatement(kind):
+    dbs, names = contract_case(99, POOLS[kind])
+    stream = AdjDbStream.from_dbs(dbs)
+    o, p = OracleLS(), LinkState()
+    o.apply(stream)
+    p.apply(stream)
+    prefixes = {f"10.9.{i}.0/24": [[names[i], "ip", "ecmp", 0, None],
+                                   [names[(3 * i + 1) % len(names)], "sr_mpls", "ksp2", 0, None]]
+                for i in range(len(names))}
+    rb = RouteBuilder(o, {d.name: dataclasses.asdict(d) for d in dbs})
+    got = p.route_dbs(names, prefixes)
+    for me in names:
+        assert got[me] == rb.build(me, prefixes), me
+
+
+def test_zero_metric_triangle():
+    """A 0-metric adjacency: the neighbour is at distance 0 and is its own
+    next hop; a node behind it ties with the direct 1-metric link."""
+    a = AdjDb("a", [create_adjacency("b", "a/b", "b/a", 0), create_adjacency("c", "a/c", "c/a", 1)], 1)
+    b = AdjDb("b", [create_adjacency("a", "b/a", "a/b", 0), create_adjacency("c", "b/c", "c/b", 1)], 2)
+    c = AdjDb("c", [create_adjacency("a", "c/a", "a/c", 1), create_adjacency("b", "c/b", "b/c", 1)], 3)
+    stream = AdjDbStream.from_dbs([a, b, c])
+    o, p = Oracle(), LinkState()
+    assert o.apply(stream) == p.apply(stream)
+    res = p.spf("a")
+    assert res == parse_spf_text(o.spf_text("a", True))
+    assert res["b"][0] == 0 and set(res["b"][1]) == {"b"}
+    assert res["c"][0] == 1 and set(res["c"][1]) == {"b", "c"}
