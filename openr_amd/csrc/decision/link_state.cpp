@@ -312,33 +312,6 @@ LinkStateChange LinkState::deleteAdjacencyDatabase(const std::string& node) {
 }
 
 // ---------------------------------------------------------------- snapshot
-namespace {
-// run f(lo, hi) over [0, n) in chunks of 512 handed out to up to 16 threads
-// (rows differ in length by 1000x: spines vs racks)
-template <class F>
-void parallelRows(uint32_t n, F&& f) {
-  constexpr uint32_t kChunk = 512;
-  const uint32_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  const uint32_t nt = std::max(1u, std::min(hw, n / (4 * kChunk)));
-  if (nt == 1) {
-    f(0u, n);
-    return;
-  }
-  std::atomic<uint32_t> next{0};
-  auto work = [&] {
-    for (;;) {
-      const uint32_t lo = next.fetch_add(kChunk);
-      if (lo >= n) return;
-      f(lo, std::min(n, lo + kChunk));
-    }
-  };
-  std::vector<std::thread> th;
-  th.reserve(nt - 1);
-  for (uint32_t t = 1; t < nt; ++t) th.emplace_back(work);
-  work();
-  for (auto& x : th) x.join();
-}
-}  // namespace
 
 // Rows in parallel (threads over node ranges; the link sets are only read):
 // 1. each row gathers its links (neighbour id, linksFromNode position, metric
@@ -377,7 +350,7 @@ const LinkState::Csr& LinkState::snapshot() {
   std::vector<uint32_t> nfirst(V + 1, 0);
   std::vector<uint8_t> rowBad(V, 0);
   std::vector<uint64_t> rowMax(V, 0);
-  parallelRows(V, [&](uint32_t lo, uint32_t hi) {
+  parallelFor(V, [&](uint32_t lo, uint32_t hi) {
     for (uint32_t u = lo; u < hi; ++u) {
       const std::string& un = c.names[u];
       c.noTransit[u] = isNodeOverloaded(un) ? 1 : 0;
@@ -429,7 +402,7 @@ const LinkState::Csr& LinkState::snapshot() {
   lap("gather");
   const size_t E = c.rowPtr[V];
   c.links.resize(nfirst[V]);
-  parallelRows(V, [&](uint32_t lo, uint32_t hi) {
+  parallelFor(V, [&](uint32_t lo, uint32_t hi) {
     for (uint32_t u = lo; u < hi; ++u) {
       uint32_t lid = nfirst[u];
       for (auto& e : rows[u]) {
@@ -448,7 +421,7 @@ const LinkState::Csr& LinkState::snapshot() {
   c.linkRank.resize(E);
   c.edgeUp.resize(E);
   std::vector<uint32_t> side(c.links.size() * 2, kInf);
-  parallelRows(V, [&](uint32_t lo, uint32_t hi) {
+  parallelFor(V, [&](uint32_t lo, uint32_t hi) {
     for (uint32_t u = lo; u < hi; ++u) {
       auto& row = rows[u];
       std::sort(row.begin(), row.end(), [](const Ent& a, const Ent& b) {
@@ -467,7 +440,7 @@ const LinkState::Csr& LinkState::snapshot() {
       }
     }
   });
-  parallelRows(V, [&](uint32_t lo, uint32_t hi) {
+  parallelFor(V, [&](uint32_t lo, uint32_t hi) {
     for (size_t e = c.rowPtr[lo]; e < c.rowPtr[hi]; ++e) {
       const uint32_t lid = c.linkId[e];
       const uint32_t mine = side[lid * 2ull] == e ? 0u : 1u;
@@ -592,22 +565,33 @@ SpfResult LinkState::buildResult(const RawRun& run, const uint32_t* nh, uint32_t
     const uint32_t v = csr_.col[e];
     if (v != run.root && (nbrs.empty() || nbrs.back() != v)) nbrs.push_back(v);
   }
-  res.reserve(V);
-  for (uint32_t v = 0; v < V; ++v) {
-    if (run.dist[v] == kInf) continue;
-    NodeSpfResult r(run.dist[v]);
-    const uint32_t* bits = nh + (size_t)v * W;
-    for (uint32_t w = 0; w < W; ++w) {
-      uint32_t b = bits[w];
-      while (b) {
-        const uint32_t i = w * 32 + (uint32_t)__builtin_ctz(b);
-        b &= b - 1;
-        r.nextHops_.insert(csr_.names[nbrs.at(i)]);
+  // node records built on host threads (next-hop sets, pathLinks), then moved
+  // into the name-keyed map
+  std::vector<uint32_t> reached;
+  reached.reserve(V);
+  for (uint32_t v = 0; v < V; ++v)
+    if (run.dist[v] != kInf) reached.push_back(v);
+  std::vector<NodeSpfResult> recs;
+  recs.reserve(reached.size());
+  for (const uint32_t v : reached) recs.emplace_back(run.dist[v]);
+  parallelFor((uint32_t)reached.size(), [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t k = lo; k < hi; ++k) {
+      const uint32_t v = reached[k];
+      NodeSpfResult& r = recs[k];
+      const uint32_t* bits = nh + (size_t)v * W;
+      for (uint32_t w = 0; w < W; ++w) {
+        uint32_t b = bits[w];
+        while (b) {
+          const uint32_t i = w * 32 + (uint32_t)__builtin_ctz(b);
+          b &= b - 1;
+          r.nextHops_.insert(csr_.names[nbrs.at(i)]);
+        }
       }
+      r.pathLinks_ = pathLinksOf(run, v, useLinkMetric);
     }
-    r.pathLinks_ = pathLinksOf(run, v, useLinkMetric);
-    res.emplace(csr_.names[v], std::move(r));
-  }
+  }, 1024);
+  res.reserve(reached.size());
+  for (size_t k = 0; k < reached.size(); ++k) res.emplace(csr_.names[reached[k]], std::move(recs[k]));
   return res;
 }
 

@@ -16,8 +16,12 @@
 // those arrays on demand.
 #pragma once
 
+#include <algorithm>
+#include <atomic>
 #include <cstdint>
+#include <exception>
 #include <memory>
+#include <thread>
 #include <optional>
 #include <stdexcept>
 #include <string>
@@ -31,6 +35,40 @@
 namespace odl {
 
 using Metric = uint64_t;
+
+// Run f(lo, hi) over [0, n) in chunks handed out to up to 16 host threads
+// (rows differ in length by 1000x: spines vs racks). The first exception a
+// chunk throws is rethrown on the calling thread after every thread joined.
+template <class F>
+void parallelFor(uint32_t n, F&& f, uint32_t chunk = 512) {
+  const uint32_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const uint32_t nt = std::max(1u, std::min(hw, n / (4 * chunk)));
+  if (nt == 1) {
+    f(0u, n);
+    return;
+  }
+  std::atomic<uint32_t> next{0};
+  std::exception_ptr err;
+  std::atomic<bool> failed{false};
+  auto work = [&] {
+    for (;;) {
+      const uint32_t lo = next.fetch_add(chunk);
+      if (lo >= n || failed.load()) return;
+      try {
+        f(lo, std::min(n, lo + chunk));
+      } catch (...) {
+        if (!failed.exchange(true)) err = std::current_exception();
+        return;
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  th.reserve(nt - 1);
+  for (uint32_t t = 1; t < nt; ++t) th.emplace_back(work);
+  work();
+  for (auto& x : th) x.join();
+  if (err) std::rethrow_exception(err);
+}
 
 struct Adjacency {
   std::string otherNodeName, ifName, otherIfName;

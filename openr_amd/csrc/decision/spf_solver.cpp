@@ -266,11 +266,25 @@ std::optional<RouteDb> SpfSolver::buildRouteDb(const std::string& me,
   const auto& dbs = ls_.getAdjacencyDatabases();
   if (!dbs.count(me)) return std::nullopt;
   RouteDb db;
-  for (const auto& pr : prefixes) {
-    auto r = prefixRoute(me, pr, opt);
-    if (!r) continue;
-    if (!db.unicast.emplace(pr.prefix, std::move(*r)).second)
-      throw std::invalid_argument("duplicate prefix " + pr.prefix);
+  // The SP prefixes read only the memoised SPF of `me` (and const link
+  // state): they are built on host threads. A prefix with a KSP2 entry runs
+  // getKthPaths, which fills a memo, so those are built on this thread.
+  ls_.getSpfResult(me);
+  std::vector<std::optional<UnicastRoute>> routes(prefixes.size());
+  std::vector<uint32_t> sp, ksp;
+  for (uint32_t i = 0; i < prefixes.size(); ++i) {
+    bool k = false;
+    for (const auto& e : prefixes[i].entries) k |= e.algo == 1;
+    (k ? ksp : sp).push_back(i);
+  }
+  parallelFor((uint32_t)sp.size(), [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t j = lo; j < hi; ++j) routes[sp[j]] = prefixRoute(me, prefixes[sp[j]], opt);
+  }, 256);
+  for (const uint32_t i : ksp) routes[i] = prefixRoute(me, prefixes[i], opt);
+  for (uint32_t i = 0; i < prefixes.size(); ++i) {
+    if (!routes[i]) continue;
+    if (!db.unicast.emplace(prefixes[i].prefix, std::move(*routes[i])).second)
+      throw std::invalid_argument("duplicate prefix " + prefixes[i].prefix);
   }
   // node-label routes (:501-598): on a label collision the smallest node name
   // keeps it (the reference's `iter->second.first < nodeName` rule, in any
@@ -280,8 +294,18 @@ std::optional<RouteDb> SpfSolver::buildRouteDb(const std::string& me,
     names.reserve(dbs.size());
     for (const auto& kv : dbs) names.push_back(kv.first);
     std::sort(names.begin(), names.end());
+    // candidate routes of every labelled node, on host threads
+    std::vector<std::vector<NextHop>> cand(names.size());
+    parallelFor((uint32_t)names.size(), [&](uint32_t lo, uint32_t hi) {
+      for (uint32_t j = lo; j < hi; ++j) {
+        const int32_t top = dbs.at(names[j]).nodeLabel;
+        if (top != 0 && isMplsLabelValid(top) && names[j] != me)
+          cand[j] = nodeLabelRoute(me, names[j]);
+      }
+    }, 256);
     std::map<int32_t, std::pair<std::string, std::vector<NextHop>>> labelToNode;
-    for (const auto& node : names) {
+    for (size_t j = 0; j < names.size(); ++j) {
+      const std::string& node = names[j];
       const int32_t top = dbs.at(node).nodeLabel;
       if (top == 0 || !isMplsLabelValid(top)) continue;
       auto it = labelToNode.find(top);
@@ -292,9 +316,8 @@ std::optional<RouteDb> SpfSolver::buildRouteDb(const std::string& me,
         labelToNode[top] = {me, {pop}};
         continue;
       }
-      std::vector<NextHop> nhs = nodeLabelRoute(me, node);
-      if (nhs.empty()) continue;
-      labelToNode[top] = {node, std::move(nhs)};
+      if (cand[j].empty()) continue;
+      labelToNode[top] = {node, std::move(cand[j])};
     }
     for (auto& kv : labelToNode) db.mpls.emplace(kv.first, std::move(kv.second.second));
   }

@@ -88,3 +88,24 @@ def test_zero_metric_triangle():
     assert res == parse_spf_text(o.spf_text("a", True))
     assert res["b"][0] == 0 and set(res["b"][1]) == {"b"}
     assert res["c"][0] == 1 and set(res["c"][1]) == {"b", "c"}
+
+
+def test_threaded_route_build_matches_restatement():
+    """2,500 nodes: the prefix and node-label routes are built on host
+    threads (parallelFor chunks of 256); same result as the restatement."""
+    from openr_amd import topology as T
+    st = T.grid(50, weighted_seed=5, max_metric=9)
+    dbs = st.to_dbs()
+    dbs[7].adjs[0].metric = 0  # host-metric mode: no GPU needed
+    stream = AdjDbStream.from_dbs(dbs)
+    o, p = OracleLS(), LinkState()
+    o.apply(stream)
+    p.apply(stream)
+    prefixes = {f"p{d.name}": [[d.name, "ip", "ecmp", 0, None]] for d in dbs}
+    prefixes["anycast"] = [["3", "ip", "ecmp", 0, None], ["2400", "ip", "ecmp", 0, None]]
+    rb = RouteBuilder(o, {d.name: dataclasses.asdict(d) for d in dbs})
+    mes = ["0", "1234", "2499"]
+    got = p.route_dbs(mes, prefixes)
+    for me in mes:
+        assert got[me] == rb.build(me, prefixes), me
+        assert sum(1 for k in got[me] if k[0] == "U") == 2500
