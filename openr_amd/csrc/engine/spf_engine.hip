@@ -37,6 +37,9 @@ struct ospf_ctx {
   uint32_t max_dn = 0;
   uint32_t depth_bound = 2;  // BFS levels any root can reach (unit metric / hop count)
   uint32_t exact_bound = 2;  // depth_bound as last computed in full (patches may raise depth_bound)
+  // >= every shortest distance: sum over nodes of the largest usable out-metric
+  // (a simple path leaves each node once); patches only add to it
+  uint64_t dist_bound = 0;
   std::vector<uint32_t> h_lvl;  // scratch of transit_detour (all UINT32_MAX between calls)
   // scratch
   // scratch per stream: batches queued on different streams run concurrently
@@ -788,9 +791,11 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   std::vector<uint32_t> dn;
   dn.reserve(E);
   uint32_t max_deg = 0, max_metric = 0, max_dn = 0, n_links = 0;
+  uint64_t dist_bound = 0;
   bool unit = true;
   for (uint32_t u = 0; u < V; ++u) {
     const uint32_t b = csr->row_ptr[u], e1 = csr->row_ptr[u + 1];
+    uint32_t row_max = 0;
     if (e1 < b || e1 > E) return fail(c, OSPF_E_INVAL, "row_ptr not monotone");
     max_deg = std::max(max_deg, e1 - b);
     dn_off[u] = (uint32_t)dn.size();
@@ -811,12 +816,14 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
         if (csr->metric[e] == 0)
           return fail(c, OSPF_E_RANGE, "metric 0 on a usable link is outside the engine contract");
         max_metric = std::max(max_metric, csr->metric[e]);
+        row_max = std::max(row_max, csr->metric[e]);
         unit &= csr->metric[e] == 1;
       }
       if (e < t) ++n_links;
       if (v != u && (e == b || csr->col[e - 1] != v)) dn.push_back(v);
     }
     max_dn = std::max<uint32_t>(max_dn, (uint32_t)dn.size() - dn_off[u]);
+    dist_bound += row_max;
     if (csr->no_transit && csr->no_transit[u]) nt[u >> 5] |= 1u << (u & 31);
   }
   dn_off[V] = (uint32_t)dn.size();
@@ -963,6 +970,7 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   c->info.unit_metric = unit ? 1u : 0u;
   c->info.version = version;
   c->info.device_bytes = tot;
+  c->dist_bound = dist_bound;
   c->loaded = true;
   return OSPF_OK;
 }
@@ -1042,8 +1050,8 @@ int ospf_run_batch_dev(ospf_ctx* c, const ospf_batch* b, void* stream) {
   if (ign && max_ignored > OSPF_MAX_IGNORED_PER_RUN)
     return fail(c, OSPF_E_RANGE, "max_ignored above OSPF_MAX_IGNORED_PER_RUN");
   const uint64_t V = c->info.n_nodes;
-  if (!hop && (uint64_t)c->info.max_metric * (V - 1) >= 0xFFFFFFFFull)
-    return fail(c, OSPF_E_RANGE, "u32 distance overflow possible (max_metric * (V-1))");
+  if (!hop && c->dist_bound >= 0xFFFFFFFFull)
+    return fail(c, OSPF_E_RANGE, "u32 distance overflow possible (sum of per-node max metrics)");
   const bool unit = hop || c->info.unit_metric;
 
   const Plan p = make_plan(c, nh_words, ign ? std::max<uint32_t>(max_ignored, 1) : 0, unit, n_roots);
@@ -1145,8 +1153,100 @@ int ospf_sync(ospf_ctx* c, void* stream) {
                 (err & 1u) ? "a root has more distinct neighbours than 32*nh_words"
                 : (err & 2u) ? "a run's ignore list exceeds max_ignored"
                 : (err & 8u) ? "a BFS level past the graph's depth bound was reached"
+                : (err & 16u) ? "derive: a root or a usable neighbour has no level row"
+                : (err & 64u) ? "a device root id is out of range"
                              : "internal: a frontier entry out of range");
   }
+  return OSPF_OK;
+}
+
+// ---------------------------------------------------------------- derive
+// All-sources next hops in two phases (spf_msbfs.hip "derive"): distances of
+// every root by the distance-only multi-source BFS (no bit-planes, one
+// traversal per 64 roots whatever their width), written as dist rows and as
+// byte level rows; then each root's next-hop words from its neighbours'
+// level rows. Unit metric or hop count, depth bound <= 253.
+int ospf_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t flags,
+                    uint32_t* d_dist, uint8_t* d_lev, void* stream) {
+  if (!c) return OSPF_E_INVAL;
+  if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  if (n == 0) return OSPF_OK;
+  if (!d_roots || !d_lev) return fail(c, OSPF_E_INVAL, "null roots / level rows");
+  if (!(flags & OSPF_HOP_COUNT) && !c->info.unit_metric)
+    return fail(c, OSPF_E_RANGE, "level rows need unit metric or hop count");
+  if (c->depth_bound > 253) return fail(c, OSPF_E_RANGE, "depth bound above 253 (byte levels)");
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t V = c->info.n_nodes, lmax = c->depth_bound + 2;
+  const size_t per_vb = align_up((size_t)V * 8ull * 6 + V * 64ull + lmax * 8ull, 256);
+  uint32_t nb_cap = 96;
+  if (const char* e = getenv("OSPF_MS_NB")) nb_cap = std::max(1, atoi(e));
+  nb_cap = (uint32_t)std::max<size_t>(1, std::min<size_t>(nb_cap, (6ull << 30) / per_vb));
+  const uint32_t total_vb = (n + 63) / 64;
+  const uint32_t nb_max = std::min(nb_cap, total_vb);
+  int rc = OSPF_OK;
+  char* sp = stream_scratch(c, s, per_vb * nb_max, &rc);
+  if (rc) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  uint32_t push_div = 8;
+  if (const char* e = getenv("OSPF_MS_PUSH_DIV")) push_div = (uint32_t)std::max(0, atoi(e));
+  ospf::MsArgs a{};
+  a.roots = d_roots;
+  a.n = n;
+  a.W = 1u << 26;  // no next-hop words: every root width passes the init check
+  a.npass = 1;
+  a.R = 64;
+  a.PP = a.OW = 1;
+  a.rep = 1;
+  a.lmax = lmax;
+  a.dbound = c->depth_bound;
+  a.kcap = 0xFFFFFFFFu;
+  a.push_div = push_div;
+  a.defer = 1;
+  a.merged = 0;
+  a.err = c->d_err;
+  a.dist = d_dist;
+  a.levrow = d_lev;
+  for (uint32_t vb0 = 0; vb0 < total_vb; vb0 += nb_max) {
+    a.vb0 = vb0;
+    a.nb = std::min(nb_max, total_vb - vb0);
+    a.front = (uint64_t*)sp;
+    a.seen = a.front + 4ull * a.nb * V;
+    a.accb = a.seen + (size_t)a.nb * V;
+    a.planes = nullptr;
+    a.lev = (uint8_t*)(a.accb + (size_t)a.nb * V);
+    a.found = (uint32_t*)(a.lev + (size_t)a.nb * V * 64ull);
+    a.mass = a.found + (size_t)a.nb * lmax;
+    HIPCHK(c, hipMemsetAsync(sp, 0, (size_t)a.nb * V * 8ull * 6 + (size_t)a.nb * V * 64ull +
+                                        (size_t)a.nb * lmax * 8ull, s));
+    hipError_t e = ospf::launch_msbfs_levels(c->g, a, c->depth_bound, s);
+    if (e != hipSuccess) return hip_fail(c, e, "launch_msbfs_levels");
+  }
+  c->spf_runs += n;
+  return OSPF_OK;
+}
+
+int ospf_nh_derive_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t nh_words,
+                       const uint8_t* d_lev, const uint32_t* d_lev_pos, uint32_t* d_nh,
+                       ospf_digest* d_digest, void* stream) {
+  if (!c) return OSPF_E_INVAL;
+  if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  if (n == 0) return OSPF_OK;
+  if (!d_roots || !d_lev || !d_lev_pos || !d_nh) return fail(c, OSPF_E_INVAL, "null argument");
+  if (nh_words == 0 || nh_words > 64) return fail(c, OSPF_E_RANGE, "derive: nh_words 1..64");
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (d_digest) HIPCHK(c, hipMemsetAsync(d_digest, 0, (size_t)n * sizeof(ospf_digest), s));
+  ospf::DeriveArgs d{};
+  d.roots = d_roots;
+  d.n = n;
+  d.W = nh_words;
+  d.lev = d_lev;
+  d.pos = d_lev_pos;
+  d.nh = d_nh;
+  d.digest = d_digest;
+  d.err = c->d_err;
+  hipError_t e = ospf::launch_nh_derive(c->g, d, s);
+  if (e != hipSuccess) return hip_fail(c, e, "launch_nh_derive");
   return OSPF_OK;
 }
 
@@ -1237,8 +1337,8 @@ int ospf_ksp2_dev(ospf_ctx* c, const ospf_ksp2* k, void* stream) {
   if (k->path_cap < 2 || k->path_cap > OSPF_MAX_IGNORED_PER_RUN)
     return fail(c, OSPF_E_INVAL, "path_cap out of range");
   const uint64_t V = c->info.n_nodes;
-  if ((uint64_t)c->info.max_metric * (V - 1) >= 0xFFFFFFFFull)
-    return fail(c, OSPF_E_RANGE, "u32 distance overflow possible (max_metric * (V-1))");
+  if (c->dist_bound >= 0xFFFFFFFFull)
+    return fail(c, OSPF_E_RANGE, "u32 distance overflow possible (sum of per-node max metrics)");
   return run_ksp2(c, k, (hipStream_t)stream);
 }
 
@@ -1417,6 +1517,8 @@ int ospf_update_links(ospf_ctx* c, const ospf_link_update* u, uint32_t n, uint64
     else c->depth_bound += grow;
   }
   refresh_graph_stats(c, new_max, deeper);
+  for (uint32_t i = 0; i < n; ++i)
+    if (u[i].up) c->dist_bound += (uint64_t)u[i].metric_lo + u[i].metric_hi;
   c->info.version = version;
   return OSPF_OK;
 }

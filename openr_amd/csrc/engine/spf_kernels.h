@@ -185,7 +185,25 @@ struct MsArgs {
   uint32_t* igb;          // [nb][igw]
   uint64_t* igm;          // [nb][E]
   uint32_t igw;
+  uint8_t* levrow;        // derive phase 1 (kp -1): [n][V] dist + 1 per (run, node)
 };
+
+// Derive phase 2 (nh_derive_kernel): next-hop words of n roots from the level
+// rows of their neighbours. pos[v] = level row of node v (0xFFFFFFFF: none).
+struct DeriveArgs {
+  const uint32_t* roots;
+  uint32_t n, W;
+  const uint8_t* lev;      // [rows][V]
+  const uint32_t* pos;     // [V]
+  uint32_t* nh;            // [n][V][W]
+  ospf_digest* digest;     // [n] (zeroed by the caller) or null
+  uint32_t* err;           // bit 1: K > 32 W, 16: a neighbour has no level row, 64: bad root
+  uint32_t tiles;          // set by the launcher
+};
+// phase 1: distances only (kp -1) + msbfs_levrows; phase 2: nh_derive
+hipError_t launch_msbfs_levels(const DevGraph& g, const MsArgs& a, uint32_t depth_bound,
+                               hipStream_t s);
+hipError_t launch_nh_derive(const DevGraph& g, const DeriveArgs& d, hipStream_t s);
 // kp = 8, 16 or 32 planes per node; depth_bound bounds the BFS level count
 hipError_t launch_msbfs_round(int kp, const DevGraph& g, const MsArgs& a, uint32_t depth_bound,
                               hipStream_t s);

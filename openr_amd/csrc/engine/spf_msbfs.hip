@@ -103,7 +103,7 @@ struct VB {
     valid = nv == 64u ? ~0ull : ((1ull << nv) - 1ull);
     seen = a.seen + (size_t)vbl * V;
     accb = a.accb + (size_t)vbl * V;
-    P = a.planes + (size_t)vbl * V * kp;
+    P = kp > 0 ? a.planes + (size_t)vbl * V * kp : nullptr;  // kp -1: distances only
     igb = kp == 0 ? a.igb + (size_t)vbl * a.igw : nullptr;
     igm = kp == 0 ? a.igm + (size_t)vbl * E : nullptr;
   }
@@ -177,6 +177,7 @@ __device__ __forceinline__ void emit_rows(const MsArgs& a, const VB& b, uint32_t
 
 template <int KP>
 __device__ __forceinline__ void load_planes(const uint64_t* P, uint32_t u, uint64_t* pu) {
+  if constexpr (KP <= 0) return;
   const uint4* q = reinterpret_cast<const uint4*>(P + (size_t)u * KP);
 #pragma unroll
   for (int k = 0; k < KP / 2; ++k) {
@@ -232,6 +233,10 @@ __global__ void __launch_bounds__(256) msbfs_init_kernel(DevGraph g, MsArgs a) {
   if (rix >= a.n) return;
   const uint32_t V = g.V;
   const uint32_t s = a.roots[rix];
+  if (s >= V) {  // device-side root list: never index past the graph
+    if (lane == 0) atomicOr(a.err, 64u);
+    return;
+  }
   const uint32_t nb0 = g.dn_off[s], nn = g.dn_off[s + 1] - nb0;
   if (nn > a.kcap || nn > 32u * a.W) {
     if (lane == 0) atomicOr(a.err, 1u);
@@ -265,7 +270,7 @@ __global__ void __launch_bounds__(256) msbfs_init_kernel(DevGraph g, MsArgs a) {
     const uint32_t lo = g.didx[e];  // index of v among s's distinct neighbours
     // plane of v in this pass (>= KP * PP, wrapped, when outside it)
     const uint32_t li = lo - 32u * a.OW * b.g;
-    const bool in = li < (uint32_t)KP * a.PP;
+    const bool in = KP > 0 && li < (uint32_t)KP * a.PP;
     const uint32_t k = li / a.PP, pb = (li % a.PP) * a.R + bit;  // plane word, bit
     const uint32_t kw = lo - 32u * b.g;  // unpacked (PP == 1) next-hop word bit
     or64(&b.seen[v], bm);
@@ -313,7 +318,7 @@ __device__ __forceinline__ void pull_scan(const DevGraph& g, const VB& b, const 
       const uint64_t f = (((uint64_t)fs[i].y << 32) | fs[i].x) & m & keep[i];
       if (!f) continue;
       acc |= f;
-      if (KP == 0) continue;
+      if (KP <= 0) continue;  // distances only (KSP2 reruns, derive mode)
       // roots whose tail has no plane bit in this pass add nothing to them
       const uint64_t fz = (((uint64_t)fs[i].w << 32) | fs[i].z) & f;
       if (!fz) continue;
@@ -802,6 +807,198 @@ __global__ void __launch_bounds__(256) msbfs_rows_multi_kernel(DevGraph g, MsArg
   }
 }
 
+// ---------------------------------------------------------------- derive
+// All-sources next hops from neighbour levels (unit metric / hop count).
+// Phase 1 (distances only, KP = -1): msbfs_levrows writes each batch's levels
+// as byte rows lev[run][node] = dist + 1 (0 = unreached) and the dist rows.
+// Phase 2 (nh_derive): the next hops of root r towards v are the distinct
+// neighbours n_k of r with an up link r-n_k, n_k transit or n_k == v, and
+// dist(n_k, v) = dist(r, v) - 1 -- exactly the reference's nextHops
+// (LinkState.cpp:885-901: a next hop n lies on a shortest r -> v path, whose
+// tail from n is a shortest n -> v path with transit intermediates, and
+// whose length is 1 + dist(n, v)). No bit-planes, one traversal per 64 roots
+// whatever their width, and the next-hop words are written once, whole.
+__global__ void __launch_bounds__(256) msbfs_levrows_kernel(DevGraph g, MsArgs a) {
+  __shared__ uint8_t s_lev[64 * 64];  // [node][root]
+  const uint32_t vbl = blockIdx.x % a.nb;
+  const VB b(a, vbl, g.V, -1);
+  const uint32_t V = g.V, tid = threadIdx.x;
+  const uint32_t v0 = (blockIdx.x / a.nb) * 64u, nv = min(64u, V - v0);
+  if (v0 == 0 && tid == 0 && a.found[vbl * a.lmax + a.dbound + 1]) atomicOr(a.err, 8u);
+  const uint32_t nr = min(a.R, a.n - b.rix0);
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(a.lev + ((size_t)vbl * V + v0) * 64u);
+    if (tid < nv * 4u) reinterpret_cast<uint4*>(s_lev)[tid] = src[tid];
+  }
+  __syncthreads();
+  const bool vec = (V & 3u) == 0 && nv == 64u;
+  for (uint32_t i = tid; i < 64u * 16u; i += kBlock) {  // (root, node quad)
+    const uint32_t r = i >> 4, q = i & 15u;
+    if (r >= nr) break;
+    uint32_t l[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) l[j] = (4u * q + j < nv) ? s_lev[(4u * q + j) * 64u + r] : 0u;
+    const size_t off = (size_t)(b.rix0 + r) * V + v0 + 4u * q;
+    if (a.dist) {
+      uint32_t* row = a.dist + off;
+      if (vec) {
+        *reinterpret_cast<uint4*>(row) = make_uint4(l[0] ? l[0] - 1u : kInf, l[1] ? l[1] - 1u : kInf,
+                                                    l[2] ? l[2] - 1u : kInf, l[3] ? l[3] - 1u : kInf);
+      } else {
+        for (uint32_t j = 0; j < 4u; ++j)
+          if (4u * q + j < nv) row[j] = l[j] ? l[j] - 1u : kInf;
+      }
+    }
+    if (vec) {
+      *reinterpret_cast<uint32_t*>(a.levrow + off) = l[0] | (l[1] << 8) | (l[2] << 16) | (l[3] << 24);
+    } else {
+      for (uint32_t j = 0; j < 4u; ++j)
+        if (4u * q + j < nv) a.levrow[off + j] = (uint8_t)l[j];
+    }
+  }
+}
+
+// Phase 2: block = (root i, tile of T = 1024 / S nodes); S threads per node
+// quad split the root's next-hop words. The root's neighbour table (level
+// row, flags) is staged in LDS; each (neighbour, quad) is one 4-B load of
+// four level bytes compared against the root's own four.
+constexpr uint32_t kDeriveMaxK = 2048;
+template <int S>
+__global__ void __launch_bounds__(256) nh_derive_kernel(DevGraph g, DeriveArgs d) {
+  __shared__ uint32_t s_pos[kDeriveMaxK];
+  __shared__ uint32_t s_nbr[kDeriveMaxK];
+  __shared__ uint8_t s_fl[kDeriveMaxK];  // bit 0: usable (an up link), bit 1: transit
+  __shared__ uint8_t s_own[1024 / S];
+  __shared__ uint64_t s_red[3 * kWavesPerBlock];
+  extern __shared__ uint32_t s_out[];  // [T][W]
+  constexpr uint32_t T = 1024u / S;
+  const uint32_t V = g.V, W = d.W, tid = threadIdx.x;
+  const uint32_t i = blockIdx.x / d.tiles, v0 = (blockIdx.x % d.tiles) * T;
+  const uint32_t nv = min(T, V - v0);
+  const uint32_t r = d.roots[i];
+  if (r >= V) {
+    if (tid == 0) atomicOr(d.err, 64u);
+    return;
+  }
+  const uint32_t nb0 = g.dn_off[r], K = g.dn_off[r + 1] - nb0;
+  const uint32_t own = d.pos[r];
+  if (K > kDeriveMaxK || K > 32u * W || own == kInf) {
+    if (tid == 0) atomicOr(d.err, own == kInf ? 16u : 1u);
+    return;
+  }
+  for (uint32_t k = tid; k < K; k += kBlock) {
+    const uint32_t n = g.dn[nb0 + k];
+    s_nbr[k] = n;
+    s_pos[k] = d.pos[n];
+    s_fl[k] = transit(g, n) ? 2u : 0u;
+  }
+  __syncthreads();
+  for (uint32_t e = g.row_ptr[r] + tid; e < g.row_ptr[r + 1]; e += kBlock) {
+    const uint32_t cx = g.colx[e];
+    if ((cx & kDown) || cx == r) continue;
+    const uint32_t k = g.didx[e];
+    if (k < K) s_fl[k] |= 1u;  // benign race: every writer sets the same bit
+  }
+  const uint8_t* orow = d.lev + (size_t)own * V;
+  for (uint32_t n = tid; n < T; n += kBlock) s_own[n] = n < nv ? orow[v0 + n] : 0u;
+  __syncthreads();
+  const bool vec = (V & 3u) == 0 && nv == T;
+  // a usable neighbour without a level row cannot be derived: error, zero bits
+  if (tid == 0 && v0 == 0) {
+    for (uint32_t k = 0; k < K; ++k)
+      if ((s_fl[k] & 1u) && s_pos[k] == kInf) {
+        atomicOr(d.err, 16u);
+        break;
+      }
+  }
+  const uint32_t q = tid / S, sub = tid % S, n0 = 4u * q;
+  uint32_t L[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) L[j] = s_own[n0 + j];
+  const bool any = (L[0] >= 2u) | (L[1] >= 2u) | (L[2] >= 2u) | (L[3] >= 2u);
+  for (uint32_t w = sub; w < W; w += S) {
+    uint32_t word[4] = {0u, 0u, 0u, 0u};
+    const uint32_t k0 = 32u * w, k1 = min(K, k0 + 32u);
+    if (any) {
+      for (uint32_t k = k0; k < k1; ++k) {
+        const uint32_t fl = s_fl[k], p = s_pos[k];
+        if (!(fl & 1u) || p == kInf) continue;
+        const uint8_t* nrow = d.lev + (size_t)p * V + v0 + n0;
+        uint32_t x4;
+        if (vec) {
+          x4 = *reinterpret_cast<const uint32_t*>(nrow);
+        } else {
+          x4 = 0;
+          for (uint32_t j = 0; j < 4u; ++j)
+            if (n0 + j < nv) x4 |= (uint32_t)nrow[j] << (8 * j);
+        }
+        const uint32_t nid = s_nbr[k];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t x = (x4 >> (8 * j)) & 0xFFu;
+          const bool ok = x != 0u && x + 1u == L[j] && ((fl & 2u) || nid == v0 + n0 + j);
+          word[j] |= (uint32_t)ok << (k - k0);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (n0 + j < T) s_out[(n0 + j) * W + w] = word[j];
+  }
+  __syncthreads();
+  // the tile's nv * W words are contiguous in the root's row
+  const uint32_t span = nv * W;
+  uint32_t* dst = d.nh + ((size_t)i * V + v0) * W;
+  if (vec && (((size_t)i * V + v0) * W & 3u) == 0 && (span & 3u) == 0) {
+    for (uint32_t x = tid; x < span / 4u; x += kBlock)
+      reinterpret_cast<uint4*>(dst)[x] = reinterpret_cast<const uint4*>(s_out)[x];
+  } else {
+    for (uint32_t x = tid; x < span; x += kBlock) dst[x] = s_out[x];
+  }
+  if (!d.digest) return;
+  uint64_t reached = 0, sumd = 0, h = 0;
+  for (uint32_t n = tid; n < nv; n += kBlock) {
+    const uint32_t l = s_own[n];
+    if (!l) continue;
+    const uint64_t kd = g.dkey[2ull * (v0 + n)], kn = g.dkey[2ull * (v0 + n) + 1];
+    reached += 1;
+    sumd += l - 1u;
+    uint64_t ws = 0;
+    for (uint32_t w = 0; w < W; ++w) {
+      const uint32_t word = s_out[n * W + w];
+      if (word) ws += digest_word_key(w, word);
+    }
+    h += kd * (uint64_t)l + kn * ws;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    reached += shfl_xor64(reached, o);
+    sumd += shfl_xor64(sumd, o);
+    h += shfl_xor64(h, o);
+  }
+  const uint32_t wave = tid >> 6;
+  if ((tid & 63u) == 0) {
+    s_red[3 * wave] = reached;
+    s_red[3 * wave + 1] = sumd;
+    s_red[3 * wave + 2] = h;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t rr = 0, sd = 0, hh = 0;
+    for (uint32_t x = 0; x < kWavesPerBlock; ++x) {
+      rr += s_red[3 * x];
+      sd += s_red[3 * x + 1];
+      hh += s_red[3 * x + 2];
+    }
+    ospf_digest* dg = d.digest + i;
+    if (rr) {
+      atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)rr);
+      atomicAdd((unsigned long long*)&dg->sum_dist, (unsigned long long)sd);
+    }
+    if (hh) atomicAdd((unsigned long long*)&dg->hash, (unsigned long long)hh);
+  }
+}
+
 // ---------------------------------------------------------------- digest
 // Digest of finished rows (runs whose rows are written per level): `segs`
 // workgroups per root, each over a node range, adding into a zeroed record.
@@ -987,6 +1184,39 @@ hipError_t launch_msbfs_round(int kp, const DevGraph& g, const MsArgs& a, uint32
     case 16: return launch_round_kp<16>(g, a, depth_bound, s);
     default: return launch_round_kp<32>(g, a, depth_bound, s);
   }
+}
+
+hipError_t launch_msbfs_levels(const DevGraph& g, const MsArgs& a, uint32_t depth_bound,
+                               hipStream_t s) {
+  const uint32_t init_blocks = (a.nb * a.R + kWavesPerBlock - 1) / kWavesPerBlock;
+  hipLaunchKernelGGL(msbfs_init_kernel<-1>, dim3(init_blocks), dim3(kBlock), 0, s, g, a);
+  const uint32_t chunks = (g.V + kBlock - 1) / kBlock;
+  const uint32_t bigblocks = (g.nbig + kWavesPerBlock - 1) / kWavesPerBlock;
+  for (uint32_t d = 1; d <= depth_bound; ++d) {
+    hipLaunchKernelGGL(msbfs_level_kernel<-1>, dim3(a.nb * (chunks + bigblocks)), dim3(kBlock), 0,
+                       s, g, a, d);
+    hipLaunchKernelGGL(msbfs_settle_kernel<-1>, dim3(a.nb * chunks), dim3(kBlock), 0, s, g, a, d);
+  }
+  hipLaunchKernelGGL(msbfs_levrows_kernel, dim3(a.nb * ((g.V + 63u) / 64u)), dim3(kBlock), 0, s, g,
+                     a);
+  return hipGetLastError();
+}
+
+hipError_t launch_nh_derive(const DevGraph& g, const DeriveArgs& d0, hipStream_t s) {
+  DeriveArgs d = d0;
+  if (d.n == 0) return hipSuccess;
+  if (d.W == 0 || d.W > kDeriveMaxK / 32u) return hipErrorInvalidValue;
+  const int S = d.W == 1 ? 1 : d.W == 2 ? 2 : 4;
+  const uint32_t T = 1024u / S;
+  d.tiles = (g.V + T - 1) / T;
+  const size_t lds = (size_t)T * d.W * 4u;
+  const dim3 grid(d.n * d.tiles);
+  switch (S) {
+    case 1: hipLaunchKernelGGL(nh_derive_kernel<1>, grid, dim3(kBlock), lds, s, g, d); break;
+    case 2: hipLaunchKernelGGL(nh_derive_kernel<2>, grid, dim3(kBlock), lds, s, g, d); break;
+    default: hipLaunchKernelGGL(nh_derive_kernel<4>, grid, dim3(kBlock), lds, s, g, d); break;
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_row_digest(const DevGraph& g, uint32_t n, const uint32_t* dist,

@@ -1,0 +1,127 @@
+"""Derive mode (ospf_levels_dev + ospf_nh_derive_dev): all-sources next hops
+from the neighbours' level rows must equal the per-batch engine path (and so
+the oracle-pinned results) bit for bit: dist rows, next-hop rows and digests,
+on unit-metric graphs with drained nodes, down and parallel links, on the
+fabric, and in hop-count mode on weighted graphs."""
+import numpy as np
+import pytest
+import torch
+
+from graphs import random_stream
+from oracle import Oracle
+from openr_amd import topology as T
+from openr_amd.adjdb import AdjDbStream
+from openr_amd.engine import Engine, EngineError
+from openr_amd.linkstate import LinkState
+
+pytestmark = pytest.mark.gpu
+
+
+def derive_all(eng, V, hop=False, roots=None):
+    dev = torch.device("cuda", 0)
+    all_ids = np.arange(V, dtype=np.uint32)
+    d_all = torch.from_numpy(all_ids.view(np.int32)).to(dev)
+    lev = torch.empty((V, V), dtype=torch.uint8, device=dev)
+    dist = torch.empty((V, V), dtype=torch.int32, device=dev)
+    eng.levels_dev(d_all.data_ptr(), V, lev.data_ptr(), d_dist=dist.data_ptr(), hop_count=hop)
+    pos = torch.from_numpy(all_ids.view(np.int32)).to(dev)
+    roots = all_ids if roots is None else np.asarray(roots, np.uint32)
+    words = np.array([eng.nh_words(int(r)) for r in roots])
+    out = {}
+    for W in sorted(set(words.tolist())):
+        grp = roots[words == W]
+        d_r = torch.from_numpy(grp.view(np.int32)).to(dev)
+        nh = torch.empty((grp.size, V, W), dtype=torch.int32, device=dev)
+        dg = torch.empty((grp.size, 3), dtype=torch.int64, device=dev)
+        eng.nh_derive_dev(d_r.data_ptr(), grp.size, W, lev.data_ptr(), pos.data_ptr(),
+                          nh.data_ptr(), d_digest=dg.data_ptr())
+        eng.sync()
+        out[W] = (grp, nh.cpu().numpy().view(np.uint32), dg.cpu().numpy().view(np.uint64))
+    eng.sync()
+    return dist.cpu().numpy().view(np.uint32), out
+
+
+def check_against_engine(stream, hop=False, roots=None):
+    ls = LinkState()
+    ls.apply(stream)
+    csr = ls.csr()
+    eng = Engine()
+    try:
+        eng.load(csr)
+        V = eng.V
+        dist, out = derive_all(eng, V, hop, roots)
+        for W, (grp, nh, dg) in out.items():
+            ref = eng.run(grp, W, hop_count=hop, want_digest=True)
+            assert np.array_equal(dist[grp], ref["dist"]), W
+            assert np.array_equal(nh, ref["nh"]), W
+            assert np.array_equal(dg, ref["digest"]), W
+    finally:
+        eng.close()
+    return ls
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_derive_random_unit_graphs(seed):
+    stream, _ = random_stream(seed, n=60, unit=True)
+    check_against_engine(stream)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_derive_hop_count_on_weighted_graphs(seed):
+    stream, _ = random_stream(100 + seed, n=50, wmax=30)
+    check_against_engine(stream, hop=True)
+
+
+def test_derive_fabric_with_drains():
+    st = T.fabric(pods=12, planes=8)
+    dbs = st.to_dbs()
+    for d in dbs:
+        if d.name in ("2-3-1", "3-5-7"):
+            d.overloaded = True
+        if d.name == "2-4-2":
+            d.adjs[0].overloaded = True
+    check_against_engine(AdjDbStream.from_dbs(dbs))
+
+
+def test_derive_wide_roots_and_digests_vs_oracle():
+    st = T.fabric(pods=70, planes=2)  # spines with 70 neighbours: 3 next-hop words
+    ls = check_against_engine(st)
+    o = Oracle(st)
+    names = ls.node_names()
+    roots = ["1-0-0", "2-7-1", "3-69-47"]
+    eng = Engine()
+    try:
+        eng.load(ls.csr())
+        _, out = derive_all(eng, eng.V, roots=[names.index(r) for r in roots])
+    finally:
+        eng.close()
+    got = {int(r): d for (grp, _, dg) in out.values() for r, d in zip(grp, dg)}
+    want = o.digests(roots)
+    for r, w in zip(roots, want):
+        assert np.array_equal(got[names.index(r)], w), r
+
+
+def test_derive_missing_neighbour_row_is_an_error():
+    st = T.fabric(pods=4, planes=2)
+    ls = LinkState()
+    ls.apply(st)
+    eng = Engine()
+    try:
+        eng.load(ls.csr())
+        V = eng.V
+        dev = torch.device("cuda", 0)
+        ids = np.arange(V, dtype=np.uint32)
+        d_all = torch.from_numpy(ids.view(np.int32)).to(dev)
+        lev = torch.empty((V, V), dtype=torch.uint8, device=dev)
+        eng.levels_dev(d_all.data_ptr(), V, lev.data_ptr())
+        pos = ids.copy()
+        pos[ls.node_names().index("2-0-0")] = 0xFFFFFFFF  # a neighbour of rack 3-0-0
+        d_pos = torch.from_numpy(pos.view(np.int32)).to(dev)
+        r = np.array([ls.node_names().index("3-0-0")], np.uint32)
+        d_r = torch.from_numpy(r.view(np.int32)).to(dev)
+        nh = torch.empty((1, V, 1), dtype=torch.int32, device=dev)
+        eng.nh_derive_dev(d_r.data_ptr(), 1, 1, lev.data_ptr(), d_pos.data_ptr(), nh.data_ptr())
+        with pytest.raises(EngineError):
+            eng.sync()
+    finally:
+        eng.close()
