@@ -157,6 +157,10 @@ def main():
                     help="profiling mode: launch only the class with this neighbour capacity "
                          "(8, 16, or 32 x next-hop words)")
     ap.add_argument("--reps", type=int, default=3, help="launches in --class-only mode")
+    ap.add_argument("--mode", choices=["auto", "derive", "batch"], default="auto",
+                    help="derive: all-sources next hops from neighbour level rows (unit "
+                         "metric, every root's neighbours in the sweep); batch: per-class "
+                         "engine batches (bit-plane next hops); auto = derive when it applies")
     ap.add_argument("--dist-parity", type=int, default=0,
                     help="N>1: rank 0 checks the gathered digests of the last timed step "
                          "for this many roots against the CPU restatement")
@@ -195,6 +199,14 @@ def main():
     flags = N.OSPF_WANT_DIST | N.OSPF_WANT_DIGEST | (0 if args.no_nh else N.OSPF_WANT_NH)
     perm = np.random.default_rng(SEED).permutation(V).astype(np.uint32)
     n_roots = default_roots if args.roots < 0 else args.roots
+    derive_ok = (n_roots <= 0 and not weighted and args.roots_per_gpu == 0 and not args.no_nh
+                 and not args.class_only and eng.info().unit_metric
+                 and int(shard.distinct_neighbors(csr["row_ptr"], csr["col"]).max()) <= 2048)
+    if args.mode == "derive" and not derive_ok:
+        raise SystemExit("derive mode needs an all-sources unit-metric sweep (strong scaling)")
+    if args.mode != "batch" and derive_ok:
+        return derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, dev,
+                           backend, coll_dev)
     pool = perm if n_roots <= 0 else perm[: min(n_roots, V)]
     nbrs = shard.distinct_neighbors(csr["row_ptr"], csr["col"])
     key = shard.first_neighbor(csr["row_ptr"], csr["col"]) if args.root_order != "random" \
@@ -314,8 +326,6 @@ def main():
                     step_digest[int(root)] = d[j]
 
     roots_total = world * B * args.steps if weak else pool.size * args.steps
-    spf_s = roots_total / dt
-    gteps = roots_total * E / dt / 1e9
 
     # roofline. The classes overlap on their streams inside the timed steps,
     # so each class is then timed ALONE (not part of `value`): R launches on
@@ -378,6 +388,221 @@ def main():
                 "(rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/<round>/pmc_traffic.json)",
     }
 
+    classes_cfg = [{"cap": c.cap, "nh_words": c.nh_words, "roots_this_rank": c.extra["n"],
+                    **{kk: c.extra["plan"][kk] for kk in ("variant", "slices", "block")},
+                    "avg_launch_ms": round(float(np.mean(c.extra["ms"])), 3),
+                    "isolated_launch_ms": round(c.extra["iso_ms"], 3)} for c in classes]
+    report(args, stream, names, pool, step_digest, dt, roots_total, E, desc, n_roots, V, world,
+           rank, dist_on, backend, int(world * B if weak else pool.size), classes_cfg, roofline,
+           "weak" if weak else "strong", "batch")
+    if dist_on:
+        torch.distributed.destroy_process_group()
+
+
+def derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, dev, backend,
+                coll_dev):
+    """All-sources step in derive mode (spf_msbfs.hip "derive"). Phase 1:
+    ospf_levels_dev over this rank's closure (its roots + their neighbours):
+    dist rows + byte level rows, one distance-only traversal per 64 roots.
+    Phase 2: ospf_nh_derive_dev per width class: next-hop rows + digests of
+    this rank's roots from the level rows. Ranks own the racks + fabric
+    switches of a block of pods and the spines of a block of planes (fabric
+    names; other graphs: slices of each width class)."""
+    rp, col = csr["row_ptr"], csr["col"]
+    perm = np.random.default_rng(SEED).permutation(V).astype(np.uint32)
+    key = shard.first_neighbor(rp, col)
+    caps = shard.neighbor_caps(shard.distinct_neighbors(rp, col))
+    all_caps = sorted(set(caps.tolist()))
+
+    def part(r):
+        if world == 1:
+            return perm
+        fp = shard.fabric_partition(names, world, r)
+        if fp is not None:
+            return fp
+        cls = shard.make_classes(perm, caps, V, key)
+        return np.concatenate([c.roots[slice(*shard.rank_slice(c.roots.size, world, r))]
+                               for c in cls])
+
+    parts = [part(r) for r in range(world)]
+    cls_all = [{cap: shard.locality_order(p[caps[p] == cap], key) for cap in all_caps}
+               for p in parts]
+    mine = parts[rank]
+    clo = shard.locality_order(shard.closure(mine, rp, col), key)
+    pos = np.full(V, 0xFFFFFFFF, np.uint32)
+    pos[clo] = np.arange(clo.size, dtype=np.uint32)
+    t0 = time.time()
+    d_clo = torch.from_numpy(clo.view(np.int32)).to(dev)
+    d_pos = torch.from_numpy(pos.view(np.int32)).to(dev)
+    lev = torch.empty((clo.size, V), dtype=torch.uint8, device=dev)
+    dist = torch.empty((clo.size, V), dtype=torch.int32, device=dev)
+    ldg = torch.empty((clo.size, 3), dtype=torch.int64, device=dev)
+    classes = []
+    for cap in all_caps:
+        roots = cls_all[rank][cap]
+        W = max(1, cap // 32) if cap > 16 else 1
+        slot = max(1, max(c[cap].size for c in cls_all))
+        classes.append(dict(cap=cap, W=W, roots=roots, n=int(roots.size),
+                            d=torch.from_numpy(roots.view(np.int32)).to(dev),
+                            nh=torch.empty((max(1, roots.size), V, W), dtype=torch.int32,
+                                           device=dev),
+                            dig=torch.zeros((slot, 3), dtype=torch.int64, device=dev),
+                            stream=torch.cuda.Stream(device=dev), ms=[]))
+    log(f"[rank {rank}] derive: {mine.size} roots, closure {clo.size}, buffers "
+        f"{(lev.numel() + dist.numel() * 4 + sum(c['nh'].numel() * 4 for c in classes)) / 2**30:.1f}"
+        f" GiB in {time.time() - t0:.1f}s")
+    main_s = torch.cuda.current_stream()
+
+    def phase1(s_):
+        eng.levels_dev(d_clo.data_ptr(), clo.size, lev.data_ptr(), d_dist=dist.data_ptr(),
+                       d_lev_digest=ldg.data_ptr(), stream=s_.cuda_stream)
+
+    def phase2(c, s_):
+        if c["n"]:
+            eng.nh_derive_dev(c["d"].data_ptr(), c["n"], c["W"], lev.data_ptr(), d_pos.data_ptr(),
+                              c["nh"].data_ptr(), d_lev_digest=ldg.data_ptr(),
+                              d_digest=c["dig"].data_ptr(), max_root_neighbors=c["cap"],
+                              stream=s_.cuda_stream)
+
+    p1_ms = []
+
+    def step(timed):
+        a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a_.record(main_s)
+        phase1(main_s)
+        b_.record(main_s)
+        done = []
+        for c in sorted(classes, key=lambda c: -c["W"] * c["n"]):
+            cs = c["stream"]
+            cs.wait_event(b_)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(cs)
+            phase2(c, cs)
+            e1.record(cs)
+            done.append(e1)
+            if timed:
+                c["ms"].append((e0, e1))
+        for e in done:
+            main_s.wait_event(e)
+        if timed:
+            p1_ms.append((a_, b_))
+        if dist_on:
+            for c in classes:
+                c["gathered"] = shard.gather_digests(c["dig"])
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    eng.sync(main_s.cuda_stream)
+    if dist_on:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if dist_on:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t_start
+    eng.sync(main_s.cuda_stream)
+    if dist_on:
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+
+    # digests of the last timed step by root id (rank 0 sees every rank's)
+    step_digest = {}
+    for c in classes:
+        if dist_on:
+            g = c["gathered"].cpu().numpy().view(np.uint64).reshape(world, -1, 3)
+            for r in range(world):
+                for j, root in enumerate(cls_all[r][c["cap"]]):
+                    step_digest[int(root)] = g[r, j]
+        else:
+            d = c["dig"].cpu().numpy().view(np.uint64)
+            for j, root in enumerate(c["roots"]):
+                step_digest[int(root)] = d[j]
+
+    # isolated launches (alone on one stream, HIP events on it): phase 1 and
+    # each class's phase 2; the roofline of the dominant one
+    iso_s = torch.cuda.Stream(device=dev)
+
+    def iso(fn):
+        ms = []
+        with torch.cuda.stream(iso_s):
+            for _ in range(args.iso_reps + 1):
+                a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a_.record(iso_s)
+                fn(iso_s)
+                b_.record(iso_s)
+                b_.synchronize()
+                ms.append(a_.elapsed_time(b_))
+        return float(np.median(ms[1:])) if len(ms) > 1 else float(ms[0])
+
+    p1_iso = iso(phase1)
+    for c in classes:
+        c["iso_ms"] = iso(lambda s_, c=c: phase2(c, s_)) if c["n"] else 0.0
+    eng.sync(iso_s.cuda_stream)
+    scans = -(-clo.size // 64) * (4 * E + 4 * (V + 1))
+    units = [{"launch": "levels", "kernel": "ospf_levels_dev (distance-only multi-source BFS: "
+              "msbfs init + level/settle pairs + levrows)", "roots_per_launch": int(clo.size),
+              "isolated_launch_ms": round(p1_iso, 3),
+              "compulsory_bytes": int(clo.size) * 4 * V + scans,
+              "traffic": pmc_traffic(args.profile_dir, "derive_levels", int(clo.size))}]
+    for c in classes:
+        if c["n"]:
+            units.append({"launch": f"derive_cap{c['cap']}",
+                          "kernel": f"ospf_nh_derive_dev (nh_derive_kernel, {c['W']} next-hop "
+                                    f"word(s))", "cap": c["cap"], "nh_words": c["W"],
+                          "roots_per_launch": c["n"], "isolated_launch_ms": round(c["iso_ms"], 3),
+                          "compulsory_bytes": c["n"] * 4 * V * c["W"],
+                          "traffic": pmc_traffic(args.profile_dir, f"derive_cap{c['cap']}", c["n"])})
+    for u in units:
+        sec = u["isolated_launch_ms"] / 1e3
+        u["achieved"] = round(u["compulsory_bytes"] / sec / 1e9, 1)
+        u["frac"] = round(u["compulsory_bytes"] / sec / 1e9 / HBM_PEAK_GBS, 4)
+        u["traffic_over_compulsory"] = (round(u["traffic"] / u["compulsory_bytes"], 2)
+                                        if u["traffic"] else None)
+    dom = max(units, key=lambda u: u["isolated_launch_ms"])
+    step_comp = sum(c["n"] * 4 * V * (1 + c["W"]) for c in classes) + scans
+    step_s = dt / args.steps
+    roofline = {
+        "bound": "hbm", "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": dom["frac"], "traffic": dom["traffic"], "kernel": dom["kernel"],
+        "roots_per_launch": dom["roots_per_launch"], "avg_launch_ms": dom["isolated_launch_ms"],
+        "compulsory_bytes": dom["compulsory_bytes"],
+        "traffic_over_compulsory": dom["traffic_over_compulsory"], "launches": units,
+        "step_compulsory_bytes": step_comp,
+        "step_frac": round(step_comp / step_s / 1e9 / HBM_PEAK_GBS, 4),
+        "note": "achieved = compulsory bytes of the dominant launch / its isolated time (HIP "
+                "events on its stream, alone): levels = dist rows written (4V per run) + one "
+                "neighbour-id + offset scan per 64-root traversal; derive = next-hop rows "
+                "written (4VW per run); the byte level rows are intermediate (traffic, not "
+                "compulsory). step_frac = (dist + next-hop rows of every root + scans) / "
+                "ms_per_step. traffic = measured HBM bytes per launch (rocprofv3 FETCH_SIZE x2 "
+                "+ WRITE_SIZE, profiles/<round>/pmc_traffic.json)",
+    }
+    p1_avg = float(np.mean([a_.elapsed_time(b_) for a_, b_ in p1_ms]))
+    classes_cfg = [{"launch": "levels", "roots_this_rank": int(clo.size),
+                    "closure_over_roots": round(clo.size / max(1, mine.size), 4),
+                    "avg_launch_ms": round(p1_avg, 3), "isolated_launch_ms": round(p1_iso, 3)}]
+    for c in classes:
+        classes_cfg.append({"cap": c["cap"], "nh_words": c["W"], "roots_this_rank": c["n"],
+                            "avg_launch_ms": round(float(np.mean(
+                                [a_.elapsed_time(b_) for a_, b_ in c["ms"]])), 3) if c["ms"] else 0.0,
+                            "isolated_launch_ms": round(c["iso_ms"], 3)})
+    report(args, stream, names, perm, step_digest, dt, V * args.steps, E, desc, 0, V, world, rank,
+           dist_on, backend, V, classes_cfg, roofline, "strong", "derive")
+    if dist_on:
+        torch.distributed.destroy_process_group()
+
+
+def report(args, stream, names, pool, step_digest, dt, roots_total, E, desc, n_roots, V, world,
+           rank, dist_on, backend, roots_per_step, classes_cfg, roofline, scaling, mode):
+    """CPU baseline + parity of the timed step's digests (rank 0) and the one
+    JSON line."""
+    spf_s = roots_total / dt
+    gteps = roots_total * E / dt / 1e9
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu:
         from oracle import Oracle  # CPU baseline leg only (the restatements under oracle/)
@@ -443,32 +668,25 @@ def main():
             "metric": METRIC, "value": round(spf_s, 2), "unit": "SPF/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak" if weak else "strong", "vs_baseline": None, "dtype": "u32",
+            "scaling": scaling, "vs_baseline": None, "dtype": "u32",
             "data": "synthetic", "gteps": round(gteps, 3),
             "config": {
                 "workload": desc + (" all-sources" if n_roots <= 0 else
                                     f" {pool.size} sampled roots") +
                 " SPF + ECMP next-hop bitsets (dist + next-hop rows written to HBM, per-root "
                 "digests)",
-                "n_nodes": V, "n_directed_edges": E,
-                "roots_per_step": int(world * B if weak else pool.size),
-                "root_classes": [{"cap": c.cap, "nh_words": c.nh_words,
-                                  "roots_this_rank": c.extra["n"],
-                                  **{kk: c.extra["plan"][kk] for kk in ("variant", "slices",
-                                                                        "block")},
-                                  "avg_launch_ms": round(float(np.mean(c.extra["ms"])), 3),
-                                  "isolated_launch_ms": round(c.extra["iso_ms"], 3)}
-                                 for c in classes],
+                "n_nodes": V, "n_directed_edges": E, "mode": mode,
+                "roots_per_step": roots_per_step,
+                "root_classes": classes_cfg,
                 "parallelism": f"root-sharded x{world}" +
-                               (", RCCL all_gather of 24-B digests" if dist_on else "")},
+                               (f", all_gather of 24-B digests ({'RCCL' if backend == 'nccl' else backend})"
+                                if dist_on else "")},
             "roofline": roofline, "cpu_baseline": cpu, "parity_vs_cpu_sample": parity,
         }
         if dist_on:
             line["gathered_roots"] = len(step_digest)
             line["dist_backend"] = backend
         print(json.dumps(line), flush=True)
-    if dist_on:
-        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -174,20 +174,24 @@ int ospf_sync(ospf_ctx* ctx, void* stream);
 
 /* All-sources next hops in two phases ("derive", unit metric or hop count).
  * ospf_levels_dev: distances of the n device roots by the distance-only
- * multi-source BFS, written as d_dist [n][V] u32 rows (optional) and as byte
- * level rows d_lev [n][V] (dist + 1, 0 = unreached).
- * ospf_nh_derive_dev: next-hop words [n][V][nh_words] (+ digests) of the n
- * device roots from level rows: d_lev_pos[v] = row of node v in d_lev
- * (0xFFFFFFFF: none). Every distinct neighbour of every root with an up link
- * must have a row (else error bit 16 at ospf_sync). Bit k of a root's word
- * k / 32 = its k-th distinct neighbour n is a next hop towards v: an up link,
- * n transit or n == v, and dist(n, v) + 1 == dist(root, v) (the reference's
- * nextHops, LinkState.cpp:885-901). Both queue on `stream`, no host wait. */
+ * multi-source BFS, written as d_dist [n][V] u32 rows (optional), byte level
+ * rows d_lev [n][V] (dist + 1, 0 = unreached) and, optional, the distance
+ * part {reached, sum dist, sum dist_key * (dist + 1)} of each run's digest.
+ * ospf_nh_derive_dev: next-hop words [n][V][nh_words] (+ complete digests) of
+ * the n device roots from level rows: d_lev_pos[v] = row of node v in d_lev
+ * (0xFFFFFFFF: none), d_lev_digest = the level rows' digest parts (needed for
+ * d_digest). Every distinct transit neighbour of every root with an up link
+ * must have a row (else error bit 16 at ospf_sync); max_root_neighbors (0 =
+ * 32 nh_words, at most 2048) bounds the roots' distinct neighbours. Bit k of a
+ * root's word k / 32 = its k-th distinct neighbour n is a next hop towards v:
+ * an up link, n transit or n == v, and dist(n, v) + 1 == dist(root, v) (the
+ * reference's nextHops, LinkState.cpp:885-901). Both queue on `stream`. */
 int ospf_levels_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n, uint32_t flags,
-                    uint32_t* d_dist, uint8_t* d_lev, void* stream);
+                    uint32_t* d_dist, uint8_t* d_lev, ospf_digest* d_lev_digest, void* stream);
 int ospf_nh_derive_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n, uint32_t nh_words,
-                       const uint8_t* d_lev, const uint32_t* d_lev_pos, uint32_t* d_nh,
-                       ospf_digest* d_digest, void* stream);
+                       uint32_t max_root_neighbors, const uint8_t* d_lev,
+                       const uint32_t* d_lev_pos, const ospf_digest* d_lev_digest,
+                       uint32_t* d_nh, ospf_digest* d_digest, void* stream);
 
 /* Kernel variant the engine would use for a large batch (for reporting):
  * 0 = Dial, LDS-resident (dist+nh in LDS), 1 = Dial, LDS dist + HBM

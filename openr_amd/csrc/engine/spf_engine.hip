@@ -1167,7 +1167,7 @@ int ospf_sync(ospf_ctx* c, void* stream) {
 // byte level rows; then each root's next-hop words from its neighbours'
 // level rows. Unit metric or hop count, depth bound <= 253.
 int ospf_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t flags,
-                    uint32_t* d_dist, uint8_t* d_lev, void* stream) {
+                    uint32_t* d_dist, uint8_t* d_lev, ospf_digest* d_lev_digest, void* stream) {
   if (!c) return OSPF_E_INVAL;
   if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
   if (n == 0) return OSPF_OK;
@@ -1206,6 +1206,8 @@ int ospf_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t f
   a.err = c->d_err;
   a.dist = d_dist;
   a.levrow = d_lev;
+  a.digest = d_lev_digest;
+  if (d_lev_digest) HIPCHK(c, hipMemsetAsync(d_lev_digest, 0, (size_t)n * sizeof(ospf_digest), s));
   for (uint32_t vb0 = 0; vb0 < total_vb; vb0 += nb_max) {
     a.vb0 = vb0;
     a.nb = std::min(nb_max, total_vb - vb0);
@@ -1226,13 +1228,18 @@ int ospf_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t f
 }
 
 int ospf_nh_derive_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t nh_words,
-                       const uint8_t* d_lev, const uint32_t* d_lev_pos, uint32_t* d_nh,
-                       ospf_digest* d_digest, void* stream) {
+                       uint32_t max_root_neighbors, const uint8_t* d_lev,
+                       const uint32_t* d_lev_pos, const ospf_digest* d_lev_digest,
+                       uint32_t* d_nh, ospf_digest* d_digest, void* stream) {
   if (!c) return OSPF_E_INVAL;
   if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
   if (n == 0) return OSPF_OK;
   if (!d_roots || !d_lev || !d_lev_pos || !d_nh) return fail(c, OSPF_E_INVAL, "null argument");
+  if (d_digest && !d_lev_digest)
+    return fail(c, OSPF_E_INVAL, "derive: digests need the level rows' digests");
   if (nh_words == 0 || nh_words > 64) return fail(c, OSPF_E_RANGE, "derive: nh_words 1..64");
+  const uint32_t cap = max_root_neighbors ? std::min(max_root_neighbors, 32u * nh_words)
+                                          : 32u * nh_words;
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(c, hipSetDevice(c->device));
   if (d_digest) HIPCHK(c, hipMemsetAsync(d_digest, 0, (size_t)n * sizeof(ospf_digest), s));
@@ -1240,8 +1247,11 @@ int ospf_nh_derive_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_
   d.roots = d_roots;
   d.n = n;
   d.W = nh_words;
+  d.cap = std::min<uint32_t>(cap, 2048u);
   d.lev = d_lev;
   d.pos = d_lev_pos;
+  d.lev_digest = d_lev_digest;
+  if (const char* e = getenv("OSPF_DERIVE_CTILES")) d.ctiles = (uint32_t)std::max(1, atoi(e));
   d.nh = d_nh;
   d.digest = d_digest;
   d.err = c->d_err;

@@ -193,12 +193,15 @@ struct MsArgs {
 struct DeriveArgs {
   const uint32_t* roots;
   uint32_t n, W;
+  uint32_t cap;            // max distinct neighbours of a root of the call (<= 2048)
   const uint8_t* lev;      // [rows][V]
   const uint32_t* pos;     // [V]
+  const ospf_digest* lev_digest;  // [rows] distance part of each row's digest (phase 1)
   uint32_t* nh;            // [n][V][W]
   ospf_digest* digest;     // [n] (zeroed by the caller) or null
-  uint32_t* err;           // bit 1: K > 32 W, 16: a neighbour has no level row, 64: bad root
-  uint32_t tiles;          // set by the launcher
+  uint32_t* err;           // bit 1: K > cap / 32 W, 16: a neighbour has no level row, 64: bad root
+  uint32_t ctiles;         // node tiles per block (0: default 8)
+  uint32_t G, tiles, chunks;  // set by the launcher
 };
 // phase 1: distances only (kp -1) + msbfs_levrows; phase 2: nh_derive
 hipError_t launch_msbfs_levels(const DevGraph& g, const MsArgs& a, uint32_t depth_bound,

@@ -820,6 +820,7 @@ __global__ void __launch_bounds__(256) msbfs_rows_multi_kernel(DevGraph g, MsArg
 // whatever their width, and the next-hop words are written once, whole.
 __global__ void __launch_bounds__(256) msbfs_levrows_kernel(DevGraph g, MsArgs a) {
   __shared__ uint8_t s_lev[64 * 64];  // [node][root]
+  __shared__ uint64_t s_kd[64];
   const uint32_t vbl = blockIdx.x % a.nb;
   const VB b(a, vbl, g.V, -1);
   const uint32_t V = g.V, tid = threadIdx.x;
@@ -830,7 +831,35 @@ __global__ void __launch_bounds__(256) msbfs_levrows_kernel(DevGraph g, MsArgs a
     const uint4* src = reinterpret_cast<const uint4*>(a.lev + ((size_t)vbl * V + v0) * 64u);
     if (tid < nv * 4u) reinterpret_cast<uint4*>(s_lev)[tid] = src[tid];
   }
+  if (a.digest && tid < 64u) s_kd[tid] = (v0 + tid < V) ? g.dkey[2ull * (v0 + tid)] : 0ull;
   __syncthreads();
+  // the distance part of each run's digest (its next-hop part is added by
+  // nh_derive): root dr = tid / 4 over nodes 16 * (tid % 4) .. + 15
+  if (a.digest) {
+    const uint32_t dr = tid >> 2, dn0 = 16u * (tid & 3u);
+    uint64_t reached = 0, sumd = 0, h = 0;
+    if (dr < nr) {
+      for (uint32_t n = dn0; n < dn0 + 16u && n < nv; ++n) {
+        const uint32_t l = s_lev[n * 64u + dr];
+        if (!l) continue;
+        reached += 1;
+        sumd += l - 1u;
+        h += s_kd[n] * (uint64_t)l;
+      }
+    }
+#pragma unroll
+    for (int o = 1; o < 4; o <<= 1) {
+      reached += shfl_xor64(reached, o);
+      sumd += shfl_xor64(sumd, o);
+      h += shfl_xor64(h, o);
+    }
+    if ((tid & 3u) == 0 && dr < nr && reached) {
+      ospf_digest* dg = a.digest + b.rix0 + dr;
+      atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)reached);
+      atomicAdd((unsigned long long*)&dg->sum_dist, (unsigned long long)sumd);
+      atomicAdd((unsigned long long*)&dg->hash, (unsigned long long)h);
+    }
+  }
   const bool vec = (V & 3u) == 0 && nv == 64u;
   for (uint32_t i = tid; i < 64u * 16u; i += kBlock) {  // (root, node quad)
     const uint32_t r = i >> 4, q = i & 15u;
@@ -858,144 +887,185 @@ __global__ void __launch_bounds__(256) msbfs_levrows_kernel(DevGraph g, MsArgs a
   }
 }
 
-// Phase 2: block = (root i, tile of T = 1024 / S nodes); S threads per node
-// quad split the root's next-hop words. The root's neighbour table (level
-// row, flags) is staged in LDS; each (neighbour, quad) is one 4-B load of
-// four level bytes compared against the root's own four.
-constexpr uint32_t kDeriveMaxK = 2048;
+// Phase 2: block = (group of G roots, chunk of C node tiles); a tile is
+// T = 1024 / S nodes, S threads per node quad splitting a root's next-hop
+// words. The group's neighbour tables (level row per usable transit
+// neighbour) are staged once per block; per tile, the group's own level bytes
+// and the node keys are staged once and reused by every root. A neighbour
+// row read is one 4-B load of four level bytes, compared with the root's own
+// four (minus one) by a SWAR zero-byte test; eight neighbours' flags gather
+// in one register per quad before they are spread into the four words.
+// A non-transit neighbour n is a next hop only towards n itself (dist 1 from
+// the root over the up link): its bit is set directly, its row never read.
+constexpr uint32_t kDeriveTab = 2048;  // LDS neighbour slots of a block's group
+constexpr uint32_t kDeriveMaxG = 16;
 template <int S>
 __global__ void __launch_bounds__(256) nh_derive_kernel(DevGraph g, DeriveArgs d) {
-  __shared__ uint32_t s_pos[kDeriveMaxK];
-  __shared__ uint32_t s_nbr[kDeriveMaxK];
-  __shared__ uint8_t s_fl[kDeriveMaxK];  // bit 0: usable (an up link), bit 1: transit
-  __shared__ uint8_t s_own[1024 / S];
-  __shared__ uint64_t s_red[3 * kWavesPerBlock];
-  extern __shared__ uint32_t s_out[];  // [T][W]
   constexpr uint32_t T = 1024u / S;
-  const uint32_t V = g.V, W = d.W, tid = threadIdx.x;
-  const uint32_t i = blockIdx.x / d.tiles, v0 = (blockIdx.x % d.tiles) * T;
-  const uint32_t nv = min(T, V - v0);
-  const uint32_t r = d.roots[i];
-  if (r >= V) {
-    if (tid == 0) atomicOr(d.err, 64u);
-    return;
+  // [G][cap] per neighbour slot: its level row; 0x80000000 | id for a
+  // non-transit usable neighbour; kInf: no up link (skip)
+  __shared__ uint32_t s_pos[kDeriveTab];
+  __shared__ uint32_t s_K[kDeriveMaxG], s_root[kDeriveMaxG], s_own[kDeriveMaxG];
+  __shared__ uint32_t s_L[kDeriveMaxG * T / 4];  // own level bytes, [G][T] packed by quads
+  __shared__ uint64_t s_kn[T];
+  __shared__ unsigned long long s_h[kDeriveMaxG];
+  extern __shared__ uint32_t s_out[];  // [T][W]
+  const uint32_t V = g.V, W = d.W, tid = threadIdx.x, G = d.G, cap = d.cap;
+  const uint32_t gi = blockIdx.x / d.chunks, ci = blockIdx.x % d.chunks;
+  const uint32_t i0 = gi * G, ng = min(G, d.n - i0);
+  // ---- neighbour tables of the group
+  if (tid < ng) {
+    const uint32_t r = d.roots[i0 + tid];
+    s_root[tid] = r;
+    s_h[tid] = 0ull;
+    s_own[tid] = kInf;
+    s_K[tid] = 0;
+    if (r >= V) {
+      atomicOr(d.err, 64u);
+    } else {
+      const uint32_t K = g.dn_off[r + 1] - g.dn_off[r];
+      s_own[tid] = d.pos[r];
+      if (K > cap || K > 32u * W || s_own[tid] == kInf)
+        atomicOr(d.err, s_own[tid] == kInf ? 16u : 1u);
+      if (s_own[tid] != kInf) s_K[tid] = min(K, cap);
+    }
   }
-  const uint32_t nb0 = g.dn_off[r], K = g.dn_off[r + 1] - nb0;
-  const uint32_t own = d.pos[r];
-  if (K > kDeriveMaxK || K > 32u * W || own == kInf) {
-    if (tid == 0) atomicOr(d.err, own == kInf ? 16u : 1u);
-    return;
-  }
-  for (uint32_t k = tid; k < K; k += kBlock) {
-    const uint32_t n = g.dn[nb0 + k];
-    s_nbr[k] = n;
-    s_pos[k] = d.pos[n];
-    s_fl[k] = transit(g, n) ? 2u : 0u;
+  for (uint32_t x = tid; x < ng * cap; x += kBlock) s_pos[x] = kInf;
+  __syncthreads();
+  for (uint32_t j = 0; j < ng; ++j) {  // mark usable neighbours (an up link) per root
+    const uint32_t r = s_root[j];
+    if (r >= V) continue;
+    for (uint32_t e = g.row_ptr[r] + tid; e < g.row_ptr[r + 1]; e += kBlock) {
+      const uint32_t cx = g.colx[e];
+      if ((cx & kDown) || cx == r) continue;
+      const uint32_t k = g.didx[e];
+      if (k < s_K[j]) s_pos[j * cap + k] = 0u;  // benign race: same value
+    }
   }
   __syncthreads();
-  for (uint32_t e = g.row_ptr[r] + tid; e < g.row_ptr[r + 1]; e += kBlock) {
-    const uint32_t cx = g.colx[e];
-    if ((cx & kDown) || cx == r) continue;
-    const uint32_t k = g.didx[e];
-    if (k < K) s_fl[k] |= 1u;  // benign race: every writer sets the same bit
+  for (uint32_t x = tid; x < ng * cap; x += kBlock) {
+    const uint32_t j = x / cap, k = x - j * cap;
+    if (k >= s_K[j] || s_pos[x] == kInf) continue;
+    const uint32_t n = g.dn[g.dn_off[s_root[j]] + k];
+    const uint32_t p = d.pos[n];
+    if (transit(g, n)) {
+      s_pos[x] = p;
+      if (p == kInf) atomicOr(d.err, 16u);
+    } else {
+      s_pos[x] = 0x80000000u | n;  // next hop towards itself only
+    }
   }
-  const uint8_t* orow = d.lev + (size_t)own * V;
-  for (uint32_t n = tid; n < T; n += kBlock) s_own[n] = n < nv ? orow[v0 + n] : 0u;
   __syncthreads();
-  const bool vec = (V & 3u) == 0 && nv == T;
-  // a usable neighbour without a level row cannot be derived: error, zero bits
-  if (tid == 0 && v0 == 0) {
-    for (uint32_t k = 0; k < K; ++k)
-      if ((s_fl[k] & 1u) && s_pos[k] == kInf) {
-        atomicOr(d.err, 16u);
-        break;
-      }
-  }
+  // ---- tiles
   const uint32_t q = tid / S, sub = tid % S, n0 = 4u * q;
-  uint32_t L[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) L[j] = s_own[n0 + j];
-  const bool any = (L[0] >= 2u) | (L[1] >= 2u) | (L[2] >= 2u) | (L[3] >= 2u);
-  for (uint32_t w = sub; w < W; w += S) {
-    uint32_t word[4] = {0u, 0u, 0u, 0u};
-    const uint32_t k0 = 32u * w, k1 = min(K, k0 + 32u);
-    if (any) {
-      for (uint32_t k = k0; k < k1; ++k) {
-        const uint32_t fl = s_fl[k], p = s_pos[k];
-        if (!(fl & 1u) || p == kInf) continue;
-        const uint8_t* nrow = d.lev + (size_t)p * V + v0 + n0;
-        uint32_t x4;
+  const uint32_t t0 = ci * d.ctiles, t1 = min(d.tiles, t0 + d.ctiles);
+  for (uint32_t t = t0; t < t1; ++t) {
+    const uint32_t v0 = t * T, nv = min(T, V - v0);
+    const bool vec = (V & 3u) == 0 && nv == T;
+    for (uint32_t x = tid; x < ng * (T / 4u); x += kBlock) {
+      const uint32_t j = x / (T / 4u), qq = x - j * (T / 4u);
+      uint32_t w4 = 0;
+      if (s_own[j] != kInf) {
+        const uint8_t* orow = d.lev + (size_t)s_own[j] * V + v0 + 4u * qq;
         if (vec) {
-          x4 = *reinterpret_cast<const uint32_t*>(nrow);
+          w4 = *reinterpret_cast<const uint32_t*>(orow);
         } else {
-          x4 = 0;
-          for (uint32_t j = 0; j < 4u; ++j)
-            if (n0 + j < nv) x4 |= (uint32_t)nrow[j] << (8 * j);
-        }
-        const uint32_t nid = s_nbr[k];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t x = (x4 >> (8 * j)) & 0xFFu;
-          const bool ok = x != 0u && x + 1u == L[j] && ((fl & 2u) || nid == v0 + n0 + j);
-          word[j] |= (uint32_t)ok << (k - k0);
+          for (uint32_t b = 0; b < 4u; ++b)
+            if (4u * qq + b < nv) w4 |= (uint32_t)orow[b] << (8 * b);
         }
       }
+      s_L[x] = w4;
     }
+    if (d.digest)
+      for (uint32_t n = tid; n < T; n += kBlock) s_kn[n] = n < nv ? g.dkey[2ull * (v0 + n) + 1] : 0ull;
+    __syncthreads();
+    for (uint32_t j = 0; j < ng; ++j) {
+      const uint32_t K = s_K[j];
+      const uint32_t L4 = s_L[j * (T / 4u) + q];
+      // per byte: L - 1 where L >= 2, else 0xFF (matches no level byte)
+      uint32_t lm1 = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (n0 + j < T) s_out[(n0 + j) * W + w] = word[j];
-  }
-  __syncthreads();
-  // the tile's nv * W words are contiguous in the root's row
-  const uint32_t span = nv * W;
-  uint32_t* dst = d.nh + ((size_t)i * V + v0) * W;
-  if (vec && (((size_t)i * V + v0) * W & 3u) == 0 && (span & 3u) == 0) {
-    for (uint32_t x = tid; x < span / 4u; x += kBlock)
-      reinterpret_cast<uint4*>(dst)[x] = reinterpret_cast<const uint4*>(s_out)[x];
-  } else {
-    for (uint32_t x = tid; x < span; x += kBlock) dst[x] = s_out[x];
-  }
-  if (!d.digest) return;
-  uint64_t reached = 0, sumd = 0, h = 0;
-  for (uint32_t n = tid; n < nv; n += kBlock) {
-    const uint32_t l = s_own[n];
-    if (!l) continue;
-    const uint64_t kd = g.dkey[2ull * (v0 + n)], kn = g.dkey[2ull * (v0 + n) + 1];
-    reached += 1;
-    sumd += l - 1u;
-    uint64_t ws = 0;
-    for (uint32_t w = 0; w < W; ++w) {
-      const uint32_t word = s_out[n * W + w];
-      if (word) ws += digest_word_key(w, word);
-    }
-    h += kd * (uint64_t)l + kn * ws;
-  }
+      for (int b = 0; b < 4; ++b) {
+        const uint32_t l = (L4 >> (8 * b)) & 0xFFu;
+        lm1 |= (l >= 2u ? l - 1u : 0xFFu) << (8 * b);
+      }
+      const uint32_t* tab = s_pos + j * cap;
+      for (uint32_t w = sub; w < W; w += S) {
+        uint32_t word[4] = {0u, 0u, 0u, 0u};
+        const uint32_t k0 = 32u * w;
+        if (lm1 != 0xFFFFFFFFu && k0 < K) {
+          for (uint32_t k8 = 0; k8 < 32u; k8 += 8u) {
+            const uint32_t kb = k0 + k8;
+            if (kb >= K) break;
+            uint32_t A = 0;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    reached += shfl_xor64(reached, o);
-    sumd += shfl_xor64(sumd, o);
-    h += shfl_xor64(h, o);
-  }
-  const uint32_t wave = tid >> 6;
-  if ((tid & 63u) == 0) {
-    s_red[3 * wave] = reached;
-    s_red[3 * wave + 1] = sumd;
-    s_red[3 * wave + 2] = h;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    uint64_t rr = 0, sd = 0, hh = 0;
-    for (uint32_t x = 0; x < kWavesPerBlock; ++x) {
-      rr += s_red[3 * x];
-      sd += s_red[3 * x + 1];
-      hh += s_red[3 * x + 2];
+            for (uint32_t kk = 0; kk < 8u; ++kk) {
+              const uint32_t p = (kb + kk < K) ? tab[kb + kk] : kInf;
+              if (p >= 0x80000000u) {
+                const uint32_t b = (p & 0x7FFFFFFFu) - (v0 + n0);
+                if (p != kInf && b < 4u) A |= 1u << (8u * b + kk);
+                continue;
+              }
+              const uint8_t* nrow = d.lev + (size_t)p * V + v0 + n0;
+              uint32_t x4;
+              if (vec) {
+                x4 = *reinterpret_cast<const uint32_t*>(nrow);
+              } else {
+                x4 = 0;
+                for (uint32_t b = 0; b < 4u; ++b)
+                  if (n0 + b < nv) x4 |= (uint32_t)nrow[b] << (8 * b);
+              }
+              const uint32_t df = x4 ^ lm1;  // zero byte: level == L - 1
+              const uint32_t z = ~(((df & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | df | 0x7F7F7F7Fu);
+              A |= (z >> 7) << kk;  // byte b, bit kk
+            }
+#pragma unroll
+            for (int b = 0; b < 4; ++b) word[b] |= ((A >> (8 * b)) & 0xFFu) << k8;
+          }
+        }
+#pragma unroll
+        for (int b = 0; b < 4; ++b) s_out[(n0 + b) * W + w] = word[b];
+      }
+      __syncthreads();
+      const uint32_t i = i0 + j, span = nv * W;
+      uint32_t* dst = d.nh + ((size_t)i * V + v0) * W;
+      if (vec && (((size_t)i * V + v0) * W & 3u) == 0 && (span & 3u) == 0) {
+        for (uint32_t x = tid; x < span / 4u; x += kBlock)
+          reinterpret_cast<uint4*>(dst)[x] = reinterpret_cast<const uint4*>(s_out)[x];
+      } else {
+        for (uint32_t x = tid; x < span; x += kBlock) dst[x] = s_out[x];
+      }
+      if (d.digest) {
+        uint64_t h = 0;
+        for (uint32_t n = tid; n < nv; n += kBlock) {
+          uint64_t ws = 0;
+          for (uint32_t w = 0; w < W; ++w) {
+            const uint32_t word = s_out[n * W + w];
+            if (word) ws += digest_word_key(w, word);
+          }
+          h += s_kn[n] * ws;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) h += shfl_xor64(h, o);
+        if ((tid & 63u) == 0 && h) atomicAdd(&s_h[j], (unsigned long long)h);
+      }
+      __syncthreads();  // s_out is rewritten by the next root
     }
+  }
+  if (d.digest && tid < ng) {
+    const uint32_t i = i0 + tid;
     ospf_digest* dg = d.digest + i;
-    if (rr) {
-      atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)rr);
-      atomicAdd((unsigned long long*)&dg->sum_dist, (unsigned long long)sd);
+    unsigned long long h = s_h[tid];
+    if (ci == 0) {  // the distance part from phase 1, once per root
+      const uint32_t p = s_own[tid];
+      if (p != kInf) {
+        const ospf_digest ld = d.lev_digest[p];
+        atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)ld.reached);
+        atomicAdd((unsigned long long*)&dg->sum_dist, (unsigned long long)ld.sum_dist);
+        h += ld.hash;
+      }
     }
-    if (hh) atomicAdd((unsigned long long*)&dg->hash, (unsigned long long)hh);
+    if (h) atomicAdd((unsigned long long*)&dg->hash, h);
   }
 }
 
@@ -1205,12 +1275,16 @@ hipError_t launch_msbfs_levels(const DevGraph& g, const MsArgs& a, uint32_t dept
 hipError_t launch_nh_derive(const DevGraph& g, const DeriveArgs& d0, hipStream_t s) {
   DeriveArgs d = d0;
   if (d.n == 0) return hipSuccess;
-  if (d.W == 0 || d.W > kDeriveMaxK / 32u) return hipErrorInvalidValue;
+  if (d.W == 0 || d.W > kDeriveTab / 32u || d.cap == 0 || d.cap > kDeriveTab)
+    return hipErrorInvalidValue;
   const int S = d.W == 1 ? 1 : d.W == 2 ? 2 : 4;
   const uint32_t T = 1024u / S;
+  d.G = std::max<uint32_t>(1, std::min<uint32_t>(kDeriveMaxG, kDeriveTab / d.cap));
   d.tiles = (g.V + T - 1) / T;
+  d.ctiles = std::max<uint32_t>(1, std::min<uint32_t>(d.tiles, d.ctiles ? d.ctiles : 8));
+  d.chunks = (d.tiles + d.ctiles - 1) / d.ctiles;
   const size_t lds = (size_t)T * d.W * 4u;
-  const dim3 grid(d.n * d.tiles);
+  const dim3 grid(((d.n + d.G - 1) / d.G) * d.chunks);
   switch (S) {
     case 1: hipLaunchKernelGGL(nh_derive_kernel<1>, grid, dim3(kBlock), lds, s, g, d); break;
     case 2: hipLaunchKernelGGL(nh_derive_kernel<2>, grid, dim3(kBlock), lds, s, g, d); break;

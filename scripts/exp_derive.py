@@ -43,6 +43,7 @@ def main():
     d_pos = torch.from_numpy(pos.view(np.int32)).to(dev)
     lev = torch.empty((V, V), dtype=torch.uint8, device=dev)
     dist = torch.empty((V, V), dtype=torch.int32, device=dev)
+    ldg = torch.empty((V, 3), dtype=torch.int64, device=dev)
     bufs = []
     for c in classes:
         bufs.append(dict(c=c, d=torch.from_numpy(c.roots.view(np.int32)).to(dev),
@@ -54,14 +55,15 @@ def main():
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
         eng.levels_dev(d_order.data_ptr(), V, lev.data_ptr(), d_dist=dist.data_ptr(),
-                       stream=s.cuda_stream)
+                       d_lev_digest=ldg.data_ptr(), stream=s.cuda_stream)
         e1.record(s)
         evs = []
         for b in bufs:
             a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a_.record(s)
             eng.nh_derive_dev(b["d"].data_ptr(), b["c"].roots.size, b["c"].nh_words, lev.data_ptr(),
-                              d_pos.data_ptr(), b["nh"].data_ptr(), d_digest=b["dg"].data_ptr(),
+                              d_pos.data_ptr(), b["nh"].data_ptr(), d_lev_digest=ldg.data_ptr(),
+                              d_digest=b["dg"].data_ptr(), max_root_neighbors=b["c"].cap,
                               stream=s.cuda_stream)
             b_.record(s)
             evs.append((b["c"].cap, a_, b_))

@@ -23,10 +23,13 @@ def derive_all(eng, V, hop=False, roots=None):
     d_all = torch.from_numpy(all_ids.view(np.int32)).to(dev)
     lev = torch.empty((V, V), dtype=torch.uint8, device=dev)
     dist = torch.empty((V, V), dtype=torch.int32, device=dev)
-    eng.levels_dev(d_all.data_ptr(), V, lev.data_ptr(), d_dist=dist.data_ptr(), hop_count=hop)
+    ldg = torch.empty((V, 3), dtype=torch.int64, device=dev)
+    eng.levels_dev(d_all.data_ptr(), V, lev.data_ptr(), d_dist=dist.data_ptr(),
+                   d_lev_digest=ldg.data_ptr(), hop_count=hop)
     pos = torch.from_numpy(all_ids.view(np.int32)).to(dev)
     roots = all_ids if roots is None else np.asarray(roots, np.uint32)
     words = np.array([eng.nh_words(int(r)) for r in roots])
+    max_nbrs = 0
     out = {}
     for W in sorted(set(words.tolist())):
         grp = roots[words == W]
@@ -34,7 +37,8 @@ def derive_all(eng, V, hop=False, roots=None):
         nh = torch.empty((grp.size, V, W), dtype=torch.int32, device=dev)
         dg = torch.empty((grp.size, 3), dtype=torch.int64, device=dev)
         eng.nh_derive_dev(d_r.data_ptr(), grp.size, W, lev.data_ptr(), pos.data_ptr(),
-                          nh.data_ptr(), d_digest=dg.data_ptr())
+                          nh.data_ptr(), d_lev_digest=ldg.data_ptr(), d_digest=dg.data_ptr(),
+                          max_root_neighbors=max_nbrs)
         eng.sync()
         out[W] = (grp, nh.cpu().numpy().view(np.uint32), dg.cpu().numpy().view(np.uint64))
     eng.sync()
@@ -60,10 +64,24 @@ def check_against_engine(stream, hop=False, roots=None):
     return ls
 
 
+@pytest.mark.parametrize("ctiles", [None, "1"])
 @pytest.mark.parametrize("seed", range(6))
-def test_derive_random_unit_graphs(seed):
+def test_derive_random_unit_graphs(seed, ctiles, monkeypatch):
+    if ctiles:
+        monkeypatch.setenv("OSPF_DERIVE_CTILES", ctiles)
     stream, _ = random_stream(seed, n=60, unit=True)
     check_against_engine(stream)
+
+
+def test_derive_grid_with_non_transit_neighbours():
+    """Overloaded nodes next to many roots: the non-transit slot path, and a
+    graph with V % 4 != 0 (byte-wise loads at the tile ends)."""
+    st = T.grid(23)
+    dbs = st.to_dbs()
+    for d in dbs:
+        if int(d.name) % 7 == 3:
+            d.overloaded = True
+    check_against_engine(AdjDbStream.from_dbs(dbs))
 
 
 @pytest.mark.parametrize("seed", range(3))
