@@ -425,7 +425,8 @@ def derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
                                for c in cls])
 
     parts = [part(r) for r in range(world)]
-    cls_all = [{cap: shard.locality_order(p[caps[p] == cap], key) for cap in all_caps}
+    lkey = shard.last_neighbor(rp, col)
+    cls_all = [{cap: shard.locality_order(p[caps[p] == cap], lkey) for cap in all_caps}
                for p in parts]
     mine = parts[rank]
     clo = shard.locality_order(shard.closure(mine, rp, col), key)

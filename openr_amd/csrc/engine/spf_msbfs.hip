@@ -911,7 +911,14 @@ __global__ void __launch_bounds__(256) nh_derive_kernel(DevGraph g, DeriveArgs d
   __shared__ unsigned long long s_h[kDeriveMaxG];
   extern __shared__ uint32_t s_out[];  // [T][W]
   const uint32_t V = g.V, W = d.W, tid = threadIdx.x, G = d.G, cap = d.cap;
-  const uint32_t gi = blockIdx.x / d.chunks, ci = blockIdx.x % d.chunks;
+  // chunk-major: the blocks in flight cover one node chunk for many groups,
+  // so neighbour rows shared by several roots are read while in L2 / MALL;
+  // within a chunk, runs of consecutive groups (similar neighbourhoods in a
+  // locality-ordered root list) go to one XCD (workgroup b runs on XCD b % 8)
+  const uint32_t ngroups = (d.n + G - 1) / G;
+  const uint32_t ci = blockIdx.x / ngroups, rr = blockIdx.x % ngroups;
+  const uint32_t full = ngroups / 8u * 8u;
+  const uint32_t gi = rr < full ? (rr % 8u) * (full / 8u) + rr / 8u : rr;
   const uint32_t i0 = gi * G, ng = min(G, d.n - i0);
   // ---- neighbour tables of the group
   if (tid < ng) {
@@ -1277,7 +1284,9 @@ hipError_t launch_nh_derive(const DevGraph& g, const DeriveArgs& d0, hipStream_t
   if (d.n == 0) return hipSuccess;
   if (d.W == 0 || d.W > kDeriveTab / 32u || d.cap == 0 || d.cap > kDeriveTab)
     return hipErrorInvalidValue;
-  const int S = d.W == 1 ? 1 : d.W == 2 ? 2 : 4;
+  // one thread per node quad does all the words up to 8; wider rows split a
+  // quad's words over 4 threads (a spine: 14 words x 32 neighbours each)
+  const int S = d.W <= 8 ? 1 : 4;
   const uint32_t T = 1024u / S;
   d.G = std::max<uint32_t>(1, std::min<uint32_t>(kDeriveMaxG, kDeriveTab / d.cap));
   d.tiles = (g.V + T - 1) / T;
@@ -1285,11 +1294,8 @@ hipError_t launch_nh_derive(const DevGraph& g, const DeriveArgs& d0, hipStream_t
   d.chunks = (d.tiles + d.ctiles - 1) / d.ctiles;
   const size_t lds = (size_t)T * d.W * 4u;
   const dim3 grid(((d.n + d.G - 1) / d.G) * d.chunks);
-  switch (S) {
-    case 1: hipLaunchKernelGGL(nh_derive_kernel<1>, grid, dim3(kBlock), lds, s, g, d); break;
-    case 2: hipLaunchKernelGGL(nh_derive_kernel<2>, grid, dim3(kBlock), lds, s, g, d); break;
-    default: hipLaunchKernelGGL(nh_derive_kernel<4>, grid, dim3(kBlock), lds, s, g, d); break;
-  }
+  if (S == 1) hipLaunchKernelGGL(nh_derive_kernel<1>, grid, dim3(kBlock), lds, s, g, d);
+  else hipLaunchKernelGGL(nh_derive_kernel<4>, grid, dim3(kBlock), lds, s, g, d);
   return hipGetLastError();
 }
 

@@ -62,6 +62,21 @@ def first_neighbor(row_ptr: np.ndarray, col: np.ndarray) -> np.ndarray:
     return key
 
 
+def last_neighbor(row_ptr: np.ndarray, col: np.ndarray) -> np.ndarray:
+    """Largest neighbour id per node (-1 for an isolated node): the derive
+    mode's locality key (roots with the same largest neighbour tend to share
+    most neighbours: a fabric's racks and fabric switches of one pod, the
+    spines of one plane), so a block's group and its neighbours' level rows
+    stay together in the caches."""
+    V = row_ptr.size - 1
+    deg = np.diff(row_ptr.astype(np.int64))
+    owner = np.repeat(np.arange(V), deg)
+    key = np.full(V, -1, np.int64)
+    ok = col != owner
+    np.maximum.at(key, owner[ok], col[ok].astype(np.int64))
+    return key
+
+
 def locality_order(roots: np.ndarray, key: np.ndarray) -> np.ndarray:
     """Roots grouped by their smallest neighbour (stable): roots hanging off
     the same hub share frontiers and next-hop planes in a multi-source batch,

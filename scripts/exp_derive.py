@@ -35,7 +35,8 @@ def main():
     perm = np.random.default_rng(0x5EED).permutation(V).astype(np.uint32)
     nbrs = shard.distinct_neighbors(csr["row_ptr"], csr["col"])
     key = shard.first_neighbor(csr["row_ptr"], csr["col"])
-    classes = shard.make_classes(perm, shard.neighbor_caps(nbrs), V, key, max_grouped_words=1)
+    classes = shard.make_classes(perm, shard.neighbor_caps(nbrs), V,
+                                 shard.last_neighbor(csr["row_ptr"], csr["col"]))
     order = np.concatenate([c.roots for c in classes])  # phase 1 order: class by class
     pos = np.empty(V, np.uint32)
     pos[order] = np.arange(V, dtype=np.uint32)
