@@ -435,7 +435,7 @@ def derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
     t0 = time.time()
     d_clo = torch.from_numpy(clo.view(np.int32)).to(dev)
     d_pos = torch.from_numpy(pos.view(np.int32)).to(dev)
-    lev = torch.empty((clo.size, V), dtype=torch.uint8, device=dev)
+    lev = torch.empty((clo.size, eng.lev_pitch), dtype=torch.uint8, device=dev)
     dist = torch.empty((clo.size, V), dtype=torch.int32, device=dev)
     ldg = torch.empty((clo.size, 3), dtype=torch.int64, device=dev)
     classes = []

@@ -175,7 +175,8 @@ int ospf_sync(ospf_ctx* ctx, void* stream);
 /* All-sources next hops in two phases ("derive", unit metric or hop count).
  * ospf_levels_dev: distances of the n device roots by the distance-only
  * multi-source BFS, written as d_dist [n][V] u32 rows (optional), byte level
- * rows d_lev [n][V] (dist + 1, 0 = unreached) and, optional, the distance
+ * rows d_lev [n][lev_pitch] (dist + 1, 0 = unreached; lev_pitch a multiple
+ * of 16 >= V, padding zeroed) and, optional, the distance
  * part {reached, sum dist, sum dist_key * (dist + 1)} of each run's digest.
  * ospf_nh_derive_dev: next-hop words [n][V][nh_words] (+ complete digests) of
  * the n device roots from level rows: d_lev_pos[v] = row of node v in d_lev
@@ -187,9 +188,10 @@ int ospf_sync(ospf_ctx* ctx, void* stream);
  * an up link, n transit or n == v, and dist(n, v) + 1 == dist(root, v) (the
  * reference's nextHops, LinkState.cpp:885-901). Both queue on `stream`. */
 int ospf_levels_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n, uint32_t flags,
-                    uint32_t* d_dist, uint8_t* d_lev, ospf_digest* d_lev_digest, void* stream);
+                    uint32_t* d_dist, uint8_t* d_lev, uint32_t lev_pitch,
+                    ospf_digest* d_lev_digest, void* stream);
 int ospf_nh_derive_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n, uint32_t nh_words,
-                       uint32_t max_root_neighbors, const uint8_t* d_lev,
+                       uint32_t max_root_neighbors, const uint8_t* d_lev, uint32_t lev_pitch,
                        const uint32_t* d_lev_pos, const ospf_digest* d_lev_digest,
                        uint32_t* d_nh, ospf_digest* d_digest, void* stream);
 

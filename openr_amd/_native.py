@@ -121,8 +121,8 @@ def engine() -> C.CDLL:
         L.ospf_run_batch_dev.argtypes = [vp, C.POINTER(ospf_batch), vp]
         L.ospf_ksp2_run.argtypes = [vp, C.POINTER(ospf_ksp2)]
         L.ospf_ksp2_dev.argtypes = [vp, C.POINTER(ospf_ksp2), vp]
-        L.ospf_levels_dev.argtypes = [vp, vp, u32, u32, vp, vp, vp, vp]
-        L.ospf_nh_derive_dev.argtypes = [vp, vp, u32, u32, u32, vp, vp, vp, vp, vp, vp]
+        L.ospf_levels_dev.argtypes = [vp, vp, u32, u32, vp, vp, u32, vp, vp]
+        L.ospf_nh_derive_dev.argtypes = [vp, vp, u32, u32, u32, vp, u32, vp, vp, vp, vp, vp]
         L.ospf_update_links.argtypes = [vp, vp, u32, u64]
         L.ospf_update_nodes.argtypes = [vp, vp, vp, u32, u64]
         L.ospf_affected_roots.argtypes = [vp, vp, u32, u32, vp, u32, vp, vp]

@@ -1167,11 +1167,14 @@ int ospf_sync(ospf_ctx* c, void* stream) {
 // byte level rows; then each root's next-hop words from its neighbours'
 // level rows. Unit metric or hop count, depth bound <= 253.
 int ospf_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t flags,
-                    uint32_t* d_dist, uint8_t* d_lev, ospf_digest* d_lev_digest, void* stream) {
+                    uint32_t* d_dist, uint8_t* d_lev, uint32_t lev_pitch,
+                    ospf_digest* d_lev_digest, void* stream) {
   if (!c) return OSPF_E_INVAL;
   if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
   if (n == 0) return OSPF_OK;
   if (!d_roots || !d_lev) return fail(c, OSPF_E_INVAL, "null roots / level rows");
+  if (lev_pitch % 16u || lev_pitch < c->info.n_nodes)
+    return fail(c, OSPF_E_INVAL, "lev_pitch: a multiple of 16 >= V");
   if (!(flags & OSPF_HOP_COUNT) && !c->info.unit_metric)
     return fail(c, OSPF_E_RANGE, "level rows need unit metric or hop count");
   if (c->depth_bound > 253) return fail(c, OSPF_E_RANGE, "depth bound above 253 (byte levels)");
@@ -1206,6 +1209,7 @@ int ospf_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t f
   a.err = c->d_err;
   a.dist = d_dist;
   a.levrow = d_lev;
+  a.lev_pitch = lev_pitch;
   a.digest = d_lev_digest;
   if (d_lev_digest) HIPCHK(c, hipMemsetAsync(d_lev_digest, 0, (size_t)n * sizeof(ospf_digest), s));
   for (uint32_t vb0 = 0; vb0 < total_vb; vb0 += nb_max) {
@@ -1228,13 +1232,15 @@ int ospf_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t f
 }
 
 int ospf_nh_derive_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t nh_words,
-                       uint32_t max_root_neighbors, const uint8_t* d_lev,
+                       uint32_t max_root_neighbors, const uint8_t* d_lev, uint32_t lev_pitch,
                        const uint32_t* d_lev_pos, const ospf_digest* d_lev_digest,
                        uint32_t* d_nh, ospf_digest* d_digest, void* stream) {
   if (!c) return OSPF_E_INVAL;
   if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
   if (n == 0) return OSPF_OK;
   if (!d_roots || !d_lev || !d_lev_pos || !d_nh) return fail(c, OSPF_E_INVAL, "null argument");
+  if (lev_pitch % 16u || lev_pitch < c->info.n_nodes)
+    return fail(c, OSPF_E_INVAL, "lev_pitch: a multiple of 16 >= V");
   if (d_digest && !d_lev_digest)
     return fail(c, OSPF_E_INVAL, "derive: digests need the level rows' digests");
   if (nh_words == 0 || nh_words > 64) return fail(c, OSPF_E_RANGE, "derive: nh_words 1..64");
@@ -1249,6 +1255,7 @@ int ospf_nh_derive_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_
   d.W = nh_words;
   d.cap = std::min<uint32_t>(cap, 2048u);
   d.lev = d_lev;
+  d.pitch = lev_pitch;
   d.pos = d_lev_pos;
   d.lev_digest = d_lev_digest;
   if (const char* e = getenv("OSPF_DERIVE_CTILES")) d.ctiles = (uint32_t)std::max(1, atoi(e));

@@ -185,7 +185,8 @@ struct MsArgs {
   uint32_t* igb;          // [nb][igw]
   uint64_t* igm;          // [nb][E]
   uint32_t igw;
-  uint8_t* levrow;        // derive phase 1 (kp -1): [n][V] dist + 1 per (run, node)
+  uint8_t* levrow;        // derive phase 1 (kp -1): [n][lev_pitch] dist + 1 per (run, node)
+  uint32_t lev_pitch;     //   bytes per level row (multiple of 16, >= V; padding zeroed)
 };
 
 // Derive phase 2 (nh_derive_kernel): next-hop words of n roots from the level
@@ -194,7 +195,8 @@ struct DeriveArgs {
   const uint32_t* roots;
   uint32_t n, W;
   uint32_t cap;            // max distinct neighbours of a root of the call (<= 2048)
-  const uint8_t* lev;      // [rows][V]
+  const uint8_t* lev;      // [rows][pitch]
+  uint32_t pitch;          // bytes per level row (multiple of 16, >= V)
   const uint32_t* pos;     // [V]
   const ospf_digest* lev_digest;  // [rows] distance part of each row's digest (phase 1)
   uint32_t* nh;            // [n][V][W]

@@ -41,6 +41,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "spf_kernels.h"
 
@@ -864,10 +865,12 @@ __global__ void __launch_bounds__(256) msbfs_levrows_kernel(DevGraph g, MsArgs a
   for (uint32_t i = tid; i < 64u * 16u; i += kBlock) {  // (root, node quad)
     const uint32_t r = i >> 4, q = i & 15u;
     if (r >= nr) break;
+    if (v0 + 4u * q >= a.lev_pitch) continue;
     uint32_t l[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) l[j] = (4u * q + j < nv) ? s_lev[(4u * q + j) * 64u + r] : 0u;
     const size_t off = (size_t)(b.rix0 + r) * V + v0 + 4u * q;
+    const size_t loff = (size_t)(b.rix0 + r) * a.lev_pitch + v0 + 4u * q;
     if (a.dist) {
       uint32_t* row = a.dist + off;
       if (vec) {
@@ -878,12 +881,8 @@ __global__ void __launch_bounds__(256) msbfs_levrows_kernel(DevGraph g, MsArgs a
           if (4u * q + j < nv) row[j] = l[j] ? l[j] - 1u : kInf;
       }
     }
-    if (vec) {
-      *reinterpret_cast<uint32_t*>(a.levrow + off) = l[0] | (l[1] << 8) | (l[2] << 16) | (l[3] << 24);
-    } else {
-      for (uint32_t j = 0; j < 4u; ++j)
-        if (4u * q + j < nv) a.levrow[off + j] = (uint8_t)l[j];
-    }
+    // rows are lev_pitch bytes (a multiple of 16): whole words, padding zeroed
+    *reinterpret_cast<uint32_t*>(a.levrow + loff) = l[0] | (l[1] << 8) | (l[2] << 16) | (l[3] << 24);
   }
 }
 
@@ -968,12 +967,12 @@ __global__ void __launch_bounds__(256) nh_derive_kernel(DevGraph g, DeriveArgs d
   const uint32_t t0 = ci * d.ctiles, t1 = min(d.tiles, t0 + d.ctiles);
   for (uint32_t t = t0; t < t1; ++t) {
     const uint32_t v0 = t * T, nv = min(T, V - v0);
-    const bool vec = (V & 3u) == 0 && nv == T;
+    const bool vec = nv == T;  // rows are pitch-aligned (16 B): whole words
     for (uint32_t x = tid; x < ng * (T / 4u); x += kBlock) {
       const uint32_t j = x / (T / 4u), qq = x - j * (T / 4u);
       uint32_t w4 = 0;
       if (s_own[j] != kInf) {
-        const uint8_t* orow = d.lev + (size_t)s_own[j] * V + v0 + 4u * qq;
+        const uint8_t* orow = d.lev + (size_t)s_own[j] * d.pitch + v0 + 4u * qq;
         if (vec) {
           w4 = *reinterpret_cast<const uint32_t*>(orow);
         } else {
@@ -1013,7 +1012,7 @@ __global__ void __launch_bounds__(256) nh_derive_kernel(DevGraph g, DeriveArgs d
                 if (p != kInf && b < 4u) A |= 1u << (8u * b + kk);
                 continue;
               }
-              const uint8_t* nrow = d.lev + (size_t)p * V + v0 + n0;
+              const uint8_t* nrow = d.lev + (size_t)p * d.pitch + v0 + n0;
               uint32_t x4;
               if (vec) {
                 x4 = *reinterpret_cast<const uint32_t*>(nrow);
@@ -1071,6 +1070,175 @@ __global__ void __launch_bounds__(256) nh_derive_kernel(DevGraph g, DeriveArgs d
         atomicAdd((unsigned long long*)&dg->sum_dist, (unsigned long long)ld.sum_dist);
         h += ld.hash;
       }
+    }
+    if (h) atomicAdd((unsigned long long*)&dg->hash, h);
+  }
+}
+
+// Narrow rows (W <= 4 words): a wave per (root, 1,024-node tile), each lane
+// 16 consecutive nodes: one 16-B load per neighbour row per lane (a wave reads
+// 1 KB of a row at once), SWAR compares on four words, the W words of the
+// lane's 16 nodes in registers, stored as the lane's contiguous 64 W bytes.
+// Block = group of G roots x chunk of tiles (chunk-major, XCD-grouped, as in
+// nh_derive_kernel); its 4 waves take (tile, root) pairs.
+template <int W>
+__global__ void __launch_bounds__(256) nh_derive16_kernel(DevGraph g, DeriveArgs d) {
+  __shared__ uint32_t s_pos[kDeriveTab];
+  __shared__ uint32_t s_K[kDeriveMaxG], s_root[kDeriveMaxG], s_own[kDeriveMaxG];
+  __shared__ unsigned long long s_h[kDeriveMaxG];
+  const uint32_t V = g.V, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t G = d.G, cap = d.cap;
+  const uint32_t ngroups = (d.n + G - 1) / G;
+  const uint32_t ci = blockIdx.x / ngroups, rr = blockIdx.x % ngroups;
+  const uint32_t full = ngroups / 8u * 8u;
+  const uint32_t gi = rr < full ? (rr % 8u) * (full / 8u) + rr / 8u : rr;
+  const uint32_t i0 = gi * G, ng = min(G, d.n - i0);
+  if (tid < ng) {
+    const uint32_t r = d.roots[i0 + tid];
+    s_root[tid] = r;
+    s_h[tid] = 0ull;
+    s_own[tid] = kInf;
+    s_K[tid] = 0;
+    if (r >= V) {
+      atomicOr(d.err, 64u);
+    } else {
+      const uint32_t K = g.dn_off[r + 1] - g.dn_off[r];
+      s_own[tid] = d.pos[r];
+      if (K > cap || K > 32u * W || s_own[tid] == kInf)
+        atomicOr(d.err, s_own[tid] == kInf ? 16u : 1u);
+      if (s_own[tid] != kInf) s_K[tid] = min(K, cap);
+    }
+  }
+  for (uint32_t x = tid; x < ng * cap; x += kBlock) s_pos[x] = kInf;
+  __syncthreads();
+  for (uint32_t j = 0; j < ng; ++j) {
+    const uint32_t r = s_root[j];
+    if (r >= V) continue;
+    for (uint32_t e = g.row_ptr[r] + tid; e < g.row_ptr[r + 1]; e += kBlock) {
+      const uint32_t cx = g.colx[e];
+      if ((cx & kDown) || cx == r) continue;
+      const uint32_t k = g.didx[e];
+      if (k < s_K[j]) s_pos[j * cap + k] = 0u;
+    }
+  }
+  __syncthreads();
+  for (uint32_t x = tid; x < ng * cap; x += kBlock) {
+    const uint32_t j = x / cap, k = x - j * cap;
+    if (k >= s_K[j] || s_pos[x] == kInf) continue;
+    const uint32_t n = g.dn[g.dn_off[s_root[j]] + k];
+    const uint32_t p = d.pos[n];
+    if (transit(g, n)) {
+      s_pos[x] = p;
+      if (p == kInf) atomicOr(d.err, 16u);
+    } else {
+      s_pos[x] = 0x80000000u | n;
+    }
+  }
+  __syncthreads();
+  const uint32_t t0 = ci * d.ctiles, t1 = min(d.tiles, t0 + d.ctiles), nt = t1 - t0;
+  for (uint32_t pr = wave; pr < nt * ng; pr += kWavesPerBlock) {
+    const uint32_t t = t0 + pr / ng, j = pr % ng;
+    const uint32_t own = s_own[j], K = s_K[j];
+    if (own == kInf) continue;
+    const uint32_t vl = t * 1024u + 16u * lane;  // this lane's first node
+    const bool live = vl < d.pitch;             // inside the (16-aligned) rows
+    uint4 L = make_uint4(0, 0, 0, 0);
+    if (live) L = *reinterpret_cast<const uint4*>(d.lev + (size_t)own * d.pitch + vl);
+    uint32_t lm1[4];
+    {
+      const uint32_t Lw[4] = {L.x, L.y, L.z, L.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const uint32_t l = (Lw[q] >> (8 * b)) & 0xFFu;
+          m |= (l >= 2u ? l - 1u : 0xFFu) << (8 * b);
+        }
+        lm1[q] = m;
+      }
+    }
+    uint32_t word[W][16];
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+#pragma unroll
+      for (int n = 0; n < 16; ++n) word[w][n] = 0u;
+    const uint32_t* tab = s_pos + j * cap;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+#pragma unroll
+      for (int k8 = 0; k8 < 32; k8 += 8) {
+        const uint32_t kb = 32u * w + k8;
+        if (kb >= K) break;
+        uint32_t A[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {
+          const uint32_t p = (kb + kk < K) ? tab[kb + kk] : kInf;
+          if (p >= 0x80000000u) {
+            const uint32_t off = (p & 0x7FFFFFFFu) - vl;
+            if (p != kInf && off < 16u) A[off >> 2] |= 1u << (8u * (off & 3u) + kk);
+            continue;
+          }
+          if (!live) continue;
+          const uint4 x = *reinterpret_cast<const uint4*>(d.lev + (size_t)p * d.pitch + vl);
+          const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t df = xw[q] ^ lm1[q];
+            const uint32_t z = ~(((df & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | df | 0x7F7F7F7Fu);
+            A[q] |= (z >> 7) << kk;
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) word[w][4 * q + b] |= ((A[q] >> (8 * b)) & 0xFFu) << k8;
+      }
+    }
+    // the lane's 16 nodes x W words: contiguous in the root's row
+    const size_t i = i0 + j;
+    uint32_t* dst = d.nh + ((size_t)i * V + vl) * W;
+    if (vl + 16u <= V && ((((size_t)i * V + vl) * W) & 3u) == 0) {
+#pragma unroll
+      for (int x = 0; x < 4 * W; ++x) {
+        uint32_t v4[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int f = 4 * x + c;  // flat index node * W + word
+          v4[c] = word[f % W][f / W];
+        }
+        reinterpret_cast<uint4*>(dst)[x] = make_uint4(v4[0], v4[1], v4[2], v4[3]);
+      }
+    } else if (vl < V) {
+      for (uint32_t n = 0; n < 16u && vl + n < V; ++n)
+#pragma unroll
+        for (int w = 0; w < W; ++w) dst[n * W + w] = word[w][n];
+    }
+    if (d.digest) {
+      uint64_t h = 0;
+#pragma unroll
+      for (int n = 0; n < 16; ++n) {
+        if (vl + n >= V) break;
+        uint64_t ws = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+          if (word[w][n]) ws += digest_word_key(w, word[w][n]);
+        if (ws) h += g.dkey[2ull * (vl + n) + 1] * ws;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) h += shfl_xor64(h, o);
+      if (lane == 0 && h) atomicAdd(&s_h[j], (unsigned long long)h);
+    }
+  }
+  __syncthreads();
+  if (d.digest && tid < ng) {
+    ospf_digest* dg = d.digest + i0 + tid;
+    unsigned long long h = s_h[tid];
+    if (ci == 0 && s_own[tid] != kInf) {
+      const ospf_digest ld = d.lev_digest[s_own[tid]];
+      atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)ld.reached);
+      atomicAdd((unsigned long long*)&dg->sum_dist, (unsigned long long)ld.sum_dist);
+      h += ld.hash;
     }
     if (h) atomicAdd((unsigned long long*)&dg->hash, h);
   }
@@ -1284,6 +1452,20 @@ hipError_t launch_nh_derive(const DevGraph& g, const DeriveArgs& d0, hipStream_t
   if (d.n == 0) return hipSuccess;
   if (d.W == 0 || d.W > kDeriveTab / 32u || d.cap == 0 || d.cap > kDeriveTab)
     return hipErrorInvalidValue;
+  if (d.W <= 4 && !getenv("OSPF_DERIVE_QUAD")) {  // lane = 16 nodes, words in registers
+    d.G = std::max<uint32_t>(1, std::min<uint32_t>(kDeriveMaxG, kDeriveTab / d.cap));
+    d.tiles = (g.V + 1023u) / 1024u;
+    d.ctiles = std::max<uint32_t>(1, std::min<uint32_t>(d.tiles, d.ctiles ? d.ctiles : 8));
+    d.chunks = (d.tiles + d.ctiles - 1) / d.ctiles;
+    const dim3 grid(((d.n + d.G - 1) / d.G) * d.chunks);
+    switch (d.W) {
+      case 1: hipLaunchKernelGGL(nh_derive16_kernel<1>, grid, dim3(kBlock), 0, s, g, d); break;
+      case 2: hipLaunchKernelGGL(nh_derive16_kernel<2>, grid, dim3(kBlock), 0, s, g, d); break;
+      case 3: hipLaunchKernelGGL(nh_derive16_kernel<3>, grid, dim3(kBlock), 0, s, g, d); break;
+      default: hipLaunchKernelGGL(nh_derive16_kernel<4>, grid, dim3(kBlock), 0, s, g, d); break;
+    }
+    return hipGetLastError();
+  }
   // one thread per node quad does all the words up to 8; wider rows split a
   // quad's words over 4 threads (a spine: 14 words x 32 neighbours each)
   const int S = d.W <= 8 ? 1 : 4;

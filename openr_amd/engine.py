@@ -155,25 +155,32 @@ class Engine:
                          d_digest or None)
         self._check(self._L.ospf_run_batch_dev(self._h, C.byref(b), stream or None))
 
+    @property
+    def lev_pitch(self) -> int:
+        """Bytes per level row for levels_dev / nh_derive_dev (V rounded up to 16)."""
+        return (self.V + 15) // 16 * 16
+
     def levels_dev(self, d_roots: int, n: int, d_lev: int, *, d_dist: int = 0,
-                   d_lev_digest: int = 0, hop_count: bool = False, stream: int = 0) -> None:
+                   d_lev_digest: int = 0, hop_count: bool = False, stream: int = 0,
+                   lev_pitch: int = 0) -> None:
         """Derive phase 1 (ospf_levels_dev): dist rows [n][V] (optional), byte
-        level rows [n][V] and the distance part of each run's digest
+        level rows [n][lev_pitch] and the distance part of each run's digest
         (optional, [n][3] u64) of the n device roots."""
         self._check(self._L.ospf_levels_dev(self._h, d_roots, n,
                                             N.OSPF_HOP_COUNT if hop_count else 0,
-                                            d_dist or None, d_lev, d_lev_digest or None,
-                                            stream or None))
+                                            d_dist or None, d_lev, lev_pitch or self.lev_pitch,
+                                            d_lev_digest or None, stream or None))
 
     def nh_derive_dev(self, d_roots: int, n: int, nh_words: int, d_lev: int, d_pos: int,
                       d_nh: int, *, d_lev_digest: int = 0, d_digest: int = 0,
-                      max_root_neighbors: int = 0, stream: int = 0) -> None:
+                      max_root_neighbors: int = 0, stream: int = 0, lev_pitch: int = 0) -> None:
         """Derive phase 2 (ospf_nh_derive_dev): next-hop rows [n][V][nh_words]
         (+ digests, completing d_lev_digest's parts) from level rows;
         d_pos[v] = level row of node v."""
         self._check(self._L.ospf_nh_derive_dev(self._h, d_roots, n, nh_words, max_root_neighbors,
-                                               d_lev, d_pos, d_lev_digest or None, d_nh,
-                                               d_digest or None, stream or None))
+                                               d_lev, lev_pitch or self.lev_pitch, d_pos,
+                                               d_lev_digest or None, d_nh, d_digest or None,
+                                               stream or None))
 
     def ksp2(self, src: int, dsts: Sequence[int], path_cap: int = 512):
         """getKthPaths(src, d, 1) and (src, d, 2) for every d (ospf_ksp2_run).

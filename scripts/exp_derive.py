@@ -42,7 +42,7 @@ def main():
     pos[order] = np.arange(V, dtype=np.uint32)
     d_order = torch.from_numpy(order.view(np.int32)).to(dev)
     d_pos = torch.from_numpy(pos.view(np.int32)).to(dev)
-    lev = torch.empty((V, V), dtype=torch.uint8, device=dev)
+    lev = torch.empty((V, eng.lev_pitch), dtype=torch.uint8, device=dev)
     dist = torch.empty((V, V), dtype=torch.int32, device=dev)
     ldg = torch.empty((V, 3), dtype=torch.int64, device=dev)
     bufs = []

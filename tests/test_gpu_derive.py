@@ -21,7 +21,7 @@ def derive_all(eng, V, hop=False, roots=None):
     dev = torch.device("cuda", 0)
     all_ids = np.arange(V, dtype=np.uint32)
     d_all = torch.from_numpy(all_ids.view(np.int32)).to(dev)
-    lev = torch.empty((V, V), dtype=torch.uint8, device=dev)
+    lev = torch.empty((V, eng.lev_pitch), dtype=torch.uint8, device=dev)
     dist = torch.empty((V, V), dtype=torch.int32, device=dev)
     ldg = torch.empty((V, 3), dtype=torch.int64, device=dev)
     eng.levels_dev(d_all.data_ptr(), V, lev.data_ptr(), d_dist=dist.data_ptr(),
@@ -130,7 +130,7 @@ def test_derive_missing_neighbour_row_is_an_error():
         dev = torch.device("cuda", 0)
         ids = np.arange(V, dtype=np.uint32)
         d_all = torch.from_numpy(ids.view(np.int32)).to(dev)
-        lev = torch.empty((V, V), dtype=torch.uint8, device=dev)
+        lev = torch.empty((V, eng.lev_pitch), dtype=torch.uint8, device=dev)
         eng.levels_dev(d_all.data_ptr(), V, lev.data_ptr())
         pos = ids.copy()
         pos[ls.node_names().index("2-0-0")] = 0xFFFFFFFF  # a neighbour of rack 3-0-0
@@ -143,3 +143,20 @@ def test_derive_missing_neighbour_row_is_an_error():
             eng.sync()
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("pods", [200, 300])  # spines with 7 / 10 next-hop words
+def test_derive_wide_word_kernels(pods):
+    st = T.fabric(pods=pods, planes=1)
+    ls = LinkState()
+    ls.apply(st)
+    names = ls.node_names()
+    roots = [names.index(r) for r in ("1-0-0", "1-0-35", "2-0-0", "2-137-0", "3-5-7", "3-199-47")]
+    check_against_engine(st, roots=roots)
+
+
+def test_derive_quad_kernel_for_narrow_rows(monkeypatch):
+    monkeypatch.setenv("OSPF_DERIVE_QUAD", "1")
+    stream, _ = random_stream(7, n=70, unit=True)
+    check_against_engine(stream)
+    check_against_engine(T.fabric(pods=12, planes=8))
