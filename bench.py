@@ -438,17 +438,28 @@ def derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
     lev = torch.empty((clo.size, eng.lev_pitch), dtype=torch.uint8, device=dev)
     dist = torch.empty((clo.size, V), dtype=torch.int32, device=dev)
     ldg = torch.empty((clo.size, 3), dtype=torch.int64, device=dev)
+    nbrs = shard.distinct_neighbors(rp, col)
+    flags = N.OSPF_WANT_DIST | N.OSPF_WANT_NH | N.OSPF_WANT_DIGEST
     classes = []
     for cap in all_caps:
         roots = cls_all[rank][cap]
         W = max(1, cap // 32) if cap > 16 else 1
         slot = max(1, max(c[cap].size for c in cls_all))
-        classes.append(dict(cap=cap, W=W, roots=roots, n=int(roots.size),
-                            d=torch.from_numpy(roots.view(np.int32)).to(dev),
-                            nh=torch.empty((max(1, roots.size), V, W), dtype=torch.int32,
-                                           device=dev),
-                            dig=torch.zeros((slot, 3), dtype=torch.int64, device=dev),
-                            stream=torch.cuda.Stream(device=dev), ms=[]))
+        # rows of up to 4 words derive from the level rows (lane-16 kernel);
+        # wider ones (spines) run the bit-plane batch path on their own
+        # stream, concurrently with phase 1 (they need no level rows)
+        kind = "derive" if W <= 4 else "batch"
+        c = dict(cap=cap, W=W, roots=roots, n=int(roots.size), kind=kind,
+                 d=torch.from_numpy(roots.view(np.int32)).to(dev),
+                 nh=torch.empty((max(1, roots.size), V, W), dtype=torch.int32, device=dev),
+                 dig=torch.zeros((slot, 3), dtype=torch.int64, device=dev),
+                 stream=torch.cuda.Stream(device=dev), ms=[])
+        if kind == "batch" and roots.size:
+            c["max_nbrs"] = int(max(1, nbrs[roots].max()))
+            c["plan"] = eng.plan(W, flags, n_roots=int(roots.size),
+                                 max_root_neighbors=c["max_nbrs"])
+            c["dist"] = torch.empty((roots.size, V), dtype=torch.int32, device=dev)
+        classes.append(c)
     log(f"[rank {rank}] derive: {mine.size} roots, closure {clo.size}, buffers "
         f"{(lev.numel() + dist.numel() * 4 + sum(c['nh'].numel() * 4 for c in classes)) / 2**30:.1f}"
         f" GiB in {time.time() - t0:.1f}s")
@@ -459,7 +470,12 @@ def derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
                        d_lev_digest=ldg.data_ptr(), stream=s_.cuda_stream)
 
     def phase2(c, s_):
-        if c["n"]:
+        if c["n"] and c["kind"] == "batch":
+            eng.run_dev(c["d"].data_ptr(), c["n"], c["W"], flags=flags,
+                        d_dist=c["dist"].data_ptr(), d_nh=c["nh"].data_ptr(),
+                        d_digest=c["dig"].data_ptr(), stream=s_.cuda_stream,
+                        max_root_neighbors=c["max_nbrs"])
+        elif c["n"]:
             eng.nh_derive_dev(c["d"].data_ptr(), c["n"], c["W"], lev.data_ptr(), d_pos.data_ptr(),
                               c["nh"].data_ptr(), d_lev_digest=ldg.data_ptr(),
                               d_digest=c["dig"].data_ptr(), max_root_neighbors=c["cap"],
@@ -470,10 +486,23 @@ def derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
     def step(timed):
         a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a_.record(main_s)
+        done = []
+        for c in classes:  # batch classes start with the step (no level rows needed)
+            if c["kind"] == "batch":
+                cs = c["stream"]
+                cs.wait_event(a_)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(cs)
+                phase2(c, cs)
+                e1.record(cs)
+                done.append(e1)
+                if timed:
+                    c["ms"].append((e0, e1))
         phase1(main_s)
         b_.record(main_s)
-        done = []
         for c in sorted(classes, key=lambda c: -c["W"] * c["n"]):
+            if c["kind"] == "batch":
+                continue
             cs = c["stream"]
             cs.wait_event(b_)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -551,9 +580,20 @@ def derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
               "compulsory_bytes": int(clo.size) * 4 * V + scans,
               "traffic": pmc_traffic(args.profile_dir, "derive_levels", int(clo.size))}]
     for c in classes:
-        if c["n"]:
+        if c["n"] and c["kind"] == "batch":
+            p = c["plan"]
+            units.append({"launch": f"batch_cap{c['cap']}",
+                          "kernel": f"variant {p['variant']} class launch ({c['W']} next-hop "
+                                    f"words: multi-source BFS with bit-planes)",
+                          "cap": c["cap"], "nh_words": c["W"], "roots_per_launch": c["n"],
+                          "isolated_launch_ms": round(c["iso_ms"], 3),
+                          "compulsory_bytes": compulsory_bytes(V, E, c["W"], c["n"], p["variant"],
+                                                               p["slices"], False),
+                          "traffic": pmc_traffic(args.profile_dir,
+                                                 f"variant{p['variant']}_cap{c['cap']}", c["n"])})
+        elif c["n"]:
             units.append({"launch": f"derive_cap{c['cap']}",
-                          "kernel": f"ospf_nh_derive_dev (nh_derive_kernel, {c['W']} next-hop "
+                          "kernel": f"ospf_nh_derive_dev (nh_derive16_kernel, {c['W']} next-hop "
                                     f"word(s))", "cap": c["cap"], "nh_words": c["W"],
                           "roots_per_launch": c["n"], "isolated_launch_ms": round(c["iso_ms"], 3),
                           "compulsory_bytes": c["n"] * 4 * V * c["W"],
@@ -565,7 +605,9 @@ def derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
         u["traffic_over_compulsory"] = (round(u["traffic"] / u["compulsory_bytes"], 2)
                                         if u["traffic"] else None)
     dom = max(units, key=lambda u: u["isolated_launch_ms"])
-    step_comp = sum(c["n"] * 4 * V * (1 + c["W"]) for c in classes) + scans
+    step_comp = sum(c["n"] * 4 * V * (1 + c["W"]) for c in classes) + scans + sum(
+        -(-c["n"] // 64) * c["plan"]["slices"] * (4 * E + 4 * (V + 1))
+        for c in classes if c["kind"] == "batch" and c["n"])
     step_s = dt / args.steps
     roofline = {
         "bound": "hbm", "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -589,6 +631,7 @@ def derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
                     "avg_launch_ms": round(p1_avg, 3), "isolated_launch_ms": round(p1_iso, 3)}]
     for c in classes:
         classes_cfg.append({"cap": c["cap"], "nh_words": c["W"], "roots_this_rank": c["n"],
+                            "path": c["kind"],
                             "avg_launch_ms": round(float(np.mean(
                                 [a_.elapsed_time(b_) for a_, b_ in c["ms"]])), 3) if c["ms"] else 0.0,
                             "isolated_launch_ms": round(c["iso_ms"], 3)})

@@ -905,10 +905,14 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
     }
   }
   const size_t sz_didx = didx.size() * 2ull;
-  size_t off[13], tot = 0;
-  const size_t szs[13] = {sz_row, sz_e,     sz_e,  sz_e,   sz_e,  sz_nt,  sz_dnoff,
-                          sz_dn,  sz_big,   sz_key, sz_le, sz_ew, sz_didx};
-  for (int i = 0; i < 13; ++i) {
+  // node keys alone, padded to 16 nodes (derive: a lane's 16 nodes in 8 loads)
+  std::vector<uint64_t> dkn((V + 15) / 16 * 16, 0ull);
+  for (uint32_t u = 0; u < V; ++u) dkn[u] = dkey[2ull * u + 1];
+  const size_t sz_kn = dkn.size() * 8ull;
+  size_t off[14], tot = 0;
+  const size_t szs[14] = {sz_row, sz_e,     sz_e,  sz_e,   sz_e,  sz_nt,  sz_dnoff,
+                          sz_dn,  sz_big,   sz_key, sz_le, sz_ew, sz_didx, sz_kn};
+  for (int i = 0; i < 14; ++i) {
     off[i] = tot;
     tot += align_up(std::max<size_t>(szs[i], 4), 256);
   }
@@ -924,10 +928,10 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
     return fail(c, OSPF_E_NOMEM, std::string("hipMalloc graph: ") + hipGetErrorString(he));
   }
   char* base = (char*)c->d_graph;
-  const void* srcs[13] = {prow.data(), pcolx.data(), pw.data(), prw.data(), plink.data(),
+  const void* srcs[14] = {prow.data(), pcolx.data(), pw.data(), prw.data(), plink.data(),
                           nt.data(), dn_off.data(), dn.data(), big.data(), dkey.data(),
-                          link_e.data(), pew.data(), didx.data()};
-  for (int i = 0; i < 13; ++i)
+                          link_e.data(), pew.data(), didx.data(), dkn.data()};
+  for (int i = 0; i < 14; ++i)
     if (szs[i] && srcs[i]) HIPCHK(c, hipMemcpy(base + off[i], srcs[i], szs[i], hipMemcpyHostToDevice));
   c->g.V = V;
   c->g.E = Ep;
@@ -946,6 +950,7 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   c->g.link_e = (const uint32_t*)(base + off[10]);
   c->g.ew = ew_ok ? (const uint2*)(base + off[11]) : nullptr;
   c->g.didx = (const uint16_t*)(base + off[12]);
+  c->g.dkn = (const uint64_t*)(base + off[13]);
   c->ew_base = ew_ok ? (const uint32_t*)(base + off[11]) : nullptr;
   c->h_row_ptr.assign(csr->row_ptr, csr->row_ptr + V + 1);
   c->h_dn_off = std::move(dn_off);

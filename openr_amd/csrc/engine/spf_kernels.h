@@ -47,6 +47,7 @@ struct DevGraph {
   // neighbours (= its next-hop bit when the row node is a root); 0xFFFF for
   // self-loops and padding
   const uint16_t* didx;
+  const uint64_t* dkn;  // [V rounded up to 16] digest_node_key(v), zero padded
 };
 
 struct RunArgs {

@@ -1216,17 +1216,26 @@ __global__ void __launch_bounds__(256) nh_derive16_kernel(DevGraph g, DeriveArgs
     }
     if (d.digest) {
       uint64_t h = 0;
+      if (live) {
+      uint64_t kn[16];
+      const uint4* kp = reinterpret_cast<const uint4*>(g.dkn + vl);  // zero past V
+#pragma unroll
+      for (int x = 0; x < 8; ++x) {
+        const uint4 k2 = kp[x];
+        kn[2 * x] = ((uint64_t)k2.y << 32) | k2.x;
+        kn[2 * x + 1] = ((uint64_t)k2.w << 32) | k2.z;
+      }
 #pragma unroll
       for (int n = 0; n < 16; ++n) {
-        if (vl + n >= V) break;
         uint64_t ws = 0;
 #pragma unroll
         for (int w = 0; w < W; ++w)
           if (word[w][n]) ws += digest_word_key(w, word[w][n]);
-        if (ws) h += g.dkey[2ull * (vl + n) + 1] * ws;
+        h += kn[n] * ws;
       }
+      }  // live
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) h += shfl_xor64(h, o);
+      for (int o = 32; o > 0; o >>= 1) h += shfl_xor64(h, o);  // every lane of the wave
       if (lane == 0 && h) atomicAdd(&s_h[j], (unsigned long long)h);
     }
   }

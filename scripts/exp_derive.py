@@ -79,7 +79,7 @@ def main():
               file=sys.stderr, flush=True)
     # check sampled roots of every class against the per-batch engine path
     ok = True
-    for b in bufs:
+    for b in (bufs if args.check > 0 else []):
         c = b["c"]
         idx = np.random.default_rng(1).choice(c.roots.size, min(args.check, c.roots.size),
                                               replace=False)
