@@ -1086,6 +1086,7 @@ __global__ void __launch_bounds__(256) nh_derive16_kernel(DevGraph g, DeriveArgs
   __shared__ uint32_t s_pos[kDeriveTab];
   __shared__ uint32_t s_K[kDeriveMaxG], s_root[kDeriveMaxG], s_own[kDeriveMaxG];
   __shared__ unsigned long long s_h[kDeriveMaxG];
+  extern __shared__ uint32_t s_stage[];  // [4 waves][1024 nodes][W]
   const uint32_t V = g.V, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint32_t G = d.G, cap = d.cap;
   const uint32_t ngroups = (d.n + G - 1) / G;
@@ -1164,30 +1165,39 @@ __global__ void __launch_bounds__(256) nh_derive16_kernel(DevGraph g, DeriveArgs
 #pragma unroll
       for (int n = 0; n < 16; ++n) word[w][n] = 0u;
     const uint32_t* tab = s_pos + j * cap;
+    const uint32_t vs = live ? vl : 0u;  // a valid address for lanes past the rows
 #pragma unroll
     for (int w = 0; w < W; ++w) {
 #pragma unroll
       for (int k8 = 0; k8 < 32; k8 += 8) {
         const uint32_t kb = 32u * w + k8;
         if (kb >= K) break;
+        // branch-free: 8 table entries, then 8 loads in flight (skipped /
+        // non-transit entries load the own row and are masked out)
+        uint32_t pp[8];
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) pp[kk] = (kb + kk < K) ? tab[kb + kk] : kInf;
+        uint4 xv[8];
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {
+          const uint32_t row = pp[kk] < 0x80000000u ? pp[kk] : own;
+          xv[kk] = *reinterpret_cast<const uint4*>(d.lev + (size_t)row * d.pitch + vs);
+        }
         uint32_t A[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) {
-          const uint32_t p = (kb + kk < K) ? tab[kb + kk] : kInf;
-          if (p >= 0x80000000u) {
-            const uint32_t off = (p & 0x7FFFFFFFu) - vl;
-            if (p != kInf && off < 16u) A[off >> 2] |= 1u << (8u * (off & 3u) + kk);
-            continue;
-          }
-          if (!live) continue;
-          const uint4 x = *reinterpret_cast<const uint4*>(d.lev + (size_t)p * d.pitch + vl);
-          const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+          const uint32_t keep = (pp[kk] < 0x80000000u && live) ? 0xFFFFFFFFu : 0u;
+          const uint32_t xw[4] = {xv[kk].x, xv[kk].y, xv[kk].z, xv[kk].w};
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const uint32_t df = xw[q] ^ lm1[q];
-            const uint32_t z = ~(((df & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | df | 0x7F7F7F7Fu);
+            const uint32_t z = ~(((df & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | df | 0x7F7F7F7Fu) & keep;
             A[q] |= (z >> 7) << kk;
           }
+          // a non-transit neighbour: a next hop towards itself only
+          const uint32_t off = (pp[kk] & 0x7FFFFFFFu) - vl;
+          if (pp[kk] >= 0x80000000u && pp[kk] != kInf && off < 16u)
+            A[off >> 2] |= 1u << (8u * (off & 3u) + kk);
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -1195,25 +1205,34 @@ __global__ void __launch_bounds__(256) nh_derive16_kernel(DevGraph g, DeriveArgs
           for (int b = 0; b < 4; ++b) word[w][4 * q + b] |= ((A[q] >> (8 * b)) & 0xFFu) << k8;
       }
     }
-    // the lane's 16 nodes x W words: contiguous in the root's row
-    const size_t i = i0 + j;
-    uint32_t* dst = d.nh + ((size_t)i * V + vl) * W;
-    if (vl + 16u <= V && ((((size_t)i * V + vl) * W) & 3u) == 0) {
+    // the tile's 1,024 nodes x W words are contiguous in the root's row:
+    // staged through this wave's LDS slice so each store instruction writes
+    // 1 KB of consecutive row (per-lane 64 W-byte runs would leave partial
+    // lines: 5.6x the row bytes written at W = 3, measured)
+    uint32_t* st = s_stage + wave * 1024u * W;
 #pragma unroll
-      for (int x = 0; x < 4 * W; ++x) {
-        uint32_t v4[4];
+    for (int x = 0; x < 4 * W; ++x) {
+      uint32_t v4[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int f = 4 * x + c;  // flat index node * W + word
-          v4[c] = word[f % W][f / W];
-        }
-        reinterpret_cast<uint4*>(dst)[x] = make_uint4(v4[0], v4[1], v4[2], v4[3]);
+      for (int c = 0; c < 4; ++c) {
+        const int f = 4 * x + c;  // flat index node * W + word within the lane
+        v4[c] = word[f % W][f / W];
       }
-    } else if (vl < V) {
-      for (uint32_t n = 0; n < 16u && vl + n < V; ++n)
-#pragma unroll
-        for (int w = 0; w < W; ++w) dst[n * W + w] = word[w][n];
+      reinterpret_cast<uint4*>(st + 16u * W * lane)[x] = make_uint4(v4[0], v4[1], v4[2], v4[3]);
     }
+    __builtin_amdgcn_wave_barrier();  // LDS ops of a wave complete in order
+    const size_t i = i0 + j;
+    const uint32_t tv0 = t * 1024u, tn = min(1024u, V - tv0);
+    uint32_t* dst = d.nh + ((size_t)i * V + tv0) * W;
+    if (tn == 1024u && ((((size_t)i * V + tv0) * W) & 3u) == 0) {
+#pragma unroll
+      for (int x = 0; x < 4 * W; ++x)
+        reinterpret_cast<uint4*>(dst)[x * 64 + lane] =
+            reinterpret_cast<const uint4*>(st)[x * 64 + lane];
+    } else {
+      for (uint32_t x = lane; x < tn * W; x += 64u) dst[x] = st[x];
+    }
+    __builtin_amdgcn_wave_barrier();  // the slice is rewritten by the next pair
     if (d.digest) {
       uint64_t h = 0;
       if (live) {
@@ -1467,11 +1486,12 @@ hipError_t launch_nh_derive(const DevGraph& g, const DeriveArgs& d0, hipStream_t
     d.ctiles = std::max<uint32_t>(1, std::min<uint32_t>(d.tiles, d.ctiles ? d.ctiles : 8));
     d.chunks = (d.tiles + d.ctiles - 1) / d.ctiles;
     const dim3 grid(((d.n + d.G - 1) / d.G) * d.chunks);
+    const size_t lds = (size_t)kWavesPerBlock * 1024u * d.W * 4u;
     switch (d.W) {
-      case 1: hipLaunchKernelGGL(nh_derive16_kernel<1>, grid, dim3(kBlock), 0, s, g, d); break;
-      case 2: hipLaunchKernelGGL(nh_derive16_kernel<2>, grid, dim3(kBlock), 0, s, g, d); break;
-      case 3: hipLaunchKernelGGL(nh_derive16_kernel<3>, grid, dim3(kBlock), 0, s, g, d); break;
-      default: hipLaunchKernelGGL(nh_derive16_kernel<4>, grid, dim3(kBlock), 0, s, g, d); break;
+      case 1: hipLaunchKernelGGL(nh_derive16_kernel<1>, grid, dim3(kBlock), lds, s, g, d); break;
+      case 2: hipLaunchKernelGGL(nh_derive16_kernel<2>, grid, dim3(kBlock), lds, s, g, d); break;
+      case 3: hipLaunchKernelGGL(nh_derive16_kernel<3>, grid, dim3(kBlock), lds, s, g, d); break;
+      default: hipLaunchKernelGGL(nh_derive16_kernel<4>, grid, dim3(kBlock), lds, s, g, d); break;
     }
     return hipGetLastError();
   }
