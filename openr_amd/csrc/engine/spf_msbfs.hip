@@ -1081,6 +1081,118 @@ __global__ void __launch_bounds__(256) nh_derive_kernel(DevGraph g, DeriveArgs d
 // lane's 16 nodes in registers, stored as the lane's contiguous 64 W bytes.
 // Block = group of G roots x chunk of tiles (chunk-major, XCD-grouped, as in
 // nh_derive_kernel); its 4 waves take (tile, root) pairs.
+// Uniform group (every root of the block's group has the same <= KM
+// neighbour slots): each tile's neighbour rows are loaded once into registers
+// and compared against every root's own levels in turn. KM is a compile-time
+// bound (slots k >= K are masked, never branched on), so the register arrays
+// stay in registers.
+template <int KM>
+__device__ __forceinline__ void derive_uniform_tiles(
+    const DevGraph& g, const DeriveArgs& d, uint32_t t0, uint32_t t1, uint32_t ng, uint32_t i0,
+    const uint32_t* s_pos, const uint32_t* s_own, uint32_t K, uint32_t* s_stage,
+    const uint64_t* s_wk, unsigned long long* s_h, bool small, uint32_t lane, uint32_t wave) {
+  const uint32_t V = g.V;
+  for (uint32_t t = t0 + wave; t < t1; t += kWavesPerBlock) {
+    const uint32_t vl = t * 1024u + 16u * lane;
+    const bool live = vl < d.pitch;
+    const uint32_t vs = live ? vl : 0u;
+    uint4 xv[KM];
+    uint32_t pp[KM];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      pp[k] = (uint32_t)k < K ? s_pos[k] : kInf;
+      const uint32_t row = pp[k] < 0x80000000u ? pp[k] : s_own[0];
+      xv[k] = *reinterpret_cast<const uint4*>(d.lev + (size_t)row * d.pitch + vs);
+    }
+    uint64_t kn[16];
+    if (d.digest) {
+      const uint4* kp = reinterpret_cast<const uint4*>(g.dkn + vs);
+#pragma unroll
+      for (int x = 0; x < 8; ++x) {
+        const uint4 k2 = kp[x];
+        kn[2 * x] = ((uint64_t)k2.y << 32) | k2.x;
+        kn[2 * x + 1] = ((uint64_t)k2.w << 32) | k2.z;
+      }
+    }
+    uint32_t* st = s_stage + wave * 1024u;
+    const uint32_t tv0 = t * 1024u, tn = min(1024u, V - tv0);
+    for (uint32_t j = 0; j < ng; ++j) {
+      uint4 L = make_uint4(0, 0, 0, 0);
+      if (live) L = *reinterpret_cast<const uint4*>(d.lev + (size_t)s_own[j] * d.pitch + vl);
+      const uint32_t Lw[4] = {L.x, L.y, L.z, L.w};
+      uint32_t lm1[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const uint32_t l = (Lw[q] >> (8 * b)) & 0xFFu;
+          m |= (l >= 2u ? l - 1u : 0xFFu) << (8 * b);
+        }
+        lm1[q] = m;
+      }
+      uint32_t A0[4] = {0u, 0u, 0u, 0u}, A1[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int k = 0; k < KM; ++k) {
+        const uint32_t keep = (pp[k] < 0x80000000u && live) ? 0xFFFFFFFFu : 0u;
+        const uint32_t xw[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w};
+        uint32_t zz[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t df = xw[q] ^ lm1[q];
+          zz[q] = (~(((df & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | df | 0x7F7F7F7Fu) & keep) >> 7;
+        }
+        const uint32_t off = (pp[k] & 0x7FFFFFFFu) - vl;
+        if (pp[k] >= 0x80000000u && pp[k] != kInf && off < 16u) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if ((off >> 2) == (uint32_t)q) zz[q] |= 1u << (8u * (off & 3u));
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (k < 8) A0[q] |= zz[q] << k;
+          else A1[q] |= zz[q] << (k - 8);
+        }
+      }
+      uint32_t word[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          word[4 * q + b] = ((A0[q] >> (8 * b)) & 0xFFu) | (((A1[q] >> (8 * b)) & 0xFFu) << 8);
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+        reinterpret_cast<uint4*>(st + 16u * lane)[x] =
+            make_uint4(word[4 * x], word[4 * x + 1], word[4 * x + 2], word[4 * x + 3]);
+      __builtin_amdgcn_wave_barrier();
+      const size_t i = i0 + j;
+      uint32_t* dst = d.nh + (size_t)i * V + tv0;
+      if (tn == 1024u && (((size_t)i * V + tv0) & 3u) == 0) {
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+          reinterpret_cast<uint4*>(dst)[x * 64 + lane] = reinterpret_cast<const uint4*>(st)[x * 64 + lane];
+      } else {
+        for (uint32_t x = lane; x < tn; x += 64u) dst[x] = st[x];
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (d.digest) {
+        uint64_t h = 0;
+        if (live) {
+#pragma unroll
+          for (int n = 0; n < 16; ++n) {
+            const uint32_t wd = word[n];
+            const uint64_t ws = small ? s_wk[wd & 0xFFu] : (wd ? digest_word_key(0, wd) : 0ull);
+            h += kn[n] * ws;
+          }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) h += shfl_xor64(h, o);
+        if (lane == 0 && h) atomicAdd(&s_h[j], (unsigned long long)h);
+      }
+    }
+  }
+}
+
 template <int W>
 __global__ void __launch_bounds__(256) nh_derive16_kernel(DevGraph g, DeriveArgs d) {
   __shared__ uint32_t s_pos[kDeriveTab];
@@ -1135,12 +1247,12 @@ __global__ void __launch_bounds__(256) nh_derive16_kernel(DevGraph g, DeriveArgs
       s_pos[x] = 0x80000000u | n;
     }
   }
-  // a uniform group (every root with the same <= 16 neighbour slots: the
+  // a uniform group (every root with the same <= 8 neighbour slots: the
   // racks of one pod) loads each tile's neighbour rows once for all its roots;
   // one-word rows of <= 8 neighbours hash their words through a 256-entry table
   __shared__ uint32_t s_uni;
   __shared__ uint64_t s_wk[256];
-  if (tid == 0) s_uni = (W == 1 && ng > 1 && s_K[0] <= 16u && s_own[0] != kInf) ? 1u : 0u;
+  if (tid == 0) s_uni = (W == 1 && ng > 1 && s_K[0] <= 8u && s_own[0] != kInf) ? 1u : 0u;
   const bool small = W == 1 && cap <= 8u;
   if (small && d.digest) s_wk[tid] = tid ? digest_word_key(0, tid) : 0ull;
   __syncthreads();
@@ -1155,100 +1267,8 @@ __global__ void __launch_bounds__(256) nh_derive16_kernel(DevGraph g, DeriveArgs
   const uint32_t t0 = ci * d.ctiles, t1 = min(d.tiles, t0 + d.ctiles), nt = t1 - t0;
   if (s_uni) {
     if constexpr (W == 1) {
-      const uint32_t K = s_K[0];
-      for (uint32_t t = t0 + wave; t < t1; t += kWavesPerBlock) {
-        const uint32_t vl = t * 1024u + 16u * lane;
-        const bool live = vl < d.pitch;
-        const uint32_t vs = live ? vl : 0u;
-        uint4 xv[16];
-        uint32_t pp[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          pp[k] = (uint32_t)k < K ? s_pos[k] : kInf;
-          const uint32_t row = pp[k] < 0x80000000u ? pp[k] : s_own[0];
-          xv[k] = (uint32_t)k < K ? *reinterpret_cast<const uint4*>(d.lev + (size_t)row * d.pitch + vs)
-                                  : make_uint4(0, 0, 0, 0);
-        }
-        uint64_t kn[16];
-        if (d.digest) {
-          const uint4* kp = reinterpret_cast<const uint4*>(g.dkn + vs);
-#pragma unroll
-          for (int x = 0; x < 8; ++x) {
-            const uint4 k2 = kp[x];
-            kn[2 * x] = ((uint64_t)k2.y << 32) | k2.x;
-            kn[2 * x + 1] = ((uint64_t)k2.w << 32) | k2.z;
-          }
-        }
-        uint32_t* st = s_stage + wave * 1024u;
-        const uint32_t tv0 = t * 1024u, tn = min(1024u, V - tv0);
-        for (uint32_t j = 0; j < ng; ++j) {
-          uint4 L = make_uint4(0, 0, 0, 0);
-          if (live) L = *reinterpret_cast<const uint4*>(d.lev + (size_t)s_own[j] * d.pitch + vl);
-          const uint32_t Lw[4] = {L.x, L.y, L.z, L.w};
-          uint32_t lm1[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            uint32_t m = 0;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-              const uint32_t l = (Lw[q] >> (8 * b)) & 0xFFu;
-              m |= (l >= 2u ? l - 1u : 0xFFu) << (8 * b);
-            }
-            lm1[q] = m;
-          }
-          uint32_t A[2][4] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
-#pragma unroll
-          for (int k = 0; k < 16; ++k) {
-            if ((uint32_t)k >= K) break;
-            const uint32_t keep = (pp[k] < 0x80000000u && live) ? 0xFFFFFFFFu : 0u;
-            const uint32_t xw[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const uint32_t df = xw[q] ^ lm1[q];
-              const uint32_t z = ~(((df & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | df | 0x7F7F7F7Fu) & keep;
-              A[k >> 3][q] |= (z >> 7) << (k & 7);
-            }
-            const uint32_t off = (pp[k] & 0x7FFFFFFFu) - vl;
-            if (pp[k] >= 0x80000000u && pp[k] != kInf && off < 16u)
-              A[k >> 3][off >> 2] |= 1u << (8u * (off & 3u) + (k & 7));
-          }
-          uint32_t word[16];
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int b = 0; b < 4; ++b)
-              word[4 * q + b] = ((A[0][q] >> (8 * b)) & 0xFFu) | (((A[1][q] >> (8 * b)) & 0xFFu) << 8);
-#pragma unroll
-          for (int x = 0; x < 4; ++x)
-            reinterpret_cast<uint4*>(st + 16u * lane)[x] =
-                make_uint4(word[4 * x], word[4 * x + 1], word[4 * x + 2], word[4 * x + 3]);
-          __builtin_amdgcn_wave_barrier();
-          const size_t i = i0 + j;
-          uint32_t* dst = d.nh + (size_t)i * V + tv0;
-          if (tn == 1024u && (((size_t)i * V + tv0) & 3u) == 0) {
-#pragma unroll
-            for (int x = 0; x < 4; ++x)
-              reinterpret_cast<uint4*>(dst)[x * 64 + lane] = reinterpret_cast<const uint4*>(st)[x * 64 + lane];
-          } else {
-            for (uint32_t x = lane; x < tn; x += 64u) dst[x] = st[x];
-          }
-          __builtin_amdgcn_wave_barrier();
-          if (d.digest) {
-            uint64_t h = 0;
-            if (live) {
-#pragma unroll
-              for (int n = 0; n < 16; ++n) {
-                const uint32_t wd = word[n];
-                const uint64_t ws = small ? s_wk[wd & 0xFFu] : (wd ? digest_word_key(0, wd) : 0ull);
-                h += kn[n] * ws;
-              }
-            }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) h += shfl_xor64(h, o);
-            if (lane == 0 && h) atomicAdd(&s_h[j], (unsigned long long)h);
-          }
-        }
-      }
+      derive_uniform_tiles<8>(g, d, t0, t1, ng, i0, s_pos, s_own, s_K[0], s_stage, s_wk, s_h,
+                              small, lane, wave);
     }
   } else
   for (uint32_t pr = wave; pr < nt * ng; pr += kWavesPerBlock) {
