@@ -88,7 +88,7 @@ struct VB {
   const uint32_t* igb;  // KSP2 mode: ignored-edge bitmap and root masks
   const uint64_t* igm;
   __device__ VB(const MsArgs& a, uint32_t vbl_, uint32_t V_, int kp, uint32_t E = 0)
-      : vbl(vbl_), V(V_) {
+      : vbl(vbl_), V(V_), fs(kp > 0 ? 2u : 1u) {
     // Multi-pass rounds: the passes of one batch write different next-hop
     // words of the same row entries, so they go to one XCD (workgroup i of a
     // launch runs on XCD i % 8 and serves state slot vbl = i % nb): slot vbl
@@ -120,8 +120,10 @@ struct VB {
   }
   // frontier record of level d: {roots with v in the frontier, those of them
   // with a non-zero plane in this pass} (16 B per node)
+  // (KP <= 0, distances only: the record is the frontier word alone, 8 B)
+  uint32_t fs;  // u64 words per frontier record: 2 with planes, 1 without
   __device__ uint64_t* front(const MsArgs& a, uint32_t d) const {
-    return a.front + ((size_t)(d & 1u) * a.nb + vbl) * V * 2u;
+    return a.front + ((size_t)(d & 1u) * a.nb + vbl) * V * fs;
   }
 };
 
@@ -277,9 +279,9 @@ __global__ void __launch_bounds__(256) msbfs_init_kernel(DevGraph g, MsArgs a) {
     or64(&b.seen[v], bm);
     if (transit(g, v)) {
       const unsigned long long old =
-          atomicOr((unsigned long long*)&f1[2u * v], (unsigned long long)bm);
+          atomicOr((unsigned long long*)&f1[b.fs * v], (unsigned long long)bm);
       if (!old) mass += g.row_ptr[v + 1] - g.row_ptr[v];  // first root to reach v
-      if (in) or64(&f1[2u * v + 1u], bm);
+      if (in) or64(&f1[b.fs * v + 1u], bm);
     }
     if (in) or64(&b.P[(size_t)v * KP + k], 1ull << pb);
     if (a.defer) {
@@ -311,7 +313,14 @@ __device__ __forceinline__ void pull_scan(const DevGraph& g, const VB& b, const 
     const uint32_t cs[4] = {c.x, c.y, c.z, c.w};
     uint4 fs[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) fs[i] = (cs[i] & kDown) ? make_uint4(0, 0, 0, 0) : fr[cs[i]];
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (KP > 0) {
+        fs[i] = (cs[i] & kDown) ? make_uint4(0, 0, 0, 0) : fr[cs[i]];
+      } else {  // 8-B records: the frontier word alone
+        const uint64_t f = (cs[i] & kDown) ? 0ull : fcur[cs[i]];
+        fs[i] = make_uint4((uint32_t)f, (uint32_t)(f >> 32), 0u, 0u);
+      }
+    }
     uint64_t keep[4] = {~0ull, ~0ull, ~0ull, ~0ull};
     if (KP == 0) b.keep4(e, keep);
 #pragma unroll
@@ -389,7 +398,7 @@ __global__ void __launch_bounds__(256) msbfs_level_kernel(DevGraph g, MsArgs a, 
     const uint32_t u = g.big[bi];
     const uint32_t beg = g.row_ptr[u], end = g.row_ptr[u + 1];
     if (push) {
-      const uint64_t fu = fcur[2u * u];
+      const uint64_t fu = fcur[b.fs * u];
       if (!fu) return;
       uint64_t pu[kpa(KP)];
       load_planes<KP>(b.P, u, pu);
@@ -407,8 +416,8 @@ __global__ void __launch_bounds__(256) msbfs_level_kernel(DevGraph g, MsArgs a, 
     for (int k = 0; k < KP; ++k) pacc[k] = wave_or64(pacc[k]);
     const bool tr = transit(g, u);
     if (lane == 0) {
-      fnext[2u * u] = tr ? acc : 0ull;
-      fnext[2u * u + 1u] = tr ? planes_roots<KP>(a, pacc) & acc : 0ull;
+      fnext[b.fs * u] = tr ? acc : 0ull;
+      if constexpr (KP > 0) fnext[2u * u + 1u] = tr ? planes_roots<KP>(a, pacc) & acc : 0ull;
       if (acc) {
         b.seen[u] = (~m & b.valid) | acc;
 #pragma unroll
@@ -431,7 +440,7 @@ __global__ void __launch_bounds__(256) msbfs_level_kernel(DevGraph g, MsArgs a, 
   const uint32_t v = blk * kBlock + threadIdx.x;
   if (push) {
     if (v >= V) return;
-    const uint64_t fu = fcur[2u * v];
+    const uint64_t fu = fcur[b.fs * v];
     if (!fu) return;
     const uint32_t beg = g.row_ptr[v], end = g.row_ptr[v + 1];
     if (end - beg > kMsBigDeg) return;
@@ -464,8 +473,8 @@ __global__ void __launch_bounds__(256) msbfs_level_kernel(DevGraph g, MsArgs a, 
       for (int k = 0; k < KP; ++k)
         if (pacc[k]) b.P[(size_t)v * KP + k] |= pacc[k];
     }
-    fnext[2u * v] = tr ? acc : 0ull;
-    fnext[2u * v + 1u] = tr ? planes_roots<KP>(a, pacc) & acc : 0ull;
+    fnext[b.fs * v] = tr ? acc : 0ull;
+    if constexpr (KP > 0) fnext[2u * v + 1u] = tr ? planes_roots<KP>(a, pacc) & acc : 0ull;
     if (tr) mass = end - beg;
   }
   emit_rows<KP>(a, b, v, acc, pacc, d + 1);
@@ -499,8 +508,8 @@ __global__ void __launch_bounds__(256) msbfs_settle_kernel(DevGraph g, MsArgs a,
       load_planes<KP>(b.P, v, pacc);
       if (tr) mass = g.row_ptr[v + 1] - g.row_ptr[v];
     }
-    fnext[2u * v] = tr ? acc : 0ull;
-    fnext[2u * v + 1u] = tr ? planes_roots<KP>(a, pacc) & acc : 0ull;
+    fnext[b.fs * v] = tr ? acc : 0ull;
+    if constexpr (KP > 0) fnext[2u * v + 1u] = tr ? planes_roots<KP>(a, pacc) & acc : 0ull;
   }
   emit_rows<KP>(a, b, v, acc, pacc, d + 1);
   mass = wave_add32(mass);
@@ -820,27 +829,29 @@ __global__ void __launch_bounds__(256) msbfs_rows_multi_kernel(DevGraph g, MsArg
 // whose length is 1 + dist(n, v)). No bit-planes, one traversal per 64 roots
 // whatever their width, and the next-hop words are written once, whole.
 __global__ void __launch_bounds__(256) msbfs_levrows_kernel(DevGraph g, MsArgs a) {
-  __shared__ uint8_t s_lev[64 * 64];  // [node][root]
-  __shared__ uint64_t s_kd[64];
+  // 128 nodes per block: a root's 128 level bytes are one whole 128-B line
+  // (64-node blocks left half lines, written back twice)
+  __shared__ uint8_t s_lev[128 * 64];  // [node][root]
+  __shared__ uint64_t s_kd[128];
   const uint32_t vbl = blockIdx.x % a.nb;
   const VB b(a, vbl, g.V, -1);
   const uint32_t V = g.V, tid = threadIdx.x;
-  const uint32_t v0 = (blockIdx.x / a.nb) * 64u, nv = min(64u, V - v0);
+  const uint32_t v0 = (blockIdx.x / a.nb) * 128u, nv = min(128u, V - v0);
   if (v0 == 0 && tid == 0 && a.found[vbl * a.lmax + a.dbound + 1]) atomicOr(a.err, 8u);
   const uint32_t nr = min(a.R, a.n - b.rix0);
   {
     const uint4* src = reinterpret_cast<const uint4*>(a.lev + ((size_t)vbl * V + v0) * 64u);
-    if (tid < nv * 4u) reinterpret_cast<uint4*>(s_lev)[tid] = src[tid];
+    for (uint32_t x = tid; x < nv * 4u; x += kBlock) reinterpret_cast<uint4*>(s_lev)[x] = src[x];
   }
-  if (a.digest && tid < 64u) s_kd[tid] = (v0 + tid < V) ? g.dkey[2ull * (v0 + tid)] : 0ull;
+  if (a.digest && tid < 128u) s_kd[tid] = (v0 + tid < V) ? g.dkey[2ull * (v0 + tid)] : 0ull;
   __syncthreads();
   // the distance part of each run's digest (its next-hop part is added by
-  // nh_derive): root dr = tid / 4 over nodes 16 * (tid % 4) .. + 15
+  // nh_derive): root dr = tid / 4 over nodes 32 * (tid % 4) .. + 31
   if (a.digest) {
-    const uint32_t dr = tid >> 2, dn0 = 16u * (tid & 3u);
+    const uint32_t dr = tid >> 2, dn0 = 32u * (tid & 3u);
     uint64_t reached = 0, sumd = 0, h = 0;
     if (dr < nr) {
-      for (uint32_t n = dn0; n < dn0 + 16u && n < nv; ++n) {
+      for (uint32_t n = dn0; n < dn0 + 32u && n < nv; ++n) {
         const uint32_t l = s_lev[n * 64u + dr];
         if (!l) continue;
         reached += 1;
@@ -861,28 +872,37 @@ __global__ void __launch_bounds__(256) msbfs_levrows_kernel(DevGraph g, MsArgs a
       atomicAdd((unsigned long long*)&dg->hash, (unsigned long long)h);
     }
   }
-  const bool vec = (V & 3u) == 0 && nv == 64u;
-  for (uint32_t i = tid; i < 64u * 16u; i += kBlock) {  // (root, node quad)
-    const uint32_t r = i >> 4, q = i & 15u;
+  const bool vec = (V & 3u) == 0 && nv == 128u;
+  for (uint32_t i = tid; i < 64u * 16u; i += kBlock) {  // (root, node octet)
+    const uint32_t r = i >> 4, o = i & 15u;
     if (r >= nr) break;
-    if (v0 + 4u * q >= a.lev_pitch) continue;
-    uint32_t l[4];
+    if (v0 + 8u * o >= a.lev_pitch) continue;
+    uint32_t l[8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) l[j] = (4u * q + j < nv) ? s_lev[(4u * q + j) * 64u + r] : 0u;
-    const size_t off = (size_t)(b.rix0 + r) * V + v0 + 4u * q;
-    const size_t loff = (size_t)(b.rix0 + r) * a.lev_pitch + v0 + 4u * q;
+    for (int j = 0; j < 8; ++j) l[j] = (8u * o + j < nv) ? s_lev[(8u * o + j) * 64u + r] : 0u;
+    const size_t off = (size_t)(b.rix0 + r) * V + v0 + 8u * o;
+    const size_t loff = (size_t)(b.rix0 + r) * a.lev_pitch + v0 + 8u * o;
     if (a.dist) {
       uint32_t* row = a.dist + off;
+      uint32_t dv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dv[j] = l[j] ? l[j] - 1u : kInf;
       if (vec) {
-        *reinterpret_cast<uint4*>(row) = make_uint4(l[0] ? l[0] - 1u : kInf, l[1] ? l[1] - 1u : kInf,
-                                                    l[2] ? l[2] - 1u : kInf, l[3] ? l[3] - 1u : kInf);
+        reinterpret_cast<uint4*>(row)[0] = make_uint4(dv[0], dv[1], dv[2], dv[3]);
+        reinterpret_cast<uint4*>(row)[1] = make_uint4(dv[4], dv[5], dv[6], dv[7]);
       } else {
-        for (uint32_t j = 0; j < 4u; ++j)
-          if (4u * q + j < nv) row[j] = l[j] ? l[j] - 1u : kInf;
+        for (uint32_t j = 0; j < 8u; ++j)
+          if (8u * o + j < nv) row[j] = dv[j];
       }
     }
     // rows are lev_pitch bytes (a multiple of 16): whole words, padding zeroed
-    *reinterpret_cast<uint32_t*>(a.levrow + loff) = l[0] | (l[1] << 8) | (l[2] << 16) | (l[3] << 24);
+    const uint32_t lo = l[0] | (l[1] << 8) | (l[2] << 16) | (l[3] << 24);
+    const uint32_t hi = l[4] | (l[5] << 8) | (l[6] << 16) | (l[7] << 24);
+    if (v0 + 8u * o + 8u <= a.lev_pitch) {
+      *reinterpret_cast<uint2*>(a.levrow + loff) = make_uint2(lo, hi);
+    } else {
+      *reinterpret_cast<uint32_t*>(a.levrow + loff) = lo;  // pitch ends mid-octet
+    }
   }
 }
 
@@ -1606,8 +1626,8 @@ hipError_t launch_msbfs_levels(const DevGraph& g, const MsArgs& a, uint32_t dept
                        s, g, a, d);
     hipLaunchKernelGGL(msbfs_settle_kernel<-1>, dim3(a.nb * chunks), dim3(kBlock), 0, s, g, a, d);
   }
-  hipLaunchKernelGGL(msbfs_levrows_kernel, dim3(a.nb * ((g.V + 63u) / 64u)), dim3(kBlock), 0, s, g,
-                     a);
+  hipLaunchKernelGGL(msbfs_levrows_kernel, dim3(a.nb * ((g.V + 127u) / 128u)), dim3(kBlock), 0, s,
+                     g, a);
   return hipGetLastError();
 }
 
