@@ -175,8 +175,9 @@ int ospf_sync(ospf_ctx* ctx, void* stream);
 /* All-sources next hops in two phases ("derive", unit metric or hop count).
  * ospf_levels_dev: distances of the n device roots by the distance-only
  * multi-source BFS, written as d_dist [n][V] u32 rows (optional), byte level
- * rows d_lev [n][lev_pitch] (dist + 1, 0 = unreached; lev_pitch a multiple
- * of 16 >= V, padding zeroed) and, optional, the distance
+ * rows d_lev [n][lev_pitch] (dist + 1; 0x7F = unreached and padding;
+ * lev_pitch a multiple of 16 >= V; needs a depth bound <= 123, else
+ * OSPF_E_RANGE) and, optional, the distance
  * part {reached, sum dist, sum dist_key * (dist + 1)} of each run's digest.
  * ospf_nh_derive_dev: next-hop words [n][V][nh_words] (+ complete digests) of
  * the n device roots from level rows: d_lev_pos[v] = row of node v in d_lev

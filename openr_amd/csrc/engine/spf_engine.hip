@@ -1182,7 +1182,8 @@ int ospf_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t f
     return fail(c, OSPF_E_INVAL, "lev_pitch: a multiple of 16 >= V");
   if (!(flags & OSPF_HOP_COUNT) && !c->info.unit_metric)
     return fail(c, OSPF_E_RANGE, "level rows need unit metric or hop count");
-  if (c->depth_bound > 253) return fail(c, OSPF_E_RANGE, "depth bound above 253 (byte levels)");
+  if (c->depth_bound > 123)  // level bytes <= 125, below nh_derive's 0x7F marker
+    return fail(c, OSPF_E_RANGE, "level rows need a depth bound <= 123");
   hipStream_t s = (hipStream_t)stream;
   const uint32_t V = c->info.n_nodes, lmax = c->depth_bound + 2;
   const size_t per_vb = align_up((size_t)V * 8ull * 6 + V * 64ull + lmax * 8ull, 256);

@@ -880,6 +880,11 @@ __global__ void __launch_bounds__(256) msbfs_levrows_kernel(DevGraph g, MsArgs a
     uint32_t l[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) l[j] = (8u * o + j < nv) ? s_lev[(8u * o + j) * 64u + r] : 0u;
+    // level row bytes: dist + 1, 0x7F for unreached and padding (levels stay
+    // <= 125: nh_derive's compare needs them below 0x7F)
+    uint32_t lb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lb[j] = l[j] ? l[j] : 0x7Fu;
     const size_t off = (size_t)(b.rix0 + r) * V + v0 + 8u * o;
     const size_t loff = (size_t)(b.rix0 + r) * a.lev_pitch + v0 + 8u * o;
     if (a.dist) {
@@ -896,8 +901,8 @@ __global__ void __launch_bounds__(256) msbfs_levrows_kernel(DevGraph g, MsArgs a
       }
     }
     // rows are lev_pitch bytes (a multiple of 16): whole words, padding zeroed
-    const uint32_t lo = l[0] | (l[1] << 8) | (l[2] << 16) | (l[3] << 24);
-    const uint32_t hi = l[4] | (l[5] << 8) | (l[6] << 16) | (l[7] << 24);
+    const uint32_t lo = lb[0] | (lb[1] << 8) | (lb[2] << 16) | (lb[3] << 24);
+    const uint32_t hi = lb[4] | (lb[5] << 8) | (lb[6] << 16) | (lb[7] << 24);
     if (v0 + 8u * o + 8u <= a.lev_pitch) {
       *reinterpret_cast<uint2*>(a.levrow + loff) = make_uint2(lo, hi);
     } else {
@@ -1008,12 +1013,13 @@ __global__ void __launch_bounds__(256) nh_derive_kernel(DevGraph g, DeriveArgs d
     for (uint32_t j = 0; j < ng; ++j) {
       const uint32_t K = s_K[j];
       const uint32_t L4 = s_L[j * (T / 4u) + q];
-      // per byte: L - 1 where L >= 2, else 0xFF (matches no level byte)
+      // per byte: L - 1 where 2 <= L < 0x7F (reached, not the root), else
+      // 0xFF (matches no level byte)
       uint32_t lm1 = 0;
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         const uint32_t l = (L4 >> (8 * b)) & 0xFFu;
-        lm1 |= (l >= 2u ? l - 1u : 0xFFu) << (8 * b);
+        lm1 |= (l >= 2u && l < 0x7Fu ? l - 1u : 0xFFu) << (8 * b);
       }
       const uint32_t* tab = s_pos + j * cap;
       for (uint32_t w = sub; w < W; w += S) {
@@ -1140,16 +1146,16 @@ __device__ __forceinline__ void derive_uniform_tiles(
       uint4 L = make_uint4(0, 0, 0, 0);
       if (live) L = *reinterpret_cast<const uint4*>(d.lev + (size_t)s_own[j] * d.pitch + vl);
       const uint32_t Lw[4] = {L.x, L.y, L.z, L.w};
-      uint32_t lm1[4];
+      uint32_t lm1[4];  // as in nh_derive16_kernel: ((L - 1) | 0x80) per byte
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         uint32_t m = 0;
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
           const uint32_t l = (Lw[q] >> (8 * b)) & 0xFFu;
-          m |= (l >= 2u ? l - 1u : 0xFFu) << (8 * b);
+          m |= (l >= 2u && l < 0x7Fu ? l - 1u : 0u) << (8 * b);
         }
-        lm1[q] = m;
+        lm1[q] = m | 0x80808080u;
       }
       uint32_t A0[4] = {0u, 0u, 0u, 0u}, A1[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
@@ -1158,10 +1164,7 @@ __device__ __forceinline__ void derive_uniform_tiles(
         const uint32_t xw[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w};
         uint32_t zz[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint32_t df = xw[q] ^ lm1[q];
-          zz[q] = (~(((df & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | df | 0x7F7F7F7Fu) & keep) >> 7;
-        }
+        for (int q = 0; q < 4; ++q) zz[q] = ((lm1[q] - xw[q]) & 0x80808080u & keep) >> 7;
         const uint32_t off = (pp[k] & 0x7FFFFFFFu) - vl;
         if (pp[k] >= 0x80000000u && pp[k] != kInf && off < 16u) {
 #pragma unroll
@@ -1299,6 +1302,10 @@ __global__ void __launch_bounds__(256) nh_derive16_kernel(DevGraph g, DeriveArgs
     const bool live = vl < d.pitch;             // inside the (16-aligned) rows
     uint4 L = make_uint4(0, 0, 0, 0);
     if (live) L = *reinterpret_cast<const uint4*>(d.lev + (size_t)own * d.pitch + vl);
+    // per byte (L - 1) | 0x80 where 2 <= L < 0x7F, else 0x80. For a transit
+    // neighbour with an up link, x >= L - 1 whenever x is reached (< 0x7F), so
+    // x == L - 1 <=> L - 1 >= x: bit 7 of ((L - 1) | 0x80) - x, no borrow
+    // between bytes (x in 1 .. 0x7F)
     uint32_t lm1[4];
     {
       const uint32_t Lw[4] = {L.x, L.y, L.z, L.w};
@@ -1308,9 +1315,9 @@ __global__ void __launch_bounds__(256) nh_derive16_kernel(DevGraph g, DeriveArgs
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
           const uint32_t l = (Lw[q] >> (8 * b)) & 0xFFu;
-          m |= (l >= 2u ? l - 1u : 0xFFu) << (8 * b);
+          m |= (l >= 2u && l < 0x7Fu ? l - 1u : 0u) << (8 * b);
         }
-        lm1[q] = m;
+        lm1[q] = m | 0x80808080u;
       }
     }
     uint32_t word[W][16];
@@ -1344,8 +1351,7 @@ __global__ void __launch_bounds__(256) nh_derive16_kernel(DevGraph g, DeriveArgs
           const uint32_t xw[4] = {xv[kk].x, xv[kk].y, xv[kk].z, xv[kk].w};
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const uint32_t df = xw[q] ^ lm1[q];
-            const uint32_t z = ~(((df & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | df | 0x7F7F7F7Fu) & keep;
+            const uint32_t z = (lm1[q] - xw[q]) & 0x80808080u & keep;
             A[q] |= (z >> 7) << kk;
           }
           // a non-transit neighbour: a next hop towards itself only
