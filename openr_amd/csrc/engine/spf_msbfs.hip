@@ -829,13 +829,16 @@ __global__ void __launch_bounds__(256) msbfs_rows_multi_kernel(DevGraph g, MsArg
 // whose length is 1 + dist(n, v)). No bit-planes, one traversal per 64 roots
 // whatever their width, and the next-hop words are written once, whole.
 __global__ void __launch_bounds__(256) msbfs_levrows_kernel(DevGraph g, MsArgs a) {
-  // 128 nodes per block: a root's 128 level bytes are one whole 128-B line
-  // (64-node blocks left half lines, written back twice)
+  // Block = (virtual batch, 128 nodes). Lane = root (conflict-free LDS reads of
+  // the [node][root] level records: four lanes share a word), wave w = nodes
+  // 32w .. 32w + 31: each lane writes its root's 32 consecutive dist values
+  // (128 B, one whole line) and level bytes (32 B).
   __shared__ uint8_t s_lev[128 * 64];  // [node][root]
   __shared__ uint64_t s_kd[128];
+  __shared__ uint64_t s_red[kWavesPerBlock][64][3];
   const uint32_t vbl = blockIdx.x % a.nb;
   const VB b(a, vbl, g.V, -1);
-  const uint32_t V = g.V, tid = threadIdx.x;
+  const uint32_t V = g.V, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint32_t v0 = (blockIdx.x / a.nb) * 128u, nv = min(128u, V - v0);
   if (v0 == 0 && tid == 0 && a.found[vbl * a.lmax + a.dbound + 1]) atomicOr(a.err, 8u);
   const uint32_t nr = min(a.R, a.n - b.rix0);
@@ -845,68 +848,77 @@ __global__ void __launch_bounds__(256) msbfs_levrows_kernel(DevGraph g, MsArgs a
   }
   if (a.digest && tid < 128u) s_kd[tid] = (v0 + tid < V) ? g.dkey[2ull * (v0 + tid)] : 0ull;
   __syncthreads();
-  // the distance part of each run's digest (its next-hop part is added by
-  // nh_derive): root dr = tid / 4 over nodes 32 * (tid % 4) .. + 31
+  const uint32_t r = lane, m0 = 32u * wave;  // this lane's root, the wave's nodes
+  uint32_t l[32];
+#pragma unroll
+  for (int j = 0; j < 32; ++j) l[j] = (m0 + j < nv) ? s_lev[(m0 + j) * 64u + r] : 0u;
   if (a.digest) {
-    const uint32_t dr = tid >> 2, dn0 = 32u * (tid & 3u);
     uint64_t reached = 0, sumd = 0, h = 0;
-    if (dr < nr) {
-      for (uint32_t n = dn0; n < dn0 + 32u && n < nv; ++n) {
-        const uint32_t l = s_lev[n * 64u + dr];
-        if (!l) continue;
-        reached += 1;
-        sumd += l - 1u;
-        h += s_kd[n] * (uint64_t)l;
-      }
-    }
 #pragma unroll
-    for (int o = 1; o < 4; o <<= 1) {
-      reached += shfl_xor64(reached, o);
-      sumd += shfl_xor64(sumd, o);
-      h += shfl_xor64(h, o);
+    for (int j = 0; j < 32; ++j) {
+      if (!l[j]) continue;
+      reached += 1;
+      sumd += l[j] - 1u;
+      h += s_kd[m0 + j] * (uint64_t)l[j];
     }
-    if ((tid & 3u) == 0 && dr < nr && reached) {
-      ospf_digest* dg = a.digest + b.rix0 + dr;
-      atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)reached);
-      atomicAdd((unsigned long long*)&dg->sum_dist, (unsigned long long)sumd);
-      atomicAdd((unsigned long long*)&dg->hash, (unsigned long long)h);
-    }
+    s_red[wave][r][0] = reached;
+    s_red[wave][r][1] = sumd;
+    s_red[wave][r][2] = h;
   }
-  const bool vec = (V & 3u) == 0 && nv == 128u;
-  for (uint32_t i = tid; i < 64u * 16u; i += kBlock) {  // (root, node octet)
-    const uint32_t r = i >> 4, o = i & 15u;
-    if (r >= nr) break;
-    if (v0 + 8u * o >= a.lev_pitch) continue;
-    uint32_t l[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) l[j] = (8u * o + j < nv) ? s_lev[(8u * o + j) * 64u + r] : 0u;
-    // level row bytes: dist + 1, 0x7F for unreached and padding (levels stay
-    // <= 125: nh_derive's compare needs them below 0x7F)
-    uint32_t lb[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) lb[j] = l[j] ? l[j] : 0x7Fu;
-    const size_t off = (size_t)(b.rix0 + r) * V + v0 + 8u * o;
-    const size_t loff = (size_t)(b.rix0 + r) * a.lev_pitch + v0 + 8u * o;
+  if (r < nr && v0 + m0 < V) {
+    const size_t off = (size_t)(b.rix0 + r) * V + v0 + m0;
     if (a.dist) {
       uint32_t* row = a.dist + off;
-      uint32_t dv[8];
+      if ((V & 3u) == 0 && m0 + 32u <= nv) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dv[j] = l[j] ? l[j] - 1u : kInf;
-      if (vec) {
-        reinterpret_cast<uint4*>(row)[0] = make_uint4(dv[0], dv[1], dv[2], dv[3]);
-        reinterpret_cast<uint4*>(row)[1] = make_uint4(dv[4], dv[5], dv[6], dv[7]);
+        for (int x = 0; x < 8; ++x) {
+          uint32_t dv[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) dv[c] = l[4 * x + c] ? l[4 * x + c] - 1u : kInf;
+          reinterpret_cast<uint4*>(row)[x] = make_uint4(dv[0], dv[1], dv[2], dv[3]);
+        }
       } else {
-        for (uint32_t j = 0; j < 8u; ++j)
-          if (8u * o + j < nv) row[j] = dv[j];
+        for (uint32_t j = 0; j < 32u && m0 + j < nv; ++j) row[j] = l[j] ? l[j] - 1u : kInf;
       }
     }
-    // rows are lev_pitch bytes (a multiple of 16): whole words, padding zeroed
-    const uint32_t lo = lb[0] | (lb[1] << 8) | (lb[2] << 16) | (lb[3] << 24);
-    const uint32_t hi = lb[4] | (lb[5] << 8) | (lb[6] << 16) | (lb[7] << 24);
-    if (v0 + 8u * o + 8u <= a.lev_pitch) {
-      *reinterpret_cast<uint2*>(a.levrow + loff) = make_uint2(lo, hi);
-    } else {
-      *reinterpret_cast<uint32_t*>(a.levrow + loff) = lo;  // pitch ends mid-octet
+    // level row bytes: dist + 1, 0x7F for unreached and padding (levels stay
+    // <= 125: nh_derive's compare needs them below 0x7F); rows are lev_pitch
+    // bytes (a multiple of 16), so the wave's 32 bytes (up to the pitch) are
+    // whole words
+    uint8_t* lrow = a.levrow + (size_t)(b.rix0 + r) * a.lev_pitch + v0 + m0;
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      if (v0 + m0 + 16u * x >= a.lev_pitch) break;
+      uint32_t w4[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t lb = l[16 * x + 4 * c + k];
+          w |= (lb ? lb : 0x7Fu) << (8 * k);
+        }
+        w4[c] = w;
+      }
+      reinterpret_cast<uint4*>(lrow)[x] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
+  }
+  if (a.digest) {
+    __syncthreads();
+    if (tid < 64u && tid < nr) {
+      uint64_t rr = 0, sd = 0, hh = 0;
+#pragma unroll
+      for (int w = 0; w < (int)kWavesPerBlock; ++w) {
+        rr += s_red[w][tid][0];
+        sd += s_red[w][tid][1];
+        hh += s_red[w][tid][2];
+      }
+      if (rr) {
+        ospf_digest* dg = a.digest + b.rix0 + tid;
+        atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)rr);
+        atomicAdd((unsigned long long*)&dg->sum_dist, (unsigned long long)sd);
+        atomicAdd((unsigned long long*)&dg->hash, (unsigned long long)hh);
+      }
     }
   }
 }
