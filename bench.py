@@ -161,6 +161,9 @@ def main():
                     help="derive: all-sources next hops from neighbour level rows (unit "
                          "metric, every root's neighbours in the sweep); batch: per-class "
                          "engine batches (bit-plane next hops); auto = derive when it applies")
+    ap.add_argument("--wide", choices=["derive", "batch"], default="derive",
+                    help="derive mode: rows of > 4 next-hop words (spines) from level rows "
+                         "(nh_derive_wide_kernel) or on the bit-plane batch path")
     ap.add_argument("--dist-parity", type=int, default=0,
                     help="N>1: rank 0 checks the gathered digests of the last timed step "
                          "for this many roots against the CPU restatement")
@@ -445,10 +448,11 @@ def derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
         roots = cls_all[rank][cap]
         W = max(1, cap // 32) if cap > 16 else 1
         slot = max(1, max(c[cap].size for c in cls_all))
-        # rows of up to 4 words derive from the level rows (lane-16 kernel);
-        # wider ones (spines) run the bit-plane batch path on their own
+        # every class derives from the level rows (lane-16 kernel up to 4
+        # words, the word-per-lane kernel above); --wide batch runs the wider
+        # ones (spines) on the bit-plane batch path instead, on their own
         # stream, concurrently with phase 1 (they need no level rows)
-        kind = "derive" if W <= 4 else "batch"
+        kind = "derive" if W <= 4 or args.wide == "derive" else "batch"
         c = dict(cap=cap, W=W, roots=roots, n=int(roots.size), kind=kind,
                  d=torch.from_numpy(roots.view(np.int32)).to(dev),
                  nh=torch.empty((max(1, roots.size), V, W), dtype=torch.int32, device=dev),
@@ -593,8 +597,9 @@ def derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
                                                  f"variant{p['variant']}_cap{c['cap']}", c["n"])})
         elif c["n"]:
             units.append({"launch": f"derive_cap{c['cap']}",
-                          "kernel": f"ospf_nh_derive_dev (nh_derive16_kernel, {c['W']} next-hop "
-                                    f"word(s))", "cap": c["cap"], "nh_words": c["W"],
+                          "kernel": f"ospf_nh_derive_dev ("
+                                    f"{'nh_derive16_kernel' if c['W'] <= 4 else 'nh_derive_wide_kernel'}"
+                                    f", {c['W']} next-hop word(s))", "cap": c["cap"], "nh_words": c["W"],
                           "roots_per_launch": c["n"], "isolated_launch_ms": round(c["iso_ms"], 3),
                           "compulsory_bytes": c["n"] * 4 * V * c["W"],
                           "traffic": pmc_traffic(args.profile_dir, f"derive_cap{c['cap']}", c["n"])})

@@ -1446,6 +1446,200 @@ __global__ void __launch_bounds__(256) nh_derive16_kernel(DevGraph g, DeriveArgs
   }
 }
 
+// Wide rows (W > 4 words: spines, whose neighbours are one switch per pod).
+// Lane = next-hop word w (its 32 neighbour slots), a wave walks 8-node chunks
+// of the block's tile. Block = up to kWideG consecutive roots x a chunk of
+// tiles; inside it, runs of roots with the same distinct-neighbour list (the
+// spines of one plane) share the neighbour loads: each lane reads its 32
+// slots' level bytes of 8 nodes once per chunk, and the word of 8 nodes is
+// recomputed only when a root's own levels differ from the previous root's
+// (all spines of a plane are equally far from nearly every node). Per root
+// only the link-up mask, the stores (W consecutive words = one node's record
+// per store instruction) and the digest terms remain.
+constexpr uint32_t kWideG = 64;
+constexpr uint32_t kWideTile = 256;
+__global__ void __launch_bounds__(256) nh_derive_wide_kernel(DevGraph g, DeriveArgs d) {
+  __shared__ uint32_t s_pos[kDeriveTab];           // slot table of the current run
+  __shared__ uint32_t s_keep[kWideG * 64];         // [root][word]: slots with an up link
+  __shared__ uint32_t s_L[kWideG * kWideTile / 4];  // own level bytes of the tile, [root][node]
+  __shared__ uint32_t s_root[kWideG], s_own[kWideG], s_K[kWideG], s_same[kWideG];
+  __shared__ unsigned long long s_h[kWideG];
+  const uint32_t V = g.V, W = d.W, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t G = d.G, cap = d.cap;
+  const uint32_t ngroups = (d.n + G - 1) / G;
+  const uint32_t ci = blockIdx.x / ngroups, rr = blockIdx.x % ngroups;
+  const uint32_t full = ngroups / 8u * 8u;
+  const uint32_t gi = rr < full ? (rr % 8u) * (full / 8u) + rr / 8u : rr;
+  const uint32_t i0 = gi * G, ng = min(G, d.n - i0);
+  if (tid < ng) {
+    const uint32_t r = d.roots[i0 + tid];
+    s_root[tid] = r;
+    s_h[tid] = 0ull;
+    s_own[tid] = kInf;
+    s_K[tid] = 0;
+    if (r >= V) {
+      atomicOr(d.err, 64u);
+    } else {
+      const uint32_t K = g.dn_off[r + 1] - g.dn_off[r];
+      s_own[tid] = d.pos[r];
+      if (K > cap || K > 32u * W || s_own[tid] == kInf)
+        atomicOr(d.err, s_own[tid] == kInf ? 16u : 1u);
+      if (s_own[tid] != kInf) s_K[tid] = min(K, cap);
+    }
+  }
+  for (uint32_t x = tid; x < ng * 64u; x += kBlock) s_keep[x] = 0u;
+  __syncthreads();
+  // usable slots per root; s_same[j]: root j has root j-1's neighbour list
+  if (tid < ng)
+    s_same[tid] = tid > 0 && s_own[tid] != kInf && s_own[tid - 1] != kInf &&
+                  s_K[tid] == s_K[tid - 1];
+  for (uint32_t j = 0; j < ng; ++j) {
+    const uint32_t r = s_root[j];
+    if (r >= V || s_own[j] == kInf) continue;
+    for (uint32_t e = g.row_ptr[r] + tid; e < g.row_ptr[r + 1]; e += kBlock) {
+      const uint32_t cx = g.colx[e];
+      if ((cx & kDown) || cx == r) continue;
+      const uint32_t k = g.didx[e];
+      if (k < s_K[j]) atomicOr(&s_keep[j * 64u + (k >> 5)], 1u << (k & 31u));
+    }
+  }
+  __syncthreads();
+  for (uint32_t j = 1; j < ng; ++j) {
+    if (!s_same[j]) continue;
+    const uint32_t* a0 = g.dn + g.dn_off[s_root[j - 1]];
+    const uint32_t* a1 = g.dn + g.dn_off[s_root[j]];
+    for (uint32_t k = tid; k < s_K[j]; k += kBlock)
+      if (a0[k] != a1[k]) s_same[j] = 0u;  // benign race: every writer stores 0
+  }
+  __syncthreads();
+  const uint32_t t0 = ci * d.ctiles, t1 = min(d.tiles, t0 + d.ctiles);
+  for (uint32_t j0 = 0; j0 < ng;) {
+    uint32_t j1 = j0 + 1;
+    while (j1 < ng && s_same[j1]) ++j1;
+    const uint32_t K = s_K[j0];
+    if (s_own[j0] == kInf) {  // a bad root (error flagged): its own run
+      j0 = j1;
+      continue;
+    }
+    // slot table: the neighbour's level row; 0x80000000 | id for a non-transit
+    // neighbour (a next hop towards itself only); kInf when no root of the run
+    // has an up link to it
+    for (uint32_t k = tid; k < K; k += kBlock) {
+      bool used = false;
+      for (uint32_t j = j0; j < j1 && !used; ++j) used = (s_keep[j * 64u + (k >> 5)] >> (k & 31u)) & 1u;
+      uint32_t p = kInf;
+      if (used) {
+        const uint32_t n = g.dn[g.dn_off[s_root[j0]] + k];
+        if (transit(g, n)) {
+          p = d.pos[n];
+          if (p == kInf) atomicOr(d.err, 16u);
+        } else {
+          p = 0x80000000u | n;
+        }
+      }
+      s_pos[k] = p;
+    }
+    const uint32_t own0 = s_own[j0];
+    for (uint32_t t = t0; t < t1; ++t) {
+      const uint32_t v0 = t * kWideTile;
+      __syncthreads();  // s_pos written / the previous tile's s_L consumed
+      for (uint32_t x = tid; x < (j1 - j0) * (kWideTile / 16u); x += kBlock) {
+        const uint32_t j = x / (kWideTile / 16u), c = x - j * (kWideTile / 16u);
+        uint4 l4 = make_uint4(0x7F7F7F7Fu, 0x7F7F7F7Fu, 0x7F7F7F7Fu, 0x7F7F7F7Fu);
+        if (v0 + 16u * c < d.pitch)
+          l4 = *reinterpret_cast<const uint4*>(d.lev + (size_t)s_own[j0 + j] * d.pitch + v0 + 16u * c);
+        reinterpret_cast<uint4*>(s_L + j * (kWideTile / 4u))[c] = l4;
+      }
+      __syncthreads();
+      for (uint32_t c = wave; c < kWideTile / 8u; c += kWavesPerBlock) {
+        const uint32_t vc = v0 + 8u * c;
+        if (vc >= V) break;  // wave-uniform
+        // this lane's 32 slots at the chunk's 8 nodes (vc + 8 <= pitch)
+        uint2 xv[32];
+        uint32_t selfw[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+          const uint32_t k = 32u * lane + i;
+          const uint32_t p = (lane < W && k < K) ? s_pos[k] : kInf;
+          const uint32_t row = p < 0x80000000u ? p : own0;
+          xv[i] = *reinterpret_cast<const uint2*>(d.lev + (size_t)row * d.pitch + vc);
+          if (p >= 0x80000000u) {
+            xv[i] = make_uint2(0x7F7F7F7Fu, 0x7F7F7F7Fu);  // never matches
+            const uint32_t off = (p & 0x7FFFFFFFu) - vc;
+            if (p != kInf && off < 8u) {
+#pragma unroll
+              for (int b = 0; b < 8; ++b)
+                if (off == (uint32_t)b) selfw[b] |= 1u << i;
+            }
+          }
+        }
+        uint64_t kn[8];
+        if (d.digest) {
+#pragma unroll
+          for (int b = 0; b < 8; ++b) kn[b] = g.dkn[vc + b];  // zero past V
+        }
+        uint32_t word[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+        uint32_t plo = 0xFFFFFFFFu, phi = 0xFFFFFFFFu;  // lm1 of the last computed word set
+        for (uint32_t j = j0; j < j1; ++j) {
+          const uint2 L8 = reinterpret_cast<const uint2*>(s_L + (j - j0) * (kWideTile / 4u))[c];
+          uint32_t lo = 0, hi = 0;  // ((L - 1) | 0x80) per byte, L - 1 := 0 outside 2 <= L < 0x7F
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const uint32_t l0 = (L8.x >> (8 * b)) & 0xFFu, l1 = (L8.y >> (8 * b)) & 0xFFu;
+            lo |= (l0 >= 2u && l0 < 0x7Fu ? l0 - 1u : 0u) << (8 * b);
+            hi |= (l1 >= 2u && l1 < 0x7Fu ? l1 - 1u : 0u) << (8 * b);
+          }
+          lo |= 0x80808080u;
+          hi |= 0x80808080u;
+          if (lo != plo || hi != phi) {  // wave-uniform (the root's own levels)
+            plo = lo;
+            phi = hi;
+#pragma unroll
+            for (int k8 = 0; k8 < 32; k8 += 8) {
+              uint32_t A0 = 0, A1 = 0;
+#pragma unroll
+              for (int kk = 0; kk < 8; ++kk) {
+                A0 |= (((lo - xv[k8 + kk].x) & 0x80808080u) >> 7) << kk;
+                A1 |= (((hi - xv[k8 + kk].y) & 0x80808080u) >> 7) << kk;
+              }
+#pragma unroll
+              for (int b = 0; b < 4; ++b) {
+                const uint32_t m = k8 ? 0xFFFFFFFFu : 0u;  // first block overwrites
+                word[b] = (word[b] & m) | (((A0 >> (8 * b)) & 0xFFu) << k8);
+                word[4 + b] = (word[4 + b] & m) | (((A1 >> (8 * b)) & 0xFFu) << k8);
+              }
+            }
+          }
+          const uint32_t keep = lane < W ? s_keep[j * 64u + lane] : 0u;
+          uint32_t* dst = d.nh + ((size_t)(i0 + j) * V + vc) * W + lane;
+          uint64_t h = 0;
+#pragma unroll
+          for (int b = 0; b < 8; ++b) {
+            const uint32_t ow = (word[b] | selfw[b]) & keep;
+            if (lane < W && vc + b < V) dst[(size_t)b * W] = ow;
+            if (d.digest && ow) h += kn[b] * digest_word_key(lane, ow);
+          }
+          if (h) atomicAdd(&s_h[j], (unsigned long long)h);
+        }
+      }
+    }
+    j0 = j1;
+    __syncthreads();  // s_pos is rewritten by the next run
+  }
+  __syncthreads();
+  if (d.digest && tid < ng) {
+    ospf_digest* dg = d.digest + i0 + tid;
+    unsigned long long h = s_h[tid];
+    if (ci == 0 && s_own[tid] != kInf) {
+      const ospf_digest ld = d.lev_digest[s_own[tid]];
+      atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)ld.reached);
+      atomicAdd((unsigned long long*)&dg->sum_dist, (unsigned long long)ld.sum_dist);
+      h += ld.hash;
+    }
+    if (h) atomicAdd((unsigned long long*)&dg->hash, h);
+  }
+}
+
 // ---------------------------------------------------------------- digest
 // Digest of finished rows (runs whose rows are written per level): `segs`
 // workgroups per root, each over a node range, adding into a zeroed record.
@@ -1667,6 +1861,17 @@ hipError_t launch_nh_derive(const DevGraph& g, const DeriveArgs& d0, hipStream_t
       case 3: hipLaunchKernelGGL(nh_derive16_kernel<3>, grid, dim3(kBlock), lds, s, g, d); break;
       default: hipLaunchKernelGGL(nh_derive16_kernel<4>, grid, dim3(kBlock), lds, s, g, d); break;
     }
+    return hipGetLastError();
+  }
+  if (d.W > 4 && !getenv("OSPF_DERIVE_GENERIC")) {  // lane = word, runs of equal lists
+    d.G = kWideG;
+    if (const char* e = getenv("OSPF_DERIVE_WIDE_G"))
+      d.G = std::max<uint32_t>(1, std::min<uint32_t>(kWideG, (uint32_t)atoi(e)));
+    d.tiles = (g.V + kWideTile - 1) / kWideTile;
+    d.ctiles = std::max<uint32_t>(1, std::min<uint32_t>(d.tiles, d.ctiles ? d.ctiles : 2));
+    d.chunks = (d.tiles + d.ctiles - 1) / d.ctiles;
+    const dim3 grid(((d.n + d.G - 1) / d.G) * d.chunks);
+    hipLaunchKernelGGL(nh_derive_wide_kernel, grid, dim3(kBlock), 0, s, g, d);
     return hipGetLastError();
   }
   // one thread per node quad does all the words up to 8; wider rows split a

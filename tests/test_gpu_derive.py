@@ -155,6 +155,26 @@ def test_derive_wide_word_kernels(pods):
     check_against_engine(st, roots=roots)
 
 
+@pytest.mark.parametrize("generic", [False, True])
+def test_derive_wide_runs_of_spines(generic, monkeypatch):
+    """Every root of a fabric whose spines have 5 next-hop words: the spines of
+    a plane share one neighbour list (runs in nh_derive_wide_kernel) while a
+    drained fabric switch (a next hop towards itself only), an overloaded
+    spine adjacency and a small G split those runs and their masks."""
+    if generic:
+        monkeypatch.setenv("OSPF_DERIVE_GENERIC", "1")
+    else:
+        monkeypatch.setenv("OSPF_DERIVE_WIDE_G", "20")  # runs straddle blocks
+    st = T.fabric(pods=150, planes=2)
+    dbs = st.to_dbs()
+    for d in dbs:
+        if d.name in ("2-3-1", "2-140-0"):
+            d.overloaded = True
+        if d.name in ("1-0-5", "1-1-30"):
+            d.adjs[7].overloaded = True
+    check_against_engine(AdjDbStream.from_dbs(dbs))
+
+
 def test_derive_quad_kernel_for_narrow_rows(monkeypatch):
     monkeypatch.setenv("OSPF_DERIVE_QUAD", "1")
     stream, _ = random_stream(7, n=70, unit=True)
