@@ -1186,7 +1186,8 @@ int ospf_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t f
     return fail(c, OSPF_E_RANGE, "level rows need a depth bound <= 123");
   hipStream_t s = (hipStream_t)stream;
   const uint32_t V = c->info.n_nodes, lmax = c->depth_bound + 2;
-  const size_t per_vb = align_up((size_t)V * 8ull * 6 + V * 64ull + lmax * 8ull, 256);
+  // per batch: frontier slots 2 x 8 B, seen 8 B, accb 8 B, level records 64 B
+  const size_t per_vb = align_up((size_t)V * 8ull * 4 + V * 64ull + lmax * 8ull, 256);
   uint32_t nb_cap = 96;
   if (const char* e = getenv("OSPF_MS_NB")) nb_cap = std::max(1, atoi(e));
   nb_cap = (uint32_t)std::max<size_t>(1, std::min<size_t>(nb_cap, (6ull << 30) / per_vb));
@@ -1221,15 +1222,19 @@ int ospf_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t f
   for (uint32_t vb0 = 0; vb0 < total_vb; vb0 += nb_max) {
     a.vb0 = vb0;
     a.nb = std::min(nb_max, total_vb - vb0);
-    a.front = (uint64_t*)sp;
-    a.seen = a.front + 4ull * a.nb * V;
+    a.front = (uint64_t*)sp;  // distances only: 8-B records, slots d & 1
+    a.seen = a.front + 2ull * a.nb * V;
     a.accb = a.seen + (size_t)a.nb * V;
     a.planes = nullptr;
     a.lev = (uint8_t*)(a.accb + (size_t)a.nb * V);
     a.found = (uint32_t*)(a.lev + (size_t)a.nb * V * 64ull);
     a.mass = a.found + (size_t)a.nb * lmax;
-    HIPCHK(c, hipMemsetAsync(sp, 0, (size_t)a.nb * V * 8ull * 6 + (size_t)a.nb * V * 64ull +
-                                        (size_t)a.nb * lmax * 8ull, s));
+    // zero: frontier slot 1 (the init kernel ORs level 1 into it; slot 0 is
+    // written whole by every level before it is read), seen, accb, found /
+    // mass. The level records are not cleared: their bytes are set once per
+    // (node, root) and read masked by seen.
+    HIPCHK(c, hipMemsetAsync(a.front + (size_t)a.nb * V, 0, (size_t)a.nb * V * 8ull * 3, s));
+    HIPCHK(c, hipMemsetAsync(a.found, 0, (size_t)a.nb * lmax * 8ull, s));
     hipError_t e = ospf::launch_msbfs_levels(c->g, a, c->depth_bound, s);
     if (e != hipSuccess) return hip_fail(c, e, "launch_msbfs_levels");
   }

@@ -136,8 +136,9 @@ __device__ __forceinline__ uint32_t gather_word(const uint64_t* p, uint32_t r) {
   return w;
 }
 
-// lev bytes of node v for the roots in `acc` := val (they are 0 before: a
-// (node, root) pair is reached once). Byte r of the 64-B record is root r.
+// lev bytes of node v for the roots in `acc` := val (a (node, root) pair is
+// reached once; the other bytes are kept, stale or not: readers mask the
+// record with seen[v]). Byte r of the 64-B record is root r.
 __device__ __forceinline__ void set_lev(const MsArgs& a, const VB& b, uint32_t v, uint64_t acc,
                                         uint32_t val) {
   uint4* rec = reinterpret_cast<uint4*>(a.lev + ((size_t)b.vbl * b.V + v) * 64u);
@@ -145,13 +146,16 @@ __device__ __forceinline__ void set_lev(const MsArgs& a, const VB& b, uint32_t v
   for (int c = 0; c < 4; ++c) {
     const uint32_t bits = (uint32_t)(acc >> (16 * c)) & 0xFFFFu;
     if (!bits) continue;
-    // nibble -> one 0x01 byte per set bit (bit i -> byte i), times val
-    auto spread = [&](uint32_t nib) { return ((nib * 0x00204081u) & 0x01010101u) * val; };
+    // nibble -> one 0x01 byte per set bit (bit i -> byte i); byte := val
+    auto put = [&](uint32_t w, uint32_t nib) {
+      const uint32_t ones = (nib * 0x00204081u) & 0x01010101u;
+      return (w & ~(ones * 0xFFu)) | ones * val;
+    };
     uint4 w = rec[c];
-    w.x |= spread(bits & 0xFu);
-    w.y |= spread((bits >> 4) & 0xFu);
-    w.z |= spread((bits >> 8) & 0xFu);
-    w.w |= spread((bits >> 12) & 0xFu);
+    w.x = put(w.x, bits & 0xFu);
+    w.y = put(w.y, (bits >> 4) & 0xFu);
+    w.z = put(w.z, (bits >> 8) & 0xFu);
+    w.w = put(w.w, (bits >> 12) & 0xFu);
     rec[c] = w;
   }
 }
@@ -249,8 +253,10 @@ __global__ void __launch_bounds__(256) msbfs_init_kernel(DevGraph g, MsArgs a) {
   uint64_t* f1 = b.front(a, 1);
   const size_t row = (size_t)rix * V;
   uint32_t* lev32 = reinterpret_cast<uint32_t*>(a.lev);
-  auto lev_or = [&](uint32_t v, uint32_t val) {  // byte `bit` of node v's record
-    atomicOr(&lev32[(((size_t)vbl * V + v) * 64u + bit) / 4u], val << (8u * (bit & 3u)));
+  auto lev_or = [&](uint32_t v, uint32_t val) {  // byte `bit` of node v's record := val
+    uint32_t* w = &lev32[(((size_t)vbl * V + v) * 64u + bit) / 4u];
+    atomicAnd(w, ~(0xFFu << (8u * (bit & 3u))));  // stale bytes: records are not cleared
+    atomicOr(w, val << (8u * (bit & 3u)));
   };
   const bool rec = !a.merged || b.g == 0;  // merged rows: pass 0 records the levels
   if (lane == 0) {
@@ -828,97 +834,150 @@ __global__ void __launch_bounds__(256) msbfs_rows_multi_kernel(DevGraph g, MsArg
 // tail from n is a shortest n -> v path with transit intermediates, and
 // whose length is 1 + dist(n, v)). No bit-planes, one traversal per 64 roots
 // whatever their width, and the next-hop words are written once, whole.
+__device__ __forceinline__ uint32_t byte_perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+// 0x01 in byte i for bit i of a nibble
+__device__ __forceinline__ uint32_t nib_bytes(uint32_t nib) {
+  return (nib * 0x00204081u) & 0x01010101u;
+}
+// one step of a transposing wave reduction: N values per lane, lanes paired
+// across offset o; afterwards value i (< N/2) of a lane is the pair's sum of
+// value i + (lane & o ? N/2 : 0)
+template <int N, typename T>
+__device__ __forceinline__ void xreduce_step(T* v, uint32_t lane, int o) {
+  const bool up = lane & (uint32_t)o;
+#pragma unroll
+  for (int i = 0; i < N / 2; ++i) {
+    const T send = up ? v[i] : v[i + N / 2];
+    const T keep = up ? v[i + N / 2] : v[i];
+    T recv;
+    if constexpr (sizeof(T) == 8) recv = shfl_xor64(send, o);
+    else recv = (T)__shfl_xor((int)send, o);
+    v[i] = keep + recv;
+  }
+}
+
 __global__ void __launch_bounds__(256) msbfs_levrows_kernel(DevGraph g, MsArgs a) {
-  // Block = (virtual batch, 128 nodes). Lane = root (conflict-free LDS reads of
-  // the [node][root] level records: four lanes share a word), wave w = nodes
-  // 32w .. 32w + 31: each lane writes its root's 32 consecutive dist values
-  // (128 B, one whole line) and level bytes (32 B).
-  __shared__ uint8_t s_lev[128 * 64];  // [node][root]
-  __shared__ uint64_t s_kd[128];
-  __shared__ uint64_t s_red[kWavesPerBlock][64][3];
+  // Block = (virtual batch, 512 nodes in two 256-node halves). Load: thread
+  // (quad q = tid % 64, root group rg = tid / 64: roots 16 rg .. 16 rg + 15)
+  // reads the 16-root slices of its four nodes' [node][root] records (bytes
+  // of roots not in seen[v] are stale: masked), transposes the 4 x 4 byte
+  // blocks with byte permutes and parks [root][quad] words (four nodes of one
+  // root) in LDS (row pitch 65 words: conflict-free both ways). Store: wave w
+  // takes roots 16 w .. 16 w + 15, lane = quad, so each store instruction
+  // writes 1 KB of consecutive dist row and 256 B of level row.
+  __shared__ uint32_t s_T[64 * 65];
   const uint32_t vbl = blockIdx.x % a.nb;
   const VB b(a, vbl, g.V, -1);
-  const uint32_t V = g.V, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const uint32_t v0 = (blockIdx.x / a.nb) * 128u, nv = min(128u, V - v0);
-  if (v0 == 0 && tid == 0 && a.found[vbl * a.lmax + a.dbound + 1]) atomicOr(a.err, 8u);
+  const uint32_t V = g.V, tid = threadIdx.x, q = tid & 63u, rg = tid >> 6;
+  const uint32_t vb0 = (blockIdx.x / a.nb) * 512u;
+  if (vb0 == 0 && tid == 0 && a.found[vbl * a.lmax + a.dbound + 1]) atomicOr(a.err, 8u);
   const uint32_t nr = min(a.R, a.n - b.rix0);
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(a.lev + ((size_t)vbl * V + v0) * 64u);
-    for (uint32_t x = tid; x < nv * 4u; x += kBlock) reinterpret_cast<uint4*>(s_lev)[x] = src[x];
+  uint32_t pk[16];        // per root of this wave: reached | sum dist << 16
+  uint64_t hh[16];        // per root: sum dist_key * (dist + 1)
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    pk[j] = 0u;
+    hh[j] = 0ull;
   }
-  if (a.digest && tid < 128u) s_kd[tid] = (v0 + tid < V) ? g.dkey[2ull * (v0 + tid)] : 0ull;
-  __syncthreads();
-  const uint32_t r = lane, m0 = 32u * wave;  // this lane's root, the wave's nodes
-  uint32_t l[32];
-#pragma unroll
-  for (int j = 0; j < 32; ++j) l[j] = (m0 + j < nv) ? s_lev[(m0 + j) * 64u + r] : 0u;
-  if (a.digest) {
-    uint64_t reached = 0, sumd = 0, h = 0;
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      if (!l[j]) continue;
-      reached += 1;
-      sumd += l[j] - 1u;
-      h += s_kd[m0 + j] * (uint64_t)l[j];
-    }
-    s_red[wave][r][0] = reached;
-    s_red[wave][r][1] = sumd;
-    s_red[wave][r][2] = h;
-  }
-  if (r < nr && v0 + m0 < V) {
-    const size_t off = (size_t)(b.rix0 + r) * V + v0 + m0;
-    if (a.dist) {
-      uint32_t* row = a.dist + off;
-      if ((V & 3u) == 0 && m0 + 32u <= nv) {
-#pragma unroll
-        for (int x = 0; x < 8; ++x) {
-          uint32_t dv[4];
-#pragma unroll
-          for (int c = 0; c < 4; ++c) dv[c] = l[4 * x + c] ? l[4 * x + c] - 1u : kInf;
-          reinterpret_cast<uint4*>(row)[x] = make_uint4(dv[0], dv[1], dv[2], dv[3]);
-        }
-      } else {
-        for (uint32_t j = 0; j < 32u && m0 + j < nv; ++j) row[j] = l[j] ? l[j] - 1u : kInf;
-      }
-    }
-    // level row bytes: dist + 1, 0x7F for unreached and padding (levels stay
-    // <= 125: nh_derive's compare needs them below 0x7F); rows are lev_pitch
-    // bytes (a multiple of 16), so the wave's 32 bytes (up to the pitch) are
-    // whole words
-    uint8_t* lrow = a.levrow + (size_t)(b.rix0 + r) * a.lev_pitch + v0 + m0;
-#pragma unroll
-    for (int x = 0; x < 2; ++x) {
-      if (v0 + m0 + 16u * x >= a.lev_pitch) break;
-      uint32_t w4[4];
+  for (uint32_t half = 0; half < 2u; ++half) {
+    const uint32_t v0 = vb0 + 256u * half;
+    if (v0 >= V) break;  // block-uniform
+    const uint32_t vq = v0 + 4u * q;
+    {
+      uint32_t x[4][4];  // [node c][word m]: roots 16 rg + 4 m .. + 3 of node vq + c
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        uint32_t w = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t lb = l[16 * x + 4 * c + k];
-          w |= (lb ? lb : 0x7Fu) << (8 * k);
+        const uint32_t v = vq + c;
+        uint4 r4 = make_uint4(0u, 0u, 0u, 0u);
+        uint32_t sn = 0;
+        if (v < V) {
+          r4 = *reinterpret_cast<const uint4*>(a.lev + ((size_t)vbl * V + v) * 64u + 16u * rg);
+          sn = (uint32_t)(b.seen[v] >> (16u * rg)) & 0xFFFFu;
         }
-        w4[c] = w;
+        x[c][0] = r4.x & (nib_bytes(sn & 0xFu) * 0xFFu);
+        x[c][1] = r4.y & (nib_bytes((sn >> 4) & 0xFu) * 0xFFu);
+        x[c][2] = r4.z & (nib_bytes((sn >> 8) & 0xFu) * 0xFFu);
+        x[c][3] = r4.w & (nib_bytes((sn >> 12) & 0xFu) * 0xFFu);
       }
-      reinterpret_cast<uint4*>(lrow)[x] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const uint32_t t0 = byte_perm(x[1][m], x[0][m], 0x05010400u);
+        const uint32_t t1 = byte_perm(x[1][m], x[0][m], 0x07030602u);
+        const uint32_t t2 = byte_perm(x[3][m], x[2][m], 0x05010400u);
+        const uint32_t t3 = byte_perm(x[3][m], x[2][m], 0x07030602u);
+        const uint32_t r0 = 16u * rg + 4u * m;
+        s_T[(r0 + 0u) * 65u + q] = byte_perm(t2, t0, 0x05040100u);
+        s_T[(r0 + 1u) * 65u + q] = byte_perm(t2, t0, 0x07060302u);
+        s_T[(r0 + 2u) * 65u + q] = byte_perm(t3, t1, 0x05040100u);
+        s_T[(r0 + 3u) * 65u + q] = byte_perm(t3, t1, 0x07060302u);
+      }
     }
+    uint64_t kd[4] = {0ull, 0ull, 0ull, 0ull};
+    if (a.digest) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) kd[c] = vq + c < V ? g.dkey[2ull * (vq + c)] : 0ull;
+    }
+    __syncthreads();
+    const bool vec = (V & 3u) == 0 && vq + 4u <= V;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t r = 16u * rg + j;  // rg = this wave
+      const uint32_t u = s_T[r * 65u + q];
+      if (r >= nr) continue;
+      // level row: dist + 1, 0x7F for unreached and padding (bytes < 0x80)
+      const uint32_t zm = ~((u | 0x80808080u) - 0x01010101u) & 0x80808080u;
+      if (vq < a.lev_pitch)
+        *reinterpret_cast<uint32_t*>(a.levrow + (size_t)(b.rix0 + r) * a.lev_pitch + vq) =
+            u | (zm - (zm >> 7));
+      uint32_t dv[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t l = (u >> (8 * c)) & 0xFFu;
+        dv[c] = l ? l - 1u : kInf;
+        if (a.digest && l) {
+          pk[j] += 1u + ((l - 1u) << 16);
+          hh[j] += kd[c] * (uint64_t)l;
+        }
+      }
+      if (a.dist) {
+        uint32_t* row = a.dist + (size_t)(b.rix0 + r) * V + vq;
+        if (vec) {
+          *reinterpret_cast<uint4*>(row) = make_uint4(dv[0], dv[1], dv[2], dv[3]);
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (vq + c < V) row[c] = dv[c];
+        }
+      }
+    }
+    __syncthreads();  // s_T is rewritten by the next half
   }
   if (a.digest) {
-    __syncthreads();
-    if (tid < 64u && tid < nr) {
-      uint64_t rr = 0, sd = 0, hh = 0;
+    // 16 roots x 64 lanes -> lane (32 a + 16 b + 8 c + 4 d) holds root 8a+4b+2c+d
+    xreduce_step<16>(pk, q, 32);
+    xreduce_step<8>(pk, q, 16);
+    xreduce_step<4>(pk, q, 8);
+    xreduce_step<2>(pk, q, 4);
+    xreduce_step<16>(hh, q, 32);
+    xreduce_step<8>(hh, q, 16);
+    xreduce_step<4>(hh, q, 8);
+    xreduce_step<2>(hh, q, 4);
+    uint32_t p = pk[0];
+    uint64_t h = hh[0];
 #pragma unroll
-      for (int w = 0; w < (int)kWavesPerBlock; ++w) {
-        rr += s_red[w][tid][0];
-        sd += s_red[w][tid][1];
-        hh += s_red[w][tid][2];
-      }
-      if (rr) {
-        ospf_digest* dg = a.digest + b.rix0 + tid;
-        atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)rr);
-        atomicAdd((unsigned long long*)&dg->sum_dist, (unsigned long long)sd);
-        atomicAdd((unsigned long long*)&dg->hash, (unsigned long long)hh);
-      }
+    for (int o = 2; o > 0; o >>= 1) {
+      p += (uint32_t)__shfl_xor((int)p, o);
+      h += shfl_xor64(h, o);
+    }
+    const uint32_t r = 16u * rg + ((q >> 5) & 1u) * 8u + ((q >> 4) & 1u) * 4u +
+                       ((q >> 3) & 1u) * 2u + ((q >> 2) & 1u);
+    if ((q & 3u) == 0 && r < nr && (p & 0xFFFFu)) {
+      ospf_digest* dg = a.digest + b.rix0 + r;
+      atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)(p & 0xFFFFu));
+      atomicAdd((unsigned long long*)&dg->sum_dist, (unsigned long long)(p >> 16));
+      atomicAdd((unsigned long long*)&dg->hash, (unsigned long long)h);
     }
   }
 }
@@ -1838,7 +1897,7 @@ hipError_t launch_msbfs_levels(const DevGraph& g, const MsArgs& a, uint32_t dept
                        s, g, a, d);
     hipLaunchKernelGGL(msbfs_settle_kernel<-1>, dim3(a.nb * chunks), dim3(kBlock), 0, s, g, a, d);
   }
-  hipLaunchKernelGGL(msbfs_levrows_kernel, dim3(a.nb * ((g.V + 127u) / 128u)), dim3(kBlock), 0, s,
+  hipLaunchKernelGGL(msbfs_levrows_kernel, dim3(a.nb * ((g.V + 511u) / 512u)), dim3(kBlock), 0, s,
                      g, a);
   return hipGetLastError();
 }
