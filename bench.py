@@ -14,7 +14,8 @@ over RCCL. The timed steps' own digests of the CPU-sample roots are checked
 against the CPU restatement (`parity_vs_cpu_sample`).
 
 Other topologies (parity / side benches, not the headline): fabric10k,
-fabric100k-w (metrics 1..64, seed 7), grid31, mesh1m (8,192 sampled roots).
+fabric100k-w and fabric10k-w (metrics 1..64, seed 7: weighted derive mode,
+wderive_main), grid31, mesh1m (8,192 sampled roots).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--topology T]
        torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
@@ -62,6 +63,9 @@ def build_topology(name: str):
     if name == "fabric100k-w":
         return (T.fabric(pods=1781, planes=8, weighted_seed=7),
                 "F100k fabric pods=1781 planes=8 (metric 1..64, seed 7)", True, 0)
+    if name == "fabric10k-w":
+        return (T.fabric(pods=173, planes=8, weighted_seed=7),
+                "F10k fabric pods=173 planes=8 (metric 1..64, seed 7)", True, 0)
     if name == "grid31":
         return T.grid(31), "G31 grid 31x31 (unit metric)", False, 0
     if name == "mesh1m":
@@ -205,11 +209,16 @@ def main():
     derive_ok = (n_roots <= 0 and not weighted and args.roots_per_gpu == 0 and not args.no_nh
                  and not args.class_only and eng.info().unit_metric
                  and int(shard.distinct_neighbors(csr["row_ptr"], csr["col"]).max()) <= 2048)
-    if args.mode == "derive" and not derive_ok:
-        raise SystemExit("derive mode needs an all-sources unit-metric sweep (strong scaling)")
     if args.mode != "batch" and derive_ok:
         return derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, dev,
                            backend, coll_dev)
+    wderive_ok = (n_roots <= 0 and not derive_ok and args.roots_per_gpu == 0 and not args.no_nh
+                  and not args.class_only)
+    if args.mode == "derive" and not (derive_ok or wderive_ok):
+        raise SystemExit("derive mode needs an all-sources sweep (strong scaling)")
+    if args.mode != "batch" and wderive_ok:
+        return wderive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, dev,
+                            backend, coll_dev, weighted)
     pool = perm if n_roots <= 0 else perm[: min(n_roots, V)]
     nbrs = shard.distinct_neighbors(csr["row_ptr"], csr["col"])
     key = shard.first_neighbor(csr["row_ptr"], csr["col"]) if args.root_order != "random" \
@@ -642,6 +651,228 @@ def derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
                             "isolated_launch_ms": round(c["iso_ms"], 3)})
     report(args, stream, names, perm, step_digest, dt, V * args.steps, E, desc, 0, V, world, rank,
            dist_on, backend, V, classes_cfg, roofline, "strong", "derive")
+    if dist_on:
+        torch.distributed.destroy_process_group()
+
+
+def wderive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, dev, backend,
+                 coll_dev, weighted):
+    """All-sources step on a weighted graph (or any graph outside derive
+    mode's unit-metric contract). Cover roots (a vertex cover S: on the
+    fabric the fabric and spine switches) run the per-root SPF kernel chosen
+    by the engine (variant 7 here), one launch per width class on its own
+    stream, their dist rows into one slab; then the leaf roots (the
+    independent set I = V \\ S: the racks) are derived from those rows by
+    ospf_wderive_dev (spf_wderive.hip). A rank owns a pod / plane block
+    (fabric) or class slices, and runs the cover rows its leaves need."""
+    rp, col = csr["row_ptr"], csr["col"]
+    perm = np.random.default_rng(SEED).permutation(V).astype(np.uint32)
+    key = shard.first_neighbor(rp, col)
+    nbrs = shard.distinct_neighbors(rp, col)
+    caps = shard.neighbor_caps(nbrs)
+    leaf = shard.leaf_set(rp, col)
+
+    def part(r):
+        if world == 1:
+            return perm
+        fp = shard.fabric_partition(names, world, r)
+        if fp is not None:
+            return fp
+        cls = shard.make_classes(perm, caps, V, key)
+        return np.concatenate([c.roots[slice(*shard.rank_slice(c.roots.size, world, r))]
+                               for c in cls])
+
+    parts = [part(r) for r in range(world)]
+    plans = [shard.wderive_plan(p, leaf, rp, col) for p in parts]
+    cover, lr = plans[rank]
+    lr = shard.locality_order(lr, key)  # racks of a pod adjacent: one run per pod
+    flags = N.OSPF_WANT_DIST | N.OSPF_WANT_NH | N.OSPF_WANT_DIGEST
+    t0 = time.time()
+    classes, off = [], 0
+    for cap in sorted(set(caps[cover].tolist())):
+        roots = shard.locality_order(cover[caps[cover] == cap], key)
+        W = max(1, cap // 32) if cap > 16 else 1
+        mx = int(max(1, nbrs[roots].max()))
+        classes.append(dict(cap=cap, W=W, roots=roots, n=int(roots.size), off=off,
+                            d=torch.from_numpy(roots.view(np.int32)).to(dev),
+                            nh=torch.empty((roots.size, V, W), dtype=torch.int32, device=dev),
+                            max_nbrs=mx,
+                            plan=eng.plan(W, flags, n_roots=int(roots.size),
+                                          max_root_neighbors=mx),
+                            stream=torch.cuda.Stream(device=dev), ms=[]))
+        off += roots.size
+    corder = np.concatenate([c["roots"] for c in classes]) if classes else \
+        np.zeros(0, np.uint32)
+    pos = np.full(V, 0xFFFFFFFF, np.uint32)
+    pos[corder] = np.arange(corder.size, dtype=np.uint32)
+    cdist = torch.empty((max(1, corder.size), V), dtype=torch.int32, device=dev)
+    d_pos = torch.from_numpy(pos.view(np.int32)).to(dev)
+    nl = int(lr.size)
+    kmax = int(nbrs[lr].max()) if nl else 0
+    d_lr = torch.from_numpy(lr.view(np.int32)).to(dev)
+    ldist = torch.empty((max(1, nl), V), dtype=torch.int32, device=dev)
+    lnh = torch.empty((max(1, nl), V), dtype=torch.int32, device=dev)
+    dig = torch.zeros((corder.size + nl, 3), dtype=torch.int64, device=dev)
+    log(f"[rank {rank}] wderive: {parts[rank].size} roots = {nl} leaves (<= {kmax} "
+        f"neighbours) + cover {corder.size} ({[(c['cap'], c['n'], c['plan']['variant']) for c in classes]}), "
+        f"buffers {(cdist.numel() + ldist.numel() + lnh.numel() + sum(c['nh'].numel() for c in classes)) * 4 / 2**30:.1f}"
+        f" GiB in {time.time() - t0:.1f}s")
+    main_s = torch.cuda.current_stream()
+
+    def cover_launch(c, s_):
+        eng.run_dev(c["d"].data_ptr(), c["n"], c["W"], flags=flags,
+                    d_dist=cdist[c["off"]].data_ptr(), d_nh=c["nh"].data_ptr(),
+                    d_digest=dig[c["off"]].data_ptr(), stream=s_.cuda_stream,
+                    max_root_neighbors=c["max_nbrs"])
+
+    def leaf_launch(s_):
+        if nl:
+            eng.wderive_dev(d_lr.data_ptr(), nl, cdist.data_ptr(), d_pos.data_ptr(),
+                            ldist.data_ptr(), d_nh=lnh.data_ptr(),
+                            d_digest=dig[corder.size].data_ptr(), max_root_neighbors=kmax,
+                            stream=s_.cuda_stream)
+
+    # owned roots' digest rows (the cover rows a rank adds for its leaves are
+    # not its roots), gathered in a padded slot per rank
+    def owned_rows(p, cv, lv):
+        own = np.zeros(V, bool)
+        own[p] = True
+        co = np.concatenate([shard.locality_order(cv[caps[cv] == cap], key)
+                             for cap in sorted(set(caps[cv].tolist()))]) if cv.size else cv
+        return co[own[co]], shard.locality_order(lv, key)
+
+    owned = [owned_rows(p, *pl) for p, pl in zip(parts, plans)]
+    slot = max(a.size + b.size for a, b in owned)
+    own_c, _ = owned[rank]
+    idx = np.concatenate([pos[own_c], corder.size + np.arange(nl)]).astype(np.int64)
+    d_idx = torch.from_numpy(idx).to(dev)
+    gbuf = torch.zeros((slot, 3), dtype=torch.int64, device=dev)
+    leaf_ms, gathered = [], {}
+
+    def step(timed):
+        a_ = torch.cuda.Event(enable_timing=True)
+        a_.record(main_s)
+        done = []
+        for c in classes:
+            cs = c["stream"]
+            cs.wait_event(a_)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(cs)
+            cover_launch(c, cs)
+            e1.record(cs)
+            done.append(e1)
+            if timed:
+                c["ms"].append((e0, e1))
+        for e in done:
+            main_s.wait_event(e)
+        l0, l1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        l0.record(main_s)
+        leaf_launch(main_s)
+        l1.record(main_s)
+        if timed:
+            leaf_ms.append((l0, l1))
+        if dist_on:
+            torch.index_select(dig, 0, d_idx, out=gbuf[: idx.size])
+            gathered["g"] = shard.gather_digests(gbuf)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    eng.sync(main_s.cuda_stream)
+    if dist_on:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if dist_on:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t_start
+    eng.sync(main_s.cuda_stream)
+    if dist_on:
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+
+    step_digest = {}
+    if dist_on:
+        g = gathered["g"].cpu().numpy().view(np.uint64).reshape(world, slot, 3)
+        for r, (a, b) in enumerate(owned):
+            for j, root in enumerate(np.concatenate([a, b])):
+                step_digest[int(root)] = g[r, j]
+    else:
+        d = dig.cpu().numpy().view(np.uint64)
+        for j, root in enumerate(np.concatenate([corder, lr])):
+            step_digest[int(root)] = d[j]
+
+    iso_s = torch.cuda.Stream(device=dev)
+
+    def iso(fn):
+        ms = []
+        with torch.cuda.stream(iso_s):
+            for _ in range(args.iso_reps + 1):
+                a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a_.record(iso_s)
+                fn(iso_s)
+                b_.record(iso_s)
+                b_.synchronize()
+                ms.append(a_.elapsed_time(b_))
+        return float(np.median(ms[1:])) if len(ms) > 1 else float(ms[0])
+
+    units = []
+    for c in classes:
+        c["iso_ms"] = iso(lambda s_, c=c: cover_launch(c, s_))
+        p = c["plan"]
+        units.append({"launch": f"cover_cap{c['cap']}",
+                      "kernel": f"variant {p['variant']} class launch ({c['W']} next-hop words)",
+                      "cap": c["cap"], "nh_words": c["W"], "roots_per_launch": c["n"],
+                      "isolated_launch_ms": round(c["iso_ms"], 3),
+                      "compulsory_bytes": compulsory_bytes(V, E, c["W"], c["n"], p["variant"],
+                                                           p["slices"], weighted),
+                      "traffic": pmc_traffic(args.profile_dir,
+                                             f"variant{p['variant']}_cap{c['cap']}", c["n"])})
+    if nl:
+        l_iso = iso(leaf_launch)
+        n_src = int(np.setdiff1d(shard.closure(lr, rp, col), lr).size)  # cover rows read
+        units.append({"launch": "wderive", "kernel": "ospf_wderive_dev (wderive_kernel: leaf "
+                      "rows from neighbours' dist rows)", "roots_per_launch": nl,
+                      "isolated_launch_ms": round(l_iso, 3),
+                      "compulsory_bytes": nl * 8 * V + n_src * 4 * V,
+                      "traffic": pmc_traffic(args.profile_dir, "wderive", nl)})
+    eng.sync(iso_s.cuda_stream)
+    for u in units:
+        sec = u["isolated_launch_ms"] / 1e3
+        u["achieved"] = round(u["compulsory_bytes"] / sec / 1e9, 1)
+        u["frac"] = round(u["compulsory_bytes"] / sec / 1e9 / HBM_PEAK_GBS, 4)
+        u["traffic_over_compulsory"] = (round(u["traffic"] / u["compulsory_bytes"], 2)
+                                        if u["traffic"] else None)
+    dom = max(units, key=lambda u: u["isolated_launch_ms"])
+    step_comp = sum(u["compulsory_bytes"] for u in units)
+    step_s = dt / args.steps
+    roofline = {
+        "bound": "hbm", "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": dom["frac"], "traffic": dom["traffic"], "kernel": dom["kernel"],
+        "roots_per_launch": dom["roots_per_launch"], "avg_launch_ms": dom["isolated_launch_ms"],
+        "compulsory_bytes": dom["compulsory_bytes"],
+        "traffic_over_compulsory": dom["traffic_over_compulsory"], "launches": units,
+        "step_compulsory_bytes": step_comp,
+        "step_frac": round(step_comp / step_s / 1e9 / HBM_PEAK_GBS, 4),
+        "note": "achieved = compulsory bytes of the dominant launch / its isolated time: cover "
+                "classes = dist + next-hop rows written + one weighted CSR scan per run; "
+                "wderive = leaf dist + next-hop rows written + the cover rows read once",
+    }
+    classes_cfg = [{"cap": c["cap"], "nh_words": c["W"], "roots_this_rank": c["n"],
+                    "path": f"cover (variant {c['plan']['variant']})",
+                    "avg_launch_ms": round(float(np.mean([a_.elapsed_time(b_) for a_, b_ in c["ms"]])), 3),
+                    "isolated_launch_ms": round(c["iso_ms"], 3)} for c in classes]
+    if nl:
+        classes_cfg.append({"launch": "wderive", "roots_this_rank": nl, "max_neighbours": kmax,
+                            "avg_launch_ms": round(float(np.mean(
+                                [a_.elapsed_time(b_) for a_, b_ in leaf_ms])), 3),
+                            "isolated_launch_ms": round(l_iso, 3)})
+    report(args, stream, names, perm, step_digest, dt, V * args.steps, E, desc, 0, V, world, rank,
+           dist_on, backend, V, classes_cfg, roofline, "strong", "wderive")
     if dist_on:
         torch.distributed.destroy_process_group()
 

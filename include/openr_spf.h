@@ -196,6 +196,25 @@ int ospf_nh_derive_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n, uint3
                        const uint32_t* d_lev_pos, const ospf_digest* d_lev_digest,
                        uint32_t* d_nh, ospf_digest* d_digest, void* stream);
 
+/* Weighted all-sources rows of leaf roots (any metric, or OSPF_HOP_COUNT; no
+ * ignored links). For a root r with distinct neighbours n_k, w_k = the
+ * smallest metric r advertises on an up link to n_k and D_k = the distance row
+ * of n_k (d_src + d_pos[n_k] * src_pitch, computed by any engine path with the
+ * same flags): dist(r, v) = min_k w_k + D_k(v) over transit n_k (an overloaded
+ * n_k only reaches itself, at w_k), and bit k of next-hop word 0 of v is set
+ * iff n_k's term is tight -- the reference's runSpf (LinkState.cpp:836-911:
+ * Bellman's equation over the root's out-links; nextHops = the first hops of
+ * the shortest paths, :885-901). Writes d_dist [n][V], d_nh [n][V] (one word
+ * per node; NULL = not wanted) and d_digest [n] (NULL = not wanted). Every
+ * root must have <= max_root_neighbors (1..32, 0 = 32) distinct neighbours,
+ * each transit one with an up link needing a row (else error bits 1 / 16 at
+ * ospf_sync). The caller derives an independent set of roots (no two
+ * adjacent: the racks of a fabric) from the rows of the others. */
+int ospf_wderive_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n, uint32_t flags,
+                     uint32_t max_root_neighbors, const uint32_t* d_src, uint64_t src_pitch,
+                     const uint32_t* d_pos, uint32_t* d_dist, uint32_t* d_nh,
+                     ospf_digest* d_digest, void* stream);
+
 /* Kernel variant the engine would use for a large batch (for reporting):
  * 0 = Dial, LDS-resident (dist+nh in LDS), 1 = Dial, LDS dist + HBM
  * next-hops, 2 = Dial, HBM state, 3 = per-root BFS with LDS bitmaps and LDS

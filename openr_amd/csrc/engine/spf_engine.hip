@@ -1278,6 +1278,50 @@ int ospf_nh_derive_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_
   return OSPF_OK;
 }
 
+// Weighted derive (spf_wderive.hip): the rows of leaf roots (<= 32 distinct
+// neighbours, every transit one with a row in d_src) by Bellman's equation
+// over their out-links. Any metric (or hop count); no ignored links.
+int ospf_wderive_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t flags,
+                     uint32_t max_root_neighbors, const uint32_t* d_src, uint64_t src_pitch, const uint32_t* d_pos,
+                     uint32_t* d_dist, uint32_t* d_nh, ospf_digest* d_digest, void* stream) {
+  if (!c) return OSPF_E_INVAL;
+  if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  if (n == 0) return OSPF_OK;
+  if (!d_roots || !d_src || !d_pos || !d_dist) return fail(c, OSPF_E_INVAL, "null argument");
+  const uint32_t V = c->info.n_nodes;
+  if (src_pitch < V) return fail(c, OSPF_E_INVAL, "wderive: src_pitch >= V");
+  if (!(flags & OSPF_HOP_COUNT) && c->dist_bound >= 0xFFFFFFFFull)
+    return fail(c, OSPF_E_RANGE, "distances may reach 2^32 - 1");
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (d_digest) HIPCHK(c, hipMemsetAsync(d_digest, 0, (size_t)n * sizeof(ospf_digest), s));
+  ospf::WDeriveArgs a{};
+  a.roots = d_roots;
+  a.n = n;
+  a.hop = (flags & OSPF_HOP_COUNT) ? 1u : 0u;
+  a.src = d_src;
+  a.src_pitch = src_pitch;
+  a.pos = d_pos;
+  a.dist = d_dist;
+  a.nh = d_nh;
+  a.digest = d_digest;
+  a.err = c->d_err;
+  const uintptr_t al = (uintptr_t)d_src | (uintptr_t)d_dist | (uintptr_t)d_nh;
+  a.vec = (V % 4u == 0 && src_pitch % 4u == 0 && (al & 15u) == 0) ? 1u : 0u;
+  if (const char* e = getenv("OSPF_WD_G")) a.G = (uint32_t)std::max(1, atoi(e));
+  if (const char* e = getenv("OSPF_WD_CTILES")) a.ctiles = (uint32_t)std::max(1, atoi(e));
+  // slot table width from the caller's bound (the roots' distinct neighbour
+  // counts are checked on the device: a wider root raises error bit 1)
+  if (max_root_neighbors > ospf::kWdMaxK)
+    return fail(c, OSPF_E_RANGE, "wderive: leaf roots have at most 32 distinct neighbours");
+  uint32_t kmax = max_root_neighbors ? max_root_neighbors : ospf::kWdMaxK;
+  if (const char* e = getenv("OSPF_WD_KMAX")) kmax = (uint32_t)std::max(1, atoi(e));
+  hipError_t e = ospf::launch_wderive(c->g, a, kmax, s);
+  if (e != hipSuccess) return hip_fail(c, e, "launch_wderive");
+  c->spf_runs += n;
+  return OSPF_OK;
+}
+
 int ospf_sssp_batch(ospf_ctx* c, const uint32_t* roots, uint32_t n_roots, const ospf_ignore* ig,
                     uint32_t flags, uint32_t nh_words, uint32_t* dist_out, uint32_t* nh_out,
                     ospf_digest* digest_out) {

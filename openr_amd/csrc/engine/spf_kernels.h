@@ -206,6 +206,27 @@ struct DeriveArgs {
   uint32_t ctiles;         // node tiles per block (0: default 8)
   uint32_t G, tiles, chunks;  // set by the launcher
 };
+// Weighted derive (spf_wderive.hip): dist + next-hop rows (one word) of n
+// leaf roots from the distance rows of their neighbours (src + pos[v] *
+// src_pitch = row of node v, kInf: none).
+constexpr uint32_t kWdG = 64;     // roots per block
+constexpr uint32_t kWdMaxK = 32;  // distinct neighbours of a leaf root
+struct WDeriveArgs {
+  const uint32_t* roots;
+  uint32_t n;
+  uint32_t hop;             // hop-count mode: every usable weight is 1
+  const uint32_t* src;      // neighbours' distance rows
+  uint64_t src_pitch;       // words per src row
+  const uint32_t* pos;      // [V]
+  uint32_t* dist;           // [n][V]
+  uint32_t* nh;             // [n][V] (one word per node) or null
+  ospf_digest* digest;      // [n] (zeroed by the caller) or null
+  uint32_t* err;            // bit 1: K > 32, 16: a transit neighbour has no row, 64: bad root
+  uint32_t vec;             // 16-B aligned rows (V, src_pitch % 4 == 0): uint4 loads / stores
+  uint32_t G, ctiles;       // roots per block, 256-node subtiles per block (0: defaults)
+  uint32_t tiles, chunks;   // set by the launcher
+};
+hipError_t launch_wderive(const DevGraph& g, WDeriveArgs a, uint32_t kmax, hipStream_t s);
 // phase 1: distances only (kp -1) + msbfs_levrows; phase 2: nh_derive
 hipError_t launch_msbfs_levels(const DevGraph& g, const MsArgs& a, uint32_t depth_bound,
                                hipStream_t s);

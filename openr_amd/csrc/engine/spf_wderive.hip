@@ -1,0 +1,262 @@
+// spf_wderive.hip — weighted all-sources rows of leaf roots from their
+// neighbours' distance rows (gfx950).
+//
+// For a root r with distinct neighbours n_0 .. n_{K-1} (ascending id = next-hop
+// bit order), w_k = the smallest metric r advertises on an up link to n_k
+// (1 in hop-count mode) and D_k = n_k's distance row, the reference's runSpf
+// (openr/decision/LinkState.cpp:836-911) gives, for v != r,
+//
+//   dist(r, v) = min over usable k of  w_k + D_k(v)        (n_k transit)
+//                                      w_k if v == n_k     (n_k overloaded)
+//   bit k of nh(r, v)  <=>  that term of k equals dist(r, v)
+//
+// A shortest r -> v path leaves r over one link to some n_k, and its tail is a
+// path of n_k's own SPF (interior nodes transit, LinkState.cpp:859-866; the
+// tail never needs r again: metrics are >= 1), so the first line is Bellman's
+// equation over r's out-links; the next hops of v are exactly the first hops
+// of its shortest paths (nextHops = union over tight predecessors, with the
+// root's own neighbours as seeds, LinkState.cpp:885-901). An overloaded
+// neighbour is reachable but never relays.
+//
+// The host runs a per-root SPF kernel for a vertex cover S of the graph and
+// derives every other root (an independent set I: all neighbours of a leaf
+// are in S) here. On the fabric, I = the 85,488 rack switches (8 fabric
+// switches each) and S = the 14,536 fabric and spine switches.
+//
+// Shape. Block = a group of up to kWdG roots x a chunk of 256-node subtiles;
+// lane = 4 consecutive nodes (16-B loads of each neighbour row, 16-B stores of
+// dist and next-hop rows: a wave writes 1 KB of each row per instruction).
+// Consecutive roots with the same neighbour slots (the racks of one pod, when
+// the host orders roots by neighbourhood) form a run: the subtile's neighbour
+// rows are loaded once into registers for the whole run, and each root adds
+// only its own link metrics, the compares and the stores. Digests (DESIGN.md
+// §4) are summed per (root, subtile) by a wave reduction into LDS.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "spf_kernels.h"
+
+namespace ospf {
+namespace {
+
+constexpr uint32_t kInf = 0xFFFFFFFFu;
+constexpr uint32_t kDown = 0x80000000u;
+constexpr uint32_t kNt = 0x80000000u;  // slot tag: overloaded neighbour (| its id)
+constexpr int kWave = 64;
+constexpr uint32_t kBlock = 256;
+constexpr uint32_t kWaves = kBlock / kWave;
+constexpr uint32_t kSub = 256;  // nodes per wave pass (4 per lane)
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t x, int o) {
+  const uint32_t lo = __shfl_xor((uint32_t)x, o, kWave);
+  const uint32_t hi = __shfl_xor((uint32_t)(x >> 32), o, kWave);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ bool transit(const DevGraph& g, uint32_t v) {
+  return !((g.nt_bits[v >> 5] >> (v & 31)) & 1u);
+}
+// w + D saturating at kInf (w = kInf: unusable slot; D = kInf: unreached)
+__device__ __forceinline__ uint32_t sat_add(uint32_t w, uint32_t D) {
+  const uint32_t c = w + D;
+  return c < D ? kInf : c;
+}
+
+template <int KM>
+__global__ void __launch_bounds__(256) wderive_kernel(DevGraph g, WDeriveArgs a) {
+  __shared__ uint32_t s_root[kWdG], s_K[kWdG], s_same[kWdG];
+  __shared__ uint32_t s_w[kWdG * KM];  // [root][slot] metric of the slot's link (kInf: none up)
+  __shared__ uint32_t s_p[kWdG * KM];  // [root][slot] row of n_k | kNt | n_k, kInf: unusable
+  __shared__ unsigned long long s_h[kWdG], s_sum[kWdG];
+  __shared__ uint32_t s_reach[kWdG];
+  __shared__ uint64_t s_wk[256];
+  const uint32_t V = g.V, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t G = a.G;
+  const uint32_t ngroups = (a.n + G - 1) / G;
+  const uint32_t ci = blockIdx.x / ngroups, gi = blockIdx.x % ngroups;
+  const uint32_t i0 = gi * G, ng = min(G, a.n - i0);
+  // ---- slot tables of the group's roots
+  if (tid < ng) {
+    const uint32_t r = a.roots[i0 + tid];
+    s_root[tid] = r;
+    s_K[tid] = 0;
+    s_h[tid] = 0ull;
+    s_sum[tid] = 0ull;
+    s_reach[tid] = 0u;
+    if (r >= V) {
+      atomicOr(a.err, 64u);
+    } else {
+      const uint32_t K = g.dn_off[r + 1] - g.dn_off[r];
+      if (K > (uint32_t)KM) atomicOr(a.err, 1u);
+      s_K[tid] = min(K, (uint32_t)KM);
+    }
+  }
+  for (uint32_t x = tid; x < ng * KM; x += kBlock) s_w[x] = kInf;
+  if (a.digest) s_wk[tid] = tid ? digest_word_key(0, tid) : 0ull;
+  __syncthreads();
+  for (uint32_t j = 0; j < ng; ++j) {  // the root's up links: smallest metric per slot
+    const uint32_t r = s_root[j];
+    if (r >= V) continue;
+    for (uint32_t e = g.row_ptr[r] + tid; e < g.row_ptr[r + 1]; e += kBlock) {
+      const uint32_t cx = g.colx[e];
+      if ((cx & kDown) || cx == r) continue;
+      const uint32_t k = g.didx[e];
+      if (k < s_K[j]) atomicMin(&s_w[j * KM + k], a.hop ? 1u : g.w[e]);
+    }
+  }
+  __syncthreads();
+  for (uint32_t x = tid; x < ng * KM; x += kBlock) {
+    const uint32_t j = x / KM, k = x - j * KM;
+    uint32_t p = kInf;
+    if (k < s_K[j] && s_w[x] != kInf) {
+      const uint32_t nb = g.dn[g.dn_off[s_root[j]] + k];
+      if (transit(g, nb)) {
+        p = a.pos[nb];
+        if (p == kInf) atomicOr(a.err, 16u);
+      } else {
+        p = kNt | nb;
+      }
+    }
+    s_p[x] = p;
+  }
+  __syncthreads();
+  if (tid < ng) {  // a run continues while the neighbour slots stay the same
+    uint32_t same = tid > 0 && s_K[tid] == s_K[tid - 1];
+    for (uint32_t k = 0; same && k < (uint32_t)KM; ++k)
+      same = s_p[tid * KM + k] == s_p[(tid - 1) * KM + k];
+    s_same[tid] = same;
+  }
+  __syncthreads();
+  // ---- subtiles
+  const bool vec = a.vec != 0;
+  const uint32_t t0 = ci * a.ctiles, t1 = min(a.tiles, t0 + a.ctiles);
+  for (uint32_t t = t0 + wave; t < t1; t += kWaves) {
+    const uint32_t v0 = t * kSub + 4u * lane;
+    const bool full = v0 + 4u <= V;
+    uint64_t dk[4], nk[4];
+    if (a.digest) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const uint32_t v = min(v0 + b, V - 1u);
+        dk[b] = g.dkey[2ull * v];
+        nk[b] = g.dkey[2ull * v + 1];
+      }
+    }
+    uint32_t D[KM][4];
+    for (uint32_t j = 0; j < ng; ++j) {
+      const uint32_t r = s_root[j];
+      if (r >= V) continue;
+      const uint32_t* sp = s_p + j * KM;
+      const uint32_t* sw = s_w + j * KM;
+      if (!s_same[j]) {  // a new run: load its neighbour rows for this subtile
+#pragma unroll
+        for (int k = 0; k < KM; ++k) {
+          const uint32_t p = sp[k];  // uniform across the wave
+          if (p < kNt) {
+            const uint32_t* row = a.src + (size_t)p * a.src_pitch;
+            if (vec && full) {
+              const uint4 x = *reinterpret_cast<const uint4*>(row + v0);
+              D[k][0] = x.x; D[k][1] = x.y; D[k][2] = x.z; D[k][3] = x.w;
+            } else {
+#pragma unroll
+              for (int b = 0; b < 4; ++b) D[k][b] = v0 + b < V ? row[v0 + b] : kInf;
+            }
+          } else if (p != kInf) {  // overloaded neighbour: reachable, never relays
+#pragma unroll
+            for (int b = 0; b < 4; ++b) D[k][b] = (v0 + b == (p & ~kNt)) ? 0u : kInf;
+          } else {
+#pragma unroll
+            for (int b = 0; b < 4; ++b) D[k][b] = kInf;
+          }
+        }
+      }
+      uint32_t m[4] = {kInf, kInf, kInf, kInf};
+#pragma unroll
+      for (int k = 0; k < KM; ++k) {
+        const uint32_t w = sw[k];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) m[b] = min(m[b], sat_add(w, D[k][b]));
+      }
+      uint32_t bits[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int k = 0; k < KM; ++k) {
+        const uint32_t w = sw[k];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) bits[b] |= (sat_add(w, D[k][b]) == m[b] ? 1u : 0u) << k;
+      }
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        if (v0 + b == r) m[b] = 0u;  // the root itself: dist 0, no next hops
+        if (m[b] == kInf || v0 + b == r) bits[b] = 0u;
+      }
+      const size_t i = i0 + j;
+      uint32_t* drow = a.dist + i * V;
+      uint32_t* nrow = a.nh ? a.nh + i * V : nullptr;
+      if (vec && full) {
+        *reinterpret_cast<uint4*>(drow + v0) = make_uint4(m[0], m[1], m[2], m[3]);
+        if (nrow) *reinterpret_cast<uint4*>(nrow + v0) = make_uint4(bits[0], bits[1], bits[2], bits[3]);
+      } else {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          if (v0 + b < V) {
+            drow[v0 + b] = m[b];
+            if (nrow) nrow[v0 + b] = bits[b];
+          }
+        }
+      }
+      if (a.digest) {
+        uint64_t h = 0, sum = 0;
+        uint32_t reach = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          if (v0 + b < V && m[b] != kInf) {
+            reach += 1u;
+            sum += m[b];
+            h += dk[b] * ((uint64_t)m[b] + 1ull);
+            if (bits[b]) h += nk[b] * (KM <= 8 ? s_wk[bits[b]] : digest_word_key(0, bits[b]));
+          }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          h += shfl_xor64(h, o);
+          sum += shfl_xor64(sum, o);
+          reach += __shfl_xor(reach, o, kWave);
+        }
+        if (lane == 0 && reach) {
+          atomicAdd(&s_h[j], (unsigned long long)h);
+          atomicAdd(&s_sum[j], (unsigned long long)sum);
+          atomicAdd(&s_reach[j], reach);
+        }
+      }
+    }
+  }
+  if (a.digest) {
+    __syncthreads();
+    if (tid < ng && s_reach[tid]) {
+      ospf_digest* dg = a.digest + i0 + tid;
+      atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)s_reach[tid]);
+      atomicAdd((unsigned long long*)&dg->sum_dist, s_sum[tid]);
+      atomicAdd((unsigned long long*)&dg->hash, s_h[tid]);
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_wderive(const DevGraph& g, WDeriveArgs a, uint32_t kmax, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
+  if (kmax > kWdMaxK) return hipErrorInvalidValue;
+  a.tiles = (g.V + kSub - 1) / kSub;
+  if (a.ctiles == 0) a.ctiles = 16;
+  a.ctiles = std::min(a.ctiles, a.tiles);
+  a.chunks = (a.tiles + a.ctiles - 1) / a.ctiles;
+  if (a.G == 0 || a.G > kWdG) a.G = kWdG;
+  const dim3 grid(((a.n + a.G - 1) / a.G) * a.chunks);
+  if (kmax <= 8) hipLaunchKernelGGL(wderive_kernel<8>, grid, dim3(kBlock), 0, s, g, a);
+  else if (kmax <= 16) hipLaunchKernelGGL(wderive_kernel<16>, grid, dim3(kBlock), 0, s, g, a);
+  else hipLaunchKernelGGL(wderive_kernel<32>, grid, dim3(kBlock), 0, s, g, a);
+  return hipGetLastError();
+}
+
+}  // namespace ospf

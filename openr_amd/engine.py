@@ -182,6 +182,20 @@ class Engine:
                                                d_lev_digest or None, d_nh, d_digest or None,
                                                stream or None))
 
+    def wderive_dev(self, d_roots: int, n: int, d_src: int, d_pos: int, d_dist: int, *,
+                    src_pitch: int = 0, d_nh: int = 0, d_digest: int = 0,
+                    max_root_neighbors: int = 0, hop_count: bool = False,
+                    stream: int = 0) -> None:
+        """Weighted derive (ospf_wderive_dev): dist rows [n][V], one-word
+        next-hop rows [n][V] and digests of n leaf roots (<= 32 distinct
+        neighbours) from their neighbours' distance rows
+        (d_src + d_pos[v] * src_pitch words)."""
+        self._check(self._L.ospf_wderive_dev(self._h, d_roots, n,
+                                             N.OSPF_HOP_COUNT if hop_count else 0,
+                                             max_root_neighbors, d_src, src_pitch or self.V,
+                                             d_pos, d_dist, d_nh or None, d_digest or None,
+                                             stream or None))
+
     def ksp2(self, src: int, dsts: Sequence[int], path_cap: int = 512):
         """getKthPaths(src, d, 1) and (src, d, 2) for every d (ospf_ksp2_run).
         Returns (k1, k2, status): per destination a list of paths (lists of

@@ -205,3 +205,49 @@ def fabric_partition(names: Sequence[str], world: int, rank: int):
     q0, q1 = rank_slice(planes, world, rank)
     mine = ((kind != 1) & (a >= p0) & (a < p1)) | ((kind == 1) & (a >= q0) & (a < q1))
     return np.nonzero(mine)[0].astype(np.uint32)
+
+
+# ---------------------------------------------------------------- weighted derive
+# Weighted all-sources sweeps run a per-root SPF kernel for a vertex cover S
+# of the graph and derive the rows of the other nodes -- an independent set I
+# of "leaf" roots with <= 32 distinct neighbours, all in S -- from their
+# neighbours' distance rows (ospf_wderive_dev). On the fabric I = the racks.
+
+def leaf_set(row_ptr: np.ndarray, col: np.ndarray, max_nbrs: int = 32) -> np.ndarray:
+    """Independent set of nodes with <= max_nbrs distinct neighbours, chosen
+    greedily by (distinct neighbours, id): a node joins when it is the
+    smallest undecided candidate among its undecided neighbours, and its
+    neighbours leave (Luby rounds with a fixed priority). Links of any state
+    count as adjacency. Returns a bool mask [V]."""
+    V = row_ptr.size - 1
+    nb = distinct_neighbors(row_ptr, col).astype(np.int64)
+    owner = np.repeat(np.arange(V), np.diff(row_ptr.astype(np.int64)))
+    colv = col.astype(np.int64)
+    real = colv != owner
+    owner, colv = owner[real], colv[real]
+    prio = nb * V + np.arange(V)
+    state = np.where(nb <= max_nbrs, 0, 2)  # 0 undecided, 1 leaf, 2 excluded
+    big = np.iinfo(np.int64).max
+    while np.any(state == 0):
+        und = state == 0
+        m = und[owner] & und[colv]
+        nbmin = np.full(V, big, np.int64)
+        np.minimum.at(nbmin, owner[m], prio[colv[m]])
+        join = und & (prio < nbmin)
+        state[join] = 1
+        state[colv[join[owner]]] = np.where(state[colv[join[owner]]] == 1, 1, 2)
+    leaf = state == 1
+    assert not np.any(leaf[owner] & leaf[colv]), "leaf set is not independent"
+    return leaf
+
+
+def wderive_plan(roots: np.ndarray, leaf: np.ndarray, row_ptr: np.ndarray, col: np.ndarray):
+    """Split a rank's roots into (cover roots run by the per-root kernel, leaf
+    roots derived): the cover set is the roots not in `leaf` plus every
+    neighbour of a derived leaf root (their rows feed the derivation), sorted
+    and unique; the leaf roots keep their order."""
+    roots = np.asarray(roots, np.uint32)
+    lr = roots[leaf[roots]]
+    cover = np.union1d(roots[~leaf[roots]], closure(lr, row_ptr, col))
+    cover = cover[~leaf[cover]] if lr.size else cover
+    return cover.astype(np.uint32), lr

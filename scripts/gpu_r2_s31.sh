@@ -1,0 +1,9 @@
+set -o pipefail
+T=${TAG:-r2s31}
+O=gpurun_out/$T
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_wderive.py tests/test_gpu_multirank.py > $O/pytest.log 2>&1 || { echo PYTEST_FAIL; tail -60 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+timeout -k 10 600 python -u bench.py --topology fabric100k-w --steps 5 --warmup 1 > $O/bench_w.json 2> $O/bench_w.err || { echo BENCH_FAIL; tail -30 $O/bench_w.err; exit 1; }
+python -c "import json;d=json.load(open('$O/bench_w.json'));print(d['value'],d['ms_per_step'],[(u['launch'],u['isolated_launch_ms'],u['frac']) for u in d['roofline']['launches']], d['parity_vs_cpu_sample'], d['cpu_baseline']['value'])"

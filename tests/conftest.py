@@ -21,9 +21,7 @@ def pytest_configure(config):
 MULTIRANK = {}
 
 
-def pytest_collection_finish(session):
-    if not any("test_gpu_multirank" in it.nodeid for it in session.items):
-        return
+def _launch_ranks(topology):
     import socket
     import subprocess
     import tempfile
@@ -37,6 +35,13 @@ def pytest_collection_finish(session):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
-           "--topology", "fabric10k", "--roots", "0", "--dist-parity", "96", "--iso-reps", "1"]
-    MULTIRANK.update(proc=subprocess.Popen(cmd, stdout=out, stderr=err, cwd=ROOT, env=env),
-                     out=out.name, err=err.name)
+           "--topology", topology, "--roots", "0", "--dist-parity", "96", "--iso-reps", "1"]
+    return dict(proc=subprocess.Popen(cmd, stdout=out, stderr=err, cwd=ROOT, env=env),
+                out=out.name, err=err.name)
+
+
+def pytest_collection_finish(session):
+    if not any("test_gpu_multirank" in it.nodeid for it in session.items):
+        return
+    # unit-metric derive mode and weighted derive mode, two ranks each
+    MULTIRANK.update(unit=_launch_ranks("fabric10k"), weighted=_launch_ranks("fabric10k-w"))

@@ -15,12 +15,14 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.timeout(600)
-def test_two_rank_bench_step_and_gather():
-    proc = MULTIRANK["proc"]
+@pytest.mark.parametrize("kind,mode", [("unit", "derive"), ("weighted", "wderive")])
+def test_two_rank_bench_step_and_gather(kind, mode):
+    run = MULTIRANK[kind]
+    proc = run["proc"]
     rc = proc.wait(timeout=540)
-    err = open(MULTIRANK["err"]).read()
+    err = open(run["err"]).read()
     assert rc == 0, err[-4000:]
-    lines = [json.loads(x) for x in open(MULTIRANK["out"]).read().splitlines()
+    lines = [json.loads(x) for x in open(run["out"]).read().splitlines()
              if x.startswith("{")]
     assert len(lines) == 1, lines  # rank 0 prints the one line
     ln = lines[0]
@@ -29,3 +31,4 @@ def test_two_rank_bench_step_and_gather():
     assert ln["parity_vs_cpu_sample"]["roots"] == 96
     assert ln["parity_vs_cpu_sample"]["equal"] is True
     assert ln["value"] > 0 and ln["config"]["roots_per_step"] == ln["config"]["n_nodes"]
+    assert ln["config"]["mode"] == mode
