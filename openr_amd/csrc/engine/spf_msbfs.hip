@@ -314,6 +314,31 @@ __device__ __forceinline__ void pull_scan(const DevGraph& g, const VB& b, const 
                                           uint64_t* pacc) {
   const uint4* q = reinterpret_cast<const uint4*>(g.colx);
   const uint4* fr = reinterpret_cast<const uint4*>(fcur);
+  if constexpr (KP <= 0) {
+    // distances only: four row quads (16 entries) per step, every load of a
+    // step issued before any is used (a fabric switch's 84-entry row is six
+    // dependent trips instead of 21); stop once every unseen root is found
+    for (; beg + 3u * STEP < end; beg += 4u * STEP) {
+      uint4 c[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) c[j] = q[(beg + j * STEP) >> 2];
+      uint64_t f[16];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t cs[4] = {c[j].x, c[j].y, c[j].z, c[j].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) f[4 * j + i] = (cs[i] & kDown) ? 0ull : fcur[cs[i]];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint64_t keep[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+        if (KP == 0) b.keep4(beg + j * STEP, keep);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc |= f[4 * j + i] & m & keep[i];
+      }
+      if (acc == m) return;
+    }
+  }
   for (uint32_t e = beg; e < end; e += STEP) {
     const uint4 c = q[e >> 2];
     const uint32_t cs[4] = {c.x, c.y, c.z, c.w};

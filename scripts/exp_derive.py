@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--pods", type=int, default=1781)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--check", type=int, default=64)
+    ap.add_argument("--no-digest", action="store_true", help="diagnostic: no digests")
+    ap.add_argument("--no-dist", action="store_true", help="diagnostic: no u32 dist rows")
     args = ap.parse_args()
     st = T.fabric(pods=args.pods, planes=8)
     ls = LinkState(stream=st)
@@ -55,16 +57,19 @@ def main():
     for rep in range(args.reps + 1):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
-        eng.levels_dev(d_order.data_ptr(), V, lev.data_ptr(), d_dist=dist.data_ptr(),
-                       d_lev_digest=ldg.data_ptr(), stream=s.cuda_stream)
+        eng.levels_dev(d_order.data_ptr(), V, lev.data_ptr(),
+                       d_dist=0 if args.no_dist else dist.data_ptr(),
+                       d_lev_digest=0 if args.no_digest else ldg.data_ptr(), stream=s.cuda_stream)
         e1.record(s)
         evs = []
         for b in bufs:
             a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a_.record(s)
             eng.nh_derive_dev(b["d"].data_ptr(), b["c"].roots.size, b["c"].nh_words, lev.data_ptr(),
-                              d_pos.data_ptr(), b["nh"].data_ptr(), d_lev_digest=ldg.data_ptr(),
-                              d_digest=b["dg"].data_ptr(), max_root_neighbors=b["c"].cap,
+                              d_pos.data_ptr(), b["nh"].data_ptr(),
+                              d_lev_digest=0 if args.no_digest else ldg.data_ptr(),
+                              d_digest=0 if args.no_digest else b["dg"].data_ptr(),
+                              max_root_neighbors=b["c"].cap,
                               stream=s.cuda_stream)
             b_.record(s)
             evs.append((b["c"].cap, a_, b_))

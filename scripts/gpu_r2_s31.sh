@@ -7,3 +7,5 @@ timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method threa
 tail -2 $O/pytest.log
 timeout -k 10 600 python -u bench.py --topology fabric100k-w --steps 5 --warmup 1 > $O/bench_w.json 2> $O/bench_w.err || { echo BENCH_FAIL; tail -30 $O/bench_w.err; exit 1; }
 python -c "import json;d=json.load(open('$O/bench_w.json'));print(d['value'],d['ms_per_step'],[(u['launch'],u['isolated_launch_ms'],u['frac']) for u in d['roofline']['launches']], d['parity_vs_cpu_sample'], d['cpu_baseline']['value'])"
+bash scripts/pmc_passes.sh $O/pmc python3 scripts/exp_derive.py --reps 1 --check 0 || { echo PMC_FAIL; exit 1; }
+python3 scripts/pmc_by_kernel.py $O/pmc/p1 $O/pmc/p2 $O/pmc/p3 > $O/pmc_by_kernel.json
