@@ -100,6 +100,15 @@ __host__ __device__ inline uint64_t digest_word_term(uint32_t v, uint32_t g, uin
   return word ? digest_node_key(v) * digest_word_key(g, word) : 0ull;
 }
 
+// 16-B store of a row that this launch never reads back (dist / next-hop
+// rows of finished runs): non-temporal, so the stream of output lines does not
+// evict the L2 lines the traversal or derivation re-reads.
+typedef uint32_t ospf_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store_row16(void* p, uint4 v) {
+  const ospf_u32x4 x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<ospf_u32x4*>(p));
+}
+
 // Dial kernels (spf_kernels.hip), any metric:
 //   variant 0 = LDS dist + LDS nh, 1 = LDS dist + HBM nh, 2 = HBM dist + HBM nh
 hipError_t launch_spf(int variant, bool unit, bool ign, const DevGraph& g, const RunArgs& a,

@@ -954,8 +954,9 @@ __global__ void __launch_bounds__(256) msbfs_levrows_kernel(DevGraph g, MsArgs a
       // level row: dist + 1, 0x7F for unreached and padding (bytes < 0x80)
       const uint32_t zm = ~((u | 0x80808080u) - 0x01010101u) & 0x80808080u;
       if (vq < a.lev_pitch)
-        *reinterpret_cast<uint32_t*>(a.levrow + (size_t)(b.rix0 + r) * a.lev_pitch + vq) =
-            u | (zm - (zm >> 7));
+        __builtin_nontemporal_store(
+            u | (zm - (zm >> 7)),
+            reinterpret_cast<uint32_t*>(a.levrow + (size_t)(b.rix0 + r) * a.lev_pitch + vq));
       uint32_t dv[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -969,7 +970,7 @@ __global__ void __launch_bounds__(256) msbfs_levrows_kernel(DevGraph g, MsArgs a
       if (a.dist) {
         uint32_t* row = a.dist + (size_t)(b.rix0 + r) * V + vq;
         if (vec) {
-          *reinterpret_cast<uint4*>(row) = make_uint4(dv[0], dv[1], dv[2], dv[3]);
+          store_row16(row, make_uint4(dv[0], dv[1], dv[2], dv[3]));
         } else {
 #pragma unroll
           for (int c = 0; c < 4; ++c)
@@ -1289,7 +1290,7 @@ __device__ __forceinline__ void derive_uniform_tiles(
       if (tn == 1024u && (((size_t)i * V + tv0) & 3u) == 0) {
 #pragma unroll
         for (int x = 0; x < 4; ++x)
-          reinterpret_cast<uint4*>(dst)[x * 64 + lane] = reinterpret_cast<const uint4*>(st)[x * 64 + lane];
+          store_row16(reinterpret_cast<uint4*>(dst) + x * 64 + lane, reinterpret_cast<const uint4*>(st)[x * 64 + lane]);
       } else {
         for (uint32_t x = lane; x < tn; x += 64u) dst[x] = st[x];
       }
@@ -1483,8 +1484,8 @@ __global__ void __launch_bounds__(256) nh_derive16_kernel(DevGraph g, DeriveArgs
     if (tn == 1024u && ((((size_t)i * V + tv0) * W) & 3u) == 0) {
 #pragma unroll
       for (int x = 0; x < 4 * W; ++x)
-        reinterpret_cast<uint4*>(dst)[x * 64 + lane] =
-            reinterpret_cast<const uint4*>(st)[x * 64 + lane];
+        store_row16(reinterpret_cast<uint4*>(dst) + x * 64 + lane,
+                    reinterpret_cast<const uint4*>(st)[x * 64 + lane]);
     } else {
       for (uint32_t x = lane; x < tn * W; x += 64u) dst[x] = st[x];
     }
@@ -1700,7 +1701,7 @@ __global__ void __launch_bounds__(256) nh_derive_wide_kernel(DevGraph g, DeriveA
 #pragma unroll
           for (int b = 0; b < 8; ++b) {
             const uint32_t ow = (word[b] | selfw[b]) & keep;
-            if (lane < W && vc + b < V) dst[(size_t)b * W] = ow;
+            if (lane < W && vc + b < V) __builtin_nontemporal_store(ow, dst + (size_t)b * W);
             if (d.digest && ow) h += kn[b] * digest_word_key(lane, ow);
           }
           if (h) atomicAdd(&s_h[j], (unsigned long long)h);

@@ -194,8 +194,8 @@ __global__ void __launch_bounds__(256) wderive_kernel(DevGraph g, WDeriveArgs a)
       uint32_t* drow = a.dist + i * V;
       uint32_t* nrow = a.nh ? a.nh + i * V : nullptr;
       if (vec && full) {
-        *reinterpret_cast<uint4*>(drow + v0) = make_uint4(m[0], m[1], m[2], m[3]);
-        if (nrow) *reinterpret_cast<uint4*>(nrow + v0) = make_uint4(bits[0], bits[1], bits[2], bits[3]);
+        store_row16(drow + v0, make_uint4(m[0], m[1], m[2], m[3]));
+        if (nrow) store_row16(nrow + v0, make_uint4(bits[0], bits[1], bits[2], bits[3]));
       } else {
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
