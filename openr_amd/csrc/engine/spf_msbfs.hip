@@ -1239,9 +1239,19 @@ __device__ __forceinline__ void derive_uniform_tiles(
     }
     uint32_t* st = s_stage + wave * 1024u;
     const uint32_t tv0 = t * 1024u, tn = min(1024u, V - tv0);
+    // The roots of a uniform group share their neighbour rows, so a root whose
+    // own level bytes over the wave's 1,024 nodes equal the previous root's
+    // has the same words there (the racks of a pod, everywhere outside their
+    // pod): the staged words and the wave's digest sum are reused and only the
+    // stores are issued again.
+    uint4 Lp = make_uint4(kInf, kInf, kInf, kInf);  // level bytes are < 0x80
+    uint64_t hw = 0;  // the previous root's wave digest sum of this tile
     for (uint32_t j = 0; j < ng; ++j) {
       uint4 L = make_uint4(0, 0, 0, 0);
       if (live) L = *reinterpret_cast<const uint4*>(d.lev + (size_t)s_own[j] * d.pitch + vl);
+      const bool same = L.x == Lp.x && L.y == Lp.y && L.z == Lp.z && L.w == Lp.w;
+      Lp = L;
+      if (__ballot(!same)) {  // some lane's levels differ: recompute the wave's words
       const uint32_t Lw[4] = {L.x, L.y, L.z, L.w};
       uint32_t lm1[4];  // as in nh_derive16_kernel: ((L - 1) | 0x80) per byte
 #pragma unroll
@@ -1280,11 +1290,26 @@ __device__ __forceinline__ void derive_uniform_tiles(
 #pragma unroll
         for (int b = 0; b < 4; ++b)
           word[4 * q + b] = ((A0[q] >> (8 * b)) & 0xFFu) | (((A1[q] >> (8 * b)) & 0xFFu) << 8);
+      __builtin_amdgcn_wave_barrier();  // the previous root's stores have read the slice
 #pragma unroll
       for (int x = 0; x < 4; ++x)
         reinterpret_cast<uint4*>(st + 16u * lane)[x] =
             make_uint4(word[4 * x], word[4 * x + 1], word[4 * x + 2], word[4 * x + 3]);
       __builtin_amdgcn_wave_barrier();
+      hw = 0;
+      if (d.digest) {
+        if (live) {
+#pragma unroll
+          for (int n = 0; n < 16; ++n) {
+            const uint32_t wd = word[n];
+            const uint64_t ws = small ? s_wk[wd & 0xFFu] : (wd ? digest_word_key(0, wd) : 0ull);
+            hw += kn[n] * ws;
+          }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) hw += shfl_xor64(hw, o);
+      }
+      }  // recomputed
       const size_t i = i0 + j;
       uint32_t* dst = d.nh + (size_t)i * V + tv0;
       if (tn == 1024u && (((size_t)i * V + tv0) & 3u) == 0) {
@@ -1294,21 +1319,7 @@ __device__ __forceinline__ void derive_uniform_tiles(
       } else {
         for (uint32_t x = lane; x < tn; x += 64u) dst[x] = st[x];
       }
-      __builtin_amdgcn_wave_barrier();
-      if (d.digest) {
-        uint64_t h = 0;
-        if (live) {
-#pragma unroll
-          for (int n = 0; n < 16; ++n) {
-            const uint32_t wd = word[n];
-            const uint64_t ws = small ? s_wk[wd & 0xFFu] : (wd ? digest_word_key(0, wd) : 0ull);
-            h += kn[n] * ws;
-          }
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) h += shfl_xor64(h, o);
-        if (lane == 0 && h) atomicAdd(&s_h[j], (unsigned long long)h);
-      }
+      if (lane == 0 && hw) atomicAdd(&s_h[j], (unsigned long long)hw);
     }
   }
 }
