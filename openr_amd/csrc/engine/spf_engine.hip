@@ -53,6 +53,9 @@ struct ospf_ctx {
   uint32_t* d_err = nullptr;
   // KSP2: traces run on an engine stream, overlapping later reruns
   hipStream_t aux = nullptr;
+  // derive phase 1: rows kernels of one round beside the next round's levels
+  hipStream_t lv_aux = nullptr;
+  hipEvent_t lv_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // traversed[2], rows done[2]
   std::vector<hipEvent_t> ev;  // [2 * slots]: rerun done / trace done per slot
 };
 
@@ -769,6 +772,9 @@ int ospf_close(ospf_ctx* c) {
   if (c->d_err) hipFree(c->d_err);
   for (hipEvent_t e : c->ev) hipEventDestroy(e);
   if (c->aux) hipStreamDestroy(c->aux);
+  for (hipEvent_t e : c->lv_ev)
+    if (e) hipEventDestroy(e);
+  if (c->lv_aux) hipStreamDestroy(c->lv_aux);
   delete c;
   return OSPF_OK;
 }
@@ -1186,6 +1192,80 @@ int ospf_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t f
     return fail(c, OSPF_E_RANGE, "level rows need a depth bound <= 123");
   hipStream_t s = (hipStream_t)stream;
   const uint32_t V = c->info.n_nodes, lmax = c->depth_bound + 2;
+  if (!getenv("OSPF_LV64")) {  // 128-root traversals (spf_levels.hip)
+    // per wide batch: frontier slots 2 x 16 B, seen 16 B, accb 16 B, records 128 B;
+    // two state buffers: the rows kernel of round k (on lv_aux) runs beside
+    // the traversal of round k + 1 (on the caller's stream): the traversal is
+    // latency-bound, the rows kernel store-bound
+    const size_t per_wb = align_up((size_t)V * 16ull * 4 + V * 128ull + lmax * 8ull, 256);
+    uint32_t nb_cap = 192;
+    if (const char* e = getenv("OSPF_LV_NB")) nb_cap = std::max(1, atoi(e));
+    const bool overlap = !getenv("OSPF_LV_SERIAL");
+    const size_t nbuf = overlap ? 2 : 1;
+    nb_cap = (uint32_t)std::max<size_t>(1, std::min<size_t>(nb_cap, (6ull << 30) / (per_wb * nbuf)));
+    const uint32_t total = (n + 127) / 128, nb_max = std::min(nb_cap, total);
+    int rc = OSPF_OK;
+    char* sp = stream_scratch(c, s, per_wb * nb_max * nbuf, &rc);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (overlap && !c->lv_aux) {
+      HIPCHK(c, hipStreamCreateWithFlags(&c->lv_aux, hipStreamNonBlocking));
+      for (hipEvent_t& e : c->lv_ev) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    ospf::LvArgs a{};
+    a.roots = d_roots;
+    a.n = n;
+    a.lmax = lmax;
+    a.dbound = c->depth_bound;
+    a.push_div = 16;
+    if (const char* e = getenv("OSPF_MS_PUSH_DIV")) a.push_div = (uint32_t)std::max(0, atoi(e));
+    a.masked = 0;
+    if (const char* e = getenv("OSPF_LV_MASKED")) a.masked = (uint32_t)atoi(e);
+    a.dist = d_dist;
+    a.levrow = d_lev;
+    a.lev_pitch = lev_pitch;
+    a.digest = d_lev_digest;
+    a.err = c->d_err;
+    if (d_lev_digest) HIPCHK(c, hipMemsetAsync(d_lev_digest, 0, (size_t)n * sizeof(ospf_digest), s));
+    uint32_t k = 0;
+    for (uint32_t vb0 = 0; vb0 < total; vb0 += nb_max, ++k) {
+      const uint32_t buf = overlap ? (k & 1u) : 0u;
+      char* base = sp + per_wb * nb_max * buf;
+      a.vb0 = vb0;
+      a.nb = std::min(nb_max, total - vb0);
+      a.front = (uint4*)base;
+      a.seen = a.front + 2ull * a.nb * V;
+      a.accb = a.seen + (size_t)a.nb * V;
+      a.lev = (uint8_t*)(a.accb + (size_t)a.nb * V);
+      a.found = (uint32_t*)(a.lev + (size_t)a.nb * V * 128ull);
+      a.mass = a.found + (size_t)a.nb * lmax;
+      // the buffer's previous rows kernel (round k - 2) must be done with it
+      if (overlap && k >= 2) HIPCHK(c, hipStreamWaitEvent(s, c->lv_ev[2 + buf], 0));
+      // zero frontier slot 1, seen, accb (contiguous) and found / mass; slot 0
+      // is written whole by every level before it is read; records are not
+      // cleared (set once per (node, root), read masked by seen)
+      HIPCHK(c, hipMemsetAsync(a.front + (size_t)a.nb * V, 0, (size_t)a.nb * V * 16ull * 3, s));
+      HIPCHK(c, hipMemsetAsync(a.found, 0, (size_t)a.nb * lmax * 8ull, s));
+      hipError_t e = ospf::launch_levels128_traverse(c->g, a, s);
+      if (e != hipSuccess) return hip_fail(c, e, "launch_levels128_traverse");
+      if (overlap) {
+        HIPCHK(c, hipEventRecord(c->lv_ev[buf], s));
+        HIPCHK(c, hipStreamWaitEvent(c->lv_aux, c->lv_ev[buf], 0));
+        e = ospf::launch_levels128_rows(c->g, a, c->lv_aux);
+        if (e != hipSuccess) return hip_fail(c, e, "launch_levels128_rows");
+        HIPCHK(c, hipEventRecord(c->lv_ev[2 + buf], c->lv_aux));
+      } else {
+        e = ospf::launch_levels128_rows(c->g, a, s);
+        if (e != hipSuccess) return hip_fail(c, e, "launch_levels128_rows");
+      }
+    }
+    if (overlap) {  // the caller's stream sees every rows kernel done
+      HIPCHK(c, hipEventRecord(c->lv_ev[2], c->lv_aux));
+      HIPCHK(c, hipStreamWaitEvent(s, c->lv_ev[2], 0));
+    }
+    c->spf_runs += n;
+    return OSPF_OK;
+  }
   // per batch: frontier slots 2 x 8 B, seen 8 B, accb 8 B, level records 64 B
   const size_t per_vb = align_up((size_t)V * 8ull * 4 + V * 64ull + lmax * 8ull, 256);
   uint32_t nb_cap = 96;

@@ -215,6 +215,35 @@ struct DeriveArgs {
   uint32_t ctiles;         // node tiles per block (0: default 8)
   uint32_t G, tiles, chunks;  // set by the launcher
 };
+// Derive phase 1 on 128-root traversals (spf_levels.hip): distance-only
+// multi-source BFS, 16-B root sets per node, then level / dist rows + the
+// distance part of each digest. Wide batch i of a round = roots
+// (vb0 + i) * 128 .. + 127 of the call.
+struct LvArgs {
+  const uint32_t* roots;
+  uint32_t n;
+  uint32_t vb0, nb;         // first wide batch of this round, wide batches in it
+  uint32_t lmax, dbound;    // stride of found / mass; levels launched 1 .. dbound
+  uint32_t push_div;        // level d pushes when frontier edge mass * push_div < E
+  uint32_t masked;          // pull scans in masked four-quad steps (else whole steps + quads)
+  uint4* front;             // [2][nb][V] frontier root sets of level d in slot d & 1
+  uint4* seen;              // [nb][V]
+  uint4* accb;              // [nb][V] push accumulator (zero between levels)
+  uint8_t* lev;             // [nb][V][128] dist + 1 per (node, root)
+  uint32_t* found;          // [nb][lmax]
+  uint32_t* mass;           // [nb][lmax]
+  uint32_t* dist;           // [n][V] or null
+  uint8_t* levrow;          // [n][lev_pitch]
+  uint32_t lev_pitch;
+  ospf_digest* digest;      // [n] distance parts (zeroed by the caller) or null
+  uint32_t* err;            // bit 8: depth bound too small, 64: bad root
+};
+// a round = init + levels (traverse), then the rows kernel; rounds of
+// different state buffers may overlap (rows of round k beside the levels of
+// round k + 1)
+hipError_t launch_levels128_traverse(const DevGraph& g, const LvArgs& a, hipStream_t s);
+hipError_t launch_levels128_rows(const DevGraph& g, const LvArgs& a, hipStream_t s);
+
 // Weighted derive (spf_wderive.hip): dist + next-hop rows (one word) of n
 // leaf roots from the distance rows of their neighbours (src + pos[v] *
 // src_pitch = row of node v, kInf: none).
