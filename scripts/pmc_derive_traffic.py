@@ -3,23 +3,26 @@
 summary (scripts/pmc_by_kernel.py over `exp_derive.py --reps 0`: one levels
 launch over all V roots and one derive launch per class), written into
 profiles/<round>/pmc_traffic.json under the keys bench.py reads:
-derive_levels (msbfs init / level / settle / levrows + the state memsets),
-derive_cap8 (nh_derive16_kernel<1>), derive_cap96 (nh_derive16_kernel<3>).
+derive_levels (lv_init / level / settle / rows, or the 64-root msbfs ones, + the
+state memsets), derive_cap8 (nh_derive16_kernel<1>), derive_cap96
+(nh_derive16_kernel<3>), derive_cap1792 (nh_derive_wide_kernel).
 hbm bytes = (2 x FETCH_SIZE + WRITE_SIZE) KiB (MI355X_MICROARCH.md: FETCH_SIZE
-x 2 on gfx950). Usage: pmc_derive_traffic.py PMC_JSON V N_CAP8 N_CAP96 OUT_JSON"""
+x 2 on gfx950). Usage: pmc_derive_traffic.py PMC_JSON V N_CAP8 N_CAP96 N_CAP1792 OUT_JSON"""
 import json
 import os
 import sys
 
 
 def main():
-    pmc, V, n8, n96, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), \
-        sys.argv[5]
+    pmc, V, n8, n96, nw, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), \
+        int(sys.argv[4]), int(sys.argv[5]), sys.argv[6]
     d = json.load(open(pmc))
     groups = {
-        "derive_levels": (V, [k for k in d if ("<-1>" in k or "levrows" in k or "fillBuffer" in k)]),
+        "derive_levels": (V, [k for k in d if ("<-1>" in k or "levrows" in k or "fillBuffer" in k
+                                              or k.startswith("lv_"))]),
         "derive_cap8": (n8, [k for k in d if k == "nh_derive16_kernel<1>"]),
         "derive_cap96": (n96, [k for k in d if k == "nh_derive16_kernel<3>"]),
+        "derive_cap1792": (nw, [k for k in d if k == "nh_derive_wide_kernel"]),
     }
     res = json.load(open(out)) if os.path.exists(out) else {}
     for key, (roots, ks) in groups.items():
