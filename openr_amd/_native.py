@@ -104,7 +104,8 @@ def _load(path: str) -> C.CDLL:
 def engine() -> C.CDLL:
     global _engine
     if _engine is None:
-        L = _load(ENGINE_SO)
+        # OPENR_SPF_ENGINE_SO: another build of the same ABI (A/B experiments)
+        L = _load(os.environ.get("OPENR_SPF_ENGINE_SO") or ENGINE_SO)
         L.ospf_open.argtypes = [i32, C.POINTER(vp)]
         L.ospf_close.argtypes = [vp]
         L.ospf_last_error.argtypes = [vp]

@@ -1,0 +1,10 @@
+set -o pipefail
+T=${TAG:-r2s41}
+O=gpurun_out/$T
+mkdir -p $O
+export TMPDIR=/tmp
+ALT=$PWD/openr_amd/lib/alt/libopenr_spf_hip.so
+for env in "OPENR_SPF_ENGINE_SO=$ALT" "OSPF_LVX=0" "OPENR_SPF_ENGINE_SO=$ALT" "OSPF_LVX=0"; do
+  env $env timeout -k 10 300 python3 scripts/exp_derive.py --reps 3 --check 0 > $O/exp.json 2> $O/exp.err || { echo EXP_FAIL; tail -5 $O/exp.err; exit 1; }
+  python3 -c "import json;d=json.load(open('$O/exp.json'));print('${env##*/}', [round(x,2) for x in d['phase1_ms']], {k:round(v,2) for k,v in d['median_phase2_ms'].items()})"
+done
