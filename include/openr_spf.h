@@ -215,6 +215,36 @@ int ospf_wderive_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n, uint32_
                      const uint32_t* d_pos, uint32_t* d_dist, uint32_t* d_nh,
                      ospf_digest* d_digest, void* stream);
 
+/* Distance rows of cover roots on weighted graphs (the cover = the nodes
+ * outside an independent set of leaves, e.g. the fabric and spine switches
+ * when the racks are the leaves). ospf_cover_prepare builds the contracted
+ * graph from the loaded graph: leaf_mask[V] (host) = 1 for leaves, no two of
+ * them adjacent; cover nodes <= 32768, leaf in-link metrics <= 65535 (else
+ * OSPF_E_RANGE). Shortest paths between cover nodes cross leaves only as
+ * single-node detours through transit leaves, so the cover's distances are
+ * those of the cover plus one shortcut edge per transit leaf detour, and a
+ * leaf's distance is the minimum over its up in-links (LinkState.cpp:836-911
+ * with metrics >= 1). ospf_cover_dist_dev writes d_dist [n][V] (link metrics;
+ * no ignored links) for n cover roots (node ids; a leaf root raises error bit
+ * 64). The prepared graph is tied to the graph version: prepare again after
+ * ospf_load_graph / ospf_update_*. Next hops then come from ospf_wderive_dev
+ * (leaves) and ospf_wderive_wide_dev (cover roots). */
+int ospf_cover_prepare(ospf_ctx* ctx, const uint8_t* leaf_mask);
+int ospf_cover_dist_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n, uint32_t* d_dist,
+                        void* stream);
+
+/* Next hops of roots with up to 128 distinct neighbours (nh_words 1..4), any
+ * metric: every row -- the roots' own and their transit neighbours' -- is in
+ * d_src at d_pos[] (computed with the same flags: ospf_cover_dist_dev for the
+ * cover, ospf_wderive_dev for the leaves); bit k of v is set iff w_k + D_k(v)
+ * == D_root(v) with n_k transit, or v == n_k and w_k == D_root(v) (the first
+ * hops of the shortest paths, LinkState.cpp:885-901). Writes d_nh
+ * [n][V][nh_words] and the complete digests (dist part from the own row). */
+int ospf_wderive_wide_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n, uint32_t flags,
+                          uint32_t nh_words, const uint32_t* d_src, uint64_t src_pitch,
+                          const uint32_t* d_pos, uint32_t* d_nh, ospf_digest* d_digest,
+                          void* stream);
+
 /* Kernel variant the engine would use for a large batch (for reporting):
  * 0 = Dial, LDS-resident (dist+nh in LDS), 1 = Dial, LDS dist + HBM
  * next-hops, 2 = Dial, HBM state, 3 = per-root BFS with LDS bitmaps and LDS

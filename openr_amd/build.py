@@ -14,7 +14,7 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 LIB = os.path.join(PKG, "lib")
-ENGINE_SRC = [os.path.join(PKG, "csrc", "engine", f) for f in ("spf_kernels.hip", "spf_bfs.hip", "spf_msbfs.hip", "spf_ksp2.hip", "spf_dial.hip", "spf_wdial.hip", "spf_wderive.hip", "spf_levels.hip", "spf_update.hip",
+ENGINE_SRC = [os.path.join(PKG, "csrc", "engine", f) for f in ("spf_kernels.hip", "spf_bfs.hip", "spf_msbfs.hip", "spf_ksp2.hip", "spf_dial.hip", "spf_wdial.hip", "spf_wderive.hip", "spf_levels.hip", "spf_cover.hip", "spf_update.hip",
                                                                  "spf_engine.hip")]
 DECISION_SRC = [os.path.join(PKG, "csrc", "decision", f)
                 for f in ("link_state.cpp", "spf_solver.cpp", "decision_capi.cpp")]

@@ -1,0 +1,188 @@
+// spf_cover.hip — distance rows of cover roots by a contracted-graph SPF with
+// LDS-resident distances (gfx950), any metric.
+//
+// Weighted all-sources sweeps split the nodes into an independent set of leaf
+// roots (no two adjacent; the racks of a fabric) and the cover (the rest).
+// Every shortest path between cover nodes visits leaves only as single-node
+// detours a -> x -> b (a leaf's neighbours are all cover nodes), and only
+// through transit leaves (overloaded nodes never relay, LinkState.cpp:
+// 859-866). So the cover's distances are those of the contracted graph C:
+// nodes = the cover, edges = the up links between cover nodes plus one
+// shortcut a -> b per transit leaf x with up links a - x - b, weight w(a -> x)
+// + w(x -> b), parallel ones collapsed to their minimum. A leaf's distance is
+// then min over its up in-links a -> x of D(a) + w(a -> x), a transit or the
+// root (Bellman's equation on the last hop) -- the reference's runSpf
+// distances (LinkState.cpp:836-911) with metrics >= 1.
+//
+// Kernel: a workgroup per root (persistent), the root's distances over the
+// cover in LDS (F100k: 14,536 cover nodes = 58 KB, two roots per CU). Dial
+// rounds by distance value t: every wave scans its share of the cover for
+// nodes at t (settled: metrics >= 1 never lower a value to t), queues the
+// transit ones (and the root), and expands the queue flat -- one trip for the
+// row bounds of up to 64 queued nodes, one for their edges -- with LDS
+// atomicMin relaxations; the next t is the minimum of the scan's unsettled
+// values and of this round's new values. The row is then written in node
+// order: cover nodes from LDS, leaves by the last-hop minimum over their
+// (padded, 16-B) in-link lists. Next hops are derived afterwards from the
+// neighbours' rows (ospf_wderive_dev).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "spf_kernels.h"
+
+namespace ospf {
+namespace {
+
+constexpr uint32_t kInf = 0xFFFFFFFFu;
+constexpr uint32_t kLeaf = 0x80000000u;
+constexpr int kWave = 64;
+constexpr uint32_t kBlock = 256;
+constexpr uint32_t kWaves = kBlock / kWave;
+constexpr uint32_t kQ = 256;  // per-wave frontier queue
+
+__device__ __forceinline__ uint32_t wave_min32(uint32_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o, kWave));
+  return x;
+}
+
+// expand queued nodes q[0 .. cnt) (this wave's) at distance t: 64 nodes per
+// pass, their edges flattened over the lanes
+__device__ __forceinline__ void expand(const CoverGraph& C, uint32_t* s_D, uint32_t* s_next,
+                                       const uint32_t* q, uint32_t cnt, uint32_t* s_pre,
+                                       uint32_t t, uint32_t lane) {
+  for (uint32_t b0 = 0; b0 < cnt; b0 += kWave) {
+    const uint32_t j = b0 + lane;
+    uint32_t beg = 0, deg = 0;
+    if (j < cnt) {
+      const uint32_t u = q[j];
+      beg = C.crow[u];
+      deg = C.crow[u + 1] - beg;
+    }
+    uint32_t inc = deg;  // inclusive prefix over the lanes
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)inc, o, kWave);
+      if (lane >= (uint32_t)o) inc += y;
+    }
+    s_pre[lane] = inc;
+    s_pre[kWave + lane] = beg;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t total = (uint32_t)__shfl((int)inc, kWave - 1, kWave);
+    for (uint32_t f = lane; f < total; f += kWave) {
+      uint32_t lo = 0, hi = kWave - 1;  // first k with pre[k] > f
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_pre[mid] > f) hi = mid;
+        else lo = mid + 1;
+      }
+      const uint32_t before = lo ? s_pre[lo - 1] : 0u;
+      const uint2 ed = C.cedge[s_pre[kWave + lo] + (f - before)];
+      const uint32_t nd = t + ed.y;
+      const uint32_t old = atomicMin(&s_D[ed.x], nd);
+      if (nd < old) atomicMin(s_next, nd);
+    }
+    __builtin_amdgcn_wave_barrier();  // s_pre is rewritten by the next pass
+  }
+}
+
+__global__ void __launch_bounds__(256) cover_spf_kernel(DevGraph g, CoverGraph C, CoverArgs a) {
+  extern __shared__ uint32_t s_D[];  // [nS] distances, then [ctr words] transit bits
+  __shared__ uint32_t s_q[kWaves][kQ];
+  __shared__ uint32_t s_pre[kWaves][2 * kWave];
+  __shared__ uint32_t s_next[2];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t nS = C.nS, V = g.V;
+  uint32_t* s_tr = s_D + nS;
+  for (uint32_t x = tid; x < (nS + 31u) / 32u; x += kBlock) s_tr[x] = C.ctr[x];
+  for (uint32_t i = blockIdx.x; i < a.n; i += gridDim.x) {
+    const uint32_t rn = a.roots[i];
+    const uint32_t r = rn < V ? C.cix[rn] : kInf;
+    if (r >= nS) {  // not a cover node (or a bad id): its row is left alone
+      if (tid == 0) atomicOr(a.err, 64u);
+      continue;
+    }
+    for (uint32_t x = tid; x < nS; x += kBlock) s_D[x] = x == r ? 0u : kInf;
+    if (tid == 0) s_next[0] = s_next[1] = kInf;
+    __syncthreads();
+    uint32_t t = 0, par = 0;
+    while (true) {
+      uint32_t* q = s_q[wave];
+      uint32_t cnt = 0, m2 = kInf;
+      for (uint32_t x0 = wave * kWave; x0 < nS; x0 += kBlock) {
+        const uint32_t x = x0 + lane;
+        const uint32_t d = x < nS ? s_D[x] : kInf;
+        if (d > t && d != kInf) m2 = min(m2, d);
+        const bool tr = x < nS && ((s_tr[x >> 5] >> (x & 31u)) & 1u);
+        const bool fr = d == t && (tr || x == r);
+        const uint64_t bal = __ballot(fr);
+        if (fr) q[cnt + __popcll(bal & ((1ull << lane) - 1ull))] = x;
+        cnt += (uint32_t)__popcll(bal);
+        if (cnt > kQ - kWave) {
+          __builtin_amdgcn_wave_barrier();
+          expand(C, s_D, &s_next[par], q, cnt, s_pre[wave], t, lane);
+          cnt = 0;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (cnt) expand(C, s_D, &s_next[par], q, cnt, s_pre[wave], t, lane);
+      m2 = wave_min32(m2);
+      if (lane == 0 && m2 != kInf) atomicMin(&s_next[par], m2);
+      __syncthreads();
+      t = s_next[par];
+      if (tid == 0) s_next[par ^ 1u] = kInf;  // the next round's slot
+      par ^= 1u;
+      if (t == kInf) break;  // every reachable cover node settled
+      __syncthreads();       // the slot reset is visible before its use
+    }
+    // the row in node order: cover nodes from LDS, leaves by their last hop
+    uint32_t* row = a.dist + (size_t)i * V;
+    for (uint32_t v = tid; v < V; v += kBlock) {
+      const uint32_t c = C.cix[v];
+      uint32_t out;
+      if (!(c & kLeaf)) {
+        out = s_D[c];
+      } else {
+        out = kInf;
+        const uint32_t l = c & ~kLeaf;
+        const uint4* la = reinterpret_cast<const uint4*>(C.ladj + C.lrow[l]);
+        const uint32_t nq = (C.lrow[l + 1] - C.lrow[l]) >> 2;
+        for (uint32_t k = 0; k < nq; ++k) {
+          const uint4 e4 = la[k];
+          const uint32_t es[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const uint32_t ci = es[b] & 0xFFFFu;
+            if (ci >= nS) continue;  // padding
+            if (!((s_tr[ci >> 5] >> (ci & 31u)) & 1u) && ci != r) continue;
+            const uint32_t d = s_D[ci];
+            if (d != kInf) out = min(out, d + (es[b] >> 16));
+          }
+        }
+      }
+      __builtin_nontemporal_store(out, row + v);
+    }
+    __syncthreads();  // s_D is reused by the next root
+  }
+}
+
+}  // namespace
+
+hipError_t launch_cover_spf(const DevGraph& g, const CoverGraph& C, const CoverArgs& a,
+                            uint32_t n_cu, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
+  const size_t lds = ((size_t)C.nS + (C.nS + 31u) / 32u) * 4u;
+  const uint32_t per_cu = std::max<uint32_t>(1, (uint32_t)((150u * 1024u) / (lds + 10u * 1024u)));
+  const uint32_t grid = std::min<uint32_t>(a.n, n_cu * std::min<uint32_t>(per_cu, 4u));
+  if (lds > 48 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)cover_spf_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(cover_spf_kernel, dim3(grid), dim3(kBlock), lds, s, g, C, a);
+  return hipGetLastError();
+}
+
+}  // namespace ospf

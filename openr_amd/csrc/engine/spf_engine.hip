@@ -56,6 +56,11 @@ struct ospf_ctx {
   // derive phase 1: rows kernels of one round beside the next round's levels
   hipStream_t lv_aux = nullptr;
   hipEvent_t lv_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // traversed[2], rows done[2]
+  // contracted cover graph (ospf_cover_prepare), valid for graph version cover_ver
+  void* d_cover = nullptr;
+  ospf::CoverGraph cover{};
+  uint64_t cover_ver = ~0ull;
+  bool cover_ok = false;
   std::vector<hipEvent_t> ev;  // [2 * slots]: rerun done / trace done per slot
 };
 
@@ -774,6 +779,7 @@ int ospf_close(ospf_ctx* c) {
   if (c->aux) hipStreamDestroy(c->aux);
   for (hipEvent_t e : c->lv_ev)
     if (e) hipEventDestroy(e);
+  if (c->d_cover) hipFree(c->d_cover);
   if (c->lv_aux) hipStreamDestroy(c->lv_aux);
   delete c;
   return OSPF_OK;
@@ -980,6 +986,7 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   c->info.max_metric = max_metric;
   c->info.unit_metric = unit ? 1u : 0u;
   c->info.version = version;
+  c->cover_ok = false;  // the contracted cover graph describes the old graph
   c->info.device_bytes = tot;
   c->dist_bound = dist_bound;
   c->loaded = true;
@@ -1402,6 +1409,167 @@ int ospf_wderive_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t 
   return OSPF_OK;
 }
 
+// Next hops of roots with up to 128 distinct neighbours (W <= 4 words) from
+// their neighbours' dist rows and their own (spf_wderive.hip), any metric.
+int ospf_wderive_wide_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t flags,
+                          uint32_t nh_words, const uint32_t* d_src, uint64_t src_pitch,
+                          const uint32_t* d_pos, uint32_t* d_nh, ospf_digest* d_digest,
+                          void* stream) {
+  if (!c) return OSPF_E_INVAL;
+  if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  if (n == 0) return OSPF_OK;
+  if (!d_roots || !d_src || !d_pos || !d_nh) return fail(c, OSPF_E_INVAL, "null argument");
+  const uint32_t V = c->info.n_nodes;
+  if (src_pitch < V) return fail(c, OSPF_E_INVAL, "wderive: src_pitch >= V");
+  if (nh_words == 0 || nh_words > 4)
+    return fail(c, OSPF_E_RANGE, "wderive_wide: 1 .. 4 next-hop words (<= 128 neighbours)");
+  if (!(flags & OSPF_HOP_COUNT) && c->dist_bound >= 0xFFFFFFFFull)
+    return fail(c, OSPF_E_RANGE, "distances may reach 2^32 - 1");
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (d_digest) HIPCHK(c, hipMemsetAsync(d_digest, 0, (size_t)n * sizeof(ospf_digest), s));
+  ospf::WDeriveArgs a{};
+  a.roots = d_roots;
+  a.n = n;
+  a.hop = (flags & OSPF_HOP_COUNT) ? 1u : 0u;
+  a.src = d_src;
+  a.src_pitch = src_pitch;
+  a.pos = d_pos;
+  a.nh = d_nh;
+  a.digest = d_digest;
+  a.err = c->d_err;
+  const uintptr_t al = (uintptr_t)d_src | (uintptr_t)d_nh;
+  a.vec = (V % 4u == 0 && src_pitch % 4u == 0 && (al & 15u) == 0) ? 1u : 0u;
+  if (const char* e = getenv("OSPF_WD_CTILES")) a.ctiles = (uint32_t)std::max(1, atoi(e));
+  hipError_t e = ospf::launch_wderive_wide(c->g, a, nh_words, s);
+  if (e != hipSuccess) return hip_fail(c, e, "launch_wderive_wide");
+  return OSPF_OK;
+}
+
+// ---------------------------------------------------------------- cover SPF
+// Contracted graph for ospf_cover_dist_dev (spf_cover.hip), built on the host
+// from the current (patched) shadows: cover = nodes with leaf_mask 0, each
+// leaf's neighbours must all be cover nodes.
+int ospf_cover_prepare(ospf_ctx* c, const uint8_t* leaf) {
+  if (!c || !leaf) return OSPF_E_INVAL;
+  if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  c->cover_ok = false;
+  const uint32_t V = c->info.n_nodes;
+  const auto& prow = c->h_prow;
+  const auto& pcolx = c->h_pcolx;
+  auto transit = [&](uint32_t u) { return !((c->h_nt[u >> 5] >> (u & 31)) & 1u); };
+  std::vector<uint32_t> cix(V), cv;
+  uint32_t nL = 0;
+  for (uint32_t v = 0; v < V; ++v) {
+    if (leaf[v]) {
+      cix[v] = 0x80000000u | nL++;
+    } else {
+      cix[v] = (uint32_t)cv.size();
+      cv.push_back(v);
+    }
+  }
+  const uint32_t nS = (uint32_t)cv.size();
+  if (nS == 0 || nS > ospf::kCoverMaxS)
+    return fail(c, OSPF_E_RANGE, "cover: 1 .. 32768 cover nodes (LDS-resident distances)");
+  std::vector<uint32_t> crow(nS + 1, 0), ctr((nS + 31) / 32, 0);
+  std::vector<uint2> cedge;
+  std::vector<std::pair<uint32_t, uint32_t>> cand;
+  for (uint32_t i = 0; i < nS; ++i) {
+    const uint32_t a = cv[i];
+    if (transit(a)) ctr[i >> 5] |= 1u << (i & 31);
+    cand.clear();
+    for (uint32_t e = prow[a]; e < prow[a + 1]; ++e) {
+      const uint32_t b = pcolx[e];
+      if ((b & 0x80000000u) || b == a) continue;  // down / padding / self
+      const uint64_t w = c->h_pw[e];
+      if (!(cix[b] & 0x80000000u)) {
+        cand.push_back({cix[b], (uint32_t)w});
+        continue;
+      }
+      if (!transit(b)) continue;  // an overloaded leaf relays nothing
+      for (uint32_t e2 = prow[b]; e2 < prow[b + 1]; ++e2) {
+        const uint32_t x = pcolx[e2];
+        if ((x & 0x80000000u) || x == b || x == a) continue;
+        if (cix[x] & 0x80000000u) return fail(c, OSPF_E_INVAL, "cover: two adjacent leaves");
+        const uint64_t ws = w + c->h_pw[e2];
+        if (ws >= 0xFFFFFFFFull) return fail(c, OSPF_E_RANGE, "cover: shortcut weight overflow");
+        cand.push_back({cix[x], (uint32_t)ws});
+      }
+    }
+    std::sort(cand.begin(), cand.end());
+    for (size_t k = 0; k < cand.size(); ++k)
+      if (k == 0 || cand[k].first != cand[k - 1].first)
+        cedge.push_back(make_uint2(cand[k].first, cand[k].second));
+    crow[i + 1] = (uint32_t)cedge.size();
+  }
+  std::vector<uint32_t> lrow(nL + 1, 0), ladj;
+  for (uint32_t v = 0, l = 0; v < V; ++v) {
+    if (!leaf[v]) continue;
+    for (uint32_t e = prow[v]; e < prow[v + 1]; ++e) {
+      const uint32_t a = pcolx[e];
+      if ((a & 0x80000000u) || a == v) continue;
+      if (cix[a] & 0x80000000u) return fail(c, OSPF_E_INVAL, "cover: two adjacent leaves");
+      if (c->h_prw[e] > 0xFFFFu) return fail(c, OSPF_E_RANGE, "cover: leaf in-link metric > 65535");
+      ladj.push_back(cix[a] | (c->h_prw[e] << 16));
+    }
+    while (ladj.size() % 4) ladj.push_back(0xFFFFu);
+    lrow[++l] = (uint32_t)ladj.size();
+  }
+  if (ladj.empty()) ladj.assign(4, 0xFFFFu);
+  if (cedge.empty()) cedge.push_back(make_uint2(0, 0));
+  // one allocation: cix | crow | ctr | lrow | ladj | cedge (16-B aligned parts)
+  const size_t o_cix = 0, o_crow = align_up(o_cix + V * 4ull, 16);
+  const size_t o_ctr = align_up(o_crow + crow.size() * 4ull, 16);
+  const size_t o_lrow = align_up(o_ctr + ctr.size() * 4ull, 16);
+  const size_t o_ladj = align_up(o_lrow + lrow.size() * 4ull, 16);
+  const size_t o_ced = align_up(o_ladj + ladj.size() * 4ull, 16);
+  const size_t bytes = o_ced + cedge.size() * 8ull;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (c->d_cover) HIPCHK(c, hipFree(c->d_cover));
+  c->d_cover = nullptr;
+  HIPCHK(c, hipMalloc(&c->d_cover, bytes));
+  char* base = (char*)c->d_cover;
+  HIPCHK(c, hipMemcpy(base + o_cix, cix.data(), V * 4ull, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(base + o_crow, crow.data(), crow.size() * 4ull, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(base + o_ctr, ctr.data(), ctr.size() * 4ull, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(base + o_lrow, lrow.data(), lrow.size() * 4ull, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(base + o_ladj, ladj.data(), ladj.size() * 4ull, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(base + o_ced, cedge.data(), cedge.size() * 8ull, hipMemcpyHostToDevice));
+  ospf::CoverGraph& C = c->cover;
+  C.nS = nS;
+  C.nL = nL;
+  C.cix = (const uint32_t*)(base + o_cix);
+  C.crow = (const uint32_t*)(base + o_crow);
+  C.ctr = (const uint32_t*)(base + o_ctr);
+  C.lrow = (const uint32_t*)(base + o_lrow);
+  C.ladj = (const uint32_t*)(base + o_ladj);
+  C.cedge = (const uint2*)(base + o_ced);
+  c->cover_ver = c->info.version;
+  c->cover_ok = true;
+  return OSPF_OK;
+}
+
+int ospf_cover_dist_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t* d_dist,
+                        void* stream) {
+  if (!c) return OSPF_E_INVAL;
+  if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  if (!c->cover_ok || c->cover_ver != c->info.version)
+    return fail(c, OSPF_E_INVAL, "cover: ospf_cover_prepare the current graph first");
+  if (n == 0) return OSPF_OK;
+  if (!d_roots || !d_dist) return fail(c, OSPF_E_INVAL, "null argument");
+  if (c->dist_bound >= 0xFFFFFFFFull) return fail(c, OSPF_E_RANGE, "distances may reach 2^32 - 1");
+  HIPCHK(c, hipSetDevice(c->device));
+  ospf::CoverArgs a{};
+  a.roots = d_roots;
+  a.n = n;
+  a.dist = d_dist;
+  a.err = c->d_err;
+  hipError_t e = ospf::launch_cover_spf(c->g, c->cover, a, (uint32_t)c->n_cu, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(c, e, "launch_cover_spf");
+  c->spf_runs += n;
+  return OSPF_OK;
+}
+
 int ospf_sssp_batch(ospf_ctx* c, const uint32_t* roots, uint32_t n_roots, const ospf_ignore* ig,
                     uint32_t flags, uint32_t nh_words, uint32_t* dist_out, uint32_t* nh_out,
                     ospf_digest* digest_out) {
@@ -1672,6 +1840,7 @@ int ospf_update_links(ospf_ctx* c, const ospf_link_update* u, uint32_t n, uint64
   for (uint32_t i = 0; i < n; ++i)
     if (u[i].up) c->dist_bound += (uint64_t)u[i].metric_lo + u[i].metric_hi;
   c->info.version = version;
+  c->cover_ok = false;  // the contracted cover graph describes the old graph
   return OSPF_OK;
 }
 
@@ -1696,6 +1865,7 @@ int ospf_update_nodes(ospf_ctx* c, const uint32_t* nodes, const uint8_t* no_tran
                       hipMemcpyHostToDevice));
   refresh_graph_stats(c, 0, deeper);
   c->info.version = version;
+  c->cover_ok = false;  // the contracted cover graph describes the old graph
   return OSPF_OK;
 }
 

@@ -244,6 +244,28 @@ struct LvArgs {
 hipError_t launch_levels128_traverse(const DevGraph& g, const LvArgs& a, hipStream_t s);
 hipError_t launch_levels128_rows(const DevGraph& g, const LvArgs& a, hipStream_t s);
 
+// Contracted-graph SPF of cover roots (spf_cover.hip): distances over the
+// cover (the nodes outside an independent set of leaves) with shortcut edges
+// through transit leaves, then full dist rows (leaves by their last hop).
+constexpr uint32_t kCoverMaxS = 32768;  // cover nodes (LDS-resident distances)
+struct CoverGraph {
+  uint32_t nS, nL;
+  const uint32_t* cix;   // [V] cover index, or 0x80000000 | leaf index
+  const uint32_t* crow;  // [nS + 1]
+  const uint2* cedge;    // [crow[nS]] {target cover index, weight}
+  const uint32_t* ctr;   // [(nS + 31) / 32] transit bits
+  const uint32_t* lrow;  // [nL + 1] (multiples of 4)
+  const uint32_t* ladj;  // [lrow[nL]] cover index | metric (cover -> leaf) << 16; 0xFFFF pads
+};
+struct CoverArgs {
+  const uint32_t* roots;  // node ids (cover nodes)
+  uint32_t n;
+  uint32_t* dist;         // [n][V]
+  uint32_t* err;          // bit 64: a root outside the cover
+};
+hipError_t launch_cover_spf(const DevGraph& g, const CoverGraph& C, const CoverArgs& a,
+                            uint32_t n_cu, hipStream_t s);
+
 // Weighted derive (spf_wderive.hip): dist + next-hop rows (one word) of n
 // leaf roots from the distance rows of their neighbours (src + pos[v] *
 // src_pitch = row of node v, kInf: none).
@@ -265,6 +287,9 @@ struct WDeriveArgs {
   uint32_t tiles, chunks;   // set by the launcher
 };
 hipError_t launch_wderive(const DevGraph& g, WDeriveArgs a, uint32_t kmax, hipStream_t s);
+// cover roots (<= 128 distinct neighbours): next-hop words [n][V][W] (W <= 4)
+// + digests from the neighbours' rows and the root's own row (all in src)
+hipError_t launch_wderive_wide(const DevGraph& g, WDeriveArgs a, uint32_t W, hipStream_t s);
 // phase 1: distances only (kp -1) + msbfs_levrows; phase 2: nh_derive
 hipError_t launch_msbfs_levels(const DevGraph& g, const MsArgs& a, uint32_t depth_bound,
                                hipStream_t s);

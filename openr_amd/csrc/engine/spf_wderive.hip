@@ -242,6 +242,195 @@ __global__ void __launch_bounds__(256) wderive_kernel(DevGraph g, WDeriveArgs a)
   }
 }
 
+// Cover roots (up to 128 distinct neighbours, W <= 4 next-hop words): the
+// next hops from the neighbours' rows against the root's own row (every row,
+// the root's included, in src at pos[]): bit k of v iff w_k + D_k(v) ==
+// D_r(v) with n_k transit, or v == n_k and w_k == D_r(v). Block = up to
+// kWdWideG roots x a chunk of 256-node subtiles, lane = 4 nodes; the W words
+// of the lane's 4 nodes stay in registers and leave through a per-wave LDS
+// slice so each store instruction writes 1 KB of consecutive row. The digest
+// (dist part from the own row) is summed per (root, subtile).
+constexpr uint32_t kWdWideG = 16;
+constexpr uint32_t kWdWideK = 128;
+template <int W>
+__global__ void __launch_bounds__(256) wderive_wide_kernel(DevGraph g, WDeriveArgs a) {
+  __shared__ uint32_t s_root[kWdWideG], s_K[kWdWideG], s_own[kWdWideG];
+  __shared__ uint32_t s_w[kWdWideG * kWdWideK];
+  __shared__ uint32_t s_p[kWdWideG * kWdWideK];
+  __shared__ unsigned long long s_h[kWdWideG], s_sum[kWdWideG];
+  __shared__ uint32_t s_reach[kWdWideG];
+  __shared__ uint32_t s_st[kWaves][kSub * W];
+  const uint32_t V = g.V, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t G = a.G;
+  const uint32_t ngroups = (a.n + G - 1) / G;
+  const uint32_t ci = blockIdx.x / ngroups, gi = blockIdx.x % ngroups;
+  const uint32_t i0 = gi * G, ng = min(G, a.n - i0);
+  if (tid < ng) {
+    const uint32_t r = a.roots[i0 + tid];
+    s_root[tid] = r;
+    s_K[tid] = 0;
+    s_own[tid] = kInf;
+    s_h[tid] = 0ull;
+    s_sum[tid] = 0ull;
+    s_reach[tid] = 0u;
+    if (r >= V) {
+      atomicOr(a.err, 64u);
+    } else {
+      const uint32_t K = g.dn_off[r + 1] - g.dn_off[r];
+      if (K > kWdWideK || K > 32u * W) atomicOr(a.err, 1u);
+      s_K[tid] = min(K, min(kWdWideK, 32u * W));
+      s_own[tid] = a.pos[r];
+      if (s_own[tid] == kInf) atomicOr(a.err, 16u);
+    }
+  }
+  for (uint32_t x = tid; x < ng * kWdWideK; x += kBlock) s_w[x] = kInf;
+  __syncthreads();
+  for (uint32_t j = 0; j < ng; ++j) {
+    const uint32_t r = s_root[j];
+    if (r >= V) continue;
+    for (uint32_t e = g.row_ptr[r] + tid; e < g.row_ptr[r + 1]; e += kBlock) {
+      const uint32_t cx = g.colx[e];
+      if ((cx & kDown) || cx == r) continue;
+      const uint32_t k = g.didx[e];
+      if (k < s_K[j]) atomicMin(&s_w[j * kWdWideK + k], a.hop ? 1u : g.w[e]);
+    }
+  }
+  __syncthreads();
+  for (uint32_t x = tid; x < ng * kWdWideK; x += kBlock) {
+    const uint32_t j = x / kWdWideK, k = x - j * kWdWideK;
+    uint32_t p = kInf;
+    if (k < s_K[j] && s_w[x] != kInf) {
+      const uint32_t nb = g.dn[g.dn_off[s_root[j]] + k];
+      if (transit(g, nb)) {
+        p = a.pos[nb];
+        if (p == kInf) atomicOr(a.err, 16u);
+      } else {
+        p = kNt | nb;
+      }
+    }
+    s_p[x] = p;
+  }
+  __syncthreads();
+  const bool vec = a.vec != 0;
+  const uint32_t t0 = ci * a.ctiles, t1 = min(a.tiles, t0 + a.ctiles);
+  uint32_t* st = s_st[wave];
+  for (uint32_t pr = wave; pr < (t1 - t0) * ng; pr += kWaves) {
+    const uint32_t t = t0 + pr / ng, j = pr % ng;
+    const uint32_t r = s_root[j], own = s_own[j];
+    if (r >= V || own == kInf) continue;
+    const uint32_t v0 = t * kSub + 4u * lane;
+    const bool full = v0 + 4u <= V;
+    auto load4 = [&](uint32_t p, uint32_t* D) {
+      const uint32_t* row = a.src + (size_t)p * a.src_pitch;
+      if (vec && full) {
+        const uint4 x = *reinterpret_cast<const uint4*>(row + v0);
+        D[0] = x.x; D[1] = x.y; D[2] = x.z; D[3] = x.w;
+      } else {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) D[b] = v0 + b < V ? row[v0 + b] : kInf;
+      }
+    };
+    uint32_t R[4];
+    load4(own, R);
+    uint32_t word[W][4];
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) word[w][b] = 0u;
+    const uint32_t* sp = s_p + j * kWdWideK;
+    const uint32_t* sw = s_w + j * kWdWideK;
+    const uint32_t K = s_K[j];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      for (uint32_t k8 = 0; k8 < 32u; k8 += 8u) {
+        const uint32_t kb = 32u * w + k8;
+        if (kb >= K) break;  // uniform
+        uint32_t D[8][4], pk[8], wk[8];
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {  // 8 rows in flight
+          pk[kk] = kb + kk < K ? sp[kb + kk] : kInf;
+          wk[kk] = kb + kk < K ? sw[kb + kk] : kInf;
+          if (pk[kk] < kNt) load4(pk[kk], D[kk]);
+          else {
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+              D[kk][b] = (pk[kk] != kInf && v0 + b == (pk[kk] & ~kNt)) ? 0u : kInf;
+          }
+        }
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const uint32_t c = sat_add(wk[kk], D[kk][b]);
+            word[w][b] |= (c == R[b] && R[b] != kInf ? 1u : 0u) << (k8 + kk);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      if (v0 + b == r)
+#pragma unroll
+        for (int w = 0; w < W; ++w) word[w][b] = 0u;  // the root: no next hops
+    // stage [node][word] and store whole 1-KB pieces of the row
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int w = 0; w < W; ++w) st[(4u * lane + b) * W + w] = word[w][b];
+    __builtin_amdgcn_wave_barrier();
+    const size_t i = i0 + j;
+    uint32_t* dst = a.nh + ((size_t)i * V + t * kSub) * W;
+    const uint32_t tn = min(kSub, V - t * kSub);
+    if (vec && tn == kSub) {
+#pragma unroll
+      for (int x = 0; x < W; ++x)
+        store_row16(reinterpret_cast<uint4*>(dst) + x * 64 + lane,
+                    reinterpret_cast<const uint4*>(st)[x * 64 + lane]);
+    } else {
+      for (uint32_t x = lane; x < tn * W; x += 64u) dst[x] = st[x];
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (a.digest) {
+      uint64_t h = 0, sum = 0;
+      uint32_t reach = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const uint32_t v = v0 + b;
+        if (v < V && R[b] != kInf) {
+          reach += 1u;
+          sum += R[b];
+          h += g.dkey[2ull * v] * ((uint64_t)R[b] + 1ull);
+          uint64_t ws = 0;
+#pragma unroll
+          for (int w = 0; w < W; ++w)
+            if (word[w][b]) ws += digest_word_key(w, word[w][b]);
+          if (ws) h += g.dkey[2ull * v + 1] * ws;
+        }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        h += shfl_xor64(h, o);
+        sum += shfl_xor64(sum, o);
+        reach += __shfl_xor(reach, o, kWave);
+      }
+      if (lane == 0 && reach) {
+        atomicAdd(&s_h[j], (unsigned long long)h);
+        atomicAdd(&s_sum[j], (unsigned long long)sum);
+        atomicAdd(&s_reach[j], reach);
+      }
+    }
+  }
+  if (a.digest) {
+    __syncthreads();
+    if (tid < ng && s_reach[tid]) {
+      ospf_digest* dg = a.digest + i0 + tid;
+      atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)s_reach[tid]);
+      atomicAdd((unsigned long long*)&dg->sum_dist, s_sum[tid]);
+      atomicAdd((unsigned long long*)&dg->hash, s_h[tid]);
+    }
+  }
+}
+
 }  // namespace
 
 hipError_t launch_wderive(const DevGraph& g, WDeriveArgs a, uint32_t kmax, hipStream_t s) {
@@ -256,6 +445,24 @@ hipError_t launch_wderive(const DevGraph& g, WDeriveArgs a, uint32_t kmax, hipSt
   if (kmax <= 8) hipLaunchKernelGGL(wderive_kernel<8>, grid, dim3(kBlock), 0, s, g, a);
   else if (kmax <= 16) hipLaunchKernelGGL(wderive_kernel<16>, grid, dim3(kBlock), 0, s, g, a);
   else hipLaunchKernelGGL(wderive_kernel<32>, grid, dim3(kBlock), 0, s, g, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_wderive_wide(const DevGraph& g, WDeriveArgs a, uint32_t W, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
+  if (W == 0 || W > 4) return hipErrorInvalidValue;
+  a.tiles = (g.V + kSub - 1) / kSub;
+  if (a.ctiles == 0) a.ctiles = 16;
+  a.ctiles = std::min(a.ctiles, a.tiles);
+  a.chunks = (a.tiles + a.ctiles - 1) / a.ctiles;
+  if (a.G == 0 || a.G > kWdWideG) a.G = kWdWideG;
+  const dim3 grid(((a.n + a.G - 1) / a.G) * a.chunks);
+  switch (W) {
+    case 1: hipLaunchKernelGGL(wderive_wide_kernel<1>, grid, dim3(kBlock), 0, s, g, a); break;
+    case 2: hipLaunchKernelGGL(wderive_wide_kernel<2>, grid, dim3(kBlock), 0, s, g, a); break;
+    case 3: hipLaunchKernelGGL(wderive_wide_kernel<3>, grid, dim3(kBlock), 0, s, g, a); break;
+    default: hipLaunchKernelGGL(wderive_wide_kernel<4>, grid, dim3(kBlock), 0, s, g, a); break;
+  }
   return hipGetLastError();
 }
 

@@ -196,6 +196,26 @@ class Engine:
                                              d_pos, d_dist, d_nh or None, d_digest or None,
                                              stream or None))
 
+    def cover_prepare(self, leaf_mask) -> None:
+        """ospf_cover_prepare: contracted graph of the cover (nodes outside the
+        independent leaf set, leaf_mask[V] bool) for cover_dist_dev."""
+        m = np.ascontiguousarray(leaf_mask, np.uint8)
+        self._check(self._L.ospf_cover_prepare(self._h, m.ctypes.data))
+
+    def cover_dist_dev(self, d_roots: int, n: int, d_dist: int, stream: int = 0) -> None:
+        """ospf_cover_dist_dev: dist rows [n][V] of n cover roots (node ids)."""
+        self._check(self._L.ospf_cover_dist_dev(self._h, d_roots, n, d_dist, stream or None))
+
+    def wderive_wide_dev(self, d_roots: int, n: int, nh_words: int, d_src: int, d_pos: int,
+                         d_nh: int, *, src_pitch: int = 0, d_digest: int = 0,
+                         hop_count: bool = False, stream: int = 0) -> None:
+        """ospf_wderive_wide_dev: next-hop rows [n][V][nh_words] (<= 4 words)
+        + digests of n roots from their own and their neighbours' dist rows."""
+        self._check(self._L.ospf_wderive_wide_dev(self._h, d_roots, n,
+                                                  N.OSPF_HOP_COUNT if hop_count else 0, nh_words,
+                                                  d_src, src_pitch or self.V, d_pos, d_nh,
+                                                  d_digest or None, stream or None))
+
     def ksp2(self, src: int, dsts: Sequence[int], path_cap: int = 512):
         """getKthPaths(src, d, 1) and (src, d, 2) for every d (ospf_ksp2_run).
         Returns (k1, k2, status): per destination a list of paths (lists of

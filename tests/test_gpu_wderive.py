@@ -170,3 +170,132 @@ def test_wderive_missing_neighbour_row_is_an_error():
             eng.sync()
     finally:
         eng.close()
+
+
+# ---------------------------------------------------------------- cover SPF
+def cover_pipeline(eng, csr, check_nh=True):
+    """Cover dist rows by the contracted-graph SPF, leaf rows by wderive,
+    cover next hops by wderive_wide; returns {root: (dist, nh, digest)}."""
+    dev = torch.device("cuda", 0)
+    V = eng.V
+    rp, col = csr["row_ptr"], csr["col"]
+    leaf = shard.leaf_set(rp, col)
+    eng.cover_prepare(leaf)
+    cover = np.nonzero(~leaf)[0].astype(np.uint32)
+    lr = np.nonzero(leaf)[0].astype(np.uint32)
+    pos = np.empty(V, np.uint32)
+    pos[cover] = np.arange(cover.size, dtype=np.uint32)
+    pos[lr] = cover.size + np.arange(lr.size, dtype=np.uint32)
+    slab = torch.empty((V, V), dtype=torch.int32, device=dev)
+    d_pos = torch.from_numpy(pos.view(np.int32)).to(dev)
+    d_c = torch.from_numpy(cover.view(np.int32)).to(dev)
+    d_l = torch.from_numpy(lr.view(np.int32)).to(dev)
+    eng.cover_dist_dev(d_c.data_ptr(), cover.size, slab.data_ptr())
+    nbrs = shard.distinct_neighbors(rp, col)
+    out = {}
+    if lr.size:
+        lnh = torch.empty((lr.size, V), dtype=torch.int32, device=dev)
+        ldg = torch.empty((lr.size, 3), dtype=torch.int64, device=dev)
+        eng.wderive_dev(d_l.data_ptr(), lr.size, slab.data_ptr(), d_pos.data_ptr(),
+                        slab[cover.size].data_ptr(), d_nh=lnh.data_ptr(), d_digest=ldg.data_ptr(),
+                        max_root_neighbors=int(nbrs[lr].max()))
+        eng.sync()
+        ln, lg = lnh.cpu().numpy().view(np.uint32), ldg.cpu().numpy().view(np.uint64)
+        for j, r in enumerate(lr):
+            out[int(r)] = (None, ln[j].reshape(V, 1), lg[j])
+    if check_nh:
+        for W in (1, 2, 3, 4):
+            grp = cover[(np.maximum(1, (nbrs[cover] + 31) // 32) == W)]
+            if not grp.size:
+                continue
+            d_g = torch.from_numpy(grp.view(np.int32)).to(dev)
+            nh = torch.empty((grp.size, V, W), dtype=torch.int32, device=dev)
+            dg = torch.empty((grp.size, 3), dtype=torch.int64, device=dev)
+            eng.wderive_wide_dev(d_g.data_ptr(), grp.size, W, slab.data_ptr(), d_pos.data_ptr(),
+                                 nh.data_ptr(), d_digest=dg.data_ptr())
+            eng.sync()
+            n_h, g_h = nh.cpu().numpy().view(np.uint32), dg.cpu().numpy().view(np.uint64)
+            for j, r in enumerate(grp):
+                out[int(r)] = (None, n_h[j], g_h[j])
+    eng.sync()
+    dist = slab.cpu().numpy().view(np.uint32)
+    return {r: (dist[pos[r]], nh, dg) for r, (_, nh, dg) in out.items()}, cover, dist, pos
+
+
+def check_cover(stream):
+    ls = LinkState()
+    ls.apply(stream)
+    csr = ls.csr()
+    eng = Engine()
+    try:
+        eng.load(csr)
+        got, cover, dist, pos = cover_pipeline(eng, csr)
+        ref = eng.run(cover, max(eng.nh_words(int(r)) for r in cover), want_nh=False)
+        assert np.array_equal(dist[pos[cover]], ref["dist"])  # every cover row
+        for r, (d, nh, dg) in got.items():
+            W = nh.shape[1]
+            want = eng.run([r], W, want_digest=True)
+            assert np.array_equal(d, want["dist"][0]), r
+            assert np.array_equal(nh, want["nh"][0]), r
+            assert np.array_equal(dg, want["digest"][0]), r
+    finally:
+        eng.close()
+    return ls, got
+
+
+@pytest.mark.parametrize("seed", range(5))
+def test_cover_spf_random_weighted_graphs(seed):
+    """Contracted-graph SPF of the cover + derived leaves + cover next hops,
+    on graphs with overloads, down and parallel links, metrics up to 60,000."""
+    stream, _ = random_stream(600 + seed, n=90, p=0.05, wmax=60_000)
+    check_cover(stream)
+
+
+def test_cover_spf_ties():
+    stream, _ = random_stream(700, n=100, p=0.05, wmax=3, overload=0.2)
+    check_cover(stream)
+
+
+def test_cover_spf_weighted_fabric_with_drains_vs_oracle():
+    st = T.fabric(pods=12, planes=8, weighted_seed=11, max_metric=200)
+    dbs = st.to_dbs()
+    for d in dbs:
+        if d.name in ("2-3-1", "3-5-7", "3-6-1"):
+            d.overloaded = True
+        if d.name in ("3-4-2", "2-7-7"):
+            d.adjs[0].overloaded = True
+    st2 = AdjDbStream.from_dbs(dbs)
+    ls, got = check_cover(st2)
+    names = ls.node_names()
+    pick = ["2-3-1", "2-0-0", "3-5-7", "3-4-2", "2-7-7", "3-11-47"]
+    want = Oracle(st2).digests(pick)
+    for nm, w in zip(pick, want):
+        assert np.array_equal(got[names.index(nm)][2], w), nm
+
+
+def test_cover_graph_goes_stale_on_updates():
+    stream, _ = random_stream(710, n=40, p=0.1, wmax=50)
+    ls = LinkState()
+    ls.apply(stream)
+    csr = ls.csr()
+    eng = Engine()
+    try:
+        eng.load(csr)
+        leaf = shard.leaf_set(csr["row_ptr"], csr["col"])
+        eng.cover_prepare(leaf)
+        V = eng.V
+        dev = torch.device("cuda", 0)
+        r = int(np.nonzero(~leaf)[0][0])
+        d_r = torch.tensor([r], dtype=torch.int32, device=dev)
+        dist = torch.empty((1, V), dtype=torch.int32, device=dev)
+        eng.cover_dist_dev(d_r.data_ptr(), 1, dist.data_ptr())
+        eng.sync()
+        eng.update_nodes([r], [1], version=7)
+        with pytest.raises(EngineError):
+            eng.cover_dist_dev(d_r.data_ptr(), 1, dist.data_ptr())
+        bad = leaf.copy()
+        bad[:] = True  # adjacent leaves
+        with pytest.raises(EngineError):
+            eng.cover_prepare(bad)
+    finally:
+        eng.close()
