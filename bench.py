@@ -168,6 +168,9 @@ def main():
     ap.add_argument("--wide", choices=["derive", "batch"], default="derive",
                     help="derive mode: rows of > 4 next-hop words (spines) from level rows "
                          "(nh_derive_wide_kernel) or on the bit-plane batch path")
+    ap.add_argument("--wcover", choices=["spf", "batch"], default="spf",
+                    help="weighted all-sources: cover roots by the contracted-graph SPF "
+                         "(ospf_cover_dist_dev + ospf_wderive_wide_dev) or per-root batches")
     ap.add_argument("--dist-parity", type=int, default=0,
                     help="N>1: rank 0 checks the gathered digests of the last timed step "
                          "for this many roots against the CPU restatement")
@@ -217,6 +220,15 @@ def main():
     if args.mode == "derive" and not (derive_ok or wderive_ok):
         raise SystemExit("derive mode needs an all-sources sweep (strong scaling)")
     if args.mode != "batch" and wderive_ok:
+        if args.wcover == "spf":
+            leaf = shard.leaf_set(csr["row_ptr"], csr["col"])
+            try:
+                eng.cover_prepare(leaf)
+            except Exception as e:  # outside the cover kernel's limits: per-root cover runs
+                log(f"[rank {rank}] cover SPF unavailable ({e}); cover roots on the batch path")
+            else:
+                return wcover_main(args, eng, csr, names, stream, desc, V, E, world, rank,
+                                   dist_on, dev, backend, coll_dev, leaf)
         return wderive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, dev,
                             backend, coll_dev, weighted)
     pool = perm if n_roots <= 0 else perm[: min(n_roots, V)]
@@ -651,6 +663,274 @@ def derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
                             "isolated_launch_ms": round(c["iso_ms"], 3)})
     report(args, stream, names, perm, step_digest, dt, V * args.steps, E, desc, 0, V, world, rank,
            dist_on, backend, V, classes_cfg, roofline, "strong", "derive")
+    if dist_on:
+        torch.distributed.destroy_process_group()
+
+
+def wcover_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, dev, backend,
+                coll_dev, leaf):
+    """All-sources step on a weighted graph, cover SPF form. (A) dist rows of
+    the cover (nodes outside the independent leaf set: the fabric and spine
+    switches) by the contracted-graph SPF (spf_cover.hip); (B) the leaves'
+    dist + next-hop rows from those rows (ospf_wderive_dev); (C) the next hops
+    of cover roots with <= 128 neighbours from their own and their
+    neighbours' rows (ospf_wderive_wide_dev). Wider cover roots (spines) run
+    the per-root batch kernel on their own stream from the step's start. A
+    rank owns a pod / plane block (fabric) or class slices, and computes the
+    rows its own roots' derivations read."""
+    rp, col = csr["row_ptr"], csr["col"]
+    perm = np.random.default_rng(SEED).permutation(V).astype(np.uint32)
+    key = shard.first_neighbor(rp, col)
+    nbrs = shard.distinct_neighbors(rp, col)
+    caps = shard.neighbor_caps(nbrs)
+    words = np.maximum(1, (nbrs + 31) // 32)
+
+    def part(r):
+        if world == 1:
+            return perm
+        fp = shard.fabric_partition(names, world, r)
+        if fp is not None:
+            return fp
+        cls = shard.make_classes(perm, caps, V, key)
+        return np.concatenate([c.roots[slice(*shard.rank_slice(c.roots.size, world, r))]
+                               for c in cls])
+
+    def plan(p):
+        p = np.asarray(p, np.uint32)
+        own_l = shard.locality_order(p[leaf[p]], key)
+        own_c = p[~leaf[p]]
+        c_der = own_c[(nbrs[own_c] <= 128)]          # (C): next hops derived
+        c_wide = own_c[(nbrs[own_c] > 128)]          # per-root batch kernel
+        nb_c = shard.closure(c_der, rp, col)
+        need_l = np.union1d(own_l, nb_c[leaf[nb_c]]).astype(np.uint32)
+        need_l = shard.locality_order(need_l, key)
+        cl = shard.closure(need_l, rp, col)
+        cover_a = np.union1d(np.union1d(own_c, cl[~leaf[cl]]), nb_c[~leaf[nb_c]]).astype(np.uint32)
+        return dict(own_l=own_l, c_der=c_der, c_wide=c_wide, need_l=need_l, cover_a=cover_a)
+
+    parts = [part(r) for r in range(world)]
+    plans = [plan(p) for p in parts]
+    P = plans[rank]
+    cover_a, need_l = P["cover_a"], P["need_l"]
+    nA, nL = int(cover_a.size), int(need_l.size)
+    pos = np.full(V, 0xFFFFFFFF, np.uint32)
+    pos[cover_a] = np.arange(nA, dtype=np.uint32)
+    pos[need_l] = nA + np.arange(nL, dtype=np.uint32)
+    t0 = time.time()
+    slab = torch.empty((max(1, nA + nL), V), dtype=torch.int32, device=dev)
+    d_pos = torch.from_numpy(pos.view(np.int32)).to(dev)
+    d_a = torch.from_numpy(cover_a.view(np.int32)).to(dev)
+    d_l = torch.from_numpy(need_l.view(np.int32)).to(dev)
+    lnh = torch.empty((max(1, nL), V), dtype=torch.int32, device=dev)
+    ldg = torch.zeros((max(1, nL), 3), dtype=torch.int64, device=dev)
+    kmax = int(nbrs[need_l].max()) if nL else 0
+    flags = N.OSPF_WANT_DIST | N.OSPF_WANT_NH | N.OSPF_WANT_DIGEST
+    cls = []  # (C) classes by next-hop words, and the wide batch class
+    for W in sorted(set(words[P["c_der"]].tolist())):
+        roots = shard.locality_order(P["c_der"][words[P["c_der"]] == W], key)
+        cls.append(dict(kind="derive", W=W, roots=roots, n=int(roots.size),
+                        d=torch.from_numpy(roots.view(np.int32)).to(dev),
+                        nh=torch.empty((roots.size, V, W), dtype=torch.int32, device=dev),
+                        dig=torch.zeros((roots.size, 3), dtype=torch.int64, device=dev), ms=[]))
+    if P["c_wide"].size:
+        roots = shard.locality_order(P["c_wide"], key)
+        W = int(words[roots].max())
+        mx = int(nbrs[roots].max())
+        cls.append(dict(kind="batch", W=W, roots=roots, n=int(roots.size), max_nbrs=mx,
+                        plan=eng.plan(W, flags, n_roots=int(roots.size), max_root_neighbors=mx),
+                        d=torch.from_numpy(roots.view(np.int32)).to(dev),
+                        nh=torch.empty((roots.size, V, W), dtype=torch.int32, device=dev),
+                        dist=torch.empty((roots.size, V), dtype=torch.int32, device=dev),
+                        dig=torch.zeros((roots.size, 3), dtype=torch.int64, device=dev),
+                        stream=torch.cuda.Stream(device=dev), ms=[]))
+    log(f"[rank {rank}] wcover: {parts[rank].size} roots: cover SPF {nA}, leaves {nL} "
+        f"(<= {kmax} neighbours), cover next hops {[(c['kind'], c['W'], c['n']) for c in cls]}, "
+        f"buffers {(slab.numel() + lnh.numel() + sum(c['nh'].numel() for c in cls)) * 4 / 2**30:.1f}"
+        f" GiB in {time.time() - t0:.1f}s")
+    main_s = torch.cuda.current_stream()
+
+    def stage_a(s_):
+        eng.cover_dist_dev(d_a.data_ptr(), nA, slab.data_ptr(), stream=s_.cuda_stream)
+
+    def stage_b(s_):
+        if nL:
+            eng.wderive_dev(d_l.data_ptr(), nL, slab.data_ptr(), d_pos.data_ptr(),
+                            slab[nA].data_ptr(), d_nh=lnh.data_ptr(), d_digest=ldg.data_ptr(),
+                            max_root_neighbors=kmax, stream=s_.cuda_stream)
+
+    def stage_c(c, s_):
+        if c["kind"] == "derive":
+            eng.wderive_wide_dev(c["d"].data_ptr(), c["n"], c["W"], slab.data_ptr(),
+                                 d_pos.data_ptr(), c["nh"].data_ptr(),
+                                 d_digest=c["dig"].data_ptr(), stream=s_.cuda_stream)
+        else:
+            eng.run_dev(c["d"].data_ptr(), c["n"], c["W"], flags=flags,
+                        d_dist=c["dist"].data_ptr(), d_nh=c["nh"].data_ptr(),
+                        d_digest=c["dig"].data_ptr(), stream=s_.cuda_stream,
+                        max_root_neighbors=c["max_nbrs"])
+
+    # owned roots' digests, gathered in a padded slot per rank
+    def owned_order(p, pl):
+        own = np.zeros(V, bool)
+        own[p] = True
+        lo = pl["need_l"][own[pl["need_l"]]]
+        co = [shard.locality_order(pl["c_der"][words[pl["c_der"]] == W], key)
+              for W in sorted(set(words[pl["c_der"]].tolist()))]
+        if pl["c_wide"].size:
+            co.append(shard.locality_order(pl["c_wide"], key))
+        return np.concatenate([lo] + co) if (lo.size or co) else lo
+
+    owned = [owned_order(p, pl) for p, pl in zip(parts, plans)]
+    slot = max(o.size for o in owned)
+    gbuf = torch.zeros((slot, 3), dtype=torch.int64, device=dev)
+    own_l_idx = torch.from_numpy(np.nonzero(np.isin(need_l, parts[rank]))[0].astype(np.int64)).to(dev)
+    stage_ms, gathered = {"A": [], "B": [], "C": []}, {}
+
+    def step(timed):
+        a0 = torch.cuda.Event(enable_timing=True)
+        a0.record(main_s)
+        done = []
+        for c in cls:  # wide cover roots: their own batch, from the start
+            if c["kind"] == "batch":
+                c["stream"].wait_event(a0)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(c["stream"])
+                stage_c(c, c["stream"])
+                e1.record(c["stream"])
+                done.append(e1)
+                if timed:
+                    c["ms"].append((e0, e1))
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        stage_a(main_s)
+        ev[1].record(main_s)
+        stage_b(main_s)
+        ev[2].record(main_s)
+        for c in cls:
+            if c["kind"] == "derive":
+                stage_c(c, main_s)
+        ev[3].record(main_s)
+        for e in done:
+            main_s.wait_event(e)
+        if timed:
+            stage_ms["A"].append((a0, ev[1]))
+            stage_ms["B"].append((ev[1], ev[2]))
+            stage_ms["C"].append((ev[2], ev[3]))
+        if dist_on:
+            parts_ = [torch.index_select(ldg, 0, own_l_idx)] + [c["dig"] for c in cls]
+            cat = torch.cat(parts_)
+            gbuf[: cat.shape[0]].copy_(cat)
+            gathered["g"] = shard.gather_digests(gbuf)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    eng.sync(main_s.cuda_stream)
+    if dist_on:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if dist_on:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t_start
+    eng.sync(main_s.cuda_stream)
+    if dist_on:
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+
+    step_digest = {}
+    if dist_on:
+        g = gathered["g"].cpu().numpy().view(np.uint64).reshape(world, slot, 3)
+        for r, o in enumerate(owned):
+            for j, root in enumerate(o):
+                step_digest[int(root)] = g[r, j]
+    else:
+        ld = ldg.cpu().numpy().view(np.uint64)
+        for j, root in enumerate(need_l):
+            step_digest[int(root)] = ld[j]
+        for c in cls:
+            d = c["dig"].cpu().numpy().view(np.uint64)
+            for j, root in enumerate(c["roots"]):
+                step_digest[int(root)] = d[j]
+
+    iso_s = torch.cuda.Stream(device=dev)
+
+    def iso(fn):
+        ms = []
+        with torch.cuda.stream(iso_s):
+            for _ in range(args.iso_reps + 1):
+                a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a_.record(iso_s)
+                fn(iso_s)
+                b_.record(iso_s)
+                b_.synchronize()
+                ms.append(a_.elapsed_time(b_))
+        return float(np.median(ms[1:])) if len(ms) > 1 else float(ms[0])
+
+    scan_c = 8 * E + 4 * (V + 1)  # one weighted CSR scan (neighbour + metric words)
+    units = [{"launch": "cover_spf", "kernel": "ospf_cover_dist_dev (cover_spf_kernel: "
+              "contracted-graph Dial, LDS-resident distances)", "roots_per_launch": nA,
+              "isolated_launch_ms": round(iso(stage_a), 3),
+              "compulsory_bytes": nA * 4 * V + scan_c,
+              "traffic": pmc_traffic(args.profile_dir, "cover_spf", nA)}]
+    if nL:
+        units.append({"launch": "wderive", "kernel": "ospf_wderive_dev (wderive_kernel: leaf "
+                      "rows from the cover rows)", "roots_per_launch": nL,
+                      "isolated_launch_ms": round(iso(stage_b), 3),
+                      "compulsory_bytes": nL * 8 * V + int(np.setdiff1d(shard.closure(
+                          need_l, rp, col), need_l).size) * 4 * V,
+                      "traffic": pmc_traffic(args.profile_dir, "wderive", nL)})
+    for c in cls:
+        c["iso_ms"] = iso(lambda s_, c=c: stage_c(c, s_))
+        if c["kind"] == "derive":
+            units.append({"launch": f"wderive_wide_w{c['W']}", "kernel": f"ospf_wderive_wide_dev "
+                          f"(wderive_wide_kernel<{c['W']}>)", "roots_per_launch": c["n"],
+                          "isolated_launch_ms": round(c["iso_ms"], 3),
+                          "compulsory_bytes": c["n"] * 4 * V * c["W"],
+                          "traffic": pmc_traffic(args.profile_dir, f"wderive_wide_w{c['W']}",
+                                                 c["n"])})
+        else:
+            p = c["plan"]
+            units.append({"launch": f"cover_batch_w{c['W']}",
+                          "kernel": f"variant {p['variant']} class launch ({c['W']} next-hop words)",
+                          "roots_per_launch": c["n"], "isolated_launch_ms": round(c["iso_ms"], 3),
+                          "compulsory_bytes": compulsory_bytes(V, E, c["W"], c["n"], p["variant"],
+                                                               p["slices"], True),
+                          "traffic": pmc_traffic(args.profile_dir,
+                                                 f"variant{p['variant']}_cap{c['W'] * 32}", c["n"])})
+    eng.sync(iso_s.cuda_stream)
+    for u in units:
+        sec = u["isolated_launch_ms"] / 1e3
+        u["achieved"] = round(u["compulsory_bytes"] / sec / 1e9, 1)
+        u["frac"] = round(u["compulsory_bytes"] / sec / 1e9 / HBM_PEAK_GBS, 4)
+        u["traffic_over_compulsory"] = (round(u["traffic"] / u["compulsory_bytes"], 2)
+                                        if u["traffic"] else None)
+    dom = max(units, key=lambda u: u["isolated_launch_ms"])
+    step_comp = sum(u["compulsory_bytes"] for u in units)
+    step_s = dt / args.steps
+    roofline = {
+        "bound": "hbm", "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": dom["frac"], "traffic": dom["traffic"], "kernel": dom["kernel"],
+        "roots_per_launch": dom["roots_per_launch"], "avg_launch_ms": dom["isolated_launch_ms"],
+        "compulsory_bytes": dom["compulsory_bytes"],
+        "traffic_over_compulsory": dom["traffic_over_compulsory"], "launches": units,
+        "step_compulsory_bytes": step_comp,
+        "step_frac": round(step_comp / step_s / 1e9 / HBM_PEAK_GBS, 4),
+        "note": "achieved = compulsory bytes of the dominant launch / its isolated time: "
+                "cover_spf = dist rows written + one weighted CSR scan; wderive = leaf dist + "
+                "next-hop rows + the cover rows read once; wderive_wide = next-hop rows; "
+                "cover_batch = rows + one weighted CSR scan per run",
+    }
+    cfg = [{"launch": k, "avg_launch_ms": round(float(np.mean([a_.elapsed_time(b_) for a_, b_ in v])), 3)}
+           for k, v in stage_ms.items() if v]
+    cfg += [{"launch": f"cover_batch_w{c['W']}", "roots_this_rank": c["n"],
+             "avg_launch_ms": round(float(np.mean([a_.elapsed_time(b_) for a_, b_ in c["ms"]])), 3)}
+            for c in cls if c["kind"] == "batch"]
+    report(args, stream, names, perm, step_digest, dt, V * args.steps, E, desc, 0, V, world, rank,
+           dist_on, backend, V, cfg, roofline, "strong", "wcover")
     if dist_on:
         torch.distributed.destroy_process_group()
 

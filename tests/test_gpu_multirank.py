@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("kind,mode", [("unit", "derive"), ("weighted", "wderive")])
+@pytest.mark.parametrize("kind,mode", [("unit", "derive"), ("weighted", "wcover")])
 def test_two_rank_bench_step_and_gather(kind, mode):
     run = MULTIRANK[kind]
     proc = run["proc"]
