@@ -71,18 +71,34 @@ __device__ __forceinline__ void expand(const CoverGraph& C, uint32_t* s_D, uint3
     s_pre[kWave + lane] = beg;
     __builtin_amdgcn_wave_barrier();
     const uint32_t total = (uint32_t)__shfl((int)inc, kWave - 1, kWave);
-    for (uint32_t f = lane; f < total; f += kWave) {
-      uint32_t lo = 0, hi = kWave - 1;  // first k with pre[k] > f
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (s_pre[mid] > f) hi = mid;
-        else lo = mid + 1;
+    // kU edges per lane per step, every load issued before any relaxation (a
+    // 1,781-edge spine is 7 trips, not 28)
+    constexpr uint32_t kU = 4;
+    for (uint32_t f0 = 0; f0 < total; f0 += kWave * kU) {
+      uint2 ed[kU];
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t f = f0 + u * kWave + lane;
+        ed[u] = make_uint2(0u, kInf);
+        if (f < total) {
+          uint32_t lo = 0, hi = kWave - 1;  // first k with pre[k] > f
+#pragma unroll
+          for (int it = 0; it < 6; ++it) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_pre[mid] > f) hi = mid;
+            else lo = mid + 1;
+          }
+          const uint32_t before = lo ? s_pre[lo - 1] : 0u;
+          ed[u] = C.cedge[s_pre[kWave + lo] + (f - before)];
+        }
       }
-      const uint32_t before = lo ? s_pre[lo - 1] : 0u;
-      const uint2 ed = C.cedge[s_pre[kWave + lo] + (f - before)];
-      const uint32_t nd = t + ed.y;
-      const uint32_t old = atomicMin(&s_D[ed.x], nd);
-      if (nd < old) atomicMin(s_next, nd);
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        if (ed[u].y == kInf) continue;
+        const uint32_t nd = t + ed[u].y;
+        const uint32_t old = atomicMin(&s_D[ed[u].x], nd);
+        if (nd < old) atomicMin(s_next, nd);
+      }
     }
     __builtin_amdgcn_wave_barrier();  // s_pre is rewritten by the next pass
   }
