@@ -684,6 +684,10 @@ def wcover_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
     nbrs = shard.distinct_neighbors(rp, col)
     caps = shard.neighbor_caps(nbrs)
     words = np.maximum(1, (nbrs + 31) // 32)
+    # cover next hops: roots sharing their largest neighbours side by side (the
+    # fabric switches of a pod share its racks' rows); OPENR_WCOVER_KEY=first
+    # groups them by their smallest neighbour instead
+    ckey = key if os.environ.get("OPENR_WCOVER_KEY") == "first" else shard.last_neighbor(rp, col)
 
     def part(r):
         if world == 1:
@@ -699,8 +703,8 @@ def wcover_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
         p = np.asarray(p, np.uint32)
         own_l = shard.locality_order(p[leaf[p]], key)
         own_c = p[~leaf[p]]
-        c_der = own_c[(nbrs[own_c] <= 128)]          # (C): next hops derived
-        c_wide = own_c[(nbrs[own_c] > 128)]          # per-root batch kernel
+        c_der = own_c[(nbrs[own_c] <= 2048)]         # (C): next hops derived
+        c_wide = own_c[(nbrs[own_c] > 2048)]         # per-root batch kernel
         nb_c = shard.closure(c_der, rp, col)
         need_l = np.union1d(own_l, nb_c[leaf[nb_c]]).astype(np.uint32)
         need_l = shard.locality_order(need_l, key)
@@ -727,11 +731,12 @@ def wcover_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
     flags = N.OSPF_WANT_DIST | N.OSPF_WANT_NH | N.OSPF_WANT_DIGEST
     cls = []  # (C) classes by next-hop words, and the wide batch class
     for W in sorted(set(words[P["c_der"]].tolist())):
-        roots = shard.locality_order(P["c_der"][words[P["c_der"]] == W], key)
+        roots = shard.locality_order(P["c_der"][words[P["c_der"]] == W], ckey)
         cls.append(dict(kind="derive", W=W, roots=roots, n=int(roots.size),
                         d=torch.from_numpy(roots.view(np.int32)).to(dev),
                         nh=torch.empty((roots.size, V, W), dtype=torch.int32, device=dev),
-                        dig=torch.zeros((roots.size, 3), dtype=torch.int64, device=dev), ms=[]))
+                        dig=torch.zeros((roots.size, 3), dtype=torch.int64, device=dev), ms=[],
+                        side=torch.cuda.Stream(device=dev)))
     if P["c_wide"].size:
         roots = shard.locality_order(P["c_wide"], key)
         W = int(words[roots].max())
@@ -774,7 +779,7 @@ def wcover_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
         own = np.zeros(V, bool)
         own[p] = True
         lo = pl["need_l"][own[pl["need_l"]]]
-        co = [shard.locality_order(pl["c_der"][words[pl["c_der"]] == W], key)
+        co = [shard.locality_order(pl["c_der"][words[pl["c_der"]] == W], ckey)
               for W in sorted(set(words[pl["c_der"]].tolist()))]
         if pl["c_wide"].size:
             co.append(shard.locality_order(pl["c_wide"], key))
@@ -803,10 +808,19 @@ def wcover_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         stage_a(main_s)
         ev[1].record(main_s)
+        # wide cover roots (spines) need only the cover rows: their derivation
+        # runs beside the leaves' and the narrow cover roots'
+        for c in cls:
+            if c["kind"] == "derive" and c["W"] > 4:
+                c["side"].wait_event(ev[1])
+                stage_c(c, c["side"])
+                e1 = torch.cuda.Event()
+                e1.record(c["side"])
+                done.append(e1)
         stage_b(main_s)
         ev[2].record(main_s)
         for c in cls:
-            if c["kind"] == "derive":
+            if c["kind"] == "derive" and c["W"] <= 4:
                 stage_c(c, main_s)
         ev[3].record(main_s)
         for e in done:

@@ -1421,8 +1421,10 @@ int ospf_wderive_wide_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint
   if (!d_roots || !d_src || !d_pos || !d_nh) return fail(c, OSPF_E_INVAL, "null argument");
   const uint32_t V = c->info.n_nodes;
   if (src_pitch < V) return fail(c, OSPF_E_INVAL, "wderive: src_pitch >= V");
-  if (nh_words == 0 || nh_words > 4)
-    return fail(c, OSPF_E_RANGE, "wderive_wide: 1 .. 4 next-hop words (<= 128 neighbours)");
+  if (nh_words == 0 || nh_words > 64)
+    return fail(c, OSPF_E_RANGE, "wderive_wide: 1 .. 64 next-hop words (<= 2048 neighbours)");
+  if (nh_words > 4 && !(flags & OSPF_HOP_COUNT) && c->info.max_metric > 0xFFFEu)
+    return fail(c, OSPF_E_RANGE, "wderive_wide: metrics <= 65534 for more than 4 words");
   if (!(flags & OSPF_HOP_COUNT) && c->dist_bound >= 0xFFFFFFFFull)
     return fail(c, OSPF_E_RANGE, "distances may reach 2^32 - 1");
   hipStream_t s = (hipStream_t)stream;

@@ -283,6 +283,7 @@ struct WDeriveArgs {
   ospf_digest* digest;      // [n] (zeroed by the caller) or null
   uint32_t* err;            // bit 1: K > 32, 16: a transit neighbour has no row, 64: bad root
   uint32_t vec;             // 16-B aligned rows (V, src_pitch % 4 == 0): uint4 loads / stores
+  uint32_t W;               // next-hop words (wide kernels)
   uint32_t G, ctiles;       // roots per block, 256-node subtiles per block (0: defaults)
   uint32_t tiles, chunks;   // set by the launcher
 };

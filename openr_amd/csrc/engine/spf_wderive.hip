@@ -431,6 +431,214 @@ __global__ void __launch_bounds__(256) wderive_wide_kernel(DevGraph g, WDeriveAr
   }
 }
 
+// Cover roots with more than 128 neighbours (W > 4 words: the spines of a
+// fabric, whose neighbours are one switch per pod). Lane = next-hop word w
+// (slots 32 w .. 32 w + 31), a wave walks 2-node chunks of the block's tile;
+// a run of consecutive roots with the same neighbour list (the spines of one
+// plane) loads each chunk's slot values once and every root of the run adds
+// its own link metrics (u16 in LDS) and compares with its own row (staged per
+// tile). Per-root digest sums stay in registers until the block ends.
+constexpr uint32_t kWlG = 8;
+constexpr uint32_t kWlK = 2048;
+constexpr uint32_t kWlTile = 256;
+__global__ void __launch_bounds__(256) wderive_lanes_kernel(DevGraph g, WDeriveArgs a) {
+  __shared__ uint32_t s_pos[kWlK];
+  __shared__ uint16_t s_w[kWlG][kWlK];
+  __shared__ uint32_t s_R[kWlG][kWlTile];
+  __shared__ uint32_t s_root[kWlG], s_K[kWlG], s_own[kWlG], s_same[kWlG];
+  __shared__ unsigned long long s_h[kWlG], s_sum[kWlG];
+  __shared__ uint32_t s_reach[kWlG];
+  const uint32_t V = g.V, W = a.W, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t G = kWlG;
+  const uint32_t ngroups = (a.n + G - 1) / G;
+  const uint32_t ci = blockIdx.x / ngroups, rr = blockIdx.x % ngroups;
+  const uint32_t full = ngroups / 8u * 8u;  // runs of groups on one XCD (block b on XCD b % 8)
+  const uint32_t gi = rr < full ? (rr % 8u) * (full / 8u) + rr / 8u : rr;
+  const uint32_t i0 = gi * G, ng = min(G, a.n - i0);
+  if (tid < ng) {
+    const uint32_t r = a.roots[i0 + tid];
+    s_root[tid] = r;
+    s_own[tid] = kInf;
+    s_K[tid] = 0;
+    s_h[tid] = 0ull;
+    s_sum[tid] = 0ull;
+    s_reach[tid] = 0u;
+    if (r >= V) {
+      atomicOr(a.err, 64u);
+    } else {
+      const uint32_t K = g.dn_off[r + 1] - g.dn_off[r];
+      if (K > kWlK || K > 32u * W) atomicOr(a.err, 1u);
+      s_K[tid] = min(K, min(kWlK, 32u * W));
+      s_own[tid] = a.pos[r];
+      if (s_own[tid] == kInf) atomicOr(a.err, 16u);
+    }
+  }
+  for (uint32_t x = tid; x < ng * kWlK; x += kBlock) s_w[x / kWlK][x % kWlK] = 0xFFFFu;
+  __syncthreads();
+  if (tid < ng)
+    s_same[tid] = tid > 0 && s_own[tid] != kInf && s_own[tid - 1] != kInf &&
+                  s_K[tid] == s_K[tid - 1];
+  for (uint32_t j = 0; j < ng; ++j) {  // the root's up links: smallest metric per slot
+    const uint32_t r = s_root[j];
+    if (r >= V || s_own[j] == kInf) continue;
+    for (uint32_t e = g.row_ptr[r] + tid; e < g.row_ptr[r + 1]; e += kBlock) {
+      const uint32_t cx = g.colx[e];
+      if ((cx & kDown) || cx == r) continue;
+      const uint32_t k = g.didx[e];
+      if (k >= s_K[j]) continue;
+      const uint32_t w = a.hop ? 1u : min(g.w[e], 0xFFFEu);  // metrics <= 65534 (host check)
+      // 16-bit min through the aligned 32-bit word
+      uint32_t* wp = reinterpret_cast<uint32_t*>(&s_w[j][k & ~1u]);
+      const uint32_t sh = 16u * (k & 1u);
+      uint32_t cw = *wp;
+      while (true) {
+        if (w >= ((cw >> sh) & 0xFFFFu)) break;
+        const uint32_t nw = (cw & ~(0xFFFFu << sh)) | (w << sh);
+        const uint32_t prev = atomicCAS(wp, cw, nw);
+        if (prev == cw) break;
+        cw = prev;
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t j = 1; j < ng; ++j) {
+    if (!s_same[j]) continue;
+    const uint32_t* a0 = g.dn + g.dn_off[s_root[j - 1]];
+    const uint32_t* a1 = g.dn + g.dn_off[s_root[j]];
+    for (uint32_t k = tid; k < s_K[j]; k += kBlock)
+      if (a0[k] != a1[k]) s_same[j] = 0u;  // benign race: every writer stores 0
+  }
+  __syncthreads();
+  uint64_t h[kWlG];
+#pragma unroll
+  for (int j = 0; j < (int)kWlG; ++j) h[j] = 0ull;
+  const uint32_t t0 = ci * a.ctiles, t1 = min(a.tiles, t0 + a.ctiles);
+  for (uint32_t j0 = 0; j0 < ng;) {
+    uint32_t j1 = j0 + 1;
+    while (j1 < ng && s_same[j1]) ++j1;
+    const uint32_t K = s_K[j0];
+    if (s_own[j0] == kInf) {
+      j0 = j1;
+      continue;
+    }
+    for (uint32_t k = tid; k < K; k += kBlock) {  // slot rows of the run
+      bool used = false;
+      for (uint32_t j = j0; j < j1 && !used; ++j) used = s_w[j][k] != 0xFFFFu;
+      uint32_t p = kInf;
+      if (used) {
+        const uint32_t nb = g.dn[g.dn_off[s_root[j0]] + k];
+        if (transit(g, nb)) {
+          p = a.pos[nb];
+          if (p == kInf) atomicOr(a.err, 16u);
+        } else {
+          p = kNt | nb;
+        }
+      }
+      s_pos[k] = p;
+    }
+    for (uint32_t t = t0; t < t1; ++t) {
+      const uint32_t v0 = t * kWlTile;
+      __syncthreads();  // s_pos written / the previous tile's s_R consumed
+      for (uint32_t x = tid; x < (j1 - j0) * kWlTile; x += kBlock) {
+        const uint32_t j = x / kWlTile, v = v0 + (x % kWlTile);
+        s_R[j][x % kWlTile] = v < V ? a.src[(size_t)s_own[j0 + j] * a.src_pitch + v] : kInf;
+      }
+      __syncthreads();
+      for (uint32_t c = wave; c < kWlTile / 2u; c += kWaves) {
+        const uint32_t vc = v0 + 2u * c;
+        if (vc >= V) break;  // wave-uniform
+        uint32_t D0[32], D1[32];
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+          const uint32_t k = 32u * lane + i;
+          const uint32_t p = (lane < W && k < K) ? s_pos[k] : kInf;
+          if (p < kNt) {
+            const uint32_t* row = a.src + (size_t)p * a.src_pitch + vc;
+            if (a.vec && vc + 1u < V) {
+              const uint2 x = *reinterpret_cast<const uint2*>(row);
+              D0[i] = x.x;
+              D1[i] = x.y;
+            } else {
+              D0[i] = row[0];
+              D1[i] = vc + 1u < V ? row[1] : kInf;
+            }
+          } else if (p != kInf) {
+            D0[i] = vc == (p & ~kNt) ? 0u : kInf;
+            D1[i] = vc + 1u == (p & ~kNt) ? 0u : kInf;
+          } else {
+            D0[i] = D1[i] = kInf;
+          }
+        }
+        uint64_t kn0 = 0, kn1 = 0, kd0 = 0, kd1 = 0;
+        if (a.digest) {
+          kd0 = g.dkey[2ull * vc];
+          kn0 = g.dkey[2ull * vc + 1];
+          if (vc + 1u < V) {
+            kd1 = g.dkey[2ull * (vc + 1u)];
+            kn1 = g.dkey[2ull * (vc + 1u) + 1];
+          }
+        }
+#pragma unroll
+        for (int jj = 0; jj < (int)kWlG; ++jj) {
+          const uint32_t j = (uint32_t)jj;
+          if (j < j0 || j >= j1) continue;  // uniform
+          const uint32_t R0 = s_R[j - j0][2u * c], R1 = s_R[j - j0][2u * c + 1u];
+          uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+          for (int i = 0; i < 32; ++i) {
+            const uint32_t k = 32u * lane + i;
+            const uint32_t wk = (lane < W && k < K) ? (uint32_t)s_w[j][k] : 0xFFFFu;
+            const uint32_t wv = wk == 0xFFFFu ? kInf : wk;
+            w0 |= (sat_add(wv, D0[i]) == R0 && R0 != kInf ? 1u : 0u) << i;
+            w1 |= (sat_add(wv, D1[i]) == R1 && R1 != kInf ? 1u : 0u) << i;
+          }
+          const uint32_t r = s_root[j];
+          if (vc == r) w0 = 0u;
+          if (vc + 1u == r) w1 = 0u;
+          uint32_t* dst = a.nh + ((size_t)(i0 + j) * V + vc) * W + lane;
+          if (lane < W) {
+            __builtin_nontemporal_store(w0, dst);
+            if (vc + 1u < V) __builtin_nontemporal_store(w1, dst + W);
+          }
+          if (a.digest) {
+            if (w0) h[jj] += kn0 * digest_word_key(lane, w0);
+            if (w1) h[jj] += kn1 * digest_word_key(lane, w1);
+            if (lane == 0) {
+              uint64_t hx = 0, sx = 0;
+              uint32_t rc = 0;
+              if (R0 != kInf) { hx += kd0 * ((uint64_t)R0 + 1ull); sx += R0; ++rc; }
+              if (vc + 1u < V && R1 != kInf) { hx += kd1 * ((uint64_t)R1 + 1ull); sx += R1; ++rc; }
+              h[jj] += hx;
+              if (rc) {
+                atomicAdd(&s_sum[j], (unsigned long long)sx);
+                atomicAdd(&s_reach[j], rc);
+              }
+            }
+          }
+        }
+      }
+    }
+    j0 = j1;
+    __syncthreads();  // s_pos is rewritten by the next run
+  }
+  if (a.digest) {
+#pragma unroll
+    for (int jj = 0; jj < (int)kWlG; ++jj) {
+      uint64_t x = h[jj];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) x += shfl_xor64(x, o);
+      if (lane == 0 && x) atomicAdd(&s_h[jj], (unsigned long long)x);
+    }
+    __syncthreads();
+    if (tid < ng && s_reach[tid]) {
+      ospf_digest* dg = a.digest + i0 + tid;
+      atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)s_reach[tid]);
+      atomicAdd((unsigned long long*)&dg->sum_dist, s_sum[tid]);
+      atomicAdd((unsigned long long*)&dg->hash, s_h[tid]);
+    }
+  }
+}
+
 }  // namespace
 
 hipError_t launch_wderive(const DevGraph& g, WDeriveArgs a, uint32_t kmax, hipStream_t s) {
@@ -450,7 +658,17 @@ hipError_t launch_wderive(const DevGraph& g, WDeriveArgs a, uint32_t kmax, hipSt
 
 hipError_t launch_wderive_wide(const DevGraph& g, WDeriveArgs a, uint32_t W, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  if (W == 0 || W > 4) return hipErrorInvalidValue;
+  if (W == 0 || W > kWlK / 32u) return hipErrorInvalidValue;
+  if (W > 4) {  // lane = word, runs of roots with one neighbour list
+    a.W = W;
+    a.tiles = (g.V + kWlTile - 1) / kWlTile;
+    if (a.ctiles == 0) a.ctiles = 4;
+    a.ctiles = std::min(a.ctiles, a.tiles);
+    a.chunks = (a.tiles + a.ctiles - 1) / a.ctiles;
+    const dim3 grid(((a.n + kWlG - 1) / kWlG) * a.chunks);
+    hipLaunchKernelGGL(wderive_lanes_kernel, grid, dim3(kBlock), 0, s, g, a);
+    return hipGetLastError();
+  }
   a.tiles = (g.V + kSub - 1) / kSub;
   if (a.ctiles == 0) a.ctiles = 16;
   a.ctiles = std::min(a.ctiles, a.tiles);

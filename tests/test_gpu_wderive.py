@@ -204,7 +204,7 @@ def cover_pipeline(eng, csr, check_nh=True):
         for j, r in enumerate(lr):
             out[int(r)] = (None, ln[j].reshape(V, 1), lg[j])
     if check_nh:
-        for W in (1, 2, 3, 4):
+        for W in sorted(set(np.maximum(1, (nbrs[cover] + 31) // 32).tolist())):
             grp = cover[(np.maximum(1, (nbrs[cover] + 31) // 32) == W)]
             if not grp.size:
                 continue
@@ -222,7 +222,10 @@ def cover_pipeline(eng, csr, check_nh=True):
     return {r: (dist[pos[r]], nh, dg) for r, (_, nh, dg) in out.items()}, cover, dist, pos
 
 
-def check_cover(stream):
+def check_cover(stream, sample=0):
+    """Every cover row against the engine; every root's (or `sample` random
+    roots' plus every root with > 4 next-hop words) dist / next hops / digest
+    against the per-root engine path."""
     ls = LinkState()
     ls.apply(stream)
     csr = ls.csr()
@@ -232,7 +235,13 @@ def check_cover(stream):
         got, cover, dist, pos = cover_pipeline(eng, csr)
         ref = eng.run(cover, max(eng.nh_words(int(r)) for r in cover), want_nh=False)
         assert np.array_equal(dist[pos[cover]], ref["dist"])  # every cover row
-        for r, (d, nh, dg) in got.items():
+        keys = sorted(got)
+        if sample:
+            rng = np.random.default_rng(3)
+            keys = sorted(set(rng.choice(keys, min(sample, len(keys)), replace=False).tolist()) |
+                          {r for r in keys if got[r][1].shape[1] > 4})
+        for r in keys:
+            d, nh, dg = got[r]
             W = nh.shape[1]
             want = eng.run([r], W, want_digest=True)
             assert np.array_equal(d, want["dist"][0]), r
@@ -299,3 +308,18 @@ def test_cover_graph_goes_stale_on_updates():
             eng.cover_prepare(bad)
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("pods,planes", [(150, 2), (300, 1)])
+def test_cover_spf_wide_spines(pods, planes):
+    """Spines with 150 / 300 neighbours (5 / 10 next-hop words): the lane-per-
+    word kernel, runs of one plane's spines, a drained fabric switch, an
+    overloaded spine adjacency and a down link."""
+    st = T.fabric(pods=pods, planes=planes, weighted_seed=5, max_metric=300)
+    dbs = st.to_dbs()
+    for d in dbs:
+        if d.name in ("2-3-0", "2-140-0"):
+            d.overloaded = True
+        if d.name in ("1-0-5", "1-0-30"):
+            d.adjs[7].overloaded = True
+    check_cover(AdjDbStream.from_dbs(dbs), sample=200)
