@@ -441,6 +441,10 @@ __global__ void __launch_bounds__(256) wderive_wide_kernel(DevGraph g, WDeriveAr
 constexpr uint32_t kWlG = 8;
 constexpr uint32_t kWlK = 2048;
 constexpr uint32_t kWlTile = 256;
+// slot k of a root's metric table sits at (k % 32) * 64 + k / 32: lane w reads
+// its slots 32 w + i at i * 64 + w, consecutive lanes consecutive u16s (the
+// k-major table put every lane of a read on two banks)
+__device__ __forceinline__ uint32_t widx(uint32_t k) { return (k & 31u) * 64u + (k >> 5); }
 __global__ void __launch_bounds__(256) wderive_lanes_kernel(DevGraph g, WDeriveArgs a) {
   __shared__ uint32_t s_pos[kWlK];
   __shared__ uint16_t s_w[kWlG][kWlK];
@@ -488,8 +492,9 @@ __global__ void __launch_bounds__(256) wderive_lanes_kernel(DevGraph g, WDeriveA
       if (k >= s_K[j]) continue;
       const uint32_t w = a.hop ? 1u : min(g.w[e], 0xFFFEu);  // metrics <= 65534 (host check)
       // 16-bit min through the aligned 32-bit word
-      uint32_t* wp = reinterpret_cast<uint32_t*>(&s_w[j][k & ~1u]);
-      const uint32_t sh = 16u * (k & 1u);
+      const uint32_t ix = widx(k);
+      uint32_t* wp = reinterpret_cast<uint32_t*>(&s_w[j][ix & ~1u]);
+      const uint32_t sh = 16u * (ix & 1u);
       uint32_t cw = *wp;
       while (true) {
         if (w >= ((cw >> sh) & 0xFFFFu)) break;
@@ -523,7 +528,7 @@ __global__ void __launch_bounds__(256) wderive_lanes_kernel(DevGraph g, WDeriveA
     }
     for (uint32_t k = tid; k < K; k += kBlock) {  // slot rows of the run
       bool used = false;
-      for (uint32_t j = j0; j < j1 && !used; ++j) used = s_w[j][k] != 0xFFFFu;
+      for (uint32_t j = j0; j < j1 && !used; ++j) used = s_w[j][widx(k)] != 0xFFFFu;
       uint32_t p = kInf;
       if (used) {
         const uint32_t nb = g.dn[g.dn_off[s_root[j0]] + k];
@@ -587,7 +592,7 @@ __global__ void __launch_bounds__(256) wderive_lanes_kernel(DevGraph g, WDeriveA
 #pragma unroll
           for (int i = 0; i < 32; ++i) {
             const uint32_t k = 32u * lane + i;
-            const uint32_t wk = (lane < W && k < K) ? (uint32_t)s_w[j][k] : 0xFFFFu;
+            const uint32_t wk = (lane < W && k < K) ? (uint32_t)s_w[j][i * 64u + lane] : 0xFFFFu;
             const uint32_t wv = wk == 0xFFFFu ? kInf : wk;
             w0 |= (sat_add(wv, D0[i]) == R0 && R0 != kInf ? 1u : 0u) << i;
             w1 |= (sat_add(wv, D1[i]) == R1 && R1 != kInf ? 1u : 0u) << i;
