@@ -153,32 +153,55 @@ __global__ void __launch_bounds__(256) cover_spf_kernel(DevGraph g, CoverGraph C
       if (t == kInf) break;  // every reachable cover node settled
       __syncthreads();       // the slot reset is visible before its use
     }
-    // the row in node order: cover nodes from LDS, leaves by their last hop
+    // the row in node order: cover nodes from LDS, leaves by their last hop;
+    // four nodes per thread per step, their first two in-link quads loaded
+    // before any is used (a rack's 8 entries)
     uint32_t* row = a.dist + (size_t)i * V;
-    for (uint32_t v = tid; v < V; v += kBlock) {
-      const uint32_t c = C.cix[v];
-      uint32_t out;
-      if (!(c & kLeaf)) {
-        out = s_D[c];
-      } else {
-        out = kInf;
-        const uint32_t l = c & ~kLeaf;
-        const uint4* la = reinterpret_cast<const uint4*>(C.ladj + C.lrow[l]);
-        const uint32_t nq = (C.lrow[l + 1] - C.lrow[l]) >> 2;
-        for (uint32_t k = 0; k < nq; ++k) {
-          const uint4 e4 = la[k];
-          const uint32_t es[4] = {e4.x, e4.y, e4.z, e4.w};
+    const uint4* la4 = reinterpret_cast<const uint4*>(C.ladj);
+    const uint4 pad = make_uint4(0xFFFFu, 0xFFFFu, 0xFFFFu, 0xFFFFu);
+    auto fold = [&](uint4 e4, uint32_t out) {
+      const uint32_t es[4] = {e4.x, e4.y, e4.z, e4.w};
 #pragma unroll
-          for (int b = 0; b < 4; ++b) {
-            const uint32_t ci = es[b] & 0xFFFFu;
-            if (ci >= nS) continue;  // padding
-            if (!((s_tr[ci >> 5] >> (ci & 31u)) & 1u) && ci != r) continue;
-            const uint32_t d = s_D[ci];
-            if (d != kInf) out = min(out, d + (es[b] >> 16));
-          }
+      for (int b = 0; b < 4; ++b) {
+        const uint32_t ci = es[b] & 0xFFFFu;
+        if (ci >= nS) continue;  // padding
+        if (!((s_tr[ci >> 5] >> (ci & 31u)) & 1u) && ci != r) continue;
+        const uint32_t d = s_D[ci];
+        if (d != kInf) out = min(out, d + (es[b] >> 16));
+      }
+      return out;
+    };
+    for (uint32_t v0 = tid; v0 < V; v0 += 4u * kBlock) {
+      uint32_t c4[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t v = v0 + (uint32_t)k * kBlock;
+        c4[k] = v < V ? C.cix[v] : 0u;
+      }
+      uint4 e0[4], e1[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        e0[k] = e1[k] = pad;
+        if (c4[k] & kLeaf) {
+          const uint32_t q0 = (c4[k] >> 5) & 0x3FFFFFFu, nq = c4[k] & 31u;
+          if (nq > 0) e0[k] = la4[q0];
+          if (nq > 1) e1[k] = la4[q0 + 1];
         }
       }
-      __builtin_nontemporal_store(out, row + v);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t v = v0 + (uint32_t)k * kBlock;
+        if (v >= V) continue;
+        uint32_t out;
+        if (!(c4[k] & kLeaf)) {
+          out = s_D[c4[k]];
+        } else {
+          out = fold(e1[k], fold(e0[k], kInf));
+          const uint32_t q0 = (c4[k] >> 5) & 0x3FFFFFFu, nq = c4[k] & 31u;
+          for (uint32_t qq = 2; qq < nq; ++qq) out = fold(la4[q0 + qq], out);
+        }
+        __builtin_nontemporal_store(out, row + v);
+      }
     }
     __syncthreads();  // s_D is reused by the next root
   }

@@ -1517,6 +1517,16 @@ int ospf_cover_prepare(ospf_ctx* c, const uint8_t* leaf) {
     while (ladj.size() % 4) ladj.push_back(0xFFFFu);
     lrow[++l] = (uint32_t)ladj.size();
   }
+  // a leaf's cix word: 0x80000000 | (its first in-link quad << 5) | quads, so
+  // the kernel reaches the list in one dependent load
+  for (uint32_t v = 0, l = 0; v < V; ++v) {
+    if (!leaf[v]) continue;
+    const uint32_t q0 = lrow[l] / 4u, nq = (lrow[l + 1] - lrow[l]) / 4u;
+    if (q0 >= (1u << 26) || nq > 31u)
+      return fail(c, OSPF_E_RANGE, "cover: a leaf with > 124 in-link entries");
+    cix[v] = 0x80000000u | (q0 << 5) | nq;
+    ++l;
+  }
   if (ladj.empty()) ladj.assign(4, 0xFFFFu);
   if (cedge.empty()) cedge.push_back(make_uint2(0, 0));
   // one allocation: cix | crow | ctr | lrow | ladj | cedge (16-B aligned parts)

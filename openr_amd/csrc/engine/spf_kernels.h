@@ -250,7 +250,7 @@ hipError_t launch_levels128_rows(const DevGraph& g, const LvArgs& a, hipStream_t
 constexpr uint32_t kCoverMaxS = 32768;  // cover nodes (LDS-resident distances)
 struct CoverGraph {
   uint32_t nS, nL;
-  const uint32_t* cix;   // [V] cover index, or 0x80000000 | leaf index
+  const uint32_t* cix;   // [V] cover index, or 0x80000000 | first ladj quad << 5 | quads
   const uint32_t* crow;  // [nS + 1]
   const uint2* cedge;    // [crow[nS]] {target cover index, weight}
   const uint32_t* ctr;   // [(nS + 31) / 32] transit bits
