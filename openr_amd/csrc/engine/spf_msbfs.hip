@@ -1246,9 +1246,14 @@ __device__ __forceinline__ void derive_uniform_tiles(
     // stores are issued again.
     uint4 Lp = make_uint4(kInf, kInf, kInf, kInf);  // level bytes are < 0x80
     uint64_t hw = 0;  // the previous root's wave digest sum of this tile
+    // the next root's own levels are loaded while this root's words are
+    // stored (one load in flight across the loop)
+    uint4 Ln = make_uint4(0, 0, 0, 0);
+    if (live) Ln = *reinterpret_cast<const uint4*>(d.lev + (size_t)s_own[0] * d.pitch + vl);
     for (uint32_t j = 0; j < ng; ++j) {
-      uint4 L = make_uint4(0, 0, 0, 0);
-      if (live) L = *reinterpret_cast<const uint4*>(d.lev + (size_t)s_own[j] * d.pitch + vl);
+      const uint4 L = Ln;
+      if (live && j + 1 < ng)
+        Ln = *reinterpret_cast<const uint4*>(d.lev + (size_t)s_own[j + 1] * d.pitch + vl);
       const bool same = L.x == Lp.x && L.y == Lp.y && L.z == Lp.z && L.w == Lp.w;
       Lp = L;
       if (__ballot(!same)) {  // some lane's levels differ: recompute the wave's words
