@@ -136,7 +136,8 @@ def host_threads() -> int:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=60,
+                    help="timed steps (default: a few seconds of timed work at F100k)")
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--topology", default="fabric100k")
     ap.add_argument("--roots", type=int, default=-1,
