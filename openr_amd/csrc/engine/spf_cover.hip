@@ -38,7 +38,7 @@ namespace {
 constexpr uint32_t kInf = 0xFFFFFFFFu;
 constexpr uint32_t kLeaf = 0x80000000u;
 constexpr int kWave = 64;
-constexpr uint32_t kBlock = 256;
+constexpr uint32_t kBlock = 512;  // 8 waves per root: shorter scans and expansions per round
 constexpr uint32_t kWaves = kBlock / kWave;
 constexpr uint32_t kQ = 256;  // per-wave frontier queue
 
@@ -104,7 +104,7 @@ __device__ __forceinline__ void expand(const CoverGraph& C, uint32_t* s_D, uint3
   }
 }
 
-__global__ void __launch_bounds__(256) cover_spf_kernel(DevGraph g, CoverGraph C, CoverArgs a) {
+__global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C, CoverArgs a) {
   extern __shared__ uint32_t s_D[];  // [nS] distances, then [ctr words] transit bits
   __shared__ uint32_t s_q[kWaves][kQ];
   __shared__ uint32_t s_pre[kWaves][2 * kWave];
