@@ -529,7 +529,9 @@ def derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
         for c in sorted(classes, key=lambda c: -c["W"] * c["n"]):
             if c["kind"] == "batch":
                 continue
-            cs = c["stream"]
+            # OPENR_DERIVE_SERIAL=1: the classes one after another on the main
+            # stream (experiment; default: each on its own stream)
+            cs = main_s if os.environ.get("OPENR_DERIVE_SERIAL") == "1" else c["stream"]
             cs.wait_event(b_)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(cs)
