@@ -73,7 +73,7 @@ __device__ __forceinline__ void expand(const CoverGraph& C, uint32_t* s_D, uint3
     const uint32_t total = (uint32_t)__shfl((int)inc, kWave - 1, kWave);
     // kU edges per lane per step, every load issued before any relaxation (a
     // 1,781-edge spine is 7 trips, not 28)
-    constexpr uint32_t kU = 8;
+    constexpr uint32_t kU = 16;
     for (uint32_t f0 = 0; f0 < total; f0 += kWave * kU) {
       uint2 ed[kU];
 #pragma unroll
