@@ -1246,6 +1246,7 @@ __device__ __forceinline__ void derive_uniform_tiles(
     // stores are issued again.
     uint4 Lp = make_uint4(kInf, kInf, kInf, kInf);  // level bytes are < 0x80
     uint64_t hw = 0;  // the previous root's wave digest sum of this tile
+    uint4 sv[4];      // this lane's four staged store pieces (kept across reused roots)
     // the next root's own levels are loaded while this root's words are
     // stored (one load in flight across the loop)
     uint4 Ln = make_uint4(0, 0, 0, 0);
@@ -1314,13 +1315,15 @@ __device__ __forceinline__ void derive_uniform_tiles(
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) hw += shfl_xor64(hw, o);
       }
+#pragma unroll
+      for (int x = 0; x < 4; ++x) sv[x] = reinterpret_cast<const uint4*>(st)[x * 64 + lane];
       }  // recomputed
       const size_t i = i0 + j;
       uint32_t* dst = d.nh + (size_t)i * V + tv0;
       if (tn == 1024u && (((size_t)i * V + tv0) & 3u) == 0) {
 #pragma unroll
         for (int x = 0; x < 4; ++x)
-          store_row16(reinterpret_cast<uint4*>(dst) + x * 64 + lane, reinterpret_cast<const uint4*>(st)[x * 64 + lane]);
+          store_row16(reinterpret_cast<uint4*>(dst) + x * 64 + lane, sv[x]);
       } else {
         for (uint32_t x = lane; x < tn; x += 64u) dst[x] = st[x];
       }
