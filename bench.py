@@ -169,6 +169,9 @@ def main():
     ap.add_argument("--wide", choices=["derive", "batch"], default="derive",
                     help="derive mode: rows of > 4 next-hop words (spines) from level rows "
                          "(nh_derive_wide_kernel) or on the bit-plane batch path")
+    ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
+                    help="derive mode: capture one step's launches in a HIP graph and replay "
+                         "it (auto: on; falls back to eager launches if capture fails)")
     ap.add_argument("--wcover", choices=["spf", "batch"], default="spf",
                     help="weighted all-sources: cover roots by the contracted-graph SPF "
                          "(ospf_cover_dist_dev + ospf_wderive_wide_dev) or per-root batches")
@@ -509,31 +512,33 @@ def derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
 
     p1_ms = []
 
-    def step(timed):
-        a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a_.record(main_s)
+    def launches(timed, base, tm=True):
+        """One step's launches, rooted at stream `base` (tm: timing events)."""
+        ev = (lambda: torch.cuda.Event(enable_timing=True)) if tm else torch.cuda.Event
+        a_, b_ = ev(), ev()
+        a_.record(base)
         done = []
         for c in classes:  # batch classes start with the step (no level rows needed)
             if c["kind"] == "batch":
                 cs = c["stream"]
                 cs.wait_event(a_)
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0, e1 = ev(), ev()
                 e0.record(cs)
                 phase2(c, cs)
                 e1.record(cs)
                 done.append(e1)
                 if timed:
                     c["ms"].append((e0, e1))
-        phase1(main_s)
-        b_.record(main_s)
+        phase1(base)
+        b_.record(base)
         for c in sorted(classes, key=lambda c: -c["W"] * c["n"]):
             if c["kind"] == "batch":
                 continue
             # OPENR_DERIVE_SERIAL=1: the classes one after another on the main
             # stream (experiment; default: each on its own stream)
-            cs = main_s if os.environ.get("OPENR_DERIVE_SERIAL") == "1" else c["stream"]
+            cs = base if os.environ.get("OPENR_DERIVE_SERIAL") == "1" else c["stream"]
             cs.wait_event(b_)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0, e1 = ev(), ev()
             e0.record(cs)
             phase2(c, cs)
             e1.record(cs)
@@ -541,9 +546,17 @@ def derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
             if timed:
                 c["ms"].append((e0, e1))
         for e in done:
-            main_s.wait_event(e)
+            base.wait_event(e)
         if timed:
             p1_ms.append((a_, b_))
+
+    graph = None
+
+    def step(timed):
+        if graph is not None:
+            graph.replay()
+        else:
+            launches(timed, main_s)
         if dist_on:
             for c in classes:
                 c["gathered"] = shard.gather_digests(c["dig"])
@@ -552,6 +565,33 @@ def derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
         step(False)
     torch.cuda.synchronize()
     eng.sync(main_s.cuda_stream)
+    graph_note = "off"
+    if args.graph != "off":
+        # the whole step (levels rounds, memsets, the width classes on their
+        # streams) as one HIP graph: small topologies are launch-bound
+        try:
+            # one eager step on the capture stream first: the engine's scratch
+            # is per stream and must exist before capture (no allocation inside)
+            cap_s = torch.cuda.Stream(device=dev)
+            cap_s.wait_stream(main_s)
+            with torch.cuda.stream(cap_s):
+                launches(False, cap_s, tm=False)
+            cap_s.synchronize()
+            eng.sync(cap_s.cuda_stream)
+            g_ = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_, stream=cap_s):
+                launches(False, cap_s, tm=False)
+            torch.cuda.synchronize()
+            graph = g_
+            graph.replay()
+            torch.cuda.synchronize()
+            eng.sync(main_s.cuda_stream)
+            graph_note = "on"
+        except Exception as e:  # capture not supported here: eager launches
+            graph = None
+            graph_note = f"off (capture failed: {str(e)[:120]})"
+            torch.cuda.synchronize()
+            log(f"[rank {rank}] graph capture failed, eager launches: {e}")
     if dist_on:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -654,15 +694,16 @@ def derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
                 "ms_per_step. traffic = measured HBM bytes per launch (rocprofv3 FETCH_SIZE x2 "
                 "+ WRITE_SIZE, profiles/<round>/pmc_traffic.json)",
     }
-    p1_avg = float(np.mean([a_.elapsed_time(b_) for a_, b_ in p1_ms]))
+    p1_avg = float(np.mean([a_.elapsed_time(b_) for a_, b_ in p1_ms])) if p1_ms else None
     classes_cfg = [{"launch": "levels", "roots_this_rank": int(clo.size),
                     "closure_over_roots": round(clo.size / max(1, mine.size), 4),
-                    "avg_launch_ms": round(p1_avg, 3), "isolated_launch_ms": round(p1_iso, 3)}]
+                    "avg_launch_ms": round(p1_avg, 3) if p1_avg is not None else None,
+                    "isolated_launch_ms": round(p1_iso, 3), "hip_graph": graph_note}]
     for c in classes:
         classes_cfg.append({"cap": c["cap"], "nh_words": c["W"], "roots_this_rank": c["n"],
                             "path": c["kind"],
                             "avg_launch_ms": round(float(np.mean(
-                                [a_.elapsed_time(b_) for a_, b_ in c["ms"]])), 3) if c["ms"] else 0.0,
+                                [a_.elapsed_time(b_) for a_, b_ in c["ms"]])), 3) if c["ms"] else None,
                             "isolated_launch_ms": round(c["iso_ms"], 3)})
     report(args, stream, names, perm, step_digest, dt, V * args.steps, E, desc, 0, V, world, rank,
            dist_on, backend, V, classes_cfg, roofline, "strong", "derive")
