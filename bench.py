@@ -5,23 +5,25 @@ BASELINE.json metric: "all-sources SPF/sec + GTEPS on 100k-node fabric
 topology at 1/2/4/8 GPUs". A *step* = one all-sources sweep: every node of
 the topology is the root of one SPF run (LinkState::runSpf,
 openr/decision/LinkState.cpp:836-911) whose distance row and next-hop bitset
-row are written to HBM, plus a 24-B digest per run. The roots are split
-over the ranks (one process per GPU, contiguous slices of each next-hop width
-class), so the total work per step is fixed: scaling "strong". Each rank
-launches one engine call per width class (rack / fabric / spine switches),
-each on its own HIP stream; for N > 1 the digest records are all-gathered
-over RCCL. The timed steps' own digests of the CPU-sample roots are checked
-against the CPU restatement (`parity_vs_cpu_sample`).
+row are written to HBM, plus a 24-B digest per run. A step is ONE C-ABI call,
+ospf_sweep_run (include/openr_spf.h): the library owns the path, the width
+classes, their streams and the HIP graph it replays. Ranks (one process per
+GPU) run the parts of the library's root partition, so the total work per
+step is fixed: scaling "strong"; for N > 1 the digest records are
+all-gathered over RCCL each step. The digests are poisoned before the timed
+loop and the last timed step's digests are checked against the CPU
+restatements on a role-stratified root set (`parity_vs_cpu_sample`).
 
 Other topologies (parity / side benches, not the headline): fabric10k,
-fabric100k-w and fabric10k-w (metrics 1..64, seed 7: weighted derive mode,
-wderive_main), grid31, mesh1m (8,192 sampled roots).
+fabric100k-w and fabric10k-w (metrics 1..64, seed 7: the weighted cover
+path), grid31, grid100 (unit 100x100 grid, diameter 198), mesh1m (8,192
+sampled roots on the per-class batch driver).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--topology T]
        torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
                 --master-port P bench.py --gpus N ...
 Profiling mode (one class alone, R launches on one stream, no JSON line):
-       python bench.py --class-only W --reps R
+       python bench.py --mode classes --class-only W --reps R
 """
 from __future__ import annotations
 
@@ -68,6 +70,8 @@ def build_topology(name: str):
                 "F10k fabric pods=173 planes=8 (metric 1..64, seed 7)", True, 0)
     if name == "grid31":
         return T.grid(31), "G31 grid 31x31 (unit metric)", False, 0
+    if name == "grid100":
+        return T.grid(100), "G100 grid 100x100 (unit metric, diameter 198)", False, 0
     if name == "mesh1m":
         return T.mesh(1_000_000, seed=42), "M1M random-geometric mesh (metric 1..16)", True, 8192
     raise SystemExit(f"unknown topology {name}")
@@ -155,26 +159,20 @@ def main():
                     help="sweep order within a width class: grouped by smallest neighbour "
                          "(multi-source batches share frontiers), the random permutation, or "
                          "auto = grouped for single-word classes only")
-    ap.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles", "r02"))
+    ap.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles", "r03"))
     ap.add_argument("--iso-reps", type=int, default=3,
                     help="isolated launches per class for the roofline (after the timed steps)")
     ap.add_argument("--class-only", type=int, default=0,
                     help="profiling mode: launch only the class with this neighbour capacity "
                          "(8, 16, or 32 x next-hop words)")
     ap.add_argument("--reps", type=int, default=3, help="launches in --class-only mode")
-    ap.add_argument("--mode", choices=["auto", "derive", "batch"], default="auto",
-                    help="derive: all-sources next hops from neighbour level rows (unit "
-                         "metric, every root's neighbours in the sweep); batch: per-class "
-                         "engine batches (bit-plane next hops); auto = derive when it applies")
-    ap.add_argument("--wide", choices=["derive", "batch"], default="derive",
-                    help="derive mode: rows of > 4 next-hop words (spines) from level rows "
-                         "(nh_derive_wide_kernel) or on the bit-plane batch path")
+    ap.add_argument("--mode", choices=["auto", "derive", "wcover", "wderive", "batch", "classes"],
+                    default="auto",
+                    help="all-sources sweep path (ospf_sweep_opts.mode; auto = the engine's "
+                         "choice); classes = the per-class batch driver below (no sweep)")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
-                    help="derive mode: capture one step's launches in a HIP graph and replay "
-                         "it (auto: on; falls back to eager launches if capture fails)")
-    ap.add_argument("--wcover", choices=["spf", "batch"], default="spf",
-                    help="weighted all-sources: cover roots by the contracted-graph SPF "
-                         "(ospf_cover_dist_dev + ospf_wderive_wide_dev) or per-root batches")
+                    help="sweeps: the library captures one run in a HIP graph and replays it "
+                         "(auto: on; eager launches if capture fails)")
     ap.add_argument("--dist-parity", type=int, default=0,
                     help="N>1: rank 0 checks the gathered digests of the last timed step "
                          "for this many roots against the CPU restatement")
@@ -213,28 +211,11 @@ def main():
     flags = N.OSPF_WANT_DIST | N.OSPF_WANT_DIGEST | (0 if args.no_nh else N.OSPF_WANT_NH)
     perm = np.random.default_rng(SEED).permutation(V).astype(np.uint32)
     n_roots = default_roots if args.roots < 0 else args.roots
-    derive_ok = (n_roots <= 0 and not weighted and args.roots_per_gpu == 0 and not args.no_nh
-                 and not args.class_only and eng.info().unit_metric
-                 and int(shard.distinct_neighbors(csr["row_ptr"], csr["col"]).max()) <= 2048)
-    if args.mode != "batch" and derive_ok:
-        return derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, dev,
-                           backend, coll_dev)
-    wderive_ok = (n_roots <= 0 and not derive_ok and args.roots_per_gpu == 0 and not args.no_nh
-                  and not args.class_only)
-    if args.mode == "derive" and not (derive_ok or wderive_ok):
-        raise SystemExit("derive mode needs an all-sources sweep (strong scaling)")
-    if args.mode != "batch" and wderive_ok:
-        if args.wcover == "spf":
-            leaf = shard.leaf_set(csr["row_ptr"], csr["col"])
-            try:
-                eng.cover_prepare(leaf)
-            except Exception as e:  # outside the cover kernel's limits: per-root cover runs
-                log(f"[rank {rank}] cover SPF unavailable ({e}); cover roots on the batch path")
-            else:
-                return wcover_main(args, eng, csr, names, stream, desc, V, E, world, rank,
-                                   dist_on, dev, backend, coll_dev, leaf)
-        return wderive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, dev,
-                            backend, coll_dev, weighted)
+    sweep_ok = (n_roots <= 0 and args.roots_per_gpu == 0 and not args.no_nh
+                and not args.class_only and args.mode != "classes")
+    if sweep_ok:
+        return sweep_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, dev,
+                          backend, coll_dev)
     pool = perm if n_roots <= 0 else perm[: min(n_roots, V)]
     nbrs = shard.distinct_neighbors(csr["row_ptr"], csr["col"])
     key = shard.first_neighbor(csr["row_ptr"], csr["col"]) if args.root_order != "random" \
@@ -250,14 +231,21 @@ def main():
     for c in classes:
         x = c.extra
         if weak:  # ranks' slices of one step must not overlap: <= m / world each
-            x["n"] = min(c.per_step, max(1, c.roots.size // world))
+            m = c.roots.size  # (a class smaller than the world: one root per rank < m)
+            x["slot"] = min(c.per_step, max(1, m // world))
+            x["n"] = x["slot"] if m >= world else (1 if rank < m else 0)
         else:  # strong: this rank's contiguous slice of the class, every step
             lo, hi = shard.rank_slice(c.roots.size, world, rank)
             x["mine"] = c.roots[lo:hi]
             x["n"] = hi - lo
             x["slot"] = -(-c.roots.size // world)  # gather slot per rank (padded)
-    classes = [c for c in classes if c.extra["n"] > 0]
+    classes = [c for c in classes if c.extra["slot" if weak else "n"] > 0]
     B = sum(c.extra["n"] for c in classes)
+    B_all = B
+    if dist_on and weak:  # ranks may run different counts (classes smaller than the world)
+        t = torch.tensor([B], dtype=torch.int64, device=coll_dev)
+        torch.distributed.all_reduce(t)
+        B_all = int(t.item())
     for c in classes:
         n, x = c.extra["n"], c.extra
         x["max_nbrs"] = int(max(1, nbrs[c.roots].max()))  # engine hint: sizes bit-planes
@@ -301,7 +289,8 @@ def main():
             with torch.cuda.stream(cs):
                 cs.wait_event(ready)
                 if weak:  # cyclic sweep of the class, disjoint slices per rank
-                    start = ((i * world + rank) * n) % c.roots.size
+                    start = rank if c.roots.size < world else \
+                        ((i * world + rank) * n) % c.roots.size
                     idx = (torch.arange(n, device=dev) + start) % c.roots.size
                     torch.index_select(x["d_all"], 0, idx, out=x["roots"])
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -353,7 +342,7 @@ def main():
                 for j, root in enumerate(x["mine"]):
                     step_digest[int(root)] = d[j]
 
-    roots_total = world * B * args.steps if weak else pool.size * args.steps
+    roots_total = B_all * args.steps if weak else pool.size * args.steps
 
     # roofline. The classes overlap on their streams inside the timed steps,
     # so each class is then timed ALONE (not part of `value`): R launches on
@@ -420,184 +409,64 @@ def main():
                     **{kk: c.extra["plan"][kk] for kk in ("variant", "slices", "block")},
                     "avg_launch_ms": round(float(np.mean(c.extra["ms"])), 3),
                     "isolated_launch_ms": round(c.extra["iso_ms"], 3)} for c in classes]
-    report(args, stream, names, pool, step_digest, dt, roots_total, E, desc, n_roots, V, world,
-           rank, dist_on, backend, int(world * B if weak else pool.size), classes_cfg, roofline,
-           "weak" if weak else "strong", "batch")
+    report(args, stream, names, csr, step_digest, dt, roots_total, E, desc, n_roots, V, world,
+           rank, dist_on, backend, int(B_all if weak else pool.size), classes_cfg, roofline,
+           "weak" if weak else "strong", "batch", pool=pool)
     if dist_on:
         torch.distributed.destroy_process_group()
 
 
-def derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, dev, backend,
-                coll_dev):
-    """All-sources step in derive mode (spf_msbfs.hip "derive"). Phase 1:
-    ospf_levels_dev over this rank's closure (its roots + their neighbours):
-    dist rows + byte level rows, one distance-only traversal per 64 roots.
-    Phase 2: ospf_nh_derive_dev per width class: next-hop rows + digests of
-    this rank's roots from the level rows. Ranks own the racks + fabric
-    switches of a block of pods and the spines of a block of planes (fabric
-    names; other graphs: slices of each width class)."""
-    rp, col = csr["row_ptr"], csr["col"]
-    perm = np.random.default_rng(SEED).permutation(V).astype(np.uint32)
-    key = shard.first_neighbor(rp, col)
-    caps = shard.neighbor_caps(shard.distinct_neighbors(rp, col))
-    all_caps = sorted(set(caps.tolist()))
-
-    def part(r):
-        if world == 1:
-            return perm
-        fp = shard.fabric_partition(names, world, r)
-        if fp is not None:
-            return fp
-        cls = shard.make_classes(perm, caps, V, key)
-        return np.concatenate([c.roots[slice(*shard.rank_slice(c.roots.size, world, r))]
-                               for c in cls])
-
-    parts = [part(r) for r in range(world)]
-    lkey = shard.last_neighbor(rp, col)
-    cls_all = [{cap: shard.locality_order(p[caps[p] == cap], lkey) for cap in all_caps}
-               for p in parts]
-    mine = parts[rank]
-    clo = shard.locality_order(shard.closure(mine, rp, col), key)
-    pos = np.full(V, 0xFFFFFFFF, np.uint32)
-    pos[clo] = np.arange(clo.size, dtype=np.uint32)
+def sweep_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, dev, backend,
+               coll_dev):
+    """All-sources step through the library's sweep (ospf_sweep_*, include/
+    openr_spf.h): one C-ABI call per step, ospf_sweep_run, queues the whole
+    sweep -- the path the engine picks for the graph (derive: distance-only
+    128-root BFS + next hops from neighbours' level rows; wcover: cover SPF +
+    leaf / cover next-hop derivation; wderive / batch), its width classes on
+    their streams, replayed from one HIP graph. Rank r runs part r of the
+    library's root partition (pod / plane blocks on a fabric); for N > 1 the
+    24-B digests are all-gathered over RCCL each step."""
+    mode = {"auto": "auto", "derive": "derive", "batch": "batch"}.get(args.mode, args.mode)
     t0 = time.time()
-    d_clo = torch.from_numpy(clo.view(np.int32)).to(dev)
-    d_pos = torch.from_numpy(pos.view(np.int32)).to(dev)
-    lev = torch.empty((clo.size, eng.lev_pitch), dtype=torch.uint8, device=dev)
-    dist = torch.empty((clo.size, V), dtype=torch.int32, device=dev)
-    ldg = torch.empty((clo.size, 3), dtype=torch.int64, device=dev)
-    nbrs = shard.distinct_neighbors(rp, col)
-    flags = N.OSPF_WANT_DIST | N.OSPF_WANT_NH | N.OSPF_WANT_DIGEST
-    classes = []
-    for cap in all_caps:
-        roots = cls_all[rank][cap]
-        W = max(1, cap // 32) if cap > 16 else 1
-        slot = max(1, max(c[cap].size for c in cls_all))
-        # every class derives from the level rows (lane-16 kernel up to 4
-        # words, the word-per-lane kernel above); --wide batch runs the wider
-        # ones (spines) on the bit-plane batch path instead, on their own
-        # stream, concurrently with phase 1 (they need no level rows)
-        kind = "derive" if W <= 4 or args.wide == "derive" else "batch"
-        c = dict(cap=cap, W=W, roots=roots, n=int(roots.size), kind=kind,
-                 d=torch.from_numpy(roots.view(np.int32)).to(dev),
-                 nh=torch.empty((max(1, roots.size), V, W), dtype=torch.int32, device=dev),
-                 dig=torch.zeros((slot, 3), dtype=torch.int64, device=dev),
-                 stream=torch.cuda.Stream(device=dev), ms=[])
-        if kind == "batch" and roots.size:
-            c["max_nbrs"] = int(max(1, nbrs[roots].max()))
-            c["plan"] = eng.plan(W, flags, n_roots=int(roots.size),
-                                 max_root_neighbors=c["max_nbrs"])
-            c["dist"] = torch.empty((roots.size, V), dtype=torch.int32, device=dev)
-        classes.append(c)
-    log(f"[rank {rank}] derive: {mine.size} roots, closure {clo.size}, buffers "
-        f"{(lev.numel() + dist.numel() * 4 + sum(c['nh'].numel() * 4 for c in classes)) / 2**30:.1f}"
-        f" GiB in {time.time() - t0:.1f}s")
+    sw = eng.sweep(mode=mode, part=rank, n_parts=world, hip_graph=args.graph != "off")
+    n = sw.n_roots
+    log(f"[rank {rank}] sweep: mode {sw.mode}, {n} roots, {sw.n_rows} rows, {sw.n_launches} "
+        f"launches, hip graph {'on' if sw.hip_graph else 'off'}, "
+        f"{sw.device_bytes / 2**30:.1f} GiB in {time.time() - t0:.1f}s")
     main_s = torch.cuda.current_stream()
+    slot = n
+    if dist_on:  # padded gather slots; every rank's root order, once
+        t = torch.tensor([n], dtype=torch.int64, device=coll_dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        slot = int(t.item())
+        rbuf = torch.full((slot,), -1, dtype=torch.int64, device=dev)
+        rbuf[:n] = torch.from_numpy(sw.roots.astype(np.int64)).to(dev)
+        groots = shard.gather_digests(rbuf.view(-1, 1).repeat(1, 3))[:, 0].cpu().numpy()
+        groots = groots.reshape(world, slot)
+    gbuf = torch.zeros((max(1, slot), 3), dtype=torch.int64, device=dev)
+    gathered = {}
 
-    def phase1(s_):
-        eng.levels_dev(d_clo.data_ptr(), clo.size, lev.data_ptr(), d_dist=dist.data_ptr(),
-                       d_lev_digest=ldg.data_ptr(), stream=s_.cuda_stream)
-
-    def phase2(c, s_):
-        if c["n"] and c["kind"] == "batch":
-            eng.run_dev(c["d"].data_ptr(), c["n"], c["W"], flags=flags,
-                        d_dist=c["dist"].data_ptr(), d_nh=c["nh"].data_ptr(),
-                        d_digest=c["dig"].data_ptr(), stream=s_.cuda_stream,
-                        max_root_neighbors=c["max_nbrs"])
-        elif c["n"]:
-            eng.nh_derive_dev(c["d"].data_ptr(), c["n"], c["W"], lev.data_ptr(), d_pos.data_ptr(),
-                              c["nh"].data_ptr(), d_lev_digest=ldg.data_ptr(),
-                              d_digest=c["dig"].data_ptr(), max_root_neighbors=c["cap"],
-                              stream=s_.cuda_stream)
-
-    p1_ms = []
-
-    def launches(timed, base, tm=True):
-        """One step's launches, rooted at stream `base` (tm: timing events)."""
-        ev = (lambda: torch.cuda.Event(enable_timing=True)) if tm else torch.cuda.Event
-        a_, b_ = ev(), ev()
-        a_.record(base)
-        done = []
-        for c in classes:  # batch classes start with the step (no level rows needed)
-            if c["kind"] == "batch":
-                cs = c["stream"]
-                cs.wait_event(a_)
-                e0, e1 = ev(), ev()
-                e0.record(cs)
-                phase2(c, cs)
-                e1.record(cs)
-                done.append(e1)
-                if timed:
-                    c["ms"].append((e0, e1))
-        phase1(base)
-        b_.record(base)
-        for c in sorted(classes, key=lambda c: -c["W"] * c["n"]):
-            if c["kind"] == "batch":
-                continue
-            # OPENR_DERIVE_SERIAL=1: the classes one after another on the main
-            # stream (experiment; default: each on its own stream)
-            cs = base if os.environ.get("OPENR_DERIVE_SERIAL") == "1" else c["stream"]
-            cs.wait_event(b_)
-            e0, e1 = ev(), ev()
-            e0.record(cs)
-            phase2(c, cs)
-            e1.record(cs)
-            done.append(e1)
-            if timed:
-                c["ms"].append((e0, e1))
-        for e in done:
-            base.wait_event(e)
-        if timed:
-            p1_ms.append((a_, b_))
-
-    graph = None
-
-    def step(timed):
-        if graph is not None:
-            graph.replay()
-        else:
-            launches(timed, main_s)
+    def step():
+        sw.run(main_s.cuda_stream)
         if dist_on:
-            for c in classes:
-                c["gathered"] = shard.gather_digests(c["dig"])
+            sw.digests_dev(gbuf.data_ptr(), main_s.cuda_stream)
+            gathered["g"] = shard.gather_digests(gbuf)
 
     for _ in range(args.warmup):
-        step(False)
+        step()
     torch.cuda.synchronize()
     eng.sync(main_s.cuda_stream)
-    graph_note = "off"
-    if args.graph != "off":
-        # the whole step (levels rounds, memsets, the width classes on their
-        # streams) as one HIP graph: small topologies are launch-bound
-        try:
-            # one eager step on the capture stream first: the engine's scratch
-            # is per stream and must exist before capture (no allocation inside)
-            cap_s = torch.cuda.Stream(device=dev)
-            cap_s.wait_stream(main_s)
-            with torch.cuda.stream(cap_s):
-                launches(False, cap_s, tm=False)
-            cap_s.synchronize()
-            eng.sync(cap_s.cuda_stream)
-            g_ = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g_, stream=cap_s):
-                launches(False, cap_s, tm=False)
-            torch.cuda.synchronize()
-            graph = g_
-            graph.replay()
-            torch.cuda.synchronize()
-            eng.sync(main_s.cuda_stream)
-            graph_note = "on"
-        except Exception as e:  # capture not supported here: eager launches
-            graph = None
-            graph_note = f"off (capture failed: {str(e)[:120]})"
-            torch.cuda.synchronize()
-            log(f"[rank {rank}] graph capture failed, eager launches: {e}")
+    # every digest the runs write set to 0xFF: a timed run that computed
+    # nothing (an empty graph replay) fails the parity check below
+    sw.poison(main_s.cuda_stream)
+    gbuf.fill_(-1)
+    torch.cuda.synchronize()
     if dist_on:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for _ in range(args.steps):
-        step(True)
+        step()
     torch.cuda.synchronize()
     if dist_on:
         torch.distributed.barrier()
@@ -610,618 +479,88 @@ def derive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on,
 
     # digests of the last timed step by root id (rank 0 sees every rank's)
     step_digest = {}
-    for c in classes:
-        if dist_on:
-            g = c["gathered"].cpu().numpy().view(np.uint64).reshape(world, -1, 3)
-            for r in range(world):
-                for j, root in enumerate(cls_all[r][c["cap"]]):
+    if dist_on:
+        g = gathered["g"].cpu().numpy().view(np.uint64).reshape(world, slot, 3)
+        for r in range(world):
+            for j, root in enumerate(groots[r]):
+                if root >= 0:
                     step_digest[int(root)] = g[r, j]
-        else:
-            d = c["dig"].cpu().numpy().view(np.uint64)
-            for j, root in enumerate(c["roots"]):
-                step_digest[int(root)] = d[j]
-
-    # isolated launches (alone on one stream, HIP events on it): phase 1 and
-    # each class's phase 2; the roofline of the dominant one
-    iso_s = torch.cuda.Stream(device=dev)
-
-    def iso(fn):
-        ms = []
-        with torch.cuda.stream(iso_s):
-            for _ in range(args.iso_reps + 1):
-                a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                a_.record(iso_s)
-                fn(iso_s)
-                b_.record(iso_s)
-                b_.synchronize()
-                ms.append(a_.elapsed_time(b_))
-        return float(np.median(ms[1:])) if len(ms) > 1 else float(ms[0])
-
-    p1_iso = iso(phase1)
-    for c in classes:
-        c["iso_ms"] = iso(lambda s_, c=c: phase2(c, s_)) if c["n"] else 0.0
-    eng.sync(iso_s.cuda_stream)
-    scans = -(-clo.size // 64) * (4 * E + 4 * (V + 1))
-    units = [{"launch": "levels", "kernel": "ospf_levels_dev (distance-only multi-source BFS: "
-              "msbfs init + level/settle pairs + levrows)", "roots_per_launch": int(clo.size),
-              "isolated_launch_ms": round(p1_iso, 3),
-              "compulsory_bytes": int(clo.size) * 4 * V + scans,
-              "traffic": pmc_traffic(args.profile_dir, "derive_levels", int(clo.size))}]
-    for c in classes:
-        if c["n"] and c["kind"] == "batch":
-            p = c["plan"]
-            units.append({"launch": f"batch_cap{c['cap']}",
-                          "kernel": f"variant {p['variant']} class launch ({c['W']} next-hop "
-                                    f"words: multi-source BFS with bit-planes)",
-                          "cap": c["cap"], "nh_words": c["W"], "roots_per_launch": c["n"],
-                          "isolated_launch_ms": round(c["iso_ms"], 3),
-                          "compulsory_bytes": compulsory_bytes(V, E, c["W"], c["n"], p["variant"],
-                                                               p["slices"], False),
-                          "traffic": pmc_traffic(args.profile_dir,
-                                                 f"variant{p['variant']}_cap{c['cap']}", c["n"])})
-        elif c["n"]:
-            units.append({"launch": f"derive_cap{c['cap']}",
-                          "kernel": f"ospf_nh_derive_dev ("
-                                    f"{'nh_derive16_kernel' if c['W'] <= 4 else 'nh_derive_wide_kernel'}"
-                                    f", {c['W']} next-hop word(s))", "cap": c["cap"], "nh_words": c["W"],
-                          "roots_per_launch": c["n"], "isolated_launch_ms": round(c["iso_ms"], 3),
-                          "compulsory_bytes": c["n"] * 4 * V * c["W"],
-                          "traffic": pmc_traffic(args.profile_dir, f"derive_cap{c['cap']}", c["n"])})
-    for u in units:
-        sec = u["isolated_launch_ms"] / 1e3
-        u["achieved"] = round(u["compulsory_bytes"] / sec / 1e9, 1)
-        u["frac"] = round(u["compulsory_bytes"] / sec / 1e9 / HBM_PEAK_GBS, 4)
-        u["traffic_over_compulsory"] = (round(u["traffic"] / u["compulsory_bytes"], 2)
-                                        if u["traffic"] else None)
-    dom = max(units, key=lambda u: u["isolated_launch_ms"])
-    step_comp = sum(c["n"] * 4 * V * (1 + c["W"]) for c in classes) + scans + sum(
-        -(-c["n"] // 64) * c["plan"]["slices"] * (4 * E + 4 * (V + 1))
-        for c in classes if c["kind"] == "batch" and c["n"])
-    step_s = dt / args.steps
-    roofline = {
-        "bound": "hbm", "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": dom["frac"], "traffic": dom["traffic"], "kernel": dom["kernel"],
-        "roots_per_launch": dom["roots_per_launch"], "avg_launch_ms": dom["isolated_launch_ms"],
-        "compulsory_bytes": dom["compulsory_bytes"],
-        "traffic_over_compulsory": dom["traffic_over_compulsory"], "launches": units,
-        "step_compulsory_bytes": step_comp,
-        "step_frac": round(step_comp / step_s / 1e9 / HBM_PEAK_GBS, 4),
-        "note": "achieved = compulsory bytes of the dominant launch / its isolated time (HIP "
-                "events on its stream, alone): levels = dist rows written (4V per run) + one "
-                "neighbour-id + offset scan per 64-root traversal; derive = next-hop rows "
-                "written (4VW per run); the byte level rows are intermediate (traffic, not "
-                "compulsory). step_frac = (dist + next-hop rows of every root + scans) / "
-                "ms_per_step. traffic = measured HBM bytes per launch (rocprofv3 FETCH_SIZE x2 "
-                "+ WRITE_SIZE, profiles/<round>/pmc_traffic.json)",
-    }
-    p1_avg = float(np.mean([a_.elapsed_time(b_) for a_, b_ in p1_ms])) if p1_ms else None
-    classes_cfg = [{"launch": "levels", "roots_this_rank": int(clo.size),
-                    "closure_over_roots": round(clo.size / max(1, mine.size), 4),
-                    "avg_launch_ms": round(p1_avg, 3) if p1_avg is not None else None,
-                    "isolated_launch_ms": round(p1_iso, 3), "hip_graph": graph_note}]
-    for c in classes:
-        classes_cfg.append({"cap": c["cap"], "nh_words": c["W"], "roots_this_rank": c["n"],
-                            "path": c["kind"],
-                            "avg_launch_ms": round(float(np.mean(
-                                [a_.elapsed_time(b_) for a_, b_ in c["ms"]])), 3) if c["ms"] else None,
-                            "isolated_launch_ms": round(c["iso_ms"], 3)})
-    report(args, stream, names, perm, step_digest, dt, V * args.steps, E, desc, 0, V, world, rank,
-           dist_on, backend, V, classes_cfg, roofline, "strong", "derive")
-    if dist_on:
-        torch.distributed.destroy_process_group()
-
-
-def wcover_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, dev, backend,
-                coll_dev, leaf):
-    """All-sources step on a weighted graph, cover SPF form. (A) dist rows of
-    the cover (nodes outside the independent leaf set: the fabric and spine
-    switches) by the contracted-graph SPF (spf_cover.hip); (B) the leaves'
-    dist + next-hop rows from those rows (ospf_wderive_dev); (C) the next hops
-    of cover roots with <= 128 neighbours from their own and their
-    neighbours' rows (ospf_wderive_wide_dev). Wider cover roots (spines) run
-    the per-root batch kernel on their own stream from the step's start. A
-    rank owns a pod / plane block (fabric) or class slices, and computes the
-    rows its own roots' derivations read."""
-    rp, col = csr["row_ptr"], csr["col"]
-    perm = np.random.default_rng(SEED).permutation(V).astype(np.uint32)
-    key = shard.first_neighbor(rp, col)
-    nbrs = shard.distinct_neighbors(rp, col)
-    caps = shard.neighbor_caps(nbrs)
-    words = np.maximum(1, (nbrs + 31) // 32)
-    # cover next hops: roots sharing their largest neighbours side by side (the
-    # fabric switches of a pod share its racks' rows); OPENR_WCOVER_KEY=first
-    # groups them by their smallest neighbour instead
-    ckey = key if os.environ.get("OPENR_WCOVER_KEY") == "first" else shard.last_neighbor(rp, col)
-
-    def part(r):
-        if world == 1:
-            return perm
-        fp = shard.fabric_partition(names, world, r)
-        if fp is not None:
-            return fp
-        cls = shard.make_classes(perm, caps, V, key)
-        return np.concatenate([c.roots[slice(*shard.rank_slice(c.roots.size, world, r))]
-                               for c in cls])
-
-    def plan(p):
-        p = np.asarray(p, np.uint32)
-        own_l = shard.locality_order(p[leaf[p]], key)
-        own_c = p[~leaf[p]]
-        c_der = own_c[(nbrs[own_c] <= 2048)]         # (C): next hops derived
-        c_wide = own_c[(nbrs[own_c] > 2048)]         # per-root batch kernel
-        nb_c = shard.closure(c_der, rp, col)
-        need_l = np.union1d(own_l, nb_c[leaf[nb_c]]).astype(np.uint32)
-        need_l = shard.locality_order(need_l, key)
-        cl = shard.closure(need_l, rp, col)
-        cover_a = np.union1d(np.union1d(own_c, cl[~leaf[cl]]), nb_c[~leaf[nb_c]]).astype(np.uint32)
-        return dict(own_l=own_l, c_der=c_der, c_wide=c_wide, need_l=need_l, cover_a=cover_a)
-
-    parts = [part(r) for r in range(world)]
-    plans = [plan(p) for p in parts]
-    P = plans[rank]
-    cover_a, need_l = P["cover_a"], P["need_l"]
-    nA, nL = int(cover_a.size), int(need_l.size)
-    pos = np.full(V, 0xFFFFFFFF, np.uint32)
-    pos[cover_a] = np.arange(nA, dtype=np.uint32)
-    pos[need_l] = nA + np.arange(nL, dtype=np.uint32)
-    t0 = time.time()
-    slab = torch.empty((max(1, nA + nL), V), dtype=torch.int32, device=dev)
-    d_pos = torch.from_numpy(pos.view(np.int32)).to(dev)
-    d_a = torch.from_numpy(cover_a.view(np.int32)).to(dev)
-    d_l = torch.from_numpy(need_l.view(np.int32)).to(dev)
-    lnh = torch.empty((max(1, nL), V), dtype=torch.int32, device=dev)
-    ldg = torch.zeros((max(1, nL), 3), dtype=torch.int64, device=dev)
-    kmax = int(nbrs[need_l].max()) if nL else 0
-    flags = N.OSPF_WANT_DIST | N.OSPF_WANT_NH | N.OSPF_WANT_DIGEST
-    cls = []  # (C) classes by next-hop words, and the wide batch class
-    for W in sorted(set(words[P["c_der"]].tolist())):
-        roots = shard.locality_order(P["c_der"][words[P["c_der"]] == W], ckey)
-        cls.append(dict(kind="derive", W=W, roots=roots, n=int(roots.size),
-                        d=torch.from_numpy(roots.view(np.int32)).to(dev),
-                        nh=torch.empty((roots.size, V, W), dtype=torch.int32, device=dev),
-                        dig=torch.zeros((roots.size, 3), dtype=torch.int64, device=dev), ms=[],
-                        side=torch.cuda.Stream(device=dev)))
-    if P["c_wide"].size:
-        roots = shard.locality_order(P["c_wide"], key)
-        W = int(words[roots].max())
-        mx = int(nbrs[roots].max())
-        cls.append(dict(kind="batch", W=W, roots=roots, n=int(roots.size), max_nbrs=mx,
-                        plan=eng.plan(W, flags, n_roots=int(roots.size), max_root_neighbors=mx),
-                        d=torch.from_numpy(roots.view(np.int32)).to(dev),
-                        nh=torch.empty((roots.size, V, W), dtype=torch.int32, device=dev),
-                        dist=torch.empty((roots.size, V), dtype=torch.int32, device=dev),
-                        dig=torch.zeros((roots.size, 3), dtype=torch.int64, device=dev),
-                        stream=torch.cuda.Stream(device=dev), ms=[]))
-    log(f"[rank {rank}] wcover: {parts[rank].size} roots: cover SPF {nA}, leaves {nL} "
-        f"(<= {kmax} neighbours), cover next hops {[(c['kind'], c['W'], c['n']) for c in cls]}, "
-        f"buffers {(slab.numel() + lnh.numel() + sum(c['nh'].numel() for c in cls)) * 4 / 2**30:.1f}"
-        f" GiB in {time.time() - t0:.1f}s")
-    main_s = torch.cuda.current_stream()
-
-    def stage_a(s_):
-        eng.cover_dist_dev(d_a.data_ptr(), nA, slab.data_ptr(), stream=s_.cuda_stream)
-
-    def stage_b(s_):
-        if nL:
-            eng.wderive_dev(d_l.data_ptr(), nL, slab.data_ptr(), d_pos.data_ptr(),
-                            slab[nA].data_ptr(), d_nh=lnh.data_ptr(), d_digest=ldg.data_ptr(),
-                            max_root_neighbors=kmax, stream=s_.cuda_stream)
-
-    def stage_c(c, s_):
-        if c["kind"] == "derive":
-            eng.wderive_wide_dev(c["d"].data_ptr(), c["n"], c["W"], slab.data_ptr(),
-                                 d_pos.data_ptr(), c["nh"].data_ptr(),
-                                 d_digest=c["dig"].data_ptr(), stream=s_.cuda_stream)
-        else:
-            eng.run_dev(c["d"].data_ptr(), c["n"], c["W"], flags=flags,
-                        d_dist=c["dist"].data_ptr(), d_nh=c["nh"].data_ptr(),
-                        d_digest=c["dig"].data_ptr(), stream=s_.cuda_stream,
-                        max_root_neighbors=c["max_nbrs"])
-
-    # owned roots' digests, gathered in a padded slot per rank
-    def owned_order(p, pl):
-        own = np.zeros(V, bool)
-        own[p] = True
-        lo = pl["need_l"][own[pl["need_l"]]]
-        co = [shard.locality_order(pl["c_der"][words[pl["c_der"]] == W], ckey)
-              for W in sorted(set(words[pl["c_der"]].tolist()))]
-        if pl["c_wide"].size:
-            co.append(shard.locality_order(pl["c_wide"], key))
-        return np.concatenate([lo] + co) if (lo.size or co) else lo
-
-    owned = [owned_order(p, pl) for p, pl in zip(parts, plans)]
-    slot = max(o.size for o in owned)
-    gbuf = torch.zeros((slot, 3), dtype=torch.int64, device=dev)
-    own_l_idx = torch.from_numpy(np.nonzero(np.isin(need_l, parts[rank]))[0].astype(np.int64)).to(dev)
-    stage_ms, gathered = {"A": [], "B": [], "C": []}, {}
-
-    def step(timed):
-        a0 = torch.cuda.Event(enable_timing=True)
-        a0.record(main_s)
-        done = []
-        for c in cls:  # wide cover roots: their own batch, from the start
-            if c["kind"] == "batch":
-                c["stream"].wait_event(a0)
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(c["stream"])
-                stage_c(c, c["stream"])
-                e1.record(c["stream"])
-                done.append(e1)
-                if timed:
-                    c["ms"].append((e0, e1))
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-        stage_a(main_s)
-        ev[1].record(main_s)
-        # wide cover roots (spines) need only the cover rows: their derivation
-        # runs beside the leaves' and the narrow cover roots'
-        for c in cls:
-            if c["kind"] == "derive" and c["W"] > 4:
-                c["side"].wait_event(ev[1])
-                stage_c(c, c["side"])
-                e1 = torch.cuda.Event()
-                e1.record(c["side"])
-                done.append(e1)
-        stage_b(main_s)
-        ev[2].record(main_s)
-        for c in cls:
-            if c["kind"] == "derive" and c["W"] <= 4:
-                stage_c(c, main_s)
-        ev[3].record(main_s)
-        for e in done:
-            main_s.wait_event(e)
-        if timed:
-            stage_ms["A"].append((a0, ev[1]))
-            stage_ms["B"].append((ev[1], ev[2]))
-            stage_ms["C"].append((ev[2], ev[3]))
-        if dist_on:
-            parts_ = [torch.index_select(ldg, 0, own_l_idx)] + [c["dig"] for c in cls]
-            cat = torch.cat(parts_)
-            gbuf[: cat.shape[0]].copy_(cat)
-            gathered["g"] = shard.gather_digests(gbuf)
-
-    for _ in range(args.warmup):
-        step(False)
-    torch.cuda.synchronize()
-    eng.sync(main_s.cuda_stream)
-    if dist_on:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
-    torch.cuda.synchronize()
-    if dist_on:
-        torch.distributed.barrier()
-    dt = time.perf_counter() - t_start
-    eng.sync(main_s.cuda_stream)
-    if dist_on:
-        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt = float(t.item())
-
-    step_digest = {}
-    if dist_on:
-        g = gathered["g"].cpu().numpy().view(np.uint64).reshape(world, slot, 3)
-        for r, o in enumerate(owned):
-            for j, root in enumerate(o):
-                step_digest[int(root)] = g[r, j]
     else:
-        ld = ldg.cpu().numpy().view(np.uint64)
-        for j, root in enumerate(need_l):
-            step_digest[int(root)] = ld[j]
-        for c in cls:
-            d = c["dig"].cpu().numpy().view(np.uint64)
-            for j, root in enumerate(c["roots"]):
-                step_digest[int(root)] = d[j]
-
-    iso_s = torch.cuda.Stream(device=dev)
-
-    def iso(fn):
-        ms = []
-        with torch.cuda.stream(iso_s):
-            for _ in range(args.iso_reps + 1):
-                a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                a_.record(iso_s)
-                fn(iso_s)
-                b_.record(iso_s)
-                b_.synchronize()
-                ms.append(a_.elapsed_time(b_))
-        return float(np.median(ms[1:])) if len(ms) > 1 else float(ms[0])
-
-    scan_c = 8 * E + 4 * (V + 1)  # one weighted CSR scan (neighbour + metric words)
-    units = [{"launch": "cover_spf", "kernel": "ospf_cover_dist_dev (cover_spf_kernel: "
-              "contracted-graph Dial, LDS-resident distances)", "roots_per_launch": nA,
-              "isolated_launch_ms": round(iso(stage_a), 3),
-              "compulsory_bytes": nA * 4 * V + scan_c,
-              "traffic": pmc_traffic(args.profile_dir, "cover_spf", nA)}]
-    if nL:
-        units.append({"launch": "wderive", "kernel": "ospf_wderive_dev (wderive_kernel: leaf "
-                      "rows from the cover rows)", "roots_per_launch": nL,
-                      "isolated_launch_ms": round(iso(stage_b), 3),
-                      "compulsory_bytes": nL * 8 * V + int(np.setdiff1d(shard.closure(
-                          need_l, rp, col), need_l).size) * 4 * V,
-                      "traffic": pmc_traffic(args.profile_dir, "wderive", nL)})
-    for c in cls:
-        c["iso_ms"] = iso(lambda s_, c=c: stage_c(c, s_))
-        if c["kind"] == "derive":
-            units.append({"launch": f"wderive_wide_w{c['W']}", "kernel": f"ospf_wderive_wide_dev "
-                          f"(wderive_wide_kernel<{c['W']}>)", "roots_per_launch": c["n"],
-                          "isolated_launch_ms": round(c["iso_ms"], 3),
-                          "compulsory_bytes": c["n"] * 4 * V * c["W"],
-                          "traffic": pmc_traffic(args.profile_dir, f"wderive_wide_w{c['W']}",
-                                                 c["n"])})
-        else:
-            p = c["plan"]
-            units.append({"launch": f"cover_batch_w{c['W']}",
-                          "kernel": f"variant {p['variant']} class launch ({c['W']} next-hop words)",
-                          "roots_per_launch": c["n"], "isolated_launch_ms": round(c["iso_ms"], 3),
-                          "compulsory_bytes": compulsory_bytes(V, E, c["W"], c["n"], p["variant"],
-                                                               p["slices"], True),
-                          "traffic": pmc_traffic(args.profile_dir,
-                                                 f"variant{p['variant']}_cap{c['W'] * 32}", c["n"])})
-    eng.sync(iso_s.cuda_stream)
-    for u in units:
-        sec = u["isolated_launch_ms"] / 1e3
-        u["achieved"] = round(u["compulsory_bytes"] / sec / 1e9, 1)
-        u["frac"] = round(u["compulsory_bytes"] / sec / 1e9 / HBM_PEAK_GBS, 4)
-        u["traffic_over_compulsory"] = (round(u["traffic"] / u["compulsory_bytes"], 2)
-                                        if u["traffic"] else None)
-    dom = max(units, key=lambda u: u["isolated_launch_ms"])
-    step_comp = sum(u["compulsory_bytes"] for u in units)
-    step_s = dt / args.steps
-    roofline = {
-        "bound": "hbm", "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": dom["frac"], "traffic": dom["traffic"], "kernel": dom["kernel"],
-        "roots_per_launch": dom["roots_per_launch"], "avg_launch_ms": dom["isolated_launch_ms"],
-        "compulsory_bytes": dom["compulsory_bytes"],
-        "traffic_over_compulsory": dom["traffic_over_compulsory"], "launches": units,
-        "step_compulsory_bytes": step_comp,
-        "step_frac": round(step_comp / step_s / 1e9 / HBM_PEAK_GBS, 4),
-        "note": "achieved = compulsory bytes of the dominant launch / its isolated time: "
-                "cover_spf = dist rows written + one weighted CSR scan; wderive = leaf dist + "
-                "next-hop rows + the cover rows read once; wderive_wide = next-hop rows; "
-                "cover_batch = rows + one weighted CSR scan per run",
-    }
-    cfg = [{"launch": k, "avg_launch_ms": round(float(np.mean([a_.elapsed_time(b_) for a_, b_ in v])), 3)}
-           for k, v in stage_ms.items() if v]
-    cfg += [{"launch": f"cover_batch_w{c['W']}", "roots_this_rank": c["n"],
-             "avg_launch_ms": round(float(np.mean([a_.elapsed_time(b_) for a_, b_ in c["ms"]])), 3)}
-            for c in cls if c["kind"] == "batch"]
-    report(args, stream, names, perm, step_digest, dt, V * args.steps, E, desc, 0, V, world, rank,
-           dist_on, backend, V, cfg, roofline, "strong", "wcover")
-    if dist_on:
-        torch.distributed.destroy_process_group()
-
-
-def wderive_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, dev, backend,
-                 coll_dev, weighted):
-    """All-sources step on a weighted graph (or any graph outside derive
-    mode's unit-metric contract). Cover roots (a vertex cover S: on the
-    fabric the fabric and spine switches) run the per-root SPF kernel chosen
-    by the engine (variant 7 here), one launch per width class on its own
-    stream, their dist rows into one slab; then the leaf roots (the
-    independent set I = V \\ S: the racks) are derived from those rows by
-    ospf_wderive_dev (spf_wderive.hip). A rank owns a pod / plane block
-    (fabric) or class slices, and runs the cover rows its leaves need."""
-    rp, col = csr["row_ptr"], csr["col"]
-    perm = np.random.default_rng(SEED).permutation(V).astype(np.uint32)
-    key = shard.first_neighbor(rp, col)
-    nbrs = shard.distinct_neighbors(rp, col)
-    caps = shard.neighbor_caps(nbrs)
-    leaf = shard.leaf_set(rp, col)
-
-    def part(r):
-        if world == 1:
-            return perm
-        fp = shard.fabric_partition(names, world, r)
-        if fp is not None:
-            return fp
-        cls = shard.make_classes(perm, caps, V, key)
-        return np.concatenate([c.roots[slice(*shard.rank_slice(c.roots.size, world, r))]
-                               for c in cls])
-
-    parts = [part(r) for r in range(world)]
-    plans = [shard.wderive_plan(p, leaf, rp, col) for p in parts]
-    cover, lr = plans[rank]
-    lr = shard.locality_order(lr, key)  # racks of a pod adjacent: one run per pod
-    flags = N.OSPF_WANT_DIST | N.OSPF_WANT_NH | N.OSPF_WANT_DIGEST
-    t0 = time.time()
-    classes, off = [], 0
-    for cap in sorted(set(caps[cover].tolist())):
-        roots = shard.locality_order(cover[caps[cover] == cap], key)
-        W = max(1, cap // 32) if cap > 16 else 1
-        mx = int(max(1, nbrs[roots].max()))
-        classes.append(dict(cap=cap, W=W, roots=roots, n=int(roots.size), off=off,
-                            d=torch.from_numpy(roots.view(np.int32)).to(dev),
-                            nh=torch.empty((roots.size, V, W), dtype=torch.int32, device=dev),
-                            max_nbrs=mx,
-                            plan=eng.plan(W, flags, n_roots=int(roots.size),
-                                          max_root_neighbors=mx),
-                            stream=torch.cuda.Stream(device=dev), ms=[]))
-        off += roots.size
-    corder = np.concatenate([c["roots"] for c in classes]) if classes else \
-        np.zeros(0, np.uint32)
-    pos = np.full(V, 0xFFFFFFFF, np.uint32)
-    pos[corder] = np.arange(corder.size, dtype=np.uint32)
-    cdist = torch.empty((max(1, corder.size), V), dtype=torch.int32, device=dev)
-    d_pos = torch.from_numpy(pos.view(np.int32)).to(dev)
-    nl = int(lr.size)
-    kmax = int(nbrs[lr].max()) if nl else 0
-    d_lr = torch.from_numpy(lr.view(np.int32)).to(dev)
-    ldist = torch.empty((max(1, nl), V), dtype=torch.int32, device=dev)
-    lnh = torch.empty((max(1, nl), V), dtype=torch.int32, device=dev)
-    dig = torch.zeros((corder.size + nl, 3), dtype=torch.int64, device=dev)
-    log(f"[rank {rank}] wderive: {parts[rank].size} roots = {nl} leaves (<= {kmax} "
-        f"neighbours) + cover {corder.size} ({[(c['cap'], c['n'], c['plan']['variant']) for c in classes]}), "
-        f"buffers {(cdist.numel() + ldist.numel() + lnh.numel() + sum(c['nh'].numel() for c in classes)) * 4 / 2**30:.1f}"
-        f" GiB in {time.time() - t0:.1f}s")
-    main_s = torch.cuda.current_stream()
-
-    def cover_launch(c, s_):
-        eng.run_dev(c["d"].data_ptr(), c["n"], c["W"], flags=flags,
-                    d_dist=cdist[c["off"]].data_ptr(), d_nh=c["nh"].data_ptr(),
-                    d_digest=dig[c["off"]].data_ptr(), stream=s_.cuda_stream,
-                    max_root_neighbors=c["max_nbrs"])
-
-    def leaf_launch(s_):
-        if nl:
-            eng.wderive_dev(d_lr.data_ptr(), nl, cdist.data_ptr(), d_pos.data_ptr(),
-                            ldist.data_ptr(), d_nh=lnh.data_ptr(),
-                            d_digest=dig[corder.size].data_ptr(), max_root_neighbors=kmax,
-                            stream=s_.cuda_stream)
-
-    # owned roots' digest rows (the cover rows a rank adds for its leaves are
-    # not its roots), gathered in a padded slot per rank
-    def owned_rows(p, cv, lv):
-        own = np.zeros(V, bool)
-        own[p] = True
-        co = np.concatenate([shard.locality_order(cv[caps[cv] == cap], key)
-                             for cap in sorted(set(caps[cv].tolist()))]) if cv.size else cv
-        return co[own[co]], shard.locality_order(lv, key)
-
-    owned = [owned_rows(p, *pl) for p, pl in zip(parts, plans)]
-    slot = max(a.size + b.size for a, b in owned)
-    own_c, _ = owned[rank]
-    idx = np.concatenate([pos[own_c], corder.size + np.arange(nl)]).astype(np.int64)
-    d_idx = torch.from_numpy(idx).to(dev)
-    gbuf = torch.zeros((slot, 3), dtype=torch.int64, device=dev)
-    leaf_ms, gathered = [], {}
-
-    def step(timed):
-        a_ = torch.cuda.Event(enable_timing=True)
-        a_.record(main_s)
-        done = []
-        for c in classes:
-            cs = c["stream"]
-            cs.wait_event(a_)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(cs)
-            cover_launch(c, cs)
-            e1.record(cs)
-            done.append(e1)
-            if timed:
-                c["ms"].append((e0, e1))
-        for e in done:
-            main_s.wait_event(e)
-        l0, l1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        l0.record(main_s)
-        leaf_launch(main_s)
-        l1.record(main_s)
-        if timed:
-            leaf_ms.append((l0, l1))
-        if dist_on:
-            torch.index_select(dig, 0, d_idx, out=gbuf[: idx.size])
-            gathered["g"] = shard.gather_digests(gbuf)
-
-    for _ in range(args.warmup):
-        step(False)
-    torch.cuda.synchronize()
-    eng.sync(main_s.cuda_stream)
-    if dist_on:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
-    torch.cuda.synchronize()
-    if dist_on:
-        torch.distributed.barrier()
-    dt = time.perf_counter() - t_start
-    eng.sync(main_s.cuda_stream)
-    if dist_on:
-        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt = float(t.item())
-
-    step_digest = {}
-    if dist_on:
-        g = gathered["g"].cpu().numpy().view(np.uint64).reshape(world, slot, 3)
-        for r, (a, b) in enumerate(owned):
-            for j, root in enumerate(np.concatenate([a, b])):
-                step_digest[int(root)] = g[r, j]
-    else:
-        d = dig.cpu().numpy().view(np.uint64)
-        for j, root in enumerate(np.concatenate([corder, lr])):
+        sw.digests_dev(gbuf.data_ptr(), main_s.cuda_stream)
+        d = gbuf.cpu().numpy().view(np.uint64)
+        for j, root in enumerate(sw.roots):
             step_digest[int(root)] = d[j]
 
-    iso_s = torch.cuda.Stream(device=dev)
-
-    def iso(fn):
-        ms = []
-        with torch.cuda.stream(iso_s):
-            for _ in range(args.iso_reps + 1):
-                a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                a_.record(iso_s)
-                fn(iso_s)
-                b_.record(iso_s)
-                b_.synchronize()
-                ms.append(a_.elapsed_time(b_))
-        return float(np.median(ms[1:])) if len(ms) > 1 else float(ms[0])
-
+    # every launch alone on its stream (HIP events there, inside the library)
+    prof = sw.profile(args.iso_reps)
     units = []
-    for c in classes:
-        c["iso_ms"] = iso(lambda s_, c=c: cover_launch(c, s_))
-        p = c["plan"]
-        units.append({"launch": f"cover_cap{c['cap']}",
-                      "kernel": f"variant {p['variant']} class launch ({c['W']} next-hop words)",
-                      "cap": c["cap"], "nh_words": c["W"], "roots_per_launch": c["n"],
-                      "isolated_launch_ms": round(c["iso_ms"], 3),
-                      "compulsory_bytes": compulsory_bytes(V, E, c["W"], c["n"], p["variant"],
-                                                           p["slices"], weighted),
-                      "traffic": pmc_traffic(args.profile_dir,
-                                             f"variant{p['variant']}_cap{c['cap']}", c["n"])})
-    if nl:
-        l_iso = iso(leaf_launch)
-        n_src = int(np.setdiff1d(shard.closure(lr, rp, col), lr).size)  # cover rows read
-        units.append({"launch": "wderive", "kernel": "ospf_wderive_dev (wderive_kernel: leaf "
-                      "rows from neighbours' dist rows)", "roots_per_launch": nl,
-                      "isolated_launch_ms": round(l_iso, 3),
-                      "compulsory_bytes": nl * 8 * V + n_src * 4 * V,
-                      "traffic": pmc_traffic(args.profile_dir, "wderive", nl)})
-    eng.sync(iso_s.cuda_stream)
-    for u in units:
-        sec = u["isolated_launch_ms"] / 1e3
-        u["achieved"] = round(u["compulsory_bytes"] / sec / 1e9, 1)
-        u["frac"] = round(u["compulsory_bytes"] / sec / 1e9 / HBM_PEAK_GBS, 4)
-        u["traffic_over_compulsory"] = (round(u["traffic"] / u["compulsory_bytes"], 2)
-                                        if u["traffic"] else None)
+    for p in prof:
+        sec = p["ms_median"] / 1e3
+        tr = pmc_traffic(args.profile_dir, p["name"], p["n_roots"])
+        units.append({"launch": p["name"], "kernel": p["kernel"], "roots_per_launch": p["n_roots"],
+                      "nh_words": p["nh_words"], "isolated_launch_ms": round(p["ms_median"], 3),
+                      "isolated_launch_ms_min": round(p["ms_min"], 3),
+                      "compulsory_bytes": p["compulsory_bytes"],
+                      "achieved": round(p["compulsory_bytes"] / sec / 1e9, 1),
+                      "frac": round(p["compulsory_bytes"] / sec / 1e9 / HBM_PEAK_GBS, 4),
+                      "traffic": tr,
+                      "traffic_over_compulsory": round(tr / p["compulsory_bytes"], 2)
+                      if tr else None})
     dom = max(units, key=lambda u: u["isolated_launch_ms"])
-    step_comp = sum(u["compulsory_bytes"] for u in units)
     step_s = dt / args.steps
     roofline = {
         "bound": "hbm", "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": dom["frac"], "traffic": dom["traffic"], "kernel": dom["kernel"],
-        "roots_per_launch": dom["roots_per_launch"], "avg_launch_ms": dom["isolated_launch_ms"],
-        "compulsory_bytes": dom["compulsory_bytes"],
+        "launch": dom["launch"], "roots_per_launch": dom["roots_per_launch"],
+        "avg_launch_ms": dom["isolated_launch_ms"], "compulsory_bytes": dom["compulsory_bytes"],
         "traffic_over_compulsory": dom["traffic_over_compulsory"], "launches": units,
-        "step_compulsory_bytes": step_comp,
-        "step_frac": round(step_comp / step_s / 1e9 / HBM_PEAK_GBS, 4),
-        "note": "achieved = compulsory bytes of the dominant launch / its isolated time: cover "
-                "classes = dist + next-hop rows written + one weighted CSR scan per run; "
-                "wderive = leaf dist + next-hop rows written + the cover rows read once",
+        "step_compulsory_bytes": sw.step_compulsory_bytes,
+        "step_frac": round(sw.step_compulsory_bytes / step_s / 1e9 / HBM_PEAK_GBS, 4),
+        "note": "achieved = compulsory bytes of the dominant launch / its isolated time (median "
+                "of HIP-event-timed launches alone on its stream, ospf_sweep_profile): levels = "
+                "dist rows written (4V per run) + one neighbour-id + offset scan per 128-root "
+                "traversal; derive = next-hop rows written (4VW per run); cover_spf = dist rows "
+                "+ one weighted CSR scan; wderive = leaf dist + next-hop rows + cover rows read "
+                "once. Level rows are intermediate (traffic, not compulsory). step_frac = the "
+                "sweep's compulsory bytes / ms_per_step. traffic = measured HBM bytes per launch "
+                "(rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/<round>/pmc_traffic.json)",
     }
-    classes_cfg = [{"cap": c["cap"], "nh_words": c["W"], "roots_this_rank": c["n"],
-                    "path": f"cover (variant {c['plan']['variant']})",
-                    "avg_launch_ms": round(float(np.mean([a_.elapsed_time(b_) for a_, b_ in c["ms"]])), 3),
-                    "isolated_launch_ms": round(c["iso_ms"], 3)} for c in classes]
-    if nl:
-        classes_cfg.append({"launch": "wderive", "roots_this_rank": nl, "max_neighbours": kmax,
-                            "avg_launch_ms": round(float(np.mean(
-                                [a_.elapsed_time(b_) for a_, b_ in leaf_ms])), 3),
-                            "isolated_launch_ms": round(l_iso, 3)})
-    report(args, stream, names, perm, step_digest, dt, V * args.steps, E, desc, 0, V, world, rank,
-           dist_on, backend, V, classes_cfg, roofline, "strong", "wderive")
+    cfg = {"mode": sw.mode, "hip_graph": sw.hip_graph, "roots_this_rank": n,
+           "rows_this_rank": sw.n_rows, "device_bytes": sw.device_bytes,
+           "closure_over_roots": round(sw.n_rows / max(1, n), 4)}
+    sw.close()
+    report(args, stream, names, csr, step_digest, dt, V * args.steps, E, desc, 0, V, world, rank,
+           dist_on, backend, V, cfg, roofline, "strong", "sweep:" + cfg["mode"])
     if dist_on:
         torch.distributed.destroy_process_group()
 
 
-def report(args, stream, names, pool, step_digest, dt, roots_total, E, desc, n_roots, V, world,
-           rank, dist_on, backend, roots_per_step, classes_cfg, roofline, scaling, mode):
+def parity_sample(csr, V: int, k: int = 256):
+    """Role-stratified parity roots: every width class (by distinct neighbours:
+    8 / 16 / 32 x next-hop words; on a fabric racks, fabric switches and
+    spines) whole when it has <= 2k members, else k drawn with seed 0x5eed."""
+    nb = shard.distinct_neighbors(csr["row_ptr"], csr["col"])
+    caps = shard.neighbor_caps(nb)
+    rng = np.random.default_rng(SEED)
+    out = []
+    for cap in sorted(set(caps.tolist())):
+        m = np.nonzero(caps == cap)[0].astype(np.uint32)
+        out.append(m if m.size <= 2 * k else np.sort(rng.choice(m, k, replace=False)))
+    return np.concatenate(out) if out else np.zeros(0, np.uint32)
+
+
+def report(args, stream, names, csr, step_digest, dt, roots_total, E, desc, n_roots, V, world,
+           rank, dist_on, backend, roots_per_step, classes_cfg, roofline, scaling, mode,
+           pool=None):
     """CPU baseline + parity of the timed step's digests (rank 0) and the one
     JSON line."""
     spf_s = roots_total / dt
     gteps = roots_total * E / dt / 1e9
     cpu = parity = None
+    perm = np.random.default_rng(SEED).permutation(V).astype(np.uint32)
+    if pool is None:
+        pool = perm
+    strat = parity_sample(csr, V) if n_roots <= 0 else pool[:256]
     if rank == 0 and world == 1 and not args.no_cpu:
         from oracle import Oracle  # CPU baseline leg only (the restatements under oracle/)
         threads = args.cpu_threads or host_threads()
@@ -1234,16 +573,18 @@ def report(args, stream, names, pool, step_digest, dt, roots_total, E, desc, n_r
         # F100k root), so there the CSR-Dijkstra restatement is the baseline
         ref_ok = args.topology != "fabric100k-w"
         mesh = args.topology == "mesh1m"
-        csr_k = 64 if mesh else max(k, 256)  # ~2 s per M1M root on one core
-        csr_ids = [int(r) for r in pool[:csr_k]]
+        # CSR-Dijkstra restatement: the role-stratified parity roots (every
+        # spine of a fabric, 256 fabric switches, 256 racks) + the baseline's
+        csr_ids = sorted(set(int(r) for r in strat) | set(sample_ids)) if not mesh else \
+            [int(r) for r in pool[:64]]
         t1 = time.perf_counter()
         fd = o.fast_digests([names[i] for i in csr_ids], threads=threads)
         ct_fast = time.perf_counter() - t1
         csr_line = {"value": round(len(csr_ids) / ct_fast, 3), "unit": "SPF/s",
                     "cores": threads, "kind": "port",
-                    "sample": f"{len(csr_ids)} roots (permutation seed 0x5eed), CSR-Dijkstra "
-                              f"restatement (oracle/, integer ids, binary heap), {threads} "
-                              f"threads, {ct_fast:.2f}s"}
+                    "sample": f"{len(csr_ids)} roots (role-stratified parity set + the "
+                              f"baseline's), CSR-Dijkstra restatement (oracle/, integer ids, "
+                              f"binary heap), {threads} threads, {ct_fast:.2f}s"}
         checks = dict(zip(csr_ids, fd))
         if ref_ok:
             n1 = 1 if mesh else 2
@@ -1267,14 +608,22 @@ def report(args, stream, names, pool, step_digest, dt, roots_total, E, desc, n_r
                        reference_shaped="not run: its make_heap per strict improvement "
                                         "(LinkState.cpp:893) takes ~10 min per root here")
         if step_digest:
+            nb = shard.distinct_neighbors(csr["row_ptr"], csr["col"])
+            caps = shard.neighbor_caps(nb)
+            by_cap = {}
+            for r in checks:
+                by_cap[int(caps[r])] = by_cap.get(int(caps[r]), 0) + 1
             parity = {"roots": len(checks),
-                      "equal": bool(all(np.array_equal(step_digest[r], d)
+                      "roots_by_neighbour_class": {str(c_): v for c_, v in sorted(by_cap.items())},
+                      "equal": bool(all(r in step_digest and np.array_equal(step_digest[r], d)
                                         for r, d in checks.items())),
-                      "source": "digests of the last timed step vs the CPU restatement(s)"}
+                      "source": "digests of the last timed step (poisoned with 0xFF before the "
+                                "timed loop) vs the CPU restatement(s)"}
 
     if rank == 0 and dist_on and args.dist_parity > 0 and step_digest:
         from oracle import Oracle  # checker only, after the timed region
-        ids = [int(r) for r in pool[: args.dist_parity]]
+        k = min(args.dist_parity, len(strat))  # spread over the width classes
+        ids = [int(r) for r in strat[np.linspace(0, len(strat) - 1, k).astype(np.int64)]]
         want = Oracle(stream).fast_digests([names[i] for i in ids], threads=host_threads())
         parity = {"roots": len(ids),
                   "equal": bool(all(np.array_equal(step_digest[r], w) for r, w in zip(ids, want))),

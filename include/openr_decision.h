@@ -38,6 +38,9 @@ typedef struct odl_ls odl_ls;
 
 /* New LinkState for `area` whose SPF engine runs on HIP device `device`. */
 int odl_create(const char* area, int device, odl_ls** out);
+/* Same over several devices of the node (device ids, may repeat): the graph
+ * is replicated, all-sources sweeps run one root partition part per device. */
+int odl_create_multi(const char* area, const int* devices, uint32_t n, odl_ls** out);
 void odl_destroy(odl_ls* ls);
 const char* odl_last_error(const odl_ls* ls);
 void odl_free(char* p);
@@ -67,6 +70,17 @@ uint32_t odl_num_links(const odl_ls* ls);
  * odl_spf_digests: one engine batch, out[3*i] = {reached, sum_dist, hash}. */
 int odl_spf_digests(odl_ls* ls, const char* roots_nl, uint32_t n, int use_link_metric,
                     uint64_t* out);
+/* All-sources: runSpf for every node in one engine sweep (ospf_sweep_*, one
+ * partition part per device), rows resident on the devices; getSpfResult of
+ * any node then copies its rows (Decision::getDecisionRouteDb for every
+ * node, Decision.cpp:309). odl_all_sources_digests: out[3 * id] for every
+ * node id (odl_node_name order). A prefetch / route build asking for at
+ * least 256 roots and half of the nodes takes the sweep by itself.
+ * odl_sweep_stats: {sweeps, rows copied, mode (OSPF_SWEEP_*), devices,
+ * hip graph}. */
+int odl_all_sources_prefetch(odl_ls* ls, int use_link_metric);
+int odl_all_sources_digests(odl_ls* ls, int use_link_metric, uint64_t* out);
+void odl_sweep_stats(const odl_ls* ls, uint64_t* out5);
 /* Fill the getSpfResult memo for many roots with one engine batch. */
 int odl_spf_prefetch(odl_ls* ls, const char* roots_nl, uint32_t n, int use_link_metric);
 /* getKthPaths(src, d, 2) for every d, masked reruns batched on the engine;

@@ -365,6 +365,146 @@ int ospf_repair_runs(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n, uint32_
                      const ospf_change* changes, uint32_t n_changes, uint32_t* d_status,
                      void* stream);
 
+/* Take links down for a while and put back exactly what was there. The
+ * reference reruns runSpf(src, true, linksToIgnore) with every link of the
+ * k = 1 paths ignored (LinkState.cpp:802-806); an ignore set beyond one
+ * run's list (OSPF_MAX_IGNORED_PER_RUN) is applied to the device graph
+ * instead. ospf_links_mask marks the links down (like ospf_update_links);
+ * ospf_links_unmask restores their entries and the planner state (level and
+ * distance bounds, metric facts, the prepared cover graph), so the pair
+ * leaves no trace in later runs. One mask at a time. */
+int ospf_links_mask(ospf_ctx* ctx, const uint32_t* link_ids, uint32_t n, uint64_t version);
+int ospf_links_unmask(ospf_ctx* ctx);
+
+/* ---------------------------------------------------------------- sweeps
+ * All-sources sweeps: runSpf (LinkState.cpp:836-911) for every node of the
+ * graph -- or for one part of a root partition (multi-GPU) -- with every
+ * root's dist row and next-hop row written to device memory the sweep owns,
+ * plus a digest per root. The reference's all-sources use is
+ * Decision::getDecisionRouteDb(node) for every node (openr/decision/
+ * Decision.cpp:309) and `breeze decision routes --nodes all` (openr/py/openr/
+ * cli/commands/decision.py:26-48): one getSpfResult per node. A sweep owns
+ * the whole orchestration -- the path, the root order, the width classes,
+ * their streams and the HIP graph one run replays:
+ *   OSPF_SWEEP_DERIVE  unit metric or hop count, depth bound <= 123, <= 2048
+ *                      distinct neighbours per node: distance-only 128-root
+ *                      BFS over the closure of the roots, then each root's
+ *                      next hops from its neighbours' level rows
+ *                      (ospf_levels_dev + ospf_nh_derive_dev);
+ *   OSPF_SWEEP_WCOVER  link metrics: distance rows of a vertex cover by the
+ *                      contracted-graph SPF, leaf rows and cover next hops
+ *                      derived from them (ospf_cover_*, ospf_wderive*_dev);
+ *   OSPF_SWEEP_WDERIVE cover rows on the per-root batch path, leaf rows
+ *                      derived (any metric, or hop count);
+ *   OSPF_SWEEP_BATCH   per width class batches (ospf_run_batch_dev).
+ * OSPF_SWEEP_AUTO takes the first that applies, in that order. Row layout:
+ * dist u32[V] per root; next hops u32[V][W] with W = max(1, ceil(distinct
+ * neighbours / 32)) words in the bit order of ospf_root_neighbors. A sweep
+ * belongs to the graph it was created on: after ospf_load_graph,
+ * ospf_update_* or ospf_links_mask, ospf_sweep_run returns OSPF_E_NOGRAPH
+ * (rows already computed stay readable). Partition (n_parts > 1): each width
+ * class, ordered by each node's largest neighbour id, is cut into n_parts
+ * contiguous slices -- a fabric's racks and fabric switches by pod, its
+ * spines by plane -- so a part's closure stays small. */
+#define OSPF_SWEEP_AUTO 0u
+#define OSPF_SWEEP_DERIVE 1u
+#define OSPF_SWEEP_WCOVER 2u
+#define OSPF_SWEEP_WDERIVE 3u
+#define OSPF_SWEEP_BATCH 4u
+
+typedef struct ospf_sweep ospf_sweep;
+typedef struct ospf_sweep_opts {
+  uint32_t flags;      /* 0 (link metrics) or OSPF_HOP_COUNT */
+  uint32_t mode;       /* OSPF_SWEEP_* */
+  uint32_t part;       /* this part of the root partition ... */
+  uint32_t n_parts;    /* ... over n_parts (0 or 1: every node) */
+  uint32_t hip_graph;  /* 1: capture one run as a HIP graph, runs replay it
+                          (eager launches if capture fails: see info) */
+} ospf_sweep_opts;
+
+typedef struct ospf_sweep_info {
+  uint32_t mode;             /* the path taken (OSPF_SWEEP_*) */
+  uint32_t n_roots;          /* roots this part owns */
+  uint32_t n_rows;           /* distance rows computed per run (closure / cover rows) */
+  uint32_t n_launches;       /* launch units (ospf_sweep_profile) */
+  uint32_t hip_graph;        /* 1: runs replay a captured graph */
+  uint32_t max_nh_words;     /* widest next-hop row of an owned root */
+  uint64_t device_bytes;     /* rows, level rows, digests, tables */
+  uint64_t step_compulsory_bytes;  /* rows written + CSR scans, per run */
+} ospf_sweep_info;
+
+/* One launch unit of a run, timed alone on its stream (HIP events). */
+typedef struct ospf_sweep_launch {
+  char name[32];
+  char kernel[112];
+  uint32_t n_roots;          /* runs the launch computes */
+  uint32_t nh_words;         /* 0 = distance rows only */
+  uint64_t compulsory_bytes; /* rows written + CSR / source rows read at least once */
+  double ms_median;          /* isolated launch time, median of the reps */
+  double ms_min;
+} ospf_sweep_launch;
+
+int ospf_sweep_create(ospf_ctx* ctx, const ospf_sweep_opts* opts, ospf_sweep** out);
+int ospf_sweep_destroy(ospf_sweep* sw);
+const char* ospf_sweep_last_error(const ospf_sweep* sw);
+int ospf_sweep_get_info(const ospf_sweep* sw, ospf_sweep_info* info);
+/* The owned roots, in digest order ([n_roots] host). */
+int ospf_sweep_roots(const ospf_sweep* sw, uint32_t* roots);
+/* One all-sources run queued on `stream` (hipStream_t; not synchronised;
+ * ospf_sync(ctx, stream) reports device errors). */
+int ospf_sweep_run(ospf_sweep* sw, void* stream);
+/* Digests of the owned roots in ospf_sweep_roots order into device memory
+ * d_out[n_roots], queued on `stream`. */
+int ospf_sweep_digests(ospf_sweep* sw, ospf_digest* d_out, void* stream);
+/* Same into host memory out[n_roots], synchronous. */
+int ospf_sweep_digests_host(ospf_sweep* sw, ospf_digest* out);
+/* Fill every digest the sweep keeps with 0xFF (a run rewrites them all; a
+ * run that did nothing is then visible). */
+int ospf_sweep_poison(ospf_sweep* sw, void* stream);
+/* Device rows of an owned root (valid until ospf_sweep_destroy). */
+int ospf_sweep_row(const ospf_sweep* sw, uint32_t root, const uint32_t** d_dist,
+                   const uint32_t** d_nh, uint32_t* nh_words);
+/* Host copies of owned roots' rows, synchronous (after the work queued on
+ * every stream is done): dist_out [n][V] and nh_out [n][V][nh_words] (each
+ * root's W words, zero padded; nh_words >= every root's W), either may be
+ * NULL. */
+int ospf_sweep_copy_rows(ospf_sweep* sw, const uint32_t* roots, uint32_t n, uint32_t nh_words,
+                         uint32_t* dist_out, uint32_t* nh_out);
+/* Time every launch unit alone on its stream: reps (>= 1) timed launches
+ * after one untimed one; fills min(cap, n_launches) records. The sweep must
+ * have run once. */
+int ospf_sweep_profile(ospf_sweep* sw, uint32_t reps, ospf_sweep_launch* out, uint32_t cap);
+
+/* ---------------------------------------------------------------- devices
+ * Several devices of one node behind one handle (SURVEY.md §8(b) ospf_open
+ * with n_gpus; Decision runs in one process on one thread,
+ * openr/Main.cpp:515-527, so the drop-in reaches the node's GPUs from
+ * there). The graph is replicated on every device; an all-sources sweep runs
+ * part i of the root partition on device i (no data-path exchange: every
+ * run is independent, rows stay device-local); the 24-B digests are gathered
+ * onto the first device by peer copies. Devices may repeat (several
+ * contexts on one device: a test of the partition on a one-GPU box). */
+typedef struct ospf_multi ospf_multi;
+typedef struct ospf_msweep ospf_msweep;
+int ospf_multi_open(const int* devices, uint32_t n, ospf_multi** out);
+int ospf_multi_close(ospf_multi* m);
+const char* ospf_multi_last_error(const ospf_multi* m);
+uint32_t ospf_multi_size(const ospf_multi* m);
+/* the context of device slot i (owned by m) */
+ospf_ctx* ospf_multi_ctx(ospf_multi* m, uint32_t i);
+int ospf_multi_load_graph(ospf_multi* m, const ospf_csr* csr, uint64_t version);
+/* One sweep per device slot (opts->part / n_parts are set per slot). */
+int ospf_msweep_create(ospf_multi* m, const ospf_sweep_opts* opts, ospf_msweep** out);
+int ospf_msweep_destroy(ospf_msweep* ms);
+/* Queue one run on every device and wait for all of them. */
+int ospf_msweep_run(ospf_msweep* ms);
+/* Digests of every node by node id (host [V]): peer copies onto the first
+ * device, one scatter by root id, one copy back. */
+int ospf_msweep_digests(ospf_msweep* ms, ospf_digest* out_by_node);
+/* The slot's sweep (row access, info) and the slot owning `root`. */
+ospf_sweep* ospf_msweep_part(ospf_msweep* ms, uint32_t slot);
+int ospf_msweep_owner(const ospf_msweep* ms, uint32_t root, uint32_t* slot);
+
 /* Runtime statistics. spf_runs counts logical runSpf executions (one per
  * root per batch), matching the reference's decision.spf_runs counter
  * (LinkState.cpp:843). */

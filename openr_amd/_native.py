@@ -31,10 +31,18 @@ ENGINE_SYMBOLS = [
     "ospf_ksp2_run", "ospf_ksp2_dev", "ospf_update_links", "ospf_update_nodes",
     "ospf_levels_dev", "ospf_nh_derive_dev", "ospf_wderive_dev", "ospf_wderive_wide_dev",
     "ospf_cover_prepare", "ospf_cover_dist_dev",
-    "ospf_affected_roots", "ospf_repair_runs",
+    "ospf_affected_roots", "ospf_repair_runs", "ospf_links_mask", "ospf_links_unmask",
+    "ospf_sweep_create", "ospf_sweep_destroy", "ospf_sweep_last_error", "ospf_sweep_get_info",
+    "ospf_sweep_roots", "ospf_sweep_run", "ospf_sweep_digests", "ospf_sweep_digests_host",
+    "ospf_sweep_poison",
+    "ospf_sweep_row", "ospf_sweep_copy_rows", "ospf_sweep_profile",
+    "ospf_multi_open", "ospf_multi_close", "ospf_multi_last_error", "ospf_multi_size",
+    "ospf_multi_ctx", "ospf_multi_load_graph", "ospf_msweep_create", "ospf_msweep_destroy",
+    "ospf_msweep_run", "ospf_msweep_digests", "ospf_msweep_part", "ospf_msweep_owner",
 ]
 DECISION_SYMBOLS = [
-    "odl_create", "odl_destroy", "odl_last_error", "odl_free", "odl_apply", "odl_spf_text",
+    "odl_create", "odl_create_multi", "odl_all_sources_prefetch", "odl_all_sources_digests",
+    "odl_sweep_stats", "odl_destroy", "odl_last_error", "odl_free", "odl_apply", "odl_spf_text",
     "odl_kth_paths_text", "odl_links_text", "odl_link_keys_text", "odl_metric_a_to_b", "odl_is_overloaded",
     "odl_spf_runs", "odl_set_incremental", "odl_incremental_stats", "odl_num_nodes", "odl_num_links", "odl_spf_digests", "odl_spf_prefetch",
     "odl_ksp2_text", "odl_route_text", "odl_route_db_text", "odl_path_a_in_b", "odl_ucmp_text", "odl_csr_size", "odl_csr_export", "odl_node_name", "odl_node_id",
@@ -83,6 +91,29 @@ class ospf_change(C.Structure):  # noqa: N801
 
 class ospf_plan_info(C.Structure):  # noqa: N801
     _fields_ = [("variant", C.c_int32), ("block", u32), ("lds_bytes", u32), ("slices", u32)]
+
+
+OSPF_SWEEP_AUTO, OSPF_SWEEP_DERIVE, OSPF_SWEEP_WCOVER, OSPF_SWEEP_WDERIVE, OSPF_SWEEP_BATCH = \
+    0, 1, 2, 3, 4
+SWEEP_MODES = {"auto": 0, "derive": 1, "wcover": 2, "wderive": 3, "batch": 4}
+SWEEP_MODE_NAMES = {v: k for k, v in SWEEP_MODES.items()}
+
+
+class ospf_sweep_opts(C.Structure):  # noqa: N801
+    _fields_ = [("flags", u32), ("mode", u32), ("part", u32), ("n_parts", u32),
+                ("hip_graph", u32)]
+
+
+class ospf_sweep_info(C.Structure):  # noqa: N801
+    _fields_ = [("mode", u32), ("n_roots", u32), ("n_rows", u32), ("n_launches", u32),
+                ("hip_graph", u32), ("max_nh_words", u32), ("device_bytes", u64),
+                ("step_compulsory_bytes", u64)]
+
+
+class ospf_sweep_launch(C.Structure):  # noqa: N801
+    _fields_ = [("name", C.c_char * 32), ("kernel", C.c_char * 112), ("n_roots", u32),
+                ("nh_words", u32), ("compulsory_bytes", u64), ("ms_median", C.c_double),
+                ("ms_min", C.c_double)]
 
 
 class ospf_graph_info(C.Structure):  # noqa: N801
@@ -135,6 +166,37 @@ def engine() -> C.CDLL:
         L.ospf_repair_runs.argtypes = [vp, vp, u32, u32, u32, vp, vp, vp, u32, vp, vp]
         L.ospf_spf_runs.argtypes = [vp]
         L.ospf_spf_runs.restype = u64
+        L.ospf_links_mask.argtypes = [vp, vp, u32, u64]
+        L.ospf_links_unmask.argtypes = [vp]
+        L.ospf_sweep_create.argtypes = [vp, C.POINTER(ospf_sweep_opts), C.POINTER(vp)]
+        L.ospf_sweep_destroy.argtypes = [vp]
+        L.ospf_sweep_last_error.argtypes = [vp]
+        L.ospf_sweep_last_error.restype = cp
+        L.ospf_sweep_get_info.argtypes = [vp, C.POINTER(ospf_sweep_info)]
+        L.ospf_sweep_roots.argtypes = [vp, vp]
+        L.ospf_sweep_run.argtypes = [vp, vp]
+        L.ospf_sweep_digests.argtypes = [vp, vp, vp]
+        L.ospf_sweep_digests_host.argtypes = [vp, vp]
+        L.ospf_sweep_poison.argtypes = [vp, vp]
+        L.ospf_sweep_row.argtypes = [vp, u32, C.POINTER(vp), C.POINTER(vp), C.POINTER(u32)]
+        L.ospf_sweep_copy_rows.argtypes = [vp, vp, u32, u32, vp, vp]
+        L.ospf_sweep_profile.argtypes = [vp, u32, vp, u32]
+        L.ospf_multi_open.argtypes = [vp, u32, C.POINTER(vp)]
+        L.ospf_multi_close.argtypes = [vp]
+        L.ospf_multi_last_error.argtypes = [vp]
+        L.ospf_multi_last_error.restype = cp
+        L.ospf_multi_size.argtypes = [vp]
+        L.ospf_multi_size.restype = u32
+        L.ospf_multi_ctx.argtypes = [vp, u32]
+        L.ospf_multi_ctx.restype = vp
+        L.ospf_multi_load_graph.argtypes = [vp, C.POINTER(ospf_csr), u64]
+        L.ospf_msweep_create.argtypes = [vp, C.POINTER(ospf_sweep_opts), C.POINTER(vp)]
+        L.ospf_msweep_destroy.argtypes = [vp]
+        L.ospf_msweep_run.argtypes = [vp]
+        L.ospf_msweep_digests.argtypes = [vp, vp]
+        L.ospf_msweep_part.argtypes = [vp, u32]
+        L.ospf_msweep_part.restype = vp
+        L.ospf_msweep_owner.argtypes = [vp, u32, C.POINTER(u32)]
         _engine = L
     return _engine
 
@@ -145,6 +207,11 @@ def decision() -> C.CDLL:
         engine()
         L = _load(DECISION_SO)
         L.odl_create.argtypes = [cp, i32, C.POINTER(vp)]
+        L.odl_create_multi.argtypes = [cp, vp, u32, C.POINTER(vp)]
+        L.odl_all_sources_prefetch.argtypes = [vp, i32]
+        L.odl_all_sources_digests.argtypes = [vp, i32, vp]
+        L.odl_sweep_stats.argtypes = [vp, vp]
+        L.odl_sweep_stats.restype = None
         L.odl_destroy.argtypes = [vp]
         L.odl_last_error.argtypes = [vp]
         L.odl_last_error.restype = cp

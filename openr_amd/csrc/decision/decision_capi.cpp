@@ -19,6 +19,7 @@ struct odl_ls {
   odl::LinkState ls;
   std::string err;
   odl_ls(const char* area, int device) : ls(area ? area : "0", device) {}
+  odl_ls(const char* area, std::vector<int> devices) : ls(area ? area : "0", std::move(devices)) {}
 };
 
 namespace {
@@ -97,6 +98,17 @@ int odl_create(const char* area, int device, odl_ls** out) {
   if (!out) return -1;
   try {
     *out = new odl_ls(area, device);
+    return 0;
+  } catch (...) {
+    *out = nullptr;
+    return -1;
+  }
+}
+
+int odl_create_multi(const char* area, const int* devices, uint32_t n, odl_ls** out) {
+  if (!out || !devices || !n) return -1;
+  try {
+    *out = new odl_ls(area, std::vector<int>(devices, devices + n));
     return 0;
   } catch (...) {
     *out = nullptr;
@@ -211,6 +223,35 @@ int odl_spf_digests(odl_ls* h, const char* roots_nl, uint32_t n, int use_link_me
     }
     return 0;
   }, -1);
+}
+
+int odl_all_sources_digests(odl_ls* h, int use_link_metric, uint64_t* out) {
+  return guard(h, [&]() -> int {
+    auto d = h->ls.allSourcesDigests(use_link_metric != 0);
+    for (size_t i = 0; i < d.size(); ++i) {
+      out[3 * i] = d[i].reached;
+      out[3 * i + 1] = d[i].sum_dist;
+      out[3 * i + 2] = d[i].hash;
+    }
+    return 0;
+  }, -1);
+}
+
+int odl_all_sources_prefetch(odl_ls* h, int use_link_metric) {
+  return guard(h, [&]() -> int {
+    h->ls.prefetchAllSources(use_link_metric != 0);
+    return 0;
+  }, -1);
+}
+
+void odl_sweep_stats(const odl_ls* h, uint64_t* out5) {
+  if (!h || !out5) return;
+  const auto& st = h->ls.sweepStats();
+  out5[0] = st.sweeps;
+  out5[1] = st.rows_copied;
+  out5[2] = st.mode;
+  out5[3] = st.devices;
+  out5[4] = st.hip_graph;
 }
 
 int odl_spf_prefetch(odl_ls* h, const char* roots_nl, uint32_t n, int use_link_metric) {

@@ -129,10 +129,18 @@ std::string Link::key() const {
 }
 
 // ---------------------------------------------------------------- LinkState
-LinkState::LinkState(std::string area, int device) : area_(std::move(area)), device_(device) {}
+LinkState::LinkState(std::string area, int device)
+    : area_(std::move(area)), device_(device), devices_{device} {}
+
+LinkState::LinkState(std::string area, std::vector<int> devices)
+    : area_(std::move(area)), device_(devices.empty() ? 0 : devices[0]), devices_(std::move(devices)) {
+  if (devices_.empty()) throw std::invalid_argument("LinkState: no device");
+}
 
 LinkState::~LinkState() {
-  if (engine_) ospf_close(engine_);
+  dropSweep();
+  if (multi_) ospf_multi_close(multi_);
+  else if (engine_) ospf_close(engine_);
 }
 
 const LinkSet& LinkState::linksFromNode(const std::string& node) const {
@@ -182,6 +190,7 @@ static size_t V_of(const LinkState::Csr& c) { return c.names.size(); }
 
 void LinkState::invalidate() {
   ++version_;
+  dropSweep();
   memoMetric_.clear();
   memoHops_.clear();
   rawMetric_.clear();
@@ -464,13 +473,21 @@ uint32_t LinkState::linkIdOf(const Link& l) const {
 void LinkState::ensureEngine() {
   snapshot();
   if (!engine_) {
-    int rc = ospf_open(device_, &engine_);
+    int rc = OSPF_OK;
+    if (devices_.size() > 1) {
+      rc = ospf_multi_open(devices_.data(), (uint32_t)devices_.size(), &multi_);
+      if (rc == OSPF_OK) engine_ = ospf_multi_ctx(multi_, 0);
+    } else {
+      rc = ospf_open(device_, &engine_);
+    }
     if (rc != OSPF_OK) {
       engine_ = nullptr;
+      multi_ = nullptr;
       throw EngineError(rc, "ospf_open failed (no MI355X device / HIP runtime?)");
     }
   }
   if (engineVersion_ != snapVersion_) {
+    dropSweep();
     ospf_csr g{};
     g.n_nodes = (uint32_t)csr_.names.size();
     g.n_edges = (uint32_t)csr_.col.size();
@@ -482,9 +499,121 @@ void LinkState::ensureEngine() {
     g.edge_up = csr_.edgeUp.data();
     g.no_transit = csr_.noTransit.data();
     g.link_rank = csr_.linkRank.data();
-    int rc = ospf_load_graph(engine_, &g, snapVersion_);
-    if (rc != OSPF_OK) throw EngineError(rc, ospf_last_error(engine_));
+    int rc = multi_ ? ospf_multi_load_graph(multi_, &g, snapVersion_)
+                    : ospf_load_graph(engine_, &g, snapVersion_);
+    if (rc != OSPF_OK)
+      throw EngineError(rc, multi_ ? ospf_multi_last_error(multi_) : ospf_last_error(engine_));
     engineVersion_ = snapVersion_;
+  }
+}
+
+void LinkState::dropSweep() {
+  if (sweep_) ospf_sweep_destroy(sweep_);
+  if (msweep_) ospf_msweep_destroy(msweep_);
+  sweep_ = nullptr;
+  msweep_ = nullptr;
+  sweepVersion_ = 0;
+}
+
+bool LinkState::sweepHas(bool useLinkMetric) const {
+  return (sweep_ || msweep_) && sweepVersion_ == snapVersion_ && sweepMetric_ == useLinkMetric &&
+         snapVersion_ == version_;
+}
+
+void LinkState::prefetchAllSources(bool useLinkMetric) {
+  snapshot();
+  if (sweepHas(useLinkMetric)) return;
+  if (useLinkMetric && hostMetric_) {  // outside the engine contract: the reference algorithm
+    prefetchSpf(csr_.names, true);
+    return;
+  }
+  ensureEngine();
+  dropSweep();
+  ospf_sweep_opts o{};
+  o.flags = useLinkMetric ? 0u : OSPF_HOP_COUNT;
+  o.mode = OSPF_SWEEP_AUTO;
+  o.hip_graph = 0;  // one run per snapshot: nothing to replay
+  int rc;
+  ospf_sweep_info info{};
+  if (multi_) {
+    rc = ospf_msweep_create(multi_, &o, &msweep_);
+    if (rc == OSPF_OK) rc = ospf_msweep_run(msweep_);
+    if (rc != OSPF_OK) {
+      const std::string m = ospf_multi_last_error(multi_);
+      dropSweep();
+      throw EngineError(rc, m);
+    }
+    ospf_sweep_get_info(ospf_msweep_part(msweep_, 0), &info);
+    sweepStats_.devices = ospf_multi_size(multi_);
+  } else {
+    rc = ospf_sweep_create(engine_, &o, &sweep_);
+    if (rc == OSPF_OK) rc = ospf_sweep_run(sweep_, nullptr);
+    if (rc == OSPF_OK) rc = ospf_sync(engine_, nullptr);
+    if (rc != OSPF_OK) {
+      const std::string m = ospf_last_error(engine_);
+      dropSweep();
+      throw EngineError(rc, m);
+    }
+    ospf_sweep_get_info(sweep_, &info);
+    sweepStats_.devices = 1;
+  }
+  sweepVersion_ = snapVersion_;
+  sweepMetric_ = useLinkMetric;
+  spfRuns_ += csr_.names.size();  // every node's runSpf, once
+  ++sweepStats_.sweeps;
+  sweepStats_.mode = info.mode;
+  sweepStats_.hip_graph = info.hip_graph;
+}
+
+void LinkState::sweepRows(const std::vector<uint32_t>& roots, uint32_t W,
+                          std::vector<uint32_t>& dist, std::vector<uint32_t>& nh) {
+  const size_t V = csr_.names.size();
+  dist.assign(roots.size() * V, kInf);
+  nh.assign(roots.size() * V * W, 0);
+  if (sweep_) {
+    const int rc = ospf_sweep_copy_rows(sweep_, roots.data(), (uint32_t)roots.size(), W,
+                                        dist.data(), nh.data());
+    if (rc != OSPF_OK) throw EngineError(rc, ospf_sweep_last_error(sweep_));
+  } else {
+    for (size_t i = 0; i < roots.size(); ++i) {
+      uint32_t slot = 0;
+      int rc = ospf_msweep_owner(msweep_, roots[i], &slot);
+      ospf_sweep* part = ospf_msweep_part(msweep_, slot);
+      if (rc == OSPF_OK)
+        rc = ospf_sweep_copy_rows(part, &roots[i], 1, W, dist.data() + i * V, nh.data() + i * V * W);
+      if (rc != OSPF_OK) throw EngineError(rc, ospf_multi_last_error(multi_));
+    }
+  }
+  sweepStats_.rows_copied += roots.size();
+}
+
+std::vector<ospf_digest> LinkState::allSourcesDigests(bool useLinkMetric) {
+  snapshot();
+  const size_t V = csr_.names.size();
+  if (useLinkMetric && hostMetric_) return spfDigests(csr_.names, true);
+  prefetchAllSources(useLinkMetric);
+  std::vector<ospf_digest> out(V);
+  if (msweep_) {
+    const int rc = ospf_msweep_digests(msweep_, out.data());
+    if (rc != OSPF_OK) throw EngineError(rc, ospf_multi_last_error(multi_));
+    return out;
+  }
+  ospf_sweep_info info{};
+  ospf_sweep_get_info(sweep_, &info);
+  std::vector<uint32_t> roots(info.n_roots);
+  ospf_sweep_roots(sweep_, roots.data());
+  std::vector<ospf_digest> tmp(roots.size());
+  const int rc = ospf_sweep_digests_host(sweep_, tmp.data());
+  if (rc != OSPF_OK) throw EngineError(rc, ospf_sweep_last_error(sweep_));
+  for (size_t i = 0; i < roots.size(); ++i) out[roots[i]] = tmp[i];
+  return out;
+}
+
+void LinkState::evictSpf(const std::vector<std::string>& roots, bool useLinkMetric) {
+  auto& memo = useLinkMetric ? memoMetric_ : memoHops_;
+  for (const auto& r : roots) {
+    memo.erase(r);
+    if (useLinkMetric) rawMetric_.erase(r);
   }
 }
 
@@ -608,30 +737,41 @@ void LinkState::prefetchSpf(const std::vector<std::string>& roots, bool useLinkM
   snapshot();
   std::unordered_map<uint32_t, std::vector<uint32_t>> byW;  // W -> roots
   std::unordered_set<std::string> queued;
+  size_t pending = 0;
   for (const auto& r : roots) {
     if (memo.count(r) || !queued.insert(r).second) continue;
-    ++spfRuns_;
     auto id = csr_.ids.find(r);
     if (id == csr_.ids.end()) {  // no adjacency DB: only the root itself
+      ++spfRuns_;
       SpfResult res;
       res.emplace(r, NodeSpfResult(0));
       memo.emplace(r, std::move(res));
       continue;
     }
     if (useLinkMetric && hostMetric_) {
+      ++spfRuns_;
       memo.emplace(r, runSpfHost(r, true, {}));
       continue;
     }
     byW[nhWordsFor(id->second)].push_back(id->second);
+    ++pending;
   }
   const size_t V = csr_.names.size();
+  // most of the nodes asked for: one all-sources sweep, rows copied from it
+  if (!sweepHas(useLinkMetric) && pending >= kSweepMinRoots && 2 * pending >= V)
+    prefetchAllSources(useLinkMetric);
+  const bool fromSweep = sweepHas(useLinkMetric);
+  if (!fromSweep) spfRuns_ += pending;  // a sweep counted every node's run
   for (auto& [W, ids] : byW) {
     const size_t chunk = std::max<size_t>(1, std::min<size_t>(ids.size(), (256ull << 20) / (V * 4 * (1 + W))));
     for (size_t c0 = 0; c0 < ids.size(); c0 += chunk) {
       std::vector<uint32_t> part(ids.begin() + c0, ids.begin() + std::min(ids.size(), c0 + chunk));
       std::vector<uint32_t> dist, nh;
       const auto t0 = std::chrono::steady_clock::now();
-      runBatch(part, nullptr, useLinkMetric, OSPF_WANT_DIST | OSPF_WANT_NH, W, &dist, &nh, nullptr);
+      if (fromSweep)
+        sweepRows(part, W, dist, nh);
+      else
+        runBatch(part, nullptr, useLinkMetric, OSPF_WANT_DIST | OSPF_WANT_NH, W, &dist, &nh, nullptr);
       const auto t1 = std::chrono::steady_clock::now();
       for (size_t i = 0; i < part.size(); ++i) {
         RawRun run{part[i], std::vector<uint32_t>(dist.begin() + i * V, dist.begin() + (i + 1) * V), {}};
@@ -785,29 +925,26 @@ const std::vector<Path>& LinkState::getKthPaths(const std::string& src, const st
       // more ignored links than a run's list holds (e.g. the host side of a
       // KSP2 destination whose k = 1 paths overflowed the device record):
       // take them down on the device graph for this one run, then restore
+      // (ospf_links_mask / unmask: the device graph and the engine's bounds
+      // come back exactly as they were; on any failure the engine is marked
+      // stale and reloaded by the next ensureEngine)
       ensureEngine();
-      std::vector<ospf_link_update> down, back;
-      for (const uint32_t lid : ign) {
-        const Link& l = *csr_.links[lid];
-        const uint32_t lo = csr_.ids.at(l.lowNode());
-        for (uint32_t e = csr_.rowPtr[lo]; e < csr_.rowPtr[lo + 1]; ++e) {
-          if (csr_.linkId[e] != lid) continue;
-          const uint32_t mlo = csr_.metric[e], mhi = csr_.metric[csr_.twin[e]];
-          down.push_back(ospf_link_update{lid, 0u, mlo, mhi});
-          back.push_back(ospf_link_update{lid, csr_.edgeUp[e] ? 1u : 0u, mlo, mhi});
-          break;
-        }
+      int rc = ospf_links_mask(engine_, ign.data(), (uint32_t)ign.size(), ~snapVersion_);
+      if (rc != OSPF_OK) {
+        const std::string m = ospf_last_error(engine_);
+        ospf_links_unmask(engine_);
+        engineVersion_ = 0;
+        throw EngineError(rc, m);
       }
-      int rc = ospf_update_links(engine_, down.data(), (uint32_t)down.size(), ~snapVersion_);
-      if (rc != OSPF_OK) throw EngineError(rc, ospf_last_error(engine_));
-      engineVersion_ = ~snapVersion_;
       dist.assign(V_of(csr_), kInf);
       rc = ospf_sssp_batch(engine_, &s, 1, nullptr, OSPF_WANT_DIST, nhWordsFor(s), dist.data(),
                            nullptr, nullptr);
-      const int rc2 = ospf_update_links(engine_, back.data(), (uint32_t)back.size(), snapVersion_);
-      if (rc != OSPF_OK || rc2 != OSPF_OK)
-        throw EngineError(rc != OSPF_OK ? rc : rc2, ospf_last_error(engine_));
-      engineVersion_ = snapVersion_;
+      const std::string m = rc != OSPF_OK ? ospf_last_error(engine_) : "";
+      const int rc2 = ospf_links_unmask(engine_);
+      if (rc != OSPF_OK || rc2 != OSPF_OK) {
+        engineVersion_ = 0;
+        throw EngineError(rc != OSPF_OK ? rc : rc2, rc != OSPF_OK ? m : ospf_last_error(engine_));
+      }
     }
     RawRun run{s, std::move(dist), std::move(ign)};
     auto d = csr_.ids.find(dst);
@@ -954,11 +1091,19 @@ void LinkState::applyIncremental(const std::vector<LinkDelta>& links,
   const bool inSync = engine_ && engineVersion_ == snapVersion_;
   ++version_;
   snapVersion_ = version_;
+  dropSweep();  // its rows describe the graph before the patch
   if (inSync) {
-    int rc = ospf_update_links(engine_, ups.data(), (uint32_t)ups.size(), snapVersion_);
-    if (rc == OSPF_OK) rc = ospf_update_nodes(engine_, nids.data(), nts.data(), (uint32_t)nids.size(),
-                                              snapVersion_);
-    if (rc != OSPF_OK) throw EngineError(rc, ospf_last_error(engine_));
+    const uint32_t nctx = multi_ ? ospf_multi_size(multi_) : 1u;
+    for (uint32_t i = 0; i < nctx; ++i) {
+      ospf_ctx* c = multi_ ? ospf_multi_ctx(multi_, i) : engine_;
+      int rc = ospf_update_links(c, ups.data(), (uint32_t)ups.size(), snapVersion_);
+      if (rc == OSPF_OK) rc = ospf_update_nodes(c, nids.data(), nts.data(), (uint32_t)nids.size(),
+                                                snapVersion_);
+      if (rc != OSPF_OK) {
+        engineVersion_ = 0;  // reload every device on the next use
+        throw EngineError(rc, ospf_last_error(c));
+      }
+    }
     engineVersion_ = snapVersion_;
   }
 }

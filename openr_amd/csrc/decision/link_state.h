@@ -212,6 +212,9 @@ struct EngineError : std::runtime_error {
 class LinkState {
  public:
   LinkState(std::string area, int device);
+  // several devices of the node (SURVEY.md §8(b) n_gpus): the graph is
+  // replicated, all-sources sweeps run one root partition part per device
+  LinkState(std::string area, std::vector<int> devices);
   ~LinkState();
   LinkState(const LinkState&) = delete;
   LinkState& operator=(const LinkState&) = delete;
@@ -242,6 +245,28 @@ class LinkState {
   void prefetchSpf(const std::vector<std::string>& roots, bool useLinkMetric);
   std::vector<ospf_digest> spfDigests(const std::vector<std::string>& roots, bool useLinkMetric);
   void prefetchKsp2(const std::string& src, const std::vector<std::string>& dsts);
+  // All-sources: runSpf for every node in one engine sweep (ospf_sweep_*,
+  // one part per device), rows kept resident on the devices; getSpfResult /
+  // prefetchSpf of any node then copies its rows instead of running again
+  // (decision.spf_runs counts the V runs of the sweep once). The reference's
+  // all-sources use is getDecisionRouteDb(node) for every node
+  // (Decision.cpp:309).
+  void prefetchAllSources(bool useLinkMetric = true);
+  // digests of every node (node-id order = snapshot().names) from one sweep
+  std::vector<ospf_digest> allSourcesDigests(bool useLinkMetric = true);
+  bool isMemoised(const std::string& root, bool useLinkMetric) const {
+    return (useLinkMetric ? memoMetric_ : memoHops_).count(root) > 0;
+  }
+  // drop memoised results (bounded host memory for all-nodes route builds)
+  void evictSpf(const std::vector<std::string>& roots, bool useLinkMetric);
+  // prefetchSpf takes the sweep when it is asked for at least this many
+  // roots not yet memoised (and at least half of the nodes)
+  static constexpr size_t kSweepMinRoots = 256;
+  struct SweepStats {
+    uint64_t sweeps = 0, rows_copied = 0;
+    uint32_t mode = 0, devices = 0, hip_graph = 0;
+  };
+  const SweepStats& sweepStats() const { return sweepStats_; }
 
   uint64_t spfRuns() const { return spfRuns_; }
 
@@ -292,6 +317,11 @@ class LinkState {
   std::vector<LinkPtr> sortedLinksOf(const std::string& node) const;
   void invalidate();
   void ensureEngine();
+  void dropSweep();
+  bool sweepHas(bool useLinkMetric) const;
+  // copy rows of roots (all owned by the current sweep) into dist / nh (W words)
+  void sweepRows(const std::vector<uint32_t>& roots, uint32_t W, std::vector<uint32_t>& dist,
+                 std::vector<uint32_t>& nh);
   uint32_t nhWordsFor(uint32_t root) const;
   void runBatch(const std::vector<uint32_t>& roots, const std::vector<std::vector<uint32_t>>* ign,
                 bool useLinkMetric, uint32_t flags, uint32_t W, std::vector<uint32_t>* dist,
@@ -320,7 +350,14 @@ class LinkState {
 
   std::string area_;
   int device_;
+  std::vector<int> devices_;
+  ospf_multi* multi_ = nullptr;  // devices_.size() > 1: owns engine_ (its slot 0)
   ospf_ctx* engine_ = nullptr;
+  ospf_sweep* sweep_ = nullptr;     // single device
+  ospf_msweep* msweep_ = nullptr;   // several devices
+  uint64_t sweepVersion_ = 0;       // snapshot version the sweep's rows describe
+  bool sweepMetric_ = true;
+  SweepStats sweepStats_;
   uint64_t engineVersion_ = 0;  // snapshot version loaded into the engine
   uint64_t version_ = 1;        // bumped on every ingest call
   uint64_t snapVersion_ = 0;

@@ -344,10 +344,30 @@ std::vector<std::optional<RouteDb>> SpfSolver::buildRouteDbs(
   std::vector<std::string> roots;
   for (const auto& me : mes)
     if (ls_.getAdjacencyDatabases().count(me)) roots.push_back(me);
-  ls_.prefetchSpf(roots, true);
   std::vector<std::optional<RouteDb>> out;
   out.reserve(mes.size());
-  for (const auto& me : mes) out.push_back(buildRouteDb(me, prefixes, opt));
+  const size_t V = ls_.numNodes();
+  if (roots.size() < LinkState::kSweepMinRoots || 2 * roots.size() < V) {
+    ls_.prefetchSpf(roots, true);
+    for (const auto& me : mes) out.push_back(buildRouteDb(me, prefixes, opt));
+    return out;
+  }
+  // Most of the nodes (Decision::getDecisionRouteDb for every node,
+  // Decision.cpp:309): one all-sources sweep on the devices, then chunks of
+  // nodes whose SpfResults are rebuilt from the resident rows, used and
+  // dropped again (results memoised before the call stay).
+  ls_.prefetchAllSources(true);
+  constexpr size_t kChunk = 512;
+  for (size_t c0 = 0; c0 < mes.size(); c0 += kChunk) {
+    const size_t c1 = std::min(mes.size(), c0 + kChunk);
+    std::vector<std::string> fresh;
+    for (size_t i = c0; i < c1; ++i)
+      if (ls_.getAdjacencyDatabases().count(mes[i]) && !ls_.isMemoised(mes[i], true))
+        fresh.push_back(mes[i]);
+    ls_.prefetchSpf(fresh, true);
+    for (size_t i = c0; i < c1; ++i) out.push_back(buildRouteDb(mes[i], prefixes, opt));
+    ls_.evictSpf(fresh, true);
+  }
   return out;
 }
 

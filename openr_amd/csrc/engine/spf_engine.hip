@@ -15,56 +15,9 @@
 #include <string>
 #include <vector>
 
-#include "spf_kernels.h"
+#include "spf_internal.h"
 
-struct ospf_ctx {
-  int device = 0;
-  size_t lds_limit = 64 * 1024;
-  int lds_attr = 0;
-  int n_cu = 256;
-  std::string err;
-  uint64_t spf_runs = 0;
-  // graph
-  bool loaded = false;
-  ospf_graph_info info{};
-  std::vector<uint32_t> h_row_ptr, h_dn_off, h_dn;  // host copies for root queries
-  // host shadows of the padded device arrays patched by ospf_update_*
-  std::vector<uint32_t> h_prow, h_pcolx, h_pw, h_prw, h_nt, h_link_e;
-  uint64_t non_unit = 0;  // usable entries with metric != 1 (exact unit_metric under patches)
-  void* d_graph = nullptr;
-  ospf::DevGraph g{};
-  const uint32_t* ew_base = nullptr;  // packed entries (g.ew) as words, for patches
-  uint32_t max_dn = 0;
-  uint32_t depth_bound = 2;  // BFS levels any root can reach (unit metric / hop count)
-  uint32_t exact_bound = 2;  // depth_bound as last computed in full (patches may raise depth_bound)
-  // >= every shortest distance: sum over nodes of the largest usable out-metric
-  // (a simple path leaves each node once); patches only add to it
-  uint64_t dist_bound = 0;
-  std::vector<uint32_t> h_lvl;  // scratch of transit_detour (all UINT32_MAX between calls)
-  // scratch
-  // scratch per stream: batches queued on different streams run concurrently
-  struct Scratch {
-    void* p = nullptr;
-    size_t bytes = 0;
-  };
-  std::map<void*, Scratch> scratch;
-  void* d_stage = nullptr;
-  size_t stage_bytes = 0;
-  uint32_t* d_err = nullptr;
-  // KSP2: traces run on an engine stream, overlapping later reruns
-  hipStream_t aux = nullptr;
-  // derive phase 1: rows kernels of one round beside the next round's levels
-  hipStream_t lv_aux = nullptr;
-  hipEvent_t lv_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // traversed[2], rows done[2]
-  // contracted cover graph (ospf_cover_prepare), valid for graph version cover_ver
-  void* d_cover = nullptr;
-  ospf::CoverGraph cover{};
-  uint64_t cover_ver = ~0ull;
-  bool cover_ok = false;
-  std::vector<hipEvent_t> ev;  // [2 * slots]: rerun done / trace done per slot
-};
-
-namespace {
+namespace ospf_int {
 
 int fail(ospf_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
@@ -75,15 +28,7 @@ int hip_fail(ospf_ctx* c, hipError_t e, const char* what) {
   return fail(c, OSPF_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-#define HIPCHK(ctx, call)                                  \
-  do {                                                     \
-    hipError_t e_ = (call);                                \
-    if (e_ != hipSuccess) return hip_fail(ctx, e_, #call); \
-  } while (0)
-
-size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
-
-int ensure(ospf_ctx* c, void** p, size_t* have, size_t need) {
+static int ensure(ospf_ctx* c, void** p, size_t* have, size_t need) {
   if (*have >= need) return OSPF_OK;
   const size_t want = std::max(need, *have * 3 / 2);
   if (*p) hipFree(*p);
@@ -98,10 +43,7 @@ int ensure(ospf_ctx* c, void** p, size_t* have, size_t need) {
   return OSPF_OK;
 }
 
-// the scratch of `stream`, grown to `need` bytes (a grown buffer replaces the
-// old one only after the stream's queued work is done with it); `slot` 1 is a
-// second buffer of the same stream (KSP2 state around nested batch calls)
-char* stream_scratch(ospf_ctx* c, void* stream, size_t need, int* rc, int slot = 0) {
+char* stream_scratch(ospf_ctx* c, void* stream, size_t need, int* rc, int slot) {
   ospf_ctx::Scratch& sc = c->scratch[(char*)stream + slot];
   *rc = OSPF_OK;
   if (sc.bytes >= need) return (char*)sc.p;
@@ -109,6 +51,22 @@ char* stream_scratch(ospf_ctx* c, void* stream, size_t need, int* rc, int slot =
   *rc = ensure(c, &sc.p, &sc.bytes, need);
   return (char*)sc.p;
 }
+
+void release_stream_scratch(ospf_ctx* c, void* stream) {
+  for (int slot = 0; slot < 2; ++slot) {
+    auto it = c->scratch.find((char*)stream + slot);
+    if (it == c->scratch.end()) continue;
+    if (it->second.p) hipFree(it->second.p);
+    c->scratch.erase(it);
+  }
+}
+
+}  // namespace ospf_int
+
+using namespace ospf_int;
+
+namespace {
+
 
 struct Plan {
   int variant;
@@ -989,7 +947,13 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   c->cover_ok = false;  // the contracted cover graph describes the old graph
   c->info.device_bytes = tot;
   c->dist_bound = dist_bound;
+  c->h_rowmax.assign(V, 0u);
+  for (uint32_t u = 0; u < V; ++u)
+    for (uint32_t e = c->h_prow[u]; e < c->h_prow[u + 1]; ++e)
+      if (!(c->h_pcolx[e] & 0x80000000u)) c->h_rowmax[u] = std::max(c->h_rowmax[u], c->h_pw[e]);
+  c->mask = ospf_ctx::Mask{};
   c->loaded = true;
+  ++c->graph_gen;
   return OSPF_OK;
 }
 
@@ -1849,10 +1813,86 @@ int ospf_update_links(ospf_ctx* c, const ospf_link_update* u, uint32_t n, uint64
     else c->depth_bound += grow;
   }
   refresh_graph_stats(c, new_max, deeper);
-  for (uint32_t i = 0; i < n; ++i)
-    if (u[i].up) c->dist_bound += (uint64_t)u[i].metric_lo + u[i].metric_hi;
+  // distance bound = sum of per-node largest usable out-metrics, kept exact
+  // (a patch that restores a metric does not ratchet it up)
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t lid = u[i].link_id;
+    for (int k = 0; k < 2; ++k) {
+      const uint32_t x = owner(c->h_link_e[2ull * lid + k]);
+      uint32_t m = 0;
+      for (uint32_t e = c->h_prow[x]; e < c->h_prow[x + 1]; ++e)
+        if (!(c->h_pcolx[e] & 0x80000000u)) m = std::max(m, c->h_pw[e]);
+      c->dist_bound = c->dist_bound - c->h_rowmax[x] + m;
+      c->h_rowmax[x] = m;
+    }
+  }
   c->info.version = version;
   c->cover_ok = false;  // the contracted cover graph describes the old graph
+  ++c->graph_gen;
+  return OSPF_OK;
+}
+
+// Take links down for a while (KSP2 ignore sets beyond one run's list) and
+// put back exactly what was there: entries and the planner state (level /
+// distance bounds, metric facts, cover graph), so a mask / unmask pair leaves
+// no trace in later runs.
+int ospf_links_mask(ospf_ctx* c, const uint32_t* lids, uint32_t n, uint64_t version) {
+  if (!c || (n && !lids)) return OSPF_E_INVAL;
+  if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  if (c->mask.on) return fail(c, OSPF_E_INVAL, "links already masked (unmask first)");
+  ospf_ctx::Mask m{};
+  m.depth_bound = c->depth_bound;
+  m.exact_bound = c->exact_bound;
+  m.max_metric = c->info.max_metric;
+  m.unit_metric = c->info.unit_metric;
+  m.dist_bound = c->dist_bound;
+  m.non_unit = c->non_unit;
+  m.version = c->info.version;
+  m.cover_ok = c->cover_ok;
+  std::vector<ospf_link_update> down(n);
+  auto owner = [&](uint32_t e) {
+    return (uint32_t)(std::upper_bound(c->h_prow.begin(), c->h_prow.end(), e) - c->h_prow.begin() - 1);
+  };
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t lid = lids[i];
+    if (lid >= c->g.n_lid || c->h_link_e[2ull * lid] == 0xFFFFFFFFu ||
+        c->h_link_e[2ull * lid + 1] == 0xFFFFFFFFu)
+      return fail(c, OSPF_E_INVAL, "unknown link id");
+    const uint32_t e0 = c->h_link_e[2ull * lid], e1 = c->h_link_e[2ull * lid + 1];
+    const bool lo0 = owner(e0) <= owner(e1);
+    const uint32_t elo = lo0 ? e0 : e1, ehi = lo0 ? e1 : e0;
+    m.lids.push_back(lid);
+    m.up.push_back((c->h_pcolx[elo] & 0x80000000u) ? 0u : 1u);
+    m.mlo.push_back(c->h_pw[elo]);
+    m.mhi.push_back(c->h_pw[ehi]);
+    down[i] = ospf_link_update{lid, 0u, c->h_pw[elo], c->h_pw[ehi]};
+  }
+  const int rc = ospf_update_links(c, down.data(), n, version);
+  if (rc != OSPF_OK) return rc;
+  m.on = true;
+  c->mask = std::move(m);
+  return OSPF_OK;
+}
+
+int ospf_links_unmask(ospf_ctx* c) {
+  if (!c) return OSPF_E_INVAL;
+  if (!c->mask.on) return OSPF_OK;
+  ospf_ctx::Mask m = std::move(c->mask);
+  c->mask = ospf_ctx::Mask{};
+  std::vector<ospf_link_update> back(m.lids.size());
+  for (size_t i = 0; i < m.lids.size(); ++i)
+    back[i] = ospf_link_update{m.lids[i], m.up[i], m.mlo[i], m.mhi[i]};
+  // metric 0 never appears on an up link of a loaded graph, so the restore
+  // passes ospf_update_links' checks
+  const int rc = ospf_update_links(c, back.data(), (uint32_t)back.size(), m.version);
+  if (rc != OSPF_OK) return rc;
+  c->depth_bound = m.depth_bound;
+  c->exact_bound = m.exact_bound;
+  c->info.max_metric = m.max_metric;
+  c->info.unit_metric = m.unit_metric;
+  c->dist_bound = m.dist_bound;
+  c->non_unit = m.non_unit;
+  c->cover_ok = m.cover_ok;
   return OSPF_OK;
 }
 
@@ -1878,6 +1918,7 @@ int ospf_update_nodes(ospf_ctx* c, const uint32_t* nodes, const uint8_t* no_tran
   refresh_graph_stats(c, 0, deeper);
   c->info.version = version;
   c->cover_ok = false;  // the contracted cover graph describes the old graph
+  ++c->graph_gen;
   return OSPF_OK;
 }
 

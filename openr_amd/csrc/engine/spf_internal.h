@@ -1,0 +1,90 @@
+// spf_internal.h — the engine context shared by the C ABI translation units
+// (spf_engine.hip: graph, batches, derive, KSP2, updates; spf_sweep.cpp:
+// all-sources sweeps and the multi-device context). Not a public header.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "spf_kernels.h"
+
+struct ospf_ctx {
+  int device = 0;
+  size_t lds_limit = 64 * 1024;
+  int lds_attr = 0;
+  int n_cu = 256;
+  std::string err;
+  uint64_t spf_runs = 0;
+  // graph
+  bool loaded = false;
+  ospf_graph_info info{};
+  std::vector<uint32_t> h_row_ptr, h_dn_off, h_dn;  // host copies for root queries
+  // host shadows of the padded device arrays patched by ospf_update_*
+  std::vector<uint32_t> h_prow, h_pcolx, h_pw, h_prw, h_nt, h_link_e;
+  uint64_t non_unit = 0;  // usable entries with metric != 1 (exact unit_metric under patches)
+  void* d_graph = nullptr;
+  ospf::DevGraph g{};
+  const uint32_t* ew_base = nullptr;  // packed entries (g.ew) as words, for patches
+  uint32_t max_dn = 0;
+  uint32_t depth_bound = 2;  // BFS levels any root can reach (unit metric / hop count)
+  uint32_t exact_bound = 2;  // depth_bound as last computed in full (patches may raise depth_bound)
+  // >= every shortest distance: sum over nodes of the largest usable out-metric
+  // (a simple path leaves each node once); patches only add to it
+  uint64_t dist_bound = 0;
+  std::vector<uint32_t> h_rowmax;  // largest usable out-metric per node (dist_bound = sum)
+  std::vector<uint32_t> h_lvl;  // scratch of transit_detour (all UINT32_MAX between calls)
+  // scratch per stream: batches queued on different streams run concurrently
+  struct Scratch {
+    void* p = nullptr;
+    size_t bytes = 0;
+  };
+  std::map<void*, Scratch> scratch;
+  void* d_stage = nullptr;
+  size_t stage_bytes = 0;
+  uint32_t* d_err = nullptr;
+  // KSP2: traces run on an engine stream, overlapping later reruns
+  hipStream_t aux = nullptr;
+  // derive phase 1: rows kernels of one round beside the next round's levels
+  hipStream_t lv_aux = nullptr;
+  hipEvent_t lv_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // traversed[2], rows done[2]
+  // contracted cover graph (ospf_cover_prepare), valid for graph version cover_ver
+  void* d_cover = nullptr;
+  ospf::CoverGraph cover{};
+  uint64_t cover_ver = ~0ull;
+  bool cover_ok = false;
+  std::vector<hipEvent_t> ev;  // [2 * slots]: rerun done / trace done per slot
+  uint64_t graph_gen = 0;      // bumped by every load / patch (sweeps check it)
+  // ospf_links_mask: the entries and planner state it replaced (restored by
+  // ospf_links_unmask)
+  struct Mask {
+    bool on = false;
+    std::vector<uint32_t> lids;
+    std::vector<uint32_t> up, mlo, mhi;  // per masked link, before
+    uint32_t depth_bound, exact_bound, max_metric, unit_metric;
+    uint64_t dist_bound, non_unit, version;
+    bool cover_ok;
+  } mask;
+};
+
+namespace ospf_int {
+
+int fail(ospf_ctx* c, int code, const std::string& msg);
+int hip_fail(ospf_ctx* c, hipError_t e, const char* what);
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+// the scratch of `stream`, grown to `need` bytes (a grown buffer replaces the
+// old one only after the stream's queued work is done with it); `slot` 1 is a
+// second buffer of the same stream (KSP2 state around nested batch calls)
+char* stream_scratch(ospf_ctx* c, void* stream, size_t need, int* rc, int slot = 0);
+// frees the scratch of `stream` (both slots); the stream must be idle
+void release_stream_scratch(ospf_ctx* c, void* stream);
+
+}  // namespace ospf_int
+
+#define HIPCHK(ctx, call)                                            \
+  do {                                                               \
+    hipError_t e_ = (call);                                          \
+    if (e_ != hipSuccess) return ospf_int::hip_fail(ctx, e_, #call); \
+  } while (0)

@@ -1,0 +1,1265 @@
+// spf_sweep.hip — all-sources sweeps and the multi-device context
+// (include/openr_spf.h, "sweeps" / "devices").
+//
+// A sweep is runSpf (openr/decision/LinkState.cpp:836-911) for every node of
+// the graph, or for one part of a root partition: the reference's
+// all-sources use is Decision::getDecisionRouteDb(node) per node
+// (openr/decision/Decision.cpp:309) and `breeze decision routes --nodes all`
+// (openr/py/openr/cli/commands/decision.py:26-48). The sweep owns what a
+// caller would otherwise orchestrate: the path (derive / weighted cover /
+// weighted derive / batch), root order and width classes, the row buffers,
+// one HIP stream per concurrent launch and the HIP graph a run replays.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <new>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "spf_internal.h"
+
+using namespace ospf_int;
+
+namespace {
+
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+__global__ void gather_digest_kernel(const ospf_digest* __restrict__ src,
+                                     const uint32_t* __restrict__ idx, uint32_t n,
+                                     ospf_digest* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = src[idx[i]];
+}
+
+__global__ void scatter_digest_kernel(const ospf_digest* __restrict__ src,
+                                      const uint32_t* __restrict__ roots, uint32_t n,
+                                      ospf_digest* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[roots[i]] = src[i];
+}
+
+// ---------------------------------------------------------------- host graph facts
+// distinct neighbours (ascending id, links of any state) come from the
+// context's host copy (ospf_load_graph: dn_off / dn)
+struct Facts {
+  uint32_t V = 0;
+  const std::vector<uint32_t>* dn_off = nullptr;
+  const std::vector<uint32_t>* dn = nullptr;
+  uint32_t nbrs(uint32_t v) const { return (*dn_off)[v + 1] - (*dn_off)[v]; }
+  // smallest / largest neighbour id (V / 0 for an isolated node)
+  uint64_t first(uint32_t v) const { return nbrs(v) ? (*dn)[(*dn_off)[v]] : V; }
+  uint64_t last(uint32_t v) const { return nbrs(v) ? (*dn)[(*dn_off)[v + 1] - 1] : 0; }
+  // launch class: 8, 16 or 32 x next-hop words (distinct neighbours)
+  uint32_t cap(uint32_t v) const {
+    const uint32_t k = nbrs(v);
+    return k <= 8 ? 8u : k <= 16 ? 16u : 32u * std::max(1u, (k + 31) / 32);
+  }
+  uint32_t words(uint32_t v) const { return std::max(1u, (nbrs(v) + 31) / 32); }
+};
+
+// stable order of `v` by key(v)
+template <class K>
+void locality_order(std::vector<uint32_t>& v, K key) {
+  std::stable_sort(v.begin(), v.end(), [&](uint32_t a, uint32_t b) { return key(a) < key(b); });
+}
+
+// sorted ids of `roots` and all their neighbours
+std::vector<uint32_t> closure(const Facts& f, const std::vector<uint32_t>& roots) {
+  std::vector<uint8_t> mark(f.V, 0);
+  for (uint32_t r : roots) {
+    mark[r] = 1;
+    for (uint32_t k = (*f.dn_off)[r]; k < (*f.dn_off)[r + 1]; ++k) mark[(*f.dn)[k]] = 1;
+  }
+  std::vector<uint32_t> out;
+  for (uint32_t v = 0; v < f.V; ++v)
+    if (mark[v]) out.push_back(v);
+  return out;
+}
+
+// [lo, hi) of part p's contiguous share of m items (sizes differ by <= 1)
+std::pair<size_t, size_t> part_slice(size_t m, uint32_t parts, uint32_t p) {
+  const size_t q = m / parts, r = m % parts;
+  const size_t lo = p * q + std::min<size_t>(p, r);
+  return {lo, lo + q + (p < r ? 1 : 0)};
+}
+
+// The roots of part p: every width class ordered by the node's largest
+// neighbour (stable in id order), cut into contiguous slices. On a fabric
+// the racks and fabric switches of a pod share their largest neighbour (a
+// fabric switch / a rack of the same pod), the spines of a plane too (the
+// plane's fabric switch in the last pod by name), so parts are pod and plane
+// blocks and a part's closure adds little. Returns the class-major order.
+std::vector<uint32_t> partition(const Facts& f, uint32_t parts, uint32_t p) {
+  std::vector<uint32_t> all(f.V);
+  std::iota(all.begin(), all.end(), 0u);
+  if (parts <= 1) return all;
+  std::vector<uint32_t> caps;
+  for (uint32_t v = 0; v < f.V; ++v) caps.push_back(f.cap(v));
+  std::vector<uint32_t> uc = caps;
+  std::sort(uc.begin(), uc.end());
+  uc.erase(std::unique(uc.begin(), uc.end()), uc.end());
+  std::vector<uint32_t> out;
+  for (uint32_t cap : uc) {
+    std::vector<uint32_t> cls;
+    for (uint32_t v = 0; v < f.V; ++v)
+      if (caps[v] == cap) cls.push_back(v);
+    locality_order(cls, [&](uint32_t v) { return f.last(v); });
+    const auto sl = part_slice(cls.size(), parts, p);
+    out.insert(out.end(), cls.begin() + sl.first, cls.begin() + sl.second);
+  }
+  return out;
+}
+
+// Independent set of nodes with <= 32 distinct neighbours, greedy in
+// (distinct neighbours, id) order: the lexicographically first maximal
+// independent set of the candidates under that priority (what Luby rounds
+// with a fixed priority also produce). Links of any state count.
+std::vector<uint8_t> leaf_set(const Facts& f, uint32_t max_nbrs = 32) {
+  std::vector<uint32_t> cand;
+  for (uint32_t v = 0; v < f.V; ++v)
+    if (f.nbrs(v) <= max_nbrs) cand.push_back(v);
+  std::stable_sort(cand.begin(), cand.end(),
+                   [&](uint32_t a, uint32_t b) { return f.nbrs(a) < f.nbrs(b); });
+  std::vector<uint8_t> leaf(f.V, 0), blocked(f.V, 0);
+  for (uint32_t v : cand) {
+    if (blocked[v]) continue;
+    leaf[v] = 1;
+    for (uint32_t k = (*f.dn_off)[v]; k < (*f.dn_off)[v + 1]; ++k) blocked[(*f.dn)[k]] = 1;
+  }
+  return leaf;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- the sweep
+struct ospf_sweep {
+  ospf_ctx* c = nullptr;
+  ospf_sweep_opts opts{};
+  uint32_t mode = 0;
+  uint64_t gen = 0;
+  std::string err;
+  uint32_t V = 0;
+  std::vector<uint32_t> roots;          // owned roots, digest order
+  std::vector<uint32_t> own_slot;       // digest slot of roots[i] in dig_all
+  // row of each owned root: device pointers, by node id (null: not owned)
+  std::vector<const uint32_t*> row_dist, row_nh;
+  std::vector<uint32_t> row_w;
+  std::vector<void*> allocs;            // device allocations
+  uint64_t device_bytes = 0;
+  ospf_digest* dig_all = nullptr;       // every digest a run writes
+  uint32_t n_dig = 0;
+  std::vector<std::pair<ospf_digest*, size_t>> dig_aux;  // intermediate digests (poisoned too)
+  uint32_t* d_own_slot = nullptr;
+  uint32_t n_rows = 0;
+  uint64_t step_comp = 0;
+  // launches
+  struct Unit {
+    std::string name, kernel;
+    int stream = 0;            // index into streams (0 = main)
+    std::vector<int> wait;     // events waited for before the launch
+    int record = -1;           // event recorded after it
+    std::function<int(hipStream_t)> fn;
+    uint32_t n_roots = 0, W = 0;
+    uint64_t comp = 0;
+  };
+  std::vector<Unit> units;
+  std::vector<hipStream_t> streams;     // [0] = main
+  std::vector<hipEvent_t> events;       // [0] = run start
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  std::vector<hipEvent_t> ev_done;      // per non-main stream
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  bool ran = false;
+};
+
+namespace {
+
+int sfail(ospf_sweep* s, int code, const std::string& m) {
+  s->err = m;
+  if (s->c) s->c->err = m;
+  return code;
+}
+
+#define SCHK(sw, call)                                                               \
+  do {                                                                               \
+    hipError_t e_ = (call);                                                          \
+    if (e_ != hipSuccess)                                                            \
+      return sfail(sw, OSPF_E_DEVICE, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T>
+int dalloc(ospf_sweep* s, T** p, size_t count) {
+  void* q = nullptr;
+  const size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+  hipError_t e = hipMalloc(&q, bytes);
+  if (e != hipSuccess)
+    return sfail(s, OSPF_E_NOMEM, "sweep: hipMalloc " + std::to_string(bytes) + " B: " +
+                                      hipGetErrorString(e));
+  s->allocs.push_back(q);
+  s->device_bytes += bytes;
+  *p = (T*)q;
+  return OSPF_OK;
+}
+
+template <class T>
+int upload(ospf_sweep* s, T** p, const std::vector<T>& h) {
+  int rc = dalloc(s, p, h.size());
+  if (rc) return rc;
+  if (!h.empty()) SCHK(s, hipMemcpy(*p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  return OSPF_OK;
+}
+
+int new_stream(ospf_sweep* s) {
+  hipStream_t st;
+  SCHK(s, hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  s->streams.push_back(st);
+  return (int)s->streams.size() - 1;
+}
+
+int new_event(ospf_sweep* s) {
+  hipEvent_t e;
+  SCHK(s, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  s->events.push_back(e);
+  return (int)s->events.size() - 1;
+}
+
+// CSR bytes one distance-only scan reads: neighbour ids + row offsets
+uint64_t scan_bytes(const ospf_ctx* c, bool weighted) {
+  return (uint64_t)(weighted ? 8 : 4) * c->info.n_edges + 4ull * (c->info.n_nodes + 1);
+}
+
+// owned root r's digest is slot `slot` of dig_all; its rows are (d, nh, W)
+void own(ospf_sweep* s, uint32_t r, uint32_t slot, const uint32_t* d, const uint32_t* nh,
+         uint32_t W) {
+  s->roots.push_back(r);
+  s->own_slot.push_back(slot);
+  s->row_dist[r] = d;
+  s->row_nh[r] = nh;
+  s->row_w[r] = W;
+}
+
+// ---------------------------------------------------------------- plans
+// DERIVE (spf_levels.hip + spf_msbfs.hip derive kernels): levels for the
+// closure of the part (its roots and all their neighbours, ordered by each
+// node's smallest neighbour so a 128-root traversal shares frontiers), then
+// one next-hop launch per width class, each on its own stream, roots ordered
+// by their largest neighbour (a pod's racks / fabric switches, a plane's
+// spines next to each other: their neighbours' level rows stay in L2 / MALL).
+int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine) {
+  ospf_ctx* c = s->c;
+  const uint32_t V = s->V;
+  const uint32_t hop = s->opts.flags & OSPF_HOP_COUNT;
+  std::vector<uint32_t> clo = closure(f, mine);
+  locality_order(clo, [&](uint32_t v) { return f.first(v); });
+  std::vector<uint32_t> pos(V, kNone);
+  for (uint32_t i = 0; i < clo.size(); ++i) pos[clo[i]] = i;
+  const uint32_t pitch = (V + 15) / 16 * 16;
+  const uint32_t nc = (uint32_t)clo.size();
+  uint32_t *d_clo, *d_pos, *dist;
+  uint8_t* lev;
+  ospf_digest* ldg;
+  int rc;
+  if ((rc = upload(s, &d_clo, clo)) || (rc = upload(s, &d_pos, pos)) ||
+      (rc = dalloc(s, &lev, (size_t)nc * pitch)) || (rc = dalloc(s, &dist, (size_t)nc * V)) ||
+      (rc = dalloc(s, &ldg, nc)))
+    return rc;
+  s->dig_aux.push_back({ldg, nc});
+  s->n_rows = nc;
+  // classes by capacity, roots by largest neighbour
+  std::vector<uint32_t> caps;
+  for (uint32_t r : mine) caps.push_back(f.cap(r));
+  std::sort(caps.begin(), caps.end());
+  caps.erase(std::unique(caps.begin(), caps.end()), caps.end());
+  struct Cls {
+    uint32_t cap, W;
+    std::vector<uint32_t> roots;
+  };
+  std::vector<Cls> cls;
+  uint32_t ndig = 0;
+  for (uint32_t cap : caps) {
+    Cls k{cap, cap > 16 ? cap / 32 : 1u, {}};
+    for (uint32_t r : mine)
+      if (f.cap(r) == cap) k.roots.push_back(r);
+    locality_order(k.roots, [&](uint32_t v) { return f.last(v); });
+    ndig += (uint32_t)k.roots.size();
+    cls.push_back(std::move(k));
+  }
+  if ((rc = dalloc(s, &s->dig_all, ndig))) return rc;
+  s->n_dig = ndig;
+  const uint64_t scans = ((nc + 127) / 128) * scan_bytes(c, false);
+  ospf_sweep::Unit lv;
+  lv.name = "levels";
+  lv.kernel = "ospf_levels_dev (lv_init + lv_level/lv_settle per level + lv_rows: distance-only "
+              "128-root BFS, dist + level rows)";
+  lv.stream = 0;
+  lv.record = 1;
+  lv.n_roots = nc;
+  lv.W = 0;
+  lv.comp = (uint64_t)nc * 4ull * V + scans;
+  lv.fn = [=](hipStream_t st) {
+    return ospf_levels_dev(c, d_clo, nc, hop, dist, lev, pitch, ldg, st);
+  };
+  if ((rc = new_event(s)) < 0) return rc;  // event 1: levels done
+  s->units.push_back(lv);
+  s->step_comp += lv.comp;
+  uint32_t slot = 0;
+  // widest rows first: their launches are the longest
+  std::vector<size_t> order(cls.size());
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+    return (uint64_t)cls[a].W * cls[a].roots.size() > (uint64_t)cls[b].W * cls[b].roots.size();
+  });
+  std::vector<ospf_sweep::Unit> der(cls.size());
+  for (size_t i = 0; i < cls.size(); ++i) {
+    Cls& k = cls[i];
+    const uint32_t n = (uint32_t)k.roots.size(), W = k.W, cap = std::min(k.cap, 2048u);
+    uint32_t *d_roots, *nh;
+    if ((rc = upload(s, &d_roots, k.roots)) || (rc = dalloc(s, &nh, (size_t)n * V * W))) return rc;
+    ospf_digest* dg = s->dig_all + slot;
+    for (uint32_t j = 0; j < n; ++j)
+      own(s, k.roots[j], slot + j, dist + (size_t)pos[k.roots[j]] * V, nh + (size_t)j * V * W, W);
+    slot += n;
+    ospf_sweep::Unit u;
+    u.name = "derive_cap" + std::to_string(k.cap);
+    u.kernel = std::string("ospf_nh_derive_dev (") +
+               (W <= 4 ? "nh_derive16_kernel" : "nh_derive_wide_kernel") + ", " +
+               std::to_string(W) + " next-hop word" + (W > 1 ? "s)" : ")");
+    const int st = new_stream(s);
+    if (st < 0) return st;
+    u.stream = st;
+    u.wait = {1};
+    u.n_roots = n;
+    u.W = W;
+    u.comp = (uint64_t)n * 4ull * V * W;
+    u.fn = [=](hipStream_t strm) {
+      return ospf_nh_derive_dev(c, d_roots, n, W, cap, lev, pitch, d_pos, ldg, nh, dg, strm);
+    };
+    der[i] = std::move(u);
+    s->step_comp += (uint64_t)n * 4ull * V * W;
+  }
+  for (size_t i : order) s->units.push_back(std::move(der[i]));
+  return OSPF_OK;
+}
+
+// BATCH: one engine batch per width class of the part, each on its own
+// stream from the run's start (ospf_run_batch_dev picks the kernel).
+int plan_batch(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine,
+               bool weighted) {
+  ospf_ctx* c = s->c;
+  const uint32_t V = s->V;
+  std::vector<uint32_t> caps;
+  for (uint32_t r : mine) caps.push_back(f.cap(r));
+  std::sort(caps.begin(), caps.end());
+  caps.erase(std::unique(caps.begin(), caps.end()), caps.end());
+  int rc;
+  if ((rc = dalloc(s, &s->dig_all, mine.size()))) return rc;
+  s->n_dig = (uint32_t)mine.size();
+  s->n_rows = (uint32_t)mine.size();
+  uint32_t slot = 0;
+  const uint32_t flags = (s->opts.flags & OSPF_HOP_COUNT) | OSPF_WANT_DIST | OSPF_WANT_NH |
+                         OSPF_WANT_DIGEST;
+  for (uint32_t cap : caps) {
+    std::vector<uint32_t> roots;
+    uint32_t mx = 1;
+    for (uint32_t r : mine)
+      if (f.cap(r) == cap) {
+        roots.push_back(r);
+        mx = std::max(mx, f.nbrs(r));
+      }
+    locality_order(roots, [&](uint32_t v) { return f.first(v); });
+    const uint32_t n = (uint32_t)roots.size(), W = std::max(1u, (cap + 31) / 32);
+    uint32_t *d_roots, *dist, *nh;
+    if ((rc = upload(s, &d_roots, roots)) || (rc = dalloc(s, &dist, (size_t)n * V)) ||
+        (rc = dalloc(s, &nh, (size_t)n * V * W)))
+      return rc;
+    ospf_digest* dg = s->dig_all + slot;
+    for (uint32_t j = 0; j < n; ++j)
+      own(s, roots[j], slot + j, dist + (size_t)j * V, nh + (size_t)j * V * W, W);
+    slot += n;
+    ospf_plan_info pi{};
+    ospf_plan_n(c, flags, W, 0, n, mx, &pi);
+    ospf_sweep::Unit u;
+    u.name = "batch_cap" + std::to_string(cap);
+    u.kernel = "ospf_run_batch_dev (variant " + std::to_string(pi.variant) + ", " +
+               std::to_string(W) + " next-hop word" + (W > 1 ? "s)" : ")");
+    const int st = new_stream(s);
+    if (st < 0) return st;
+    u.stream = st;
+    u.wait = {0};
+    u.n_roots = n;
+    u.W = W;
+    const uint64_t scans = pi.variant == 5 ? (uint64_t)((n + 63) / 64) * pi.slices
+                                           : (uint64_t)n;
+    u.comp = (uint64_t)n * 4ull * V * (1 + W) + scans * scan_bytes(c, weighted && pi.variant != 5);
+    u.fn = [=](hipStream_t strm) {
+      ospf_batch b{};
+      b.d_roots = d_roots;
+      b.n_roots = n;
+      b.flags = flags;
+      b.nh_words = W;
+      b.max_root_neighbors = mx;
+      b.d_dist = dist;
+      b.d_nh = nh;
+      b.d_digest = dg;
+      return ospf_run_batch_dev(c, &b, strm);
+    };
+    s->step_comp += u.comp;
+    s->units.push_back(std::move(u));
+  }
+  return OSPF_OK;
+}
+
+// WCOVER (spf_cover.hip + spf_wderive.hip): an independent set of leaves
+// (<= 32 distinct neighbours; on a fabric the racks), the cover = the rest.
+// (A) distance rows of the cover nodes the part needs by the contracted-graph
+// SPF; (B) the leaves' dist + next-hop rows from their neighbours' rows;
+// (C) next hops of cover roots (<= 2048 neighbours) from their own and their
+// neighbours' rows, one launch per word count (> 4 words beside B). Cover
+// roots beyond 2048 neighbours run their own batch from the start.
+int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine,
+                const std::vector<uint8_t>& leaf) {
+  ospf_ctx* c = s->c;
+  const uint32_t V = s->V;
+  std::vector<uint32_t> own_l, own_c, c_der, c_wide;
+  for (uint32_t r : mine) (leaf[r] ? own_l : own_c).push_back(r);
+  for (uint32_t r : own_c) (f.nbrs(r) <= 2048 ? c_der : c_wide).push_back(r);
+  locality_order(own_l, [&](uint32_t v) { return f.first(v); });
+  std::sort(own_c.begin(), own_c.end());
+  const std::vector<uint32_t> nb_c = closure(f, c_der);
+  std::vector<uint8_t> in_l(V, 0);
+  for (uint32_t r : own_l) in_l[r] = 1;
+  std::vector<uint32_t> extra_l;  // leaves the cover next hops read, not owned
+  for (uint32_t v : nb_c)
+    if (leaf[v] && !in_l[v]) extra_l.push_back(v);
+  locality_order(extra_l, [&](uint32_t v) { return f.first(v); });
+  std::vector<uint32_t> need_l = own_l;
+  need_l.insert(need_l.end(), extra_l.begin(), extra_l.end());
+  const std::vector<uint32_t> cl = closure(f, need_l);
+  std::vector<uint8_t> in_a(V, 0);
+  for (uint32_t v : own_c) in_a[v] = 1;
+  for (uint32_t v : cl)
+    if (!leaf[v]) in_a[v] = 1;
+  for (uint32_t v : nb_c)
+    if (!leaf[v]) in_a[v] = 1;
+  std::vector<uint32_t> cover_a;
+  for (uint32_t v = 0; v < V; ++v)
+    if (in_a[v]) cover_a.push_back(v);
+  const uint32_t nA = (uint32_t)cover_a.size(), nL = (uint32_t)need_l.size();
+  std::vector<uint32_t> pos(V, kNone);
+  for (uint32_t i = 0; i < nA; ++i) pos[cover_a[i]] = i;
+  for (uint32_t i = 0; i < nL; ++i) pos[need_l[i]] = nA + i;
+  uint32_t *slab, *d_pos, *d_a, *d_l, *lnh;
+  int rc;
+  if ((rc = dalloc(s, &slab, (size_t)(nA + nL) * V)) || (rc = upload(s, &d_pos, pos)) ||
+      (rc = upload(s, &d_a, cover_a)) || (rc = upload(s, &d_l, need_l)) ||
+      (rc = dalloc(s, &lnh, (size_t)nL * V)))
+    return rc;
+  uint32_t kmax = 1;
+  for (uint32_t r : need_l) kmax = std::max(kmax, f.nbrs(r));
+  // digests: cover classes (owned), then need_l (owned leaves first)
+  std::vector<uint32_t> wset;
+  for (uint32_t r : c_der) wset.push_back(f.words(r));
+  std::sort(wset.begin(), wset.end());
+  wset.erase(std::unique(wset.begin(), wset.end()), wset.end());
+  const uint32_t ndig = (uint32_t)(c_der.size() + c_wide.size() + nL);
+  if ((rc = dalloc(s, &s->dig_all, ndig))) return rc;
+  s->n_dig = ndig;
+  s->n_rows = nA + nL;
+  const uint32_t flags = OSPF_WANT_DIST | OSPF_WANT_NH | OSPF_WANT_DIGEST;
+  uint32_t slot = 0;
+  int ev_a = new_event(s);  // cover rows done
+  if (ev_a < 0) return ev_a;
+  // wide cover roots: their own batch, from the start
+  if (!c_wide.empty()) {
+    std::vector<uint32_t> roots = c_wide;
+    locality_order(roots, [&](uint32_t v) { return f.first(v); });
+    uint32_t W = 1, mx = 1;
+    for (uint32_t r : roots) {
+      W = std::max(W, f.words(r));
+      mx = std::max(mx, f.nbrs(r));
+    }
+    const uint32_t n = (uint32_t)roots.size();
+    uint32_t *d_roots, *dist, *nh;
+    if ((rc = upload(s, &d_roots, roots)) || (rc = dalloc(s, &dist, (size_t)n * V)) ||
+        (rc = dalloc(s, &nh, (size_t)n * V * W)))
+      return rc;
+    ospf_digest* dg = s->dig_all + slot;
+    for (uint32_t j = 0; j < n; ++j)
+      own(s, roots[j], slot + j, dist + (size_t)j * V, nh + (size_t)j * V * W, W);
+    slot += n;
+    ospf_sweep::Unit u;
+    u.name = "cover_batch_w" + std::to_string(W);
+    u.kernel = "ospf_run_batch_dev (" + std::to_string(W) + " next-hop words)";
+    const int st = new_stream(s);
+    if (st < 0) return st;
+    u.stream = st;
+    u.wait = {0};
+    u.n_roots = n;
+    u.W = W;
+    u.comp = (uint64_t)n * 4ull * V * (1 + W) + (uint64_t)n * scan_bytes(c, true);
+    u.fn = [=](hipStream_t strm) {
+      ospf_batch b{};
+      b.d_roots = d_roots;
+      b.n_roots = n;
+      b.flags = flags;
+      b.nh_words = W;
+      b.max_root_neighbors = mx;
+      b.d_dist = dist;
+      b.d_nh = nh;
+      b.d_digest = dg;
+      return ospf_run_batch_dev(c, &b, strm);
+    };
+    s->step_comp += u.comp;
+    s->units.push_back(std::move(u));
+  }
+  // (A) cover rows
+  {
+    ospf_sweep::Unit u;
+    u.name = "cover_spf";
+    u.kernel = "ospf_cover_dist_dev (cover_spf_kernel: contracted-graph Dial, LDS-resident "
+               "distances)";
+    u.stream = 0;
+    u.record = ev_a;
+    u.n_roots = nA;
+    u.comp = (uint64_t)nA * 4ull * V + scan_bytes(c, true);
+    u.fn = [=](hipStream_t strm) { return ospf_cover_dist_dev(c, d_a, nA, slab, strm); };
+    s->step_comp += u.comp;
+    s->units.push_back(std::move(u));
+  }
+  // (C) classes of cover roots by word count
+  std::vector<ospf_sweep::Unit> narrow;
+  for (uint32_t W : wset) {
+    std::vector<uint32_t> roots;
+    for (uint32_t r : c_der)
+      if (f.words(r) == W) roots.push_back(r);
+    locality_order(roots, [&](uint32_t v) { return f.last(v); });
+    const uint32_t n = (uint32_t)roots.size();
+    uint32_t *d_roots, *nh;
+    if ((rc = upload(s, &d_roots, roots)) || (rc = dalloc(s, &nh, (size_t)n * V * W))) return rc;
+    ospf_digest* dg = s->dig_all + slot;
+    for (uint32_t j = 0; j < n; ++j)
+      own(s, roots[j], slot + j, slab + (size_t)pos[roots[j]] * V, nh + (size_t)j * V * W, W);
+    slot += n;
+    ospf_sweep::Unit u;
+    u.name = "wderive_wide_w" + std::to_string(W);
+    u.kernel = std::string("ospf_wderive_wide_dev (") +
+               (W <= 4 ? "wderive_wide_kernel<" + std::to_string(W) + ">"
+                       : std::string("wderive_lanes_kernel")) + ")";
+    u.n_roots = n;
+    u.W = W;
+    u.comp = (uint64_t)n * 4ull * V * W;
+    u.fn = [=](hipStream_t strm) {
+      return ospf_wderive_wide_dev(c, d_roots, n, 0, W, slab, V, d_pos, nh, dg, strm);
+    };
+    s->step_comp += u.comp;
+    bool reads_leaf = false;  // a neighbour's row comes from (B)
+    for (uint32_t r : roots)
+      for (uint32_t k = (*f.dn_off)[r]; k < (*f.dn_off)[r + 1] && !reads_leaf; ++k)
+        reads_leaf = leaf[(*f.dn)[k]] != 0;
+    if (W > 4 && !reads_leaf) {  // needs only the cover rows: beside the leaves
+      const int st = new_stream(s);
+      if (st < 0) return st;
+      u.stream = st;
+      u.wait = {ev_a};
+      s->units.push_back(std::move(u));
+    } else {
+      u.stream = 0;
+      narrow.push_back(std::move(u));
+    }
+  }
+  // (B) leaves, then the narrow cover classes (they read leaf rows)
+  {
+    ospf_digest* dg = s->dig_all + slot;
+    for (uint32_t j = 0; j < own_l.size(); ++j)
+      own(s, own_l[j], slot + j, slab + (size_t)(nA + j) * V, lnh + (size_t)j * V, 1);
+    slot += nL;
+    ospf_sweep::Unit u;
+    u.name = "wderive";
+    u.kernel = "ospf_wderive_dev (wderive_kernel: leaf rows from the cover rows)";
+    u.stream = 0;
+    u.n_roots = nL;
+    u.W = 1;
+    u.comp = (uint64_t)nL * 8ull * V +
+             (uint64_t)(cl.size() - std::min(cl.size(), (size_t)nL)) * 4ull * V;
+    uint32_t* ldist = slab + (size_t)nA * V;
+    u.fn = [=](hipStream_t strm) {
+      if (!nL) return OSPF_OK;
+      return ospf_wderive_dev(c, d_l, nL, 0, kmax, slab, V, d_pos, ldist, lnh, dg, strm);
+    };
+    s->step_comp += u.comp;
+    s->units.push_back(std::move(u));
+  }
+  for (auto& u : narrow) s->units.push_back(std::move(u));
+  return OSPF_OK;
+}
+
+// WDERIVE: cover roots (the part's non-leaves plus every neighbour of its
+// leaves) on the per-root batch path, one launch per class on its own
+// stream; then the leaves derived from those rows.
+int plan_wderive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine,
+                 const std::vector<uint8_t>& leaf) {
+  ospf_ctx* c = s->c;
+  const uint32_t V = s->V;
+  const uint32_t hop = s->opts.flags & OSPF_HOP_COUNT;
+  std::vector<uint32_t> lr, cov;
+  std::vector<uint8_t> own_m(V, 0);
+  for (uint32_t r : mine) {
+    own_m[r] = 1;
+    if (leaf[r]) lr.push_back(r);
+  }
+  std::vector<uint8_t> in_c(V, 0);
+  for (uint32_t r : mine)
+    if (!leaf[r]) in_c[r] = 1;
+  for (uint32_t v : closure(f, lr))
+    if (!leaf[v]) in_c[v] = 1;
+  for (uint32_t v = 0; v < V; ++v)
+    if (in_c[v]) cov.push_back(v);
+  locality_order(lr, [&](uint32_t v) { return f.first(v); });
+  std::vector<uint32_t> caps;
+  for (uint32_t r : cov) caps.push_back(f.cap(r));
+  std::sort(caps.begin(), caps.end());
+  caps.erase(std::unique(caps.begin(), caps.end()), caps.end());
+  const uint32_t nC = (uint32_t)cov.size(), nl = (uint32_t)lr.size();
+  uint32_t *cdist, *d_pos, *d_lr, *ldist, *lnh;
+  int rc;
+  if ((rc = dalloc(s, &cdist, (size_t)nC * V)) || (rc = upload(s, &d_lr, lr)) ||
+      (rc = dalloc(s, &ldist, (size_t)nl * V)) || (rc = dalloc(s, &lnh, (size_t)nl * V)) ||
+      (rc = dalloc(s, &s->dig_all, nC + nl)))
+    return rc;
+  s->n_dig = nC + nl;
+  s->n_rows = nC + nl;
+  std::vector<uint32_t> pos(V, kNone);
+  uint32_t off = 0;
+  const uint32_t flags = hop | OSPF_WANT_DIST | OSPF_WANT_NH | OSPF_WANT_DIGEST;
+  std::vector<int> done;
+  for (uint32_t cap : caps) {
+    std::vector<uint32_t> roots;
+    uint32_t mx = 1;
+    for (uint32_t r : cov)
+      if (f.cap(r) == cap) {
+        roots.push_back(r);
+        mx = std::max(mx, f.nbrs(r));
+      }
+    locality_order(roots, [&](uint32_t v) { return f.first(v); });
+    const uint32_t n = (uint32_t)roots.size(), W = std::max(1u, (cap + 31) / 32);
+    uint32_t *d_roots, *nh;
+    if ((rc = upload(s, &d_roots, roots)) || (rc = dalloc(s, &nh, (size_t)n * V * W))) return rc;
+    uint32_t* dist = cdist + (size_t)off * V;
+    ospf_digest* dg = s->dig_all + off;
+    for (uint32_t j = 0; j < n; ++j) {
+      pos[roots[j]] = off + j;
+      if (own_m[roots[j]])
+        own(s, roots[j], off + j, dist + (size_t)j * V, nh + (size_t)j * V * W, W);
+    }
+    off += n;
+    ospf_plan_info pi{};
+    ospf_plan_n(c, flags, W, 0, n, mx, &pi);
+    ospf_sweep::Unit u;
+    u.name = "cover_cap" + std::to_string(cap);
+    u.kernel = "ospf_run_batch_dev (variant " + std::to_string(pi.variant) + ", " +
+               std::to_string(W) + " next-hop word" + (W > 1 ? "s)" : ")");
+    const int st = new_stream(s);
+    if (st < 0) return st;
+    const int ev = new_event(s);
+    if (ev < 0) return ev;
+    u.stream = st;
+    u.wait = {0};
+    u.record = ev;
+    done.push_back(ev);
+    u.n_roots = n;
+    u.W = W;
+    const uint64_t scans = pi.variant == 5 ? (uint64_t)((n + 63) / 64) * pi.slices : n;
+    u.comp = (uint64_t)n * 4ull * V * (1 + W) + scans * scan_bytes(c, !hop && pi.variant != 5);
+    u.fn = [=](hipStream_t strm) {
+      ospf_batch b{};
+      b.d_roots = d_roots;
+      b.n_roots = n;
+      b.flags = flags;
+      b.nh_words = W;
+      b.max_root_neighbors = mx;
+      b.d_dist = dist;
+      b.d_nh = nh;
+      b.d_digest = dg;
+      return ospf_run_batch_dev(c, &b, strm);
+    };
+    s->step_comp += u.comp;
+    s->units.push_back(std::move(u));
+  }
+  if ((rc = upload(s, &d_pos, pos))) return rc;
+  // owned leaves: digests after the cover rows
+  for (uint32_t j = 0; j < nl; ++j)
+    own(s, lr[j], nC + j, ldist + (size_t)j * V, lnh + (size_t)j * V, 1);
+  uint32_t kmax = 1;
+  for (uint32_t r : lr) kmax = std::max(kmax, f.nbrs(r));
+  ospf_sweep::Unit u;
+  u.name = "wderive";
+  u.kernel = "ospf_wderive_dev (wderive_kernel: leaf rows from neighbours' dist rows)";
+  u.stream = 0;
+  u.wait = done;
+  u.n_roots = nl;
+  u.W = 1;
+  u.comp = (uint64_t)nl * 8ull * V + (uint64_t)nC * 4ull * V;
+  ospf_digest* dg = s->dig_all + nC;
+  u.fn = [=](hipStream_t strm) {
+    if (!nl) return OSPF_OK;
+    return ospf_wderive_dev(c, d_lr, nl, hop, kmax, cdist, V, d_pos, ldist, lnh, dg, strm);
+  };
+  s->step_comp += u.comp;
+  s->units.push_back(std::move(u));
+  return OSPF_OK;
+}
+
+// queue one run's launches; the run starts when `origin` (the main stream)
+// reaches this point and ends when main has waited for every other stream
+int enqueue(ospf_sweep* s) {
+  hipStream_t main = s->streams[0];
+  SCHK(s, hipEventRecord(s->events[0], main));
+  for (auto& u : s->units) {
+    hipStream_t st = s->streams[u.stream];
+    for (int e : u.wait)
+      if (!(e == 0 && u.stream == 0)) SCHK(s, hipStreamWaitEvent(st, s->events[e], 0));
+    const int rc = u.fn(st);
+    if (rc != OSPF_OK) return sfail(s, rc, std::string(u.name) + ": " + ospf_last_error(s->c));
+    if (u.record >= 0) SCHK(s, hipEventRecord(s->events[u.record], st));
+  }
+  for (size_t i = 1; i < s->streams.size(); ++i) {
+    SCHK(s, hipEventRecord(s->ev_done[i], s->streams[i]));
+    SCHK(s, hipStreamWaitEvent(main, s->ev_done[i], 0));
+  }
+  return OSPF_OK;
+}
+
+int run_eager(ospf_sweep* s, hipStream_t caller) {
+  SCHK(s, hipEventRecord(s->ev_in, caller));
+  SCHK(s, hipStreamWaitEvent(s->streams[0], s->ev_in, 0));
+  const int rc = enqueue(s);
+  if (rc) return rc;
+  SCHK(s, hipEventRecord(s->ev_out, s->streams[0]));
+  SCHK(s, hipStreamWaitEvent(caller, s->ev_out, 0));
+  return OSPF_OK;
+}
+
+void release(ospf_sweep* s) {
+  if (s->c) hipSetDevice(s->c->device);
+  for (hipStream_t st : s->streams)
+    if (st) hipStreamSynchronize(st);
+  if (s->exec) hipGraphExecDestroy(s->exec);
+  if (s->graph) hipGraphDestroy(s->graph);
+  for (void* p : s->allocs) hipFree(p);
+  for (hipEvent_t e : s->events) hipEventDestroy(e);
+  for (hipEvent_t e : s->ev_done)
+    if (e) hipEventDestroy(e);
+  if (s->ev_in) hipEventDestroy(s->ev_in);
+  if (s->ev_out) hipEventDestroy(s->ev_out);
+  for (hipStream_t st : s->streams) {
+    if (!st) continue;
+    if (s->c) release_stream_scratch(s->c, st);
+    hipStreamDestroy(st);
+  }
+  s->allocs.clear();
+  s->streams.clear();
+}
+
+}  // namespace
+
+extern "C" {
+
+int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
+  if (!c || !o || !out) return OSPF_E_INVAL;
+  *out = nullptr;
+  if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  if (c->mask.on) return fail(c, OSPF_E_INVAL, "sweep: links are masked (ospf_links_unmask)");
+  const uint32_t parts = std::max(1u, o->n_parts);
+  if (o->part >= parts) return fail(c, OSPF_E_INVAL, "sweep: part >= n_parts");
+  if (o->mode > OSPF_SWEEP_BATCH) return fail(c, OSPF_E_INVAL, "sweep: unknown mode");
+  if (o->flags & ~OSPF_HOP_COUNT) return fail(c, OSPF_E_INVAL, "sweep: flags = 0 or OSPF_HOP_COUNT");
+  const bool hop = o->flags & OSPF_HOP_COUNT;
+  if (!hop && c->dist_bound >= 0xFFFFFFFFull)
+    return fail(c, OSPF_E_RANGE, "u32 distance overflow possible (sum of per-node max metrics)");
+  ospf_sweep* s = new (std::nothrow) ospf_sweep();
+  if (!s) return OSPF_E_NOMEM;
+  s->c = c;
+  s->opts = *o;
+  s->gen = c->graph_gen;
+  s->V = c->info.n_nodes;
+  const uint32_t V = s->V;
+  s->row_dist.assign(V, nullptr);
+  s->row_nh.assign(V, nullptr);
+  s->row_w.assign(V, 0);
+  auto bail = [&](int rc) {
+    const std::string m = s->err.empty() ? std::string(ospf_last_error(c)) : s->err;
+    release(s);
+    delete s;
+    c->err = m;
+    return rc;
+  };
+  if (hipSetDevice(c->device) != hipSuccess) return bail(fail(c, OSPF_E_DEVICE, "hipSetDevice"));
+  if (new_stream(s) < 0 || new_event(s) < 0) return bail(OSPF_E_DEVICE);
+  if (hipEventCreateWithFlags(&s->ev_in, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&s->ev_out, hipEventDisableTiming) != hipSuccess)
+    return bail(fail(c, OSPF_E_DEVICE, "hipEventCreate"));
+  Facts f;
+  f.V = V;
+  f.dn_off = &c->h_dn_off;
+  f.dn = &c->h_dn;
+  const std::vector<uint32_t> mine = partition(f, parts, o->part);
+  // path
+  const bool unit = hop || c->info.unit_metric;
+  const bool derive_ok = unit && c->max_dn <= 2048 && c->depth_bound <= 123;
+  std::vector<uint8_t> leaf;
+  bool any_leaf = false;
+  uint32_t mode = o->mode;
+  if (mode == OSPF_SWEEP_AUTO || mode == OSPF_SWEEP_WCOVER || mode == OSPF_SWEEP_WDERIVE) {
+    if (!(mode == OSPF_SWEEP_AUTO && derive_ok)) {
+      leaf = leaf_set(f);
+      for (uint8_t x : leaf) any_leaf |= x != 0;
+    }
+  }
+  if (mode == OSPF_SWEEP_AUTO) {
+    if (derive_ok) {
+      mode = OSPF_SWEEP_DERIVE;
+    } else if (!hop && any_leaf && ospf_cover_prepare(c, leaf.data()) == OSPF_OK) {
+      mode = OSPF_SWEEP_WCOVER;
+    } else if (any_leaf) {
+      mode = OSPF_SWEEP_WDERIVE;
+    } else {
+      mode = OSPF_SWEEP_BATCH;
+    }
+  } else if (mode == OSPF_SWEEP_DERIVE && !derive_ok) {
+    return bail(fail(c, OSPF_E_RANGE, "sweep: derive needs unit metric or hop count, a depth "
+                                      "bound <= 123 and <= 2048 distinct neighbours per node"));
+  } else if (mode == OSPF_SWEEP_WCOVER) {
+    if (hop) return bail(fail(c, OSPF_E_INVAL, "sweep: the cover path runs link metrics"));
+    const int rc = ospf_cover_prepare(c, leaf.data());
+    if (rc) return bail(rc);
+  }
+  s->mode = mode;
+  int rc = OSPF_OK;
+  switch (mode) {
+    case OSPF_SWEEP_DERIVE: rc = plan_derive(s, f, mine); break;
+    case OSPF_SWEEP_WCOVER: rc = plan_wcover(s, f, mine, leaf); break;
+    case OSPF_SWEEP_WDERIVE: rc = plan_wderive(s, f, mine, leaf); break;
+    default: rc = plan_batch(s, f, mine, !unit); break;
+  }
+  if (rc) return bail(rc);
+  if (upload(s, &s->d_own_slot, s->own_slot)) return bail(OSPF_E_NOMEM);
+  s->ev_done.assign(s->streams.size(), nullptr);
+  for (size_t i = 1; i < s->streams.size(); ++i)
+    if (hipEventCreateWithFlags(&s->ev_done[i], hipEventDisableTiming) != hipSuccess)
+      return bail(fail(c, OSPF_E_DEVICE, "hipEventCreate"));
+  // one eager run: sizes every stream's scratch (nothing may allocate inside
+  // a capture) and surfaces launch errors here
+  const uint64_t runs0 = c->spf_runs;
+  if ((rc = run_eager(s, s->streams[0]))) return bail(rc);
+  if (hipStreamSynchronize(s->streams[0]) != hipSuccess)
+    return bail(fail(c, OSPF_E_DEVICE, "sweep: first run failed"));
+  if ((rc = ospf_sync(c, s->streams[0]))) return bail(rc);
+  s->ran = true;
+  if (o->hip_graph) {
+    hipStream_t m = s->streams[0];
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ex = nullptr;
+    bool ok = hipStreamBeginCapture(m, hipStreamCaptureModeRelaxed) == hipSuccess;
+    if (ok) {
+      const int erc = enqueue(s);
+      ok = hipStreamEndCapture(m, &g) == hipSuccess && erc == OSPF_OK && g;
+    }
+    ok = ok && hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) == hipSuccess;
+    if (ok) {
+      s->graph = g;
+      s->exec = ex;
+    } else {
+      if (ex) hipGraphExecDestroy(ex);
+      if (g) hipGraphDestroy(g);
+      (void)hipGetLastError();
+      s->err.clear();
+    }
+  }
+  c->spf_runs = runs0;
+  *out = s;
+  return OSPF_OK;
+}
+
+int ospf_sweep_destroy(ospf_sweep* s) {
+  if (!s) return OSPF_E_INVAL;
+  release(s);
+  delete s;
+  return OSPF_OK;
+}
+
+const char* ospf_sweep_last_error(const ospf_sweep* s) {
+  return s ? s->err.c_str() : "null sweep";
+}
+
+int ospf_sweep_get_info(const ospf_sweep* s, ospf_sweep_info* info) {
+  if (!s || !info) return OSPF_E_INVAL;
+  info->mode = s->mode;
+  info->n_roots = (uint32_t)s->roots.size();
+  info->n_rows = s->n_rows;
+  info->n_launches = (uint32_t)s->units.size();
+  info->hip_graph = s->exec ? 1u : 0u;
+  uint32_t mw = 0;
+  for (uint32_t r : s->roots) mw = std::max(mw, s->row_w[r]);
+  info->max_nh_words = mw;
+  info->device_bytes = s->device_bytes;
+  info->step_compulsory_bytes = s->step_comp;
+  return OSPF_OK;
+}
+
+int ospf_sweep_roots(const ospf_sweep* s, uint32_t* roots) {
+  if (!s || (!roots && !s->roots.empty())) return OSPF_E_INVAL;
+  std::copy(s->roots.begin(), s->roots.end(), roots);
+  return OSPF_OK;
+}
+
+int ospf_sweep_run(ospf_sweep* s, void* stream) {
+  if (!s) return OSPF_E_INVAL;
+  ospf_ctx* c = s->c;
+  if (c->graph_gen != s->gen || c->mask.on)
+    return sfail(s, OSPF_E_NOGRAPH, "sweep: the graph changed since the sweep was created");
+  SCHK(s, hipSetDevice(c->device));
+  const uint64_t runs0 = c->spf_runs;
+  if (s->exec) {
+    SCHK(s, hipGraphLaunch(s->exec, (hipStream_t)stream));
+  } else {
+    const int rc = run_eager(s, (hipStream_t)stream);
+    if (rc) return rc;
+  }
+  c->spf_runs = runs0 + s->roots.size();
+  return OSPF_OK;
+}
+
+int ospf_sweep_digests(ospf_sweep* s, ospf_digest* d_out, void* stream) {
+  if (!s || (!d_out && !s->roots.empty())) return OSPF_E_INVAL;
+  const uint32_t n = (uint32_t)s->roots.size();
+  if (!n) return OSPF_OK;
+  SCHK(s, hipSetDevice(s->c->device));
+  hipLaunchKernelGGL(gather_digest_kernel, dim3((n + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, s->dig_all, s->d_own_slot, n, d_out);
+  SCHK(s, hipGetLastError());
+  return OSPF_OK;
+}
+
+int ospf_sweep_digests_host(ospf_sweep* s, ospf_digest* out) {
+  if (!s || (!out && !s->roots.empty())) return OSPF_E_INVAL;
+  const size_t n = s->roots.size();
+  if (!n) return OSPF_OK;
+  SCHK(s, hipSetDevice(s->c->device));
+  ospf_digest* d = nullptr;
+  SCHK(s, hipMalloc(&d, n * sizeof(ospf_digest)));
+  int rc = ospf_sweep_digests(s, d, nullptr);
+  hipError_t e = hipSuccess;
+  if (rc == OSPF_OK) e = hipMemcpy(out, d, n * sizeof(ospf_digest), hipMemcpyDeviceToHost);
+  hipFree(d);
+  if (e != hipSuccess) return sfail(s, OSPF_E_DEVICE, std::string("hipMemcpy: ") + hipGetErrorString(e));
+  return rc;
+}
+
+int ospf_sweep_poison(ospf_sweep* s, void* stream) {
+  if (!s) return OSPF_E_INVAL;
+  SCHK(s, hipSetDevice(s->c->device));
+  SCHK(s, hipMemsetAsync(s->dig_all, 0xFF, (size_t)std::max(1u, s->n_dig) * sizeof(ospf_digest),
+                         (hipStream_t)stream));
+  for (auto& a : s->dig_aux)
+    SCHK(s, hipMemsetAsync(a.first, 0xFF, std::max<size_t>(1, a.second) * sizeof(ospf_digest),
+                           (hipStream_t)stream));
+  return OSPF_OK;
+}
+
+int ospf_sweep_row(const ospf_sweep* s, uint32_t root, const uint32_t** d_dist,
+                   const uint32_t** d_nh, uint32_t* nh_words) {
+  if (!s || root >= s->V) return OSPF_E_INVAL;
+  if (!s->row_dist[root]) return OSPF_E_RANGE;
+  if (d_dist) *d_dist = s->row_dist[root];
+  if (d_nh) *d_nh = s->row_nh[root];
+  if (nh_words) *nh_words = s->row_w[root];
+  return OSPF_OK;
+}
+
+int ospf_sweep_copy_rows(ospf_sweep* s, const uint32_t* roots, uint32_t n, uint32_t nh_words,
+                         uint32_t* dist_out, uint32_t* nh_out) {
+  if (!s || (n && !roots)) return OSPF_E_INVAL;
+  const uint32_t V = s->V;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (roots[i] >= V || !s->row_dist[roots[i]])
+      return sfail(s, OSPF_E_RANGE, "sweep: root " + std::to_string(roots[i]) + " not owned");
+    if (nh_out && s->row_w[roots[i]] > nh_words)
+      return sfail(s, OSPF_E_INVAL, "sweep: nh_words below a root's next-hop words");
+  }
+  SCHK(s, hipSetDevice(s->c->device));
+  SCHK(s, hipDeviceSynchronize());
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t r = roots[i], W = s->row_w[r];
+    if (dist_out)
+      SCHK(s, hipMemcpy(dist_out + (size_t)i * V, s->row_dist[r], (size_t)V * 4,
+                        hipMemcpyDeviceToHost));
+    if (nh_out) {
+      uint32_t* dst = nh_out + (size_t)i * V * nh_words;
+      if (W == nh_words) {
+        SCHK(s, hipMemcpy(dst, s->row_nh[r], (size_t)V * W * 4, hipMemcpyDeviceToHost));
+      } else {
+        std::memset(dst, 0, (size_t)V * nh_words * 4);
+        SCHK(s, hipMemcpy2D(dst, (size_t)nh_words * 4, s->row_nh[r], (size_t)W * 4, (size_t)W * 4,
+                            V, hipMemcpyDeviceToHost));
+      }
+    }
+  }
+  return OSPF_OK;
+}
+
+int ospf_sweep_profile(ospf_sweep* s, uint32_t reps, ospf_sweep_launch* out, uint32_t cap) {
+  if (!s || (cap && !out)) return OSPF_E_INVAL;
+  if (!s->ran) return sfail(s, OSPF_E_INVAL, "sweep: profile needs one run first");
+  ospf_ctx* c = s->c;
+  if (c->graph_gen != s->gen) return sfail(s, OSPF_E_NOGRAPH, "sweep: the graph changed");
+  reps = std::max(1u, reps);
+  SCHK(s, hipSetDevice(c->device));
+  SCHK(s, hipDeviceSynchronize());
+  const uint64_t runs0 = c->spf_runs;
+  hipEvent_t a, b;
+  SCHK(s, hipEventCreate(&a));
+  SCHK(s, hipEventCreate(&b));
+  for (size_t i = 0; i < s->units.size() && i < cap; ++i) {
+    auto& u = s->units[i];
+    hipStream_t st = s->streams[u.stream];
+    std::vector<double> ms;
+    for (uint32_t k = 0; k <= reps; ++k) {
+      SCHK(s, hipEventRecord(a, st));
+      const int rc = u.fn(st);
+      if (rc) return sfail(s, rc, u.name + ": " + ospf_last_error(c));
+      SCHK(s, hipEventRecord(b, st));
+      SCHK(s, hipEventSynchronize(b));
+      float t = 0;
+      SCHK(s, hipEventElapsedTime(&t, a, b));
+      if (k) ms.push_back(t);
+    }
+    std::sort(ms.begin(), ms.end());
+    ospf_sweep_launch& L = out[i];
+    std::memset(&L, 0, sizeof(L));
+    std::snprintf(L.name, sizeof(L.name), "%s", u.name.c_str());
+    std::snprintf(L.kernel, sizeof(L.kernel), "%s", u.kernel.c_str());
+    L.n_roots = u.n_roots;
+    L.nh_words = u.W;
+    L.compulsory_bytes = u.comp;
+    L.ms_median = ms[ms.size() / 2];
+    L.ms_min = ms.front();
+  }
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+  c->spf_runs = runs0;
+  return ospf_sync(c, nullptr);
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- devices
+struct ospf_multi {
+  std::vector<ospf_ctx*> ctx;
+  std::string err;
+};
+
+struct ospf_msweep {
+  ospf_multi* m = nullptr;
+  std::vector<ospf_sweep*> parts;
+  std::vector<uint32_t> owner;          // slot owning each node (kNone: none)
+  uint32_t V = 0;
+  ospf_digest* d_all = nullptr;         // device 0: [total owned] part digests, part order
+  uint32_t* d_roots = nullptr;          // device 0: their root ids
+  ospf_digest* d_by_node = nullptr;     // device 0: [V]
+  std::vector<ospf_digest*> d_part;     // per slot (on its device): [n_roots]
+  uint32_t total = 0;
+};
+
+extern "C" {
+
+int ospf_multi_open(const int* devices, uint32_t n, ospf_multi** out) {
+  if (!devices || !n || !out) return OSPF_E_INVAL;
+  *out = nullptr;
+  ospf_multi* m = new (std::nothrow) ospf_multi();
+  if (!m) return OSPF_E_NOMEM;
+  for (uint32_t i = 0; i < n; ++i) {
+    ospf_ctx* c = nullptr;
+    const int rc = ospf_open(devices[i], &c);
+    if (rc) {
+      for (ospf_ctx* x : m->ctx) ospf_close(x);
+      delete m;
+      return rc;
+    }
+    m->ctx.push_back(c);
+  }
+  // peer access between distinct devices (xGMI); same-device slots need none
+  for (uint32_t i = 0; i < n; ++i)
+    for (uint32_t j = 0; j < n; ++j) {
+      if (devices[i] == devices[j]) continue;
+      int can = 0;
+      hipDeviceCanAccessPeer(&can, devices[i], devices[j]);
+      if (can) {
+        hipSetDevice(devices[i]);
+        hipDeviceEnablePeerAccess(devices[j], 0);
+        (void)hipGetLastError();  // already enabled
+      }
+    }
+  *out = m;
+  return OSPF_OK;
+}
+
+int ospf_multi_close(ospf_multi* m) {
+  if (!m) return OSPF_E_INVAL;
+  for (ospf_ctx* c : m->ctx) ospf_close(c);
+  delete m;
+  return OSPF_OK;
+}
+
+const char* ospf_multi_last_error(const ospf_multi* m) { return m ? m->err.c_str() : "null"; }
+
+uint32_t ospf_multi_size(const ospf_multi* m) { return m ? (uint32_t)m->ctx.size() : 0u; }
+
+ospf_ctx* ospf_multi_ctx(ospf_multi* m, uint32_t i) {
+  return (m && i < m->ctx.size()) ? m->ctx[i] : nullptr;
+}
+
+int ospf_multi_load_graph(ospf_multi* m, const ospf_csr* csr, uint64_t version) {
+  if (!m) return OSPF_E_INVAL;
+  for (ospf_ctx* c : m->ctx) {
+    const int rc = ospf_load_graph(c, csr, version);
+    if (rc) {
+      m->err = ospf_last_error(c);
+      return rc;
+    }
+  }
+  return OSPF_OK;
+}
+
+int ospf_msweep_destroy(ospf_msweep* ms) {
+  if (!ms) return OSPF_E_INVAL;
+  for (size_t i = 0; i < ms->parts.size(); ++i) {
+    if (i < ms->d_part.size() && ms->d_part[i]) {
+      hipSetDevice(ms->m->ctx[i]->device);
+      hipFree(ms->d_part[i]);
+    }
+    ospf_sweep_destroy(ms->parts[i]);
+  }
+  if (!ms->m->ctx.empty()) hipSetDevice(ms->m->ctx[0]->device);
+  if (ms->d_all) hipFree(ms->d_all);
+  if (ms->d_roots) hipFree(ms->d_roots);
+  if (ms->d_by_node) hipFree(ms->d_by_node);
+  delete ms;
+  return OSPF_OK;
+}
+
+int ospf_msweep_create(ospf_multi* m, const ospf_sweep_opts* o, ospf_msweep** out) {
+  if (!m || !o || !out || m->ctx.empty()) return OSPF_E_INVAL;
+  *out = nullptr;
+  ospf_msweep* ms = new (std::nothrow) ospf_msweep();
+  if (!ms) return OSPF_E_NOMEM;
+  ms->m = m;
+  const uint32_t n = (uint32_t)m->ctx.size();
+  auto bail = [&](int rc, const std::string& msg) {
+    m->err = msg;
+    ospf_msweep_destroy(ms);
+    return rc;
+  };
+  ms->V = m->ctx[0]->info.n_nodes;
+  ms->owner.assign(ms->V, kNone);
+  std::vector<uint32_t> all_roots;
+  for (uint32_t i = 0; i < n; ++i) {
+    ospf_sweep_opts oi = *o;
+    oi.part = i;
+    oi.n_parts = n;
+    ospf_sweep* s = nullptr;
+    const int rc = ospf_sweep_create(m->ctx[i], &oi, &s);
+    if (rc) return bail(rc, ospf_last_error(m->ctx[i]));
+    ms->parts.push_back(s);
+    for (uint32_t r : s->roots) ms->owner[r] = i;
+    all_roots.insert(all_roots.end(), s->roots.begin(), s->roots.end());
+    ospf_digest* dp = nullptr;
+    hipSetDevice(m->ctx[i]->device);
+    if (hipMalloc(&dp, std::max<size_t>(1, s->roots.size()) * sizeof(ospf_digest)) != hipSuccess)
+      return bail(OSPF_E_NOMEM, "msweep: hipMalloc");
+    ms->d_part.push_back(dp);
+  }
+  ms->total = (uint32_t)all_roots.size();
+  hipSetDevice(m->ctx[0]->device);
+  if (hipMalloc(&ms->d_all, std::max<size_t>(1, ms->total) * sizeof(ospf_digest)) != hipSuccess ||
+      hipMalloc(&ms->d_roots, std::max<size_t>(1, ms->total) * 4) != hipSuccess ||
+      hipMalloc(&ms->d_by_node, (size_t)ms->V * sizeof(ospf_digest)) != hipSuccess)
+    return bail(OSPF_E_NOMEM, "msweep: hipMalloc");
+  if (hipMemcpy(ms->d_roots, all_roots.data(), all_roots.size() * 4, hipMemcpyHostToDevice) !=
+      hipSuccess)
+    return bail(OSPF_E_DEVICE, "msweep: hipMemcpy");
+  *out = ms;
+  return OSPF_OK;
+}
+
+int ospf_msweep_run(ospf_msweep* ms) {
+  if (!ms) return OSPF_E_INVAL;
+  // queue every device's run first, then wait: the devices run concurrently
+  for (size_t i = 0; i < ms->parts.size(); ++i) {
+    const int rc = ospf_sweep_run(ms->parts[i], nullptr);
+    if (rc) {
+      ms->m->err = ospf_sweep_last_error(ms->parts[i]);
+      return rc;
+    }
+  }
+  for (size_t i = 0; i < ms->parts.size(); ++i) {
+    const int rc = ospf_sync(ms->m->ctx[i], nullptr);
+    if (rc) {
+      ms->m->err = ospf_last_error(ms->m->ctx[i]);
+      return rc;
+    }
+  }
+  return OSPF_OK;
+}
+
+int ospf_msweep_digests(ospf_msweep* ms, ospf_digest* out) {
+  if (!ms || !out) return OSPF_E_INVAL;
+  ospf_ctx* c0 = ms->m->ctx[0];
+  size_t off = 0;
+  for (size_t i = 0; i < ms->parts.size(); ++i) {
+    ospf_sweep* s = ms->parts[i];
+    const size_t n = s->roots.size();
+    int rc = ospf_sweep_digests(s, ms->d_part[i], nullptr);
+    if (rc) {
+      ms->m->err = s->err;
+      return rc;
+    }
+    hipSetDevice(ms->m->ctx[i]->device);
+    if (hipDeviceSynchronize() != hipSuccess) return OSPF_E_DEVICE;
+    if (n && hipMemcpyPeer(ms->d_all + off, c0->device, ms->d_part[i], ms->m->ctx[i]->device,
+                           n * sizeof(ospf_digest)) != hipSuccess) {
+      ms->m->err = "msweep: hipMemcpyPeer";
+      return OSPF_E_DEVICE;
+    }
+    off += n;
+  }
+  hipSetDevice(c0->device);
+  hipMemset(ms->d_by_node, 0, (size_t)ms->V * sizeof(ospf_digest));
+  if (ms->total)
+    hipLaunchKernelGGL(scatter_digest_kernel, dim3((ms->total + 255) / 256), dim3(256), 0, 0,
+                       ms->d_all, ms->d_roots, ms->total, ms->d_by_node);
+  if (hipMemcpy(out, ms->d_by_node, (size_t)ms->V * sizeof(ospf_digest), hipMemcpyDeviceToHost) !=
+      hipSuccess) {
+    ms->m->err = "msweep: hipMemcpy";
+    return OSPF_E_DEVICE;
+  }
+  return OSPF_OK;
+}
+
+ospf_sweep* ospf_msweep_part(ospf_msweep* ms, uint32_t slot) {
+  return (ms && slot < ms->parts.size()) ? ms->parts[slot] : nullptr;
+}
+
+int ospf_msweep_owner(const ospf_msweep* ms, uint32_t root, uint32_t* slot) {
+  if (!ms || !slot || root >= ms->V) return OSPF_E_INVAL;
+  if (ms->owner[root] == kNone) return OSPF_E_RANGE;
+  *slot = ms->owner[root];
+  return OSPF_OK;
+}
+
+}  // extern "C"

@@ -269,3 +269,174 @@ class Engine:
 
     def sync(self, stream: int = 0) -> None:
         self._check(self._L.ospf_sync(self._h, stream or None))
+
+    def links_mask(self, link_ids, version: int) -> None:
+        ids = np.ascontiguousarray(link_ids, np.uint32)
+        self._check(self._L.ospf_links_mask(self._h, ids.ctypes.data, ids.size, version))
+
+    def links_unmask(self) -> None:
+        self._check(self._L.ospf_links_unmask(self._h))
+
+    def sweep(self, **kw) -> "Sweep":
+        return Sweep(self, **kw)
+
+
+class Sweep:
+    """All-sources sweep (ospf_sweep_*): runSpf for every node of the graph,
+    or for part `part` of `n_parts` of the root partition; the library owns
+    the path, the width classes, their streams, the row buffers and the HIP
+    graph one run replays. ``run(stream)`` queues one sweep."""
+
+    def __init__(self, engine: "Engine", *, hop_count: bool = False, mode: str = "auto",
+                 part: int = 0, n_parts: int = 1, hip_graph: bool = True, _handle=None):
+        self._L = N.engine()
+        self.engine = engine
+        if _handle is not None:  # a part of an ospf_msweep (owned by it)
+            self._h, self._owned = _handle, False
+        else:
+            o = N.ospf_sweep_opts(N.OSPF_HOP_COUNT if hop_count else 0, N.SWEEP_MODES[mode],
+                                  part, n_parts, int(hip_graph))
+            h = C.c_void_p()
+            rc = self._L.ospf_sweep_create(engine._h, C.byref(o), C.byref(h))
+            if rc != 0:
+                raise EngineError(rc, self._L.ospf_last_error(engine._h).decode())
+            self._h, self._owned = h, True
+        gi = N.ospf_sweep_info()
+        self._check(self._L.ospf_sweep_get_info(self._h, C.byref(gi)))
+        self.mode = N.SWEEP_MODE_NAMES[gi.mode]
+        self.n_roots = int(gi.n_roots)
+        self.n_rows = int(gi.n_rows)
+        self.n_launches = int(gi.n_launches)
+        self.hip_graph = bool(gi.hip_graph)
+        self.max_nh_words = int(gi.max_nh_words)
+        self.device_bytes = int(gi.device_bytes)
+        self.step_compulsory_bytes = int(gi.step_compulsory_bytes)
+        r = np.zeros(max(1, self.n_roots), np.uint32)
+        self._check(self._L.ospf_sweep_roots(self._h, r.ctypes.data))
+        self.roots = r[: self.n_roots]
+
+    def close(self):
+        if getattr(self, "_h", None) and self._owned:
+            self._L.ospf_sweep_destroy(self._h)
+        self._h = None
+
+    __del__ = close
+
+    def _check(self, rc: int):
+        if rc != 0:
+            raise EngineError(rc, self._L.ospf_sweep_last_error(self._h).decode())
+
+    def run(self, stream: int = 0) -> None:
+        self._check(self._L.ospf_sweep_run(self._h, stream or None))
+
+    def digests_dev(self, d_out: int, stream: int = 0) -> None:
+        """Digests of the owned roots (roots order) into device memory [n][3] u64."""
+        self._check(self._L.ospf_sweep_digests(self._h, d_out, stream or None))
+
+    def poison(self, stream: int = 0) -> None:
+        self._check(self._L.ospf_sweep_poison(self._h, stream or None))
+
+    def row(self, root: int):
+        """(device dist row pointer, device next-hop row pointer, next-hop words)."""
+        d, nh, w = C.c_void_p(), C.c_void_p(), C.c_uint32()
+        self._check(self._L.ospf_sweep_row(self._h, int(root), C.byref(d), C.byref(nh),
+                                           C.byref(w)))
+        return d.value, nh.value, int(w.value)
+
+    def rows(self, roots: Sequence[int], nh_words: int = 0):
+        """Host copies of owned roots' rows: dist [n, V] u32, nh [n, V, W] u32
+        (W = nh_words or the widest of the roots)."""
+        roots = np.ascontiguousarray(roots, np.uint32)
+        V = self.engine.V
+        W = nh_words or max([self.row(r)[2] for r in roots.tolist()] or [1])
+        dist = np.zeros((roots.size, V), np.uint32)
+        nh = np.zeros((roots.size, V, W), np.uint32)
+        self._check(self._L.ospf_sweep_copy_rows(self._h, roots.ctypes.data, roots.size, W,
+                                                 dist.ctypes.data, nh.ctypes.data))
+        return dist, nh
+
+    def profile(self, reps: int = 3):
+        """Every launch unit timed alone on its stream -> list of dicts."""
+        cap = max(1, self.n_launches)
+        arr = (N.ospf_sweep_launch * cap)()
+        self._check(self._L.ospf_sweep_profile(self._h, reps, arr, cap))
+        return [dict(name=a.name.decode(), kernel=a.kernel.decode(), n_roots=int(a.n_roots),
+                     nh_words=int(a.nh_words), compulsory_bytes=int(a.compulsory_bytes),
+                     ms_median=float(a.ms_median), ms_min=float(a.ms_min))
+                for a in arr[: self.n_launches]]
+
+
+class Multi:
+    """Several devices behind one handle (ospf_multi_*): the graph replicated,
+    sweeps partitioned by device slot, digests gathered by peer copies."""
+
+    def __init__(self, devices: Sequence[int]):
+        self._L = N.engine()
+        devs = np.ascontiguousarray(devices, np.int32)
+        h = C.c_void_p()
+        rc = self._L.ospf_multi_open(devs.ctypes.data, devs.size, C.byref(h))
+        if rc != 0:
+            raise EngineError(rc, f"ospf_multi_open({list(devices)}) failed")
+        self._h = h
+        self.n = int(self._L.ospf_multi_size(h))
+        self.V = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.ospf_multi_close(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def _check(self, rc: int):
+        if rc != 0:
+            raise EngineError(rc, self._L.ospf_multi_last_error(self._h).decode())
+
+    def load(self, csr: Dict[str, np.ndarray], version: int = 1) -> None:
+        s, keep = csr_struct(csr)
+        self._check(self._L.ospf_multi_load_graph(self._h, C.byref(s), version))
+        self.V = int(s.n_nodes)
+
+
+class MultiSweep:
+    """ospf_msweep_*: one sweep part per device slot of a Multi."""
+
+    def __init__(self, multi: Multi, *, hop_count: bool = False, mode: str = "auto",
+                 hip_graph: bool = True):
+        self._L = N.engine()
+        self.multi = multi
+        o = N.ospf_sweep_opts(N.OSPF_HOP_COUNT if hop_count else 0, N.SWEEP_MODES[mode], 0, 0,
+                              int(hip_graph))
+        h = C.c_void_p()
+        rc = self._L.ospf_msweep_create(multi._h, C.byref(o), C.byref(h))
+        if rc != 0:
+            raise EngineError(rc, self._L.ospf_multi_last_error(multi._h).decode())
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.ospf_msweep_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def run(self) -> None:
+        self.multi._check(self._L.ospf_msweep_run(self._h))
+
+    def digests(self) -> np.ndarray:
+        out = np.zeros((self.multi.V, 3), np.uint64)
+        self.multi._check(self._L.ospf_msweep_digests(self._h, out.ctypes.data))
+        return out
+
+    def owner(self, root: int) -> int:
+        s = C.c_uint32()
+        self.multi._check(self._L.ospf_msweep_owner(self._h, int(root), C.byref(s)))
+        return int(s.value)
+
+    def part_roots(self, slot: int) -> np.ndarray:
+        h = self._L.ospf_msweep_part(self._h, slot)
+        gi = N.ospf_sweep_info()
+        self._L.ospf_sweep_get_info(h, C.byref(gi))
+        r = np.zeros(max(1, gi.n_roots), np.uint32)
+        self._L.ospf_sweep_roots(h, r.ctypes.data)
+        return r[: gi.n_roots]

@@ -49,10 +49,17 @@ def _parse_spf(t: str) -> Dict[str, Tuple[int, tuple, tuple]]:
 class LinkState:
     """odl::LinkState over the MI355X SPF engine (device `device`)."""
 
-    def __init__(self, area: str = "0", device: int = 0, stream: Optional[AdjDbStream] = None):
+    def __init__(self, area: str = "0", device: int = 0, stream: Optional[AdjDbStream] = None,
+                 devices: Optional[Sequence[int]] = None):
         self._L = N.decision()
         h = C.c_void_p()
-        if self._L.odl_create(area.encode(), device, C.byref(h)) != 0:
+        if devices is not None and len(devices) > 1:
+            devs = np.ascontiguousarray(devices, np.int32)
+            rc = self._L.odl_create_multi(area.encode(), devs.ctypes.data, devs.size, C.byref(h))
+        else:
+            rc = self._L.odl_create(area.encode(), device if devices is None else devices[0],
+                                    C.byref(h))
+        if rc != 0:
             raise LinkStateError("odl_create failed")
         self._h = h
         if stream is not None:
@@ -235,6 +242,24 @@ class LinkState:
                                    int(use_link_metric), out.ctypes.data) != 0:
             raise LinkStateError(self._err())
         return out
+
+    def all_sources_digests(self, use_link_metric: bool = True) -> np.ndarray:
+        """Digests of every node (node id order) from one all-sources sweep."""
+        out = np.zeros((self.num_nodes(), 3), np.uint64)
+        if self._L.odl_all_sources_digests(self._h, int(use_link_metric), out.ctypes.data) != 0:
+            raise LinkStateError(self._err())
+        return out
+
+    def prefetch_all(self, use_link_metric: bool = True) -> None:
+        if self._L.odl_all_sources_prefetch(self._h, int(use_link_metric)) != 0:
+            raise LinkStateError(self._err())
+
+    def sweep_stats(self) -> Dict[str, int]:
+        out = (C.c_uint64 * 5)()
+        self._L.odl_sweep_stats(self._h, out)
+        return {"sweeps": int(out[0]), "rows_copied": int(out[1]),
+                "mode": N.SWEEP_MODE_NAMES.get(int(out[2]), str(out[2])),
+                "devices": int(out[3]), "hip_graph": int(out[4])}
 
     def prefetch(self, roots: Sequence[str], use_link_metric: bool = True) -> None:
         if self._L.odl_spf_prefetch(self._h, "\n".join(roots).encode(), len(roots),

@@ -116,9 +116,13 @@ def rank_slice(m: int, world: int, rank: int):
 
 def step_roots(cls: RootClass, step: int, world: int, rank: int) -> np.ndarray:
     """Roots of `cls` that `rank` runs in `step` of a weak-scaling cyclic
-    sweep; disjoint across ranks within a step (n <= m / world per rank)."""
+    sweep; disjoint across ranks within a step (n <= m / world per rank; a
+    class smaller than the world gives one root to each rank < m and none to
+    the others)."""
     m = cls.roots.size
-    n = min(cls.per_step, max(1, m // world))
+    if m < world:
+        return cls.roots[[rank]] if rank < m else cls.roots[:0]
+    n = min(cls.per_step, m // world)
     start = ((step * world + rank) * n) % m
     return cls.roots[(np.arange(n) + start) % m]
 

@@ -1,0 +1,34 @@
+#!/bin/bash
+# Round-3 GPU session driver. Steps (space-separated in STEPS):
+#   sweep   pytest tests/test_gpu_sweep.py
+#   gpu     the whole -m gpu suite
+#   scale   tests/test_gpu_scale.py only
+#   bench   python bench.py (default headline config)
+#   benchT  python bench.py --topology $TOPO
+#   prof    rocprofv3 --kernel-trace --stats of a short bench
+# Each GPU step has its own time limit; the first failure ends the call.
+set -u
+TAG=${1:-s}; OUT=gpurun_out/r3_$TAG; mkdir -p "$OUT"; export TMPDIR=/tmp
+STEPS=${STEPS:-"sweep bench"}
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+for st in $STEPS; do
+  case $st in
+    sweep) timeout -k 10 600 $PYT tests/test_gpu_sweep.py > "$OUT/sweep.log" 2>&1; rc=$?
+           tail -5 "$OUT/sweep.log";;
+    gpu)   timeout -k 10 1000 $PYT -q -m gpu tests > "$OUT/gpu.log" 2>&1; rc=$?
+           tail -5 "$OUT/gpu.log";;
+    scale) timeout -k 10 900 $PYT -s tests/test_gpu_scale.py ${SCALE_K:+-k "$SCALE_K"} > "$OUT/scale.log" 2>&1; rc=$?
+           tail -8 "$OUT/scale.log";;
+    bench) timeout -k 10 420 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.json" 2> "$OUT/bench.err"; rc=$?
+           cat "$OUT/bench.json"; tail -3 "$OUT/bench.err";;
+    benchT) timeout -k 10 600 python bench.py --topology $TOPO ${BENCH_ARGS:-} > "$OUT/bench_$TOPO.json" 2> "$OUT/bench_$TOPO.err"; rc=$?
+           cat "$OUT/bench_$TOPO.json"; tail -3 "$OUT/bench_$TOPO.err";;
+    prof)  timeout -k 10 420 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- \
+             python bench.py --steps 5 --warmup 1 --no-cpu ${PROF_ARGS:-} > "$OUT/prof_bench.json" 2> "$OUT/prof.err"; rc=$?
+           tail -3 "$OUT/prof.err";;
+    *) echo "unknown step $st"; rc=2;;
+  esac
+  echo "step $st rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+done
+exit 0

@@ -1,6 +1,6 @@
 """bench.py's multi-GPU path, rehearsed with two ranks on one GPU: the real
-step code (per-rank strong-scaling slices of every width class on the
-product engine), the all-gather of the timed step's digests, max-over-ranks
+step code (ospf_sweep_run over the rank's part of the library's root
+partition), the all-gather of the timed step's digests, max-over-ranks
 timing, and rank 0's check of the gathered digests against the CPU
 restatement. Collectives run on gloo here (RCCL will not put two ranks on
 one device); RCCL itself is exercised only by the driver's 8-GPU runs. The
@@ -31,4 +31,4 @@ def test_two_rank_bench_step_and_gather(kind, mode):
     assert ln["parity_vs_cpu_sample"]["roots"] == 96
     assert ln["parity_vs_cpu_sample"]["equal"] is True
     assert ln["value"] > 0 and ln["config"]["roots_per_step"] == ln["config"]["n_nodes"]
-    assert ln["config"]["mode"] == mode
+    assert ln["config"]["mode"] == "sweep:" + mode  # the library's sweep, one call per step

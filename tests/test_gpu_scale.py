@@ -127,3 +127,59 @@ def test_m1m_sampled_roots_and_triangle_checks():
         tight = np.zeros(V, bool)
         tight[col[relax][d[col[relax]] == cand]] = True
         assert np.all(tight[reached] | (np.arange(V)[reached] == r))
+
+
+@pytest.mark.timeout(900)
+def test_f100k_all_sources_sweep_role_stratified():
+    """The headline path at full size: the F100k
+    all-sources sweep (derive: ospf_levels_dev + ospf_nh_derive_dev behind
+    ospf_sweep_run) against the CSR-Dijkstra restatement on EVERY spine (288,
+    56-word rows), 256 fabric switches and 256 racks; reached == V for every
+    root; and derive == the per-batch engine path bit for bit -- digests of a
+    1,000-root sample across the three classes, whole dist + next-hop rows of
+    8 roots per class."""
+    from openr_amd.engine import Sweep
+    st = T.fabric(pods=1781, planes=8)
+    o, p = both(st)
+    names = p.node_names()
+    V = len(names)
+    csr = p.csr()
+    eng = Engine()
+    eng.load(csr)
+    sw = Sweep(eng)
+    assert sw.mode == "derive"
+    sw.run()
+    eng.sync()
+    d = np.zeros((V, 3), np.uint64)
+    sw._check(sw._L.ospf_sweep_digests_host(sw._h, d.ctypes.data))
+    got = np.zeros_like(d)
+    got[sw.roots] = d
+    note("F100k sweep digests")
+    assert np.all(got[:, 0] == V)  # connected, no drains: every run reaches V
+    role = np.array([int(n.split("-")[0]) for n in names])
+    rng = np.random.default_rng(0x5EED)
+    spines = np.nonzero(role == 1)[0]
+    fsw = np.sort(rng.choice(np.nonzero(role == 2)[0], 256, replace=False))
+    rsw = np.sort(rng.choice(np.nonzero(role == 3)[0], 256, replace=False))
+    assert spines.size == 288
+    strat = np.concatenate([spines, fsw, rsw])
+    want = o.fast_digests([names[i] for i in strat], True, threads=16)
+    note("F100k CSR-Dijkstra digests of the stratified set")
+    bad = [names[r] for j, r in enumerate(strat) if not np.array_equal(got[r], want[j])]
+    assert not bad, bad[:8]
+    # derive == batch on a 1,000-root sample (100 spines, 300 FSWs, 600 RSWs)
+    pick = {1: np.sort(rng.choice(spines, 100, replace=False)),
+            2: np.sort(rng.choice(np.nonzero(role == 2)[0], 300, replace=False)),
+            3: np.sort(rng.choice(np.nonzero(role == 3)[0], 600, replace=False))}
+    for k, grp in pick.items():
+        W = max(eng.nh_words(int(r)) for r in grp)
+        ref = eng.run(grp, W, want_dist=False, want_nh=False, want_digest=True)["digest"]
+        assert np.array_equal(got[grp], ref), k
+        few = grp[:8]
+        rows = eng.run(few, W)
+        dist, nh = sw.rows(few, W)
+        assert np.array_equal(dist, rows["dist"]), k
+        assert np.array_equal(nh, rows["nh"]), k
+    note("F100k derive == batch")
+    sw.close()
+    eng.close()

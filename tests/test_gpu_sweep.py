@@ -1,0 +1,283 @@
+"""All-sources sweeps through the library (ospf_sweep_*, include/openr_spf.h):
+every path the engine can take (derive, weighted cover, weighted derive,
+batch) must give every root the rows and digest of the per-batch engine path
+-- itself oracle-pinned -- bit for bit; the multi-device context
+(ospf_multi_* / ospf_msweep_*) must partition the roots and gather the same
+digests; odl::LinkState's all-sources entry points must use the sweep.
+Reference semantics: LinkState::runSpf, openr/decision/LinkState.cpp:836-911;
+the all-sources caller is Decision::getDecisionRouteDb per node
+(openr/decision/Decision.cpp:309)."""
+import numpy as np
+import pytest
+
+from graphs import drained_fabric, random_stream
+from oracle import Oracle
+from openr_amd import topology as T
+from openr_amd.engine import Engine, EngineError, Multi, MultiSweep, Sweep
+from openr_amd.linkstate import LinkState
+
+pytestmark = pytest.mark.gpu
+
+
+def engine_for(stream):
+    ls = LinkState()
+    ls.apply(stream)
+    csr = ls.csr()
+    eng = Engine()
+    eng.load(csr)
+    return ls, csr, eng
+
+
+def sweep_digests(sw):
+    d = np.zeros((max(1, sw.n_roots), 3), np.uint64)
+    sw._check(sw._L.ospf_sweep_digests_host(sw._h, d.ctypes.data))
+    return dict(zip(sw.roots.tolist(), d[: sw.n_roots]))
+
+
+def check_sweep_vs_batch(eng, mode="auto", hop=False, rows_for=None, hip_graph=True,
+                         want_mode=None):
+    """Every root's digest from the sweep == the batch path's; rows too for
+    `rows_for` roots (all when None and the graph is small)."""
+    V = eng.V
+    sw = Sweep(eng, mode=mode, hop_count=hop, hip_graph=hip_graph)
+    try:
+        if want_mode:
+            assert sw.mode == want_mode
+        assert sorted(sw.roots.tolist()) == list(range(V))
+        sw.run()
+        eng.sync()
+        got = sweep_digests(sw)
+        words = np.array([eng.nh_words(r) for r in range(V)])
+        for W in sorted(set(words.tolist())):
+            grp = np.nonzero(words == W)[0].astype(np.uint32)
+            ref = eng.run(grp, W, hop_count=hop, want_digest=True)
+            for j, r in enumerate(grp.tolist()):
+                assert np.array_equal(got[r], ref["digest"][j]), (mode, r)
+            pick = grp if rows_for is None else np.intersect1d(grp, rows_for)
+            if pick.size:
+                idx = np.searchsorted(grp, pick)
+                dist, nh = sw.rows(pick, W)
+                assert np.array_equal(dist, ref["dist"][idx]), (mode, W)
+                assert np.array_equal(nh, ref["nh"][idx]), (mode, W)
+        return sw.mode
+    finally:
+        sw.close()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_sweep_random_unit_graphs_every_mode(seed):
+    stream, _ = random_stream(seed, n=70, unit=True)
+    _, _, eng = engine_for(stream)
+    try:
+        assert check_sweep_vs_batch(eng, "auto") == "derive"
+        for mode in ("derive", "wderive", "batch"):
+            check_sweep_vs_batch(eng, mode)
+        check_sweep_vs_batch(eng, "derive", hip_graph=False)
+        check_sweep_vs_batch(eng, "auto", hop=True)
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_sweep_random_weighted_graphs_every_mode(seed):
+    stream, _ = random_stream(seed + 10, n=70, unit=False, wmax=50)
+    _, _, eng = engine_for(stream)
+    try:
+        m = check_sweep_vs_batch(eng, "auto")
+        assert m in ("wcover", "wderive")
+        for mode in ("wderive", "batch"):
+            check_sweep_vs_batch(eng, mode)
+        try:
+            check_sweep_vs_batch(eng, "wcover")
+        except EngineError as e:  # outside the cover kernel's limits
+            assert e.code == -4, e
+        check_sweep_vs_batch(eng, "auto", hop=True)  # hop count: derive on any metric
+    finally:
+        eng.close()
+
+
+def test_sweep_fabric_with_drains_vs_oracle():
+    """A fabric (3 width classes) with drained switches and down links: the
+    derive sweep == batch path, and the digests == the CPU restatement."""
+    st = drained_fabric(6, 4, seed=3)
+    ls, csr, eng = engine_for(st)
+    try:
+        assert check_sweep_vs_batch(eng, "auto", rows_for=np.arange(0, eng.V, 7)) == "derive"
+        names = ls.node_names()
+        sw = Sweep(eng)
+        sw.run()
+        got = sweep_digests(sw)
+        want = Oracle(st).fast_digests(names)
+        for r in range(eng.V):
+            assert np.array_equal(got[r], want[r]), names[r]
+        sw.close()
+    finally:
+        eng.close()
+
+
+def test_sweep_weighted_fabric_cover_path():
+    st = T.fabric(pods=8, planes=4, weighted_seed=7)
+    ls, csr, eng = engine_for(st)
+    try:
+        assert check_sweep_vs_batch(eng, "auto", rows_for=np.arange(0, eng.V, 5),
+                                    want_mode="wcover") == "wcover"
+        check_sweep_vs_batch(eng, "wderive", rows_for=np.arange(0, eng.V, 11))
+    finally:
+        eng.close()
+
+
+def test_sweep_deep_unit_grid_does_not_raise():
+    """Unit 100 x 100 grid: diameter 198, past derive's 123-level bound. AUTO
+    must take another path and stay exact; sampled
+    roots vs the CSR-Dijkstra restatement."""
+    st = T.grid(100)
+    ls, csr, eng = engine_for(st)
+    try:
+        sw = Sweep(eng)
+        assert sw.mode != "derive"
+        sw.run()
+        eng.sync()
+        got = sweep_digests(sw)
+        assert len(got) == eng.V
+        names = ls.node_names()
+        pick = [0, 99, 4950, 5049, 9900, 9999] + list(range(101, 9999, 997))
+        want = Oracle(st).fast_digests([names[i] for i in pick])
+        for i, r in enumerate(pick):
+            assert np.array_equal(got[r], want[i]), names[r]
+        with pytest.raises(EngineError):
+            Sweep(eng, mode="derive")
+        sw.close()
+    finally:
+        eng.close()
+
+
+def test_sweep_poison_and_profile():
+    st = T.fabric(pods=4, planes=4)
+    ls, csr, eng = engine_for(st)
+    try:
+        sw = Sweep(eng)
+        sw.run()
+        eng.sync()
+        good = sweep_digests(sw)
+        sw.poison()
+        eng.sync()
+        bad = sweep_digests(sw)
+        assert all(np.all(v == np.uint64(0xFFFFFFFFFFFFFFFF)) for v in bad.values())
+        sw.run()  # a replay rewrites every digest
+        eng.sync()
+        again = sweep_digests(sw)
+        assert all(np.array_equal(good[r], again[r]) for r in good)
+        prof = sw.profile(2)
+        assert [p["name"] for p in prof][0] == "levels"
+        assert all(p["ms_median"] > 0 and p["compulsory_bytes"] > 0 for p in prof)
+        assert sw.step_compulsory_bytes == sum(p["compulsory_bytes"] for p in prof)
+        sw.close()
+    finally:
+        eng.close()
+
+
+def test_sweep_partition_parts_cover_every_root_once():
+    st = T.fabric(pods=9, planes=4)
+    ls, csr, eng = engine_for(st)
+    try:
+        full = Sweep(eng)
+        full.run()
+        want = sweep_digests(full)
+        full.close()
+        seen = {}
+        for n_parts in (2, 3):
+            seen.clear()
+            for p in range(n_parts):
+                sw = Sweep(eng, part=p, n_parts=n_parts)
+                sw.run()
+                for r, d in sweep_digests(sw).items():
+                    assert r not in seen
+                    seen[r] = d
+                assert sw.n_rows <= 1.6 * max(1, sw.n_roots) + 64
+                sw.close()
+            assert len(seen) == eng.V
+            assert all(np.array_equal(seen[r], want[r]) for r in range(eng.V))
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("topo", ["unit", "weighted"])
+def test_multi_device_context_two_slots_on_device0(topo):
+    """ospf_multi with two contexts on device 0: parts on each slot, digests
+    gathered by peer copies (same-device copies here; RCCL / xGMI across
+    devices is unexercised until a multi-GPU node runs it)."""
+    st = T.fabric(pods=6, planes=4, weighted_seed=7 if topo == "weighted" else None)
+    ls, csr, eng = engine_for(st)
+    try:
+        full = Sweep(eng)
+        full.run()
+        want = sweep_digests(full)
+        full.close()
+    finally:
+        eng.close()
+    m = Multi([0, 0])
+    try:
+        m.load(csr)
+        ms = MultiSweep(m)
+        ms.run()
+        got = ms.digests()
+        for r in range(m.V):
+            assert np.array_equal(got[r], want[r]), r
+        a, b = ms.part_roots(0), ms.part_roots(1)
+        assert np.intersect1d(a, b).size == 0 and a.size + b.size == m.V
+        assert ms.owner(int(a[0])) == 0 and ms.owner(int(b[0])) == 1
+        ms.close()
+    finally:
+        m.close()
+
+
+def test_linkstate_all_sources_uses_the_sweep():
+    st = drained_fabric(5, 4, seed=1, down=0.0)
+    p = LinkState(stream=st)
+    names = p.node_names()
+    runs0 = p.spf_runs
+    d_all = p.all_sources_digests()
+    st_ = p.sweep_stats()
+    assert st_["sweeps"] == 1 and st_["mode"] == "derive"
+    assert p.spf_runs - runs0 == len(names)
+    q = LinkState(stream=st)
+    d_batch = q.digests(names)
+    assert np.array_equal(d_all, d_batch)
+    # getSpfResult of any node now comes from the sweep's rows, no new runs
+    o = Oracle(st)
+    runs1 = p.spf_runs
+    for r in names[:: max(1, len(names) // 12)]:
+        assert p.spf_text(r) == o.spf_text(r), r
+    assert p.spf_runs == runs1
+    assert p.sweep_stats()["rows_copied"] > 0
+
+
+def test_linkstate_multi_device_prefetch_and_route_dbs():
+    """odl_create_multi over two slots of device 0: an all-nodes route build
+    takes the sweep (parts per slot) and equals the single-device build."""
+    st = T.fabric(pods=4, planes=4)
+    a = LinkState(stream=st, devices=[0, 0])
+    b = LinkState(stream=st)
+    names = a.node_names()
+    prefixes = {f"10.{i // 256}.{i % 256}.0/24": [(n, "ip", "ecmp", 0, None)]
+                for i, n in enumerate(names[::3])}
+    ra = a.route_dbs(names, prefixes)
+    sa = a.sweep_stats()
+    assert sa["sweeps"] == 1 and sa["devices"] == 2
+    rb = b.route_dbs(names, prefixes)
+    assert ra == rb
+    assert np.array_equal(a.all_sources_digests(), b.digests(names))
+
+
+def test_sweep_invalidated_by_graph_change():
+    st = T.fabric(pods=3, planes=2)
+    ls, csr, eng = engine_for(st)
+    try:
+        sw = Sweep(eng)
+        sw.run()
+        eng.update_links([(0, 0, int(csr["metric"][0]), int(csr["metric"][0]))], version=2)
+        with pytest.raises(EngineError):
+            sw.run()
+        sw.close()
+    finally:
+        eng.close()
