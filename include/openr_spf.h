@@ -196,6 +196,27 @@ int ospf_nh_derive_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n, uint3
                        const uint32_t* d_lev_pos, const ospf_digest* d_lev_digest,
                        uint32_t* d_nh, ospf_digest* d_digest, void* stream);
 
+/* All-sources rows of leaf roots from level rows (unit metric or hop count;
+ * spf_leaf.hip). A leaf r (no two leaves adjacent, <= 32 distinct
+ * neighbours n_k) has dist(r, v) = 1 + min_k dist(n_k, v) over n_k with an
+ * up link r-n_k (a non-transit n_k reaches only itself) and next hops = the
+ * tight n_k -- LinkState::runSpf's Bellman equation over the root's
+ * out-links (LinkState.cpp:836-911, :859-866, :885-901). Reads the level rows
+ * of every usable transit neighbour (d_lev at d_pos[n], e.g. from
+ * ospf_levels_dev) and writes the roots' own level rows and dist rows at
+ * d_pos[root] (d_dist [rows][V], NULL = not wanted), one-word next-hop rows
+ * d_nh [n][V] in root order and complete digests d_digest [n] (NULL = not
+ * wanted). Groups: d_groups [n_groups + 1] offsets into the roots, <= 64
+ * roots each, every root of a group with the same distinct neighbours and
+ * usable links (the racks of a pod: a tile's neighbour rows are read once
+ * per group; a group that is not uniform raises error bit 128); NULL = one
+ * root per group. max_root_neighbors (0 = 32) bounds every root's distinct
+ * neighbours. Needs a depth bound <= 123. Queued on `stream`. */
+int ospf_leaf_derive_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n,
+                         const uint32_t* d_groups, uint32_t n_groups, uint32_t max_root_neighbors,
+                         uint8_t* d_lev, uint32_t lev_pitch, const uint32_t* d_pos,
+                         uint32_t* d_dist, uint32_t* d_nh, ospf_digest* d_digest, void* stream);
+
 /* Weighted all-sources rows of leaf roots (any metric, or OSPF_HOP_COUNT; no
  * ignored links). For a root r with distinct neighbours n_k, w_k = the
  * smallest metric r advertises on an up link to n_k and D_k = the distance row

@@ -1137,6 +1137,7 @@ int ospf_sync(ospf_ctx* c, void* stream) {
                 : (err & 8u) ? "a BFS level past the graph's depth bound was reached"
                 : (err & 16u) ? "derive: a root or a usable neighbour has no level row"
                 : (err & 64u) ? "a device root id is out of range"
+                : (err & 128u) ? "leaf derive: a group's roots do not share their slot table"
                              : "internal: a frontier entry out of range");
   }
   return OSPF_OK;
@@ -1326,6 +1327,44 @@ int ospf_nh_derive_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_
   d.err = c->d_err;
   hipError_t e = ospf::launch_nh_derive(c->g, d, s);
   if (e != hipSuccess) return hip_fail(c, e, "launch_nh_derive");
+  return OSPF_OK;
+}
+
+// Leaf derive (spf_leaf.hip): level, dist and next-hop rows of leaf roots
+// from their neighbours' level rows. Unit metric or hop count.
+int ospf_leaf_derive_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n,
+                         const uint32_t* d_groups, uint32_t n_groups, uint32_t max_root_neighbors,
+                         uint8_t* d_lev, uint32_t lev_pitch, const uint32_t* d_pos,
+                         uint32_t* d_dist, uint32_t* d_nh, ospf_digest* d_digest, void* stream) {
+  if (!c) return OSPF_E_INVAL;
+  if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  if (n == 0) return OSPF_OK;
+  if (!d_roots || !d_lev || !d_pos || !d_nh) return fail(c, OSPF_E_INVAL, "null argument");
+  if (lev_pitch % 16u || lev_pitch < c->info.n_nodes)
+    return fail(c, OSPF_E_INVAL, "lev_pitch: a multiple of 16 >= V");
+  if (d_groups && n_groups == 0) return fail(c, OSPF_E_INVAL, "leaf derive: no groups");
+  if (max_root_neighbors > 32)
+    return fail(c, OSPF_E_RANGE, "leaf derive: leaf roots have at most 32 distinct neighbours");
+  if (c->depth_bound > 123) return fail(c, OSPF_E_RANGE, "level rows need a depth bound <= 123");
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (d_digest) HIPCHK(c, hipMemsetAsync(d_digest, 0, (size_t)n * sizeof(ospf_digest), s));
+  ospf::LeafArgs a{};
+  a.roots = d_roots;
+  a.n = n;
+  a.grp = d_groups;
+  a.ngroups = d_groups ? n_groups : n;
+  a.lev = d_lev;
+  a.pitch = lev_pitch;
+  a.pos = d_pos;
+  a.dist = d_dist;
+  a.nh = d_nh;
+  a.digest = d_digest;
+  a.err = c->d_err;
+  if (const char* e = getenv("OSPF_LEAF_CTILES")) a.ctiles = (uint32_t)std::max(1, atoi(e));
+  hipError_t e = ospf::launch_leaf_derive(c->g, a, max_root_neighbors ? max_root_neighbors : 32u, s);
+  if (e != hipSuccess) return hip_fail(c, e, "launch_leaf_derive");
+  c->spf_runs += n;
   return OSPF_OK;
 }
 

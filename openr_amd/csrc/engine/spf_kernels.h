@@ -295,6 +295,28 @@ hipError_t launch_wderive_wide(const DevGraph& g, WDeriveArgs a, uint32_t W, hip
 hipError_t launch_msbfs_levels(const DevGraph& g, const MsArgs& a, uint32_t depth_bound,
                                hipStream_t s);
 hipError_t launch_nh_derive(const DevGraph& g, const DeriveArgs& d, hipStream_t s);
+
+// Leaf derive (spf_leaf.hip), unit metric / hop count: the level, dist and
+// one-word next-hop rows of leaf roots (<= 32 distinct neighbours, every
+// usable transit neighbour's level row present) from their neighbours' level
+// rows. Roots of a group share their slot table (same distinct neighbours,
+// same usable links): each tile's neighbour rows are read once per group.
+constexpr uint32_t kLeafMaxG = 64;
+struct LeafArgs {
+  const uint32_t* roots;  // [n] leaf node ids
+  uint32_t n;
+  const uint32_t* grp;    // [ngroups + 1] offsets into roots (null: one root per group)
+  uint32_t ngroups;
+  uint8_t* lev;           // [rows][pitch]: neighbours' rows read, the roots' rows written
+  uint32_t pitch;
+  const uint32_t* pos;    // [V] row of each node in lev / dist (kInf: none)
+  uint32_t* dist;         // [rows][V] (same row index as lev) or null
+  uint32_t* nh;           // [n][V] one next-hop word per node, root order
+  ospf_digest* digest;    // [n] (zeroed by the caller) or null
+  uint32_t* err;
+  uint32_t tiles, ctiles; // 1,024-node tiles of the rows, tiles per block
+};
+hipError_t launch_leaf_derive(const DevGraph& g, const LeafArgs& a, uint32_t kmax, hipStream_t s);
 // kp = 8, 16 or 32 planes per node; depth_bound bounds the BFS level count
 hipError_t launch_msbfs_round(int kp, const DevGraph& g, const MsArgs& a, uint32_t depth_bound,
                               hipStream_t s);

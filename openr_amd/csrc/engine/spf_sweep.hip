@@ -245,35 +245,128 @@ void own(ospf_sweep* s, uint32_t r, uint32_t slot, const uint32_t* d, const uint
 }
 
 // ---------------------------------------------------------------- plans
-// DERIVE (spf_levels.hip + spf_msbfs.hip derive kernels): levels for the
-// closure of the part (its roots and all their neighbours, ordered by each
-// node's smallest neighbour so a 128-root traversal shares frontiers), then
-// one next-hop launch per width class, each on its own stream, roots ordered
-// by their largest neighbour (a pod's racks / fabric switches, a plane's
-// spines next to each other: their neighbours' level rows stay in L2 / MALL).
+// Usable-slot signature of a leaf root (bit k: an up link to its k-th
+// distinct neighbour), from the context's padded host shadows.
+uint32_t usable_slots(const ospf_ctx* c, uint32_t r) {
+  uint32_t use = 0;
+  const uint32_t* dn = c->h_dn.data() + c->h_dn_off[r];
+  const uint32_t K = c->h_dn_off[r + 1] - c->h_dn_off[r];
+  for (uint32_t e = c->h_prow[r]; e < c->h_prow[r + 1]; ++e) {
+    const uint32_t cx = c->h_pcolx[e];
+    if ((cx & 0x80000000u) || cx == r) continue;
+    const uint32_t k = (uint32_t)(std::lower_bound(dn, dn + K, cx) - dn);
+    if (k < 32u) use |= 1u << k;
+  }
+  return use;
+}
+
+// Leaf roots ordered so that roots with the same slot table (distinct
+// neighbours + usable links: the racks of a pod) are adjacent, cut into
+// groups of <= kLeafMaxG; returns the group offsets.
+std::vector<uint32_t> leaf_groups(const ospf_ctx* c, const Facts& f, std::vector<uint32_t>& roots) {
+  std::vector<uint32_t> use(roots.size());
+  for (size_t i = 0; i < roots.size(); ++i) use[i] = usable_slots(c, roots[i]);
+  std::vector<uint32_t> ord(roots.size());
+  std::iota(ord.begin(), ord.end(), 0u);
+  auto same_nbrs = [&](uint32_t a, uint32_t b) {
+    return f.nbrs(a) == f.nbrs(b) &&
+           std::equal(f.dn->begin() + (*f.dn_off)[a], f.dn->begin() + (*f.dn_off)[a + 1],
+                      f.dn->begin() + (*f.dn_off)[b]);
+  };
+  std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
+    const uint32_t a = roots[x], b = roots[y];
+    if (f.nbrs(a) != f.nbrs(b)) return f.first(a) != f.first(b) ? f.first(a) < f.first(b)
+                                                                 : f.nbrs(a) < f.nbrs(b);
+    const int cmp = std::lexicographical_compare(
+                        f.dn->begin() + (*f.dn_off)[a], f.dn->begin() + (*f.dn_off)[a + 1],
+                        f.dn->begin() + (*f.dn_off)[b], f.dn->begin() + (*f.dn_off)[b + 1])
+                        ? -1
+                        : (same_nbrs(a, b) ? 0 : 1);
+    if (cmp) return cmp < 0;
+    return use[x] < use[y];
+  });
+  std::vector<uint32_t> out(roots.size()), uo(roots.size());
+  for (size_t i = 0; i < ord.size(); ++i) {
+    out[i] = roots[ord[i]];
+    uo[i] = use[ord[i]];
+  }
+  roots.swap(out);
+  std::vector<uint32_t> grp{0u};
+  for (uint32_t i = 1; i <= roots.size(); ++i) {
+    const uint32_t g0 = grp.back();
+    if (i == roots.size() || i - g0 >= ospf::kLeafMaxG || uo[i] != uo[g0] ||
+        !same_nbrs(roots[i], roots[g0]))
+      grp.push_back(i);
+  }
+  return grp;
+}
+
+// DERIVE (spf_levels.hip, spf_leaf.hip, spf_msbfs.hip derive kernels), unit
+// metric / hop count. The part's roots split into leaves (an independent set
+// of nodes with <= 32 distinct neighbours: a fabric's racks) and the cover.
+// (A) levels: the distance-only 128-root BFS for the cover rows the part
+// needs (its cover roots, their neighbours and the leaves' neighbours),
+// ordered by each node's smallest neighbour so a traversal shares frontiers;
+// (B) the leaves' level, dist and next-hop rows from their neighbours' level
+// rows, groups of leaves with one slot table reading each tile once;
+// (C) one next-hop launch per width class of cover roots, roots ordered by
+// their largest neighbour (their neighbours' level rows stay in L2 / MALL);
+// classes that read no leaf row run beside (B) on their own stream.
 int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine) {
   ospf_ctx* c = s->c;
   const uint32_t V = s->V;
   const uint32_t hop = s->opts.flags & OSPF_HOP_COUNT;
-  std::vector<uint32_t> clo = closure(f, mine);
+  std::vector<uint8_t> leaf;
+  if (!getenv("OSPF_SWEEP_NOLEAF")) leaf = leaf_set(f);
+  else leaf.assign(V, 0);
+  std::vector<uint32_t> own_l, own_c;
+  for (uint32_t r : mine) (leaf[r] ? own_l : own_c).push_back(r);
+  // leaves whose rows the cover roots' next hops read
+  const std::vector<uint32_t> nb_c = closure(f, own_c);
+  std::vector<uint8_t> in_l(V, 0);
+  for (uint32_t r : own_l) in_l[r] = 1;
+  std::vector<uint32_t> extra_l;
+  for (uint32_t v : nb_c)
+    if (leaf[v] && !in_l[v]) extra_l.push_back(v);
+  std::vector<uint32_t> grp = leaf_groups(c, f, own_l);
+  std::vector<uint32_t> grp_x = leaf_groups(c, f, extra_l);
+  std::vector<uint32_t> need_l = own_l;
+  need_l.insert(need_l.end(), extra_l.begin(), extra_l.end());
+  for (size_t i = 1; i < grp_x.size(); ++i) grp.push_back((uint32_t)own_l.size() + grp_x[i]);
+  const uint32_t nL = (uint32_t)need_l.size(), ngr = (uint32_t)grp.size() - 1;
+  // cover rows: own cover roots + every non-leaf neighbour of a needed root
+  std::vector<uint8_t> in_a(V, 0);
+  for (uint32_t v : own_c) in_a[v] = 1;
+  for (uint32_t v : closure(f, need_l))
+    if (!leaf[v]) in_a[v] = 1;
+  for (uint32_t v : nb_c)
+    if (!leaf[v]) in_a[v] = 1;
+  std::vector<uint32_t> clo;
+  for (uint32_t v = 0; v < V; ++v)
+    if (in_a[v]) clo.push_back(v);
   locality_order(clo, [&](uint32_t v) { return f.first(v); });
-  std::vector<uint32_t> pos(V, kNone);
-  for (uint32_t i = 0; i < clo.size(); ++i) pos[clo[i]] = i;
-  const uint32_t pitch = (V + 15) / 16 * 16;
   const uint32_t nc = (uint32_t)clo.size();
-  uint32_t *d_clo, *d_pos, *dist;
+  std::vector<uint32_t> pos(V, kNone);
+  for (uint32_t i = 0; i < nc; ++i) pos[clo[i]] = i;
+  for (uint32_t i = 0; i < nL; ++i) pos[need_l[i]] = nc + i;
+  const uint32_t pitch = (V + 15) / 16 * 16;
+  const uint32_t rows = nc + nL;
+  uint32_t *d_clo = nullptr, *d_pos, *dist, *d_l = nullptr, *d_grp = nullptr, *lnh = nullptr;
   uint8_t* lev;
   ospf_digest* ldg;
   int rc;
-  if ((rc = upload(s, &d_clo, clo)) || (rc = upload(s, &d_pos, pos)) ||
-      (rc = dalloc(s, &lev, (size_t)nc * pitch)) || (rc = dalloc(s, &dist, (size_t)nc * V)) ||
-      (rc = dalloc(s, &ldg, nc)))
+  if ((rc = upload(s, &d_pos, pos)) || (rc = dalloc(s, &lev, (size_t)rows * pitch)) ||
+      (rc = dalloc(s, &dist, (size_t)rows * V)) || (rc = dalloc(s, &ldg, std::max(1u, nc))))
     return rc;
-  s->dig_aux.push_back({ldg, nc});
-  s->n_rows = nc;
-  // classes by capacity, roots by largest neighbour
+  if (nc && (rc = upload(s, &d_clo, clo))) return rc;
+  if (nL && ((rc = upload(s, &d_l, need_l)) || (rc = upload(s, &d_grp, grp)) ||
+             (rc = dalloc(s, &lnh, (size_t)nL * V))))
+    return rc;
+  s->dig_aux.push_back({ldg, std::max(1u, nc)});
+  s->n_rows = rows;
+  // cover classes by capacity, roots by largest neighbour
   std::vector<uint32_t> caps;
-  for (uint32_t r : mine) caps.push_back(f.cap(r));
+  for (uint32_t r : own_c) caps.push_back(f.cap(r));
   std::sort(caps.begin(), caps.end());
   caps.erase(std::unique(caps.begin(), caps.end()), caps.end());
   struct Cls {
@@ -281,41 +374,41 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     std::vector<uint32_t> roots;
   };
   std::vector<Cls> cls;
-  uint32_t ndig = 0;
+  uint32_t ndig = (uint32_t)own_c.size() + nL;
   for (uint32_t cap : caps) {
     Cls k{cap, cap > 16 ? cap / 32 : 1u, {}};
-    for (uint32_t r : mine)
+    for (uint32_t r : own_c)
       if (f.cap(r) == cap) k.roots.push_back(r);
     locality_order(k.roots, [&](uint32_t v) { return f.last(v); });
-    ndig += (uint32_t)k.roots.size();
     cls.push_back(std::move(k));
   }
   if ((rc = dalloc(s, &s->dig_all, ndig))) return rc;
   s->n_dig = ndig;
-  const uint64_t scans = ((nc + 127) / 128) * scan_bytes(c, false);
-  ospf_sweep::Unit lv;
-  lv.name = "levels";
-  lv.kernel = "ospf_levels_dev (lv_init + lv_level/lv_settle per level + lv_rows: distance-only "
-              "128-root BFS, dist + level rows)";
-  lv.stream = 0;
-  lv.record = 1;
-  lv.n_roots = nc;
-  lv.W = 0;
-  lv.comp = (uint64_t)nc * 4ull * V + scans;
-  lv.fn = [=](hipStream_t st) {
-    return ospf_levels_dev(c, d_clo, nc, hop, dist, lev, pitch, ldg, st);
-  };
-  if ((rc = new_event(s)) < 0) return rc;  // event 1: levels done
-  s->units.push_back(lv);
-  s->step_comp += lv.comp;
+  const int ev_a = new_event(s), ev_b = new_event(s);  // levels done, leaves done
+  if (ev_a < 0 || ev_b < 0) return ev_a < 0 ? ev_a : ev_b;
+  if (nc) {
+    ospf_sweep::Unit lv;
+    lv.name = "levels";
+    lv.kernel = "ospf_levels_dev (lv_init + lv_level/lv_settle per level + lv_rows: "
+                "distance-only 128-root BFS, dist + level rows)";
+    lv.stream = 0;
+    lv.record = ev_a;
+    lv.n_roots = nc;
+    lv.comp = (uint64_t)nc * 4ull * V + ((nc + 127) / 128) * scan_bytes(c, false);
+    lv.fn = [=](hipStream_t st) {
+      return ospf_levels_dev(c, d_clo, nc, hop, dist, lev, pitch, ldg, st);
+    };
+    s->step_comp += lv.comp;
+    s->units.push_back(lv);
+  }
+  // (C) cover classes: slots 0 .. |own_c| of the digests
   uint32_t slot = 0;
-  // widest rows first: their launches are the longest
   std::vector<size_t> order(cls.size());
   std::iota(order.begin(), order.end(), 0);
   std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
     return (uint64_t)cls[a].W * cls[a].roots.size() > (uint64_t)cls[b].W * cls[b].roots.size();
   });
-  std::vector<ospf_sweep::Unit> der(cls.size());
+  std::vector<ospf_sweep::Unit> side, after;
   for (size_t i = 0; i < cls.size(); ++i) {
     Cls& k = cls[i];
     const uint32_t n = (uint32_t)k.roots.size(), W = k.W, cap = std::min(k.cap, 2048u);
@@ -325,6 +418,10 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     for (uint32_t j = 0; j < n; ++j)
       own(s, k.roots[j], slot + j, dist + (size_t)pos[k.roots[j]] * V, nh + (size_t)j * V * W, W);
     slot += n;
+    bool reads_leaf = false;
+    for (uint32_t r : k.roots)
+      for (uint32_t q = (*f.dn_off)[r]; q < (*f.dn_off)[r + 1] && !reads_leaf; ++q)
+        reads_leaf = leaf[(*f.dn)[q]] != 0;
     ospf_sweep::Unit u;
     u.name = "derive_cap" + std::to_string(k.cap);
     u.kernel = std::string("ospf_nh_derive_dev (") +
@@ -333,17 +430,43 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     const int st = new_stream(s);
     if (st < 0) return st;
     u.stream = st;
-    u.wait = {1};
+    u.wait = {reads_leaf ? ev_b : ev_a};
     u.n_roots = n;
     u.W = W;
     u.comp = (uint64_t)n * 4ull * V * W;
     u.fn = [=](hipStream_t strm) {
       return ospf_nh_derive_dev(c, d_roots, n, W, cap, lev, pitch, d_pos, ldg, nh, dg, strm);
     };
-    der[i] = std::move(u);
-    s->step_comp += (uint64_t)n * 4ull * V * W;
+    s->step_comp += u.comp;
+    (reads_leaf ? after : side).push_back(std::move(u));
   }
-  for (size_t i : order) s->units.push_back(std::move(der[i]));
+  // (B) leaves: digests after the cover roots' (owned first, then the extra)
+  if (nL) {
+    uint32_t kmax = 1;
+    for (uint32_t r : need_l) kmax = std::max(kmax, f.nbrs(r));
+    for (uint32_t j = 0; j < own_l.size(); ++j)
+      own(s, own_l[j], slot + j, dist + (size_t)(nc + j) * V, lnh + (size_t)j * V, 1);
+    ospf_digest* dg = s->dig_all + slot;
+    ospf_sweep::Unit u;
+    u.name = "leaf";
+    u.kernel = "ospf_leaf_derive_dev (leaf_derive_kernel: level + dist + next-hop rows of leaf "
+               "roots from their neighbours' level rows)";
+    u.stream = 0;
+    u.record = ev_b;
+    u.n_roots = nL;
+    u.W = 1;
+    u.comp = (uint64_t)nL * 8ull * V;
+    u.fn = [=](hipStream_t strm) {
+      return ospf_leaf_derive_dev(c, d_l, nL, d_grp, ngr, kmax, lev, pitch, d_pos, dist, lnh, dg,
+                                  strm);
+    };
+    s->step_comp += u.comp;
+    for (auto& x : side) s->units.push_back(std::move(x));
+    s->units.push_back(std::move(u));
+  } else {  // no leaf rows: no class waits for them
+    for (auto& x : side) s->units.push_back(std::move(x));
+  }
+  for (auto& x : after) s->units.push_back(std::move(x));
   return OSPF_OK;
 }
 

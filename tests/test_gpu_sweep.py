@@ -281,3 +281,34 @@ def test_sweep_invalidated_by_graph_change():
         sw.close()
     finally:
         eng.close()
+
+
+def test_leaf_derive_rejects_a_non_uniform_group():
+    """ospf_leaf_derive_dev checks that a group's roots share their slot table
+    (error bit 128 at ospf_sync) instead of deriving wrong rows."""
+    import ctypes as C
+    import torch
+    st = drained_fabric(4, 4, seed=5, drain=0.0, down=0.0)
+    ls, csr, eng = engine_for(st)
+    try:
+        names = ls.node_names()
+        V = eng.V
+        racks = [i for i, n in enumerate(names) if n.startswith("3-")]
+        a, b = racks[0], next(r for r in racks if names[r].split("-")[1] != names[a].split("-")[1])
+        dev = torch.device("cuda", 0)
+        pitch = eng.lev_pitch
+        allv = np.arange(V, dtype=np.uint32)
+        lev = torch.empty((V, pitch), dtype=torch.uint8, device=dev)
+        d_all = torch.from_numpy(allv.view(np.int32)).to(dev)
+        eng.levels_dev(d_all.data_ptr(), V, lev.data_ptr())
+        roots = torch.from_numpy(np.array([a, b], np.uint32).view(np.int32)).to(dev)
+        grp = torch.from_numpy(np.array([0, 2], np.uint32).view(np.int32)).to(dev)
+        nh = torch.empty((2, V), dtype=torch.int32, device=dev)
+        rc = eng._L.ospf_leaf_derive_dev(eng._h, roots.data_ptr(), 2, grp.data_ptr(), 1, 8,
+                                         lev.data_ptr(), pitch, d_all.data_ptr(), None,
+                                         nh.data_ptr(), None, None)
+        assert rc == 0
+        with pytest.raises(EngineError):
+            eng.sync()
+    finally:
+        eng.close()
