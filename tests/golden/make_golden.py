@@ -635,6 +635,224 @@ fixtures.append(dict(
                           f"3|U|{_dflt}": [H("3/6", 6, 10)]}),
     ])]))
 
+# SimpleRingTopologyFixture.MultiPathTest (DecisionTest.cpp:2231-2365):
+# node + adjacency labels, 12 unicast + 16 node-label + 8 adjacency routes
+def _ring_full(extra=None):
+    e = {
+        f"1|U|{ADDR[4]}": [H("1/2", 2, 20), H("1/3", 3, 20)],
+        "1|M|4": [H("1/2", 2, 20, "SWAP", [4]), H("1/3", 3, 20, "SWAP", [4])],
+        f"1|U|{ADDR[3]}": [H("1/3", 3, 10)], "1|M|3": [H("1/3", 3, 10, "PHP")],
+        f"1|U|{ADDR[2]}": [H("1/2", 2, 10)], "1|M|2": [H("1/2", 2, 10, "PHP")],
+        "1|M|1": [POP], **adj_routes(1, ring[0]["adjs"]),
+        f"2|U|{ADDR[4]}": [H("2/4", 4, 10)], "2|M|4": [H("2/4", 4, 10, "PHP")],
+        f"2|U|{ADDR[3]}": [H("2/1", 1, 20), H("2/4", 4, 20)],
+        "2|M|3": [H("2/1", 1, 20, "SWAP", [3]), H("2/4", 4, 20, "SWAP", [3])],
+        f"2|U|{ADDR[1]}": [H("2/1", 1, 10)], "2|M|1": [H("2/1", 1, 10, "PHP")],
+        "2|M|2": [POP], **adj_routes(2, ring[1]["adjs"]),
+        f"3|U|{ADDR[4]}": [H("3/4", 4, 10)], "3|M|4": [H("3/4", 4, 10, "PHP")],
+        f"3|U|{ADDR[2]}": [H("3/1", 1, 20), H("3/4", 4, 20)],
+        "3|M|2": [H("3/1", 1, 20, "SWAP", [2]), H("3/4", 4, 20, "SWAP", [2])],
+        f"3|U|{ADDR[1]}": [H("3/1", 1, 10)], "3|M|1": [H("3/1", 1, 10, "PHP")],
+        "3|M|3": [POP], **adj_routes(3, ring[2]["adjs"]),
+        f"4|U|{ADDR[3]}": [H("4/3", 3, 10)], "4|M|3": [H("4/3", 3, 10, "PHP")],
+        f"4|U|{ADDR[2]}": [H("4/2", 2, 10)], "4|M|2": [H("4/2", 2, 10, "PHP")],
+        f"4|U|{ADDR[1]}": [H("4/2", 2, 20), H("4/3", 3, 20)],
+        "4|M|1": [H("4/2", 2, 20, "SWAP", [1]), H("4/3", 3, 20, "SWAP", [1])],
+        "4|M|4": [POP], **adj_routes(4, ring[3]["adjs"])}
+    e.update(extra or {})
+    return e
+
+
+fixtures.append(dict(
+    name="decision_simple_ring_multipath_routes",
+    source="openr/decision/tests/DecisionTest.cpp:2231-2365",
+    steps=[dict(dbs=ring, expect_changes=ring_changes, checks=[
+        route_map([1, 2, 3, 4], ring_pfx, expect_size=36, expect=_ring_full())])]))
+
+# SimpleRingTopologyFixture.AttachedNodesTest (DecisionTest.cpp:3058-3108):
+# the default route from nodes 1 and 4; attached nodes get none
+_ring_dflt = dict(ring_pfx, **{"::/0": [["1", "ip", "ecmp", 0, None], ["4", "ip", "ecmp", 0, None]]})
+fixtures.append(dict(
+    name="decision_simple_ring_attached_nodes",
+    source="openr/decision/tests/DecisionTest.cpp:3058-3108",
+    steps=[dict(dbs=ring, expect_changes=ring_changes, checks=[
+        route_map([1, 2, 3, 4], _ring_dflt, expect_size=38,
+                  expect={"2|U|::/0": [H("2/1", 1, 10), H("2/4", 4, 10)],
+                          "3|U|::/0": [H("3/1", 1, 10), H("3/4", 4, 10)]},
+                  expect_absent=["1|U|::/0", "4|U|::/0"])])]))
+
+# SimpleRingTopologyFixture.DuplicateMplsRoutes (DecisionTest.cpp:2174-2226):
+# node 1 takes node 2's label 2; every node keeps exactly one route to label
+# 2 (the reference counts the duplicate, :2195-2198). Which node keeps it is
+# buildRouteDb's rule (SpfSolver.cpp:525-539: on a collision the node whose
+# name sorts first keeps the label, whatever the iteration order): node 1.
+# Then node 1 goes back to label 1: label 2 is node 2's again, nothing else
+# is withdrawn (:2211-2225).
+_r1dup = db(1, [dadj(1, 2), dadj(1, 3)], 2)
+fixtures.append(dict(
+    name="decision_simple_ring_duplicate_mpls_routes",
+    source="openr/decision/tests/DecisionTest.cpp:2174-2226",
+    steps=[
+        dict(dbs=ring, expect_changes=ring_changes),
+        dict(dbs=[_r1dup], expect_changes=[[False, False, True, None]], checks=[
+            route_map([1, 2, 3, 4], ring_pfx,
+                      expect_counts={"1": [3, 5], "2": [3, 5], "3": [3, 5], "4": [3, 5]},
+                      expect={"1|M|2": [POP], "2|M|2": [H("2/1", 1, 10, "PHP")],
+                              "3|M|2": [H("3/1", 1, 10, "PHP")],
+                              "4|M|2": [H("4/2", 2, 20, "SWAP", [2]),
+                                        H("4/3", 3, 20, "SWAP", [2])]},
+                      expect_absent=["1|M|1", "2|M|1", "3|M|1", "4|M|1"])]),
+        dict(dbs=[ring[0]], expect_changes=[[False, False, True, None]], checks=[
+            route_map([1, 2, 3, 4], ring_pfx, expect_size=36, expect=_ring_full())]),
+    ]))
+
+# ParallelAdjRingTopologyFixture.MultiPathTest (DecisionTest.cpp:3711-3857):
+# the same route map as ShortestPathTest (multipath is ignored)
+fixtures.append(dict(
+    name="decision_parallel_adj_ring_multipath_routes",
+    source="openr/decision/tests/DecisionTest.cpp:3711-3857",
+    steps=[dict(
+        dbs=pr, expect_changes=[[False, None, None, None], [True, None, None, None],
+                                [True, None, None, None], [True, None, None, None]],
+        checks=[route_map([1, 2, 3, 4], ring_pfx, expect_size=44, expect={
+            f"1|U|{ADDR[4]}": _p1_4, "1|M|4": _sw(_p1_4, 4),
+            f"1|U|{ADDR[3]}": [H("3/1", 3, 11)], "1|M|3": [H("3/1", 3, 11, "PHP")],
+            f"1|U|{ADDR[2]}": [H("2/1", 2, 11), H("2/2", 2, 11)],
+            "1|M|2": _sw([H("2/1", 2, 11), H("2/2", 2, 11)], None),
+            "1|M|1": [POP], **adj_routes(1, pr[0]["adjs"]),
+            f"2|U|{ADDR[4]}": [H("4/1", 4, 11)], "2|M|4": [H("4/1", 4, 11, "PHP")],
+            f"2|U|{ADDR[3]}": _p2_3, "2|M|3": _sw(_p2_3, 3),
+            f"2|U|{ADDR[1]}": [H("1/1", 1, 11), H("1/2", 1, 11)],
+            "2|M|1": _sw([H("1/1", 1, 11), H("1/2", 1, 11)], None),
+            "2|M|2": [POP], **adj_routes(2, pr[1]["adjs"]),
+            f"3|U|{ADDR[4]}": [H("4/1", 4, 11)], "3|M|4": [H("4/1", 4, 11, "PHP")],
+            f"3|U|{ADDR[2]}": _p3_2, "3|M|2": _sw(_p3_2, 2),
+            f"3|U|{ADDR[1]}": [H("1/1", 1, 11)], "3|M|1": [H("1/1", 1, 11, "PHP")],
+            "3|M|3": [POP], **adj_routes(3, pr[2]["adjs"]),
+            f"4|U|{ADDR[3]}": [H("3/1", 3, 11)], "4|M|3": [H("3/1", 3, 11, "PHP")],
+            f"4|U|{ADDR[2]}": [H("2/1", 2, 11)], "4|M|2": [H("2/1", 2, 11, "PHP")],
+            f"4|U|{ADDR[1]}": _p4_1, "4|M|1": _sw(_p4_1, 1),
+            "4|M|4": [POP], **adj_routes(4, pr[3]["adjs"])})])]))
+
+# SimpleRingTopologyFixture.IpToMplsLabelPrepend (DecisionTest.cpp:2374-2536),
+# v6 / no prefix type: node 1's addr1 entry is SR_MPLS + SP_ECMP (:2403-2418).
+# Case 1 (:2419-2437) whole; case 3's prepend label (:2463-2478) for nodes 1
+# and 4 only -- the reference keeps case 2's minNexthop = 2 there, which
+# removes the routes of nodes 2 and 3 (RIB policy, not restated). Case 4
+# needs static MPLS routes (updateStaticMplsRoutes): not restated.
+_pp = 10001
+fixtures.append(dict(
+    name="decision_ip_to_mpls_label_prepend",
+    source="openr/decision/tests/DecisionTest.cpp:2374-2536",
+    steps=[dict(dbs=ring, expect_changes=ring_changes, checks=[
+        route_map([1, 2, 3, 4], {ADDR[1]: [["1", "sr_mpls", "ecmp", 0, None]]},
+                  expect={f"2|U|{ADDR[1]}": [H("2/1", 1, 10)],
+                          f"3|U|{ADDR[1]}": [H("3/1", 1, 10)],
+                          f"4|U|{ADDR[1]}": [H("4/2", 2, 20, "PUSH", [1]),
+                                             H("4/3", 3, 20, "PUSH", [1])]},
+                  expect_absent=[f"1|U|{ADDR[1]}"]),
+        route_map([1, 4], {ADDR[1]: [["1", "sr_mpls", "ecmp", 0, _pp]]},
+                  expect={f"4|U|{ADDR[1]}": [H("4/2", 2, 20, "PUSH", [_pp, 1]),
+                                             H("4/3", 3, 20, "PUSH", [_pp, 1])]},
+                  expect_absent=[f"1|U|{ADDR[1]}"]),
+    ])]))
+
+# ConnectivityTest.CompatibilityNodeTest (DecisionTest.cpp:1564-1688):
+# adjacencies of the "old" kind (labels 10000xx, metric 20 on 1-2)
+_c12_1 = adj("2", "1/2", "2/1", 10, 1000021)
+_c12_2 = adj("2", "1/2", "2/1", 20, 1000022)
+_c13 = adj("3", "1/3", "3/1", 10, 1000031)
+_c21 = adj("1", "2/1", "1/2", 10, 1000011)
+_c23 = adj("3", "2/3", "3/2", 10, 100003)
+_c32 = adj("2", "3/2", "2/3", 10, 100002)
+_c31 = adj("1", "3/1", "1/3", 10, 1000011)
+_cpx = loopbacks([1, 2, 3])
+fixtures.append(dict(
+    name="decision_connectivity_compatibility_node",
+    source="openr/decision/tests/DecisionTest.cpp:1564-1688",
+    steps=[
+        dict(dbs=[db(2, [_c21, _c23], 2), db(3, [_c32, _c31], 3), db(1, [_c12_1], 1)],
+             expect_changes=[[False, None, None, None], [True, None, None, None],
+                             [True, None, None, None]]),
+        dict(dbs=[db(1, [_c12_1, _c13], 1)], expect_changes=[[True, None, None, None]]),
+        dict(dbs=[db(1, [_c12_2, _c13], 1)], expect_changes=[[True, None, None, None]],
+             checks=[route_map([1, 2, 3], _cpx, expect_size=21, expect={
+                 f"1|U|{ADDR[2]}": [H("1/2", 2, 20), H("1/3", 3, 20)],
+                 f"1|U|{ADDR[3]}": [H("1/3", 3, 10)],
+                 "1|M|2": [H("1/2", 2, 20, "PHP"), H("1/3", 3, 20, "SWAP", [2])],
+                 "1|M|3": [H("1/3", 3, 10, "PHP")],
+                 "1|M|1": [POP], **adj_routes(1, [_c12_2, _c13]),
+                 f"2|U|{ADDR[3]}": [H("2/3", 3, 10)], f"2|U|{ADDR[1]}": [H("2/1", 1, 10)],
+                 "2|M|1": [H("2/1", 1, 10, "PHP")], "2|M|3": [H("2/3", 3, 10, "PHP")],
+                 f"3|U|{ADDR[2]}": [H("3/2", 2, 10)], f"3|U|{ADDR[1]}": [H("3/1", 1, 10)],
+                 "3|M|1": [H("3/1", 1, 10, "PHP")], "3|M|2": [H("3/2", 2, 10, "PHP")],
+                 "3|M|3": [POP], **adj_routes(3, [_c32, _c31])})]),
+        dict(dbs=[db(1, [_c12_2], 0)], expect_changes=[[True, None, None, None]]),
+        dict(dbs=[db(3, [_c32], 0)], expect_changes=[[False, None, None, None]]),
+        dict(dbs=[db(1, [_c12_2, _c13], 0)], expect_changes=[[False, None, None, None]]),
+    ]))
+
+# DecisionTest.Ip2MplsRoutes (DecisionTest.cpp:4254-4550): SR_MPLS loopbacks
+# of 1-3, the default route from 4 and 5, no adjacency labels; 15 unicast +
+# 25 node-label routes
+def _ia(other, ifn, oif, metric):
+    return adj(str(other), ifn, oif, metric, 0)
+
+
+_ip = [db(1, [_ia(2, "2/1", "1/1", 10), _ia(2, "2/2", "1/2", 10), _ia(3, "3/1", "1/1", 10)], 1),
+       db(2, [_ia(1, "1/1", "2/1", 10), _ia(1, "1/2", "2/2", 10), _ia(4, "4/1", "2/1", 10),
+              _ia(5, "5/1", "2/1", 10)], 2),
+       db(3, [_ia(1, "1/1", "3/1", 10), _ia(4, "4/1", "3/1", 20), _ia(5, "5/1", "3/1", 10)], 3),
+       db(4, [_ia(2, "2/1", "4/1", 10), _ia(3, "3/1", "4/1", 20)], 4),
+       db(5, [_ia(2, "2/1", "5/1", 10), _ia(3, "3/1", "5/1", 10)], 5)]
+_ipx = {ADDR[1]: [["1", "sr_mpls", "ecmp", 0, None]], ADDR[2]: [["2", "sr_mpls", "ecmp", 0, None]],
+        ADDR[3]: [["3", "sr_mpls", "ecmp", 0, None]],
+        "::/0": [["4", "sr_mpls", "ecmp", 0, None], ["5", "sr_mpls", "ecmp", 0, None]]}
+fixtures.append(dict(
+    name="decision_ip2mpls_routes",
+    source="openr/decision/tests/DecisionTest.cpp:4254-4550",
+    steps=[dict(
+        dbs=_ip, expect_changes=[[False, None, None, None]] + [[True, None, None, None]] * 4,
+        checks=[route_map([1, 2, 3, 4, 5], _ipx, expect_size=40, expect={
+            "1|M|1": [POP],
+            f"1|U|{ADDR[2]}": [H("2/2", 2, 10), H("2/1", 2, 10)],
+            f"1|U|{ADDR[3]}": [H("3/1", 3, 10)],
+            "1|U|::/0": [H("3/1", 3, 20, "PUSH", [5]), H("2/2", 2, 20, "PUSH", [4]),
+                         H("2/2", 2, 20, "PUSH", [5]), H("2/1", 2, 20, "PUSH", [4]),
+                         H("2/1", 2, 20, "PUSH", [5])],
+            "1|M|2": [H("2/1", 2, 10, "PHP"), H("2/2", 2, 10, "PHP")],
+            "1|M|3": [H("3/1", 3, 10, "PHP")],
+            "1|M|4": [H("2/1", 2, 20, "SWAP", [4]), H("2/2", 2, 20, "SWAP", [4])],
+            "1|M|5": [H("2/1", 2, 20, "SWAP", [5]), H("2/2", 2, 20, "SWAP", [5]),
+                      H("3/1", 3, 20, "SWAP", [5])],
+            "2|M|2": [POP],
+            f"2|U|{ADDR[1]}": [H("1/1", 1, 10), H("1/2", 1, 10)],
+            f"2|U|{ADDR[3]}": [H("1/1", 1, 20, "PUSH", [3]), H("1/2", 1, 20, "PUSH", [3]),
+                               H("5/1", 5, 20, "PUSH", [3])],
+            "2|U|::/0": [H("4/1", 4, 10), H("5/1", 5, 10)],
+            "2|M|1": [H("1/1", 1, 10, "PHP"), H("1/2", 1, 10, "PHP")],
+            "2|M|3": [H("1/1", 1, 20, "SWAP", [3]), H("1/2", 1, 20, "SWAP", [3]),
+                      H("5/1", 5, 20, "SWAP", [3])],
+            "2|M|4": [H("4/1", 4, 10, "PHP")], "2|M|5": [H("5/1", 5, 10, "PHP")],
+            "3|M|3": [POP],
+            f"3|U|{ADDR[1]}": [H("1/1", 1, 10)],
+            f"3|U|{ADDR[2]}": [H("1/1", 1, 20, "PUSH", [2]), H("5/1", 5, 20, "PUSH", [2])],
+            "3|U|::/0": [H("5/1", 5, 10)],
+            "3|M|1": [H("1/1", 1, 10, "PHP")],
+            "3|M|2": [H("1/1", 1, 20, "SWAP", [2]), H("5/1", 5, 20, "SWAP", [2])],
+            "3|M|4": [H("4/1", 4, 20, "PHP")], "3|M|5": [H("5/1", 5, 10, "PHP")],
+            "4|M|4": [POP],
+            f"4|U|{ADDR[1]}": [H("2/1", 2, 20, "PUSH", [1])],
+            f"4|U|{ADDR[2]}": [H("2/1", 2, 10)], f"4|U|{ADDR[3]}": [H("3/1", 3, 20)],
+            "4|M|1": [H("2/1", 2, 20, "SWAP", [1])], "4|M|2": [H("2/1", 2, 10, "PHP")],
+            "4|M|3": [H("3/1", 3, 20, "PHP")], "4|M|5": [H("2/1", 2, 20, "SWAP", [5])],
+            "5|M|5": [POP],
+            f"5|U|{ADDR[1]}": [H("2/1", 2, 20, "PUSH", [1]), H("3/1", 3, 20, "PUSH", [1])],
+            f"5|U|{ADDR[2]}": [H("2/1", 2, 10)], f"5|U|{ADDR[3]}": [H("3/1", 3, 10)],
+            "5|M|1": [H("2/1", 2, 20, "SWAP", [1]), H("3/1", 3, 20, "SWAP", [1])],
+            "5|M|2": [H("2/1", 2, 10, "PHP")], "5|M|3": [H("3/1", 3, 10, "PHP")],
+            "5|M|4": [H("2/1", 2, 20, "SWAP", [4])]})])]))
+
 # LinkStateTest.pathAInPathB (LinkStateTest.cpp:211-254)
 _l1, _l2, _l3 = "1%1/2|2%2/1", "2%2/3|3%3/2", "1%1/3|3%3/1"
 fixtures.append(dict(
