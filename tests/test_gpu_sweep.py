@@ -286,7 +286,6 @@ def test_sweep_invalidated_by_graph_change():
 def test_leaf_derive_rejects_a_non_uniform_group():
     """ospf_leaf_derive_dev checks that a group's roots share their slot table
     (error bit 128 at ospf_sync) instead of deriving wrong rows."""
-    import ctypes as C
     import torch
     st = drained_fabric(4, 4, seed=5, drain=0.0, down=0.0)
     ls, csr, eng = engine_for(st)
@@ -294,7 +293,9 @@ def test_leaf_derive_rejects_a_non_uniform_group():
         names = ls.node_names()
         V = eng.V
         racks = [i for i, n in enumerate(names) if n.startswith("3-")]
-        a, b = racks[0], next(r for r in racks if names[r].split("-")[1] != names[a].split("-")[1])
+        a = racks[0]
+        pod_a = names[a].split("-")[1]
+        b = next(r for r in racks if names[r].split("-")[1] != pod_a)
         dev = torch.device("cuda", 0)
         pitch = eng.lev_pitch
         allv = np.arange(V, dtype=np.uint32)
