@@ -196,6 +196,24 @@ int ospf_nh_derive_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n, uint3
                        const uint32_t* d_lev_pos, const ospf_digest* d_lev_digest,
                        uint32_t* d_nh, ospf_digest* d_digest, void* stream);
 
+/* Next hops (nh_words 1..4) from twin classes (spf_twin.hip), otherwise as
+ * ospf_nh_derive_dev. Twins = nodes with the same usable distinct
+ * neighbours and the same transit bit: their level rows agree except at the
+ * members' own positions (dist(a, v) == dist(b, v) for v outside {a, b},
+ * dist(a, b) == dist(b, a); LinkState.cpp:836-911 with unit weights), so a
+ * root reads one row per class of its neighbours (a fabric switch: its
+ * pod's racks, its plane's spines) instead of one per neighbour.
+ * d_twin_class [V] = class of each node, d_twin_rep / d_twin_second
+ * [classes] = its smallest member (whose level row is read) and another
+ * member (0xFFFFFFFF for a class of one). A root whose usable transit
+ * neighbours span more than 16 classes raises error bit 256. */
+int ospf_nh_derive_twin_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n, uint32_t nh_words,
+                            uint32_t max_root_neighbors, const uint8_t* d_lev,
+                            uint32_t lev_pitch, const uint32_t* d_lev_pos,
+                            const ospf_digest* d_lev_digest, const uint32_t* d_twin_class,
+                            const uint32_t* d_twin_rep, const uint32_t* d_twin_second,
+                            uint32_t* d_nh, ospf_digest* d_digest, void* stream);
+
 /* All-sources rows of leaf roots from level rows (unit metric or hop count;
  * spf_leaf.hip). A leaf r (no two leaves adjacent, <= 32 distinct
  * neighbours n_k) has dist(r, v) = 1 + min_k dist(n_k, v) over n_k with an

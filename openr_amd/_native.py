@@ -29,7 +29,8 @@ ENGINE_SYMBOLS = [
     "ospf_root_neighbors", "ospf_sssp_batch", "ospf_sssp_batch_dev", "ospf_sync",
     "ospf_plan_variant", "ospf_plan", "ospf_plan_n", "ospf_spf_runs", "ospf_run_batch_dev",
     "ospf_ksp2_run", "ospf_ksp2_dev", "ospf_update_links", "ospf_update_nodes",
-    "ospf_levels_dev", "ospf_nh_derive_dev", "ospf_leaf_derive_dev", "ospf_wderive_dev", "ospf_wderive_wide_dev",
+    "ospf_levels_dev", "ospf_nh_derive_dev", "ospf_leaf_derive_dev",
+    "ospf_nh_derive_twin_dev", "ospf_wderive_dev", "ospf_wderive_wide_dev",
     "ospf_cover_prepare", "ospf_cover_dist_dev",
     "ospf_affected_roots", "ospf_repair_runs", "ospf_links_mask", "ospf_links_unmask",
     "ospf_sweep_create", "ospf_sweep_destroy", "ospf_sweep_last_error", "ospf_sweep_get_info",
@@ -156,6 +157,8 @@ def engine() -> C.CDLL:
         L.ospf_ksp2_dev.argtypes = [vp, C.POINTER(ospf_ksp2), vp]
         L.ospf_levels_dev.argtypes = [vp, vp, u32, u32, vp, vp, u32, vp, vp]
         L.ospf_nh_derive_dev.argtypes = [vp, vp, u32, u32, u32, vp, u32, vp, vp, vp, vp, vp]
+        L.ospf_nh_derive_twin_dev.argtypes = [vp, vp, u32, u32, u32, vp, u32, vp, vp, vp, vp, vp,
+                                              vp, vp, vp]
         L.ospf_leaf_derive_dev.argtypes = [vp, vp, u32, vp, u32, u32, vp, u32, vp, vp, vp, vp, vp]
         L.ospf_wderive_dev.argtypes = [vp, vp, u32, u32, u32, vp, u64, vp, vp, vp, vp, vp]
         L.ospf_wderive_wide_dev.argtypes = [vp, vp, u32, u32, u32, vp, u64, vp, vp, vp, vp]

@@ -1138,6 +1138,7 @@ int ospf_sync(ospf_ctx* c, void* stream) {
                 : (err & 16u) ? "derive: a root or a usable neighbour has no level row"
                 : (err & 64u) ? "a device root id is out of range"
                 : (err & 128u) ? "leaf derive: a group's roots do not share their slot table"
+                : (err & 256u) ? "twin derive: a root's neighbours span more than 16 twin classes"
                              : "internal: a frontier entry out of range");
   }
   return OSPF_OK;
@@ -1327,6 +1328,49 @@ int ospf_nh_derive_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_
   d.err = c->d_err;
   hipError_t e = ospf::launch_nh_derive(c->g, d, s);
   if (e != hipSuccess) return hip_fail(c, e, "launch_nh_derive");
+  return OSPF_OK;
+}
+
+// Twin derive (spf_twin.hip): next-hop rows of roots whose usable transit
+// neighbours fall into few twin classes (<= 16), from one representative
+// level row per class.
+int ospf_nh_derive_twin_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t nh_words,
+                            uint32_t max_root_neighbors, const uint8_t* d_lev,
+                            uint32_t lev_pitch, const uint32_t* d_lev_pos,
+                            const ospf_digest* d_lev_digest, const uint32_t* d_twin_class,
+                            const uint32_t* d_twin_rep, const uint32_t* d_twin_second,
+                            uint32_t* d_nh, ospf_digest* d_digest, void* stream) {
+  if (!c) return OSPF_E_INVAL;
+  if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  if (n == 0) return OSPF_OK;
+  if (!d_roots || !d_lev || !d_lev_pos || !d_nh || !d_twin_class || !d_twin_rep || !d_twin_second)
+    return fail(c, OSPF_E_INVAL, "null argument");
+  if (lev_pitch % 16u || lev_pitch < c->info.n_nodes)
+    return fail(c, OSPF_E_INVAL, "lev_pitch: a multiple of 16 >= V");
+  if (d_digest && !d_lev_digest)
+    return fail(c, OSPF_E_INVAL, "derive: digests need the level rows' digests");
+  if (nh_words == 0 || nh_words > 4) return fail(c, OSPF_E_RANGE, "twin derive: nh_words 1..4");
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (d_digest) HIPCHK(c, hipMemsetAsync(d_digest, 0, (size_t)n * sizeof(ospf_digest), s));
+  ospf::TwinArgs a{};
+  a.roots = d_roots;
+  a.n = n;
+  a.W = nh_words;
+  a.cap = max_root_neighbors ? std::min(max_root_neighbors, 32u * nh_words) : 32u * nh_words;
+  a.lev = d_lev;
+  a.pitch = lev_pitch;
+  a.pos = d_lev_pos;
+  a.lev_digest = d_lev_digest;
+  a.tcls = d_twin_class;
+  a.trep = d_twin_rep;
+  a.tsec = d_twin_second;
+  a.nh = d_nh;
+  a.digest = d_digest;
+  a.err = c->d_err;
+  if (const char* e = getenv("OSPF_TWIN_CTILES")) a.ctiles = (uint32_t)std::max(1, atoi(e));
+  hipError_t e = ospf::launch_nh_derive_twin(c->g, a, s);
+  if (e != hipSuccess) return hip_fail(c, e, "launch_nh_derive_twin");
   return OSPF_OK;
 }
 

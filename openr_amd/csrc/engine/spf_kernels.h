@@ -296,6 +296,29 @@ hipError_t launch_msbfs_levels(const DevGraph& g, const MsArgs& a, uint32_t dept
                                hipStream_t s);
 hipError_t launch_nh_derive(const DevGraph& g, const DeriveArgs& d, hipStream_t s);
 
+// Twin derive (spf_twin.hip): next-hop words (W <= 4) of roots whose
+// usable transit neighbours fall into few twin classes -- nodes with the
+// same usable distinct neighbours and the same transit bit, whose level rows
+// agree everywhere except at the members' own positions -- so a tile reads
+// one representative row per class instead of one row per neighbour.
+constexpr uint32_t kTwinMaxC = 16;
+struct TwinArgs {
+  const uint32_t* roots;
+  uint32_t n, W, cap;
+  const uint8_t* lev;
+  uint32_t pitch;
+  const uint32_t* pos;
+  const ospf_digest* lev_digest;
+  const uint32_t* tcls;   // [V] twin class of each node
+  const uint32_t* trep;   // [classes] representative (smallest id)
+  const uint32_t* tsec;   // [classes] second member (kInf: a class of one)
+  uint32_t* nh;           // [n][V][W]
+  ospf_digest* digest;    // [n] (zeroed by the caller) or null
+  uint32_t* err;          // + bit 256: a root with more than kTwinMaxC classes
+  uint32_t tiles, ctiles, chunks;
+};
+hipError_t launch_nh_derive_twin(const DevGraph& g, const TwinArgs& a, hipStream_t s);
+
 // Leaf derive (spf_leaf.hip), unit metric / hop count: the level, dist and
 // one-word next-hop rows of leaf roots (<= 32 distinct neighbours, every
 // usable transit neighbour's level row present) from their neighbours' level

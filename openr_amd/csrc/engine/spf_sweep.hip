@@ -301,6 +301,75 @@ std::vector<uint32_t> leaf_groups(const ospf_ctx* c, const Facts& f, std::vector
   return grp;
 }
 
+// Twin classes (spf_twin.hip): nodes with the same usable distinct
+// neighbours and the same transit bit. cls[v] = class id, rep / sec = the
+// smallest two members of each class (sec = kNone for a class of one).
+struct Twins {
+  std::vector<uint32_t> cls, rep, sec;
+};
+Twins twin_classes(const ospf_ctx* c) {
+  const uint32_t V = c->info.n_nodes;
+  std::vector<uint32_t> off(V + 1, 0), lst;
+  std::vector<uint64_t> key(V);
+  lst.reserve(c->h_dn.size());
+  for (uint32_t u = 0; u < V; ++u) {
+    off[u] = (uint32_t)lst.size();
+    const size_t b = lst.size();
+    for (uint32_t e = c->h_prow[u]; e < c->h_prow[u + 1]; ++e) {
+      const uint32_t x = c->h_pcolx[e];
+      if ((x & 0x80000000u) || x == u) continue;
+      lst.push_back(x);
+    }
+    std::sort(lst.begin() + b, lst.end());
+    lst.erase(std::unique(lst.begin() + b, lst.end()), lst.end());
+    const bool tr = !((c->h_nt[u >> 5] >> (u & 31)) & 1u);
+    uint64_t h = tr ? 0x9E3779B97F4A7C15ull : 0xC2B2AE3D27D4EB4Full;
+    for (size_t i = b; i < lst.size(); ++i) h = ospf::digest_mix(h ^ lst[i]) + i - b;
+    key[u] = h;
+  }
+  off[V] = (uint32_t)lst.size();
+  auto same = [&](uint32_t a, uint32_t b) {
+    const bool ta = !((c->h_nt[a >> 5] >> (a & 31)) & 1u), tb = !((c->h_nt[b >> 5] >> (b & 31)) & 1u);
+    return ta == tb && off[a + 1] - off[a] == off[b + 1] - off[b] &&
+           std::equal(lst.begin() + off[a], lst.begin() + off[a + 1], lst.begin() + off[b]);
+  };
+  std::vector<uint32_t> ord(V);
+  std::iota(ord.begin(), ord.end(), 0u);
+  std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
+  Twins t;
+  t.cls.assign(V, kNone);
+  for (size_t i = 0; i < V;) {
+    size_t j = i;
+    while (j < V && key[ord[j]] == key[ord[i]]) ++j;
+    // within a hash run, split by exact equality (collisions are rare)
+    for (size_t p = i; p < j; ++p) {
+      const uint32_t u = ord[p];
+      if (t.cls[u] != kNone) continue;
+      const uint32_t id = (uint32_t)t.rep.size();
+      t.rep.push_back(u);
+      t.sec.push_back(kNone);
+      t.cls[u] = id;
+      for (size_t q = p + 1; q < j; ++q) {
+        const uint32_t w = ord[q];
+        if (t.cls[w] != kNone || !same(u, w)) continue;
+        t.cls[w] = id;
+      }
+    }
+    i = j;
+  }
+  // representative = smallest member, second = the next one
+  for (uint32_t u = 0; u < V; ++u) {
+    const uint32_t id = t.cls[u];
+    if (u < t.rep[id]) {
+      t.sec[id] = t.rep[id];
+      t.rep[id] = u;
+    } else if (u != t.rep[id] && (t.sec[id] == kNone || u < t.sec[id])) {
+      t.sec[id] = u;
+    }
+  }
+  return t;
+}
+
 // DERIVE (spf_levels.hip, spf_leaf.hip, spf_msbfs.hip derive kernels), unit
 // metric / hop count. The part's roots split into leaves (an independent set
 // of nodes with <= 32 distinct neighbours: a fabric's racks) and the cover.
@@ -385,6 +454,32 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   if ((rc = dalloc(s, &s->dig_all, ndig))) return rc;
   s->n_dig = ndig;
   const int ev_a = new_event(s), ev_b = new_event(s);  // levels done, leaves done
+  // twin classes: a class of <= 4-word roots whose usable transit
+  // neighbours span few classes reads one row per class (spf_twin.hip)
+  Twins tw;
+  uint32_t *d_tcls = nullptr, *d_trep = nullptr, *d_tsec = nullptr;
+  auto twin_ok = [&](const std::vector<uint32_t>& roots) {
+    if (getenv("OSPF_SWEEP_NOTWIN")) return false;
+    uint64_t slots = 0, classes = 0;
+    for (uint32_t r : roots) {
+      std::vector<uint32_t> cs;
+      for (uint32_t e = c->h_prow[r]; e < c->h_prow[r + 1]; ++e) {
+        const uint32_t x = c->h_pcolx[e];
+        if ((x & 0x80000000u) || x == r || ((c->h_nt[x >> 5] >> (x & 31)) & 1u)) continue;
+        cs.push_back(tw.cls[x]);
+      }
+      slots += f.nbrs(r);
+      std::sort(cs.begin(), cs.end());
+      cs.erase(std::unique(cs.begin(), cs.end()), cs.end());
+      if (cs.size() > ospf::kTwinMaxC) return false;
+      classes += cs.size();
+    }
+    // worth it when a class covers several slots (OSPF_SWEEP_TWIN=1: always)
+    return getenv("OSPF_SWEEP_TWIN") || slots >= 3 * std::max<uint64_t>(1, classes);
+  };
+  bool any_w4 = false;
+  for (auto& k : cls) any_w4 |= k.W <= 4;
+  if (any_w4 && !getenv("OSPF_SWEEP_NOTWIN")) tw = twin_classes(c);
   if (ev_a < 0 || ev_b < 0) return ev_a < 0 ? ev_a : ev_b;
   if (nc) {
     ospf_sweep::Unit lv;
@@ -424,9 +519,16 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
         reads_leaf = leaf[(*f.dn)[q]] != 0;
     ospf_sweep::Unit u;
     u.name = "derive_cap" + std::to_string(k.cap);
-    u.kernel = std::string("ospf_nh_derive_dev (") +
-               (W <= 4 ? "nh_derive16_kernel" : "nh_derive_wide_kernel") + ", " +
-               std::to_string(W) + " next-hop word" + (W > 1 ? "s)" : ")");
+    const bool twin = W <= 4 && !tw.cls.empty() && twin_ok(k.roots);
+    if (twin && !d_tcls) {
+      if ((rc = upload(s, &d_tcls, tw.cls)) || (rc = upload(s, &d_trep, tw.rep)) ||
+          (rc = upload(s, &d_tsec, tw.sec)))
+        return rc;
+    }
+    u.kernel = std::string(twin ? "ospf_nh_derive_twin_dev (" : "ospf_nh_derive_dev (") +
+               (twin ? "nh_derive_twin_kernel" : W <= 4 ? "nh_derive16_kernel"
+                                                        : "nh_derive_wide_kernel") +
+               ", " + std::to_string(W) + " next-hop word" + (W > 1 ? "s)" : ")");
     const int st = new_stream(s);
     if (st < 0) return st;
     u.stream = st;
@@ -434,9 +536,17 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     u.n_roots = n;
     u.W = W;
     u.comp = (uint64_t)n * 4ull * V * W;
-    u.fn = [=](hipStream_t strm) {
-      return ospf_nh_derive_dev(c, d_roots, n, W, cap, lev, pitch, d_pos, ldg, nh, dg, strm);
-    };
+    if (twin) {
+      const uint32_t *tc = d_tcls, *tr = d_trep, *ts = d_tsec;
+      u.fn = [=](hipStream_t strm) {
+        return ospf_nh_derive_twin_dev(c, d_roots, n, W, cap, lev, pitch, d_pos, ldg, tc, tr, ts,
+                                       nh, dg, strm);
+      };
+    } else {
+      u.fn = [=](hipStream_t strm) {
+        return ospf_nh_derive_dev(c, d_roots, n, W, cap, lev, pitch, d_pos, ldg, nh, dg, strm);
+      };
+    }
     s->step_comp += u.comp;
     (reads_leaf ? after : side).push_back(std::move(u));
   }

@@ -1,0 +1,298 @@
+// spf_twin.hip — next hops of roots with twin neighbours (gfx950), unit
+// metric / hop count.
+//
+// The derive rule (LinkState::runSpf's nextHops, openr/decision/
+// LinkState.cpp:885-901, with unit weights): the k-th distinct neighbour n_k
+// of root r is a next hop towards v iff the link r-n_k is up, n_k is transit
+// or n_k == v, and dist(n_k, v) + 1 == dist(r, v). nh_derive16_kernel reads
+// one level row per neighbour: 84 rows per fabric switch (48 racks of its
+// pod, 36 spines of its plane) for 3 next-hop words per node.
+//
+// Twins. Two nodes a, b with the same usable distinct neighbours and the
+// same transit bit (never adjacent: each would be its own neighbour) have
+// dist(a, v) == dist(b, v) for every v outside {a, b}: a shortest path from
+// either leaves through the same first hops, and overloaded nodes relay for
+// neither (:859-866). And dist(a, b) == dist(b, a) (unit weights, the same
+// transit conditions both ways). So a class of twins has ONE level row R
+// (its representative's), except that member m sits at level 1 at its own
+// position and, at the representative's position, every other member sits
+// at X = R(any other member). A pod's racks are one class, a plane's spines
+// another: a fabric switch reads its own row and two class rows per tile.
+//
+// Per lane 16 nodes (one 16-B load per row), a class is tight where
+// R == L - 1 (L = the root's own level bytes; the borrow-free SWAR test of
+// nh_derive16_kernel) and contributes its usable slots' bits at once. The
+// members' own positions are patched afterwards (a neighbour is a next hop
+// towards itself; at the representative the class is re-tested against X),
+// on the words staged in LDS for the coalesced row stores, and the digest
+// terms are taken from the patched words.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "spf_kernels.h"
+
+namespace ospf {
+namespace {
+
+constexpr uint32_t kInf = 0xFFFFFFFFu;
+constexpr uint32_t kDown = 0x80000000u;
+constexpr uint32_t kBlock = 256;
+constexpr uint32_t kWaves = kBlock / 64u;
+constexpr uint32_t kMaxK = 128;  // W <= 4 words
+
+__device__ __forceinline__ bool transit(const DevGraph& g, uint32_t v) {
+  return !((g.nt_bits[v >> 5] >> (v & 31)) & 1u);
+}
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t x, int o) {
+  const uint32_t lo = __shfl_xor((uint32_t)x, o, 64);
+  const uint32_t hi = __shfl_xor((uint32_t)(x >> 32), o, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+template <int W>
+__global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, TwinArgs a) {
+  __shared__ uint32_t s_nb[kMaxK];     // distinct neighbours (ascending)
+  __shared__ uint32_t s_slot[kMaxK];   // per slot: class index, 0x100 non-transit, kInf unusable
+  __shared__ uint32_t s_use[4];
+  __shared__ uint32_t s_ccls[kTwinMaxC], s_crow[kTwinMaxC], s_crep[kTwinMaxC], s_cx[kTwinMaxC];
+  __shared__ uint32_t s_cmask[kTwinMaxC][4];
+  __shared__ uint32_t s_nc, s_K, s_own, s_root, s_bad;
+  __shared__ unsigned long long s_h;
+  extern __shared__ uint32_t s_stage[];  // [4 waves][1024 nodes][W]
+  const uint32_t V = g.V, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  // XCD-aware order: XCD x (blocks x, x + 8, ...) walks a contiguous range
+  // of (root, chunk) items, so roots sharing class rows share its L2
+  const uint32_t T = a.n * a.chunks, T8 = T / 8u * 8u, b = blockIdx.x;
+  const uint32_t item = b < T8 ? (b % 8u) * (T8 / 8u) + b / 8u : b;
+  const uint32_t i = item / a.chunks, ci = item % a.chunks;
+  if (tid == 0) {
+    const uint32_t r = a.roots[i];
+    s_root = r;
+    s_h = 0ull;
+    s_bad = 0u;
+    s_nc = 0u;
+    s_own = r < V ? a.pos[r] : kInf;
+    s_K = r < V ? g.dn_off[r + 1] - g.dn_off[r] : 0u;
+    if (r >= V) atomicOr(a.err, 64u);
+    else if (s_own == kInf) atomicOr(a.err, 16u);
+    else if (s_K > a.cap || s_K > 32u * W) atomicOr(a.err, 1u);
+  }
+  if (tid < 4) s_use[tid] = 0u;
+  __syncthreads();
+  const uint32_t r = s_root, K = min(s_K, (uint32_t)(32 * W)), own = s_own;
+  if (r >= V || own == kInf) return;
+  for (uint32_t e = g.row_ptr[r] + tid; e < g.row_ptr[r + 1]; e += kBlock) {
+    const uint32_t cx = g.colx[e];
+    if ((cx & kDown) || cx == r) continue;
+    const uint32_t k = g.didx[e];
+    if (k < K) atomicOr(&s_use[k >> 5], 1u << (k & 31u));
+  }
+  if (tid < K) s_nb[tid] = g.dn[g.dn_off[r] + tid];
+  __syncthreads();
+  if (tid == 0) {  // classes of the usable transit slots (K <= 128, once per block)
+    uint32_t nc = 0;
+    for (uint32_t k = 0; k < K; ++k) {
+      if (!((s_use[k >> 5] >> (k & 31u)) & 1u)) {
+        s_slot[k] = kInf;
+        continue;
+      }
+      const uint32_t n = s_nb[k];
+      if (!transit(g, n)) {
+        s_slot[k] = 0x100u;
+        continue;
+      }
+      const uint32_t c = a.tcls[n];
+      uint32_t j = 0;
+      while (j < nc && s_ccls[j] != c) ++j;
+      if (j == nc) {
+        if (nc == kTwinMaxC) {
+          s_bad = 1u;
+          break;
+        }
+        s_ccls[nc] = c;
+        for (int w = 0; w < 4; ++w) s_cmask[nc][w] = 0u;
+        ++nc;
+      }
+      s_cmask[j][k >> 5] |= 1u << (k & 31u);
+      s_slot[k] = j;
+    }
+    s_nc = nc;
+    if (s_bad) atomicOr(a.err, 256u);
+  }
+  __syncthreads();
+  if (s_bad) return;
+  const uint32_t nc = s_nc;
+  if (tid < nc) {
+    const uint32_t c = s_ccls[tid], rep = a.trep[c], sec = a.tsec[c];
+    const uint32_t row = a.pos[rep];
+    s_crep[tid] = rep;
+    s_crow[tid] = row;
+    if (row == kInf) atomicOr(a.err, 16u);
+    // X: level of another member at the representative's position
+    s_cx[tid] = (sec != kInf && row != kInf) ? a.lev[(size_t)row * a.pitch + sec] : 0x7Fu;
+  }
+  __syncthreads();
+  for (uint32_t x = 0; x < nc; ++x)
+    if (s_crow[x] == kInf) return;
+  const uint32_t t0 = ci * a.ctiles, t1 = min(a.tiles, t0 + a.ctiles);
+  uint32_t* st = s_stage + wave * 1024u * W;
+  uint64_t h = 0;
+  for (uint32_t t = t0 + wave; t < t1; t += kWaves) {
+    const uint32_t tv0 = t * 1024u, vl = tv0 + 16u * lane;
+    const bool live = vl < a.pitch;
+    const uint32_t vs = live ? vl : 0u;
+    const uint4 L = *reinterpret_cast<const uint4*>(a.lev + (size_t)own * a.pitch + vs);
+    uint32_t lm1[4];
+    {
+      const uint32_t Lw[4] = {L.x, L.y, L.z, L.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+          const uint32_t l = (Lw[q] >> (8 * bb)) & 0xFFu;
+          m |= (l >= 2u && l < 0x7Fu ? l - 1u : 0u) << (8 * bb);
+        }
+        lm1[q] = m | 0x80808080u;
+      }
+    }
+    uint32_t word[W][16];
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+#pragma unroll
+      for (int n = 0; n < 16; ++n) word[w][n] = 0u;
+    for (uint32_t j = 0; j < nc; ++j) {
+      const uint4 R = *reinterpret_cast<const uint4*>(a.lev + (size_t)s_crow[j] * a.pitch + vs);
+      const uint32_t Rw[4] = {R.x, R.y, R.z, R.w};
+      uint32_t cm[W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) cm[w] = s_cmask[j][w];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t z = live ? (lm1[q] - Rw[q]) & 0x80808080u : 0u;
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+          const uint32_t sel = 0u - ((z >> (8 * bb + 7)) & 1u);
+#pragma unroll
+          for (int w = 0; w < W; ++w) word[w][4 * q + bb] |= sel & cm[w];
+        }
+      }
+    }
+    // stage [node][word] in this wave's LDS slice
+#pragma unroll
+    for (int x = 0; x < 4 * W; ++x) {
+      uint32_t v4[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int f = 4 * x + c;
+        v4[c] = word[f % W][f / W];
+      }
+      reinterpret_cast<uint4*>(st + 16u * W * lane)[x] = make_uint4(v4[0], v4[1], v4[2], v4[3]);
+    }
+    __builtin_amdgcn_wave_barrier();
+    // members' own positions inside this tile (slots are sorted by node id)
+    if (lane == 0) {
+      uint32_t lo = 0, hi = K;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_nb[mid] < tv0) lo = mid + 1; else hi = mid;
+      }
+      for (uint32_t k = lo; k < K && s_nb[k] < tv0 + 1024u; ++k) {
+        const uint32_t sk = s_slot[k];
+        if (sk == kInf) continue;
+        const uint32_t n = s_nb[k], o = n - tv0;
+        const uint32_t Ln = a.lev[(size_t)own * a.pitch + n];
+        uint32_t nw[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) nw[w] = st[o * W + w];
+        if (sk != 0x100u && n == s_crep[sk]) {  // re-test the class against X
+          const bool tight = Ln >= 2u && Ln < 0x7Fu && s_cx[sk] + 1u == Ln;
+#pragma unroll
+          for (int w = 0; w < W; ++w) nw[w] = (nw[w] & ~s_cmask[sk][w]) | (tight ? s_cmask[sk][w] : 0u);
+        }
+        // n itself: level 1 of its own row, a next hop iff dist(r, n) == 1
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+          if ((uint32_t)w == (k >> 5)) {
+            const uint32_t bit = 1u << (k & 31u);
+            nw[w] = (nw[w] & ~bit) | (Ln == 2u ? bit : 0u);
+          }
+#pragma unroll
+        for (int w = 0; w < W; ++w) st[o * W + w] = nw[w];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const size_t dst0 = ((size_t)i * V + tv0) * W;
+    const uint32_t tn = tv0 < V ? min(1024u, V - tv0) : 0u;
+    if (tn == 1024u && (dst0 & 3u) == 0) {
+#pragma unroll
+      for (int x = 0; x < 4 * W; ++x)
+        store_row16(reinterpret_cast<uint4*>(a.nh + dst0) + x * 64 + lane,
+                    reinterpret_cast<const uint4*>(st)[x * 64 + lane]);
+    } else {
+      for (uint32_t x = lane; x < tn * W; x += 64u) a.nh[dst0 + x] = st[x];
+    }
+    if (a.digest && live) {
+      const uint4* kp = reinterpret_cast<const uint4*>(g.dkn + vl);  // zero past V
+#pragma unroll
+      for (int x = 0; x < 8; ++x) {
+        const uint4 k2 = kp[x];
+        const uint64_t kn[2] = {((uint64_t)k2.y << 32) | k2.x, ((uint64_t)k2.w << 32) | k2.z};
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+          const uint32_t nd = 2 * x + y;
+          uint64_t ws = 0;
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            const uint32_t wd = st[(16u * lane + nd) * W + w];
+            if (wd) ws += digest_word_key(w, wd);
+          }
+          h += kn[y] * ws;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the slice is rewritten by the next tile
+  }
+  if (a.digest) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) h += shfl_xor64(h, o);
+    if (lane == 0 && h) atomicAdd(&s_h, (unsigned long long)h);
+    __syncthreads();
+    if (tid == 0) {
+      ospf_digest* dg = a.digest + i;
+      unsigned long long hh = s_h;
+      if (ci == 0) {
+        const ospf_digest ld = a.lev_digest[own];
+        atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)ld.reached);
+        atomicAdd((unsigned long long*)&dg->sum_dist, (unsigned long long)ld.sum_dist);
+        hh += ld.hash;
+      }
+      if (hh) atomicAdd((unsigned long long*)&dg->hash, hh);
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_nh_derive_twin(const DevGraph& g, const TwinArgs& a0, hipStream_t s) {
+  TwinArgs a = a0;
+  if (a.n == 0) return hipSuccess;
+  if (a.W == 0 || a.W > 4) return hipErrorInvalidValue;
+  a.tiles = (g.V + 1023u) / 1024u;
+  if (!a.ctiles) a.ctiles = 16;
+  a.ctiles = std::max(1u, std::min(a.tiles, a.ctiles));
+  a.chunks = (a.tiles + a.ctiles - 1) / a.ctiles;
+  const dim3 grid(a.n * a.chunks);
+  const size_t lds = (size_t)kWaves * 1024u * a.W * 4u;
+  switch (a.W) {
+    case 1: hipLaunchKernelGGL(nh_derive_twin_kernel<1>, grid, dim3(kBlock), lds, s, g, a); break;
+    case 2: hipLaunchKernelGGL(nh_derive_twin_kernel<2>, grid, dim3(kBlock), lds, s, g, a); break;
+    case 3: hipLaunchKernelGGL(nh_derive_twin_kernel<3>, grid, dim3(kBlock), lds, s, g, a); break;
+    default: hipLaunchKernelGGL(nh_derive_twin_kernel<4>, grid, dim3(kBlock), lds, s, g, a); break;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace ospf

@@ -313,3 +313,34 @@ def test_leaf_derive_rejects_a_non_uniform_group():
             eng.sync()
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_twin_derive_forced_on_random_and_drained_graphs(seed, monkeypatch):
+    """spf_twin.hip on every <= 4-word class (OSPF_SWEEP_TWIN=1 skips the
+    benefit test): random unit graphs (few twins: classes of one, the patch
+    path at every neighbour), a drained fabric (racks with a down link leave
+    their pod's class) and a grid with overloaded nodes -- all equal to the
+    batch path bit for bit."""
+    monkeypatch.setenv("OSPF_SWEEP_TWIN", "1")
+    stream, _ = random_stream(seed + 20, n=60, unit=True)
+    _, _, eng = engine_for(stream)
+    try:
+        check_sweep_vs_batch(eng, "derive")
+        check_sweep_vs_batch(eng, "derive", hop=True)
+    finally:
+        eng.close()
+    _, _, eng = engine_for(drained_fabric(5, 4, seed=seed, drain=0.08, down=0.05))
+    try:
+        check_sweep_vs_batch(eng, "derive")
+    finally:
+        eng.close()
+    dbs = T.grid(14).to_dbs()
+    for d in dbs[seed::17]:
+        d.overloaded = True
+    from openr_amd.adjdb import AdjDbStream
+    _, _, eng = engine_for(AdjDbStream.from_dbs(dbs))
+    try:
+        check_sweep_vs_batch(eng, "derive")
+    finally:
+        eng.close()
