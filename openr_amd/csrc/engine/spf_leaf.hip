@@ -60,6 +60,7 @@ __device__ __forceinline__ uint32_t beq7(uint32_t x, uint32_t y) {
 template <int KM>
 __global__ void __launch_bounds__(kBlock) leaf_derive_kernel(DevGraph g, LeafArgs a) {
   __shared__ uint32_t s_root[kLeafMaxG], s_own[kLeafMaxG], s_use[kLeafMaxG];
+  __shared__ uint32_t s_rb[kLeafMaxG], s_re[kLeafMaxG];
   __shared__ uint32_t s_tab[32];
   __shared__ unsigned long long s_dr[kLeafMaxG], s_ds[kLeafMaxG], s_dh[kLeafMaxG];
   __shared__ unsigned long long s_br, s_bs, s_bh;
@@ -86,11 +87,15 @@ __global__ void __launch_bounds__(kBlock) leaf_derive_kernel(DevGraph g, LeafArg
   const bool small = KM <= 8;
   if (small && a.digest) s_wk[tid] = tid ? digest_word_key(0, tid) : 0ull;
   __syncthreads();
-  // usable slots of every root of the group (bit k: an up link to n_k)
-  for (uint32_t j = 0; j < ng; ++j) {
-    const uint32_t r = s_root[j];
-    if (r >= V) continue;
-    for (uint32_t e = g.row_ptr[r] + tid; e < g.row_ptr[r + 1]; e += kBlock) {
+  // usable slots of every root of the group (bit k: an up link to n_k):
+  // (root, entry) pairs spread over the block, padded rows <= 64 entries per
+  // root per pass
+  if (tid < ng) s_rb[tid] = s_root[tid] < V ? g.row_ptr[s_root[tid]] : 0u;
+  if (tid < ng) s_re[tid] = s_root[tid] < V ? g.row_ptr[s_root[tid] + 1] : 0u;
+  __syncthreads();
+  for (uint32_t x = tid; x < ng * 64u; x += kBlock) {
+    const uint32_t j = x >> 6, r = s_root[j];
+    for (uint32_t e = s_rb[j] + (x & 63u); e < s_re[j]; e += 64u) {
       const uint32_t cx = g.colx[e];
       if ((cx & kDown) || cx == r) continue;
       const uint32_t k = g.didx[e];

@@ -54,7 +54,9 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t x, int o) {
 template <int W>
 __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, TwinArgs a) {
   __shared__ uint32_t s_nb[kMaxK];     // distinct neighbours (ascending)
-  __shared__ uint32_t s_slot[kMaxK];   // per slot: class index, 0x100 non-transit, kInf unusable
+  __shared__ uint32_t s_slot[kMaxK];   // per slot: class id (0xFFFFFFFE non-transit, kInf unusable)
+  __shared__ uint32_t s_first[kMaxK];  // first slot of the same class
+  __shared__ uint32_t s_cid[kMaxK];    // per slot: class index, 0x100 non-transit, kInf unusable
   __shared__ uint32_t s_use[4];
   __shared__ uint32_t s_ccls[kTwinMaxC], s_crow[kTwinMaxC], s_crep[kTwinMaxC], s_cx[kTwinMaxC];
   __shared__ uint32_t s_cmask[kTwinMaxC][4];
@@ -91,32 +93,49 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
   }
   if (tid < K) s_nb[tid] = g.dn[g.dn_off[r] + tid];
   __syncthreads();
-  if (tid == 0) {  // classes of the usable transit slots (K <= 128, once per block)
+  // class of every usable transit slot (loads in parallel), first slot of
+  // each class, then one pass over the slot table in LDS
+  if (tid < K) {
+    const uint32_t n = s_nb[tid];
+    uint32_t v = kInf;  // unusable
+    if ((s_use[tid >> 5] >> (tid & 31u)) & 1u) v = transit(g, n) ? a.tcls[n] : 0xFFFFFFFEu;
+    s_slot[tid] = v;
+  }
+  __syncthreads();
+  if (tid < K) {
+    const uint32_t v = s_slot[tid];
+    uint32_t first = tid;
+    if (v < 0xFFFFFFFEu)
+      for (uint32_t k = 0; k < tid; ++k)
+        if (s_slot[k] == v) {
+          first = k;
+          break;
+        }
+    s_first[tid] = first;
+  }
+  __syncthreads();
+  if (tid == 0) {
     uint32_t nc = 0;
     for (uint32_t k = 0; k < K; ++k) {
-      if (!((s_use[k >> 5] >> (k & 31u)) & 1u)) {
-        s_slot[k] = kInf;
+      const uint32_t v = s_slot[k];
+      if (v >= 0xFFFFFFFEu) {
+        s_cid[k] = v == kInf ? kInf : 0x100u;
         continue;
       }
-      const uint32_t n = s_nb[k];
-      if (!transit(g, n)) {
-        s_slot[k] = 0x100u;
-        continue;
-      }
-      const uint32_t c = a.tcls[n];
-      uint32_t j = 0;
-      while (j < nc && s_ccls[j] != c) ++j;
-      if (j == nc) {
+      uint32_t j;
+      if (s_first[k] == k) {
         if (nc == kTwinMaxC) {
           s_bad = 1u;
           break;
         }
-        s_ccls[nc] = c;
-        for (int w = 0; w < 4; ++w) s_cmask[nc][w] = 0u;
-        ++nc;
+        j = nc++;
+        s_ccls[j] = v;
+        for (int w = 0; w < 4; ++w) s_cmask[j][w] = 0u;
+      } else {
+        j = s_cid[s_first[k]];
       }
       s_cmask[j][k >> 5] |= 1u << (k & 31u);
-      s_slot[k] = j;
+      s_cid[k] = j;
     }
     s_nc = nc;
     if (s_bad) atomicOr(a.err, 256u);
@@ -200,13 +219,13 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
         if (s_nb[mid] < tv0) lo = mid + 1; else hi = mid;
       }
       for (uint32_t k = lo; k < K && s_nb[k] < tv0 + 1024u; ++k) {
-        const uint32_t sk = s_slot[k];
+        const uint32_t sk = s_cid[k];
         if (sk == kInf) continue;
         const uint32_t n = s_nb[k], o = n - tv0;
         const uint32_t Ln = a.lev[(size_t)own * a.pitch + n];
-        uint32_t nw[W];
+        uint32_t nw[W], ow[W];
 #pragma unroll
-        for (int w = 0; w < W; ++w) nw[w] = st[o * W + w];
+        for (int w = 0; w < W; ++w) nw[w] = ow[w] = st[o * W + w];
         if (sk != 0x100u && n == s_crep[sk]) {  // re-test the class against X
           const bool tight = Ln >= 2u && Ln < 0x7Fu && s_cx[sk] + 1u == Ln;
 #pragma unroll
@@ -221,6 +240,13 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
           }
 #pragma unroll
         for (int w = 0; w < W; ++w) st[o * W + w] = nw[w];
+        if (a.digest && n < V) {  // the digest terms below are of the unpatched words
+          uint64_t d = 0;
+#pragma unroll
+          for (int w = 0; w < W; ++w)
+            d += (nw[w] ? digest_word_key(w, nw[w]) : 0ull) - (ow[w] ? digest_word_key(w, ow[w]) : 0ull);
+          h += g.dkn[n] * d;
+        }
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -242,13 +268,10 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
         const uint64_t kn[2] = {((uint64_t)k2.y << 32) | k2.x, ((uint64_t)k2.w << 32) | k2.z};
 #pragma unroll
         for (int y = 0; y < 2; ++y) {
-          const uint32_t nd = 2 * x + y;
           uint64_t ws = 0;
 #pragma unroll
-          for (int w = 0; w < W; ++w) {
-            const uint32_t wd = st[(16u * lane + nd) * W + w];
-            if (wd) ws += digest_word_key(w, wd);
-          }
+          for (int w = 0; w < W; ++w)
+            if (word[w][2 * x + y]) ws += digest_word_key(w, word[w][2 * x + y]);
           h += kn[y] * ws;
         }
       }
@@ -281,7 +304,7 @@ hipError_t launch_nh_derive_twin(const DevGraph& g, const TwinArgs& a0, hipStrea
   if (a.n == 0) return hipSuccess;
   if (a.W == 0 || a.W > 4) return hipErrorInvalidValue;
   a.tiles = (g.V + 1023u) / 1024u;
-  if (!a.ctiles) a.ctiles = 16;
+  if (!a.ctiles) a.ctiles = a.tiles;  // one block per root: the slot setup once
   a.ctiles = std::max(1u, std::min(a.tiles, a.ctiles));
   a.chunks = (a.tiles + a.ctiles - 1) / a.ctiles;
   const dim3 grid(a.n * a.chunks);
