@@ -235,6 +235,16 @@ int ospf_leaf_derive_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n,
                          uint8_t* d_lev, uint32_t lev_pitch, const uint32_t* d_pos,
                          uint32_t* d_dist, uint32_t* d_nh, ospf_digest* d_digest, void* stream);
 
+/* Same, with d_lev_out [n] (device): the level row each root's level bytes
+ * are written to, 0xFFFFFFFF = not kept (their dist and next-hop rows are
+ * still written); NULL = d_pos[root] (ospf_leaf_derive_dev). A sweep keeps
+ * only the rows its next-hop launches read: one per twin class. */
+int ospf_leaf_derive2_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n,
+                          const uint32_t* d_groups, uint32_t n_groups,
+                          uint32_t max_root_neighbors, uint8_t* d_lev, uint32_t lev_pitch,
+                          const uint32_t* d_pos, const uint32_t* d_lev_out, uint32_t* d_dist,
+                          uint32_t* d_nh, ospf_digest* d_digest, void* stream);
+
 /* Weighted all-sources rows of leaf roots (any metric, or OSPF_HOP_COUNT; no
  * ignored links). For a root r with distinct neighbours n_k, w_k = the
  * smallest metric r advertises on an up link to n_k and D_k = the distance row

@@ -30,7 +30,7 @@ ENGINE_SYMBOLS = [
     "ospf_plan_variant", "ospf_plan", "ospf_plan_n", "ospf_spf_runs", "ospf_run_batch_dev",
     "ospf_ksp2_run", "ospf_ksp2_dev", "ospf_update_links", "ospf_update_nodes",
     "ospf_levels_dev", "ospf_nh_derive_dev", "ospf_leaf_derive_dev",
-    "ospf_nh_derive_twin_dev", "ospf_wderive_dev", "ospf_wderive_wide_dev",
+    "ospf_nh_derive_twin_dev", "ospf_leaf_derive2_dev", "ospf_wderive_dev", "ospf_wderive_wide_dev",
     "ospf_cover_prepare", "ospf_cover_dist_dev",
     "ospf_affected_roots", "ospf_repair_runs", "ospf_links_mask", "ospf_links_unmask",
     "ospf_sweep_create", "ospf_sweep_destroy", "ospf_sweep_last_error", "ospf_sweep_get_info",
@@ -160,6 +160,8 @@ def engine() -> C.CDLL:
         L.ospf_nh_derive_twin_dev.argtypes = [vp, vp, u32, u32, u32, vp, u32, vp, vp, vp, vp, vp,
                                               vp, vp, vp]
         L.ospf_leaf_derive_dev.argtypes = [vp, vp, u32, vp, u32, u32, vp, u32, vp, vp, vp, vp, vp]
+        L.ospf_leaf_derive2_dev.argtypes = [vp, vp, u32, vp, u32, u32, vp, u32, vp, vp, vp, vp,
+                                            vp, vp]
         L.ospf_wderive_dev.argtypes = [vp, vp, u32, u32, u32, vp, u64, vp, vp, vp, vp, vp]
         L.ospf_wderive_wide_dev.argtypes = [vp, vp, u32, u32, u32, vp, u64, vp, vp, vp, vp]
         L.ospf_cover_prepare.argtypes = [vp, vp]

@@ -1380,6 +1380,15 @@ int ospf_leaf_derive_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n,
                          const uint32_t* d_groups, uint32_t n_groups, uint32_t max_root_neighbors,
                          uint8_t* d_lev, uint32_t lev_pitch, const uint32_t* d_pos,
                          uint32_t* d_dist, uint32_t* d_nh, ospf_digest* d_digest, void* stream) {
+  return ospf_leaf_derive2_dev(c, d_roots, n, d_groups, n_groups, max_root_neighbors, d_lev,
+                               lev_pitch, d_pos, nullptr, d_dist, d_nh, d_digest, stream);
+}
+
+int ospf_leaf_derive2_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n,
+                          const uint32_t* d_groups, uint32_t n_groups,
+                          uint32_t max_root_neighbors, uint8_t* d_lev, uint32_t lev_pitch,
+                          const uint32_t* d_pos, const uint32_t* d_lev_out, uint32_t* d_dist,
+                          uint32_t* d_nh, ospf_digest* d_digest, void* stream) {
   if (!c) return OSPF_E_INVAL;
   if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
   if (n == 0) return OSPF_OK;
@@ -1402,6 +1411,7 @@ int ospf_leaf_derive_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n,
   a.pitch = lev_pitch;
   a.pos = d_pos;
   a.dist = d_dist;
+  a.levrow = d_lev_out;
   a.nh = d_nh;
   a.digest = d_digest;
   a.err = c->d_err;

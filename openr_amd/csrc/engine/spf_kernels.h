@@ -334,6 +334,7 @@ struct LeafArgs {
   uint32_t pitch;
   const uint32_t* pos;    // [V] row of each node in lev / dist (kInf: none)
   uint32_t* dist;         // [rows][V] (same row index as lev) or null
+  const uint32_t* levrow; // [n] level row each root's bytes go to (kInf: not kept); null: pos
   uint32_t* nh;           // [n][V] one next-hop word per node, root order
   ospf_digest* digest;    // [n] (zeroed by the caller) or null
   uint32_t* err;

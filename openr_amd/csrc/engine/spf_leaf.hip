@@ -59,7 +59,7 @@ __device__ __forceinline__ uint32_t beq7(uint32_t x, uint32_t y) {
 
 template <int KM>
 __global__ void __launch_bounds__(kBlock) leaf_derive_kernel(DevGraph g, LeafArgs a) {
-  __shared__ uint32_t s_root[kLeafMaxG], s_own[kLeafMaxG], s_use[kLeafMaxG];
+  __shared__ uint32_t s_root[kLeafMaxG], s_own[kLeafMaxG], s_use[kLeafMaxG], s_lrow[kLeafMaxG];
   __shared__ uint32_t s_rb[kLeafMaxG], s_re[kLeafMaxG];
   __shared__ uint32_t s_tab[32];
   __shared__ unsigned long long s_dr[kLeafMaxG], s_ds[kLeafMaxG], s_dh[kLeafMaxG];
@@ -74,6 +74,7 @@ __global__ void __launch_bounds__(kBlock) leaf_derive_kernel(DevGraph g, LeafArg
     const uint32_t r = a.roots[i0 + tid];
     s_root[tid] = r;
     s_own[tid] = r < V ? a.pos[r] : kInf;
+    s_lrow[tid] = a.levrow ? a.levrow[i0 + tid] : s_own[tid];
     s_use[tid] = 0u;
     s_dr[tid] = s_ds[tid] = s_dh[tid] = 0ull;
     if (r >= V) atomicOr(a.err, 64u);
@@ -215,7 +216,9 @@ __global__ void __launch_bounds__(kBlock) leaf_derive_kernel(DevGraph g, LeafArg
             wj[b] = 0u;
           }
       }
-      __builtin_nontemporal_store(Lj, reinterpret_cast<uint32_t*>(a.lev + (size_t)own * a.pitch + v0));
+      const uint32_t lrow = s_lrow[j];
+      if (lrow != kInf)
+        __builtin_nontemporal_store(Lj, reinterpret_cast<uint32_t*>(a.lev + (size_t)lrow * a.pitch + v0));
       if (v0 >= V) continue;
       uint32_t* nrow = a.nh + (size_t)(i0 + j) * V + v0;
       uint32_t* drow = a.dist ? a.dist + (size_t)own * V + v0 : nullptr;

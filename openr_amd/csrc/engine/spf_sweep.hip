@@ -504,6 +504,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     return (uint64_t)cls[a].W * cls[a].roots.size() > (uint64_t)cls[b].W * cls[b].roots.size();
   });
   std::vector<ospf_sweep::Unit> side, after;
+  bool all_leaf_rows = false;  // a class reads every neighbour's row (not twins)
   for (size_t i = 0; i < cls.size(); ++i) {
     Cls& k = cls[i];
     const uint32_t n = (uint32_t)k.roots.size(), W = k.W, cap = std::min(k.cap, 2048u);
@@ -548,6 +549,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       };
     }
     s->step_comp += u.comp;
+    if (reads_leaf && !twin) all_leaf_rows = true;
     (reads_leaf ? after : side).push_back(std::move(u));
   }
   // (B) leaves: digests after the cover roots' (owned first, then the extra)
@@ -557,6 +559,15 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     for (uint32_t j = 0; j < own_l.size(); ++j)
       own(s, own_l[j], slot + j, dist + (size_t)(nc + j) * V, lnh + (size_t)j * V, 1);
     ospf_digest* dg = s->dig_all + slot;
+    // level rows kept: every leaf's when a next-hop launch reads neighbours
+    // row by row, else only the twin classes' representatives
+    uint32_t* d_lout = nullptr;
+    if (!all_leaf_rows && !tw.cls.empty() && !getenv("OSPF_SWEEP_ALL_LEAF_ROWS")) {
+      std::vector<uint32_t> lout(nL);
+      for (uint32_t j = 0; j < nL; ++j)
+        lout[j] = tw.rep[tw.cls[need_l[j]]] == need_l[j] ? nc + j : kNone;
+      if ((rc = upload(s, &d_lout, lout))) return rc;
+    }
     ospf_sweep::Unit u;
     u.name = "leaf";
     u.kernel = "ospf_leaf_derive_dev (leaf_derive_kernel: level + dist + next-hop rows of leaf "
@@ -567,8 +578,8 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     u.W = 1;
     u.comp = (uint64_t)nL * 8ull * V;
     u.fn = [=](hipStream_t strm) {
-      return ospf_leaf_derive_dev(c, d_l, nL, d_grp, ngr, kmax, lev, pitch, d_pos, dist, lnh, dg,
-                                  strm);
+      return ospf_leaf_derive2_dev(c, d_l, nL, d_grp, ngr, kmax, lev, pitch, d_pos, d_lout, dist,
+                                   lnh, dg, strm);
     };
     s->step_comp += u.comp;
     for (auto& x : side) s->units.push_back(std::move(x));

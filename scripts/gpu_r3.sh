@@ -23,9 +23,20 @@ for st in $STEPS; do
            cat "$OUT/bench.json"; tail -3 "$OUT/bench.err";;
     benchT) timeout -k 10 600 python bench.py --topology $TOPO ${BENCH_ARGS:-} > "$OUT/bench_$TOPO.json" 2> "$OUT/bench_$TOPO.err"; rc=$?
            cat "$OUT/bench_$TOPO.json"; tail -3 "$OUT/bench_$TOPO.err";;
-    prof)  timeout -k 10 420 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- \
+    prof)  timeout -k 10 420 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
              python bench.py --steps 5 --warmup 1 --no-cpu ${PROF_ARGS:-} > "$OUT/prof_bench.json" 2> "$OUT/prof.err"; rc=$?
            tail -3 "$OUT/prof.err";;
+    csv)   timeout -k 10 420 rocprofv3 --kernel-trace --stats -d "$OUT/csv" -o run --output-format csv -- \
+             python bench.py --steps 5 --warmup 1 --no-cpu ${PROF_ARGS:-} > "$OUT/csv_bench.json" 2> "$OUT/csv.err"; rc=$?
+           tail -2 "$OUT/csv.err";;
+    pmc)   rc=0; i=0
+           for P in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY"; do
+             i=$((i+1))
+             timeout -s KILL 120 rocprofv3 --pmc $P -d "$OUT/pmc$i" -o run --output-format csv -- \
+               python bench.py --steps 1 --warmup 0 --no-cpu --iso-reps 1 ${PROF_ARGS:-} > "$OUT/pmc$i.log" 2>&1; rc=$?
+             echo "pmc pass $i rc=$rc"; [ $rc -eq 0 ] || break
+           done
+           [ $rc -eq 0 ] && python scripts/pmc_by_kernel.py "$OUT"/pmc* > "$OUT/pmc_by_kernel.json";;
     *) echo "unknown step $st"; rc=2;;
   esac
   echo "step $st rc=$rc"
