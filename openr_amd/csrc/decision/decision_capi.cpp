@@ -338,6 +338,13 @@ char* odl_route_db_text(odl_ls* h, const char* mes_nl, uint32_t n_mes, const cha
       std::stringstream es(ln.substr(t + 1));
       for (std::string x; std::getline(es, x, ',');) {
         if (x.empty()) continue;
+        // node:fwd:algo:weight[:prepend] -- a node name holding ':' or ','
+        // would shift the fields: this text ABI rejects it (the C++ API
+        // takes any name)
+        const size_t colons = (size_t)std::count(x.begin(), x.end(), ':');
+        if (colons < 3 || colons > 4)
+          throw std::invalid_argument("prefix entry needs node:fwd:algo:weight[:prepend] "
+                                      "(node names with ':' or ',' are not supported here): " + x);
         size_t pos = 0;
         odl::PrefixEntry e;
         e.node = field(x, pos, ':');
@@ -374,8 +381,17 @@ char* odl_route_db_text(odl_ls* h, const char* mes_nl, uint32_t n_mes, const cha
         os << me << "\tNONE\n";
         continue;
       }
+      // fields are tab-separated, records newline-separated: names holding
+      // either cannot be written unambiguously by this text ABI
+      auto plain = [](const std::string& f) {
+        if (f.find_first_of("\t\n") != std::string::npos)
+          throw std::invalid_argument("name with a tab or newline in the route text: " + f);
+      };
+      plain(me);
       auto put = [&](const char* kind, const std::string& key, const std::vector<odl::NextHop>& nhs) {
         for (const auto& x : nhs) {
+          plain(x.ifName);
+          plain(x.neighbor);
           os << me << '\t' << kind << '\t' << key << '\t' << x.ifName << '\t' << x.neighbor << '\t'
              << x.metric << '\t' << (int)x.op << '\t';
           for (size_t j = 0; j < x.labels.size(); ++j) os << (j ? "," : "") << x.labels[j];

@@ -34,7 +34,12 @@ int32_t SpfSolver::nodeLabel(const std::string& node) const {
 MinCostNextHops SpfSolver::nextHopsWithMetric(const std::string& me,
                                               const std::vector<std::string>& dsts,
                                               bool perDestination) {
-  const SpfResult& spf = ls_.getSpfResult(me);
+  return nextHopsWithMetric(ls_.getSpfResult(me), dsts, perDestination);
+}
+
+MinCostNextHops SpfSolver::nextHopsWithMetric(const SpfResult& spf,
+                                              const std::vector<std::string>& dsts,
+                                              bool perDestination) {
   // the closest destinations (:1062-1077)
   MinCostNextHops out;
   out.shortest = std::numeric_limits<Metric>::max();
@@ -52,8 +57,8 @@ MinCostNextHops SpfSolver::nextHopsWithMetric(const std::string& me,
   // their next-hop neighbours with the remaining distance (:1079-1086)
   for (const auto& d : closest)
     for (const auto& nh : spf.at(d).nextHops())
-      out.viaNode[{nh, perDestination ? d : std::string()}] =
-          out.shortest - *ls_.getMetricFromAToB(me, nh);
+      // getMetricFromAToB(me, nh): nh is a reached neighbour of me
+      out.viaNode[{nh, perDestination ? d : std::string()}] = out.shortest - spf.at(nh).metric();
   return out;
 }
 
@@ -127,8 +132,13 @@ std::vector<NextHop> SpfSolver::ecmpRoute(const std::string& me,
 }
 
 std::vector<NextHop> SpfSolver::nodeLabelRoute(const std::string& me, const std::string& dst) {
+  return nodeLabelRoute(me, dst, ls_.getSpfResult(me));
+}
+
+std::vector<NextHop> SpfSolver::nodeLabelRoute(const std::string& me, const std::string& dst,
+                                               const SpfResult& mine) {
   if (dst == me) return {};  // POP_AND_LOOKUP, not an SPF product
-  auto m = nextHopsWithMetric(me, {dst}, false);
+  auto m = nextHopsWithMetric(mine, {dst}, false);
   if (m.viaNode.empty()) return {};
   return nextHopsThrift(me, {dst}, false, m, nodeLabel(dst), {}, nullptr);
 }
@@ -190,8 +200,12 @@ std::vector<NextHop> SpfSolver::ksp2Paths(const std::string& me,
 
 std::optional<UnicastRoute> SpfSolver::prefixRoute(const std::string& me, const PrefixRoute& pr,
                                                    const RouteOptions& opt) {
+  return prefixRoute(me, pr, opt, ls_.getSpfResult(me));
+}
+
+std::optional<UnicastRoute> SpfSolver::prefixRoute(const std::string& me, const PrefixRoute& pr,
+                                                   const RouteOptions& opt, const SpfResult& mine) {
   // entries of reachable announcers only (:225-253)
-  const SpfResult& mine = ls_.getSpfResult(me);
   std::map<std::string, const PrefixEntry*> entries;
   for (const auto& e : pr.entries)
     if (mine.count(e.node)) entries.emplace(e.node, &e);
@@ -225,7 +239,7 @@ std::optional<UnicastRoute> SpfSolver::prefixRoute(const std::string& me, const 
     std::vector<std::string> filtered = best;
     if (hasMe && perDestination && entries.at(me)->prependLabel)
       filtered.erase(std::find(filtered.begin(), filtered.end(), me));
-    const MinCostNextHops m = nextHopsWithMetric(me, filtered, perDestination);
+    const MinCostNextHops m = nextHopsWithMetric(mine, filtered, perDestination);
     shortest = m.shortest;
     if (!m.viaNode.empty()) {
       // getNodeUcmpResult (:1091-1161): weights of the best announcers at the
@@ -269,7 +283,9 @@ std::optional<RouteDb> SpfSolver::buildRouteDb(const std::string& me,
   // The SP prefixes read only the memoised SPF of `me` (and const link
   // state): they are built on host threads. A prefix with a KSP2 entry runs
   // getKthPaths, which fills a memo, so those are built on this thread.
-  ls_.getSpfResult(me);
+  // `mine` is looked up (and memoised) here, on the calling thread; the
+  // host threads below only read it
+  const SpfResult& mine = ls_.getSpfResult(me);
   std::vector<std::optional<UnicastRoute>> routes(prefixes.size());
   std::vector<uint32_t> sp, ksp;
   for (uint32_t i = 0; i < prefixes.size(); ++i) {
@@ -278,7 +294,7 @@ std::optional<RouteDb> SpfSolver::buildRouteDb(const std::string& me,
     (k ? ksp : sp).push_back(i);
   }
   parallelFor((uint32_t)sp.size(), [&](uint32_t lo, uint32_t hi) {
-    for (uint32_t j = lo; j < hi; ++j) routes[sp[j]] = prefixRoute(me, prefixes[sp[j]], opt);
+    for (uint32_t j = lo; j < hi; ++j) routes[sp[j]] = prefixRoute(me, prefixes[sp[j]], opt, mine);
   }, 256);
   for (const uint32_t i : ksp) routes[i] = prefixRoute(me, prefixes[i], opt);
   for (uint32_t i = 0; i < prefixes.size(); ++i) {
@@ -300,7 +316,7 @@ std::optional<RouteDb> SpfSolver::buildRouteDb(const std::string& me,
       for (uint32_t j = lo; j < hi; ++j) {
         const int32_t top = dbs.at(names[j]).nodeLabel;
         if (top != 0 && isMplsLabelValid(top) && names[j] != me)
-          cand[j] = nodeLabelRoute(me, names[j]);
+          cand[j] = nodeLabelRoute(me, names[j], mine);
       }
     }, 256);
     std::map<int32_t, std::pair<std::string, std::vector<NextHop>>> labelToNode;

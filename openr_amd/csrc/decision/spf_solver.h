@@ -98,16 +98,26 @@ class SpfSolver {
   // getNextHopsWithMetric (SpfSolver.cpp:1043-1089)
   MinCostNextHops nextHopsWithMetric(const std::string& me, const std::vector<std::string>& dsts,
                                      bool perDestination);
+  // the same over `me`'s SPF result, read-only (safe on the route build's
+  // host threads: no memo lookup, no insertion)
+  static MinCostNextHops nextHopsWithMetric(const SpfResult& mine,
+                                            const std::vector<std::string>& dsts,
+                                            bool perDestination);
   // SP_ECMP unicast route from single-node IP announcers (empty: no route)
   std::vector<NextHop> ecmpRoute(const std::string& me, const std::vector<std::string>& announcers);
   // MPLS node-label route towards `dst` with its node label (PHP / SWAP)
   std::vector<NextHop> nodeLabelRoute(const std::string& me, const std::string& dst);
+  std::vector<NextHop> nodeLabelRoute(const std::string& me, const std::string& dst,
+                                      const SpfResult& mine);
   // KSP2_ED_ECMP route (SR-MPLS label stacks) over `announcers` (entries
   // without prepend labels)
   std::vector<NextHop> ksp2Route(const std::string& me, const std::vector<std::string>& announcers);
   // createRouteForPrefix (SpfSolver.cpp:197-458), one area, non-BGP
   std::optional<UnicastRoute> prefixRoute(const std::string& me, const PrefixRoute& pr,
                                           const RouteOptions& opt);
+  // over `me`'s SPF result (`mine`): what buildRouteDb runs on host threads
+  std::optional<UnicastRoute> prefixRoute(const std::string& me, const PrefixRoute& pr,
+                                          const RouteOptions& opt, const SpfResult& mine);
   // SpfSolver::buildRouteDb (SpfSolver.cpp:460-646), one area: unicast routes
   // of `prefixes`, MPLS node-label routes of every node (POP_AND_LOOKUP for
   // our own label, PHP / SWAP towards the others, :501-598) and

@@ -1139,6 +1139,7 @@ int ospf_sync(ospf_ctx* c, void* stream) {
                 : (err & 64u) ? "a device root id is out of range"
                 : (err & 128u) ? "leaf derive: a group's roots do not share their slot table"
                 : (err & 256u) ? "twin derive: a root's neighbours span more than 16 twin classes"
+                : (err & 512u) ? "wderive: a metric above 65534 in a > 4-word next-hop derivation"
                              : "internal: a frontier entry out of range");
   }
   return OSPF_OK;

@@ -490,7 +490,10 @@ __global__ void __launch_bounds__(256) wderive_lanes_kernel(DevGraph g, WDeriveA
       if ((cx & kDown) || cx == r) continue;
       const uint32_t k = g.didx[e];
       if (k >= s_K[j]) continue;
-      const uint32_t w = a.hop ? 1u : min(g.w[e], 0xFFFEu);  // metrics <= 65534 (host check)
+      // u16 slot table: a metric above 65534 cannot be represented, and is
+      // reported (error bit 512) rather than clamped silently
+      if (!a.hop && g.w[e] > 0xFFFEu) atomicOr(a.err, 512u);
+      const uint32_t w = a.hop ? 1u : min(g.w[e], 0xFFFEu);
       // 16-bit min through the aligned 32-bit word
       const uint32_t ix = widx(k);
       uint32_t* wp = reinterpret_cast<uint32_t*>(&s_w[j][ix & ~1u]);
