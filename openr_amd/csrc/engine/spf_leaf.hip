@@ -139,16 +139,27 @@ __global__ void __launch_bounds__(kBlock) leaf_derive_kernel(DevGraph g, LeafArg
   uint32_t br = 0;
   uint64_t bs = 0, bh = 0;
   const uint32_t t0 = ci * a.ctiles, t1 = min(a.tiles, t0 + a.ctiles);
-  for (uint32_t t = t0; t < t1; ++t) {
+  // the neighbour words of the next tile are loaded before this tile's
+  // stores are issued (one tile of loads in flight per wave)
+  auto load_x = [&](uint32_t t, uint32_t* x) {
     const uint32_t v0 = t * 1024u + wave * 256u + 4u * lane;
-    if (v0 >= a.pitch) continue;
-    uint32_t x[KM];
+    const bool ok = t < t1 && v0 < a.pitch;
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
-      const bool rowk = tab[k] < 0x80000000u;
+      const bool rowk = ok && tab[k] < 0x80000000u;
       x[k] = rowk ? *reinterpret_cast<const uint32_t*>(a.lev + (size_t)tab[k] * a.pitch + v0)
                   : kNoRow;
     }
+  };
+  uint32_t xn[KM];
+  load_x(t0, xn);
+  for (uint32_t t = t0; t < t1; ++t) {
+    const uint32_t v0 = t * 1024u + wave * 256u + 4u * lane;
+    uint32_t x[KM];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) x[k] = xn[k];
+    load_x(t + 1, xn);
+    if (v0 >= a.pitch) continue;
     uint32_t m = kNoRow;
 #pragma unroll
     for (int k = 0; k < KM; ++k) m = bmin7(m, x[k]);

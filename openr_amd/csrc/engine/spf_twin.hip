@@ -158,11 +158,28 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
   const uint32_t t0 = ci * a.ctiles, t1 = min(a.tiles, t0 + a.ctiles);
   uint32_t* st = s_stage + wave * 1024u * W;
   uint64_t h = 0;
+  // the own and class rows of the wave's next tile are loaded before this
+  // tile is computed and stored (up to 1 + 3 classes prefetched)
+  constexpr uint32_t kPre = 3;
+  auto load_t = [&](uint32_t t, uint4& L, uint4* R) {
+    const uint32_t vl = t * 1024u + 16u * lane;
+    const uint32_t vs = (t < t1 && vl < a.pitch) ? vl : 0u;
+    L = *reinterpret_cast<const uint4*>(a.lev + (size_t)own * a.pitch + vs);
+#pragma unroll
+    for (uint32_t j = 0; j < kPre; ++j)
+      if (j < nc) R[j] = *reinterpret_cast<const uint4*>(a.lev + (size_t)s_crow[j] * a.pitch + vs);
+  };
+  uint4 Ln, Rn[kPre];
+  load_t(t0 + wave, Ln, Rn);
   for (uint32_t t = t0 + wave; t < t1; t += kWaves) {
     const uint32_t tv0 = t * 1024u, vl = tv0 + 16u * lane;
     const bool live = vl < a.pitch;
     const uint32_t vs = live ? vl : 0u;
-    const uint4 L = *reinterpret_cast<const uint4*>(a.lev + (size_t)own * a.pitch + vs);
+    const uint4 L = Ln;
+    uint4 Rp[kPre];
+#pragma unroll
+    for (uint32_t j = 0; j < kPre; ++j) Rp[j] = Rn[j];
+    load_t(t + kWaves, Ln, Rn);
     uint32_t lm1[4];
     {
       const uint32_t Lw[4] = {L.x, L.y, L.z, L.w};
@@ -183,7 +200,14 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
 #pragma unroll
       for (int n = 0; n < 16; ++n) word[w][n] = 0u;
     for (uint32_t j = 0; j < nc; ++j) {
-      const uint4 R = *reinterpret_cast<const uint4*>(a.lev + (size_t)s_crow[j] * a.pitch + vs);
+      uint4 R;
+      if (j < kPre) {
+#pragma unroll
+        for (uint32_t q = 0; q < kPre; ++q)
+          if (q == j) R = Rp[q];
+      } else {
+        R = *reinterpret_cast<const uint4*>(a.lev + (size_t)s_crow[j] * a.pitch + vs);
+      }
       const uint32_t Rw[4] = {R.x, R.y, R.z, R.w};
       uint32_t cm[W];
 #pragma unroll
