@@ -397,42 +397,6 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   std::vector<uint32_t> extra_l;
   for (uint32_t v : nb_c)
     if (leaf[v] && !in_l[v]) extra_l.push_back(v);
-  std::vector<uint32_t> grp = leaf_groups(c, f, own_l);
-  std::vector<uint32_t> grp_x = leaf_groups(c, f, extra_l);
-  std::vector<uint32_t> need_l = own_l;
-  need_l.insert(need_l.end(), extra_l.begin(), extra_l.end());
-  for (size_t i = 1; i < grp_x.size(); ++i) grp.push_back((uint32_t)own_l.size() + grp_x[i]);
-  const uint32_t nL = (uint32_t)need_l.size(), ngr = (uint32_t)grp.size() - 1;
-  // cover rows: own cover roots + every non-leaf neighbour of a needed root
-  std::vector<uint8_t> in_a(V, 0);
-  for (uint32_t v : own_c) in_a[v] = 1;
-  for (uint32_t v : closure(f, need_l))
-    if (!leaf[v]) in_a[v] = 1;
-  for (uint32_t v : nb_c)
-    if (!leaf[v]) in_a[v] = 1;
-  std::vector<uint32_t> clo;
-  for (uint32_t v = 0; v < V; ++v)
-    if (in_a[v]) clo.push_back(v);
-  locality_order(clo, [&](uint32_t v) { return f.first(v); });
-  const uint32_t nc = (uint32_t)clo.size();
-  std::vector<uint32_t> pos(V, kNone);
-  for (uint32_t i = 0; i < nc; ++i) pos[clo[i]] = i;
-  for (uint32_t i = 0; i < nL; ++i) pos[need_l[i]] = nc + i;
-  const uint32_t pitch = (V + 15) / 16 * 16;
-  const uint32_t rows = nc + nL;
-  uint32_t *d_clo = nullptr, *d_pos, *dist, *d_l = nullptr, *d_grp = nullptr, *lnh = nullptr;
-  uint8_t* lev;
-  ospf_digest* ldg;
-  int rc;
-  if ((rc = upload(s, &d_pos, pos)) || (rc = dalloc(s, &lev, (size_t)rows * pitch)) ||
-      (rc = dalloc(s, &dist, (size_t)rows * V)) || (rc = dalloc(s, &ldg, std::max(1u, nc))))
-    return rc;
-  if (nc && (rc = upload(s, &d_clo, clo))) return rc;
-  if (nL && ((rc = upload(s, &d_l, need_l)) || (rc = upload(s, &d_grp, grp)) ||
-             (rc = dalloc(s, &lnh, (size_t)nL * V))))
-    return rc;
-  s->dig_aux.push_back({ldg, std::max(1u, nc)});
-  s->n_rows = rows;
   // cover classes by capacity, roots by largest neighbour
   std::vector<uint32_t> caps;
   for (uint32_t r : own_c) caps.push_back(f.cap(r));
@@ -441,25 +405,26 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   struct Cls {
     uint32_t cap, W;
     std::vector<uint32_t> roots;
+    bool twin = false, reads_leaf = false;
   };
   std::vector<Cls> cls;
-  uint32_t ndig = (uint32_t)own_c.size() + nL;
   for (uint32_t cap : caps) {
     Cls k{cap, cap > 16 ? cap / 32 : 1u, {}};
     for (uint32_t r : own_c)
       if (f.cap(r) == cap) k.roots.push_back(r);
     locality_order(k.roots, [&](uint32_t v) { return f.last(v); });
+    for (uint32_t r : k.roots)
+      for (uint32_t q = (*f.dn_off)[r]; q < (*f.dn_off)[r + 1] && !k.reads_leaf; ++q)
+        k.reads_leaf = leaf[(*f.dn)[q]] != 0;
     cls.push_back(std::move(k));
   }
-  if ((rc = dalloc(s, &s->dig_all, ndig))) return rc;
-  s->n_dig = ndig;
-  const int ev_a = new_event(s), ev_b = new_event(s);  // levels done, leaves done
   // twin classes: a class of <= 4-word roots whose usable transit
   // neighbours span few classes reads one row per class (spf_twin.hip)
   Twins tw;
-  uint32_t *d_tcls = nullptr, *d_trep = nullptr, *d_tsec = nullptr;
+  bool any_w4 = false;
+  for (auto& k : cls) any_w4 |= k.W <= 4;
+  if (any_w4 && !getenv("OSPF_SWEEP_NOTWIN")) tw = twin_classes(c);
   auto twin_ok = [&](const std::vector<uint32_t>& roots) {
-    if (getenv("OSPF_SWEEP_NOTWIN")) return false;
     uint64_t slots = 0, classes = 0;
     for (uint32_t r : roots) {
       std::vector<uint32_t> cs;
@@ -477,10 +442,71 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     // worth it when a class covers several slots (OSPF_SWEEP_TWIN=1: always)
     return getenv("OSPF_SWEEP_TWIN") || slots >= 3 * std::max<uint64_t>(1, classes);
   };
-  bool any_w4 = false;
-  for (auto& k : cls) any_w4 |= k.W <= 4;
-  if (any_w4 && !getenv("OSPF_SWEEP_NOTWIN")) tw = twin_classes(c);
-  if (ev_a < 0 || ev_b < 0) return ev_a < 0 ? ev_a : ev_b;
+  bool all_leaf_rows = false;  // a class reads every neighbour's row (not twins)
+  for (auto& k : cls) {
+    k.twin = k.W <= 4 && !tw.cls.empty() && twin_ok(k.roots);
+    if (k.reads_leaf && !k.twin) all_leaf_rows = true;
+  }
+  all_leaf_rows |= tw.cls.empty() || getenv("OSPF_SWEEP_ALL_LEAF_ROWS") != nullptr;
+  // leaves: when only twin representatives' level rows are read, the
+  // representatives go first in a launch of their own, so the next hops of
+  // the cover roots start while the other leaves' rows are written
+  std::vector<uint32_t> reps, rest;
+  for (const auto* L : {&own_l, &extra_l})
+    for (uint32_t x : *L) ((!all_leaf_rows && tw.rep[tw.cls[x]] == x) ? reps : rest).push_back(x);
+  std::vector<uint32_t> grp_r = leaf_groups(c, f, reps);
+  std::vector<uint32_t> grp = leaf_groups(c, f, rest);
+  std::vector<uint32_t> need_l = reps;
+  need_l.insert(need_l.end(), rest.begin(), rest.end());
+  const uint32_t nR = (uint32_t)reps.size(), nL = (uint32_t)need_l.size();
+  // cover rows: own cover roots + every non-leaf neighbour of a needed root
+  std::vector<uint8_t> in_a(V, 0);
+  for (uint32_t v : own_c) in_a[v] = 1;
+  for (uint32_t v : closure(f, need_l))
+    if (!leaf[v]) in_a[v] = 1;
+  for (uint32_t v : nb_c)
+    if (!leaf[v]) in_a[v] = 1;
+  std::vector<uint32_t> clo;
+  for (uint32_t v = 0; v < V; ++v)
+    if (in_a[v]) clo.push_back(v);
+  locality_order(clo, [&](uint32_t v) { return f.first(v); });
+  const uint32_t nc = (uint32_t)clo.size();
+  std::vector<uint32_t> pos(V, kNone);
+  for (uint32_t i = 0; i < nc; ++i) pos[clo[i]] = i;
+  for (uint32_t i = 0; i < nL; ++i) pos[need_l[i]] = nc + i;
+  const uint32_t pitch = (V + 15) / 16 * 16;
+  const uint32_t rows = nc + nL;
+  uint32_t *d_clo = nullptr, *d_pos, *dist, *d_l = nullptr, *lnh = nullptr;
+  uint32_t *d_grp_r = nullptr, *d_grp = nullptr, *d_lout = nullptr;
+  uint8_t* lev;
+  ospf_digest* ldg;
+  int rc;
+  if ((rc = upload(s, &d_pos, pos)) || (rc = dalloc(s, &lev, (size_t)rows * pitch)) ||
+      (rc = dalloc(s, &dist, (size_t)rows * V)) || (rc = dalloc(s, &ldg, std::max(1u, nc))))
+    return rc;
+  if (nc && (rc = upload(s, &d_clo, clo))) return rc;
+  if (nL && ((rc = upload(s, &d_l, need_l)) || (rc = dalloc(s, &lnh, (size_t)nL * V))))
+    return rc;
+  if (nR && (rc = upload(s, &d_grp_r, grp_r))) return rc;
+  if (nL > nR && (rc = upload(s, &d_grp, grp))) return rc;
+  if (!all_leaf_rows && nL > nR) {  // the other leaves' level bytes are not kept
+    std::vector<uint32_t> lout(nL - nR, kNone);
+    if ((rc = upload(s, &d_lout, lout))) return rc;
+  }
+  uint32_t *d_tcls = nullptr, *d_trep = nullptr, *d_tsec = nullptr;
+  bool any_twin = false;
+  for (auto& k : cls) any_twin |= k.twin;
+  if (any_twin && ((rc = upload(s, &d_tcls, tw.cls)) || (rc = upload(s, &d_trep, tw.rep)) ||
+                   (rc = upload(s, &d_tsec, tw.sec))))
+    return rc;
+  s->dig_aux.push_back({ldg, std::max(1u, nc)});
+  s->n_rows = rows;
+  const uint32_t ndig = (uint32_t)own_c.size() + nL;
+  if ((rc = dalloc(s, &s->dig_all, ndig))) return rc;
+  s->n_dig = ndig;
+  // events: levels done, representative leaves done, every leaf done
+  const int ev_a = new_event(s), ev_r = new_event(s), ev_b = new_event(s);
+  if (ev_a < 0 || ev_r < 0 || ev_b < 0) return ev_a < 0 ? ev_a : ev_r < 0 ? ev_r : ev_b;
   if (nc) {
     ospf_sweep::Unit lv;
     lv.name = "levels";
@@ -496,7 +522,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     s->step_comp += lv.comp;
     s->units.push_back(lv);
   }
-  // (C) cover classes: slots 0 .. |own_c| of the digests
+  // (C) cover classes: digest slots 0 .. |own_c|
   uint32_t slot = 0;
   std::vector<size_t> order(cls.size());
   std::iota(order.begin(), order.end(), 0);
@@ -504,7 +530,6 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     return (uint64_t)cls[a].W * cls[a].roots.size() > (uint64_t)cls[b].W * cls[b].roots.size();
   });
   std::vector<ospf_sweep::Unit> side, after;
-  bool all_leaf_rows = false;  // a class reads every neighbour's row (not twins)
   for (size_t i = 0; i < cls.size(); ++i) {
     Cls& k = cls[i];
     const uint32_t n = (uint32_t)k.roots.size(), W = k.W, cap = std::min(k.cap, 2048u);
@@ -514,30 +539,21 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     for (uint32_t j = 0; j < n; ++j)
       own(s, k.roots[j], slot + j, dist + (size_t)pos[k.roots[j]] * V, nh + (size_t)j * V * W, W);
     slot += n;
-    bool reads_leaf = false;
-    for (uint32_t r : k.roots)
-      for (uint32_t q = (*f.dn_off)[r]; q < (*f.dn_off)[r + 1] && !reads_leaf; ++q)
-        reads_leaf = leaf[(*f.dn)[q]] != 0;
     ospf_sweep::Unit u;
     u.name = "derive_cap" + std::to_string(k.cap);
-    const bool twin = W <= 4 && !tw.cls.empty() && twin_ok(k.roots);
-    if (twin && !d_tcls) {
-      if ((rc = upload(s, &d_tcls, tw.cls)) || (rc = upload(s, &d_trep, tw.rep)) ||
-          (rc = upload(s, &d_tsec, tw.sec)))
-        return rc;
-    }
-    u.kernel = std::string(twin ? "ospf_nh_derive_twin_dev (" : "ospf_nh_derive_dev (") +
-               (twin ? "nh_derive_twin_kernel" : W <= 4 ? "nh_derive16_kernel"
-                                                        : "nh_derive_wide_kernel") +
+    u.kernel = std::string(k.twin ? "ospf_nh_derive_twin_dev (" : "ospf_nh_derive_dev (") +
+               (k.twin ? "nh_derive_twin_kernel" : W <= 4 ? "nh_derive16_kernel"
+                                                          : "nh_derive_wide_kernel") +
                ", " + std::to_string(W) + " next-hop word" + (W > 1 ? "s)" : ")");
     const int st = new_stream(s);
     if (st < 0) return st;
     u.stream = st;
-    u.wait = {reads_leaf ? ev_b : ev_a};
+    // twin classes read only the representatives' rows; others every row
+    u.wait = {!k.reads_leaf ? ev_a : k.twin ? ev_r : ev_b};
     u.n_roots = n;
     u.W = W;
     u.comp = (uint64_t)n * 4ull * V * W;
-    if (twin) {
+    if (k.twin) {
       const uint32_t *tc = d_tcls, *tr = d_trep, *ts = d_tsec;
       u.fn = [=](hipStream_t strm) {
         return ospf_nh_derive_twin_dev(c, d_roots, n, W, cap, lev, pitch, d_pos, ldg, tc, tr, ts,
@@ -549,43 +565,70 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       };
     }
     s->step_comp += u.comp;
-    if (reads_leaf && !twin) all_leaf_rows = true;
-    (reads_leaf ? after : side).push_back(std::move(u));
+    (k.reads_leaf ? after : side).push_back(std::move(u));
   }
-  // (B) leaves: digests after the cover roots' (owned first, then the extra)
+  for (auto& x : side) s->units.push_back(std::move(x));
+  // (B) leaves: digest slots after the cover roots'; representatives first
   if (nL) {
     uint32_t kmax = 1;
     for (uint32_t r : need_l) kmax = std::max(kmax, f.nbrs(r));
-    for (uint32_t j = 0; j < own_l.size(); ++j)
-      own(s, own_l[j], slot + j, dist + (size_t)(nc + j) * V, lnh + (size_t)j * V, 1);
+    for (uint32_t j = 0; j < nL; ++j)
+      if (in_l[need_l[j]])
+        own(s, need_l[j], slot + j, dist + (size_t)(nc + j) * V, lnh + (size_t)j * V, 1);
     ospf_digest* dg = s->dig_all + slot;
-    // level rows kept: every leaf's when a next-hop launch reads neighbours
-    // row by row, else only the twin classes' representatives
-    uint32_t* d_lout = nullptr;
-    if (!all_leaf_rows && !tw.cls.empty() && !getenv("OSPF_SWEEP_ALL_LEAF_ROWS")) {
-      std::vector<uint32_t> lout(nL);
-      for (uint32_t j = 0; j < nL; ++j)
-        lout[j] = tw.rep[tw.cls[need_l[j]]] == need_l[j] ? nc + j : kNone;
-      if ((rc = upload(s, &d_lout, lout))) return rc;
+    const uint32_t ngr_r = nR ? (uint32_t)grp_r.size() - 1 : 0u;
+    const uint32_t ngr = nL > nR ? (uint32_t)grp.size() - 1 : 0u;
+    if (nR) {
+      ospf_sweep::Unit u;
+      u.name = "leaf_reps";
+      u.kernel = "ospf_leaf_derive2_dev (leaf_derive_kernel: twin representatives' level + dist "
+                 "+ next-hop rows)";
+      u.stream = 0;
+      u.record = ev_r;
+      u.n_roots = nR;
+      u.W = 1;
+      u.comp = (uint64_t)nR * 8ull * V;
+      u.fn = [=](hipStream_t strm) {
+        return ospf_leaf_derive2_dev(c, d_l, nR, d_grp_r, ngr_r, kmax, lev, pitch, d_pos, nullptr,
+                                     dist, lnh, dg, strm);
+      };
+      s->step_comp += u.comp;
+      s->units.push_back(std::move(u));
     }
-    ospf_sweep::Unit u;
-    u.name = "leaf";
-    u.kernel = "ospf_leaf_derive_dev (leaf_derive_kernel: level + dist + next-hop rows of leaf "
-               "roots from their neighbours' level rows)";
-    u.stream = 0;
-    u.record = ev_b;
-    u.n_roots = nL;
-    u.W = 1;
-    u.comp = (uint64_t)nL * 8ull * V;
-    u.fn = [=](hipStream_t strm) {
-      return ospf_leaf_derive2_dev(c, d_l, nL, d_grp, ngr, kmax, lev, pitch, d_pos, d_lout, dist,
-                                   lnh, dg, strm);
-    };
-    s->step_comp += u.comp;
-    for (auto& x : side) s->units.push_back(std::move(x));
-    s->units.push_back(std::move(u));
-  } else {  // no leaf rows: no class waits for them
-    for (auto& x : side) s->units.push_back(std::move(x));
+    if (nL > nR) {
+      ospf_sweep::Unit u;
+      u.name = "leaf";
+      u.kernel = "ospf_leaf_derive2_dev (leaf_derive_kernel: level + dist + next-hop rows of leaf "
+                 "roots from their neighbours' level rows)";
+      const uint32_t n = nL - nR;
+      if (nR) {  // beside the cover roots' next hops, on a stream of its own
+        const int st = new_stream(s);
+        if (st < 0) return st;
+        u.stream = st;
+        u.wait = {ev_a};
+      } else {
+        u.stream = 0;
+      }
+      u.record = ev_b;
+      u.n_roots = n;
+      u.W = 1;
+      u.comp = (uint64_t)n * 8ull * V;
+      const uint32_t* dl = d_l + nR;
+      uint32_t* nh = lnh + (size_t)nR * V;
+      ospf_digest* dg2 = dg + nR;
+      const uint32_t* lo = d_lout;
+      u.fn = [=](hipStream_t strm) {
+        return ospf_leaf_derive2_dev(c, dl, n, d_grp, ngr, kmax, lev, pitch, d_pos, lo, dist, nh,
+                                     dg2, strm);
+      };
+      s->step_comp += u.comp;
+      s->units.push_back(std::move(u));
+    }
+  }
+  if (nR && nL == nR) {  // every leaf is a representative: ev_b = ev_r
+    for (auto& u : after)
+      for (int& e : u.wait)
+        if (e == ev_b) e = ev_r;
   }
   for (auto& x : after) s->units.push_back(std::move(x));
   return OSPF_OK;
