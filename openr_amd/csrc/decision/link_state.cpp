@@ -289,9 +289,24 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db) 
     if (ch.topologyChanged) applyIncremental(deltas, nodeDeltas);
     return ch;
   }
-  // Memo survives non-topology updates exactly as in the reference
-  // (LinkState.cpp:721-724); the CSR is re-snapshotted on any update because
-  // node ids (name ranks) may have changed.
+  // The same nodes and links: the snapshot stays (node ids are name ranks,
+  // unchanged). Metric / up / overload changes are patched into the CSR and
+  // the device graph in place; the memo is dropped on a topology change,
+  // exactly as in the reference (LinkState.cpp:751-754), and survives
+  // attribute-only updates (:721-724: labels, weights).
+  if (!structural && snapVersion_ == version_ && keepsContract) {
+    distBound_ = bound;
+    if (ch.topologyChanged) {
+      memoMetric_.clear();
+      memoHops_.clear();
+      rawMetric_.clear();
+      memoKsp_.clear();
+    }
+    if (!deltas.empty() || !nodeDeltas.empty()) patchGraph(deltas, nodeDeltas);
+    return ch;
+  }
+  // a link or node added / removed (node ids may move), or a metric leaving
+  // the engine contract: the CSR is snapshotted again
   if (ch.topologyChanged) {
     invalidate();
   } else {
@@ -1062,7 +1077,13 @@ void LinkState::applyIncremental(const std::vector<LinkDelta>& links,
     }
   }
   memoKsp_.clear();  // KSP2 masked reruns are not tracked
-  // CSR + device graph, in place (same ids, same links)
+  patchGraph(links, nodes);
+}
+
+// The CSR and the device graph, patched in place (same node ids, same
+// links): metrics, up state, overload bits.
+void LinkState::patchGraph(const std::vector<LinkDelta>& links,
+                           const std::vector<std::string>& nodes) {
   std::vector<ospf_link_update> ups;
   for (const auto& d : links) {
     const Link& l = *d.link;

@@ -347,6 +347,7 @@ class LinkState {
   };
   void applyIncremental(const std::vector<LinkDelta>& links,
                         const std::vector<std::string>& nodes);
+  void patchGraph(const std::vector<LinkDelta>& links, const std::vector<std::string>& nodes);
 
   std::string area_;
   int device_;

@@ -163,6 +163,42 @@ def test_incremental_updates_keep_parity():
     assert p.spf_runs == o.spf_runs
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_default_mode_events_patch_in_place(seed):
+    """Default (non-incremental) mode: metric, link up / down and overload
+    events on the same nodes and links are patched into the CSR and the
+    device graph in place (no re-snapshot), the memo is still
+    dropped on every topology change and kept on label-only updates
+    (LinkState.cpp:721-724, 751-754): link-metric and hop-count results,
+    KSP2 paths and decision.spf_runs equal the oracle's after every event."""
+    st, names = random_stream(700 + seed, n=36)
+    o, p = both(st)
+    rng = np.random.default_rng(seed)
+    dbs = st.to_dbs()
+    for step in range(12):
+        db = dbs[int(rng.integers(len(dbs)))]
+        kind = step % 4
+        if kind == 0:
+            db.overloaded = not db.overloaded
+        elif kind == 1 and db.adjs:
+            a = db.adjs[int(rng.integers(len(db.adjs)))]
+            a.metric = int(rng.integers(1, 40))
+        elif kind == 2 and db.adjs:
+            a = db.adjs[int(rng.integers(len(db.adjs)))]
+            a.overloaded = not a.overloaded
+        else:
+            db.node_label += 7
+        upd = AdjDbStream.from_dbs([db])
+        assert o.apply(upd) == p.apply(upd)
+        for r in names[:6]:
+            assert p.spf_text(r) == o.spf_text(r), (step, r)
+            assert p.spf_text(r, False) == o.spf_text(r, False), (step, r)
+        a_, b_ = names[int(rng.integers(len(names)))], names[int(rng.integers(len(names)))]
+        for k in (1, 2):
+            assert p.kth_paths(a_, b_, k) == o.kth_paths(a_, b_, k), (step, a_, b_, k)
+        assert p.spf_runs == o.spf_runs, step
+
+
 def test_grid31_all_sources_digests():
     st = T.grid(31)
     o, p = both(st)
