@@ -37,6 +37,11 @@ __global__ void gather_digest_kernel(const ospf_digest* __restrict__ src,
   if (i < n) out[i] = src[idx[i]];
 }
 
+// Empty dispatch queued before each launch unit by ospf_sweep_profile: in a
+// rocprofv3 kernel trace or counter collection its dispatches cut the
+// profile phase into units (scripts/sweep_unit_stats.py).
+__global__ void sweep_unit_mark_kernel(uint32_t unit) { (void)unit; }
+
 __global__ void scatter_digest_kernel(const ospf_digest* __restrict__ src,
                                       const uint32_t* __restrict__ roots, uint32_t n,
                                       ospf_digest* __restrict__ out) {
@@ -1316,6 +1321,8 @@ int ospf_sweep_profile(ospf_sweep* s, uint32_t reps, ospf_sweep_launch* out, uin
     auto& u = s->units[i];
     hipStream_t st = s->streams[u.stream];
     std::vector<double> ms;
+    hipLaunchKernelGGL(sweep_unit_mark_kernel, dim3(1), dim3(64), 0, st, (uint32_t)i);
+    SCHK(s, hipGetLastError());
     for (uint32_t k = 0; k <= reps; ++k) {
       SCHK(s, hipEventRecord(a, st));
       const int rc = u.fn(st);
@@ -1337,6 +1344,9 @@ int ospf_sweep_profile(ospf_sweep* s, uint32_t reps, ospf_sweep_launch* out, uin
     L.ms_median = ms[ms.size() / 2];
     L.ms_min = ms.front();
   }
+  hipLaunchKernelGGL(sweep_unit_mark_kernel, dim3(1), dim3(64), 0, s->streams[0],
+                     (uint32_t)s->units.size());
+  SCHK(s, hipStreamSynchronize(s->streams[0]));
   hipEventDestroy(a);
   hipEventDestroy(b);
   c->spf_runs = runs0;

@@ -37,6 +37,24 @@ for st in $STEPS; do
              echo "pmc pass $i rc=$rc"; [ $rc -eq 0 ] || break
            done
            [ $rc -eq 0 ] && python scripts/pmc_by_kernel.py "$OUT"/pmc* > "$OUT/pmc_by_kernel.json";;
+    unitprof)  # per-launch-unit kernel time + HBM traffic of the sweep (scripts/sweep_unit_stats.py)
+           timeout -k 10 420 rocprofv3 --kernel-trace --stats -d "$OUT/utrace" -o run --output-format csv -- \
+             python bench.py --steps 5 --warmup 1 --no-cpu --iso-reps 3 ${PROF_ARGS:-} > "$OUT/utrace_bench.json" 2> "$OUT/utrace.err"; rc=$?
+           [ $rc -eq 0 ] && OSPF_LV_SERIAL=1 timeout -k 10 420 rocprofv3 --kernel-trace --stats -d "$OUT/utrace_serial" -o run --output-format csv -- \
+             python bench.py --steps 2 --warmup 1 --no-cpu --iso-reps 3 ${PROF_ARGS:-} > "$OUT/utrace_serial_bench.json" 2>> "$OUT/utrace.err"; rc=$?
+           i=0
+           for P in FETCH_SIZE WRITE_SIZE; do
+             [ $rc -eq 0 ] || break
+             i=$((i+1))
+             timeout -s KILL 180 rocprofv3 --pmc $P -d "$OUT/upmc$i" -o run --output-format csv -- \
+               python bench.py --steps 1 --warmup 0 --no-cpu --iso-reps 1 ${PROF_ARGS:-} > "$OUT/upmc$i.json" 2> "$OUT/upmc$i.err"; rc=$?
+             echo "pmc pass $P rc=$rc"
+           done
+           if [ $rc -eq 0 ]; then
+             python scripts/sweep_unit_stats.py --bench "$OUT/utrace_bench.json" --trace "$OUT/utrace" --reps 3 --out "$OUT/units_trace.json" &&
+             python scripts/sweep_unit_stats.py --bench "$OUT/utrace_serial_bench.json" --trace "$OUT/utrace_serial" --reps 3 --out "$OUT/units_trace_serial.json" &&
+             python scripts/sweep_unit_stats.py --bench "$OUT/upmc1.json" --pmc "$OUT/upmc1" "$OUT/upmc2" --reps 1 --out "$OUT/pmc_traffic.json"; rc=$?
+           fi;;
     *) echo "unknown step $st"; rc=2;;
   esac
   echo "step $st rc=$rc"
