@@ -166,7 +166,7 @@ def main():
                     help="profiling mode: launch only the class with this neighbour capacity "
                          "(8, 16, or 32 x next-hop words)")
     ap.add_argument("--reps", type=int, default=3, help="launches in --class-only mode")
-    ap.add_argument("--mode", choices=["auto", "derive", "wcover", "wderive", "batch", "classes"],
+    ap.add_argument("--mode", choices=["auto", "derive", "wcover", "wderive", "batch", "lds", "classes"],
                     default="auto",
                     help="all-sources sweep path (ospf_sweep_opts.mode; auto = the engine's "
                          "choice); classes = the per-class batch driver below (no sweep)")

@@ -214,6 +214,26 @@ int ospf_nh_derive_twin_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n, 
                             const uint32_t* d_twin_rep, const uint32_t* d_twin_second,
                             uint32_t* d_nh, ospf_digest* d_digest, void* stream);
 
+/* Level + dist rows from twin classes, no traversal (spf_twin.hip; unit
+ * metric or hop count, depth bound <= 123). For a root r whose usable transit
+ * neighbours fall into <= 16 twin classes (d_twin_class / d_twin_rep as for
+ * ospf_nh_derive_twin_dev), every class's representative having a level row
+ * in d_lev at d_pos: dist(r, v) = 1 + min over the classes of the
+ * representative's dist(rep, v), except 0 at r and 1 at every usable
+ * neighbour -- Bellman's equation over r's out-links (LinkState.cpp:836-911,
+ * overloaded neighbours reach only themselves, :859-866): twins' rows agree
+ * outside their members, and every member of a neighbour class is a usable
+ * neighbour of r. Writes r's level row (d_lev at d_pos[r]), its dist row
+ * (d_dist + d_pos[r] * V; NULL = not wanted) and the distance part of its
+ * digest (d_lev_digest[d_pos[r]], stored; NULL = not wanted). Error bits at
+ * ospf_sync: 1 (> 128 distinct neighbours), 16 (a class row missing), 256
+ * (> 16 classes). On a fabric the fabric switches' rows come from one rack
+ * row of their pod and one spine row of their plane. */
+int ospf_twin_levels_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n, uint8_t* d_lev,
+                         uint32_t lev_pitch, const uint32_t* d_pos, const uint32_t* d_twin_class,
+                         const uint32_t* d_twin_rep, uint32_t* d_dist, ospf_digest* d_lev_digest,
+                         void* stream);
+
 /* All-sources rows of leaf roots from level rows (unit metric or hop count;
  * spf_leaf.hip). A leaf r (no two leaves adjacent, <= 32 distinct
  * neighbours n_k) has dist(r, v) = 1 + min_k dist(n_k, v) over n_k with an
@@ -244,6 +264,24 @@ int ospf_leaf_derive2_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n,
                           uint32_t max_root_neighbors, uint8_t* d_lev, uint32_t lev_pitch,
                           const uint32_t* d_pos, const uint32_t* d_lev_out, uint32_t* d_dist,
                           uint32_t* d_nh, ospf_digest* d_digest, void* stream);
+
+/* All-sources rows of small graphs in one launch (spf_small.hip), unit
+ * metric or OSPF_HOP_COUNT: a wave per root, the padded CSR and the root's
+ * BFS state (visited bits, u16 levels, queue, next-hop words) in LDS --
+ * LinkState::runSpf (LinkState.cpp:836-911) with unit weights, next hops as
+ * :885-901 (the first hops of the shortest paths; overloaded nodes never
+ * relay, :859-866). Writes d_dist [n][V], d_nh [n][V][nh_words] and
+ * d_digest [n] (each NULL = not wanted); nh_words 1..4 must cover every
+ * root's distinct neighbours (else error bit 1 at ospf_sync). flags may
+ * carry OSPF_HOP_COUNT (the WANT bits are ignored: the buffers decide).
+ * OSPF_E_RANGE when the graph is outside the kernel's contract (V > 65535,
+ * or the CSR + one root's state does not fit in LDS): ospf_lds_sweep_fits
+ * says beforehand. Queued on `stream`. Replaces the per-node
+ * Decision::getDecisionRouteDb loop (Decision.cpp:309) for small areas. */
+int ospf_lds_sweep_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n, uint32_t flags,
+                       uint32_t nh_words, uint32_t* d_dist, uint32_t* d_nh,
+                       ospf_digest* d_digest, void* stream);
+int ospf_lds_sweep_fits(const ospf_ctx* ctx, uint32_t flags, uint32_t nh_words);
 
 /* Weighted all-sources rows of leaf roots (any metric, or OSPF_HOP_COUNT; no
  * ignored links). For a root r with distinct neighbours n_k, w_k = the
@@ -445,8 +483,12 @@ int ospf_links_unmask(ospf_ctx* ctx);
  *                      derived from them (ospf_cover_*, ospf_wderive*_dev);
  *   OSPF_SWEEP_WDERIVE cover rows on the per-root batch path, leaf rows
  *                      derived (any metric, or hop count);
- *   OSPF_SWEEP_BATCH   per width class batches (ospf_run_batch_dev).
- * OSPF_SWEEP_AUTO takes the first that applies, in that order. Row layout:
+ *   OSPF_SWEEP_BATCH   per width class batches (ospf_run_batch_dev);
+ *   OSPF_SWEEP_LDS     small graphs, unit metric or hop count, <= 4 next-hop
+ *                      words: one launch per width class, a wave per root
+ *                      with the graph in LDS (ospf_lds_sweep_dev).
+ * OSPF_SWEEP_AUTO takes LDS when it applies, then the others in the order
+ * above. Row layout:
  * dist u32[V] per root; next hops u32[V][W] with W = max(1, ceil(distinct
  * neighbours / 32)) words in the bit order of ospf_root_neighbors. A sweep
  * belongs to the graph it was created on: after ospf_load_graph,
@@ -460,6 +502,7 @@ int ospf_links_unmask(ospf_ctx* ctx);
 #define OSPF_SWEEP_WCOVER 2u
 #define OSPF_SWEEP_WDERIVE 3u
 #define OSPF_SWEEP_BATCH 4u
+#define OSPF_SWEEP_LDS 5u
 
 typedef struct ospf_sweep ospf_sweep;
 typedef struct ospf_sweep_opts {

@@ -31,6 +31,7 @@ ENGINE_SYMBOLS = [
     "ospf_ksp2_run", "ospf_ksp2_dev", "ospf_update_links", "ospf_update_nodes",
     "ospf_levels_dev", "ospf_nh_derive_dev", "ospf_leaf_derive_dev",
     "ospf_nh_derive_twin_dev", "ospf_leaf_derive2_dev", "ospf_wderive_dev", "ospf_wderive_wide_dev",
+    "ospf_lds_sweep_dev", "ospf_lds_sweep_fits", "ospf_twin_levels_dev",
     "ospf_cover_prepare", "ospf_cover_dist_dev",
     "ospf_affected_roots", "ospf_repair_runs", "ospf_links_mask", "ospf_links_unmask",
     "ospf_sweep_create", "ospf_sweep_destroy", "ospf_sweep_last_error", "ospf_sweep_get_info",
@@ -96,7 +97,7 @@ class ospf_plan_info(C.Structure):  # noqa: N801
 
 OSPF_SWEEP_AUTO, OSPF_SWEEP_DERIVE, OSPF_SWEEP_WCOVER, OSPF_SWEEP_WDERIVE, OSPF_SWEEP_BATCH = \
     0, 1, 2, 3, 4
-SWEEP_MODES = {"auto": 0, "derive": 1, "wcover": 2, "wderive": 3, "batch": 4}
+SWEEP_MODES = {"auto": 0, "derive": 1, "wcover": 2, "wderive": 3, "batch": 4, "lds": 5}
 SWEEP_MODE_NAMES = {v: k for k, v in SWEEP_MODES.items()}
 
 
@@ -160,6 +161,9 @@ def engine() -> C.CDLL:
         L.ospf_nh_derive_twin_dev.argtypes = [vp, vp, u32, u32, u32, vp, u32, vp, vp, vp, vp, vp,
                                               vp, vp, vp]
         L.ospf_leaf_derive_dev.argtypes = [vp, vp, u32, vp, u32, u32, vp, u32, vp, vp, vp, vp, vp]
+        L.ospf_lds_sweep_dev.argtypes = [vp, vp, u32, u32, u32, vp, vp, vp, vp]
+        L.ospf_lds_sweep_fits.argtypes = [vp, u32, u32]
+        L.ospf_twin_levels_dev.argtypes = [vp, vp, u32, vp, u32, vp, vp, vp, vp, vp, vp]
         L.ospf_leaf_derive2_dev.argtypes = [vp, vp, u32, vp, u32, u32, vp, u32, vp, vp, vp, vp,
                                             vp, vp]
         L.ospf_wderive_dev.argtypes = [vp, vp, u32, u32, u32, vp, u64, vp, vp, vp, vp, vp]

@@ -1375,6 +1375,43 @@ int ospf_nh_derive_twin_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, ui
   return OSPF_OK;
 }
 
+// Twin levels (spf_twin.hip): level + dist rows of roots from the
+// representative rows of their neighbours' twin classes (no traversal).
+int ospf_twin_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint8_t* d_lev,
+                         uint32_t lev_pitch, const uint32_t* d_pos, const uint32_t* d_twin_class,
+                         const uint32_t* d_twin_rep, uint32_t* d_dist, ospf_digest* d_lev_digest,
+                         void* stream) {
+  if (!c) return OSPF_E_INVAL;
+  if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  if (n == 0) return OSPF_OK;
+  if (!d_roots || !d_lev || !d_pos || !d_twin_class || !d_twin_rep)
+    return fail(c, OSPF_E_INVAL, "null argument");
+  if (lev_pitch % 16u || lev_pitch < c->info.n_nodes)
+    return fail(c, OSPF_E_INVAL, "lev_pitch: a multiple of 16 >= V");
+  if (c->depth_bound > 123) return fail(c, OSPF_E_RANGE, "level rows need a depth bound <= 123");
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(c, hipSetDevice(c->device));
+  ospf::TwinArgs a{};
+  a.roots = d_roots;
+  a.n = n;
+  a.W = 4;
+  a.cap = 128;
+  a.lev = d_lev;
+  a.lev_w = d_lev;
+  a.pitch = lev_pitch;
+  a.pos = d_pos;
+  a.tcls = d_twin_class;
+  a.trep = d_twin_rep;
+  a.tsec = nullptr;
+  a.dist = d_dist;
+  a.lev_digest_w = d_lev_digest;
+  a.err = c->d_err;
+  hipError_t e = ospf::launch_twin_levels(c->g, a, s);
+  if (e != hipSuccess) return hip_fail(c, e, "launch_twin_levels");
+  c->spf_runs += n;
+  return OSPF_OK;
+}
+
 // Leaf derive (spf_leaf.hip): level, dist and next-hop rows of leaf roots
 // from their neighbours' level rows. Unit metric or hop count.
 int ospf_leaf_derive_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n,
@@ -1419,6 +1456,53 @@ int ospf_leaf_derive2_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n,
   if (const char* e = getenv("OSPF_LEAF_CTILES")) a.ctiles = (uint32_t)std::max(1, atoi(e));
   hipError_t e = ospf::launch_leaf_derive(c->g, a, max_root_neighbors ? max_root_neighbors : 32u, s);
   if (e != hipSuccess) return hip_fail(c, e, "launch_leaf_derive");
+  c->spf_runs += n;
+  return OSPF_OK;
+}
+
+// Small-graph sweep (spf_small.hip): waves per block that fit the LDS (0 =
+// the graph does not fit, or the run is outside the kernel's contract).
+static uint32_t lds_sweep_waves(const ospf_ctx* c, uint32_t flags, uint32_t W) {
+  if (!c->loaded || W == 0 || W > 4) return 0;
+  if (!(flags & OSPF_HOP_COUNT) && !c->info.unit_metric) return 0;
+  const uint32_t V = c->info.n_nodes;
+  if (V == 0 || V > 65535u || c->h_prow.size() != (size_t)V + 1) return 0;
+  const uint32_t Ep = c->h_prow[V];
+  for (uint32_t w = 4; w >= 1; --w)
+    if (ospf::small_lds_bytes(V, Ep, W, w) <= c->lds_limit) return w;
+  return 0;
+}
+
+int ospf_lds_sweep_fits(const ospf_ctx* c, uint32_t flags, uint32_t nh_words) {
+  return c && lds_sweep_waves(c, flags, nh_words) ? 1 : 0;
+}
+
+int ospf_lds_sweep_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t flags,
+                       uint32_t nh_words, uint32_t* d_dist, uint32_t* d_nh,
+                       ospf_digest* d_digest, void* stream) {
+  if (!c) return OSPF_E_INVAL;
+  if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  if (n == 0) return OSPF_OK;
+  if (!d_roots) return fail(c, OSPF_E_INVAL, "null roots");
+  if (flags & ~(OSPF_HOP_COUNT | OSPF_WANT_DIST | OSPF_WANT_NH | OSPF_WANT_DIGEST))
+    return fail(c, OSPF_E_INVAL, "lds sweep: flags");
+  const uint32_t waves = lds_sweep_waves(c, flags, nh_words);
+  if (!waves)
+    return fail(c, OSPF_E_RANGE, "lds sweep: needs unit metric or hop count, nh_words 1..4, "
+                                 "V <= 65535 and the graph in LDS");
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(c, hipSetDevice(c->device));
+  ospf::SmallArgs a{};
+  a.roots = d_roots;
+  a.n = n;
+  a.Ep = c->h_prow[c->info.n_nodes];
+  a.waves = waves;
+  a.dist = d_dist;
+  a.nh = d_nh;
+  a.digest = d_digest;
+  a.err = c->d_err;
+  hipError_t e = ospf::launch_lds_sweep(c->g, a, nh_words, s);
+  if (e != hipSuccess) return hip_fail(c, e, "launch_lds_sweep");
   c->spf_runs += n;
   return OSPF_OK;
 }

@@ -316,8 +316,16 @@ struct TwinArgs {
   ospf_digest* digest;    // [n] (zeroed by the caller) or null
   uint32_t* err;          // + bit 256: a root with more than kTwinMaxC classes
   uint32_t tiles, ctiles, chunks;
+  // twin_levels_kernel: the roots' own rows at pos[root]
+  uint8_t* lev_w;             // level rows written (same buffer as lev)
+  uint32_t* dist;             // [rows][V] or null
+  ospf_digest* lev_digest_w;  // [rows] distance parts (stored) or null
 };
 hipError_t launch_nh_derive_twin(const DevGraph& g, const TwinArgs& a, hipStream_t s);
+// level + dist rows (+ the distance part of the digest) of roots whose usable
+// transit neighbours fall into <= kTwinMaxC twin classes, from the classes'
+// representative level rows (one block per root)
+hipError_t launch_twin_levels(const DevGraph& g, const TwinArgs& a, hipStream_t s);
 
 // Leaf derive (spf_leaf.hip), unit metric / hop count: the level, dist and
 // one-word next-hop rows of leaf roots (<= 32 distinct neighbours, every
@@ -341,6 +349,40 @@ struct LeafArgs {
   uint32_t tiles, ctiles; // 1,024-node tiles of the rows, tiles per block
 };
 hipError_t launch_leaf_derive(const DevGraph& g, const LeafArgs& a, uint32_t kmax, hipStream_t s);
+
+// Small-graph sweep (spf_small.hip), unit metric / hop count: one wave per
+// root, the padded CSR (row offsets, entries, transit bits) copied into LDS
+// once per block, each wave's BFS state in its LDS slice. LDS words: graph
+// = row offsets (V + 1, rounded to 4) + Ep entries + transit words (rounded
+// to 4); per wave = visited bits + u16 levels + u16 queue + V * W next-hop
+// words (each rounded to 4 words).
+struct SmallLayout {
+  uint32_t rp_words, nt_words, graph_words;
+  uint32_t vis_words, half_words, wave_words;
+};
+__host__ __device__ inline SmallLayout small_layout(uint32_t V, uint32_t Ep, uint32_t W) {
+  auto r4 = [](uint32_t x) { return (x + 3u) & ~3u; };
+  SmallLayout L;
+  L.rp_words = r4(V + 1u);
+  L.nt_words = r4((V + 31u) / 32u);
+  L.graph_words = L.rp_words + r4(Ep) + L.nt_words;
+  L.vis_words = L.nt_words;
+  L.half_words = r4((V + 1u) / 2u);
+  L.wave_words = L.vis_words + 2u * L.half_words + r4(V * W);
+  return L;
+}
+struct SmallArgs {
+  const uint32_t* roots;
+  uint32_t n;
+  uint32_t Ep;            // padded CSR entries (row_ptr[V], a multiple of 4)
+  uint32_t waves;         // waves (roots in flight) per block, 1..4
+  uint32_t* dist;         // [n][V] or null
+  uint32_t* nh;           // [n][V][W] or null
+  ospf_digest* digest;    // [n] or null (written, not added)
+  uint32_t* err;          // bit 1: a root with more than 32 W distinct neighbours, 64: bad root
+};
+size_t small_lds_bytes(uint32_t V, uint32_t Ep, uint32_t W, uint32_t waves);
+hipError_t launch_lds_sweep(const DevGraph& g, const SmallArgs& a, uint32_t W, hipStream_t s);
 // kp = 8, 16 or 32 planes per node; depth_bound bounds the BFS level count
 hipError_t launch_msbfs_round(int kp, const DevGraph& g, const MsArgs& a, uint32_t depth_bound,
                               hipStream_t s);

@@ -375,17 +375,26 @@ Twins twin_classes(const ospf_ctx* c) {
   return t;
 }
 
-// DERIVE (spf_levels.hip, spf_leaf.hip, spf_msbfs.hip derive kernels), unit
-// metric / hop count. The part's roots split into leaves (an independent set
-// of nodes with <= 32 distinct neighbours: a fabric's racks) and the cover.
-// (A) levels: the distance-only 128-root BFS for the cover rows the part
-// needs (its cover roots, their neighbours and the leaves' neighbours),
-// ordered by each node's smallest neighbour so a traversal shares frontiers;
+// DERIVE (spf_levels.hip, spf_twin.hip, spf_leaf.hip, spf_msbfs.hip derive
+// kernels), unit metric / hop count. The part's roots split into leaves (an
+// independent set of nodes with <= 32 distinct neighbours: a fabric's racks)
+// and the cover.
+// (A) levels: the distance-only 128-root BFS for the seed rows -- the cover
+//     rows the part needs (its cover roots, their neighbours, the leaves'
+//     neighbours) that no twin class derives, plus the leaf representatives
+//     of the classes the derived rows and the twin next-hop launches read --
+//     ordered by each node's smallest neighbour so a traversal shares frontiers;
+// (A') twin levels: the other cover rows from the representative rows of
+//     their neighbours' twin classes (ospf_twin_levels_dev: a fabric switch
+//     from one rack row of its pod and one spine row of its plane), no
+//     traversal; without twins every cover row is a BFS row and the leaf
+//     representatives come first in (B) instead;
 // (B) the leaves' level, dist and next-hop rows from their neighbours' level
-// rows, groups of leaves with one slot table reading each tile once;
+//     rows (next-hop rows only for BFS'd representatives), groups of leaves
+//     with one slot table reading each tile once;
 // (C) one next-hop launch per width class of cover roots, roots ordered by
-// their largest neighbour (their neighbours' level rows stay in L2 / MALL);
-// classes that read no leaf row run beside (B) on their own stream.
+//     their largest neighbour (their neighbours' level rows stay in L2 / MALL),
+//     on their own streams beside (B).
 int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine) {
   ospf_ctx* c = s->c;
   const uint32_t V = s->V;
@@ -424,24 +433,28 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     cls.push_back(std::move(k));
   }
   // twin classes: a class of <= 4-word roots whose usable transit
-  // neighbours span few classes reads one row per class (spf_twin.hip)
+  // neighbours span few classes reads one row per class (spf_twin.hip), and
+  // so can a cover row (twin levels)
   Twins tw;
-  bool any_w4 = false;
-  for (auto& k : cls) any_w4 |= k.W <= 4;
-  if (any_w4 && !getenv("OSPF_SWEEP_NOTWIN")) tw = twin_classes(c);
+  if (!getenv("OSPF_SWEEP_NOTWIN")) tw = twin_classes(c);
+  // classes of r's usable transit neighbours (sorted, unique); false past kTwinMaxC
+  std::vector<uint32_t> cs;
+  auto classes_of = [&](uint32_t r) {
+    cs.clear();
+    for (uint32_t e = c->h_prow[r]; e < c->h_prow[r + 1]; ++e) {
+      const uint32_t x = c->h_pcolx[e];
+      if ((x & 0x80000000u) || x == r || ((c->h_nt[x >> 5] >> (x & 31)) & 1u)) continue;
+      cs.push_back(tw.cls[x]);
+    }
+    std::sort(cs.begin(), cs.end());
+    cs.erase(std::unique(cs.begin(), cs.end()), cs.end());
+    return cs.size() <= ospf::kTwinMaxC;
+  };
   auto twin_ok = [&](const std::vector<uint32_t>& roots) {
     uint64_t slots = 0, classes = 0;
     for (uint32_t r : roots) {
-      std::vector<uint32_t> cs;
-      for (uint32_t e = c->h_prow[r]; e < c->h_prow[r + 1]; ++e) {
-        const uint32_t x = c->h_pcolx[e];
-        if ((x & 0x80000000u) || x == r || ((c->h_nt[x >> 5] >> (x & 31)) & 1u)) continue;
-        cs.push_back(tw.cls[x]);
-      }
+      if (!classes_of(r)) return false;
       slots += f.nbrs(r);
-      std::sort(cs.begin(), cs.end());
-      cs.erase(std::unique(cs.begin(), cs.end()), cs.end());
-      if (cs.size() > ospf::kTwinMaxC) return false;
       classes += cs.size();
     }
     // worth it when a class covers several slots (OSPF_SWEEP_TWIN=1: always)
@@ -453,17 +466,8 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     if (k.reads_leaf && !k.twin) all_leaf_rows = true;
   }
   all_leaf_rows |= tw.cls.empty() || getenv("OSPF_SWEEP_ALL_LEAF_ROWS") != nullptr;
-  // leaves: when only twin representatives' level rows are read, the
-  // representatives go first in a launch of their own, so the next hops of
-  // the cover roots start while the other leaves' rows are written
-  std::vector<uint32_t> reps, rest;
-  for (const auto* L : {&own_l, &extra_l})
-    for (uint32_t x : *L) ((!all_leaf_rows && tw.rep[tw.cls[x]] == x) ? reps : rest).push_back(x);
-  std::vector<uint32_t> grp_r = leaf_groups(c, f, reps);
-  std::vector<uint32_t> grp = leaf_groups(c, f, rest);
-  std::vector<uint32_t> need_l = reps;
-  need_l.insert(need_l.end(), rest.begin(), rest.end());
-  const uint32_t nR = (uint32_t)reps.size(), nL = (uint32_t)need_l.size();
+  std::vector<uint32_t> need_l = own_l;
+  need_l.insert(need_l.end(), extra_l.begin(), extra_l.end());
   // cover rows: own cover roots + every non-leaf neighbour of a needed root
   std::vector<uint8_t> in_a(V, 0);
   for (uint32_t v : own_c) in_a[v] = 1;
@@ -471,47 +475,115 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     if (!leaf[v]) in_a[v] = 1;
   for (uint32_t v : nb_c)
     if (!leaf[v]) in_a[v] = 1;
-  std::vector<uint32_t> clo;
-  for (uint32_t v = 0; v < V; ++v)
-    if (in_a[v]) clo.push_back(v);
+  uint32_t n_cover = 0;
+  for (uint32_t v = 0; v < V; ++v) n_cover += in_a[v];
+  // (A') cover rows derived from twin classes; their classes' representatives
+  // are BFS rows (a derived representative leaves the set: repeat until
+  // stable), and so are the leaf representatives the twin next hops read
+  std::vector<uint8_t> in_d(V, 0), seed(V, 0);
+  bool twin_lv = !tw.cls.empty() && !getenv("OSPF_SWEEP_NOTWINLV");
+  if (twin_lv) {
+    for (uint32_t v = 0; v < V; ++v)
+      if (in_a[v] && f.nbrs(v) <= 128 && classes_of(v)) in_d[v] = 1;
+    for (bool changed = true; changed;) {
+      changed = false;
+      for (uint32_t v = 0; v < V; ++v) {
+        if (!in_d[v]) continue;
+        classes_of(v);
+        for (uint32_t k : cs)
+          if (in_d[tw.rep[k]]) {
+            in_d[tw.rep[k]] = 0;
+            changed = true;
+          }
+      }
+    }
+    auto seed_reps = [&](uint32_t v) {
+      classes_of(v);
+      for (uint32_t k : cs)
+        if (leaf[tw.rep[k]]) seed[tw.rep[k]] = 1;
+    };
+    for (uint32_t v = 0; v < V; ++v)
+      if (in_d[v]) seed_reps(v);
+    for (auto& k : cls)
+      if (k.twin)
+        for (uint32_t r : k.roots) seed_reps(r);
+    uint32_t nbfs = 0;
+    for (uint32_t v = 0; v < V; ++v) nbfs += (in_a[v] && !in_d[v]) || seed[v];
+    // worth it when the traversal shrinks to half (OSPF_SWEEP_TWINLV=1: always)
+    if (!getenv("OSPF_SWEEP_TWINLV") && 2ull * nbfs > n_cover) twin_lv = false;
+    if (!twin_lv) {
+      std::fill(in_d.begin(), in_d.end(), 0);
+      std::fill(seed.begin(), seed.end(), 0);
+    }
+  }
+  // leaves: with twin levels, BFS'd representatives first (next-hop rows
+  // only), then the others; without, when only twin representatives' level
+  // rows are read, the representatives go first in a launch of their own,
+  // so the next hops of the cover roots start while the other leaves' rows
+  // are written
+  std::vector<uint32_t> reps, rest;
+  for (uint32_t x : need_l) {
+    const bool first = twin_lv ? seed[x] != 0 : (!all_leaf_rows && tw.rep[tw.cls[x]] == x);
+    (first ? reps : rest).push_back(x);
+  }
+  std::vector<uint32_t> grp_r = leaf_groups(c, f, reps);
+  std::vector<uint32_t> grp = leaf_groups(c, f, rest);
+  need_l = reps;
+  need_l.insert(need_l.end(), rest.begin(), rest.end());
+  const uint32_t nR = (uint32_t)reps.size(), nL = (uint32_t)need_l.size();
+  // rows: BFS rows (cover rows not derived + seed leaves), derived cover
+  // rows, then the leaves that are not BFS rows
+  std::vector<uint32_t> clo, drv;
+  for (uint32_t v = 0; v < V; ++v) {
+    if ((in_a[v] && !in_d[v]) || seed[v]) clo.push_back(v);
+    else if (in_d[v]) drv.push_back(v);
+  }
   locality_order(clo, [&](uint32_t v) { return f.first(v); });
-  const uint32_t nc = (uint32_t)clo.size();
+  locality_order(drv, [&](uint32_t v) { return f.last(v); });
+  const uint32_t nc = (uint32_t)clo.size(), nd = (uint32_t)drv.size();
   std::vector<uint32_t> pos(V, kNone);
   for (uint32_t i = 0; i < nc; ++i) pos[clo[i]] = i;
-  for (uint32_t i = 0; i < nL; ++i) pos[need_l[i]] = nc + i;
+  for (uint32_t i = 0; i < nd; ++i) pos[drv[i]] = nc + i;
+  uint32_t rows = nc + nd;
+  for (uint32_t i = 0; i < nL; ++i)
+    if (pos[need_l[i]] == kNone) pos[need_l[i]] = rows++;
   const uint32_t pitch = (V + 15) / 16 * 16;
-  const uint32_t rows = nc + nL;
-  uint32_t *d_clo = nullptr, *d_pos, *dist, *d_l = nullptr, *lnh = nullptr;
+  uint32_t *d_clo = nullptr, *d_drv = nullptr, *d_pos, *dist, *d_l = nullptr, *lnh = nullptr;
   uint32_t *d_grp_r = nullptr, *d_grp = nullptr, *d_lout = nullptr;
   uint8_t* lev;
   ospf_digest* ldg;
   int rc;
   if ((rc = upload(s, &d_pos, pos)) || (rc = dalloc(s, &lev, (size_t)rows * pitch)) ||
-      (rc = dalloc(s, &dist, (size_t)rows * V)) || (rc = dalloc(s, &ldg, std::max(1u, nc))))
+      (rc = dalloc(s, &dist, (size_t)rows * V)) || (rc = dalloc(s, &ldg, std::max(1u, nc + nd))))
     return rc;
   if (nc && (rc = upload(s, &d_clo, clo))) return rc;
+  if (nd && (rc = upload(s, &d_drv, drv))) return rc;
   if (nL && ((rc = upload(s, &d_l, need_l)) || (rc = dalloc(s, &lnh, (size_t)nL * V))))
     return rc;
   if (nR && (rc = upload(s, &d_grp_r, grp_r))) return rc;
   if (nL > nR && (rc = upload(s, &d_grp, grp))) return rc;
-  if (!all_leaf_rows && nL > nR) {  // the other leaves' level bytes are not kept
-    std::vector<uint32_t> lout(nL - nR, kNone);
+  // level bytes not kept: BFS'd representatives (their BFS rows stay), and
+  // the other leaves unless a non-twin class reads every leaf row
+  const bool drop_rest = !all_leaf_rows && nL > nR;
+  if (drop_rest || (twin_lv && nR)) {
+    std::vector<uint32_t> lout(std::max(drop_rest ? nL - nR : 0u, twin_lv ? nR : 0u), kNone);
     if ((rc = upload(s, &d_lout, lout))) return rc;
   }
   uint32_t *d_tcls = nullptr, *d_trep = nullptr, *d_tsec = nullptr;
-  bool any_twin = false;
+  bool any_twin = nd > 0;
   for (auto& k : cls) any_twin |= k.twin;
   if (any_twin && ((rc = upload(s, &d_tcls, tw.cls)) || (rc = upload(s, &d_trep, tw.rep)) ||
                    (rc = upload(s, &d_tsec, tw.sec))))
     return rc;
-  s->dig_aux.push_back({ldg, std::max(1u, nc)});
+  s->dig_aux.push_back({ldg, std::max(1u, nc + nd)});
   s->n_rows = rows;
   const uint32_t ndig = (uint32_t)own_c.size() + nL;
   if ((rc = dalloc(s, &s->dig_all, ndig))) return rc;
   s->n_dig = ndig;
-  // events: levels done, representative leaves done, every leaf done
-  const int ev_a = new_event(s), ev_r = new_event(s), ev_b = new_event(s);
-  if (ev_a < 0 || ev_r < 0 || ev_b < 0) return ev_a < 0 ? ev_a : ev_r < 0 ? ev_r : ev_b;
+  // events: levels done, cover rows done (= levels without twin levels),
+  // representative leaves done, every leaf done
+  const int ev_a = new_event(s), ev_t = new_event(s), ev_r = new_event(s), ev_b = new_event(s);
+  if (ev_a < 0 || ev_t < 0 || ev_r < 0 || ev_b < 0) return std::min({ev_a, ev_t, ev_r, ev_b});
   if (nc) {
     ospf_sweep::Unit lv;
     lv.name = "levels";
@@ -527,13 +599,26 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     s->step_comp += lv.comp;
     s->units.push_back(lv);
   }
+  if (nd) {
+    ospf_sweep::Unit u;
+    u.name = "twin_levels";
+    u.kernel = "ospf_twin_levels_dev (twin_levels_kernel: level + dist rows from the neighbour "
+               "classes' representative rows)";
+    u.stream = 0;
+    u.record = ev_t;
+    u.n_roots = nd;
+    // dist rows written + the class rows read once (level rows are intermediate)
+    u.comp = (uint64_t)nd * 4ull * V;
+    const uint32_t *tc = d_tcls, *tr = d_trep;
+    u.fn = [=](hipStream_t st) {
+      return ospf_twin_levels_dev(c, d_drv, nd, lev, pitch, d_pos, tc, tr, dist, ldg, st);
+    };
+    s->step_comp += u.comp;
+    s->units.push_back(u);
+  }
+  const int ev_cov = nd ? ev_t : ev_a;
   // (C) cover classes: digest slots 0 .. |own_c|
   uint32_t slot = 0;
-  std::vector<size_t> order(cls.size());
-  std::iota(order.begin(), order.end(), 0);
-  std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
-    return (uint64_t)cls[a].W * cls[a].roots.size() > (uint64_t)cls[b].W * cls[b].roots.size();
-  });
   std::vector<ospf_sweep::Unit> side, after;
   for (size_t i = 0; i < cls.size(); ++i) {
     Cls& k = cls[i];
@@ -553,8 +638,9 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     const int st = new_stream(s);
     if (st < 0) return st;
     u.stream = st;
-    // twin classes read only the representatives' rows; others every row
-    u.wait = {!k.reads_leaf ? ev_a : k.twin ? ev_r : ev_b};
+    // twin classes read the representatives' rows (BFS'd with twin levels);
+    // the others every neighbour's row
+    u.wait = {!k.reads_leaf ? ev_cov : k.twin ? (twin_lv ? ev_cov : ev_r) : ev_b};
     u.n_roots = n;
     u.W = W;
     u.comp = (uint64_t)n * 4ull * V * W;
@@ -570,7 +656,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       };
     }
     s->step_comp += u.comp;
-    (k.reads_leaf ? after : side).push_back(std::move(u));
+    (u.wait[0] == ev_b || u.wait[0] == ev_r ? after : side).push_back(std::move(u));
   }
   for (auto& x : side) s->units.push_back(std::move(x));
   // (B) leaves: digest slots after the cover roots'; representatives first
@@ -579,23 +665,34 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     for (uint32_t r : need_l) kmax = std::max(kmax, f.nbrs(r));
     for (uint32_t j = 0; j < nL; ++j)
       if (in_l[need_l[j]])
-        own(s, need_l[j], slot + j, dist + (size_t)(nc + j) * V, lnh + (size_t)j * V, 1);
+        own(s, need_l[j], slot + j, dist + (size_t)pos[need_l[j]] * V, lnh + (size_t)j * V, 1);
     ospf_digest* dg = s->dig_all + slot;
     const uint32_t ngr_r = nR ? (uint32_t)grp_r.size() - 1 : 0u;
     const uint32_t ngr = nL > nR ? (uint32_t)grp.size() - 1 : 0u;
     if (nR) {
       ospf_sweep::Unit u;
-      u.name = "leaf_reps";
-      u.kernel = "ospf_leaf_derive2_dev (leaf_derive_kernel: twin representatives' level + dist "
-                 "+ next-hop rows)";
-      u.stream = 0;
+      u.name = twin_lv ? "leaf_seeds" : "leaf_reps";
+      u.kernel = twin_lv ? "ospf_leaf_derive2_dev (leaf_derive_kernel: next-hop rows of BFS'd "
+                           "leaf representatives)"
+                         : "ospf_leaf_derive2_dev (leaf_derive_kernel: twin representatives' level "
+                           "+ dist + next-hop rows)";
+      if (twin_lv) {  // beside the other leaves, after the cover rows
+        const int st = new_stream(s);
+        if (st < 0) return st;
+        u.stream = st;
+        u.wait = {ev_cov};
+      } else {
+        u.stream = 0;
+      }
       u.record = ev_r;
       u.n_roots = nR;
       u.W = 1;
-      u.comp = (uint64_t)nR * 8ull * V;
+      u.comp = (uint64_t)nR * (twin_lv ? 4ull : 8ull) * V;
+      const uint32_t* lo = twin_lv ? d_lout : nullptr;
+      uint32_t* dd = twin_lv ? nullptr : dist;
       u.fn = [=](hipStream_t strm) {
-        return ospf_leaf_derive2_dev(c, d_l, nR, d_grp_r, ngr_r, kmax, lev, pitch, d_pos, nullptr,
-                                     dist, lnh, dg, strm);
+        return ospf_leaf_derive2_dev(c, d_l, nR, d_grp_r, ngr_r, kmax, lev, pitch, d_pos, lo, dd,
+                                     lnh, dg, strm);
       };
       s->step_comp += u.comp;
       s->units.push_back(std::move(u));
@@ -606,7 +703,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       u.kernel = "ospf_leaf_derive2_dev (leaf_derive_kernel: level + dist + next-hop rows of leaf "
                  "roots from their neighbours' level rows)";
       const uint32_t n = nL - nR;
-      if (nR) {  // beside the cover roots' next hops, on a stream of its own
+      if (nR && !twin_lv) {  // beside the cover roots' next hops, on a stream of its own
         const int st = new_stream(s);
         if (st < 0) return st;
         u.stream = st;
@@ -621,7 +718,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       const uint32_t* dl = d_l + nR;
       uint32_t* nh = lnh + (size_t)nR * V;
       ospf_digest* dg2 = dg + nR;
-      const uint32_t* lo = d_lout;
+      const uint32_t* lo = drop_rest ? d_lout : nullptr;
       u.fn = [=](hipStream_t strm) {
         return ospf_leaf_derive2_dev(c, dl, n, d_grp, ngr, kmax, lev, pitch, d_pos, lo, dist, nh,
                                      dg2, strm);
@@ -630,11 +727,14 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       s->units.push_back(std::move(u));
     }
   }
-  if (nR && nL == nR) {  // every leaf is a representative: ev_b = ev_r
+  // an event no launch records stands for the one before it
+  auto alias = [&](int from, int to) {
     for (auto& u : after)
       for (int& e : u.wait)
-        if (e == ev_b) e = ev_r;
-  }
+        if (e == from) e = to;
+  };
+  if (!(nL > nR)) alias(ev_b, nR ? ev_r : ev_cov);
+  if (!nR) alias(ev_r, ev_cov);
   for (auto& x : after) s->units.push_back(std::move(x));
   return OSPF_OK;
 }
@@ -700,6 +800,63 @@ int plan_batch(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine,
       b.d_nh = nh;
       b.d_digest = dg;
       return ospf_run_batch_dev(c, &b, strm);
+    };
+    s->step_comp += u.comp;
+    s->units.push_back(std::move(u));
+  }
+  return OSPF_OK;
+}
+
+// LDS (spf_small.hip): small graphs, one launch per next-hop width (W <= 4)
+// -- a wave per root with the graph in LDS; the widest class on the main
+// stream, the others beside it.
+int plan_lds(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine) {
+  ospf_ctx* c = s->c;
+  const uint32_t V = s->V;
+  const uint32_t hop = s->opts.flags & OSPF_HOP_COUNT;
+  std::vector<uint32_t> ws;
+  for (uint32_t r : mine) ws.push_back(f.words(r));
+  std::sort(ws.begin(), ws.end());
+  ws.erase(std::unique(ws.begin(), ws.end()), ws.end());
+  int rc;
+  if ((rc = dalloc(s, &s->dig_all, mine.size()))) return rc;
+  s->n_dig = (uint32_t)mine.size();
+  s->n_rows = (uint32_t)mine.size();
+  uint32_t slot = 0;
+  bool first = true;
+  for (auto it = ws.rbegin(); it != ws.rend(); ++it) {
+    const uint32_t W = *it;
+    std::vector<uint32_t> roots;
+    for (uint32_t r : mine)
+      if (f.words(r) == W) roots.push_back(r);
+    const uint32_t n = (uint32_t)roots.size();
+    uint32_t *d_roots, *dist, *nh;
+    if ((rc = upload(s, &d_roots, roots)) || (rc = dalloc(s, &dist, (size_t)n * V)) ||
+        (rc = dalloc(s, &nh, (size_t)n * V * W)))
+      return rc;
+    ospf_digest* dg = s->dig_all + slot;
+    for (uint32_t j = 0; j < n; ++j)
+      own(s, roots[j], slot + j, dist + (size_t)j * V, nh + (size_t)j * V * W, W);
+    slot += n;
+    ospf_sweep::Unit u;
+    u.name = "lds_w" + std::to_string(W);
+    u.kernel = "ospf_lds_sweep_dev (lds_sweep_kernel<" + std::to_string(W) +
+               ">: a wave per root, graph + BFS state in LDS)";
+    if (first) {
+      u.stream = 0;
+    } else {
+      const int st = new_stream(s);
+      if (st < 0) return st;
+      u.stream = st;
+      u.wait = {0};
+    }
+    first = false;
+    u.n_roots = n;
+    u.W = W;
+    // rows written + the padded CSR each block copies in (read once from HBM)
+    u.comp = (uint64_t)n * 4ull * V * (1 + W) + scan_bytes(c, false);
+    u.fn = [=](hipStream_t strm) {
+      return ospf_lds_sweep_dev(c, d_roots, n, hop, W, dist, nh, dg, strm);
     };
     s->step_comp += u.comp;
     s->units.push_back(std::move(u));
@@ -1069,7 +1226,7 @@ int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
   if (c->mask.on) return fail(c, OSPF_E_INVAL, "sweep: links are masked (ospf_links_unmask)");
   const uint32_t parts = std::max(1u, o->n_parts);
   if (o->part >= parts) return fail(c, OSPF_E_INVAL, "sweep: part >= n_parts");
-  if (o->mode > OSPF_SWEEP_BATCH) return fail(c, OSPF_E_INVAL, "sweep: unknown mode");
+  if (o->mode > OSPF_SWEEP_LDS) return fail(c, OSPF_E_INVAL, "sweep: unknown mode");
   if (o->flags & ~OSPF_HOP_COUNT) return fail(c, OSPF_E_INVAL, "sweep: flags = 0 or OSPF_HOP_COUNT");
   const bool hop = o->flags & OSPF_HOP_COUNT;
   if (!hop && c->dist_bound >= 0xFFFFFFFFull)
@@ -1104,6 +1261,10 @@ int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
   // path
   const bool unit = hop || c->info.unit_metric;
   const bool derive_ok = unit && c->max_dn <= 2048 && c->depth_bound <= 123;
+  // small graphs: every root's next hops in <= 4 words and the graph in LDS
+  const uint32_t max_w = std::max(1u, (c->max_dn + 31) / 32);
+  const bool lds_ok = unit && max_w <= 4 && ospf_lds_sweep_fits(c, o->flags, max_w) &&
+                      !getenv("OSPF_SWEEP_NOLDS");
   std::vector<uint8_t> leaf;
   bool any_leaf = false;
   uint32_t mode = o->mode;
@@ -1114,7 +1275,9 @@ int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
     }
   }
   if (mode == OSPF_SWEEP_AUTO) {
-    if (derive_ok) {
+    if (lds_ok) {
+      mode = OSPF_SWEEP_LDS;
+    } else if (derive_ok) {
       mode = OSPF_SWEEP_DERIVE;
     } else if (!hop && any_leaf && ospf_cover_prepare(c, leaf.data()) == OSPF_OK) {
       mode = OSPF_SWEEP_WCOVER;
@@ -1126,6 +1289,9 @@ int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
   } else if (mode == OSPF_SWEEP_DERIVE && !derive_ok) {
     return bail(fail(c, OSPF_E_RANGE, "sweep: derive needs unit metric or hop count, a depth "
                                       "bound <= 123 and <= 2048 distinct neighbours per node"));
+  } else if (mode == OSPF_SWEEP_LDS && !lds_ok) {
+    return bail(fail(c, OSPF_E_RANGE, "sweep: lds needs unit metric or hop count, <= 128 "
+                                      "distinct neighbours per node and the graph in LDS"));
   } else if (mode == OSPF_SWEEP_WCOVER) {
     if (hop) return bail(fail(c, OSPF_E_INVAL, "sweep: the cover path runs link metrics"));
     const int rc = ospf_cover_prepare(c, leaf.data());
@@ -1137,6 +1303,7 @@ int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
     case OSPF_SWEEP_DERIVE: rc = plan_derive(s, f, mine); break;
     case OSPF_SWEEP_WCOVER: rc = plan_wcover(s, f, mine, leaf); break;
     case OSPF_SWEEP_WDERIVE: rc = plan_wderive(s, f, mine, leaf); break;
+    case OSPF_SWEEP_LDS: rc = plan_lds(s, f, mine); break;
     default: rc = plan_batch(s, f, mine, !unit); break;
   }
   if (rc) return bail(rc);

@@ -51,110 +51,126 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t x, int o) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-template <int W>
-__global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, TwinArgs a) {
-  __shared__ uint32_t s_nb[kMaxK];     // distinct neighbours (ascending)
-  __shared__ uint32_t s_slot[kMaxK];   // per slot: class id (0xFFFFFFFE non-transit, kInf unusable)
-  __shared__ uint32_t s_first[kMaxK];  // first slot of the same class
-  __shared__ uint32_t s_cid[kMaxK];    // per slot: class index, 0x100 non-transit, kInf unusable
-  __shared__ uint32_t s_use[4];
-  __shared__ uint32_t s_ccls[kTwinMaxC], s_crow[kTwinMaxC], s_crep[kTwinMaxC], s_cx[kTwinMaxC];
-  __shared__ uint32_t s_cmask[kTwinMaxC][4];
-  __shared__ uint32_t s_nc, s_K, s_own, s_root, s_bad;
-  __shared__ unsigned long long s_h;
-  extern __shared__ uint32_t s_stage[];  // [4 waves][1024 nodes][W]
-  const uint32_t V = g.V, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  // XCD-aware order: XCD x (blocks x, x + 8, ...) walks a contiguous range
-  // of (root, chunk) items, so roots sharing class rows share its L2
-  const uint32_t T = a.n * a.chunks, T8 = T / 8u * 8u, b = blockIdx.x;
-  const uint32_t item = b < T8 ? (b % 8u) * (T8 / 8u) + b / 8u : b;
-  const uint32_t i = item / a.chunks, ci = item % a.chunks;
+// LDS tables of one root's neighbour classes, shared by the twin kernels.
+struct TwinTab {
+  uint32_t nb[kMaxK];     // distinct neighbours (ascending)
+  uint32_t slot[kMaxK];   // per slot: class id (0xFFFFFFFE non-transit, kInf unusable)
+  uint32_t first[kMaxK];  // first slot of the same class
+  uint32_t cid[kMaxK];    // per slot: class index, 0x100 non-transit, kInf unusable
+  uint32_t use[4];
+  uint32_t ccls[kTwinMaxC], crow[kTwinMaxC], crep[kTwinMaxC], cx[kTwinMaxC];
+  uint32_t cmask[kTwinMaxC][4];
+  uint32_t nc, K, own, root, bad;
+};
+
+// Block-wide: the classes of root a.roots[i]'s usable transit neighbours,
+// each with its representative's level row (crow) and slot mask. False (for
+// the whole block) when the root or a class row is missing (error bits set).
+__device__ bool twin_setup(const DevGraph& g, const TwinArgs& a, uint32_t i, uint32_t words,
+                           TwinTab& T) {
+  const uint32_t V = g.V, tid = threadIdx.x;
   if (tid == 0) {
     const uint32_t r = a.roots[i];
-    s_root = r;
-    s_h = 0ull;
-    s_bad = 0u;
-    s_nc = 0u;
-    s_own = r < V ? a.pos[r] : kInf;
-    s_K = r < V ? g.dn_off[r + 1] - g.dn_off[r] : 0u;
+    T.root = r;
+    T.bad = 0u;
+    T.nc = 0u;
+    T.own = r < V ? a.pos[r] : kInf;
+    T.K = r < V ? g.dn_off[r + 1] - g.dn_off[r] : 0u;
     if (r >= V) atomicOr(a.err, 64u);
-    else if (s_own == kInf) atomicOr(a.err, 16u);
-    else if (s_K > a.cap || s_K > 32u * W) atomicOr(a.err, 1u);
+    else if (T.own == kInf) atomicOr(a.err, 16u);
+    else if (T.K > a.cap || T.K > 32u * words) atomicOr(a.err, 1u);
   }
-  if (tid < 4) s_use[tid] = 0u;
+  if (tid < 4) T.use[tid] = 0u;
   __syncthreads();
-  const uint32_t r = s_root, K = min(s_K, (uint32_t)(32 * W)), own = s_own;
-  if (r >= V || own == kInf) return;
+  const uint32_t r = T.root, K = min(T.K, 32u * words);
+  if (r >= V || T.own == kInf) return false;
   for (uint32_t e = g.row_ptr[r] + tid; e < g.row_ptr[r + 1]; e += kBlock) {
     const uint32_t cx = g.colx[e];
     if ((cx & kDown) || cx == r) continue;
     const uint32_t k = g.didx[e];
-    if (k < K) atomicOr(&s_use[k >> 5], 1u << (k & 31u));
+    if (k < K) atomicOr(&T.use[k >> 5], 1u << (k & 31u));
   }
-  if (tid < K) s_nb[tid] = g.dn[g.dn_off[r] + tid];
+  if (tid < K) T.nb[tid] = g.dn[g.dn_off[r] + tid];
   __syncthreads();
   // class of every usable transit slot (loads in parallel), first slot of
   // each class, then one pass over the slot table in LDS
   if (tid < K) {
-    const uint32_t n = s_nb[tid];
+    const uint32_t n = T.nb[tid];
     uint32_t v = kInf;  // unusable
-    if ((s_use[tid >> 5] >> (tid & 31u)) & 1u) v = transit(g, n) ? a.tcls[n] : 0xFFFFFFFEu;
-    s_slot[tid] = v;
+    if ((T.use[tid >> 5] >> (tid & 31u)) & 1u) v = transit(g, n) ? a.tcls[n] : 0xFFFFFFFEu;
+    T.slot[tid] = v;
   }
   __syncthreads();
   if (tid < K) {
-    const uint32_t v = s_slot[tid];
+    const uint32_t v = T.slot[tid];
     uint32_t first = tid;
     if (v < 0xFFFFFFFEu)
       for (uint32_t k = 0; k < tid; ++k)
-        if (s_slot[k] == v) {
+        if (T.slot[k] == v) {
           first = k;
           break;
         }
-    s_first[tid] = first;
+    T.first[tid] = first;
   }
   __syncthreads();
   if (tid == 0) {
     uint32_t nc = 0;
     for (uint32_t k = 0; k < K; ++k) {
-      const uint32_t v = s_slot[k];
+      const uint32_t v = T.slot[k];
       if (v >= 0xFFFFFFFEu) {
-        s_cid[k] = v == kInf ? kInf : 0x100u;
+        T.cid[k] = v == kInf ? kInf : 0x100u;
         continue;
       }
       uint32_t j;
-      if (s_first[k] == k) {
+      if (T.first[k] == k) {
         if (nc == kTwinMaxC) {
-          s_bad = 1u;
+          T.bad = 1u;
           break;
         }
         j = nc++;
-        s_ccls[j] = v;
-        for (int w = 0; w < 4; ++w) s_cmask[j][w] = 0u;
+        T.ccls[j] = v;
+        for (int w = 0; w < 4; ++w) T.cmask[j][w] = 0u;
       } else {
-        j = s_cid[s_first[k]];
+        j = T.cid[T.first[k]];
       }
-      s_cmask[j][k >> 5] |= 1u << (k & 31u);
-      s_cid[k] = j;
+      T.cmask[j][k >> 5] |= 1u << (k & 31u);
+      T.cid[k] = j;
     }
-    s_nc = nc;
-    if (s_bad) atomicOr(a.err, 256u);
+    T.nc = nc;
+    if (T.bad) atomicOr(a.err, 256u);
   }
   __syncthreads();
-  if (s_bad) return;
-  const uint32_t nc = s_nc;
+  if (T.bad) return false;
+  const uint32_t nc = T.nc;
   if (tid < nc) {
-    const uint32_t c = s_ccls[tid], rep = a.trep[c], sec = a.tsec[c];
+    const uint32_t c = T.ccls[tid], rep = a.trep[c], sec = a.tsec ? a.tsec[c] : kInf;
     const uint32_t row = a.pos[rep];
-    s_crep[tid] = rep;
-    s_crow[tid] = row;
+    T.crep[tid] = rep;
+    T.crow[tid] = row;
     if (row == kInf) atomicOr(a.err, 16u);
     // X: level of another member at the representative's position
-    s_cx[tid] = (sec != kInf && row != kInf) ? a.lev[(size_t)row * a.pitch + sec] : 0x7Fu;
+    T.cx[tid] = (sec != kInf && row != kInf) ? a.lev[(size_t)row * a.pitch + sec] : 0x7Fu;
   }
   __syncthreads();
   for (uint32_t x = 0; x < nc; ++x)
-    if (s_crow[x] == kInf) return;
+    if (T.crow[x] == kInf) return false;
+  return true;
+}
+
+template <int W>
+__global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, TwinArgs a) {
+  __shared__ TwinTab T;
+  __shared__ unsigned long long s_h;
+  extern __shared__ uint32_t s_stage[];  // [4 waves][1024 nodes][W]
+  const uint32_t V = g.V, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  // XCD-aware order: XCD x (blocks x, x + 8, ...) walks a contiguous range
+  // of (root, chunk) items, so roots sharing class rows share its L2
+  const uint32_t NT = a.n * a.chunks, T8 = NT / 8u * 8u, b = blockIdx.x;
+  const uint32_t item = b < T8 ? (b % 8u) * (T8 / 8u) + b / 8u : b;
+  const uint32_t i = item / a.chunks, ci = item % a.chunks;
+  if (tid == 0) s_h = 0ull;
+  if (!twin_setup(g, a, i, W, T)) return;
+  const uint32_t K = min(T.K, (uint32_t)(32 * W)), own = T.own, nc = T.nc;
   const uint32_t t0 = ci * a.ctiles, t1 = min(a.tiles, t0 + a.ctiles);
   uint32_t* st = s_stage + wave * 1024u * W;
   uint64_t h = 0;
@@ -167,7 +183,7 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
     L = *reinterpret_cast<const uint4*>(a.lev + (size_t)own * a.pitch + vs);
 #pragma unroll
     for (uint32_t j = 0; j < kPre; ++j)
-      if (j < nc) R[j] = *reinterpret_cast<const uint4*>(a.lev + (size_t)s_crow[j] * a.pitch + vs);
+      if (j < nc) R[j] = *reinterpret_cast<const uint4*>(a.lev + (size_t)T.crow[j] * a.pitch + vs);
   };
   uint4 Ln, Rn[kPre];
   load_t(t0 + wave, Ln, Rn);
@@ -206,12 +222,12 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
         for (uint32_t q = 0; q < kPre; ++q)
           if (q == j) R = Rp[q];
       } else {
-        R = *reinterpret_cast<const uint4*>(a.lev + (size_t)s_crow[j] * a.pitch + vs);
+        R = *reinterpret_cast<const uint4*>(a.lev + (size_t)T.crow[j] * a.pitch + vs);
       }
       const uint32_t Rw[4] = {R.x, R.y, R.z, R.w};
       uint32_t cm[W];
 #pragma unroll
-      for (int w = 0; w < W; ++w) cm[w] = s_cmask[j][w];
+      for (int w = 0; w < W; ++w) cm[w] = T.cmask[j][w];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint32_t z = live ? (lm1[q] - Rw[q]) & 0x80808080u : 0u;
@@ -240,20 +256,20 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
       uint32_t lo = 0, hi = K;
       while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (s_nb[mid] < tv0) lo = mid + 1; else hi = mid;
+        if (T.nb[mid] < tv0) lo = mid + 1; else hi = mid;
       }
-      for (uint32_t k = lo; k < K && s_nb[k] < tv0 + 1024u; ++k) {
-        const uint32_t sk = s_cid[k];
+      for (uint32_t k = lo; k < K && T.nb[k] < tv0 + 1024u; ++k) {
+        const uint32_t sk = T.cid[k];
         if (sk == kInf) continue;
-        const uint32_t n = s_nb[k], o = n - tv0;
+        const uint32_t n = T.nb[k], o = n - tv0;
         const uint32_t Ln = a.lev[(size_t)own * a.pitch + n];
         uint32_t nw[W], ow[W];
 #pragma unroll
         for (int w = 0; w < W; ++w) nw[w] = ow[w] = st[o * W + w];
-        if (sk != 0x100u && n == s_crep[sk]) {  // re-test the class against X
-          const bool tight = Ln >= 2u && Ln < 0x7Fu && s_cx[sk] + 1u == Ln;
+        if (sk != 0x100u && n == T.crep[sk]) {  // re-test the class against X
+          const bool tight = Ln >= 2u && Ln < 0x7Fu && T.cx[sk] + 1u == Ln;
 #pragma unroll
-          for (int w = 0; w < W; ++w) nw[w] = (nw[w] & ~s_cmask[sk][w]) | (tight ? s_cmask[sk][w] : 0u);
+          for (int w = 0; w < W; ++w) nw[w] = (nw[w] & ~T.cmask[sk][w]) | (tight ? T.cmask[sk][w] : 0u);
         }
         // n itself: level 1 of its own row, a next hop iff dist(r, n) == 1
 #pragma unroll
@@ -321,6 +337,123 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
   }
 }
 
+
+// byte-wise min of 7-bit bytes: bit 7 of (a | 0x80) - b is set iff a >= b
+__device__ __forceinline__ uint32_t bmin7(uint32_t a, uint32_t b) {
+  const uint32_t ge = ((a | 0x80808080u) - b) & 0x80808080u;
+  const uint32_t m = (ge << 1) - (ge >> 7);  // 0xFF in the bytes where a >= b
+  return (b & m) | (a & ~m);
+}
+
+// Level + dist rows of a root from its neighbour classes (twin Bellman).
+// dist(r, v) = 1 + min over the classes of the representative's row R_j(v)
+// for v outside r and its usable neighbours; 0 at r; 1 at every usable
+// neighbour, transit or not -- LinkState::runSpf's Bellman equation over the
+// root's out-links with unit weights (LinkState.cpp:836-911; overloaded
+// neighbours reach only themselves, :859-866): twins' rows agree except at
+// their members' positions, and every member of a neighbour's class is
+// itself a usable neighbour of r (twins share their usable neighbours, r
+// among them). So a fabric switch reads two class rows (its pod's racks,
+// its plane's spines) instead of a traversal. Lane = 4 nodes, wave = 256
+// nodes per step, block = one root over every node; the distance part of
+// the digest is stored (not added).
+__global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinArgs a) {
+  __shared__ TwinTab T;
+  __shared__ unsigned long long s_r[kWaves], s_s[kWaves], s_hh[kWaves];
+  extern __shared__ uint32_t s_nbm[];  // [(pitch + 31) / 32] usable-neighbour bits
+  const uint32_t V = g.V, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t b = blockIdx.x, T8 = a.n / 8u * 8u;  // XCD-aware root order
+  const uint32_t i = b < T8 ? (b % 8u) * (T8 / 8u) + b / 8u : b;
+  if (!twin_setup(g, a, i, 4, T)) return;
+  const uint32_t K = min(T.K, kMaxK), own = T.own, nc = T.nc, r = T.root;
+  const uint32_t nw = (a.pitch + 31u) / 32u;
+  for (uint32_t x = tid; x < nw; x += kBlock) s_nbm[x] = 0u;
+  __syncthreads();
+  if (tid < K && T.cid[tid] != kInf) atomicOr(&s_nbm[T.nb[tid] >> 5], 1u << (T.nb[tid] & 31u));
+  __syncthreads();
+  uint32_t crow[kTwinMaxC];
+#pragma unroll
+  for (uint32_t j = 0; j < kTwinMaxC; ++j) crow[j] = j < nc ? T.crow[j] : 0u;
+  const uint32_t chunks = a.pitch / 256u;
+  auto load_x = [&](uint32_t c, uint32_t* x) {
+    const uint32_t v0 = c < chunks ? c * 256u + 4u * lane : 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < kTwinMaxC; ++j)
+      x[j] = j < nc ? *reinterpret_cast<const uint32_t*>(a.lev + (size_t)crow[j] * a.pitch + v0)
+                    : 0x7F7F7F7Fu;
+  };
+  uint64_t br = 0, bs = 0, bh = 0;
+  const bool vec = (V & 3u) == 0;
+  uint32_t xn[kTwinMaxC];
+  load_x(wave, xn);
+  for (uint32_t c = wave; c < chunks + (a.pitch % 256u ? 1u : 0u); c += kWaves) {
+    const uint32_t v0 = c * 256u + 4u * lane;
+    uint32_t m = 0x7F7F7F7Fu;
+    if (c < chunks) {
+#pragma unroll
+      for (uint32_t j = 0; j < kTwinMaxC; ++j) m = bmin7(m, xn[j]);
+      load_x(c + kWaves, xn);
+    } else if (v0 < a.pitch) {  // tail chunk (pitch is a multiple of 16, not of 256)
+      for (uint32_t j = 0; j < nc; ++j)
+        m = bmin7(m, *reinterpret_cast<const uint32_t*>(a.lev + (size_t)crow[j] * a.pitch + v0));
+    }
+    if (v0 >= a.pitch) continue;
+    uint32_t L = (m + 0x01010101u) - (((m + 0x01010101u) & 0x80808080u) >> 7);
+    const uint32_t nb4 = (s_nbm[v0 >> 5] >> (v0 & 31u)) & 0xFu;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if ((nb4 >> q) & 1u) L = (L & ~(0xFFu << (8 * q))) | (2u << (8 * q));
+    const uint32_t off = r - v0;
+    if (off < 4u) L = (L & ~(0xFFu << (8u * off))) | (1u << (8u * off));
+    __builtin_nontemporal_store(L, reinterpret_cast<uint32_t*>(a.lev_w + (size_t)own * a.pitch + v0));
+    if (v0 >= V) continue;
+    uint32_t dv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t l = (L >> (8 * q)) & 0xFFu;
+      dv[q] = l < 0x7Fu ? l - 1u : kInf;
+      if (l < 0x7Fu && v0 + q < V) {
+        br += 1u;
+        bs += l - 1u;
+        bh += g.dkey[2ull * (v0 + q)] * (uint64_t)l;
+      }
+    }
+    if (a.dist) {
+      uint32_t* drow = a.dist + (size_t)own * V + v0;
+      if (vec) {
+        store_row16(drow, make_uint4(dv[0], dv[1], dv[2], dv[3]));
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (v0 + q < V) drow[q] = dv[q];
+      }
+    }
+  }
+  if (a.lev_digest_w) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      br += shfl_xor64(br, o);
+      bs += shfl_xor64(bs, o);
+      bh += shfl_xor64(bh, o);
+    }
+    if (lane == 0) {
+      s_r[wave] = br;
+      s_s[wave] = bs;
+      s_hh[wave] = bh;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      ospf_digest d{0ull, 0ull, 0ull};
+      for (uint32_t w = 0; w < kWaves; ++w) {
+        d.reached += s_r[w];
+        d.sum_dist += s_s[w];
+        d.hash += s_hh[w];
+      }
+      a.lev_digest_w[own] = d;
+    }
+  }
+}
+
 }  // namespace
 
 hipError_t launch_nh_derive_twin(const DevGraph& g, const TwinArgs& a0, hipStream_t s) {
@@ -342,4 +475,18 @@ hipError_t launch_nh_derive_twin(const DevGraph& g, const TwinArgs& a0, hipStrea
   return hipGetLastError();
 }
 
+}  // namespace ospf
+
+namespace ospf {
+hipError_t launch_twin_levels(const DevGraph& g, const TwinArgs& a, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
+  const size_t lds = 4ull * ((a.pitch + 31u) / 32u);
+  if (lds > 64u * 1024u) {
+    const hipError_t e = hipFuncSetAttribute((const void*)twin_levels_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(twin_levels_kernel, dim3(a.n), dim3(kBlock), lds, s, g, a);
+  return hipGetLastError();
+}
 }  // namespace ospf

@@ -41,3 +41,15 @@ def drained_fabric(pods, planes, seed=0, drain=0.05, down=0.03, weighted_seed=No
             if rng.random() < down:
                 a.overloaded = True
     return AdjDbStream.from_dbs(dbs)
+
+
+def path_dbs(n):
+    """A path p000 - p001 - ... of n nodes with unit metrics: n - 1 levels
+    deep from either end (names sort in path order)."""
+    names = [f"p{i:04d}" for i in range(n)]
+    adjs = {nm: [] for nm in names}
+    for i in range(n - 1):
+        a, b = names[i], names[i + 1]
+        adjs[a].append(create_adjacency(b, f"{a}-{b}", f"{b}-{a}", 1))
+        adjs[b].append(create_adjacency(a, f"{b}-{a}", f"{a}-{b}", 1))
+    return [AdjDb(nm, adjs[nm], i + 1) for i, nm in enumerate(names)]

@@ -69,11 +69,13 @@ def test_sweep_random_unit_graphs_every_mode(seed):
     stream, _ = random_stream(seed, n=70, unit=True)
     _, _, eng = engine_for(stream)
     try:
-        assert check_sweep_vs_batch(eng, "auto") == "derive"
-        for mode in ("derive", "wderive", "batch"):
+        assert check_sweep_vs_batch(eng, "auto") == "lds"  # a small graph: the LDS sweep
+        for mode in ("derive", "wderive", "batch", "lds"):
             check_sweep_vs_batch(eng, mode)
         check_sweep_vs_batch(eng, "derive", hip_graph=False)
+        check_sweep_vs_batch(eng, "lds", hip_graph=False)
         check_sweep_vs_batch(eng, "auto", hop=True)
+        check_sweep_vs_batch(eng, "derive", hop=True)
     finally:
         eng.close()
 
@@ -91,7 +93,10 @@ def test_sweep_random_weighted_graphs_every_mode(seed):
             check_sweep_vs_batch(eng, "wcover")
         except EngineError as e:  # outside the cover kernel's limits
             assert e.code == -4, e
-        check_sweep_vs_batch(eng, "auto", hop=True)  # hop count: derive on any metric
+        check_sweep_vs_batch(eng, "auto", hop=True)  # hop count: lds / derive on any metric
+        check_sweep_vs_batch(eng, "lds", hop=True)
+        with pytest.raises(EngineError):  # link metrics != 1: not the LDS kernel's contract
+            Sweep(eng, mode="lds")
     finally:
         eng.close()
 
@@ -102,15 +107,17 @@ def test_sweep_fabric_with_drains_vs_oracle():
     st = drained_fabric(6, 4, seed=3)
     ls, csr, eng = engine_for(st)
     try:
-        assert check_sweep_vs_batch(eng, "auto", rows_for=np.arange(0, eng.V, 7)) == "derive"
+        assert check_sweep_vs_batch(eng, "auto", rows_for=np.arange(0, eng.V, 7)) == "lds"
+        check_sweep_vs_batch(eng, "derive", rows_for=np.arange(0, eng.V, 7))
         names = ls.node_names()
-        sw = Sweep(eng)
-        sw.run()
-        got = sweep_digests(sw)
         want = Oracle(st).fast_digests(names)
-        for r in range(eng.V):
-            assert np.array_equal(got[r], want[r]), names[r]
-        sw.close()
+        for mode in ("lds", "derive"):
+            sw = Sweep(eng, mode=mode)
+            sw.run()
+            got = sweep_digests(sw)
+            for r in range(eng.V):
+                assert np.array_equal(got[r], want[r]), (mode, names[r])
+            sw.close()
     finally:
         eng.close()
 
@@ -151,11 +158,12 @@ def test_sweep_deep_unit_grid_does_not_raise():
         eng.close()
 
 
-def test_sweep_poison_and_profile():
+@pytest.mark.parametrize("mode", ["derive", "lds"])
+def test_sweep_poison_and_profile(mode):
     st = T.fabric(pods=4, planes=4)
     ls, csr, eng = engine_for(st)
     try:
-        sw = Sweep(eng)
+        sw = Sweep(eng, mode=mode)
         sw.run()
         eng.sync()
         good = sweep_digests(sw)
@@ -168,7 +176,7 @@ def test_sweep_poison_and_profile():
         again = sweep_digests(sw)
         assert all(np.array_equal(good[r], again[r]) for r in good)
         prof = sw.profile(2)
-        assert [p["name"] for p in prof][0] == "levels"
+        assert prof[0]["name"] == "levels" if mode == "derive" else prof[0]["name"].startswith("lds_w")
         assert all(p["ms_median"] > 0 and p["compulsory_bytes"] > 0 for p in prof)
         assert sw.step_compulsory_bytes == sum(p["compulsory_bytes"] for p in prof)
         sw.close()
@@ -176,11 +184,12 @@ def test_sweep_poison_and_profile():
         eng.close()
 
 
-def test_sweep_partition_parts_cover_every_root_once():
+@pytest.mark.parametrize("mode", ["auto", "derive"])
+def test_sweep_partition_parts_cover_every_root_once(mode):
     st = T.fabric(pods=9, planes=4)
     ls, csr, eng = engine_for(st)
     try:
-        full = Sweep(eng)
+        full = Sweep(eng, mode=mode)
         full.run()
         want = sweep_digests(full)
         full.close()
@@ -188,12 +197,13 @@ def test_sweep_partition_parts_cover_every_root_once():
         for n_parts in (2, 3):
             seen.clear()
             for p in range(n_parts):
-                sw = Sweep(eng, part=p, n_parts=n_parts)
+                sw = Sweep(eng, part=p, n_parts=n_parts, mode=mode)
                 sw.run()
                 for r, d in sweep_digests(sw).items():
                     assert r not in seen
                     seen[r] = d
-                assert sw.n_rows <= 1.6 * max(1, sw.n_roots) + 64
+                # closure rows (+ the BFS'd leaf representatives of twin levels)
+                assert sw.n_rows <= 1.6 * max(1, sw.n_roots) + 64 + (9 if mode == "derive" else 0)
                 sw.close()
             assert len(seen) == eng.V
             assert all(np.array_equal(seen[r], want[r]) for r in range(eng.V))
@@ -201,15 +211,16 @@ def test_sweep_partition_parts_cover_every_root_once():
         eng.close()
 
 
-@pytest.mark.parametrize("topo", ["unit", "weighted"])
+@pytest.mark.parametrize("topo", ["unit", "weighted", "unit-derive"])
 def test_multi_device_context_two_slots_on_device0(topo):
     """ospf_multi with two contexts on device 0: parts on each slot, digests
     gathered by peer copies (same-device copies here; RCCL / xGMI across
     devices is unexercised until a multi-GPU node runs it)."""
     st = T.fabric(pods=6, planes=4, weighted_seed=7 if topo == "weighted" else None)
+    mode = "derive" if topo == "unit-derive" else "auto"
     ls, csr, eng = engine_for(st)
     try:
-        full = Sweep(eng)
+        full = Sweep(eng, mode=mode)
         full.run()
         want = sweep_digests(full)
         full.close()
@@ -218,7 +229,7 @@ def test_multi_device_context_two_slots_on_device0(topo):
     m = Multi([0, 0])
     try:
         m.load(csr)
-        ms = MultiSweep(m)
+        ms = MultiSweep(m, mode=mode)
         ms.run()
         got = ms.digests()
         for r in range(m.V):
@@ -238,7 +249,7 @@ def test_linkstate_all_sources_uses_the_sweep():
     runs0 = p.spf_runs
     d_all = p.all_sources_digests()
     st_ = p.sweep_stats()
-    assert st_["sweeps"] == 1 and st_["mode"] == "derive"
+    assert st_["sweeps"] == 1 and st_["mode"] in ("lds", "derive")
     assert p.spf_runs - runs0 == len(names)
     q = LinkState(stream=st)
     d_batch = q.digests(names)
@@ -342,5 +353,127 @@ def test_twin_derive_forced_on_random_and_drained_graphs(seed, monkeypatch):
     _, _, eng = engine_for(AdjDbStream.from_dbs(dbs))
     try:
         check_sweep_vs_batch(eng, "derive")
+    finally:
+        eng.close()
+
+
+def test_lds_sweep_grid31_every_root_vs_oracle():
+    """BASELINE config 2 (all-sources SPF + ECMP next hops on the ~1,000-node
+    grid, LDS-resident per-root work): the 31 x 31 grid's sweep takes the LDS
+    path in one launch; every one of the 961 roots' digests equals the
+    CSR-Dijkstra restatement, rows equal the batch path for a sample, and
+    the other sweep paths agree."""
+    st = T.grid(31)
+    ls, csr, eng = engine_for(st)
+    try:
+        sw = Sweep(eng)
+        assert sw.mode == "lds" and sw.n_launches == 1
+        sw.run()
+        eng.sync()
+        got = sweep_digests(sw)
+        names = ls.node_names()
+        want = Oracle(st).fast_digests(names)
+        bad = [names[r] for r in range(eng.V) if not np.array_equal(got[r], want[r])]
+        assert not bad, bad[:8]
+        sw.close()
+        check_sweep_vs_batch(eng, "lds", rows_for=np.arange(0, eng.V, 13))
+        check_sweep_vs_batch(eng, "derive", rows_for=np.arange(0, eng.V, 29))
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_lds_sweep_wide_rows_and_drains(seed):
+    """Spines with 40 distinct neighbours (2 next-hop words), drained switches
+    (overloaded nodes never relay) and down links: the LDS sweep == the batch
+    path bit for bit, dist and next-hop rows included, and == the CPU
+    restatement's digests."""
+    st = drained_fabric(40, 2, seed=seed, drain=0.06, down=0.04)
+    ls, csr, eng = engine_for(st)
+    try:
+        if not eng._L.ospf_lds_sweep_fits(eng._h, 0, 2):
+            pytest.skip("graph does not fit this device's LDS")
+        check_sweep_vs_batch(eng, "lds", rows_for=np.arange(0, eng.V, 5), want_mode="lds")
+        check_sweep_vs_batch(eng, "lds", hop=True, rows_for=np.arange(0, eng.V, 17))
+        names = ls.node_names()
+        want = Oracle(st).fast_digests(names)
+        sw = Sweep(eng, mode="lds")
+        sw.run()
+        got = sweep_digests(sw)
+        assert all(np.array_equal(got[r], want[r]) for r in range(eng.V))
+        sw.close()
+    finally:
+        eng.close()
+
+
+def test_lds_sweep_direct_abi_and_limits():
+    """ospf_lds_sweep_dev straight through the C ABI: a path graph deeper than
+    255 levels (u16 levels), a repeated root, nh_words wider than needed
+    (upper words zero), and OSPF_E_RANGE for a graph past the LDS budget."""
+    import torch
+    from openr_amd.adjdb import AdjDbStream
+    from graphs import path_dbs
+    st = AdjDbStream.from_dbs(path_dbs(600))
+    ls, csr, eng = engine_for(st)
+    try:
+        V = eng.V
+        dev = torch.device("cuda", 0)
+        roots = np.array([0, V - 1, 0, 299], np.uint32)
+        d_roots = torch.from_numpy(roots.view(np.int32)).to(dev)
+        dist = torch.empty((4, V), dtype=torch.int32, device=dev)
+        nh = torch.full((4, V, 2), -1, dtype=torch.int32, device=dev)
+        dg = torch.zeros((4, 3), dtype=torch.int64, device=dev)
+        rc = eng._L.ospf_lds_sweep_dev(eng._h, d_roots.data_ptr(), 4, 0, 2, dist.data_ptr(),
+                                       nh.data_ptr(), dg.data_ptr(), None)
+        assert rc == 0
+        eng.sync()
+        ref = eng.run(roots, 2, want_digest=True)
+        assert np.array_equal(dist.cpu().numpy().view(np.uint32), ref["dist"])
+        assert np.array_equal(nh.cpu().numpy().view(np.uint32), ref["nh"])
+        assert np.array_equal(dg.cpu().numpy().view(np.uint64), ref["digest"])
+        assert ref["dist"][1].max() == V - 1  # 599 levels deep
+    finally:
+        eng.close()
+    big = T.grid(100)
+    _, _, eng = engine_for(big)
+    try:
+        assert not eng._L.ospf_lds_sweep_fits(eng._h, 0, 1)
+        with pytest.raises(EngineError):
+            Sweep(eng, mode="lds")
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_twin_levels_forced_and_off(seed, monkeypatch):
+    """ospf_twin_levels_dev inside the derive sweep (fabric switches' rows
+    from a rack row of their pod and a spine row of their plane): forced on
+    (OSPF_SWEEP_TWINLV=1) for drained fabrics and random graphs, and turned
+    off (OSPF_SWEEP_NOTWINLV=1): both == the batch path bit for bit, and ==
+    the CPU restatement's digests on the fabric."""
+    st = drained_fabric(7, 4, seed=seed + 3, drain=0.07, down=0.05)
+    for env in ("OSPF_SWEEP_TWINLV", "OSPF_SWEEP_NOTWINLV"):
+        monkeypatch.setenv(env, "1")
+        ls, csr, eng = engine_for(st)
+        try:
+            check_sweep_vs_batch(eng, "derive", rows_for=np.arange(0, eng.V, 3))
+            names = ls.node_names()
+            want = Oracle(st).fast_digests(names)
+            sw = Sweep(eng, mode="derive")
+            sw.run()
+            got = sweep_digests(sw)
+            assert all(np.array_equal(got[r], want[r]) for r in range(eng.V)), env
+            if env == "OSPF_SWEEP_TWINLV":
+                assert "twin_levels" in [p["name"] for p in sw.profile(1)]
+            sw.close()
+        finally:
+            eng.close()
+        monkeypatch.delenv(env)
+    monkeypatch.setenv("OSPF_SWEEP_TWINLV", "1")
+    stream, _ = random_stream(seed + 40, n=80, unit=True, p=0.1)
+    _, _, eng = engine_for(stream)
+    try:
+        check_sweep_vs_batch(eng, "derive")
+        check_sweep_vs_batch(eng, "derive", hop=True)
     finally:
         eng.close()
