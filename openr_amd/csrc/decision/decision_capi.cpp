@@ -124,6 +124,40 @@ int odl_apply(odl_ls* h, const oadj_stream* s, uint32_t first, uint32_t count,
               oadj_change* changes) {
   return guard(h, [&]() -> int {
     if (!s) throw std::invalid_argument("null stream");
+    bool deletes = false;
+    for (uint32_t k = 0; k < count && s->db_delete; ++k)
+      deletes |= first + k < s->n_dbs && s->db_delete[first + k];
+    if (!deletes && count >= 64 && first + count <= s->n_dbs) {
+      // a batch of updates: databases built on host threads, then applied in
+      // order (LinkState::updateAdjacencyDatabases: in parallel when every
+      // database is a new node)
+      std::vector<odl::AdjacencyDatabase> dbs(count);
+      odl::parallelFor(count, [&](uint32_t lo, uint32_t hi) {
+        for (uint32_t k = lo; k < hi; ++k) {
+          const uint32_t i = first + k;
+          odl::AdjacencyDatabase& db = dbs[k];
+          db.thisNodeName = at(s, s->db_name[i]);
+          db.isOverloaded = s->db_overloaded[i] != 0;
+          db.nodeLabel = s->db_node_label[i];
+          db.adjacencies.resize(s->db_adj_off[i + 1] - s->db_adj_off[i]);
+          for (uint64_t a = s->db_adj_off[i]; a < s->db_adj_off[i + 1]; ++a) {
+            odl::Adjacency& x = db.adjacencies[a - s->db_adj_off[i]];
+            x.otherNodeName = at(s, s->adj_other[a]);
+            x.ifName = at(s, s->adj_if[a]);
+            x.otherIfName = at(s, s->adj_other_if[a]);
+            x.metric = s->adj_metric[a];
+            x.adjLabel = s->adj_label[a];
+            x.isOverloaded = s->adj_overloaded[a] != 0;
+            x.weight = s->adj_weight[a];
+          }
+        }
+      }, 256);
+      const auto chs = h->ls.updateAdjacencyDatabases(dbs);
+      for (uint32_t k = 0; changes && k < count; ++k)
+        changes[k] = oadj_change{chs[k].topologyChanged, chs[k].linkAttributesChanged,
+                                 chs[k].nodeLabelChanged, (int32_t)chs[k].addedLinks.size()};
+      return 0;
+    }
     for (uint32_t k = 0; k < count; ++k) {
       const uint32_t i = first + k;
       if (i >= s->n_dbs) throw std::out_of_range("stream index");

@@ -315,6 +315,141 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db) 
   return ch;
 }
 
+// Bulk path: every database is a node not yet known. Such a node has no
+// links before its own update (a link needs both databases), and its update
+// creates the links to the nodes known by then -- before the batch, earlier
+// in it, or itself -- in Link order, inserted into the low then the high
+// node's LinkSet and into allLinks_. Built here: databases and adjacency
+// indexes per node in parallel, each node's created links in parallel (the
+// indexes are only read), then every node's LinkSet filled in parallel with
+// its links in the sequential insertion order (creation order), so each
+// unordered_set ends up with the same buckets and iteration order.
+std::vector<LinkStateChange> LinkState::updateAdjacencyDatabases(std::vector<AdjacencyDatabase>& dbs) {
+  const uint32_t n = (uint32_t)dbs.size();
+  std::vector<LinkStateChange> out(n);
+  bool bulk = n >= 64 && !getenv("ODL_NO_BULK_INGEST");
+  std::unordered_map<std::string, uint32_t> posOf;
+  if (bulk) {
+    posOf.reserve(n);
+    for (uint32_t i = 0; i < n && bulk; ++i)
+      bulk = !adjDbs_.count(dbs[i].thisNodeName) && posOf.emplace(dbs[i].thisNodeName, i).second;
+  }
+  if (!bulk) {
+    for (uint32_t i = 0; i < n; ++i) out[i] = updateAdjacencyDatabase(dbs[i]);
+    return out;
+  }
+  using Clock = std::chrono::steady_clock;
+  const bool timing = getenv("ODL_SPF_TIMING") != nullptr;
+  Clock::time_point tp[6];
+  tp[0] = Clock::now();
+  std::vector<AdjacencyDatabase*> dbp(n);
+  std::vector<std::unordered_map<std::string, uint32_t>*> idxp(n);
+  // (no order of these maps or of allLinks_ is observed: node ids are name
+  // ranks; only the per-node LinkSets' iteration order is, and those are not
+  // reserved)
+  adjDbs_.reserve(adjDbs_.size() + n);
+  adjIndex_.reserve(adjIndex_.size() + n);
+  nodeOverloads_.reserve(nodeOverloads_.size() + n);
+  linkMap_.reserve(linkMap_.size() + n);
+  for (uint32_t i = 0; i < n; ++i) {
+    const std::string me = dbs[i].thisNodeName;
+    nodeOverloads_.emplace(me, dbs[i].isOverloaded);  // a new node is not a change
+    out[i].nodeLabelChanged = dbs[i].nodeLabel != 0;
+    AdjacencyDatabase& slot = adjDbs_[me];
+    slot = std::move(dbs[i]);
+    dbp[i] = &slot;
+    idxp[i] = &adjIndex_[me];
+  }
+  parallelFor(n, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t i = lo; i < hi; ++i) {
+      auto& idx = *idxp[i];
+      idx.clear();
+      const auto& adj = dbp[i]->adjacencies;
+      for (uint32_t k = 0; k < adj.size(); ++k)
+        idx.emplace(tripleKey(adj[k].otherNodeName, adj[k].ifName, adj[k].otherIfName), k);
+    }
+  }, 256);
+  // links each update creates, in Link order
+  tp[1] = Clock::now();
+  // (link, batch position of its other end or kNone) per update
+  std::vector<std::vector<std::pair<LinkPtr, uint32_t>>> created(n);
+  parallelFor(n, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t i = lo; i < hi; ++i) {
+      const AdjacencyDatabase& db = *dbp[i];
+      auto& v = created[i];
+      for (const auto& a : db.adjacencies) {
+        auto p = posOf.find(a.otherNodeName);
+        if (p != posOf.end() && p->second > i) continue;  // created by that node's update
+        if (LinkPtr l = makeLink(db.thisNodeName, a))
+          v.emplace_back(std::move(l), p != posOf.end() ? p->second : kInf);
+      }
+      std::sort(v.begin(), v.end(), [](const auto& a, const auto& b) {
+        return a.first->orderedBefore(*b.first);
+      });
+    }
+  }, 256);
+  tp[2] = Clock::now();
+  // every touched node's insertions in creation order (low end, then high)
+  std::unordered_map<std::string, uint32_t> other;  // nodes known before the batch
+  std::vector<std::vector<LinkPtr>> ins(n);
+  bool anyTopo = false;
+  for (uint32_t i = 0; i < n; ++i) {
+    out[i].addedLinks.reserve(created[i].size());
+    for (auto& c : created[i]) {
+      const LinkPtr& l = c.first;
+      if (c.second == i) throw std::logic_error("duplicate link " + l->key());  // a self-link
+      uint32_t o = c.second;
+      if (o == kInf) {
+        auto q = other.emplace(l->otherNode(dbp[i]->thisNodeName), (uint32_t)ins.size());
+        if (q.second) ins.emplace_back();
+        o = q.first->second;
+      }
+      const bool meLow = l->lowNode() == dbp[i]->thisNodeName;
+      ins[meLow ? i : o].push_back(l);
+      ins[meLow ? o : i].push_back(l);
+      out[i].topologyChanged |= l->isUp();
+      out[i].addedLinks.push_back(std::move(c.first));
+    }
+    anyTopo |= out[i].topologyChanged;
+    created[i].clear();
+  }
+  tp[3] = Clock::now();
+  std::vector<LinkSet*> setp(ins.size());
+  for (uint32_t i = 0; i < n; ++i) setp[i] = &linkMap_[dbp[i]->thisNodeName];
+  for (const auto& o : other) setp[o.second] = &linkMap_[o.first];
+  std::atomic<bool> dup{false};
+  size_t added = 0;
+  for (uint32_t i = 0; i < n; ++i) added += out[i].addedLinks.size();
+  allLinks_.reserve(allLinks_.size() + added);
+  std::thread all([&] {  // allLinks_ in creation order, beside the per-node sets
+    for (uint32_t i = 0; i < n; ++i)
+      for (const LinkPtr& l : out[i].addedLinks)
+        if (!allLinks_.insert(l).second) dup = true;
+  });
+  try {
+    parallelFor((uint32_t)ins.size(), [&](uint32_t lo, uint32_t hi) {
+      for (uint32_t u = lo; u < hi; ++u)
+        for (const LinkPtr& l : ins[u])
+          if (!setp[u]->insert(l).second) dup = true;
+    }, 256);
+  } catch (...) {
+    all.join();
+    throw;
+  }
+  all.join();
+  tp[4] = Clock::now();
+  if (timing) {
+    auto ms = [&](int a) { return std::chrono::duration<double, std::milli>(tp[a + 1] - tp[a]).count(); };
+    std::fprintf(stderr, "ODL_INGEST dbs=%u index_ms=%.1f links_ms=%.1f order_ms=%.1f sets_ms=%.1f\n",
+                 n, ms(0), ms(1), ms(2), ms(3));
+  }
+  if (dup) throw std::logic_error("duplicate link in an adjacency database batch");
+  // one version step per database, as in turn (a new node is structural)
+  version_ += n - (anyTopo ? 1u : 0u);
+  if (anyTopo) invalidate();
+  return out;
+}
+
 LinkStateChange LinkState::deleteAdjacencyDatabase(const std::string& node) {
   LinkStateChange ch;
   auto db = adjDbs_.find(node);

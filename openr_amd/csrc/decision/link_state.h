@@ -221,6 +221,12 @@ class LinkState {
 
   LinkStateChange updateAdjacencyDatabase(const AdjacencyDatabase& db);
   LinkStateChange deleteAdjacencyDatabase(const std::string& node);
+  // A batch of databases in order (Decision's debounced batch,
+  // Decision.cpp:731-765; the initial sync delivers the whole area): the same
+  // state and change records as updateAdjacencyDatabase on each in turn. A
+  // batch of nodes not yet known (no name twice) is built with host threads.
+  // The databases are moved from.
+  std::vector<LinkStateChange> updateAdjacencyDatabases(std::vector<AdjacencyDatabase>& dbs);
 
   const LinkSet& linksFromNode(const std::string& node) const;
   bool isNodeOverloaded(const std::string& node) const;

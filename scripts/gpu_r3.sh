@@ -55,6 +55,16 @@ for st in $STEPS; do
              python scripts/sweep_unit_stats.py --bench "$OUT/utrace_serial_bench.json" --trace "$OUT/utrace_serial" --reps 3 --out "$OUT/units_trace_serial.json" &&
              python scripts/sweep_unit_stats.py --bench "$OUT/upmc1.json" --pmc "$OUT/upmc1" "$OUT/upmc2" --reps 1 --out "$OUT/pmc_traffic.json"; rc=$?
            fi;;
+    ab)    # A/B of env knobs on the default bench: AB="NAME=1 OTHER=1 ..." (one run each + baseline)
+           rc=0
+           for kv in base ${AB:-}; do
+             if [ "$kv" = base ]; then E=""; else E="$kv"; fi
+             timeout -k 10 300 env $E python bench.py --steps 20 --warmup 2 --cpu-sample 8 --iso-reps 2 ${AB_ARGS:-} > "$OUT/ab_$kv.json" 2> "$OUT/ab_$kv.err"; rc=$?
+             echo "ab $kv rc=$rc $(python -c "import json,sys; d=json.load(open('$OUT/ab_$kv.json')); print(d['value'], d['ms_per_step'], d['parity_vs_cpu_sample'])" 2>/dev/null)"
+             [ $rc -eq 0 ] || break
+           done;;
+    derive) timeout -k 10 600 $PYT tests/test_gpu_derive.py tests/test_gpu_wderive.py > "$OUT/derive.log" 2>&1; rc=$?
+           tail -3 "$OUT/derive.log";;
     *) echo "unknown step $st"; rc=2;;
   esac
   echo "step $st rc=$rc"
