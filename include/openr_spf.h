@@ -227,9 +227,14 @@ int ospf_nh_derive_twin_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n, 
  * (d_dist + d_pos[r] * V; NULL = not wanted) and the distance part of its
  * digest (d_lev_digest[d_pos[r]], stored; NULL = not wanted). Error bits at
  * ospf_sync: 1 (> 128 distinct neighbours), 16 (a class row missing), 256
- * (> 16 classes). On a fabric the fabric switches' rows come from one rack
- * row of their pod and one spine row of their plane. */
-int ospf_twin_levels_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n, uint8_t* d_lev,
+ * (> 16 classes, or > 16 distinct class rows in a group). d_groups
+ * [n_groups + 1]: offsets into the roots, <= 8 roots per group, the roots of
+ * a group reading <= 16 class rows together (each chunk's rows loaded once
+ * for the group); NULL = one root per group. On a fabric the fabric
+ * switches' rows come from one rack row of their pod and one spine row of
+ * their plane (group = a pod's fabric switches). */
+int ospf_twin_levels_dev(ospf_ctx* ctx, const uint32_t* d_roots, uint32_t n,
+                         const uint32_t* d_groups, uint32_t n_groups, uint8_t* d_lev,
                          uint32_t lev_pitch, const uint32_t* d_pos, const uint32_t* d_twin_class,
                          const uint32_t* d_twin_rep, uint32_t* d_dist, ospf_digest* d_lev_digest,
                          void* stream);

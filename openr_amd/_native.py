@@ -163,7 +163,7 @@ def engine() -> C.CDLL:
         L.ospf_leaf_derive_dev.argtypes = [vp, vp, u32, vp, u32, u32, vp, u32, vp, vp, vp, vp, vp]
         L.ospf_lds_sweep_dev.argtypes = [vp, vp, u32, u32, u32, vp, vp, vp, vp]
         L.ospf_lds_sweep_fits.argtypes = [vp, u32, u32]
-        L.ospf_twin_levels_dev.argtypes = [vp, vp, u32, vp, u32, vp, vp, vp, vp, vp, vp]
+        L.ospf_twin_levels_dev.argtypes = [vp, vp, u32, vp, u32, vp, u32, vp, vp, vp, vp, vp, vp]
         L.ospf_leaf_derive2_dev.argtypes = [vp, vp, u32, vp, u32, u32, vp, u32, vp, vp, vp, vp,
                                             vp, vp]
         L.ospf_wderive_dev.argtypes = [vp, vp, u32, u32, u32, vp, u64, vp, vp, vp, vp, vp]

@@ -1377,7 +1377,8 @@ int ospf_nh_derive_twin_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, ui
 
 // Twin levels (spf_twin.hip): level + dist rows of roots from the
 // representative rows of their neighbours' twin classes (no traversal).
-int ospf_twin_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint8_t* d_lev,
+int ospf_twin_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n,
+                         const uint32_t* d_groups, uint32_t n_groups, uint8_t* d_lev,
                          uint32_t lev_pitch, const uint32_t* d_pos, const uint32_t* d_twin_class,
                          const uint32_t* d_twin_rep, uint32_t* d_dist, ospf_digest* d_lev_digest,
                          void* stream) {
@@ -1403,6 +1404,9 @@ int ospf_twin_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint8
   a.tcls = d_twin_class;
   a.trep = d_twin_rep;
   a.tsec = nullptr;
+  a.grp = d_groups;
+  a.ngroups = d_groups ? n_groups : n;
+  if (d_groups && n_groups == 0) return fail(c, OSPF_E_INVAL, "twin levels: no groups");
   a.dist = d_dist;
   a.lev_digest_w = d_lev_digest;
   a.err = c->d_err;

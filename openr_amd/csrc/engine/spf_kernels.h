@@ -317,6 +317,8 @@ struct TwinArgs {
   uint32_t* err;          // + bit 256: a root with more than kTwinMaxC classes
   uint32_t tiles, ctiles, chunks;
   // twin_levels_kernel: the roots' own rows at pos[root]
+  const uint32_t* grp;        // [ngroups + 1] root groups (<= 8 roots, <= 16 class rows each) or null
+  uint32_t ngroups;
   uint8_t* lev_w;             // level rows written (same buffer as lev)
   uint32_t* dist;             // [rows][V] or null
   ospf_digest* lev_digest_w;  // [rows] distance parts (stored) or null

@@ -1745,188 +1745,6 @@ __global__ void __launch_bounds__(256) nh_derive_wide_kernel(DevGraph g, DeriveA
 }
 
 
-// Wide rows, v2 (W > 4 words: spines). Block = up to kWideG consecutive
-// roots x a chunk of 256-node tiles, wave = 64 nodes, lane = one node. For a
-// run of roots with the same distinct-neighbour list (the spines of one
-// plane) the words of the run's first root are computed once per tile --
-// for each slot a one-byte load per lane, so a wave reads 64 consecutive
-// level bytes of each neighbour row (every row's tile bytes cross L2 once) --
-// and staged in LDS [node][word]. Each root of the run then stores the
-// staged words masked by its usable links, one coalesced pass over the
-// wave's 64 x W words (64 W consecutive words of the row); at the few nodes
-// where its own level differs from the first root's (the run's members
-// themselves) the pass recomputes the word from the slot bytes.
-__global__ void __launch_bounds__(256) nh_derive_wide2_kernel(DevGraph g, DeriveArgs d) {
-  __shared__ uint32_t s_pos[kDeriveTab];  // slot table of the current run
-  __shared__ uint32_t s_root[kWideG], s_own[kWideG], s_K[kWideG], s_same[kWideG];
-  __shared__ unsigned long long s_h[kWideG];
-  extern __shared__ uint32_t s_dyn[];     // keep [G][W], then stage [4 waves][64 nodes][W]
-  const uint32_t V = g.V, W = d.W, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const uint32_t G = d.G, cap = d.cap;
-  const uint32_t Wp = W | 1u;  // odd stage pitch: a lane per node writes conflict-free
-  uint32_t* s_keep = s_dyn;
-  uint32_t* st = s_dyn + G * W + wave * 64u * Wp;
-  const uint32_t ngroups = (d.n + G - 1) / G;
-  const uint32_t ci = blockIdx.x / ngroups, rr = blockIdx.x % ngroups;
-  const uint32_t full = ngroups / 8u * 8u;
-  const uint32_t gi = rr < full ? (rr % 8u) * (full / 8u) + rr / 8u : rr;
-  const uint32_t i0 = gi * G, ng = min(G, d.n - i0);
-  if (tid < ng) {
-    const uint32_t r = d.roots[i0 + tid];
-    s_root[tid] = r;
-    s_h[tid] = 0ull;
-    s_own[tid] = kInf;
-    s_K[tid] = 0;
-    if (r >= V) {
-      atomicOr(d.err, 64u);
-    } else {
-      const uint32_t K = g.dn_off[r + 1] - g.dn_off[r];
-      s_own[tid] = d.pos[r];
-      if (K > cap || K > 32u * W || s_own[tid] == kInf)
-        atomicOr(d.err, s_own[tid] == kInf ? 16u : 1u);
-      if (s_own[tid] != kInf) s_K[tid] = min(K, cap);
-    }
-  }
-  for (uint32_t x = tid; x < ng * W; x += kBlock) s_keep[x] = 0u;
-  __syncthreads();
-  if (tid < ng)
-    s_same[tid] = tid > 0 && s_own[tid] != kInf && s_own[tid - 1] != kInf &&
-                  s_K[tid] == s_K[tid - 1];
-  for (uint32_t j = 0; j < ng; ++j) {
-    const uint32_t r = s_root[j];
-    if (r >= V || s_own[j] == kInf) continue;
-    for (uint32_t e = g.row_ptr[r] + tid; e < g.row_ptr[r + 1]; e += kBlock) {
-      const uint32_t cx = g.colx[e];
-      if ((cx & kDown) || cx == r) continue;
-      const uint32_t k = g.didx[e];
-      if (k < s_K[j]) atomicOr(&s_keep[j * W + (k >> 5)], 1u << (k & 31u));
-    }
-  }
-  __syncthreads();
-  for (uint32_t j = 1; j < ng; ++j) {
-    if (!s_same[j]) continue;
-    const uint32_t* a0 = g.dn + g.dn_off[s_root[j - 1]];
-    const uint32_t* a1 = g.dn + g.dn_off[s_root[j]];
-    for (uint32_t k = tid; k < s_K[j]; k += kBlock)
-      if (a0[k] != a1[k]) s_same[j] = 0u;  // benign race: every writer stores 0
-  }
-  __syncthreads();
-  // word w of node v for a root whose level there is L (slot table s_pos):
-  // bit i = slot 32 w + i is a next hop (its row one level closer, or the
-  // neighbour itself when it does not relay)
-  auto word_at = [&](uint32_t v, uint32_t w, uint32_t L, uint32_t K) {
-    uint32_t word = 0;
-    if (L < 2u || L >= 0x7Fu) return word;
-    for (uint32_t i = 0; i < 32u; ++i) {
-      const uint32_t k = 32u * w + i;
-      if (k >= K) break;
-      const uint32_t p = s_pos[k];
-      if (p == kInf) continue;
-      const bool hit = p < 0x80000000u ? d.lev[(size_t)p * d.pitch + v] + 1u == L
-                                       : ((p & 0x7FFFFFFFu) == v && L == 2u);
-      word |= (hit ? 1u : 0u) << i;
-    }
-    return word;
-  };
-  const uint32_t t0 = ci * d.ctiles, t1 = min(d.tiles, t0 + d.ctiles);
-  for (uint32_t j0 = 0; j0 < ng;) {
-    uint32_t j1 = j0 + 1;
-    while (j1 < ng && s_same[j1]) ++j1;
-    const uint32_t K = s_K[j0];
-    if (s_own[j0] == kInf) {  // a bad root (error flagged): its own run
-      j0 = j1;
-      continue;
-    }
-    __syncthreads();  // the previous run is done with s_pos
-    for (uint32_t k = tid; k < K; k += kBlock) {
-      bool used = false;
-      for (uint32_t j = j0; j < j1 && !used; ++j) used = (s_keep[j * W + (k >> 5)] >> (k & 31u)) & 1u;
-      uint32_t p = kInf;
-      if (used) {
-        const uint32_t n = g.dn[g.dn_off[s_root[j0]] + k];
-        if (transit(g, n)) {
-          p = d.pos[n];
-          if (p == kInf) atomicOr(d.err, 16u);
-        } else {
-          p = 0x80000000u | n;
-        }
-      }
-      s_pos[k] = p;
-    }
-    __syncthreads();
-    const uint32_t own0 = s_own[j0];
-    for (uint32_t t = t0; t < t1; ++t) {
-      const uint32_t vb = t * kWideTile + wave * 64u;  // this wave's 64 nodes
-      if (vb >= V) break;                               // wave-uniform
-      const uint32_t v = vb + lane;
-      const bool live = v < V;
-      const uint32_t vs = live ? v : vb;
-      const uint32_t L0 = d.lev[(size_t)own0 * d.pitch + vs];
-      // the first root's words, staged [node][word]
-      for (uint32_t w = 0; w < W; ++w) {
-        uint32_t word = 0;
-        if (L0 >= 2u && L0 < 0x7Fu) {
-#pragma unroll 8
-          for (uint32_t i = 0; i < 32u; ++i) {
-            const uint32_t k = 32u * w + i;
-            const uint32_t p = k < K ? s_pos[k] : kInf;  // wave-uniform
-            bool hit = false;
-            if (p < 0x80000000u) hit = d.lev[(size_t)p * d.pitch + vs] + 1u == L0;
-            else if (p != kInf) hit = (p & 0x7FFFFFFFu) == v && L0 == 2u;
-            word |= (hit ? 1u : 0u) << i;
-          }
-        }
-        st[lane * Wp + w] = word;
-      }
-      __builtin_amdgcn_wave_barrier();
-      const uint32_t nv = min(64u, V - vb);
-      for (uint32_t j = j0; j < j1; ++j) {
-        const uint32_t Lj = j == j0 ? L0 : d.lev[(size_t)s_own[j] * d.pitch + vs];
-        const uint64_t diff = __ballot(live && Lj != L0);
-        uint32_t* dst = d.nh + ((size_t)(i0 + j) * V + vb) * W;
-        uint64_t h = 0;
-        const uint32_t dn = 64u / W, dw = 64u % W;
-        uint32_t node = lane / W, w = lane % W;
-        for (uint32_t x = lane; x < nv * W; x += 64u) {
-          uint32_t word = st[node * Wp + w];
-          if ((diff >> node) & 1ull) {
-            const uint32_t Lx = d.lev[(size_t)s_own[j] * d.pitch + vb + node];
-            word = word_at(vb + node, w, Lx, K);
-          }
-          word &= s_keep[j * W + w];
-          __builtin_nontemporal_store(word, dst + x);
-          if (d.digest && word) h += g.dkn[vb + node] * digest_word_key(w, word);
-          node += dn;
-          w += dw;
-          if (w >= W) {
-            w -= W;
-            ++node;
-          }
-        }
-        if (d.digest) {
-#pragma unroll
-          for (int o = 32; o > 0; o >>= 1) h += shfl_xor64(h, o);
-          if (lane == 0 && h) atomicAdd(&s_h[j], (unsigned long long)h);
-        }
-      }
-      __builtin_amdgcn_wave_barrier();  // the stage is rewritten by the next tile
-    }
-    j0 = j1;
-  }
-  __syncthreads();
-  if (d.digest && tid < ng) {
-    ospf_digest* dg = d.digest + i0 + tid;
-    unsigned long long h = s_h[tid];
-    if (ci == 0 && s_own[tid] != kInf) {
-      const ospf_digest ld = d.lev_digest[s_own[tid]];
-      atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)ld.reached);
-      atomicAdd((unsigned long long*)&dg->sum_dist, (unsigned long long)ld.sum_dist);
-      h += ld.hash;
-    }
-    if (h) atomicAdd((unsigned long long*)&dg->hash, h);
-  }
-}
-
 // ---------------------------------------------------------------- digest
 // Digest of finished rows (runs whose rows are written per level): `segs`
 // workgroups per root, each over a node range, adding into a zeroed record.
@@ -2157,21 +1975,10 @@ hipError_t launch_nh_derive(const DevGraph& g, const DeriveArgs& d0, hipStream_t
     if (const char* e = getenv("OSPF_DERIVE_WIDE_G"))
       d.G = std::max<uint32_t>(1, std::min<uint32_t>(kWideG, (uint32_t)atoi(e)));
     d.tiles = (g.V + kWideTile - 1) / kWideTile;
-    const bool v1 = getenv("OSPF_DERIVE_WIDE1") != nullptr;  // lane = word (round 2)
-    d.ctiles = std::max<uint32_t>(1, std::min<uint32_t>(d.tiles, d.ctiles ? d.ctiles : v1 ? 2 : 1));
+    d.ctiles = std::max<uint32_t>(1, std::min<uint32_t>(d.tiles, d.ctiles ? d.ctiles : 2));
     d.chunks = (d.tiles + d.ctiles - 1) / d.ctiles;
     const dim3 grid(((d.n + d.G - 1) / d.G) * d.chunks);
-    if (v1) {
-      hipLaunchKernelGGL(nh_derive_wide_kernel, grid, dim3(kBlock), 0, s, g, d);
-      return hipGetLastError();
-    }
-    const size_t lds = 4ull * (d.W * d.G + (d.W | 1u) * kWavesPerBlock * 64u);
-    if (lds > 64u * 1024u) {
-      const hipError_t e = hipFuncSetAttribute((const void*)nh_derive_wide2_kernel,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(nh_derive_wide2_kernel, grid, dim3(kBlock), lds, s, g, d);
+    hipLaunchKernelGGL(nh_derive_wide_kernel, grid, dim3(kBlock), 0, s, g, d);
     return hipGetLastError();
   }
   // one thread per node quad does all the words up to 8; wider rows split a

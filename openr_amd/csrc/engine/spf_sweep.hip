@@ -544,6 +544,69 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   std::vector<uint32_t> pos(V, kNone);
   for (uint32_t i = 0; i < nc; ++i) pos[clo[i]] = i;
   for (uint32_t i = 0; i < nd; ++i) pos[drv[i]] = nc + i;
+  // twin-levels groups: <= 8 consecutive derived rows (a pod's fabric
+  // switches) reading <= kTwinMaxC class rows together
+  std::vector<uint32_t> dgo{0u};
+  if (nd) {
+    std::vector<uint32_t> cl;
+    for (uint32_t i = 0; i < nd; ++i) {
+      classes_of(drv[i]);
+      std::vector<uint32_t> u = cl;
+      u.insert(u.end(), cs.begin(), cs.end());
+      std::sort(u.begin(), u.end());
+      u.erase(std::unique(u.begin(), u.end()), u.end());
+      if (i > dgo.back() && (i - dgo.back() >= 8u || u.size() > ospf::kTwinMaxC)) {
+        dgo.push_back(i);
+        u = cs;
+      }
+      cl.swap(u);
+    }
+    dgo.push_back(nd);
+  }
+  const uint32_t n_dgrp = (uint32_t)dgo.size() - 1;
+  // pipeline stages: the derived rows in S stages of whole groups (blocks of
+  // pods on a fabric); a leaf group or a twin next-hop root waits only for
+  // the stage of the derived rows it reads, so the leaves' row stores run
+  // beside the later stages (OSPF_SWEEP_STAGES, default 8)
+  uint32_t S = 0;
+  if (nd) {
+    S = 8;
+    if (const char* e = getenv("OSPF_SWEEP_STAGES")) S = (uint32_t)std::max(1, atoi(e));
+    S = std::min(S, n_dgrp);
+  }
+  std::vector<uint32_t> sg(S + 1, 0u);  // first group of each stage
+  std::vector<int> stage_of(V, -1);     // stage of a node's derived row
+  for (uint32_t k = 0; k <= S; ++k) sg[k] = (uint32_t)((uint64_t)k * n_dgrp / std::max(1u, S));
+  for (uint32_t k = 0; k < S; ++k)
+    for (uint32_t i = dgo[sg[k]]; i < dgo[sg[k + 1]]; ++i) stage_of[drv[i]] = (int)k;
+  auto dep_of = [&](uint32_t r, bool self) {  // latest stage r's rows need (0 if none)
+    int d = self ? stage_of[r] : -1;
+    for (uint32_t q = (*f.dn_off)[r]; q < (*f.dn_off)[r + 1]; ++q) d = std::max(d, stage_of[(*f.dn)[q]]);
+    return std::max(d, 0);
+  };
+  std::vector<uint32_t> lsg(S + 1, 0u);  // first leaf group of each stage (rest)
+  if (S > 1 && nL > nR) {
+    const uint32_t ngr0 = (uint32_t)grp.size() - 1;
+    std::vector<uint32_t> gi(ngr0), gdep(ngr0);
+    for (uint32_t x = 0; x < ngr0; ++x) {
+      gi[x] = x;
+      gdep[x] = (uint32_t)dep_of(rest[grp[x]], false);
+    }
+    std::stable_sort(gi.begin(), gi.end(), [&](uint32_t a, uint32_t b) { return gdep[a] < gdep[b]; });
+    std::vector<uint32_t> r2, g2{0u};
+    for (uint32_t x : gi) {
+      r2.insert(r2.end(), rest.begin() + grp[x], rest.begin() + grp[x + 1]);
+      g2.push_back((uint32_t)r2.size());
+    }
+    rest.swap(r2);
+    grp.swap(g2);
+    need_l.resize(nR);
+    need_l.insert(need_l.end(), rest.begin(), rest.end());
+    for (uint32_t k = 0, x = 0; k <= S; ++k) {
+      while (x < ngr0 && gdep[gi[x]] < k) ++x;
+      lsg[k] = k == S ? ngr0 : x;
+    }
+  }
   uint32_t rows = nc + nd;
   for (uint32_t i = 0; i < nL; ++i)
     if (pos[need_l[i]] == kNone) pos[need_l[i]] = rows++;
@@ -584,6 +647,11 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   // representative leaves done, every leaf done
   const int ev_a = new_event(s), ev_t = new_event(s), ev_r = new_event(s), ev_b = new_event(s);
   if (ev_a < 0 || ev_t < 0 || ev_r < 0 || ev_b < 0) return std::min({ev_a, ev_t, ev_r, ev_b});
+  std::vector<int> ev_s(S);  // stage k of the derived rows done (the last = ev_t)
+  for (uint32_t k = 0; k < S; ++k) {
+    ev_s[k] = k + 1 == S ? ev_t : new_event(s);
+    if (ev_s[k] < 0) return ev_s[k];
+  }
   if (nc) {
     ospf_sweep::Unit lv;
     lv.name = "levels";
@@ -599,19 +667,25 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     s->step_comp += lv.comp;
     s->units.push_back(lv);
   }
-  if (nd) {
+  for (uint32_t k = 0; k < S; ++k) {
+    const uint32_t i0 = dgo[sg[k]], n = dgo[sg[k + 1]] - i0;
+    std::vector<uint32_t> gk;
+    for (uint32_t g = sg[k]; g <= sg[k + 1]; ++g) gk.push_back(dgo[g] - i0);
+    uint32_t* d_gk;
+    if ((rc = upload(s, &d_gk, gk))) return rc;
+    const uint32_t ngk = sg[k + 1] - sg[k];
     ospf_sweep::Unit u;
-    u.name = "twin_levels";
+    u.name = S > 1 ? "twin_levels_s" + std::to_string(k) : std::string("twin_levels");
     u.kernel = "ospf_twin_levels_dev (twin_levels_kernel: level + dist rows from the neighbour "
                "classes' representative rows)";
     u.stream = 0;
-    u.record = ev_t;
-    u.n_roots = nd;
-    // dist rows written + the class rows read once (level rows are intermediate)
-    u.comp = (uint64_t)nd * 4ull * V;
-    const uint32_t *tc = d_tcls, *tr = d_trep;
+    u.record = ev_s[k];
+    u.n_roots = n;
+    // dist rows written (level rows are intermediate)
+    u.comp = (uint64_t)n * 4ull * V;
+    const uint32_t *tc = d_tcls, *tr = d_trep, *dr = d_drv + i0;
     u.fn = [=](hipStream_t st) {
-      return ospf_twin_levels_dev(c, d_drv, nd, lev, pitch, d_pos, tc, tr, dist, ldg, st);
+      return ospf_twin_levels_dev(c, dr, n, d_gk, ngk, lev, pitch, d_pos, tc, tr, dist, ldg, st);
     };
     s->step_comp += u.comp;
     s->units.push_back(u);
@@ -622,6 +696,10 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   std::vector<ospf_sweep::Unit> side, after;
   for (size_t i = 0; i < cls.size(); ++i) {
     Cls& k = cls[i];
+    if (k.twin && twin_lv && S > 1)
+      std::stable_sort(k.roots.begin(), k.roots.end(), [&](uint32_t a, uint32_t b) {
+        return dep_of(a, true) < dep_of(b, true);
+      });
     const uint32_t n = (uint32_t)k.roots.size(), W = k.W, cap = std::min(k.cap, 2048u);
     uint32_t *d_roots, *nh;
     if ((rc = upload(s, &d_roots, k.roots)) || (rc = dalloc(s, &nh, (size_t)n * V * W))) return rc;
@@ -629,14 +707,44 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     for (uint32_t j = 0; j < n; ++j)
       own(s, k.roots[j], slot + j, dist + (size_t)pos[k.roots[j]] * V, nh + (size_t)j * V * W, W);
     slot += n;
+    const int st = new_stream(s);
+    if (st < 0) return st;
+    if (k.twin && twin_lv && S > 1) {
+      // one launch per stage of the roots' own rows (roots were ordered by
+      // stage above), beside the later stages
+      for (uint32_t q = 0, a0 = 0; q < S; ++q) {
+        uint32_t a1 = a0;
+        while (a1 < n && (uint32_t)dep_of(k.roots[a1], true) <= q) ++a1;
+        if (a1 == a0) continue;
+        ospf_sweep::Unit u;
+        u.name = "derive_cap" + std::to_string(k.cap) + "_s" + std::to_string(q);
+        u.kernel = "ospf_nh_derive_twin_dev (nh_derive_twin_kernel, " + std::to_string(W) +
+                   " next-hop word" + (W > 1 ? "s)" : ")");
+        u.stream = st;
+        u.wait = {ev_s[q]};
+        u.n_roots = a1 - a0;
+        u.W = W;
+        u.comp = (uint64_t)(a1 - a0) * 4ull * V * W;
+        const uint32_t *tc = d_tcls, *tr = d_trep, *ts = d_tsec, *rr = d_roots + a0;
+        const uint32_t m = a1 - a0;
+        uint32_t* nhq = nh + (size_t)a0 * V * W;
+        ospf_digest* dq = dg + a0;
+        u.fn = [=](hipStream_t strm) {
+          return ospf_nh_derive_twin_dev(c, rr, m, W, cap, lev, pitch, d_pos, ldg, tc, tr, ts, nhq,
+                                         dq, strm);
+        };
+        s->step_comp += u.comp;
+        side.push_back(std::move(u));
+        a0 = a1;
+      }
+      continue;
+    }
     ospf_sweep::Unit u;
     u.name = "derive_cap" + std::to_string(k.cap);
     u.kernel = std::string(k.twin ? "ospf_nh_derive_twin_dev (" : "ospf_nh_derive_dev (") +
                (k.twin ? "nh_derive_twin_kernel" : W <= 4 ? "nh_derive16_kernel"
                                                           : "nh_derive_wide_kernel") +
                ", " + std::to_string(W) + " next-hop word" + (W > 1 ? "s)" : ")");
-    const int st = new_stream(s);
-    if (st < 0) return st;
     u.stream = st;
     // twin classes read the representatives' rows (BFS'd with twin levels);
     // the others every neighbour's row
@@ -697,7 +805,40 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       s->step_comp += u.comp;
       s->units.push_back(std::move(u));
     }
-    if (nL > nR) {
+    if (nL > nR && twin_lv && S > 1) {
+      const int lst = new_stream(s);
+      if (lst < 0) return lst;
+      for (uint32_t q = 0; q < S; ++q) {
+        const uint32_t g0 = lsg[q], g1 = lsg[q + 1];
+        if (g1 == g0) continue;
+        const uint32_t i0 = grp[g0], n = grp[g1] - i0;
+        std::vector<uint32_t> gq;
+        for (uint32_t g = g0; g <= g1; ++g) gq.push_back(grp[g] - i0);
+        uint32_t* d_gq;
+        if ((rc = upload(s, &d_gq, gq))) return rc;
+        ospf_sweep::Unit u;
+        u.name = "leaf_s" + std::to_string(q);
+        u.kernel = "ospf_leaf_derive2_dev (leaf_derive_kernel: level + dist + next-hop rows of leaf "
+                   "roots from their neighbours' level rows)";
+        u.stream = lst;
+        u.wait = {ev_s[q]};
+        if (g1 == (uint32_t)grp.size() - 1) u.record = ev_b;
+        u.n_roots = n;
+        u.W = 1;
+        u.comp = (uint64_t)n * 8ull * V;
+        const uint32_t* dl = d_l + nR + i0;
+        uint32_t* nh = lnh + (size_t)(nR + i0) * V;
+        ospf_digest* dg2 = dg + nR + i0;
+        const uint32_t* lo = drop_rest ? d_lout : nullptr;
+        const uint32_t ngq = g1 - g0;
+        u.fn = [=](hipStream_t strm) {
+          return ospf_leaf_derive2_dev(c, dl, n, d_gq, ngq, kmax, lev, pitch, d_pos, lo, dist, nh,
+                                       dg2, strm);
+        };
+        s->step_comp += u.comp;
+        s->units.push_back(std::move(u));
+      }
+    } else if (nL > nR) {
       ospf_sweep::Unit u;
       u.name = "leaf";
       u.kernel = "ospf_leaf_derive2_dev (leaf_derive_kernel: level + dist + next-hop rows of leaf "

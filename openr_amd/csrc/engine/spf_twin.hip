@@ -354,106 +354,172 @@ __device__ __forceinline__ uint32_t bmin7(uint32_t a, uint32_t b) {
 // their members' positions, and every member of a neighbour's class is
 // itself a usable neighbour of r (twins share their usable neighbours, r
 // among them). So a fabric switch reads two class rows (its pod's racks,
-// its plane's spines) instead of a traversal. Lane = 4 nodes, wave = 256
-// nodes per step, block = one root over every node; the distance part of
-// the digest is stored (not added).
+// its plane's spines) instead of a traversal.
+// Block = a group of up to kTwinLvG roots whose classes' rows number <= 16
+// (a pod's fabric switches: one rack row + the 8 planes' spine rows): per
+// 256-node chunk a wave loads each of the group's rows once (lane = 4
+// nodes), then per root takes the min over its rows, patches its own and its
+// neighbours' positions (each root's sorted neighbour list walked by a
+// cursor) and stores 256 B of level row + 1 KB of dist row per instruction.
+// The distance part of each root's digest is stored (not added).
+constexpr uint32_t kTwinLvG = 8;
 __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinArgs a) {
-  __shared__ TwinTab T;
-  __shared__ unsigned long long s_r[kWaves], s_s[kWaves], s_hh[kWaves];
-  extern __shared__ uint32_t s_nbm[];  // [(pitch + 31) / 32] usable-neighbour bits
+  __shared__ TwinTab T;                       // setup scratch, one root at a time
+  __shared__ uint32_t s_nb[kTwinLvG][kMaxK];  // usable neighbours (ascending), per root
+  __shared__ uint32_t s_nnb[kTwinLvG], s_root[kTwinLvG], s_own[kTwinLvG], s_umask[kTwinLvG];
+  __shared__ uint32_t s_urow[kTwinMaxC], s_nu, s_ok;
+  __shared__ unsigned long long s_d[kWaves][kTwinLvG][3];
   const uint32_t V = g.V, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const uint32_t b = blockIdx.x, T8 = a.n / 8u * 8u;  // XCD-aware root order
-  const uint32_t i = b < T8 ? (b % 8u) * (T8 / 8u) + b / 8u : b;
-  if (!twin_setup(g, a, i, 4, T)) return;
-  const uint32_t K = min(T.K, kMaxK), own = T.own, nc = T.nc, r = T.root;
-  const uint32_t nw = (a.pitch + 31u) / 32u;
-  for (uint32_t x = tid; x < nw; x += kBlock) s_nbm[x] = 0u;
-  __syncthreads();
-  if (tid < K && T.cid[tid] != kInf) atomicOr(&s_nbm[T.nb[tid] >> 5], 1u << (T.nb[tid] & 31u));
-  __syncthreads();
-  uint32_t crow[kTwinMaxC];
+  const uint32_t b = blockIdx.x, B8 = a.ngroups / 8u * 8u;  // XCD-aware group order
+  const uint32_t gi = b < B8 ? (b % 8u) * (B8 / 8u) + b / 8u : b;
+  const uint32_t i0 = a.grp ? a.grp[gi] : gi;
+  const uint32_t ng = a.grp ? min(kTwinLvG, a.grp[gi + 1] - i0) : 1u;
+  if (tid == 0) {
+    s_nu = 0u;
+    s_ok = 1u;
+  }
+  for (uint32_t j = 0; j < ng; ++j) {
+    if (!twin_setup(g, a, i0 + j, 4, T)) return;  // block-uniform; error bits set
+    const uint32_t K = min(T.K, kMaxK);
+    if (tid < 64) {  // usable neighbours in ascending order (wave 0)
+      uint32_t cnt = 0;
+      for (uint32_t base = 0; base < K; base += 64u) {
+        const uint32_t k = base + lane;
+        const bool f = k < K && T.cid[k] != kInf;
+        const uint64_t bal = __ballot(f);
+        if (f) s_nb[j][cnt + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = T.nb[k];
+        cnt += (uint32_t)__popcll(bal);
+      }
+      if (lane == 0) s_nnb[j] = cnt;
+    }
+    if (tid == 0) {
+      s_root[j] = T.root;
+      s_own[j] = T.own;
+      uint32_t mask = 0;
+      for (uint32_t x = 0; x < T.nc; ++x) {
+        uint32_t u = 0;
+        while (u < s_nu && s_urow[u] != T.crow[x]) ++u;
+        if (u == s_nu) {
+          if (u == kTwinMaxC) {
+            s_ok = 0u;
+            atomicOr(a.err, 256u);
+            break;
+          }
+          s_urow[s_nu++] = T.crow[x];
+        }
+        mask |= 1u << u;
+      }
+      s_umask[j] = mask;
+    }
+    __syncthreads();  // T is rewritten by the next root
+  }
+  if (!s_ok) return;
+  const uint32_t nu = s_nu;
+  uint32_t urow[kTwinMaxC];
 #pragma unroll
-  for (uint32_t j = 0; j < kTwinMaxC; ++j) crow[j] = j < nc ? T.crow[j] : 0u;
-  const uint32_t chunks = a.pitch / 256u;
+  for (uint32_t u = 0; u < kTwinMaxC; ++u) urow[u] = u < nu ? s_urow[u] : 0u;
+  const uint32_t nchunks = (a.pitch + 255u) / 256u;
   auto load_x = [&](uint32_t c, uint32_t* x) {
-    const uint32_t v0 = c < chunks ? c * 256u + 4u * lane : 0u;
+    const uint32_t v0 = c * 256u + 4u * lane;
+    const bool ok = c < nchunks && v0 < a.pitch;
 #pragma unroll
-    for (uint32_t j = 0; j < kTwinMaxC; ++j)
-      x[j] = j < nc ? *reinterpret_cast<const uint32_t*>(a.lev + (size_t)crow[j] * a.pitch + v0)
-                    : 0x7F7F7F7Fu;
+    for (uint32_t u = 0; u < kTwinMaxC; ++u)
+      x[u] = (u < nu && ok) ? *reinterpret_cast<const uint32_t*>(a.lev + (size_t)urow[u] * a.pitch + v0)
+                            : 0x7F7F7F7Fu;
   };
-  uint64_t br = 0, bs = 0, bh = 0;
+  uint32_t br[kTwinLvG], cur[kTwinLvG];
+  uint64_t bs[kTwinLvG], bh[kTwinLvG];
+#pragma unroll
+  for (uint32_t j = 0; j < kTwinLvG; ++j) {
+    br[j] = 0u;
+    cur[j] = 0u;
+    bs[j] = bh[j] = 0ull;
+  }
   const bool vec = (V & 3u) == 0;
   uint32_t xn[kTwinMaxC];
   load_x(wave, xn);
-  for (uint32_t c = wave; c < chunks + (a.pitch % 256u ? 1u : 0u); c += kWaves) {
-    const uint32_t v0 = c * 256u + 4u * lane;
-    uint32_t m = 0x7F7F7F7Fu;
-    if (c < chunks) {
+  for (uint32_t c = wave; c < nchunks; c += kWaves) {
+    const uint32_t c0 = c * 256u, v0 = c0 + 4u * lane;
+    uint32_t x[kTwinMaxC];
 #pragma unroll
-      for (uint32_t j = 0; j < kTwinMaxC; ++j) m = bmin7(m, xn[j]);
-      load_x(c + kWaves, xn);
-    } else if (v0 < a.pitch) {  // tail chunk (pitch is a multiple of 16, not of 256)
-      for (uint32_t j = 0; j < nc; ++j)
-        m = bmin7(m, *reinterpret_cast<const uint32_t*>(a.lev + (size_t)crow[j] * a.pitch + v0));
-    }
-    if (v0 >= a.pitch) continue;
-    uint32_t L = (m + 0x01010101u) - (((m + 0x01010101u) & 0x80808080u) >> 7);
-    const uint32_t nb4 = (s_nbm[v0 >> 5] >> (v0 & 31u)) & 0xFu;
+    for (uint32_t u = 0; u < kTwinMaxC; ++u) x[u] = xn[u];
+    load_x(c + kWaves, xn);
+    if (v0 >= a.pitch) continue;  // no wave-level work below (cursors are per wave: see skip)
+    uint64_t kd[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if ((nb4 >> q) & 1u) L = (L & ~(0xFFu << (8 * q))) | (2u << (8 * q));
-    const uint32_t off = r - v0;
-    if (off < 4u) L = (L & ~(0xFFu << (8u * off))) | (1u << (8u * off));
-    __builtin_nontemporal_store(L, reinterpret_cast<uint32_t*>(a.lev_w + (size_t)own * a.pitch + v0));
-    if (v0 >= V) continue;
-    uint32_t dv[4];
+    for (int q = 0; q < 4; ++q) kd[q] = v0 + q < V ? g.dkey[2ull * (v0 + q)] : 0ull;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t l = (L >> (8 * q)) & 0xFFu;
-      dv[q] = l < 0x7Fu ? l - 1u : kInf;
-      if (l < 0x7Fu && v0 + q < V) {
-        br += 1u;
-        bs += l - 1u;
-        bh += g.dkey[2ull * (v0 + q)] * (uint64_t)l;
+    for (uint32_t j = 0; j < kTwinLvG; ++j) {
+      if (j >= ng) break;
+      const uint32_t mask = s_umask[j];
+      uint32_t m = 0x7F7F7F7Fu;
+#pragma unroll
+      for (uint32_t u = 0; u < kTwinMaxC; ++u)
+        if ((mask >> u) & 1u) m = bmin7(m, x[u]);
+      uint32_t L = (m + 0x01010101u) - (((m + 0x01010101u) & 0x80808080u) >> 7);
+      // neighbours in this chunk: level 2 (the list is ascending; chunks of a
+      // wave ascend, so the cursor skips the other waves' chunks)
+      const uint32_t nn = s_nnb[j];
+      while (cur[j] < nn && s_nb[j][cur[j]] < c0) ++cur[j];
+      while (cur[j] < nn && s_nb[j][cur[j]] < c0 + 256u) {
+        const uint32_t n = s_nb[j][cur[j]++], o = n - v0;
+        if (o < 4u) L = (L & ~(0xFFu << (8u * o))) | (2u << (8u * o));
       }
-    }
-    if (a.dist) {
-      uint32_t* drow = a.dist + (size_t)own * V + v0;
-      if (vec) {
-        store_row16(drow, make_uint4(dv[0], dv[1], dv[2], dv[3]));
-      } else {
+      const uint32_t off = s_root[j] - v0;
+      if (off < 4u) L = (L & ~(0xFFu << (8u * off))) | (1u << (8u * off));
+      const uint32_t own = s_own[j];
+      __builtin_nontemporal_store(L, reinterpret_cast<uint32_t*>(a.lev_w + (size_t)own * a.pitch + v0));
+      if (v0 >= V) continue;
+      uint32_t dv[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (v0 + q < V) drow[q] = dv[q];
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t l = (L >> (8 * q)) & 0xFFu;
+        dv[q] = l < 0x7Fu ? l - 1u : kInf;
+        if (l < 0x7Fu && v0 + q < V) {
+          br[j] += 1u;
+          bs[j] += l - 1u;
+          bh[j] += kd[q] * (uint64_t)l;
+        }
+      }
+      if (a.dist) {
+        uint32_t* drow = a.dist + (size_t)own * V + v0;
+        if (vec) {
+          store_row16(drow, make_uint4(dv[0], dv[1], dv[2], dv[3]));
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (v0 + q < V) drow[q] = dv[q];
+        }
       }
     }
   }
-  if (a.lev_digest_w) {
+  if (!a.lev_digest_w) return;
+#pragma unroll
+  for (uint32_t j = 0; j < kTwinLvG; ++j) {
+    uint64_t r64 = br[j];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-      br += shfl_xor64(br, o);
-      bs += shfl_xor64(bs, o);
-      bh += shfl_xor64(bh, o);
+      r64 += shfl_xor64(r64, o);
+      bs[j] += shfl_xor64(bs[j], o);
+      bh[j] += shfl_xor64(bh[j], o);
     }
     if (lane == 0) {
-      s_r[wave] = br;
-      s_s[wave] = bs;
-      s_hh[wave] = bh;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      ospf_digest d{0ull, 0ull, 0ull};
-      for (uint32_t w = 0; w < kWaves; ++w) {
-        d.reached += s_r[w];
-        d.sum_dist += s_s[w];
-        d.hash += s_hh[w];
-      }
-      a.lev_digest_w[own] = d;
+      s_d[wave][j][0] = r64;
+      s_d[wave][j][1] = bs[j];
+      s_d[wave][j][2] = bh[j];
     }
   }
+  __syncthreads();
+  if (tid < ng) {
+    ospf_digest d{0ull, 0ull, 0ull};
+    for (uint32_t w = 0; w < kWaves; ++w) {
+      d.reached += s_d[w][tid][0];
+      d.sum_dist += s_d[w][tid][1];
+      d.hash += s_d[w][tid][2];
+    }
+    a.lev_digest_w[s_own[tid]] = d;
+  }
 }
-
 }  // namespace
 
 hipError_t launch_nh_derive_twin(const DevGraph& g, const TwinArgs& a0, hipStream_t s) {
@@ -480,13 +546,7 @@ hipError_t launch_nh_derive_twin(const DevGraph& g, const TwinArgs& a0, hipStrea
 namespace ospf {
 hipError_t launch_twin_levels(const DevGraph& g, const TwinArgs& a, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  const size_t lds = 4ull * ((a.pitch + 31u) / 32u);
-  if (lds > 64u * 1024u) {
-    const hipError_t e = hipFuncSetAttribute((const void*)twin_levels_kernel,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-  }
-  hipLaunchKernelGGL(twin_levels_kernel, dim3(a.n), dim3(kBlock), lds, s, g, a);
+  hipLaunchKernelGGL(twin_levels_kernel, dim3(a.grp ? a.ngroups : a.n), dim3(kBlock), 0, s, g, a);
   return hipGetLastError();
 }
 }  // namespace ospf

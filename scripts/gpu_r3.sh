@@ -58,7 +58,7 @@ for st in $STEPS; do
     ab)    # A/B of env knobs on the default bench: AB="NAME=1 OTHER=1 ..." (one run each + baseline)
            rc=0
            for kv in base ${AB:-}; do
-             if [ "$kv" = base ]; then E=""; else E="$kv"; fi
+             if [ "$kv" = base ]; then E=""; else E="${kv//,/ }"; fi
              timeout -k 10 300 env $E python bench.py --steps 20 --warmup 2 --cpu-sample 8 --iso-reps 2 ${AB_ARGS:-} > "$OUT/ab_$kv.json" 2> "$OUT/ab_$kv.err"; rc=$?
              echo "ab $kv rc=$rc $(python -c "import json,sys; d=json.load(open('$OUT/ab_$kv.json')); print(d['value'], d['ms_per_step'], d['parity_vs_cpu_sample'])" 2>/dev/null)"
              [ $rc -eq 0 ] || break
