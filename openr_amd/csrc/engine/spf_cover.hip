@@ -29,6 +29,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "spf_kernels.h"
 
@@ -104,6 +105,195 @@ __device__ __forceinline__ void expand(const CoverGraph& C, uint32_t* s_D, uint3
   }
 }
 
+// The root's row in node order: cover nodes from LDS, leaves by their last
+// hop (min over their up in-links from transit cover nodes or the root);
+// four nodes per thread per step, their first two in-link quads loaded before
+// any is used (a rack's 8 entries).
+__device__ __forceinline__ void write_row(const DevGraph& g, const CoverGraph& C, uint32_t* row,
+                                          const uint32_t* s_D, const uint32_t* s_tr, uint32_t r,
+                                          uint32_t tid, uint32_t nthreads) {
+  const uint32_t nS = C.nS, V = g.V;
+  const uint4* la4 = reinterpret_cast<const uint4*>(C.ladj);
+  const uint4 pad = make_uint4(0xFFFFu, 0xFFFFu, 0xFFFFu, 0xFFFFu);
+  auto fold = [&](uint4 e4, uint32_t out) {
+    const uint32_t es[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const uint32_t ci = es[b] & 0xFFFFu;
+      if (ci >= nS) continue;  // padding
+      if (!((s_tr[ci >> 5] >> (ci & 31u)) & 1u) && ci != r) continue;
+      const uint32_t d = s_D[ci];
+      if (d != kInf) out = min(out, d + (es[b] >> 16));
+    }
+    return out;
+  };
+  for (uint32_t v0 = tid; v0 < V; v0 += 4u * nthreads) {
+    uint32_t c4[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t v = v0 + (uint32_t)k * nthreads;
+      c4[k] = v < V ? C.cix[v] : 0u;
+    }
+    uint4 e0[4], e1[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      e0[k] = e1[k] = pad;
+      if (c4[k] & kLeaf) {
+        const uint32_t q0 = (c4[k] >> 5) & 0x3FFFFFFu, nq = c4[k] & 31u;
+        if (nq > 0) e0[k] = la4[q0];
+        if (nq > 1) e1[k] = la4[q0 + 1];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t v = v0 + (uint32_t)k * nthreads;
+      if (v >= V) continue;
+      uint32_t out;
+      if (!(c4[k] & kLeaf)) {
+        out = s_D[c4[k]];
+      } else {
+        out = fold(e1[k], fold(e0[k], kInf));
+        const uint32_t q0 = (c4[k] >> 5) & 0x3FFFFFFu, nq = c4[k] & 31u;
+        for (uint32_t qq = 2; qq < nq; ++qq) out = fold(la4[q0 + qq], out);
+      }
+      __builtin_nontemporal_store(out, row + v);
+    }
+  }
+}
+
+// Frontier Bellman-Ford over the contracted graph (the cover SPF's default):
+// a round expands the transit cover nodes whose distance dropped in the
+// previous round (and the root in the first), each from its current
+// distance, their edges flattened over each wave; a relaxation that lowers a
+// distance (LDS atomicMin) puts the node into the next round's frontier
+// bitmap. Exact at the fixed point (metrics >= 1): the rounds follow the hop
+// depth of the shortest paths (a fabric's cover: ~10), not the distance
+// values (Dial: one round, with a scan of the cover, per value).
+__device__ __forceinline__ void expand_bf(const CoverGraph& C, uint32_t* s_D, uint32_t* nxt,
+                                          const uint32_t* q, uint32_t cnt, uint32_t* s_pre,
+                                          uint32_t* s_any, uint32_t lane) {
+  for (uint32_t b0 = 0; b0 < cnt; b0 += kWave) {
+    const uint32_t j = b0 + lane;
+    uint32_t beg = 0, deg = 0, du = kInf;
+    if (j < cnt) {
+      const uint32_t u = q[j];
+      beg = C.crow[u];
+      deg = C.crow[u + 1] - beg;
+      du = s_D[u];
+    }
+    uint32_t inc = deg;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)inc, o, kWave);
+      if (lane >= (uint32_t)o) inc += y;
+    }
+    s_pre[lane] = inc;
+    s_pre[kWave + lane] = beg;
+    s_pre[2 * kWave + lane] = du;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t total = (uint32_t)__shfl((int)inc, kWave - 1, kWave);
+    constexpr uint32_t kU = 16;
+    bool any = false;
+    for (uint32_t f0 = 0; f0 < total; f0 += kWave * kU) {
+      uint2 ed[kU];
+      uint32_t base[kU];
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t f = f0 + u * kWave + lane;
+        ed[u] = make_uint2(0u, kInf);
+        base[u] = kInf;
+        if (f < total) {
+          uint32_t lo = 0, hi = kWave - 1;  // first k with pre[k] > f
+#pragma unroll
+          for (int it = 0; it < 6; ++it) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_pre[mid] > f) hi = mid;
+            else lo = mid + 1;
+          }
+          const uint32_t before = lo ? s_pre[lo - 1] : 0u;
+          ed[u] = C.cedge[s_pre[kWave + lo] + (f - before)];
+          base[u] = s_pre[2 * kWave + lo];
+        }
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        if (ed[u].y == kInf || base[u] == kInf) continue;
+        const uint32_t nd = base[u] + ed[u].y;
+        const uint32_t v = ed[u].x;
+        if (nd < atomicMin(&s_D[v], nd)) {
+          atomicOr(&nxt[v >> 5], 1u << (v & 31u));
+          any = true;
+        }
+      }
+    }
+    if (__ballot(any) && lane == 0) *s_any = 1u;
+    __builtin_amdgcn_wave_barrier();  // s_pre is rewritten by the next pass
+  }
+}
+
+__global__ void __launch_bounds__(512) cover_bf_kernel(DevGraph g, CoverGraph C, CoverArgs a) {
+  extern __shared__ uint32_t s_D[];  // [nS] distances, [nw] transit bits, [2][nw] frontiers
+  __shared__ uint32_t s_q[kWaves][kQ];
+  __shared__ uint32_t s_pre[kWaves][3 * kWave];
+  __shared__ uint32_t s_any[2];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t nS = C.nS, V = g.V, nw = (nS + 31u) / 32u;
+  uint32_t* s_tr = s_D + nS;
+  uint32_t* s_f = s_tr + nw;
+  for (uint32_t x = tid; x < nw; x += kBlock) s_tr[x] = C.ctr[x];
+  for (uint32_t i = blockIdx.x; i < a.n; i += gridDim.x) {
+    const uint32_t rn = a.roots[i];
+    const uint32_t r = rn < V ? C.cix[rn] : kInf;
+    if (r >= nS) {  // not a cover node (or a bad id): its row is left alone
+      if (tid == 0) atomicOr(a.err, 64u);
+      continue;
+    }
+    for (uint32_t x = tid; x < nS; x += kBlock) s_D[x] = x == r ? 0u : kInf;
+    for (uint32_t x = tid; x < 2u * nw; x += kBlock) s_f[x] = x == (r >> 5) ? 1u << (r & 31u) : 0u;
+    if (tid == 0) s_any[0] = s_any[1] = 0u;
+    __syncthreads();
+    uint32_t par = 0;
+    while (true) {
+      uint32_t* cur = s_f + par * nw;
+      uint32_t* nxt = s_f + (par ^ 1u) * nw;
+      uint32_t* q = s_q[wave];
+      uint32_t cnt = 0;
+      for (uint32_t w0 = wave * kWave; w0 < nw; w0 += kBlock) {
+        const uint32_t w = w0 + lane;
+        uint32_t bits = 0;
+        if (w < nw) {
+          bits = cur[w];
+          if (bits) cur[w] = 0u;  // clean for the round after next
+          bits &= s_tr[w] | (w == (r >> 5) ? 1u << (r & 31u) : 0u);  // transit or the root
+        }
+        while (__ballot(bits != 0u)) {
+          const bool has = bits != 0u;
+          const uint32_t u = has ? 32u * w + (uint32_t)__builtin_ctz(bits) : 0u;
+          if (has) bits &= bits - 1u;
+          const uint64_t bal = __ballot(has);
+          if (has) q[cnt + __popcll(bal & ((1ull << lane) - 1ull))] = u;
+          cnt += (uint32_t)__popcll(bal);
+          if (cnt > kQ - kWave) {
+            __builtin_amdgcn_wave_barrier();
+            expand_bf(C, s_D, nxt, q, cnt, s_pre[wave], &s_any[par ^ 1u], lane);
+            cnt = 0;
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (cnt) expand_bf(C, s_D, nxt, q, cnt, s_pre[wave], &s_any[par ^ 1u], lane);
+      __syncthreads();
+      const bool more = s_any[par ^ 1u] != 0u;
+      __syncthreads();  // every thread has read the flag
+      if (tid == 0) s_any[par ^ 1u] = 0u;
+      par ^= 1u;
+      if (!more) break;  // no distance dropped: the fixed point
+    }
+    write_row(g, C, a.dist + (size_t)i * V, s_D, s_tr, r, tid, kBlock);
+    __syncthreads();  // s_D is reused by the next root
+  }
+}
+
 __global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C, CoverArgs a) {
   extern __shared__ uint32_t s_D[];  // [nS] distances, then [ctr words] transit bits
   __shared__ uint32_t s_q[kWaves][kQ];
@@ -153,56 +343,7 @@ __global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C
       if (t == kInf) break;  // every reachable cover node settled
       __syncthreads();       // the slot reset is visible before its use
     }
-    // the row in node order: cover nodes from LDS, leaves by their last hop;
-    // four nodes per thread per step, their first two in-link quads loaded
-    // before any is used (a rack's 8 entries)
-    uint32_t* row = a.dist + (size_t)i * V;
-    const uint4* la4 = reinterpret_cast<const uint4*>(C.ladj);
-    const uint4 pad = make_uint4(0xFFFFu, 0xFFFFu, 0xFFFFu, 0xFFFFu);
-    auto fold = [&](uint4 e4, uint32_t out) {
-      const uint32_t es[4] = {e4.x, e4.y, e4.z, e4.w};
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const uint32_t ci = es[b] & 0xFFFFu;
-        if (ci >= nS) continue;  // padding
-        if (!((s_tr[ci >> 5] >> (ci & 31u)) & 1u) && ci != r) continue;
-        const uint32_t d = s_D[ci];
-        if (d != kInf) out = min(out, d + (es[b] >> 16));
-      }
-      return out;
-    };
-    for (uint32_t v0 = tid; v0 < V; v0 += 4u * kBlock) {
-      uint32_t c4[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t v = v0 + (uint32_t)k * kBlock;
-        c4[k] = v < V ? C.cix[v] : 0u;
-      }
-      uint4 e0[4], e1[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        e0[k] = e1[k] = pad;
-        if (c4[k] & kLeaf) {
-          const uint32_t q0 = (c4[k] >> 5) & 0x3FFFFFFu, nq = c4[k] & 31u;
-          if (nq > 0) e0[k] = la4[q0];
-          if (nq > 1) e1[k] = la4[q0 + 1];
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t v = v0 + (uint32_t)k * kBlock;
-        if (v >= V) continue;
-        uint32_t out;
-        if (!(c4[k] & kLeaf)) {
-          out = s_D[c4[k]];
-        } else {
-          out = fold(e1[k], fold(e0[k], kInf));
-          const uint32_t q0 = (c4[k] >> 5) & 0x3FFFFFFu, nq = c4[k] & 31u;
-          for (uint32_t qq = 2; qq < nq; ++qq) out = fold(la4[q0 + qq], out);
-        }
-        __builtin_nontemporal_store(out, row + v);
-      }
-    }
+    write_row(g, C, a.dist + (size_t)i * V, s_D, s_tr, r, tid, kBlock);
     __syncthreads();  // s_D is reused by the next root
   }
 }
@@ -212,6 +353,18 @@ __global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C
 hipError_t launch_cover_spf(const DevGraph& g, const CoverGraph& C, const CoverArgs& a,
                             uint32_t n_cu, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
+  if (!getenv("OSPF_COVER_DIAL")) {  // frontier Bellman-Ford (default)
+    const size_t lds = ((size_t)C.nS + 3u * ((C.nS + 31u) / 32u)) * 4u;
+    const uint32_t per_cu = std::max<uint32_t>(1, (uint32_t)((150u * 1024u) / (lds + 12u * 1024u)));
+    const uint32_t grid = std::min<uint32_t>(a.n, n_cu * std::min<uint32_t>(per_cu, 4u));
+    if (lds > 48 * 1024) {
+      hipError_t e = hipFuncSetAttribute((const void*)cover_bf_kernel,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(cover_bf_kernel, dim3(grid), dim3(kBlock), lds, s, g, C, a);
+    return hipGetLastError();
+  }
   const size_t lds = ((size_t)C.nS + (C.nS + 31u) / 32u) * 4u;
   const uint32_t per_cu = std::max<uint32_t>(1, (uint32_t)((150u * 1024u) / (lds + 10u * 1024u)));
   const uint32_t grid = std::min<uint32_t>(a.n, n_cu * std::min<uint32_t>(per_cu, 4u));
