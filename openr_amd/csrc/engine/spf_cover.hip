@@ -161,7 +161,9 @@ __device__ __forceinline__ void write_row(const DevGraph& g, const CoverGraph& C
   }
 }
 
-// Frontier Bellman-Ford over the contracted graph (the cover SPF's default):
+// Frontier Bellman-Ford over the contracted graph (OSPF_COVER_BF=1; measured
+// slower than the Dial rounds on the weighted F100k, 341 vs 83 ms: the
+// spines' 1,781-edge rows are re-expanded at every improvement):
 // a round expands the transit cover nodes whose distance dropped in the
 // previous round (and the root in the first), each from its current
 // distance, their edges flattened over each wave; a relaxation that lowers a
@@ -353,7 +355,7 @@ __global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C
 hipError_t launch_cover_spf(const DevGraph& g, const CoverGraph& C, const CoverArgs& a,
                             uint32_t n_cu, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  if (!getenv("OSPF_COVER_DIAL")) {  // frontier Bellman-Ford (default)
+  if (getenv("OSPF_COVER_BF")) {  // frontier Bellman-Ford (F100k-w: 341 vs 83 ms Dial)
     const size_t lds = ((size_t)C.nS + 3u * ((C.nS + 31u) / 32u)) * 4u;
     const uint32_t per_cu = std::max<uint32_t>(1, (uint32_t)((150u * 1024u) / (lds + 12u * 1024u)));
     const uint32_t grid = std::min<uint32_t>(a.n, n_cu * std::min<uint32_t>(per_cu, 4u));

@@ -1843,14 +1843,28 @@ __global__ void __launch_bounds__(256) nh_derive_wide3_kernel(DevGraph g, Derive
     for (uint32_t t = t0; t < t1; ++t) {
       const uint32_t v0 = t * kW3Tile;
       __syncthreads();  // s_pos written / the previous tile's bytes consumed
-      for (uint32_t k = tid; k < K; k += kBlock) {
-        const uint32_t p = s_pos[k];
-        uint4 x = make_uint4(~0u, ~0u, ~0u, ~0u);
-        if (p < 0x80000000u) {
-          x = *reinterpret_cast<const uint4*>(d.lev + (size_t)p * d.pitch + v0);
-        } else if (p != kInf) {
+      // every slot load of the thread in flight at once (K <= 2048: <= 8 each)
+      uint32_t pk[kDeriveTab / kBlock];
+      uint4 xk[kDeriveTab / kBlock];
+#pragma unroll
+      for (uint32_t m = 0; m < kDeriveTab / kBlock; ++m) {
+        const uint32_t k = tid + m * kBlock;
+        pk[m] = k < K ? s_pos[k] : kInf;
+      }
+#pragma unroll
+      for (uint32_t m = 0; m < kDeriveTab / kBlock; ++m) {
+        const uint32_t row = pk[m] < 0x80000000u ? pk[m] : s_own[j0];  // a valid row, masked below
+        xk[m] = *reinterpret_cast<const uint4*>(d.lev + (size_t)row * d.pitch + v0);
+      }
+#pragma unroll
+      for (uint32_t m = 0; m < kDeriveTab / kBlock; ++m) {
+        const uint32_t k = tid + m * kBlock, p = pk[m];
+        if (k >= K) break;
+        uint4 x = xk[m];
+        if (p >= 0x80000000u) {
+          x = make_uint4(~0u, ~0u, ~0u, ~0u);
           const uint32_t o = (p & 0x7FFFFFFFu) - v0;
-          if (o < kW3Tile) {
+          if (p != kInf && o < kW3Tile) {
             uint32_t w4[4] = {x.x, x.y, x.z, x.w};
             w4[o >> 2] = (w4[o >> 2] & ~(0xFFu << (8u * (o & 3u)))) | (1u << (8u * (o & 3u)));
             x = make_uint4(w4[0], w4[1], w4[2], w4[3]);

@@ -370,8 +370,10 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinArg
   __shared__ uint32_t s_urow[kTwinMaxC], s_nu, s_ok;
   __shared__ unsigned long long s_d[kWaves][kTwinLvG][3];
   const uint32_t V = g.V, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const uint32_t b = blockIdx.x, B8 = a.ngroups / 8u * 8u;  // XCD-aware group order
-  const uint32_t gi = b < B8 ? (b % 8u) * (B8 / 8u) + b / 8u : b;
+  // block = (group, part of the chunk range); XCD-aware order over the items
+  const uint32_t NB = a.ngroups * a.chunks, B8 = NB / 8u * 8u, b = blockIdx.x;
+  const uint32_t item = b < B8 ? (b % 8u) * (B8 / 8u) + b / 8u : b;
+  const uint32_t gi = item / a.chunks, part = item % a.chunks;
   const uint32_t i0 = a.grp ? a.grp[gi] : gi;
   const uint32_t ng = a.grp ? min(kTwinLvG, a.grp[gi + 1] - i0) : 1u;
   if (tid == 0) {
@@ -419,13 +421,18 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinArg
 #pragma unroll
   for (uint32_t u = 0; u < kTwinMaxC; ++u) urow[u] = u < nu ? s_urow[u] : 0u;
   const uint32_t nchunks = (a.pitch + 255u) / 256u;
-  auto load_x = [&](uint32_t c, uint32_t* x) {
+  const uint32_t cb = (uint32_t)((uint64_t)part * nchunks / a.chunks);
+  const uint32_t ce = (uint32_t)((uint64_t)(part + 1) * nchunks / a.chunks);
+  // the next chunk's rows and distance keys are loaded before this one is used
+  auto load_x = [&](uint32_t c, uint32_t* x, uint64_t* kd) {
     const uint32_t v0 = c * 256u + 4u * lane;
-    const bool ok = c < nchunks && v0 < a.pitch;
+    const bool ok = c < ce && v0 < a.pitch;
 #pragma unroll
     for (uint32_t u = 0; u < kTwinMaxC; ++u)
       x[u] = (u < nu && ok) ? *reinterpret_cast<const uint32_t*>(a.lev + (size_t)urow[u] * a.pitch + v0)
                             : 0x7F7F7F7Fu;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) kd[q] = ok && v0 + q < V ? g.dkey[2ull * (v0 + q)] : 0ull;
   };
   uint32_t br[kTwinLvG], cur[kTwinLvG];
   uint64_t bs[kTwinLvG], bh[kTwinLvG];
@@ -437,17 +444,18 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinArg
   }
   const bool vec = (V & 3u) == 0;
   uint32_t xn[kTwinMaxC];
-  load_x(wave, xn);
-  for (uint32_t c = wave; c < nchunks; c += kWaves) {
+  uint64_t kdn[4];
+  load_x(cb + wave, xn, kdn);
+  for (uint32_t c = cb + wave; c < ce; c += kWaves) {
     const uint32_t c0 = c * 256u, v0 = c0 + 4u * lane;
     uint32_t x[kTwinMaxC];
-#pragma unroll
-    for (uint32_t u = 0; u < kTwinMaxC; ++u) x[u] = xn[u];
-    load_x(c + kWaves, xn);
-    if (v0 >= a.pitch) continue;  // no wave-level work below (cursors are per wave: see skip)
     uint64_t kd[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) kd[q] = v0 + q < V ? g.dkey[2ull * (v0 + q)] : 0ull;
+    for (uint32_t u = 0; u < kTwinMaxC; ++u) x[u] = xn[u];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) kd[q] = kdn[q];
+    load_x(c + kWaves, xn, kdn);
+    if (v0 >= a.pitch) continue;  // no wave-level work below (cursors are per wave: see skip)
 #pragma unroll
     for (uint32_t j = 0; j < kTwinLvG; ++j) {
       if (j >= ng) break;
@@ -517,8 +525,17 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinArg
       d.sum_dist += s_d[w][tid][1];
       d.hash += s_d[w][tid][2];
     }
-    a.lev_digest_w[s_own[tid]] = d;
+    ospf_digest* o = a.lev_digest_w + s_own[tid];  // zeroed by twin_zero_kernel
+    atomicAdd((unsigned long long*)&o->reached, (unsigned long long)d.reached);
+    atomicAdd((unsigned long long*)&o->sum_dist, (unsigned long long)d.sum_dist);
+    atomicAdd((unsigned long long*)&o->hash, (unsigned long long)d.hash);
   }
+}
+
+__global__ void twin_zero_kernel(const uint32_t* roots, uint32_t n, const uint32_t* pos,
+                                 uint32_t V, ospf_digest* out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && roots[i] < V && pos[roots[i]] != kInf) out[pos[roots[i]]] = ospf_digest{0ull, 0ull, 0ull};
 }
 }  // namespace
 
@@ -546,7 +563,16 @@ hipError_t launch_nh_derive_twin(const DevGraph& g, const TwinArgs& a0, hipStrea
 namespace ospf {
 hipError_t launch_twin_levels(const DevGraph& g, const TwinArgs& a, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(twin_levels_kernel, dim3(a.grp ? a.ngroups : a.n), dim3(kBlock), 0, s, g, a);
+  TwinArgs b = a;
+  if (!b.grp) b.ngroups = b.n;
+  // parts of the chunk range per group: ~4096 blocks, >= 8 chunks each
+  const uint32_t nchunks = (b.pitch + 255u) / 256u;
+  b.chunks = b.ctiles ? b.ctiles
+                      : std::max(1u, std::min(std::max(1u, nchunks / 8u), 4096u / std::max(1u, b.ngroups)));
+  if (b.lev_digest_w)
+    hipLaunchKernelGGL(twin_zero_kernel, dim3((b.n + 255u) / 256u), dim3(256), 0, s, b.roots, b.n, b.pos,
+                       g.V, b.lev_digest_w);
+  hipLaunchKernelGGL(twin_levels_kernel, dim3(b.ngroups * b.chunks), dim3(kBlock), 0, s, g, b);
   return hipGetLastError();
 }
 }  // namespace ospf
