@@ -694,6 +694,72 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
 
 }  // namespace
 
+namespace ospf_int {
+
+int twin_lv_build(ospf_ctx* c, const std::vector<uint32_t>& roots, const std::vector<uint32_t>& groups,
+                  const std::vector<uint32_t>& pos, const std::vector<uint32_t>& cls,
+                  const std::vector<uint32_t>& rep, TwinLvHost& out) {
+  const uint32_t V = c->info.n_nodes, n = (uint32_t)roots.size();
+  out = TwinLvHost{};
+  out.grp = groups;
+  if (out.grp.empty())
+    for (uint32_t i = 0; i <= n; ++i) out.grp.push_back(i);
+  if (out.grp.front() != 0 || out.grp.back() != n)
+    return fail(c, OSPF_E_INVAL, "twin levels: group offsets must run 0 .. n");
+  out.nbo.assign(1, 0u);
+  std::vector<uint32_t> rows;  // this root's class rows
+  for (size_t gi = 0; gi + 1 < out.grp.size(); ++gi) {
+    const uint32_t g0 = out.grp[gi], g1 = out.grp[gi + 1];
+    if (g1 < g0 || g1 - g0 > ospf::kTwinLvG)
+      return fail(c, OSPF_E_RANGE, "twin levels: a group of more than 8 roots");
+    std::vector<uint32_t> urow;
+    for (uint32_t i = g0; i < g1; ++i) {
+      const uint32_t r = roots[i];
+      if (r >= V || pos[r] == 0xFFFFFFFFu) return fail(c, OSPF_E_RANGE, "twin levels: a root without a row");
+      rows.clear();
+      const size_t nb0 = out.nbl.size();
+      for (uint32_t e = c->h_prow[r]; e < c->h_prow[r + 1]; ++e) {
+        const uint32_t x = c->h_pcolx[e];
+        if ((x & 0x80000000u) || x == r) continue;
+        if (out.nbl.size() == nb0 || out.nbl.back() != x) out.nbl.push_back(x);  // rows ascend
+        if ((c->h_nt[x >> 5] >> (x & 31)) & 1u) continue;  // overloaded: reaches only itself
+        const uint32_t k = cls[x];
+        const uint32_t row = k < rep.size() && rep[k] < V ? pos[rep[k]] : 0xFFFFFFFFu;
+        if (row == 0xFFFFFFFFu) return fail(c, OSPF_E_RANGE, "twin levels: a class row is missing");
+        rows.push_back(row);
+      }
+      if (out.nbl.size() - nb0 > 128)
+        return fail(c, OSPF_E_RANGE, "twin levels: more than 128 usable neighbours");
+      out.nbo.push_back((uint32_t)out.nbl.size());
+      uint32_t mask = 0;
+      for (uint32_t row : rows) {
+        uint32_t u = 0;
+        while (u < urow.size() && urow[u] != row) ++u;
+        if (u == urow.size()) {
+          if (u == ospf::kTwinMaxC)
+            return fail(c, OSPF_E_RANGE, "twin levels: more than 16 class rows in a group");
+          urow.push_back(row);
+        }
+        mask |= 1u << u;
+      }
+      out.rinfo.push_back(make_uint4(r, pos[r], mask, (uint32_t)nb0));
+    }
+    urow.resize(ospf::kTwinMaxC, 0xFFFFFFFFu);
+    out.grow.insert(out.grow.end(), urow.begin(), urow.end());
+  }
+  return OSPF_OK;
+}
+
+int twin_lv_launch(ospf_ctx* c, const ospf::TwinLvPlan& p, void* stream) {
+  HIPCHK(c, hipSetDevice(c->device));
+  const hipError_t e = ospf::launch_twin_levels(c->g, p, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(c, e, "launch_twin_levels");
+  c->spf_runs += p.n;
+  return OSPF_OK;
+}
+
+}  // namespace ospf_int
+
 extern "C" {
 
 int ospf_open(int device, ospf_ctx** out) {
@@ -1377,6 +1443,9 @@ int ospf_nh_derive_twin_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, ui
 
 // Twin levels (spf_twin.hip): level + dist rows of roots from the
 // representative rows of their neighbours' twin classes (no traversal).
+
+// The public entry reads its (device) inputs back, plans on the host and
+// waits for the launch (the sweep plans once and replays).
 int ospf_twin_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n,
                          const uint32_t* d_groups, uint32_t n_groups, uint8_t* d_lev,
                          uint32_t lev_pitch, const uint32_t* d_pos, const uint32_t* d_twin_class,
@@ -1390,29 +1459,58 @@ int ospf_twin_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n,
   if (lev_pitch % 16u || lev_pitch < c->info.n_nodes)
     return fail(c, OSPF_E_INVAL, "lev_pitch: a multiple of 16 >= V");
   if (c->depth_bound > 123) return fail(c, OSPF_E_RANGE, "level rows need a depth bound <= 123");
+  if (d_groups && n_groups == 0) return fail(c, OSPF_E_INVAL, "twin levels: no groups");
+  const uint32_t V = c->info.n_nodes;
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(c, hipSetDevice(c->device));
-  ospf::TwinArgs a{};
-  a.roots = d_roots;
+  HIPCHK(c, hipStreamSynchronize(s));
+  std::vector<uint32_t> roots(n), pos(V), cls(V), groups;
+  HIPCHK(c, hipMemcpy(roots.data(), d_roots, n * 4ull, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(pos.data(), d_pos, V * 4ull, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(cls.data(), d_twin_class, V * 4ull, hipMemcpyDeviceToHost));
+  uint32_t ncls = 0;
+  for (uint32_t k : cls)
+    if (k != 0xFFFFFFFFu) ncls = std::max(ncls, k + 1);
+  std::vector<uint32_t> rep(ncls);
+  if (ncls) HIPCHK(c, hipMemcpy(rep.data(), d_twin_rep, ncls * 4ull, hipMemcpyDeviceToHost));
+  if (d_groups) {
+    groups.resize(n_groups + 1);
+    HIPCHK(c, hipMemcpy(groups.data(), d_groups, (n_groups + 1) * 4ull, hipMemcpyDeviceToHost));
+  }
+  ospf_int::TwinLvHost h;
+  int rc = ospf_int::twin_lv_build(c, roots, groups, pos, cls, rep, h);
+  if (rc) return rc;
+  void* buf = nullptr;
+  const size_t b0 = h.grp.size() * 4, b1 = h.grow.size() * 4, b2 = h.rinfo.size() * 16,
+               b3 = h.nbo.size() * 4, b4 = std::max<size_t>(4, h.nbl.size() * 4);
+  HIPCHK(c, hipMalloc(&buf, b0 + b1 + b2 + b3 + b4 + 64));
+  char* p = (char*)buf;
+  ospf::TwinLvPlan a{};
   a.n = n;
-  a.W = 4;
-  a.cap = 128;
+  a.ngroups = (uint32_t)h.grp.size() - 1;
+  a.rinfo = (const uint4*)p;
+  HIPCHK(c, hipMemcpy(p, h.rinfo.data(), b2, hipMemcpyHostToDevice));
+  p += b2;
+  a.grp = (const uint32_t*)p;
+  HIPCHK(c, hipMemcpy(p, h.grp.data(), b0, hipMemcpyHostToDevice));
+  p += b0;
+  a.grow = (const uint32_t*)p;
+  HIPCHK(c, hipMemcpy(p, h.grow.data(), b1, hipMemcpyHostToDevice));
+  p += b1;
+  a.nbo = (const uint32_t*)p;
+  HIPCHK(c, hipMemcpy(p, h.nbo.data(), b3, hipMemcpyHostToDevice));
+  p += b3;
+  a.nbl = (const uint32_t*)p;
+  if (!h.nbl.empty()) HIPCHK(c, hipMemcpy(p, h.nbl.data(), h.nbl.size() * 4, hipMemcpyHostToDevice));
   a.lev = d_lev;
-  a.lev_w = d_lev;
   a.pitch = lev_pitch;
-  a.pos = d_pos;
-  a.tcls = d_twin_class;
-  a.trep = d_twin_rep;
-  a.tsec = nullptr;
-  a.grp = d_groups;
-  a.ngroups = d_groups ? n_groups : n;
-  if (d_groups && n_groups == 0) return fail(c, OSPF_E_INVAL, "twin levels: no groups");
   a.dist = d_dist;
-  a.lev_digest_w = d_lev_digest;
-  a.err = c->d_err;
-  hipError_t e = ospf::launch_twin_levels(c->g, a, s);
-  if (e != hipSuccess) return hip_fail(c, e, "launch_twin_levels");
-  c->spf_runs += n;
+  a.lev_digest = d_lev_digest;
+  rc = ospf_int::twin_lv_launch(c, a, s);
+  const hipError_t e = hipStreamSynchronize(s);
+  hipFree(buf);
+  if (rc) return rc;
+  if (e != hipSuccess) return hip_fail(c, e, "twin levels");
   return OSPF_OK;
 }
 

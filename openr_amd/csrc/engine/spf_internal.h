@@ -81,6 +81,23 @@ char* stream_scratch(ospf_ctx* c, void* stream, size_t need, int* rc, int slot =
 // frees the scratch of `stream` (both slots); the stream must be idle
 void release_stream_scratch(ospf_ctx* c, void* stream);
 
+// Host plan of twin levels (spf_twin.hip twin_levels_kernel) for `roots` in
+// order, cut into the caller's groups (offsets; empty = one root per group):
+// per root its usable distinct neighbours (ascending) and the level-row
+// positions (pos[rep[class]]) of its usable transit neighbours' classes, per
+// group the union of those rows. OSPF_E_RANGE when a root has more than 128
+// usable neighbours, a group more than kTwinMaxC class rows, or a class row
+// is missing.
+struct TwinLvHost {
+  std::vector<uint32_t> grp, grow, nbo, nbl;
+  std::vector<uint4> rinfo;
+};
+int twin_lv_build(ospf_ctx* c, const std::vector<uint32_t>& roots, const std::vector<uint32_t>& groups,
+                  const std::vector<uint32_t>& pos, const std::vector<uint32_t>& cls,
+                  const std::vector<uint32_t>& rep, TwinLvHost& out);
+// queue a planned twin-levels launch (device copies of the plan's arrays)
+int twin_lv_launch(ospf_ctx* c, const ospf::TwinLvPlan& p, void* stream);
+
 }  // namespace ospf_int
 
 #define HIPCHK(ctx, call)                                            \

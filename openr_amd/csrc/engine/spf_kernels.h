@@ -317,17 +317,27 @@ struct TwinArgs {
   uint32_t* err;          // + bit 256: a root with more than kTwinMaxC classes
   uint32_t tiles, ctiles, chunks;
   // twin_levels_kernel: the roots' own rows at pos[root]
-  const uint32_t* grp;        // [ngroups + 1] root groups (<= 8 roots, <= 16 class rows each) or null
-  uint32_t ngroups;
-  uint8_t* lev_w;             // level rows written (same buffer as lev)
-  uint32_t* dist;             // [rows][V] or null
-  ospf_digest* lev_digest_w;  // [rows] distance parts (stored) or null
 };
 hipError_t launch_nh_derive_twin(const DevGraph& g, const TwinArgs& a, hipStream_t s);
-// level + dist rows (+ the distance part of the digest) of roots whose usable
-// transit neighbours fall into <= kTwinMaxC twin classes, from the classes'
-// representative level rows (one block per root)
-hipError_t launch_twin_levels(const DevGraph& g, const TwinArgs& a, hipStream_t s);
+// Twin levels (twin_levels_kernel): level + dist rows (+ the distance part of
+// the digest) of roots from the level rows of their neighbours' twin classes'
+// representatives; the caller plans the groups on the host (<= kTwinLvG
+// roots, <= kTwinMaxC class rows per group).
+constexpr uint32_t kTwinLvG = 8;
+struct TwinLvPlan {
+  uint32_t n, ngroups;
+  const uint32_t* grp;    // [ngroups + 1] root offsets
+  const uint32_t* grow;   // [ngroups][kTwinMaxC] class rows (level-row positions; kInf unused)
+  const uint4* rinfo;     // [n] {root, own row, mask over the group's class rows, nbl offset}
+  const uint32_t* nbo;    // [n + 1] offsets into nbl
+  const uint32_t* nbl;    // usable distinct neighbours of each root, ascending (<= 128)
+  uint8_t* lev;           // level rows: class rows read, the roots' own rows written
+  uint32_t pitch;
+  uint32_t* dist;         // [rows][V] or null
+  ospf_digest* lev_digest;  // [rows] distance parts (zeroed, then added) or null
+  uint32_t parts;         // blocks per group over the node range (0: launcher's choice)
+};
+hipError_t launch_twin_levels(const DevGraph& g, const TwinLvPlan& a, hipStream_t s);
 
 // Leaf derive (spf_leaf.hip), unit metric / hop count: the level, dist and
 // one-word next-hop rows of leaf roots (<= 32 distinct neighbours, every

@@ -611,7 +611,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   for (uint32_t i = 0; i < nL; ++i)
     if (pos[need_l[i]] == kNone) pos[need_l[i]] = rows++;
   const uint32_t pitch = (V + 15) / 16 * 16;
-  uint32_t *d_clo = nullptr, *d_drv = nullptr, *d_pos, *dist, *d_l = nullptr, *lnh = nullptr;
+  uint32_t *d_clo = nullptr, *d_pos, *dist, *d_l = nullptr, *lnh = nullptr;
   uint32_t *d_grp_r = nullptr, *d_grp = nullptr, *d_lout = nullptr;
   uint8_t* lev;
   ospf_digest* ldg;
@@ -620,7 +620,6 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       (rc = dalloc(s, &dist, (size_t)rows * V)) || (rc = dalloc(s, &ldg, std::max(1u, nc + nd))))
     return rc;
   if (nc && (rc = upload(s, &d_clo, clo))) return rc;
-  if (nd && (rc = upload(s, &d_drv, drv))) return rc;
   if (nL && ((rc = upload(s, &d_l, need_l)) || (rc = dalloc(s, &lnh, (size_t)nL * V))))
     return rc;
   if (nR && (rc = upload(s, &d_grp_r, grp_r))) return rc;
@@ -669,11 +668,29 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   }
   for (uint32_t k = 0; k < S; ++k) {
     const uint32_t i0 = dgo[sg[k]], n = dgo[sg[k + 1]] - i0;
-    std::vector<uint32_t> gk;
+    std::vector<uint32_t> gk, rk(drv.begin() + i0, drv.begin() + i0 + n);
     for (uint32_t g = sg[k]; g <= sg[k + 1]; ++g) gk.push_back(dgo[g] - i0);
-    uint32_t* d_gk;
-    if ((rc = upload(s, &d_gk, gk))) return rc;
-    const uint32_t ngk = sg[k + 1] - sg[k];
+    // the stage's plan, built once on the host (spf_twin.hip twin_levels_kernel)
+    ospf_int::TwinLvHost h;
+    if ((rc = ospf_int::twin_lv_build(c, rk, gk, pos, tw.cls, tw.rep, h))) return sfail(s, rc, c->err);
+    ospf::TwinLvPlan plan{};
+    uint32_t *d_grp2, *d_grow, *d_nbo, *d_nbl;
+    uint4* d_rinfo;
+    if ((rc = upload(s, &d_grp2, h.grp)) || (rc = upload(s, &d_grow, h.grow)) ||
+        (rc = upload(s, &d_nbo, h.nbo)) || (rc = upload(s, &d_nbl, h.nbl)) ||
+        (rc = upload(s, &d_rinfo, h.rinfo)))
+      return rc;
+    plan.n = n;
+    plan.ngroups = (uint32_t)h.grp.size() - 1;
+    plan.grp = d_grp2;
+    plan.grow = d_grow;
+    plan.rinfo = d_rinfo;
+    plan.nbo = d_nbo;
+    plan.nbl = d_nbl;
+    plan.lev = lev;
+    plan.pitch = pitch;
+    plan.dist = dist;
+    plan.lev_digest = ldg;
     ospf_sweep::Unit u;
     u.name = S > 1 ? "twin_levels_s" + std::to_string(k) : std::string("twin_levels");
     u.kernel = "ospf_twin_levels_dev (twin_levels_kernel: level + dist rows from the neighbour "
@@ -683,10 +700,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     u.n_roots = n;
     // dist rows written (level rows are intermediate)
     u.comp = (uint64_t)n * 4ull * V;
-    const uint32_t *tc = d_tcls, *tr = d_trep, *dr = d_drv + i0;
-    u.fn = [=](hipStream_t st) {
-      return ospf_twin_levels_dev(c, dr, n, d_gk, ngk, lev, pitch, d_pos, tc, tr, dist, ldg, st);
-    };
+    u.fn = [=](hipStream_t st) { return ospf_int::twin_lv_launch(c, plan, st); };
     s->step_comp += u.comp;
     s->units.push_back(u);
   }
@@ -749,6 +763,9 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     // twin classes read the representatives' rows (BFS'd with twin levels);
     // the others every neighbour's row
     u.wait = {!k.reads_leaf ? ev_cov : k.twin ? (twin_lv ? ev_cov : ev_r) : ev_b};
+    // every leaf row (ev_b) does not imply every derived cover row when the
+    // last leaf stage precedes the last twin-levels stage
+    if (u.wait[0] == ev_b && nd) u.wait.push_back(ev_cov);
     u.n_roots = n;
     u.W = W;
     u.comp = (uint64_t)n * 4ull * V * W;

@@ -362,67 +362,40 @@ __device__ __forceinline__ uint32_t bmin7(uint32_t a, uint32_t b) {
 // neighbours' positions (each root's sorted neighbour list walked by a
 // cursor) and stores 256 B of level row + 1 KB of dist row per instruction.
 // The distance part of each root's digest is stored (not added).
-constexpr uint32_t kTwinLvG = 8;
-__global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinArgs a) {
-  __shared__ TwinTab T;                       // setup scratch, one root at a time
+__global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvPlan a) {
   __shared__ uint32_t s_nb[kTwinLvG][kMaxK];  // usable neighbours (ascending), per root
   __shared__ uint32_t s_nnb[kTwinLvG], s_root[kTwinLvG], s_own[kTwinLvG], s_umask[kTwinLvG];
-  __shared__ uint32_t s_urow[kTwinMaxC], s_nu, s_ok;
   __shared__ unsigned long long s_d[kWaves][kTwinLvG][3];
   const uint32_t V = g.V, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   // block = (group, part of the chunk range); XCD-aware order over the items
-  const uint32_t NB = a.ngroups * a.chunks, B8 = NB / 8u * 8u, b = blockIdx.x;
+  const uint32_t NB = a.ngroups * a.parts, B8 = NB / 8u * 8u, b = blockIdx.x;
   const uint32_t item = b < B8 ? (b % 8u) * (B8 / 8u) + b / 8u : b;
-  const uint32_t gi = item / a.chunks, part = item % a.chunks;
-  const uint32_t i0 = a.grp ? a.grp[gi] : gi;
-  const uint32_t ng = a.grp ? min(kTwinLvG, a.grp[gi + 1] - i0) : 1u;
-  if (tid == 0) {
-    s_nu = 0u;
-    s_ok = 1u;
+  const uint32_t gi = item / a.parts, part = item % a.parts;
+  const uint32_t i0 = a.grp[gi];
+  const uint32_t ng = min(kTwinLvG, a.grp[gi + 1] - i0);
+  if (tid < ng) {
+    const uint4 ri = a.rinfo[i0 + tid];
+    s_root[tid] = ri.x;
+    s_own[tid] = ri.y;
+    s_umask[tid] = ri.z;
+    s_nnb[tid] = min(kMaxK, a.nbo[i0 + tid + 1] - ri.w);
   }
-  for (uint32_t j = 0; j < ng; ++j) {
-    if (!twin_setup(g, a, i0 + j, 4, T)) return;  // block-uniform; error bits set
-    const uint32_t K = min(T.K, kMaxK);
-    if (tid < 64) {  // usable neighbours in ascending order (wave 0)
-      uint32_t cnt = 0;
-      for (uint32_t base = 0; base < K; base += 64u) {
-        const uint32_t k = base + lane;
-        const bool f = k < K && T.cid[k] != kInf;
-        const uint64_t bal = __ballot(f);
-        if (f) s_nb[j][cnt + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = T.nb[k];
-        cnt += (uint32_t)__popcll(bal);
-      }
-      if (lane == 0) s_nnb[j] = cnt;
-    }
-    if (tid == 0) {
-      s_root[j] = T.root;
-      s_own[j] = T.own;
-      uint32_t mask = 0;
-      for (uint32_t x = 0; x < T.nc; ++x) {
-        uint32_t u = 0;
-        while (u < s_nu && s_urow[u] != T.crow[x]) ++u;
-        if (u == s_nu) {
-          if (u == kTwinMaxC) {
-            s_ok = 0u;
-            atomicOr(a.err, 256u);
-            break;
-          }
-          s_urow[s_nu++] = T.crow[x];
-        }
-        mask |= 1u << u;
-      }
-      s_umask[j] = mask;
-    }
-    __syncthreads();  // T is rewritten by the next root
+  for (uint32_t x = tid; x < ng * kMaxK; x += kBlock) {
+    const uint32_t j = x / kMaxK, k = x % kMaxK;
+    const uint32_t o = a.nbo[i0 + j];
+    if (o + k < a.nbo[i0 + j + 1]) s_nb[j][k] = a.nbl[o + k];
   }
-  if (!s_ok) return;
-  const uint32_t nu = s_nu;
   uint32_t urow[kTwinMaxC];
+  uint32_t nu = 0;
 #pragma unroll
-  for (uint32_t u = 0; u < kTwinMaxC; ++u) urow[u] = u < nu ? s_urow[u] : 0u;
+  for (uint32_t u = 0; u < kTwinMaxC; ++u) {
+    urow[u] = a.grow[(size_t)gi * kTwinMaxC + u];
+    nu += urow[u] != kInf ? 1u : 0u;
+  }
+  __syncthreads();
   const uint32_t nchunks = (a.pitch + 255u) / 256u;
-  const uint32_t cb = (uint32_t)((uint64_t)part * nchunks / a.chunks);
-  const uint32_t ce = (uint32_t)((uint64_t)(part + 1) * nchunks / a.chunks);
+  const uint32_t cb = (uint32_t)((uint64_t)part * nchunks / a.parts);
+  const uint32_t ce = (uint32_t)((uint64_t)(part + 1) * nchunks / a.parts);
   // the next chunk's rows and distance keys are loaded before this one is used
   auto load_x = [&](uint32_t c, uint32_t* x, uint64_t* kd) {
     const uint32_t v0 = c * 256u + 4u * lane;
@@ -476,7 +449,7 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinArg
       const uint32_t off = s_root[j] - v0;
       if (off < 4u) L = (L & ~(0xFFu << (8u * off))) | (1u << (8u * off));
       const uint32_t own = s_own[j];
-      __builtin_nontemporal_store(L, reinterpret_cast<uint32_t*>(a.lev_w + (size_t)own * a.pitch + v0));
+      __builtin_nontemporal_store(L, reinterpret_cast<uint32_t*>(a.lev + (size_t)own * a.pitch + v0));
       if (v0 >= V) continue;
       uint32_t dv[4];
 #pragma unroll
@@ -501,7 +474,7 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinArg
       }
     }
   }
-  if (!a.lev_digest_w) return;
+  if (!a.lev_digest) return;
 #pragma unroll
   for (uint32_t j = 0; j < kTwinLvG; ++j) {
     uint64_t r64 = br[j];
@@ -525,18 +498,18 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinArg
       d.sum_dist += s_d[w][tid][1];
       d.hash += s_d[w][tid][2];
     }
-    ospf_digest* o = a.lev_digest_w + s_own[tid];  // zeroed by twin_zero_kernel
+    ospf_digest* o = a.lev_digest + s_own[tid];  // zeroed by twin_zero_kernel
     atomicAdd((unsigned long long*)&o->reached, (unsigned long long)d.reached);
     atomicAdd((unsigned long long*)&o->sum_dist, (unsigned long long)d.sum_dist);
     atomicAdd((unsigned long long*)&o->hash, (unsigned long long)d.hash);
   }
 }
 
-__global__ void twin_zero_kernel(const uint32_t* roots, uint32_t n, const uint32_t* pos,
-                                 uint32_t V, ospf_digest* out) {
+__global__ void twin_zero_kernel(const uint4* rinfo, uint32_t n, ospf_digest* out) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n && roots[i] < V && pos[roots[i]] != kInf) out[pos[roots[i]]] = ospf_digest{0ull, 0ull, 0ull};
+  if (i < n) out[rinfo[i].y] = ospf_digest{0ull, 0ull, 0ull};
 }
+
 }  // namespace
 
 hipError_t launch_nh_derive_twin(const DevGraph& g, const TwinArgs& a0, hipStream_t s) {
@@ -561,18 +534,17 @@ hipError_t launch_nh_derive_twin(const DevGraph& g, const TwinArgs& a0, hipStrea
 }  // namespace ospf
 
 namespace ospf {
-hipError_t launch_twin_levels(const DevGraph& g, const TwinArgs& a, hipStream_t s) {
-  if (a.n == 0) return hipSuccess;
-  TwinArgs b = a;
-  if (!b.grp) b.ngroups = b.n;
+hipError_t launch_twin_levels(const DevGraph& g, const TwinLvPlan& a0, hipStream_t s) {
+  if (a0.n == 0) return hipSuccess;
+  TwinLvPlan a = a0;
   // parts of the chunk range per group: ~4096 blocks, >= 8 chunks each
-  const uint32_t nchunks = (b.pitch + 255u) / 256u;
-  b.chunks = b.ctiles ? b.ctiles
-                      : std::max(1u, std::min(std::max(1u, nchunks / 8u), 4096u / std::max(1u, b.ngroups)));
-  if (b.lev_digest_w)
-    hipLaunchKernelGGL(twin_zero_kernel, dim3((b.n + 255u) / 256u), dim3(256), 0, s, b.roots, b.n, b.pos,
-                       g.V, b.lev_digest_w);
-  hipLaunchKernelGGL(twin_levels_kernel, dim3(b.ngroups * b.chunks), dim3(kBlock), 0, s, g, b);
+  const uint32_t nchunks = (a.pitch + 255u) / 256u;
+  if (!a.parts)
+    a.parts = std::max(1u, std::min(std::max(1u, nchunks / 8u), 4096u / std::max(1u, a.ngroups)));
+  if (a.lev_digest)
+    hipLaunchKernelGGL(twin_zero_kernel, dim3((a.n + 255u) / 256u), dim3(256), 0, s, a.rinfo, a.n,
+                       a.lev_digest);
+  hipLaunchKernelGGL(twin_levels_kernel, dim3(a.ngroups * a.parts), dim3(kBlock), 0, s, g, a);
   return hipGetLastError();
 }
 }  // namespace ospf

@@ -63,6 +63,8 @@ for st in $STEPS; do
              echo "ab $kv rc=$rc $(python -c "import json,sys; d=json.load(open('$OUT/ab_$kv.json')); print(d['value'], d['ms_per_step'], d['parity_vs_cpu_sample'])" 2>/dev/null)"
              [ $rc -eq 0 ] || break
            done;;
+    debug) timeout -k 10 300 python scripts/debug/${DBG:-stage_digests.py} > "$OUT/debug.log" 2>&1; rc=$?
+           tail -30 "$OUT/debug.log";;
     derive) timeout -k 10 600 $PYT tests/test_gpu_derive.py tests/test_gpu_wderive.py > "$OUT/derive.log" 2>&1; rc=$?
            tail -3 "$OUT/derive.log";;
     *) echo "unknown step $st"; rc=2;;
