@@ -2171,8 +2171,10 @@ hipError_t launch_nh_derive(const DevGraph& g, const DeriveArgs& d0, hipStream_t
     if (const char* e = getenv("OSPF_DERIVE_WIDE_G"))
       d.G = std::max<uint32_t>(1, std::min<uint32_t>(kWideG, (uint32_t)atoi(e)));
     const size_t lds3 = 4ull * d.W * d.G + (size_t)d.cap * kW3Pitch;
-    if (d.W <= 64 && (d.pitch % kW3Tile) == 0 && !getenv("OSPF_DERIVE_WIDE1")) {
-      // tile-staged: ~4096 blocks of 16-node tiles
+    if (d.W <= 64 && (d.pitch % kW3Tile) == 0 && getenv("OSPF_DERIVE_WIDE3")) {
+      // tile-staged, ~4096 blocks of 16-node tiles (F100k spines: 9.6 ms
+      // against 5.9 for nh_derive_wide_kernel: the per-block setup of 64
+      // roots' slot tables is paid 4.5x as often; not the default)
       const uint32_t ngroups = (d.n + d.G - 1) / d.G;
       d.tiles = (g.V + kW3Tile - 1) / kW3Tile;
       if (!d.ctiles) d.ctiles = std::max<uint32_t>(1, d.tiles / std::max<uint32_t>(1, 4096u / ngroups));

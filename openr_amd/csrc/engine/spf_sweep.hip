@@ -567,10 +567,12 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   // pipeline stages: the derived rows in S stages of whole groups (blocks of
   // pods on a fabric); a leaf group or a twin next-hop root waits only for
   // the stage of the derived rows it reads, so the leaves' row stores run
-  // beside the later stages (OSPF_SWEEP_STAGES, default 8)
+  // beside the later stages (OSPF_SWEEP_STAGES; default 1: F100k measured
+  // 24.2 ms per sweep with one stage, 26.3 with 4, 28.1 with 8 -- the later
+  // phase is HBM-bound and the staged twin-level launches lose efficiency)
   uint32_t S = 0;
   if (nd) {
-    S = 8;
+    S = 1;
     if (const char* e = getenv("OSPF_SWEEP_STAGES")) S = (uint32_t)std::max(1, atoi(e));
     S = std::min(S, n_dgrp);
   }
