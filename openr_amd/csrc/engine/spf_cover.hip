@@ -296,6 +296,97 @@ __global__ void __launch_bounds__(512) cover_bf_kernel(DevGraph g, CoverGraph C,
   }
 }
 
+// Delta-stepping over the contracted graph (the cover SPF's default): the
+// distance axis in buckets of width delta; a bucket's round expands the
+// "dirty" transit cover nodes (distance lowered since their last expansion)
+// whose distance lies below the bucket's end, and repeats until none is left
+// there (light edges may lower a node inside the bucket again); the next
+// bucket starts at the smallest dirty distance. Exact at the fixed point
+// (metrics >= 1). A round scans the dirty bitmap (nS / 32 words), not the
+// distances: F100k-w has ~350 distance values but ~a dozen buckets.
+__global__ void __launch_bounds__(512) cover_delta_kernel(DevGraph g, CoverGraph C, CoverArgs a,
+                                                          uint32_t delta) {
+  extern __shared__ uint32_t s_D[];  // [nS] distances, [nw] transit bits, [nw] dirty bits
+  __shared__ uint32_t s_q[kWaves][kQ];
+  __shared__ uint32_t s_pre[kWaves][3 * kWave];
+  __shared__ uint32_t s_any[2], s_min;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t nS = C.nS, V = g.V, nw = (nS + 31u) / 32u;
+  uint32_t* s_tr = s_D + nS;
+  uint32_t* s_dirty = s_tr + nw;
+  for (uint32_t x = tid; x < nw; x += kBlock) s_tr[x] = C.ctr[x];
+  for (uint32_t i = blockIdx.x; i < a.n; i += gridDim.x) {
+    const uint32_t rn = a.roots[i];
+    const uint32_t r = rn < V ? C.cix[rn] : kInf;
+    if (r >= nS) {  // not a cover node (or a bad id): its row is left alone
+      if (tid == 0) atomicOr(a.err, 64u);
+      continue;
+    }
+    for (uint32_t x = tid; x < nS; x += kBlock) s_D[x] = x == r ? 0u : kInf;
+    for (uint32_t x = tid; x < nw; x += kBlock) s_dirty[x] = x == (r >> 5) ? 1u << (r & 31u) : 0u;
+    if (tid == 0) {
+      s_any[0] = s_any[1] = 0u;
+      s_min = kInf;
+    }
+    __syncthreads();
+    uint32_t hi = delta, par = 0;
+    while (true) {
+      uint32_t* q = s_q[wave];
+      uint32_t cnt = 0, m2 = kInf;
+      bool popped = false;
+      for (uint32_t w0 = wave * kWave; w0 < nw; w0 += kBlock) {
+        const uint32_t w = w0 + lane;
+        uint32_t bits = w < nw ? s_dirty[w] : 0u, take = 0u;
+        for (uint32_t b = bits; b; b &= b - 1u) {
+          const uint32_t u = 32u * w + (uint32_t)__builtin_ctz(b);
+          const uint32_t d = s_D[u];
+          if (d < hi) take |= b & (0u - b);
+          else m2 = min(m2, d);
+        }
+        if (take) {
+          atomicAnd(&s_dirty[w], ~take);  // a later improvement sets the bit again
+          popped = true;
+          take &= s_tr[w] | (w == (r >> 5) ? 1u << (r & 31u) : 0u);  // transit or the root
+        }
+        while (__ballot(take != 0u)) {
+          const bool has = take != 0u;
+          const uint32_t u = has ? 32u * w + (uint32_t)__builtin_ctz(take) : 0u;
+          if (has) take &= take - 1u;
+          const uint64_t bal = __ballot(has);
+          if (has) q[cnt + __popcll(bal & ((1ull << lane) - 1ull))] = u;
+          cnt += (uint32_t)__popcll(bal);
+          if (cnt > kQ - kWave) {
+            __builtin_amdgcn_wave_barrier();
+            expand_bf(C, s_D, s_dirty, q, cnt, s_pre[wave], &s_any[par], lane);
+            cnt = 0;
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (cnt) expand_bf(C, s_D, s_dirty, q, cnt, s_pre[wave], &s_any[par], lane);
+      if (__ballot(popped) && lane == 0) s_any[par] = 1u;
+      m2 = wave_min32(m2);
+      if (lane == 0 && m2 != kInf) atomicMin(&s_min, m2);
+      __syncthreads();
+      const bool again = s_any[par] != 0u;
+      const uint32_t nxt = s_min;
+      __syncthreads();  // every thread has read the flags
+      if (tid == 0) {
+        s_any[par] = 0u;
+        s_min = kInf;
+      }
+      par ^= 1u;
+      if (!again) {  // the bucket below hi is settled: on to the next dirty distance
+        if (nxt == kInf) break;
+        hi = nxt + delta;
+      }
+      __syncthreads();  // the flag resets are visible before their use
+    }
+    write_row(g, C, a.dist + (size_t)i * V, s_D, s_tr, r, tid, kBlock);
+    __syncthreads();  // s_D is reused by the next root
+  }
+}
+
 __global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C, CoverArgs a) {
   extern __shared__ uint32_t s_D[];  // [nS] distances, then [ctr words] transit bits
   __shared__ uint32_t s_q[kWaves][kQ];
@@ -355,6 +446,20 @@ __global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C
 hipError_t launch_cover_spf(const DevGraph& g, const CoverGraph& C, const CoverArgs& a,
                             uint32_t n_cu, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
+  if (!getenv("OSPF_COVER_DIAL") && !getenv("OSPF_COVER_BF")) {  // delta-stepping (default)
+    uint32_t delta = 32;
+    if (const char* e = getenv("OSPF_COVER_DELTA")) delta = (uint32_t)std::max(1, atoi(e));
+    const size_t lds = ((size_t)C.nS + 2u * ((C.nS + 31u) / 32u)) * 4u;
+    const uint32_t per_cu = std::max<uint32_t>(1, (uint32_t)((150u * 1024u) / (lds + 12u * 1024u)));
+    const uint32_t grid = std::min<uint32_t>(a.n, n_cu * std::min<uint32_t>(per_cu, 4u));
+    if (lds > 48 * 1024) {
+      hipError_t e = hipFuncSetAttribute((const void*)cover_delta_kernel,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(cover_delta_kernel, dim3(grid), dim3(kBlock), lds, s, g, C, a, delta);
+    return hipGetLastError();
+  }
   if (getenv("OSPF_COVER_BF")) {  // frontier Bellman-Ford (F100k-w: 341 vs 83 ms Dial)
     const size_t lds = ((size_t)C.nS + 3u * ((C.nS + 31u) / 32u)) * 4u;
     const uint32_t per_cu = std::max<uint32_t>(1, (uint32_t)((150u * 1024u) / (lds + 12u * 1024u)));
