@@ -161,16 +161,9 @@ __device__ __forceinline__ void write_row(const DevGraph& g, const CoverGraph& C
   }
 }
 
-// Frontier Bellman-Ford over the contracted graph (OSPF_COVER_BF=1; measured
-// slower than the Dial rounds on the weighted F100k, 341 vs 83 ms: the
-// spines' 1,781-edge rows are re-expanded at every improvement):
-// a round expands the transit cover nodes whose distance dropped in the
-// previous round (and the root in the first), each from its current
-// distance, their edges flattened over each wave; a relaxation that lowers a
-// distance (LDS atomicMin) puts the node into the next round's frontier
-// bitmap. Exact at the fixed point (metrics >= 1): the rounds follow the hop
-// depth of the shortest paths (a fabric's cover: ~10), not the distance
-// values (Dial: one round, with a scan of the cover, per value).
+// Expansion of queued nodes each from its own current distance, for the
+// delta-stepping variant: a relaxation that lowers a distance (LDS atomicMin)
+// sets the node's dirty bit and the round's flag.
 __device__ __forceinline__ void expand_bf(const CoverGraph& C, uint32_t* s_D, uint32_t* nxt,
                                           const uint32_t* q, uint32_t cnt, uint32_t* s_pre,
                                           uint32_t* s_any, uint32_t lane) {
@@ -233,77 +226,16 @@ __device__ __forceinline__ void expand_bf(const CoverGraph& C, uint32_t* s_D, ui
   }
 }
 
-__global__ void __launch_bounds__(512) cover_bf_kernel(DevGraph g, CoverGraph C, CoverArgs a) {
-  extern __shared__ uint32_t s_D[];  // [nS] distances, [nw] transit bits, [2][nw] frontiers
-  __shared__ uint32_t s_q[kWaves][kQ];
-  __shared__ uint32_t s_pre[kWaves][3 * kWave];
-  __shared__ uint32_t s_any[2];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const uint32_t nS = C.nS, V = g.V, nw = (nS + 31u) / 32u;
-  uint32_t* s_tr = s_D + nS;
-  uint32_t* s_f = s_tr + nw;
-  for (uint32_t x = tid; x < nw; x += kBlock) s_tr[x] = C.ctr[x];
-  for (uint32_t i = blockIdx.x; i < a.n; i += gridDim.x) {
-    const uint32_t rn = a.roots[i];
-    const uint32_t r = rn < V ? C.cix[rn] : kInf;
-    if (r >= nS) {  // not a cover node (or a bad id): its row is left alone
-      if (tid == 0) atomicOr(a.err, 64u);
-      continue;
-    }
-    for (uint32_t x = tid; x < nS; x += kBlock) s_D[x] = x == r ? 0u : kInf;
-    for (uint32_t x = tid; x < 2u * nw; x += kBlock) s_f[x] = x == (r >> 5) ? 1u << (r & 31u) : 0u;
-    if (tid == 0) s_any[0] = s_any[1] = 0u;
-    __syncthreads();
-    uint32_t par = 0;
-    while (true) {
-      uint32_t* cur = s_f + par * nw;
-      uint32_t* nxt = s_f + (par ^ 1u) * nw;
-      uint32_t* q = s_q[wave];
-      uint32_t cnt = 0;
-      for (uint32_t w0 = wave * kWave; w0 < nw; w0 += kBlock) {
-        const uint32_t w = w0 + lane;
-        uint32_t bits = 0;
-        if (w < nw) {
-          bits = cur[w];
-          if (bits) cur[w] = 0u;  // clean for the round after next
-          bits &= s_tr[w] | (w == (r >> 5) ? 1u << (r & 31u) : 0u);  // transit or the root
-        }
-        while (__ballot(bits != 0u)) {
-          const bool has = bits != 0u;
-          const uint32_t u = has ? 32u * w + (uint32_t)__builtin_ctz(bits) : 0u;
-          if (has) bits &= bits - 1u;
-          const uint64_t bal = __ballot(has);
-          if (has) q[cnt + __popcll(bal & ((1ull << lane) - 1ull))] = u;
-          cnt += (uint32_t)__popcll(bal);
-          if (cnt > kQ - kWave) {
-            __builtin_amdgcn_wave_barrier();
-            expand_bf(C, s_D, nxt, q, cnt, s_pre[wave], &s_any[par ^ 1u], lane);
-            cnt = 0;
-          }
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-      if (cnt) expand_bf(C, s_D, nxt, q, cnt, s_pre[wave], &s_any[par ^ 1u], lane);
-      __syncthreads();
-      const bool more = s_any[par ^ 1u] != 0u;
-      __syncthreads();  // every thread has read the flag
-      if (tid == 0) s_any[par ^ 1u] = 0u;
-      par ^= 1u;
-      if (!more) break;  // no distance dropped: the fixed point
-    }
-    write_row(g, C, a.dist + (size_t)i * V, s_D, s_tr, r, tid, kBlock);
-    __syncthreads();  // s_D is reused by the next root
-  }
-}
-
-// Delta-stepping over the contracted graph (the cover SPF's default): the
-// distance axis in buckets of width delta; a bucket's round expands the
-// "dirty" transit cover nodes (distance lowered since their last expansion)
-// whose distance lies below the bucket's end, and repeats until none is left
-// there (light edges may lower a node inside the bucket again); the next
-// bucket starts at the smallest dirty distance. Exact at the fixed point
-// (metrics >= 1). A round scans the dirty bitmap (nS / 32 words), not the
-// distances: F100k-w has ~350 distance values but ~a dozen buckets.
+// Delta-stepping over the contracted graph (OSPF_COVER_DELTA=d; not the
+// default): the distance axis in buckets of width d; a bucket's round
+// expands the "dirty" transit cover nodes (distance lowered since their last
+// expansion) whose distance lies below the bucket's end, and repeats until
+// none is left there; the next bucket starts at the smallest dirty distance.
+// Exact at the fixed point (metrics >= 1), and a round scans the dirty bitmap
+// (nS / 32 words) instead of the distances. Measured on F100k-w: 162 / 257 /
+// 318 ms at d = 8 / 32 / 64 against 82 ms for the Dial rounds (and 341 ms for
+// plain frontier Bellman-Ford): every re-expansion of a spine relaxes all its
+// 1,781 edges again; a light / heavy edge split would be the next step.
 __global__ void __launch_bounds__(512) cover_delta_kernel(DevGraph g, CoverGraph C, CoverArgs a,
                                                           uint32_t delta) {
   extern __shared__ uint32_t s_D[];  // [nS] distances, [nw] transit bits, [nw] dirty bits
@@ -446,9 +378,8 @@ __global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C
 hipError_t launch_cover_spf(const DevGraph& g, const CoverGraph& C, const CoverArgs& a,
                             uint32_t n_cu, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  if (!getenv("OSPF_COVER_DIAL") && !getenv("OSPF_COVER_BF")) {  // delta-stepping (default)
-    uint32_t delta = 32;
-    if (const char* e = getenv("OSPF_COVER_DELTA")) delta = (uint32_t)std::max(1, atoi(e));
+  if (const char* e = getenv("OSPF_COVER_DELTA")) {  // delta-stepping (experiment)
+    const uint32_t delta = (uint32_t)std::max(1, atoi(e));
     const size_t lds = ((size_t)C.nS + 2u * ((C.nS + 31u) / 32u)) * 4u;
     const uint32_t per_cu = std::max<uint32_t>(1, (uint32_t)((150u * 1024u) / (lds + 12u * 1024u)));
     const uint32_t grid = std::min<uint32_t>(a.n, n_cu * std::min<uint32_t>(per_cu, 4u));
@@ -458,18 +389,6 @@ hipError_t launch_cover_spf(const DevGraph& g, const CoverGraph& C, const CoverA
       if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(cover_delta_kernel, dim3(grid), dim3(kBlock), lds, s, g, C, a, delta);
-    return hipGetLastError();
-  }
-  if (getenv("OSPF_COVER_BF")) {  // frontier Bellman-Ford (F100k-w: 341 vs 83 ms Dial)
-    const size_t lds = ((size_t)C.nS + 3u * ((C.nS + 31u) / 32u)) * 4u;
-    const uint32_t per_cu = std::max<uint32_t>(1, (uint32_t)((150u * 1024u) / (lds + 12u * 1024u)));
-    const uint32_t grid = std::min<uint32_t>(a.n, n_cu * std::min<uint32_t>(per_cu, 4u));
-    if (lds > 48 * 1024) {
-      hipError_t e = hipFuncSetAttribute((const void*)cover_bf_kernel,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(cover_bf_kernel, dim3(grid), dim3(kBlock), lds, s, g, C, a);
     return hipGetLastError();
   }
   const size_t lds = ((size_t)C.nS + (C.nS + 31u) / 32u) * 4u;
