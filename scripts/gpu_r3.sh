@@ -55,6 +55,10 @@ for st in $STEPS; do
              python scripts/sweep_unit_stats.py --bench "$OUT/utrace_serial_bench.json" --trace "$OUT/utrace_serial" --reps 3 --out "$OUT/units_trace_serial.json" &&
              python scripts/sweep_unit_stats.py --bench "$OUT/upmc1.json" --pmc "$OUT/upmc1" "$OUT/upmc2" --reps 1 --out "$OUT/pmc_traffic.json"; rc=$?
            fi;;
+    upmcsq)  # per-unit SQ counters (instructions, busy / wait cycles) of the sweep
+           timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY -d "$OUT/upmcsq" -o run --output-format csv -- \
+             python bench.py --steps 1 --warmup 0 --no-cpu --iso-reps 1 ${PROF_ARGS:-} > "$OUT/upmcsq.json" 2> "$OUT/upmcsq.err"; rc=$?
+           [ $rc -eq 0 ] && python scripts/sweep_unit_stats.py --bench "$OUT/upmcsq.json" --pmc "$OUT/upmcsq" --reps 1 --out "$OUT/pmc_sq.json" > /dev/null; rc=$?;;
     ab)    # A/B of env knobs on the default bench: AB="NAME=1 OTHER=1 ..." (one run each + baseline)
            rc=0
            for kv in base ${AB:-}; do
