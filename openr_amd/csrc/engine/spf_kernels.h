@@ -215,6 +215,25 @@ struct DeriveArgs {
   uint32_t ctiles;         // node tiles per block (0: default 8)
   uint32_t G, tiles, chunks;  // set by the launcher
 };
+// Wide next hops planned on the host (spf_msbfs.hip nh_wide_plan_kernel):
+// runs of roots with the same distinct-neighbour list (<= 64 roots), each
+// run's slot table and each root's usable-slot words.
+struct WidePlan {
+  uint32_t n, W, nruns;
+  const uint32_t* run;    // [nruns + 1] root offsets
+  const uint32_t* soff;   // [nruns + 1] offsets into slots (K <= 2048 per run)
+  const uint32_t* slots;  // level row | 0x80000000 | node (non-transit) | 0xFFFFFFFF (unused)
+  const uint32_t* keep;   // [n][W] usable-slot words
+  const uint32_t* own;    // [n] each root's level row
+  const uint8_t* lev;
+  uint32_t pitch;
+  const ospf_digest* lev_digest;  // [rows] distance parts of the level rows
+  uint32_t* nh;           // [n][V][W]
+  ospf_digest* digest;    // [n] (zeroed by the launcher) or null
+  uint32_t tiles, ctiles, chunks;  // set by the launcher (ctiles 0: its choice)
+};
+hipError_t launch_wide_plan(const DevGraph& g, const WidePlan& p, hipStream_t s);
+
 // Derive phase 1 on 128-root traversals (spf_levels.hip): distance-only
 // multi-source BFS, 16-B root sets per node, then level / dist rows + the
 // distance part of each digest. Wide batch i of a round = roots

@@ -1746,192 +1746,136 @@ __global__ void __launch_bounds__(256) nh_derive_wide_kernel(DevGraph g, DeriveA
 
 
 
-// Wide rows, tile-staged (W > 4 words: spines, W <= 64). Block = up to
-// kWideG consecutive roots x a chunk of 16-node tiles, blocks XCD-major over
-// the chunks (an XCD's resident blocks hold consecutive tiles, so their
-// 16-B pieces of each neighbour row's 128-B lines meet in its L2). Per tile
-// and run of roots with the same neighbour list: the K neighbour rows' 16
-// level bytes are staged in LDS slot-major (one 16-B load per slot; a slot
+// Wide rows, planned and tile-staged (W > 4 words: spines; the sweep's
+// path). The host plans runs of roots with the same distinct-neighbour list
+// (the spines of one plane, <= kWideG roots), each run's slot table (a
+// neighbour's level row, 0x80000000 | node for a non-transit neighbour, kInf
+// when no root of the run has an up link to it) and each root's usable-slot
+// words, so a block's setup is a few coalesced loads. Block = (run, chunk of
+// 16-node tiles), XCD-major over the chunks (an XCD's resident blocks hold
+// consecutive tiles, so the 16-B pieces of each neighbour row's 128-B lines
+// meet in its L2). Per tile the K rows' 16 level bytes are staged in LDS
+// slot-major (one 16-B load per slot, all of a thread's in flight; a slot
 // without a transit row holds 0xFF, a non-transit neighbour 0x01 at its own
-// position: a next hop towards itself exactly when the root is one hop
-// away); then wave q takes nodes 4q .. 4q + 3 of the tile, lane = next-hop
-// word w: 32 LDS words per word, each byte compared with L - 1 for 4 nodes
-// at once (SWAR). A root whose own levels at the 4 nodes equal the previous
-// root's keeps the words (the spines of a plane differ only at their own
+// position: a next hop towards itself exactly when the root is one hop away);
+// then wave q takes nodes 4q .. 4q + 3 of the tile, lane = next-hop word w:
+// 32 LDS words per word, each byte compared with L - 1 for 4 nodes at once
+// (SWAR). A root whose own levels at the 4 nodes equal the previous root's
+// keeps the words (the spines of a plane differ only at their own
 // positions); each root stores its 4 nodes' records (W consecutive words per
 // store instruction) masked by its usable links.
 constexpr uint32_t kW3Tile = 16, kW3Pitch = 20;
-__global__ void __launch_bounds__(256) nh_derive_wide3_kernel(DevGraph g, DeriveArgs d) {
-  __shared__ uint32_t s_pos[kDeriveTab];  // slot table of the current run
-  __shared__ uint32_t s_root[kWideG], s_own[kWideG], s_K[kWideG], s_same[kWideG];
+__global__ void __launch_bounds__(256) nh_wide_plan_kernel(DevGraph g, WidePlan d) {
+  __shared__ uint32_t s_pos[kDeriveTab];  // the run's slot table
+  __shared__ uint32_t s_own[kWideG];
   __shared__ unsigned long long s_h[kWideG];
   extern __shared__ uint32_t s_dyn[];     // keep [G][W], then the staged bytes [K][kW3Pitch]
   const uint32_t V = g.V, W = d.W, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const uint32_t G = d.G, cap = d.cap;
-  uint32_t* s_keep = s_dyn;
-  uint8_t* B = reinterpret_cast<uint8_t*>(s_dyn + G * W);
-  const uint32_t ngroups = (d.n + G - 1) / G;
-  const uint32_t NB = ngroups * d.chunks, NB8 = NB / 8u * 8u, bb = blockIdx.x;
+  const uint32_t NB = d.nruns * d.chunks, NB8 = NB / 8u * 8u, bb = blockIdx.x;
   const uint32_t item = bb < NB8 ? (bb % 8u) * (NB8 / 8u) + bb / 8u : bb;
-  const uint32_t ci = item / ngroups, gi = item % ngroups;
-  const uint32_t i0 = gi * G, ng = min(G, d.n - i0);
+  const uint32_t ci = item / d.nruns, ri = item % d.nruns;
+  const uint32_t j0 = d.run[ri], ng = min(kWideG, d.run[ri + 1] - j0);
+  const uint32_t s0 = d.soff[ri], K = min(kDeriveTab, d.soff[ri + 1] - s0);
+  uint32_t* s_keep = s_dyn;
+  uint8_t* B = reinterpret_cast<uint8_t*>(s_dyn + kWideG * W);
+  for (uint32_t k = tid; k < K; k += kBlock) s_pos[k] = d.slots[s0 + k];
+  for (uint32_t x = tid; x < ng * W; x += kBlock) s_keep[x] = d.keep[(size_t)j0 * W + x];
   if (tid < ng) {
-    const uint32_t r = d.roots[i0 + tid];
-    s_root[tid] = r;
+    s_own[tid] = d.own[j0 + tid];
     s_h[tid] = 0ull;
-    s_own[tid] = kInf;
-    s_K[tid] = 0;
-    if (r >= V) {
-      atomicOr(d.err, 64u);
-    } else {
-      const uint32_t K = g.dn_off[r + 1] - g.dn_off[r];
-      s_own[tid] = d.pos[r];
-      if (K > cap || K > 32u * W || s_own[tid] == kInf)
-        atomicOr(d.err, s_own[tid] == kInf ? 16u : 1u);
-      if (s_own[tid] != kInf) s_K[tid] = min(K, cap);
-    }
-  }
-  for (uint32_t x = tid; x < ng * W; x += kBlock) s_keep[x] = 0u;
-  __syncthreads();
-  if (tid < ng)
-    s_same[tid] = tid > 0 && s_own[tid] != kInf && s_own[tid - 1] != kInf &&
-                  s_K[tid] == s_K[tid - 1];
-  for (uint32_t j = 0; j < ng; ++j) {
-    const uint32_t r = s_root[j];
-    if (r >= V || s_own[j] == kInf) continue;
-    for (uint32_t e = g.row_ptr[r] + tid; e < g.row_ptr[r + 1]; e += kBlock) {
-      const uint32_t cx = g.colx[e];
-      if ((cx & kDown) || cx == r) continue;
-      const uint32_t k = g.didx[e];
-      if (k < s_K[j]) atomicOr(&s_keep[j * W + (k >> 5)], 1u << (k & 31u));
-    }
-  }
-  __syncthreads();
-  for (uint32_t j = 1; j < ng; ++j) {
-    if (!s_same[j]) continue;
-    const uint32_t* a0 = g.dn + g.dn_off[s_root[j - 1]];
-    const uint32_t* a1 = g.dn + g.dn_off[s_root[j]];
-    for (uint32_t k = tid; k < s_K[j]; k += kBlock)
-      if (a0[k] != a1[k]) s_same[j] = 0u;  // benign race: every writer stores 0
   }
   __syncthreads();
   const uint32_t t0 = ci * d.ctiles, t1 = min(d.tiles, t0 + d.ctiles);
-  for (uint32_t j0 = 0; j0 < ng;) {
-    uint32_t j1 = j0 + 1;
-    while (j1 < ng && s_same[j1]) ++j1;
-    const uint32_t K = s_K[j0];
-    if (s_own[j0] == kInf) {  // a bad root (error flagged): its own run
-      j0 = j1;
-      continue;
+  for (uint32_t t = t0; t < t1; ++t) {
+    const uint32_t v0 = t * kW3Tile;
+    if (t > t0) __syncthreads();  // the previous tile's bytes are consumed
+    // every slot load of the thread in flight at once (K <= 2048: <= 8 each)
+    uint32_t pk[kDeriveTab / kBlock];
+    uint4 xk[kDeriveTab / kBlock];
+#pragma unroll
+    for (uint32_t m = 0; m < kDeriveTab / kBlock; ++m) {
+      const uint32_t k = tid + m * kBlock;
+      pk[m] = k < K ? s_pos[k] : kInf;
     }
-    __syncthreads();  // the previous run is done with s_pos and B
-    for (uint32_t k = tid; k < K; k += kBlock) {
-      bool used = false;
-      for (uint32_t j = j0; j < j1 && !used; ++j) used = (s_keep[j * W + (k >> 5)] >> (k & 31u)) & 1u;
-      uint32_t p = kInf;
-      if (used) {
-        const uint32_t n = g.dn[g.dn_off[s_root[j0]] + k];
-        if (transit(g, n)) {
-          p = d.pos[n];
-          if (p == kInf) atomicOr(d.err, 16u);
-        } else {
-          p = 0x80000000u | n;
-        }
-      }
-      s_pos[k] = p;
+#pragma unroll
+    for (uint32_t m = 0; m < kDeriveTab / kBlock; ++m) {
+      const uint32_t row = pk[m] < 0x80000000u ? pk[m] : s_own[0];  // a valid row, masked below
+      xk[m] = *reinterpret_cast<const uint4*>(d.lev + (size_t)row * d.pitch + v0);
     }
-    for (uint32_t t = t0; t < t1; ++t) {
-      const uint32_t v0 = t * kW3Tile;
-      __syncthreads();  // s_pos written / the previous tile's bytes consumed
-      // every slot load of the thread in flight at once (K <= 2048: <= 8 each)
-      uint32_t pk[kDeriveTab / kBlock];
-      uint4 xk[kDeriveTab / kBlock];
 #pragma unroll
-      for (uint32_t m = 0; m < kDeriveTab / kBlock; ++m) {
-        const uint32_t k = tid + m * kBlock;
-        pk[m] = k < K ? s_pos[k] : kInf;
-      }
-#pragma unroll
-      for (uint32_t m = 0; m < kDeriveTab / kBlock; ++m) {
-        const uint32_t row = pk[m] < 0x80000000u ? pk[m] : s_own[j0];  // a valid row, masked below
-        xk[m] = *reinterpret_cast<const uint4*>(d.lev + (size_t)row * d.pitch + v0);
-      }
-#pragma unroll
-      for (uint32_t m = 0; m < kDeriveTab / kBlock; ++m) {
-        const uint32_t k = tid + m * kBlock, p = pk[m];
-        if (k >= K) break;
-        uint4 x = xk[m];
-        if (p >= 0x80000000u) {
-          x = make_uint4(~0u, ~0u, ~0u, ~0u);
-          const uint32_t o = (p & 0x7FFFFFFFu) - v0;
-          if (p != kInf && o < kW3Tile) {
-            uint32_t w4[4] = {x.x, x.y, x.z, x.w};
-            w4[o >> 2] = (w4[o >> 2] & ~(0xFFu << (8u * (o & 3u)))) | (1u << (8u * (o & 3u)));
-            x = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-          }
+    for (uint32_t m = 0; m < kDeriveTab / kBlock; ++m) {
+      const uint32_t k = tid + m * kBlock, p = pk[m];
+      if (k >= K) break;
+      uint4 x = xk[m];
+      if (p >= 0x80000000u) {
+        x = make_uint4(~0u, ~0u, ~0u, ~0u);
+        const uint32_t o = (p & 0x7FFFFFFFu) - v0;
+        if (p != kInf && o < kW3Tile) {
+          uint32_t w4[4] = {x.x, x.y, x.z, x.w};
+          w4[o >> 2] = (w4[o >> 2] & ~(0xFFu << (8u * (o & 3u)))) | (1u << (8u * (o & 3u)));
+          x = make_uint4(w4[0], w4[1], w4[2], w4[3]);
         }
-        uint32_t* bw = reinterpret_cast<uint32_t*>(B + (size_t)k * kW3Pitch);
-        bw[0] = x.x;
-        bw[1] = x.y;
-        bw[2] = x.z;
-        bw[3] = x.w;
       }
-      __syncthreads();
-      const uint32_t nq = v0 + 4u * wave;  // this wave's 4 nodes
-      if (nq >= V) continue;                // wave-uniform (no barrier below)
-      uint64_t kn[4];
+      uint32_t* bw = reinterpret_cast<uint32_t*>(B + (size_t)k * kW3Pitch);
+      bw[0] = x.x;
+      bw[1] = x.y;
+      bw[2] = x.z;
+      bw[3] = x.w;
+    }
+    __syncthreads();
+    const uint32_t nq = v0 + 4u * wave;  // this wave's 4 nodes
+    if (nq >= V) continue;                // wave-uniform (the next barrier is reached by all)
+    uint64_t kn[4];
 #pragma unroll
-      for (int b = 0; b < 4; ++b) kn[b] = d.digest ? g.dkn[nq + b] : 0ull;  // zero past V
-      uint32_t word[4] = {0u, 0u, 0u, 0u}, Lp = 0xFFFFFFFFu;
-      for (uint32_t j = j0; j < j1; ++j) {
-        const uint32_t L = *reinterpret_cast<const uint32_t*>(d.lev + (size_t)s_own[j] * d.pitch + nq);
-        if (L != Lp) {  // wave-uniform: the root's own levels at the 4 nodes
-          Lp = L;
-          // L - 1 per byte where 2 <= L < 0x7F, else 0xFE (matches nothing)
-          uint32_t lm1 = 0;
-#pragma unroll
-          for (int b = 0; b < 4; ++b) {
-            const uint32_t l = (L >> (8 * b)) & 0xFFu;
-            lm1 |= (l >= 2u && l < 0x7Fu ? l - 1u : 0xFEu) << (8 * b);
-          }
-#pragma unroll
-          for (int b = 0; b < 4; ++b) word[b] = 0u;
-          if (lane < W) {
-#pragma unroll 8
-            for (uint32_t i = 0; i < 32u; ++i) {
-              const uint32_t k = 32u * lane + i;
-              const uint32_t x = k < K ? *reinterpret_cast<const uint32_t*>(B + (size_t)k * kW3Pitch + 4u * wave)
-                                       : ~0u;
-              const uint32_t y = x ^ lm1;  // bit 7 of each byte of eq: that byte of y is zero
-              const uint32_t eq = ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u;
-#pragma unroll
-              for (int b = 0; b < 4; ++b) word[b] |= ((eq >> (8 * b + 7)) & 1u) << i;
-            }
-          }
-        }
-        const uint32_t keep = lane < W ? s_keep[j * W + lane] : 0u;
-        uint32_t* dst = d.nh + ((size_t)(i0 + j) * V + nq) * W + lane;
-        uint64_t h = 0;
+    for (int b = 0; b < 4; ++b) kn[b] = d.digest ? g.dkn[nq + b] : 0ull;  // zero past V
+    uint32_t word[4] = {0u, 0u, 0u, 0u}, Lp = 0xFFFFFFFFu;
+    for (uint32_t j = 0; j < ng; ++j) {
+      const uint32_t L = *reinterpret_cast<const uint32_t*>(d.lev + (size_t)s_own[j] * d.pitch + nq);
+      if (L != Lp) {  // wave-uniform: the root's own levels at the 4 nodes
+        Lp = L;
+        // L - 1 per byte where 2 <= L < 0x7F, else 0xFE (matches nothing)
+        uint32_t lm1 = 0;
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-          const uint32_t ow = word[b] & keep;
-          if (lane < W && nq + b < V) __builtin_nontemporal_store(ow, dst + (size_t)b * W);
-          if (d.digest && ow) h += kn[b] * digest_word_key(lane, ow);
+          const uint32_t l = (L >> (8 * b)) & 0xFFu;
+          lm1 |= (l >= 2u && l < 0x7Fu ? l - 1u : 0xFEu) << (8 * b);
         }
-        if (d.digest) {
 #pragma unroll
-          for (int o = 32; o > 0; o >>= 1) h += shfl_xor64(h, o);
-          if (lane == 0 && h) atomicAdd(&s_h[j], (unsigned long long)h);
+        for (int b = 0; b < 4; ++b) word[b] = 0u;
+        if (lane < W) {
+#pragma unroll 8
+          for (uint32_t i = 0; i < 32u; ++i) {
+            const uint32_t k = 32u * lane + i;
+            const uint32_t x = k < K ? *reinterpret_cast<const uint32_t*>(B + (size_t)k * kW3Pitch + 4u * wave)
+                                     : ~0u;
+            const uint32_t y = x ^ lm1;  // bit 7 of each byte of eq: that byte of y is zero
+            const uint32_t eq = ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) word[b] |= ((eq >> (8 * b + 7)) & 1u) << i;
+          }
         }
       }
+      const uint32_t keep = lane < W ? s_keep[j * W + lane] : 0u;
+      uint32_t* dst = d.nh + ((size_t)(j0 + j) * V + nq) * W + lane;
+      uint64_t h = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const uint32_t ow = word[b] & keep;
+        if (lane < W && nq + b < V) __builtin_nontemporal_store(ow, dst + (size_t)b * W);
+        if (d.digest && ow) h += kn[b] * digest_word_key(lane, ow);
+      }
+      if (d.digest) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) h += shfl_xor64(h, o);
+        if (lane == 0 && h) atomicAdd(&s_h[j], (unsigned long long)h);
+      }
     }
-    j0 = j1;
   }
   __syncthreads();
   if (d.digest && tid < ng) {
-    ospf_digest* dg = d.digest + i0 + tid;
+    ospf_digest* dg = d.digest + j0 + tid;
     unsigned long long h = s_h[tid];
-    if (ci == 0 && s_own[tid] != kInf) {
+    if (ci == 0) {
       const ospf_digest ld = d.lev_digest[s_own[tid]];
       atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)ld.reached);
       atomicAdd((unsigned long long*)&dg->sum_dist, (unsigned long long)ld.sum_dist);
@@ -2170,24 +2114,6 @@ hipError_t launch_nh_derive(const DevGraph& g, const DeriveArgs& d0, hipStream_t
     d.G = kWideG;
     if (const char* e = getenv("OSPF_DERIVE_WIDE_G"))
       d.G = std::max<uint32_t>(1, std::min<uint32_t>(kWideG, (uint32_t)atoi(e)));
-    const size_t lds3 = 4ull * d.W * d.G + (size_t)d.cap * kW3Pitch;
-    if (d.W <= 64 && (d.pitch % kW3Tile) == 0 && getenv("OSPF_DERIVE_WIDE3")) {
-      // tile-staged, ~4096 blocks of 16-node tiles (F100k spines: 9.6 ms
-      // against 5.9 for nh_derive_wide_kernel: the per-block setup of 64
-      // roots' slot tables is paid 4.5x as often; not the default)
-      const uint32_t ngroups = (d.n + d.G - 1) / d.G;
-      d.tiles = (g.V + kW3Tile - 1) / kW3Tile;
-      if (!d.ctiles) d.ctiles = std::max<uint32_t>(1, d.tiles / std::max<uint32_t>(1, 4096u / ngroups));
-      d.ctiles = std::min(d.ctiles, d.tiles);
-      d.chunks = (d.tiles + d.ctiles - 1) / d.ctiles;
-      if (lds3 > 64u * 1024u) {
-        const hipError_t e = hipFuncSetAttribute((const void*)nh_derive_wide3_kernel,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds3);
-        if (e != hipSuccess) return e;
-      }
-      hipLaunchKernelGGL(nh_derive_wide3_kernel, dim3(ngroups * d.chunks), dim3(kBlock), lds3, s, g, d);
-      return hipGetLastError();
-    }
     d.tiles = (g.V + kWideTile - 1) / kWideTile;
     d.ctiles = std::max<uint32_t>(1, std::min<uint32_t>(d.tiles, d.ctiles ? d.ctiles : 2));
     d.chunks = (d.tiles + d.ctiles - 1) / d.ctiles;
@@ -2207,6 +2133,29 @@ hipError_t launch_nh_derive(const DevGraph& g, const DeriveArgs& d0, hipStream_t
   const dim3 grid(((d.n + d.G - 1) / d.G) * d.chunks);
   if (S == 1) hipLaunchKernelGGL(nh_derive_kernel<1>, grid, dim3(kBlock), lds, s, g, d);
   else hipLaunchKernelGGL(nh_derive_kernel<4>, grid, dim3(kBlock), lds, s, g, d);
+  return hipGetLastError();
+}
+
+hipError_t launch_wide_plan(const DevGraph& g, const WidePlan& p0, hipStream_t s) {
+  WidePlan p = p0;
+  if (p.n == 0) return hipSuccess;
+  if (p.W < 1 || p.W > 64 || p.pitch % kW3Tile) return hipErrorInvalidValue;
+  p.tiles = (g.V + kW3Tile - 1) / kW3Tile;
+  // ~4096 blocks; a chunk of >= 7 tiles covers a 128-B line of every row
+  if (!p.ctiles) p.ctiles = std::max<uint32_t>(7, p.tiles / std::max<uint32_t>(1, 4096u / p.nruns));
+  p.ctiles = std::min(p.ctiles, p.tiles);
+  p.chunks = (p.tiles + p.ctiles - 1) / p.ctiles;
+  const size_t lds = 4ull * kWideG * p.W + (size_t)kDeriveTab * kW3Pitch;
+  if (lds > 64u * 1024u) {
+    const hipError_t e = hipFuncSetAttribute((const void*)nh_wide_plan_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  if (p.digest) {
+    const hipError_t e = hipMemsetAsync(p.digest, 0, (size_t)p.n * sizeof(ospf_digest), s);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(nh_wide_plan_kernel, dim3(p.nruns * p.chunks), dim3(kBlock), lds, s, g, p);
   return hipGetLastError();
 }
 

@@ -375,6 +375,64 @@ Twins twin_classes(const ospf_ctx* c) {
   return t;
 }
 
+// Host plan of the wide next-hop kernel (nh_wide_plan_kernel) for a class
+// of roots (in order): runs of <= kWideG roots with the same distinct
+// neighbours, each run's slot table over level-row positions, each root's
+// usable-slot words.
+struct WideHost {
+  std::vector<uint32_t> run, soff, slots, keep, own;
+};
+int wide_plan_build(ospf_ctx* c, const Facts& f, const std::vector<uint32_t>& roots, uint32_t W,
+                    const std::vector<uint32_t>& pos, WideHost& h) {
+  const uint32_t n = (uint32_t)roots.size();
+  h = WideHost{};
+  h.keep.assign((size_t)n * W, 0u);
+  auto same = [&](uint32_t a, uint32_t b) {
+    return f.nbrs(a) == f.nbrs(b) &&
+           std::equal(f.dn->begin() + (*f.dn_off)[a], f.dn->begin() + (*f.dn_off)[a + 1],
+                      f.dn->begin() + (*f.dn_off)[b]);
+  };
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t r = roots[i];
+    if (pos[r] == kNone) return fail(c, OSPF_E_RANGE, "wide plan: a root without a level row");
+    h.own.push_back(pos[r]);
+    const uint32_t* dn = f.dn->data() + (*f.dn_off)[r];
+    const uint32_t K = f.nbrs(r);
+    if (K > 32u * W || K > 2048u) return fail(c, OSPF_E_RANGE, "wide plan: too many neighbours");
+    for (uint32_t e = c->h_prow[r]; e < c->h_prow[r + 1]; ++e) {
+      const uint32_t x = c->h_pcolx[e];
+      if ((x & 0x80000000u) || x == r) continue;
+      const uint32_t k = (uint32_t)(std::lower_bound(dn, dn + K, x) - dn);
+      h.keep[(size_t)i * W + (k >> 5)] |= 1u << (k & 31u);
+    }
+    if (i == 0 || i - h.run.back() >= 64u || !same(roots[h.run.back()], r)) h.run.push_back(i);
+  }
+  h.run.push_back(n);
+  h.soff.push_back(0u);
+  for (size_t q = 0; q + 1 < h.run.size(); ++q) {
+    const uint32_t r0 = roots[h.run[q]], K = f.nbrs(r0);
+    const uint32_t* dn = f.dn->data() + (*f.dn_off)[r0];
+    for (uint32_t k = 0; k < K; ++k) {
+      bool used = false;
+      for (uint32_t i = h.run[q]; i < h.run[q + 1] && !used; ++i)
+        used = (h.keep[(size_t)i * W + (k >> 5)] >> (k & 31u)) & 1u;
+      uint32_t v = kNone;
+      if (used) {
+        const uint32_t x = dn[k];
+        if ((c->h_nt[x >> 5] >> (x & 31)) & 1u) {
+          v = 0x80000000u | x;
+        } else {
+          v = pos[x];
+          if (v == kNone) return fail(c, OSPF_E_RANGE, "wide plan: a neighbour without a level row");
+        }
+      }
+      h.slots.push_back(v);
+    }
+    h.soff.push_back((uint32_t)h.slots.size());
+  }
+  return OSPF_OK;
+}
+
 // DERIVE (spf_levels.hip, spf_twin.hip, spf_leaf.hip, spf_msbfs.hip derive
 // kernels), unit metric / hop count. The part's roots split into leaves (an
 // independent set of nodes with <= 32 distinct neighbours: a fabric's racks)
@@ -753,6 +811,48 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
         side.push_back(std::move(u));
         a0 = a1;
       }
+      continue;
+    }
+    if (!k.twin && W > 4 && W <= 64 && !getenv("OSPF_DERIVE_WIDE1")) {
+      // spines: the planned tile-staged kernel (host-built runs and slot tables)
+      WideHost wh;
+      if ((rc = wide_plan_build(c, f, k.roots, W, pos, wh))) return sfail(s, rc, c->err);
+      ospf::WidePlan plan{};
+      uint32_t *d_run, *d_soff, *d_slots, *d_keep, *d_own;
+      if ((rc = upload(s, &d_run, wh.run)) || (rc = upload(s, &d_soff, wh.soff)) ||
+          (rc = upload(s, &d_slots, wh.slots)) || (rc = upload(s, &d_keep, wh.keep)) ||
+          (rc = upload(s, &d_own, wh.own)))
+        return rc;
+      plan.n = n;
+      plan.W = W;
+      plan.nruns = (uint32_t)wh.run.size() - 1;
+      plan.run = d_run;
+      plan.soff = d_soff;
+      plan.slots = d_slots;
+      plan.keep = d_keep;
+      plan.own = d_own;
+      plan.lev = lev;
+      plan.pitch = pitch;
+      plan.lev_digest = ldg;
+      plan.nh = nh;
+      plan.digest = dg;
+      ospf_sweep::Unit u;
+      u.name = "derive_cap" + std::to_string(k.cap);
+      u.kernel = "nh_wide_plan_kernel (" + std::to_string(W) + " next-hop words: host-planned runs, "
+                 "16-node tiles staged in LDS)";
+      u.stream = st;
+      u.wait = {!k.reads_leaf ? ev_cov : ev_b};
+      if (u.wait[0] == ev_b && nd) u.wait.push_back(ev_cov);
+      u.n_roots = n;
+      u.W = W;
+      u.comp = (uint64_t)n * 4ull * V * W;
+      u.fn = [=](hipStream_t strm) {
+        const hipError_t e = ospf::launch_wide_plan(c->g, plan, strm);
+        if (e != hipSuccess) return hip_fail(c, e, "launch_wide_plan");
+        return (int)OSPF_OK;
+      };
+      s->step_comp += u.comp;
+      (u.wait[0] == ev_b ? after : side).push_back(std::move(u));
       continue;
     }
     ospf_sweep::Unit u;
