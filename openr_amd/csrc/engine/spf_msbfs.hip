@@ -1828,9 +1828,12 @@ __global__ void __launch_bounds__(256) nh_wide_plan_kernel(DevGraph g, WidePlan 
     uint64_t kn[4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) kn[b] = d.digest ? g.dkn[nq + b] : 0ull;  // zero past V
+    // every root's own levels at the 4 nodes in one trip: lane j holds root j's
+    const uint32_t Lmine =
+        lane < ng ? *reinterpret_cast<const uint32_t*>(d.lev + (size_t)s_own[lane] * d.pitch + nq) : 0u;
     uint32_t word[4] = {0u, 0u, 0u, 0u}, Lp = 0xFFFFFFFFu;
     for (uint32_t j = 0; j < ng; ++j) {
-      const uint32_t L = *reinterpret_cast<const uint32_t*>(d.lev + (size_t)s_own[j] * d.pitch + nq);
+      const uint32_t L = (uint32_t)__shfl((int)Lmine, (int)j, 64);
       if (L != Lp) {  // wave-uniform: the root's own levels at the 4 nodes
         Lp = L;
         // L - 1 per byte where 2 <= L < 0x7F, else 0xFE (matches nothing)
