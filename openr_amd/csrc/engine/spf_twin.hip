@@ -161,6 +161,7 @@ template <int W>
 __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, TwinArgs a) {
   __shared__ TwinTab T;
   __shared__ unsigned long long s_h;
+  __shared__ uint32_t s_Lb[kWaves][256];  // own level bytes of each wave's tile
   extern __shared__ uint32_t s_stage[];  // [4 waves][1024 nodes][W]
   const uint32_t V = g.V, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   // XCD-aware order: XCD x (blocks x, x + 8, ...) walks a contiguous range
@@ -250,19 +251,27 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
       }
       reinterpret_cast<uint4*>(st + 16u * W * lane)[x] = make_uint4(v4[0], v4[1], v4[2], v4[3]);
     }
+    reinterpret_cast<uint4*>(s_Lb[wave])[lane] = L;  // the root's own level bytes of the tile
     __builtin_amdgcn_wave_barrier();
-    // members' own positions inside this tile (slots are sorted by node id)
-    if (lane == 0) {
+    // members' own positions inside this tile (slots are sorted by node id),
+    // a lane per neighbour: distinct neighbours patch distinct nodes
+    {
       uint32_t lo = 0, hi = K;
       while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
         if (T.nb[mid] < tv0) lo = mid + 1; else hi = mid;
       }
-      for (uint32_t k = lo; k < K && T.nb[k] < tv0 + 1024u; ++k) {
+      uint32_t end = lo;
+      hi = K;
+      while (end < hi) {
+        const uint32_t mid = (end + hi) >> 1;
+        if (T.nb[mid] < tv0 + 1024u) end = mid + 1; else hi = mid;
+      }
+      for (uint32_t k = lo + lane; k < end; k += 64u) {
         const uint32_t sk = T.cid[k];
         if (sk == kInf) continue;
         const uint32_t n = T.nb[k], o = n - tv0;
-        const uint32_t Ln = a.lev[(size_t)own * a.pitch + n];
+        const uint32_t Ln = (s_Lb[wave][o >> 2] >> (8u * (o & 3u))) & 0xFFu;
         uint32_t nw[W], ow[W];
 #pragma unroll
         for (int w = 0; w < W; ++w) nw[w] = ow[w] = st[o * W + w];
