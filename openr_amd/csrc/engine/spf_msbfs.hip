@@ -1832,6 +1832,10 @@ __global__ void __launch_bounds__(256) nh_wide_plan_kernel(DevGraph g, WidePlan 
     const uint32_t Lmine =
         lane < ng ? *reinterpret_cast<const uint32_t*>(d.lev + (size_t)s_own[lane] * d.pitch + nq) : 0u;
     uint32_t word[4] = {0u, 0u, 0u, 0u}, Lp = 0xFFFFFFFFu;
+    // the word key of each node's masked word, kept while the next root's
+    // masked word is the same (the roots of a run mostly store equal words)
+    uint32_t kw_word[4] = {0u, 0u, 0u, 0u};
+    uint64_t kw_key[4] = {0ull, 0ull, 0ull, 0ull};
     for (uint32_t j = 0; j < ng; ++j) {
       const uint32_t L = (uint32_t)__shfl((int)Lmine, (int)j, 64);
       if (L != Lp) {  // wave-uniform: the root's own levels at the 4 nodes
@@ -1865,13 +1869,16 @@ __global__ void __launch_bounds__(256) nh_wide_plan_kernel(DevGraph g, WidePlan 
       for (int b = 0; b < 4; ++b) {
         const uint32_t ow = word[b] & keep;
         if (lane < W && nq + b < V) __builtin_nontemporal_store(ow, dst + (size_t)b * W);
-        if (d.digest && ow) h += kn[b] * digest_word_key(lane, ow);
+        if (d.digest && ow) {
+          if (ow != kw_word[b]) {
+            kw_word[b] = ow;
+            kw_key[b] = digest_word_key(lane, ow);
+          }
+          h += kn[b] * kw_key[b];
+        }
       }
-      if (d.digest) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) h += shfl_xor64(h, o);
-        if (lane == 0 && h) atomicAdd(&s_h[j], (unsigned long long)h);
-      }
+      // few lanes hold a non-zero word: their terms go straight to the root's sum
+      if (d.digest && h) atomicAdd(&s_h[j], (unsigned long long)h);
     }
   }
   __syncthreads();

@@ -441,7 +441,8 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
 #pragma unroll
     for (uint32_t j = 0; j < kTwinLvG; ++j) {
       if (j >= ng) break;
-      const uint32_t mask = s_umask[j];
+      // the root's class rows (a scalar mask: untaken rows cost a branch)
+      const uint32_t mask = __builtin_amdgcn_readfirstlane(s_umask[j]);
       uint32_t m = 0x7F7F7F7Fu;
 #pragma unroll
       for (uint32_t u = 0; u < kTwinMaxC; ++u)
