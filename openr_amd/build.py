@@ -31,7 +31,8 @@ ENGINE_SO = os.path.join(LIB, "libopenr_spf_hip.so")
 DECISION_SO = os.path.join(LIB, "libopenr_decision.so")
 HEADERS = [os.path.join(ROOT, "include", h)
            for h in ("openr_spf.h", "openr_decision.h", "openr_adjdb.h")] + \
-    [os.path.join(PKG, "csrc", "engine", h) for h in ("spf_kernels.h", "spf_internal.h")] + \
+    [os.path.join(PKG, "csrc", "engine", h) for h in ("spf_kernels.h", "spf_internal.h")]
+DECISION_HEADERS = HEADERS + \
     [os.path.join(PKG, "csrc", "decision", h) for h in ("link_state.h", "spf_solver.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -74,7 +75,7 @@ def build(force: bool = False, verbose_resources: bool = False) -> None:
     objs = [_obj(s) for s in ENGINE_SRC]
     if force or todo or _newer(ENGINE_SO, objs):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", ENGINE_SO] + objs)
-    if force or _newer(DECISION_SO, DECISION_SRC + HEADERS + [ENGINE_SO]):
+    if force or _newer(DECISION_SO, DECISION_SRC + DECISION_HEADERS + [ENGINE_SO]):
         _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra",
               "-Wno-unused-parameter", "-o", DECISION_SO] + DECISION_SRC +
              ["-L" + LIB, "-lopenr_spf_hip", "-Wl,-rpath,$ORIGIN"])

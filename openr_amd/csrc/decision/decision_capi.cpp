@@ -131,6 +131,7 @@ int odl_apply(odl_ls* h, const oadj_stream* s, uint32_t first, uint32_t count,
       // a batch of updates: databases built on host threads, then applied in
       // order (LinkState::updateAdjacencyDatabases: in parallel when every
       // database is a new node)
+      const auto t0 = std::chrono::steady_clock::now();
       std::vector<odl::AdjacencyDatabase> dbs(count);
       odl::parallelFor(count, [&](uint32_t lo, uint32_t hi) {
         for (uint32_t k = lo; k < hi; ++k) {
@@ -152,6 +153,9 @@ int odl_apply(odl_ls* h, const oadj_stream* s, uint32_t first, uint32_t count,
           }
         }
       }, 256);
+      if (getenv("ODL_SPF_TIMING"))
+        std::fprintf(stderr, "ODL_INGEST build_dbs_ms=%.1f\n",
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
       const auto chs = h->ls.updateAdjacencyDatabases(dbs);
       for (uint32_t k = 0; changes && k < count; ++k)
         changes[k] = oadj_change{chs[k].topologyChanged, chs[k].linkAttributesChanged,

@@ -30,20 +30,9 @@ inline uint64_t fold(uint64_t hi, uint64_t lo) {
   return b * kMul;
 }
 
-inline uint64_t hashPair(const std::pair<std::string, std::string>& p) {
+inline uint64_t hashEnd(const std::string& node, const std::string& iface) {
   const std::hash<std::string> h;
-  return fold(h(p.first), h(p.second));
-}
-
-inline std::string tripleKey(const std::string& a, const std::string& b, const std::string& c) {
-  std::string k;
-  k.reserve(a.size() + b.size() + c.size() + 2);
-  k += a;
-  k += '\0';
-  k += b;
-  k += '\0';
-  k += c;
-  return k;
+  return fold(h(node), h(iface));  // std::hash<std::pair<string, string>>
 }
 
 constexpr uint32_t kInf = OSPF_DIST_INF;
@@ -51,27 +40,30 @@ constexpr uint32_t kInf = OSPF_DIST_INF;
 }  // namespace
 
 // ---------------------------------------------------------------- Link
-size_t Link::hashOf(const std::pair<std::string, std::string>& a,
-                    const std::pair<std::string, std::string>& b) {
-  return fold(hashPair(a), hashPair(b));
+size_t Link::hashOf(const End& lo, const End& hi) {
+  return fold(hashEnd(lo.node, lo.iface), hashEnd(hi.node, hi.iface));
 }
 
-static std::pair<std::pair<std::string, std::string>, std::pair<std::string, std::string>>
-orderedEnds(const std::string& n1, const std::string& i1, const std::string& n2,
-            const std::string& i2) {
-  auto x = std::make_pair(n1, i1), y = std::make_pair(n2, i2);
-  if (y < x) std::swap(x, y);
-  return {x, y};
+size_t LinkState::AdjKeyHash::operator()(const AdjKey& k) const {
+  const std::hash<std::string_view> h;
+  return fold(h(k.other), fold(h(k.ifn), h(k.oifn)));
 }
 
+static bool endLess(const std::string& n1, const std::string& i1, const std::string& n2,
+                    const std::string& i2) {
+  const int c = n1.compare(n2);
+  return c < 0 || (c == 0 && i1 < i2);
+}
+
+// The ends are stored once, end_[lo_] holding the smaller (node, iface) pair
+// -- the reference's n1/if1 after its ordering (LinkState.cpp:95-110).
 Link::Link(const std::string& n1, const Adjacency& a1, const std::string& n2, const Adjacency& a2)
     : hash([&] {
-        auto o = orderedEnds(n1, a1.ifName, n2, a2.ifName);
-        return hashOf(o.first, o.second);
+        return endLess(n2, a2.ifName, n1, a1.ifName)
+                   ? fold(hashEnd(n2, a2.ifName), hashEnd(n1, a1.ifName))
+                   : fold(hashEnd(n1, a1.ifName), hashEnd(n2, a2.ifName));
       }()) {
-  auto o = orderedEnds(n1, a1.ifName, n2, a2.ifName);
-  low_ = o.first;
-  high_ = o.second;
+  lo_ = endLess(n2, a2.ifName, n1, a1.ifName) ? 1 : 0;
   const Adjacency* adj[2] = {&a1, &a2};
   const std::string* nn[2] = {&n1, &n2};
   for (int i = 0; i < 2; ++i) {
@@ -118,14 +110,18 @@ void Link::setAdjLabelFrom(const std::string& n, int32_t l) { endOf(n).adjLabel 
 void Link::setWeightFrom(const std::string& n, int64_t w) { endOf(n).weight = w; }
 
 bool Link::sameLink(const Link& o) const {
-  return hash == o.hash && low_ == o.low_ && high_ == o.high_;
+  const End &a = end_[lo_], &b = end_[lo_ ^ 1], &c = o.end_[o.lo_], &d = o.end_[o.lo_ ^ 1];
+  return hash == o.hash && a.node == c.node && a.iface == c.iface && b.node == d.node &&
+         b.iface == d.iface;
 }
 bool Link::orderedBefore(const Link& o) const {
   if (hash != o.hash) return hash < o.hash;
-  return std::tie(low_, high_) < std::tie(o.low_, o.high_);
+  const End &a = end_[lo_], &b = end_[lo_ ^ 1], &c = o.end_[o.lo_], &d = o.end_[o.lo_ ^ 1];
+  return std::tie(a.node, a.iface, b.node, b.iface) < std::tie(c.node, c.iface, d.node, d.iface);
 }
 std::string Link::key() const {
-  return low_.first + "%" + low_.second + "|" + high_.first + "%" + high_.second;
+  const End &a = end_[lo_], &b = end_[lo_ ^ 1];
+  return a.node + "%" + a.iface + "|" + b.node + "%" + b.iface;
 }
 
 // ---------------------------------------------------------------- LinkState
@@ -159,7 +155,7 @@ LinkPtr LinkState::makeLink(const std::string& node, const Adjacency& adj) const
   if (other == adjDbs_.end()) return nullptr;
   auto idx = adjIndex_.find(adj.otherNodeName);
   if (idx == adjIndex_.end()) return nullptr;
-  auto hit = idx->second.find(tripleKey(node, adj.otherIfName, adj.ifName));
+  auto hit = idx->second.find(AdjKey{node, adj.otherIfName, adj.ifName});
   if (hit == idx->second.end()) return nullptr;
   return std::make_shared<Link>(node, adj, adj.otherNodeName,
                                 other->second.adjacencies[hit->second]);
@@ -167,13 +163,13 @@ LinkPtr LinkState::makeLink(const std::string& node, const Adjacency& adj) const
 
 void LinkState::addLink(const LinkPtr& l) {
   if (!linkMap_[l->lowNode()].insert(l).second || !linkMap_[l->highNode()].insert(l).second ||
-      !allLinks_.insert(l).second)
+      !shardOf(*l).insert(l).second)
     throw std::logic_error("duplicate link " + l->key());
 }
 
 void LinkState::removeLink(const LinkPtr& l) {
   if (!linkMap_.at(l->lowNode()).erase(l) || !linkMap_.at(l->highNode()).erase(l) ||
-      !allLinks_.erase(l))
+      !shardOf(*l).erase(l))
     throw std::logic_error("missing link " + l->key());
 }
 
@@ -205,12 +201,12 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db) 
   bool structural = !known;  // a link or node added / removed (incremental mode)
   std::vector<LinkDelta> deltas;
   std::vector<std::string> nodeDeltas;
-  adjDbs_[me] = db;
   auto& idx = adjIndex_[me];
-  idx.clear();
-  for (uint32_t i = 0; i < db.adjacencies.size(); ++i) {
-    const auto& a = db.adjacencies[i];
-    idx.emplace(tripleKey(a.otherNodeName, a.ifName, a.otherIfName), i);
+  idx.clear();  // (its views point into the database replaced here)
+  const AdjacencyDatabase& kept = adjDbs_[me] = db;
+  for (uint32_t i = 0; i < kept.adjacencies.size(); ++i) {
+    const auto& a = kept.adjacencies[i];
+    idx.emplace(AdjKey{a.otherNodeName, a.ifName, a.otherIfName}, i);
   }
 
   std::vector<LinkPtr> before = sortedLinksOf(me);
@@ -325,6 +321,7 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db) 
 // its links in the sequential insertion order (creation order), so each
 // unordered_set ends up with the same buckets and iteration order.
 std::vector<LinkStateChange> LinkState::updateAdjacencyDatabases(std::vector<AdjacencyDatabase>& dbs) {
+  const auto tIn = std::chrono::steady_clock::now();
   const uint32_t n = (uint32_t)dbs.size();
   std::vector<LinkStateChange> out(n);
   bool bulk = n >= 64 && !getenv("ODL_NO_BULK_INGEST");
@@ -343,7 +340,7 @@ std::vector<LinkStateChange> LinkState::updateAdjacencyDatabases(std::vector<Adj
   Clock::time_point tp[6];
   tp[0] = Clock::now();
   std::vector<AdjacencyDatabase*> dbp(n);
-  std::vector<std::unordered_map<std::string, uint32_t>*> idxp(n);
+  std::vector<std::unordered_map<AdjKey, uint32_t, AdjKeyHash>*> idxp(n);
   // (no order of these maps or of allLinks_ is observed: node ids are name
   // ranks; only the per-node LinkSets' iteration order is, and those are not
   // reserved)
@@ -365,8 +362,9 @@ std::vector<LinkStateChange> LinkState::updateAdjacencyDatabases(std::vector<Adj
       auto& idx = *idxp[i];
       idx.clear();
       const auto& adj = dbp[i]->adjacencies;
+      idx.reserve(adj.size());
       for (uint32_t k = 0; k < adj.size(); ++k)
-        idx.emplace(tripleKey(adj[k].otherNodeName, adj[k].ifName, adj[k].otherIfName), k);
+        idx.emplace(AdjKey{adj[k].otherNodeName, adj[k].ifName, adj[k].otherIfName}, k);
     }
   }, 256);
   // links each update creates, in Link order
@@ -391,57 +389,53 @@ std::vector<LinkStateChange> LinkState::updateAdjacencyDatabases(std::vector<Adj
   tp[2] = Clock::now();
   // every touched node's insertions in creation order (low end, then high)
   std::unordered_map<std::string, uint32_t> other;  // nodes known before the batch
-  std::vector<std::vector<LinkPtr>> ins(n);
+  // (pointers into out[i].addedLinks, reserved up front: no reallocation)
+  std::vector<std::vector<const LinkPtr*>> ins(n);
+  std::array<std::vector<const LinkPtr*>, kLinkShards> shardIns;
   bool anyTopo = false;
   for (uint32_t i = 0; i < n; ++i) {
     out[i].addedLinks.reserve(created[i].size());
     for (auto& c : created[i]) {
-      const LinkPtr& l = c.first;
-      if (c.second == i) throw std::logic_error("duplicate link " + l->key());  // a self-link
+      out[i].addedLinks.push_back(std::move(c.first));
+      const LinkPtr* l = &out[i].addedLinks.back();
+      if (c.second == i) throw std::logic_error("duplicate link " + (*l)->key());  // a self-link
       uint32_t o = c.second;
       if (o == kInf) {
-        auto q = other.emplace(l->otherNode(dbp[i]->thisNodeName), (uint32_t)ins.size());
+        auto q = other.emplace((*l)->otherNode(dbp[i]->thisNodeName), (uint32_t)ins.size());
         if (q.second) ins.emplace_back();
         o = q.first->second;
       }
-      const bool meLow = l->lowNode() == dbp[i]->thisNodeName;
+      const bool meLow = (*l)->lowNode() == dbp[i]->thisNodeName;
       ins[meLow ? i : o].push_back(l);
       ins[meLow ? o : i].push_back(l);
-      out[i].topologyChanged |= l->isUp();
-      out[i].addedLinks.push_back(std::move(c.first));
+      out[i].topologyChanged |= (*l)->isUp();
+      shardIns[((*l)->hash >> 7) % kLinkShards].push_back(l);
     }
     anyTopo |= out[i].topologyChanged;
-    created[i].clear();
   }
+  created = {};
   tp[3] = Clock::now();
   std::vector<LinkSet*> setp(ins.size());
   for (uint32_t i = 0; i < n; ++i) setp[i] = &linkMap_[dbp[i]->thisNodeName];
   for (const auto& o : other) setp[o.second] = &linkMap_[o.first];
   std::atomic<bool> dup{false};
-  size_t added = 0;
-  for (uint32_t i = 0; i < n; ++i) added += out[i].addedLinks.size();
-  allLinks_.reserve(allLinks_.size() + added);
-  std::thread all([&] {  // allLinks_ in creation order, beside the per-node sets
-    for (uint32_t i = 0; i < n; ++i)
-      for (const LinkPtr& l : out[i].addedLinks)
-        if (!allLinks_.insert(l).second) dup = true;
-  });
-  try {
-    parallelFor((uint32_t)ins.size(), [&](uint32_t lo, uint32_t hi) {
-      for (uint32_t u = lo; u < hi; ++u)
-        for (const LinkPtr& l : ins[u])
-          if (!setp[u]->insert(l).second) dup = true;
-    }, 256);
-  } catch (...) {
-    all.join();
-    throw;
-  }
-  all.join();
+  parallelFor((uint32_t)ins.size(), [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t u = lo; u < hi; ++u)
+      for (const LinkPtr* l : ins[u])
+        if (!setp[u]->insert(*l).second) dup = true;
+  }, 256);
+  parallelFor(kLinkShards, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t s = lo; s < hi; ++s) {
+      allLinks_[s].reserve(allLinks_[s].size() + shardIns[s].size());
+      for (const LinkPtr* l : shardIns[s])
+        if (!allLinks_[s].insert(*l).second) dup = true;
+    }
+  }, 1);
   tp[4] = Clock::now();
   if (timing) {
     auto ms = [&](int a) { return std::chrono::duration<double, std::milli>(tp[a + 1] - tp[a]).count(); };
-    std::fprintf(stderr, "ODL_INGEST dbs=%u index_ms=%.1f links_ms=%.1f order_ms=%.1f sets_ms=%.1f\n",
-                 n, ms(0), ms(1), ms(2), ms(3));
+    std::fprintf(stderr, "ODL_INGEST dbs=%u check_ms=%.1f index_ms=%.1f links_ms=%.1f order_ms=%.1f sets_ms=%.1f\n",
+                 n, std::chrono::duration<double, std::milli>(tp[0] - tIn).count(), ms(0), ms(1), ms(2), ms(3));
   }
   if (dup) throw std::logic_error("duplicate link in an adjacency database batch");
   // one version step per database, as in turn (a new node is structural)
@@ -457,7 +451,7 @@ LinkStateChange LinkState::deleteAdjacencyDatabase(const std::string& node) {
   auto lm = linkMap_.find(node);
   if (lm != linkMap_.end()) {
     for (const auto& l : lm->second) {
-      if (!linkMap_.at(l->otherNode(node)).erase(l) || !allLinks_.erase(l))
+      if (!linkMap_.at(l->otherNode(node)).erase(l) || !shardOf(*l).erase(l))
         throw std::logic_error("inconsistent link map");
     }
     linkMap_.erase(lm);

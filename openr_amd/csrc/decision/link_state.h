@@ -17,6 +17,7 @@
 #pragma once
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cstdint>
 #include <exception>
@@ -25,6 +26,7 @@
 #include <optional>
 #include <stdexcept>
 #include <string>
+#include <string_view>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -104,8 +106,8 @@ class Link {
   void setAdjLabelFrom(const std::string& n, int32_t l);
   void setWeightFrom(const std::string& n, int64_t w);
 
-  const std::string& lowNode() const { return low_.first; }
-  const std::string& highNode() const { return high_.first; }
+  const std::string& lowNode() const { return end_[lo_].node; }
+  const std::string& highNode() const { return end_[lo_ ^ 1].node; }
   bool sameLink(const Link& o) const;
   bool orderedBefore(const Link& o) const;  // Link::operator< (hash, names)
   std::string key() const;                  // "n1%if1|n2%if2" (ordered)
@@ -129,9 +131,8 @@ class Link {
   End& endOf(const std::string& n);
   const End& endOf(const std::string& n) const;
   End end_[2];
-  std::pair<std::string, std::string> low_, high_;
-  static size_t hashOf(const std::pair<std::string, std::string>& a,
-                       const std::pair<std::string, std::string>& b);
+  uint8_t lo_ = 0;  // end_[lo_] is the lower (node, iface) pair, end_[lo_ ^ 1] the higher
+  static size_t hashOf(const End& lo, const End& hi);
 };
 
 using LinkPtr = std::shared_ptr<Link>;
@@ -230,7 +231,11 @@ class LinkState {
 
   const LinkSet& linksFromNode(const std::string& node) const;
   bool isNodeOverloaded(const std::string& node) const;
-  size_t numLinks() const { return allLinks_.size(); }
+  size_t numLinks() const {
+    size_t k = 0;
+    for (const auto& s : allLinks_) k += s.size();
+    return k;
+  }
   size_t numNodes() const { return adjDbs_.size(); }
   const std::unordered_map<std::string, AdjacencyDatabase>& getAdjacencyDatabases() const {
     return adjDbs_;
@@ -376,11 +381,23 @@ class LinkState {
   IncrementalStats incStats_;
 
   std::unordered_map<std::string, LinkSet> linkMap_;
-  LinkSet allLinks_;
+  // every link, in shards by hash (only membership and the count are read;
+  // the bulk path fills the shards on separate threads)
+  static constexpr uint32_t kLinkShards = 16;
+  std::array<LinkSet, kLinkShards> allLinks_;
+  LinkSet& shardOf(const Link& l) { return allLinks_[(l.hash >> 7) % kLinkShards]; }
   std::unordered_map<std::string, bool> nodeOverloads_;
   std::unordered_map<std::string, AdjacencyDatabase> adjDbs_;
-  // (otherNodeName \0 ifName \0 otherIfName) -> first adjacency index, per node
-  std::unordered_map<std::string, std::unordered_map<std::string, uint32_t>> adjIndex_;
+  // per node: (otherNodeName, ifName, otherIfName) -> adjacency position; the
+  // views point into adjDbs_[node]'s own strings and are rebuilt with it
+  struct AdjKey {
+    std::string_view other, ifn, oifn;
+    bool operator==(const AdjKey& o) const { return other == o.other && ifn == o.ifn && oifn == o.oifn; }
+  };
+  struct AdjKeyHash {
+    size_t operator()(const AdjKey& k) const;
+  };
+  std::unordered_map<std::string, std::unordered_map<AdjKey, uint32_t, AdjKeyHash>> adjIndex_;
 
   std::unordered_map<std::string, SpfResult> memoMetric_, memoHops_;
   std::unordered_map<std::string, RawRun> rawMetric_;  // unmasked runs (useLinkMetric)
