@@ -335,6 +335,14 @@ __global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C
       if (tid == 0) atomicOr(a.err, 64u);
       continue;
     }
+    if (a.dload) {  // cover columns given (closure rows): the full row only
+      const uint32_t* src = a.dload + (size_t)i * nS;
+      for (uint32_t x = tid; x < nS; x += kBlock) s_D[x] = src[x];
+      __syncthreads();
+      write_row(g, C, a.dist + (size_t)a.rowpos[i] * V, s_D, s_tr, r, tid, kBlock);
+      __syncthreads();
+      continue;
+    }
     for (uint32_t x = tid; x < nS; x += kBlock) s_D[x] = x == r ? 0u : kInf;
     if (tid == 0) s_next[0] = s_next[1] = kInf;
     __syncthreads();
@@ -368,17 +376,85 @@ __global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C
       if (t == kInf) break;  // every reachable cover node settled
       __syncthreads();       // the slot reset is visible before its use
     }
-    write_row(g, C, a.dist + (size_t)i * V, s_D, s_tr, r, tid, kBlock);
+    if (a.dcomp) {  // the cover columns as a seed of the closure
+      const bool tr = (s_tr[r >> 5] >> (r & 31u)) & 1u;
+      uint32_t* dst = a.dcomp + (size_t)i * nS;
+      for (uint32_t x = tid; x < nS; x += kBlock) dst[x] = tr ? s_D[x] : (x == r ? 0u : kInf);
+    }
+    const uint32_t rp = a.rowpos ? a.rowpos[i] : i;
+    if (rp != kInf) write_row(g, C, a.dist + (size_t)rp * V, s_D, s_tr, r, tid, kBlock);
     __syncthreads();  // s_D is reused by the next root
   }
 }
 
+// Cover closure: block = (component, 256 cover columns), lane = column; the
+// component's members' accumulators stay in registers while the seeds'
+// columns stream past (8 loads in flight), the per-member constants are
+// block-uniform (scalar loads). Blocks are ordered column-chunk-major and
+// spread so that one XCD's resident blocks share a chunk of the seed rows in
+// its L2.
+__device__ __forceinline__ uint32_t sat_add32(uint32_t c, uint32_t x) {
+  const uint32_t s = c + x;
+  return (x == kInf || c == kInf || s < c) ? kInf : s;
+}
+template <int KW>
+__global__ void __launch_bounds__(256) closure_kernel(ClosurePlan p) {
+  const uint32_t nb = gridDim.x, b = blockIdx.x;
+  const uint32_t full = nb / 8u * 8u;
+  const uint32_t item = b < full ? (b % 8u) * (full / 8u) + b / 8u : b;
+  const uint32_t chunk = item / p.ncomp, ci = item % p.ncomp;
+  const uint32_t v = chunk * 256u + threadIdx.x;
+  const bool ok = v < p.nS;
+  const uint2 cm = p.comp[ci];
+  uint32_t acc[KW];
+#pragma unroll
+  for (int f = 0; f < KW; ++f) acc[f] = kInf;
+  const uint32_t* cst = p.cst + (size_t)cm.x * KW;
+  const uint32_t* jl = p.jl + cm.x;
+  for (uint32_t j0 = 0; j0 < cm.y; j0 += 8u) {
+    uint32_t x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t j = j0 + (uint32_t)u;
+      x[u] = (ok && j < cm.y) ? p.seedC[(size_t)jl[j] * p.nS + v] : kInf;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t j = j0 + (uint32_t)u;
+      if (j >= cm.y) break;  // uniform
+#pragma unroll
+      for (int f = 0; f < KW; ++f) acc[f] = min(acc[f], sat_add32(cst[j * KW + f], x[u]));
+    }
+  }
+  const uint32_t* mem = p.mem + (size_t)ci * KW;
+  const uint32_t* dl = p.dloc + (size_t)ci * KW * KW;
+#pragma unroll
+  for (int m = 0; m < KW; ++m)
+    if (mem[m] == v)
+#pragma unroll
+      for (int f = 0; f < KW; ++f) acc[f] = min(acc[f], dl[f * KW + m]);
+  const uint32_t* out = p.out + (size_t)ci * KW;
+#pragma unroll
+  for (int f = 0; f < KW; ++f)
+    if (ok && out[f] != kInf) p.dc[(size_t)out[f] * p.nS + v] = acc[f];
+}
+
 }  // namespace
+
+hipError_t launch_closure(const ClosurePlan& p, uint32_t KW, hipStream_t s) {
+  if (p.ncomp == 0) return hipSuccess;
+  const dim3 grid(p.ncomp * p.chunks);
+  if (KW <= 8) hipLaunchKernelGGL(closure_kernel<8>, grid, dim3(256), 0, s, p);
+  else if (KW <= 16) hipLaunchKernelGGL(closure_kernel<16>, grid, dim3(256), 0, s, p);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
 
 hipError_t launch_cover_spf(const DevGraph& g, const CoverGraph& C, const CoverArgs& a,
                             uint32_t n_cu, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  if (const char* e = getenv("OSPF_COVER_DELTA")) {  // delta-stepping (experiment)
+  const char* e = getenv("OSPF_COVER_DELTA");
+  if (e && !a.rowpos && !a.dcomp && !a.dload) {  // delta-stepping (experiment)
     const uint32_t delta = (uint32_t)std::max(1, atoi(e));
     const size_t lds = ((size_t)C.nS + 2u * ((C.nS + 31u) / 32u)) * 4u;
     const uint32_t per_cu = std::max<uint32_t>(1, (uint32_t)((150u * 1024u) / (lds + 12u * 1024u)));

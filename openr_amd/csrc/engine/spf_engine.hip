@@ -760,6 +760,189 @@ int twin_lv_launch(ospf_ctx* c, const ospf::TwinLvPlan& p, void* stream) {
 
 }  // namespace ospf_int
 
+// Closure split of the contracted graph C (host copy in c->h_cc*): seeds =
+// the cover nodes of degree >= tau for the largest of C's few largest
+// degrees tau at which every component of C minus the seeds has at most
+// kClosureMaxK nodes and the seeds are at most max(64, nS / 8) (F100k: the
+// 288 spines; components = the pods' 8 fabric switches). No split: empty.
+static void cover_closure_split(ospf_ctx* c) {
+  const uint32_t nS = (uint32_t)c->h_ccv.size();
+  c->cl_seed.clear();
+  c->cl_comp_of.assign(nS, ~0u);
+  c->cl_comp_off.assign(1, 0u);
+  c->cl_comp_mem.clear();
+  if (getenv("OSPF_COVER_NOCLOSURE") || nS < 2) return;
+  const auto& crow = c->h_ccrow;
+  const auto& ced = c->h_cedge;
+  std::vector<uint32_t> deg(nS), dd;
+  for (uint32_t i = 0; i < nS; ++i) deg[i] = crow[i + 1] - crow[i];
+  dd = deg;
+  std::sort(dd.begin(), dd.end(), std::greater<uint32_t>());
+  dd.erase(std::unique(dd.begin(), dd.end()), dd.end());
+  const uint32_t max_seeds = std::max<uint32_t>(64u, nS / 8u);
+  std::vector<uint32_t> par(nS), sz(nS);
+  auto find = [&](uint32_t x) {
+    while (par[x] != x) x = par[x] = par[par[x]];
+    return x;
+  };
+  for (size_t t = 0; t < std::min<size_t>(dd.size(), 8); ++t) {
+    const uint32_t tau = dd[t];
+    uint32_t ns = 0;
+    for (uint32_t i = 0; i < nS; ++i) ns += deg[i] >= tau;
+    if (ns > max_seeds || ns == nS) break;
+    for (uint32_t i = 0; i < nS; ++i) {
+      par[i] = i;
+      sz[i] = 1;
+    }
+    for (uint32_t i = 0; i < nS; ++i) {
+      if (deg[i] >= tau) continue;
+      for (uint32_t e = crow[i]; e < crow[i + 1]; ++e) {
+        const uint32_t j = ced[e].x;
+        if (deg[j] >= tau) continue;
+        uint32_t a = find(i), b = find(j);
+        if (a == b) continue;
+        if (sz[a] < sz[b]) std::swap(a, b);
+        par[b] = a;
+        sz[a] += sz[b];
+      }
+    }
+    bool fits = true;
+    for (uint32_t i = 0; i < nS && fits; ++i)
+      if (deg[i] < tau && sz[find(i)] > ospf::kClosureMaxK) fits = false;
+    if (getenv("OSPF_SWEEP_DEBUG"))
+      fprintf(stderr, "cover split: nS %u tau %u seeds %u fits %d\n", nS, tau, ns, (int)fits);
+    if (!fits) continue;
+    std::vector<uint32_t> id(nS, ~0u), cnt;
+    for (uint32_t i = 0; i < nS; ++i) {
+      if (deg[i] >= tau) {
+        c->cl_seed.push_back(i);
+        continue;
+      }
+      const uint32_t rt = find(i);
+      if (id[rt] == ~0u) {
+        id[rt] = (uint32_t)cnt.size();
+        cnt.push_back(0);
+      }
+      c->cl_comp_of[i] = id[rt];
+      ++cnt[id[rt]];
+    }
+    c->cl_comp_off.assign(cnt.size() + 1, 0u);
+    for (size_t k = 0; k < cnt.size(); ++k) c->cl_comp_off[k + 1] = c->cl_comp_off[k] + cnt[k];
+    c->cl_comp_mem.assign(c->cl_comp_off.back(), 0u);
+    std::vector<uint32_t> fill(c->cl_comp_off.begin(), c->cl_comp_off.end() - 1);
+    for (uint32_t i = 0; i < nS; ++i)
+      if (c->cl_comp_of[i] != ~0u) c->cl_comp_mem[fill[c->cl_comp_of[i]]++] = i;
+    return;
+  }
+}
+
+namespace ospf_int {
+int closure_build(ospf_ctx* c, const std::vector<uint32_t>& roots,
+                  const std::vector<uint32_t>& seed_row, ClosureHost& h) {
+  constexpr uint32_t kN = ~0u;
+  const uint32_t nS = (uint32_t)c->h_ccv.size();
+  if (c->cl_seed.empty()) return fail(c, OSPF_E_INVAL, "closure: no seed split of the cover");
+  std::vector<uint32_t> cidx(c->info.n_nodes, kN);
+  for (uint32_t i = 0; i < nS; ++i) cidx[c->h_ccv[i]] = i;
+  const uint32_t ncomp_all = (uint32_t)c->cl_comp_off.size() - 1;
+  std::vector<uint32_t> slot(ncomp_all, kN), comps;
+  uint32_t kmax = 1;
+  for (uint32_t r : roots) {
+    const uint32_t ci = r < cidx.size() ? cidx[r] : kN;
+    if (ci == kN || c->cl_comp_of[ci] == kN)
+      return fail(c, OSPF_E_INVAL, "closure: a root is not a non-seed cover node");
+    const uint32_t k = c->cl_comp_of[ci];
+    if (slot[k] == kN) {
+      slot[k] = (uint32_t)comps.size();
+      comps.push_back(k);
+      kmax = std::max(kmax, c->cl_comp_off[k + 1] - c->cl_comp_off[k]);
+    }
+  }
+  const uint32_t KW = kmax <= 8 ? 8u : 16u;
+  const uint32_t nq = (uint32_t)comps.size();
+  h.KW = KW;
+  h.comp.assign(nq, make_uint2(0, 0));
+  h.jl.clear();
+  h.cst.clear();
+  h.mem.assign((size_t)nq * KW, kN);
+  h.dloc.assign((size_t)nq * KW * KW, kN);
+  h.out.assign((size_t)nq * KW, kN);
+  auto transit = [&](uint32_t i) { return (c->h_cctr[i >> 5] >> (i & 31u)) & 1u; };
+  const auto& crow = c->h_ccrow;
+  const auto& ced = c->h_cedge;
+  std::vector<uint32_t> jof(nS, kN);  // seed -> term of the current component
+  std::vector<uint64_t> d(KW);
+  for (uint32_t i = 0; i < (uint32_t)roots.size(); ++i) {
+    const uint32_t ci = cidx[roots[i]], k = c->cl_comp_of[ci];
+    const uint32_t* M = c->cl_comp_mem.data() + c->cl_comp_off[k];
+    const uint32_t kk = c->cl_comp_off[k + 1] - c->cl_comp_off[k];
+    const uint32_t m = (uint32_t)(std::find(M, M + kk, ci) - M);
+    h.out[(size_t)slot[k] * KW + m] = i;
+  }
+  for (uint32_t q = 0; q < nq; ++q) {
+    const uint32_t k = comps[q];
+    const uint32_t* M = c->cl_comp_mem.data() + c->cl_comp_off[k];
+    const uint32_t kk = c->cl_comp_off[k + 1] - c->cl_comp_off[k];
+    auto local = [&](uint32_t x) {
+      for (uint32_t m = 0; m < kk; ++m)
+        if (M[m] == x) return m;
+      return kN;
+    };
+    for (uint32_t m = 0; m < kk; ++m) h.mem[(size_t)q * KW + m] = M[m];
+    const uint32_t joff = (uint32_t)h.jl.size();
+    std::vector<uint32_t> used;  // seeds given a term (jof reset after)
+    for (uint32_t f = 0; f < kk; ++f) {
+      // distances inside the component from f: members relay when transit
+      // (f itself always: the root), Bellman-Ford over <= 16 nodes
+      std::fill(d.begin(), d.end(), UINT64_MAX);
+      d[f] = 0;
+      for (uint32_t it = 0; it < kk; ++it) {
+        bool ch = false;
+        for (uint32_t u = 0; u < kk; ++u) {
+          if (d[u] == UINT64_MAX || (u != f && !transit(M[u]))) continue;
+          for (uint32_t e = crow[M[u]]; e < crow[M[u] + 1]; ++e) {
+            const uint32_t x = local(ced[e].x);
+            if (x == kN) continue;
+            const uint64_t nd = d[u] + ced[e].y;
+            if (nd < d[x]) {
+              d[x] = nd;
+              ch = true;
+            }
+          }
+        }
+        if (!ch) break;
+      }
+      for (uint32_t m = 0; m < kk; ++m)
+        h.dloc[((size_t)q * KW + f) * KW + m] = d[m] >= 0xFFFFFFFFull ? kN : (uint32_t)d[m];
+      for (uint32_t g = 0; g < kk; ++g) {
+        if (d[g] == UINT64_MAX || (g != f && !transit(M[g]))) continue;
+        for (uint32_t e = crow[M[g]]; e < crow[M[g] + 1]; ++e) {
+          const uint32_t x = ced[e].x;
+          if (c->cl_comp_of[x] != kN) continue;  // not a seed
+          if (jof[x] == kN) {
+            if (seed_row[x] == kN) return fail(c, OSPF_E_INVAL, "closure: a seed row is missing");
+            jof[x] = (uint32_t)h.jl.size() - joff;
+            h.jl.push_back(seed_row[x]);
+            h.cst.resize(h.jl.size() * KW, kN);
+            used.push_back(x);
+          }
+          const uint64_t cc = d[g] + ced[e].y;
+          uint32_t& dst = h.cst[(size_t)(joff + jof[x]) * KW + f];
+          if (cc < dst) dst = (uint32_t)cc;
+        }
+      }
+    }
+    h.comp[q] = make_uint2(joff, (uint32_t)h.jl.size() - joff);
+    for (uint32_t x : used) jof[x] = kN;
+  }
+  if (h.jl.empty()) {  // no seed terms at all: one unused row keeps the arrays non-empty
+    h.jl.push_back(0);
+    h.cst.assign(KW, kN);
+  }
+  return OSPF_OK;
+}
+}  // namespace ospf_int
+
 extern "C" {
 
 int ospf_open(int device, ospf_ctx** out) {
@@ -1771,6 +1954,11 @@ int ospf_cover_prepare(ospf_ctx* c, const uint8_t* leaf) {
     cix[v] = 0x80000000u | (q0 << 5) | nq;
     ++l;
   }
+  c->h_ccv = cv;
+  c->h_ccrow = crow;
+  c->h_cctr = ctr;
+  c->h_cedge = cedge;
+  cover_closure_split(c);
   if (ladj.empty()) ladj.assign(4, 0xFFFFu);
   if (cedge.empty()) cedge.push_back(make_uint2(0, 0));
   // one allocation: cix | crow | ctr | lrow | ladj | cedge (16-B aligned parts)

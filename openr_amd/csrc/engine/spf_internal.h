@@ -55,6 +55,14 @@ struct ospf_ctx {
   ospf::CoverGraph cover{};
   uint64_t cover_ver = ~0ull;
   bool cover_ok = false;
+  // host copy of the contracted graph, and its closure split (when one
+  // exists): seeds = the cover nodes of largest degree, every other cover
+  // node in a component of C minus the seeds of <= kClosureMaxK nodes
+  std::vector<uint32_t> h_ccv, h_ccrow, h_cctr;  // cover index -> node id, CSR, transit bits
+  std::vector<uint2> h_cedge;
+  std::vector<uint32_t> cl_seed;               // cover indices of the seeds
+  std::vector<uint32_t> cl_comp_of;            // per cover index: component, or ~0u (seed)
+  std::vector<uint32_t> cl_comp_off, cl_comp_mem;  // members (cover indices) per component
   std::vector<hipEvent_t> ev;  // [2 * slots]: rerun done / trace done per slot
   uint64_t graph_gen = 0;      // bumped by every load / patch (sweeps check it)
   // ospf_links_mask: the entries and planner state it replaced (restored by
@@ -97,6 +105,18 @@ int twin_lv_build(ospf_ctx* c, const std::vector<uint32_t>& roots, const std::ve
                   const std::vector<uint32_t>& rep, TwinLvHost& out);
 // queue a planned twin-levels launch (device copies of the plan's arrays)
 int twin_lv_launch(ospf_ctx* c, const ospf::TwinLvPlan& p, void* stream);
+
+// Host plan of the cover closure (spf_cover.hip closure_kernel) for the
+// closure roots `roots` (node ids, non-seed cover nodes; dc row i = roots[i])
+// with the seeds' cover columns at seedC row seed_row[cover index] (~0u: not
+// given -> OSPF_E_INVAL). KW = 8 or 16 (largest component, padded).
+struct ClosureHost {
+  uint32_t KW = 8;
+  std::vector<uint2> comp;
+  std::vector<uint32_t> jl, cst, mem, dloc, out;
+};
+int closure_build(ospf_ctx* c, const std::vector<uint32_t>& roots,
+                  const std::vector<uint32_t>& seed_row, ClosureHost& h);
 
 }  // namespace ospf_int
 

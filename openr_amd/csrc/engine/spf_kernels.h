@@ -279,11 +279,34 @@ struct CoverGraph {
 struct CoverArgs {
   const uint32_t* roots;  // node ids (cover nodes)
   uint32_t n;
-  uint32_t* dist;         // [n][V]
+  uint32_t* dist;         // [n][V] (row i), or row rowpos[i] when rowpos is set
   uint32_t* err;          // bit 64: a root outside the cover
+  const uint32_t* rowpos = nullptr;  // [n] row of root i in dist (0xFFFFFFFF: none)
+  uint32_t* dcomp = nullptr;         // [n][nS] cover columns out (a non-transit root:
+                                     // 0 at itself, unreached elsewhere -- it relays nothing)
+  const uint32_t* dload = nullptr;   // [n][nS] cover columns given: no Dial, rows only
 };
 hipError_t launch_cover_spf(const DevGraph& g, const CoverGraph& C, const CoverArgs& a,
                             uint32_t n_cu, hipStream_t s);
+
+// Cover closure (spf_cover.hip closure_kernel): the cover columns of the
+// roots of small components of C minus a seed set, from the seeds' cover
+// columns: D_f(v) = min( dloc_f(v) for v in f's component,
+//                        min over seeds s of cst_f(s) + D_s(v) ),
+// cst_f(s) = min over members g usable from f of dloc_f(g) + w(g -> s).
+constexpr uint32_t kClosureMaxK = 16;
+struct ClosurePlan {
+  uint32_t ncomp, nS, chunks;
+  const uint2* comp;       // [ncomp] {first seed term, seed terms}
+  const uint32_t* jl;      // [terms] seed row in seedC
+  const uint32_t* cst;     // [terms][KW] constants per member (unreached: 0xFFFFFFFF)
+  const uint32_t* mem;     // [ncomp][KW] member cover index (0xFFFFFFFF: none)
+  const uint32_t* dloc;    // [ncomp][KW][KW] member f -> member m
+  const uint32_t* out;     // [ncomp][KW] dc row of member f (0xFFFFFFFF: not needed)
+  const uint32_t* seedC;   // [seeds][nS]
+  uint32_t* dc;            // [rows][nS]
+};
+hipError_t launch_closure(const ClosurePlan& p, uint32_t KW, hipStream_t s);
 
 // Weighted derive (spf_wderive.hip): dist + next-hop rows (one word) of n
 // leaf roots from the distance rows of their neighbours (src + pos[v] *

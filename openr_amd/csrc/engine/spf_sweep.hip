@@ -1227,8 +1227,118 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     s->step_comp += u.comp;
     s->units.push_back(std::move(u));
   }
-  // (A) cover rows
-  {
+  // (A) cover rows: by the closure when the cover splits into seeds and
+  // small components (the seeds' Dial, the closure's cover columns, then the
+  // full rows), else every row by the Dial
+  std::vector<uint32_t> seeds, clos;
+  ospf_int::ClosureHost ch;
+  bool closure = !c->cl_seed.empty() && !getenv("OSPF_COVER_NOCLOSURE");
+  if (closure) {
+    const uint32_t nS = (uint32_t)c->h_ccv.size();
+    std::vector<uint32_t> seed_row(nS, kNone);
+    for (uint32_t j = 0; j < c->cl_seed.size(); ++j) {
+      seed_row[c->cl_seed[j]] = j;
+      seeds.push_back(c->h_ccv[c->cl_seed[j]]);
+    }
+    std::vector<uint8_t> is_seed(V, 0);
+    for (uint32_t v : seeds) is_seed[v] = 1;
+    for (uint32_t v : cover_a)
+      if (!is_seed[v]) clos.push_back(v);
+    closure = clos.size() >= seeds.size() && ospf_int::closure_build(c, clos, seed_row, ch) == OSPF_OK;
+  }
+  if (getenv("OSPF_SWEEP_DEBUG"))
+    fprintf(stderr, "plan_wcover: cover %u seeds %zu comps %zu closure roots %zu -> %s (%s)\n", nA,
+            c->cl_seed.size(), c->cl_comp_off.size() - 1, clos.size(), closure ? "closure" : "dial",
+            c->err.c_str());
+  if (closure) {
+    const uint32_t nS = (uint32_t)c->h_ccv.size(), nsd = (uint32_t)seeds.size();
+    const uint32_t ncl = (uint32_t)clos.size();
+    std::vector<uint32_t> seed_rp(nsd), clos_rp(ncl);
+    for (uint32_t j = 0; j < nsd; ++j) seed_rp[j] = pos[seeds[j]];  // kNone: not a row here
+    for (uint32_t j = 0; j < ncl; ++j) clos_rp[j] = pos[clos[j]];
+    uint32_t *d_sd, *d_srp, *d_cl, *d_crp, *seedC, *dc, *d_jl, *d_cst, *d_mem, *d_dloc, *d_out;
+    uint2* d_comp;
+    if ((rc = upload(s, &d_sd, seeds)) || (rc = upload(s, &d_srp, seed_rp)) ||
+        (rc = upload(s, &d_cl, clos)) || (rc = upload(s, &d_crp, clos_rp)) ||
+        (rc = dalloc(s, &seedC, (size_t)nsd * nS)) || (rc = dalloc(s, &dc, (size_t)ncl * nS)) ||
+        (rc = upload(s, &d_comp, ch.comp)) || (rc = upload(s, &d_jl, ch.jl)) ||
+        (rc = upload(s, &d_cst, ch.cst)) || (rc = upload(s, &d_mem, ch.mem)) ||
+        (rc = upload(s, &d_dloc, ch.dloc)) || (rc = upload(s, &d_out, ch.out)))
+      return rc;
+    ospf::ClosurePlan cp{};
+    cp.ncomp = (uint32_t)ch.comp.size();
+    cp.nS = nS;
+    cp.chunks = (nS + 255u) / 256u;
+    cp.comp = d_comp;
+    cp.jl = d_jl;
+    cp.cst = d_cst;
+    cp.mem = d_mem;
+    cp.dloc = d_dloc;
+    cp.out = d_out;
+    cp.seedC = seedC;
+    cp.dc = dc;
+    const uint32_t KW = ch.KW;
+    {
+      ospf_sweep::Unit u;
+      u.name = "cover_seeds";
+      u.kernel = "cover_spf_kernel (contracted-graph Dial of the closure's seeds, LDS-resident "
+                 "distances; their cover columns out)";
+      u.stream = 0;
+      u.n_roots = nsd;
+      u.comp = (uint64_t)nsd * 4ull * V + scan_bytes(c, true);
+      u.fn = [=](hipStream_t strm) {
+        ospf::CoverArgs a{};
+        a.roots = d_sd;
+        a.n = nsd;
+        a.dist = slab;
+        a.err = c->d_err;
+        a.rowpos = d_srp;
+        a.dcomp = seedC;
+        const hipError_t e = ospf::launch_cover_spf(c->g, c->cover, a, (uint32_t)c->n_cu, strm);
+        return e == hipSuccess ? OSPF_OK : ospf_int::hip_fail(c, e, "launch_cover_spf");
+      };
+      s->step_comp += u.comp;
+      s->units.push_back(std::move(u));
+    }
+    {
+      ospf_sweep::Unit u;
+      u.name = "cover_closure";
+      u.kernel = "closure_kernel<" + std::to_string(KW) +
+                 "> (cover columns of the components' roots from the seeds' columns)";
+      u.stream = 0;
+      u.n_roots = ncl;
+      u.comp = (uint64_t)ncl * 4ull * nS;
+      u.fn = [=](hipStream_t strm) {
+        const hipError_t e = ospf::launch_closure(cp, KW, strm);
+        return e == hipSuccess ? OSPF_OK : ospf_int::hip_fail(c, e, "launch_closure");
+      };
+      s->step_comp += u.comp;
+      s->units.push_back(std::move(u));
+    }
+    {
+      ospf_sweep::Unit u;
+      u.name = "cover_rows";
+      u.kernel = "cover_spf_kernel (full rows of the closure's roots: cover columns given, leaves "
+                 "by their last hop)";
+      u.stream = 0;
+      u.record = ev_a;
+      u.n_roots = ncl;
+      u.comp = (uint64_t)ncl * 4ull * V;
+      u.fn = [=](hipStream_t strm) {
+        ospf::CoverArgs a{};
+        a.roots = d_cl;
+        a.n = ncl;
+        a.dist = slab;
+        a.err = c->d_err;
+        a.rowpos = d_crp;
+        a.dload = dc;
+        const hipError_t e = ospf::launch_cover_spf(c->g, c->cover, a, (uint32_t)c->n_cu, strm);
+        return e == hipSuccess ? OSPF_OK : ospf_int::hip_fail(c, e, "launch_cover_spf");
+      };
+      s->step_comp += u.comp;
+      s->units.push_back(std::move(u));
+    }
+  } else {
     ospf_sweep::Unit u;
     u.name = "cover_spf";
     u.kernel = "ospf_cover_dist_dev (cover_spf_kernel: contracted-graph Dial, LDS-resident "

@@ -27,13 +27,15 @@ def random_stream(seed, n=40, p=0.15, parallel=0.2, overload=0.1, down=0.1, wmax
     return AdjDbStream.from_dbs([dbs[i] for i in rng.permutation(n)]), names
 
 
-def drained_fabric(pods, planes, seed=0, drain=0.05, down=0.03, weighted_seed=None):
+def drained_fabric(pods, planes, seed=0, drain=0.05, down=0.03, weighted_seed=None,
+                   ssw_per_plane=None):
     """topology.fabric with a random share of drained (overloaded) nodes and
     of adjacencies reported overloaded (links down), seeded."""
     from openr_amd import topology as T
     from openr_amd.adjdb import AdjDbStream
     rng = np.random.default_rng(seed)
-    dbs = T.fabric(pods=pods, planes=planes, weighted_seed=weighted_seed).to_dbs()
+    kw = {} if ssw_per_plane is None else {"ssw_per_plane": ssw_per_plane}
+    dbs = T.fabric(pods=pods, planes=planes, weighted_seed=weighted_seed, **kw).to_dbs()
     for d in dbs:
         if rng.random() < drain:
             d.overloaded = True

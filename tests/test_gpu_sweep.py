@@ -133,6 +133,27 @@ def test_sweep_weighted_fabric_cover_path():
         eng.close()
 
 
+@pytest.mark.parametrize("drain", [0.0, 0.08])
+def test_sweep_weighted_fabric_closure(drain):
+    """A weighted fabric whose cover splits into seeds (the spines) and small
+    components (a pod's fabric switches): the closure path -- the seeds' Dial,
+    closure_kernel's cover columns, then the full rows -- == the batch path bit
+    for bit, with drained (overloaded) switches and down links."""
+    # 40 pods: a spine has 40 > 32 neighbours, so it is no leaf candidate and
+    # stays in the cover (as on F100k)
+    st = drained_fabric(40, 4, seed=5, drain=drain, down=0.03 if drain else 0.0,
+                        weighted_seed=11, ssw_per_plane=4)
+    _, _, eng = engine_for(st)
+    try:
+        sw = Sweep(eng, mode="wcover")
+        names = [p["name"] for p in sw.profile(1)]
+        sw.close()
+        assert "cover_closure" in names and "cover_seeds" in names, names
+        check_sweep_vs_batch(eng, "wcover", rows_for=np.arange(0, eng.V, 7))
+    finally:
+        eng.close()
+
+
 def test_sweep_deep_unit_grid_does_not_raise():
     """Unit 100 x 100 grid: diameter 198, past derive's 123-level bound. AUTO
     must take another path and stay exact; sampled
