@@ -330,6 +330,55 @@ struct WDeriveArgs {
   uint32_t tiles, chunks;   // set by the launcher
 };
 hipError_t launch_wderive(const DevGraph& g, WDeriveArgs a, uint32_t kmax, hipStream_t s);
+
+// Weighted next hops of wide cover roots by runs (spf_wderive.hip
+// wnh_runs_kernel): runs of <= kWrRun consecutive roots with the same distinct
+// neighbours (a plane's spines); block = (run, 64-node tile), lane = node, a
+// wave per next-hop word: the word's 32 slot values of the lane's node are
+// loaded once (coalesced rows) and every root of the run compares them with
+// its own row and metrics.
+constexpr uint32_t kWrRun = 40;
+constexpr uint32_t kWrTile = 64;
+struct WRunsPlan {
+  uint32_t nruns, W, tiles;
+  const uint4* run;        // {first root, roots, slot offset, -}
+  const uint32_t* slots;   // [runs][32 W]: row in src | 0x80000000 | node (relays nothing) | ~0u
+  const uint32_t* wt;      // [roots][32 W] metric of the root's usable link per slot (~0u: none)
+  const uint32_t* own;     // [roots] row of the root in src
+  const uint32_t* rootid;  // [roots] node id
+  const uint32_t* src;
+  uint64_t pitch;
+  uint32_t* nh;            // [roots][V][W]
+  ospf_digest* digest;     // [roots] or null (zeroed by the launcher)
+  uint32_t nroots;
+};
+hipError_t launch_wnh_runs(const DevGraph& g, const WRunsPlan& p, hipStream_t s);
+
+// Weighted next hops of narrow cover roots (W <= 4) by hub rows
+// (spf_wderive.hip wnh_hub_kernel): the rows many roots read (a fabric's
+// spines) are staged per 64-node tile in LDS once per block, each group's own
+// rows (a pod's racks and fabric switches) per group; wave = root, lane =
+// node, the root's slot refs and metrics block-uniform (scalar loads).
+constexpr uint32_t kHubMax = 320;   // hub rows (80 KB of LDS per 64-node tile)
+constexpr uint32_t kHubLoc = 64;    // rows of a group
+constexpr uint32_t kHubGrpRoots = 16;
+constexpr uint32_t kHubTile = 64;
+struct HubPlan {
+  uint32_t nhub, ngroups, gchunk, tiles, tchunk, W, nroots;
+  const uint32_t* hub;     // [nhub] rows in src
+  const uint4* grp;        // [ngroups] {first root, roots, first local row, local rows}
+  const uint32_t* loc;     // group rows: row in src | 0x80000000 | node (relays nothing)
+  const uint32_t* ref;     // [roots][32 W] LDS row per slot: hub j, nhub + group row l, or
+                           // nhub + kHubLoc (unreached: an unusable slot)
+  const uint32_t* wt;      // [roots][32 W] metric per slot (~0u: unusable)
+  const uint32_t* ownl;    // [roots] LDS row of the root's own row (nhub + l)
+  const uint32_t* rootid;  // [roots]
+  const uint32_t* src;
+  uint64_t pitch;
+  uint32_t* nh;            // [roots][V][W]
+  ospf_digest* digest;     // [roots] or null (zeroed by the launcher)
+};
+hipError_t launch_wnh_hub(const DevGraph& g, const HubPlan& p, hipStream_t s);
 // cover roots (<= 128 distinct neighbours): next-hop words [n][V][W] (W <= 4)
 // + digests from the neighbours' rows and the root's own row (all in src)
 hipError_t launch_wderive_wide(const DevGraph& g, WDeriveArgs a, uint32_t W, hipStream_t s);

@@ -433,6 +433,184 @@ int wide_plan_build(ospf_ctx* c, const Facts& f, const std::vector<uint32_t>& ro
   return OSPF_OK;
 }
 
+// Host plan of the weighted run kernel (wnh_runs_kernel) for wide cover
+// roots (in order): runs of <= kWrRun roots with the same distinct
+// neighbours; per run its slot table over dist-row positions (padded to 32 W),
+// per root the smallest metric of its up links per slot.
+struct WRunsHost {
+  std::vector<uint4> run;
+  std::vector<uint32_t> slots, wt, own, rootid;
+};
+int wruns_build(ospf_ctx* c, const Facts& f, const std::vector<uint32_t>& roots, uint32_t W,
+                const std::vector<uint32_t>& pos, WRunsHost& h) {
+  const uint32_t n = (uint32_t)roots.size(), KW = 32u * W;
+  h = WRunsHost{};
+  h.wt.assign((size_t)n * KW, kNone);
+  auto same = [&](uint32_t a, uint32_t b) {
+    return f.nbrs(a) == f.nbrs(b) &&
+           std::equal(f.dn->begin() + (*f.dn_off)[a], f.dn->begin() + (*f.dn_off)[a + 1],
+                      f.dn->begin() + (*f.dn_off)[b]);
+  };
+  std::vector<uint32_t> first;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t r = roots[i];
+    if (pos[r] == kNone) return fail(c, OSPF_E_RANGE, "wruns plan: a root without a row");
+    h.own.push_back(pos[r]);
+    h.rootid.push_back(r);
+    const uint32_t* dn = f.dn->data() + (*f.dn_off)[r];
+    const uint32_t K = f.nbrs(r);
+    if (K > KW) return fail(c, OSPF_E_RANGE, "wruns plan: too many neighbours");
+    for (uint32_t e = c->h_prow[r]; e < c->h_prow[r + 1]; ++e) {
+      const uint32_t x = c->h_pcolx[e];
+      if ((x & 0x80000000u) || x == r) continue;
+      const uint32_t k = (uint32_t)(std::lower_bound(dn, dn + K, x) - dn);
+      uint32_t& m = h.wt[(size_t)i * KW + k];
+      m = std::min(m, c->h_pw[e]);
+    }
+    if (i == 0 || i - first.back() >= ospf::kWrRun || !same(roots[first.back()], r)) first.push_back(i);
+  }
+  first.push_back(n);
+  for (size_t q = 0; q + 1 < first.size(); ++q) {
+    const uint32_t r0 = roots[first[q]], K = f.nbrs(r0);
+    const uint32_t* dn = f.dn->data() + (*f.dn_off)[r0];
+    const uint32_t off = (uint32_t)h.slots.size();
+    for (uint32_t k = 0; k < KW; ++k) {
+      bool used = false;
+      for (uint32_t i = first[q]; i < first[q + 1] && k < K && !used; ++i)
+        used = h.wt[(size_t)i * KW + k] != kNone;
+      uint32_t v = kNone;
+      if (used) {
+        const uint32_t x = dn[k];
+        if ((c->h_nt[x >> 5] >> (x & 31)) & 1u) {
+          v = 0x80000000u | x;
+        } else {
+          v = pos[x];
+          if (v == kNone) return fail(c, OSPF_E_RANGE, "wruns plan: a neighbour without a row");
+        }
+      }
+      h.slots.push_back(v);
+    }
+    h.run.push_back(make_uint4(first[q], first[q + 1] - first[q], off, 0u));
+  }
+  return OSPF_OK;
+}
+
+// Host plan of the weighted hub kernel (wnh_hub_kernel) for narrow cover
+// roots (W <= 4, in order): hub rows = the transit neighbours most roots read
+// (>= 16 roots, at most kHubMax, most-read first); groups = runs of <= 16
+// consecutive roots whose own rows plus non-hub transit neighbours' rows
+// number <= kHubLoc. OSPF_E_RANGE when a root alone needs more group rows.
+struct HubHost {
+  std::vector<uint32_t> hub, loc, ref, wt, ownl, rootid;
+  std::vector<uint4> grp;
+};
+int hub_build(ospf_ctx* c, const Facts& f, const std::vector<uint32_t>& roots, uint32_t W,
+              const std::vector<uint32_t>& pos, HubHost& h) {
+  const uint32_t n = (uint32_t)roots.size(), KW = 32u * W, V = f.V;
+  h = HubHost{};
+  h.wt.assign((size_t)n * KW, kNone);
+  auto nt = [&](uint32_t x) { return (c->h_nt[x >> 5] >> (x & 31)) & 1u; };
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t r = roots[i];
+    const uint32_t* dn = f.dn->data() + (*f.dn_off)[r];
+    const uint32_t K = f.nbrs(r);
+    if (K > KW) return fail(c, OSPF_E_RANGE, "hub plan: too many neighbours");
+    for (uint32_t e = c->h_prow[r]; e < c->h_prow[r + 1]; ++e) {
+      const uint32_t x = c->h_pcolx[e];
+      if ((x & 0x80000000u) || x == r) continue;
+      const uint32_t k = (uint32_t)(std::lower_bound(dn, dn + K, x) - dn);
+      uint32_t& m = h.wt[(size_t)i * KW + k];
+      m = std::min(m, c->h_pw[e]);
+    }
+  }
+  std::vector<uint32_t> cnt(V, 0u);
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t r = roots[i];
+    const uint32_t* dn = f.dn->data() + (*f.dn_off)[r];
+    for (uint32_t k = 0; k < f.nbrs(r); ++k)
+      if (h.wt[(size_t)i * KW + k] != kNone && !nt(dn[k])) ++cnt[dn[k]];
+  }
+  std::vector<uint32_t> cand;
+  for (uint32_t v = 0; v < V; ++v)
+    if (cnt[v] >= 16u) cand.push_back(v);
+  std::stable_sort(cand.begin(), cand.end(), [&](uint32_t a, uint32_t b) { return cnt[a] > cnt[b]; });
+  if (cand.size() > ospf::kHubMax) cand.resize(ospf::kHubMax);
+  std::vector<uint32_t> hub_of(V, kNone);
+  for (uint32_t j = 0; j < cand.size(); ++j) {
+    hub_of[cand[j]] = j;
+    if (pos[cand[j]] == kNone) return fail(c, OSPF_E_RANGE, "hub plan: a neighbour without a row");
+    h.hub.push_back(pos[cand[j]]);
+  }
+  std::vector<uint32_t> locs;  // the open group's row nodes
+  auto need = [&](uint32_t i, std::vector<uint32_t>& out) {
+    const uint32_t r = roots[i];
+    const uint32_t* dn = f.dn->data() + (*f.dn_off)[r];
+    out.assign(1, r);
+    for (uint32_t k = 0; k < f.nbrs(r); ++k)
+      if (h.wt[(size_t)i * KW + k] != kNone && (nt(dn[k]) || hub_of[dn[k]] == kNone))
+        out.push_back(nt(dn[k]) && dn[k] != r ? (0x80000000u | dn[k]) : dn[k]);
+  };
+  auto close = [&](uint32_t first, uint32_t end) {
+    h.grp.push_back(make_uint4(first, end - first, (uint32_t)h.loc.size(), (uint32_t)locs.size()));
+    for (uint32_t x : locs) {
+      if (x & 0x80000000u) {
+        h.loc.push_back(x);
+        continue;
+      }
+      if (pos[x] == kNone) return false;
+      h.loc.push_back(pos[x]);
+    }
+    return true;
+  };
+  std::vector<uint32_t> nd;
+  uint32_t gfirst = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    need(i, nd);
+    std::vector<uint32_t> merged = locs;
+    for (uint32_t x : nd)
+      if (std::find(merged.begin(), merged.end(), x) == merged.end()) merged.push_back(x);
+    if (i > gfirst && (merged.size() > ospf::kHubLoc || i - gfirst >= ospf::kHubGrpRoots)) {
+      if (!close(gfirst, i)) return fail(c, OSPF_E_RANGE, "hub plan: a row is missing");
+      gfirst = i;
+      locs.clear();
+      merged.clear();
+      for (uint32_t x : nd)
+        if (std::find(merged.begin(), merged.end(), x) == merged.end()) merged.push_back(x);
+    }
+    if (merged.size() > ospf::kHubLoc) return fail(c, OSPF_E_RANGE, "hub plan: a root needs > 64 group rows");
+    locs = merged;
+  }
+  if (n && !close(gfirst, n)) return fail(c, OSPF_E_RANGE, "hub plan: a row is missing");
+  // slot refs and own rows per root
+  h.ref.assign((size_t)n * KW, kNone);
+  for (const uint4& gr : h.grp) {
+    const uint32_t* L = h.loc.data() + gr.z;
+    const uint32_t nhub = (uint32_t)h.hub.size();
+    for (uint32_t i = gr.x; i < gr.x + gr.y; ++i) {
+      const uint32_t r = roots[i];
+      const uint32_t* dn = f.dn->data() + (*f.dn_off)[r];
+      auto lidx = [&](uint32_t tag) {  // src row or 0x80000000 | node
+        for (uint32_t l = 0; l < gr.w; ++l)
+          if (L[l] == tag) return nhub + l;
+        return kNone;
+      };
+      h.ownl.push_back(lidx(pos[r]));
+      h.rootid.push_back(r);
+      for (uint32_t k = 0; k < KW; ++k) {
+        uint32_t& rf = h.ref[(size_t)i * KW + k];
+        rf = nhub + ospf::kHubLoc;  // the unreached row
+        if (k >= f.nbrs(r) || h.wt[(size_t)i * KW + k] == kNone) continue;
+        const uint32_t x = dn[k];
+        if (nt(x) && x != r) rf = lidx(0x80000000u | x);
+        else if (hub_of[x] != kNone) rf = hub_of[x];
+        else rf = lidx(pos[x]);
+        if (rf == kNone) return fail(c, OSPF_E_RANGE, "hub plan: a slot row is missing");
+      }
+    }
+  }
+  return OSPF_OK;
+}
+
 // DERIVE (spf_levels.hip, spf_twin.hip, spf_leaf.hip, spf_msbfs.hip derive
 // kernels), unit metric / hop count. The part's roots split into leaves (an
 // independent set of nodes with <= 32 distinct neighbours: a fabric's racks)
@@ -1376,6 +1554,76 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     u.fn = [=](hipStream_t strm) {
       return ospf_wderive_wide_dev(c, d_roots, n, 0, W, slab, V, d_pos, nh, dg, strm);
     };
+    HubHost hh;
+    if (W <= 4 && getenv("OSPF_WNH_HUB") && hub_build(c, f, roots, W, pos, hh) == OSPF_OK) {
+      uint4* d_grp;
+      uint32_t *d_hub, *d_loc, *d_ref, *d_wt, *d_ownl, *d_rid;
+      if ((rc = upload(s, &d_grp, hh.grp)) || (rc = upload(s, &d_hub, hh.hub.empty() ? std::vector<uint32_t>{0u} : hh.hub)) ||
+          (rc = upload(s, &d_loc, hh.loc)) || (rc = upload(s, &d_ref, hh.ref)) ||
+          (rc = upload(s, &d_wt, hh.wt)) || (rc = upload(s, &d_ownl, hh.ownl)) ||
+          (rc = upload(s, &d_rid, hh.rootid)))
+        return rc;
+      ospf::HubPlan hp{};
+      hp.nhub = (uint32_t)hh.hub.size();
+      hp.ngroups = (uint32_t)hh.grp.size();
+      hp.tiles = (V + ospf::kHubTile - 1) / ospf::kHubTile;
+      hp.tchunk = std::min<uint32_t>(8u, hp.tiles);
+      // groups per block: <= 32 (512 roots), fewer while the grid is small
+      hp.gchunk = 32u;
+      while (hp.gchunk > 1u &&
+             ((hp.ngroups + hp.gchunk - 1) / hp.gchunk) * ((hp.tiles + hp.tchunk - 1) / hp.tchunk) <
+                 8u * (uint32_t)c->n_cu)
+        hp.gchunk /= 2u;
+      hp.W = W;
+      hp.nroots = n;
+      hp.hub = d_hub;
+      hp.grp = d_grp;
+      hp.loc = d_loc;
+      hp.ref = d_ref;
+      hp.wt = d_wt;
+      hp.ownl = d_ownl;
+      hp.rootid = d_rid;
+      hp.src = slab;
+      hp.pitch = V;
+      hp.nh = nh;
+      hp.digest = dg;
+      u.kernel = "wnh_hub_kernel<" + std::to_string(W) + "> (hub rows per tile in LDS, a group's "
+                 "rows per group, wave = root, lane = node)";
+      u.fn = [=](hipStream_t strm) {
+        const hipError_t e = ospf::launch_wnh_hub(c->g, hp, strm);
+        return e == hipSuccess ? OSPF_OK : ospf_int::hip_fail(c, e, "launch_wnh_hub");
+      };
+    }
+    if (W > 4 && getenv("OSPF_WNH_RUNS")) {  // runs of roots with one neighbour list
+      WRunsHost wh;
+      if ((rc = wruns_build(c, f, roots, W, pos, wh))) return rc;
+      uint4* d_run;
+      uint32_t *d_sl, *d_wt, *d_own, *d_rid;
+      if ((rc = upload(s, &d_run, wh.run)) || (rc = upload(s, &d_sl, wh.slots)) ||
+          (rc = upload(s, &d_wt, wh.wt)) || (rc = upload(s, &d_own, wh.own)) ||
+          (rc = upload(s, &d_rid, wh.rootid)))
+        return rc;
+      ospf::WRunsPlan wp{};
+      wp.nruns = (uint32_t)wh.run.size();
+      wp.nroots = n;
+      wp.W = W;
+      wp.tiles = (V + ospf::kWrTile - 1) / ospf::kWrTile;
+      wp.run = d_run;
+      wp.slots = d_sl;
+      wp.wt = d_wt;
+      wp.own = d_own;
+      wp.rootid = d_rid;
+      wp.src = slab;
+      wp.pitch = V;
+      wp.nh = nh;
+      wp.digest = dg;
+      u.kernel = "wnh_runs_kernel (runs of roots with one neighbour list, lane = node, a wave "
+                 "per next-hop word)";
+      u.fn = [=](hipStream_t strm) {
+        const hipError_t e = ospf::launch_wnh_runs(c->g, wp, strm);
+        return e == hipSuccess ? OSPF_OK : ospf_int::hip_fail(c, e, "launch_wnh_runs");
+      };
+    }
     s->step_comp += u.comp;
     bool reads_leaf = false;  // a neighbour's row comes from (B)
     for (uint32_t r : roots)

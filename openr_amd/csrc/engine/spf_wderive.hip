@@ -647,7 +647,241 @@ __global__ void __launch_bounds__(256) wderive_lanes_kernel(DevGraph g, WDeriveA
   }
 }
 
+__global__ void __launch_bounds__(256) wnh_runs_kernel(DevGraph g, WRunsPlan p) {
+  __shared__ uint32_t s_R[kWrRun][kWrTile];
+  __shared__ unsigned long long s_h[kWrRun], s_sum[kWrRun];
+  __shared__ uint32_t s_reach[kWrRun];
+  const uint32_t V = g.V, W = p.W, tid = threadIdx.x, lane = tid & 63u;
+  // wave-uniform (scalar loads of the slot and metric tables)
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t b = blockIdx.x, nb = gridDim.x, full = nb / 8u * 8u;
+  const uint32_t item = b < full ? (b % 8u) * (full / 8u) + b / 8u : b;
+  const uint32_t ri = item % p.nruns, tile = item / p.nruns;
+  const uint4 rn = p.run[ri];
+  const uint32_t nr = rn.y, v0 = tile * kWrTile, v = v0 + lane;
+  if (tid < nr) {
+    s_h[tid] = 0ull;
+    s_sum[tid] = 0ull;
+    s_reach[tid] = 0u;
+  }
+  __syncthreads();
+  for (uint32_t x = tid; x < nr * kWrTile; x += 256u) {
+    const uint32_t j = x / kWrTile, vv = v0 + (x % kWrTile);
+    const uint32_t R = vv < V ? p.src[(size_t)p.own[rn.x + j] * p.pitch + vv] : kInf;
+    s_R[j][x % kWrTile] = R;
+    if (p.digest && R != kInf) {
+      atomicAdd(&s_reach[j], 1u);
+      atomicAdd(&s_sum[j], (unsigned long long)R);
+      atomicAdd(&s_h[j], (unsigned long long)(g.dkey[2ull * vv] * ((uint64_t)R + 1ull)));
+    }
+  }
+  __syncthreads();
+  const uint64_t nkey = (p.digest && v < V) ? g.dkey[2ull * v + 1] : 0ull;
+  for (uint32_t w = wave; w < W; w += 4u) {
+    const uint32_t slv = lane < 32u ? p.slots[rn.z + 32u * w + lane] : kInf;
+    uint32_t D[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const uint32_t sv = (uint32_t)__builtin_amdgcn_readlane((int)slv, i);
+      if (sv < kNt) D[i] = v < V ? p.src[(size_t)sv * p.pitch + v] : kInf;
+      else D[i] = (sv != kInf && v == (sv & ~kNt)) ? 0u : kInf;
+    }
+    const uint32_t* wrow = p.wt + (size_t)rn.x * 32u * W + 32u * w + lane;
+    uint32_t wnext = lane < 32u ? wrow[0] : 0u;  // root j + 1's metrics load while j computes
+    for (uint32_t j = 0; j < nr; ++j) {
+      const uint32_t R = s_R[j][lane];
+      const uint32_t wtv = wnext;
+      if (j + 1u < nr) wnext = lane < 32u ? wrow[(size_t)(j + 1u) * 32u * W] : 0u;
+      uint32_t word = 0u;
+#pragma unroll
+      for (int i = 0; i < 32; ++i) {  // w + D == R without overflow: R >= D, R - D == w
+        const uint32_t wk = (uint32_t)__builtin_amdgcn_readlane((int)wtv, i);
+        word |= (R >= D[i] && R - D[i] == wk ? 1u : 0u) << i;
+      }
+      if (R == kInf || v == p.rootid[rn.x + j]) word = 0u;
+      if (v < V) __builtin_nontemporal_store(word, p.nh + ((size_t)(rn.x + j) * V + v) * W + w);
+      if (p.digest && __ballot(word != 0u)) {
+        uint64_t h = word ? nkey * digest_word_key(w, word) : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) h += shfl_xor64(h, o);
+        if (lane == 0) atomicAdd(&s_h[j], (unsigned long long)h);
+      }
+    }
+  }
+  if (p.digest) {
+    __syncthreads();
+    if (tid < nr && s_reach[tid]) {
+      ospf_digest* dg = p.digest + rn.x + tid;
+      atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)s_reach[tid]);
+      atomicAdd((unsigned long long*)&dg->sum_dist, s_sum[tid]);
+      atomicAdd((unsigned long long*)&dg->hash, s_h[tid]);
+    } else if (tid < nr && s_h[tid]) {
+      atomicAdd((unsigned long long*)&p.digest[rn.x + tid].hash, s_h[tid]);
+    }
+  }
+}
+
+// Block = (chunk of tchunk 64-node tiles, chunk of gchunk groups), 512
+// threads; blocks of one tile chunk are spread over the XCDs in order, so the
+// hub rows of a tile are read from one XCD's L2 by its resident blocks. One
+// LDS row array: the hub rows, the group's rows (an overloaded neighbour's
+// row is 0 at itself only), one unreached row -- every slot a single LDS read,
+// no branch on the slot kind.
+template <int W>
+__global__ void __launch_bounds__(512) wnh_hub_kernel(DevGraph g, HubPlan p) {
+  extern __shared__ uint32_t s_rows[];  // [nhub + kHubLoc + 1][64]
+  __shared__ unsigned long long s_h[512], s_sum[512];
+  __shared__ uint32_t s_reach[512];
+  const uint32_t V = g.V, tid = threadIdx.x, lane = tid & 63u;
+  // wave-uniform: a root's slot table and metrics by scalar loads
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t b = blockIdx.x, nb = gridDim.x, full = nb / 8u * 8u;
+  const uint32_t item = b < full ? (b % 8u) * (full / 8u) + b / 8u : b;
+  const uint32_t ngc = (p.ngroups + p.gchunk - 1) / p.gchunk;
+  const uint32_t tc = item / ngc, gc = item % ngc;
+  const uint32_t g0 = gc * p.gchunk, g1 = min(p.ngroups, g0 + p.gchunk);
+  const uint32_t r0 = p.grp[g0].x;
+  const uint32_t nrb = p.grp[g1 - 1].x + p.grp[g1 - 1].y - r0;  // roots of the block (<= 512)
+  uint32_t* s_loc = s_rows + (size_t)p.nhub * kHubTile;
+  for (uint32_t x = tid; x < nrb; x += 512u) {
+    s_h[x] = 0ull;
+    s_sum[x] = 0ull;
+    s_reach[x] = 0u;
+  }
+  if (tid < kHubTile) s_loc[kHubLoc * kHubTile + tid] = kInf;  // the unreached row
+  const uint32_t t0 = tc * p.tchunk, t1 = min(p.tiles, t0 + p.tchunk);
+  for (uint32_t t = t0; t < t1; ++t) {
+    const uint32_t v0 = t * kHubTile, v = v0 + lane;
+    __syncthreads();  // the previous tile's hub rows are consumed
+    for (uint32_t x = tid; x < p.nhub * kHubTile; x += 512u) {
+      const uint32_t vv = v0 + (x % kHubTile);
+      s_rows[x] = vv < V ? p.src[(size_t)p.hub[x / kHubTile] * p.pitch + vv] : kInf;
+    }
+    const uint64_t dk0 = v < V ? g.dkey[2ull * v] : 0ull, dk1 = v < V ? g.dkey[2ull * v + 1] : 0ull;
+    for (uint32_t gi = g0; gi < g1; ++gi) {
+      const uint4 gr = p.grp[gi];
+      __syncthreads();  // the previous group's rows are consumed (and the hub staged)
+      for (uint32_t x = tid; x < gr.w * kHubTile; x += 512u) {
+        const uint32_t vv = v0 + (x % kHubTile), lr = p.loc[gr.z + x / kHubTile];
+        uint32_t d = kInf;
+        if (lr < kNt) d = vv < V ? p.src[(size_t)lr * p.pitch + vv] : kInf;
+        else if (vv == (lr & ~kNt)) d = 0u;
+        s_loc[x] = d;
+      }
+      __syncthreads();
+      for (uint32_t j = wave; j < gr.y; j += 8u) {
+        const uint32_t ri = gr.x + j;
+        const uint32_t R = s_rows[p.ownl[ri] * kHubTile + lane];
+        const uint32_t* rf = p.ref + (size_t)ri * 32u * W;
+        const uint32_t* wt = p.wt + (size_t)ri * 32u * W;
+        uint32_t word[W], rvs[W], wvs[W];
+        // the words' 32 slot refs / metrics: coalesced loads, all in flight,
+        // then read lane by lane into scalar registers
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          rvs[w] = lane < 32u ? rf[32 * w + lane] : 0u;
+          wvs[w] = lane < 32u ? wt[32 * w + lane] : 0u;
+        }
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          const uint32_t rv = rvs[w], wv = wvs[w];
+          uint32_t x = 0u;
+#pragma unroll
+          for (int i = 0; i < 32; ++i) {
+            const uint32_t ri_ = (uint32_t)__builtin_amdgcn_readlane((int)rv, i);
+            const uint32_t wk = (uint32_t)__builtin_amdgcn_readlane((int)wv, i);
+            const uint32_t D = s_rows[ri_ * kHubTile + lane];
+            x |= (R >= D && R - D == wk ? 1u : 0u) << i;
+          }
+          word[w] = x;
+        }
+        if (R == kInf || v == p.rootid[ri]) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) word[w] = 0u;
+        }
+        if (v < V) {
+          uint32_t* dst = p.nh + ((size_t)ri * V + v) * W;
+#pragma unroll
+          for (int w = 0; w < W; ++w) __builtin_nontemporal_store(word[w], dst + w);
+        }
+        if (p.digest) {
+          uint64_t h = 0ull, sum = 0ull;
+          uint32_t reach = 0u;
+          if (v < V && R != kInf) {
+            reach = 1u;
+            sum = R;
+            h = dk0 * ((uint64_t)R + 1ull);
+            uint64_t ws = 0ull;
+#pragma unroll
+            for (int w = 0; w < W; ++w)
+              if (word[w]) ws += digest_word_key((uint32_t)w, word[w]);
+            h += dk1 * ws;
+          }
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) {
+            h += shfl_xor64(h, o);
+            sum += shfl_xor64(sum, o);
+            reach += __shfl_xor(reach, o, kWave);
+          }
+          if (lane == 0 && reach) {
+            s_h[ri - r0] += h;  // one wave per root at a time
+            s_sum[ri - r0] += sum;
+            s_reach[ri - r0] += reach;
+          }
+        }
+      }
+    }
+  }
+  if (p.digest) {
+    __syncthreads();
+    for (uint32_t x = tid; x < nrb; x += 512u) {
+      if (!s_reach[x]) continue;
+      ospf_digest* dg = p.digest + r0 + x;
+      atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)s_reach[x]);
+      atomicAdd((unsigned long long*)&dg->sum_dist, s_sum[x]);
+      atomicAdd((unsigned long long*)&dg->hash, s_h[x]);
+    }
+  }
+}
+
 }  // namespace
+
+hipError_t launch_wnh_hub(const DevGraph& g, const HubPlan& p, hipStream_t s) {
+  if (p.ngroups == 0) return hipSuccess;
+  if (p.nhub > kHubMax || p.W == 0 || p.W > 4) return hipErrorInvalidValue;
+  if (p.digest) {
+    const hipError_t e = hipMemsetAsync(p.digest, 0, (size_t)p.nroots * sizeof(ospf_digest), s);
+    if (e != hipSuccess) return e;
+  }
+  const size_t lds = (size_t)(p.nhub + kHubLoc + 1u) * kHubTile * 4u;
+  const uint32_t ngc = (p.ngroups + p.gchunk - 1) / p.gchunk;
+  const dim3 grid(ngc * ((p.tiles + p.tchunk - 1) / p.tchunk));
+  const void* fn = p.W == 1 ? (const void*)wnh_hub_kernel<1>
+                 : p.W == 2 ? (const void*)wnh_hub_kernel<2>
+                 : p.W == 3 ? (const void*)wnh_hub_kernel<3>
+                            : (const void*)wnh_hub_kernel<4>;
+  if (lds > 48 * 1024) {
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  switch (p.W) {
+    case 1: hipLaunchKernelGGL(wnh_hub_kernel<1>, grid, dim3(512), lds, s, g, p); break;
+    case 2: hipLaunchKernelGGL(wnh_hub_kernel<2>, grid, dim3(512), lds, s, g, p); break;
+    case 3: hipLaunchKernelGGL(wnh_hub_kernel<3>, grid, dim3(512), lds, s, g, p); break;
+    default: hipLaunchKernelGGL(wnh_hub_kernel<4>, grid, dim3(512), lds, s, g, p); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_wnh_runs(const DevGraph& g, const WRunsPlan& p, hipStream_t s) {
+  if (p.nruns == 0) return hipSuccess;
+  if (p.digest) {
+    const hipError_t e = hipMemsetAsync(p.digest, 0, (size_t)p.nroots * sizeof(ospf_digest), s);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(wnh_runs_kernel, dim3(p.nruns * p.tiles), dim3(256), 0, s, g, p);
+  return hipGetLastError();
+}
 
 hipError_t launch_wderive(const DevGraph& g, WDeriveArgs a, uint32_t kmax, hipStream_t s) {
   if (a.n == 0) return hipSuccess;

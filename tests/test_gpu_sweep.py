@@ -154,6 +154,34 @@ def test_sweep_weighted_fabric_closure(drain):
         eng.close()
 
 
+@pytest.mark.parametrize("opt_in", [False, True])
+@pytest.mark.parametrize("drain", [0.0, 0.05])
+def test_sweep_weighted_wide_cover_roots_runs(drain, opt_in, monkeypatch):
+    """Spines with > 128 neighbours (W = 5 next-hop words) on the weighted
+    cover path == the batch path bit for bit, with drained switches and down
+    links: by the default kernels, and by the opt-in wnh_runs_kernel (runs of
+    a plane's spines, lane = node, a wave per word) + wnh_hub_kernel (hub rows
+    in LDS per tile) -- OSPF_WNH_RUNS / OSPF_WNH_HUB."""
+    if opt_in:
+        monkeypatch.setenv("OSPF_WNH_RUNS", "1")
+        monkeypatch.setenv("OSPF_WNH_HUB", "1")
+    st = drained_fabric(130, 2, seed=9, drain=drain, down=0.02 if drain else 0.0,
+                        weighted_seed=3, ssw_per_plane=4)
+    _, _, eng = engine_for(st)
+    try:
+        sw = Sweep(eng, mode="wcover")
+        prof = sw.profile(1)
+        sw.close()
+        wide = [p for p in prof if p["name"].startswith("wderive_wide_w")]
+        assert any(int(p["name"].rsplit("w", 1)[1]) > 4 for p in wide), [p["name"] for p in prof]
+        if opt_in:
+            kern = " ".join(p.get("kernel", "") for p in wide)
+            assert "wnh_runs_kernel" in kern and "wnh_hub_kernel" in kern, kern
+        check_sweep_vs_batch(eng, "wcover", rows_for=np.arange(0, eng.V, 13))
+    finally:
+        eng.close()
+
+
 def test_sweep_deep_unit_grid_does_not_raise():
     """Unit 100 x 100 grid: diameter 198, past derive's 123-level bound. AUTO
     must take another path and stay exact; sampled
