@@ -379,7 +379,10 @@ __global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C
     if (a.dcomp) {  // the cover columns as a seed of the closure
       const bool tr = (s_tr[r >> 5] >> (r & 31u)) & 1u;
       uint32_t* dst = a.dcomp + (size_t)i * nS;
-      for (uint32_t x = tid; x < nS; x += kBlock) dst[x] = tr ? s_D[x] : (x == r ? 0u : kInf);
+      for (uint32_t x = tid; x < nS; x += kBlock) {
+        const uint32_t d = tr ? s_D[x] : (x == r ? 0u : kInf);
+        dst[x] = d == kInf ? kClInf : d;
+      }
     }
     const uint32_t rp = a.rowpos ? a.rowpos[i] : i;
     if (rp != kInf) write_row(g, C, a.dist + (size_t)rp * V, s_D, s_tr, r, tid, kBlock);
@@ -393,10 +396,6 @@ __global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C
 // block-uniform (scalar loads). Blocks are ordered column-chunk-major and
 // spread so that one XCD's resident blocks share a chunk of the seed rows in
 // its L2.
-__device__ __forceinline__ uint32_t sat_add32(uint32_t c, uint32_t x) {
-  const uint32_t s = c + x;
-  return (x == kInf || c == kInf || s < c) ? kInf : s;
-}
 template <int KW>
 __global__ void __launch_bounds__(256) closure_kernel(ClosurePlan p) {
   const uint32_t nb = gridDim.x, b = blockIdx.x;
@@ -408,7 +407,7 @@ __global__ void __launch_bounds__(256) closure_kernel(ClosurePlan p) {
   const uint2 cm = p.comp[ci];
   uint32_t acc[KW];
 #pragma unroll
-  for (int f = 0; f < KW; ++f) acc[f] = kInf;
+  for (int f = 0; f < KW; ++f) acc[f] = kClInf;
   const uint32_t* cst = p.cst + (size_t)cm.x * KW;
   const uint32_t* jl = p.jl + cm.x;
   for (uint32_t j0 = 0; j0 < cm.y; j0 += 8u) {
@@ -416,14 +415,14 @@ __global__ void __launch_bounds__(256) closure_kernel(ClosurePlan p) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const uint32_t j = j0 + (uint32_t)u;
-      x[u] = (ok && j < cm.y) ? p.seedC[(size_t)jl[j] * p.nS + v] : kInf;
+      x[u] = (ok && j < cm.y) ? p.seedC[(size_t)jl[j] * p.nS + v] : kClInf;
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const uint32_t j = j0 + (uint32_t)u;
       if (j >= cm.y) break;  // uniform
 #pragma unroll
-      for (int f = 0; f < KW; ++f) acc[f] = min(acc[f], sat_add32(cst[j * KW + f], x[u]));
+      for (int f = 0; f < KW; ++f) acc[f] = min(acc[f], cst[j * KW + f] + x[u]);  // < 2^31: no wrap
     }
   }
   const uint32_t* mem = p.mem + (size_t)ci * KW;
@@ -436,9 +435,8 @@ __global__ void __launch_bounds__(256) closure_kernel(ClosurePlan p) {
   const uint32_t* out = p.out + (size_t)ci * KW;
 #pragma unroll
   for (int f = 0; f < KW; ++f)
-    if (ok && out[f] != kInf) p.dc[(size_t)out[f] * p.nS + v] = acc[f];
+    if (ok && out[f] != kInf) p.dc[(size_t)out[f] * p.nS + v] = acc[f] >= kClInf ? kInf : acc[f];
 }
-
 }  // namespace
 
 hipError_t launch_closure(const ClosurePlan& p, uint32_t KW, hipStream_t s) {

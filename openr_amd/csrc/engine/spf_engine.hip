@@ -842,6 +842,7 @@ int closure_build(ospf_ctx* c, const std::vector<uint32_t>& roots,
   constexpr uint32_t kN = ~0u;
   const uint32_t nS = (uint32_t)c->h_ccv.size();
   if (c->cl_seed.empty()) return fail(c, OSPF_E_INVAL, "closure: no seed split of the cover");
+  if (c->dist_bound >= ospf::kClInf) return fail(c, OSPF_E_RANGE, "closure: distances may reach 2^30");
   std::vector<uint32_t> cidx(c->info.n_nodes, kN);
   for (uint32_t i = 0; i < nS; ++i) cidx[c->h_ccv[i]] = i;
   const uint32_t ncomp_all = (uint32_t)c->cl_comp_off.size() - 1;
@@ -913,7 +914,7 @@ int closure_build(ospf_ctx* c, const std::vector<uint32_t>& roots,
         if (!ch) break;
       }
       for (uint32_t m = 0; m < kk; ++m)
-        h.dloc[((size_t)q * KW + f) * KW + m] = d[m] >= 0xFFFFFFFFull ? kN : (uint32_t)d[m];
+        h.dloc[((size_t)q * KW + f) * KW + m] = d[m] >= ospf::kClInf ? ospf::kClInf : (uint32_t)d[m];
       for (uint32_t g = 0; g < kk; ++g) {
         if (d[g] == UINT64_MAX || (g != f && !transit(M[g]))) continue;
         for (uint32_t e = crow[M[g]]; e < crow[M[g] + 1]; ++e) {
@@ -923,12 +924,12 @@ int closure_build(ospf_ctx* c, const std::vector<uint32_t>& roots,
             if (seed_row[x] == kN) return fail(c, OSPF_E_INVAL, "closure: a seed row is missing");
             jof[x] = (uint32_t)h.jl.size() - joff;
             h.jl.push_back(seed_row[x]);
-            h.cst.resize(h.jl.size() * KW, kN);
+            h.cst.resize(h.jl.size() * KW, ospf::kClInf);
             used.push_back(x);
           }
           const uint64_t cc = d[g] + ced[e].y;
           uint32_t& dst = h.cst[(size_t)(joff + jof[x]) * KW + f];
-          if (cc < dst) dst = (uint32_t)cc;
+          if (cc < dst) dst = (uint32_t)cc;  // (dst <= kClInf)
         }
       }
     }
@@ -937,7 +938,7 @@ int closure_build(ospf_ctx* c, const std::vector<uint32_t>& roots,
   }
   if (h.jl.empty()) {  // no seed terms at all: one unused row keeps the arrays non-empty
     h.jl.push_back(0);
-    h.cst.assign(KW, kN);
+    h.cst.assign(KW, ospf::kClInf);
   }
   return OSPF_OK;
 }
@@ -1842,6 +1843,15 @@ int ospf_wderive_wide_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint
                           uint32_t nh_words, const uint32_t* d_src, uint64_t src_pitch,
                           const uint32_t* d_pos, uint32_t* d_nh, ospf_digest* d_digest,
                           void* stream) {
+  return ospf_int::wderive_wide(c, d_roots, n, flags, nh_words, d_src, src_pitch, d_pos, d_nh,
+                                d_digest, stream, 0u);
+}
+}  // extern "C"
+
+int ospf_int::wderive_wide(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t flags,
+                           uint32_t nh_words, const uint32_t* d_src, uint64_t src_pitch,
+                           const uint32_t* d_pos, uint32_t* d_nh, ospf_digest* d_digest,
+                           void* stream, uint32_t ctiles) {
   if (!c) return OSPF_E_INVAL;
   if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
   if (n == 0) return OSPF_OK;
@@ -1869,11 +1879,16 @@ int ospf_wderive_wide_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint
   a.err = c->d_err;
   const uintptr_t al = (uintptr_t)d_src | (uintptr_t)d_nh;
   a.vec = (V % 4u == 0 && src_pitch % 4u == 0 && (al & 15u) == 0) ? 1u : 0u;
+  a.ctiles = ctiles;
   if (const char* e = getenv("OSPF_WD_CTILES")) a.ctiles = (uint32_t)std::max(1, atoi(e));
+  if (const char* e = getenv(nh_words > 4 ? "OSPF_WL_CTILES" : "OSPF_WW_CTILES"))
+    a.ctiles = (uint32_t)std::max(1, atoi(e));
+  if (const char* e = getenv("OSPF_WD_G")) a.G = (uint32_t)std::max(1, atoi(e));
   hipError_t e = ospf::launch_wderive_wide(c->g, a, nh_words, s);
   if (e != hipSuccess) return hip_fail(c, e, "launch_wderive_wide");
   return OSPF_OK;
 }
+extern "C" {
 
 // ---------------------------------------------------------------- cover SPF
 // Contracted graph for ospf_cover_dist_dev (spf_cover.hip), built on the host

@@ -118,6 +118,14 @@ struct ClosureHost {
 int closure_build(ospf_ctx* c, const std::vector<uint32_t>& roots,
                   const std::vector<uint32_t>& seed_row, ClosureHost& h);
 
+// ospf_wderive_wide_dev with a chunk size (256-node tiles per block; 0: the
+// launcher's default) -- the sweep's wide cover roots run beside the leaves
+// with larger chunks (fewer blocks, so the leaves keep most of the GPU)
+int wderive_wide(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t flags,
+                 uint32_t nh_words, const uint32_t* d_src, uint64_t src_pitch,
+                 const uint32_t* d_pos, uint32_t* d_nh, ospf_digest* d_digest, void* stream,
+                 uint32_t ctiles);
+
 }  // namespace ospf_int
 
 #define HIPCHK(ctx, call)                                            \

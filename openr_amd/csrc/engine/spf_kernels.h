@@ -282,8 +282,8 @@ struct CoverArgs {
   uint32_t* dist;         // [n][V] (row i), or row rowpos[i] when rowpos is set
   uint32_t* err;          // bit 64: a root outside the cover
   const uint32_t* rowpos = nullptr;  // [n] row of root i in dist (0xFFFFFFFF: none)
-  uint32_t* dcomp = nullptr;         // [n][nS] cover columns out (a non-transit root:
-                                     // 0 at itself, unreached elsewhere -- it relays nothing)
+  uint32_t* dcomp = nullptr;         // [n][nS] cover columns out, unreached = kClInf (a
+                                     // non-transit root: 0 at itself only -- it relays nothing)
   const uint32_t* dload = nullptr;   // [n][nS] cover columns given: no Dial, rows only
 };
 hipError_t launch_cover_spf(const DevGraph& g, const CoverGraph& C, const CoverArgs& a,
@@ -295,16 +295,20 @@ hipError_t launch_cover_spf(const DevGraph& g, const CoverGraph& C, const CoverA
 //                        min over seeds s of cst_f(s) + D_s(v) ),
 // cst_f(s) = min over members g usable from f of dloc_f(g) + w(g -> s).
 constexpr uint32_t kClosureMaxK = 16;
+// unreached in the closure's seed columns, constants and local distances:
+// 2^30 (the closure runs when every distance is below it), so a sum of two
+// never wraps and any sum with an unreached part stays >= 2^30
+constexpr uint32_t kClInf = 0x40000000u;
 struct ClosurePlan {
   uint32_t ncomp, nS, chunks;
   const uint2* comp;       // [ncomp] {first seed term, seed terms}
   const uint32_t* jl;      // [terms] seed row in seedC
-  const uint32_t* cst;     // [terms][KW] constants per member (unreached: 0xFFFFFFFF)
+  const uint32_t* cst;     // [terms][KW] constants per member (unreached: kClInf)
   const uint32_t* mem;     // [ncomp][KW] member cover index (0xFFFFFFFF: none)
-  const uint32_t* dloc;    // [ncomp][KW][KW] member f -> member m
+  const uint32_t* dloc;    // [ncomp][KW][KW] member f -> member m (unreached: kClInf)
   const uint32_t* out;     // [ncomp][KW] dc row of member f (0xFFFFFFFF: not needed)
-  const uint32_t* seedC;   // [seeds][nS]
-  uint32_t* dc;            // [rows][nS]
+  const uint32_t* seedC;   // [seeds][nS] (unreached: kClInf)
+  uint32_t* dc;            // [rows][nS] (unreached: 0xFFFFFFFF)
 };
 hipError_t launch_closure(const ClosurePlan& p, uint32_t KW, hipStream_t s);
 
