@@ -361,17 +361,18 @@ __global__ void __launch_bounds__(256) wderive_wide_kernel(DevGraph g, WDeriveAr
         for (int kk = 0; kk < 8; ++kk) {
 #pragma unroll
           for (int b = 0; b < 4; ++b) {
-            const uint32_t c = sat_add(wk[kk], D[kk][b]);
-            word[w][b] |= (c == R[b] && R[b] != kInf ? 1u : 0u) << (k8 + kk);
+            // w + D == R without the saturating add: R >= D and R - D == w
+            // (an unreached R clears the words below)
+            word[w][b] |= (R[b] >= D[kk][b] && R[b] - D[kk][b] == wk[kk] ? 1u : 0u) << (k8 + kk);
           }
         }
       }
     }
 #pragma unroll
     for (int b = 0; b < 4; ++b)
-      if (v0 + b == r)
+      if (v0 + b == r || R[b] == kInf)
 #pragma unroll
-        for (int w = 0; w < W; ++w) word[w][b] = 0u;  // the root: no next hops
+        for (int w = 0; w < W; ++w) word[w][b] = 0u;  // the root / unreached: no next hops
     // stage [node][word] and store whole 1-KB pieces of the row
 #pragma unroll
     for (int b = 0; b < 4; ++b)
@@ -597,9 +598,11 @@ __global__ void __launch_bounds__(256) wderive_lanes_kernel(DevGraph g, WDeriveA
             const uint32_t k = 32u * lane + i;
             const uint32_t wk = (lane < W && k < K) ? (uint32_t)s_w[j][i * 64u + lane] : 0xFFFFu;
             const uint32_t wv = wk == 0xFFFFu ? kInf : wk;
-            w0 |= (sat_add(wv, D0[i]) == R0 && R0 != kInf ? 1u : 0u) << i;
-            w1 |= (sat_add(wv, D1[i]) == R1 && R1 != kInf ? 1u : 0u) << i;
+            w0 |= (R0 >= D0[i] && R0 - D0[i] == wv ? 1u : 0u) << i;
+            w1 |= (R1 >= D1[i] && R1 - D1[i] == wv ? 1u : 0u) << i;
           }
+          if (R0 == kInf) w0 = 0u;
+          if (R1 == kInf) w1 = 0u;
           const uint32_t r = s_root[j];
           if (vc == r) w0 = 0u;
           if (vc + 1u == r) w1 = 0u;

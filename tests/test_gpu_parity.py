@@ -945,3 +945,32 @@ def test_ksp2_ignore_set_above_run_list_cap():
     q = LinkState()
     q.apply(stream)
     assert q.ksp2_text("s", ["d", "a"]) == o.ksp2_text("s", ["d", "a"])
+
+
+def test_ksp2_ignore_overflow_repeated_keeps_metric_runs():
+    """ADVICE r02 (link_state.cpp KSP2 path): a k = 2 run whose ignore set
+    overflows one run's list masks those links on the device and restores them
+    (ospf_links_mask / unmask) -- repeated calls must not ratchet the engine's
+    distance bound: with metrics of 100,000 twelve calls would push a bound
+    that grew by every restored link past 2^32, and later link-metric runs
+    would fail. Every call and the runs after it equal the oracle."""
+    n_mid, M = 1100, 100000
+    dbs = {"s": [], "d": [], "a": [], "b": []}
+    for i in range(n_mid):
+        m = f"m{i:04d}"
+        dbs[m] = [create_adjacency("s", f"{m}/s", f"s/{m}", M),
+                  create_adjacency("d", f"{m}/d", f"d/{m}", M)]
+        dbs["s"].append(create_adjacency(m, f"s/{m}", f"{m}/s", M))
+        dbs["d"].append(create_adjacency(m, f"d/{m}", f"{m}/d", M))
+    for x, y in (("s", "a"), ("a", "b"), ("b", "d")):
+        dbs[x].append(create_adjacency(y, f"{x}/{y}", f"{y}/{x}", M))
+        dbs[y].append(create_adjacency(x, f"{y}/{x}", f"{x}/{y}", M))
+    stream = AdjDbStream.from_dbs(AdjDb(n, a, i + 1) for i, (n, a) in enumerate(dbs.items()))
+    o, p = Oracle(), LinkState()
+    assert o.apply(stream) == p.apply(stream)
+    want2 = o.kth_paths("s", "d", 2)
+    assert len(want2) == 1 and len(want2[0]) == 3
+    for _ in range(12):
+        assert p.kth_paths("s", "d", 2) == want2
+    for root in ("s", "d", "a", "m0007"):
+        assert p.spf(root) == parse_spf_text(o.spf_text(root, True)), root
