@@ -260,6 +260,34 @@ def test_sweep_partition_parts_cover_every_root_once(mode):
         eng.close()
 
 
+def test_sweep_partition_weighted_closure():
+    """Root-sharded weighted sweeps on the closure path (each part Dials every
+    seed, closes only its own components' roots): 2 and 3 parts gather every
+    root once with the full sweep's digests."""
+    st = drained_fabric(40, 4, seed=6, drain=0.04, down=0.02, weighted_seed=13,
+                        ssw_per_plane=4)
+    _, _, eng = engine_for(st)
+    try:
+        full = Sweep(eng, mode="wcover")
+        assert "cover_closure" in [p["name"] for p in full.profile(1)]
+        full.run()
+        want = sweep_digests(full)
+        full.close()
+        for n_parts in (2, 3):
+            seen = {}
+            for p in range(n_parts):
+                sw = Sweep(eng, part=p, n_parts=n_parts, mode="wcover")
+                sw.run()
+                for r, d in sweep_digests(sw).items():
+                    assert r not in seen
+                    seen[r] = d
+                sw.close()
+            assert len(seen) == eng.V
+            assert all(np.array_equal(seen[r], want[r]) for r in range(eng.V)), n_parts
+    finally:
+        eng.close()
+
+
 @pytest.mark.parametrize("topo", ["unit", "weighted", "unit-derive"])
 def test_multi_device_context_two_slots_on_device0(topo):
     """ospf_multi with two contexts on device 0: parts on each slot, digests
