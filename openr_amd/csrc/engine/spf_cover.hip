@@ -451,6 +451,7 @@ hipError_t launch_closure(const ClosurePlan& p, uint32_t KW, hipStream_t s) {
 hipError_t launch_cover_spf(const DevGraph& g, const CoverGraph& C, const CoverArgs& a,
                             uint32_t n_cu, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
+  if (a.dload && !a.rowpos) return hipErrorInvalidValue;  // load mode writes rows by position
   const char* e = getenv("OSPF_COVER_DELTA");
   if (e && !a.rowpos && !a.dcomp && !a.dload) {  // delta-stepping (experiment)
     const uint32_t delta = (uint32_t)std::max(1, atoi(e));

@@ -1422,7 +1422,9 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     for (uint32_t v : seeds) is_seed[v] = 1;
     for (uint32_t v : cover_a)
       if (!is_seed[v]) clos.push_back(v);
+    const std::string err0 = c->err;  // a plan that does not apply is no error of the sweep
     closure = clos.size() >= seeds.size() && ospf_int::closure_build(c, clos, seed_row, ch) == OSPF_OK;
+    if (!closure) c->err = err0;
   }
   if (getenv("OSPF_SWEEP_DEBUG"))
     fprintf(stderr, "plan_wcover: cover %u seeds %zu comps %zu closure roots %zu -> %s (%s)\n", nA,
@@ -1558,7 +1560,10 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       return ospf_int::wderive_wide(c, d_roots, n, 0, W, slab, V, d_pos, nh, dg, strm, ct);
     };
     HubHost hh;
-    if (W <= 4 && getenv("OSPF_WNH_HUB") && hub_build(c, f, roots, W, pos, hh) == OSPF_OK) {
+    const std::string err0 = c->err;
+    const bool hub = W <= 4 && getenv("OSPF_WNH_HUB") && hub_build(c, f, roots, W, pos, hh) == OSPF_OK;
+    if (!hub) c->err = err0;  // not applicable: the lanes / wide kernels run
+    if (hub) {
       uint4* d_grp;
       uint32_t *d_hub, *d_loc, *d_ref, *d_wt, *d_ownl, *d_rid;
       if ((rc = upload(s, &d_grp, hh.grp)) || (rc = upload(s, &d_hub, hh.hub.empty() ? std::vector<uint32_t>{0u} : hh.hub)) ||
@@ -1597,9 +1602,11 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
         return e == hipSuccess ? OSPF_OK : ospf_int::hip_fail(c, e, "launch_wnh_hub");
       };
     }
-    if (W > 4 && getenv("OSPF_WNH_RUNS")) {  // runs of roots with one neighbour list
-      WRunsHost wh;
-      if ((rc = wruns_build(c, f, roots, W, pos, wh))) return rc;
+    WRunsHost wh;
+    const std::string err1 = c->err;
+    const bool runs = W > 4 && getenv("OSPF_WNH_RUNS") && wruns_build(c, f, roots, W, pos, wh) == OSPF_OK;
+    if (!runs) c->err = err1;
+    if (runs) {  // runs of roots with one neighbour list
       uint4* d_run;
       uint32_t *d_sl, *d_wt, *d_own, *d_rid;
       if ((rc = upload(s, &d_run, wh.run)) || (rc = upload(s, &d_sl, wh.slots)) ||
