@@ -252,6 +252,12 @@ __global__ void __launch_bounds__(256) wderive_kernel(DevGraph g, WDeriveArgs a)
 // (dist part from the own row) is summed per (root, subtile).
 constexpr uint32_t kWdWideG = 16;
 constexpr uint32_t kWdWideK = 128;
+// neighbour rows loaded per batch (all in flight before the compares); 16
+// measured slower on F100k-w (75.7 vs 49.8 ms: 130 VGPRs, 3 waves per SIMD)
+#ifndef OSPF_WIDE_BATCH
+#define OSPF_WIDE_BATCH 8
+#endif
+constexpr uint32_t kWideBatch = OSPF_WIDE_BATCH;
 template <int W>
 __global__ void __launch_bounds__(256) wderive_wide_kernel(DevGraph g, WDeriveArgs a) {
   __shared__ uint32_t s_root[kWdWideG], s_K[kWdWideG], s_own[kWdWideG];
@@ -342,12 +348,12 @@ __global__ void __launch_bounds__(256) wderive_wide_kernel(DevGraph g, WDeriveAr
     const uint32_t K = s_K[j];
 #pragma unroll
     for (int w = 0; w < W; ++w) {
-      for (uint32_t k8 = 0; k8 < 32u; k8 += 8u) {
+      for (uint32_t k8 = 0; k8 < 32u; k8 += kWideBatch) {
         const uint32_t kb = 32u * w + k8;
         if (kb >= K) break;  // uniform
-        uint32_t D[8][4], pk[8], wk[8];
+        uint32_t D[kWideBatch][4], pk[kWideBatch], wk[kWideBatch];
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) {  // 8 rows in flight
+        for (int kk = 0; kk < (int)kWideBatch; ++kk) {  // kWideBatch rows in flight
           pk[kk] = kb + kk < K ? sp[kb + kk] : kInf;
           wk[kk] = kb + kk < K ? sw[kb + kk] : kInf;
           if (pk[kk] < kNt) load4(pk[kk], D[kk]);
@@ -358,7 +364,7 @@ __global__ void __launch_bounds__(256) wderive_wide_kernel(DevGraph g, WDeriveAr
           }
         }
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) {
+        for (int kk = 0; kk < (int)kWideBatch; ++kk) {
 #pragma unroll
           for (int b = 0; b < 4; ++b) {
             // w + D == R without the saturating add: R >= D and R - D == w
