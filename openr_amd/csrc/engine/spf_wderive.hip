@@ -452,6 +452,7 @@ constexpr uint32_t kWlTile = 256;
 // its slots 32 w + i at i * 64 + w, consecutive lanes consecutive u16s (the
 // k-major table put every lane of a read on two banks)
 __device__ __forceinline__ uint32_t widx(uint32_t k) { return (k & 31u) * 64u + (k >> 5); }
+template <uint32_t NC>  // nodes per chunk: 2 (8-B loads) or 4 (16-B loads)
 __global__ void __launch_bounds__(256) wderive_lanes_kernel(DevGraph g, WDeriveArgs a) {
   __shared__ uint32_t s_pos[kWlK];
   __shared__ uint16_t s_w[kWlG][kWlK];
@@ -559,72 +560,90 @@ __global__ void __launch_bounds__(256) wderive_lanes_kernel(DevGraph g, WDeriveA
         s_R[j][x % kWlTile] = v < V ? a.src[(size_t)s_own[j0 + j] * a.src_pitch + v] : kInf;
       }
       __syncthreads();
-      for (uint32_t c = wave; c < kWlTile / 2u; c += kWaves) {
-        const uint32_t vc = v0 + 2u * c;
+      for (uint32_t c = wave; c < kWlTile / NC; c += kWaves) {
+        const uint32_t vc = v0 + NC * c;
         if (vc >= V) break;  // wave-uniform
-        uint32_t D0[32], D1[32];
+        uint32_t D[NC][32];
 #pragma unroll
         for (int i = 0; i < 32; ++i) {
           const uint32_t k = 32u * lane + i;
           const uint32_t p = (lane < W && k < K) ? s_pos[k] : kInf;
           if (p < kNt) {
             const uint32_t* row = a.src + (size_t)p * a.src_pitch + vc;
-            if (a.vec && vc + 1u < V) {
-              const uint2 x = *reinterpret_cast<const uint2*>(row);
-              D0[i] = x.x;
-              D1[i] = x.y;
+            if (a.vec && vc + NC - 1u < V) {
+              if constexpr (NC == 4) {
+                const uint4 x = *reinterpret_cast<const uint4*>(row);
+                D[0][i] = x.x;
+                D[1][i] = x.y;
+                D[2][i] = x.z;
+                D[3][i] = x.w;
+              } else {
+                const uint2 x = *reinterpret_cast<const uint2*>(row);
+                D[0][i] = x.x;
+                D[1][i] = x.y;
+              }
             } else {
-              D0[i] = row[0];
-              D1[i] = vc + 1u < V ? row[1] : kInf;
+#pragma unroll
+              for (uint32_t n = 0; n < NC; ++n) D[n][i] = vc + n < V ? row[n] : kInf;
             }
-          } else if (p != kInf) {
-            D0[i] = vc == (p & ~kNt) ? 0u : kInf;
-            D1[i] = vc + 1u == (p & ~kNt) ? 0u : kInf;
           } else {
-            D0[i] = D1[i] = kInf;
+#pragma unroll
+            for (uint32_t n = 0; n < NC; ++n)
+              D[n][i] = (p != kInf && vc + n == (p & ~kNt)) ? 0u : kInf;
           }
         }
-        uint64_t kn0 = 0, kn1 = 0, kd0 = 0, kd1 = 0;
-        if (a.digest) {
-          kd0 = g.dkey[2ull * vc];
-          kn0 = g.dkey[2ull * vc + 1];
-          if (vc + 1u < V) {
-            kd1 = g.dkey[2ull * (vc + 1u)];
-            kn1 = g.dkey[2ull * (vc + 1u) + 1];
+        uint64_t kn[NC], kd[NC];
+#pragma unroll
+        for (uint32_t n = 0; n < NC; ++n) {
+          kn[n] = kd[n] = 0ull;
+          if (a.digest && vc + n < V) {
+            kd[n] = g.dkey[2ull * (vc + n)];
+            kn[n] = g.dkey[2ull * (vc + n) + 1];
           }
         }
 #pragma unroll
         for (int jj = 0; jj < (int)kWlG; ++jj) {
           const uint32_t j = (uint32_t)jj;
           if (j < j0 || j >= j1) continue;  // uniform
-          const uint32_t R0 = s_R[j - j0][2u * c], R1 = s_R[j - j0][2u * c + 1u];
-          uint32_t w0 = 0, w1 = 0;
+          uint32_t R[NC], wd[NC];
+#pragma unroll
+          for (uint32_t n = 0; n < NC; ++n) {
+            R[n] = s_R[j - j0][NC * c + n];
+            wd[n] = 0u;
+          }
 #pragma unroll
           for (int i = 0; i < 32; ++i) {
             const uint32_t k = 32u * lane + i;
             const uint32_t wk = (lane < W && k < K) ? (uint32_t)s_w[j][i * 64u + lane] : 0xFFFFu;
             const uint32_t wv = wk == 0xFFFFu ? kInf : wk;
-            w0 |= (R0 >= D0[i] && R0 - D0[i] == wv ? 1u : 0u) << i;
-            w1 |= (R1 >= D1[i] && R1 - D1[i] == wv ? 1u : 0u) << i;
+#pragma unroll
+            for (uint32_t n = 0; n < NC; ++n)
+              wd[n] |= (R[n] >= D[n][i] && R[n] - D[n][i] == wv ? 1u : 0u) << i;
           }
-          if (R0 == kInf) w0 = 0u;
-          if (R1 == kInf) w1 = 0u;
           const uint32_t r = s_root[j];
-          if (vc == r) w0 = 0u;
-          if (vc + 1u == r) w1 = 0u;
+#pragma unroll
+          for (uint32_t n = 0; n < NC; ++n)
+            if (R[n] == kInf || vc + n == r) wd[n] = 0u;
           uint32_t* dst = a.nh + ((size_t)(i0 + j) * V + vc) * W + lane;
           if (lane < W) {
-            __builtin_nontemporal_store(w0, dst);
-            if (vc + 1u < V) __builtin_nontemporal_store(w1, dst + W);
+#pragma unroll
+            for (uint32_t n = 0; n < NC; ++n)
+              if (vc + n < V) __builtin_nontemporal_store(wd[n], dst + (size_t)n * W);
           }
           if (a.digest) {
-            if (w0) h[jj] += kn0 * digest_word_key(lane, w0);
-            if (w1) h[jj] += kn1 * digest_word_key(lane, w1);
+#pragma unroll
+            for (uint32_t n = 0; n < NC; ++n)
+              if (wd[n]) h[jj] += kn[n] * digest_word_key(lane, wd[n]);
             if (lane == 0) {
               uint64_t hx = 0, sx = 0;
               uint32_t rc = 0;
-              if (R0 != kInf) { hx += kd0 * ((uint64_t)R0 + 1ull); sx += R0; ++rc; }
-              if (vc + 1u < V && R1 != kInf) { hx += kd1 * ((uint64_t)R1 + 1ull); sx += R1; ++rc; }
+#pragma unroll
+              for (uint32_t n = 0; n < NC; ++n)
+                if (vc + n < V && R[n] != kInf) {
+                  hx += kd[n] * ((uint64_t)R[n] + 1ull);
+                  sx += R[n];
+                  ++rc;
+                }
               h[jj] += hx;
               if (rc) {
                 atomicAdd(&s_sum[j], (unsigned long long)sx);
@@ -917,7 +936,11 @@ hipError_t launch_wderive_wide(const DevGraph& g, WDeriveArgs a, uint32_t W, hip
     a.ctiles = std::min(a.ctiles, a.tiles);
     a.chunks = (a.tiles + a.ctiles - 1) / a.ctiles;
     const dim3 grid(((a.n + kWlG - 1) / kWlG) * a.chunks);
-    hipLaunchKernelGGL(wderive_lanes_kernel, grid, dim3(kBlock), 0, s, g, a);
+    // 4 nodes per chunk (16-B loads of each slot row): F100k-w spines 71 -> 40
+    // ms in the sweep (OSPF_WL_NC=2: the 8-B form)
+    const char* nc = getenv("OSPF_WL_NC");
+    if (nc && atoi(nc) == 2) hipLaunchKernelGGL(wderive_lanes_kernel<2>, grid, dim3(kBlock), 0, s, g, a);
+    else hipLaunchKernelGGL(wderive_lanes_kernel<4>, grid, dim3(kBlock), 0, s, g, a);
     return hipGetLastError();
   }
   a.tiles = (g.V + kSub - 1) / kSub;
