@@ -63,6 +63,11 @@ uint64_t odl_spf_runs(const odl_ls* ls);
  * Stats: {patches applied, results kept, results dropped}. */
 void odl_set_incremental(odl_ls* ls, int on);
 void odl_incremental_stats(const odl_ls* ls, uint64_t* out3);
+/* {whole CSR snapshots, whole device graph loads, updates whose added /
+ * removed links were patched in place (ospf_update_rows), rows rebuilt by
+ * them}: a [LINK UP] / [LINK DOWN] between known nodes (LinkState.cpp:632-657)
+ * takes no snapshot and no load. */
+void odl_topology_stats(const odl_ls* ls, uint64_t* out4);
 uint32_t odl_num_nodes(const odl_ls* ls);
 uint32_t odl_num_links(const odl_ls* ls);
 

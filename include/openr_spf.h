@@ -416,6 +416,25 @@ int ospf_update_links(ospf_ctx* ctx, const ospf_link_update* updates, uint32_t n
 int ospf_update_nodes(ospf_ctx* ctx, const uint32_t* nodes, const uint8_t* no_transit,
                       uint32_t n, uint64_t version);
 
+/* Structural update in place: links added or removed between existing nodes
+ * -- LinkState's [LINK UP] / [LINK DOWN] (LinkState.cpp:632-657; Decision
+ * applies them per adjacency database, Decision.cpp:743-765). `csr` is the
+ * caller's whole CSR after the change (same nodes and node ids, any link ids:
+ * a removed link's id simply no longer appears, an added link may take a new
+ * or a retired id), `rows` the nodes whose rows changed (both ends of every
+ * added / removed link). The engine rebuilds those rows (and, when a row's
+ * parallel links to a neighbour may have been reordered, that neighbour's
+ * row) in their padded slots, moving the rows after a row that outgrows its
+ * slots, and refreshes the distinct-neighbour lists, link positions and
+ * planner bounds. O(changed rows) host work plus device copies; sweeps made
+ * before the call return OSPF_E_NOGRAPH. OSPF_E_RANGE when the layout's
+ * reserve (~3 % of entries, distinct neighbours, link ids) is exhausted, a
+ * metric leaves the contract, or the node count differs: reload with
+ * ospf_load_graph. On any error the context is unchanged except after a
+ * device error (then reload). */
+int ospf_update_rows(ospf_ctx* ctx, const ospf_csr* csr, const uint32_t* rows, uint32_t n,
+                     uint64_t version);
+
 /* One change of a batch, for ospf_affected_roots. LINK: endpoints a, b;
  * before / after: up, metric advertised by a (w_ab) and by b (w_ba). NODE:
  * node a changed its overload bit (either way). */
@@ -508,10 +527,15 @@ int ospf_links_unmask(ospf_ctx* ctx);
 #define OSPF_SWEEP_WDERIVE 3u
 #define OSPF_SWEEP_BATCH 4u
 #define OSPF_SWEEP_LDS 5u
+/* opts.flags: create without the eager first run (hip_graph must be 0); the
+ * first ospf_sweep_run is then the first run. A caller that runs the sweep
+ * once per graph version (odl::LinkState; ospf_msweep_create, which starts
+ * every device's first run together) pays one run instead of two. */
+#define OSPF_SWEEP_DEFER 0x100u
 
 typedef struct ospf_sweep ospf_sweep;
 typedef struct ospf_sweep_opts {
-  uint32_t flags;      /* 0 (link metrics) or OSPF_HOP_COUNT */
+  uint32_t flags;      /* 0 (link metrics) or OSPF_HOP_COUNT, | OSPF_SWEEP_DEFER */
   uint32_t mode;       /* OSPF_SWEEP_* */
   uint32_t part;       /* this part of the root partition ... */
   uint32_t n_parts;    /* ... over n_parts (0 or 1: every node) */
@@ -595,9 +619,16 @@ int ospf_msweep_create(ospf_multi* m, const ospf_sweep_opts* opts, ospf_msweep**
 int ospf_msweep_destroy(ospf_msweep* ms);
 /* Queue one run on every device and wait for all of them. */
 int ospf_msweep_run(ospf_msweep* ms);
-/* Digests of every node by node id (host [V]): peer copies onto the first
- * device, one scatter by root id, one copy back. */
+/* Digests of every node by node id (host [V]). With distinct devices the
+ * parts' 24-B records (padded to the largest part) are all-gathered by ONE
+ * RCCL ncclAllGather over xGMI (communicators from ncclCommInitAll in this
+ * process, made once per ospf_multi); with a device given twice (RCCL takes
+ * one rank per GPU) or OSPF_RCCL=0, peer copies onto the first device. Then
+ * one scatter by root id and one copy back. OSPF_RCCL=1 takes RCCL for a
+ * single device too (a one-rank communicator). */
 int ospf_msweep_digests(ospf_msweep* ms, ospf_digest* out_by_node);
+/* 1: this sweep's digests are gathered by RCCL, 0: by peer copies. */
+uint32_t ospf_msweep_gather_backend(const ospf_msweep* ms);
 /* The slot's sweep (row access, info) and the slot owning `root`. */
 ospf_sweep* ospf_msweep_part(ospf_msweep* ms, uint32_t slot);
 int ospf_msweep_owner(const ospf_msweep* ms, uint32_t root, uint32_t* slot);

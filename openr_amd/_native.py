@@ -23,12 +23,13 @@ OSPF_HOP_COUNT = 0x1
 OSPF_WANT_DIST = 0x2
 OSPF_WANT_NH = 0x4
 OSPF_WANT_DIGEST = 0x8
+OSPF_SWEEP_DEFER = 0x100
 
 ENGINE_SYMBOLS = [
     "ospf_open", "ospf_close", "ospf_last_error", "ospf_load_graph", "ospf_graph_info_get",
     "ospf_root_neighbors", "ospf_sssp_batch", "ospf_sssp_batch_dev", "ospf_sync",
     "ospf_plan_variant", "ospf_plan", "ospf_plan_n", "ospf_spf_runs", "ospf_run_batch_dev",
-    "ospf_ksp2_run", "ospf_ksp2_dev", "ospf_update_links", "ospf_update_nodes",
+    "ospf_ksp2_run", "ospf_ksp2_dev", "ospf_update_links", "ospf_update_nodes", "ospf_update_rows",
     "ospf_levels_dev", "ospf_nh_derive_dev", "ospf_leaf_derive_dev",
     "ospf_nh_derive_twin_dev", "ospf_leaf_derive2_dev", "ospf_wderive_dev", "ospf_wderive_wide_dev",
     "ospf_lds_sweep_dev", "ospf_lds_sweep_fits", "ospf_twin_levels_dev",
@@ -41,12 +42,13 @@ ENGINE_SYMBOLS = [
     "ospf_multi_open", "ospf_multi_close", "ospf_multi_last_error", "ospf_multi_size",
     "ospf_multi_ctx", "ospf_multi_load_graph", "ospf_msweep_create", "ospf_msweep_destroy",
     "ospf_msweep_run", "ospf_msweep_digests", "ospf_msweep_part", "ospf_msweep_owner",
+    "ospf_msweep_gather_backend",
 ]
 DECISION_SYMBOLS = [
     "odl_create", "odl_create_multi", "odl_all_sources_prefetch", "odl_all_sources_digests",
     "odl_sweep_stats", "odl_destroy", "odl_last_error", "odl_free", "odl_apply", "odl_spf_text",
     "odl_kth_paths_text", "odl_links_text", "odl_link_keys_text", "odl_metric_a_to_b", "odl_is_overloaded",
-    "odl_spf_runs", "odl_set_incremental", "odl_incremental_stats", "odl_num_nodes", "odl_num_links", "odl_spf_digests", "odl_spf_prefetch",
+    "odl_spf_runs", "odl_set_incremental", "odl_incremental_stats", "odl_topology_stats", "odl_num_nodes", "odl_num_links", "odl_spf_digests", "odl_spf_prefetch",
     "odl_ksp2_text", "odl_route_text", "odl_route_db_text", "odl_path_a_in_b", "odl_ucmp_text", "odl_csr_size", "odl_csr_export", "odl_node_name", "odl_node_id",
 ]
 
@@ -172,6 +174,7 @@ def engine() -> C.CDLL:
         L.ospf_cover_dist_dev.argtypes = [vp, vp, u32, vp, vp]
         L.ospf_update_links.argtypes = [vp, vp, u32, u64]
         L.ospf_update_nodes.argtypes = [vp, vp, vp, u32, u64]
+        L.ospf_update_rows.argtypes = [vp, C.POINTER(ospf_csr), vp, u32, u64]
         L.ospf_affected_roots.argtypes = [vp, vp, u32, u32, vp, u32, vp, vp]
         L.ospf_repair_runs.argtypes = [vp, vp, u32, u32, u32, vp, vp, vp, u32, vp, vp]
         L.ospf_spf_runs.argtypes = [vp]
@@ -207,6 +210,8 @@ def engine() -> C.CDLL:
         L.ospf_msweep_part.argtypes = [vp, u32]
         L.ospf_msweep_part.restype = vp
         L.ospf_msweep_owner.argtypes = [vp, u32, C.POINTER(u32)]
+        L.ospf_msweep_gather_backend.argtypes = [vp]
+        L.ospf_msweep_gather_backend.restype = u32
         _engine = L
     return _engine
 
@@ -250,6 +255,8 @@ def decision() -> C.CDLL:
         L.odl_set_incremental.restype = None
         L.odl_incremental_stats.argtypes = [vp, vp]
         L.odl_incremental_stats.restype = None
+        L.odl_topology_stats.argtypes = [vp, vp]
+        L.odl_topology_stats.restype = None
         L.odl_num_nodes.argtypes = [vp]
         L.odl_num_nodes.restype = u32
         L.odl_num_links.argtypes = [vp]

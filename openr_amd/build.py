@@ -74,7 +74,8 @@ def build(force: bool = False, verbose_resources: bool = False) -> None:
             list(ex.map(compile_one, todo))
     objs = [_obj(s) for s in ENGINE_SRC]
     if force or todo or _newer(ENGINE_SO, objs):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", ENGINE_SO] + objs)
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", ENGINE_SO] + objs +
+             ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"])
     if force or _newer(DECISION_SO, DECISION_SRC + DECISION_HEADERS + [ENGINE_SO]):
         _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra",
               "-Wno-unused-parameter", "-o", DECISION_SO] + DECISION_SRC +

@@ -221,7 +221,7 @@ char* odl_links_text(odl_ls* h, const char* node) {
 char* odl_link_keys_text(odl_ls* h) {
   return guard(h, [&]() -> char* {
     std::ostringstream os;
-    for (const auto& l : h->ls.snapshot().links) os << l->key() << '\n';
+    for (const auto& l : h->ls.snapshot().links) os << (l ? l->key() : std::string()) << '\n';
     return dup(os.str());
   }, (char*)nullptr);
 }
@@ -246,6 +246,14 @@ void odl_incremental_stats(const odl_ls* h, uint64_t* out) {
   out[0] = st.patches;
   out[1] = st.kept;
   out[2] = st.dropped;
+}
+void odl_topology_stats(const odl_ls* h, uint64_t* out4) {
+  if (!h || !out4) return;
+  const auto& st = h->ls.topologyStats();
+  out4[0] = st.snapshots;
+  out4[1] = st.loads;
+  out4[2] = st.link_patches;
+  out4[3] = st.rows_patched;
 }
 uint32_t odl_num_nodes(const odl_ls* h) { return h ? (uint32_t)h->ls.numNodes() : 0; }
 uint32_t odl_num_links(const odl_ls* h) { return h ? (uint32_t)h->ls.numLinks() : 0; }

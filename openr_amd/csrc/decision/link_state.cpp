@@ -2,6 +2,7 @@
 #include "link_state.h"
 
 #include <cstdlib>
+#include <cstring>
 #include <numeric>
 #include <set>
 #include <algorithm>
@@ -184,13 +185,16 @@ std::vector<LinkPtr> LinkState::sortedLinksOf(const std::string& node) const {
 
 static size_t V_of(const LinkState::Csr& c) { return c.names.size(); }
 
+void LinkState::clearMemo() {
+  memoMetric_.clear();
+  memoHops_.clear();
+  memoKsp_.clear();
+}
+
 void LinkState::invalidate() {
   ++version_;
   dropSweep();
-  memoMetric_.clear();
-  memoHops_.clear();
-  rawMetric_.clear();
-  memoKsp_.clear();
+  clearMemo();
 }
 
 LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db) {
@@ -201,6 +205,7 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db) 
   bool structural = !known;  // a link or node added / removed (incremental mode)
   std::vector<LinkDelta> deltas;
   std::vector<std::string> nodeDeltas;
+  std::vector<LinkPtr> removedLinks;
   auto& idx = adjIndex_[me];
   idx.clear();  // (its views point into the database replaced here)
   const AdjacencyDatabase& kept = adjDbs_[me] = db;
@@ -243,6 +248,7 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db) 
       structural = true;
       ch.topologyChanged |= before[j]->isUp();
       removeLink(before[j]);
+      removedLinks.push_back(before[j]);
       ++j;
     } else {
       const Link& fresh = *after[i];
@@ -279,7 +285,27 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db) 
       bound += keepsContract ? m : 0;
     }
   }
+  // links added between known nodes: their metrics join the bound
+  for (const auto& l : ch.addedLinks)
+    for (const Metric m : {l->metricFrom(l->lowNode()), l->metricFrom(l->highNode())}) {
+      keepsContract &= m >= 1 && m <= 0xFFFFFFFFull;
+      bound += keepsContract ? m : 0;
+    }
   keepsContract &= bound < 0xFFFFFFFFull;
+  // [LINK UP] / [LINK DOWN] between known nodes (LinkState.cpp:632-657): the
+  // snapshot and the device graph are patched in place; the memo is dropped on
+  // a topology change as in the reference (:751-754) -- in incremental mode
+  // too (its kept-root rule covers metric / up / overload changes only)
+  if (known && structural && snapVersion_ == version_ && keepsContract &&
+      !getenv("ODL_NO_LINK_PATCH")) {
+    if (ch.topologyChanged || incremental_) {
+      if (incremental_) incStats_.dropped += memoMetric_.size() + memoHops_.size();
+      clearMemo();
+    }
+    patchStructure(ch.addedLinks, removedLinks);
+    if (!deltas.empty() || !nodeDeltas.empty()) patchGraph(deltas, nodeDeltas);
+    return ch;
+  }
   if (incremental_ && !structural && snapVersion_ == version_ && keepsContract) {
     distBound_ = bound;
     if (ch.topologyChanged) applyIncremental(deltas, nodeDeltas);
@@ -292,12 +318,7 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db) 
   // attribute-only updates (:721-724: labels, weights).
   if (!structural && snapVersion_ == version_ && keepsContract) {
     distBound_ = bound;
-    if (ch.topologyChanged) {
-      memoMetric_.clear();
-      memoHops_.clear();
-      rawMetric_.clear();
-      memoKsp_.clear();
-    }
+    if (ch.topologyChanged) clearMemo();
     if (!deltas.empty() || !nodeDeltas.empty()) patchGraph(deltas, nodeDeltas);
     return ch;
   }
@@ -475,7 +496,7 @@ LinkStateChange LinkState::deleteAdjacencyDatabase(const std::string& node) {
 // 3. the lower end writes the link id into the Link, the upper end reads it;
 // 4. rows are sorted by (neighbour id, rank) and written, then twins.
 const LinkState::Csr& LinkState::snapshot() {
-  if (snapVersion_ == version_) return csr_;
+  if (snapVersion_ == version_) return *csr_;
   const bool tm = getenv("ODL_SNAP_TIMING") != nullptr;
   auto t0 = std::chrono::steady_clock::now();
   auto lap = [&](const char* what) {
@@ -484,7 +505,7 @@ const LinkState::Csr& LinkState::snapshot() {
     fprintf(stderr, "snapshot %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(t - t0).count());
     t0 = t;
   };
-  rawMetric_.clear();  // dist rows are indexed by the old node ids
+  ++topoStats_.snapshots;
   Csr c;
   c.names.reserve(adjDbs_.size());
   for (const auto& kv : adjDbs_) c.names.push_back(kv.first);
@@ -567,6 +588,9 @@ const LinkState::Csr& LinkState::snapshot() {
     }
   });
   lap("link ids");
+  // room for the links patchStructure may add in place
+  for (auto* v : {&c.col, &c.metric, &c.linkId, &c.twin, &c.linkRank}) v->reserve(E + 4096 + E / 64);
+  c.edgeUp.reserve(E + 4096 + E / 64);
   c.col.resize(E);
   c.metric.resize(E);
   c.linkId.resize(E);
@@ -601,15 +625,16 @@ const LinkState::Csr& LinkState::snapshot() {
     }
   });
   lap("rows");
-  csr_ = std::move(c);
+  c.rowMax = std::move(rowMax);
+  csr_ = std::make_shared<Csr>(std::move(c));
   lap("move");
   snapVersion_ = version_;
-  return csr_;
+  return *csr_;
 }
 
 uint32_t LinkState::linkIdOf(const Link& l) const {
   const uint32_t lid = l.snapLid;
-  if (lid >= csr_.links.size() || csr_.links[lid].get() != &l)
+  if (lid >= csr_->links.size() || csr_->links[lid].get() != &l)
     throw std::out_of_range("link not in the CSR snapshot");
   return lid;
 }
@@ -633,20 +658,21 @@ void LinkState::ensureEngine() {
   if (engineVersion_ != snapVersion_) {
     dropSweep();
     ospf_csr g{};
-    g.n_nodes = (uint32_t)csr_.names.size();
-    g.n_edges = (uint32_t)csr_.col.size();
-    g.row_ptr = csr_.rowPtr.data();
-    g.col = csr_.col.data();
-    g.metric = csr_.metric.data();
-    g.link_id = csr_.linkId.data();
-    g.twin = csr_.twin.data();
-    g.edge_up = csr_.edgeUp.data();
-    g.no_transit = csr_.noTransit.data();
-    g.link_rank = csr_.linkRank.data();
+    g.n_nodes = (uint32_t)csr_->names.size();
+    g.n_edges = (uint32_t)csr_->col.size();
+    g.row_ptr = csr_->rowPtr.data();
+    g.col = csr_->col.data();
+    g.metric = csr_->metric.data();
+    g.link_id = csr_->linkId.data();
+    g.twin = csr_->twin.data();
+    g.edge_up = csr_->edgeUp.data();
+    g.no_transit = csr_->noTransit.data();
+    g.link_rank = csr_->linkRank.data();
     int rc = multi_ ? ospf_multi_load_graph(multi_, &g, snapVersion_)
                     : ospf_load_graph(engine_, &g, snapVersion_);
     if (rc != OSPF_OK)
       throw EngineError(rc, multi_ ? ospf_multi_last_error(multi_) : ospf_last_error(engine_));
+    ++topoStats_.loads;
     engineVersion_ = snapVersion_;
   }
 }
@@ -668,15 +694,17 @@ void LinkState::prefetchAllSources(bool useLinkMetric) {
   snapshot();
   if (sweepHas(useLinkMetric)) return;
   if (useLinkMetric && hostMetric_) {  // outside the engine contract: the reference algorithm
-    prefetchSpf(csr_.names, true);
+    prefetchSpf(csr_->names, true);
     return;
   }
   ensureEngine();
   dropSweep();
   ospf_sweep_opts o{};
-  o.flags = useLinkMetric ? 0u : OSPF_HOP_COUNT;
+  // one run per snapshot: nothing to replay, and the create makes no run of
+  // its own (OSPF_SWEEP_DEFER): the run below is the only one
+  o.flags = (useLinkMetric ? 0u : OSPF_HOP_COUNT) | OSPF_SWEEP_DEFER;
   o.mode = OSPF_SWEEP_AUTO;
-  o.hip_graph = 0;  // one run per snapshot: nothing to replay
+  o.hip_graph = 0;
   int rc;
   ospf_sweep_info info{};
   if (multi_) {
@@ -691,10 +719,11 @@ void LinkState::prefetchAllSources(bool useLinkMetric) {
     sweepStats_.devices = ospf_multi_size(multi_);
   } else {
     rc = ospf_sweep_create(engine_, &o, &sweep_);
-    if (rc == OSPF_OK) rc = ospf_sweep_run(sweep_, nullptr);
+    bool runErr = false;  // ospf_sweep_run reports through the sweep's own error
+    if (rc == OSPF_OK) runErr = (rc = ospf_sweep_run(sweep_, nullptr)) != OSPF_OK;
     if (rc == OSPF_OK) rc = ospf_sync(engine_, nullptr);
     if (rc != OSPF_OK) {
-      const std::string m = ospf_last_error(engine_);
+      const std::string m = runErr ? ospf_sweep_last_error(sweep_) : ospf_last_error(engine_);
       dropSweep();
       throw EngineError(rc, m);
     }
@@ -703,7 +732,7 @@ void LinkState::prefetchAllSources(bool useLinkMetric) {
   }
   sweepVersion_ = snapVersion_;
   sweepMetric_ = useLinkMetric;
-  spfRuns_ += csr_.names.size();  // every node's runSpf, once
+  spfRuns_ += csr_->names.size();  // every node's runSpf, once
   ++sweepStats_.sweeps;
   sweepStats_.mode = info.mode;
   sweepStats_.hip_graph = info.hip_graph;
@@ -711,7 +740,7 @@ void LinkState::prefetchAllSources(bool useLinkMetric) {
 
 void LinkState::sweepRows(const std::vector<uint32_t>& roots, uint32_t W,
                           std::vector<uint32_t>& dist, std::vector<uint32_t>& nh) {
-  const size_t V = csr_.names.size();
+  const size_t V = csr_->names.size();
   dist.assign(roots.size() * V, kInf);
   nh.assign(roots.size() * V * W, 0);
   if (sweep_) {
@@ -722,10 +751,11 @@ void LinkState::sweepRows(const std::vector<uint32_t>& roots, uint32_t W,
     for (size_t i = 0; i < roots.size(); ++i) {
       uint32_t slot = 0;
       int rc = ospf_msweep_owner(msweep_, roots[i], &slot);
+      if (rc != OSPF_OK)
+        throw EngineError(rc, "all-sources sweep: no part owns node " + csr_->names[roots[i]]);
       ospf_sweep* part = ospf_msweep_part(msweep_, slot);
-      if (rc == OSPF_OK)
-        rc = ospf_sweep_copy_rows(part, &roots[i], 1, W, dist.data() + i * V, nh.data() + i * V * W);
-      if (rc != OSPF_OK) throw EngineError(rc, ospf_multi_last_error(multi_));
+      rc = ospf_sweep_copy_rows(part, &roots[i], 1, W, dist.data() + i * V, nh.data() + i * V * W);
+      if (rc != OSPF_OK) throw EngineError(rc, ospf_sweep_last_error(part));
     }
   }
   sweepStats_.rows_copied += roots.size();
@@ -733,8 +763,8 @@ void LinkState::sweepRows(const std::vector<uint32_t>& roots, uint32_t W,
 
 std::vector<ospf_digest> LinkState::allSourcesDigests(bool useLinkMetric) {
   snapshot();
-  const size_t V = csr_.names.size();
-  if (useLinkMetric && hostMetric_) return spfDigests(csr_.names, true);
+  const size_t V = csr_->names.size();
+  if (useLinkMetric && hostMetric_) return spfDigests(csr_->names, true);
   prefetchAllSources(useLinkMetric);
   std::vector<ospf_digest> out(V);
   if (msweep_) {
@@ -755,16 +785,13 @@ std::vector<ospf_digest> LinkState::allSourcesDigests(bool useLinkMetric) {
 
 void LinkState::evictSpf(const std::vector<std::string>& roots, bool useLinkMetric) {
   auto& memo = useLinkMetric ? memoMetric_ : memoHops_;
-  for (const auto& r : roots) {
-    memo.erase(r);
-    if (useLinkMetric) rawMetric_.erase(r);
-  }
+  for (const auto& r : roots) memo.erase(r);
 }
 
 uint32_t LinkState::nhWordsFor(uint32_t root) const {
   uint32_t n = 0;
-  for (uint32_t e = csr_.rowPtr[root]; e < csr_.rowPtr[root + 1]; ++e)
-    if (csr_.col[e] != root && (e == csr_.rowPtr[root] || csr_.col[e - 1] != csr_.col[e])) ++n;
+  for (uint32_t e = csr_->rowPtr[root]; e < csr_->rowPtr[root + 1]; ++e)
+    if (csr_->col[e] != root && (e == csr_->rowPtr[root] || csr_->col[e - 1] != csr_->col[e])) ++n;
   return std::max<uint32_t>(1, (n + 31) / 32);
 }
 
@@ -773,7 +800,7 @@ void LinkState::runBatch(const std::vector<uint32_t>& roots,
                          uint32_t flags, uint32_t W, std::vector<uint32_t>* dist,
                          std::vector<uint32_t>* nh, std::vector<ospf_digest>* dig) {
   ensureEngine();
-  const size_t V = csr_.names.size(), n = roots.size();
+  const size_t V = csr_->names.size(), n = roots.size();
   if (!useLinkMetric) flags |= OSPF_HOP_COUNT;
   if (dist) dist->assign(n * V, kInf);
   if (nh) nh->assign(n * V * W, 0);
@@ -796,28 +823,28 @@ void LinkState::runBatch(const std::vector<uint32_t>& roots,
   if (rc != OSPF_OK) throw EngineError(rc, ospf_last_error(engine_));
 }
 
-std::vector<PathLink> LinkState::pathLinksOf(const RawRun& run, uint32_t v,
-                                             bool useLinkMetric) const {
+// ---------------------------------------------------------------- results
+std::vector<PathLink> SpfRows::pathLinksOf(uint32_t v) const {
   std::vector<PathLink> out;
-  const uint32_t dv = run.dist[v];
-  if (v == run.root || dv == kInf) return out;
+  const CsrSnapshot& c = *csr;
+  const uint32_t dv = dist[v];
+  if (v == root || dv == kInf) return out;
   struct Cand {
     uint32_t du, u, rank, lid;
   };
   std::vector<Cand> cands;
-  for (uint32_t e = csr_.rowPtr[v]; e < csr_.rowPtr[v + 1]; ++e) {
-    if (!csr_.edgeUp[e]) continue;
-    const uint32_t lid = csr_.linkId[e];
-    if (!run.ignored.empty() && std::binary_search(run.ignored.begin(), run.ignored.end(), lid))
-      continue;
-    const uint32_t u = csr_.col[e];
-    const uint32_t du = run.dist[u];
+  for (uint32_t e = c.rowPtr[v]; e < c.rowPtr[v + 1]; ++e) {
+    if (!c.edgeUp[e]) continue;
+    const uint32_t lid = c.linkId[e];
+    if (!ignored.empty() && std::binary_search(ignored.begin(), ignored.end(), lid)) continue;
+    const uint32_t u = c.col[e];
+    const uint32_t du = dist[u];
     if (du == kInf) continue;
-    const uint32_t t = csr_.twin[e];  // entry u -> v: metric advertised by u
-    const uint64_t w = useLinkMetric ? csr_.metric[t] : 1u;
+    const uint32_t t = c.twin[e];  // entry u -> v: metric advertised by u
+    const uint64_t w = useLinkMetric ? c.metric[t] : 1u;
     if ((uint64_t)du + w != dv) continue;
-    if (u != run.root && csr_.noTransit[u]) continue;
-    cands.push_back({du, u, csr_.linkRank[t], lid});
+    if (u != root && c.noTransit[u]) continue;
+    cands.push_back({du, u, c.linkRank[t], lid});
   }
   // reference order: predecessor pop order (dist, name) then the link's
   // position in linksFromNode(predecessor)
@@ -825,47 +852,111 @@ std::vector<PathLink> LinkState::pathLinksOf(const RawRun& run, uint32_t v,
     return std::tie(a.du, a.u, a.rank) < std::tie(b.du, b.u, b.rank);
   });
   out.reserve(cands.size());
-  for (const auto& c : cands) out.push_back(PathLink{csr_.links[c.lid], csr_.names[c.u]});
+  for (const auto& x : cands) out.push_back(PathLink{c.links[x.lid], c.names[x.u]});
   return out;
 }
 
-SpfResult LinkState::buildResult(const RawRun& run, const uint32_t* nh, uint32_t W,
-                                 bool useLinkMetric) {
-  SpfResult res;
-  const uint32_t V = (uint32_t)csr_.names.size();
-  std::vector<uint32_t> nbrs;
-  for (uint32_t e = csr_.rowPtr[run.root]; e < csr_.rowPtr[run.root + 1]; ++e) {
-    const uint32_t v = csr_.col[e];
-    if (v != run.root && (nbrs.empty() || nbrs.back() != v)) nbrs.push_back(v);
-  }
-  // node records built on host threads (next-hop sets, pathLinks), then moved
-  // into the name-keyed map
-  std::vector<uint32_t> reached;
-  reached.reserve(V);
-  for (uint32_t v = 0; v < V; ++v)
-    if (run.dist[v] != kInf) reached.push_back(v);
-  std::vector<NodeSpfResult> recs;
-  recs.reserve(reached.size());
-  for (const uint32_t v : reached) recs.emplace_back(run.dist[v]);
-  parallelFor((uint32_t)reached.size(), [&](uint32_t lo, uint32_t hi) {
-    for (uint32_t k = lo; k < hi; ++k) {
-      const uint32_t v = reached[k];
-      NodeSpfResult& r = recs[k];
-      const uint32_t* bits = nh + (size_t)v * W;
-      for (uint32_t w = 0; w < W; ++w) {
-        uint32_t b = bits[w];
-        while (b) {
-          const uint32_t i = w * 32 + (uint32_t)__builtin_ctz(b);
-          b &= b - 1;
-          r.nextHops_.insert(csr_.names[nbrs.at(i)]);
-        }
-      }
-      r.pathLinks_ = pathLinksOf(run, v, useLinkMetric);
+std::unordered_set<std::string> SpfRows::nextHopsOf(uint32_t v) const {
+  std::unordered_set<std::string> out;
+  if (nh.empty()) return out;
+  const uint32_t* bits = nh.data() + (size_t)v * W;
+  for (uint32_t w = 0; w < W; ++w)
+    for (uint32_t b = bits[w]; b; b &= b - 1) {
+      const uint32_t i = w * 32 + (uint32_t)__builtin_ctz(b);
+      out.insert(csr->names[nbrs.at(i)]);
     }
-  }, 1024);
-  res.reserve(reached.size());
-  for (size_t k = 0; k < reached.size(); ++k) res.emplace(csr_.names[reached[k]], std::move(recs[k]));
-  return res;
+  return out;
+}
+
+SpfResult::SpfResult(std::shared_ptr<const SpfRows> rows) : rows_(std::move(rows)) {
+  const auto& d = rows_->dist;
+  size_t n = 0;
+  for (const uint32_t x : d) n += x != kInf;
+  reached_.reserve(n);
+  for (uint32_t v = 0; v < (uint32_t)d.size(); ++v)
+    if (d[v] != kInf) reached_.push_back(v);
+  slot_ = std::make_unique<std::atomic<value_type*>[]>(n);  // value-initialised: null
+}
+
+SpfResult::SpfResult(SpfResult&& o) noexcept
+    : map_(std::move(o.map_)), rows_(std::move(o.rows_)), reached_(std::move(o.reached_)),
+      slot_(std::move(o.slot_)) {
+  o.reached_.clear();
+}
+
+SpfResult& SpfResult::operator=(SpfResult&& o) noexcept {
+  if (this != &o) {
+    release();
+    map_ = std::move(o.map_);
+    rows_ = std::move(o.rows_);
+    reached_ = std::move(o.reached_);
+    slot_ = std::move(o.slot_);
+    o.reached_.clear();
+  }
+  return *this;
+}
+
+void SpfResult::release() {
+  if (slot_)
+    for (size_t k = 0; k < reached_.size(); ++k) delete slot_[k].load(std::memory_order_relaxed);
+  slot_.reset();
+}
+
+const SpfResult::value_type& SpfResult::entry(size_t k) const {
+  value_type* p = slot_[k].load(std::memory_order_acquire);
+  if (p) return *p;
+  const uint32_t v = reached_[k];
+  auto* fresh = new value_type(std::piecewise_construct, std::forward_as_tuple(rows_->csr->names[v]),
+                               std::forward_as_tuple(NodeSpfResult(rows_->dist[v], rows_.get(), v)));
+  if (slot_[k].compare_exchange_strong(p, fresh, std::memory_order_acq_rel)) return *fresh;
+  delete fresh;  // another thread made it first
+  return *p;
+}
+
+SpfResult::const_iterator SpfResult::begin() const {
+  const_iterator it;
+  it.r_ = this;
+  if (!rows_) it.m_ = map_.begin();
+  return it;
+}
+
+SpfResult::const_iterator SpfResult::end() const {
+  const_iterator it;
+  it.r_ = this;
+  if (rows_) it.k_ = reached_.size();
+  else it.m_ = map_.end();
+  return it;
+}
+
+SpfResult::const_iterator SpfResult::find(const std::string& node) const {
+  if (!rows_) {
+    const_iterator it;
+    it.r_ = this;
+    it.m_ = map_.find(node);
+    return it;
+  }
+  const auto& ids = rows_->csr->ids;
+  auto id = ids.find(node);
+  if (id == ids.end() || rows_->dist[id->second] == kInf) return end();
+  const_iterator it;
+  it.r_ = this;
+  it.k_ = (size_t)(std::lower_bound(reached_.begin(), reached_.end(), id->second) - reached_.begin());
+  return it;
+}
+
+const NodeSpfResult& SpfResult::at(const std::string& node) const {
+  auto it = find(node);
+  if (it == end()) throw std::out_of_range("SpfResult::at: " + node);
+  return it->second;
+}
+
+std::vector<uint32_t> LinkState::nbrsOf(uint32_t root) const {
+  std::vector<uint32_t> out;
+  for (uint32_t e = csr_->rowPtr[root]; e < csr_->rowPtr[root + 1]; ++e) {
+    const uint32_t v = csr_->col[e];
+    if (v != root && (out.empty() || out.back() != v)) out.push_back(v);
+  }
+  return out;
 }
 
 const SpfResult& LinkState::getSpfResult(const std::string& node, bool useLinkMetric) {
@@ -884,12 +975,12 @@ void LinkState::prefetchSpf(const std::vector<std::string>& roots, bool useLinkM
   size_t pending = 0;
   for (const auto& r : roots) {
     if (memo.count(r) || !queued.insert(r).second) continue;
-    auto id = csr_.ids.find(r);
-    if (id == csr_.ids.end()) {  // no adjacency DB: only the root itself
+    auto id = csr_->ids.find(r);
+    if (id == csr_->ids.end()) {  // no adjacency DB: only the root itself
       ++spfRuns_;
-      SpfResult res;
+      SpfResult::Map res;
       res.emplace(r, NodeSpfResult(0));
-      memo.emplace(r, std::move(res));
+      memo.emplace(r, SpfResult(std::move(res)));
       continue;
     }
     if (useLinkMetric && hostMetric_) {
@@ -900,7 +991,7 @@ void LinkState::prefetchSpf(const std::vector<std::string>& roots, bool useLinkM
     byW[nhWordsFor(id->second)].push_back(id->second);
     ++pending;
   }
-  const size_t V = csr_.names.size();
+  const size_t V = csr_->names.size();
   // most of the nodes asked for: one all-sources sweep, rows copied from it
   if (!sweepHas(useLinkMetric) && pending >= kSweepMinRoots && 2 * pending >= V)
     prefetchAllSources(useLinkMetric);
@@ -918,11 +1009,15 @@ void LinkState::prefetchSpf(const std::vector<std::string>& roots, bool useLinkM
         runBatch(part, nullptr, useLinkMetric, OSPF_WANT_DIST | OSPF_WANT_NH, W, &dist, &nh, nullptr);
       const auto t1 = std::chrono::steady_clock::now();
       for (size_t i = 0; i < part.size(); ++i) {
-        RawRun run{part[i], std::vector<uint32_t>(dist.begin() + i * V, dist.begin() + (i + 1) * V), {}};
-        SpfResult res = buildResult(run, nh.data() + i * V * W, W, useLinkMetric);
-        const std::string& name = csr_.names[part[i]];
-        memo.emplace(name, std::move(res));
-        if (useLinkMetric) rawMetric_.emplace(name, std::move(run));
+        auto rows = std::make_shared<SpfRows>();
+        rows->csr = csr_;
+        rows->root = part[i];
+        rows->W = W;
+        rows->useLinkMetric = useLinkMetric;
+        rows->dist.assign(dist.begin() + i * V, dist.begin() + (i + 1) * V);
+        rows->nh.assign(nh.begin() + i * V * W, nh.begin() + (i + 1) * V * W);
+        rows->nbrs = nbrsOf(part[i]);
+        memo.emplace(csr_->names[part[i]], SpfResult(std::move(rows)));
       }
       if (getenv("ODL_SPF_TIMING")) {
         const auto t2 = std::chrono::steady_clock::now();
@@ -943,8 +1038,8 @@ std::vector<ospf_digest> LinkState::spfDigests(const std::vector<std::string>& r
   uint32_t W = 1;
   for (size_t i = 0; i < roots.size(); ++i) {
     ++spfRuns_;
-    auto id = csr_.ids.find(roots[i]);
-    if (id == csr_.ids.end()) {
+    auto id = csr_->ids.find(roots[i]);
+    if (id == csr_->ids.end()) {
       // root without a database: result {root: 0}; node_term(0xFFFFFFFF, 0)
       uint64_t x = (0xFFFFFFFFull << 32);
       x ^= x >> 30;
@@ -980,27 +1075,26 @@ std::optional<Metric> LinkState::getMetricFromAToB(const std::string& a, const s
   return it->second.metric();
 }
 
-const LinkState::RawRun& LinkState::rawSpf(const std::string& node) {
-  getSpfResult(node, true);
+std::shared_ptr<const SpfRows> LinkState::rawSpf(const std::string& node) {
+  const SpfResult& r = getSpfResult(node, true);
+  if (r.rows()) return r.rows();
+  // a memoised result without engine rows: re-derive the distances (not a
+  // new logical runSpf)
   snapshot();
-  auto it = rawMetric_.find(node);
-  if (it == rawMetric_.end()) {
-    // node ids moved under a memoised result (a non-topology update added or
-    // removed a node): re-derive the arrays; not a new logical runSpf.
-    const uint32_t s = csr_.ids.at(node);
-    std::vector<uint32_t> dist;
-    runBatch({s}, nullptr, true, OSPF_WANT_DIST, nhWordsFor(s), &dist, nullptr, nullptr);
-    it = rawMetric_.emplace(node, RawRun{s, std::move(dist), {}}).first;
-  }
-  return it->second;
+  const uint32_t s = csr_->ids.at(node);
+  auto rows = std::make_shared<SpfRows>();
+  rows->csr = csr_;
+  rows->root = s;
+  runBatch({s}, nullptr, true, OSPF_WANT_DIST, nhWordsFor(s), &rows->dist, nullptr, nullptr);
+  return rows;
 }
 
-std::optional<Path> LinkState::trace(const RawRun& run, uint32_t src, uint32_t x,
+std::optional<Path> LinkState::trace(const SpfRows& run, uint32_t src, uint32_t x,
                                      std::unordered_set<const Link*>& seen) const {
   if (x == src) return Path{};
-  for (const auto& pl : pathLinksOf(run, x, true)) {
+  for (const auto& pl : run.pathLinksOf(x)) {
     if (!seen.insert(pl.link.get()).second) continue;
-    auto p = trace(run, src, csr_.ids.at(pl.prevNode), seen);
+    auto p = trace(run, src, run.csr->ids.at(pl.prevNode), seen);
     if (p) {
       p->push_back(pl.link);
       return p;
@@ -1009,7 +1103,7 @@ std::optional<Path> LinkState::trace(const RawRun& run, uint32_t src, uint32_t x
   return std::nullopt;
 }
 
-std::vector<Path> LinkState::tracePaths(const RawRun& run, uint32_t src, uint32_t dst) const {
+std::vector<Path> LinkState::tracePaths(const SpfRows& run, uint32_t src, uint32_t dst) const {
   std::vector<Path> out;
   if (run.dist[dst] == kInf) return out;
   std::unordered_set<const Link*> seen;
@@ -1050,14 +1144,14 @@ const std::vector<Path>& LinkState::getKthPaths(const std::string& src, const st
     }
   } else if (skip.empty()) {
     const SpfResult& r = getSpfResult(src, true);
-    if (r.count(dst) && csr_.ids.count(src)) {
-      const RawRun& run = rawSpf(src);
-      paths = tracePaths(run, csr_.ids.at(src), csr_.ids.at(dst));
+    if (r.count(dst) && csr_->ids.count(src)) {
+      const auto run = rawSpf(src);
+      paths = tracePaths(*run, run->csr->ids.at(src), run->csr->ids.at(dst));
     }
   } else {
     ++spfRuns_;
     snapshot();
-    const uint32_t s = csr_.ids.at(src);
+    const uint32_t s = csr_->ids.at(src);
     std::vector<uint32_t> ign;
     for (const auto& l : skip) ign.push_back(linkIdOf(*l));
     std::sort(ign.begin(), ign.end());
@@ -1080,7 +1174,7 @@ const std::vector<Path>& LinkState::getKthPaths(const std::string& src, const st
         engineVersion_ = 0;
         throw EngineError(rc, m);
       }
-      dist.assign(V_of(csr_), kInf);
+      dist.assign(V_of(*csr_), kInf);
       rc = ospf_sssp_batch(engine_, &s, 1, nullptr, OSPF_WANT_DIST, nhWordsFor(s), dist.data(),
                            nullptr, nullptr);
       const std::string m = rc != OSPF_OK ? ospf_last_error(engine_) : "";
@@ -1090,9 +1184,13 @@ const std::vector<Path>& LinkState::getKthPaths(const std::string& src, const st
         throw EngineError(rc != OSPF_OK ? rc : rc2, rc != OSPF_OK ? m : ospf_last_error(engine_));
       }
     }
-    RawRun run{s, std::move(dist), std::move(ign)};
-    auto d = csr_.ids.find(dst);
-    if (d != csr_.ids.end()) paths = tracePaths(run, s, d->second);
+    SpfRows run;
+    run.csr = csr_;
+    run.root = s;
+    run.dist = std::move(dist);
+    run.ignored = std::move(ign);
+    auto d = csr_->ids.find(dst);
+    if (d != csr_->ids.end()) paths = tracePaths(run, s, d->second);
   }
   return memoKsp_.emplace(key, std::move(paths)).first->second;
 }
@@ -1103,14 +1201,14 @@ void LinkState::prefetchKsp2(const std::string& src, const std::vector<std::stri
     for (const auto& d : dsts) getKthPaths(src, d, 2);
     return;
   }
-  auto sid = csr_.ids.find(src);
+  auto sid = csr_->ids.find(src);
   std::vector<uint32_t> ids;
   std::vector<const std::string*> names;
   std::unordered_set<std::string> queued;
   for (const auto& d : dsts) {
     if (memoKsp_.count(kspKey(src, d, 2)) || !queued.insert(d).second) continue;
-    auto did = csr_.ids.find(d);
-    if (sid == csr_.ids.end() || did == csr_.ids.end()) {
+    auto did = csr_->ids.find(d);
+    if (sid == csr_->ids.end() || did == csr_->ids.end()) {
       getKthPaths(src, d, 2);  // a side without an adjacency DB: no paths, host
       continue;
     }
@@ -1143,7 +1241,7 @@ void LinkState::prefetchKsp2(const std::string& src, const std::vector<std::stri
     for (uint32_t p = 0, q = 1; p < rec[0]; ++p) {
       const uint32_t len = rec[q];
       paths[p].reserve(len);
-      for (uint32_t j = 0; j < len; ++j) paths[p].push_back(csr_.links.at(rec[q + 1 + j]));
+      for (uint32_t j = 0; j < len; ++j) paths[p].push_back(csr_->links.at(rec[q + 1 + j]));
       q += 1 + len;
     }
     return paths;
@@ -1196,7 +1294,6 @@ void LinkState::applyIncremental(const std::vector<LinkDelta>& links,
     auto& memo = mode == 0 ? memoMetric_ : memoHops_;
     for (auto it = memo.begin(); it != memo.end();) {
       if (affected(it->first, it->second, mode == 1)) {
-        if (mode == 0) rawMetric_.erase(it->first);
         it = memo.erase(it);
         ++incStats_.dropped;
       } else {
@@ -1217,26 +1314,35 @@ void LinkState::patchGraph(const std::vector<LinkDelta>& links,
   for (const auto& d : links) {
     const Link& l = *d.link;
     const uint32_t lid = linkIdOf(l);
-    const uint32_t lo = csr_.ids.at(l.lowNode());
+    const uint32_t lo = csr_->ids.at(l.lowNode());
     auto clamp = [](Metric m) { return (m >= 1 && m <= 0xFFFFFFFFull) ? (uint32_t)m : 0u; };
     const uint32_t mlo = clamp(l.metricFrom(l.lowNode())), mhi = clamp(l.metricFrom(l.highNode()));
-    for (uint32_t e = csr_.rowPtr[lo]; e < csr_.rowPtr[lo + 1]; ++e) {
-      if (csr_.linkId[e] != lid) continue;
-      const uint32_t t = csr_.twin[e];
-      csr_.metric[e] = mlo;
-      csr_.metric[t] = mhi;
-      csr_.edgeUp[e] = csr_.edgeUp[t] = l.isUp() ? 1 : 0;
+    for (uint32_t e = csr_->rowPtr[lo]; e < csr_->rowPtr[lo + 1]; ++e) {
+      if (csr_->linkId[e] != lid) continue;
+      const uint32_t t = csr_->twin[e];
+      csr_->metric[e] = mlo;
+      csr_->metric[t] = mhi;
+      csr_->edgeUp[e] = csr_->edgeUp[t] = l.isUp() ? 1 : 0;
       break;
     }
     ups.push_back(ospf_link_update{lid, l.isUp() ? 1u : 0u, mlo, mhi});
+    for (const std::string* n : {&l.lowNode(), &l.highNode()}) {  // largest in-range out-metric
+      const uint32_t u = csr_->ids.at(*n);
+      uint64_t mx = 0;
+      for (const auto& x : linksFromNode(*n)) {
+        const Metric m = x->metricFrom(*n);
+        if (m >= 1 && m <= 0xFFFFFFFFull) mx = std::max<uint64_t>(mx, m);
+      }
+      csr_->rowMax[u] = mx;
+    }
   }
   std::vector<uint32_t> nids;
   std::vector<uint8_t> nts;
   for (const auto& x : nodes) {
-    const uint32_t id = csr_.ids.at(x);
-    csr_.noTransit[id] = isNodeOverloaded(x) ? 1 : 0;
+    const uint32_t id = csr_->ids.at(x);
+    csr_->noTransit[id] = isNodeOverloaded(x) ? 1 : 0;
     nids.push_back(id);
-    nts.push_back(csr_.noTransit[id]);
+    nts.push_back(csr_->noTransit[id]);
   }
   const bool inSync = engine_ && engineVersion_ == snapVersion_;
   ++version_;
@@ -1256,6 +1362,183 @@ void LinkState::patchGraph(const std::vector<LinkDelta>& links,
     }
     engineVersion_ = snapVersion_;
   }
+}
+
+// Links added / removed between known nodes, in place (LinkState.cpp:632-657
+// [LINK UP] / [LINK DOWN]; node ids stay). The rows of the links' ends are
+// rebuilt from their LinkSets (a set's iteration order -- the link ranks --
+// may change on an insert), the arrays between them move as blocks, twins are
+// remapped, and the engine patches the same rows (ospf_update_rows). O(E)
+// block moves on host threads, no re-snapshot, no device reload.
+void LinkState::patchStructure(const std::vector<LinkPtr>& added,
+                               const std::vector<LinkPtr>& removed) {
+  // a kept memoised result reads this snapshot's ranks lazily: give it its own
+  if (csr_.use_count() > 1) csr_ = std::make_shared<Csr>(*csr_);
+  Csr& c = *csr_;
+  const uint32_t V = (uint32_t)c.names.size();
+  std::vector<uint32_t> rows;
+  for (const auto* set : {&added, &removed})
+    for (const auto& l : *set) {
+      rows.push_back(c.ids.at(l->lowNode()));
+      rows.push_back(c.ids.at(l->highNode()));
+    }
+  std::sort(rows.begin(), rows.end());
+  rows.erase(std::unique(rows.begin(), rows.end()), rows.end());
+  for (const auto& l : removed) {
+    const uint32_t lid = linkIdOf(*l);
+    c.links[lid] = nullptr;
+    c.freeLids.push_back(lid);
+  }
+  std::sort(c.freeLids.begin(), c.freeLids.end(), std::greater<uint32_t>());
+  for (const auto& l : added) {
+    uint32_t lid;
+    if (!c.freeLids.empty()) {  // the smallest retired id
+      lid = c.freeLids.back();
+      c.freeLids.pop_back();
+    } else {
+      lid = (uint32_t)c.links.size();
+      c.links.emplace_back();
+    }
+    c.links[lid] = l;
+    l->snapLid = lid;
+  }
+  // the new rows, (neighbour id, rank) order
+  struct Ent {
+    uint32_t v, rank, metric, lid;
+    uint8_t up;
+  };
+  const size_t K = rows.size();
+  std::vector<std::vector<Ent>> nrow(K);
+  for (size_t k = 0; k < K; ++k) {
+    const uint32_t u = rows[k];
+    const std::string& un = c.names[u];
+    uint32_t rank = 0;
+    uint64_t mx = 0;
+    for (const auto& l : linksFromNode(un)) {
+      const Metric m = l->metricOfEnd(l->endIndex(un));
+      const bool inRange = m >= 1 && m <= 0xFFFFFFFFull;
+      mx = std::max<uint64_t>(mx, inRange ? m : 0);
+      nrow[k].push_back(Ent{c.ids.at(l->otherNode(un)), rank++, inRange ? (uint32_t)m : 1u,
+                            l->snapLid, (uint8_t)(l->isUp() ? 1 : 0)});
+    }
+    std::sort(nrow[k].begin(), nrow[k].end(), [](const Ent& a, const Ent& b) {
+      return a.v != b.v ? a.v < b.v : a.rank < b.rank;
+    });
+    c.rowMax[u] = mx;
+  }
+  // offsets: segment s (0..K) = the unchanged rows between changed rows
+  // s - 1 and s, moved by shift[s]
+  const std::vector<uint32_t> old = c.rowPtr;
+  const size_t E0 = old[V];
+  std::vector<int64_t> shift(K + 1, 0);
+  for (size_t k = 0; k < K; ++k)
+    shift[k + 1] = shift[k] + (int64_t)nrow[k].size() - (int64_t)(old[rows[k] + 1] - old[rows[k]]);
+  const size_t E1 = (size_t)((int64_t)E0 + shift[K]);
+  for (uint32_t u = 0, k = 0; u < V; ++u) {
+    const bool ch = k < K && rows[k] == u;
+    c.rowPtr[u + 1] = c.rowPtr[u] + (ch ? (uint32_t)nrow[k++].size() : old[u + 1] - old[u]);
+  }
+  auto segLo = [&](size_t s) { return s == 0 ? (size_t)0 : (size_t)old[rows[s - 1] + 1]; };
+  auto segHi = [&](size_t s) { return s == K ? E0 : (size_t)old[rows[s]]; };
+  auto move = [&](auto& a) {
+    using T = typename std::decay_t<decltype(a)>::value_type;
+    if (E1 > E0) a.resize(E1);
+    for (size_t s = 1; s <= K; ++s)  // leftwards first, in order
+      if (shift[s] < 0 && segHi(s) > segLo(s))
+        std::memmove(a.data() + (int64_t)segLo(s) + shift[s], a.data() + segLo(s),
+                     (segHi(s) - segLo(s)) * sizeof(T));
+    for (size_t s = K; s >= 1; --s)  // then rightwards, from the end
+      if (shift[s] > 0 && segHi(s) > segLo(s))
+        std::memmove(a.data() + (int64_t)segLo(s) + shift[s], a.data() + segLo(s),
+                     (segHi(s) - segLo(s)) * sizeof(T));
+    if (E1 < E0) a.resize(E1);
+  };
+  std::vector<std::function<void()>> jobs = {[&] { move(c.col); }, [&] { move(c.metric); },
+                                            [&] { move(c.linkId); }, [&] { move(c.twin); },
+                                            [&] { move(c.linkRank); }, [&] { move(c.edgeUp); }};
+  parallelFor((uint32_t)jobs.size(), [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t j = lo; j < hi; ++j) jobs[j]();
+  }, 1);
+  // the rebuilt rows
+  for (size_t k = 0; k < K; ++k) {
+    size_t e = c.rowPtr[rows[k]];
+    for (const Ent& x : nrow[k]) {
+      c.col[e] = x.v;
+      c.metric[e] = x.metric;
+      c.linkId[e] = x.lid;
+      c.linkRank[e] = x.rank;
+      c.edgeUp[e] = x.up;
+      c.twin[e] = kInf;
+      ++e;
+    }
+  }
+  // twins of unchanged entries: an old position in a segment moves with it;
+  // one inside a changed row is set from that row below
+  std::vector<uint32_t> starts(K);
+  for (size_t k = 0; k < K; ++k) starts[k] = old[rows[k]];
+  auto remap = [&](uint32_t t) -> uint32_t {
+    const size_t i = (size_t)(std::upper_bound(starts.begin(), starts.end(), t) - starts.begin());
+    if (i > 0 && t < old[rows[i - 1] + 1]) return kInf;  // inside changed row i - 1
+    return (uint32_t)((int64_t)t + shift[i]);
+  };
+  for (size_t s = 0; s <= K; ++s) {
+    const size_t lo = (size_t)((int64_t)segLo(s) + shift[s]), hi = (size_t)((int64_t)segHi(s) + shift[s]);
+    if (hi <= lo) continue;
+    parallelFor((uint32_t)(hi - lo), [&](uint32_t a, uint32_t b) {
+      for (size_t e = lo + a; e < lo + b; ++e) c.twin[e] = remap(c.twin[e]);
+    }, 1u << 16);
+  }
+  for (size_t k = 0; k < K; ++k) {
+    const uint32_t u = rows[k];
+    for (size_t e = c.rowPtr[u]; e < c.rowPtr[u + 1]; ++e) {
+      if (c.twin[e] != kInf) continue;  // set from the partner row already
+      const uint32_t x = c.col[e], lid = c.linkId[e];
+      size_t q = c.rowPtr[x];
+      while (q < c.rowPtr[x + 1] && !(c.linkId[q] == lid && q != e)) ++q;
+      if (q == c.rowPtr[x + 1]) throw std::logic_error("patchStructure: link without a twin");
+      c.twin[e] = (uint32_t)q;
+      c.twin[q] = (uint32_t)e;
+    }
+  }
+  uint64_t bound = 0;
+  for (uint32_t u = 0; u < V; ++u) bound = std::min<uint64_t>(bound + c.rowMax[u], ~0ull >> 1);
+  distBound_ = bound;
+  ++topoStats_.link_patches;
+  topoStats_.rows_patched += K;
+  const bool inSync = engine_ && engineVersion_ == snapVersion_;
+  ++version_;
+  snapVersion_ = version_;
+  dropSweep();  // its rows describe the graph before the patch
+  if (inSync) patchEngineRows(rows);
+}
+
+void LinkState::patchEngineRows(const std::vector<uint32_t>& rows) {
+  const Csr& c = *csr_;
+  ospf_csr g{};
+  g.n_nodes = (uint32_t)c.names.size();
+  g.n_edges = (uint32_t)c.col.size();
+  g.row_ptr = c.rowPtr.data();
+  g.col = c.col.data();
+  g.metric = c.metric.data();
+  g.link_id = c.linkId.data();
+  g.twin = c.twin.data();
+  g.edge_up = c.edgeUp.data();
+  g.no_transit = c.noTransit.data();
+  g.link_rank = c.linkRank.data();
+  const uint32_t nctx = multi_ ? ospf_multi_size(multi_) : 1u;
+  for (uint32_t i = 0; i < nctx; ++i) {
+    ospf_ctx* x = multi_ ? ospf_multi_ctx(multi_, i) : engine_;
+    const int rc = ospf_update_rows(x, &g, rows.data(), (uint32_t)rows.size(), snapVersion_);
+    if (rc == OSPF_E_RANGE) {  // the device layout's reserve is spent: reload
+      engineVersion_ = 0;
+      return;
+    }
+    if (rc != OSPF_OK) {
+      engineVersion_ = 0;  // reload every device on the next use
+      throw EngineError(rc, ospf_last_error(x));
+    }
+  }
+  engineVersion_ = snapVersion_;
 }
 
 void NodeUcmpResult::normalizeNextHopWeights() {
@@ -1334,7 +1617,7 @@ SpfResult LinkState::runSpfHost(const std::string& root, bool useLinkMetric,
   // Dijkstra with the reference's queue order -- (metric, name), keys only
   // ever lowered by a strictly better path -- and its u64 arithmetic, so a
   // wrapped negative metric behaves exactly as there.
-  SpfResult done;
+  SpfResult::Map done;
   std::unordered_map<std::string, NodeSpfResult> open;
   std::set<std::pair<Metric, std::string>> order;
   open.emplace(root, NodeSpfResult(0));
@@ -1367,7 +1650,7 @@ SpfResult LinkState::runSpfHost(const std::string& root, bool useLinkMetric,
       if (o.nextHops_.empty()) o.nextHops_.insert(other);  // a neighbour of the root
     }
   }
-  return done;
+  return SpfResult(std::move(done));
 }
 
 std::vector<Path> LinkState::tracePathsHost(const SpfResult& res, const std::string& src,
@@ -1403,18 +1686,18 @@ ospf_digest LinkState::digestHost(const std::string& root, const SpfResult& res)
     x ^= x >> 31;
     return x;
   };
-  const uint32_t r = csr_.ids.at(root);
+  const uint32_t r = csr_->ids.at(root);
   std::unordered_map<std::string, uint32_t> bit;
-  for (uint32_t e = csr_.rowPtr[r]; e < csr_.rowPtr[r + 1]; ++e) {
-    const uint32_t v = csr_.col[e];
-    if (v != r && !bit.count(csr_.names[v])) {
+  for (uint32_t e = csr_->rowPtr[r]; e < csr_->rowPtr[r + 1]; ++e) {
+    const uint32_t v = csr_->col[e];
+    if (v != r && !bit.count(csr_->names[v])) {
       const uint32_t i = (uint32_t)bit.size();
-      bit.emplace(csr_.names[v], i);
+      bit.emplace(csr_->names[v], i);
     }
   }
   ospf_digest d{0, 0, 0};
   for (const auto& [name, nr] : res) {
-    const uint32_t v = csr_.ids.at(name);
+    const uint32_t v = csr_->ids.at(name);
     const uint64_t kd = mix((uint64_t)v ^ 0x2545F4914F6CDD1DULL) | 1ull;
     const uint64_t kn = mix((uint64_t)v ^ 0xD6E8FEB86659FD93ULL) | 1ull;
     std::map<uint32_t, uint32_t> words;

@@ -21,7 +21,9 @@
 #include <atomic>
 #include <cstdint>
 #include <exception>
+#include <iterator>
 #include <memory>
+#include <mutex>
 #include <thread>
 #include <optional>
 #include <stdexcept>
@@ -149,21 +151,151 @@ struct PathLink {
   std::string prevNode;
 };
 
+// The CSR snapshot the engine sees: node id = rank of the name in byte order,
+// rows sorted by (neighbour id, linkRank), linkRank = position of the link in
+// linksFromNode(row node), link ids handed out on first sight in node order
+// (later: an added link takes a retired id or a new one). Shared with the
+// engine-backed SpfResults made on it (they index its rows).
+struct CsrSnapshot {
+  std::vector<std::string> names;                 // id -> name (sorted)
+  std::unordered_map<std::string, uint32_t> ids;  // name -> id
+  std::vector<uint32_t> rowPtr, col, metric, linkId, twin, linkRank;
+  std::vector<uint8_t> edgeUp, noTransit;
+  std::vector<LinkPtr> links;      // link id -> link (null: a retired id)
+  std::vector<uint32_t> freeLids;  // retired ids, taken again by added links
+  std::vector<uint64_t> rowMax;    // largest in-contract out-metric per node
+};
+
+// One engine run (or KSP2 masked rerun): distance and next-hop rows of the
+// root, kept with the snapshot they index; SpfResult entries are rebuilt from
+// them on first access.
+struct SpfRows {
+  std::shared_ptr<const CsrSnapshot> csr;
+  uint32_t root = 0;
+  uint32_t W = 1;                 // next-hop words per node
+  bool useLinkMetric = true;
+  std::vector<uint32_t> dist;     // [V], OSPF_DIST_INF = unreached
+  std::vector<uint32_t> nh;       // [V][W] (empty: next hops not kept)
+  std::vector<uint32_t> nbrs;     // the root's distinct neighbours = next-hop bit order
+  std::vector<uint32_t> ignored;  // sorted link ids the run ignored
+  // pathLinks of v: every usable tight in-link (l, u), u transit or the root,
+  // in (u's pop order (dist, name), l's position in linksFromNode(u)) order
+  // (LinkState.cpp:885-901)
+  std::vector<PathLink> pathLinksOf(uint32_t v) const;
+  std::unordered_set<std::string> nextHopsOf(uint32_t v) const;
+};
+
+// LinkState::NodeSpfResult (LinkState.h:211-268). A result of the engine
+// keeps only its metric eagerly; nextHops and pathLinks are rebuilt from the
+// run's rows on first access (thread-safe: the route build reads results on
+// host threads), so getSpfResult costs O(V) words, not O(V) hash sets.
 class NodeSpfResult {
  public:
   explicit NodeSpfResult(Metric m) : metric_(m) {}
+  NodeSpfResult(NodeSpfResult&& o) noexcept
+      : metric_(o.metric_), pathLinks_(std::move(o.pathLinks_)), nextHops_(std::move(o.nextHops_)),
+        rows_(o.rows_), node_(o.node_) {}
+  NodeSpfResult& operator=(NodeSpfResult&& o) noexcept {
+    metric_ = o.metric_;
+    pathLinks_ = std::move(o.pathLinks_);
+    nextHops_ = std::move(o.nextHops_);
+    rows_ = o.rows_;
+    node_ = o.node_;
+    return *this;
+  }
+  // a copy is a materialised one
+  NodeSpfResult(const NodeSpfResult& o)
+      : metric_(o.metric_), pathLinks_(o.pathLinks()), nextHops_(o.nextHops()) {}
   Metric metric() const { return metric_; }
-  const std::vector<PathLink>& pathLinks() const { return pathLinks_; }
-  const std::unordered_set<std::string>& nextHops() const { return nextHops_; }
+  const std::vector<PathLink>& pathLinks() const {
+    if (rows_) std::call_once(plOnce_, [this] { pathLinks_ = rows_->pathLinksOf(node_); });
+    return pathLinks_;
+  }
+  const std::unordered_set<std::string>& nextHops() const {
+    if (rows_) std::call_once(nhOnce_, [this] { nextHops_ = rows_->nextHopsOf(node_); });
+    return nextHops_;
+  }
 
  private:
   friend class LinkState;
+  friend class SpfResult;
+  NodeSpfResult(Metric m, const SpfRows* rows, uint32_t node) : metric_(m), rows_(rows), node_(node) {}
   Metric metric_;
-  std::vector<PathLink> pathLinks_;
-  std::unordered_set<std::string> nextHops_;
+  mutable std::vector<PathLink> pathLinks_;
+  mutable std::unordered_set<std::string> nextHops_;
+  const SpfRows* rows_ = nullptr;  // lazy: the run's rows (owned by the SpfResult)
+  uint32_t node_ = 0;
+  mutable std::once_flag plOnce_, nhOnce_;
 };
 
-using SpfResult = std::unordered_map<std::string, NodeSpfResult>;
+// LinkState::SpfResult (LinkState.h:267-268: unordered_map<string,
+// NodeSpfResult>) with the map's read interface -- find / count / at / size /
+// iteration over (name, NodeSpfResult) pairs. A host-path result is a map; an
+// engine result holds the run's rows and makes an entry the first time it is
+// looked up or iterated over (iteration in node id = name order).
+class SpfResult {
+ public:
+  using value_type = std::pair<const std::string, NodeSpfResult>;
+  using Map = std::unordered_map<std::string, NodeSpfResult>;
+  class const_iterator {
+   public:
+    using iterator_category = std::forward_iterator_tag;
+    using value_type = SpfResult::value_type;
+    using difference_type = std::ptrdiff_t;
+    using pointer = const value_type*;
+    using reference = const value_type&;
+    const_iterator() = default;
+    reference operator*() const { return r_->rows_ ? r_->entry(k_) : *m_; }
+    pointer operator->() const { return &**this; }
+    const_iterator& operator++() {
+      if (r_->rows_) ++k_;
+      else ++m_;
+      return *this;
+    }
+    const_iterator operator++(int) {
+      const_iterator t = *this;
+      ++*this;
+      return t;
+    }
+    bool operator==(const const_iterator& o) const { return r_ == o.r_ && k_ == o.k_ && m_ == o.m_; }
+    bool operator!=(const const_iterator& o) const { return !(*this == o); }
+
+   private:
+    friend class SpfResult;
+    const SpfResult* r_ = nullptr;
+    Map::const_iterator m_{};
+    size_t k_ = 0;
+  };
+  using iterator = const_iterator;
+
+  SpfResult() = default;
+  explicit SpfResult(Map&& m) : map_(std::move(m)) {}
+  explicit SpfResult(std::shared_ptr<const SpfRows> rows);
+  SpfResult(SpfResult&& o) noexcept;
+  SpfResult& operator=(SpfResult&& o) noexcept;
+  SpfResult(const SpfResult&) = delete;
+  SpfResult& operator=(const SpfResult&) = delete;
+  ~SpfResult() { release(); }
+
+  size_t size() const { return rows_ ? reached_.size() : map_.size(); }
+  bool empty() const { return size() == 0; }
+  const_iterator begin() const;
+  const_iterator end() const;
+  const_iterator find(const std::string& node) const;
+  size_t count(const std::string& node) const { return find(node) != end() ? 1 : 0; }
+  const NodeSpfResult& at(const std::string& node) const;
+  // the engine run behind the result (null for a host-path result)
+  const std::shared_ptr<const SpfRows>& rows() const { return rows_; }
+
+ private:
+  const value_type& entry(size_t k) const;  // reached_[k]'s entry, made on first use
+  void release();
+  Map map_;
+  std::shared_ptr<const SpfRows> rows_;
+  std::vector<uint32_t> reached_;  // reached node ids, ascending
+  std::unique_ptr<std::atomic<value_type*>[]> slot_;  // [reached_.size()]
+};
+
 using Path = std::vector<LinkPtr>;
 
 // thrift::PrefixForwardingAlgorithm values of the two UCMP algorithms
@@ -298,13 +430,7 @@ class LinkState {
   const IncrementalStats& incrementalStats() const { return incStats_; }
 
   // ---- CSR snapshot (what the engine sees) ----
-  struct Csr {
-    std::vector<std::string> names;                 // id -> name (sorted)
-    std::unordered_map<std::string, uint32_t> ids;  // name -> id
-    std::vector<uint32_t> rowPtr, col, metric, linkId, twin, linkRank;
-    std::vector<uint8_t> edgeUp, noTransit;
-    std::vector<LinkPtr> links;                     // link id -> link
-  };
+  using Csr = CsrSnapshot;
   const Csr& snapshot();
   uint32_t linkIdOf(const Link& l) const;  // id in the current snapshot
   // true when the current snapshot is outside the engine's metric contract:
@@ -314,19 +440,24 @@ class LinkState {
     snapshot();
     return hostMetric_;
   }
+  // Links added or removed between known nodes ([LINK UP] / [LINK DOWN],
+  // LinkState.cpp:632-657) patch the snapshot and the device graph in place
+  // (ospf_update_rows) instead of a new snapshot and device load.
+  struct TopologyStats {
+    uint64_t snapshots = 0;     // whole CSR snapshots taken
+    uint64_t loads = 0;         // whole device graph loads
+    uint64_t link_patches = 0;  // updates patched in place with links added / removed
+    uint64_t rows_patched = 0;  // CSR rows rebuilt by them
+  };
+  const TopologyStats& topologyStats() const { return topoStats_; }
 
  private:
-  struct RawRun {  // one engine run kept for pathLinks / trace reconstruction
-    uint32_t root;
-    std::vector<uint32_t> dist;
-    std::vector<uint32_t> ignored;  // sorted link ids
-  };
-
   LinkPtr makeLink(const std::string& node, const Adjacency& adj) const;
   void addLink(const LinkPtr& l);
   void removeLink(const LinkPtr& l);
   std::vector<LinkPtr> sortedLinksOf(const std::string& node) const;
   void invalidate();
+  void clearMemo();
   void ensureEngine();
   void dropSweep();
   bool sweepHas(bool useLinkMetric) const;
@@ -334,15 +465,16 @@ class LinkState {
   void sweepRows(const std::vector<uint32_t>& roots, uint32_t W, std::vector<uint32_t>& dist,
                  std::vector<uint32_t>& nh);
   uint32_t nhWordsFor(uint32_t root) const;
+  std::vector<uint32_t> nbrsOf(uint32_t root) const;  // distinct neighbours (bit order)
   void runBatch(const std::vector<uint32_t>& roots, const std::vector<std::vector<uint32_t>>* ign,
                 bool useLinkMetric, uint32_t flags, uint32_t W, std::vector<uint32_t>* dist,
                 std::vector<uint32_t>* nh, std::vector<ospf_digest>* dig);
-  SpfResult buildResult(const RawRun& run, const uint32_t* nh, uint32_t W, bool useLinkMetric);
-  std::vector<PathLink> pathLinksOf(const RawRun& run, uint32_t v, bool useLinkMetric) const;
-  std::optional<Path> trace(const RawRun& run, uint32_t src, uint32_t x,
+  std::optional<Path> trace(const SpfRows& run, uint32_t src, uint32_t x,
                             std::unordered_set<const Link*>& seen) const;
-  std::vector<Path> tracePaths(const RawRun& run, uint32_t src, uint32_t dst) const;
-  const RawRun& rawSpf(const std::string& node);
+  std::vector<Path> tracePaths(const SpfRows& run, uint32_t src, uint32_t dst) const;
+  // the engine rows of getSpfResult(node, true) (the memo's, or a re-run
+  // when the memoised result came from another snapshot)
+  std::shared_ptr<const SpfRows> rawSpf(const std::string& node);
   // LinkState::runSpf (LinkState.cpp:836-911) on the host, u64 metrics with
   // the reference's wrap-around, for graphs outside the engine contract
   SpfResult runSpfHost(const std::string& root, bool useLinkMetric,
@@ -356,9 +488,14 @@ class LinkState {
     bool up0;
     Metric mlo0, mhi0;  // metric advertised by lowNode / highNode before
   };
+  // links added / removed between known nodes: the rows of their ends
+  // rebuilt in the snapshot (same node ids), then ospf_update_rows
+  void patchStructure(const std::vector<LinkPtr>& added, const std::vector<LinkPtr>& removed);
   void applyIncremental(const std::vector<LinkDelta>& links,
                         const std::vector<std::string>& nodes);
   void patchGraph(const std::vector<LinkDelta>& links, const std::vector<std::string>& nodes);
+  // links of the rows in `rows` to the engine (ospf_update_rows), or a reload
+  void patchEngineRows(const std::vector<uint32_t>& rows);
 
   std::string area_;
   int device_;
@@ -373,7 +510,8 @@ class LinkState {
   uint64_t engineVersion_ = 0;  // snapshot version loaded into the engine
   uint64_t version_ = 1;        // bumped on every ingest call
   uint64_t snapVersion_ = 0;
-  Csr csr_;
+  std::shared_ptr<Csr> csr_ = std::make_shared<Csr>();
+  TopologyStats topoStats_;
   bool hostMetric_ = false;   // snapshot outside the engine's metric contract
   uint64_t distBound_ = 0;    // >= every simple-path metric sum of the snapshot
   uint64_t spfRuns_ = 0;
@@ -400,7 +538,6 @@ class LinkState {
   std::unordered_map<std::string, std::unordered_map<AdjKey, uint32_t, AdjKeyHash>> adjIndex_;
 
   std::unordered_map<std::string, SpfResult> memoMetric_, memoHops_;
-  std::unordered_map<std::string, RawRun> rawMetric_;  // unmasked runs (useLinkMetric)
   std::unordered_map<std::string, std::vector<Path>> memoKsp_;
 };
 

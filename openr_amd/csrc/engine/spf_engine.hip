@@ -1083,6 +1083,13 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   }
   // entries of each link id (KSP2 ignore masks); ids above 2^28 disable them
   const uint32_t n_lid = (E && max_lid < (1u << 28)) ? max_lid + 1 : 0;
+  // Reserves for structural patches (ospf_update_rows, links added / removed
+  // in place): per-entry arrays, distinct neighbours and link ids get ~3 %
+  // headroom past their current use; an update that outgrows one returns
+  // OSPF_E_RANGE and the caller reloads.
+  auto reserve = [](size_t used) { return used + std::max<size_t>(1024, used / 32); };
+  const size_t cap_e = align_up(reserve(Ep), 4), cap_dn = reserve(dn.size()),
+               cap_lid = n_lid ? reserve(n_lid) : 0;
   std::vector<uint32_t> link_e(std::max<size_t>(2ull * n_lid, 2), 0xFFFFFFFFu);
   for (uint32_t e = 0; e < Ep && n_lid; ++e) {
     if (plink[e] == 0xFFFFFFFFu) continue;
@@ -1132,9 +1139,14 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   size_t off[14], tot = 0;
   const size_t szs[14] = {sz_row, sz_e,     sz_e,  sz_e,   sz_e,  sz_nt,  sz_dnoff,
                           sz_dn,  sz_big,   sz_key, sz_le, sz_ew, sz_didx, sz_kn};
+  // allocated: the per-entry arrays, dn and link_e with their reserves, big
+  // for every node
+  const size_t caps[14] = {sz_row, cap_e * 4, cap_e * 4, cap_e * 4, cap_e * 4, sz_nt, sz_dnoff,
+                           cap_dn * 4, V * 4ull, sz_key, std::max<size_t>(2 * cap_lid, 2) * 4,
+                           ew_ok ? cap_e * 8 : sz_ew, cap_e * 2, sz_kn};
   for (int i = 0; i < 14; ++i) {
     off[i] = tot;
-    tot += align_up(std::max<size_t>(szs[i], 4), 256);
+    tot += align_up(std::max<size_t>(caps[i], 4), 256);
   }
   HIPCHK(c, hipSetDevice(c->device));
   if (c->d_graph) {
@@ -1172,6 +1184,10 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   c->g.didx = (const uint16_t*)(base + off[12]);
   c->g.dkn = (const uint64_t*)(base + off[13]);
   c->ew_base = ew_ok ? (const uint32_t*)(base + off[11]) : nullptr;
+  c->cap_e = cap_e;
+  c->cap_dn = cap_dn;
+  c->cap_lid = cap_lid;
+  c->h_plink = std::move(plink);
   c->h_row_ptr.assign(csr->row_ptr, csr->row_ptr + V + 1);
   c->h_dn_off = std::move(dn_off);
   c->h_dn = std::move(dn);
@@ -2399,6 +2415,340 @@ int ospf_update_nodes(ospf_ctx* c, const uint32_t* nodes, const uint8_t* no_tran
   HIPCHK(c, hipMemcpy((void*)c->g.nt_bits, c->h_nt.data(), c->h_nt.size() * 4ull,
                       hipMemcpyHostToDevice));
   refresh_graph_stats(c, 0, deeper);
+  c->info.version = version;
+  c->cover_ok = false;  // the contracted cover graph describes the old graph
+  ++c->graph_gen;
+  return OSPF_OK;
+}
+
+// Structural patch (include/openr_spf.h). Validation first -- a rejected
+// call leaves the context as it was -- then, with the device idle: rows that
+// outgrow their padded slots move the tail of every per-entry array (device
+// copies through the stage buffer, host shadows by insertion, row offsets and
+// link positions shifted), the rebuilt rows are written into their slots
+// (one scatter launch for every changed word), the distinct-neighbour lists
+// and the planner facts follow.
+int ospf_update_rows(ospf_ctx* c, const ospf_csr* csr, const uint32_t* rows, uint32_t n,
+                     uint64_t version) {
+  if (!c || !csr || (n && !rows)) return OSPF_E_INVAL;
+  if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
+  if (c->mask.on) return fail(c, OSPF_E_INVAL, "update_rows: links are masked (ospf_links_unmask)");
+  const uint32_t V = c->info.n_nodes;
+  if (csr->n_nodes != V) return fail(c, OSPF_E_RANGE, "update_rows: the node count changed (reload)");
+  const uint32_t E = csr->n_edges;
+  if (!csr->row_ptr || (E && (!csr->col || !csr->metric || !csr->link_id || !csr->twin ||
+                              !csr->edge_up)))
+    return fail(c, OSPF_E_INVAL, "null CSR array");
+  if (csr->row_ptr[0] != 0 || csr->row_ptr[V] != E)
+    return fail(c, OSPF_E_INVAL, "row_ptr must start at 0 and end at n_edges");
+  constexpr uint32_t kNo = 0xFFFFFFFFu;
+  const uint32_t* rp = csr->row_ptr;
+  auto row_ok = [&](uint32_t u) { return rp[u] <= rp[u + 1] && rp[u + 1] <= E; };
+  // rows to rebuild: the given ones, and every neighbour holding parallel
+  // links to one of them (their order follows the given row's link ranks)
+  std::vector<uint32_t> R;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t u = rows[i];
+    if (u >= V) return fail(c, OSPF_E_INVAL, "update_rows: row out of range");
+    if (!row_ok(u)) return fail(c, OSPF_E_INVAL, "row_ptr not monotone");
+    R.push_back(u);
+    for (uint32_t e = rp[u] + 1; e < rp[u + 1]; ++e)
+      if (csr->col[e] == csr->col[e - 1] && csr->col[e] != u && csr->col[e] < V) R.push_back(csr->col[e]);
+  }
+  std::sort(R.begin(), R.end());
+  R.erase(std::unique(R.begin(), R.end()), R.end());
+  struct Row {
+    uint32_t u, cap0, len, need, grow;
+    std::vector<uint32_t> colx, w, rw, lid, dn;
+    std::vector<uint16_t> didx;
+  };
+  std::vector<Row> nr(R.size());
+  std::vector<uint8_t> inR(V, 0);
+  for (uint32_t u : R) inR[u] = 1;
+  std::vector<uint32_t> ord;
+  uint32_t new_max = 0, max_deg = c->info.max_degree, max_dn = c->max_dn;
+  size_t grow_tot = 0, dn_tot = c->h_dn.size();
+  std::vector<uint32_t> old_lids, new_lids;
+  for (size_t k = 0; k < R.size(); ++k) {
+    const uint32_t u = R[k], b = rp[u], len = rp[u + 1] - b;
+    if (!row_ok(u)) return fail(c, OSPF_E_INVAL, "row_ptr not monotone");
+    Row& x = nr[k];
+    x.u = u;
+    x.len = len;
+    x.cap0 = c->h_prow[u + 1] - c->h_prow[u];
+    x.need = (len + 3u) & ~3u;
+    x.grow = x.need > x.cap0 ? ((x.need - x.cap0 + 3u) & ~3u) + 8u : 0u;
+    grow_tot += x.grow;
+    max_deg = std::max(max_deg, len);
+    ord.resize(len);
+    for (uint32_t j = 0; j < len; ++j) {
+      const uint32_t e = b + j, v = csr->col[e], t = csr->twin[e];
+      if (v >= V) return fail(c, OSPF_E_INVAL, "col out of range");
+      if (j && csr->col[e - 1] > v) return fail(c, OSPF_E_INVAL, "rows must be sorted by col");
+      if (t >= E || csr->twin[t] != e || csr->col[t] != u || !row_ok(v) || t < rp[v] ||
+          t >= rp[v + 1] || csr->link_id[t] != csr->link_id[e])
+        return fail(c, OSPF_E_INVAL, "twin/link_id inconsistent");
+      if (csr->edge_up[e] != csr->edge_up[t])
+        return fail(c, OSPF_E_INVAL, "edge_up must match on both directions of a link");
+      if (csr->edge_up[e] && (csr->metric[e] == 0 || csr->metric[t] == 0))
+        return fail(c, OSPF_E_RANGE, "metric 0 on a usable link is outside the engine contract");
+      if (csr->link_id[e] >= c->cap_lid)
+        return fail(c, OSPF_E_RANGE, "update_rows: link id past the reserve (reload)");
+      ord[j] = e;
+    }
+    if (csr->link_rank)
+      std::stable_sort(ord.begin(), ord.end(), [&](uint32_t p, uint32_t q) {
+        if (csr->col[p] != csr->col[q]) return csr->col[p] < csr->col[q];
+        return csr->link_rank[csr->twin[p]] < csr->link_rank[csr->twin[q]];
+      });
+    x.colx.assign(x.need, 0x80000000u);
+    x.w.assign(x.need, 0u);
+    x.rw.assign(x.need, 0u);
+    x.lid.assign(x.need, kNo);
+    x.didx.assign(x.need, 0xFFFFu);
+    uint32_t kk = 0, prev = kNo;
+    for (uint32_t j = 0; j < len; ++j) {
+      const uint32_t e = ord[j], v = csr->col[e];
+      const bool up = csr->edge_up[e] != 0;
+      x.colx[j] = v | (up ? 0u : 0x80000000u);
+      x.w[j] = csr->metric[e];
+      x.rw[j] = csr->metric[csr->twin[e]];
+      x.lid[j] = csr->link_id[e];
+      new_lids.push_back(x.lid[j]);
+      if (up) new_max = std::max(new_max, x.w[j]);
+      if (v == u) continue;  // self-loop: no next-hop bit
+      if (prev != kNo && v != prev) ++kk;
+      if (v != prev) x.dn.push_back(v);
+      prev = v;
+      x.didx[j] = (uint16_t)kk;
+    }
+    if (x.dn.size() > OSPF_MAX_ROOT_NEIGHBORS)
+      return fail(c, OSPF_E_RANGE, "a node has more distinct neighbours than OSPF_MAX_ROOT_NEIGHBORS");
+    max_dn = std::max<uint32_t>(max_dn, (uint32_t)x.dn.size());
+    dn_tot += x.dn.size() - (c->h_dn_off[u + 1] - c->h_dn_off[u]);
+    for (uint32_t e = c->h_prow[u]; e < c->h_prow[u + 1]; ++e)
+      if (c->h_plink[e] != kNo) old_lids.push_back(c->h_plink[e]);
+  }
+  const size_t Ep0 = c->h_prow[V];
+  if (Ep0 + grow_tot > c->cap_e)
+    return fail(c, OSPF_E_RANGE, "update_rows: entry reserve exhausted (reload)");
+  if (dn_tot > c->cap_dn) return fail(c, OSPF_E_RANGE, "update_rows: neighbour reserve exhausted (reload)");
+  std::sort(old_lids.begin(), old_lids.end());
+  std::sort(new_lids.begin(), new_lids.end());
+  // a link id new to these rows must be free (retired) before the call
+  for (size_t i = 0; i < new_lids.size(); ++i) {
+    const uint32_t l = new_lids[i];
+    if (i && new_lids[i - 1] == l) continue;
+    if (std::binary_search(old_lids.begin(), old_lids.end(), l)) continue;
+    if (l < c->g.n_lid && (c->h_link_e[2ull * l] != kNo || c->h_link_e[2ull * l + 1] != kNo))
+      return fail(c, OSPF_E_INVAL, "update_rows: an added link's id is still in use");
+  }
+  // transit connectivity the rows gain or lose (level bound, below): a pair
+  // joined by a usable link after but not before, both ends transit, keeps
+  // the bound only when the old graph already connects it
+  auto transit = [&](uint32_t x) { return !((c->h_nt[x >> 5] >> (x & 31)) & 1u); };
+  bool deeper = false;
+  std::vector<std::pair<uint32_t, uint32_t>> lost;
+  for (const Row& x : nr) {
+    if (!transit(x.u)) continue;
+    std::vector<uint32_t> before, after;
+    for (uint32_t e = c->h_prow[x.u]; e < c->h_prow[x.u + 1]; ++e)
+      if (!(c->h_pcolx[e] & 0x80000000u) && transit(c->h_pcolx[e])) before.push_back(c->h_pcolx[e]);
+    for (uint32_t j = 0; j < x.len; ++j)
+      if (!(x.colx[j] & 0x80000000u) && transit(x.colx[j])) after.push_back(x.colx[j]);
+    std::sort(before.begin(), before.end());
+    before.erase(std::unique(before.begin(), before.end()), before.end());
+    std::sort(after.begin(), after.end());
+    after.erase(std::unique(after.begin(), after.end()), after.end());
+    for (uint32_t v : after)
+      if (v > x.u && !std::binary_search(before.begin(), before.end(), v) && !deeper)
+        deeper = transit_detour(c, x.u, v, 1u << 20) == kNo;
+    for (uint32_t v : before)
+      if (v > x.u && !std::binary_search(after.begin(), after.end(), v)) lost.push_back({x.u, v});
+  }
+
+  // ---- commit
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipDeviceSynchronize());  // no batch may be reading the graph
+  uint32_t* base = (uint32_t*)c->d_graph;
+  auto woff = [&](const void* p) { return (size_t)((const char*)p - (const char*)base) / 4; };
+  // positions of the old lids inside rebuilt rows leave link_e (the other
+  // end's position stays when that row is not rebuilt)
+  std::vector<uint32_t> touched;  // link ids whose link_e words change
+  for (const Row& x : nr)
+    for (uint32_t e = c->h_prow[x.u]; e < c->h_prow[x.u + 1]; ++e) {
+      const uint32_t l = c->h_plink[e];
+      if (l == kNo) continue;
+      for (int s = 0; s < 2; ++s)
+        if (c->h_link_e[2ull * l + s] == e) c->h_link_e[2ull * l + s] = kNo;
+      touched.push_back(l);
+    }
+  // grow rows (last first: earlier positions stay put)
+  std::vector<size_t> grow_ix;
+  for (size_t k = 0; k < nr.size(); ++k)
+    if (nr[k].grow) grow_ix.push_back(k);
+  struct Arr {
+    char* p;
+    size_t esz;
+  };
+  std::vector<Arr> arrs = {{(char*)c->g.colx, 4}, {(char*)c->g.w, 4}, {(char*)c->g.rw, 4},
+                           {(char*)c->g.link_id, 4}, {(char*)c->g.didx, 2}};
+  if (c->g.ew) arrs.push_back({(char*)c->ew_base, 8});
+  size_t Ep = Ep0;
+  for (auto it = grow_ix.rbegin(); it != grow_ix.rend(); ++it) {
+    const Row& x = nr[*it];
+    const uint32_t pos = c->h_prow[x.u + 1], d = x.grow;
+    const size_t tail = Ep - pos;
+    if (tail) {
+      int rc = ensure(c, &c->d_stage, &c->stage_bytes, tail * 8);
+      if (rc) return rc;
+      for (const Arr& a : arrs) {
+        HIPCHK(c, hipMemcpy(c->d_stage, a.p + pos * a.esz, tail * a.esz, hipMemcpyDeviceToDevice));
+        HIPCHK(c, hipMemcpy(a.p + ((size_t)pos + d) * a.esz, c->d_stage, tail * a.esz,
+                            hipMemcpyDeviceToDevice));
+      }
+    }
+    c->h_pcolx.insert(c->h_pcolx.begin() + pos, d, 0x80000000u);
+    c->h_pw.insert(c->h_pw.begin() + pos, d, 0u);
+    c->h_prw.insert(c->h_prw.begin() + pos, d, 0u);
+    c->h_plink.insert(c->h_plink.begin() + pos, d, kNo);
+    for (uint32_t v = x.u + 1; v <= V; ++v) c->h_prow[v] += d;
+    for (auto& p : c->h_link_e)
+      if (p != kNo && p >= pos) p += d;
+    hipError_t he = ospf::launch_shift_add(base + woff(c->g.row_ptr), V + 1, x.u + 1, 0u, d, nullptr);
+    if (he == hipSuccess && c->g.n_lid)
+      he = ospf::launch_shift_add(base + woff(c->g.link_e), 2 * c->g.n_lid, 0u, pos, d, nullptr);
+    if (he != hipSuccess) return hip_fail(c, he, "launch_shift_add");
+    Ep += d;
+  }
+  // rebuilt rows into their slots; every changed word through one scatter
+  std::vector<uint32_t> idx, val;
+  auto put = [&](size_t word, uint32_t v) {
+    idx.push_back((uint32_t)word);
+    val.push_back(v);
+  };
+  const size_t o_colx = woff(c->g.colx), o_w = woff(c->g.w), o_rw = woff(c->g.rw),
+               o_lid = woff(c->g.link_id), o_didx = woff(c->g.didx), o_ew = woff(c->ew_base),
+               o_le = woff(c->g.link_e);
+  uint32_t lid_max = c->g.n_lid;
+  bool big_change = false;
+  for (Row& x : nr) {
+    const uint32_t b = c->h_prow[x.u], cap = c->h_prow[x.u + 1] - b;
+    big_change |= (x.cap0 > ospf::kMsBigDeg) != (cap > ospf::kMsBigDeg);
+    uint32_t m = 0;
+    for (uint32_t j = 0; j < cap; ++j) {
+      const size_t e = (size_t)b + j;
+      const bool inrow = j < x.need;
+      const uint32_t cx = inrow ? x.colx[j] : 0x80000000u, w = inrow ? x.w[j] : 0u,
+                     rw = inrow ? x.rw[j] : 0u, l = inrow ? x.lid[j] : kNo;
+      if (!(c->h_pcolx[e] & 0x80000000u) && c->h_pw[e] != 1) --c->non_unit;
+      if (!(cx & 0x80000000u) && w != 1) ++c->non_unit;
+      if (!(cx & 0x80000000u)) m = std::max(m, w);
+      c->h_pcolx[e] = cx;
+      c->h_pw[e] = w;
+      c->h_prw[e] = rw;
+      c->h_plink[e] = l;
+      put(o_colx + e, cx);
+      put(o_w + e, w);
+      put(o_rw + e, rw);
+      put(o_lid + e, l);
+      if (c->g.ew) {
+        if (w > 0xFFFFu || rw > 0xFFFFu) {
+          c->g.ew = nullptr;
+        } else {
+          put(o_ew + 2 * e, cx);
+          put(o_ew + 2 * e + 1, w | (rw << 16));
+        }
+      }
+      if (l != kNo) {
+        uint32_t* le = &c->h_link_e[2ull * l];
+        (le[0] == kNo ? le[0] : le[1]) = (uint32_t)e;
+        touched.push_back(l);
+        lid_max = std::max(lid_max, l + 1);
+      }
+    }
+    for (uint32_t j = 0; j < cap; j += 2) {  // didx: two u16 per word (rows start 8-B aligned)
+      const uint32_t lo = j < x.need ? x.didx[j] : 0xFFFFu, hi = j + 1 < x.need ? x.didx[j + 1] : 0xFFFFu;
+      put(o_didx + ((size_t)b + j) / 2, lo | (hi << 16));
+    }
+    c->dist_bound = c->dist_bound - c->h_rowmax[x.u] + m;
+    c->h_rowmax[x.u] = m;
+  }
+  c->g.n_lid = lid_max;
+  std::sort(touched.begin(), touched.end());
+  touched.erase(std::unique(touched.begin(), touched.end()), touched.end());
+  for (uint32_t l : touched) {
+    put(o_le + 2ull * l, c->h_link_e[2ull * l]);
+    put(o_le + 2ull * l + 1, c->h_link_e[2ull * l + 1]);
+  }
+  // distinct neighbours: a row whose count changes moves the lists after it
+  // (last first, like the entry arrays; dn_off shifted on both sides), then
+  // every rebuilt row's list is written in place
+  const size_t o_dn = woff(c->g.dn);
+  for (auto it = nr.rbegin(); it != nr.rend(); ++it) {
+    const Row& x = *it;
+    const uint32_t lo = c->h_dn_off[x.u], hi = c->h_dn_off[x.u + 1];
+    const int64_t delta = (int64_t)x.dn.size() - (int64_t)(hi - lo);
+    if (!delta) continue;
+    const size_t tail = c->h_dn.size() - hi;
+    if (tail) {
+      int rc = ensure(c, &c->d_stage, &c->stage_bytes, tail * 4);
+      if (rc) return rc;
+      HIPCHK(c, hipMemcpy(c->d_stage, c->g.dn + hi, tail * 4, hipMemcpyDeviceToDevice));
+      HIPCHK(c, hipMemcpy((void*)(c->g.dn + (int64_t)hi + delta), c->d_stage, tail * 4,
+                          hipMemcpyDeviceToDevice));
+    }
+    if (delta > 0) c->h_dn.insert(c->h_dn.begin() + hi, (size_t)delta, 0u);
+    else c->h_dn.erase(c->h_dn.begin() + ((int64_t)hi + delta), c->h_dn.begin() + hi);
+    for (uint32_t v = x.u + 1; v <= V; ++v) c->h_dn_off[v] += (uint32_t)delta;
+    hipError_t he = ospf::launch_shift_add(base + woff(c->g.dn_off), V + 1, x.u + 1, 0u,
+                                           (uint32_t)delta, nullptr);
+    if (he != hipSuccess) return hip_fail(c, he, "launch_shift_add");
+  }
+  for (const Row& x : nr)
+    for (size_t k = 0; k < x.dn.size(); ++k) {
+      c->h_dn[c->h_dn_off[x.u] + k] = x.dn[k];
+      put(o_dn + c->h_dn_off[x.u] + k, x.dn[k]);
+    }
+  if (!idx.empty()) {
+    int rc = ensure(c, &c->d_stage, &c->stage_bytes, idx.size() * 8ull + 256);
+    if (rc) return rc;
+    uint32_t* d_idx = (uint32_t*)c->d_stage;
+    uint32_t* d_val = d_idx + idx.size();
+    HIPCHK(c, hipMemcpy(d_idx, idx.data(), idx.size() * 4ull, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(d_val, val.data(), val.size() * 4ull, hipMemcpyHostToDevice));
+    hipError_t e = ospf::launch_scatter(base, d_idx, d_val, (uint32_t)idx.size(), nullptr);
+    if (e != hipSuccess) return hip_fail(c, e, "launch_scatter");
+  }
+  if (big_change) {
+    std::vector<uint32_t> big;
+    for (uint32_t u = 0; u < V; ++u)
+      if (c->h_prow[u + 1] - c->h_prow[u] > ospf::kMsBigDeg) big.push_back(u);
+    if (!big.empty())
+      HIPCHK(c, hipMemcpy((void*)c->g.big, big.data(), big.size() * 4ull, hipMemcpyHostToDevice));
+    c->g.nbig = (uint32_t)big.size();
+  }
+  HIPCHK(c, hipDeviceSynchronize());
+  c->g.E = (uint32_t)Ep;
+  c->max_dn = max_dn;
+  c->h_row_ptr.assign(rp, rp + V + 1);
+  c->info.n_edges = E;
+  c->info.n_links = E / 2;
+  c->info.max_degree = max_deg;
+  // level bound after transit links were lost: the detour rule of
+  // ospf_update_links (a split component recomputes it)
+  uint32_t grow = 0;
+  for (const auto& ab : lost) {
+    if (deeper) break;
+    const uint32_t k = transit_detour(c, ab.first, ab.second, 1u << 20);
+    if (k == kNo) deeper = true;
+    else grow += k - 1;
+  }
+  if (!deeper && grow) {
+    if (c->depth_bound + grow > c->exact_bound + 8) deeper = true;
+    else c->depth_bound += grow;
+  }
+  refresh_graph_stats(c, new_max, deeper);
   c->info.version = version;
   c->cover_ok = false;  // the contracted cover graph describes the old graph
   ++c->graph_gen;

@@ -23,7 +23,10 @@ struct ospf_ctx {
   ospf_graph_info info{};
   std::vector<uint32_t> h_row_ptr, h_dn_off, h_dn;  // host copies for root queries
   // host shadows of the padded device arrays patched by ospf_update_*
-  std::vector<uint32_t> h_prow, h_pcolx, h_pw, h_prw, h_nt, h_link_e;
+  std::vector<uint32_t> h_prow, h_pcolx, h_pw, h_prw, h_nt, h_link_e, h_plink;
+  // allocated capacity of the per-entry arrays (entries), of dn and of link_e
+  // (link ids): the reserves of ospf_update_rows
+  size_t cap_e = 0, cap_dn = 0, cap_lid = 0;
   uint64_t non_unit = 0;  // usable entries with metric != 1 (exact unit_metric under patches)
   void* d_graph = nullptr;
   ospf::DevGraph g{};

@@ -534,6 +534,10 @@ hipError_t launch_or_bits(uint32_t* st, uint32_t n, uint32_t bits, hipStream_t s
 // incremental updates (spf_update.hip): base[idx[i]] = val[i]; affected runs
 hipError_t launch_scatter(uint32_t* base, const uint32_t* idx, const uint32_t* val, uint32_t n,
                           hipStream_t s);
+// structural patches: a[i] += d for i in [from, n) where a[i] >= thresh and
+// a[i] != UINT32_MAX (row offsets / entry positions past a grown row)
+hipError_t launch_shift_add(uint32_t* a, uint32_t n, uint32_t from, uint32_t thresh, uint32_t d,
+                            hipStream_t s);
 hipError_t launch_affected(const DevGraph& g, const uint32_t* dist, uint32_t n_roots, bool hop,
                            const ospf_change* ch, uint32_t n_ch, uint8_t* out, hipStream_t s);
 struct RepairArgs {

@@ -22,6 +22,8 @@
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "spf_internal.h"
 
 using namespace ospf_int;
@@ -46,7 +48,7 @@ __global__ void scatter_digest_kernel(const ospf_digest* __restrict__ src,
                                       const uint32_t* __restrict__ roots, uint32_t n,
                                       ospf_digest* __restrict__ out) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[roots[i]] = src[i];
+  if (i < n && roots[i] != kNone) out[roots[i]] = src[i];
 }
 
 // ---------------------------------------------------------------- host graph facts
@@ -1855,7 +1857,12 @@ int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
   const uint32_t parts = std::max(1u, o->n_parts);
   if (o->part >= parts) return fail(c, OSPF_E_INVAL, "sweep: part >= n_parts");
   if (o->mode > OSPF_SWEEP_LDS) return fail(c, OSPF_E_INVAL, "sweep: unknown mode");
-  if (o->flags & ~OSPF_HOP_COUNT) return fail(c, OSPF_E_INVAL, "sweep: flags = 0 or OSPF_HOP_COUNT");
+  if (o->flags & ~(OSPF_HOP_COUNT | OSPF_SWEEP_DEFER))
+    return fail(c, OSPF_E_INVAL, "sweep: flags = 0 or OSPF_HOP_COUNT, | OSPF_SWEEP_DEFER");
+  const bool defer = (o->flags & OSPF_SWEEP_DEFER) != 0;
+  if (defer && o->hip_graph)
+    return fail(c, OSPF_E_INVAL, "sweep: OSPF_SWEEP_DEFER needs hip_graph = 0 (the capture "
+                                 "follows the first run)");
   const bool hop = o->flags & OSPF_HOP_COUNT;
   if (!hop && c->dist_bound >= 0xFFFFFFFFull)
     return fail(c, OSPF_E_RANGE, "u32 distance overflow possible (sum of per-node max metrics)");
@@ -1891,7 +1898,7 @@ int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
   const bool derive_ok = unit && c->max_dn <= 2048 && c->depth_bound <= 123;
   // small graphs: every root's next hops in <= 4 words and the graph in LDS
   const uint32_t max_w = std::max(1u, (c->max_dn + 31) / 32);
-  const bool lds_ok = unit && max_w <= 4 && ospf_lds_sweep_fits(c, o->flags, max_w) &&
+  const bool lds_ok = unit && max_w <= 4 && ospf_lds_sweep_fits(c, o->flags & OSPF_HOP_COUNT, max_w) &&
                       !getenv("OSPF_SWEEP_NOLDS");
   std::vector<uint8_t> leaf;
   bool any_leaf = false;
@@ -1940,6 +1947,10 @@ int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
   for (size_t i = 1; i < s->streams.size(); ++i)
     if (hipEventCreateWithFlags(&s->ev_done[i], hipEventDisableTiming) != hipSuccess)
       return bail(fail(c, OSPF_E_DEVICE, "hipEventCreate"));
+  if (defer) {  // the caller's first ospf_sweep_run is the first run
+    *out = s;
+    return OSPF_OK;
+  }
   // one eager run: sizes every stream's scratch (nothing may allocate inside
   // a capture) and surfaces launch errors here
   const uint64_t runs0 = c->spf_runs;
@@ -2018,6 +2029,7 @@ int ospf_sweep_run(ospf_sweep* s, void* stream) {
     const int rc = run_eager(s, (hipStream_t)stream);
     if (rc) return rc;
   }
+  s->ran = true;
   c->spf_runs = runs0 + s->roots.size();
   return OSPF_OK;
 }
@@ -2154,6 +2166,12 @@ int ospf_sweep_profile(ospf_sweep* s, uint32_t reps, ospf_sweep_launch* out, uin
 struct ospf_multi {
   std::vector<ospf_ctx*> ctx;
   std::string err;
+  // RCCL communicators, one per device slot (ncclCommInitAll in this
+  // process): the digest gather of a sweep is one ncclAllGather over xGMI.
+  // 0 = not tried, 1 = live, -1 = unavailable (duplicate devices -- RCCL
+  // takes one rank per GPU -- or init failed: peer copies instead)
+  int rccl = 0;
+  std::vector<ncclComm_t> comms;
 };
 
 struct ospf_msweep {
@@ -2164,9 +2182,41 @@ struct ospf_msweep {
   ospf_digest* d_all = nullptr;         // device 0: [total owned] part digests, part order
   uint32_t* d_roots = nullptr;          // device 0: their root ids
   ospf_digest* d_by_node = nullptr;     // device 0: [V]
-  std::vector<ospf_digest*> d_part;     // per slot (on its device): [n_roots]
+  std::vector<ospf_digest*> d_part;     // per slot (on its device): [slot] (padded)
   uint32_t total = 0;
+  // RCCL gather: every part's digests padded to `slot` entries, all-gathered
+  // into d_recv on every device; d_roots_pad (device 0) = the root of each
+  // gathered entry (kNone: padding)
+  uint32_t slot = 0;
+  std::vector<ospf_digest*> d_recv;     // per slot (on its device): [n_parts * slot]
+  uint32_t* d_roots_pad = nullptr;
 };
+
+namespace {
+// RCCL communicators for the multi context, once: distinct devices only
+// (OSPF_RCCL=1 also takes a single device -- a one-rank communicator, which
+// exercises the path on a one-GPU box; OSPF_RCCL=0 keeps peer copies)
+bool multi_rccl(ospf_multi* m) {
+  if (m->rccl) return m->rccl > 0;
+  m->rccl = -1;
+  const char* e = getenv("OSPF_RCCL");
+  if (e && e[0] == '0') return false;
+  const size_t n = m->ctx.size();
+  std::vector<int> devs;
+  for (ospf_ctx* c : m->ctx) devs.push_back(c->device);
+  std::vector<int> u = devs;
+  std::sort(u.begin(), u.end());
+  if (std::unique(u.begin(), u.end()) != u.end()) return false;  // a device twice
+  if (n < 2 && !(e && e[0] == '1')) return false;
+  m->comms.assign(n, nullptr);
+  if (ncclCommInitAll(m->comms.data(), (int)n, devs.data()) != ncclSuccess) {
+    m->comms.clear();
+    return false;
+  }
+  m->rccl = 1;
+  return true;
+}
+}  // namespace
 
 extern "C" {
 
@@ -2203,6 +2253,8 @@ int ospf_multi_open(const int* devices, uint32_t n, ospf_multi** out) {
 
 int ospf_multi_close(ospf_multi* m) {
   if (!m) return OSPF_E_INVAL;
+  for (ncclComm_t cm : m->comms)
+    if (cm) ncclCommDestroy(cm);
   for (ospf_ctx* c : m->ctx) ospf_close(c);
   delete m;
   return OSPF_OK;
@@ -2231,12 +2283,13 @@ int ospf_multi_load_graph(ospf_multi* m, const ospf_csr* csr, uint64_t version) 
 int ospf_msweep_destroy(ospf_msweep* ms) {
   if (!ms) return OSPF_E_INVAL;
   for (size_t i = 0; i < ms->parts.size(); ++i) {
-    if (i < ms->d_part.size() && ms->d_part[i]) {
-      hipSetDevice(ms->m->ctx[i]->device);
-      hipFree(ms->d_part[i]);
-    }
+    hipSetDevice(ms->m->ctx[i]->device);
+    if (i < ms->d_part.size() && ms->d_part[i]) hipFree(ms->d_part[i]);
+    if (i < ms->d_recv.size() && ms->d_recv[i]) hipFree(ms->d_recv[i]);
     ospf_sweep_destroy(ms->parts[i]);
   }
+  if (!ms->m->ctx.empty()) hipSetDevice(ms->m->ctx[0]->device);
+  if (ms->d_roots_pad) hipFree(ms->d_roots_pad);
   if (!ms->m->ctx.empty()) hipSetDevice(ms->m->ctx[0]->device);
   if (ms->d_all) hipFree(ms->d_all);
   if (ms->d_roots) hipFree(ms->d_roots);
@@ -2264,17 +2317,42 @@ int ospf_msweep_create(ospf_multi* m, const ospf_sweep_opts* o, ospf_msweep** ou
     ospf_sweep_opts oi = *o;
     oi.part = i;
     oi.n_parts = n;
+    // without HIP graphs no part runs at create: ospf_msweep_run starts every
+    // device's first run together (a capture needs its part's eager run)
+    if (!o->hip_graph) oi.flags |= OSPF_SWEEP_DEFER;
     ospf_sweep* s = nullptr;
     const int rc = ospf_sweep_create(m->ctx[i], &oi, &s);
     if (rc) return bail(rc, ospf_last_error(m->ctx[i]));
     ms->parts.push_back(s);
     for (uint32_t r : s->roots) ms->owner[r] = i;
     all_roots.insert(all_roots.end(), s->roots.begin(), s->roots.end());
+    ms->slot = std::max<uint32_t>(ms->slot, (uint32_t)s->roots.size());
+  }
+  ms->slot = std::max(ms->slot, 1u);
+  for (uint32_t i = 0; i < n; ++i) {  // digests padded to the widest part
     ospf_digest* dp = nullptr;
     hipSetDevice(m->ctx[i]->device);
-    if (hipMalloc(&dp, std::max<size_t>(1, s->roots.size()) * sizeof(ospf_digest)) != hipSuccess)
+    if (hipMalloc(&dp, (size_t)ms->slot * sizeof(ospf_digest)) != hipSuccess)
       return bail(OSPF_E_NOMEM, "msweep: hipMalloc");
     ms->d_part.push_back(dp);
+    if (hipMemset(dp, 0, (size_t)ms->slot * sizeof(ospf_digest)) != hipSuccess)
+      return bail(OSPF_E_DEVICE, "msweep: hipMemset");
+  }
+  if (multi_rccl(m)) {
+    for (uint32_t i = 0; i < n; ++i) {
+      ospf_digest* dr = nullptr;
+      hipSetDevice(m->ctx[i]->device);
+      if (hipMalloc(&dr, (size_t)n * ms->slot * sizeof(ospf_digest)) != hipSuccess)
+        return bail(OSPF_E_NOMEM, "msweep: hipMalloc");
+      ms->d_recv.push_back(dr);
+    }
+    std::vector<uint32_t> pad((size_t)n * ms->slot, kNone);
+    for (uint32_t i = 0; i < n; ++i)
+      std::copy(ms->parts[i]->roots.begin(), ms->parts[i]->roots.end(), pad.begin() + (size_t)i * ms->slot);
+    hipSetDevice(m->ctx[0]->device);
+    if (hipMalloc(&ms->d_roots_pad, pad.size() * 4) != hipSuccess ||
+        hipMemcpy(ms->d_roots_pad, pad.data(), pad.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+      return bail(OSPF_E_NOMEM, "msweep: root table");
   }
   ms->total = (uint32_t)all_roots.size();
   hipSetDevice(m->ctx[0]->device);
@@ -2312,6 +2390,40 @@ int ospf_msweep_run(ospf_msweep* ms) {
 int ospf_msweep_digests(ospf_msweep* ms, ospf_digest* out) {
   if (!ms || !out) return OSPF_E_INVAL;
   ospf_ctx* c0 = ms->m->ctx[0];
+  if (!ms->d_recv.empty()) {
+    // every part's digests (queued on its device's stream), then ONE
+    // ncclAllGather of the padded records; device 0 scatters them by root
+    const size_t n = ms->parts.size();
+    for (size_t i = 0; i < n; ++i) {
+      const int rc = ospf_sweep_digests(ms->parts[i], ms->d_part[i], nullptr);
+      if (rc) {
+        ms->m->err = ms->parts[i]->err;
+        return rc;
+      }
+    }
+    ncclResult_t nr = ncclGroupStart();
+    for (size_t i = 0; i < n && nr == ncclSuccess; ++i) {
+      hipSetDevice(ms->m->ctx[i]->device);
+      nr = ncclAllGather(ms->d_part[i], ms->d_recv[i], (size_t)ms->slot * 3, ncclUint64,
+                         ms->m->comms[i], (hipStream_t)0);
+    }
+    const ncclResult_t ne = ncclGroupEnd();
+    if (nr != ncclSuccess || ne != ncclSuccess) {
+      ms->m->err = std::string("msweep: ncclAllGather: ") + ncclGetErrorString(nr != ncclSuccess ? nr : ne);
+      return OSPF_E_DEVICE;
+    }
+    hipSetDevice(c0->device);
+    hipMemset(ms->d_by_node, 0, (size_t)ms->V * sizeof(ospf_digest));
+    const uint32_t tot = (uint32_t)(n * ms->slot);
+    hipLaunchKernelGGL(scatter_digest_kernel, dim3((tot + 255) / 256), dim3(256), 0, 0,
+                       ms->d_recv[0], ms->d_roots_pad, tot, ms->d_by_node);
+    if (hipMemcpy(out, ms->d_by_node, (size_t)ms->V * sizeof(ospf_digest), hipMemcpyDeviceToHost) !=
+        hipSuccess) {
+      ms->m->err = "msweep: hipMemcpy";
+      return OSPF_E_DEVICE;
+    }
+    return OSPF_OK;
+  }
   size_t off = 0;
   for (size_t i = 0; i < ms->parts.size(); ++i) {
     ospf_sweep* s = ms->parts[i];
@@ -2345,6 +2457,10 @@ int ospf_msweep_digests(ospf_msweep* ms, ospf_digest* out) {
 
 ospf_sweep* ospf_msweep_part(ospf_msweep* ms, uint32_t slot) {
   return (ms && slot < ms->parts.size()) ? ms->parts[slot] : nullptr;
+}
+
+uint32_t ospf_msweep_gather_backend(const ospf_msweep* ms) {
+  return (ms && !ms->d_recv.empty()) ? 1u : 0u;
 }
 
 int ospf_msweep_owner(const ospf_msweep* ms, uint32_t root, uint32_t* slot) {

@@ -27,6 +27,15 @@ __global__ void scatter_kernel(uint32_t* base, const uint32_t* idx, const uint32
   if (i < n) base[idx[i]] = val[i];
 }
 
+__global__ void shift_add_kernel(uint32_t* a, uint32_t n, uint32_t from, uint32_t thresh,
+                                 uint32_t d) {
+  const uint32_t i = from + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const uint32_t x = a[i];
+    if (x != 0xFFFFFFFFu && x >= thresh) a[i] = x + d;
+  }
+}
+
 // can `x`'s relaxations matter to the run whose distance row is `d`?
 __device__ bool node_matters(const DevGraph& g, const uint32_t* d, uint32_t x, bool hop) {
   const uint32_t dx = d[x];
@@ -289,6 +298,14 @@ hipError_t launch_repair(const DevGraph& g, const RepairArgs& a, hipStream_t s) 
 hipError_t launch_scatter(uint32_t* base, const uint32_t* idx, const uint32_t* val, uint32_t n,
                           hipStream_t s) {
   if (n) hipLaunchKernelGGL(scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, s, base, idx, val, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_shift_add(uint32_t* a, uint32_t n, uint32_t from, uint32_t thresh, uint32_t d,
+                            hipStream_t s) {
+  if (n > from)
+    hipLaunchKernelGGL(shift_add_kernel, dim3((n - from + 255) / 256), dim3(256), 0, s, a, n, from,
+                       thresh, d);
   return hipGetLastError();
 }
 

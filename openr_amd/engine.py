@@ -243,6 +243,14 @@ class Engine:
         arr = (N.ospf_link_update * max(len(ups), 1))(*[N.ospf_link_update(*u) for u in ups])
         self._check(self._L.ospf_update_links(self._h, arr, len(ups), version))
 
+    def update_rows(self, csr: Dict[str, np.ndarray], rows, version: int) -> None:
+        """ospf_update_rows: links added / removed in place; `csr` is the
+        whole CSR after the change, `rows` the nodes whose rows changed."""
+        s, keep = csr_struct(csr)
+        r = np.ascontiguousarray(rows, np.uint32)
+        self._check(self._L.ospf_update_rows(self._h, C.byref(s), r.ctypes.data if r.size else None,
+                                             r.size, version))
+
     def update_nodes(self, nodes, no_transit, version: int) -> None:
         n = np.ascontiguousarray(nodes, np.uint32)
         t = np.ascontiguousarray(no_transit, np.uint8)
@@ -427,6 +435,11 @@ class MultiSweep:
         out = np.zeros((self.multi.V, 3), np.uint64)
         self.multi._check(self._L.ospf_msweep_digests(self._h, out.ctypes.data))
         return out
+
+    @property
+    def gather_backend(self) -> str:
+        """'rccl' (one ncclAllGather of the parts' digests) or 'peer'."""
+        return "rccl" if self._L.ospf_msweep_gather_backend(self._h) else "peer"
 
     def owner(self, root: int) -> int:
         s = C.c_uint32()

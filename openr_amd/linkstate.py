@@ -229,6 +229,15 @@ class LinkState:
         self._L.odl_incremental_stats(self._h, out)
         return {"patches": int(out[0]), "kept": int(out[1]), "dropped": int(out[2])}
 
+    def topology_stats(self) -> Dict[str, int]:
+        """{snapshots, loads, link_patches, rows_patched}: links added /
+        removed between known nodes patch the CSR and the device graph in
+        place (odl_topology_stats)."""
+        out = (C.c_uint64 * 4)()
+        self._L.odl_topology_stats(self._h, out)
+        return {"snapshots": int(out[0]), "loads": int(out[1]), "link_patches": int(out[2]),
+                "rows_patched": int(out[3])}
+
     def num_nodes(self) -> int:
         return int(self._L.odl_num_nodes(self._h))
 

@@ -10,8 +10,10 @@ what Decision runs per route rebuild on one node --
 
 timed through odl::LinkState on the MI355X, phase by phase (ODL_SPF_TIMING
 lines from libopenr_decision), cold (snapshot + device load) and warm, and
-after a link-metric event with incremental patching off / on; next to the
-CPU restatement of runSpf on the same root (oracle/, reference-shaped).
+after a link-metric event and a [LINK DOWN] / [LINK UP] pair (adjacency
+withdrawn and restored, patched in place: apply, getSpfResult(me), an
+all-sources re-sweep) with incremental patching off / on; next to the CPU
+restatement of runSpf on the same root (oracle/, reference-shaped).
 
 Usage: python scripts/prod_callstack.py [--pods 1781] > out.json
 """
@@ -107,6 +109,27 @@ def main():
         _, wall, _ = timed(lambda: p.apply(ev))
         out[f"{tag}_event_apply_ms"] = round(wall, 3)
         stack(p, args.me, f"{tag}_after_event")
+        # [LINK DOWN] / [LINK UP] (LinkState.cpp:632-657): the rack withdraws
+        # its adjacency to its pod's first fabric switch, then restores it;
+        # each: apply, getSpfResult(me), and a whole all-sources re-sweep
+        t0 = p.topology_stats()
+        adj = db.adjs.pop(0)
+        for kind in ("link_down", "link_up"):
+            if kind == "link_up":
+                db.adjs.insert(0, adj)
+            ev = AdjDbStream.from_dbs([db])
+            _, wall, _ = timed(lambda: p.apply(ev))
+            out[f"{tag}_{kind}_apply_ms"] = round(wall, 3)
+            _, wall, cap = timed(lambda: p.prefetch([args.me]))
+            out[f"{tag}_{kind}_getSpfResult_ms"] = round(wall, 3)
+            out[f"{tag}_{kind}_engine_ms"] = sum(cap.values("engine_ms"))
+            _, wall, _ = timed(lambda: p.prefetch_all())
+            out[f"{tag}_{kind}_all_sources_sweep_ms"] = round(wall, 3)
+            print(f"{tag} {kind}: apply {out[f'{tag}_{kind}_apply_ms']} ms, getSpfResult "
+                  f"{out[f'{tag}_{kind}_getSpfResult_ms']} ms, sweep "
+                  f"{out[f'{tag}_{kind}_all_sources_sweep_ms']} ms", file=sys.stderr, flush=True)
+        t1 = p.topology_stats()
+        out[f"{tag}_link_events_topology_stats"] = {k: t1[k] - t0[k] for k in t1}
         del p
     if not args.no_cpu:
         from oracle import Oracle  # CPU restatement, same root

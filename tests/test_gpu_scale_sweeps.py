@@ -1,0 +1,153 @@
+"""Full-size parity of the all-sources sweeps under the reference's edge cases
+(VERDICT r03 next #2): the F100k fabric with drained (overloaded) nodes and
+down links on the unit-metric derive sweep, and the weighted F100k (metrics
+1..64, seed 7) with and without drains on the weighted cover sweep.
+
+Each sweep's per-root digests are checked against the CSR-Dijkstra CPU
+restatement (oracle/, test infrastructure) on every spine, every drained node,
+a sample of the nodes incident to a down link and 256 random fabric / rack
+switches; whole dist + next-hop rows of >= 32 roots per width class are
+compared with the per-batch engine path; every root's reached count is checked
+against a host BFS of the usable graph.
+
+Reference semantics: LinkState::runSpf (openr/decision/LinkState.cpp:836-911),
+overloaded nodes recorded but never relaying (:859-866), Link::isUp
+(:242-245)."""
+import time
+
+import numpy as np
+import pytest
+
+from graphs import drained_fabric
+from oracle import Oracle
+from openr_amd import topology as T
+from openr_amd.engine import Engine, Sweep
+from openr_amd.linkstate import LinkState
+
+pytestmark = pytest.mark.gpu
+
+T0 = time.time()
+
+
+def note(msg):
+    print(f"[{time.time() - T0:7.1f}s] {msg}", flush=True)
+
+
+def reached_counts(csr, roots):
+    """Nodes each root reaches over usable links, non-transit nodes relaying
+    only as the root (scipy BFS over the transit subgraph + one hop)."""
+    from scipy.sparse import csr_matrix
+    from scipy.sparse.csgraph import connected_components
+    V = csr["row_ptr"].size - 1
+    rp = csr["row_ptr"].astype(np.int64)
+    src = np.repeat(np.arange(V), np.diff(rp))
+    col = csr["col"].astype(np.int64)
+    up = csr["edge_up"].astype(bool)
+    nt = csr["no_transit"].astype(bool)
+    keep = up & ~nt[src] & ~nt[col]
+    g = csr_matrix((np.ones(int(keep.sum()), np.int8), (src[keep], col[keep])), shape=(V, V))
+    _, comp = connected_components(g, directed=False)
+    # per component of the transit subgraph: its transit nodes and the
+    # non-transit nodes one usable link away (reached, never relaying)
+    size = np.bincount(comp[~nt], minlength=comp.max() + 1)
+    e = up & ~nt[src] & nt[col]
+    ntadj = {}
+    for k, x in set(zip(comp[src[e]].tolist(), col[e].tolist())):
+        ntadj.setdefault(k, set()).add(x)
+    out = []
+    for r in roots:
+        r = int(r)
+        if not nt[r]:
+            out.append(int(size[comp[r]]) + len(ntadj.get(comp[r], ())))
+            continue
+        # an overloaded root relays its own links: the components of its
+        # transit neighbours, their non-transit neighbours, its own neighbours
+        lo, hi = rp[r], rp[r + 1]
+        nb = {int(x) for x, u in zip(col[lo:hi], up[lo:hi]) if u}
+        ks = {int(comp[x]) for x in nb if not nt[x]}
+        seen = {r} | {x for x in nb if nt[x]}
+        for k in ks:
+            seen |= ntadj.get(k, set())
+        out.append(sum(int(size[k]) for k in ks) + len(seen))
+    return np.array(out)
+
+
+def check_sweep(stream, want_mode, hop=False, seed=0x5EED, extra=()):
+    o, p = Oracle(), LinkState()
+    assert o.apply(stream) == p.apply(stream)
+    note("ingested")
+    names = p.node_names()
+    V = len(names)
+    csr = p.csr()
+    eng = Engine()
+    eng.load(csr)
+    sw = Sweep(eng, hop_count=hop)
+    assert sw.mode == want_mode
+    assert sorted(sw.roots.tolist()) == list(range(V))
+    sw.run()
+    eng.sync()
+    d = np.zeros((V, 3), np.uint64)
+    sw._check(sw._L.ospf_sweep_digests_host(sw._h, d.ctypes.data))
+    got = np.zeros_like(d)
+    got[sw.roots] = d
+    note(f"sweep ({sw.mode}) digests")
+    role = np.array([int(n.split("-")[0]) for n in names])
+    rng = np.random.default_rng(seed)
+    nt = np.nonzero(csr["no_transit"])[0]
+    rp = csr["row_ptr"].astype(np.int64)
+    src = np.repeat(np.arange(V), np.diff(rp))
+    down_nodes = np.unique(src[csr["edge_up"] == 0])
+    inc = np.sort(rng.choice(down_nodes, min(512, down_nodes.size), replace=False)) \
+        if down_nodes.size else np.zeros(0, np.int64)
+    spines = np.nonzero(role == 1)[0]
+    fsw = np.sort(rng.choice(np.nonzero(role == 2)[0], 256, replace=False))
+    rsw = np.sort(rng.choice(np.nonzero(role == 3)[0], 256, replace=False))
+    strat = np.unique(np.concatenate([spines, nt, inc, fsw, rsw, np.asarray(extra, np.int64)]))
+    want = o.fast_digests([names[i] for i in strat], not hop, threads=16)
+    note(f"CSR-Dijkstra digests of {strat.size} roots ({nt.size} drained, {inc.size} "
+         f"incident to a down link)")
+    bad = [names[r] for j, r in enumerate(strat) if not np.array_equal(got[r], want[j])]
+    assert not bad, (len(bad), bad[:8])
+    # reached count of every root (size-independent property over all V runs)
+    chk = np.unique(np.concatenate([strat, rng.choice(V, 2048, replace=False)]))
+    assert np.array_equal(got[chk, 0].astype(np.int64), reached_counts(csr, chk))
+    note("reached counts")
+    # whole rows of >= 32 roots per width class == the per-batch engine path
+    words = np.array([eng.nh_words(int(r)) for r in range(V)])
+    for W in sorted(set(words.tolist())):
+        grp = np.nonzero(words == W)[0]
+        few = np.sort(rng.choice(grp, min(32, grp.size), replace=False)).astype(np.uint32)
+        # the class's drained roots and roots next to a down link first
+        spec = np.intersect1d(grp, np.concatenate([nt, inc]))[:16].astype(np.uint32)
+        few = np.unique(np.concatenate([spec, few]))[:48]
+        ref = eng.run(few, W, hop_count=hop, want_digest=True)
+        dist, nh = sw.rows(few, W)
+        assert np.array_equal(dist, ref["dist"]), W
+        assert np.array_equal(nh, ref["nh"]), W
+        assert np.array_equal(got[few], ref["digest"]), W
+    note("rows == batch path")
+    sw.close()
+    eng.close()
+
+
+@pytest.mark.timeout(900)
+def test_f100k_drained_unit_derive_sweep():
+    """Unit-metric F100k with 2 % drained nodes and 1 % of the adjacencies
+    reported overloaded: twin classes split (racks with a down link leave
+    their pod's class), leaf groups turn non-uniform, non-transit slots."""
+    check_sweep(drained_fabric(1781, 8, seed=11, drain=0.02, down=0.01), "derive")
+
+
+@pytest.mark.timeout(900)
+def test_f100k_weighted_cover_sweep():
+    """The weighted F100k (metrics 1..64, seed 7): cover SPF + closure, leaf
+    rows, fabric-switch and spine next hops (bench.py --topology
+    fabric100k-w)."""
+    check_sweep(T.fabric(pods=1781, planes=8, weighted_seed=7), "wcover")
+
+
+@pytest.mark.timeout(900)
+def test_f100k_weighted_drained_cover_sweep():
+    """The weighted F100k with 2 % drained nodes and 1 % down adjacencies."""
+    check_sweep(drained_fabric(1781, 8, seed=12, drain=0.02, down=0.01, weighted_seed=7),
+                "wcover")
