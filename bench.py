@@ -429,6 +429,7 @@ def sweep_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, 
     mode = {"auto": "auto", "derive": "derive", "batch": "batch"}.get(args.mode, args.mode)
     t0 = time.time()
     sw = eng.sweep(mode=mode, part=rank, n_parts=world, hip_graph=args.graph != "off")
+    create_s = time.time() - t0
     n = sw.n_roots
     log(f"[rank {rank}] sweep: mode {sw.mode}, {n} roots, {sw.n_rows} rows, {sw.n_launches} "
         f"launches, hip graph {'on' if sw.hip_graph else 'off'}, "
@@ -527,10 +528,32 @@ def sweep_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, 
     }
     cfg = {"mode": sw.mode, "hip_graph": sw.hip_graph, "roots_this_rank": n,
            "rows_this_rank": sw.n_rows, "device_bytes": sw.device_bytes,
-           "closure_over_roots": round(sw.n_rows / max(1, n), 4)}
+           "closure_over_roots": round(sw.n_rows / max(1, n), 4),
+           "sweep_create_ms": round(create_s * 1e3, 1),
+           "sweep_create_note": "ospf_sweep_create: host plan (partition, leaf set, twin "
+                                "classes, row positions), allocation, one eager run and the HIP "
+                                "graph capture; paid once per graph version, not in `value`"}
+    trav = sw.step_traversed_edges
     sw.close()
+    # what a production caller pays once per graph version (odl::LinkState:
+    # a deferred create -- plan + allocation -- then one eager run)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    sw2 = eng.sweep(mode=mode, part=rank, n_parts=world, defer=True)
+    t2 = time.perf_counter()
+    sw2.run(main_s.cuda_stream)
+    torch.cuda.synchronize()
+    eng.sync(main_s.cuda_stream)
+    t3 = time.perf_counter()
+    sw2.close()
+    cfg["first_sweep_after_graph_change"] = {
+        "plan_ms": round((t2 - t1) * 1e3, 1), "first_run_ms": round((t3 - t2) * 1e3, 1),
+        "total_ms": round((t3 - t1) * 1e3, 1),
+        "note": "a new graph version: ospf_sweep_create(OSPF_SWEEP_DEFER) + the first (eager, "
+                "no HIP graph) run, as odl::LinkState::prefetchAllSources pays it"}
     report(args, stream, names, csr, step_digest, dt, V * args.steps, E, desc, 0, V, world, rank,
-           dist_on, backend, V, cfg, roofline, "strong", "sweep:" + cfg["mode"])
+           dist_on, backend, V, cfg, roofline, "strong", "sweep:" + cfg["mode"],
+           trav_edges=trav * args.steps)
     if dist_on:
         torch.distributed.destroy_process_group()
 
@@ -551,11 +574,15 @@ def parity_sample(csr, V: int, k: int = 256):
 
 def report(args, stream, names, csr, step_digest, dt, roots_total, E, desc, n_roots, V, world,
            rank, dist_on, backend, roots_per_step, classes_cfg, roofline, scaling, mode,
-           pool=None):
+           pool=None, trav_edges=None):
     """CPU baseline + parity of the timed step's digests (rank 0) and the one
-    JSON line."""
+    JSON line. gteps = edges the traversal kernels relaxed (trav_edges over
+    the timed steps; every root of a per-root / batch path traverses E) / t;
+    gteps_all_pairs_equiv = roots x E_dir / t, what per-root SSSPs would have
+    to relax for the same rows (derived rows relax none)."""
     spf_s = roots_total / dt
-    gteps = roots_total * E / dt / 1e9
+    gteps_eq = roots_total * E / dt / 1e9
+    gteps = (trav_edges if trav_edges is not None else roots_total * E) / dt / 1e9
     cpu = parity = None
     perm = np.random.default_rng(SEED).permutation(V).astype(np.uint32)
     if pool is None:
@@ -637,6 +664,11 @@ def report(args, stream, names, csr, step_digest, dt, roots_total, E, desc, n_ro
             "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": scaling, "vs_baseline": None, "dtype": "u32",
             "data": "synthetic", "gteps": round(gteps, 3),
+            "gteps_all_pairs_equiv": round(gteps_eq, 3),
+            "gteps_note": "gteps = edges relaxed by the traversal kernels per second (seed BFS "
+                          "rows x E_dir, or the cover Dial's rows x contracted edges; rows "
+                          "derived from neighbours' rows relax no edge); gteps_all_pairs_equiv "
+                          "= roots x E_dir / t (not work done)",
             "config": {
                 "workload": desc + (" all-sources" if n_roots <= 0 else
                                     f" {pool.size} sampled roots") +

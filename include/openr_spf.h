@@ -552,6 +552,11 @@ typedef struct ospf_sweep_info {
   uint32_t max_nh_words;     /* widest next-hop row of an owned root */
   uint64_t device_bytes;     /* rows, level rows, digests, tables */
   uint64_t step_compulsory_bytes;  /* rows written + CSR scans, per run */
+  /* edges the run's traversal kernels relax: traversed rows x edges of the
+   * graph they traverse (derive: seed BFS rows x E; weighted cover: seeds'
+   * Dial rows x contracted-graph edges; batch / LDS: roots x E). Rows
+   * derived from other rows relax no edge. TEPS = this / run time. */
+  uint64_t step_traversed_edges;
 } ospf_sweep_info;
 
 /* One launch unit of a run, timed alone on its stream (HIP events). */

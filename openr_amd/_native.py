@@ -111,7 +111,7 @@ class ospf_sweep_opts(C.Structure):  # noqa: N801
 class ospf_sweep_info(C.Structure):  # noqa: N801
     _fields_ = [("mode", u32), ("n_roots", u32), ("n_rows", u32), ("n_launches", u32),
                 ("hip_graph", u32), ("max_nh_words", u32), ("device_bytes", u64),
-                ("step_compulsory_bytes", u64)]
+                ("step_compulsory_bytes", u64), ("step_traversed_edges", u64)]
 
 
 class ospf_sweep_launch(C.Structure):  # noqa: N801

@@ -164,6 +164,7 @@ struct ospf_sweep {
   std::vector<std::pair<ospf_digest*, size_t>> dig_aux;  // intermediate digests (poisoned too)
   uint32_t* d_own_slot = nullptr;
   uint32_t n_rows = 0;
+  uint64_t trav_edges = 0;  // edges scanned by the run's traversal kernels (TEPS)
   uint64_t step_comp = 0;
   // launches
   struct Unit {
@@ -879,6 +880,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     return rc;
   s->dig_aux.push_back({ldg, std::max(1u, nc + nd)});
   s->n_rows = rows;
+  s->trav_edges = (uint64_t)nc * c->info.n_edges;  // the seed BFS rows; the rest is derived
   const uint32_t ndig = (uint32_t)own_c.size() + nL;
   if ((rc = dalloc(s, &s->dig_all, ndig))) return rc;
   s->n_dig = ndig;
@@ -1193,6 +1195,7 @@ int plan_batch(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine,
   if ((rc = dalloc(s, &s->dig_all, mine.size()))) return rc;
   s->n_dig = (uint32_t)mine.size();
   s->n_rows = (uint32_t)mine.size();
+  s->trav_edges = (uint64_t)mine.size() * c->info.n_edges;
   uint32_t slot = 0;
   const uint32_t flags = (s->opts.flags & OSPF_HOP_COUNT) | OSPF_WANT_DIST | OSPF_WANT_NH |
                          OSPF_WANT_DIGEST;
@@ -1262,6 +1265,7 @@ int plan_lds(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine) {
   if ((rc = dalloc(s, &s->dig_all, mine.size()))) return rc;
   s->n_dig = (uint32_t)mine.size();
   s->n_rows = (uint32_t)mine.size();
+  s->trav_edges = (uint64_t)mine.size() * c->info.n_edges;
   uint32_t slot = 0;
   bool first = true;
   for (auto it = ws.rbegin(); it != ws.rend(); ++it) {
@@ -1428,6 +1432,9 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     closure = clos.size() >= seeds.size() && ospf_int::closure_build(c, clos, seed_row, ch) == OSPF_OK;
     if (!closure) c->err = err0;
   }
+  // the Dial over the contracted cover graph: the seeds' rows (closure) or
+  // every cover row
+  s->trav_edges = (uint64_t)(closure ? seeds.size() : nA) * c->h_cedge.size();
   if (getenv("OSPF_SWEEP_DEBUG"))
     fprintf(stderr, "plan_wcover: cover %u seeds %zu comps %zu closure roots %zu -> %s (%s)\n", nA,
             c->cl_seed.size(), c->cl_comp_off.size() - 1, clos.size(), closure ? "closure" : "dial",
@@ -1713,6 +1720,7 @@ int plan_wderive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& min
     return rc;
   s->n_dig = nC + nl;
   s->n_rows = nC + nl;
+  s->trav_edges = (uint64_t)nC * c->info.n_edges;  // cover rows on the batch path
   std::vector<uint32_t> pos(V, kNone);
   uint32_t off = 0;
   const uint32_t flags = hop | OSPF_WANT_DIST | OSPF_WANT_NH | OSPF_WANT_DIGEST;
@@ -2007,6 +2015,7 @@ int ospf_sweep_get_info(const ospf_sweep* s, ospf_sweep_info* info) {
   info->max_nh_words = mw;
   info->device_bytes = s->device_bytes;
   info->step_compulsory_bytes = s->step_comp;
+  info->step_traversed_edges = s->trav_edges;
   return OSPF_OK;
 }
 

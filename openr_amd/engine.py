@@ -296,14 +296,18 @@ class Sweep:
     graph one run replays. ``run(stream)`` queues one sweep."""
 
     def __init__(self, engine: "Engine", *, hop_count: bool = False, mode: str = "auto",
-                 part: int = 0, n_parts: int = 1, hip_graph: bool = True, _handle=None):
+                 part: int = 0, n_parts: int = 1, hip_graph: bool = True, defer: bool = False,
+                 _handle=None):
         self._L = N.engine()
         self.engine = engine
         if _handle is not None:  # a part of an ospf_msweep (owned by it)
             self._h, self._owned = _handle, False
         else:
-            o = N.ospf_sweep_opts(N.OSPF_HOP_COUNT if hop_count else 0, N.SWEEP_MODES[mode],
-                                  part, n_parts, int(hip_graph))
+            # defer: no eager run at create (hip_graph must be off): the
+            # first run() is the first run (OSPF_SWEEP_DEFER)
+            o = N.ospf_sweep_opts((N.OSPF_HOP_COUNT if hop_count else 0) |
+                                  (N.OSPF_SWEEP_DEFER if defer else 0), N.SWEEP_MODES[mode],
+                                  part, n_parts, int(hip_graph and not defer))
             h = C.c_void_p()
             rc = self._L.ospf_sweep_create(engine._h, C.byref(o), C.byref(h))
             if rc != 0:
@@ -319,6 +323,7 @@ class Sweep:
         self.max_nh_words = int(gi.max_nh_words)
         self.device_bytes = int(gi.device_bytes)
         self.step_compulsory_bytes = int(gi.step_compulsory_bytes)
+        self.step_traversed_edges = int(gi.step_traversed_edges)
         r = np.zeros(max(1, self.n_roots), np.uint32)
         self._check(self._L.ospf_sweep_roots(self._h, r.ctypes.data))
         self.roots = r[: self.n_roots]
