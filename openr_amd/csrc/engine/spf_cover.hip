@@ -161,6 +161,113 @@ __device__ __forceinline__ void write_row(const DevGraph& g, const CoverGraph& C
   }
 }
 
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t x, int o) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x, o, kWave);
+  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), o, kWave);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Load mode with next hops (closure roots): the dist row as write_row, the
+// next-hop row [V][NW] -- cover columns from the closure's masks, a leaf by
+// the OR of its tight last hops' masks (the root itself as a last hop: the
+// leaf's own bit; LinkState.cpp:885-901) -- and the run's digest (DESIGN.md
+// §4) summed into dg.
+template <int NW>
+__device__ void write_row_nh(const DevGraph& g, const CoverGraph& C, uint32_t* row,
+                             uint32_t* nhrow, const uint32_t* s_D, const uint32_t* s_tr,
+                             uint32_t r, uint32_t rn, const uint32_t* cm, ospf_digest* dg,
+                             unsigned long long* s_acc, uint32_t tid, uint32_t nthreads) {
+  const uint32_t nS = C.nS, V = g.V, lane = tid & 63u;
+  const uint4* la4 = reinterpret_cast<const uint4*>(C.ladj);
+  const uint32_t* dn = g.dn + g.dn_off[rn];
+  const uint32_t K = g.dn_off[rn + 1] - g.dn_off[rn];
+  auto usable = [&](uint32_t ci) {
+    return ci < nS && (ci == r || ((s_tr[ci >> 5] >> (ci & 31u)) & 1u));
+  };
+  uint64_t h = 0, sum = 0;
+  uint32_t reach = 0;
+  for (uint32_t v = tid; v < V; v += nthreads) {
+    const uint32_t cx = C.cix[v];
+    uint32_t out, m[NW];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) m[w] = 0u;
+    if (!(cx & kLeaf)) {
+      out = s_D[cx];
+#pragma unroll
+      for (int w = 0; w < NW; ++w) m[w] = cm[(size_t)cx * NW + w];
+    } else {
+      const uint32_t q0 = (cx >> 5) & 0x3FFFFFFu, nq = cx & 31u;
+      out = kInf;
+      for (uint32_t qq = 0; qq < nq; ++qq) {
+        const uint4 e4 = la4[q0 + qq];
+        const uint32_t es[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const uint32_t ci = es[b] & 0xFFFFu;
+          if (!usable(ci) || s_D[ci] == kInf) continue;
+          out = min(out, s_D[ci] + (es[b] >> 16));
+        }
+      }
+      if (out != kInf)
+        for (uint32_t qq = 0; qq < nq; ++qq) {
+          const uint4 e4 = la4[q0 + qq];
+          const uint32_t es[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const uint32_t ci = es[b] & 0xFFFFu;
+            if (!usable(ci) || s_D[ci] == kInf || s_D[ci] + (es[b] >> 16) != out) continue;
+            if (ci == r) {  // a neighbour of the root: its own bit
+              uint32_t lo = 0, hi = K;
+              while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (dn[mid] < v) lo = mid + 1;
+                else hi = mid;
+              }
+              if (lo < 32u * NW) m[lo >> 5] |= 1u << (lo & 31u);
+            } else {
+#pragma unroll
+              for (int w = 0; w < NW; ++w) m[w] |= cm[(size_t)ci * NW + w];
+            }
+          }
+        }
+    }
+    if (v == rn || out == kInf) {
+#pragma unroll
+      for (int w = 0; w < NW; ++w) m[w] = 0u;
+    }
+    __builtin_nontemporal_store(out, row + v);
+#pragma unroll
+    for (int w = 0; w < NW; ++w) __builtin_nontemporal_store(m[w], nhrow + (size_t)v * NW + w);
+    if (out != kInf) {
+      reach += 1u;
+      sum += out;
+      h += g.dkey[2ull * v] * ((uint64_t)out + 1ull);
+      uint64_t ws = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w)
+        if (m[w]) ws += digest_word_key((uint32_t)w, m[w]);
+      if (ws) h += g.dkey[2ull * v + 1] * ws;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    h += shfl_xor64(h, o);
+    sum += shfl_xor64(sum, o);
+    reach += (uint32_t)__shfl_xor((int)reach, o, kWave);
+  }
+  if (lane == 0 && reach) {
+    atomicAdd(&s_acc[0], (unsigned long long)reach);
+    atomicAdd(&s_acc[1], (unsigned long long)sum);
+    atomicAdd(&s_acc[2], (unsigned long long)h);
+  }
+  __syncthreads();
+  if (tid == 0 && dg) {
+    atomicAdd((unsigned long long*)&dg->reached, s_acc[0]);
+    atomicAdd((unsigned long long*)&dg->sum_dist, s_acc[1]);
+    atomicAdd((unsigned long long*)&dg->hash, s_acc[2]);
+  }
+}
+
 // Expansion of queued nodes each from its own current distance, for the
 // delta-stepping variant: a relaxation that lowers a distance (LDS atomicMin)
 // sets the node's dirty bit and the round's flag.
@@ -324,6 +431,7 @@ __global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C
   __shared__ uint32_t s_q[kWaves][kQ];
   __shared__ uint32_t s_pre[kWaves][2 * kWave];
   __shared__ uint32_t s_next[2];
+  __shared__ unsigned long long s_acc[3];  // load mode with next hops: digest sums
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint32_t nS = C.nS, V = g.V;
   uint32_t* s_tr = s_D + nS;
@@ -338,8 +446,22 @@ __global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C
     if (a.dload) {  // cover columns given (closure rows): the full row only
       const uint32_t* src = a.dload + (size_t)i * nS;
       for (uint32_t x = tid; x < nS; x += kBlock) s_D[x] = src[x];
+      if (tid < 3) s_acc[tid] = 0ull;
       __syncthreads();
-      write_row(g, C, a.dist + (size_t)a.rowpos[i] * V, s_D, s_tr, r, tid, kBlock);
+      uint32_t* drow = a.dist + (size_t)a.rowpos[i] * V;
+      if (a.nhload) {  // and the next-hop row + digest from the masks
+        const uint32_t* cm = a.nhload + (size_t)i * nS * a.NW;
+        uint32_t* nrow = a.nh + (size_t)i * V * a.NW;
+        ospf_digest* dg = a.digest ? a.digest + i : nullptr;
+        switch (a.NW) {
+          case 1: write_row_nh<1>(g, C, drow, nrow, s_D, s_tr, r, rn, cm, dg, s_acc, tid, kBlock); break;
+          case 2: write_row_nh<2>(g, C, drow, nrow, s_D, s_tr, r, rn, cm, dg, s_acc, tid, kBlock); break;
+          case 3: write_row_nh<3>(g, C, drow, nrow, s_D, s_tr, r, rn, cm, dg, s_acc, tid, kBlock); break;
+          default: write_row_nh<4>(g, C, drow, nrow, s_D, s_tr, r, rn, cm, dg, s_acc, tid, kBlock); break;
+        }
+      } else {
+        write_row(g, C, drow, s_D, s_tr, r, tid, kBlock);
+      }
       __syncthreads();
       continue;
     }
@@ -396,6 +518,72 @@ __global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C
 // block-uniform (scalar loads). Blocks are ordered column-chunk-major and
 // spread so that one XCD's resident blocks share a chunk of the seed rows in
 // its L2.
+// With next-hop masks (NW words, KW = 8): per member the mask of its best
+// terms (a strictly better term replaces it, an equal one is ORed in) -- the
+// next hops of f towards v are the first hops of f's shortest paths to the
+// first seed s on a shortest f -> v path (LinkState.cpp:885-901: a path's
+// next hop is its first hop; the tail from s is s's own shortest path).
+template <int NW>
+__global__ void __launch_bounds__(256) closure_nh_kernel(ClosurePlan p) {
+  constexpr int KW = 8;
+  const uint32_t nb = gridDim.x, b = blockIdx.x;
+  const uint32_t full = nb / 8u * 8u;
+  const uint32_t item = b < full ? (b % 8u) * (full / 8u) + b / 8u : b;
+  const uint32_t chunk = item / p.ncomp, ci = item % p.ncomp;
+  const uint32_t v = chunk * 256u + threadIdx.x;
+  const bool ok = v < p.nS;
+  const uint2 cm = p.comp[ci];
+  uint32_t acc[KW], mk[KW][NW];
+#pragma unroll
+  for (int f = 0; f < KW; ++f) {
+    acc[f] = kClInf;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) mk[f][w] = 0u;
+  }
+  auto take = [&](int f, uint32_t c, const uint32_t* m) {
+    const bool lt = c < acc[f], le = c <= acc[f];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) mk[f][w] = (lt ? 0u : mk[f][w]) | (le ? m[w] : 0u);
+    acc[f] = min(acc[f], c);
+  };
+  const uint32_t* cst = p.cst + (size_t)cm.x * KW;
+  const uint32_t* fh = p.fh + (size_t)cm.x * KW * NW;
+  const uint32_t* jl = p.jl + cm.x;
+  for (uint32_t j0 = 0; j0 < cm.y; j0 += 8u) {
+    uint32_t x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t j = j0 + (uint32_t)u;
+      x[u] = (ok && j < cm.y) ? p.seedC[(size_t)jl[j] * p.nS + v] : kClInf;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t j = j0 + (uint32_t)u;
+      if (j >= cm.y) break;  // uniform
+#pragma unroll
+      for (int f = 0; f < KW; ++f) take(f, cst[j * KW + f] + x[u], fh + ((size_t)j * KW + f) * NW);
+    }
+  }
+  const uint32_t* mem = p.mem + (size_t)ci * KW;
+  const uint32_t* dl = p.dloc + (size_t)ci * KW * KW;
+  const uint32_t* fl = p.fhloc + (size_t)ci * KW * KW * NW;
+#pragma unroll
+  for (int m = 0; m < KW; ++m)
+    if (mem[m] == v)
+#pragma unroll
+      for (int f = 0; f < KW; ++f) take(f, dl[f * KW + m], fl + ((size_t)f * KW + m) * NW);
+  const uint32_t* out = p.out + (size_t)ci * KW;
+#pragma unroll
+  for (int f = 0; f < KW; ++f) {
+    if (!ok || out[f] == kInf) continue;
+    const bool un = acc[f] >= kClInf;
+    p.dc[(size_t)out[f] * p.nS + v] = un ? kInf : acc[f];
+    uint32_t* dm = p.dcm + ((size_t)out[f] * p.nS + v) * NW;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) dm[w] = un ? 0u : mk[f][w];
+  }
+}
+
 template <int KW>
 __global__ void __launch_bounds__(256) closure_kernel(ClosurePlan p) {
   const uint32_t nb = gridDim.x, b = blockIdx.x;
@@ -442,6 +630,17 @@ __global__ void __launch_bounds__(256) closure_kernel(ClosurePlan p) {
 hipError_t launch_closure(const ClosurePlan& p, uint32_t KW, hipStream_t s) {
   if (p.ncomp == 0) return hipSuccess;
   const dim3 grid(p.ncomp * p.chunks);
+  if (p.NW) {
+    if (KW != 8 || !p.fh || !p.fhloc || !p.dcm) return hipErrorInvalidValue;
+    switch (p.NW) {
+      case 1: hipLaunchKernelGGL(closure_nh_kernel<1>, grid, dim3(256), 0, s, p); break;
+      case 2: hipLaunchKernelGGL(closure_nh_kernel<2>, grid, dim3(256), 0, s, p); break;
+      case 3: hipLaunchKernelGGL(closure_nh_kernel<3>, grid, dim3(256), 0, s, p); break;
+      case 4: hipLaunchKernelGGL(closure_nh_kernel<4>, grid, dim3(256), 0, s, p); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   if (KW <= 8) hipLaunchKernelGGL(closure_kernel<8>, grid, dim3(256), 0, s, p);
   else if (KW <= 16) hipLaunchKernelGGL(closure_kernel<16>, grid, dim3(256), 0, s, p);
   else return hipErrorInvalidValue;
@@ -452,6 +651,7 @@ hipError_t launch_cover_spf(const DevGraph& g, const CoverGraph& C, const CoverA
                             uint32_t n_cu, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
   if (a.dload && !a.rowpos) return hipErrorInvalidValue;  // load mode writes rows by position
+  if (a.nhload && (!a.dload || !a.nh || a.NW == 0 || a.NW > kClMaxNW)) return hipErrorInvalidValue;
   const char* e = getenv("OSPF_COVER_DELTA");
   if (e && !a.rowpos && !a.dcomp && !a.dload) {  // delta-stepping (experiment)
     const uint32_t delta = (uint32_t)std::max(1, atoi(e));

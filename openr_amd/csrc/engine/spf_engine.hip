@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <map>
+#include <unordered_map>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -838,11 +839,12 @@ static void cover_closure_split(ospf_ctx* c) {
 
 namespace ospf_int {
 int closure_build(ospf_ctx* c, const std::vector<uint32_t>& roots,
-                  const std::vector<uint32_t>& seed_row, ClosureHost& h) {
+                  const std::vector<uint32_t>& seed_row, ClosureHost& h, uint32_t NW) {
   constexpr uint32_t kN = ~0u;
   const uint32_t nS = (uint32_t)c->h_ccv.size();
   if (c->cl_seed.empty()) return fail(c, OSPF_E_INVAL, "closure: no seed split of the cover");
   if (c->dist_bound >= ospf::kClInf) return fail(c, OSPF_E_RANGE, "closure: distances may reach 2^30");
+  if (NW > ospf::kClMaxNW) return fail(c, OSPF_E_RANGE, "closure: next-hop masks of more than 4 words");
   std::vector<uint32_t> cidx(c->info.n_nodes, kN);
   for (uint32_t i = 0; i < nS; ++i) cidx[c->h_ccv[i]] = i;
   const uint32_t ncomp_all = (uint32_t)c->cl_comp_off.size() - 1;
@@ -860,19 +862,35 @@ int closure_build(ospf_ctx* c, const std::vector<uint32_t>& roots,
     }
   }
   const uint32_t KW = kmax <= 8 ? 8u : 16u;
+  if (NW && KW != 8) return fail(c, OSPF_E_RANGE, "closure: next-hop masks need components of <= 8");
   const uint32_t nq = (uint32_t)comps.size();
   h.KW = KW;
+  h.NW = NW;
   h.comp.assign(nq, make_uint2(0, 0));
   h.jl.clear();
   h.cst.clear();
+  h.fh.clear();
   h.mem.assign((size_t)nq * KW, kN);
   h.dloc.assign((size_t)nq * KW * KW, kN);
+  h.fhloc.assign((size_t)nq * KW * KW * NW, 0u);
   h.out.assign((size_t)nq * KW, kN);
   auto transit = [&](uint32_t i) { return (c->h_cctr[i >> 5] >> (i & 31u)) & 1u; };
+  auto node_transit = [&](uint32_t v) { return !((c->h_nt[v >> 5] >> (v & 31u)) & 1u); };
   const auto& crow = c->h_ccrow;
   const auto& ced = c->h_cedge;
   std::vector<uint32_t> jof(nS, kN);  // seed -> term of the current component
   std::vector<uint64_t> d(KW);
+  // next-hop masks (NW words) per member: first hops of f's shortest paths
+  // to it inside the component
+  std::vector<uint32_t> Mk((size_t)KW * ospf::kClMaxNW);
+  // f's contracted out-edges with the next-hop bits achieving each one's
+  // weight: the direct link (bit of the neighbour) and every transit leaf
+  // detour f -> x -> b (bit of x), LinkState.cpp:885-901 with f the root
+  struct EM {
+    uint64_t w;
+    uint32_t m[ospf::kClMaxNW];
+  };
+  std::unordered_map<uint32_t, EM> em;
   for (uint32_t i = 0; i < (uint32_t)roots.size(); ++i) {
     const uint32_t ci = cidx[roots[i]], k = c->cl_comp_of[ci];
     const uint32_t* M = c->cl_comp_mem.data() + c->cl_comp_off[k];
@@ -893,11 +911,58 @@ int closure_build(ospf_ctx* c, const std::vector<uint32_t>& roots,
     const uint32_t joff = (uint32_t)h.jl.size();
     std::vector<uint32_t> used;  // seeds given a term (jof reset after)
     for (uint32_t f = 0; f < kk; ++f) {
-      // distances inside the component from f: members relay when transit
-      // (f itself always: the root), Bellman-Ford over <= 16 nodes
+      if (NW) {  // f's out-edge masks from its CSR row
+        em.clear();
+        const uint32_t fn = c->h_ccv[M[f]];
+        const uint32_t* dn = c->h_dn.data() + c->h_dn_off[fn];
+        const uint32_t K = c->h_dn_off[fn + 1] - c->h_dn_off[fn];
+        if (K > 32u * NW) return fail(c, OSPF_E_RANGE, "closure: a root with more neighbours than masks");
+        auto cand = [&](uint32_t cb, uint64_t w, uint32_t bit) {
+          auto it = em.find(cb);
+          if (it == em.end()) {
+            EM x{w, {0u, 0u, 0u, 0u}};
+            x.m[bit >> 5] = 1u << (bit & 31u);
+            em.emplace(cb, x);
+          } else if (w < it->second.w) {
+            it->second = EM{w, {0u, 0u, 0u, 0u}};
+            it->second.m[bit >> 5] = 1u << (bit & 31u);
+          } else if (w == it->second.w) {
+            it->second.m[bit >> 5] |= 1u << (bit & 31u);
+          }
+        };
+        for (uint32_t e = c->h_prow[fn]; e < c->h_prow[fn + 1]; ++e) {
+          const uint32_t y = c->h_pcolx[e];
+          if ((y & 0x80000000u) || y == fn) continue;  // down / padding, self-loop
+          const uint32_t bit = (uint32_t)(std::lower_bound(dn, dn + K, y) - dn);
+          if (cidx[y] != kN) {
+            cand(cidx[y], c->h_pw[e], bit);
+          } else if (node_transit(y)) {  // a leaf detour
+            for (uint32_t e2 = c->h_prow[y]; e2 < c->h_prow[y + 1]; ++e2) {
+              const uint32_t b = c->h_pcolx[e2];
+              if ((b & 0x80000000u) || b == y || b == fn || cidx[b] == kN) continue;
+              cand(cidx[b], (uint64_t)c->h_pw[e] + c->h_pw[e2], bit);
+            }
+          }
+        }
+      }
+      // the mask an edge u -> (cover index x, weight w) hands on: f's own edge
+      // masks from f, the tail's mask otherwise
+      auto emask = [&](uint32_t u, uint32_t x, uint64_t w, const uint32_t*& m) {
+        if (u != f) {
+          m = Mk.data() + (size_t)u * ospf::kClMaxNW;
+          return true;
+        }
+        auto it = em.find(x);
+        if (it == em.end() || it->second.w != w) return false;  // inconsistent contraction
+        m = it->second.m;
+        return true;
+      };
+      // distances (and masks) inside the component from f: members relay when
+      // transit (f itself always: the root), Bellman-Ford over <= 16 nodes
       std::fill(d.begin(), d.end(), UINT64_MAX);
+      std::fill(Mk.begin(), Mk.end(), 0u);
       d[f] = 0;
-      for (uint32_t it = 0; it < kk; ++it) {
+      for (uint32_t it = 0; it <= kk; ++it) {
         bool ch = false;
         for (uint32_t u = 0; u < kk; ++u) {
           if (d[u] == UINT64_MAX || (u != f && !transit(M[u]))) continue;
@@ -905,16 +970,30 @@ int closure_build(ospf_ctx* c, const std::vector<uint32_t>& roots,
             const uint32_t x = local(ced[e].x);
             if (x == kN) continue;
             const uint64_t nd = d[u] + ced[e].y;
+            const uint32_t* m = nullptr;
+            if (NW && !emask(u, ced[e].x, ced[e].y, m))
+              return fail(c, OSPF_E_RANGE, "closure: contracted edge without its next hops");
+            uint32_t* mx = Mk.data() + (size_t)x * ospf::kClMaxNW;
             if (nd < d[x]) {
               d[x] = nd;
+              for (uint32_t w = 0; w < NW; ++w) mx[w] = m[w];
               ch = true;
+            } else if (NW && nd == d[x]) {
+              for (uint32_t w = 0; w < NW; ++w) {
+                ch |= (mx[w] | m[w]) != mx[w];
+                mx[w] |= m[w];
+              }
             }
           }
         }
         if (!ch) break;
       }
-      for (uint32_t m = 0; m < kk; ++m)
+      for (uint32_t m = 0; m < kk; ++m) {
         h.dloc[((size_t)q * KW + f) * KW + m] = d[m] >= ospf::kClInf ? ospf::kClInf : (uint32_t)d[m];
+        for (uint32_t w = 0; w < NW; ++w)
+          h.fhloc[(((size_t)q * KW + f) * KW + m) * NW + w] =
+              d[m] >= ospf::kClInf ? 0u : Mk[(size_t)m * ospf::kClMaxNW + w];
+      }
       for (uint32_t g = 0; g < kk; ++g) {
         if (d[g] == UINT64_MAX || (g != f && !transit(M[g]))) continue;
         for (uint32_t e = crow[M[g]]; e < crow[M[g] + 1]; ++e) {
@@ -925,11 +1004,21 @@ int closure_build(ospf_ctx* c, const std::vector<uint32_t>& roots,
             jof[x] = (uint32_t)h.jl.size() - joff;
             h.jl.push_back(seed_row[x]);
             h.cst.resize(h.jl.size() * KW, ospf::kClInf);
+            h.fh.resize(h.jl.size() * KW * NW, 0u);
             used.push_back(x);
           }
           const uint64_t cc = d[g] + ced[e].y;
-          uint32_t& dst = h.cst[(size_t)(joff + jof[x]) * KW + f];
-          if (cc < dst) dst = (uint32_t)cc;  // (dst <= kClInf)
+          const size_t ti = (size_t)(joff + jof[x]) * KW + f;
+          uint32_t& dst = h.cst[ti];
+          const uint32_t* m = nullptr;
+          if (NW && !emask(g, x, ced[e].y, m))
+            return fail(c, OSPF_E_RANGE, "closure: contracted edge without its next hops");
+          if (cc < dst) {  // (dst <= kClInf)
+            dst = (uint32_t)cc;
+            for (uint32_t w = 0; w < NW; ++w) h.fh[ti * NW + w] = m[w];
+          } else if (NW && cc == dst) {
+            for (uint32_t w = 0; w < NW; ++w) h.fh[ti * NW + w] |= m[w];
+          }
         }
       }
     }
@@ -939,7 +1028,10 @@ int closure_build(ospf_ctx* c, const std::vector<uint32_t>& roots,
   if (h.jl.empty()) {  // no seed terms at all: one unused row keeps the arrays non-empty
     h.jl.push_back(0);
     h.cst.assign(KW, ospf::kClInf);
+    h.fh.assign((size_t)KW * std::max(NW, 1u), 0u);
   }
+  if (h.fh.empty()) h.fh.assign(1, 0u);
+  if (h.fhloc.empty()) h.fhloc.assign(1, 0u);
   return OSPF_OK;
 }
 }  // namespace ospf_int
@@ -2570,6 +2662,8 @@ int ospf_update_rows(ospf_ctx* c, const ospf_csr* csr, const uint32_t* rows, uin
   // ---- commit
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipDeviceSynchronize());  // no batch may be reading the graph
+  if (!new_lids.empty() && 2ull * (new_lids.back() + 1) > c->h_link_e.size())
+    c->h_link_e.resize(2ull * (new_lids.back() + 1), kNo);  // ids past the last one in use
   uint32_t* base = (uint32_t*)c->d_graph;
   auto woff = [&](const void* p) { return (size_t)((const char*)p - (const char*)base) / 4; };
   // positions of the old lids inside rebuilt rows leave link_e (the other

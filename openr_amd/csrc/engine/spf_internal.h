@@ -113,13 +113,18 @@ int twin_lv_launch(ospf_ctx* c, const ospf::TwinLvPlan& p, void* stream);
 // closure roots `roots` (node ids, non-seed cover nodes; dc row i = roots[i])
 // with the seeds' cover columns at seedC row seed_row[cover index] (~0u: not
 // given -> OSPF_E_INVAL). KW = 8 or 16 (largest component, padded).
+// NW > 0 (<= kClMaxNW, components of <= 8): also the next-hop masks -- fh
+// [term][member][NW] the first hops of the member's shortest paths to the
+// term's seed inside the component, fhloc [component][member][member][NW]
+// those to each member -- so the closure writes the next hops of its cover
+// columns (bit k = the root's k-th distinct neighbour).
 struct ClosureHost {
-  uint32_t KW = 8;
+  uint32_t KW = 8, NW = 0;
   std::vector<uint2> comp;
-  std::vector<uint32_t> jl, cst, mem, dloc, out;
+  std::vector<uint32_t> jl, cst, mem, dloc, out, fh, fhloc;
 };
 int closure_build(ospf_ctx* c, const std::vector<uint32_t>& roots,
-                  const std::vector<uint32_t>& seed_row, ClosureHost& h);
+                  const std::vector<uint32_t>& seed_row, ClosureHost& h, uint32_t NW = 0);
 
 // ospf_wderive_wide_dev with a chunk size (256-node tiles per block; 0: the
 // launcher's default) -- the sweep's wide cover roots run beside the leaves

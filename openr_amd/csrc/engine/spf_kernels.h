@@ -285,6 +285,15 @@ struct CoverArgs {
   uint32_t* dcomp = nullptr;         // [n][nS] cover columns out, unreached = kClInf (a
                                      // non-transit root: 0 at itself only -- it relays nothing)
   const uint32_t* dload = nullptr;   // [n][nS] cover columns given: no Dial, rows only
+  // load mode with next hops (closure roots): the cover columns' next-hop
+  // masks [n][nS][NW] given; the root's next-hop row [V][NW] written at
+  // nh + rowpos-independent i * V * NW (leaves: OR over their tight last
+  // hops, the root's own leaves their bit) and its digest (zeroed by the
+  // caller) accumulated
+  const uint32_t* nhload = nullptr;
+  uint32_t* nh = nullptr;
+  uint32_t NW = 0;
+  ospf_digest* digest = nullptr;
 };
 hipError_t launch_cover_spf(const DevGraph& g, const CoverGraph& C, const CoverArgs& a,
                             uint32_t n_cu, hipStream_t s);
@@ -309,7 +318,15 @@ struct ClosurePlan {
   const uint32_t* out;     // [ncomp][KW] dc row of member f (0xFFFFFFFF: not needed)
   const uint32_t* seedC;   // [seeds][nS] (unreached: kClInf)
   uint32_t* dc;            // [rows][nS] (unreached: 0xFFFFFFFF)
+  // next-hop masks (NW words, 0: none; KW = 8): fh [terms][KW][NW], fhloc
+  // [ncomp][KW][KW][NW] first hops to the term's seed / to member m; dcm
+  // [rows][nS][NW] the cover columns' next hops out (tight terms ORed)
+  uint32_t NW = 0;
+  const uint32_t* fh = nullptr;
+  const uint32_t* fhloc = nullptr;
+  uint32_t* dcm = nullptr;
 };
+constexpr uint32_t kClMaxNW = 4;
 hipError_t launch_closure(const ClosurePlan& p, uint32_t KW, hipStream_t s);
 
 // Weighted derive (spf_wderive.hip): dist + next-hop rows (one word) of n

@@ -1355,12 +1355,60 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     return rc;
   uint32_t kmax = 1;
   for (uint32_t r : need_l) kmax = std::max(kmax, f.nbrs(r));
-  // digests: cover classes (owned), then need_l (owned leaves first)
+  // (A) plan: cover rows by the closure when the cover splits into seeds and
+  // small components (the seeds' Dial, the closure's cover columns, then the
+  // full rows), else every row by the Dial. With one word count <= 4 over
+  // the closure roots, the closure also carries their next hops (masks of
+  // first hops per seed term): their next-hop rows then come out of the
+  // rows unit and no neighbour-row derivation runs for them.
+  std::vector<uint32_t> seeds, clos;
+  ospf_int::ClosureHost ch;
+  bool closure = !c->cl_seed.empty() && !getenv("OSPF_COVER_NOCLOSURE");
+  uint32_t NW = 0;
+  if (closure) {
+    const uint32_t nS = (uint32_t)c->h_ccv.size();
+    std::vector<uint32_t> seed_row(nS, kNone);
+    for (uint32_t j = 0; j < c->cl_seed.size(); ++j) {
+      seed_row[c->cl_seed[j]] = j;
+      seeds.push_back(c->h_ccv[c->cl_seed[j]]);
+    }
+    std::vector<uint8_t> is_seed(V, 0);
+    for (uint32_t v : seeds) is_seed[v] = 1;
+    for (uint32_t v : cover_a)
+      if (!is_seed[v]) clos.push_back(v);
+    const std::string err0 = c->err;  // a plan that does not apply is no error of the sweep
+    NW = clos.empty() ? 0u : f.words(clos[0]);
+    for (uint32_t r : clos)
+      if (f.words(r) != NW) NW = 0;
+    if (NW > ospf::kClMaxNW || getenv("OSPF_CLOSURE_NONH")) NW = 0;
+    closure = clos.size() >= seeds.size() && ospf_int::closure_build(c, clos, seed_row, ch, NW) == OSPF_OK;
+    if (!closure && NW) {  // the masks do not apply: distances only
+      NW = 0;
+      closure = ospf_int::closure_build(c, clos, seed_row, ch, 0) == OSPF_OK;
+    }
+    if (!closure) {
+      c->err = err0;
+      NW = 0;
+    }
+  }
+  const bool cl_nh = closure && NW > 0;
+  std::vector<uint8_t> nh_by_closure(V, 0);
+  if (cl_nh)
+    for (uint32_t r : clos) nh_by_closure[r] = 1;
+  {
+    std::vector<uint32_t> keep;
+    for (uint32_t r : c_der)
+      if (!nh_by_closure[r]) keep.push_back(r);
+    c_der.swap(keep);
+  }
+  // digests: cover classes (owned), then need_l (owned leaves first), then
+  // the closure roots (next hops by the closure)
   std::vector<uint32_t> wset;
   for (uint32_t r : c_der) wset.push_back(f.words(r));
   std::sort(wset.begin(), wset.end());
   wset.erase(std::unique(wset.begin(), wset.end()), wset.end());
-  const uint32_t ndig = (uint32_t)(c_der.size() + c_wide.size() + nL);
+  const uint32_t ncl_dig = cl_nh ? (uint32_t)clos.size() : 0u;
+  const uint32_t ndig = (uint32_t)(c_der.size() + c_wide.size() + nL) + ncl_dig;
   if ((rc = dalloc(s, &s->dig_all, ndig))) return rc;
   s->n_dig = ndig;
   s->n_rows = nA + nL;
@@ -1411,27 +1459,6 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     s->step_comp += u.comp;
     s->units.push_back(std::move(u));
   }
-  // (A) cover rows: by the closure when the cover splits into seeds and
-  // small components (the seeds' Dial, the closure's cover columns, then the
-  // full rows), else every row by the Dial
-  std::vector<uint32_t> seeds, clos;
-  ospf_int::ClosureHost ch;
-  bool closure = !c->cl_seed.empty() && !getenv("OSPF_COVER_NOCLOSURE");
-  if (closure) {
-    const uint32_t nS = (uint32_t)c->h_ccv.size();
-    std::vector<uint32_t> seed_row(nS, kNone);
-    for (uint32_t j = 0; j < c->cl_seed.size(); ++j) {
-      seed_row[c->cl_seed[j]] = j;
-      seeds.push_back(c->h_ccv[c->cl_seed[j]]);
-    }
-    std::vector<uint8_t> is_seed(V, 0);
-    for (uint32_t v : seeds) is_seed[v] = 1;
-    for (uint32_t v : cover_a)
-      if (!is_seed[v]) clos.push_back(v);
-    const std::string err0 = c->err;  // a plan that does not apply is no error of the sweep
-    closure = clos.size() >= seeds.size() && ospf_int::closure_build(c, clos, seed_row, ch) == OSPF_OK;
-    if (!closure) c->err = err0;
-  }
   // the Dial over the contracted cover graph: the seeds' rows (closure) or
   // every cover row
   s->trav_edges = (uint64_t)(closure ? seeds.size() : nA) * c->h_cedge.size();
@@ -1467,6 +1494,25 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     cp.seedC = seedC;
     cp.dc = dc;
     const uint32_t KW = ch.KW;
+    // next hops of the closure roots: masks in, the cover columns' masks out
+    // of the closure, rows + digests out of the rows unit
+    uint32_t *d_fh = nullptr, *d_fhl = nullptr, *dcm = nullptr, *cnh = nullptr;
+    ospf_digest* cdg = nullptr;
+    if (cl_nh) {
+      if ((rc = upload(s, &d_fh, ch.fh)) || (rc = upload(s, &d_fhl, ch.fhloc)) ||
+          (rc = dalloc(s, &dcm, (size_t)ncl * nS * NW)) || (rc = dalloc(s, &cnh, (size_t)ncl * V * NW)))
+        return rc;
+      cp.NW = NW;
+      cp.fh = d_fh;
+      cp.fhloc = d_fhl;
+      cp.dcm = dcm;
+      cdg = s->dig_all + (ndig - ncl_dig);
+      std::vector<uint8_t> mine_m(V, 0);
+      for (uint32_t r : mine) mine_m[r] = 1;
+      for (uint32_t j = 0; j < ncl; ++j)
+        if (mine_m[clos[j]])
+          own(s, clos[j], ndig - ncl_dig + j, slab + (size_t)clos_rp[j] * V, cnh + (size_t)j * V * NW, NW);
+    }
     {
       ospf_sweep::Unit u;
       u.name = "cover_seeds";
@@ -1492,11 +1538,14 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     {
       ospf_sweep::Unit u;
       u.name = "cover_closure";
-      u.kernel = "closure_kernel<" + std::to_string(KW) +
-                 "> (cover columns of the components' roots from the seeds' columns)";
+      u.kernel = cl_nh ? "closure_nh_kernel<" + std::to_string(NW) +
+                             "> (cover columns + their next-hop masks of the components' roots "
+                             "from the seeds' columns)"
+                       : "closure_kernel<" + std::to_string(KW) +
+                             "> (cover columns of the components' roots from the seeds' columns)";
       u.stream = 0;
       u.n_roots = ncl;
-      u.comp = (uint64_t)ncl * 4ull * nS;
+      u.comp = (uint64_t)ncl * 4ull * nS * (1 + NW);
       u.fn = [=](hipStream_t strm) {
         const hipError_t e = ospf::launch_closure(cp, KW, strm);
         return e == hipSuccess ? OSPF_OK : ospf_int::hip_fail(c, e, "launch_closure");
@@ -1507,13 +1556,18 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     {
       ospf_sweep::Unit u;
       u.name = "cover_rows";
-      u.kernel = "cover_spf_kernel (full rows of the closure's roots: cover columns given, leaves "
-                 "by their last hop)";
+      u.kernel = cl_nh ? "cover_spf_kernel (full dist + next-hop rows and digests of the "
+                         "closure's roots: cover columns given, leaves by their last hop)"
+                       : "cover_spf_kernel (full rows of the closure's roots: cover columns "
+                         "given, leaves by their last hop)";
       u.stream = 0;
       u.record = ev_a;
       u.n_roots = ncl;
-      u.comp = (uint64_t)ncl * 4ull * V;
+      u.W = NW;
+      u.comp = (uint64_t)ncl * 4ull * V * (1 + NW);
       u.fn = [=](hipStream_t strm) {
+        if (cdg && hipMemsetAsync(cdg, 0, (size_t)ncl * sizeof(ospf_digest), strm) != hipSuccess)
+          return ospf_int::fail(c, OSPF_E_DEVICE, "hipMemsetAsync closure digests");
         ospf::CoverArgs a{};
         a.roots = d_cl;
         a.n = ncl;
@@ -1521,6 +1575,10 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
         a.err = c->d_err;
         a.rowpos = d_crp;
         a.dload = dc;
+        a.nhload = dcm;
+        a.nh = cnh;
+        a.NW = NW;
+        a.digest = cdg;
         const hipError_t e = ospf::launch_cover_spf(c->g, c->cover, a, (uint32_t)c->n_cu, strm);
         return e == hipSuccess ? OSPF_OK : ospf_int::hip_fail(c, e, "launch_cover_spf");
       };
