@@ -38,12 +38,13 @@ def lib():
         L.orc_free.argtypes = [vp]
         L.orc_apply.argtypes = [vp, vp, u32, u32, vp]
         for f in ("orc_spf_text", "orc_kth_paths_text", "orc_links_text", "orc_ksp2_text",
-                  "orc_ucmp_text"):
+                  "orc_ucmp_text", "orc_ksp2_text_threads"):
             getattr(L, f).restype = C.POINTER(C.c_char)
         L.orc_spf_text.argtypes = [vp, cp, i32]
         L.orc_kth_paths_text.argtypes = [vp, cp, cp, i32]
         L.orc_links_text.argtypes = [vp, cp]
         L.orc_ksp2_text.argtypes = [vp, cp, cp, u32]
+        L.orc_ksp2_text_threads.argtypes = [vp, cp, cp, u32, i32]
         L.orc_ucmp_text.argtypes = [vp, cp, cp, u32, i32, i32]
         L.orc_metric_a_to_b.argtypes = [vp, cp, cp, i32]
         L.orc_metric_a_to_b.restype = C.c_int64
@@ -103,7 +104,11 @@ class Oracle:
         t = _take(lib().orc_kth_paths_text(self._h, src.encode(), dst.encode(), k))
         return [ln.split(",") for ln in t.splitlines()]
 
-    def ksp2_text(self, src: str, dsts: Sequence[str]) -> str:
+    def ksp2_text(self, src: str, dsts: Sequence[str], threads: int = 1) -> str:
+        if threads > 1:
+            return _take(lib().orc_ksp2_text_threads(self._h, src.encode(),
+                                                     "\n".join(dsts).encode(), len(dsts),
+                                                     threads))
         return _take(lib().orc_ksp2_text(self._h, src.encode(),
                                          "\n".join(dsts).encode(), len(dsts)))
 

@@ -974,6 +974,69 @@ char* orc_ksp2_text(void* h, const char* src, const char* dstsNl, uint32_t n) {
   return dupString(os.str());
 }
 
+// orc_ksp2_text on `threads` host threads (the KSP2 bench's CPU baseline):
+// the memoised SPF of src is made once, then every destination's
+// getKthPaths(src, d, 1) trace, its masked rerun runSpf(src, true, k = 1
+// links) and the k = 2 trace run on the threads (LinkState.cpp:790-819,
+// kthPaths above without the shared memo). Same text as orc_ksp2_text.
+char* orc_ksp2_text_threads(void* h, const char* src, const char* dstsNl, uint32_t n,
+                            int threads) {
+  Oracle* o = (Oracle*)h;
+  std::vector<std::string> dsts;
+  const char* p = dstsNl;
+  for (uint32_t i = 0; i < n; ++i) {
+    const char* q = strchr(p, '\n');
+    if (!q) q = p + strlen(p);
+    dsts.emplace_back(p, q);
+    p = *q ? q + 1 : q;
+  }
+  const std::string s(src);
+  const SpfResult& base = o->g.spf(s, true);  // serial: the memo is not shared below
+  auto tracesOf = [&](const SpfResult& r, const std::string& d) {
+    std::vector<Path> paths;
+    if (!r.count(d)) return paths;
+    EdgeSet seen;
+    auto pth = o->g.trace(s, d, r, seen);
+    while (pth && !pth->empty()) {
+      paths.push_back(std::move(*pth));
+      pth = o->g.trace(s, d, r, seen);
+    }
+    return paths;
+  };
+  std::vector<std::string> out(n);
+  std::atomic<uint32_t> next{0};
+  auto work = [&]() {
+    for (uint32_t i; (i = next.fetch_add(1)) < n;) {
+      const std::vector<Path> k1 = tracesOf(base, dsts[i]);
+      EdgeSet skip;
+      for (const auto& path : k1)
+        for (const auto& e : path) skip.insert(e);
+      std::vector<Path> k2;
+      if (skip.empty()) {
+        k2 = k1;
+      } else {
+        const SpfResult r = o->g.dijkstra(s, true, &skip);
+        k2 = tracesOf(r, dsts[i]);
+      }
+      std::ostringstream os;
+      for (const auto& path : k2) {
+        for (size_t j = 0; j < path.size(); ++j) os << (j ? "," : "") << path[j]->key();
+        os << '\n';
+      }
+      os << "=\n";
+      out[i] = os.str();
+    }
+  };
+  if (threads < 1) threads = 1;
+  std::vector<std::thread> pool;
+  for (int t = 1; t < threads; ++t) pool.emplace_back(work);
+  work();
+  for (auto& t : pool) t.join();
+  std::string all;
+  for (const auto& x : out) all += x;
+  return dupString(all);
+}
+
 }  // extern "C"
 
 // Iteration order of std::unordered_map<int, T> built from an initializer

@@ -99,7 +99,8 @@ def test_link_down_up_random_graphs(seed, unit):
     assert s1["link_patches"] - s0["link_patches"] == events
     assert p.spf_runs == o.spf_runs
     # all-sources sweep and every root's digest on the patched graph
-    assert np.array_equal(p.all_sources_digests(), o.fast_digests(names, True, threads=8))
+    ids = p.node_names()  # all_sources_digests: node-id order
+    assert np.array_equal(p.all_sources_digests(), o.fast_digests(ids, True, threads=8))
     check(o, p, names, rng, all_digests=True)
 
 

@@ -35,3 +35,15 @@ def test_fast_matches_reference_shaped_generators(stream):
     names = LinkState(stream=st).node_names()
     roots = names[:: max(1, len(names) // 40)]
     assert np.array_equal(o.fast_digests(roots, threads=4), o.digests(roots, threads=4))
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_threaded_ksp2_matches_serial(seed):
+    """The KSP2 bench's multi-threaded CPU baseline (orc_ksp2_text_threads)
+    gives the reference-shaped getKthPaths(src, d, 2) text of the serial
+    restatement for every destination."""
+    from graphs import random_stream
+    st, names = random_stream(300 + seed, n=30, p=0.25)
+    o, o2 = Oracle(st), Oracle(st)
+    for src in names[:4]:
+        assert o2.ksp2_text(src, names, threads=4) == o.ksp2_text(src, names)
