@@ -302,8 +302,10 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db) 
       if (incremental_) incStats_.dropped += memoMetric_.size() + memoHops_.size();
       clearMemo();
     }
-    patchStructure(ch.addedLinks, removedLinks);
+    // kept links' metric / up changes first (on the rows as they are), so the
+    // rebuilt rows and their partners agree when the structure is patched
     if (!deltas.empty() || !nodeDeltas.empty()) patchGraph(deltas, nodeDeltas);
+    patchStructure(ch.addedLinks, removedLinks);
     return ch;
   }
   if (incremental_ && !structural && snapVersion_ == version_ && keepsContract) {

@@ -53,10 +53,16 @@ def main():
     ap.add_argument("--planes", type=int, default=8)
     ap.add_argument("--src", default="2-0-0")
     ap.add_argument("--cap", type=int, default=1024, help="record words per destination and k")
-    ap.add_argument("--parity-sample", type=int, default=6)
+    ap.add_argument("--parity-sample", type=int, default=256,
+                    help="destinations checked against the oracle and timed on the CPU "
+                         "(role-stratified: spines of every plane, fabric and rack switches)")
     ap.add_argument("--parity-extra", default="1-3-5,1-7-35,3-900-17")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the host cores granted")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-lfa", action="store_true", help="KSP2 launches only (PMC passes)")
     ap.add_argument("--iso-reps", type=int, default=3)
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r04", "ksp2_pmc.json"),
+                    help="measured HBM bytes per KSP2 launch (scripts/pmc_sum.py)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -100,7 +106,7 @@ def main():
         c = cols[rp[u]:rp[u + 1]]
         return len(set(int(x) for x in c) - {int(u)})
     lfa = {}
-    for u in mine:
+    for u in ([] if args.no_lfa else mine):
         cnt = nbr_count(int(u))
         lfa.setdefault(max(1, (cnt + 31) // 32), []).append((int(u), cnt))
     lfa_bufs = []
@@ -172,19 +178,35 @@ def main():
         keys = ls.link_keys()
         ls_ids = {nm: i for i, nm in enumerate(names)}
         rng = np.random.default_rng(0x5EED)
-        sample = [int(x) for x in rng.choice(n, args.parity_sample, replace=False)]
-        # plus spines of other planes and a far rack: the widest k = 2 DAGs
+        # role-stratified destinations: a quarter spines spread over every
+        # plane (other planes' spines: the widest k = 2 DAGs), the rest fabric
+        # and rack switches of other pods and of the source's own pod
+        role = np.array([int(names[int(x)].split("-")[0]) for x in dsts])
+        k = args.parity_sample
+        pick = []
+        for r_, share in ((1, k // 4), (2, (3 * k) // 8), (3, k - k // 4 - (3 * k) // 8)):
+            cand = np.nonzero(role == r_)[0]
+            if cand.size:
+                pick.extend(int(x) for x in rng.choice(cand, min(share, cand.size), replace=False))
+        sample = sorted(set(pick))
         for nm in args.parity_extra.split(","):
             if nm in ls_ids:
-                sample.append(int(np.searchsorted(dsts, ls_ids[nm])))
+                j = int(np.searchsorted(dsts, ls_ids[nm]))
+                if j < n and dsts[j] == ls_ids[nm] and j not in sample:
+                    sample.append(j)
         r1 = decode_paths(k1.cpu().numpy().view(np.uint32)[sample], status[sample],
                           N.OSPF_KSP_OVF1)
         r2 = decode_paths(k2.cpu().numpy().view(np.uint32)[sample], status[sample],
                           N.OSPF_KSP_OVF1 | N.OSPF_KSP_OVF2)
         o = Oracle(stream)
         sn = [names[int(dsts[i])] for i in sample]
+        threads = args.cpu_threads or max(1, min(len(os.sched_getaffinity(0)),
+                                                 int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+                                                 or len(os.sched_getaffinity(0))))
         tc = time.perf_counter()
-        txt = o.ksp2_text(args.src, sn)  # k = 2 per destination (k = 1 inside)
+        # k = 2 per destination (the source's SPF once, then k = 1 trace,
+        # masked rerun and k = 2 trace per destination on the threads)
+        txt = o.ksp2_text(args.src, sn, threads=threads)
         ct = time.perf_counter() - tc
         want2 = [blk for blk in txt.split("=\n")][: len(sn)]
         ok = True
@@ -195,12 +217,19 @@ def main():
                 continue  # host-path destinations are not the device's result
             ok &= got1 == o.kth_paths(args.src, d, 1)
             ok &= got2 == want2[j]
-        parity = bool(ok)
-        cpu = {"value": round(len(sn) / ct, 4), "unit": "destinations/s", "cores": 1,
+        parity = {"equal": bool(ok), "destinations": len(sn),
+                  "by_role": {"spine": int(sum(1 for x in sn if x.startswith("1-"))),
+                              "fabric": int(sum(1 for x in sn if x.startswith("2-"))),
+                              "rack": int(sum(1 for x in sn if x.startswith("3-")))},
+                  "source": "device k = 1 and k = 2 path records vs the reference-shaped "
+                            "getKthPaths restatement (oracle/), link by link"}
+        cpu = {"value": round(len(sn) / ct, 4), "unit": "destinations/s", "cores": threads,
                "kind": "port",
-               "sample": f"{len(sn)} destinations (seed 0x5eed) of the same workload: "
-                         f"reference-shaped getKthPaths(src, d, 2) restatement (oracle/), "
-                         f"1 thread, {ct:.2f}s"}
+               "sample": f"{len(sn)} role-stratified destinations (seed 0x5eed) of the same "
+                         f"workload: reference-shaped getKthPaths(src, d, 2) restatement "
+                         f"(oracle/: the source's SPF once, then per destination the k = 1 "
+                         f"trace, the masked runSpf and the k = 2 trace), {threads} threads, "
+                         f"{ct:.2f}s"}
     # compulsory bytes of this rank's KSP2 launch: one neighbour-id + offset
     # scan for the source's SPF and one per 64 masked reruns (they run 64 per
     # multi-source traversal), plus the path-record words actually written
@@ -221,6 +250,15 @@ def main():
     scan = 4 * E + 4 * (V + 1)
     reruns_mine = int(np.count_nonzero(status & N.OSPF_KSP_RERUN))
     comp = (1 + -(-reruns_mine // 64)) * scan + 4 * words
+    traffic = None
+    if os.path.exists(args.pmc_json):
+        try:
+            with open(args.pmc_json) as f:
+                pj = json.load(f)
+            if pj.get("destinations_per_launch") == n:
+                traffic = pj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
     if rank == 0:
         total = V
         bytes_run = 8 * E + 4 * (V + 1) + 4 * V  # SURVEY 8(d) bytes_root, no next-hop rows
@@ -241,7 +279,9 @@ def main():
                        "parallelism": f"destination-sharded x{world}"},
             "isolated_ms": {"ksp2_rank0": round(ksp_ms, 3), "lfa_rank0": round(lfa_ms, 3)},
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "traffic_over_compulsory": round(traffic / comp, 2) if traffic else None,
                          "kernel": "ospf_ksp2_dev (k=1 trace, masked multi-source BFS, k=2 "
                                    "trace)", "compulsory_bytes": int(comp),
                          "avg_launch_ms": round(ksp_ms, 3), "destinations_per_launch": n,

@@ -51,8 +51,11 @@ def test_patched_snapshot_equals_resnapshot(seed):
     for step in range(40):
         a = names[int(rng.integers(len(names)))]
         kind = int(rng.integers(3))
-        if kind == 0 and dbs[a].adjs:  # withdraw
+        if kind == 0 and dbs[a].adjs:  # withdraw (+ metric / overload changes of others)
             dbs[a].adjs.pop(int(rng.integers(len(dbs[a].adjs))))
+            if len(dbs[a].adjs) > 1 and rng.random() < 0.5:
+                dbs[a].adjs[0].overloaded = not dbs[a].adjs[0].overloaded
+                dbs[a].adjs[1].metric = int(rng.integers(1, 30))
             ups = [dbs[a]]
         else:  # add a link (maybe parallel to one that exists)
             b = names[int(rng.integers(len(names)))]
