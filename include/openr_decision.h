@@ -125,6 +125,47 @@ int odl_path_a_in_b(const char* a_nl, uint32_t na, const char* b_nl, uint32_t nb
 char* odl_route_db_text(odl_ls* ls, const char* mes_nl, uint32_t n_mes, const char* prefixes_nl,
                         uint32_t n, int flags);
 
+/* odl_route_db_text's databases as one binary buffer (no text formatting or
+ * parsing on either side; every string stored once). *out is malloc'd (free
+ * with odl_free_buf), *bytes its size. Layout (little-endian, sections 8-B
+ * aligned, offsets from the buffer start; string fields are offsets into the
+ * NUL-terminated string section):
+ *   odl_rdb_header; odl_rdb_node[n_nodes] (one per requested node, in order);
+ *   odl_rdb_route[n_routes] (per node: unicast by prefix, then MPLS by label);
+ *   odl_rdb_nh[n_nhs] (per route, sorted as in the text); int32 labels[];
+ *   strings.
+ * Replaces the text hop of Decision's route publication
+ * (Decision::getDecisionRouteDb -> DecisionRouteDb, SpfSolver.h:80-98). */
+#define ODL_RDB_MAGIC 0x4244524Fu /* "ORDB" */
+typedef struct {
+  uint32_t magic, version;
+  uint64_t bytes;
+  uint32_t n_nodes, n_routes, n_nhs, n_labels;
+  uint64_t off_nodes, off_routes, off_nhs, off_labels, off_strings, str_bytes;
+} odl_rdb_header;
+typedef struct {
+  uint32_t name;    /* string */
+  uint32_t found;   /* 0: unknown node (the reference's nullopt) */
+  uint32_t first_route, n_unicast, n_mpls, pad;
+} odl_rdb_node;
+typedef struct {
+  uint32_t kind;        /* 0 unicast, 1 MPLS */
+  uint32_t key;         /* unicast: prefix string; MPLS: the label */
+  uint32_t igp_cost;    /* unicast */
+  uint32_t has_weight;  /* unicast: ucmp_weight set */
+  int64_t ucmp_weight;
+  uint32_t first_nh, n_nh;
+} odl_rdb_route;
+typedef struct {
+  uint32_t if_name, neighbor; /* strings */
+  int32_t metric, weight;
+  uint32_t op;                /* 0 none, 1 PHP, 2 SWAP, 3 PUSH, 4 POP_AND_LOOKUP */
+  uint32_t first_label, n_labels, pad;
+} odl_rdb_nh;
+int odl_route_db_bin(odl_ls* ls, const char* mes_nl, uint32_t n_mes, const char* prefixes_nl,
+                     uint32_t n, int flags, void** out, uint64_t* bytes);
+void odl_free_buf(void* p);
+
 /* LinkState::resolveUcmpWeights (LinkState.cpp:913-1033) over
  * getSpfResult(root): leaves_nl = n lines "name\tweight"; algo 2 =
  * SP_UCMP_ADJ_WEIGHT_PROPAGATION, 3 = SP_UCMP_PREFIX_WEIGHT_PROPAGATION.

@@ -49,7 +49,7 @@ DECISION_SYMBOLS = [
     "odl_sweep_stats", "odl_destroy", "odl_last_error", "odl_free", "odl_apply", "odl_spf_text",
     "odl_kth_paths_text", "odl_links_text", "odl_link_keys_text", "odl_metric_a_to_b", "odl_is_overloaded",
     "odl_spf_runs", "odl_set_incremental", "odl_incremental_stats", "odl_topology_stats", "odl_num_nodes", "odl_num_links", "odl_spf_digests", "odl_spf_prefetch",
-    "odl_ksp2_text", "odl_route_text", "odl_route_db_text", "odl_path_a_in_b", "odl_ucmp_text", "odl_csr_size", "odl_csr_export", "odl_node_name", "odl_node_id",
+    "odl_ksp2_text", "odl_route_text", "odl_route_db_text", "odl_route_db_bin", "odl_free_buf", "odl_path_a_in_b", "odl_ucmp_text", "odl_csr_size", "odl_csr_export", "odl_node_name", "odl_node_id",
 ]
 
 
@@ -243,6 +243,10 @@ def decision() -> C.CDLL:
         L.odl_ksp2_text.argtypes = [vp, cp, cp, u32]
         L.odl_route_text.argtypes = [vp, cp, cp, u32, i32]
         L.odl_route_db_text.argtypes = [vp, cp, u32, cp, u32, i32]
+        L.odl_route_db_bin.argtypes = [vp, cp, u32, cp, u32, i32, C.POINTER(vp), C.POINTER(u64)]
+        L.odl_route_db_bin.restype = i32
+        L.odl_free_buf.argtypes = [vp]
+        L.odl_free_buf.restype = None
         L.odl_path_a_in_b.argtypes = [cp, u32, cp, u32]
         L.odl_path_a_in_b.restype = i32
         L.odl_ucmp_text.argtypes = [vp, cp, cp, u32, i32, i32]

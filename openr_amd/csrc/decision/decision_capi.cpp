@@ -366,9 +366,10 @@ int odl_path_a_in_b(const char* a_nl, uint32_t na, const char* b_nl, uint32_t nb
   }
 }
 
-char* odl_route_db_text(odl_ls* h, const char* mes_nl, uint32_t n_mes, const char* prefixes_nl,
-                        uint32_t n, int flags) {
-  return guard(h, [&]() -> char* {
+namespace {
+// the prefix lines of odl_route_db_text / _bin -> PrefixRoutes, then the build
+std::vector<std::optional<odl::RouteDb>> buildDbs(odl_ls* h, const std::vector<std::string>& mes,
+                                                  const char* prefixes_nl, uint32_t n, int flags) {
     auto field = [](const std::string& s, size_t& pos, char sep) {
       const size_t e = s.find(sep, pos);
       std::string out = s.substr(pos, e == std::string::npos ? std::string::npos : e - pos);
@@ -412,14 +413,22 @@ char* odl_route_db_text(odl_ls* h, const char* mes_nl, uint32_t n_mes, const cha
     opt.nodeSegmentLabels = flags & 1;
     opt.adjacencyLabels = flags & 2;
     opt.ucmp = flags & 4;
-    const auto mes = splitNl(mes_nl, n_mes);
     odl::SpfSolver solver(h->ls);
     const auto t0 = std::chrono::steady_clock::now();
-    const auto dbs = solver.buildRouteDbs(mes, prefixes, opt);
+    auto dbs = solver.buildRouteDbs(mes, prefixes, opt);
     if (getenv("ODL_SPF_TIMING"))
       fprintf(stderr, "route_timing mes=%zu prefixes=%zu build_route_db_ms=%.3f\n", mes.size(),
               prefixes.size(),
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    return dbs;
+}
+}  // namespace
+
+char* odl_route_db_text(odl_ls* h, const char* mes_nl, uint32_t n_mes, const char* prefixes_nl,
+                        uint32_t n, int flags) {
+  return guard(h, [&]() -> char* {
+    const auto mes = splitNl(mes_nl, n_mes);
+    const auto dbs = buildDbs(h, mes, prefixes_nl, n, flags);
     std::ostringstream os;
     for (size_t i = 0; i < mes.size(); ++i) {
       const auto& me = mes[i];
@@ -455,6 +464,103 @@ char* odl_route_db_text(odl_ls* h, const char* mes_nl, uint32_t n_mes, const cha
     return dup(os.str());
   }, (char*)nullptr);
 }
+
+int odl_route_db_bin(odl_ls* h, const char* mes_nl, uint32_t n_mes, const char* prefixes_nl,
+                     uint32_t n, int flags, void** out, uint64_t* bytes) {
+  return guard(h, [&]() -> int {
+    if (!out) throw std::invalid_argument("null output pointer");
+    *out = nullptr;
+    const auto mes = splitNl(mes_nl, n_mes);
+    const auto dbs = buildDbs(h, mes, prefixes_nl, n, flags);
+    std::vector<odl_rdb_node> nodes(mes.size());
+    std::vector<odl_rdb_route> routes;
+    std::vector<odl_rdb_nh> nhs;
+    std::vector<int32_t> labels;
+    std::string strs;
+    // every string once (names, interfaces, prefixes): offset into strs
+    std::unordered_map<std::string, uint32_t> ids;
+    auto sid = [&](const std::string& x) -> uint32_t {
+      auto it = ids.find(x);
+      if (it != ids.end()) return it->second;
+      const uint32_t o = (uint32_t)strs.size();
+      strs.append(x);
+      strs.push_back('\0');
+      ids.emplace(x, o);
+      return o;
+    };
+    auto put = [&](odl_rdb_route& r, const std::vector<odl::NextHop>& v) {
+      r.first_nh = (uint32_t)nhs.size();
+      r.n_nh = (uint32_t)v.size();
+      for (const auto& x : v) {
+        odl_rdb_nh e{};
+        e.if_name = sid(x.ifName);
+        e.neighbor = sid(x.neighbor);
+        e.metric = x.metric;
+        e.weight = x.weight;
+        e.op = (uint32_t)x.op;
+        e.first_label = (uint32_t)labels.size();
+        e.n_labels = (uint32_t)x.labels.size();
+        labels.insert(labels.end(), x.labels.begin(), x.labels.end());
+        nhs.push_back(e);
+      }
+    };
+    for (size_t i = 0; i < mes.size(); ++i) {
+      odl_rdb_node& nd = nodes[i];
+      nd.name = sid(mes[i]);
+      nd.first_route = (uint32_t)routes.size();
+      if (!dbs[i]) continue;
+      nd.found = 1;
+      nd.n_unicast = (uint32_t)dbs[i]->unicast.size();
+      nd.n_mpls = (uint32_t)dbs[i]->mpls.size();
+      for (const auto& kv : dbs[i]->unicast) {
+        odl_rdb_route r{};
+        r.kind = 0;
+        r.key = sid(kv.first);
+        r.igp_cost = kv.second.igpCost;
+        r.has_weight = kv.second.weight.has_value();
+        r.ucmp_weight = kv.second.weight.value_or(0);
+        put(r, kv.second.nextHops);
+        routes.push_back(r);
+      }
+      for (const auto& kv : dbs[i]->mpls) {
+        odl_rdb_route r{};
+        r.kind = 1;
+        r.key = (uint32_t)kv.first;
+        put(r, kv.second);
+        routes.push_back(r);
+      }
+    }
+    auto al = [](uint64_t x) { return (x + 7) & ~7ull; };
+    odl_rdb_header hd{};
+    hd.magic = ODL_RDB_MAGIC;
+    hd.version = 1;
+    hd.n_nodes = (uint32_t)nodes.size();
+    hd.n_routes = (uint32_t)routes.size();
+    hd.n_nhs = (uint32_t)nhs.size();
+    hd.n_labels = (uint32_t)labels.size();
+    hd.off_nodes = al(sizeof(hd));
+    hd.off_routes = al(hd.off_nodes + nodes.size() * sizeof(odl_rdb_node));
+    hd.off_nhs = al(hd.off_routes + routes.size() * sizeof(odl_rdb_route));
+    hd.off_labels = al(hd.off_nhs + nhs.size() * sizeof(odl_rdb_nh));
+    hd.off_strings = al(hd.off_labels + labels.size() * sizeof(int32_t));
+    hd.str_bytes = strs.size();
+    hd.bytes = al(hd.off_strings + strs.size());
+    char* b = (char*)std::calloc(1, hd.bytes);
+    if (!b) throw std::bad_alloc();
+    std::memcpy(b, &hd, sizeof(hd));
+    auto cp = [&](uint64_t off, const void* src, size_t nb) { if (nb) std::memcpy(b + off, src, nb); };
+    cp(hd.off_nodes, nodes.data(), nodes.size() * sizeof(odl_rdb_node));
+    cp(hd.off_routes, routes.data(), routes.size() * sizeof(odl_rdb_route));
+    cp(hd.off_nhs, nhs.data(), nhs.size() * sizeof(odl_rdb_nh));
+    cp(hd.off_labels, labels.data(), labels.size() * sizeof(int32_t));
+    cp(hd.off_strings, strs.data(), strs.size());
+    *out = b;
+    if (bytes) *bytes = hd.bytes;
+    return 0;
+  }, -1);
+}
+
+void odl_free_buf(void* p) { std::free(p); }
 
 char* odl_ucmp_text(odl_ls* h, const char* root, const char* leaves_nl, uint32_t n, int algo,
                     int use_link_metric) {

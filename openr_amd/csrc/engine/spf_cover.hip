@@ -173,7 +173,7 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t x, int o) {
 // leaf's own bit; LinkState.cpp:885-901) -- and the run's digest (DESIGN.md
 // §4) summed into dg.
 template <int NW>
-__device__ void write_row_nh(const DevGraph& g, const CoverGraph& C, uint32_t* row,
+__device__ __forceinline__ void write_row_nh(const DevGraph& g, const CoverGraph& C, uint32_t* row,
                              uint32_t* nhrow, const uint32_t* s_D, const uint32_t* s_tr,
                              uint32_t r, uint32_t rn, const uint32_t* cm, ospf_digest* dg,
                              unsigned long long* s_acc, uint32_t tid, uint32_t nthreads) {
@@ -262,6 +262,223 @@ __device__ void write_row_nh(const DevGraph& g, const CoverGraph& C, uint32_t* r
   }
   __syncthreads();
   if (tid == 0 && dg) {
+    atomicAdd((unsigned long long*)&dg->reached, s_acc[0]);
+    atomicAdd((unsigned long long*)&dg->sum_dist, s_acc[1]);
+    atomicAdd((unsigned long long*)&dg->hash, s_acc[2]);
+  }
+}
+
+// Seed next hops, during the Dial: the cover nodes this wave scans that
+// settled at t (metrics >= 1: their tight in-edges come from nodes settled
+// before t, whose masks are written) get the OR over their tight in-edges
+// a -> b (a transit or the root, D(a) + w == t) of a's mask, or, for the
+// root's own edge, of its first-hop bits (cfh: the direct link's or the
+// detour leaf's position in the root's distinct neighbours) -- the
+// reference's next hops (LinkState.cpp:885-901: a path's next hop is its
+// first hop). Lane = mask word; up to 8 predecessor masks loaded at once.
+__device__ __forceinline__ void seed_masks(const CoverGraph& C, const uint32_t* s_D,
+                                           const uint32_t* s_tr, uint32_t r, uint32_t t,
+                                           uint32_t* __restrict__ cm, uint32_t NW, uint32_t* s_mw,
+                                           uint32_t wave, uint32_t lane) {
+  const uint32_t nS = C.nS;
+  const bool wl = lane < NW;
+  for (uint32_t x0 = wave * kWave; x0 < nS; x0 += kBlock) {
+    const uint32_t x = x0 + lane;
+    uint64_t ball = __ballot(x < nS && x != r && s_D[x] == t);
+    while (ball) {
+      const uint32_t b = x0 + (uint32_t)__builtin_ctzll(ball);
+      ball &= ball - 1ull;
+      const uint32_t beg = C.crin[b], end = C.crin[b + 1];
+      uint32_t acc = 0u;
+      for (uint32_t e0 = beg; e0 < end; e0 += kWave) {
+        const uint32_t e = e0 + lane;
+        uint32_t src = kInf;
+        bool tight = false;
+        if (e < end) {
+          const uint2 ew = C.cein[e];
+          src = ew.x;
+          const bool ok = src == r || ((s_tr[src >> 5] >> (src & 31u)) & 1u);
+          const uint32_t ds = s_D[src];
+          tight = ok && ds != kInf && ds + ew.y == t;
+        }
+        const uint64_t br = __ballot(tight && src == r);
+        if (br) {  // the root's own C edge to b: its first hops
+          const uint32_t ce = C.ceix[e0 + (uint32_t)__builtin_ctzll(br)];
+          const uint32_t fo = C.cfh_off[ce], fe = C.cfh_off[ce + 1];
+          for (uint32_t k = fo + lane; k < fe; k += kWave) {
+            const uint32_t bit = C.cfh[k];
+            atomicOr(&s_mw[bit >> 5], 1u << (bit & 31u));
+          }
+          __builtin_amdgcn_wave_barrier();
+          acc |= s_mw[lane];
+          __builtin_amdgcn_wave_barrier();
+          s_mw[lane] = 0u;
+          __builtin_amdgcn_wave_barrier();
+        }
+        uint64_t bt = __ballot(tight && src != r);
+        while (bt) {
+          uint32_t m[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            m[u] = 0u;
+            if (bt) {
+              const int j = __builtin_ctzll(bt);
+              bt &= bt - 1ull;
+              const uint32_t a = (uint32_t)__shfl((int)src, j, kWave);
+              if (wl) m[u] = cm[(size_t)a * NW + lane];
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) acc |= m[u];
+        }
+      }
+      if (wl) cm[(size_t)b * NW + lane] = acc;
+    }
+  }
+}
+
+// The seed root's dist row, next-hop row [V][NW] (NW <= 64) and digest:
+// lane = node for the distances and the tight last hops of a leaf (its
+// first two recorded, the root as a last hop by the leaf's bit), then lane
+// = mask word over the 64 nodes, four at a time, their masks loaded before
+// any is used (a cover column's mask as it is; a leaf's the OR over its
+// tight last hops', LinkState.cpp:885-901).
+__device__ __forceinline__ void write_row_nhw(const DevGraph& g, const CoverGraph& C, uint32_t* row,
+                              uint32_t* __restrict__ nhrow, const uint32_t* s_D,
+                              const uint32_t* s_tr, uint32_t r, uint32_t rn,
+                              const uint32_t* __restrict__ cm, uint32_t NW, ospf_digest* dg,
+                              unsigned long long* s_acc, uint32_t wave, uint32_t lane) {
+  const uint32_t nS = C.nS, V = g.V;
+  const uint4* la4 = reinterpret_cast<const uint4*>(C.ladj);
+  const uint32_t* dn = g.dn + g.dn_off[rn];
+  const uint32_t K = g.dn_off[rn + 1] - g.dn_off[rn];
+  const bool wl = lane < NW;
+  auto usable = [&](uint32_t ci) {
+    return ci < nS && (ci == r || ((s_tr[ci >> 5] >> (ci & 31u)) & 1u));
+  };
+  auto fold = [&](uint4 e4, uint32_t out) {
+    const uint32_t es[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const uint32_t ci = es[b] & 0xFFFFu;
+      if (!usable(ci)) continue;
+      const uint32_t d = s_D[ci];
+      if (d != kInf) out = min(out, d + (es[b] >> 16));
+    }
+    return out;
+  };
+  auto rootbit = [&](uint32_t v) {
+    uint32_t lo = 0, hi = K;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (dn[mid] < v) lo = mid + 1;
+      else hi = mid;
+    }
+    return lo;
+  };
+  const uint4 pad = make_uint4(0xFFFFu, 0xFFFFu, 0xFFFFu, 0xFFFFu);
+  uint64_t h = 0, sum = 0;
+  uint32_t reach = 0;
+  for (uint32_t v0 = wave * kWave; v0 < V; v0 += kBlock) {
+    const uint32_t v = v0 + lane;
+    // lane = node: distance, first two tight last hops (cover indices), the
+    // root's bit, and whether more remain (then the word pass rescans)
+    uint32_t out = kInf, t0 = kInf, t1 = kInf, rb = kInf, more = 0u;
+    if (v < V) {
+      const uint32_t cx = C.cix[v];
+      if (!(cx & kLeaf)) {
+        out = s_D[cx];
+        if (cx != r) t0 = cx;
+      } else {
+        const uint32_t q0 = (cx >> 5) & 0x3FFFFFFu, nq = cx & 31u;
+        const uint4 e0 = nq > 0 ? la4[q0] : pad, e1 = nq > 1 ? la4[q0 + 1] : pad;
+        out = fold(e1, fold(e0, kInf));
+        for (uint32_t qq = 2; qq < nq; ++qq) out = fold(la4[q0 + qq], out);
+        if (out != kInf) {
+          bool hit_r = false;
+          auto tight = [&](uint32_t e) {
+            const uint32_t ci = e & 0xFFFFu;
+            if (!usable(ci) || s_D[ci] == kInf || s_D[ci] + (e >> 16) != out) return;
+            if (ci == r) hit_r = true;
+            else if (t0 == kInf) t0 = ci;
+            else if (t1 == kInf) t1 = ci;
+            else more = 1u;
+          };
+          tight(e0.x); tight(e0.y); tight(e0.z); tight(e0.w);
+          tight(e1.x); tight(e1.y); tight(e1.z); tight(e1.w);
+          if (hit_r) rb = rootbit(v);
+          if (nq > 2) more = 1u;
+        }
+      }
+      if (v == rn || out == kInf) t0 = t1 = rb = kInf, more = 0u;
+      __builtin_nontemporal_store(out, row + v);
+      if (out != kInf) {
+        reach += 1u;
+        sum += out;
+        h += g.dkey[2ull * v] * ((uint64_t)out + 1ull);
+      }
+    }
+    // lane = word: the 64 nodes' masks, four nodes per step
+    const uint32_t cnt = min((uint32_t)kWave, V - v0);
+    for (uint32_t j0 = 0; j0 < cnt; j0 += 4u) {
+      uint32_t m[4][2], sv[4][2];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int j = (int)min(j0 + (uint32_t)u, cnt - 1u);
+        sv[u][0] = (uint32_t)__builtin_amdgcn_readlane((int)t0, j);
+        sv[u][1] = (uint32_t)__builtin_amdgcn_readlane((int)t1, j);
+        if (j0 + (uint32_t)u >= cnt) sv[u][0] = sv[u][1] = kInf;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          m[u][p] = (sv[u][p] != kInf && wl) ? cm[(size_t)sv[u][p] * NW + lane] : 0u;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t j = min(j0 + (uint32_t)u, cnt - 1u);
+        if (j0 + (uint32_t)u >= cnt) continue;  // uniform
+        const uint32_t vj = v0 + j;
+        uint32_t acc = m[u][0] | m[u][1];
+        const uint32_t rbj = (uint32_t)__builtin_amdgcn_readlane((int)rb, (int)j);
+        if (rbj != kInf && (rbj >> 5) == lane) acc |= 1u << (rbj & 31u);
+        if (__builtin_amdgcn_readlane((int)more, (int)j)) {  // rare: every last hop again
+          const uint32_t cx = C.cix[vj], q0 = (cx >> 5) & 0x3FFFFFFu, nq = cx & 31u;
+          const uint32_t outj = (uint32_t)__builtin_amdgcn_readlane((int)out, (int)j);
+          bool hit_r = false;
+          auto orm = [&](uint32_t e) {
+            const uint32_t ci = e & 0xFFFFu;
+            if (!usable(ci) || s_D[ci] == kInf || s_D[ci] + (e >> 16) != outj) return;
+            if (ci == r) hit_r = true;
+            else if (wl) acc |= cm[(size_t)ci * NW + lane];
+          };
+          for (uint32_t qq = 0; qq < nq; ++qq) {
+            const uint4 e4 = la4[q0 + qq];
+            orm(e4.x); orm(e4.y); orm(e4.z); orm(e4.w);
+          }
+          if (hit_r) {
+            const uint32_t bit = rootbit(vj);
+            if ((bit >> 5) == lane) acc |= 1u << (bit & 31u);
+          }
+        }
+        if (wl) __builtin_nontemporal_store(acc, nhrow + (size_t)vj * NW + lane);
+        if (acc && wl) h += g.dkey[2ull * vj + 1] * digest_word_key(lane, acc);
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    h += shfl_xor64(h, o);
+    sum += shfl_xor64(sum, o);
+    reach += (uint32_t)__shfl_xor((int)reach, o, kWave);
+  }
+  if (lane == 0) {
+    atomicAdd(&s_acc[0], (unsigned long long)reach);
+    atomicAdd(&s_acc[1], (unsigned long long)sum);
+    atomicAdd(&s_acc[2], (unsigned long long)h);
+  }
+  __syncthreads();
+  if (wave == 0 && lane == 0 && dg) {
     atomicAdd((unsigned long long*)&dg->reached, s_acc[0]);
     atomicAdd((unsigned long long*)&dg->sum_dist, s_acc[1]);
     atomicAdd((unsigned long long*)&dg->hash, s_acc[2]);
@@ -431,11 +648,13 @@ __global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C
   __shared__ uint32_t s_q[kWaves][kQ];
   __shared__ uint32_t s_pre[kWaves][2 * kWave];
   __shared__ uint32_t s_next[2];
-  __shared__ unsigned long long s_acc[3];  // load mode with next hops: digest sums
+  __shared__ unsigned long long s_acc[3];  // rows with next hops: digest sums
+  __shared__ uint32_t s_mw[kWaves][kWave];   // seed masks: the root's first-hop bits
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint32_t nS = C.nS, V = g.V;
   uint32_t* s_tr = s_D + nS;
   for (uint32_t x = tid; x < (nS + 31u) / 32u; x += kBlock) s_tr[x] = C.ctr[x];
+  s_mw[wave][lane] = 0u;
   for (uint32_t i = blockIdx.x; i < a.n; i += gridDim.x) {
     const uint32_t rn = a.roots[i];
     const uint32_t r = rn < V ? C.cix[rn] : kInf;
@@ -465,8 +684,11 @@ __global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C
       __syncthreads();
       continue;
     }
+    const uint32_t np = a.nhpos ? a.nhpos[i] : kInf;
+    uint32_t* cmk = np != kInf ? a.nhm + (size_t)np * nS * a.NW : nullptr;
     for (uint32_t x = tid; x < nS; x += kBlock) s_D[x] = x == r ? 0u : kInf;
     if (tid == 0) s_next[0] = s_next[1] = kInf;
+    if (tid < 3) s_acc[tid] = 0ull;
     __syncthreads();
     uint32_t t = 0, par = 0;
     while (true) {
@@ -489,6 +711,7 @@ __global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C
       }
       __builtin_amdgcn_wave_barrier();
       if (cnt) expand(C, s_D, &s_next[par], q, cnt, s_pre[wave], t, lane);
+      if (cmk) seed_masks(C, s_D, s_tr, r, t, cmk, a.NW, s_mw[wave], wave, lane);
       m2 = wave_min32(m2);
       if (lane == 0 && m2 != kInf) atomicMin(&s_next[par], m2);
       __syncthreads();
@@ -507,7 +730,11 @@ __global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C
       }
     }
     const uint32_t rp = a.rowpos ? a.rowpos[i] : i;
-    if (rp != kInf) write_row(g, C, a.dist + (size_t)rp * V, s_D, s_tr, r, tid, kBlock);
+    if (cmk && rp != kInf)
+      write_row_nhw(g, C, a.dist + (size_t)rp * V, a.nh + (size_t)np * V * a.NW, s_D, s_tr, r, rn,
+                    cmk, a.NW, a.digest ? a.digest + np : nullptr, s_acc, wave, lane);
+    else if (rp != kInf)
+      write_row(g, C, a.dist + (size_t)rp * V, s_D, s_tr, r, tid, kBlock);
     __syncthreads();  // s_D is reused by the next root
   }
 }
@@ -652,6 +879,8 @@ hipError_t launch_cover_spf(const DevGraph& g, const CoverGraph& C, const CoverA
   if (a.n == 0) return hipSuccess;
   if (a.dload && !a.rowpos) return hipErrorInvalidValue;  // load mode writes rows by position
   if (a.nhload && (!a.dload || !a.nh || a.NW == 0 || a.NW > kClMaxNW)) return hipErrorInvalidValue;
+  if (a.nhpos && (a.dload || !a.nhm || !a.nh || a.NW == 0 || a.NW > kSeedMaxNW))
+    return hipErrorInvalidValue;
   const char* e = getenv("OSPF_COVER_DELTA");
   if (e && !a.rowpos && !a.dcomp && !a.dload) {  // delta-stepping (experiment)
     const uint32_t delta = (uint32_t)std::max(1, atoi(e));
@@ -667,7 +896,7 @@ hipError_t launch_cover_spf(const DevGraph& g, const CoverGraph& C, const CoverA
     return hipGetLastError();
   }
   const size_t lds = ((size_t)C.nS + (C.nS + 31u) / 32u) * 4u;
-  const uint32_t per_cu = std::max<uint32_t>(1, (uint32_t)((150u * 1024u) / (lds + 10u * 1024u)));
+  const uint32_t per_cu = std::max<uint32_t>(1, (uint32_t)((150u * 1024u) / (lds + 14u * 1024u)));
   const uint32_t grid = std::min<uint32_t>(a.n, n_cu * std::min<uint32_t>(per_cu, 4u));
   if (lds > 48 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)cover_spf_kernel,

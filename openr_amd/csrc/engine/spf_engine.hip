@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <map>
 #include <unordered_map>
@@ -2025,34 +2026,66 @@ int ospf_cover_prepare(ospf_ctx* c, const uint8_t* leaf) {
     return fail(c, OSPF_E_RANGE, "cover: 1 .. 32768 cover nodes (LDS-resident distances)");
   std::vector<uint32_t> crow(nS + 1, 0), ctr((nS + 31) / 32, 0);
   std::vector<uint2> cedge;
-  std::vector<std::pair<uint32_t, uint32_t>> cand;
+  // per C edge the first hops from its source achieving its weight: the
+  // head's own bit for a direct link, the leaf's for a detour (bit = the
+  // position in the source's distinct neighbours): a seed root's next hops
+  // start there (spf_cover.hip, seed next-hop masks)
+  std::vector<uint32_t> cfh_off(1, 0u), cfh;
+  std::vector<std::array<uint32_t, 3>> cand;  // {head, weight, first-hop bit}
   for (uint32_t i = 0; i < nS; ++i) {
     const uint32_t a = cv[i];
     if (transit(a)) ctr[i >> 5] |= 1u << (i & 31);
     cand.clear();
+    const uint32_t* dn = c->h_dn.data() + c->h_dn_off[a];
+    const uint32_t K = c->h_dn_off[a + 1] - c->h_dn_off[a];
+    auto bit_of = [&](uint32_t y) { return (uint32_t)(std::lower_bound(dn, dn + K, y) - dn); };
     for (uint32_t e = prow[a]; e < prow[a + 1]; ++e) {
       const uint32_t b = pcolx[e];
       if ((b & 0x80000000u) || b == a) continue;  // down / padding / self
       const uint64_t w = c->h_pw[e];
       if (!(cix[b] & 0x80000000u)) {
-        cand.push_back({cix[b], (uint32_t)w});
+        cand.push_back({cix[b], (uint32_t)w, bit_of(b)});
         continue;
       }
       if (!transit(b)) continue;  // an overloaded leaf relays nothing
+      const uint32_t lb = bit_of(b);
       for (uint32_t e2 = prow[b]; e2 < prow[b + 1]; ++e2) {
         const uint32_t x = pcolx[e2];
         if ((x & 0x80000000u) || x == b || x == a) continue;
         if (cix[x] & 0x80000000u) return fail(c, OSPF_E_INVAL, "cover: two adjacent leaves");
         const uint64_t ws = w + c->h_pw[e2];
         if (ws >= 0xFFFFFFFFull) return fail(c, OSPF_E_RANGE, "cover: shortcut weight overflow");
-        cand.push_back({cix[x], (uint32_t)ws});
+        cand.push_back({cix[x], (uint32_t)ws, lb});
       }
     }
     std::sort(cand.begin(), cand.end());
-    for (size_t k = 0; k < cand.size(); ++k)
-      if (k == 0 || cand[k].first != cand[k - 1].first)
-        cedge.push_back(make_uint2(cand[k].first, cand[k].second));
+    for (size_t k = 0; k < cand.size(); ++k) {
+      const bool head = k == 0 || cand[k][0] != cand[k - 1][0];
+      if (head) {
+        cedge.push_back(make_uint2(cand[k][0], cand[k][1]));
+        cfh_off.push_back((uint32_t)cfh.size());
+      }
+      // the minimum-weight entries of a head (sorted: they lead its group)
+      if (cand[k][1] == cedge.back().y && (head || cand[k][2] != cand[k - 1][2]))
+        cfh.push_back(cand[k][2]);
+      cfh_off.back() = (uint32_t)cfh.size();
+    }
     crow[i + 1] = (uint32_t)cedge.size();
+  }
+  // the reverse contracted graph (in-edges per node: source, weight, and the
+  // edge's index for its first hops)
+  std::vector<uint32_t> crin(nS + 1, 0u), ceix(cedge.size());
+  std::vector<uint2> cein(cedge.size());
+  for (const uint2& x : cedge) ++crin[x.x + 1];
+  for (uint32_t i = 0; i < nS; ++i) crin[i + 1] += crin[i];
+  {
+    std::vector<uint32_t> fill(crin.begin(), crin.end() - 1);
+    for (uint32_t i = 0; i < nS; ++i)
+      for (uint32_t e = crow[i]; e < crow[i + 1]; ++e) {
+        const uint32_t q = fill[cedge[e].x]++;
+        cein[q] = make_uint2(i, cedge[e].y);
+        ceix[q] = e;
+      }
   }
   std::vector<uint32_t> lrow(nL + 1, 0), ladj;
   for (uint32_t v = 0, l = 0; v < V; ++v) {
@@ -2083,14 +2116,25 @@ int ospf_cover_prepare(ospf_ctx* c, const uint8_t* leaf) {
   c->h_cedge = cedge;
   cover_closure_split(c);
   if (ladj.empty()) ladj.assign(4, 0xFFFFu);
-  if (cedge.empty()) cedge.push_back(make_uint2(0, 0));
-  // one allocation: cix | crow | ctr | lrow | ladj | cedge (16-B aligned parts)
+  if (cedge.empty()) {
+    cedge.push_back(make_uint2(0, 0));
+    cein.push_back(make_uint2(0, 0));
+    ceix.push_back(0);
+  }
+  if (cfh.empty()) cfh.push_back(0);
+  // one allocation: cix | crow | ctr | lrow | ladj | cedge | cfh_off | cfh |
+  // crin | cein | ceix (16-B aligned parts)
   const size_t o_cix = 0, o_crow = align_up(o_cix + V * 4ull, 16);
   const size_t o_ctr = align_up(o_crow + crow.size() * 4ull, 16);
   const size_t o_lrow = align_up(o_ctr + ctr.size() * 4ull, 16);
   const size_t o_ladj = align_up(o_lrow + lrow.size() * 4ull, 16);
   const size_t o_ced = align_up(o_ladj + ladj.size() * 4ull, 16);
-  const size_t bytes = o_ced + cedge.size() * 8ull;
+  const size_t o_cfo = align_up(o_ced + cedge.size() * 8ull, 16);
+  const size_t o_cfh = align_up(o_cfo + cfh_off.size() * 4ull, 16);
+  const size_t o_crin = align_up(o_cfh + cfh.size() * 4ull, 16);
+  const size_t o_cein = align_up(o_crin + crin.size() * 4ull, 16);
+  const size_t o_ceix = align_up(o_cein + cein.size() * 8ull, 16);
+  const size_t bytes = o_ceix + ceix.size() * 4ull;
   HIPCHK(c, hipSetDevice(c->device));
   if (c->d_cover) HIPCHK(c, hipFree(c->d_cover));
   c->d_cover = nullptr;
@@ -2102,7 +2146,17 @@ int ospf_cover_prepare(ospf_ctx* c, const uint8_t* leaf) {
   HIPCHK(c, hipMemcpy(base + o_lrow, lrow.data(), lrow.size() * 4ull, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(base + o_ladj, ladj.data(), ladj.size() * 4ull, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(base + o_ced, cedge.data(), cedge.size() * 8ull, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(base + o_cfo, cfh_off.data(), cfh_off.size() * 4ull, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(base + o_cfh, cfh.data(), cfh.size() * 4ull, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(base + o_crin, crin.data(), crin.size() * 4ull, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(base + o_cein, cein.data(), cein.size() * 8ull, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(base + o_ceix, ceix.data(), ceix.size() * 4ull, hipMemcpyHostToDevice));
   ospf::CoverGraph& C = c->cover;
+  C.cfh_off = (const uint32_t*)(base + o_cfo);
+  C.cfh = (const uint32_t*)(base + o_cfh);
+  C.crin = (const uint32_t*)(base + o_crin);
+  C.cein = (const uint2*)(base + o_cein);
+  C.ceix = (const uint32_t*)(base + o_ceix);
   C.nS = nS;
   C.nL = nL;
   C.cix = (const uint32_t*)(base + o_cix);

@@ -275,6 +275,15 @@ struct CoverGraph {
   const uint32_t* ctr;   // [(nS + 31) / 32] transit bits
   const uint32_t* lrow;  // [nL + 1] (multiples of 4)
   const uint32_t* ladj;  // [lrow[nL]] cover index | metric (cover -> leaf) << 16; 0xFFFF pads
+  // first hops of each C edge from its source (bits of the source's distinct
+  // neighbours achieving the edge's weight): cfh[cfh_off[e] .. cfh_off[e+1])
+  const uint32_t* cfh_off;  // [crow[nS] + 1]
+  const uint32_t* cfh;
+  // reverse contracted graph: in-edges of cover node i at crin[i] ..
+  // crin[i+1]: {source cover index, weight}, and the edge's index in cedge
+  const uint32_t* crin;     // [nS + 1]
+  const uint2* cein;
+  const uint32_t* ceix;
 };
 struct CoverArgs {
   const uint32_t* roots;  // node ids (cover nodes)
@@ -294,7 +303,16 @@ struct CoverArgs {
   uint32_t* nh = nullptr;
   uint32_t NW = 0;
   ospf_digest* digest = nullptr;
+  // Dial mode with next hops (seed roots, NW <= kSeedMaxNW): for root i with
+  // nhpos[i] != 0xFFFFFFFF the cover nodes' next-hop masks are built during
+  // the Dial (a node settled at t ORs its tight in-edges' masks: the root's
+  // own edges give their first-hop bits, cfh) into nhm + nhpos[i] * nS * NW,
+  // then the next-hop row [V][NW] into nh + nhpos[i] * V * NW and the digest
+  // (zeroed by the caller) into digest + nhpos[i]
+  const uint32_t* nhpos = nullptr;
+  uint32_t* nhm = nullptr;
 };
+constexpr uint32_t kSeedMaxNW = 64;
 hipError_t launch_cover_spf(const DevGraph& g, const CoverGraph& C, const CoverArgs& a,
                             uint32_t n_cu, hipStream_t s);
 

@@ -1395,6 +1395,24 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   std::vector<uint8_t> nh_by_closure(V, 0);
   if (cl_nh)
     for (uint32_t r : clos) nh_by_closure[r] = 1;
+  // the part's seeds (<= 64 next-hop words): next-hop masks during their
+  // Dial, rows + digests after it (cover_spf_kernel seed mode)
+  std::vector<uint32_t> sd_nh;
+  uint32_t NWs = 0;
+  if (closure && !getenv("OSPF_SEED_NONH")) {
+    std::vector<uint8_t> in_d(V, 0);
+    for (uint32_t r : c_der) in_d[r] = 1;
+    for (uint32_t r : seeds)
+      if (in_d[r]) {
+        sd_nh.push_back(r);
+        NWs = std::max(NWs, f.words(r));
+      }
+    if (NWs > ospf::kSeedMaxNW) {
+      sd_nh.clear();
+      NWs = 0;
+    }
+    for (uint32_t r : sd_nh) nh_by_closure[r] = 1;
+  }
   {
     std::vector<uint32_t> keep;
     for (uint32_t r : c_der)
@@ -1408,7 +1426,9 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   std::sort(wset.begin(), wset.end());
   wset.erase(std::unique(wset.begin(), wset.end()), wset.end());
   const uint32_t ncl_dig = cl_nh ? (uint32_t)clos.size() : 0u;
-  const uint32_t ndig = (uint32_t)(c_der.size() + c_wide.size() + nL) + ncl_dig;
+  const uint32_t nsn = (uint32_t)sd_nh.size();
+  const uint32_t ndig = (uint32_t)(c_der.size() + c_wide.size() + nL) + ncl_dig + nsn;
+  const uint32_t cl_dig0 = ndig - nsn - ncl_dig, sn_dig0 = ndig - nsn;
   if ((rc = dalloc(s, &s->dig_all, ndig))) return rc;
   s->n_dig = ndig;
   s->n_rows = nA + nL;
@@ -1506,22 +1526,42 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       cp.fh = d_fh;
       cp.fhloc = d_fhl;
       cp.dcm = dcm;
-      cdg = s->dig_all + (ndig - ncl_dig);
+      cdg = s->dig_all + cl_dig0;
       std::vector<uint8_t> mine_m(V, 0);
       for (uint32_t r : mine) mine_m[r] = 1;
       for (uint32_t j = 0; j < ncl; ++j)
         if (mine_m[clos[j]])
-          own(s, clos[j], ndig - ncl_dig + j, slab + (size_t)clos_rp[j] * V, cnh + (size_t)j * V * NW, NW);
+          own(s, clos[j], cl_dig0 + j, slab + (size_t)clos_rp[j] * V, cnh + (size_t)j * V * NW, NW);
+    }
+    // next hops of the part's seeds out of their Dial
+    uint32_t *d_snp = nullptr, *snm = nullptr, *snh = nullptr;
+    ospf_digest* sdg = nullptr;
+    if (nsn) {
+      std::vector<uint32_t> snp(nsd, kNone), at(V, kNone);
+      for (uint32_t k = 0; k < nsn; ++k) at[sd_nh[k]] = k;
+      for (uint32_t j = 0; j < nsd; ++j) snp[j] = at[seeds[j]];
+      if ((rc = upload(s, &d_snp, snp)) || (rc = dalloc(s, &snm, (size_t)nsn * nS * NWs)) ||
+          (rc = dalloc(s, &snh, (size_t)nsn * V * NWs)))
+        return rc;
+      sdg = s->dig_all + sn_dig0;
+      for (uint32_t k = 0; k < nsn; ++k)
+        own(s, sd_nh[k], sn_dig0 + k, slab + (size_t)pos[sd_nh[k]] * V, snh + (size_t)k * V * NWs, NWs);
     }
     {
       ospf_sweep::Unit u;
       u.name = "cover_seeds";
-      u.kernel = "cover_spf_kernel (contracted-graph Dial of the closure's seeds, LDS-resident "
-                 "distances; their cover columns out)";
+      u.kernel = nsn ? "cover_spf_kernel (seeds' Dial, next-hop masks at settle; cover columns, "
+                       "dist + next-hop rows, digests)"
+                     : "cover_spf_kernel (contracted-graph Dial of the closure's seeds, LDS-resident "
+                       "distances; their cover columns out)";
       u.stream = 0;
       u.n_roots = nsd;
-      u.comp = (uint64_t)nsd * 4ull * V + scan_bytes(c, true);
+      u.W = NWs;
+      u.comp = (uint64_t)nsd * 4ull * V + scan_bytes(c, true) +
+               (uint64_t)nsn * 4ull * NWs * (V + 2ull * nS);
       u.fn = [=](hipStream_t strm) {
+        if (sdg && hipMemsetAsync(sdg, 0, (size_t)nsn * sizeof(ospf_digest), strm) != hipSuccess)
+          return ospf_int::fail(c, OSPF_E_DEVICE, "hipMemsetAsync seed digests");
         ospf::CoverArgs a{};
         a.roots = d_sd;
         a.n = nsd;
@@ -1529,6 +1569,13 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
         a.err = c->d_err;
         a.rowpos = d_srp;
         a.dcomp = seedC;
+        if (nsn) {
+          a.nhpos = d_snp;
+          a.nhm = snm;
+          a.nh = snh;
+          a.NW = NWs;
+          a.digest = sdg;
+        }
         const hipError_t e = ospf::launch_cover_spf(c->g, c->cover, a, (uint32_t)c->n_cu, strm);
         return e == hipSuccess ? OSPF_OK : ospf_int::hip_fail(c, e, "launch_cover_spf");
       };

@@ -36,6 +36,70 @@ def parse_ucmp_text(t: str) -> Dict[str, Tuple[int, Dict[str, Tuple[str, int]]]]
 
 UCMP_ALGOS = {"adj": 2, "prefix": 3}  # SP_UCMP_{ADJ,PREFIX}_WEIGHT_PROPAGATION
 
+# odl_route_db_bin records (include/openr_decision.h)
+RDB_MAGIC = 0x4244524F
+RDB_HEADER = np.dtype([("magic", "<u4"), ("version", "<u4"), ("bytes", "<u8"),
+                       ("n_nodes", "<u4"), ("n_routes", "<u4"), ("n_nhs", "<u4"),
+                       ("n_labels", "<u4"), ("off_nodes", "<u8"), ("off_routes", "<u8"),
+                       ("off_nhs", "<u8"), ("off_labels", "<u8"), ("off_strings", "<u8"),
+                       ("str_bytes", "<u8")])
+RDB_NODE = np.dtype([("name", "<u4"), ("found", "<u4"), ("first_route", "<u4"),
+                     ("n_unicast", "<u4"), ("n_mpls", "<u4"), ("pad", "<u4")])
+RDB_ROUTE = np.dtype([("kind", "<u4"), ("key", "<u4"), ("igp_cost", "<u4"),
+                      ("has_weight", "<u4"), ("ucmp_weight", "<i8"), ("first_nh", "<u4"),
+                      ("n_nh", "<u4")])
+RDB_NH = np.dtype([("if_name", "<u4"), ("neighbor", "<u4"), ("metric", "<i4"),
+                   ("weight", "<i4"), ("op", "<u4"), ("first_label", "<u4"),
+                   ("n_labels", "<u4"), ("pad", "<u4")])
+_OPS = {0: "", 1: "PHP", 2: "SWAP", 3: "PUSH", 4: "POP"}
+
+
+def decode_route_db_bin(buf: bytes):
+    """odl_route_db_bin buffer -> route_dbs' dict (same shape as the text)."""
+    hd = np.frombuffer(buf, RDB_HEADER, 1)[0]
+    if int(hd["magic"]) != RDB_MAGIC or int(hd["version"]) != 1 or int(hd["bytes"]) != len(buf):
+        raise ValueError("not an odl route-db buffer")
+    nodes = np.frombuffer(buf, RDB_NODE, int(hd["n_nodes"]), int(hd["off_nodes"]))
+    routes = np.frombuffer(buf, RDB_ROUTE, int(hd["n_routes"]), int(hd["off_routes"]))
+    nhs = np.frombuffer(buf, RDB_NH, int(hd["n_nhs"]), int(hd["off_nhs"]))
+    labels = np.frombuffer(buf, "<i4", int(hd["n_labels"]), int(hd["off_labels"])).tolist()
+    so = int(hd["off_strings"])
+    strs = buf[so: so + int(hd["str_bytes"])]
+    cache = {}
+
+    def sget(o):
+        o = int(o)
+        v = cache.get(o)
+        if v is None:
+            v = cache[o] = strs[o: strs.index(b"\0", o)].decode()
+        return v
+
+    out = {}
+    for nd in nodes:
+        me = sget(nd["name"])
+        if not nd["found"]:
+            out[me] = None
+            continue
+        db = {"routes": {}}
+        r0 = int(nd["first_route"])
+        for r in routes[r0: r0 + int(nd["n_unicast"]) + int(nd["n_mpls"])]:
+            if r["kind"] == 0:
+                key = sget(r["key"])
+                db["routes"][key] = (int(r["igp_cost"]),
+                                     int(r["ucmp_weight"]) if r["has_weight"] else None)
+                kk = ("U", key)
+            else:
+                kk = ("M", str(int(np.int32(np.uint32(r["key"])))))
+            f0 = int(r["first_nh"])
+            if r["n_nh"]:
+                db[kk] = {(sget(x["if_name"]), sget(x["neighbor"]), int(x["metric"]),
+                           _OPS[int(x["op"])],
+                           tuple(labels[int(x["first_label"]): int(x["first_label"]) + int(x["n_labels"])]),
+                           int(x["weight"]))
+                          for x in nhs[f0: f0 + int(r["n_nh"])]}
+        out[me] = db
+    return out
+
 
 def _parse_spf(t: str) -> Dict[str, Tuple[int, tuple, tuple]]:
     out = {}
@@ -125,7 +189,8 @@ class LinkState:
         return out or None
 
     def route_dbs(self, mes: Sequence[str], prefixes: Dict[str, Sequence],
-                  node_labels: bool = True, adj_labels: bool = True, ucmp: bool = False):
+                  node_labels: bool = True, adj_labels: bool = True, ucmp: bool = False,
+                  binary: bool = True):
         """SpfSolver::buildRouteDb (odl::SpfSolver, C++) for every node in
         `mes`, over SPF results from one batched engine launch.
 
@@ -146,6 +211,18 @@ class LinkState:
                           f"{'' if prepend is None else int(prepend)}")
             lines.append(f"{p}\t{','.join(es)}")
         flags = int(node_labels) | (2 if adj_labels else 0) | (4 if ucmp else 0)
+        if binary:  # odl_route_db_bin: records + a string table, no text
+            buf, nb = C.c_void_p(), C.c_uint64()
+            rc = self._L.odl_route_db_bin(self._h, "\n".join(mes).encode(), len(mes),
+                                          "\n".join(lines).encode(), len(lines), flags,
+                                          C.byref(buf), C.byref(nb))
+            if rc != 0:
+                raise LinkStateError(self._err())
+            try:
+                raw = C.string_at(buf.value, nb.value)
+            finally:
+                self._L.odl_free_buf(buf)
+            return decode_route_db_bin(raw)
         t = self._take(self._L.odl_route_db_text(
             self._h, "\n".join(mes).encode(), len(mes), "\n".join(lines).encode(),
             len(lines), flags))

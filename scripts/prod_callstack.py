@@ -87,7 +87,9 @@ def main():
         prefixes = {f"lo-{n}": [[n, "ip", "ecmp", 0, None]] for n in names}
         _, wall_r, cap_r = timed(lambda: p.route_dbs([me], prefixes))
         rec["route_build_ms"] = sum(cap_r.values("build_route_db_ms"))
-        rec["route_build_wall_ms_incl_text"] = round(wall_r, 3)
+        rec["route_build_wall_ms_incl_binary_abi"] = round(wall_r, 3)
+        _, wall_t, _ = timed(lambda: p.route_dbs([me], prefixes, binary=False))
+        rec["route_build_wall_ms_incl_text_abi"] = round(wall_t, 3)
         rec["total_ms"] = round(rec["getSpfResult_wall_ms"] + rec["route_build_ms"], 3)
         out[label] = rec
         print(f"{label}: {rec}", file=sys.stderr, flush=True)

@@ -67,7 +67,9 @@ def test_route_dbs_match_restatement(seed, ucmp):
     cur = {d.name: dataclasses.asdict(d) for d in dbs}
     rb = RouteBuilder(o, cur, ucmp=ucmp)
     want = {me: rb.build(me, prefixes) for me in names + ["unknown"]}
-    got = p.route_dbs(names + ["unknown"], prefixes, ucmp=ucmp)
+    got = p.route_dbs(names + ["unknown"], prefixes, ucmp=ucmp)  # odl_route_db_bin
+    # the binary records decode to exactly the text ABI's databases
+    assert got == p.route_dbs(names + ["unknown"], prefixes, ucmp=ucmp, binary=False)
     assert got["unknown"] is None
     n_routes = 0
     for me in names:

@@ -146,23 +146,30 @@ def test_sweep_weighted_fabric_closure(drain):
     _, _, eng = engine_for(st)
     try:
         sw = Sweep(eng, mode="wcover")
-        names = [p["name"] for p in sw.profile(1)]
+        prof = sw.profile(1)
         sw.close()
+        names = [p["name"] for p in prof]
         assert "cover_closure" in names and "cover_seeds" in names, names
+        # the seeds' next hops come out of their Dial (masks at settle)
+        seeds_k = [p.get("kernel", "") for p in prof if p["name"] == "cover_seeds"][0]
+        assert "next-hop masks" in seeds_k, seeds_k
         check_sweep_vs_batch(eng, "wcover", rows_for=np.arange(0, eng.V, 7))
     finally:
         eng.close()
 
 
-@pytest.mark.parametrize("opt_in", [False, True])
+@pytest.mark.parametrize("opt_in", ["seed", "derive", "opt_in"])
 @pytest.mark.parametrize("drain", [0.0, 0.05])
 def test_sweep_weighted_wide_cover_roots_runs(drain, opt_in, monkeypatch):
     """Spines with > 128 neighbours (W = 5 next-hop words) on the weighted
     cover path == the batch path bit for bit, with drained switches and down
-    links: by the default kernels, and by the opt-in wnh_runs_kernel (runs of
-    a plane's spines, lane = node, a wave per word) + wnh_hub_kernel (hub rows
-    in LDS per tile) -- OSPF_WNH_RUNS / OSPF_WNH_HUB."""
-    if opt_in:
+    links: next hops by the seeds' Dial (masks at settle, the default), by
+    the neighbour-row derivation (OSPF_SEED_NONH), and by the opt-in
+    wnh_runs_kernel (runs of a plane's spines, lane = node, a wave per word)
+    + wnh_hub_kernel (hub rows in LDS per tile) -- OSPF_WNH_RUNS / OSPF_WNH_HUB."""
+    if opt_in != "seed":
+        monkeypatch.setenv("OSPF_SEED_NONH", "1")
+    if opt_in == "opt_in":
         monkeypatch.setenv("OSPF_WNH_RUNS", "1")
         monkeypatch.setenv("OSPF_WNH_HUB", "1")
     st = drained_fabric(130, 2, seed=9, drain=drain, down=0.02 if drain else 0.0,
@@ -173,8 +180,12 @@ def test_sweep_weighted_wide_cover_roots_runs(drain, opt_in, monkeypatch):
         prof = sw.profile(1)
         sw.close()
         wide = [p for p in prof if p["name"].startswith("wderive_wide_w")]
-        assert any(int(p["name"].rsplit("w", 1)[1]) > 4 for p in wide), [p["name"] for p in prof]
-        if opt_in:
+        if opt_in == "seed":
+            seeds_k = " ".join(p.get("kernel", "") for p in prof if p["name"] == "cover_seeds")
+            assert "next-hop masks" in seeds_k, [p["name"] for p in prof]
+        else:
+            assert any(int(p["name"].rsplit("w", 1)[1]) > 4 for p in wide), [p["name"] for p in prof]
+        if opt_in == "opt_in":
             kern = " ".join(p.get("kernel", "") for p in wide)
             assert "wnh_runs_kernel" in kern and "wnh_hub_kernel" in kern, kern
         check_sweep_vs_batch(eng, "wcover", rows_for=np.arange(0, eng.V, 13))
