@@ -155,6 +155,14 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-nh", action="store_true", help="skip next-hop output (diagnostic)")
     ap.add_argument("--serial-streams", action="store_true", help="one stream for all classes")
+    ap.add_argument("--part-of", type=int, default=-1,
+                    help="sweep one part of the all-sources sweep's root partition into K parts "
+                         "(a contiguous block of the partition's order; the middle part), "
+                         "K x N parts over N ranks; -1: mesh1m 122 (~8.2k roots), else off")
+    ap.add_argument("--root-sample", choices=["random", "block"], default="random",
+                    help="sampled roots (--roots / mesh1m): a random sample, or one block of "
+                         "consecutive node ids (a contiguous slice of the all-sources sweep; "
+                         "mesh ids follow a Hilbert curve)")
     ap.add_argument("--root-order", choices=["auto", "locality", "random"], default="auto",
                     help="sweep order within a width class: grouped by smallest neighbour "
                          "(multi-source batches share frontiers), the random permutation, or "
@@ -166,7 +174,8 @@ def main():
                     help="profiling mode: launch only the class with this neighbour capacity "
                          "(8, 16, or 32 x next-hop words)")
     ap.add_argument("--reps", type=int, default=3, help="launches in --class-only mode")
-    ap.add_argument("--mode", choices=["auto", "derive", "wcover", "wderive", "batch", "lds", "classes"],
+    ap.add_argument("--mode", choices=["auto", "derive", "wcover", "wderive", "wmulti", "batch", "lds",
+                                       "classes"],
                     default="auto",
                     help="all-sources sweep path (ospf_sweep_opts.mode; auto = the engine's "
                          "choice); classes = the per-class batch driver below (no sweep)")
@@ -211,12 +220,19 @@ def main():
     flags = N.OSPF_WANT_DIST | N.OSPF_WANT_DIGEST | (0 if args.no_nh else N.OSPF_WANT_NH)
     perm = np.random.default_rng(SEED).permutation(V).astype(np.uint32)
     n_roots = default_roots if args.roots < 0 else args.roots
+    if args.part_of < 0:
+        args.part_of = 122 if (args.topology == "mesh1m" and args.roots < 0) else 0
+    if args.part_of > 0:
+        n_roots = 0  # the part's roots, through the sweep
     sweep_ok = (n_roots <= 0 and args.roots_per_gpu == 0 and not args.no_nh
                 and not args.class_only and args.mode != "classes")
     if sweep_ok:
         return sweep_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, dev,
                           backend, coll_dev)
     pool = perm if n_roots <= 0 else perm[: min(n_roots, V)]
+    if n_roots > 0 and args.root_sample == "block":  # ids [V/2 - n/2, V/2 + n/2)
+        k = min(n_roots, V)
+        pool = np.arange(V // 2 - k // 2, V // 2 - k // 2 + k, dtype=np.uint32)
     nbrs = shard.distinct_neighbors(csr["row_ptr"], csr["col"])
     key = shard.first_neighbor(csr["row_ptr"], csr["col"]) if args.root_order != "random" \
         else None
@@ -427,8 +443,10 @@ def sweep_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, 
     library's root partition (pod / plane blocks on a fabric); for N > 1 the
     24-B digests are all-gathered over RCCL each step."""
     mode = {"auto": "auto", "derive": "derive", "batch": "batch"}.get(args.mode, args.mode)
+    K = max(1, args.part_of)
+    part, n_parts = (K // 2) * world + rank, world * K  # K = 1: rank of world
     t0 = time.time()
-    sw = eng.sweep(mode=mode, part=rank, n_parts=world, hip_graph=args.graph != "off")
+    sw = eng.sweep(mode=mode, part=part, n_parts=n_parts, hip_graph=args.graph != "off")
     create_s = time.time() - t0
     n = sw.n_roots
     log(f"[rank {rank}] sweep: mode {sw.mode}, {n} roots, {sw.n_rows} rows, {sw.n_launches} "
@@ -534,12 +552,13 @@ def sweep_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, 
                                 "classes, row positions), allocation, one eager run and the HIP "
                                 "graph capture; paid once per graph version, not in `value`"}
     trav = sw.step_traversed_edges
+    sw_roots = sw.roots.copy()
     sw.close()
     # what a production caller pays once per graph version (odl::LinkState:
     # a deferred create -- plan + allocation -- then one eager run)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    sw2 = eng.sweep(mode=mode, part=rank, n_parts=world, defer=True)
+    sw2 = eng.sweep(mode=mode, part=part, n_parts=n_parts, defer=True)
     t2 = time.perf_counter()
     sw2.run(main_s.cuda_stream)
     torch.cuda.synchronize()
@@ -551,9 +570,26 @@ def sweep_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, 
         "total_ms": round((t3 - t1) * 1e3, 1),
         "note": "a new graph version: ospf_sweep_create(OSPF_SWEEP_DEFER) + the first (eager, "
                 "no HIP graph) run, as odl::LinkState::prefetchAllSources pays it"}
-    report(args, stream, names, csr, step_digest, dt, V * args.steps, E, desc, 0, V, world, rank,
-           dist_on, backend, V, cfg, roofline, "strong", "sweep:" + cfg["mode"],
-           trav_edges=trav * args.steps)
+    if K > 1:  # one part per rank of a K x N partition: the parts' roots, not V
+        tot = n
+        if dist_on:
+            t = torch.tensor([n], dtype=torch.int64, device=coll_dev)
+            torch.distributed.all_reduce(t)
+            tot = int(t.item())
+        cfg["part_of"] = {"parts": n_parts, "part_of_rank0": (K // 2) * world,
+                          "roots_all_ranks": tot,
+                          "note": "a contiguous block of the all-sources sweep's root partition "
+                                  "(each width class in largest-neighbour order, cut into "
+                                  "n_parts slices); value = its roots / step time"}
+        report(args, stream, names, csr, step_digest, dt, tot * args.steps, E, desc, tot, V,
+               world, rank, dist_on, backend, tot, cfg, roofline, "strong", "sweep:" + cfg["mode"],
+               pool=np.sort(sw_roots), trav_edges=trav * args.steps,
+               scope=f" part {(K // 2) * world} .. +{world} of {n_parts} of the all-sources sweep "
+                     f"({tot} roots)")
+    else:
+        report(args, stream, names, csr, step_digest, dt, V * args.steps, E, desc, 0, V, world,
+               rank, dist_on, backend, V, cfg, roofline, "strong", "sweep:" + cfg["mode"],
+               trav_edges=trav * args.steps)
     if dist_on:
         torch.distributed.destroy_process_group()
 
@@ -574,7 +610,7 @@ def parity_sample(csr, V: int, k: int = 256):
 
 def report(args, stream, names, csr, step_digest, dt, roots_total, E, desc, n_roots, V, world,
            rank, dist_on, backend, roots_per_step, classes_cfg, roofline, scaling, mode,
-           pool=None, trav_edges=None):
+           pool=None, trav_edges=None, scope=None):
     """CPU baseline + parity of the timed step's digests (rank 0) and the one
     JSON line. gteps = edges the traversal kernels relaxed (trav_edges over
     the timed steps; every root of a per-root / batch path traverses E) / t;
@@ -670,12 +706,14 @@ def report(args, stream, names, csr, step_digest, dt, roots_total, E, desc, n_ro
                           "derived from neighbours' rows relax no edge); gteps_all_pairs_equiv "
                           "= roots x E_dir / t (not work done)",
             "config": {
-                "workload": desc + (" all-sources" if n_roots <= 0 else
+                "workload": desc + (scope if scope else " all-sources" if n_roots <= 0 else
                                     f" {pool.size} sampled roots") +
                 " SPF + ECMP next-hop bitsets (dist + next-hop rows written to HBM, per-root "
                 "digests)",
                 "n_nodes": V, "n_directed_edges": E, "mode": mode,
                 "roots_per_step": roots_per_step,
+                "root_sample": "partition part" if scope else
+                               args.root_sample if n_roots > 0 else "all",
                 "root_classes": classes_cfg,
                 "parallelism": f"root-sharded x{world}" +
                                (f", all_gather of 24-B digests ({'RCCL' if backend == 'nccl' else backend})"

@@ -510,7 +510,12 @@ int ospf_links_unmask(ospf_ctx* ctx);
  *   OSPF_SWEEP_BATCH   per width class batches (ospf_run_batch_dev);
  *   OSPF_SWEEP_LDS     small graphs, unit metric or hop count, <= 4 next-hop
  *                      words: one launch per width class, a wave per root
- *                      with the graph in LDS (ospf_lds_sweep_dev).
+ *                      with the graph in LDS (ospf_lds_sweep_dev);
+ *   OSPF_SWEEP_WMULTI  any metric (or hop count), large graphs without a
+ *                      small cover (meshes): the rows the part needs by a
+ *                      multi-root traversal (groups of 32 roots adjacent in
+ *                      id order, [node][root] distances, Delta-stepping),
+ *                      leaf rows and next hops derived from them.
  * OSPF_SWEEP_AUTO takes LDS when it applies, then the others in the order
  * above. Row layout:
  * dist u32[V] per root; next hops u32[V][W] with W = max(1, ceil(distinct
@@ -527,6 +532,7 @@ int ospf_links_unmask(ospf_ctx* ctx);
 #define OSPF_SWEEP_WDERIVE 3u
 #define OSPF_SWEEP_BATCH 4u
 #define OSPF_SWEEP_LDS 5u
+#define OSPF_SWEEP_WMULTI 6u
 /* opts.flags: create without the eager first run (hip_graph must be 0); the
  * first ospf_sweep_run is then the first run. A caller that runs the sweep
  * once per graph version (odl::LinkState; ospf_msweep_create, which starts

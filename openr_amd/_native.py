@@ -99,7 +99,8 @@ class ospf_plan_info(C.Structure):  # noqa: N801
 
 OSPF_SWEEP_AUTO, OSPF_SWEEP_DERIVE, OSPF_SWEEP_WCOVER, OSPF_SWEEP_WDERIVE, OSPF_SWEEP_BATCH = \
     0, 1, 2, 3, 4
-SWEEP_MODES = {"auto": 0, "derive": 1, "wcover": 2, "wderive": 3, "batch": 4, "lds": 5}
+SWEEP_MODES = {"auto": 0, "derive": 1, "wcover": 2, "wderive": 3, "batch": 4, "lds": 5,
+               "wmulti": 6}
 SWEEP_MODE_NAMES = {v: k for k, v in SWEEP_MODES.items()}
 
 

@@ -22,7 +22,7 @@ OBJ = os.path.join(LIB, "obj")
 ENGINE_SRC = [os.path.join(PKG, "csrc", "engine", f)
               for f in ("spf_kernels.hip", "spf_bfs.hip", "spf_msbfs.hip", "spf_ksp2.hip",
                         "spf_dial.hip", "spf_wdial.hip", "spf_wderive.hip", "spf_levels.hip",
-                        "spf_cover.hip", "spf_update.hip", "spf_leaf.hip", "spf_twin.hip", "spf_small.hip",
+                        "spf_cover.hip", "spf_msdist.hip", "spf_update.hip", "spf_leaf.hip", "spf_twin.hip", "spf_small.hip",
                         "spf_engine.hip",
                         "spf_sweep.hip")]
 DECISION_SRC = [os.path.join(PKG, "csrc", "decision", f)

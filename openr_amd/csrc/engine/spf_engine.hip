@@ -389,8 +389,11 @@ int run_wdial(ospf_ctx* c, const ospf_batch* b, bool hop, hipStream_t s) {
   while (G < 16 && n < (uint64_t)c->n_cu * (16 / G)) G *= 2;
   if (const char* e = getenv("OSPF_WD_GROUP")) G = (uint32_t)std::max(1, std::min(16, atoi(e)));
   while (16 % G) --G;
-  const uint32_t ngroups =
+  uint32_t ngroups =
       std::max<uint32_t>(1, std::min<uint32_t>(n, (uint32_t)c->n_cu * (16 / G)));
+  // knob: fewer roots in flight (their frontiers' state lines stay cached)
+  if (const char* e = getenv("OSPF_WD_NGROUPS"))
+    ngroups = std::max<uint32_t>(1, std::min<uint32_t>(ngroups, (uint32_t)atoi(e)));
   size_t budget = 4096ull << 20;
   if (const char* e = getenv("OSPF_WD_LIST_MB")) budget = (size_t)std::max(1, atoi(e)) << 20;
   const size_t eb = delta > 1 ? 8 : 4;

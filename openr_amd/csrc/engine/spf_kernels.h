@@ -145,6 +145,24 @@ struct WDialArgs {
 };
 hipError_t launch_wdial(const DevGraph& g, const WDialArgs& a, hipStream_t s);
 
+// Multi-root distances (spf_msdist.hip): groups of 32 roots, one workgroup
+// per group, label-correcting Delta-stepping with [node][root] state in the
+// block's scratch (msdist_scratch_bytes per `blocks` concurrent groups).
+struct MsDistArgs {
+  const uint32_t* roots;  // [n] node ids, neighbours adjacent (a group shares its wavefront)
+  uint32_t n;
+  uint32_t ngroups;       // ceil(n / 32)
+  uint32_t blocks;        // concurrent groups (grid)
+  uint32_t delta;         // bucket width (>= 1)
+  uint32_t hop;           // hop-count mode
+  uint32_t* dist;         // rows: dist + rowpos[i] * pitch (or i * pitch)
+  uint64_t pitch;
+  const uint32_t* rowpos;
+  uint32_t* scratch;
+};
+size_t msdist_scratch_bytes(uint32_t V, uint32_t blocks);
+hipError_t launch_msdist(const DevGraph& g, const MsDistArgs& a, hipStream_t s);
+
 // BFS kernel (spf_bfs.hip), unit metric / hop count, LDS bitmaps:
 //   nh_lds = variant 3 (byte next-hops in LDS for roots with <= 8 neighbours),
 //   otherwise variant 4 (next-hops in HBM).

@@ -1790,6 +1790,143 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   return OSPF_OK;
 }
 
+// WMULTI: the distance rows the part needs -- its non-leaf roots and every
+// neighbour of its roots that is not one of its leaves -- from the multi-root
+// traversal (spf_msdist.hip: groups of 32 roots adjacent in id order share a
+// wavefront), then the leaves' rows derived from their neighbours' rows
+// (ospf_wderive_dev), then the non-leaf roots' next hops from their own and
+// their neighbours' rows (ospf_wderive_wide_dev). For large graphs where the
+// cover does not fit the contracted-graph kernel (a mesh).
+int plan_wmulti(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine,
+                const std::vector<uint8_t>& leaf) {
+  ospf_ctx* c = s->c;
+  const uint32_t V = s->V;
+  const uint32_t hop = s->opts.flags & OSPF_HOP_COUNT;
+  std::vector<uint8_t> own_m(V, 0), in_s(V, 0);
+  std::vector<uint32_t> own_l, own_c;
+  for (uint32_t r : mine) own_m[r] = 1;
+  for (uint32_t r : mine) {
+    (leaf[r] ? own_l : own_c).push_back(r);
+    if (f.nbrs(r) > 2048) return fail(c, OSPF_E_RANGE, "wmulti: a root with > 2048 neighbours");
+    if (!leaf[r]) in_s[r] = 1;
+    for (uint32_t k = (*f.dn_off)[r]; k < (*f.dn_off)[r + 1]; ++k) {
+      const uint32_t n = (*f.dn)[k];
+      if (!(leaf[n] && own_m[n])) in_s[n] = 1;
+    }
+  }
+  std::vector<uint32_t> srows;  // ascending ids: neighbours share a group
+  for (uint32_t v = 0; v < V; ++v)
+    if (in_s[v]) srows.push_back(v);
+  const uint32_t nS = (uint32_t)srows.size(), nL = (uint32_t)own_l.size();
+  std::vector<uint32_t> pos(V, kNone);
+  for (uint32_t i = 0; i < nS; ++i) pos[srows[i]] = i;
+  for (uint32_t j = 0; j < nL; ++j) pos[own_l[j]] = nS + j;
+  // concurrent groups: two per CU, within a scratch budget (OSPF_MSD_MB, 32 GB)
+  const uint32_t ngroups = (nS + 31u) / 32u;
+  size_t budget = 32768ull << 20;
+  if (const char* e = getenv("OSPF_MSD_MB")) budget = (size_t)std::max(64, atoi(e)) << 20;
+  const size_t per = ospf::msdist_scratch_bytes(V, 1);
+  uint32_t blocks = std::min<uint32_t>(std::max(1u, ngroups), 2u * (uint32_t)c->n_cu);
+  blocks = std::max<uint32_t>(1, std::min<uint32_t>(blocks, (uint32_t)(budget / per)));
+  if (const char* e = getenv("OSPF_MSD_BLOCKS")) blocks = std::max(1, std::min((int)blocks, atoi(e)));
+  uint32_t delta = hop ? 1u : std::max<uint32_t>(1, c->info.max_metric);
+  if (const char* e = getenv("OSPF_MSD_DELTA")) delta = (uint32_t)std::max(1, atoi(e));
+  uint32_t *slab, *d_pos, *d_s, *d_l, *lnh, *scratch;
+  int rc;
+  if ((rc = dalloc(s, &slab, (size_t)(nS + nL) * V)) || (rc = upload(s, &d_pos, pos)) ||
+      (rc = upload(s, &d_s, srows.empty() ? std::vector<uint32_t>{0u} : srows)) ||
+      (rc = upload(s, &d_l, own_l.empty() ? std::vector<uint32_t>{0u} : own_l)) ||
+      (rc = dalloc(s, &lnh, (size_t)std::max(1u, nL) * V)) ||
+      (rc = dalloc(s, &scratch, per / 4u * blocks)))
+    return rc;
+  std::vector<uint32_t> wset;
+  for (uint32_t r : own_c) wset.push_back(f.words(r));
+  std::sort(wset.begin(), wset.end());
+  wset.erase(std::unique(wset.begin(), wset.end()), wset.end());
+  const uint32_t ndig = (uint32_t)(own_c.size() + nL);
+  if ((rc = dalloc(s, &s->dig_all, std::max(1u, ndig)))) return rc;
+  s->n_dig = ndig;
+  s->n_rows = nS + nL;
+  s->trav_edges = (uint64_t)nS * c->info.n_edges;
+  {
+    ospf_sweep::Unit u;
+    u.name = "msdist";
+    u.kernel = "msdist_kernel (groups of 32 roots, [node][root] distances, label-correcting "
+               "Delta-stepping)";
+    u.stream = 0;
+    u.n_roots = nS;
+    u.comp = (uint64_t)nS * 4ull * V + (uint64_t)ngroups * scan_bytes(c, !hop);
+    u.fn = [=](hipStream_t strm) {
+      ospf::MsDistArgs a{};
+      a.roots = d_s;
+      a.n = nS;
+      a.ngroups = ngroups;
+      a.blocks = std::min(blocks, ngroups);
+      a.delta = delta;
+      a.hop = hop ? 1u : 0u;
+      a.dist = slab;
+      a.pitch = V;
+      a.scratch = scratch;
+      const hipError_t e = ospf::launch_msdist(c->g, a, strm);
+      if (e != hipSuccess) return ospf_int::hip_fail(c, e, "launch_msdist");
+      c->spf_runs += nS;
+      return OSPF_OK;
+    };
+    s->step_comp += u.comp;
+    s->units.push_back(std::move(u));
+  }
+  uint32_t slot = 0;
+  {  // leaves from their neighbours' rows
+    ospf_digest* dg = s->dig_all + slot;
+    for (uint32_t j = 0; j < nL; ++j)
+      own(s, own_l[j], slot + j, slab + (size_t)(nS + j) * V, lnh + (size_t)j * V, 1);
+    slot += nL;
+    uint32_t kmax = 1;
+    for (uint32_t r : own_l) kmax = std::max(kmax, f.nbrs(r));
+    ospf_sweep::Unit u;
+    u.name = "wderive";
+    u.kernel = "ospf_wderive_dev (wderive_kernel: leaf rows from neighbours' dist rows)";
+    u.stream = 0;
+    u.n_roots = nL;
+    u.W = 1;
+    u.comp = (uint64_t)nL * 8ull * V;
+    uint32_t* ldist = slab + (size_t)nS * V;
+    u.fn = [=](hipStream_t strm) {
+      if (!nL) return OSPF_OK;
+      return ospf_wderive_dev(c, d_l, nL, hop, kmax, slab, V, d_pos, ldist, lnh, dg, strm);
+    };
+    s->step_comp += u.comp;
+    s->units.push_back(std::move(u));
+  }
+  for (uint32_t W : wset) {  // next hops of the non-leaf roots
+    std::vector<uint32_t> roots;
+    for (uint32_t r : own_c)
+      if (f.words(r) == W) roots.push_back(r);
+    const uint32_t n = (uint32_t)roots.size();
+    uint32_t *d_roots, *nh;
+    if ((rc = upload(s, &d_roots, roots)) || (rc = dalloc(s, &nh, (size_t)n * V * W))) return rc;
+    ospf_digest* dg = s->dig_all + slot;
+    for (uint32_t j = 0; j < n; ++j)
+      own(s, roots[j], slot + j, slab + (size_t)pos[roots[j]] * V, nh + (size_t)j * V * W, W);
+    slot += n;
+    ospf_sweep::Unit u;
+    u.name = "wderive_wide_w" + std::to_string(W);
+    u.kernel = std::string("ospf_wderive_wide_dev (") +
+               (W <= 4 ? "wderive_wide_kernel<" + std::to_string(W) + ">"
+                       : std::string("wderive_lanes_kernel")) + ")";
+    u.stream = 0;
+    u.n_roots = n;
+    u.W = W;
+    u.comp = (uint64_t)n * 4ull * V * W;
+    u.fn = [=](hipStream_t strm) {
+      return ospf_int::wderive_wide(c, d_roots, n, hop, W, slab, V, d_pos, nh, dg, strm, 0);
+    };
+    s->step_comp += u.comp;
+    s->units.push_back(std::move(u));
+  }
+  return OSPF_OK;
+}
+
 // WDERIVE: cover roots (the part's non-leaves plus every neighbour of its
 // leaves) on the per-root batch path, one launch per class on its own
 // stream; then the leaves derived from those rows.
@@ -1969,7 +2106,7 @@ int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
   if (c->mask.on) return fail(c, OSPF_E_INVAL, "sweep: links are masked (ospf_links_unmask)");
   const uint32_t parts = std::max(1u, o->n_parts);
   if (o->part >= parts) return fail(c, OSPF_E_INVAL, "sweep: part >= n_parts");
-  if (o->mode > OSPF_SWEEP_LDS) return fail(c, OSPF_E_INVAL, "sweep: unknown mode");
+  if (o->mode > OSPF_SWEEP_WMULTI) return fail(c, OSPF_E_INVAL, "sweep: unknown mode");
   if (o->flags & ~(OSPF_HOP_COUNT | OSPF_SWEEP_DEFER))
     return fail(c, OSPF_E_INVAL, "sweep: flags = 0 or OSPF_HOP_COUNT, | OSPF_SWEEP_DEFER");
   const bool defer = (o->flags & OSPF_SWEEP_DEFER) != 0;
@@ -2016,7 +2153,8 @@ int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
   std::vector<uint8_t> leaf;
   bool any_leaf = false;
   uint32_t mode = o->mode;
-  if (mode == OSPF_SWEEP_AUTO || mode == OSPF_SWEEP_WCOVER || mode == OSPF_SWEEP_WDERIVE) {
+  if (mode == OSPF_SWEEP_AUTO || mode == OSPF_SWEEP_WCOVER || mode == OSPF_SWEEP_WDERIVE ||
+      mode == OSPF_SWEEP_WMULTI) {
     if (!(mode == OSPF_SWEEP_AUTO && derive_ok)) {
       leaf = leaf_set(f);
       for (uint8_t x : leaf) any_leaf |= x != 0;
@@ -2051,6 +2189,7 @@ int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
     case OSPF_SWEEP_DERIVE: rc = plan_derive(s, f, mine); break;
     case OSPF_SWEEP_WCOVER: rc = plan_wcover(s, f, mine, leaf); break;
     case OSPF_SWEEP_WDERIVE: rc = plan_wderive(s, f, mine, leaf); break;
+    case OSPF_SWEEP_WMULTI: rc = plan_wmulti(s, f, mine, leaf); break;
     case OSPF_SWEEP_LDS: rc = plan_lds(s, f, mine); break;
     default: rc = plan_batch(s, f, mine, !unit); break;
   }

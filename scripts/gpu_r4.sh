@@ -79,6 +79,22 @@ for st in $STEPS; do
            tail -5 "$OUT/script.out"; tail -5 "$OUT/script.err";;
     derive) timeout -k 10 600 $PYT tests/test_gpu_derive.py tests/test_gpu_wderive.py > "$OUT/derive.log" 2>&1; rc=$?
            tail -3 "$OUT/derive.log";;
+    records)  # all-sources throughput without fabric symmetry (no twins to derive from)
+           rc=0
+           for spec in "grid100:" "grid31:" "fabric100k:OSPF_SWEEP_NOTWIN=1,OSPF_SWEEP_NOTWINLV=1" "fabric100k-w:OSPF_SEED_NONH=1,OSPF_CLOSURE_NONH=1"; do
+             T=${spec%%:*}; E=${spec#*:}; E=${E//,/ }; tag=${T}${E:+_ab}
+             timeout -k 10 420 env $E python bench.py --topology $T --steps 10 --warmup 2 --cpu-sample 8 > "$OUT/rec_$tag.json" 2> "$OUT/rec_$tag.err"; rc=$?
+             echo "record $tag rc=$rc $(head -c 300 "$OUT/rec_$tag.json")"
+             [ $rc -eq 0 ] || break
+           done;;
+    m1m)   # M1M: multi-root sweep part (wmulti) vs the per-root Dial batch (+ in-flight knob)
+           rc=0
+           for spec in "wmulti:--mode wmulti" ${M1M_EXTRA:-}; do
+             tag=${spec%%:*}; A=${spec#*:}; A=${A//,/ }
+             timeout -k 10 500 python bench.py --topology mesh1m --steps ${M1M_STEPS:-3} --warmup 1 --cpu-sample 4 $A > "$OUT/m1m_$tag.json" 2> "$OUT/m1m_$tag.err"; rc=$?
+             echo "m1m $tag rc=$rc $(python -c "import json; d=json.load(open('$OUT/m1m_$tag.json')); print(d['value'], d['ms_per_step'], d['parity_vs_cpu_sample'])" 2>/dev/null)"
+             [ $rc -eq 0 ] || break
+           done;;
     *) echo "unknown step $st"; rc=2;;
   esac
   echo "step $st rc=$rc"

@@ -167,8 +167,9 @@ def test_sweep_weighted_wide_cover_roots_runs(drain, opt_in, monkeypatch):
     the neighbour-row derivation (OSPF_SEED_NONH), and by the opt-in
     wnh_runs_kernel (runs of a plane's spines, lane = node, a wave per word)
     + wnh_hub_kernel (hub rows in LDS per tile) -- OSPF_WNH_RUNS / OSPF_WNH_HUB."""
-    if opt_in != "seed":
+    if opt_in != "seed":  # the neighbour-row kernels (no masks from the Dial / closure)
         monkeypatch.setenv("OSPF_SEED_NONH", "1")
+        monkeypatch.setenv("OSPF_CLOSURE_NONH", "1")
     if opt_in == "opt_in":
         monkeypatch.setenv("OSPF_WNH_RUNS", "1")
         monkeypatch.setenv("OSPF_WNH_HUB", "1")
@@ -189,6 +190,61 @@ def test_sweep_weighted_wide_cover_roots_runs(drain, opt_in, monkeypatch):
             kern = " ".join(p.get("kernel", "") for p in wide)
             assert "wnh_runs_kernel" in kern and "wnh_hub_kernel" in kern, kern
         check_sweep_vs_batch(eng, "wcover", rows_for=np.arange(0, eng.V, 13))
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_sweep_wmulti_random_graphs(seed):
+    """The multi-root traversal (OSPF_SWEEP_WMULTI: groups of 32 roots share a
+    wavefront, [node][root] distances) + derived leaf rows and next hops ==
+    the batch path bit for bit: weighted random graphs with overloaded nodes,
+    hop count, and a drained weighted fabric; parts of a partition too."""
+    stream, _ = random_stream(seed + 40, n=90, unit=False, wmax=30)
+    _, _, eng = engine_for(stream)
+    try:
+        check_sweep_vs_batch(eng, "wmulti", want_mode="wmulti")
+        check_sweep_vs_batch(eng, "wmulti", hop=True, want_mode="wmulti")
+        check_sweep_vs_batch(eng, "wmulti", hip_graph=False, want_mode="wmulti")
+    finally:
+        eng.close()
+
+
+def test_sweep_wmulti_drained_fabric_and_mesh(monkeypatch):
+    st = drained_fabric(12, 4, seed=6, drain=0.05, down=0.03, weighted_seed=5)
+    _, _, eng = engine_for(st)
+    try:
+        check_sweep_vs_batch(eng, "wmulti", rows_for=np.arange(0, eng.V, 5), want_mode="wmulti")
+        monkeypatch.setenv("OSPF_MSD_DELTA", "3")  # narrow buckets: more phases, same rows
+        check_sweep_vs_batch(eng, "wmulti", rows_for=np.arange(0, eng.V, 9), want_mode="wmulti")
+        monkeypatch.delenv("OSPF_MSD_DELTA")
+    finally:
+        eng.close()
+    st = T.mesh(6000, seed=3)
+    ls, csr, eng = engine_for(st)
+    try:
+        V = eng.V
+        full = Sweep(eng, mode="wmulti")
+        full.run()
+        eng.sync()
+        got = sweep_digests(full)
+        full.close()
+        names = ls.node_names()
+        pick = list(range(0, V, 97)) + [V - 1]
+        want = Oracle(st).fast_digests([names[i] for i in pick])
+        for j, r in enumerate(pick):
+            assert np.array_equal(got[r], want[j]), names[r]
+        for n_parts in (3,):  # parts: every root once, same digests
+            seen = {}
+            for p in range(n_parts):
+                sw = Sweep(eng, part=p, n_parts=n_parts, mode="wmulti")
+                sw.run()
+                eng.sync()
+                seen.update(sweep_digests(sw))
+                sw.close()
+            assert sorted(seen) == list(range(V))
+            for r in range(0, V, 13):
+                assert np.array_equal(seen[r], got[r]), r
     finally:
         eng.close()
 
