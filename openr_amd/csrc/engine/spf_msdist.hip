@@ -54,27 +54,28 @@ __device__ __forceinline__ uint32_t ld2(const uint32_t* p) {
 }
 
 struct MsdState {
-  uint32_t* D;      // [V][32]
-  uint32_t* dirty;  // [V]
-  uint32_t* stamp;  // [V]
-  uint32_t* LA;     // [V]
-  uint32_t* LB;     // [V]
+  uint32_t* D;       // [V][32]
+  uint32_t* dirty;   // [V]
+  uint32_t* stampP;  // [V] phase that listed the node for the next phase
+  uint32_t* stampN;  // [V] bucket that listed the node for the next bucket
+  uint32_t* L;       // [3][V]: current, next phase, next bucket (rotating)
 };
 
 __device__ __forceinline__ MsdState state_of(const MsDistArgs& a, uint32_t b, uint32_t V) {
-  const size_t per = (size_t)V * (kR + 4u);
+  const size_t per = (size_t)V * (kR + 6u);
   uint32_t* base = a.scratch + per * b;
   MsdState s;
   s.D = base;
   s.dirty = base + (size_t)V * kR;
-  s.stamp = s.dirty + V;
-  s.LA = s.stamp + V;
-  s.LB = s.LA + V;
+  s.stampP = s.dirty + V;
+  s.stampN = s.stampP + V;
+  s.L = s.stampN + V;
   return s;
 }
 
 __global__ void __launch_bounds__(kBlock) msdist_kernel(DevGraph g, MsDistArgs a) {
-  __shared__ uint32_t s_nA, s_nB, s_minB, s_hi;
+  // list fills (current, next phase, next bucket), their buffers, the bucket
+  __shared__ uint32_t s_nC, s_nP, s_nN, s_minN, s_hi, s_kb, s_ci, s_pi, s_ni;
   __shared__ uint32_t s_t[kTiles][32][33];  // row transpose tiles
   const uint32_t tid = threadIdx.x, lane = tid & 31u, hw = tid >> 5;
   const uint32_t hbase = (tid & 63u) & 32u;  // this half's first lane in the wave
@@ -90,43 +91,50 @@ __global__ void __launch_bounds__(kBlock) msdist_kernel(DevGraph g, MsDistArgs a
       for (size_t x = tid; x < n4; x += kBlock) d4[x] = inf4;
       for (uint32_t x = tid; x < V; x += kBlock) {
         st.dirty[x] = 0u;
-        st.stamp[x] = kInf;
+        st.stampP[x] = kInf;
+        st.stampN[x] = kInf;
       }
     }
     if (tid == 0) {
-      s_nA = 0u;
+      s_nC = s_nP = s_nN = 0u;
+      s_minN = kInf;
       s_hi = a.delta;
+      s_kb = 0u;
+      s_ci = 0u;
+      s_pi = 1u;
+      s_ni = 2u;
     }
     __syncthreads();
-    // my root (lane < nr)
     const uint32_t myroot = lane < nr ? a.roots[r0 + lane] : kInf;
     if (hw == 0 && lane < nr) {
       st.D[(size_t)myroot * kR + lane] = 0u;
       atomicOr(&st.dirty[myroot], 1u << lane);
-      if (atomicExch(&st.stamp[myroot], 0u) != 0u) st.LA[atomicAdd(&s_nA, 1u)] = myroot;
+      if (atomicExch(&st.stampP[myroot], 0u) != 0u) st.L[atomicAdd(&s_nC, 1u)] = myroot;
     }
     __syncthreads();
-    uint32_t* LA = st.LA;
-    uint32_t* LB = st.LB;
     uint32_t phase = 0;
     while (true) {
-      const uint32_t n = s_nA, hi = s_hi;
-      if (n == 0) break;  // block-uniform
-      __syncthreads();    // every thread has read s_nA / s_hi
-      if (tid == 0) {
-        s_nB = 0u;
-        s_minB = kInf;
-      }
+      const uint32_t n = s_nC, hi = s_hi, kb1 = s_kb + 1u;
+      uint32_t* LC = st.L + (size_t)s_ci * V;
+      uint32_t* LP = st.L + (size_t)s_pi * V;
+      uint32_t* LN = st.L + (size_t)s_ni * V;
+      if (n == 0) break;  // block-uniform: no list holds anything
+      __syncthreads();    // every thread has read the shared words
+      if (tid == 0) s_nP = 0u;
       __syncthreads();
       const uint32_t nph = phase + 1u;
-      uint32_t minB = kInf;
-      auto push = [&](uint32_t y) {  // a half-wave's lane 0: list y for the next phase
-        if (atomicExch(&st.stamp[y], nph) != nph) LB[atomicAdd(&s_nB, 1u)] = y;
+      uint32_t minN = kInf;
+      // a half-wave's lane 0: list y for the next phase / the next bucket
+      auto pushP = [&](uint32_t y) {
+        if (atomicExch(&st.stampP[y], nph) != nph) LP[atomicAdd(&s_nP, 1u)] = y;
+      };
+      auto pushN = [&](uint32_t y) {
+        if (atomicExch(&st.stampN[y], kb1) != kb1) LN[atomicAdd(&s_nN, 1u)] = y;
       };
       for (uint32_t i0 = hw * kU; i0 < n; i0 += kHW * kU) {
         uint32_t v[kU], take[kU], beg[kU], deg[kU], d[kU];
 #pragma unroll
-        for (uint32_t u = 0; u < kU; ++u) v[u] = i0 + u < n ? ld2(LA + i0 + u) : kInf;
+        for (uint32_t u = 0; u < kU; ++u) v[u] = i0 + u < n ? ld2(LC + i0 + u) : kInf;
 #pragma unroll
         for (uint32_t u = 0; u < kU; ++u) {
           take[u] = 0u;
@@ -148,12 +156,15 @@ __global__ void __launch_bounds__(kBlock) msdist_kernel(DevGraph g, MsDistArgs a
           const bool relay = v[u] == myroot || !((g.nt_bits[v[u] >> 5] >> (v[u] & 31u)) & 1u);
           const bool act = mine && relay && d[u] < hi;
           const bool later = mine && relay && d[u] >= hi;
+          // roots already past the bucket: their bits back, the node on the
+          // next bucket's list (it is there already when they were lowered
+          // from this bucket: the stamp keeps one entry)
           const uint32_t lm = (uint32_t)(__ballot(later) >> hbase);
           if (lm) {
-            minB = min(minB, later ? d[u] : kInf);
+            minN = min(minN, later ? d[u] : kInf);
             if (lane == 0) {
               atomicOr(&st.dirty[v[u]], lm);
-              push(v[u]);
+              pushN(v[u]);
             }
           }
           if (!(uint32_t)(__ballot(act) >> hbase)) continue;
@@ -184,29 +195,39 @@ __global__ void __launch_bounds__(kBlock) msdist_kernel(DevGraph g, MsDistArgs a
                 imp = nd < atomicMin(&st.D[(size_t)y * kR + lane], nd);
               }
               const uint32_t im = (uint32_t)(__ballot(imp) >> hbase);
-              if (im) {
-                minB = min(minB, imp ? nd : kInf);
-                if (lane == 0) {
-                  atomicOr(&st.dirty[y], im);
-                  push(y);
-                }
+              if (!im) continue;
+              const uint32_t ip = (uint32_t)(__ballot(imp && nd < hi) >> hbase);
+              if (im & ~ip) minN = min(minN, imp && nd >= hi ? nd : kInf);
+              if (lane == 0) {
+                atomicOr(&st.dirty[y], im);
+                if (ip) pushP(y);
+                if (im & ~ip) pushN(y);
               }
             }
           }
         }
       }
-      // the smallest listed distance of the next phase
 #pragma unroll
-      for (int o = 16; o > 0; o >>= 1) minB = min(minB, (uint32_t)__shfl_xor((int)minB, o, 64));
-      if (lane == 0 && minB != kInf) atomicMin(&s_minB, minB);
+      for (int o = 16; o > 0; o >>= 1) minN = min(minN, (uint32_t)__shfl_xor((int)minN, o, 64));
+      if (lane == 0 && minN != kInf) atomicMin(&s_minN, minN);
       __syncthreads();
       if (tid == 0) {
-        s_nA = s_nB;
-        if (s_minB != kInf && s_minB >= s_hi) s_hi = (s_minB / a.delta + 1u) * a.delta;
+        const uint32_t c = s_ci, p = s_pi, nx = s_ni;
+        if (s_nP > 0) {  // more of this bucket
+          s_ci = p;
+          s_pi = c;
+          s_nC = s_nP;
+        } else {         // the bucket is settled: on to the next one
+          s_ci = nx;
+          s_pi = c;
+          s_ni = p;
+          s_nC = s_nN;
+          s_nN = 0u;
+          if (s_minN != kInf) s_hi = max(s_hi + a.delta, (s_minN / a.delta + 1u) * a.delta);
+          s_minN = kInf;
+          s_kb += 1u;
+        }
       }
-      uint32_t* t = LA;
-      LA = LB;
-      LB = t;
       phase = nph;
       __syncthreads();
     }
@@ -237,7 +258,7 @@ __global__ void __launch_bounds__(kBlock) msdist_kernel(DevGraph g, MsDistArgs a
 }  // namespace
 
 size_t msdist_scratch_bytes(uint32_t V, uint32_t blocks) {
-  return (size_t)V * (kR + 4u) * 4u * blocks;
+  return (size_t)V * (kR + 6u) * 4u * blocks;
 }
 
 hipError_t launch_msdist(const DevGraph& g, const MsDistArgs& a, hipStream_t s) {
