@@ -176,7 +176,8 @@ template <int NW>
 __device__ __forceinline__ void write_row_nh(const DevGraph& g, const CoverGraph& C, uint32_t* row,
                              uint32_t* nhrow, const uint32_t* s_D, const uint32_t* s_tr,
                              uint32_t r, uint32_t rn, const uint32_t* cm, ospf_digest* dg,
-                             unsigned long long* s_acc, uint32_t tid, uint32_t nthreads) {
+                             unsigned long long* s_acc, uint32_t* s_st, uint32_t tid,
+                             uint32_t nthreads) {
   const uint32_t nS = C.nS, V = g.V, lane = tid & 63u;
   const uint4* la4 = reinterpret_cast<const uint4*>(C.ladj);
   const uint32_t* dn = g.dn + g.dn_off[rn];
@@ -186,68 +187,81 @@ __device__ __forceinline__ void write_row_nh(const DevGraph& g, const CoverGraph
   };
   uint64_t h = 0, sum = 0;
   uint32_t reach = 0;
-  for (uint32_t v = tid; v < V; v += nthreads) {
-    const uint32_t cx = C.cix[v];
-    uint32_t out, m[NW];
+  // a block step = nthreads consecutive nodes; their next-hop words leave
+  // through LDS as one contiguous run (lane-strided NW-word records would
+  // write partial lines)
+  for (uint32_t v0 = 0; v0 < V; v0 += nthreads) {
+    const uint32_t v = v0 + tid;
+    uint32_t out = kInf, m[NW];
 #pragma unroll
     for (int w = 0; w < NW; ++w) m[w] = 0u;
-    if (!(cx & kLeaf)) {
-      out = s_D[cx];
+    if (v < V) {
+      const uint32_t cx = C.cix[v];
+      if (!(cx & kLeaf)) {
+        out = s_D[cx];
 #pragma unroll
-      for (int w = 0; w < NW; ++w) m[w] = cm[(size_t)cx * NW + w];
-    } else {
-      const uint32_t q0 = (cx >> 5) & 0x3FFFFFFu, nq = cx & 31u;
-      out = kInf;
-      for (uint32_t qq = 0; qq < nq; ++qq) {
-        const uint4 e4 = la4[q0 + qq];
-        const uint32_t es[4] = {e4.x, e4.y, e4.z, e4.w};
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const uint32_t ci = es[b] & 0xFFFFu;
-          if (!usable(ci) || s_D[ci] == kInf) continue;
-          out = min(out, s_D[ci] + (es[b] >> 16));
-        }
-      }
-      if (out != kInf)
+        for (int w = 0; w < NW; ++w) m[w] = cm[(size_t)cx * NW + w];
+      } else {
+        const uint32_t q0 = (cx >> 5) & 0x3FFFFFFu, nq = cx & 31u;
         for (uint32_t qq = 0; qq < nq; ++qq) {
           const uint4 e4 = la4[q0 + qq];
           const uint32_t es[4] = {e4.x, e4.y, e4.z, e4.w};
 #pragma unroll
           for (int b = 0; b < 4; ++b) {
             const uint32_t ci = es[b] & 0xFFFFu;
-            if (!usable(ci) || s_D[ci] == kInf || s_D[ci] + (es[b] >> 16) != out) continue;
-            if (ci == r) {  // a neighbour of the root: its own bit
-              uint32_t lo = 0, hi = K;
-              while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (dn[mid] < v) lo = mid + 1;
-                else hi = mid;
-              }
-              if (lo < 32u * NW) m[lo >> 5] |= 1u << (lo & 31u);
-            } else {
-#pragma unroll
-              for (int w = 0; w < NW; ++w) m[w] |= cm[(size_t)ci * NW + w];
-            }
+            if (!usable(ci) || s_D[ci] == kInf) continue;
+            out = min(out, s_D[ci] + (es[b] >> 16));
           }
         }
-    }
-    if (v == rn || out == kInf) {
+        if (out != kInf)
+          for (uint32_t qq = 0; qq < nq; ++qq) {
+            const uint4 e4 = la4[q0 + qq];
+            const uint32_t es[4] = {e4.x, e4.y, e4.z, e4.w};
 #pragma unroll
-      for (int w = 0; w < NW; ++w) m[w] = 0u;
-    }
-    __builtin_nontemporal_store(out, row + v);
+            for (int b = 0; b < 4; ++b) {
+              const uint32_t ci = es[b] & 0xFFFFu;
+              if (!usable(ci) || s_D[ci] == kInf || s_D[ci] + (es[b] >> 16) != out) continue;
+              if (ci == r) {  // a neighbour of the root: its own bit
+                uint32_t lo = 0, hi = K;
+                while (lo < hi) {
+                  const uint32_t mid = (lo + hi) >> 1;
+                  if (dn[mid] < v) lo = mid + 1;
+                  else hi = mid;
+                }
+                if (lo < 32u * NW) m[lo >> 5] |= 1u << (lo & 31u);
+              } else {
 #pragma unroll
-    for (int w = 0; w < NW; ++w) __builtin_nontemporal_store(m[w], nhrow + (size_t)v * NW + w);
-    if (out != kInf) {
-      reach += 1u;
-      sum += out;
-      h += g.dkey[2ull * v] * ((uint64_t)out + 1ull);
-      uint64_t ws = 0;
+                for (int w = 0; w < NW; ++w) m[w] |= cm[(size_t)ci * NW + w];
+              }
+            }
+          }
+      }
+      if (v == rn || out == kInf) {
 #pragma unroll
-      for (int w = 0; w < NW; ++w)
-        if (m[w]) ws += digest_word_key((uint32_t)w, m[w]);
-      if (ws) h += g.dkey[2ull * v + 1] * ws;
+        for (int w = 0; w < NW; ++w) m[w] = 0u;
+      }
+      __builtin_nontemporal_store(out, row + v);
+      if (out != kInf) {
+        reach += 1u;
+        sum += out;
+        h += g.dkey[2ull * v] * ((uint64_t)out + 1ull);
+        uint64_t ws = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w)
+          if (m[w]) ws += digest_word_key((uint32_t)w, m[w]);
+        if (ws) h += g.dkey[2ull * v + 1] * ws;
+      }
     }
+#pragma unroll
+    for (int w = 0; w < NW; ++w) s_st[tid * NW + w] = m[w];
+    __syncthreads();
+    const size_t base = (size_t)v0 * NW, lim = (size_t)V * NW;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const size_t i = (size_t)w * nthreads + tid;
+      if (base + i < lim) __builtin_nontemporal_store(s_st[i], nhrow + base + i);
+    }
+    __syncthreads();  // s_st is rewritten by the next step
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -672,11 +686,12 @@ __global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C
         const uint32_t* cm = a.nhload + (size_t)i * nS * a.NW;
         uint32_t* nrow = a.nh + (size_t)i * V * a.NW;
         ospf_digest* dg = a.digest ? a.digest + i : nullptr;
+        uint32_t* s_st = &s_q[0][0];  // kWaves * kQ = 2048 words >= kBlock * NW (NW <= 4)
         switch (a.NW) {
-          case 1: write_row_nh<1>(g, C, drow, nrow, s_D, s_tr, r, rn, cm, dg, s_acc, tid, kBlock); break;
-          case 2: write_row_nh<2>(g, C, drow, nrow, s_D, s_tr, r, rn, cm, dg, s_acc, tid, kBlock); break;
-          case 3: write_row_nh<3>(g, C, drow, nrow, s_D, s_tr, r, rn, cm, dg, s_acc, tid, kBlock); break;
-          default: write_row_nh<4>(g, C, drow, nrow, s_D, s_tr, r, rn, cm, dg, s_acc, tid, kBlock); break;
+          case 1: write_row_nh<1>(g, C, drow, nrow, s_D, s_tr, r, rn, cm, dg, s_acc, s_st, tid, kBlock); break;
+          case 2: write_row_nh<2>(g, C, drow, nrow, s_D, s_tr, r, rn, cm, dg, s_acc, s_st, tid, kBlock); break;
+          case 3: write_row_nh<3>(g, C, drow, nrow, s_D, s_tr, r, rn, cm, dg, s_acc, s_st, tid, kBlock); break;
+          default: write_row_nh<4>(g, C, drow, nrow, s_D, s_tr, r, rn, cm, dg, s_acc, s_st, tid, kBlock); break;
         }
       } else {
         write_row(g, C, drow, s_D, s_tr, r, tid, kBlock);

@@ -311,7 +311,7 @@ int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
     a.defer = defer ? 1u : 0u;
     a.merged = merged ? 1u : 0u;
     a.digest = (defer && dig) ? b->d_digest + r0 : nullptr;
-    if (a.digest) HIPCHK(c, hipMemsetAsync(a.digest, 0, (size_t)n * sizeof(ospf_digest), s));
+    if (a.digest) HIPCHK(c, ospf::zero_async(a.digest, (size_t)n * sizeof(ospf_digest), s));
     a.err = c->d_err;
     a.dist = dist_scr ? (uint32_t*)(sp + state_bytes)
                       : ((flags & OSPF_WANT_DIST) ? b->d_dist + (size_t)r0 * V : nullptr);
@@ -330,7 +330,7 @@ int run_msbfs(ospf_ctx* c, const ospf_batch* b, hipStream_t s) {
       a.lev = (uint8_t*)(a.planes + (size_t)a.nb * V * kp);  // 16-B aligned (uint4 access)
       a.found = (uint32_t*)(a.lev + (defer ? (size_t)a.nb * V * 64ull : 0));
       a.mass = a.found + (size_t)a.nb * lmax;
-      HIPCHK(c, hipMemsetAsync(sp, 0, (size_t)a.nb * V * 8ull * (6 + kp) +
+      HIPCHK(c, ospf::zero_async(sp, (size_t)a.nb * V * 8ull * (6 + kp) +
                                           (defer ? (size_t)a.nb * V * 64ull : 0) +
                                           (size_t)a.nb * lmax * 8ull, s));
       hipError_t e = ospf::launch_msbfs_round(kp, c->g, a, c->depth_bound, s);
@@ -544,8 +544,8 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
     tc.ign_out = d_ign + (size_t)c0 * cap;
     tc.cnt_out = d_cnt + c0;
     tc.status = k->status + c0;
-    HIPCHK(c, hipMemsetAsync(d_dead, 0, (size_t)tc.n * dw * 4ull, s));
-    HIPCHK(c, hipMemsetAsync(t.heavy_ctr, 0, 8, s));
+    HIPCHK(c, ospf::zero_async(d_dead, (size_t)tc.n * dw * 4ull, s));
+    HIPCHK(c, ospf::zero_async(t.heavy_ctr, 8, s));
     e = ospf::launch_ksp_trace(false, c->g, tc, s);
     if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_trace k1");
   }
@@ -596,9 +596,9 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
       const size_t zero = (char*)(a.igb + (size_t)a.nb * igw) - st;
       a.igm = (uint64_t*)(st + align_up(zero, 256));
       a.lev = lev;
-      HIPCHK(c, hipMemsetAsync(st, 0, zero, s));
+      HIPCHK(c, ospf::zero_async(st, zero, s));
       if (r >= slots) HIPCHK(c, hipStreamWaitEvent(s, ev_tr[slot], 0));  // slot's trace done
-      HIPCHK(c, hipMemsetAsync(lev, 0, (size_t)a.nb * V * 64ull, s));
+      HIPCHK(c, ospf::zero_async(lev, (size_t)a.nb * V * 64ull, s));
       e = ospf::launch_ksp_masks(c->g, a, d_ign, d_cnt, cap, s);
       if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_masks");
       uint32_t d = std::max<uint32_t>(2, c->depth_bound);
@@ -648,8 +648,8 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
       t2.dead = dead;
       t2.heavy = (uint32_t*)((char*)dead + align_up((size_t)nb_max * 64ull * dw * 4ull, 256));
       t2.heavy_ctr = t2.heavy + nb_max * 64u;
-      HIPCHK(c, hipMemsetAsync(dead, 0, (size_t)t2.n * dw * 4ull, c->aux));
-      HIPCHK(c, hipMemsetAsync(t2.heavy_ctr, 0, 8, c->aux));
+      HIPCHK(c, ospf::zero_async(dead, (size_t)t2.n * dw * 4ull, c->aux));
+      HIPCHK(c, ospf::zero_async(t2.heavy_ctr, 8, c->aux));
       e = ospf::launch_ksp_trace(true, c->g, t2, c->aux);
       if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_trace k2");
       HIPCHK(c, hipEventRecord(ev_tr[slot], c->aux));
@@ -688,8 +688,8 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
       t2.cnt_out = nullptr;
       t2.status = k->status + r0;
       t2.k = 2;
-      HIPCHK(c, hipMemsetAsync(d_dead, 0, (size_t)t2.n * dw * 4ull, s));
-      HIPCHK(c, hipMemsetAsync(t2.heavy_ctr, 0, 8, s));
+      HIPCHK(c, ospf::zero_async(d_dead, (size_t)t2.n * dw * 4ull, s));
+      HIPCHK(c, ospf::zero_async(t2.heavy_ctr, 8, s));
       e = ospf::launch_ksp_trace(false, c->g, t2, s);
       if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_trace k2");
     }
@@ -1453,7 +1453,7 @@ int ospf_run_batch_dev(ospf_ctx* c, const ospf_batch* b, void* stream) {
 
   HIPCHK(c, hipSetDevice(c->device));
   if (a.slices > 1 && (flags & OSPF_WANT_DIGEST))  // slices add into the records
-    HIPCHK(c, hipMemsetAsync(d_digest, 0, n_roots * sizeof(ospf_digest), (hipStream_t)stream));
+    HIPCHK(c, ospf::zero_async(d_digest, n_roots * sizeof(ospf_digest), (hipStream_t)stream));
   hipError_t e = p.variant == 6
       ? ospf::launch_dial(ign, c->g, a, n_roots, p.lds, (hipStream_t)stream)
       : p.variant >= 3
@@ -1562,7 +1562,7 @@ int ospf_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t f
     a.lev_pitch = lev_pitch;
     a.digest = d_lev_digest;
     a.err = c->d_err;
-    if (d_lev_digest) HIPCHK(c, hipMemsetAsync(d_lev_digest, 0, (size_t)n * sizeof(ospf_digest), s));
+    if (d_lev_digest) HIPCHK(c, ospf::zero_async(d_lev_digest, (size_t)n * sizeof(ospf_digest), s));
     uint32_t k = 0;
     for (uint32_t vb0 = 0; vb0 < total; vb0 += nb_max, ++k) {
       const uint32_t buf = overlap ? (k & 1u) : 0u;
@@ -1580,8 +1580,8 @@ int ospf_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t f
       // zero frontier slot 1, seen, accb (contiguous) and found / mass; slot 0
       // is written whole by every level before it is read; records are not
       // cleared (set once per (node, root), read masked by seen)
-      HIPCHK(c, hipMemsetAsync(a.front + (size_t)a.nb * V, 0, (size_t)a.nb * V * 16ull * 3, s));
-      HIPCHK(c, hipMemsetAsync(a.found, 0, (size_t)a.nb * lmax * 8ull, s));
+      HIPCHK(c, ospf::zero_async(a.front + (size_t)a.nb * V, (size_t)a.nb * V * 16ull * 3, s));
+      HIPCHK(c, ospf::zero_async(a.found, (size_t)a.nb * lmax * 8ull, s));
       hipError_t e = ospf::launch_levels128_traverse(c->g, a, s);
       if (e != hipSuccess) return hip_fail(c, e, "launch_levels128_traverse");
       if (overlap) {
@@ -1634,7 +1634,7 @@ int ospf_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t f
   a.levrow = d_lev;
   a.lev_pitch = lev_pitch;
   a.digest = d_lev_digest;
-  if (d_lev_digest) HIPCHK(c, hipMemsetAsync(d_lev_digest, 0, (size_t)n * sizeof(ospf_digest), s));
+  if (d_lev_digest) HIPCHK(c, ospf::zero_async(d_lev_digest, (size_t)n * sizeof(ospf_digest), s));
   for (uint32_t vb0 = 0; vb0 < total_vb; vb0 += nb_max) {
     a.vb0 = vb0;
     a.nb = std::min(nb_max, total_vb - vb0);
@@ -1649,8 +1649,8 @@ int ospf_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t f
     // written whole by every level before it is read), seen, accb, found /
     // mass. The level records are not cleared: their bytes are set once per
     // (node, root) and read masked by seen.
-    HIPCHK(c, hipMemsetAsync(a.front + (size_t)a.nb * V, 0, (size_t)a.nb * V * 8ull * 3, s));
-    HIPCHK(c, hipMemsetAsync(a.found, 0, (size_t)a.nb * lmax * 8ull, s));
+    HIPCHK(c, ospf::zero_async(a.front + (size_t)a.nb * V, (size_t)a.nb * V * 8ull * 3, s));
+    HIPCHK(c, ospf::zero_async(a.found, (size_t)a.nb * lmax * 8ull, s));
     hipError_t e = ospf::launch_msbfs_levels(c->g, a, c->depth_bound, s);
     if (e != hipSuccess) return hip_fail(c, e, "launch_msbfs_levels");
   }
@@ -1675,7 +1675,7 @@ int ospf_nh_derive_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_
                                           : 32u * nh_words;
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(c, hipSetDevice(c->device));
-  if (d_digest) HIPCHK(c, hipMemsetAsync(d_digest, 0, (size_t)n * sizeof(ospf_digest), s));
+  if (d_digest) HIPCHK(c, ospf::zero_async(d_digest, (size_t)n * sizeof(ospf_digest), s));
   ospf::DeriveArgs d{};
   d.roots = d_roots;
   d.n = n;
@@ -1715,7 +1715,7 @@ int ospf_nh_derive_twin_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, ui
   if (nh_words == 0 || nh_words > 4) return fail(c, OSPF_E_RANGE, "twin derive: nh_words 1..4");
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(c, hipSetDevice(c->device));
-  if (d_digest) HIPCHK(c, hipMemsetAsync(d_digest, 0, (size_t)n * sizeof(ospf_digest), s));
+  if (d_digest) HIPCHK(c, ospf::zero_async(d_digest, (size_t)n * sizeof(ospf_digest), s));
   ospf::TwinArgs a{};
   a.roots = d_roots;
   a.n = n;
@@ -1837,7 +1837,7 @@ int ospf_leaf_derive2_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n,
   if (c->depth_bound > 123) return fail(c, OSPF_E_RANGE, "level rows need a depth bound <= 123");
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(c, hipSetDevice(c->device));
-  if (d_digest) HIPCHK(c, hipMemsetAsync(d_digest, 0, (size_t)n * sizeof(ospf_digest), s));
+  if (d_digest) HIPCHK(c, ospf::zero_async(d_digest, (size_t)n * sizeof(ospf_digest), s));
   ospf::LeafArgs a{};
   a.roots = d_roots;
   a.n = n;
@@ -1921,7 +1921,7 @@ int ospf_wderive_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t 
     return fail(c, OSPF_E_RANGE, "distances may reach 2^32 - 1");
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(c, hipSetDevice(c->device));
-  if (d_digest) HIPCHK(c, hipMemsetAsync(d_digest, 0, (size_t)n * sizeof(ospf_digest), s));
+  if (d_digest) HIPCHK(c, ospf::zero_async(d_digest, (size_t)n * sizeof(ospf_digest), s));
   ospf::WDeriveArgs a{};
   a.roots = d_roots;
   a.n = n;
@@ -1978,7 +1978,7 @@ int ospf_int::wderive_wide(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uin
     return fail(c, OSPF_E_RANGE, "distances may reach 2^32 - 1");
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(c, hipSetDevice(c->device));
-  if (d_digest) HIPCHK(c, hipMemsetAsync(d_digest, 0, (size_t)n * sizeof(ospf_digest), s));
+  if (d_digest) HIPCHK(c, ospf::zero_async(d_digest, (size_t)n * sizeof(ospf_digest), s));
   ospf::WDeriveArgs a{};
   a.roots = d_roots;
   a.n = n;

@@ -589,6 +589,16 @@ hipError_t launch_scatter(uint32_t* base, const uint32_t* idx, const uint32_t* v
                           hipStream_t s);
 // structural patches: a[i] += d for i in [from, n) where a[i] >= thresh and
 // a[i] != UINT32_MAX (row offsets / entry positions past a grown row)
+// a[0 .. n) = v (a kernel node, also inside captured graphs)
+hipError_t launch_fill32(uint32_t* a, size_t n, uint32_t v, hipStream_t s);
+// Zero / fill device memory with a kernel instead of hipMemsetAsync: memset
+// nodes of a captured sweep graph replayed right after a caller's memset on
+// the same stream were seen writing pointer-like values into digest slots
+// (ROCm 7.2, gfx950; scripts/debug/replay_parity.py), kernel nodes never.
+inline hipError_t zero_async(void* p, size_t bytes, hipStream_t s) {
+  if (bytes & 3u) return hipMemsetAsync(p, 0, bytes, s);
+  return launch_fill32(static_cast<uint32_t*>(p), bytes / 4u, 0u, s);
+}
 hipError_t launch_shift_add(uint32_t* a, uint32_t n, uint32_t from, uint32_t thresh, uint32_t d,
                             hipStream_t s);
 hipError_t launch_affected(const DevGraph& g, const uint32_t* dist, uint32_t n_roots, bool hop,

@@ -2162,7 +2162,7 @@ hipError_t launch_wide_plan(const DevGraph& g, const WidePlan& p0, hipStream_t s
     if (e != hipSuccess) return e;
   }
   if (p.digest) {
-    const hipError_t e = hipMemsetAsync(p.digest, 0, (size_t)p.n * sizeof(ospf_digest), s);
+    const hipError_t e = ospf::zero_async(p.digest, (size_t)p.n * sizeof(ospf_digest), s);
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(nh_wide_plan_kernel, dim3(p.nruns * p.chunks), dim3(kBlock), lds, s, g, p);
@@ -2171,7 +2171,7 @@ hipError_t launch_wide_plan(const DevGraph& g, const WidePlan& p0, hipStream_t s
 
 hipError_t launch_row_digest(const DevGraph& g, uint32_t n, const uint32_t* dist,
                              const uint32_t* nh, uint32_t W, ospf_digest* out, hipStream_t s) {
-  hipError_t e = hipMemsetAsync(out, 0, (size_t)n * sizeof(ospf_digest), s);
+  hipError_t e = ospf::zero_async(out, (size_t)n * sizeof(ospf_digest), s);
   if (e != hipSuccess) return e;
   // enough workgroups to fill the chip; segment bounds are multiples of 4
   // nodes so the 16-B loads stay aligned

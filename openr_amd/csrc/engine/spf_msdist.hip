@@ -28,7 +28,7 @@
 // (ospf_wderive_dev / ospf_wderive_wide_dev: the first hops of the shortest
 // paths, LinkState.cpp:885-901).
 //
-// Shape: one workgroup (1,024 threads) per group, persistent over groups; a
+// Shape: one workgroup (512 threads) per group, persistent over groups; a
 // half-wave per listed node (lane = root), two nodes per half-wave in flight.
 // The group's state lives in the block's scratch: dist [V][32], dirty bits,
 // stamps and two lists [V]. The dirty bits and distances are updated with
@@ -44,7 +44,7 @@ namespace {
 constexpr uint32_t kInf = 0xFFFFFFFFu;
 constexpr uint32_t kDown = 0x80000000u;
 constexpr uint32_t kR = 32;        // roots per group (a half-wave)
-constexpr uint32_t kBlock = 1024;  // threads per group
+constexpr uint32_t kBlock = 512;   // threads per group
 constexpr uint32_t kHW = kBlock / kR;
 constexpr uint32_t kU = 2;         // nodes per half-wave in flight
 constexpr uint32_t kTiles = 8;     // 32-node tiles per transpose step (33.8 KB of LDS)
@@ -52,6 +52,18 @@ constexpr uint32_t kTiles = 8;     // 32-node tiles per transpose step (33.8 KB 
 __device__ __forceinline__ uint32_t ld2(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// the group's state is touched by its own workgroup only: workgroup-scope
+// atomics (performed in the CU's L2, not at the memory side)
+__device__ __forceinline__ uint32_t wmin(uint32_t* p, uint32_t v) {
+  return __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void wor(uint32_t* p, uint32_t v) {
+  __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t wxchg(uint32_t* p, uint32_t v) {
+  return __hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+constexpr uint32_t kE = 8;  // edges of a node relaxed with their atomics in flight together
 
 struct MsdState {
   uint32_t* D;       // [V][32]
@@ -73,7 +85,7 @@ __device__ __forceinline__ MsdState state_of(const MsDistArgs& a, uint32_t b, ui
   return s;
 }
 
-__global__ void __launch_bounds__(kBlock) msdist_kernel(DevGraph g, MsDistArgs a) {
+__global__ void __launch_bounds__(kBlock, 4) msdist_kernel(DevGraph g, MsDistArgs a) {
   // list fills (current, next phase, next bucket), their buffers, the bucket
   __shared__ uint32_t s_nC, s_nP, s_nN, s_minN, s_hi, s_kb, s_ci, s_pi, s_ni;
   __shared__ uint32_t s_t[kTiles][32][33];  // row transpose tiles
@@ -108,8 +120,8 @@ __global__ void __launch_bounds__(kBlock) msdist_kernel(DevGraph g, MsDistArgs a
     const uint32_t myroot = lane < nr ? a.roots[r0 + lane] : kInf;
     if (hw == 0 && lane < nr) {
       st.D[(size_t)myroot * kR + lane] = 0u;
-      atomicOr(&st.dirty[myroot], 1u << lane);
-      if (atomicExch(&st.stampP[myroot], 0u) != 0u) st.L[atomicAdd(&s_nC, 1u)] = myroot;
+      wor(&st.dirty[myroot], 1u << lane);
+      if (wxchg(&st.stampP[myroot], 0u) != 0u) st.L[atomicAdd(&s_nC, 1u)] = myroot;
     }
     __syncthreads();
     uint32_t phase = 0;
@@ -126,10 +138,10 @@ __global__ void __launch_bounds__(kBlock) msdist_kernel(DevGraph g, MsDistArgs a
       uint32_t minN = kInf;
       // a half-wave's lane 0: list y for the next phase / the next bucket
       auto pushP = [&](uint32_t y) {
-        if (atomicExch(&st.stampP[y], nph) != nph) LP[atomicAdd(&s_nP, 1u)] = y;
+        if (wxchg(&st.stampP[y], nph) != nph) LP[atomicAdd(&s_nP, 1u)] = y;
       };
       auto pushN = [&](uint32_t y) {
-        if (atomicExch(&st.stampN[y], kb1) != kb1) LN[atomicAdd(&s_nN, 1u)] = y;
+        if (wxchg(&st.stampN[y], kb1) != kb1) LN[atomicAdd(&s_nN, 1u)] = y;
       };
       for (uint32_t i0 = hw * kU; i0 < n; i0 += kHW * kU) {
         uint32_t v[kU], take[kU], beg[kU], deg[kU], d[kU];
@@ -140,7 +152,7 @@ __global__ void __launch_bounds__(kBlock) msdist_kernel(DevGraph g, MsDistArgs a
           take[u] = 0u;
           beg[u] = deg[u] = 0u;
           if (v[u] == kInf) continue;
-          if (lane == 0) take[u] = atomicExch(&st.dirty[v[u]], 0u);
+          if (lane == 0) take[u] = wxchg(&st.dirty[v[u]], 0u);
           beg[u] = g.row_ptr[v[u]];
           deg[u] = g.row_ptr[v[u] + 1] - beg[u];
         }
@@ -163,7 +175,7 @@ __global__ void __launch_bounds__(kBlock) msdist_kernel(DevGraph g, MsDistArgs a
           if (lm) {
             minN = min(minN, later ? d[u] : kInf);
             if (lane == 0) {
-              atomicOr(&st.dirty[v[u]], lm);
+              wor(&st.dirty[v[u]], lm);
               pushN(v[u]);
             }
           }
@@ -184,24 +196,43 @@ __global__ void __launch_bounds__(kBlock) msdist_kernel(DevGraph g, MsDistArgs a
               if (a.hop) yw = 1u;
             }
             const uint32_t cnt = min(kR, deg[u] - e0);
-            for (uint32_t j = 0; j < cnt; ++j) {
-              const uint32_t y = (uint32_t)__shfl((int)ycol, (int)(hbase + j), 64);
-              const uint32_t w = (uint32_t)__shfl((int)yw, (int)(hbase + j), 64);
-              if (y & kDown) continue;  // down link / padding (half-uniform)
-              bool imp = false;
-              uint32_t nd = kInf;
-              if (act) {
-                nd = d[u] + w;
-                imp = nd < atomicMin(&st.D[(size_t)y * kR + lane], nd);
+            for (uint32_t j0 = 0; j0 < cnt; j0 += kE) {
+              // kE edges: every atomicMin issued before any result is used
+              uint32_t yy[kE], nd[kE], old[kE];
+#pragma unroll
+              for (uint32_t k = 0; k < kE; ++k) {
+                const uint32_t j = min(j0 + k, cnt - 1u);
+                yy[k] = (uint32_t)__shfl((int)ycol, (int)(hbase + j), 64);
+                const uint32_t w = (uint32_t)__shfl((int)yw, (int)(hbase + j), 64);
+                if (j0 + k >= cnt) yy[k] = kDown;  // past the row (half-uniform)
+                nd[k] = d[u] + w;
+                old[k] = 0u;
+                if (act && !(yy[k] & kDown)) old[k] = wmin(&st.D[(size_t)yy[k] * kR + lane], nd[k]);
               }
-              const uint32_t im = (uint32_t)(__ballot(imp) >> hbase);
-              if (!im) continue;
-              const uint32_t ip = (uint32_t)(__ballot(imp && nd < hi) >> hbase);
-              if (im & ~ip) minN = min(minN, imp && nd >= hi ? nd : kInf);
+              uint32_t im[kE], ip[kE];
+#pragma unroll
+              for (uint32_t k = 0; k < kE; ++k) {
+                const bool imp = act && !(yy[k] & kDown) && nd[k] < old[k];
+                im[k] = (uint32_t)(__ballot(imp) >> hbase);
+                ip[k] = (uint32_t)(__ballot(imp && nd[k] < hi) >> hbase);
+                if (imp && nd[k] >= hi) minN = min(minN, nd[k]);
+              }
               if (lane == 0) {
-                atomicOr(&st.dirty[y], im);
-                if (ip) pushP(y);
-                if (im & ~ip) pushN(y);
+                uint32_t sp[kE], sn[kE];
+#pragma unroll
+                for (uint32_t k = 0; k < kE; ++k) {
+                  sp[k] = sn[k] = 0u;
+                  if (!im[k]) continue;
+                  wor(&st.dirty[yy[k]], im[k]);
+                  if (ip[k]) sp[k] = wxchg(&st.stampP[yy[k]], nph);
+                  if (im[k] & ~ip[k]) sn[k] = wxchg(&st.stampN[yy[k]], kb1);
+                }
+#pragma unroll
+                for (uint32_t k = 0; k < kE; ++k) {
+                  if (!im[k]) continue;
+                  if (ip[k] && sp[k] != nph) LP[atomicAdd(&s_nP, 1u)] = yy[k];
+                  if ((im[k] & ~ip[k]) && sn[k] != kb1) LN[atomicAdd(&s_nN, 1u)] = yy[k];
+                }
               }
             }
           }
@@ -231,22 +262,23 @@ __global__ void __launch_bounds__(kBlock) msdist_kernel(DevGraph g, MsDistArgs a
       phase = nph;
       __syncthreads();
     }
-    // rows: [V][32] -> 32 rows of V through LDS, 16 tiles of 32 nodes per
-    // step: half-wave hw reads node v0 + 32 k + hw (its 32 roots, 128 B),
-    // then writes root hw's 32 nodes of each tile (128 B per store)
+    // rows: [V][32] -> 32 rows of V through LDS, 8 tiles of 32 nodes per
+    // step: half-waves read nodes (their 32 roots, 128 B each), then write
+    // roots' 32 nodes of each tile (128 B per store)
     for (uint32_t v0 = 0; v0 < V; v0 += 32u * kTiles) {
 #pragma unroll
-      for (uint32_t k = 0; k < kTiles; ++k) {
-        const uint32_t v = v0 + 32u * k + hw;
-        s_t[k][hw][lane] = v < V ? ld2(&st.D[(size_t)v * kR + lane]) : kInf;
-      }
+      for (uint32_t k = 0; k < kTiles; ++k)
+        for (uint32_t x = hw; x < 32u; x += kHW) {
+          const uint32_t v = v0 + 32u * k + x;
+          s_t[k][x][lane] = v < V ? ld2(&st.D[(size_t)v * kR + lane]) : kInf;
+        }
       __syncthreads();
-      if (hw < nr) {
-        uint32_t* row = a.dist + (size_t)(a.rowpos ? a.rowpos[r0 + hw] : r0 + hw) * a.pitch;
+      for (uint32_t rr = hw; rr < nr; rr += kHW) {
+        uint32_t* row = a.dist + (size_t)(a.rowpos ? a.rowpos[r0 + rr] : r0 + rr) * a.pitch;
 #pragma unroll
         for (uint32_t k = 0; k < kTiles; ++k) {
           const uint32_t v = v0 + 32u * k + lane;
-          if (v < V) __builtin_nontemporal_store(s_t[k][lane][hw], row + v);
+          if (v < V) __builtin_nontemporal_store(s_t[k][lane][rr], row + v);
         }
       }
       __syncthreads();

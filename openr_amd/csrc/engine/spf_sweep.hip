@@ -1560,8 +1560,8 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       u.comp = (uint64_t)nsd * 4ull * V + scan_bytes(c, true) +
                (uint64_t)nsn * 4ull * NWs * (V + 2ull * nS);
       u.fn = [=](hipStream_t strm) {
-        if (sdg && hipMemsetAsync(sdg, 0, (size_t)nsn * sizeof(ospf_digest), strm) != hipSuccess)
-          return ospf_int::fail(c, OSPF_E_DEVICE, "hipMemsetAsync seed digests");
+        if (sdg && ospf::zero_async(sdg, (size_t)nsn * sizeof(ospf_digest), strm) != hipSuccess)
+          return ospf_int::fail(c, OSPF_E_DEVICE, "zero seed digests");
         ospf::CoverArgs a{};
         a.roots = d_sd;
         a.n = nsd;
@@ -1613,8 +1613,8 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       u.W = NW;
       u.comp = (uint64_t)ncl * 4ull * V * (1 + NW);
       u.fn = [=](hipStream_t strm) {
-        if (cdg && hipMemsetAsync(cdg, 0, (size_t)ncl * sizeof(ospf_digest), strm) != hipSuccess)
-          return ospf_int::fail(c, OSPF_E_DEVICE, "hipMemsetAsync closure digests");
+        if (cdg && ospf::zero_async(cdg, (size_t)ncl * sizeof(ospf_digest), strm) != hipSuccess)
+          return ospf_int::fail(c, OSPF_E_DEVICE, "zero closure digests");
         ospf::CoverArgs a{};
         a.roots = d_cl;
         a.n = ncl;
@@ -2316,11 +2316,12 @@ int ospf_sweep_digests_host(ospf_sweep* s, ospf_digest* out) {
 int ospf_sweep_poison(ospf_sweep* s, void* stream) {
   if (!s) return OSPF_E_INVAL;
   SCHK(s, hipSetDevice(s->c->device));
-  SCHK(s, hipMemsetAsync(s->dig_all, 0xFF, (size_t)std::max(1u, s->n_dig) * sizeof(ospf_digest),
-                         (hipStream_t)stream));
+  // a kernel, not hipMemsetAsync: see ospf::zero_async
+  SCHK(s, ospf::launch_fill32((uint32_t*)s->dig_all, (size_t)std::max(1u, s->n_dig) * 6u,
+                              0xFFFFFFFFu, (hipStream_t)stream));
   for (auto& a : s->dig_aux)
-    SCHK(s, hipMemsetAsync(a.first, 0xFF, std::max<size_t>(1, a.second) * sizeof(ospf_digest),
-                           (hipStream_t)stream));
+    SCHK(s, ospf::launch_fill32((uint32_t*)a.first, std::max<size_t>(1, a.second) * 6u, 0xFFFFFFFFu,
+                                (hipStream_t)stream));
   return OSPF_OK;
 }
 

@@ -11,6 +11,7 @@
 // nextHops, pathLinks, LinkState.cpp:836-911) is then bit-identical, so only
 // the flagged runs need to be re-run.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <stdint.h>
 
 #include "spf_kernels.h"
@@ -298,6 +299,19 @@ hipError_t launch_repair(const DevGraph& g, const RepairArgs& a, hipStream_t s) 
 hipError_t launch_scatter(uint32_t* base, const uint32_t* idx, const uint32_t* val, uint32_t n,
                           hipStream_t s) {
   if (n) hipLaunchKernelGGL(scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, s, base, idx, val, n);
+  return hipGetLastError();
+}
+
+__global__ void fill32_kernel(uint32_t* a, size_t n, uint32_t v) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    a[i] = v;
+}
+
+hipError_t launch_fill32(uint32_t* a, size_t n, uint32_t v, hipStream_t s) {
+  if (n) {
+    const size_t blocks = std::min<size_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(fill32_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, a, n, v);
+  }
   return hipGetLastError();
 }
 

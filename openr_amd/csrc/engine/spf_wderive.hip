@@ -878,7 +878,7 @@ hipError_t launch_wnh_hub(const DevGraph& g, const HubPlan& p, hipStream_t s) {
   if (p.ngroups == 0) return hipSuccess;
   if (p.nhub > kHubMax || p.W == 0 || p.W > 4) return hipErrorInvalidValue;
   if (p.digest) {
-    const hipError_t e = hipMemsetAsync(p.digest, 0, (size_t)p.nroots * sizeof(ospf_digest), s);
+    const hipError_t e = ospf::zero_async(p.digest, (size_t)p.nroots * sizeof(ospf_digest), s);
     if (e != hipSuccess) return e;
   }
   const size_t lds = (size_t)(p.nhub + kHubLoc + 1u) * kHubTile * 4u;
@@ -904,7 +904,7 @@ hipError_t launch_wnh_hub(const DevGraph& g, const HubPlan& p, hipStream_t s) {
 hipError_t launch_wnh_runs(const DevGraph& g, const WRunsPlan& p, hipStream_t s) {
   if (p.nruns == 0) return hipSuccess;
   if (p.digest) {
-    const hipError_t e = hipMemsetAsync(p.digest, 0, (size_t)p.nroots * sizeof(ospf_digest), s);
+    const hipError_t e = ospf::zero_async(p.digest, (size_t)p.nroots * sizeof(ospf_digest), s);
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(wnh_runs_kernel, dim3(p.nruns * p.tiles), dim3(256), 0, s, g, p);

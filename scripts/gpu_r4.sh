@@ -95,6 +95,21 @@ for st in $STEPS; do
              echo "m1m $tag rc=$rc $(python -c "import json; d=json.load(open('$OUT/m1m_$tag.json')); print(d['value'], d['ms_per_step'], d['parity_vs_cpu_sample'])" 2>/dev/null)"
              [ $rc -eq 0 ] || break
            done;;
+    ksp2)  # KSP2 side bench: two PMC passes (3 KSP2 launches each), their sum, then the bench
+           rc=0; i=0
+           for P in FETCH_SIZE WRITE_SIZE; do
+             i=$((i+1))
+             timeout -s KILL 240 rocprofv3 --pmc $P -d "$OUT/kpmc$i" -o run --output-format csv -- \
+               python scripts/bench_ksp2.py --steps 1 --warmup 0 --iso-reps 1 --no-cpu --no-lfa > "$OUT/kpmc$i.json" 2> "$OUT/kpmc$i.err"; rc=$?
+             echo "ksp2 pmc $P rc=$rc"; [ $rc -eq 0 ] || break
+           done
+           if [ $rc -eq 0 ]; then
+             ND=$(python -c "import json; print(json.load(open('$OUT/kpmc1.json'))['roofline']['destinations_per_launch'])")
+             python scripts/pmc_sum.py "$OUT/kpmc1" "$OUT/kpmc2" --launches 3 --match "ospf::" --extra destinations_per_launch=$ND > "$OUT/ksp2_pmc.json" &&
+             mkdir -p profiles/r04 && cp "$OUT/ksp2_pmc.json" profiles/r04/ksp2_pmc.json &&
+             timeout -k 10 600 python scripts/bench_ksp2.py > "$OUT/ksp2.json" 2> "$OUT/ksp2.err"; rc=$?
+             head -c 600 "$OUT/ksp2.json"; tail -3 "$OUT/ksp2.err"
+           fi;;
     *) echo "unknown step $st"; rc=2;;
   esac
   echo "step $st rc=$rc"
