@@ -146,8 +146,8 @@ struct WDialArgs {
 hipError_t launch_wdial(const DevGraph& g, const WDialArgs& a, hipStream_t s);
 
 // Multi-root distances (spf_msdist.hip): groups of 32 roots, one workgroup
-// per group, label-correcting Delta-stepping with [node][root] state in the
-// block's scratch (msdist_scratch_bytes per `blocks` concurrent groups).
+// per group, Bellman-Ford by pulls in Delta buckets with [node][root] state in
+// the block's scratch (msdist_scratch_bytes per `blocks` concurrent groups).
 struct MsDistArgs {
   const uint32_t* roots;  // [n] node ids, neighbours adjacent (a group shares its wavefront)
   uint32_t n;
@@ -159,6 +159,7 @@ struct MsDistArgs {
   uint64_t pitch;
   const uint32_t* rowpos;
   uint32_t* scratch;
+  unsigned long long* stats = nullptr;  // debug: {phases, frontier nodes, candidates, -}
 };
 size_t msdist_scratch_bytes(uint32_t V, uint32_t blocks);
 hipError_t launch_msdist(const DevGraph& g, const MsDistArgs& a, hipStream_t s);

@@ -8,31 +8,30 @@
 // rows). Roots that are neighbours in the graph (consecutive ids of a
 // Hilbert-ordered mesh, one part of an all-sources sweep) have nearly the same
 // wavefront: with the 32 roots' distances of a node in one 128-B line, one
-// visit of the node reads its CSR row once and relaxes its out-edges for all
-// of its active roots with one coalesced 128-B atomic per edge.
+// visit of a node serves all 32 roots.
 //
-// Algorithm: label-correcting Delta-stepping over the group. A node is on the
-// phase's list when some root of the group has a tentative distance at it
-// that was lowered since the node last relaxed for that root (its "dirty"
-// bit). A phase takes every listed node, claims its dirty bits, and relaxes
-// its out-edges for the claimed roots whose distance lies below the current
-// bucket end `hi` (and whose root may transit the node: an overloaded node
-// relays only its own root's paths, LinkState.cpp:859-866); claimed roots at
-// or past `hi` give their bits back and the node stays listed. Every lowered
-// distance sets the head's dirty bit and lists the head for the next phase
-// (once per phase: a stamp per node). When nothing left on the next list lies
-// below `hi`, the bucket advances past the smallest listed distance. The
-// fixed point is the shortest-distance table whatever the order (metrics >=
-// 1); the buckets only keep the work near the wavefront. Next hops and
-// digests are not computed here: the sweep derives them from these rows
-// (ospf_wderive_dev / ospf_wderive_wide_dev: the first hops of the shortest
-// paths, LinkState.cpp:885-901).
+// Algorithm: Bellman-Ford by pulls in Delta buckets, no per-root atomics. A
+// phase has a frontier F: nodes whose distance for some root was lowered in
+// the previous phase to a value below the bucket end `hi`. (1) Expand: every
+// neighbour of F becomes a candidate (once per phase: a stamp). (2) Pull:
+// each candidate y, owned by one half-wave (lane = root), takes
+// min(D[y], D[u] + w(u -> y)) over its up in-links from nodes u that relay for
+// that root (transit, or the root itself: LinkState.cpp:859-866) and whose
+// value lies below `hi`; lowered roots put y on the next frontier (below `hi`)
+// or on the deferred list (at or past `hi`, with its smallest such value).
+// When a phase leaves no frontier, the bucket advances past the smallest
+// deferred value and the deferred nodes below the new end form the frontier.
+// At the end every value has been pulled by every neighbour after its last
+// change: the shortest distances (metrics >= 1, any order). Writes are
+// owner-only (a candidate once per phase), so the state needs no per-root
+// atomics; readers see old or new values, both upper bounds, and a lowered
+// value is always followed by its node's expansion. Next hops and digests
+// come from the rows afterwards (ospf_wderive_dev / ospf_wderive_wide_dev:
+// the first hops of the shortest paths, LinkState.cpp:885-901).
 //
-// Shape: one workgroup (512 threads) per group, persistent over groups; a
-// half-wave per listed node (lane = root), two nodes per half-wave in flight.
-// The group's state lives in the block's scratch: dist [V][32], dirty bits,
-// stamps and two lists [V]. The dirty bits and distances are updated with
-// L2 atomics by the block's own threads only (one CU, one L2): coherent.
+// Shape: one workgroup (512 threads, 16 half-waves) per group, persistent over
+// groups; group state in the block's scratch: dist [V][32], two stamps, the
+// pending value per node and five lists [V].
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -46,48 +45,45 @@ constexpr uint32_t kDown = 0x80000000u;
 constexpr uint32_t kR = 32;        // roots per group (a half-wave)
 constexpr uint32_t kBlock = 512;   // threads per group
 constexpr uint32_t kHW = kBlock / kR;
-constexpr uint32_t kU = 2;         // nodes per half-wave in flight
+constexpr uint32_t kU = 4;         // candidates per half-wave pulled at once
+constexpr uint32_t kE = 4;         // in-links per candidate per step, loads in flight together
 constexpr uint32_t kTiles = 8;     // 32-node tiles per transpose step (33.8 KB of LDS)
+constexpr uint32_t kWords = kR + 8u;  // scratch words per node
 
 __device__ __forceinline__ uint32_t ld2(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// the group's state is touched by its own workgroup only: workgroup-scope
-// atomics (performed in the CU's L2, not at the memory side)
-__device__ __forceinline__ uint32_t wmin(uint32_t* p, uint32_t v) {
-  return __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void wor(uint32_t* p, uint32_t v) {
-  __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 __device__ __forceinline__ uint32_t wxchg(uint32_t* p, uint32_t v) {
   return __hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-constexpr uint32_t kE = 8;  // edges of a node relaxed with their atomics in flight together
+__device__ __forceinline__ uint32_t wamin(uint32_t* p, uint32_t v) {
+  return __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 struct MsdState {
-  uint32_t* D;       // [V][32]
-  uint32_t* dirty;   // [V]
-  uint32_t* stampP;  // [V] phase that listed the node for the next phase
-  uint32_t* stampN;  // [V] bucket that listed the node for the next bucket
-  uint32_t* L;       // [3][V]: current, next phase, next bucket (rotating)
+  uint32_t* D;     // [V][32]
+  uint32_t* stC;   // [V] phase that made the node a candidate
+  uint32_t* stF;   // [V] phase that put the node on a frontier
+  uint32_t* pend;  // [V] smallest deferred value (kInf: not on the deferred list)
+  uint32_t* L;     // [5][V]: lists, roles rotating (s_buf)
 };
 
 __device__ __forceinline__ MsdState state_of(const MsDistArgs& a, uint32_t b, uint32_t V) {
-  const size_t per = (size_t)V * (kR + 6u);
-  uint32_t* base = a.scratch + per * b;
+  uint32_t* base = a.scratch + (size_t)V * kWords * b;
   MsdState s;
   s.D = base;
-  s.dirty = base + (size_t)V * kR;
-  s.stampP = s.dirty + V;
-  s.stampN = s.stampP + V;
-  s.L = s.stampN + V;
+  s.stC = base + (size_t)V * kR;
+  s.stF = s.stC + V;
+  s.pend = s.stF + V;
+  s.L = s.pend + V;
   return s;
 }
 
 __global__ void __launch_bounds__(kBlock, 4) msdist_kernel(DevGraph g, MsDistArgs a) {
-  // list fills (current, next phase, next bucket), their buffers, the bucket
-  __shared__ uint32_t s_nC, s_nP, s_nN, s_minN, s_hi, s_kb, s_ci, s_pi, s_ni;
+  // list roles: 0 frontier, 1 next frontier, 2 candidates, 3 deferred,
+  // 4 deferred being rebuilt; s_buf[role] = its buffer, s_n[role] = its fill
+  __shared__ uint32_t s_n[5], s_buf[5];
+  __shared__ uint32_t s_hi, s_minD, s_minD2;
   __shared__ uint32_t s_t[kTiles][32][33];  // row transpose tiles
   const uint32_t tid = threadIdx.x, lane = tid & 31u, hw = tid >> 5;
   const uint32_t hbase = (tid & 63u) & 32u;  // this half's first lane in the wave
@@ -95,171 +91,210 @@ __global__ void __launch_bounds__(kBlock, 4) msdist_kernel(DevGraph g, MsDistArg
   const MsdState st = state_of(a, blockIdx.x, V);
   for (uint32_t grp = blockIdx.x; grp < a.ngroups; grp += gridDim.x) {
     const uint32_t r0 = grp * kR, nr = min(kR, a.n - r0);
-    // fresh state: every distance unreached, no dirty bit, no stamp
     {
       uint4* d4 = reinterpret_cast<uint4*>(st.D);
       const size_t n4 = (size_t)V * kR / 4u;
       const uint4 inf4 = make_uint4(kInf, kInf, kInf, kInf);
       for (size_t x = tid; x < n4; x += kBlock) d4[x] = inf4;
       for (uint32_t x = tid; x < V; x += kBlock) {
-        st.dirty[x] = 0u;
-        st.stampP[x] = kInf;
-        st.stampN[x] = kInf;
+        st.stC[x] = kInf;
+        st.stF[x] = kInf;
+        st.pend[x] = kInf;
       }
     }
+    if (tid < 5) {
+      s_n[tid] = 0u;
+      s_buf[tid] = tid;
+    }
     if (tid == 0) {
-      s_nC = s_nP = s_nN = 0u;
-      s_minN = kInf;
       s_hi = a.delta;
-      s_kb = 0u;
-      s_ci = 0u;
-      s_pi = 1u;
-      s_ni = 2u;
+      s_minD = kInf;
     }
     __syncthreads();
     const uint32_t myroot = lane < nr ? a.roots[r0 + lane] : kInf;
     if (hw == 0 && lane < nr) {
       st.D[(size_t)myroot * kR + lane] = 0u;
-      wor(&st.dirty[myroot], 1u << lane);
-      if (wxchg(&st.stampP[myroot], 0u) != 0u) st.L[atomicAdd(&s_nC, 1u)] = myroot;
+      if (wxchg(&st.stF[myroot], 0u) != 0u) st.L[atomicAdd(&s_n[0], 1u)] = myroot;
     }
     __syncthreads();
-    uint32_t phase = 0;
+    uint32_t phase = 1;
     while (true) {
-      const uint32_t n = s_nC, hi = s_hi, kb1 = s_kb + 1u;
-      uint32_t* LC = st.L + (size_t)s_ci * V;
-      uint32_t* LP = st.L + (size_t)s_pi * V;
-      uint32_t* LN = st.L + (size_t)s_ni * V;
-      if (n == 0) break;  // block-uniform: no list holds anything
-      __syncthreads();    // every thread has read the shared words
-      if (tid == 0) s_nP = 0u;
+      const uint32_t nF = s_n[0];
+      if (nF == 0) {
+        // the bucket is done: advance past the smallest deferred value; the
+        // deferred nodes below the new end form the frontier
+        const uint32_t nD = s_n[3];
+        if (nD == 0) break;  // block-uniform: nothing left anywhere
+        const uint32_t hi = max(s_hi + a.delta, (s_minD / a.delta + 1u) * a.delta);
+        uint32_t* LDef = st.L + (size_t)s_buf[3] * V;
+        uint32_t* LDef2 = st.L + (size_t)s_buf[4] * V;
+        uint32_t* LF = st.L + (size_t)s_buf[0] * V;
+        __syncthreads();  // every thread has read the fills
+        if (tid == 0) s_minD2 = kInf;
+        __syncthreads();
+        uint32_t mn = kInf;
+        for (uint32_t i = tid; i < nD; i += kBlock) {
+          const uint32_t y = ld2(LDef + i);
+          const uint32_t p = ld2(&st.pend[y]);
+          if (p < hi) {
+            st.pend[y] = kInf;
+            if (wxchg(&st.stF[y], phase) != phase) LF[atomicAdd(&s_n[0], 1u)] = y;
+          } else {
+            LDef2[atomicAdd(&s_n[4], 1u)] = y;
+            mn = min(mn, p);
+          }
+        }
+        for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+        if ((tid & 63u) == 0 && mn != kInf) atomicMin(&s_minD2, mn);
+        __syncthreads();
+        if (tid == 0) {
+          s_hi = hi;
+          s_n[3] = s_n[4];
+          s_n[4] = 0u;
+          const uint32_t t = s_buf[3];
+          s_buf[3] = s_buf[4];
+          s_buf[4] = t;
+          s_minD = s_minD2;
+        }
+        phase += 1u;
+        __syncthreads();
+        continue;
+      }
+      const uint32_t hi = s_hi;
+      uint32_t* LF = st.L + (size_t)s_buf[0] * V;
+      uint32_t* LNF = st.L + (size_t)s_buf[1] * V;
+      uint32_t* LC = st.L + (size_t)s_buf[2] * V;
+      uint32_t* LDef = st.L + (size_t)s_buf[3] * V;
+      if (a.stats && tid == 0) {
+        atomicAdd(&a.stats[0], 1ull);
+        atomicAdd(&a.stats[1], (unsigned long long)nF);
+      }
+      // (1) expand: the frontier's neighbours become candidates (lane = edge)
+      for (uint32_t i = hw; i < nF; i += kHW) {
+        const uint32_t f = ld2(LF + i);
+        const uint32_t beg = g.row_ptr[f], deg = g.row_ptr[f + 1] - beg;
+        for (uint32_t e0 = 0; e0 < deg; e0 += kR) {
+          uint32_t y = kDown;
+          if (e0 + lane < deg) y = g.ew ? g.ew[beg + e0 + lane].x : g.colx[beg + e0 + lane];
+          const bool fresh = !(y & kDown) && wxchg(&st.stC[y], phase) != phase;
+          const uint32_t m = (uint32_t)(__ballot(fresh) >> hbase);
+          if (!m) continue;
+          uint32_t pos = 0;
+          if (lane == 0) pos = atomicAdd(&s_n[2], (uint32_t)__popc(m));
+          pos = (uint32_t)__shfl((int)pos, (int)hbase, 64);
+          if (fresh) LC[pos + __popc(m & ((1u << lane) - 1u))] = y;
+        }
+      }
       __syncthreads();
-      const uint32_t nph = phase + 1u;
-      uint32_t minN = kInf;
-      // a half-wave's lane 0: list y for the next phase / the next bucket
-      auto pushP = [&](uint32_t y) {
-        if (wxchg(&st.stampP[y], nph) != nph) LP[atomicAdd(&s_nP, 1u)] = y;
-      };
-      auto pushN = [&](uint32_t y) {
-        if (wxchg(&st.stampN[y], kb1) != kb1) LN[atomicAdd(&s_nN, 1u)] = y;
-      };
-      for (uint32_t i0 = hw * kU; i0 < n; i0 += kHW * kU) {
-        uint32_t v[kU], take[kU], beg[kU], deg[kU], d[kU];
+      const uint32_t nC = s_n[2];
+      if (a.stats && tid == 0) atomicAdd(&a.stats[2], (unsigned long long)nC);
+      // (2) pull: kU candidates per half-wave at once, lane = root; their
+      // first 32 in-links' loads in flight together (kE per candidate per
+      // step), the rest of a wider row after
+      uint32_t mnD = kInf;
+      for (uint32_t i0 = hw * kU; i0 < nC; i0 += kHW * kU) {
+        uint32_t y[kU], beg[kU], deg[kU], dy[kU], best[kU], ucol[kU], uw[kU];
 #pragma unroll
-        for (uint32_t u = 0; u < kU; ++u) v[u] = i0 + u < n ? ld2(LC + i0 + u) : kInf;
+        for (uint32_t u = 0; u < kU; ++u) y[u] = i0 + u < nC ? ld2(LC + i0 + u) : kInf;
 #pragma unroll
         for (uint32_t u = 0; u < kU; ++u) {
-          take[u] = 0u;
           beg[u] = deg[u] = 0u;
-          if (v[u] == kInf) continue;
-          if (lane == 0) take[u] = wxchg(&st.dirty[v[u]], 0u);
-          beg[u] = g.row_ptr[v[u]];
-          deg[u] = g.row_ptr[v[u] + 1] - beg[u];
+          if (y[u] == kInf) continue;
+          beg[u] = g.row_ptr[y[u]];
+          deg[u] = g.row_ptr[y[u] + 1] - beg[u];
         }
+        uint32_t dmax = 0;
 #pragma unroll
         for (uint32_t u = 0; u < kU; ++u) {
-          take[u] = (uint32_t)__shfl((int)take[u], (int)hbase, 64);
-          d[u] = (take[u] >> lane) & 1u ? ld2(&st.D[(size_t)v[u] * kR + lane]) : kInf;
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < kU; ++u) {
-          if (v[u] == kInf) continue;
-          const bool mine = (take[u] >> lane) & 1u;
-          const bool relay = v[u] == myroot || !((g.nt_bits[v[u] >> 5] >> (v[u] & 31u)) & 1u);
-          const bool act = mine && relay && d[u] < hi;
-          const bool later = mine && relay && d[u] >= hi;
-          // roots already past the bucket: their bits back, the node on the
-          // next bucket's list (it is there already when they were lowered
-          // from this bucket: the stamp keeps one entry)
-          const uint32_t lm = (uint32_t)(__ballot(later) >> hbase);
-          if (lm) {
-            minN = min(minN, later ? d[u] : kInf);
-            if (lane == 0) {
-              wor(&st.dirty[v[u]], lm);
-              pushN(v[u]);
+          dy[u] = y[u] == kInf ? 0u : ld2(&st.D[(size_t)y[u] * kR + lane]);
+          best[u] = dy[u];
+          ucol[u] = kDown;
+          uw[u] = 0u;
+          if (lane < deg[u]) {
+            const uint32_t e = beg[u] + lane;
+            if (g.ew) {
+              const uint2 x = g.ew[e];
+              ucol[u] = x.x;
+              uw[u] = x.y >> 16;  // metric of the link u -> y
+            } else {
+              ucol[u] = g.colx[e];
+              uw[u] = g.rw[e];
             }
+            if (a.hop) uw[u] = 1u;
           }
-          if (!(uint32_t)(__ballot(act) >> hbase)) continue;
-          // the row's entries over the lanes, then one edge at a time
-          for (uint32_t e0 = 0; e0 < deg[u]; e0 += kR) {
-            uint32_t ycol = kDown, yw = 0u;
-            if (e0 + lane < deg[u]) {
-              const uint32_t e = beg[u] + e0 + lane;
-              if (g.ew) {
-                const uint2 x = g.ew[e];
-                ycol = x.x;
-                yw = x.y & 0xFFFFu;
-              } else {
-                ycol = g.colx[e];
-                yw = g.w[e];
-              }
-              if (a.hop) yw = 1u;
+          dmax = max(dmax, min(deg[u], kR));
+        }
+        for (uint32_t j0 = 0; j0 < dmax; j0 += kE) {
+          uint32_t uu[kU][kE], du[kU][kE];
+#pragma unroll
+          for (uint32_t u = 0; u < kU; ++u)
+#pragma unroll
+            for (uint32_t k = 0; k < kE; ++k) {
+              uu[u][k] = (uint32_t)__shfl((int)ucol[u], (int)(hbase + min(j0 + k, kR - 1u)), 64);
+              if (j0 + k >= min(deg[u], kR)) uu[u][k] = kDown;
+              du[u][k] = (uu[u][k] & kDown) ? kInf : ld2(&st.D[(size_t)uu[u][k] * kR + lane]);
             }
-            const uint32_t cnt = min(kR, deg[u] - e0);
-            for (uint32_t j0 = 0; j0 < cnt; j0 += kE) {
-              // kE edges: every atomicMin issued before any result is used
-              uint32_t yy[kE], nd[kE], old[kE];
 #pragma unroll
-              for (uint32_t k = 0; k < kE; ++k) {
-                const uint32_t j = min(j0 + k, cnt - 1u);
-                yy[k] = (uint32_t)__shfl((int)ycol, (int)(hbase + j), 64);
-                const uint32_t w = (uint32_t)__shfl((int)yw, (int)(hbase + j), 64);
-                if (j0 + k >= cnt) yy[k] = kDown;  // past the row (half-uniform)
-                nd[k] = d[u] + w;
-                old[k] = 0u;
-                if (act && !(yy[k] & kDown)) old[k] = wmin(&st.D[(size_t)yy[k] * kR + lane], nd[k]);
-              }
-              uint32_t im[kE], ip[kE];
+          for (uint32_t u = 0; u < kU; ++u)
 #pragma unroll
-              for (uint32_t k = 0; k < kE; ++k) {
-                const bool imp = act && !(yy[k] & kDown) && nd[k] < old[k];
-                im[k] = (uint32_t)(__ballot(imp) >> hbase);
-                ip[k] = (uint32_t)(__ballot(imp && nd[k] < hi) >> hbase);
-                if (imp && nd[k] >= hi) minN = min(minN, nd[k]);
-              }
-              if (lane == 0) {
-                uint32_t sp[kE], sn[kE];
+            for (uint32_t k = 0; k < kE; ++k) {
+              const uint32_t w = (uint32_t)__shfl((int)uw[u], (int)(hbase + min(j0 + k, kR - 1u)), 64);
+              if (du[u][k] >= hi) continue;  // unreached, or not settled into the bucket yet
+              const uint32_t x = uu[u][k];
+              const bool relay = x == myroot || !((g.nt_bits[x >> 5] >> (x & 31u)) & 1u);
+              if (relay) best[u] = min(best[u], du[u][k] + w);
+            }
+        }
 #pragma unroll
-                for (uint32_t k = 0; k < kE; ++k) {
-                  sp[k] = sn[k] = 0u;
-                  if (!im[k]) continue;
-                  wor(&st.dirty[yy[k]], im[k]);
-                  if (ip[k]) sp[k] = wxchg(&st.stampP[yy[k]], nph);
-                  if (im[k] & ~ip[k]) sn[k] = wxchg(&st.stampN[yy[k]], kb1);
-                }
+        for (uint32_t u = 0; u < kU; ++u) {
+          for (uint32_t e = kR; e < deg[u]; ++e) {  // rows past 32 in-links (rare)
+            uint32_t x, w;
+            if (g.ew) {
+              const uint2 q = g.ew[beg[u] + e];
+              x = q.x;
+              w = q.y >> 16;
+            } else {
+              x = g.colx[beg[u] + e];
+              w = g.rw[beg[u] + e];
+            }
+            if (a.hop) w = 1u;
+            if (x & kDown) continue;
+            const uint32_t dx = ld2(&st.D[(size_t)x * kR + lane]);
+            const bool relay = x == myroot || !((g.nt_bits[x >> 5] >> (x & 31u)) & 1u);
+            if (dx < hi && relay) best[u] = min(best[u], dx + w);
+          }
+        }
 #pragma unroll
-                for (uint32_t k = 0; k < kE; ++k) {
-                  if (!im[k]) continue;
-                  if (ip[k] && sp[k] != nph) LP[atomicAdd(&s_nP, 1u)] = yy[k];
-                  if ((im[k] & ~ip[k]) && sn[k] != kb1) LN[atomicAdd(&s_nN, 1u)] = yy[k];
-                }
-              }
+        for (uint32_t u = 0; u < kU; ++u) {
+          if (y[u] == kInf) continue;
+          const bool ch = best[u] < dy[u];
+          if (ch) st.D[(size_t)y[u] * kR + lane] = best[u];
+          const uint32_t cm = (uint32_t)(__ballot(ch) >> hbase);
+          if (!cm) continue;
+          const uint32_t lt = (uint32_t)(__ballot(ch && best[u] < hi) >> hbase);
+          uint32_t late = (ch && best[u] >= hi) ? best[u] : kInf;
+          for (int o = 16; o > 0; o >>= 1) late = min(late, (uint32_t)__shfl_xor((int)late, o, 64));
+          if (lane == 0) {
+            if (lt && wxchg(&st.stF[y[u]], phase) != phase) LNF[atomicAdd(&s_n[1], 1u)] = y[u];
+            if (late != kInf) {
+              mnD = min(mnD, late);
+              if (wamin(&st.pend[y[u]], late) == kInf) LDef[atomicAdd(&s_n[3], 1u)] = y[u];
             }
           }
         }
       }
-#pragma unroll
-      for (int o = 16; o > 0; o >>= 1) minN = min(minN, (uint32_t)__shfl_xor((int)minN, o, 64));
-      if (lane == 0 && minN != kInf) atomicMin(&s_minN, minN);
+      for (int o = 32; o > 0; o >>= 1) mnD = min(mnD, (uint32_t)__shfl_xor((int)mnD, o, 64));
+      if ((tid & 63u) == 0 && mnD != kInf) atomicMin(&s_minD, mnD);
       __syncthreads();
-      if (tid == 0) {
-        const uint32_t c = s_ci, p = s_pi, nx = s_ni;
-        if (s_nP > 0) {  // more of this bucket
-          s_ci = p;
-          s_pi = c;
-          s_nC = s_nP;
-        } else {         // the bucket is settled: on to the next one
-          s_ci = nx;
-          s_pi = c;
-          s_ni = p;
-          s_nC = s_nN;
-          s_nN = 0u;
-          if (s_minN != kInf) s_hi = max(s_hi + a.delta, (s_minN / a.delta + 1u) * a.delta);
-          s_minN = kInf;
-          s_kb += 1u;
-        }
+      if (tid == 0) {  // next frontier -> frontier; candidates emptied
+        s_n[0] = s_n[1];
+        s_n[1] = 0u;
+        s_n[2] = 0u;
+        const uint32_t t = s_buf[0];
+        s_buf[0] = s_buf[1];
+        s_buf[1] = t;
       }
-      phase = nph;
+      phase += 1u;
       __syncthreads();
     }
     // rows: [V][32] -> 32 rows of V through LDS, 8 tiles of 32 nodes per
@@ -283,14 +318,13 @@ __global__ void __launch_bounds__(kBlock, 4) msdist_kernel(DevGraph g, MsDistArg
       }
       __syncthreads();
     }
-    __syncthreads();
   }
 }
 
 }  // namespace
 
 size_t msdist_scratch_bytes(uint32_t V, uint32_t blocks) {
-  return (size_t)V * (kR + 6u) * 4u * blocks;
+  return (size_t)V * kWords * 4u * blocks;
 }
 
 hipError_t launch_msdist(const DevGraph& g, const MsDistArgs& a, hipStream_t s) {

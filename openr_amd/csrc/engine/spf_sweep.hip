@@ -1821,9 +1821,9 @@ int plan_wmulti(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   std::vector<uint32_t> pos(V, kNone);
   for (uint32_t i = 0; i < nS; ++i) pos[srows[i]] = i;
   for (uint32_t j = 0; j < nL; ++j) pos[own_l[j]] = nS + j;
-  // concurrent groups: two per CU, within a scratch budget (OSPF_MSD_MB, 32 GB)
+  // concurrent groups: two per CU, within a scratch budget (OSPF_MSD_MB, 64 GB)
   const uint32_t ngroups = (nS + 31u) / 32u;
-  size_t budget = 32768ull << 20;
+  size_t budget = 65536ull << 20;
   if (const char* e = getenv("OSPF_MSD_MB")) budget = (size_t)std::max(64, atoi(e)) << 20;
   const size_t per = ospf::msdist_scratch_bytes(V, 1);
   uint32_t blocks = std::min<uint32_t>(std::max(1u, ngroups), 2u * (uint32_t)c->n_cu);
@@ -1867,8 +1867,23 @@ int plan_wmulti(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       a.dist = slab;
       a.pitch = V;
       a.scratch = scratch;
+      const bool dbg = getenv("OSPF_MSD_STATS") != nullptr;
+      unsigned long long* st = nullptr;
+      if (dbg && (hipMalloc(&st, 32) != hipSuccess || hipMemset(st, 0, 32) != hipSuccess))
+        return ospf_int::fail(c, OSPF_E_DEVICE, "msdist stats");
+      a.stats = st;
       const hipError_t e = ospf::launch_msdist(c->g, a, strm);
       if (e != hipSuccess) return ospf_int::hip_fail(c, e, "launch_msdist");
+      if (dbg) {  // debug only (never inside a capture: OSPF_MSD_STATS runs eager sweeps)
+        unsigned long long h[4];
+        hipStreamSynchronize(strm);
+        hipMemcpy(h, st, 32, hipMemcpyDeviceToHost);
+        hipFree(st);
+        fprintf(stderr, "msdist: %u rows, %u groups: phases %llu (%.1f per group), frontier "
+                "nodes %llu (%.2f per node per group), candidates %llu (%.2f per node per group)\n",
+                nS, ngroups, h[0], (double)h[0] / ngroups, h[1],
+                (double)h[1] / ((double)ngroups * V), h[2], (double)h[2] / ((double)ngroups * V));
+      }
       c->spf_runs += nS;
       return OSPF_OK;
     };
