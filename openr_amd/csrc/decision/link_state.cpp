@@ -6,6 +6,7 @@
 #include <numeric>
 #include <set>
 #include <algorithm>
+#include <unordered_set>
 #include <functional>
 #include <map>
 #include <stdexcept>
@@ -186,9 +187,32 @@ std::vector<LinkPtr> LinkState::sortedLinksOf(const std::string& node) const {
 static size_t V_of(const LinkState::Csr& c) { return c.names.size(); }
 
 void LinkState::clearMemo() {
+  if (memoMetric_.empty() && memoHops_.empty() && memoKsp_.empty()) return;
+  // A route build materialises every entry of its results (~100k node
+  // results with next-hop sets and path links at F100k): freeing them took
+  // most of an event's apply time. They are unreachable once dropped, so a
+  // background thread frees them; the snapshot references they hold are
+  // counted so patchStructure knows they are no readers.
+  using Memo = std::unordered_map<std::string, SpfResult>;
+  struct Dead {
+    Memo a, b;
+    std::unordered_map<std::string, std::vector<Path>> k;
+  };
+  auto* dead = new Dead{std::move(memoMetric_), std::move(memoHops_), std::move(memoKsp_)};
   memoMetric_.clear();
   memoHops_.clear();
   memoKsp_.clear();
+  std::unordered_set<const SpfRows*> rows;
+  for (const Memo* m : {&dead->a, &dead->b})
+    for (const auto& kv : *m)
+      if (kv.second.rows() && kv.second.rows()->csr == csr_) rows.insert(kv.second.rows().get());
+  const long r = (long)rows.size();
+  auto cnt = reapRefs_;
+  cnt->fetch_add(r);
+  std::thread([dead, cnt, r] {
+    delete dead;
+    cnt->fetch_sub(r);
+  }).detach();
 }
 
 void LinkState::invalidate() {
@@ -1374,8 +1398,10 @@ void LinkState::patchGraph(const std::vector<LinkDelta>& links,
 // block moves on host threads, no re-snapshot, no device reload.
 void LinkState::patchStructure(const std::vector<LinkPtr>& added,
                                const std::vector<LinkPtr>& removed) {
+  dropSweep();  // its rows describe the graph before the patch
   // a kept memoised result reads this snapshot's ranks lazily: give it its own
-  if (csr_.use_count() > 1) csr_ = std::make_shared<Csr>(*csr_);
+  // (results being released by clearMemo's thread are no readers)
+  if (csr_.use_count() - 1 - reapRefs_->load() > 0) csr_ = std::make_shared<Csr>(*csr_);
   Csr& c = *csr_;
   const uint32_t V = (uint32_t)c.names.size();
   std::vector<uint32_t> rows;
@@ -1510,7 +1536,6 @@ void LinkState::patchStructure(const std::vector<LinkPtr>& added,
   const bool inSync = engine_ && engineVersion_ == snapVersion_;
   ++version_;
   snapVersion_ = version_;
-  dropSweep();  // its rows describe the graph before the patch
   if (inSync) patchEngineRows(rows);
 }
 

@@ -539,6 +539,10 @@ class LinkState {
 
   std::unordered_map<std::string, SpfResult> memoMetric_, memoHops_;
   std::unordered_map<std::string, std::vector<Path>> memoKsp_;
+  // references to csr_ held by memoised results being released on a
+  // background thread (clearMemo): patchStructure mutates the snapshot in
+  // place when no other holder is left
+  std::shared_ptr<std::atomic<long>> reapRefs_ = std::make_shared<std::atomic<long>>(0);
 };
 
 }  // namespace odl
