@@ -132,16 +132,28 @@ __global__ void __launch_bounds__(kBlock, 4) msdist_kernel(DevGraph g, MsDistArg
         __syncthreads();  // every thread has read the fills
         if (tid == 0) s_minD2 = kInf;
         __syncthreads();
+        // half-wave per deferred node (lane = root): below the new end it
+        // joins the frontier; its roots still at or past the end (never
+        // propagated: values past `hi` are never pulled) keep it deferred
         uint32_t mn = kInf;
-        for (uint32_t i = tid; i < nD; i += kBlock) {
+        for (uint32_t i = hw; i < nD; i += kHW) {
           const uint32_t y = ld2(LDef + i);
           const uint32_t p = ld2(&st.pend[y]);
+          uint32_t keep = p;
           if (p < hi) {
-            st.pend[y] = kInf;
-            if (wxchg(&st.stF[y], phase) != phase) LF[atomicAdd(&s_n[0], 1u)] = y;
-          } else {
-            LDef2[atomicAdd(&s_n[4], 1u)] = y;
-            mn = min(mn, p);
+            const uint32_t d = ld2(&st.D[(size_t)y * kR + lane]);
+            keep = d >= hi && d != kInf ? d : kInf;
+            for (int o = 16; o > 0; o >>= 1) keep = min(keep, (uint32_t)__shfl_xor((int)keep, o, 64));
+          }
+          if (lane == 0) {
+            if (p < hi) {
+              st.pend[y] = keep;
+              if (wxchg(&st.stF[y], phase) != phase) LF[atomicAdd(&s_n[0], 1u)] = y;
+            }
+            if (keep != kInf) {
+              LDef2[atomicAdd(&s_n[4], 1u)] = y;
+              mn = min(mn, keep);
+            }
           }
         }
         for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
