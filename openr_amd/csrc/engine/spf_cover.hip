@@ -189,52 +189,82 @@ __device__ __forceinline__ void write_row_nh(const DevGraph& g, const CoverGraph
   uint32_t reach = 0;
   // a block step = nthreads consecutive nodes; their next-hop words leave
   // through LDS as one contiguous run (lane-strided NW-word records would
-  // write partial lines)
+  // write partial lines). Loads run ahead: the next step's first two in-link
+  // quads and the step after's cover index are issued before this step's
+  // nodes are folded.
+  const uint4 pad = make_uint4(0xFFFFu, 0xFFFFu, 0xFFFFu, 0xFFFFu);
+  auto quads = [&](uint32_t vv, uint32_t cx, uint4& a, uint4& b) {
+    a = b = pad;
+    if (vv < V && (cx & kLeaf)) {
+      const uint32_t q0 = (cx >> 5) & 0x3FFFFFFu, nq = cx & 31u;
+      if (nq > 0) a = la4[q0];
+      if (nq > 1) b = la4[q0 + 1];
+    }
+  };
+  uint32_t cxA = tid < V ? C.cix[tid] : 0u;
+  uint32_t cxB = tid + nthreads < V ? C.cix[tid + nthreads] : 0u;
+  uint4 qA0, qA1;
+  quads(tid, cxA, qA0, qA1);
   for (uint32_t v0 = 0; v0 < V; v0 += nthreads) {
     const uint32_t v = v0 + tid;
+    uint4 qB0, qB1;
+    quads(v + nthreads, cxB, qB0, qB1);
+    const uint32_t cxC = v + 2u * nthreads < V ? C.cix[v + 2u * nthreads] : 0u;
     uint32_t out = kInf, m[NW];
 #pragma unroll
     for (int w = 0; w < NW; ++w) m[w] = 0u;
     if (v < V) {
-      const uint32_t cx = C.cix[v];
+      const uint32_t cx = cxA;
       if (!(cx & kLeaf)) {
         out = s_D[cx];
 #pragma unroll
         for (int w = 0; w < NW; ++w) m[w] = cm[(size_t)cx * NW + w];
       } else {
         const uint32_t q0 = (cx >> 5) & 0x3FFFFFFu, nq = cx & 31u;
-        for (uint32_t qq = 0; qq < nq; ++qq) {
+        const uint32_t es[8] = {qA0.x, qA0.y, qA0.z, qA0.w, qA1.x, qA1.y, qA1.z, qA1.w};
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          const uint32_t ci = es[b] & 0xFFFFu;
+          if (!usable(ci) || s_D[ci] == kInf) continue;
+          out = min(out, s_D[ci] + (es[b] >> 16));
+        }
+        for (uint32_t qq = 2; qq < nq; ++qq) {
           const uint4 e4 = la4[q0 + qq];
-          const uint32_t es[4] = {e4.x, e4.y, e4.z, e4.w};
+          const uint32_t ex[4] = {e4.x, e4.y, e4.z, e4.w};
 #pragma unroll
           for (int b = 0; b < 4; ++b) {
-            const uint32_t ci = es[b] & 0xFFFFu;
+            const uint32_t ci = ex[b] & 0xFFFFu;
             if (!usable(ci) || s_D[ci] == kInf) continue;
-            out = min(out, s_D[ci] + (es[b] >> 16));
+            out = min(out, s_D[ci] + (ex[b] >> 16));
           }
         }
-        if (out != kInf)
-          for (uint32_t qq = 0; qq < nq; ++qq) {
-            const uint4 e4 = la4[q0 + qq];
-            const uint32_t es[4] = {e4.x, e4.y, e4.z, e4.w};
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-              const uint32_t ci = es[b] & 0xFFFFu;
-              if (!usable(ci) || s_D[ci] == kInf || s_D[ci] + (es[b] >> 16) != out) continue;
-              if (ci == r) {  // a neighbour of the root: its own bit
-                uint32_t lo = 0, hi = K;
-                while (lo < hi) {
-                  const uint32_t mid = (lo + hi) >> 1;
-                  if (dn[mid] < v) lo = mid + 1;
-                  else hi = mid;
-                }
-                if (lo < 32u * NW) m[lo >> 5] |= 1u << (lo & 31u);
-              } else {
-#pragma unroll
-                for (int w = 0; w < NW; ++w) m[w] |= cm[(size_t)ci * NW + w];
-              }
+        auto tight = [&](uint32_t e) {
+          const uint32_t ci = e & 0xFFFFu;
+          if (!usable(ci) || s_D[ci] == kInf || s_D[ci] + (e >> 16) != out) return;
+          if (ci == r) {  // a neighbour of the root: its own bit
+            uint32_t lo = 0, hi = K;
+            while (lo < hi) {
+              const uint32_t mid = (lo + hi) >> 1;
+              if (dn[mid] < v) lo = mid + 1;
+              else hi = mid;
             }
+            if (lo < 32u * NW) m[lo >> 5] |= 1u << (lo & 31u);
+          } else {
+#pragma unroll
+            for (int w = 0; w < NW; ++w) m[w] |= cm[(size_t)ci * NW + w];
           }
+        };
+        if (out != kInf) {
+#pragma unroll
+          for (int b = 0; b < 8; ++b) tight(es[b]);
+          for (uint32_t qq = 2; qq < nq; ++qq) {
+            const uint4 e4 = la4[q0 + qq];
+            tight(e4.x);
+            tight(e4.y);
+            tight(e4.z);
+            tight(e4.w);
+          }
+        }
       }
       if (v == rn || out == kInf) {
 #pragma unroll
@@ -262,6 +292,10 @@ __device__ __forceinline__ void write_row_nh(const DevGraph& g, const CoverGraph
       if (base + i < lim) __builtin_nontemporal_store(s_st[i], nhrow + base + i);
     }
     __syncthreads();  // s_st is rewritten by the next step
+    cxA = cxB;
+    qA0 = qB0;
+    qA1 = qB1;
+    cxB = cxC;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
