@@ -212,17 +212,7 @@ class LinkState:
             lines.append(f"{p}\t{','.join(es)}")
         flags = int(node_labels) | (2 if adj_labels else 0) | (4 if ucmp else 0)
         if binary:  # odl_route_db_bin: records + a string table, no text
-            buf, nb = C.c_void_p(), C.c_uint64()
-            rc = self._L.odl_route_db_bin(self._h, "\n".join(mes).encode(), len(mes),
-                                          "\n".join(lines).encode(), len(lines), flags,
-                                          C.byref(buf), C.byref(nb))
-            if rc != 0:
-                raise LinkStateError(self._err())
-            try:
-                raw = C.string_at(buf.value, nb.value)
-            finally:
-                self._L.odl_free_buf(buf)
-            return decode_route_db_bin(raw)
+            return decode_route_db_bin(self.route_db_bin_raw(mes, lines, flags))
         t = self._take(self._L.odl_route_db_text(
             self._h, "\n".join(mes).encode(), len(mes), "\n".join(lines).encode(),
             len(lines), flags))
@@ -241,6 +231,20 @@ class LinkState:
                     (ifn, nbr, int(metric), ops[op],
                      tuple(int(x) for x in labels.split(",") if x), int(w)))
         return out
+
+    def route_db_bin_raw(self, mes: Sequence[str], prefix_lines: Sequence[str], flags: int) -> bytes:
+        """odl_route_db_bin as raw bytes (prefix_lines in the text ABI's
+        "prefix\tentries" form): what a C / C++ caller gets, before decoding."""
+        buf, nb = C.c_void_p(), C.c_uint64()
+        rc = self._L.odl_route_db_bin(self._h, "\n".join(mes).encode(), len(mes),
+                                      "\n".join(prefix_lines).encode(), len(prefix_lines), flags,
+                                      C.byref(buf), C.byref(nb))
+        if rc != 0:
+            raise LinkStateError(self._err())
+        try:
+            return C.string_at(buf.value, nb.value)
+        finally:
+            self._L.odl_free_buf(buf)
 
     @staticmethod
     def path_a_in_b(a: Sequence[str], b: Sequence[str]) -> bool:

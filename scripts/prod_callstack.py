@@ -85,11 +85,17 @@ def main():
                "build_result_ms": sum(cap.values("build_result_ms"))}
         names = p.node_names()
         prefixes = {f"lo-{n}": [[n, "ip", "ecmp", 0, None]] for n in names}
-        _, wall_r, cap_r = timed(lambda: p.route_dbs([me], prefixes))
+        lines = [f"{pfx}\t{ents[0][0]}:0:0:0:" for pfx, ents in prefixes.items()]
+        raw, wall_r, cap_r = timed(lambda: p.route_db_bin_raw([me], lines, 3))
         rec["route_build_ms"] = sum(cap_r.values("build_route_db_ms"))
         rec["route_build_wall_ms_incl_binary_abi"] = round(wall_r, 3)
+        rec["route_db_binary_bytes"] = len(raw)
+        t = time.perf_counter()
+        from openr_amd.linkstate import decode_route_db_bin
+        decode_route_db_bin(raw)
+        rec["python_decode_of_binary_ms"] = round((time.perf_counter() - t) * 1e3, 1)
         _, wall_t, _ = timed(lambda: p.route_dbs([me], prefixes, binary=False))
-        rec["route_build_wall_ms_incl_text_abi"] = round(wall_t, 3)
+        rec["route_build_wall_ms_incl_text_abi_and_python_parse"] = round(wall_t, 3)
         rec["total_ms"] = round(rec["getSpfResult_wall_ms"] + rec["route_build_ms"], 3)
         out[label] = rec
         print(f"{label}: {rec}", file=sys.stderr, flush=True)
