@@ -809,25 +809,18 @@ __global__ void __launch_bounds__(256) closure_nh_kernel(ClosurePlan p) {
   const uint32_t v = chunk * 256u + threadIdx.x;
   const bool ok = v < p.nS;
   const uint2 cm = p.comp[ci];
-  // per member: the best value and its first two tight terms (seed term j,
-  // or kLoc | m for member m's local distance); a third tight term sets a
-  // flag and the masks are then recomputed over every term (rare). The mask
-  // words are only read at the end: two compares and three selects per
-  // (term, member) instead of a masked OR of every word.
-  constexpr uint32_t kLoc = 0x80000000u, kNoT = 0xFFFFFFFFu;
-  uint32_t acc[KW], t1[KW], t2[KW], many = 0u;
+  uint32_t acc[KW], mk[KW][NW];
 #pragma unroll
   for (int f = 0; f < KW; ++f) {
     acc[f] = kClInf;
-    t1[f] = t2[f] = kNoT;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) mk[f][w] = 0u;
   }
-  auto take = [&](int f, uint32_t c, uint32_t id) {
-    const bool lt = c < acc[f], eq = c == acc[f];
-    many |= (eq && t2[f] != kNoT) ? (1u << f) : 0u;
-    many = lt ? (many & ~(1u << f)) : many;
-    t2[f] = lt ? kNoT : (eq && t2[f] == kNoT ? id : t2[f]);
-    t1[f] = lt ? id : t1[f];
-    acc[f] = lt ? c : acc[f];
+  auto take = [&](int f, uint32_t c, const uint32_t* m) {
+    const bool lt = c < acc[f], le = c <= acc[f];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) mk[f][w] = (lt ? 0u : mk[f][w]) | (le ? m[w] : 0u);
+    acc[f] = min(acc[f], c);
   };
   const uint32_t* cst = p.cst + (size_t)cm.x * KW;
   const uint32_t* fh = p.fh + (size_t)cm.x * KW * NW;
@@ -844,7 +837,7 @@ __global__ void __launch_bounds__(256) closure_nh_kernel(ClosurePlan p) {
       const uint32_t j = j0 + (uint32_t)u;
       if (j >= cm.y) break;  // uniform
 #pragma unroll
-      for (int f = 0; f < KW; ++f) take(f, cst[j * KW + f] + x[u], j);
+      for (int f = 0; f < KW; ++f) take(f, cst[j * KW + f] + x[u], fh + ((size_t)j * KW + f) * NW);
     }
   }
   const uint32_t* mem = p.mem + (size_t)ci * KW;
@@ -854,49 +847,16 @@ __global__ void __launch_bounds__(256) closure_nh_kernel(ClosurePlan p) {
   for (int m = 0; m < KW; ++m)
     if (mem[m] == v)
 #pragma unroll
-      for (int f = 0; f < KW; ++f) take(f, dl[f * KW + m], kLoc | (uint32_t)m);
+      for (int f = 0; f < KW; ++f) take(f, dl[f * KW + m], fl + ((size_t)f * KW + m) * NW);
   const uint32_t* out = p.out + (size_t)ci * KW;
-  auto fhw = [&](int f, uint32_t id, int w) -> uint32_t {
-    if (id == kNoT) return 0u;
-    return (id & kLoc) ? fl[((size_t)f * KW + (id & 0xFFu)) * NW + w]
-                       : fh[((size_t)id * KW + f) * NW + w];
-  };
 #pragma unroll
   for (int f = 0; f < KW; ++f) {
-    if (out[f] == kInf) continue;  // uniform
+    if (!ok || out[f] == kInf) continue;
     const bool un = acc[f] >= kClInf;
-    uint32_t mk[NW];
-#pragma unroll
-    for (int w = 0; w < NW; ++w) mk[w] = un ? 0u : (fhw(f, t1[f], w) | fhw(f, t2[f], w));
-    const bool slow = ok && !un && ((many >> f) & 1u);
-    if (__ballot(slow)) {  // three or more tight terms: OR over every one
-      for (uint32_t j0 = 0; j0 < cm.y; j0 += 8u) {
-        uint32_t x[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const uint32_t j = j0 + (uint32_t)u;
-          x[u] = (slow && j < cm.y) ? p.seedC[(size_t)jl[j] * p.nS + v] : kClInf;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const uint32_t j = j0 + (uint32_t)u;
-          if (j >= cm.y) break;  // uniform
-          if (slow && cst[j * KW + f] + x[u] == acc[f])
-#pragma unroll
-            for (int w = 0; w < NW; ++w) mk[w] |= fh[((size_t)j * KW + f) * NW + w];
-        }
-      }
-#pragma unroll
-      for (int m = 0; m < KW; ++m)
-        if (slow && mem[m] == v && dl[f * KW + m] == acc[f])
-#pragma unroll
-          for (int w = 0; w < NW; ++w) mk[w] |= fl[((size_t)f * KW + m) * NW + w];
-    }
-    if (!ok) continue;
     p.dc[(size_t)out[f] * p.nS + v] = un ? kInf : acc[f];
     uint32_t* dm = p.dcm + ((size_t)out[f] * p.nS + v) * NW;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) dm[w] = mk[w];
+    for (int w = 0; w < NW; ++w) dm[w] = un ? 0u : mk[f][w];
   }
 }
 
