@@ -691,6 +691,39 @@ __global__ void __launch_bounds__(512) cover_delta_kernel(DevGraph g, CoverGraph
   }
 }
 
+// Closure rows with next hops (load mode + masks) in a kernel of their own:
+// the Dial kernel's register budget (its widest path) capped it at two
+// 512-thread roots per CU; here a root gets 1,024 threads at <= 64 VGPRs, two
+// roots per CU (the cover columns' 58 KB of LDS each), twice the waves to
+// hide the in-link and mask gathers.
+constexpr uint32_t kRowsBlock = 1024;
+template <int NW>
+__global__ void __launch_bounds__(kRowsBlock, 8) cover_rows_kernel(DevGraph g, CoverGraph C,
+                                                                   CoverArgs a) {
+  extern __shared__ uint32_t s_D[];  // [nS] cover columns, then [ctr words] transit bits
+  __shared__ uint32_t s_st[kRowsBlock * NW];
+  __shared__ unsigned long long s_acc[3];
+  const uint32_t tid = threadIdx.x, nS = C.nS, V = g.V;
+  uint32_t* s_tr = s_D + nS;
+  for (uint32_t x = tid; x < (nS + 31u) / 32u; x += kRowsBlock) s_tr[x] = C.ctr[x];
+  for (uint32_t i = blockIdx.x; i < a.n; i += gridDim.x) {
+    const uint32_t rn = a.roots[i];
+    const uint32_t r = rn < V ? C.cix[rn] : kInf;
+    if (r >= nS) {
+      if (tid == 0) atomicOr(a.err, 64u);
+      continue;
+    }
+    const uint32_t* src = a.dload + (size_t)i * nS;
+    for (uint32_t x = tid; x < nS; x += kRowsBlock) s_D[x] = src[x];
+    if (tid < 3) s_acc[tid] = 0ull;
+    __syncthreads();
+    write_row_nh<NW>(g, C, a.dist + (size_t)a.rowpos[i] * V, a.nh + (size_t)i * V * NW, s_D, s_tr,
+                     r, rn, a.nhload + (size_t)i * nS * NW, a.digest ? a.digest + i : nullptr, s_acc,
+                     s_st, tid, kRowsBlock);
+    __syncthreads();
+  }
+}
+
 __global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C, CoverArgs a) {
   extern __shared__ uint32_t s_D[];  // [nS] distances, then [ctr words] transit bits
   __shared__ uint32_t s_q[kWaves][kQ];
@@ -818,8 +851,10 @@ __global__ void __launch_bounds__(256) closure_nh_kernel(ClosurePlan p) {
   }
   auto take = [&](int f, uint32_t c, const uint32_t* m) {
     const bool lt = c < acc[f], le = c <= acc[f];
+    if (__ballot(le)) {  // wave-uniform: most terms improve no lane (terms sorted by constant)
 #pragma unroll
-    for (int w = 0; w < NW; ++w) mk[f][w] = (lt ? 0u : mk[f][w]) | (le ? m[w] : 0u);
+      for (int w = 0; w < NW; ++w) mk[f][w] = (lt ? 0u : mk[f][w]) | (le ? m[w] : 0u);
+    }
     acc[f] = min(acc[f], c);
   };
   const uint32_t* cst = p.cst + (size_t)cm.x * KW;
@@ -945,6 +980,24 @@ hipError_t launch_cover_spf(const DevGraph& g, const CoverGraph& C, const CoverA
     return hipGetLastError();
   }
   const size_t lds = ((size_t)C.nS + (C.nS + 31u) / 32u) * 4u;
+  if (a.nhload && !getenv("OSPF_COVER_ROWS_IN_DIAL")) {  // closure rows with next hops
+    const uint32_t grid = std::min<uint32_t>(a.n, n_cu * 2u);
+    auto go = [&](const void* k) -> hipError_t {
+      if (lds > 48 * 1024) {
+        const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+      }
+      return hipSuccess;
+    };
+    hipError_t e = hipSuccess;
+    switch (a.NW) {
+      case 1: if ((e = go((const void*)cover_rows_kernel<1>)) == hipSuccess) hipLaunchKernelGGL(cover_rows_kernel<1>, dim3(grid), dim3(kRowsBlock), lds, s, g, C, a); break;
+      case 2: if ((e = go((const void*)cover_rows_kernel<2>)) == hipSuccess) hipLaunchKernelGGL(cover_rows_kernel<2>, dim3(grid), dim3(kRowsBlock), lds, s, g, C, a); break;
+      case 3: if ((e = go((const void*)cover_rows_kernel<3>)) == hipSuccess) hipLaunchKernelGGL(cover_rows_kernel<3>, dim3(grid), dim3(kRowsBlock), lds, s, g, C, a); break;
+      default: if ((e = go((const void*)cover_rows_kernel<4>)) == hipSuccess) hipLaunchKernelGGL(cover_rows_kernel<4>, dim3(grid), dim3(kRowsBlock), lds, s, g, C, a); break;
+    }
+    return e != hipSuccess ? e : hipGetLastError();
+  }
   const uint32_t per_cu = std::max<uint32_t>(1, (uint32_t)((150u * 1024u) / (lds + 14u * 1024u)));
   const uint32_t grid = std::min<uint32_t>(a.n, n_cu * std::min<uint32_t>(per_cu, 4u));
   if (lds > 48 * 1024) {

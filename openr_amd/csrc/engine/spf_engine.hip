@@ -1026,6 +1026,30 @@ int closure_build(ospf_ctx* c, const std::vector<uint32_t>& roots,
         }
       }
     }
+    // terms in ascending order of their smallest constant: a column's best
+    // value tends to come early, so later terms rarely tie or beat it and the
+    // kernel's mask updates (taken only when some lane does) are mostly skipped
+    {
+      const uint32_t nt = (uint32_t)h.jl.size() - joff;
+      std::vector<uint32_t> ord(nt), key(nt, ospf::kClInf);
+      for (uint32_t t = 0; t < nt; ++t) {
+        ord[t] = t;
+        for (uint32_t f = 0; f < KW; ++f) key[t] = std::min(key[t], h.cst[(size_t)(joff + t) * KW + f]);
+      }
+      std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
+      std::vector<uint32_t> jl2(nt), cst2((size_t)nt * KW), fh2((size_t)nt * KW * NW);
+      for (uint32_t t = 0; t < nt; ++t) {
+        const uint32_t o = ord[t];
+        jl2[t] = h.jl[joff + o];
+        std::copy_n(h.cst.begin() + (size_t)(joff + o) * KW, KW, cst2.begin() + (size_t)t * KW);
+        if (NW)
+          std::copy_n(h.fh.begin() + (size_t)(joff + o) * KW * NW, (size_t)KW * NW,
+                      fh2.begin() + (size_t)t * KW * NW);
+      }
+      std::copy(jl2.begin(), jl2.end(), h.jl.begin() + joff);
+      std::copy(cst2.begin(), cst2.end(), h.cst.begin() + (size_t)joff * KW);
+      if (NW) std::copy(fh2.begin(), fh2.end(), h.fh.begin() + (size_t)joff * KW * NW);
+    }
     h.comp[q] = make_uint2(joff, (uint32_t)h.jl.size() - joff);
     for (uint32_t x : used) jof[x] = kN;
   }
