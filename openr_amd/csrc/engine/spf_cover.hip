@@ -691,6 +691,37 @@ __global__ void __launch_bounds__(512) cover_delta_kernel(DevGraph g, CoverGraph
   }
 }
 
+// Rows of the seeds whose next-hop masks the Dial kept: their full cover
+// columns back into LDS, then write_row_nhw (dist + next-hop rows, digest).
+__global__ void __launch_bounds__(512) seed_rows_kernel(DevGraph g, CoverGraph C,
+                                                        const uint32_t* roots, uint32_t n,
+                                                        const uint32_t* dfull, const uint32_t* nhm,
+                                                        uint32_t NW, uint32_t* dist,
+                                                        const uint32_t* rowpos, uint32_t* nh,
+                                                        ospf_digest* digest, uint32_t* err) {
+  extern __shared__ uint32_t s_D[];  // [nS] columns, then [ctr words] transit bits
+  __shared__ unsigned long long s_acc[3];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t nS = C.nS, V = g.V;
+  uint32_t* s_tr = s_D + nS;
+  for (uint32_t x = tid; x < (nS + 31u) / 32u; x += kBlock) s_tr[x] = C.ctr[x];
+  for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
+    const uint32_t rn = roots[k];
+    const uint32_t r = rn < V ? C.cix[rn] : kInf;
+    if (r >= nS) {
+      if (tid == 0) atomicOr(err, 64u);
+      continue;
+    }
+    const uint32_t* src = dfull + (size_t)k * nS;
+    for (uint32_t x = tid; x < nS; x += kBlock) s_D[x] = src[x];
+    if (tid < 3) s_acc[tid] = 0ull;
+    __syncthreads();
+    write_row_nhw(g, C, dist + (size_t)rowpos[k] * V, nh + (size_t)k * V * NW, s_D, s_tr, r, rn,
+                  nhm + (size_t)k * nS * NW, NW, digest ? digest + k : nullptr, s_acc, wave, lane);
+    __syncthreads();
+  }
+}
+
 // Closure rows with next hops (load mode + masks) in a kernel of their own:
 // the Dial kernel's register budget (its widest path) capped it at two
 // 512-thread roots per CU; here a root gets 1,024 threads at <= 64 VGPRs, two
@@ -812,7 +843,10 @@ __global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C
       }
     }
     const uint32_t rp = a.rowpos ? a.rowpos[i] : i;
-    if (cmk && rp != kInf)
+    if (cmk && a.dfull) {  // the rows follow on another stream (launch_seed_rows)
+      uint32_t* dst = a.dfull + (size_t)np * nS;
+      for (uint32_t x = tid; x < nS; x += kBlock) dst[x] = s_D[x];
+    } else if (cmk && rp != kInf)
       write_row_nhw(g, C, a.dist + (size_t)rp * V, a.nh + (size_t)np * V * a.NW, s_D, s_tr, r, rn,
                     cmk, a.NW, a.digest ? a.digest + np : nullptr, s_acc, wave, lane);
     else if (rp != kInf)
@@ -937,6 +971,25 @@ __global__ void __launch_bounds__(256) closure_kernel(ClosurePlan p) {
     if (ok && out[f] != kInf) p.dc[(size_t)out[f] * p.nS + v] = acc[f] >= kClInf ? kInf : acc[f];
 }
 }  // namespace
+
+hipError_t launch_seed_rows(const DevGraph& g, const CoverGraph& C, const uint32_t* roots,
+                            uint32_t n, const uint32_t* dfull, const uint32_t* nhm, uint32_t NW,
+                            uint32_t* dist, const uint32_t* rowpos, uint32_t* nh,
+                            ospf_digest* digest, uint32_t* err, uint32_t n_cu, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (!roots || !dfull || !nhm || !dist || !rowpos || !nh || NW == 0 || NW > kSeedMaxNW)
+    return hipErrorInvalidValue;
+  const size_t lds = ((size_t)C.nS + (C.nS + 31u) / 32u) * 4u;
+  if (lds > 48 * 1024) {
+    const hipError_t e = hipFuncSetAttribute((const void*)seed_rows_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  const uint32_t grid = std::min<uint32_t>(n, 2u * n_cu);
+  hipLaunchKernelGGL(seed_rows_kernel, dim3(grid), dim3(kBlock), lds, s, g, C, roots, n, dfull, nhm,
+                     NW, dist, rowpos, nh, digest, err);
+  return hipGetLastError();
+}
 
 hipError_t launch_closure(const ClosurePlan& p, uint32_t KW, hipStream_t s) {
   if (p.ncomp == 0) return hipSuccess;

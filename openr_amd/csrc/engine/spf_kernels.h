@@ -330,7 +330,17 @@ struct CoverArgs {
   // (zeroed by the caller) into digest + nhpos[i]
   const uint32_t* nhpos = nullptr;
   uint32_t* nhm = nullptr;
+  // with nhpos: the seeds' full cover columns out at dfull + nhpos[i] * nS
+  // and their rows left to launch_seed_rows (another stream)
+  uint32_t* dfull = nullptr;
 };
+// The rows of the seeds whose masks the Dial kept (dfull, nhm from
+// cover_spf_kernel): dist + next-hop rows + digests, root k of roots[] at
+// dist + rowpos[k] * V, nh + k * V * NW, digest + k.
+hipError_t launch_seed_rows(const DevGraph& g, const CoverGraph& C, const uint32_t* roots,
+                            uint32_t n, const uint32_t* dfull, const uint32_t* nhm, uint32_t NW,
+                            uint32_t* dist, const uint32_t* rowpos, uint32_t* nh,
+                            ospf_digest* digest, uint32_t* err, uint32_t n_cu, hipStream_t s);
 constexpr uint32_t kSeedMaxNW = 64;
 hipError_t launch_cover_spf(const DevGraph& g, const CoverGraph& C, const CoverArgs& a,
                             uint32_t n_cu, hipStream_t s);

@@ -1486,6 +1486,7 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     fprintf(stderr, "plan_wcover: cover %u seeds %zu comps %zu closure roots %zu -> %s (%s)\n", nA,
             c->cl_seed.size(), c->cl_comp_off.size() - 1, clos.size(), closure ? "closure" : "dial",
             c->err.c_str());
+  int seed_rows_ev = -1;  // the seeds' rows, when on a stream of their own
   if (closure) {
     const uint32_t nS = (uint32_t)c->h_ccv.size(), nsd = (uint32_t)seeds.size();
     const uint32_t ncl = (uint32_t)clos.size();
@@ -1534,14 +1535,23 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
           own(s, clos[j], cl_dig0 + j, slab + (size_t)clos_rp[j] * V, cnh + (size_t)j * V * NW, NW);
     }
     // next hops of the part's seeds out of their Dial
-    uint32_t *d_snp = nullptr, *snm = nullptr, *snh = nullptr;
+    uint32_t *d_snp = nullptr, *snm = nullptr, *snh = nullptr, *sdf = nullptr, *d_sroots = nullptr,
+             *d_srp2 = nullptr;
     ospf_digest* sdg = nullptr;
+    // the seeds' rows on a stream of their own, beside the closure and its
+    // rows (OSPF_SEED_ROWS_INLINE: inside the Dial's launch)
+    const bool seed_side = nsn && !getenv("OSPF_SEED_ROWS_INLINE");
     if (nsn) {
-      std::vector<uint32_t> snp(nsd, kNone), at(V, kNone);
-      for (uint32_t k = 0; k < nsn; ++k) at[sd_nh[k]] = k;
+      std::vector<uint32_t> snp(nsd, kNone), at(V, kNone), srp2(nsn);
+      for (uint32_t k = 0; k < nsn; ++k) {
+        at[sd_nh[k]] = k;
+        srp2[k] = pos[sd_nh[k]];
+      }
       for (uint32_t j = 0; j < nsd; ++j) snp[j] = at[seeds[j]];
       if ((rc = upload(s, &d_snp, snp)) || (rc = dalloc(s, &snm, (size_t)nsn * nS * NWs)) ||
-          (rc = dalloc(s, &snh, (size_t)nsn * V * NWs)))
+          (rc = dalloc(s, &snh, (size_t)nsn * V * NWs)) ||
+          (seed_side && ((rc = dalloc(s, &sdf, (size_t)nsn * nS)) || (rc = upload(s, &d_sroots, sd_nh)) ||
+                         (rc = upload(s, &d_srp2, srp2)))))
         return rc;
       sdg = s->dig_all + sn_dig0;
       for (uint32_t k = 0; k < nsn; ++k)
@@ -1560,7 +1570,8 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       u.comp = (uint64_t)nsd * 4ull * V + scan_bytes(c, true) +
                (uint64_t)nsn * 4ull * NWs * (V + 2ull * nS);
       u.fn = [=](hipStream_t strm) {
-        if (sdg && ospf::zero_async(sdg, (size_t)nsn * sizeof(ospf_digest), strm) != hipSuccess)
+        if (sdg && !seed_side &&
+            ospf::zero_async(sdg, (size_t)nsn * sizeof(ospf_digest), strm) != hipSuccess)
           return ospf_int::fail(c, OSPF_E_DEVICE, "zero seed digests");
         ospf::CoverArgs a{};
         a.roots = d_sd;
@@ -1575,11 +1586,42 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
           a.nh = snh;
           a.NW = NWs;
           a.digest = sdg;
+          a.dfull = sdf;  // null: rows inside this launch
         }
         const hipError_t e = ospf::launch_cover_spf(c->g, c->cover, a, (uint32_t)c->n_cu, strm);
         return e == hipSuccess ? OSPF_OK : ospf_int::hip_fail(c, e, "launch_cover_spf");
       };
       s->step_comp += u.comp;
+      if (seed_side) {
+        u.record = new_event(s);
+        if (u.record < 0) return u.record;
+      }
+      s->units.push_back(std::move(u));
+    }
+    if (seed_side) {  // the seeds' rows beside the closure
+      const int ev_seeds = s->units.back().record;
+      ospf_sweep::Unit u;
+      u.name = "seed_rows";
+      u.kernel = "seed_rows_kernel (the seeds' dist + next-hop rows and digests from their columns "
+                 "and masks)";
+      const int st = new_stream(s);
+      if (st < 0) return st;
+      u.stream = st;
+      u.wait = {ev_seeds};
+      seed_rows_ev = new_event(s);
+      if (seed_rows_ev < 0) return seed_rows_ev;
+      u.record = seed_rows_ev;
+      u.n_roots = nsn;
+      u.W = NWs;
+      u.comp = (uint64_t)nsn * 4ull * V * (1 + NWs);
+      s->units.back().comp -= u.comp;  // counted once
+      u.fn = [=](hipStream_t strm) {
+        if (sdg && ospf::zero_async(sdg, (size_t)nsn * sizeof(ospf_digest), strm) != hipSuccess)
+          return ospf_int::fail(c, OSPF_E_DEVICE, "zero seed digests");
+        const hipError_t e = ospf::launch_seed_rows(c->g, c->cover, d_sroots, nsn, sdf, snm, NWs, slab,
+                                                    d_srp2, snh, sdg, c->d_err, (uint32_t)c->n_cu, strm);
+        return e == hipSuccess ? OSPF_OK : ospf_int::hip_fail(c, e, "launch_seed_rows");
+      };
       s->units.push_back(std::move(u));
     }
     {
@@ -1758,9 +1800,11 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       if (st < 0) return st;
       u.stream = st;
       u.wait = {ev_a};
+      if (seed_rows_ev >= 0) u.wait.push_back(seed_rows_ev);  // may read a seed's row
       s->units.push_back(std::move(u));
     } else {
       u.stream = 0;
+      if (seed_rows_ev >= 0) u.wait.push_back(seed_rows_ev);
       narrow.push_back(std::move(u));
     }
   }
@@ -1779,6 +1823,14 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     u.comp = (uint64_t)nL * 8ull * V +
              (uint64_t)(cl.size() - std::min(cl.size(), (size_t)nL)) * 4ull * V;
     uint32_t* ldist = slab + (size_t)nA * V;
+    if (seed_rows_ev >= 0) {  // a leaf next to a seed reads the seed's row
+      std::vector<uint8_t> is_sn(V, 0);
+      for (uint32_t r : sd_nh) is_sn[r] = 1;
+      bool near = false;
+      for (uint32_t r : need_l)
+        for (uint32_t k = (*f.dn_off)[r]; k < (*f.dn_off)[r + 1] && !near; ++k) near = is_sn[(*f.dn)[k]] != 0;
+      if (near) u.wait.push_back(seed_rows_ev);
+    }
     u.fn = [=](hipStream_t strm) {
       if (!nL) return OSPF_OK;
       return ospf_wderive_dev(c, d_l, nL, 0, kmax, slab, V, d_pos, ldist, lnh, dg, strm);
