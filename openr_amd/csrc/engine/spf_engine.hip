@@ -435,6 +435,7 @@ int run_wdial(ospf_ctx* c, const ospf_batch* b, bool hop, hipStream_t s) {
   a.ngroups = ngroups;
   a.pk_bits = pk_bits;
   a.pk = pk_bits ? (uint32_t*)(sp + sz_lists + sz_dist + sz_nh) : nullptr;
+  a.wg_scope = getenv("OSPF_WD_WGSCOPE") ? 1u : 0u;
   HIPCHK(c, hipSetDevice(c->device));
   hipError_t e = ospf::launch_wdial(c->g, a, s);
   if (e != hipSuccess) return hip_fail(c, e, "launch_wdial");

@@ -142,6 +142,7 @@ struct WDialArgs {
   uint32_t ngroups;
   uint32_t pk_bits;         // 0, or 8 / 16: packed (dist << K | next hops) state
   uint32_t* pk;             // [ngroups][V] packed words (pk_bits != 0)
+  uint32_t wg_scope = 0;    // 1: workgroup-scope state atomics (a run is one workgroup's)
 };
 hipError_t launch_wdial(const DevGraph& g, const WDialArgs& a, hipStream_t s);
 

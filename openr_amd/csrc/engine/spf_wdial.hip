@@ -71,6 +71,16 @@ __device__ __forceinline__ uint32_t ld2(const uint32_t* p) {
 __device__ __forceinline__ void or2(uint32_t* p, uint32_t v) {
   __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// a run's state is touched by its own workgroup only: with `wg` (knob
+// OSPF_WD_WGSCOPE) the state atomics are workgroup-scope
+__device__ __forceinline__ void or2s(uint32_t* p, uint32_t v, bool wg) {
+  if (wg) __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  else __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t amins(uint32_t* p, uint32_t v, bool wg) {
+  return wg ? __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+            : atomicMin(p, v);
+}
 __device__ __forceinline__ uint32_t wmin(uint32_t x) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) x = min(x, (uint32_t)__shfl_xor(x, o, kWave));
@@ -250,7 +260,7 @@ struct GRun {
         }
 #pragma unroll
         for (uint32_t u = 0; u < kUnroll; ++u)
-          if (v[u]) or2(pk + x[u], v[u]);
+          if (v[u]) or2s(pk + x[u], v[u], a.wg_scope);
       } else if (W == 1) {
         uint32_t v[kUnroll];
 #pragma unroll
@@ -262,7 +272,7 @@ struct GRun {
         }
 #pragma unroll
         for (uint32_t u = 0; u < kUnroll; ++u)
-          if (v[u]) or2(nh + x[u], v[u]);
+          if (v[u]) or2s(nh + x[u], v[u], a.wg_scope);
       } else {
 #pragma unroll
         for (uint32_t u = 0; u < kUnroll; ++u) {
@@ -270,7 +280,7 @@ struct GRun {
           uint32_t* row = nh + (size_t)x[u] * W;
           if (cx[u] == root) {
             const uint32_t b = lbound(nbr, nbr_n, x[u]);
-            or2(row + (b >> 5), 1u << (b & 31u));
+            or2s(row + (b >> 5), 1u << (b & 31u), a.wg_scope);
           } else if (transit(cx[u])) {
             const uint32_t* src = nh + (size_t)cx[u] * W;
             for (uint32_t w0 = 0; w0 < W; w0 += 8) {  // 8 loads in flight, then the ORs
@@ -279,7 +289,7 @@ struct GRun {
               for (uint32_t k = 0; k < 8; ++k) v[k] = w0 + k < W ? ld2(src + w0 + k) : 0u;
 #pragma unroll
               for (uint32_t k = 0; k < 8; ++k)
-                if (v[k]) or2(row + w0 + k, v[k]);
+                if (v[k]) or2s(row + w0 + k, v[k], a.wg_scope);
             }
           }
         }
@@ -296,9 +306,9 @@ struct GRun {
             ctl->overflow = 1u;
             continue;
           }
-          old[u] = field(atomicMin(&pk[cx[u]], nd[u] << K));
+          old[u] = field(amins(&pk[cx[u]], nd[u] << K, a.wg_scope));
         } else {
-          old[u] = atomicMin(&dist[cx[u]], nd[u]);
+          old[u] = amins(&dist[cx[u]], nd[u], a.wg_scope);
         }
       }
 #pragma unroll
