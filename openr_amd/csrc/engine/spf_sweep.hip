@@ -1487,6 +1487,8 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
             c->cl_seed.size(), c->cl_comp_off.size() - 1, clos.size(), closure ? "closure" : "dial",
             c->err.c_str());
   int seed_rows_ev = -1;  // the seeds' rows, when on a stream of their own
+  std::vector<uint32_t> row_chunk(V, kNone);  // closure root -> its rows chunk
+  std::vector<int> rows_ev;                   // events of the rows chunks
   if (closure) {
     const uint32_t nS = (uint32_t)c->h_ccv.size(), nsd = (uint32_t)seeds.size();
     const uint32_t ncl = (uint32_t)clos.size();
@@ -1642,32 +1644,45 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       s->step_comp += u.comp;
       s->units.push_back(std::move(u));
     }
-    {
+    // the closure roots' rows in K chunks (in closure order: a fabric's pods),
+    // each recording an event, so the leaf rows of the chunks done can run
+    // beside the next chunk (OSPF_WCOVER_NOSTAGE: one launch)
+    const uint32_t K = (nL && ncl >= 64 && !getenv("OSPF_WCOVER_NOSTAGE")) ? 4u : 1u;
+    for (uint32_t k = 0; k < K; ++k) {
+      const uint32_t lo = (uint32_t)((uint64_t)ncl * k / K), hi = (uint32_t)((uint64_t)ncl * (k + 1) / K);
+      for (uint32_t j = lo; j < hi; ++j) row_chunk[clos[j]] = k;
       ospf_sweep::Unit u;
-      u.name = "cover_rows";
-      u.kernel = cl_nh ? "cover_spf_kernel (full dist + next-hop rows and digests of the "
-                         "closure's roots: cover columns given, leaves by their last hop)"
+      u.name = K > 1 ? "cover_rows_s" + std::to_string(k) : std::string("cover_rows");
+      u.kernel = cl_nh ? "cover_rows_kernel (full dist + next-hop rows and digests of the closure's "
+                         "roots: cover columns given, leaves by their last hop)"
                        : "cover_spf_kernel (full rows of the closure's roots: cover columns "
                          "given, leaves by their last hop)";
       u.stream = 0;
-      u.record = ev_a;
-      u.n_roots = ncl;
+      if (k + 1 == K) {
+        u.record = ev_a;
+      } else {
+        u.record = new_event(s);
+        if (u.record < 0) return u.record;
+      }
+      rows_ev.push_back(u.record);
+      u.n_roots = hi - lo;
       u.W = NW;
-      u.comp = (uint64_t)ncl * 4ull * V * (1 + NW);
+      u.comp = (uint64_t)(hi - lo) * 4ull * V * (1 + NW);
       u.fn = [=](hipStream_t strm) {
-        if (cdg && ospf::zero_async(cdg, (size_t)ncl * sizeof(ospf_digest), strm) != hipSuccess)
+        if (hi == lo) return OSPF_OK;
+        if (cdg && ospf::zero_async(cdg + lo, (size_t)(hi - lo) * sizeof(ospf_digest), strm) != hipSuccess)
           return ospf_int::fail(c, OSPF_E_DEVICE, "zero closure digests");
         ospf::CoverArgs a{};
-        a.roots = d_cl;
-        a.n = ncl;
+        a.roots = d_cl + lo;
+        a.n = hi - lo;
         a.dist = slab;
         a.err = c->d_err;
-        a.rowpos = d_crp;
-        a.dload = dc;
-        a.nhload = dcm;
-        a.nh = cnh;
+        a.rowpos = d_crp + lo;
+        a.dload = dc + (size_t)lo * nS;
+        a.nhload = dcm ? dcm + (size_t)lo * nS * NW : nullptr;
+        a.nh = cnh ? cnh + (size_t)lo * V * NW : nullptr;
         a.NW = NW;
-        a.digest = cdg;
+        a.digest = cdg ? cdg + lo : nullptr;
         const hipError_t e = ospf::launch_cover_spf(c->g, c->cover, a, (uint32_t)c->n_cu, strm);
         return e == hipSuccess ? OSPF_OK : ospf_int::hip_fail(c, e, "launch_cover_spf");
       };
@@ -1809,6 +1824,56 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     }
   }
   // (B) leaves, then the narrow cover classes (they read leaf rows)
+  if (rows_ev.size() > 1 && nL) {  // leaf chunks beside the closure rows' chunks
+    ospf_digest* dg = s->dig_all + slot;
+    for (uint32_t j = 0; j < own_l.size(); ++j)
+      own(s, own_l[j], slot + j, slab + (size_t)(nA + j) * V, lnh + (size_t)j * V, 1);
+    slot += nL;
+    std::vector<uint8_t> is_sn(V, 0);
+    for (uint32_t r : sd_nh) is_sn[r] = 1;
+    const int lst = new_stream(s);
+    if (lst < 0) return lst;
+    const uint32_t KL = 4;
+    int last = -1;
+    for (uint32_t k = 0; k < KL; ++k) {
+      const uint32_t lo = (uint32_t)((uint64_t)nL * k / KL), hi = (uint32_t)((uint64_t)nL * (k + 1) / KL);
+      uint32_t dep = 0;
+      bool seedn = false;
+      for (uint32_t j = lo; j < hi; ++j)
+        for (uint32_t e = (*f.dn_off)[need_l[j]]; e < (*f.dn_off)[need_l[j] + 1]; ++e) {
+          const uint32_t x = (*f.dn)[e];
+          if (row_chunk[x] != kNone) dep = std::max(dep, row_chunk[x]);
+          else if (is_sn[x]) seedn = true;
+        }
+      ospf_sweep::Unit u;
+      u.name = "wderive_s" + std::to_string(k);
+      u.kernel = "ospf_wderive_dev (wderive_kernel: leaf rows from the cover rows, a chunk)";
+      u.stream = lst;
+      u.wait = {rows_ev[dep]};
+      if (seedn && seed_rows_ev >= 0) u.wait.push_back(seed_rows_ev);
+      u.record = new_event(s);
+      if (u.record < 0) return u.record;
+      last = u.record;
+      u.n_roots = hi - lo;
+      u.W = 1;
+      u.comp = (uint64_t)(hi - lo) * 8ull * V;
+      uint32_t* ldist = slab + (size_t)(nA + lo) * V;
+      uint32_t* lnh_k = lnh + (size_t)lo * V;
+      const uint32_t* d_lk = d_l + lo;
+      ospf_digest* dgk = dg + lo;
+      u.fn = [=](hipStream_t strm) {
+        if (hi == lo) return OSPF_OK;
+        return ospf_wderive_dev(c, d_lk, hi - lo, 0, kmax, slab, V, d_pos, ldist, lnh_k, dgk, strm);
+      };
+      s->step_comp += u.comp;
+      s->units.push_back(std::move(u));
+    }
+    for (auto& u : narrow) {
+      u.wait.push_back(last);
+      s->units.push_back(std::move(u));
+    }
+    return OSPF_OK;
+  }
   {
     ospf_digest* dg = s->dig_all + slot;
     for (uint32_t j = 0; j < own_l.size(); ++j)
