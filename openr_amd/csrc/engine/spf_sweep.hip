@@ -1644,10 +1644,12 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       s->step_comp += u.comp;
       s->units.push_back(std::move(u));
     }
-    // the closure roots' rows in K chunks (in closure order: a fabric's pods),
-    // each recording an event, so the leaf rows of the chunks done can run
-    // beside the next chunk (OSPF_WCOVER_NOSTAGE: one launch)
-    const uint32_t K = (nL && ncl >= 64 && !getenv("OSPF_WCOVER_NOSTAGE")) ? 4u : 1u;
+    // opt-in (OSPF_WCOVER_STAGE): the closure roots' rows in K chunks (in
+    // closure order: a fabric's pods), each recording an event, so the leaf
+    // rows of the chunks done run beside the next chunk. Measured slower on
+    // the weighted F100k (58.5 vs 54.9 ms, a22): the bandwidth-bound leaf
+    // launch takes the CUs the latency-bound rows launch needs.
+    const uint32_t K = (nL && ncl >= 64 && getenv("OSPF_WCOVER_STAGE")) ? 4u : 1u;
     for (uint32_t k = 0; k < K; ++k) {
       const uint32_t lo = (uint32_t)((uint64_t)ncl * k / K), hi = (uint32_t)((uint64_t)ncl * (k + 1) / K);
       for (uint32_t j = lo; j < hi; ++j) row_chunk[clos[j]] = k;
