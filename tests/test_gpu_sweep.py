@@ -133,14 +133,17 @@ def test_sweep_weighted_fabric_cover_path():
         eng.close()
 
 
+@pytest.mark.parametrize("stage", [False, True])
 @pytest.mark.parametrize("drain", [0.0, 0.08])
-def test_sweep_weighted_fabric_closure(drain):
+def test_sweep_weighted_fabric_closure(drain, stage, monkeypatch):
     """A weighted fabric whose cover splits into seeds (the spines) and small
     components (a pod's fabric switches): the closure path -- the seeds' Dial,
     closure_kernel's cover columns, then the full rows -- == the batch path bit
     for bit, with drained (overloaded) switches and down links."""
     # 40 pods: a spine has 40 > 32 neighbours, so it is no leaf candidate and
     # stays in the cover (as on F100k)
+    if stage:  # closure rows in chunks, leaf chunks on a second stream (opt-in)
+        monkeypatch.setenv("OSPF_WCOVER_STAGE", "1")
     st = drained_fabric(40, 4, seed=5, drain=drain, down=0.03 if drain else 0.0,
                         weighted_seed=11, ssw_per_plane=4)
     _, _, eng = engine_for(st)
