@@ -7,6 +7,8 @@
 #include <set>
 #include <algorithm>
 #include <unordered_set>
+#include <system_error>
+#include <thread>
 #include <functional>
 #include <map>
 #include <stdexcept>
@@ -209,10 +211,15 @@ void LinkState::clearMemo() {
   const long r = (long)rows.size();
   auto cnt = reapRefs_;
   cnt->fetch_add(r);
-  std::thread([dead, cnt, r] {
+  try {
+    std::thread([dead, cnt, r] {
+      delete dead;
+      cnt->fetch_sub(r);
+    }).detach();
+  } catch (const std::system_error&) {  // no thread to spare: free here
     delete dead;
     cnt->fetch_sub(r);
-  }).detach();
+  }
 }
 
 void LinkState::invalidate() {
