@@ -31,6 +31,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -135,6 +136,60 @@ def host_threads() -> int:
     n = len(os.sched_getaffinity(0))
     omp = os.environ.get("OMP_NUM_THREADS")
     return max(1, min(n, int(omp))) if omp and omp.isdigit() else n
+
+
+class BusySampler:
+    """GPU activity during the timed region, independent of our own clocks:
+    the amdgpu driver's gpu_busy_percent of this device (sysfs, by its PCI
+    address) sampled every 5 ms on a host thread."""
+
+    def __init__(self, dev_index: int):
+        self.path = None
+        self.vals = []
+        try:
+            p = torch.cuda.get_device_properties(dev_index)
+            addr = f"{getattr(p, 'pci_domain_id', 0):04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+            cand = f"/sys/bus/pci/devices/{addr}/gpu_busy_percent"
+            if os.path.exists(cand):
+                self.path = cand
+        except Exception:  # noqa: BLE001 -- evidence only; absent on some hosts
+            self.path = None
+        self._stop = threading.Event()
+        self._t = None
+
+    def _run(self):
+        while not self._stop.is_set():
+            try:
+                with open(self.path) as f:
+                    self.vals.append(int(f.read().strip()))
+            except (OSError, ValueError):
+                return
+            self._stop.wait(0.005)
+
+    def __enter__(self):
+        if self.path:
+            self._t = threading.Thread(target=self._run, daemon=True)
+            self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        if self._t:
+            self._t.join()
+        BUSY["timed"] = self.summary()
+
+    def summary(self):
+        if not self.vals:
+            return {"source": self.path, "samples": 0,
+                    "note": "no gpu_busy_percent file for this device"}
+        v = np.asarray(self.vals, dtype=np.float64)
+        return {"source": self.path, "samples": int(v.size), "mean_pct": round(float(v.mean()), 1),
+                "min_pct": int(v.min()), "max_pct": int(v.max()),
+                "note": "amdgpu gpu_busy_percent of this device sampled every 5 ms over the timed "
+                        "loop (the driver's counter, not our HIP events)"}
+
+
+BUSY = {}
 
 
 def main():
@@ -329,13 +384,14 @@ def main():
     if dist_on:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i, True)
-    torch.cuda.synchronize()
-    if dist_on:
-        torch.distributed.barrier()
-    dt = time.perf_counter() - t_start
+    with BusySampler(torch.cuda.current_device()):
+        t_start = time.perf_counter()
+        for i in range(args.steps):
+            step(args.warmup + i, True)
+        torch.cuda.synchronize()
+        if dist_on:
+            torch.distributed.barrier()
+        dt = time.perf_counter() - t_start
     eng.sync(main_s.cuda_stream)  # raises if the device error word was set
     if dist_on:
         t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
@@ -483,13 +539,14 @@ def sweep_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, 
     if dist_on:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if dist_on:
-        torch.distributed.barrier()
-    dt = time.perf_counter() - t_start
+    with BusySampler(torch.cuda.current_device()):
+        t_start = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        if dist_on:
+            torch.distributed.barrier()
+        dt = time.perf_counter() - t_start
     eng.sync(main_s.cuda_stream)
     if dist_on:
         t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
@@ -719,6 +776,7 @@ def report(args, stream, names, csr, step_digest, dt, roots_total, E, desc, n_ro
                                (f", all_gather of 24-B digests ({'RCCL' if backend == 'nccl' else backend})"
                                 if dist_on else "")},
             "roofline": roofline, "cpu_baseline": cpu, "parity_vs_cpu_sample": parity,
+            "gpu_busy": BUSY.get("timed"),
         }
         if dist_on:
             line["gathered_roots"] = len(step_digest)

@@ -691,6 +691,164 @@ __global__ void __launch_bounds__(512) cover_delta_kernel(DevGraph g, CoverGraph
   }
 }
 
+// Closure rows by node tiles: block = (chunk of kLtTiles node tiles, chunk of
+// kLtRoots roots). A tile is <= 256 consecutive nodes whose own cover indices
+// (cover nodes) and in-links' cover indices (leaves) form a union U of <= 256
+// slots; thread = node, its entries (slot | 0x100 for its own cover column,
+// else slot | metric << 16) in registers for every root of the chunk. Per
+// root the values and masks of U are staged in LDS (loaded one root ahead),
+// the node's dist and next-hop words computed (a leaf: LinkState.cpp:885-901
+// over its tight last hops; the root as a last hop gives the leaf's own bit)
+// and both rows stored as contiguous runs; per-root digests summed in LDS over
+// the block's tiles, one global add each at the end.
+template <int NW>
+__global__ void __launch_bounds__(256) closure_tile_rows_kernel(DevGraph g, CoverGraph C,
+                                                                ClosureRowsPlan p) {
+  __shared__ uint32_t s_val[kLtRoots][kLtU], s_u[kLtU], s_tr[kLtU];
+  __shared__ uint32_t s_m[kLtRoots][kLtU * NW];
+  __shared__ uint32_t s_st[2][kLtNodes * NW];
+  __shared__ unsigned long long s_acc[kLtRoots][3];
+  const uint32_t tid = threadIdx.x, V = g.V, lane = tid & 63u;
+  const uint32_t nch = (p.ntiles + kLtTiles - 1) / kLtTiles;
+  const uint32_t tch = blockIdx.x % nch, rch = blockIdx.x / nch;
+  const uint32_t i0 = rch * kLtRoots, i1 = min(p.nroots, i0 + kLtRoots), nr = i1 > i0 ? i1 - i0 : 0u;
+  for (uint32_t x = tid; x < kLtRoots * 3u; x += 256u) (&s_acc[0][0])[x] = 0ull;
+  const uint32_t ta = tch * kLtTiles, tb = min(p.ntiles, ta + kLtTiles);
+  uint32_t buf = 0;
+  for (uint32_t t = ta; t < tb; ++t) {
+    const uint4 tl = p.tile[t];  // {first node, nodes, first U entry, U size}
+    const bool ok = tid < tl.y;
+    const uint32_t v = tl.x + (ok ? tid : 0u);
+    uint32_t e[kLtE];
+    {
+      const uint4* src = reinterpret_cast<const uint4*>(p.tle + (size_t)v * kLtE);
+#pragma unroll
+      for (int q = 0; q < (int)kLtE / 4; ++q) {
+        const uint4 x = src[q];
+        e[4 * q] = ok ? x.x : kInf;
+        e[4 * q + 1] = ok ? x.y : kInf;
+        e[4 * q + 2] = ok ? x.z : kInf;
+        e[4 * q + 3] = ok ? x.w : kInf;
+      }
+    }
+    // every root's slot values and masks of the tile, all loads in flight
+    // (<= kLtRoots x kLtU / 256 per thread)
+    constexpr uint32_t kPer = kLtRoots * kLtU / 256u;
+    uint32_t lv[kPer], lm[kPer][NW];
+#pragma unroll
+    for (uint32_t q = 0; q < kPer; ++q) {
+      const uint32_t x = tid + q * 256u, j = x / kLtU, k = x % kLtU;
+      lv[q] = kInf;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) lm[q][w] = 0u;
+      if (k < tl.w && i0 + j < i1) {
+        const size_t b = (size_t)(i0 + j) * p.nS + p.tu[tl.z + k];
+        lv[q] = p.dc[b];
+#pragma unroll
+        for (int w = 0; w < NW; ++w) lm[q][w] = p.dcm[b * NW + w];
+      }
+    }
+    __syncthreads();  // the previous tile's slots are consumed
+    if (tid < tl.w) {
+      const uint32_t ci = p.tu[tl.z + tid];
+      s_u[tid] = ci;
+      s_tr[tid] = (C.ctr[ci >> 5] >> (ci & 31u)) & 1u;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kPer; ++q) {
+      const uint32_t x = tid + q * 256u, j = x / kLtU, k = x % kLtU;
+      s_val[j][k] = lv[q];
+#pragma unroll
+      for (int w = 0; w < NW; ++w) s_m[j][k * NW + w] = lm[q][w];
+    }
+    __syncthreads();
+    for (uint32_t i = i0; i < i1; ++i, buf ^= 1u) {
+      const uint32_t r = p.rcov[i], rn = p.roots[i];
+      const uint32_t* sv = s_val[i - i0];
+      const uint32_t* sm = s_m[i - i0];
+      uint32_t out = kInf, m[NW];
+#pragma unroll
+      for (int w = 0; w < NW; ++w) m[w] = 0u;
+      if ((e[0] & 0x100u) && e[0] != kInf) {  // a cover node: its own column
+        const uint32_t sl = e[0] & 0xFFu;
+        out = sv[sl];
+        if (v != rn && out != kInf) {
+#pragma unroll
+          for (int w = 0; w < NW; ++w) m[w] = sm[sl * NW + w];
+        }
+      } else {
+        auto usable = [&](uint32_t sl) { return s_tr[sl] != 0u || s_u[sl] == r; };
+#pragma unroll
+        for (int q = 0; q < (int)kLtE; ++q) {
+          if (e[q] == kInf) continue;
+          const uint32_t sl = e[q] & 0xFFu, x = sv[sl];
+          if (x != kInf && usable(sl)) out = min(out, x + (e[q] >> 16));
+        }
+        if (out != kInf) {
+#pragma unroll
+          for (int q = 0; q < (int)kLtE; ++q) {
+            if (e[q] == kInf) continue;
+            const uint32_t sl = e[q] & 0xFFu, x = sv[sl];
+            if (x == kInf || !usable(sl) || x + (e[q] >> 16) != out) continue;
+            if (s_u[sl] == r) {  // a neighbour of the root: its own bit
+              const uint32_t* dn = g.dn + g.dn_off[rn];
+              uint32_t lo = 0, hi = g.dn_off[rn + 1] - g.dn_off[rn];
+              while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (dn[mid] < v) lo = mid + 1;
+                else hi = mid;
+              }
+              if (lo < 32u * NW) m[lo >> 5] |= 1u << (lo & 31u);
+            } else {
+#pragma unroll
+              for (int w = 0; w < NW; ++w) m[w] |= sm[sl * NW + w];
+            }
+          }
+        }
+      }
+      uint64_t h = 0, sum = 0;
+      uint32_t reach = 0;
+      if (ok) {
+        __builtin_nontemporal_store(out, p.dist + (size_t)p.rowpos[i] * V + v);
+        if (out != kInf) {
+          reach = 1u;
+          sum = out;
+          h = g.dkey[2ull * v] * ((uint64_t)out + 1ull);
+          uint64_t ws = 0;
+#pragma unroll
+          for (int w = 0; w < NW; ++w)
+            if (m[w]) ws += digest_word_key((uint32_t)w, m[w]);
+          if (ws) h += g.dkey[2ull * v + 1] * ws;
+        }
+      }
+#pragma unroll
+      for (int w = 0; w < NW; ++w) s_st[buf][tid * NW + w] = m[w];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        h += shfl_xor64(h, o);
+        sum += shfl_xor64(sum, o);
+        reach += (uint32_t)__shfl_xor((int)reach, o, kWave);
+      }
+      if (lane == 0 && reach) {
+        atomicAdd(&s_acc[i - i0][0], (unsigned long long)reach);
+        atomicAdd(&s_acc[i - i0][1], (unsigned long long)sum);
+        atomicAdd(&s_acc[i - i0][2], (unsigned long long)h);
+      }
+      __syncthreads();
+      uint32_t* nrow = p.nh + ((size_t)i * V + tl.x) * NW;
+      for (uint32_t x = tid; x < tl.y * NW; x += 256u) __builtin_nontemporal_store(s_st[buf][x], nrow + x);
+    }
+  }
+  __syncthreads();
+  if (p.digest)
+    for (uint32_t j = tid; j < nr; j += 256u)
+      if (s_acc[j][0]) {
+        atomicAdd((unsigned long long*)&p.digest[i0 + j].reached, s_acc[j][0]);
+        atomicAdd((unsigned long long*)&p.digest[i0 + j].sum_dist, s_acc[j][1]);
+        atomicAdd((unsigned long long*)&p.digest[i0 + j].hash, s_acc[j][2]);
+      }
+}
+
 // Rows of the seeds whose next-hop masks the Dial kept: their full cover
 // columns back into LDS, then write_row_nhw (dist + next-hop rows, digest).
 __global__ void __launch_bounds__(512) seed_rows_kernel(DevGraph g, CoverGraph C,
@@ -971,6 +1129,22 @@ __global__ void __launch_bounds__(256) closure_kernel(ClosurePlan p) {
     if (ok && out[f] != kInf) p.dc[(size_t)out[f] * p.nS + v] = acc[f] >= kClInf ? kInf : acc[f];
 }
 }  // namespace
+
+hipError_t launch_closure_rows(const DevGraph& g, const CoverGraph& C, const ClosureRowsPlan& p,
+                               hipStream_t s) {
+  if (p.nroots == 0 || p.ntiles == 0) return hipSuccess;
+  if (p.NW == 0 || p.NW > kClMaxNW || !p.dc || !p.dcm || !p.dist || !p.nh || !p.tile || !p.tle ||
+      !p.tu)
+    return hipErrorInvalidValue;
+  const dim3 grid(((p.ntiles + kLtTiles - 1) / kLtTiles) * ((p.nroots + kLtRoots - 1) / kLtRoots));
+  switch (p.NW) {
+    case 1: hipLaunchKernelGGL(closure_tile_rows_kernel<1>, grid, dim3(256), 0, s, g, C, p); break;
+    case 2: hipLaunchKernelGGL(closure_tile_rows_kernel<2>, grid, dim3(256), 0, s, g, C, p); break;
+    case 3: hipLaunchKernelGGL(closure_tile_rows_kernel<3>, grid, dim3(256), 0, s, g, C, p); break;
+    default: hipLaunchKernelGGL(closure_tile_rows_kernel<4>, grid, dim3(256), 0, s, g, C, p); break;
+  }
+  return hipGetLastError();
+}
 
 hipError_t launch_seed_rows(const DevGraph& g, const CoverGraph& C, const uint32_t* roots,
                             uint32_t n, const uint32_t* dfull, const uint32_t* nhm, uint32_t NW,

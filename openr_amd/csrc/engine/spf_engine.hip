@@ -2142,6 +2142,9 @@ int ospf_cover_prepare(ospf_ctx* c, const uint8_t* leaf) {
   c->h_ccrow = crow;
   c->h_cctr = ctr;
   c->h_cedge = cedge;
+  c->h_cix = cix;
+  c->h_lrow = lrow;
+  c->h_ladj = ladj;
   cover_closure_split(c);
   if (ladj.empty()) ladj.assign(4, 0xFFFFu);
   if (cedge.empty()) {

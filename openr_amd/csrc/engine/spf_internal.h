@@ -62,6 +62,7 @@ struct ospf_ctx {
   // exists): seeds = the cover nodes of largest degree, every other cover
   // node in a component of C minus the seeds of <= kClosureMaxK nodes
   std::vector<uint32_t> h_ccv, h_ccrow, h_cctr;  // cover index -> node id, CSR, transit bits
+  std::vector<uint32_t> h_cix, h_lrow, h_ladj;   // node -> cover index / leaf word, leaf in-links
   std::vector<uint2> h_cedge;
   std::vector<uint32_t> cl_seed;               // cover indices of the seeds
   std::vector<uint32_t> cl_comp_of;            // per cover index: component, or ~0u (seed)

@@ -375,6 +375,29 @@ struct ClosurePlan {
   uint32_t* dcm = nullptr;
 };
 constexpr uint32_t kClMaxNW = 4;
+
+// Closure roots' full rows from their cover columns + masks (dc / dcm) by
+// node tiles (closure_tile_rows_kernel): tiles of <= kLtNodes consecutive
+// nodes whose own / in-link cover indices form a union U of <= kLtU slots,
+// <= kLtE entries per node, kLtTiles tiles x kLtRoots roots per block.
+constexpr uint32_t kLtNodes = 256, kLtU = 64, kLtE = 16, kLtRoots = 32, kLtTiles = 8;
+struct ClosureRowsPlan {
+  uint32_t nroots, nS, NW, ntiles;
+  const uint32_t* roots;   // [nroots] node ids
+  const uint32_t* rcov;    // [nroots] their cover indices
+  const uint32_t* rowpos;  // [nroots] dist row positions
+  const uint32_t* dc;      // [nroots][nS]
+  const uint32_t* dcm;     // [nroots][nS][NW]
+  uint32_t* dist;          // rows at dist + rowpos[i] * V
+  uint32_t* nh;            // [nroots][V][NW]
+  ospf_digest* digest;     // [nroots] (zeroed by the caller)
+  const uint4* tile;       // [ntiles] {first node, nodes, first U entry, U size}
+  const uint32_t* tle;     // [V][kLtE] slot | 0x100 (own column) or slot | metric << 16;
+                           // 0xFFFFFFFF: none
+  const uint32_t* tu;      // [U entries] cover indices
+};
+hipError_t launch_closure_rows(const DevGraph& g, const CoverGraph& C, const ClosureRowsPlan& p,
+                               hipStream_t s);
 hipError_t launch_closure(const ClosurePlan& p, uint32_t KW, hipStream_t s);
 
 // Weighted derive (spf_wderive.hip): dist + next-hop rows (one word) of n

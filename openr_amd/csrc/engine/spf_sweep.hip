@@ -1308,6 +1308,60 @@ int plan_lds(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine) {
   return OSPF_OK;
 }
 
+// Node tiles for the closure rows (launch_closure_rows): consecutive nodes, a
+// tile closed at kLtNodes nodes or when its union of cover indices (a cover
+// node's own, a leaf's in-links') would pass kLtU. False when a leaf has
+// more than kLtE in-links.
+struct NodeTiles {
+  std::vector<uint4> tile;
+  std::vector<uint32_t> le, u;
+};
+bool node_tiles(const ospf_ctx* c, NodeTiles& t) {
+  const std::vector<uint32_t>& cix = c->h_cix;
+  const uint32_t V = (uint32_t)cix.size(), nS = (uint32_t)c->h_ccv.size();
+  std::vector<uint32_t> slot(nS, kNone), ul;
+  uint32_t first = 0;
+  auto close = [&](uint32_t end) {
+    if (end == first) return;
+    t.tile.push_back(make_uint4(first, end - first, (uint32_t)t.u.size(), (uint32_t)ul.size()));
+    for (uint32_t ci : ul) {
+      t.u.push_back(ci);
+      slot[ci] = kNone;
+    }
+    ul.clear();
+    first = end;
+  };
+  t.le.assign((size_t)V * ospf::kLtE, 0xFFFFFFFFu);
+  for (uint32_t v = 0, l = 0; v < V; ++v) {
+    uint32_t ent[ospf::kLtE], ne = 0, fresh = 0;
+    if (cix[v] & 0x80000000u) {
+      for (uint32_t x = c->h_lrow[l]; x < c->h_lrow[l + 1]; ++x) {
+        const uint32_t w = c->h_ladj[x], ci = w & 0xFFFFu;
+        if (ci >= nS) continue;  // padding
+        if (ne == ospf::kLtE) return false;
+        ent[ne++] = w;
+        if (slot[ci] == kNone) ++fresh;  // (a repeat counts twice: a bound)
+      }
+      ++l;
+    } else {
+      ent[ne++] = cix[v];
+      if (slot[cix[v]] == kNone) ++fresh;
+    }
+    if (v - first == ospf::kLtNodes || ul.size() + fresh > ospf::kLtU) close(v);
+    for (uint32_t q = 0; q < ne; ++q) {
+      const uint32_t ci = ent[q] & 0xFFFFu;
+      if (slot[ci] == kNone) {
+        slot[ci] = (uint32_t)ul.size();
+        ul.push_back(ci);
+      }
+      t.le[(size_t)v * ospf::kLtE + q] =
+          (cix[v] & 0x80000000u) ? (slot[ci] | (ent[q] & 0xFFFF0000u)) : (slot[ci] | 0x100u);
+    }
+  }
+  close(V);
+  return true;
+}
+
 // WCOVER (spf_cover.hip + spf_wderive.hip): an independent set of leaves
 // (<= 32 distinct neighbours; on a fabric the racks), the cover = the rest.
 // (A) distance rows of the cover nodes the part needs by the contracted-graph
@@ -1650,12 +1704,48 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     // the weighted F100k (58.5 vs 54.9 ms, a22): the bandwidth-bound leaf
     // launch takes the CUs the latency-bound rows launch needs.
     const uint32_t K = (nL && ncl >= 64 && getenv("OSPF_WCOVER_STAGE")) ? 4u : 1u;
+    // opt-in (OSPF_COVER_ROWS_TILED): with next hops, the rows by node tiles x
+    // root chunks (closure_tile_rows_kernel) instead of a node-order pass per
+    // root; exact, but measured 2x slower on the weighted F100k (35.3 vs
+    // 16.9 ms, a27 / a28)
+    bool tiled = false;
+    ospf::ClosureRowsPlan rp{};
+    if (cl_nh && K == 1 && getenv("OSPF_COVER_ROWS_TILED")) {
+      NodeTiles nt;
+      tiled = node_tiles(c, nt) && !nt.tile.empty();
+      if (tiled) {
+        std::vector<uint32_t> rcov(ncl);
+        for (uint32_t j = 0; j < ncl; ++j) rcov[j] = c->h_cix[clos[j]];
+        uint32_t *d_rcov, *d_tle, *d_tu;
+        uint4* d_tile;
+        if ((rc = upload(s, &d_rcov, rcov)) || (rc = upload(s, &d_tile, nt.tile)) ||
+            (rc = upload(s, &d_tle, nt.le)) || (rc = upload(s, &d_tu, nt.u)))
+          return rc;
+        rp.nroots = ncl;
+        rp.nS = nS;
+        rp.NW = NW;
+        rp.ntiles = (uint32_t)nt.tile.size();
+        rp.roots = d_cl;
+        rp.rcov = d_rcov;
+        rp.rowpos = d_crp;
+        rp.dc = dc;
+        rp.dcm = dcm;
+        rp.dist = slab;
+        rp.nh = cnh;
+        rp.digest = cdg;
+        rp.tile = d_tile;
+        rp.tle = d_tle;
+        rp.tu = d_tu;
+      }
+    }
     for (uint32_t k = 0; k < K; ++k) {
       const uint32_t lo = (uint32_t)((uint64_t)ncl * k / K), hi = (uint32_t)((uint64_t)ncl * (k + 1) / K);
       for (uint32_t j = lo; j < hi; ++j) row_chunk[clos[j]] = k;
       ospf_sweep::Unit u;
       u.name = K > 1 ? "cover_rows_s" + std::to_string(k) : std::string("cover_rows");
-      u.kernel = cl_nh ? "cover_rows_kernel (full dist + next-hop rows and digests of the closure's "
+      u.kernel = tiled ? "closure_tile_rows_kernel (the closure roots' dist + next-hop rows and "
+                         "digests by node tiles: cover columns given, leaves by their last hops)"
+                 : cl_nh ? "cover_rows_kernel (full dist + next-hop rows and digests of the closure's "
                          "roots: cover columns given, leaves by their last hop)"
                        : "cover_spf_kernel (full rows of the closure's roots: cover columns "
                          "given, leaves by their last hop)";
@@ -1674,6 +1764,10 @@ int plan_wcover(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
         if (hi == lo) return OSPF_OK;
         if (cdg && ospf::zero_async(cdg + lo, (size_t)(hi - lo) * sizeof(ospf_digest), strm) != hipSuccess)
           return ospf_int::fail(c, OSPF_E_DEVICE, "zero closure digests");
+        if (tiled) {
+          const hipError_t e = ospf::launch_closure_rows(c->g, c->cover, rp, strm);
+          return e == hipSuccess ? OSPF_OK : ospf_int::hip_fail(c, e, "launch_closure_rows");
+        }
         ospf::CoverArgs a{};
         a.roots = d_cl + lo;
         a.n = hi - lo;

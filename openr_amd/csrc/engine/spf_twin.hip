@@ -41,6 +41,7 @@ constexpr uint32_t kDown = 0x80000000u;
 constexpr uint32_t kBlock = 256;
 constexpr uint32_t kWaves = kBlock / 64u;
 constexpr uint32_t kMaxK = 128;  // W <= 4 words
+constexpr uint32_t kComboC = 6;  // classes whose mask combinations are tabled
 
 __device__ __forceinline__ bool transit(const DevGraph& g, uint32_t v) {
   return !((g.nt_bits[v >> 5] >> (v & 31)) & 1u);
@@ -161,6 +162,7 @@ template <int W>
 __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, TwinArgs a) {
   __shared__ TwinTab T;
   __shared__ unsigned long long s_h;
+  __shared__ uint64_t s_wk[1u << kComboC];
   __shared__ uint32_t s_Lb[kWaves][256];  // own level bytes of each wave's tile
   extern __shared__ uint32_t s_stage[];  // [4 waves][1024 nodes][W]
   const uint32_t V = g.V, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
@@ -172,6 +174,22 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
   if (tid == 0) s_h = 0ull;
   if (!twin_setup(g, a, i, W, T)) return;
   const uint32_t K = min(T.K, (uint32_t)(32 * W)), own = T.own, nc = T.nc;
+  // an unpatched word is the OR of the tight classes' masks: with <= 6
+  // classes its digest key is one of 2^nc, tabled in LDS (one lookup per node
+  // instead of W splitmix hashes)
+  const bool ctab = a.digest && nc <= kComboC;
+  if (ctab && tid < (1u << nc)) {
+    uint64_t ws = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      uint32_t m = 0;
+      for (uint32_t j = 0; j < nc; ++j)
+        if ((tid >> j) & 1u) m |= T.cmask[j][w];
+      if (m) ws += digest_word_key(w, m);
+    }
+    s_wk[tid] = ws;
+  }
+  __syncthreads();
   const uint32_t t0 = ci * a.ctiles, t1 = min(a.tiles, t0 + a.ctiles);
   uint32_t* st = s_stage + wave * 1024u * W;
   uint64_t h = 0;
@@ -211,7 +229,7 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
         lm1[q] = m | 0x80808080u;
       }
     }
-    uint32_t word[W][16];
+    uint32_t word[W][16], cbp[4] = {0u, 0u, 0u, 0u};  // cbp: tight-class bits, a byte per node
 #pragma unroll
     for (int w = 0; w < W; ++w)
 #pragma unroll
@@ -232,6 +250,7 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint32_t z = live ? (lm1[q] - Rw[q]) & 0x80808080u : 0u;
+        if (ctab) cbp[q] |= ((z >> 7) & 0x01010101u) << j;
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb) {
           const uint32_t sel = 0u - ((z >> (8 * bb + 7)) & 1u);
@@ -317,10 +336,15 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
         const uint64_t kn[2] = {((uint64_t)k2.y << 32) | k2.x, ((uint64_t)k2.w << 32) | k2.z};
 #pragma unroll
         for (int y = 0; y < 2; ++y) {
+          const int n = 2 * x + y;
           uint64_t ws = 0;
+          if (ctab) {
+            ws = s_wk[(cbp[n >> 2] >> (8 * (n & 3))) & 0xFFu];
+          } else {
 #pragma unroll
-          for (int w = 0; w < W; ++w)
-            if (word[w][2 * x + y]) ws += digest_word_key(w, word[w][2 * x + y]);
+            for (int w = 0; w < W; ++w)
+              if (word[w][n]) ws += digest_word_key(w, word[w][n]);
+          }
           h += kn[y] * ws;
         }
       }

@@ -133,7 +133,7 @@ def test_sweep_weighted_fabric_cover_path():
         eng.close()
 
 
-@pytest.mark.parametrize("stage", [False, True])
+@pytest.mark.parametrize("stage", [False, True, "tiled"])
 @pytest.mark.parametrize("drain", [0.0, 0.08])
 def test_sweep_weighted_fabric_closure(drain, stage, monkeypatch):
     """A weighted fabric whose cover splits into seeds (the spines) and small
@@ -142,7 +142,9 @@ def test_sweep_weighted_fabric_closure(drain, stage, monkeypatch):
     for bit, with drained (overloaded) switches and down links."""
     # 40 pods: a spine has 40 > 32 neighbours, so it is no leaf candidate and
     # stays in the cover (as on F100k)
-    if stage:  # closure rows in chunks, leaf chunks on a second stream (opt-in)
+    if stage == "tiled":  # closure rows by node tiles x root chunks (opt-in)
+        monkeypatch.setenv("OSPF_COVER_ROWS_TILED", "1")
+    elif stage:  # closure rows in chunks, leaf chunks on a second stream (opt-in)
         monkeypatch.setenv("OSPF_WCOVER_STAGE", "1")
     st = drained_fabric(40, 4, seed=5, drain=drain, down=0.03 if drain else 0.0,
                         weighted_seed=11, ssw_per_plane=4)
@@ -156,6 +158,8 @@ def test_sweep_weighted_fabric_closure(drain, stage, monkeypatch):
         # the seeds' next hops come out of their Dial (masks at settle)
         seeds_k = [p.get("kernel", "") for p in prof if p["name"] == "cover_seeds"][0]
         assert "next-hop masks" in seeds_k, seeds_k
+        rows_k = [p.get("kernel", "") for p in prof if p["name"].startswith("cover_rows")]
+        assert ("closure_tile_rows_kernel" in rows_k[0]) == (stage == "tiled"), rows_k
         check_sweep_vs_batch(eng, "wcover", rows_for=np.arange(0, eng.V, 7))
     finally:
         eng.close()
