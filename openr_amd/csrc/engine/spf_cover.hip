@@ -316,6 +316,150 @@ __device__ __forceinline__ void write_row_nh(const DevGraph& g, const CoverGraph
   }
 }
 
+// write_row_nh over a TAGGED column array: s_D[k] | 0x80000000 where cover
+// node k is non-transit and not the root (it relays for no leaf), s_D[nS] =
+// kInf (the padding slot). A leaf's term is then one saturating add per
+// in-link, tight where it equals the minimum; no transit-bit lookups.
+template <int NW>
+__device__ __forceinline__ void write_row_nh_tag(const DevGraph& g, const CoverGraph& C, uint32_t* row,
+                             uint32_t* nhrow, const uint32_t* s_D, const uint32_t* s_tr,
+                             uint32_t r, uint32_t rn, const uint32_t* cm, ospf_digest* dg,
+                             unsigned long long* s_acc, uint32_t* s_st, uint32_t tid,
+                             uint32_t nthreads) {
+  const uint32_t nS = C.nS, V = g.V, lane = tid & 63u;
+  const uint4* la4 = reinterpret_cast<const uint4*>(C.ladj);
+  const uint32_t* dn = g.dn + g.dn_off[rn];
+  const uint32_t K = g.dn_off[rn + 1] - g.dn_off[rn];
+  uint64_t h = 0, sum = 0;
+  uint32_t reach = 0;
+  // a block step = nthreads consecutive nodes; their next-hop words leave
+  // through LDS as one contiguous run (lane-strided NW-word records would
+  // write partial lines). Loads run ahead: the next step's first two in-link
+  // quads and the step after's cover index are issued before this step's
+  // nodes are folded.
+  const uint4 pad = make_uint4(0xFFFFu, 0xFFFFu, 0xFFFFu, 0xFFFFu);
+  auto quads = [&](uint32_t vv, uint32_t cx, uint4& a, uint4& b) {
+    a = b = pad;
+    if (vv < V && (cx & kLeaf)) {
+      const uint32_t q0 = (cx >> 5) & 0x3FFFFFFu, nq = cx & 31u;
+      if (nq > 0) a = la4[q0];
+      if (nq > 1) b = la4[q0 + 1];
+    }
+  };
+  uint32_t cxA = tid < V ? C.cix[tid] : 0u;
+  uint32_t cxB = tid + nthreads < V ? C.cix[tid + nthreads] : 0u;
+  uint4 qA0, qA1;
+  quads(tid, cxA, qA0, qA1);
+  for (uint32_t v0 = 0; v0 < V; v0 += nthreads) {
+    const uint32_t v = v0 + tid;
+    uint4 qB0, qB1;
+    quads(v + nthreads, cxB, qB0, qB1);
+    const uint32_t cxC = v + 2u * nthreads < V ? C.cix[v + 2u * nthreads] : 0u;
+    uint32_t out = kInf, m[NW];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) m[w] = 0u;
+    if (v < V) {
+      const uint32_t cx = cxA;
+      if (!(cx & kLeaf)) {
+        out = s_D[cx];
+        if (out != kInf) out &= 0x7FFFFFFFu;  // a non-transit cover node's own column
+#pragma unroll
+        for (int w = 0; w < NW; ++w) m[w] = cm[(size_t)cx * NW + w];
+      } else {
+        const uint32_t q0 = (cx >> 5) & 0x3FFFFFFu, nq = cx & 31u;
+        const uint32_t es[8] = {qA0.x, qA0.y, qA0.z, qA0.w, qA1.x, qA1.y, qA1.z, qA1.w};
+        // a term: the tagged column (bit 31: a non-transit last hop, kInf:
+        // unreached or padding) + the in-link's metric, saturating
+        auto term = [&](uint32_t e) {
+          const uint32_t x = s_D[min(e & 0xFFFFu, nS)], c = x + (e >> 16);
+          return c < x ? kInf : c;
+        };
+#pragma unroll
+        for (int b = 0; b < 8; ++b) out = min(out, term(es[b]));
+        for (uint32_t qq = 2; qq < nq; ++qq) {
+          const uint4 e4 = la4[q0 + qq];
+          out = min(out, min(min(term(e4.x), term(e4.y)), min(term(e4.z), term(e4.w))));
+        }
+        auto tight = [&](uint32_t e) {
+          if ((e & 0xFFFFu) == r) {  // a neighbour of the root: its own bit
+            uint32_t lo = 0, hi = K;
+            while (lo < hi) {
+              const uint32_t mid = (lo + hi) >> 1;
+              if (dn[mid] < v) lo = mid + 1;
+              else hi = mid;
+            }
+            if (lo < 32u * NW) m[lo >> 5] |= 1u << (lo & 31u);
+          } else {
+            const uint32_t ci = e & 0xFFFFu;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) m[w] |= cm[(size_t)ci * NW + w];
+          }
+        };
+        if (out >= 0x80000000u) {  // no usable last hop reaches v
+          out = kInf;
+        } else {
+#pragma unroll
+          for (int b = 0; b < 8; ++b)
+            if (term(es[b]) == out) tight(es[b]);
+          for (uint32_t qq = 2; qq < nq; ++qq) {
+            const uint4 e4 = la4[q0 + qq];
+            if (term(e4.x) == out) tight(e4.x);
+            if (term(e4.y) == out) tight(e4.y);
+            if (term(e4.z) == out) tight(e4.z);
+            if (term(e4.w) == out) tight(e4.w);
+          }
+        }
+      }
+      if (v == rn || out == kInf) {
+#pragma unroll
+        for (int w = 0; w < NW; ++w) m[w] = 0u;
+      }
+      __builtin_nontemporal_store(out, row + v);
+      if (out != kInf) {
+        reach += 1u;
+        sum += out;
+        h += g.dkey[2ull * v] * ((uint64_t)out + 1ull);
+        uint64_t ws = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w)
+          if (m[w]) ws += digest_word_key((uint32_t)w, m[w]);
+        if (ws) h += g.dkey[2ull * v + 1] * ws;
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < NW; ++w) s_st[tid * NW + w] = m[w];
+    __syncthreads();
+    const size_t base = (size_t)v0 * NW, lim = (size_t)V * NW;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const size_t i = (size_t)w * nthreads + tid;
+      if (base + i < lim) __builtin_nontemporal_store(s_st[i], nhrow + base + i);
+    }
+    __syncthreads();  // s_st is rewritten by the next step
+    cxA = cxB;
+    qA0 = qB0;
+    qA1 = qB1;
+    cxB = cxC;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    h += shfl_xor64(h, o);
+    sum += shfl_xor64(sum, o);
+    reach += (uint32_t)__shfl_xor((int)reach, o, kWave);
+  }
+  if (lane == 0 && reach) {
+    atomicAdd(&s_acc[0], (unsigned long long)reach);
+    atomicAdd(&s_acc[1], (unsigned long long)sum);
+    atomicAdd(&s_acc[2], (unsigned long long)h);
+  }
+  __syncthreads();
+  if (tid == 0 && dg) {
+    atomicAdd((unsigned long long*)&dg->reached, s_acc[0]);
+    atomicAdd((unsigned long long*)&dg->sum_dist, s_acc[1]);
+    atomicAdd((unsigned long long*)&dg->hash, s_acc[2]);
+  }
+}
+
 // Seed next hops, during the Dial: the cover nodes this wave scans that
 // settled at t (metrics >= 1: their tight in-edges come from nodes settled
 // before t, whose masks are written) get the OR over their tight in-edges
@@ -889,12 +1033,13 @@ constexpr uint32_t kRowsBlock = 1024;
 template <int NW>
 __global__ void __launch_bounds__(kRowsBlock, 8) cover_rows_kernel(DevGraph g, CoverGraph C,
                                                                    CoverArgs a) {
-  extern __shared__ uint32_t s_D[];  // [nS] cover columns, then [ctr words] transit bits
+  extern __shared__ uint32_t s_D[];  // [nS + 1] tagged cover columns, then [ctr words] transit bits
   __shared__ uint32_t s_st[kRowsBlock * NW];
   __shared__ unsigned long long s_acc[3];
   const uint32_t tid = threadIdx.x, nS = C.nS, V = g.V;
-  uint32_t* s_tr = s_D + nS;
+  uint32_t* s_tr = s_D + nS + 1u;
   for (uint32_t x = tid; x < (nS + 31u) / 32u; x += kRowsBlock) s_tr[x] = C.ctr[x];
+  if (tid == 0) s_D[nS] = kInf;
   for (uint32_t i = blockIdx.x; i < a.n; i += gridDim.x) {
     const uint32_t rn = a.roots[i];
     const uint32_t r = rn < V ? C.cix[rn] : kInf;
@@ -903,10 +1048,14 @@ __global__ void __launch_bounds__(kRowsBlock, 8) cover_rows_kernel(DevGraph g, C
       continue;
     }
     const uint32_t* src = a.dload + (size_t)i * nS;
-    for (uint32_t x = tid; x < nS; x += kRowsBlock) s_D[x] = src[x];
+    for (uint32_t x = tid; x < nS; x += kRowsBlock) {
+      const uint32_t d = src[x];  // < 2^31 when reached (the Dial's bound)
+      const bool relay = x == r || ((s_tr[x >> 5] >> (x & 31u)) & 1u);
+      s_D[x] = (d == kInf || relay) ? d : (d | 0x80000000u);
+    }
     if (tid < 3) s_acc[tid] = 0ull;
     __syncthreads();
-    write_row_nh<NW>(g, C, a.dist + (size_t)a.rowpos[i] * V, a.nh + (size_t)i * V * NW, s_D, s_tr,
+    write_row_nh_tag<NW>(g, C, a.dist + (size_t)a.rowpos[i] * V, a.nh + (size_t)i * V * NW, s_D, s_tr,
                      r, rn, a.nhload + (size_t)i * nS * NW, a.digest ? a.digest + i : nullptr, s_acc,
                      s_st, tid, kRowsBlock);
     __syncthreads();
@@ -1209,6 +1358,7 @@ hipError_t launch_cover_spf(const DevGraph& g, const CoverGraph& C, const CoverA
   const size_t lds = ((size_t)C.nS + (C.nS + 31u) / 32u) * 4u;
   if (a.nhload && !getenv("OSPF_COVER_ROWS_IN_DIAL")) {  // closure rows with next hops
     const uint32_t grid = std::min<uint32_t>(a.n, n_cu * 2u);
+    const size_t lds = ((size_t)C.nS + 1u + (C.nS + 31u) / 32u) * 4u;  // + the padding slot
     auto go = [&](const void* k) -> hipError_t {
       if (lds > 48 * 1024) {
         const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
