@@ -48,6 +48,28 @@ __device__ __forceinline__ uint32_t wave_min32(uint32_t x) {
   for (int o = 32; o > 0; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o, kWave));
   return x;
 }
+__device__ __forceinline__ uint32_t wave_max32(uint32_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, kWave));
+  return x;
+}
+// Closure early exit (wave-uniform): the terms are sorted by their smallest
+// constant over the members, and a seed column is >= 0, so once that constant
+// exceeds every lane's accumulator of every member in use no later term can
+// improve or tie any of them.
+template <int KW>
+__device__ __forceinline__ bool closure_done(const uint32_t* acc, const uint32_t* cst_j,
+                                             uint32_t used, bool ok) {
+  uint32_t mx = 0, cmin = kClInf;
+#pragma unroll
+  for (int f = 0; f < KW; ++f)
+    if ((used >> f) & 1u) {
+      mx = max(mx, acc[f]);
+      cmin = min(cmin, cst_j[f]);
+    }
+  mx = wave_max32(ok ? mx : 0u);
+  return cmin > mx;
+}
 
 // expand queued nodes q[0 .. cnt) (this wave's) at distance t: 64 nodes per
 // pass, their edges flattened over the lanes
@@ -1201,7 +1223,11 @@ __global__ void __launch_bounds__(256) closure_nh_kernel(ClosurePlan p) {
   const uint32_t* cst = p.cst + (size_t)cm.x * KW;
   const uint32_t* fh = p.fh + (size_t)cm.x * KW * NW;
   const uint32_t* jl = p.jl + cm.x;
+  uint32_t used = 0;  // members with an output row
+#pragma unroll
+  for (int f = 0; f < KW; ++f) used |= (p.out[(size_t)ci * KW + f] != kInf ? 1u : 0u) << f;
   for (uint32_t j0 = 0; j0 < cm.y; j0 += 8u) {
+    if (j0 && closure_done<KW>(acc, cst + (size_t)j0 * KW, used, ok)) break;
     uint32_t x[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -1250,7 +1276,11 @@ __global__ void __launch_bounds__(256) closure_kernel(ClosurePlan p) {
   for (int f = 0; f < KW; ++f) acc[f] = kClInf;
   const uint32_t* cst = p.cst + (size_t)cm.x * KW;
   const uint32_t* jl = p.jl + cm.x;
+  uint32_t used = 0;  // members with an output row
+#pragma unroll
+  for (int f = 0; f < KW; ++f) used |= (p.out[(size_t)ci * KW + f] != kInf ? 1u : 0u) << f;
   for (uint32_t j0 = 0; j0 < cm.y; j0 += 8u) {
+    if (j0 && closure_done<KW>(acc, cst + (size_t)j0 * KW, used, ok)) break;
     uint32_t x[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {

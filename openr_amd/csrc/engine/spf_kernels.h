@@ -100,6 +100,22 @@ __host__ __device__ inline uint64_t digest_word_term(uint32_t v, uint32_t g, uin
   return word ? digest_node_key(v) * digest_word_key(g, word) : 0ull;
 }
 
+// Sum over each 16-lane row of a wave, every lane of the row getting it:
+// DPP quad permutes + row rotations (VALU only; no LDS permute round trips).
+template <int kCtrl>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t x) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, kCtrl, 0xF, 0xF, true);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), kCtrl, 0xF, 0xF, true);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t row_sum64(uint64_t x) {
+  x += dpp_u64<0xB1>(x);   // quad_perm [1, 0, 3, 2]
+  x += dpp_u64<0x4E>(x);   // quad_perm [2, 3, 0, 1]
+  x += dpp_u64<0x124>(x);  // row_ror:4
+  x += dpp_u64<0x128>(x);  // row_ror:8
+  return x;
+}
+
 // 16-B store of a row that this launch never reads back (dist / next-hop
 // rows of finished runs): non-temporal, so the stream of output lines does not
 // evict the L2 lines the traversal or derivation re-reads.

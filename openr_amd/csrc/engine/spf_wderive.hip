@@ -206,27 +206,24 @@ __global__ void __launch_bounds__(256) wderive_kernel(DevGraph g, WDeriveArgs a)
         }
       }
       if (a.digest) {
-        uint64_t h = 0, sum = 0;
-        uint32_t reach = 0;
+        // reached count in the top byte of the distance sum (a row of 16
+        // lanes: <= 64 nodes, sum < 2^38), both summed per row by DPP and
+        // added to the root's LDS sums by the row's first lane
+        uint64_t h = 0, sr = 0;
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
           if (v0 + b < V && m[b] != kInf) {
-            reach += 1u;
-            sum += m[b];
+            sr += (uint64_t)m[b] + (1ull << 56);
             h += dk[b] * ((uint64_t)m[b] + 1ull);
             if (bits[b]) h += nk[b] * (KM <= 8 ? s_wk[bits[b]] : digest_word_key(0, bits[b]));
           }
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          h += shfl_xor64(h, o);
-          sum += shfl_xor64(sum, o);
-          reach += __shfl_xor(reach, o, kWave);
-        }
-        if (lane == 0 && reach) {
+        h = row_sum64(h);
+        sr = row_sum64(sr);
+        if ((lane & 15u) == 0 && sr) {
           atomicAdd(&s_h[j], (unsigned long long)h);
-          atomicAdd(&s_sum[j], (unsigned long long)sum);
-          atomicAdd(&s_reach[j], reach);
+          atomicAdd(&s_sum[j], (unsigned long long)(sr & ((1ull << 56) - 1ull)));
+          atomicAdd(&s_reach[j], (uint32_t)(sr >> 56));
         }
       }
     }
