@@ -561,8 +561,11 @@ __device__ __forceinline__ void write_row_nhw(const DevGraph& g, const CoverGrap
                               uint32_t* __restrict__ nhrow, const uint32_t* s_D,
                               const uint32_t* s_tr, uint32_t r, uint32_t rn,
                               const uint32_t* __restrict__ cm, uint32_t NW, ospf_digest* dg,
-                              unsigned long long* s_acc, uint32_t wave, uint32_t lane) {
-  const uint32_t nS = C.nS, V = g.V;
+                              unsigned long long* s_acc, uint32_t wave, uint32_t lane,
+                              uint32_t vbeg, uint32_t vend) {
+  // nodes [vbeg, vend) of the row (vbeg a multiple of 64); the digest parts
+  // of several ranges add up
+  const uint32_t nS = C.nS, V = vend;
   const uint4* la4 = reinterpret_cast<const uint4*>(C.ladj);
   const uint32_t* dn = g.dn + g.dn_off[rn];
   const uint32_t K = g.dn_off[rn + 1] - g.dn_off[rn];
@@ -593,7 +596,7 @@ __device__ __forceinline__ void write_row_nhw(const DevGraph& g, const CoverGrap
   const uint4 pad = make_uint4(0xFFFFu, 0xFFFFu, 0xFFFFu, 0xFFFFu);
   uint64_t h = 0, sum = 0;
   uint32_t reach = 0;
-  for (uint32_t v0 = wave * kWave; v0 < V; v0 += kBlock) {
+  for (uint32_t v0 = vbeg + wave * kWave; v0 < V; v0 += kBlock) {
     const uint32_t v = v0 + lane;
     // lane = node: distance, first two tight last hops (cover indices), the
     // root's bit, and whether more remain (then the word pass rescans)
@@ -1022,26 +1025,34 @@ __global__ void __launch_bounds__(512) seed_rows_kernel(DevGraph g, CoverGraph C
                                                         const uint32_t* dfull, const uint32_t* nhm,
                                                         uint32_t NW, uint32_t* dist,
                                                         const uint32_t* rowpos, uint32_t* nh,
-                                                        ospf_digest* digest, uint32_t* err) {
+                                                        ospf_digest* digest, uint32_t* err,
+                                                        uint32_t nch) {
   extern __shared__ uint32_t s_D[];  // [nS] columns, then [ctr words] transit bits
   __shared__ unsigned long long s_acc[3];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint32_t nS = C.nS, V = g.V;
   uint32_t* s_tr = s_D + nS;
   for (uint32_t x = tid; x < (nS + 31u) / 32u; x += kBlock) s_tr[x] = C.ctr[x];
-  for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
+  // items = (root, node range): a root's row in nch ranges, so a few hundred
+  // seeds still fill the chip (each item reloads the root's columns)
+  const uint32_t span = ((V + nch - 1) / nch + kWave - 1) / kWave * kWave;
+  for (uint32_t it = blockIdx.x; it < n * nch; it += gridDim.x) {
+    const uint32_t k = it % n, c = it / n;
     const uint32_t rn = roots[k];
     const uint32_t r = rn < V ? C.cix[rn] : kInf;
     if (r >= nS) {
-      if (tid == 0) atomicOr(err, 64u);
+      if (tid == 0 && c == 0) atomicOr(err, 64u);
       continue;
     }
+    const uint32_t vb = c * span, ve = min(V, vb + span);
+    if (vb >= ve) continue;  // block-uniform
     const uint32_t* src = dfull + (size_t)k * nS;
     for (uint32_t x = tid; x < nS; x += kBlock) s_D[x] = src[x];
     if (tid < 3) s_acc[tid] = 0ull;
     __syncthreads();
     write_row_nhw(g, C, dist + (size_t)rowpos[k] * V, nh + (size_t)k * V * NW, s_D, s_tr, r, rn,
-                  nhm + (size_t)k * nS * NW, NW, digest ? digest + k : nullptr, s_acc, wave, lane);
+                  nhm + (size_t)k * nS * NW, NW, digest ? digest + k : nullptr, s_acc, wave, lane, vb,
+                  ve);
     __syncthreads();
   }
 }
@@ -1177,7 +1188,7 @@ __global__ void __launch_bounds__(512) cover_spf_kernel(DevGraph g, CoverGraph C
       for (uint32_t x = tid; x < nS; x += kBlock) dst[x] = s_D[x];
     } else if (cmk && rp != kInf)
       write_row_nhw(g, C, a.dist + (size_t)rp * V, a.nh + (size_t)np * V * a.NW, s_D, s_tr, r, rn,
-                    cmk, a.NW, a.digest ? a.digest + np : nullptr, s_acc, wave, lane);
+                    cmk, a.NW, a.digest ? a.digest + np : nullptr, s_acc, wave, lane, 0u, V);
     else if (rp != kInf)
       write_row(g, C, a.dist + (size_t)rp * V, s_D, s_tr, r, tid, kBlock);
     __syncthreads();  // s_D is reused by the next root
@@ -1338,9 +1349,11 @@ hipError_t launch_seed_rows(const DevGraph& g, const CoverGraph& C, const uint32
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  const uint32_t grid = std::min<uint32_t>(n, 2u * n_cu);
+  // >= ~8 items per CU: ranges of >= 4,096 nodes
+  const uint32_t nch = std::max(1u, std::min((8u * n_cu + n - 1) / n, (g.V + 4095u) / 4096u));
+  const uint32_t grid = std::min<uint32_t>(n * nch, 2u * n_cu);
   hipLaunchKernelGGL(seed_rows_kernel, dim3(grid), dim3(kBlock), lds, s, g, C, roots, n, dfull, nhm,
-                     NW, dist, rowpos, nh, digest, err);
+                     NW, dist, rowpos, nh, digest, err, nch);
   return hipGetLastError();
 }
 
