@@ -1773,7 +1773,11 @@ __global__ void __launch_bounds__(256) nh_wide_plan_kernel(DevGraph g, WidePlan 
   const uint32_t V = g.V, W = d.W, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint32_t NB = d.nruns * d.chunks, NB8 = NB / 8u * 8u, bb = blockIdx.x;
   const uint32_t item = bb < NB8 ? (bb % 8u) * (NB8 / 8u) + bb / 8u : bb;
-  const uint32_t ci = item / d.nruns, ri = item % d.nruns;
+  // run-major items (an XCD's resident blocks serve one run, when there are
+  // 8), and a block's tiles strided by the chunk count: the blocks of a run
+  // move through the row together, so the 8 tiles whose 16-B pieces share each
+  // neighbour row's 128-B lines are in flight on one XCD at once
+  const uint32_t ri = item / d.chunks, ci = item % d.chunks;
   const uint32_t j0 = d.run[ri], ng = min(kWideG, d.run[ri + 1] - j0);
   const uint32_t s0 = d.soff[ri], K = min(kDeriveTab, d.soff[ri + 1] - s0);
   uint32_t* s_keep = s_dyn;
@@ -1785,10 +1789,9 @@ __global__ void __launch_bounds__(256) nh_wide_plan_kernel(DevGraph g, WidePlan 
     s_h[tid] = 0ull;
   }
   __syncthreads();
-  const uint32_t t0 = ci * d.ctiles, t1 = min(d.tiles, t0 + d.ctiles);
-  for (uint32_t t = t0; t < t1; ++t) {
+  for (uint32_t t = ci; t < d.tiles; t += d.chunks) {
     const uint32_t v0 = t * kW3Tile;
-    if (t > t0) __syncthreads();  // the previous tile's bytes are consumed
+    if (t > ci) __syncthreads();  // the previous tile's bytes are consumed
     // every slot load of the thread in flight at once (K <= 2048: <= 8 each)
     uint32_t pk[kDeriveTab / kBlock];
     uint4 xk[kDeriveTab / kBlock];
