@@ -62,6 +62,12 @@ uint64_t odl_spf_runs(const odl_ls* ls);
  * memoised SPF of roots a metric / up / overload-only update cannot affect.
  * Stats: {patches applied, results kept, results dropped}. */
 void odl_set_incremental(odl_ls* ls, int on);
+/* Every SPF / KSP2 / digest of this LinkState on the host with the
+ * reference's algorithm (LinkState.cpp:836-911), the engine never opened: a
+ * GPU-free run of the ingest / in-place patch / memo logic (sanitizer builds;
+ * also the environment variable ODL_HOST_SPF at creation). Not a fallback:
+ * off by default, and nothing switches it on by itself. */
+void odl_set_host_spf(odl_ls* ls, int on);
 void odl_incremental_stats(const odl_ls* ls, uint64_t* out3);
 /* {whole CSR snapshots, whole device graph loads, updates whose added /
  * removed links were patched in place (ospf_update_rows), rows rebuilt by

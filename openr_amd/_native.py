@@ -48,7 +48,7 @@ DECISION_SYMBOLS = [
     "odl_create", "odl_create_multi", "odl_all_sources_prefetch", "odl_all_sources_digests",
     "odl_sweep_stats", "odl_destroy", "odl_last_error", "odl_free", "odl_apply", "odl_spf_text",
     "odl_kth_paths_text", "odl_links_text", "odl_link_keys_text", "odl_metric_a_to_b", "odl_is_overloaded",
-    "odl_spf_runs", "odl_set_incremental", "odl_incremental_stats", "odl_topology_stats", "odl_num_nodes", "odl_num_links", "odl_spf_digests", "odl_spf_prefetch",
+    "odl_spf_runs", "odl_set_incremental", "odl_set_host_spf", "odl_incremental_stats", "odl_topology_stats", "odl_num_nodes", "odl_num_links", "odl_spf_digests", "odl_spf_prefetch",
     "odl_ksp2_text", "odl_route_text", "odl_route_db_text", "odl_route_db_bin", "odl_free_buf", "odl_path_a_in_b", "odl_ucmp_text", "odl_csr_size", "odl_csr_export", "odl_node_name", "odl_node_id",
 ]
 
@@ -221,7 +221,7 @@ def decision() -> C.CDLL:
     global _decision
     if _decision is None:
         engine()
-        L = _load(DECISION_SO)
+        L = _load(os.environ.get("OPENR_DECISION_SO") or DECISION_SO)
         L.odl_create.argtypes = [cp, i32, C.POINTER(vp)]
         L.odl_create_multi.argtypes = [cp, vp, u32, C.POINTER(vp)]
         L.odl_all_sources_prefetch.argtypes = [vp, i32]
@@ -258,6 +258,8 @@ def decision() -> C.CDLL:
         L.odl_spf_runs.restype = u64
         L.odl_set_incremental.argtypes = [vp, i32]
         L.odl_set_incremental.restype = None
+        L.odl_set_host_spf.argtypes = [vp, i32]
+        L.odl_set_host_spf.restype = None
         L.odl_incremental_stats.argtypes = [vp, vp]
         L.odl_incremental_stats.restype = None
         L.odl_topology_stats.argtypes = [vp, vp]

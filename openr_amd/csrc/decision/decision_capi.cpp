@@ -240,6 +240,9 @@ uint64_t odl_spf_runs(const odl_ls* h) { return h ? h->ls.spfRuns() : 0; }
 void odl_set_incremental(odl_ls* h, int on) {
   if (h) h->ls.setIncremental(on != 0);
 }
+void odl_set_host_spf(odl_ls* h, int on) {
+  if (h) h->ls.setHostSpf(on != 0);
+}
 void odl_incremental_stats(const odl_ls* h, uint64_t* out) {
   if (!h || !out) return;
   const auto& st = h->ls.incrementalStats();

@@ -14,6 +14,9 @@
 #include <stdexcept>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
 #include <cstdio>
 #include <thread>
 #include <tuple>
@@ -44,6 +47,53 @@ constexpr uint32_t kInf = OSPF_DIST_INF;
 }  // namespace
 
 // ---------------------------------------------------------------- Link
+// One thread per LinkState frees dropped memos, in the order they were
+// dropped; the LinkState's destructor drains the queue and joins it, so no
+// release outlives the object (r04 had a detached thread per event). Only
+// memory unreachable from the LinkState is handed over: the SpfResults own
+// their rows and entries, and the Links / snapshots they share are
+// reference-counted (std::shared_ptr, atomic counts).
+struct MemoReaper {
+  using Memo = std::unordered_map<std::string, SpfResult>;
+  struct Dead {
+    Memo a, b;
+    std::unordered_map<std::string, std::vector<Path>> k;
+  };
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::unique_ptr<Dead>> q;
+  bool stop = false;
+  std::thread th;
+  MemoReaper() : th([this] { loop(); }) {}
+  ~MemoReaper() {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      stop = true;
+    }
+    cv.notify_one();
+    th.join();
+  }
+  void push(std::unique_ptr<Dead> d) {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      q.push_back(std::move(d));
+    }
+    cv.notify_one();
+  }
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv.wait(lk, [this] { return stop || !q.empty(); });
+      if (q.empty()) return;  // stop, and everything freed
+      std::unique_ptr<Dead> d = std::move(q.front());
+      q.pop_front();
+      lk.unlock();
+      d.reset();
+      lk.lock();
+    }
+  }
+};
+
 size_t Link::hashOf(const End& lo, const End& hi) {
   return fold(hashEnd(lo.node, lo.iface), hashEnd(hi.node, hi.iface));
 }
@@ -130,14 +180,18 @@ std::string Link::key() const {
 
 // ---------------------------------------------------------------- LinkState
 LinkState::LinkState(std::string area, int device)
-    : area_(std::move(area)), device_(device), devices_{device} {}
+    : area_(std::move(area)), device_(device), devices_{device} {
+  hostOnly_ = getenv("ODL_HOST_SPF") != nullptr;
+}
 
 LinkState::LinkState(std::string area, std::vector<int> devices)
     : area_(std::move(area)), device_(devices.empty() ? 0 : devices[0]), devices_(std::move(devices)) {
   if (devices_.empty()) throw std::invalid_argument("LinkState: no device");
+  hostOnly_ = getenv("ODL_HOST_SPF") != nullptr;
 }
 
 LinkState::~LinkState() {
+  reaper_.reset();  // drains the dropped memos, joins the thread
   dropSweep();
   if (multi_) ospf_multi_close(multi_);
   else if (engine_) ospf_close(engine_);
@@ -192,34 +246,19 @@ void LinkState::clearMemo() {
   if (memoMetric_.empty() && memoHops_.empty() && memoKsp_.empty()) return;
   // A route build materialises every entry of its results (~100k node
   // results with next-hop sets and path links at F100k): freeing them took
-  // most of an event's apply time. They are unreachable once dropped, so a
-  // background thread frees them; the snapshot references they hold are
-  // counted so patchStructure knows they are no readers.
-  using Memo = std::unordered_map<std::string, SpfResult>;
-  struct Dead {
-    Memo a, b;
-    std::unordered_map<std::string, std::vector<Path>> k;
-  };
-  auto* dead = new Dead{std::move(memoMetric_), std::move(memoHops_), std::move(memoKsp_)};
-  memoMetric_.clear();
-  memoHops_.clear();
-  memoKsp_.clear();
-  std::unordered_set<const SpfRows*> rows;
-  for (const Memo* m : {&dead->a, &dead->b})
-    for (const auto& kv : *m)
-      if (kv.second.rows() && kv.second.rows()->csr == csr_) rows.insert(kv.second.rows().get());
-  const long r = (long)rows.size();
-  auto cnt = reapRefs_;
-  cnt->fetch_add(r);
-  try {
-    std::thread([dead, cnt, r] {
-      delete dead;
-      cnt->fetch_sub(r);
-    }).detach();
-  } catch (const std::system_error&) {  // no thread to spare: free here
-    delete dead;
-    cnt->fetch_sub(r);
+  // most of an event's apply time, so the reaper thread frees them.
+  auto dead = std::make_unique<MemoReaper::Dead>();
+  dead->a.swap(memoMetric_);
+  dead->b.swap(memoHops_);
+  dead->k.swap(memoKsp_);
+  if (!reaper_) {
+    try {
+      reaper_ = std::make_unique<MemoReaper>();
+    } catch (const std::system_error&) {  // no thread to spare: free here
+      return;
+    }
   }
+  reaper_->push(std::move(dead));
 }
 
 void LinkState::invalidate() {
@@ -726,8 +765,8 @@ bool LinkState::sweepHas(bool useLinkMetric) const {
 void LinkState::prefetchAllSources(bool useLinkMetric) {
   snapshot();
   if (sweepHas(useLinkMetric)) return;
-  if (useLinkMetric && hostMetric_) {  // outside the engine contract: the reference algorithm
-    prefetchSpf(csr_->names, true);
+  if (hostRun(useLinkMetric)) {  // outside the engine contract: the reference algorithm
+    prefetchSpf(csr_->names, useLinkMetric);
     return;
   }
   ensureEngine();
@@ -797,7 +836,7 @@ void LinkState::sweepRows(const std::vector<uint32_t>& roots, uint32_t W,
 std::vector<ospf_digest> LinkState::allSourcesDigests(bool useLinkMetric) {
   snapshot();
   const size_t V = csr_->names.size();
-  if (useLinkMetric && hostMetric_) return spfDigests(csr_->names, true);
+  if (hostRun(useLinkMetric)) return spfDigests(csr_->names, useLinkMetric);
   prefetchAllSources(useLinkMetric);
   std::vector<ospf_digest> out(V);
   if (msweep_) {
@@ -1016,9 +1055,9 @@ void LinkState::prefetchSpf(const std::vector<std::string>& roots, bool useLinkM
       memo.emplace(r, SpfResult(std::move(res)));
       continue;
     }
-    if (useLinkMetric && hostMetric_) {
+    if (hostRun(useLinkMetric)) {
       ++spfRuns_;
-      memo.emplace(r, runSpfHost(r, true, {}));
+      memo.emplace(r, runSpfHost(r, useLinkMetric, {}));
       continue;
     }
     byW[nhWordsFor(id->second)].push_back(id->second);
@@ -1083,8 +1122,8 @@ std::vector<ospf_digest> LinkState::spfDigests(const std::vector<std::string>& r
       out[i] = ospf_digest{1, 0, x};
       continue;
     }
-    if (useLinkMetric && hostMetric_) {
-      out[i] = digestHost(roots[i], runSpfHost(roots[i], true, {}));
+    if (hostRun(useLinkMetric)) {
+      out[i] = digestHost(roots[i], runSpfHost(roots[i], useLinkMetric, {}));
       continue;
     }
     ids.push_back(id->second);
@@ -1168,7 +1207,7 @@ const std::vector<Path>& LinkState::getKthPaths(const std::string& src, const st
         if (skipSet.insert(l.get()).second) skip.push_back(l);
   std::vector<Path> paths;
   snapshot();
-  if (hostMetric_) {
+  if (hostRun(true)) {
     if (skip.empty()) {
       paths = tracePathsHost(getSpfResult(src, true), src, dst);
     } else {
@@ -1230,7 +1269,7 @@ const std::vector<Path>& LinkState::getKthPaths(const std::string& src, const st
 
 void LinkState::prefetchKsp2(const std::string& src, const std::vector<std::string>& dsts) {
   snapshot();
-  if (hostMetric_) {
+  if (hostRun(true)) {
     for (const auto& d : dsts) getKthPaths(src, d, 2);
     return;
   }
@@ -1407,8 +1446,11 @@ void LinkState::patchStructure(const std::vector<LinkPtr>& added,
                                const std::vector<LinkPtr>& removed) {
   dropSweep();  // its rows describe the graph before the patch
   // a kept memoised result reads this snapshot's ranks lazily: give it its own
-  // (results being released by clearMemo's thread are no readers)
-  if (csr_.use_count() - 1 - reapRefs_->load() > 0) csr_ = std::make_shared<Csr>(*csr_);
+  // (results handed to the reaper are no readers; only the live memo is)
+  bool kept = false;
+  for (const auto* m : {&memoMetric_, &memoHops_})
+    for (const auto& kv : *m) kept |= kv.second.rows() && kv.second.rows()->csr == csr_;
+  if (kept) csr_ = std::make_shared<Csr>(*csr_);
   Csr& c = *csr_;
   const uint32_t V = (uint32_t)c.names.size();
   std::vector<uint32_t> rows;

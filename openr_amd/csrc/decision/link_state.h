@@ -342,6 +342,8 @@ struct EngineError : std::runtime_error {
   EngineError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
 };
 
+struct MemoReaper;
+
 class LinkState {
  public:
   LinkState(std::string area, int device);
@@ -440,6 +442,12 @@ class LinkState {
     snapshot();
     return hostMetric_;
   }
+  // Every SPF / KSP2 / digest on the host (runSpfHost, the reference
+  // algorithm), the engine never opened: a GPU-free run of the whole ingest /
+  // patch / memo logic (sanitizer builds, link-event sequences on the CPU).
+  // Also set by the environment variable ODL_HOST_SPF at construction.
+  void setHostSpf(bool on) { hostOnly_ = on; }
+  bool hostSpf() const { return hostOnly_; }
   // Links added or removed between known nodes ([LINK UP] / [LINK DOWN],
   // LinkState.cpp:632-657) patch the snapshot and the device graph in place
   // (ospf_update_rows) instead of a new snapshot and device load.
@@ -513,6 +521,8 @@ class LinkState {
   std::shared_ptr<Csr> csr_ = std::make_shared<Csr>();
   TopologyStats topoStats_;
   bool hostMetric_ = false;   // snapshot outside the engine's metric contract
+  bool hostOnly_ = false;     // setHostSpf: no engine at all
+  bool hostRun(bool useLinkMetric) const { return hostOnly_ || (useLinkMetric && hostMetric_); }
   uint64_t distBound_ = 0;    // >= every simple-path metric sum of the snapshot
   uint64_t spfRuns_ = 0;
   bool incremental_ = false;
@@ -539,10 +549,9 @@ class LinkState {
 
   std::unordered_map<std::string, SpfResult> memoMetric_, memoHops_;
   std::unordered_map<std::string, std::vector<Path>> memoKsp_;
-  // references to csr_ held by memoised results being released on a
-  // background thread (clearMemo): patchStructure mutates the snapshot in
-  // place when no other holder is left
-  std::shared_ptr<std::atomic<long>> reapRefs_ = std::make_shared<std::atomic<long>>(0);
+  // frees dropped memos on one background thread (clearMemo); joined by the
+  // destructor
+  std::unique_ptr<struct MemoReaper> reaper_;
 };
 
 }  // namespace odl

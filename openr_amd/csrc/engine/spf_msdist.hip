@@ -125,7 +125,12 @@ __global__ void __launch_bounds__(kBlock, 4) msdist_kernel(DevGraph g, MsDistArg
         // deferred nodes below the new end form the frontier
         const uint32_t nD = s_n[3];
         if (nD == 0) break;  // block-uniform: nothing left anywhere
-        const uint32_t hi = max(s_hi + a.delta, (s_minD / a.delta + 1u) * a.delta);
+        // in 64 bits, saturated at kInf: near 2^32 the u32 form wrapped to a
+        // small end no deferred value passes, and the block never drained;
+        // a saturated end lets every finite deferred value join
+        const uint64_t hi64 = max((uint64_t)s_hi + a.delta,
+                                  ((uint64_t)(s_minD / a.delta) + 1u) * a.delta);
+        const uint32_t hi = hi64 >= (uint64_t)kInf ? kInf : (uint32_t)hi64;
         uint32_t* LDef = st.L + (size_t)s_buf[3] * V;
         uint32_t* LDef2 = st.L + (size_t)s_buf[4] * V;
         uint32_t* LF = st.L + (size_t)s_buf[0] * V;

@@ -305,6 +305,13 @@ class LinkState:
         cannot affect (odl_set_incremental; off = the reference's behaviour)."""
         self._L.odl_set_incremental(self._h, int(on))
 
+    def set_host_spf(self, on: bool = True) -> None:
+        """Run every SPF / KSP2 / digest of this LinkState on the host with the
+        reference's algorithm, the engine never opened (odl_set_host_spf): a
+        GPU-free run of the ingest / patch / memo logic, for sanitizer builds
+        and CPU tests. Off by default."""
+        self._L.odl_set_host_spf(self._h, int(on))
+
     def incremental_stats(self) -> Dict[str, int]:
         out = (C.c_uint64 * 3)()
         self._L.odl_incremental_stats(self._h, out)

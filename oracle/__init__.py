@@ -17,7 +17,7 @@ from typing import List, Sequence, Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_SO = os.path.join(_HERE, "build", "liboracle.so")
+_SO = os.environ.get("OPENR_ORACLE_SO") or os.path.join(_HERE, "build", "liboracle.so")
 _lib = None
 
 

@@ -13,6 +13,7 @@ import pytest
 from graphs import drained_fabric, random_stream
 from oracle import Oracle
 from openr_amd import topology as T
+from openr_amd.adjdb import AdjDb, AdjDbStream, create_adjacency
 from openr_amd.engine import Engine, EngineError, Multi, MultiSweep, Sweep
 from openr_amd.linkstate import LinkState
 
@@ -252,6 +253,39 @@ def test_sweep_wmulti_drained_fabric_and_mesh(monkeypatch):
             assert sorted(seen) == list(range(V))
             for r in range(0, V, 13):
                 assert np.array_equal(seen[r], got[r]), r
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("delta", [None, "4"])
+def test_sweep_wmulti_distances_near_2_32(delta, monkeypatch):
+    """Distances up to 2^32 - 3 (metrics near 2^31, distance bound 2^32 - 2,
+    the engine's limit): the multi-root traversal's bucket end is computed in
+    64 bits and saturates, so the last bucket (whose end passes 2^32) drains
+    instead of wrapping to a small end no deferred value reaches (ADVICE r04:
+    spf_msdist.hip bucket end). Digests == the CSR-Dijkstra restatement."""
+    if delta:
+        monkeypatch.setenv("OSPF_MSD_DELTA", delta)
+    big = 2 ** 31 - 1
+    # a -> b -> c forward at ~2^31 each, back at 1; d hangs off c at 1 both ways
+    spec = {"a": [("b", big)], "b": [("a", 1), ("c", big - 3)],
+            "c": [("b", 1), ("d", 1)], "d": [("c", 1)]}
+    # bound = big + (big - 3) + 1 + 1 = 2^32 - 4 < 2^32 - 1
+    dbs = [AdjDb(n, [create_adjacency(m, f"{n}-{m}", f"{m}-{n}", w) for m, w in spec[n]], i + 1)
+           for i, n in enumerate(sorted(spec))]
+    st = AdjDbStream.from_dbs(dbs)
+    ls, csr, eng = engine_for(st)
+    try:
+        sw = Sweep(eng, mode="wmulti", hip_graph=False)
+        assert sw.mode == "wmulti"
+        sw.run()
+        eng.sync()
+        got = sweep_digests(sw)
+        sw.close()
+        names = ls.node_names()
+        want = Oracle(st).fast_digests(names)
+        for r in range(eng.V):
+            assert np.array_equal(got[r], want[r]), names[r]
     finally:
         eng.close()
 
