@@ -2039,19 +2039,34 @@ int plan_wmulti(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   size_t budget = 65536ull << 20;
   if (const char* e = getenv("OSPF_MSD_MB")) budget = (size_t)std::max(64, atoi(e)) << 20;
   const size_t per = ospf::msdist_scratch_bytes(V, 1);
-  uint32_t blocks = std::min<uint32_t>(std::max(1u, ngroups), 2u * (uint32_t)c->n_cu);
-  blocks = std::max<uint32_t>(1, std::min<uint32_t>(blocks, (uint32_t)(budget / per)));
-  if (const char* e = getenv("OSPF_MSD_BLOCKS")) blocks = std::max(1, std::min((int)blocks, atoi(e)));
   uint32_t delta = hop ? 1u : std::max<uint32_t>(1, c->info.max_metric);
   if (const char* e = getenv("OSPF_MSD_DELTA")) delta = (uint32_t)std::max(1, atoi(e));
-  uint32_t *slab, *d_pos, *d_s, *d_l, *lnh, *scratch;
+  uint32_t *slab, *d_pos, *d_s, *d_l, *lnh, *scratch = nullptr;
   int rc;
   if ((rc = dalloc(s, &slab, (size_t)(nS + nL) * V)) || (rc = upload(s, &d_pos, pos)) ||
       (rc = upload(s, &d_s, srows.empty() ? std::vector<uint32_t>{0u} : srows)) ||
       (rc = upload(s, &d_l, own_l.empty() ? std::vector<uint32_t>{0u} : own_l)) ||
-      (rc = dalloc(s, &lnh, (size_t)std::max(1u, nL) * V)) ||
-      (rc = dalloc(s, &scratch, per / 4u * blocks)))
+      (rc = dalloc(s, &lnh, (size_t)std::max(1u, nL) * V)))
     return rc;
+  // the scratch also fits what the device has left (other parts' sweeps,
+  // smaller devices), with a 1 GB margin; fewer blocks when an allocation
+  // still fails
+  {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess)
+      budget = std::min(budget, fr > (1ull << 30) ? fr - (1ull << 30) : per);
+  }
+  uint32_t blocks = std::min<uint32_t>(std::max(1u, ngroups), 2u * (uint32_t)c->n_cu);
+  blocks = std::max<uint32_t>(1, std::min<uint32_t>(blocks, (uint32_t)(budget / per)));
+  if (const char* e = getenv("OSPF_MSD_BLOCKS")) blocks = std::max(1, std::min((int)blocks, atoi(e)));
+  for (;;) {
+    if (hipMalloc((void**)&scratch, per * blocks) == hipSuccess) break;
+    (void)hipGetLastError();
+    if (blocks == 1) return sfail(s, OSPF_E_NOMEM, "wmulti: no room for one traversal's scratch");
+    blocks = std::max(1u, blocks / 2);
+  }
+  s->allocs.push_back(scratch);
+  s->device_bytes += per * blocks;
   std::vector<uint32_t> wset;
   for (uint32_t r : own_c) wset.push_back(f.words(r));
   std::sort(wset.begin(), wset.end());
@@ -2519,6 +2534,8 @@ int ospf_sweep_digests(ospf_sweep* s, ospf_digest* d_out, void* stream) {
   if (!s || (!d_out && !s->roots.empty())) return OSPF_E_INVAL;
   const uint32_t n = (uint32_t)s->roots.size();
   if (!n) return OSPF_OK;
+  // a deferred sweep (OSPF_SWEEP_DEFER) has no rows or digests before its run
+  if (!s->ran) return sfail(s, OSPF_E_INVAL, "sweep: digests before the first run");
   SCHK(s, hipSetDevice(s->c->device));
   hipLaunchKernelGGL(gather_digest_kernel, dim3((n + 255) / 256), dim3(256), 0,
                      (hipStream_t)stream, s->dig_all, s->d_own_slot, n, d_out);
@@ -2555,7 +2572,7 @@ int ospf_sweep_poison(ospf_sweep* s, void* stream) {
 
 int ospf_sweep_row(const ospf_sweep* s, uint32_t root, const uint32_t** d_dist,
                    const uint32_t** d_nh, uint32_t* nh_words) {
-  if (!s || root >= s->V) return OSPF_E_INVAL;
+  if (!s || root >= s->V || !s->ran) return OSPF_E_INVAL;  // no rows before the first run
   if (!s->row_dist[root]) return OSPF_E_RANGE;
   if (d_dist) *d_dist = s->row_dist[root];
   if (d_nh) *d_nh = s->row_nh[root];
@@ -2566,6 +2583,7 @@ int ospf_sweep_row(const ospf_sweep* s, uint32_t root, const uint32_t** d_dist,
 int ospf_sweep_copy_rows(ospf_sweep* s, const uint32_t* roots, uint32_t n, uint32_t nh_words,
                          uint32_t* dist_out, uint32_t* nh_out) {
   if (!s || (n && !roots)) return OSPF_E_INVAL;
+  if (!s->ran) return sfail(s, OSPF_E_INVAL, "sweep: rows before the first run");
   const uint32_t V = s->V;
   for (uint32_t i = 0; i < n; ++i) {
     if (roots[i] >= V || !s->row_dist[roots[i]])
