@@ -2054,7 +2054,7 @@ int plan_wmulti(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   {
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) == hipSuccess)
-      budget = std::min(budget, fr > (1ull << 30) ? fr - (1ull << 30) : per);
+      budget = std::min<size_t>(budget, fr > (1ull << 30) ? fr - (1ull << 30) : per);
   }
   uint32_t blocks = std::min<uint32_t>(std::max(1u, ngroups), 2u * (uint32_t)c->n_cu);
   blocks = std::max<uint32_t>(1, std::min<uint32_t>(blocks, (uint32_t)(budget / per)));
