@@ -392,6 +392,15 @@ int ospf_ksp2_run(ospf_ctx* ctx, const ospf_ksp2* args);
  * stream itself between rounds only when a masked run is deeper than the
  * graph's static depth bound. */
 int ospf_ksp2_dev(ospf_ctx* ctx, const ospf_ksp2* args, void* stream);
+/* The k = 2 masked reruns run as decremental SSSP from the source's row (the
+ * nodes whose every tight in-link the ignored links cut, directly or through
+ * other such nodes, get new distances; the rest keep the source's) with the
+ * trace fused in one launch; a run past that kernel's LDS budgets takes the
+ * full masked rerun. Cumulative counts of this context since open: out3 =
+ * {runs by the decremental kernel, runs sent to the full reruns, affected
+ * nodes summed over the decremental runs}. OSPF_KSP_NODECR in the environment
+ * sends every run to the full reruns. */
+int ospf_ksp2_stats(const ospf_ctx* ctx, uint64_t* out3);
 
 /* Incremental updates (Decision.cpp:918-996 re-runs SPF after
  * every debounced adjacency batch; LinkState clears every memoised result on

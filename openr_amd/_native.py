@@ -29,7 +29,7 @@ ENGINE_SYMBOLS = [
     "ospf_open", "ospf_close", "ospf_last_error", "ospf_load_graph", "ospf_graph_info_get",
     "ospf_root_neighbors", "ospf_sssp_batch", "ospf_sssp_batch_dev", "ospf_sync",
     "ospf_plan_variant", "ospf_plan", "ospf_plan_n", "ospf_spf_runs", "ospf_run_batch_dev",
-    "ospf_ksp2_run", "ospf_ksp2_dev", "ospf_update_links", "ospf_update_nodes", "ospf_update_rows",
+    "ospf_ksp2_run", "ospf_ksp2_dev", "ospf_ksp2_stats", "ospf_update_links", "ospf_update_nodes", "ospf_update_rows",
     "ospf_levels_dev", "ospf_nh_derive_dev", "ospf_leaf_derive_dev",
     "ospf_nh_derive_twin_dev", "ospf_leaf_derive2_dev", "ospf_wderive_dev", "ospf_wderive_wide_dev",
     "ospf_lds_sweep_dev", "ospf_lds_sweep_fits", "ospf_twin_levels_dev",
@@ -159,6 +159,7 @@ def engine() -> C.CDLL:
         L.ospf_run_batch_dev.argtypes = [vp, C.POINTER(ospf_batch), vp]
         L.ospf_ksp2_run.argtypes = [vp, C.POINTER(ospf_ksp2)]
         L.ospf_ksp2_dev.argtypes = [vp, C.POINTER(ospf_ksp2), vp]
+        L.ospf_ksp2_stats.argtypes = [vp, vp]
         L.ospf_levels_dev.argtypes = [vp, vp, u32, u32, vp, vp, u32, vp, vp]
         L.ospf_nh_derive_dev.argtypes = [vp, vp, u32, u32, u32, vp, u32, vp, vp, vp, vp, vp]
         L.ospf_nh_derive_twin_dev.argtypes = [vp, vp, u32, u32, u32, vp, u32, vp, vp, vp, vp, vp,

@@ -55,7 +55,7 @@ char* stream_scratch(ospf_ctx* c, void* stream, size_t need, int* rc, int slot) 
 }
 
 void release_stream_scratch(ospf_ctx* c, void* stream) {
-  for (int slot = 0; slot < 2; ++slot) {
+  for (int slot = 0; slot < 4; ++slot) {
     auto it = c->scratch.find((char*)stream + slot);
     if (it == c->scratch.end()) continue;
     if (it->second.p) hipFree(it->second.p);
@@ -550,150 +550,235 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
     e = ospf::launch_ksp_trace(false, c->g, tc, s);
     if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_trace k1");
   }
+  const ospf::TraceArgs t_k1 = t;
 
-  // 3: masked reruns + k = 2
-  HIPCHK(c, hipMemsetD32Async(d_roots, (int)src, ms ? n : chunk, s));
-  if (ms) {
-    if (!c->aux) HIPCHK(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
-    while (c->ev.size() < 2 * (size_t)slots + 1) {
-      hipEvent_t x;
-      HIPCHK(c, hipEventCreateWithFlags(&x, hipEventDisableTiming));
-      c->ev.push_back(x);
-    }
-    hipEvent_t* ev_bfs = c->ev.data();
-    hipEvent_t* ev_tr = c->ev.data() + slots;
-    hipEvent_t ev_end = c->ev[2 * slots];
-    char* ring = st + per_vb * nb_max;
-    std::vector<uint32_t> found;
-    for (uint32_t r = 0, vb0 = 0; vb0 < total_vb; ++r, vb0 += nb_max) {
-      const uint32_t slot = r % slots;
-      uint8_t* lev = (uint8_t*)(ring + (size_t)slot * (sz_lev + sz_sdead));
-      uint32_t* dead = (uint32_t*)(ring + (size_t)slot * (sz_lev + sz_sdead) + sz_lev);
-      ospf::MsArgs a{};
-      a.roots = d_roots;
-      a.n = n;
-      a.W = W;
-      a.npass = 1;
-      a.R = 64;
-      a.PP = 1;
-      a.OW = 1;
-      a.rep = 1;
-      a.vb0 = vb0;
-      a.nb = std::min(nb_max, total_vb - vb0);
-      a.lmax = lmax;
-      a.kcap = nn;
-      a.push_div = 8;
-      if (const char* x = getenv("OSPF_MS_PUSH_DIV")) a.push_div = (uint32_t)std::max(0, atoi(x));
-      a.defer = 1;
-      a.err = c->d_err;
-      a.front = (uint64_t*)st;
-      a.seen = a.front + 4ull * a.nb * V;
-      a.accb = a.seen + (size_t)a.nb * V;
-      a.planes = a.accb + (size_t)a.nb * V;
-      a.found = (uint32_t*)a.planes;
-      a.mass = a.found + (size_t)a.nb * lmax;
-      a.igw = (uint32_t)igw;
-      a.igb = a.mass + (size_t)a.nb * lmax;
-      const size_t zero = (char*)(a.igb + (size_t)a.nb * igw) - st;
-      a.igm = (uint64_t*)(st + align_up(zero, 256));
-      a.lev = lev;
-      HIPCHK(c, ospf::zero_async(st, zero, s));
-      if (r >= slots) HIPCHK(c, hipStreamWaitEvent(s, ev_tr[slot], 0));  // slot's trace done
-      HIPCHK(c, ospf::zero_async(lev, (size_t)a.nb * V * 64ull, s));
-      e = ospf::launch_ksp_masks(c->g, a, d_ign, d_cnt, cap, s);
-      if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_masks");
-      uint32_t d = std::max<uint32_t>(2, c->depth_bound);
-      // test knob: start with fewer levels (exercises the continuation below)
-      if (const char* x = getenv("OSPF_KSP_D0")) d = std::max(2, std::min((int)d, atoi(x)));
-      e = ospf::launch_msbfs_ksp(c->g, a, 1, d, s);
-      if (e != hipSuccess) return hip_fail(c, e, "launch_msbfs_ksp");
-      // masked runs may be deeper than the graph's bound: continue while any
-      // batch still has a frontier (levels up to 253: lev bytes hold dist + 1)
-      std::vector<uint32_t> deep;
-      for (;;) {
-        found.resize((size_t)a.nb * lmax);
-        HIPCHK(c, hipMemcpyAsync(found.data(), a.found, found.size() * 4ull, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipStreamSynchronize(s));
-        deep.clear();
-        for (uint32_t j = 0; j < a.nb; ++j)
-          if (found[(size_t)j * lmax + d]) deep.push_back(j);
-        if (deep.empty()) break;
-        if (d >= 254) {  // these runs keep OVF2: their levels stop at 254
-          for (uint32_t j : deep) {
-            const uint32_t r0 = (vb0 + j) * 64u;
-            e = ospf::launch_or_bits(k->status + r0, std::min(64u, n - r0), OSPF_KSP_OVF2, s);
-            if (e != hipSuccess) return hip_fail(c, e, "launch_or_bits");
-          }
-          break;
-        }
-        const uint32_t d1 = std::min<uint32_t>(d + 8, 254);
-        e = ospf::launch_msbfs_ksp(c->g, a, d, d1, s);
-        if (e != hipSuccess) return hip_fail(c, e, "launch_msbfs_ksp");
-        d = d1;
+  // 3: masked reruns + k = 2 over a set of runs (all of them, or the ones the
+  // decremental kernel left): the multi-source BFS with per-run ignore masks
+  // (unit metric) or per-run rows
+  auto full_reruns = [&](const uint32_t* R_dsts, uint32_t R_n, const uint32_t* R_ign,
+                         const uint32_t* R_cnt, uint32_t* R_status, uint32_t* R_k2) -> int {
+    ospf::TraceArgs t = t_k1;
+    const uint32_t total_vb = (R_n + 63) / 64;  // this set's virtual batches (<= the carve's)
+    HIPCHK(c, hipMemsetD32Async(d_roots, (int)src, ms ? R_n : chunk, s));
+    if (ms) {
+      if (!c->aux) HIPCHK(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+      while (c->ev.size() < 2 * (size_t)slots + 1) {
+        hipEvent_t x;
+        HIPCHK(c, hipEventCreateWithFlags(&x, hipEventDisableTiming));
+        c->ev.push_back(x);
       }
-      HIPCHK(c, hipEventRecord(ev_bfs[slot], s));
-      HIPCHK(c, hipStreamWaitEvent(c->aux, ev_bfs[slot], 0));
-      const uint32_t r0 = vb0 * 64u;
-      ospf::TraceArgs t2 = t;
-      t2.dsts = k->dsts + r0;
-      t2.n = std::min<uint32_t>(a.nb * 64u, n - r0);
-      t2.rows = nullptr;
-      t2.lev = lev;
-      t2.ign = d_ign + (size_t)r0 * cap;
-      t2.ign_cnt = d_cnt + r0;
-      t2.out = k->k2 + (size_t)r0 * cap;
-      t2.ign_out = nullptr;
-      t2.cnt_out = nullptr;
-      t2.status = k->status + r0;
-      t2.k = 2;
-      t2.dead = dead;
-      t2.heavy = (uint32_t*)((char*)dead + align_up((size_t)nb_max * 64ull * dw * 4ull, 256));
-      t2.heavy_ctr = t2.heavy + nb_max * 64u;
-      HIPCHK(c, ospf::zero_async(dead, (size_t)t2.n * dw * 4ull, c->aux));
-      HIPCHK(c, ospf::zero_async(t2.heavy_ctr, 8, c->aux));
-      e = ospf::launch_ksp_trace(true, c->g, t2, c->aux);
-      if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_trace k2");
-      HIPCHK(c, hipEventRecord(ev_tr[slot], c->aux));
+      hipEvent_t* ev_bfs = c->ev.data();
+      hipEvent_t* ev_tr = c->ev.data() + slots;
+      hipEvent_t ev_end = c->ev[2 * slots];
+      char* ring = st + per_vb * nb_max;
+      std::vector<uint32_t> found;
+      for (uint32_t r = 0, vb0 = 0; vb0 < total_vb; ++r, vb0 += nb_max) {
+        const uint32_t slot = r % slots;
+        uint8_t* lev = (uint8_t*)(ring + (size_t)slot * (sz_lev + sz_sdead));
+        uint32_t* dead = (uint32_t*)(ring + (size_t)slot * (sz_lev + sz_sdead) + sz_lev);
+        ospf::MsArgs a{};
+        a.roots = d_roots;
+        a.n = R_n;
+        a.W = W;
+        a.npass = 1;
+        a.R = 64;
+        a.PP = 1;
+        a.OW = 1;
+        a.rep = 1;
+        a.vb0 = vb0;
+        a.nb = std::min(nb_max, total_vb - vb0);
+        a.lmax = lmax;
+        a.kcap = nn;
+        a.push_div = 8;
+        if (const char* x = getenv("OSPF_MS_PUSH_DIV")) a.push_div = (uint32_t)std::max(0, atoi(x));
+        a.defer = 1;
+        a.err = c->d_err;
+        a.front = (uint64_t*)st;
+        a.seen = a.front + 4ull * a.nb * V;
+        a.accb = a.seen + (size_t)a.nb * V;
+        a.planes = a.accb + (size_t)a.nb * V;
+        a.found = (uint32_t*)a.planes;
+        a.mass = a.found + (size_t)a.nb * lmax;
+        a.igw = (uint32_t)igw;
+        a.igb = a.mass + (size_t)a.nb * lmax;
+        const size_t zero = (char*)(a.igb + (size_t)a.nb * igw) - st;
+        a.igm = (uint64_t*)(st + align_up(zero, 256));
+        a.lev = lev;
+        HIPCHK(c, ospf::zero_async(st, zero, s));
+        if (r >= slots) HIPCHK(c, hipStreamWaitEvent(s, ev_tr[slot], 0));  // slot's trace done
+        HIPCHK(c, ospf::zero_async(lev, (size_t)a.nb * V * 64ull, s));
+        e = ospf::launch_ksp_masks(c->g, a, R_ign, R_cnt, cap, s);
+        if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_masks");
+        uint32_t d = std::max<uint32_t>(2, c->depth_bound);
+        // test knob: start with fewer levels (exercises the continuation below)
+        if (const char* x = getenv("OSPF_KSP_D0")) d = std::max(2, std::min((int)d, atoi(x)));
+        e = ospf::launch_msbfs_ksp(c->g, a, 1, d, s);
+        if (e != hipSuccess) return hip_fail(c, e, "launch_msbfs_ksp");
+        // masked runs may be deeper than the graph's bound: continue while any
+        // batch still has a frontier (levels up to 253: lev bytes hold dist + 1)
+        std::vector<uint32_t> deep;
+        for (;;) {
+          found.resize((size_t)a.nb * lmax);
+          HIPCHK(c, hipMemcpyAsync(found.data(), a.found, found.size() * 4ull, hipMemcpyDeviceToHost, s));
+          HIPCHK(c, hipStreamSynchronize(s));
+          deep.clear();
+          for (uint32_t j = 0; j < a.nb; ++j)
+            if (found[(size_t)j * lmax + d]) deep.push_back(j);
+          if (deep.empty()) break;
+          if (d >= 254) {  // these runs keep OVF2: their levels stop at 254
+            for (uint32_t j : deep) {
+              const uint32_t r0 = (vb0 + j) * 64u;
+              e = ospf::launch_or_bits(R_status + r0, std::min(64u, R_n - r0), OSPF_KSP_OVF2, s);
+              if (e != hipSuccess) return hip_fail(c, e, "launch_or_bits");
+            }
+            break;
+          }
+          const uint32_t d1 = std::min<uint32_t>(d + 8, 254);
+          e = ospf::launch_msbfs_ksp(c->g, a, d, d1, s);
+          if (e != hipSuccess) return hip_fail(c, e, "launch_msbfs_ksp");
+          d = d1;
+        }
+        HIPCHK(c, hipEventRecord(ev_bfs[slot], s));
+        HIPCHK(c, hipStreamWaitEvent(c->aux, ev_bfs[slot], 0));
+        const uint32_t r0 = vb0 * 64u;
+        ospf::TraceArgs t2 = t;
+        t2.dsts = R_dsts + r0;
+        t2.n = std::min<uint32_t>(a.nb * 64u, R_n - r0);
+        t2.rows = nullptr;
+        t2.lev = lev;
+        t2.ign = R_ign + (size_t)r0 * cap;
+        t2.ign_cnt = R_cnt + r0;
+        t2.out = R_k2 + (size_t)r0 * cap;
+        t2.ign_out = nullptr;
+        t2.cnt_out = nullptr;
+        t2.status = R_status + r0;
+        t2.k = 2;
+        t2.dead = dead;
+        t2.heavy = (uint32_t*)((char*)dead + align_up((size_t)nb_max * 64ull * dw * 4ull, 256));
+        t2.heavy_ctr = t2.heavy + nb_max * 64u;
+        HIPCHK(c, ospf::zero_async(dead, (size_t)t2.n * dw * 4ull, c->aux));
+        HIPCHK(c, ospf::zero_async(t2.heavy_ctr, 8, c->aux));
+        e = ospf::launch_ksp_trace(true, c->g, t2, c->aux);
+        if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_trace k2");
+        HIPCHK(c, hipEventRecord(ev_tr[slot], c->aux));
+      }
+      HIPCHK(c, hipEventRecord(ev_end, c->aux));
+      HIPCHK(c, hipStreamWaitEvent(s, ev_end, 0));
+      c->spf_runs += R_n;
+    } else {
+      uint32_t* d_rows = (uint32_t*)st;
+      uint32_t* d_off = (uint32_t*)(st + align_up((size_t)chunk * V * 4ull, 256));
+      e = ospf::launch_iota(d_off, chunk, cap, s);
+      if (e != hipSuccess) return hip_fail(c, e, "launch_iota");
+      for (uint32_t r0 = 0; r0 < R_n; r0 += chunk) {
+        const uint32_t nc = std::min(chunk, R_n - r0);
+        ospf_batch b{};
+        b.d_roots = d_roots;
+        b.n_roots = nc;
+        b.d_ign_offsets = d_off;
+        b.d_ign_ids = R_ign + (size_t)r0 * cap;
+        b.max_ignored = cap;
+        b.flags = OSPF_WANT_DIST;
+        b.nh_words = W;
+        b.max_root_neighbors = nn;
+        b.d_dist = d_rows;
+        rc = ospf_run_batch_dev(c, &b, s);
+        if (rc) return rc;
+        ospf::TraceArgs t2 = t;
+        t2.dsts = R_dsts + r0;
+        t2.n = nc;
+        t2.rows = d_rows;
+        t2.row_stride = V;
+        t2.ign = R_ign + (size_t)r0 * cap;
+        t2.ign_cnt = R_cnt + r0;
+        t2.out = R_k2 + (size_t)r0 * cap;
+        t2.ign_out = nullptr;
+        t2.cnt_out = nullptr;
+        t2.status = R_status + r0;
+        t2.k = 2;
+        HIPCHK(c, ospf::zero_async(d_dead, (size_t)t2.n * dw * 4ull, s));
+        HIPCHK(c, ospf::zero_async(t2.heavy_ctr, 8, s));
+        e = ospf::launch_ksp_trace(false, c->g, t2, s);
+        if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_trace k2");
+      }
     }
-    HIPCHK(c, hipEventRecord(ev_end, c->aux));
-    HIPCHK(c, hipStreamWaitEvent(s, ev_end, 0));
-    c->spf_runs += n;
-  } else {
-    uint32_t* d_rows = (uint32_t*)st;
-    uint32_t* d_off = (uint32_t*)(st + align_up((size_t)chunk * V * 4ull, 256));
-    e = ospf::launch_iota(d_off, chunk, cap, s);
-    if (e != hipSuccess) return hip_fail(c, e, "launch_iota");
-    for (uint32_t r0 = 0; r0 < n; r0 += chunk) {
-      const uint32_t nc = std::min(chunk, n - r0);
-      ospf_batch b{};
-      b.d_roots = d_roots;
-      b.n_roots = nc;
-      b.d_ign_offsets = d_off;
-      b.d_ign_ids = d_ign + (size_t)r0 * cap;
-      b.max_ignored = cap;
-      b.flags = OSPF_WANT_DIST;
-      b.nh_words = W;
-      b.max_root_neighbors = nn;
-      b.d_dist = d_rows;
-      rc = ospf_run_batch_dev(c, &b, s);
-      if (rc) return rc;
-      ospf::TraceArgs t2 = t;
-      t2.dsts = k->dsts + r0;
-      t2.n = nc;
-      t2.rows = d_rows;
-      t2.row_stride = V;
-      t2.ign = d_ign + (size_t)r0 * cap;
-      t2.ign_cnt = d_cnt + r0;
-      t2.out = k->k2 + (size_t)r0 * cap;
-      t2.ign_out = nullptr;
-      t2.cnt_out = nullptr;
-      t2.status = k->status + r0;
-      t2.k = 2;
-      HIPCHK(c, ospf::zero_async(d_dead, (size_t)t2.n * dw * 4ull, s));
-      HIPCHK(c, ospf::zero_async(t2.heavy_ctr, 8, s));
-      e = ospf::launch_ksp_trace(false, c->g, t2, s);
-      if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_trace k2");
+    return OSPF_OK;
+  };
+  if (getenv("OSPF_KSP_NODECR")) return full_reruns(k->dsts, n, d_ign, d_cnt, k->status, k->k2);
+  // decremental reruns (spf_ksp2.hip): the source's row + per-run lost
+  // supports; the runs past its budgets through full_reruns, compacted
+  {
+    const size_t dwb = align_up((size_t)dw * 4ull, 256);
+    const uint32_t nblk = std::max<uint32_t>(1, ospf::ksp_decr_blocks_per_cu() * (uint32_t)c->n_cu);
+    const uint32_t hblk = 2u * (uint32_t)c->n_cu;  // ksp_decr_heavy_kernel: 2 per CU
+    const size_t sz_tc = align_up(V * 4ull, 256), sz_fb = align_up(n * 4ull, 256), sz_ctr = 256,
+                 sz_dd = dwb * std::max(nblk, hblk);
+    char* dp = stream_scratch(c, s, sz_tc + 2 * sz_fb + sz_ctr + sz_dd, &rc, 2);
+    if (rc) return rc;
+    uint32_t* d_tc = (uint32_t*)dp;
+    uint32_t* d_fb = (uint32_t*)(dp + sz_tc);
+    uint32_t* d_hq = (uint32_t*)(dp + sz_tc + sz_fb);
+    uint32_t* d_ctr = (uint32_t*)(dp + sz_tc + 2 * sz_fb);
+    uint32_t* d_dd = (uint32_t*)(dp + sz_tc + 2 * sz_fb + sz_ctr);
+    HIPCHK(c, ospf::zero_async(d_ctr, 32, s));
+    e = ospf::launch_ksp_hint(c->g, src, d_dist1, d_tc, s);
+    if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_hint");
+    ospf::TraceArgs td = t_k1;
+    td.rows = d_dist1;
+    td.row_stride = 0;
+    td.lev = nullptr;
+    td.ign = d_ign;
+    td.ign_cnt = d_cnt;
+    td.out = k->k2;
+    td.ign_out = nullptr;
+    td.cnt_out = nullptr;
+    td.status = k->status;
+    td.k = 2;
+    td.dead = d_dd;
+    td.dead_words = (uint32_t)(dwb / 4);
+    td.tc = d_tc;
+    td.fb = d_fb;
+    td.ctr = d_ctr;
+    td.heavy = d_hq;
+    td.heavy_ctr = d_ctr + 4;
+    td.err = c->d_err;
+    e = ospf::launch_ksp_decr(c->g, td, nblk, s);
+    if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_decr");
+    if (td.budget) {
+      e = ospf::launch_ksp_decr_heavy(c->g, td, hblk, s);
+      if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_decr_heavy");
     }
+    uint32_t ctr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    HIPCHK(c, hipMemcpyAsync(ctr, d_ctr, 32, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    if (getenv("OSPF_KSP_DEBUG"))
+      fprintf(stderr, "ksp2 decr: runs %u decided %u fallbacks %u (A %u, map %u) heavy %u affected %u\n",
+              n, ctr[2], ctr[1], ctr[6], ctr[7], ctr[4], ctr[3]);
+    c->ksp_decr_stats[0] += ctr[2];
+    c->ksp_decr_stats[1] += ctr[1];
+    c->ksp_decr_stats[2] += ctr[3];
+    const uint32_t nfb = ctr[1];
+    c->spf_runs += n - nfb;  // (full_reruns counts its own)
+    if (nfb == 0) return OSPF_OK;
+    // compact the fallbacks: dsts, status, ignore sets, counts; k2 records back
+    const size_t sz_fd = align_up(nfb * 4ull, 256), sz_fr = align_up((size_t)nfb * cap * 4ull, 256);
+    char* fp = stream_scratch(c, s, 3 * sz_fd + 2 * sz_fr, &rc, 3);
+    if (rc) return rc;
+    uint32_t* f_dsts = (uint32_t*)fp;
+    uint32_t* f_status = (uint32_t*)(fp + sz_fd);
+    uint32_t* f_cnt = (uint32_t*)(fp + 2 * sz_fd);
+    uint32_t* f_ign = (uint32_t*)(fp + 3 * sz_fd);
+    uint32_t* f_k2 = (uint32_t*)(fp + 3 * sz_fd + sz_fr);
+    if ((e = ospf::launch_rows_gather(f_dsts, k->dsts, d_fb, nfb, 1, true, s)) != hipSuccess ||
+        (e = ospf::launch_rows_gather(f_status, k->status, d_fb, nfb, 1, true, s)) != hipSuccess ||
+        (e = ospf::launch_rows_gather(f_cnt, d_cnt, d_fb, nfb, 1, true, s)) != hipSuccess ||
+        (e = ospf::launch_rows_gather(f_ign, d_ign, d_fb, nfb, cap, true, s)) != hipSuccess)
+      return hip_fail(c, e, "launch_rows_gather");
+    rc = full_reruns(f_dsts, nfb, f_ign, f_cnt, f_status, f_k2);
+    if (rc) return rc;
+    if ((e = ospf::launch_rows_gather(k->status, f_status, d_fb, nfb, 1, false, s)) != hipSuccess ||
+        (e = ospf::launch_rows_gather(k->k2, f_k2, d_fb, nfb, cap, false, s)) != hipSuccess)
+      return hip_fail(c, e, "launch_rows_gather");
   }
   return OSPF_OK;
 }
@@ -1527,6 +1612,7 @@ int ospf_sync(ospf_ctx* c, void* stream) {
                 : (err & 128u) ? "leaf derive: a group's roots do not share their slot table"
                 : (err & 256u) ? "twin derive: a root's neighbours span more than 16 twin classes"
                 : (err & 512u) ? "wderive: a metric above 65534 in a > 4-word next-hop derivation"
+                : (err & 2048u) ? "internal: a heavy KSP2 run no longer fits the decremental budgets"
                              : "internal: a frontier entry out of range");
   }
   return OSPF_OK;
@@ -2312,6 +2398,12 @@ int ospf_ksp2_dev(ospf_ctx* c, const ospf_ksp2* k, void* stream) {
   if (c->dist_bound >= 0xFFFFFFFFull)
     return fail(c, OSPF_E_RANGE, "u32 distance overflow possible (sum of per-node max metrics)");
   return run_ksp2(c, k, (hipStream_t)stream);
+}
+
+int ospf_ksp2_stats(const ospf_ctx* c, uint64_t* out) {
+  if (!c || !out) return OSPF_E_INVAL;
+  for (int i = 0; i < 3; ++i) out[i] = c->ksp_decr_stats[i];
+  return OSPF_OK;
 }
 
 int ospf_ksp2_run(ospf_ctx* c, const ospf_ksp2* k) {

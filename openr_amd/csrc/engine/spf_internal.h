@@ -18,6 +18,7 @@ struct ospf_ctx {
   int n_cu = 256;
   std::string err;
   uint64_t spf_runs = 0;
+  uint64_t ksp_decr_stats[3] = {0, 0, 0};  // ospf_ksp2_stats
   // graph
   bool loaded = false;
   ospf_graph_info info{};

@@ -631,8 +631,32 @@ struct TraceArgs {
   uint32_t budget;          // DFS steps before a run goes to the heavy kernel (0 = none)
   uint32_t* heavy;          // [n] queued run indices
   uint32_t* heavy_ctr;      // [2] {queued, taken}, zeroed by the caller
+  // decremental reruns (launch_ksp_decr): rows = the source's dist row
+  const uint32_t* tc;       // [V] hint: link of each node's first support (launch_ksp_hint)
+  uint32_t* fb;             // [n] runs left to the full masked reruns
+  uint32_t* ctr;            // [8] {next run, fallbacks, runs decided, affected nodes, heavy
+                            //  queued / taken, A overflows, hash overflows}, zeroed
+  uint32_t* err;            // the engine's device error word
 };
 hipError_t launch_ksp_trace(bool lev, const DevGraph& g, const TraceArgs& t, hipStream_t s);
+// KSP2 k = 2 by decremental SSSP (spf_ksp2.hip): hint[v] = the link id of
+// v's first usable in-link (u, v) in row order with u transit (or the
+// source) and dist(u) + w(u -> v) == dist(v) in the source's dist row
+hipError_t launch_ksp_hint(const DevGraph& g, uint32_t src, const uint32_t* dist, uint32_t* hint,
+                           hipStream_t s);
+// each run's masked distances from the source's row by propagating the lost
+// tight supports of its ignored links, then its k = 2 trace over them;
+// runs beyond the kernel's LDS budgets are listed in t.fb (t.ctr[1] of them)
+// for the full masked reruns. t.dead: [blocks][dead_words], zeroed.
+hipError_t launch_ksp_decr(const DevGraph& g, const TraceArgs& t, uint32_t blocks, hipStream_t s);
+uint32_t ksp_decr_blocks_per_cu();
+// the runs ksp_decr queued as heavy (t.heavy / t.heavy_ctr): 16 waves each;
+// t.dead: [blocks][dead_words]; t.err: the engine's error word
+hipError_t launch_ksp_decr_heavy(const DevGraph& g, const TraceArgs& t, uint32_t blocks,
+                                 hipStream_t s);
+// a[j][0 .. w) = b[idx[j]][0 .. w) (gather = true) or a[idx[j]] = b[j] (scatter), j < n
+hipError_t launch_rows_gather(uint32_t* a, const uint32_t* b, const uint32_t* idx, uint32_t n,
+                              uint32_t w, bool gather, hipStream_t s);
 // st[i] |= bits, i < n
 hipError_t launch_or_bits(uint32_t* st, uint32_t n, uint32_t bits, hipStream_t s);
 // incremental updates (spf_update.hip): base[idx[i]] = val[i]; affected runs

@@ -77,19 +77,32 @@ __device__ __forceinline__ uint64_t wave_min64(uint64_t x) {
   return x;
 }
 
-template <bool LEV>
-__device__ __forceinline__ uint32_t dist_of(const DevGraph& g, const TraceArgs& t, uint32_t i,
-                                            uint32_t u) {
-  if (LEV) {
-    const uint32_t l = t.lev[((size_t)(i >> 6) * g.V + u) * 64u + (i & 63u)];
+// distance sources of a run's trace: the source's (or a run's) dist row, the
+// level bytes of the multi-source BFS, or the decremental form (below)
+struct DistRows {
+  const uint32_t* row;
+  __device__ uint32_t operator()(uint32_t u) const { return row[u]; }
+};
+struct DistLev {
+  const uint8_t* lev;  // the run's byte at [u][64]
+  __device__ uint32_t operator()(uint32_t u) const {
+    const uint32_t l = lev[(size_t)u * 64u];
     return l ? l - 1u : kInf;
   }
-  return t.rows[(size_t)i * t.row_stride + u];
+};
+template <bool LEV>
+__device__ __forceinline__ auto dist_src(const DevGraph& g, const TraceArgs& t, uint32_t i) {
+  if constexpr (LEV) {
+    return DistLev{t.lev + (size_t)(i >> 6) * g.V * 64u + (i & 63u)};
+  } else {
+    return DistRows{t.rows + (size_t)i * t.row_stride};
+  }
 }
 
 // the DFS of one run (one wave); see the file comment
-template <bool LEV>
+template <class DS, uint32_t HS = kHash>
 struct Tracer {
+  static constexpr uint32_t kHS = HS, kHM = HS / 4u * 3u;  // claim slots, claims allowed
   const DevGraph& g;
   const TraceArgs& t;
   uint32_t i, lane, src, dst;
@@ -97,14 +110,15 @@ struct Tracer {
   uint32_t nign;
   volatile uint32_t* hs;  // claimed links (the paths found), kHash slots
   uint32_t* dead;
+  DS ds;
 
-  __device__ uint32_t dist(uint32_t u) const { return dist_of<LEV>(g, t, i, u); }
+  __device__ uint32_t dist(uint32_t u) const { return ds(u); }
   __device__ static uint32_t hslot(uint32_t lid) {
     return (uint32_t)(((uint64_t)lid * 0x9E3779B97F4A7C15ull) >> 40);
   }
   __device__ bool claimed(uint32_t lid) const {  // per lane
     for (uint32_t h = hslot(lid);; ++h) {
-      const uint32_t x = hs[h & (kHash - 1u)];
+      const uint32_t x = hs[h & (kHS - 1u)];
       if (x == lid + 1u) return true;
       if (x == 0u) return false;
     }
@@ -112,7 +126,7 @@ struct Tracer {
   __device__ void claim(uint32_t lid) const {  // wave-uniform lid, not yet claimed
     const uint32_t h = hslot(lid);
     for (uint32_t p0 = 0;; p0 += kWave) {
-      const uint32_t slot = (h + p0 + lane) & (kHash - 1u);
+      const uint32_t slot = (h + p0 + lane) & (kHS - 1u);
       const uint64_t em = __ballot(hs[slot] == 0u);
       if (em) {
         if (lane == (uint32_t)(__ffsll((unsigned long long)em) - 1)) hs[slot] = lid + 1u;
@@ -235,7 +249,7 @@ struct Tracer {
   // append the path on the stack to the record at word w, claim its links
   __device__ bool emit(uint32_t* out, volatile uint32_t* stk, uint32_t depth, uint32_t& w,
                        uint32_t& npaths, uint32_t& nclaim) const {
-    if (w + 1u + depth > t.stride || nclaim + depth > kHashMax) return false;
+    if (w + 1u + depth > t.stride || nclaim + depth > kHM) return false;
     // path from src to dst: the stack bottom-up is dst -> src
     for (uint32_t k = lane; k < depth; k += kWave) out[w + 1u + k] = g.link_id[stk[depth - 1u - k]];
     if (lane == 0) out[w] = depth;
@@ -282,9 +296,9 @@ struct Tracer {
 
 // run setup shared by both kernels: false = nothing to trace (record and
 // status already final)
-template <bool LEV>
+template <class DS, uint32_t HS>
 __device__ bool trace_setup(const DevGraph& g, const TraceArgs& t, uint32_t i, uint32_t lane,
-                            Tracer<LEV>& tr) {
+                            Tracer<DS, HS>& tr) {
   uint32_t* out = t.out + (size_t)i * t.stride;
   tr.ign = nullptr;
   tr.nign = 0;
@@ -326,9 +340,10 @@ __global__ void __launch_bounds__(256) ksp_trace_kernel(DevGraph g, TraceArgs t)
   const uint32_t i = blockIdx.x * kWaves + wv;
   if (i >= t.n) return;
   volatile uint32_t* stk = s_stack[wv];
-  Tracer<LEV> tr{g, t, i, lane, t.src, t.dsts[i], nullptr, 0, s_hash[wv],
-                 t.dead + (size_t)i * t.dead_words};
-  if (!trace_setup<LEV>(g, t, i, lane, tr)) return;
+  Tracer<decltype(dist_src<LEV>(g, t, i))> tr{g, t, i, lane, t.src, t.dsts[i], nullptr, 0,
+                                              s_hash[wv], t.dead + (size_t)i * t.dead_words,
+                                              dist_src<LEV>(g, t, i)};
+  if (!trace_setup(g, t, i, lane, tr)) return;
   for (uint32_t k = lane; k < kHash; k += kWave) tr.hs[k] = 0u;
   uint32_t* out = t.out + (size_t)i * t.stride;
   uint32_t npaths = 0, w = 1, steps = 0, nclaim = 0;
@@ -357,119 +372,598 @@ __global__ void __launch_bounds__(256) ksp_trace_kernel(DevGraph g, TraceArgs t)
 // reaches src is the reference's choice (every earlier one failed). Blocks
 // take runs from the queue until it is empty.
 constexpr uint32_t kHeavyWaves = 16;
+struct HeavyLds {
+  uint32_t stack[kHeavyWaves][kStack];
+  uint64_t cand[kHeavyWaves];
+  int32_t res[kHeavyWaves];
+  uint32_t ctl[4];
+};
+// the 16-wave trace of run i, resuming from its record; `hs` = the block's
+// claim hash (kHash slots), every wave of the block calls it
+template <class DS>
+__device__ void heavy_trace(const DevGraph& g, const TraceArgs& t, uint32_t i, Tracer<DS, kHash>& tr,
+                            uint32_t* hs, HeavyLds& H) {
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  uint32_t* out = t.out + (size_t)i * t.stride;
+  for (uint32_t k = threadIdx.x; k < kHash; k += blockDim.x) hs[k] = 0u;
+  __syncthreads();
+  // resume: the paths the single-wave pass found
+  uint32_t npaths = 0, w = 1, nclaim = 0;
+  if (wv == 0) {
+    npaths = out[0];
+    for (uint32_t p = 0; p < npaths; ++p) {
+      const uint32_t len = out[w];
+      for (uint32_t k = 0; k < len; ++k) tr.claim(out[w + 1u + k]);
+      nclaim += len;
+      w += 1u + len;
+    }
+  }
+  __syncthreads();
+  bool ovf = false;
+  uint32_t steps = 0;
+  for (;;) {  // one traceOnePath per iteration
+    if (wv == 0) H.ctl[1] = tr.src_open() ? 1u : 0u;
+    __syncthreads();
+    if (!H.ctl[1]) break;
+    uint64_t lo = 0;
+    int winner = -1;
+    bool stop = false;
+    for (;;) {  // dst's candidates, 16 at a time
+      if (wv == 0) {  // the next (up to) 16 candidates of dst in row order
+        uint32_t m = 0;
+        const uint32_t dv = tr.dist(tr.dst);
+        const uint32_t beg = g.row_ptr[tr.dst], end = g.row_ptr[tr.dst + 1];
+        uint32_t base = lo ? max(beg, (uint32_t)lo) : beg;
+        for (; base < end && m < kHeavyWaves; base += kWave) {
+          const uint32_t e = base + lane;
+          uint32_t du = 0;
+          const bool ok = e < end && tr.cand(tr.dst, dv, e, du);
+          const uint64_t bal = __ballot(ok);
+          const uint32_t rank = m + __popcll(bal & ((1ull << lane) - 1ull));
+          if (ok && rank < kHeavyWaves) H.cand[rank] = ((uint64_t)(dv - 1u) << 32) | e;
+          const uint32_t got = m + (uint32_t)__popcll(bal);
+          if (got >= kHeavyWaves) {  // resume after the 16th
+            uint64_t b2 = bal;
+            for (uint32_t k = m; k < kHeavyWaves - 1u; ++k) b2 &= b2 - 1ull;
+            base += (uint32_t)(__ffsll((unsigned long long)b2) - 1) + 1u - kWave;
+            m = kHeavyWaves;
+            base += kWave;
+            break;
+          }
+          m = got;
+        }
+        lo = ((uint64_t)(dv - 1u) << 32) | min(base, end);
+        H.ctl[2] = m;
+      }
+      __syncthreads();
+      const uint32_t m = H.ctl[2];
+      if (m == 0) {
+        stop = true;
+        break;
+      }
+      if (wv < m) {
+        uint32_t depth = 1, st2 = 0;
+        H.stack[wv][0] = (uint32_t)H.cand[wv];
+        const int r = tr.dfs(H.stack[wv], depth, 1, st2, kSteps);
+        if (lane == 0) H.res[wv] = r == 1 ? (int32_t)depth : (r < 0 ? -1 : 0);
+      }
+      __syncthreads();
+      uint32_t k = 0;
+      for (; k < m; ++k)
+        if (H.res[k] != 0) break;
+      if (k < m) {
+        if (H.res[k] < 0) ovf = true;
+        else winner = (int)k;
+        break;
+      }
+    }
+    __syncthreads();
+    if (ovf || stop || winner < 0) break;
+    if (wv == 0 && !tr.emit(out, H.stack[winner], (uint32_t)H.res[winner], w, npaths, nclaim))
+      H.ctl[3] = 1u;
+    else if (wv == 0)
+      H.ctl[3] = 0u;
+    __syncthreads();
+    if (H.ctl[3]) {
+      ovf = true;
+      break;
+    }
+    if (++steps > kSteps) {
+      ovf = true;
+      break;
+    }
+  }
+  __syncthreads();
+  if (wv == 0) tr.finish(out, npaths, ovf, hs);
+  __syncthreads();
+}
+
+// Heavy runs (the DFS took more than the budget, e.g. a spine behind 1,780
+// pods): a workgroup of 16 waves per run, resuming from the paths already in
+// its record. Each traceOnePath takes dst's candidates 16 at a time in order;
+// wave j searches below candidate j with the same claims and shared dead
+// marks (facts: a node once dead stays dead), and the lowest candidate that
+// reaches src is the reference's choice (every earlier one failed). Blocks
+// take runs from the queue until it is empty.
 template <bool LEV>
 __global__ void __launch_bounds__(1024) ksp_heavy_kernel(DevGraph g, TraceArgs t) {
   __shared__ uint32_t s_hash[kHash];
-  __shared__ uint32_t s_stack[kHeavyWaves][kStack];
-  __shared__ uint64_t s_cand[kHeavyWaves];
-  __shared__ int32_t s_res[kHeavyWaves];
-  __shared__ uint32_t s_ctl[4];
-  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  __shared__ HeavyLds H;
+  const uint32_t lane = threadIdx.x & 63u;
   for (;;) {
     if (threadIdx.x == 0) {
       const uint32_t q = atomicAdd(&t.heavy_ctr[1], 1u);
-      s_ctl[0] = q < __hip_atomic_load(&t.heavy_ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+      H.ctl[0] = q < __hip_atomic_load(&t.heavy_ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                      ? t.heavy[q] : kInf;
     }
     __syncthreads();
-    const uint32_t i = s_ctl[0];
+    const uint32_t i = H.ctl[0];
+    __syncthreads();
     if (i == kInf) return;
-    uint32_t* out = t.out + (size_t)i * t.stride;
-    Tracer<LEV> tr{g, t, i, lane, t.src, t.dsts[i], nullptr, 0, s_hash,
-                   t.dead + (size_t)i * t.dead_words};
-    trace_setup<LEV>(g, t, i, lane, tr);  // (a queued run always has work)
-    for (uint32_t k = threadIdx.x; k < kHash; k += blockDim.x) s_hash[k] = 0u;
-    __syncthreads();
-    // resume: the paths the single-wave pass found
-    uint32_t npaths = 0, w = 1, nclaim = 0;
-    if (wv == 0) {
-      npaths = out[0];
-      for (uint32_t p = 0; p < npaths; ++p) {
-        const uint32_t len = out[w];
-        for (uint32_t k = 0; k < len; ++k) tr.claim(out[w + 1u + k]);
-        nclaim += len;
-        w += 1u + len;
-      }
-    }
-    __syncthreads();
-    bool ovf = false;
-    uint32_t steps = 0;
-    for (;;) {  // one traceOnePath per iteration
-      if (wv == 0) s_ctl[1] = tr.src_open() ? 1u : 0u;
-      __syncthreads();
-      if (!s_ctl[1]) break;
-      uint64_t lo = 0;
-      int winner = -1;
-      bool stop = false;
-      for (;;) {  // dst's candidates, 16 at a time
-        if (wv == 0) {  // the next (up to) 16 candidates of dst in row order
-          uint32_t m = 0;
-          const uint32_t dv = tr.dist(tr.dst);
-          const uint32_t beg = g.row_ptr[tr.dst], end = g.row_ptr[tr.dst + 1];
-          uint32_t base = lo ? max(beg, (uint32_t)lo) : beg;
-          for (; base < end && m < kHeavyWaves; base += kWave) {
-            const uint32_t e = base + lane;
-            uint32_t du = 0;
-            const bool ok = e < end && tr.cand(tr.dst, dv, e, du);
-            const uint64_t bal = __ballot(ok);
-            const uint32_t rank = m + __popcll(bal & ((1ull << lane) - 1ull));
-            if (ok && rank < kHeavyWaves) s_cand[rank] = ((uint64_t)(dv - 1u) << 32) | e;
-            const uint32_t got = m + (uint32_t)__popcll(bal);
-            if (got >= kHeavyWaves) {  // resume after the 16th
-              uint64_t b2 = bal;
-              for (uint32_t k = m; k < kHeavyWaves - 1u; ++k) b2 &= b2 - 1ull;
-              base += (uint32_t)(__ffsll((unsigned long long)b2) - 1) + 1u - kWave;
-              m = kHeavyWaves;
-              base += kWave;
-              break;
-            }
-            m = got;
-          }
-          lo = ((uint64_t)(dv - 1u) << 32) | min(base, end);
-          s_ctl[2] = m;
-        }
-        __syncthreads();
-        const uint32_t m = s_ctl[2];
-        if (m == 0) {
-          stop = true;
-          break;
-        }
-        if (wv < m) {
-          uint32_t depth = 1, st2 = 0;
-          s_stack[wv][0] = (uint32_t)s_cand[wv];
-          const int r = tr.dfs(s_stack[wv], depth, 1, st2, kSteps);
-          if (lane == 0) s_res[wv] = r == 1 ? (int32_t)depth : (r < 0 ? -1 : 0);
-        }
-        __syncthreads();
-        uint32_t k = 0;
-        for (; k < m; ++k)
-          if (s_res[k] != 0) break;
-        if (k < m) {
-          if (s_res[k] < 0) ovf = true;
-          else winner = (int)k;
-          break;
-        }
-      }
-      __syncthreads();
-      if (ovf || stop || winner < 0) break;
-      if (wv == 0 && !tr.emit(out, s_stack[winner], (uint32_t)s_res[winner], w, npaths, nclaim))
-        s_ctl[3] = 1u;
-      else if (wv == 0)
-        s_ctl[3] = 0u;
-      __syncthreads();
-      if (s_ctl[3]) {
-        ovf = true;
-        break;
-      }
-      if (++steps > kSteps) {
-        ovf = true;
-        break;
-      }
-    }
-    __syncthreads();
-    if (wv == 0) tr.finish(out, npaths, ovf, s_hash);
-    __syncthreads();
+    Tracer<decltype(dist_src<LEV>(g, t, i))> tr{g, t, i, lane, t.src, t.dsts[i], nullptr, 0, s_hash,
+                                                t.dead + (size_t)i * t.dead_words,
+                                                dist_src<LEV>(g, t, i)};
+    trace_setup(g, t, i, lane, tr);  // (a queued run always has work)
+    heavy_trace(g, t, i, tr, s_hash, H);
   }
+}
+
+// ---------------------------------------------------------------- decremental reruns
+// The k = 2 rerun of destination d is runSpf(src, true, I_d) with I_d the
+// links of d's k = 1 paths (LinkState.cpp:797-805). Removing links only
+// lengthens paths, and a node keeps its distance iff one of its supports --
+// tight in-links (u, v) of the source's SPF: u transit or src, dist(u) +
+// w(u -> v) == dist(v) -- survives with u unaffected. The affected set A is
+// the fixed point of lost supports: an ignored link loses its tight
+// directions, an affected node loses its tight out-links. Each node has a
+// hint, the link of its first support (ksp_hint_kernel); a lost support that
+// is not a node's hint changes nothing while the hint stands, so a node gets
+// an LDS entry only once its hint is lost: then its surviving supports are
+// counted once (tails unaffected, or affected and not yet expanded -- those
+// decrement it when they are), and it joins A when the count reaches zero.
+// On the fabric a rack's run touches ~2 nodes (F100k) where the full rerun
+// scans the whole graph. The masked distances of A: its boundary terms
+// (unaffected transit in-neighbours over usable, unignored links), then
+// Bellman-Ford rounds over links inside A; every other node keeps the
+// source's distance (DistDecr). The k = 2 trace then runs over them. Runs
+// past the LDS budgets (A, hash, ignore list, claimed links) go to the full
+// masked reruns; traces past the step budget to the 16-wave kernel.
+constexpr uint32_t kAffFlag = 0x80000000u;
+__device__ __forceinline__ uint32_t dslot(uint32_t u) { return (u * 0x9E3779B1u) >> 20; }
+
+template <uint32_t MAP, uint32_t AFF, uint32_t IGN, uint32_t HS>
+struct DecrLdsT {
+  static constexpr uint32_t kMap = MAP, kFill = MAP / 4u * 3u, kAff = AFF, kIgn = IGN, kHS = HS;
+  uint32_t keys[MAP];  // node + 1 (0: empty)
+  uint32_t vals[MAP];  // supports left (hint lost), or kAffFlag | index in aff
+  uint32_t aff[AFF];
+  uint32_t dp[AFF];    // masked distance of aff[k]
+  uint32_t ign[IGN];
+  uint32_t hash[HS];   // the trace's claimed links
+  uint32_t stack[kStack];
+  uint32_t pend[64];   // nodes whose hint was just lost (their supports to count)
+  uint32_t nkeys, naff, ovf, run, npend;
+};
+using DecrSmall = DecrLdsT<512, 192, 256, 512>;     // ~10 KB: ~16 runs per CU in flight
+using DecrHeavy = DecrLdsT<4096, 1024, 1024, kHash>;
+
+template <class L_>
+struct DistDecr {
+  const uint32_t* D;  // the source's dist row
+  const L_* L;
+  __device__ uint32_t operator()(uint32_t u) const {
+    const volatile uint32_t* keys = L->keys;
+    for (uint32_t h = dslot(u);; ++h) {
+      const uint32_t k = keys[h & (L_::kMap - 1u)];
+      if (k == u + 1u) {
+        const uint32_t v = ((const volatile uint32_t*)L->vals)[h & (L_::kMap - 1u)];
+        return (v & kAffFlag) ? ((const volatile uint32_t*)L->dp)[v & ~kAffFlag] : D[u];
+      }
+      if (k == 0u) return D[u];
+    }
+  }
+};
+
+// hint[v] = link id of v's first support in row order (kInf: none)
+__global__ void __launch_bounds__(256) ksp_hint_kernel(DevGraph g, uint32_t src,
+                                                       const uint32_t* __restrict__ D,
+                                                       uint32_t* __restrict__ hint) {
+  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= g.V) return;
+  const uint32_t dv = D[v];
+  uint32_t h = kInf;
+  if (dv != kInf && v != src) {
+    for (uint32_t e = g.row_ptr[v]; e < g.row_ptr[v + 1]; ++e) {
+      const uint32_t u = g.colx[e];
+      if ((u & kDown) || u == v) continue;
+      const uint32_t du = D[u];
+      if (du == kInf || (uint64_t)du + g.rw[e] != dv) continue;
+      if (u != src && ((g.nt_bits[u >> 5] >> (u & 31u)) & 1u)) continue;
+      h = g.link_id[e];
+      break;
+    }
+  }
+  hint[v] = h;
+}
+
+template <class L_>
+__device__ __forceinline__ uint32_t map_find(const L_& L, uint32_t u) {  // slot, kInf: absent
+  const volatile uint32_t* keys = L.keys;
+  for (uint32_t h = dslot(u);; ++h) {
+    const uint32_t k = keys[h & (L_::kMap - 1u)];
+    if (k == u + 1u) return h & (L_::kMap - 1u);
+    if (k == 0u) return kInf;
+  }
+}
+// index of u in A, kInf: not affected
+template <class L_>
+__device__ __forceinline__ uint32_t aff_ix(const L_& L, uint32_t u) {
+  const uint32_t sl = map_find(L, u);
+  if (sl == kInf) return kInf;
+  const uint32_t v = ((const volatile uint32_t*)L.vals)[sl];
+  return (v & kAffFlag) ? (v & ~kAffFlag) : kInf;
+}
+// a new key (this lane's node u, not present): its slot, kInf on overflow
+template <class L_>
+__device__ __forceinline__ uint32_t map_insert(L_& L, uint32_t u) {
+  volatile uint32_t* keys = L.keys;
+  uint32_t h = dslot(u);
+  for (uint32_t p = 0; p < L_::kMap; ++p, ++h) {
+    const uint32_t sl = h & (L_::kMap - 1u);
+    if (keys[sl] != 0u) {
+      if (keys[sl] == u + 1u) return sl;
+      continue;
+    }
+    const uint32_t old = atomicCAS(&L.keys[sl], 0u, u + 1u);
+    if (old == 0u) {
+      if (atomicAdd(&L.nkeys, 1u) >= L_::kFill) L.ovf = 1u;
+      return sl;
+    }
+    if (old == u + 1u) return sl;
+  }
+  L.ovf = 1u;
+  return kInf;
+}
+template <class L_>
+__device__ __forceinline__ void make_affected(L_& L, uint32_t slot, uint32_t v) {
+  const uint32_t k = atomicAdd(&L.naff, 1u);
+  if (k >= L_::kAff) {
+    L.ovf = 1u;
+    return;
+  }
+  L.aff[k] = v;
+  L.vals[slot] = kAffFlag | k;
+}
+
+// Steps (0)-(3) of run i by one wave into L; false: past a budget (the full
+// rerun). na = |A|, or kInf when the ignored links cut the source off.
+template <class L_>
+__device__ bool decr_prepare(L_& L, const DevGraph& g, const TraceArgs& t, uint32_t i,
+                             uint32_t lane, uint32_t& nign, uint32_t& na) {
+  const uint32_t* D = t.rows;
+  const uint32_t* hint = t.tc;
+  const uint32_t src = t.src;
+  auto transit = [&](uint32_t u) { return u == src || !((g.nt_bits[u >> 5] >> (u & 31u)) & 1u); };
+  auto ignored = [&](uint32_t lid) { return nign && in_sorted(L.ign, nign, lid); };
+  const uint32_t* gign = t.ign + (size_t)i * t.stride;
+  nign = min(t.ign_cnt[i], t.stride);
+  if (nign > L_::kIgn) return false;
+  for (uint32_t k = lane; k < L_::kMap; k += kWave) {
+    L.keys[k] = 0u;
+    L.vals[k] = 0u;
+  }
+  for (uint32_t k = lane; k < nign; k += kWave) L.ign[k] = gign[k];
+  if (lane == 0) {
+    L.nkeys = 0u;
+    L.naff = 0u;
+    L.ovf = 0u;
+    L.npend = 0u;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  // (0) the ignored links may cut every usable link of the source: then the
+  // rerun reaches nothing but src
+  {
+    bool open = false;
+    for (uint32_t e = g.row_ptr[src] + lane; e < g.row_ptr[src + 1]; e += kWave) {
+      const uint32_t x = g.colx[e];
+      if (!(x & kDown) && x != src && !ignored(g.link_id[e])) open = true;
+    }
+    if (!__ballot(open)) {
+      na = kInf;
+      return true;
+    }
+  }
+  volatile uint32_t* vpend = L.pend;
+  // count the supports of the pending nodes (their hint just lost): tails
+  // unaffected, or affected and not yet expanded (index >= qexp, the count
+  // of expanded nodes); none -> A
+  auto settle_pending = [&](uint32_t qexp) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t np = min(((volatile uint32_t&)L.npend), 64u);
+    if (((volatile uint32_t&)L.npend) > 64u) L.ovf = 1u;
+    for (uint32_t j = 0; j < np; ++j) {
+      const uint32_t x = vpend[j];
+      const uint32_t dx = D[x];
+      uint32_t cnt = 0;
+      for (uint32_t e = g.row_ptr[x] + lane; e < g.row_ptr[x + 1]; e += kWave) {
+        const uint32_t u = g.colx[e];
+        if ((u & kDown) || u == x) continue;
+        const uint32_t du = D[u];
+        if (du == kInf || (uint64_t)du + g.rw[e] != dx || !transit(u)) continue;
+        if (ignored(g.link_id[e])) continue;
+        const uint32_t ui = aff_ix(L, u);
+        if (ui != kInf && ui < qexp) continue;  // lost already (expanded)
+        ++cnt;
+      }
+      for (int o = 32; o > 0; o >>= 1) cnt += (uint32_t)__shfl_xor((int)cnt, o, kWave);
+      if (lane == 0) {
+        const uint32_t sl = map_find(L, x);
+        if (cnt == 0u) make_affected(L, sl, x);
+        else L.vals[sl] = cnt;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (lane == 0) L.npend = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+  };
+  // the support (., x) over link lid is lost: the hint -> x pending; else a
+  // counted support of a settled x -> one fewer. While x is pending, only
+  // the node being expanded loses supports of x, and the settle does not
+  // count them.
+  constexpr uint32_t kPend = 0x7FFFFFFFu;
+  auto lose = [&](uint32_t x, uint32_t lid, bool is_ign) {
+    const bool is_hint = hint[x] == lid;
+    const uint32_t sl = map_find(L, x);
+    if (is_hint) {
+      if (sl != kInf) return;  // (cannot happen: a hint is lost once)
+      const uint32_t ns = map_insert(L, x);
+      if (ns == kInf) return;
+      L.vals[ns] = kPend;
+      const uint32_t k = atomicAdd(&L.npend, 1u);
+      if (k < 64u) L.pend[k] = x;
+      return;
+    }
+    if (is_ign || sl == kInf) return;  // the hint stands, or ignored links were never counted
+    const uint32_t v = ((volatile uint32_t*)L.vals)[sl];
+    if ((v & kAffFlag) || v == kPend) return;
+    if (atomicSub(&L.vals[sl], 1u) == 1u) make_affected(L, sl, x);
+  };
+  // (1) the ignored links' tight directions: 32 links per step, lane =
+  // (link, direction), so a step leaves <= 64 nodes pending
+  for (uint32_t k0 = 0; k0 < nign; k0 += 32u) {
+    const uint32_t k = k0 + (lane & 31u);
+    if (k < nign) {
+      const uint32_t l = L.ign[k];
+      const uint32_t e0 = l < g.n_lid ? g.link_e[2u * l] : kInf;
+      const uint32_t e1 = l < g.n_lid ? g.link_e[2u * l + 1u] : kInf;
+      if (e0 != kInf && e1 != kInf) {
+        const uint32_t b = g.colx[e0], a = g.colx[e1];  // e0 in a's row, e1 in b's row
+        if (!(b & kDown) && !(a & kDown) && a != b) {  // a down link supports nothing
+          // this lane's direction: u -> x over entry e of u's row
+          const bool fwd = lane < 32u;
+          const uint32_t u = fwd ? a : b, x = fwd ? b : a, e = fwd ? e0 : e1;
+          const uint32_t du = D[u];
+          if (du != kInf && transit(u) && (uint64_t)du + g.w[e] == D[x]) lose(x, l, true);
+        }
+      }
+    }
+    settle_pending(0u);
+  }
+  // (2) affected nodes in order lose their tight out-links
+  for (uint32_t q = 0;; ++q) {
+    const uint32_t nq = ((volatile uint32_t&)L.naff);
+    if (((volatile uint32_t&)L.ovf) || q >= min(nq, L_::kAff)) break;
+    const uint32_t v = ((volatile uint32_t*)L.aff)[q];
+    if (!transit(v)) continue;
+    const uint32_t dv = D[v];
+    const uint32_t beg = g.row_ptr[v], end = g.row_ptr[v + 1];
+    for (uint32_t e0 = beg; e0 < end; e0 += kWave) {
+      const uint32_t e = e0 + lane;
+      bool go = false;
+      uint32_t x = 0, lid = 0;
+      if (e < end) {
+        x = g.colx[e];
+        if (!(x & kDown) && x != v && (uint64_t)dv + g.w[e] == D[x]) {
+          lid = g.link_id[e];
+          go = !ignored(lid);
+        }
+      }
+      if (go) lose(x, lid, false);
+      settle_pending(q + 1u);  // (<= 64 pending per step)
+    }
+  }
+  if (((volatile uint32_t&)L.ovf)) {
+    if (lane == 0) atomicAdd(&t.ctr[((volatile uint32_t&)L.naff) > L_::kAff ? 6 : 7], 1u);
+    return false;
+  }
+  na = ((volatile uint32_t&)L.naff);
+  // (3) masked distances of A: boundary terms, then rounds over A's own links
+  bool inner = false;
+  for (uint32_t q = 0; q < na; ++q) {
+    const uint32_t a = ((volatile uint32_t*)L.aff)[q];
+    uint32_t best = kInf;
+    for (uint32_t e = g.row_ptr[a] + lane; e < g.row_ptr[a + 1]; e += kWave) {
+      const uint32_t u = g.colx[e];
+      if ((u & kDown) || u == a || !transit(u)) continue;
+      if (ignored(g.link_id[e])) continue;
+      if (aff_ix(L, u) != kInf) {
+        inner = true;
+        continue;
+      }
+      const uint32_t du = D[u];
+      if (du == kInf) continue;
+      best = min(best, du + g.rw[e]);
+    }
+    for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, kWave));
+    if (lane == 0) L.dp[q] = best;
+  }
+  if (__ballot(inner)) {
+    for (uint32_t round = 0; round <= na; ++round) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      bool changed = false;
+      for (uint32_t q = 0; q < na; ++q) {
+        const uint32_t a = ((volatile uint32_t*)L.aff)[q];
+        uint32_t best = ((volatile uint32_t*)L.dp)[q];
+        const uint32_t b0 = best;
+        for (uint32_t e = g.row_ptr[a] + lane; e < g.row_ptr[a + 1]; e += kWave) {
+          const uint32_t u = g.colx[e];
+          if ((u & kDown) || u == a || !transit(u)) continue;
+          const uint32_t ui = aff_ix(L, u);
+          if (ui == kInf || ignored(g.link_id[e])) continue;
+          const uint32_t du = ((volatile uint32_t*)L.dp)[ui];
+          if (du == kInf) continue;
+          best = min(best, du + g.rw[e]);
+        }
+        for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, kWave));
+        if (best < b0) {
+          changed = true;
+          if (lane == 0) L.dp[q] = best;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+      }
+      if (!changed) break;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  return true;
+}
+
+// One wave per run (blocks of one wave, runs taken from t.ctr[0]).
+__global__ void __launch_bounds__(64) ksp_decr_kernel(DevGraph g, TraceArgs t) {
+  __shared__ DecrSmall L;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t src = t.src;
+  uint32_t* dead = t.dead + (size_t)blockIdx.x * t.dead_words;
+  for (;;) {
+    if (lane == 0) L.run = atomicAdd(&t.ctr[0], 1u);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t i = ((volatile uint32_t&)L.run);
+    if (i >= t.n) return;
+    uint32_t* out = t.out + (size_t)i * t.stride;
+    const uint32_t st = t.status[i];
+    if (st & OSPF_KSP_OVF1) {  // no k = 1 paths, so no ignore set: not computed
+      if (lane == 0) t.status[i] = st | OSPF_KSP_OVF2;
+      continue;
+    }
+    if (!(st & OSPF_KSP_RERUN)) {  // k = 1 found nothing: neither does k = 2
+      if (lane == 0) out[0] = 0u;
+      continue;
+    }
+    auto fallback = [&]() {
+      if (lane == 0) t.fb[atomicAdd(&t.ctr[1], 1u)] = i;
+    };
+    uint32_t nign = 0, na = 0;
+    if (!decr_prepare(L, g, t, i, lane, nign, na)) {
+      fallback();
+      continue;
+    }
+    const uint32_t dst = t.dsts[i];
+    Tracer<DistDecr<DecrSmall>, DecrSmall::kHS> tr{g, t, i, lane, src, dst, L.ign, nign, L.hash, dead,
+                                                   DistDecr<DecrSmall>{t.rows, &L}};
+    // no paths (LinkState.cpp:808-809): src == dst, dst unreached, or the
+    // source cut off by the ignored links
+    if (na == kInf || dst == src || tr.dist(dst) == kInf) {
+      if (lane == 0) {
+        out[0] = 0u;
+        atomicAdd(&t.ctr[2], 1u);
+      }
+      continue;
+    }
+    for (uint32_t k = lane; k < DecrSmall::kHS; k += kWave) tr.hs[k] = 0u;
+    for (uint32_t k = lane; k < t.dead_words; k += kWave) dead[k] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    volatile uint32_t* stk = L.stack;
+    uint32_t npaths = 0, w = 1, steps = 0, nclaim = 0;
+    bool ovf = false, heavy = false, tier = false;
+    const uint32_t budget = t.budget ? t.budget : kSteps;
+    if (lane == 0) out[0] = 0u;
+    while (!ovf && tr.src_open()) {
+      uint32_t depth = 0;
+      const int r = tr.dfs(stk, depth, 0, steps, budget);
+      if (r == 0) break;
+      if (r == -1 && t.budget) {  // a long failing search: resumed by 16 waves
+        heavy = true;
+        break;
+      }
+      if (r == 1 && nclaim + depth > tr.kHM && w + 1u + depth <= t.stride) {
+        tier = true;  // more claimed links than this kernel's hash holds
+        break;
+      }
+      if (r < 0 || !tr.emit(out, stk, depth, w, npaths, nclaim)) ovf = true;
+      if (t.budget) steps = 0;
+    }
+    if (tier) {
+      fallback();
+      continue;
+    }
+    if (lane == 0) {
+      atomicAdd(&t.ctr[2], 1u);
+      atomicAdd(&t.ctr[3], na);
+    }
+    if (heavy) {  // the paths so far stay in the record
+      if (lane == 0) t.heavy[atomicAdd(&t.heavy_ctr[0], 1u)] = i;
+      continue;
+    }
+    tr.finish(out, npaths, ovf, tr.hs);
+  }
+}
+
+// Heavy decremental runs: the block's first wave recomputes the run's
+// affected set and distances (the wider budgets hold whatever the small
+// kernel held), then 16 waves resume its trace (heavy_trace).
+__global__ void __launch_bounds__(1024) ksp_decr_heavy_kernel(DevGraph g, TraceArgs t) {
+  extern __shared__ uint4 s_raw[];
+  DecrHeavy& L = *reinterpret_cast<DecrHeavy*>(s_raw);
+  __shared__ HeavyLds H;
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  uint32_t* dead = t.dead + (size_t)blockIdx.x * t.dead_words;
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const uint32_t q = atomicAdd(&t.heavy_ctr[1], 1u);
+      H.ctl[0] = q < __hip_atomic_load(&t.heavy_ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                     ? t.heavy[q] : kInf;
+    }
+    __syncthreads();
+    const uint32_t i = H.ctl[0];
+    __syncthreads();
+    if (i == kInf) return;
+    uint32_t nign = 0, na = 0;
+    if (wv == 0) {
+      const bool ok = decr_prepare(L, g, t, i, lane, nign, na);
+      if (lane == 0) {
+        H.ctl[3] = ok ? nign : kInf;
+        if (!ok) atomicOr(&t.err[0], 2048u);  // cannot happen: it fit before
+      }
+    }
+    for (uint32_t k = threadIdx.x; k < t.dead_words; k += blockDim.x) dead[k] = 0u;
+    __syncthreads();
+    nign = H.ctl[3];
+    if (nign == kInf) {
+      if (threadIdx.x == 0) t.status[i] |= OSPF_KSP_OVF2;
+      continue;
+    }
+    Tracer<DistDecr<DecrHeavy>, kHash> tr{g, t, i, lane, t.src, t.dsts[i], L.ign, nign, L.hash, dead,
+                                          DistDecr<DecrHeavy>{t.rows, &L}};
+    heavy_trace(g, t, i, tr, L.hash, H);
+  }
+}
+
+__global__ void rows_gather_kernel(uint32_t* a, const uint32_t* b, const uint32_t* idx, uint32_t n,
+                                   uint32_t w, bool gather) {
+  const uint32_t j = blockIdx.x;
+  if (j >= n) return;
+  const uint32_t r = idx[j];
+  uint32_t* dst = a + (size_t)(gather ? j : r) * w;
+  const uint32_t* from = b + (size_t)(gather ? r : j) * w;
+  for (uint32_t k = threadIdx.x; k < w; k += blockDim.x) dst[k] = from[k];
 }
 
 __global__ void iota_kernel(uint32_t* out, uint32_t n, uint32_t stride) {
@@ -503,6 +997,42 @@ hipError_t launch_ksp_trace(bool lev, const DevGraph& g, const TraceArgs& t, hip
     else
       hipLaunchKernelGGL(ksp_heavy_kernel<false>, hg, dim3(64 * kHeavyWaves), 0, s, g, t);
   }
+  return hipGetLastError();
+}
+
+
+hipError_t launch_ksp_hint(const DevGraph& g, uint32_t src, const uint32_t* dist, uint32_t* hint,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(ksp_hint_kernel, dim3((g.V + 255) / 256), dim3(256), 0, s, g, src, dist, hint);
+  return hipGetLastError();
+}
+
+uint32_t ksp_decr_blocks_per_cu() {
+  return std::min<uint32_t>(16u, (160u * 1024u) / (uint32_t)sizeof(DecrSmall));
+}
+
+hipError_t launch_ksp_decr(const DevGraph& g, const TraceArgs& t, uint32_t blocks, hipStream_t s) {
+  if (t.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(ksp_decr_kernel, dim3(blocks), dim3(kWave), 0, s, g, t);
+  return hipGetLastError();
+}
+
+hipError_t launch_ksp_decr_heavy(const DevGraph& g, const TraceArgs& t, uint32_t blocks,
+                                 hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)ksp_decr_heavy_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(DecrHeavy));
+    attr = true;
+  }
+  hipLaunchKernelGGL(ksp_decr_heavy_kernel, dim3(blocks), dim3(64 * kHeavyWaves), sizeof(DecrHeavy), s,
+                     g, t);
+  return hipGetLastError();
+}
+
+hipError_t launch_rows_gather(uint32_t* a, const uint32_t* b, const uint32_t* idx, uint32_t n,
+                              uint32_t w, bool gather, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(rows_gather_kernel, dim3(n), dim3(256), 0, s, a, b, idx, n, w, gather);
   return hipGetLastError();
 }
 

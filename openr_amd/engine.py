@@ -232,6 +232,13 @@ class Engine:
         return (decode_paths(k1[:n], st[:n], N.OSPF_KSP_OVF1),
                 decode_paths(k2[:n], st[:n], N.OSPF_KSP_OVF2 | N.OSPF_KSP_OVF1), st[:n])
 
+    def ksp2_stats(self) -> dict:
+        """ospf_ksp2_stats: k = 2 runs by the decremental kernel, runs sent to
+        the full masked reruns, affected nodes summed (since open)."""
+        out = np.zeros(3, np.uint64)
+        self._check(self._L.ospf_ksp2_stats(self._h, out.ctypes.data))
+        return {"decremental": int(out[0]), "full_reruns": int(out[1]), "affected": int(out[2])}
+
     def ksp2_dev(self, src: int, d_dsts: int, n: int, path_cap: int, d_k1: int, d_k2: int,
                  d_status: int, stream: int = 0) -> None:
         a = N.ospf_ksp2(src, d_dsts, n, path_cap, d_k1, d_k2, d_status)

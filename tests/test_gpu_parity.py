@@ -11,6 +11,7 @@ from graphs import random_stream
 from oracle import Oracle, parse_spf_text
 from openr_amd import topology as T
 from openr_amd.adjdb import AdjDb, AdjDbStream, create_adjacency
+from openr_amd import _native as N
 from openr_amd.engine import Engine, EngineError
 from openr_amd.linkstate import LinkState
 
@@ -75,6 +76,7 @@ KSP_KNOBS = {
     "tiny_records": {"ODL_KSP_CAP": "6"},     # record overflow -> host path per destination
     "heavy": {"OSPF_KSP_BUDGET": "3"},        # most runs resumed by the 16-wave kernel
     "no_heavy": {"OSPF_KSP_NOHEAVY": "1"},    # single-wave DFS only
+    "no_decr": {"OSPF_KSP_NODECR": "1"},      # every k = 2 run by the full masked reruns
 }
 
 
@@ -105,6 +107,43 @@ def test_fabric_ksp2_from_fsw_all_destinations(budget, monkeypatch):
     dsts = p.node_names()
     assert p.ksp2_text("2-0-0", dsts) == o.ksp2_text("2-0-0", dsts)
     assert p.spf_runs == o.spf_runs
+
+
+@pytest.mark.parametrize("unit", [True, False])
+@pytest.mark.parametrize("seed", range(4))
+def test_ksp2_decremental_equals_full_reruns(seed, unit, monkeypatch):
+    """The k = 2 masked reruns by decremental SSSP (ospf_ksp2: lost tight
+    supports from the source's row, fused trace) give every destination the
+    same records and status words as the full masked reruns (OSPF_KSP_NODECR;
+    itself oracle-pinned above), and the decremental kernel takes runs: random
+    graphs with parallel / down links and overloaded nodes, and a drained
+    fabric whose destinations include every role."""
+    from graphs import drained_fabric
+    for st in (random_stream(700 + seed, n=120, p=0.05, unit=unit)[0],
+               drained_fabric(10, 4, seed=seed, drain=0.04, down=0.03,
+                              weighted_seed=None if unit else seed + 1)):
+        p, csr = _csr_of(st)
+        names = p.node_names()
+        V = len(names)
+        eng = Engine(0)
+        eng.load(csr)
+        try:
+            for src in (0, V // 3, V - 1):
+                dsts = list(range(V))
+                s0 = eng.ksp2_stats()
+                k1, k2, stt = eng.ksp2(src, dsts, path_cap=512)
+                s1 = eng.ksp2_stats()
+                monkeypatch.setenv("OSPF_KSP_NODECR", "1")
+                f1, f2, fst = eng.ksp2(src, dsts, path_cap=512)
+                monkeypatch.delenv("OSPF_KSP_NODECR")
+                assert k1 == f1 and k2 == f2, src
+                assert np.array_equal(stt, fst), src
+                reruns = int(np.count_nonzero(stt & N.OSPF_KSP_RERUN))
+                took = s1["decremental"] - s0["decremental"]
+                sent = s1["full_reruns"] - s0["full_reruns"]
+                assert took + sent == reruns and (reruns == 0 or took > 0), (took, sent, reruns)
+        finally:
+            eng.close()
 
 
 def test_engine_ksp2_budget_status():

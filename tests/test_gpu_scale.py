@@ -90,6 +90,65 @@ def test_f100k_ksp2_and_lfa_from_fsw():
     assert np.array_equal(p.digests(nbrs), o.fast_digests(nbrs, True, threads=16))
 
 
+def _role_stratified(names, k=256, extra=("1-3-5", "1-7-35", "3-900-17")):
+    """scripts/bench_ksp2.py's parity sample: a quarter spines spread over
+    every plane, 3/8 fabric switches, the rest racks (seed 0x5eed), + extras"""
+    rng = np.random.default_rng(0x5EED)
+    role = np.array([int(nm.split("-")[0]) for nm in names])
+    pick = []
+    for r_, share in ((1, k // 4), (2, (3 * k) // 8), (3, k - k // 4 - (3 * k) // 8)):
+        cand = np.nonzero(role == r_)[0]
+        pick.extend(int(x) for x in rng.choice(cand, min(share, cand.size), replace=False))
+    out = sorted(set(pick))
+    idx = {nm: i for i, nm in enumerate(names)}
+    out += [idx[x] for x in extra if idx[x] not in out]
+    return [names[i] for i in out]
+
+
+@pytest.mark.timeout(900)
+def test_f100k_ksp2_role_stratified_vs_oracle():
+    """BASELINE config 4 at full size: KSP2 (k = 1 and k = 2 paths, text)
+    from "2-0-0" to 259 role-stratified destinations through
+    odl::LinkState (device KSP2, decremental k = 2 reruns) == the oracle's
+    reference-shaped getKthPaths; then every destination's records from the
+    decremental reruns == those of the full masked reruns (engine level)."""
+    from openr_amd import _native as N
+    st = T.fabric(pods=1781, planes=8)
+    o, p = both(st)
+    names = p.node_names()
+    src = "2-0-0"
+    sn = _role_stratified(names)
+    assert len(sn) == 259
+    got = p.ksp2_text(src, sn)
+    note("F100k KSP2 259 destinations on the GPU")
+    want = o.ksp2_text(src, sn, threads=16)
+    note("oracle KSP2")
+    assert got == want
+    eng = Engine(0)
+    eng.load(p.csr())
+    try:
+        s = names.index(src)
+        dsts = list(range(len(names)))
+        s0 = eng.ksp2_stats()
+        k1, k2, stt = eng.ksp2(s, dsts, path_cap=1024)
+        s1 = eng.ksp2_stats()
+        import os
+        os.environ["OSPF_KSP_NODECR"] = "1"
+        try:
+            f1, f2, fst = eng.ksp2(s, dsts, path_cap=1024)
+        finally:
+            del os.environ["OSPF_KSP_NODECR"]
+        assert np.array_equal(stt, fst)
+        assert k1 == f1 and k2 == f2
+        took = s1["decremental"] - s0["decremental"]
+        reruns = int(np.count_nonzero(stt & N.OSPF_KSP_RERUN))
+        note(f"decremental {took} of {reruns} reruns, "
+             f"{(s1['affected'] - s0['affected']) / max(1, took):.1f} affected nodes per run")
+        assert took > 0.5 * reruns
+    finally:
+        eng.close()
+
+
 @pytest.mark.timeout(900)
 def test_m1m_sampled_roots_and_triangle_checks():
     st = T.mesh(1_000_000, seed=42)
