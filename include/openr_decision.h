@@ -61,6 +61,36 @@ uint64_t odl_spf_runs(const odl_ls* ls);
 /* Incremental mode (off by default; odl::LinkState::setIncremental): keep the
  * memoised SPF of roots a metric / up / overload-only update cannot affect.
  * Stats: {patches applied, results kept, results dropped}. */
+/* KvStore publications (the step before LinkState in Decision): compact-
+ * thrift values decoded on host threads (adjdb_thrift.cpp).
+ *
+ * odl_apply_kvs -- Decision::processPublication's LinkState part
+ * (Decision.cpp:846-870): keys[i] / values[i] (value_lens[i] bytes,
+ * values[i] == NULL: a TTL-only update) in the caller's keyVals iteration
+ * order; an "adj:" key's value (a CompactSerializer thrift::AdjacencyDatabase,
+ * Types.thrift:175-207) goes to updateAdjacencyDatabase (updateKeyInLsdb
+ * :743-765), other keys are skipped; then each expired "adj:" key deletes
+ * the node getNodeNameFromKey names (deleteKeyFromLsdb :812-826). my_node !=
+ * NULL applies filterUnuseableAdjacency (:568-600). changes: n + n_expired
+ * records (zero for skipped keys) or NULL. */
+int odl_apply_kvs(odl_ls* ls, uint32_t n, const char* const* keys, const uint8_t* const* values,
+                  const uint64_t* value_lens, uint32_t n_expired, const char* const* expired,
+                  const char* my_node, oadj_change* changes);
+/* Same from a whole compact-thrift thrift::Publication (KvStore.thrift:270-
+ * 320) in `buf`: keyVals in wire order, then expiredKeys. n_changes_out (may
+ * be NULL) = number of records; changes (may be NULL) holds up to
+ * max_changes of them. */
+int odl_apply_publication(odl_ls* ls, const uint8_t* buf, uint64_t len, const char* my_node,
+                          oadj_change* changes, uint32_t max_changes, uint32_t* n_changes_out);
+/* Decode n compact-thrift AdjacencyDatabase values into a columnar stream
+ * (include/openr_adjdb.h; adj_only_used_by_other filled, db_delete all 0),
+ * owned by *out until odl_adjdbs_free. NULL on malformed input, with the
+ * reason in odl_adjdbs_error. */
+typedef struct odl_adjdbs odl_adjdbs;
+odl_adjdbs* odl_adjdbs_decode(const uint8_t* const* values, const uint64_t* lens, uint32_t n);
+const oadj_stream* odl_adjdbs_stream(const odl_adjdbs* d);
+const char* odl_adjdbs_error(void);
+void odl_adjdbs_free(odl_adjdbs* d);
 void odl_set_incremental(odl_ls* ls, int on);
 /* Every SPF / KSP2 / digest of this LinkState on the host with the
  * reference's algorithm (LinkState.cpp:836-911), the engine never opened: a

@@ -181,3 +181,45 @@ def merge(*streams: Optional[AdjDbStream]) -> AdjDbStream:
         if s is not None:
             dbs.extend(s.to_dbs())
     return AdjDbStream.from_dbs(dbs)
+
+
+def decode_adjdbs(values: Sequence[bytes]) -> AdjDbStream:
+    """Compact-thrift thrift::AdjacencyDatabase values (KvStore "adj:" keys)
+    decoded on host threads by libopenr_decision (odl_adjdbs_decode) into a
+    columnar stream; the columns are copied out and the C object freed."""
+    from . import _native as N
+    L = N.decision()
+    n = len(values)
+    keep = [bytes(v) for v in values]
+    ptrs = (C.c_void_p * max(n, 1))(*[C.cast(C.c_char_p(v), C.c_void_p).value for v in keep])
+    lens = (C.c_uint64 * max(n, 1))(*[len(v) for v in keep])
+    h = L.odl_adjdbs_decode(ptrs, lens, n)
+    if not h:
+        raise ValueError("odl_adjdbs_decode: " + L.odl_adjdbs_error().decode())
+    try:
+        s = oadj_stream.from_address(L.odl_adjdbs_stream(h))
+
+        def col(ptr, count, dt):
+            if count == 0:
+                return np.zeros(0, dt)
+            return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(np.ctypeslib.as_ctypes_type(dt))),
+                                         (count,)).copy()
+        n_dbs, n_str = s.n_dbs, s.n_str
+        adj_off = col(s.db_adj_off, n_dbs + 1, np.uint64)
+        na = int(adj_off[-1]) if n_dbs else 0
+        str_off = col(s.str_off, n_str + 1, np.uint64)
+        data = C.string_at(s.str_data, int(str_off[-1])) if n_str else b""
+        strings = [data[int(str_off[i]):int(str_off[i + 1])].decode() for i in range(n_str)]
+        cols = dict(
+            db_name=col(s.db_name, n_dbs, np.uint32), db_overloaded=col(s.db_overloaded, n_dbs, np.uint8),
+            db_node_label=col(s.db_node_label, n_dbs, np.int32), db_delete=col(s.db_delete, n_dbs, np.uint8),
+            db_adj_off=adj_off, adj_other=col(s.adj_other, na, np.uint32),
+            adj_if=col(s.adj_if, na, np.uint32), adj_other_if=col(s.adj_other_if, na, np.uint32),
+            adj_metric=col(s.adj_metric, na, np.int32), adj_label=col(s.adj_label, na, np.int32),
+            adj_overloaded=col(s.adj_overloaded, na, np.uint8), adj_weight=col(s.adj_weight, na, np.int64),
+            adj_only_used_by_other=col(s.adj_only_used_by_other, na, np.uint8))
+        if n_dbs == 0:
+            cols["db_adj_off"] = np.zeros(1, np.uint64)
+        return AdjDbStream(strings, cols)
+    finally:
+        L.odl_adjdbs_free(h)

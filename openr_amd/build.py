@@ -26,14 +26,14 @@ ENGINE_SRC = [os.path.join(PKG, "csrc", "engine", f)
                         "spf_engine.hip",
                         "spf_sweep.hip")]
 DECISION_SRC = [os.path.join(PKG, "csrc", "decision", f)
-                for f in ("link_state.cpp", "spf_solver.cpp", "decision_capi.cpp")]
+                for f in ("link_state.cpp", "spf_solver.cpp", "adjdb_thrift.cpp", "decision_capi.cpp")]
 ENGINE_SO = os.path.join(LIB, "libopenr_spf_hip.so")
 DECISION_SO = os.path.join(LIB, "libopenr_decision.so")
 HEADERS = [os.path.join(ROOT, "include", h)
            for h in ("openr_spf.h", "openr_decision.h", "openr_adjdb.h")] + \
     [os.path.join(PKG, "csrc", "engine", h) for h in ("spf_kernels.h", "spf_internal.h")]
 DECISION_HEADERS = HEADERS + \
-    [os.path.join(PKG, "csrc", "decision", h) for h in ("link_state.h", "spf_solver.h")]
+    [os.path.join(PKG, "csrc", "decision", h) for h in ("link_state.h", "spf_solver.h", "adjdb_thrift.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"

@@ -14,6 +14,7 @@
 #include "../../../include/openr_decision.h"
 #include "link_state.h"
 #include "spf_solver.h"
+#include "adjdb_thrift.h"
 
 struct odl_ls {
   odl::LinkState ls;
@@ -240,6 +241,47 @@ uint64_t odl_spf_runs(const odl_ls* h) { return h ? h->ls.spfRuns() : 0; }
 void odl_set_incremental(odl_ls* h, int on) {
   if (h) h->ls.setIncremental(on != 0);
 }
+int odl_apply_kvs(odl_ls* h, uint32_t n, const char* const* keys, const uint8_t* const* values,
+                  const uint64_t* value_lens, uint32_t n_expired, const char* const* expired,
+                  const char* my_node, oadj_change* changes) {
+  return guard(h, [&]() -> int {
+    if ((n && (!keys || !values || !value_lens)) || (n_expired && !expired))
+      throw std::invalid_argument("null key-value arrays");
+    std::vector<odl::LinkState::KvIn> kvs(n);
+    for (uint32_t i = 0; i < n; ++i) {
+      kvs[i].key = keys[i];
+      kvs[i].hasValue = values[i] != nullptr;
+      if (values[i]) kvs[i].value = std::string_view((const char*)values[i], (size_t)value_lens[i]);
+    }
+    std::vector<std::string_view> exp(expired, expired + n_expired);
+    const std::string me = my_node ? my_node : "";
+    const auto chs = h->ls.applyKvs(kvs, exp, my_node ? &me : nullptr);
+    for (size_t k = 0; changes && k < chs.size(); ++k)
+      changes[k] = oadj_change{chs[k].topologyChanged, chs[k].linkAttributesChanged,
+                               chs[k].nodeLabelChanged, (int32_t)chs[k].addedLinks.size()};
+    return 0;
+  }, -1);
+}
+
+int odl_apply_publication(odl_ls* h, const uint8_t* buf, uint64_t len, const char* my_node,
+                          oadj_change* changes, uint32_t max_changes, uint32_t* n_changes_out) {
+  return guard(h, [&]() -> int {
+    if (!buf && len) throw std::invalid_argument("null publication buffer");
+    odl::PublicationView pv;
+    odl::thrift_compact::parsePublication(buf, (size_t)len, pv);
+    std::vector<odl::LinkState::KvIn> kvs(pv.keyVals.size());
+    for (size_t i = 0; i < kvs.size(); ++i)
+      kvs[i] = odl::LinkState::KvIn{pv.keyVals[i].key, pv.keyVals[i].value, pv.keyVals[i].hasValue};
+    const std::string me = my_node ? my_node : "";
+    const auto chs = h->ls.applyKvs(kvs, pv.expiredKeys, my_node ? &me : nullptr);
+    if (n_changes_out) *n_changes_out = (uint32_t)chs.size();
+    for (size_t k = 0; changes && k < chs.size() && k < max_changes; ++k)
+      changes[k] = oadj_change{chs[k].topologyChanged, chs[k].linkAttributesChanged,
+                               chs[k].nodeLabelChanged, (int32_t)chs[k].addedLinks.size()};
+    return 0;
+  }, -1);
+}
+
 void odl_set_host_spf(odl_ls* h, int on) {
   if (h) h->ls.setHostSpf(on != 0);
 }
@@ -641,5 +683,31 @@ int64_t odl_node_id(odl_ls* h, const char* name) {
     return it == c.ids.end() ? -1 : (int64_t)it->second;
   }, (int64_t)-2);
 }
+
+struct odl_adjdbs {
+  odl::AdjDbColumns cols;
+};
+static thread_local std::string g_adjdbs_err;
+odl_adjdbs* odl_adjdbs_decode(const uint8_t* const* values, const uint64_t* lens, uint32_t n) {
+  try {
+    if (n && (!values || !lens)) throw std::invalid_argument("null value arrays");
+    auto* d = new odl_adjdbs;
+    try {
+      d->cols.decode(values, lens, n);
+    } catch (...) {
+      delete d;
+      throw;
+    }
+    return d;
+  } catch (const std::exception& e) {
+    g_adjdbs_err = e.what();
+  } catch (...) {
+    g_adjdbs_err = "unknown error";
+  }
+  return nullptr;
+}
+const oadj_stream* odl_adjdbs_stream(const odl_adjdbs* d) { return d ? &d->cols.stream : nullptr; }
+const char* odl_adjdbs_error(void) { return g_adjdbs_err.c_str(); }
+void odl_adjdbs_free(odl_adjdbs* d) { delete d; }
 
 }  // extern "C"

@@ -80,6 +80,7 @@ struct Adjacency {
   int32_t adjLabel = 0;
   bool isOverloaded = false;
   int64_t weight = 1;
+  bool adjOnlyUsedByOtherNode = false;  // read by Decision's filter only
 };
 
 struct AdjacencyDatabase {
@@ -362,6 +363,20 @@ class LinkState {
   // batch of nodes not yet known (no name twice) is built with host threads.
   // The databases are moved from.
   std::vector<LinkStateChange> updateAdjacencyDatabases(std::vector<AdjacencyDatabase>& dbs);
+  // Decision::processPublication's LinkState part (Decision.cpp:846-870):
+  // every key-value in order -- an "adj:" key with a value decoded from
+  // compact thrift (on host threads) and applied (updateKeyInLsdb,
+  // :743-765), TTL-only values and other keys skipped -- then every expired
+  // "adj:" key deleted (deleteKeyFromLsdb, :812-826). myNodeName (may be
+  // null) turns on filterUnuseableAdjacency (:568-600). One change record
+  // per key-value, then per expired key (empty for skipped ones).
+  struct KvIn {
+    std::string_view key, value;
+    bool hasValue = false;
+  };
+  std::vector<LinkStateChange> applyKvs(const std::vector<KvIn>& kvs,
+                                        const std::vector<std::string_view>& expired,
+                                        const std::string* myNodeName);
 
   const LinkSet& linksFromNode(const std::string& node) const;
   bool isNodeOverloaded(const std::string& node) const;

@@ -53,7 +53,6 @@ constexpr uint32_t kBlock = 256;
 constexpr uint32_t kWaves = kBlock / kWave;
 constexpr uint32_t kStack = 256;      // links per path
 constexpr uint32_t kHash = 2048;      // visited-set slots (power of 2)
-constexpr uint32_t kHashMax = 1536;   // links of the paths of one (src, dst, k)
 constexpr uint32_t kSteps = 1u << 22; // DFS steps per run (termination guard)
 constexpr uint32_t kLook = 16;        // lookahead row length limit
 

@@ -305,6 +305,35 @@ class LinkState:
         cannot affect (odl_set_incremental; off = the reference's behaviour)."""
         self._L.odl_set_incremental(self._h, int(on))
 
+    def apply_kvs(self, key_vals, expired=(), my_node: Optional[str] = None):
+        """Decision::processPublication's LinkState part (odl_apply_kvs):
+        key_vals = [(key, compact-thrift AdjacencyDatabase bytes or None)] in
+        keyVals iteration order, then expired keys. Change records as tuples
+        (topology, link attributes, node label, added links)."""
+        n, ne = len(key_vals), len(expired)
+        keys = (C.c_char_p * max(n, 1))(*[k.encode() for k, _ in key_vals])
+        bufs = [v for _, v in key_vals]
+        vals = (C.c_void_p * max(n, 1))(*[(C.cast(C.c_char_p(v), C.c_void_p).value if v is not None
+                                            else None) for v in bufs])
+        lens = (C.c_uint64 * max(n, 1))(*[len(v) if v is not None else 0 for v in bufs])
+        exp = (C.c_char_p * max(ne, 1))(*[k.encode() for k in expired])
+        ch = change_array(n + ne)
+        if self._L.odl_apply_kvs(self._h, n, keys, vals, lens, ne, exp,
+                                 my_node.encode() if my_node is not None else None, ch) != 0:
+            raise LinkStateError(self._err())
+        return changes_to_list(ch, n + ne)
+
+    def apply_publication(self, buf: bytes, my_node: Optional[str] = None):
+        """A whole compact-thrift thrift::Publication (odl_apply_publication)."""
+        nout = C.c_uint32(0)
+        cap = 1 << 20
+        ch = change_array(cap)
+        if self._L.odl_apply_publication(self._h, buf, len(buf),
+                                         my_node.encode() if my_node is not None else None,
+                                         ch, cap, C.byref(nout)) != 0:
+            raise LinkStateError(self._err())
+        return changes_to_list(ch, min(int(nout.value), cap))
+
     def set_host_spf(self, on: bool = True) -> None:
         """Run every SPF / KSP2 / digest of this LinkState on the host with the
         reference's algorithm, the engine never opened (odl_set_host_spf): a

@@ -32,7 +32,7 @@ build)
   D=$ROOT/openr_amd/csrc/decision
   CXX=/opt/rocm/lib/llvm/bin/clang++
   $CXX -O1 -g -std=c++17 -fPIC -shared $SAN -o "$OUT/libopenr_decision.so" \
-    $D/link_state.cpp $D/spf_solver.cpp $D/decision_capi.cpp \
+    $D/link_state.cpp $D/spf_solver.cpp $D/adjdb_thrift.cpp $D/decision_capi.cpp \
     -L"$OUT" -lopenr_spf_hip -Wl,-rpath,'$ORIGIN' -Wl,-rpath,"$CLANGRT"
   $CXX -O1 -g -std=c++17 -fPIC -shared -pthread $SAN -o "$OUT/liboracle.so" "$ROOT/oracle/linkstate_oracle.cpp" \
     -Wl,-rpath,"$CLANGRT"

@@ -13,7 +13,7 @@ OUT=/tmp/openr_san/${SAN//,/_}
 mkdir -p "$OUT"
 D=$ROOT/openr_amd/csrc/decision
 FL="-O1 -g -fno-omit-frame-pointer -std=c++17 -fPIC -shared -fsanitize=$SAN"
-g++ $FL -o "$OUT/libopenr_decision.so" $D/link_state.cpp $D/spf_solver.cpp $D/decision_capi.cpp \
+g++ $FL -o "$OUT/libopenr_decision.so" $D/link_state.cpp $D/spf_solver.cpp $D/adjdb_thrift.cpp $D/decision_capi.cpp \
   -L"$ROOT/openr_amd/lib" -lopenr_spf_hip -Wl,-rpath,"$ROOT/openr_amd/lib"
 g++ $FL -pthread -o "$OUT/liboracle.so" "$ROOT/oracle/linkstate_oracle.cpp"
 case $SAN in
