@@ -160,6 +160,20 @@ int odl_path_a_in_b(const char* a_nl, uint32_t na, const char* b_nl, uint32_t nb
  * (SWAP: the swap label; PUSH: bottom of stack first). */
 char* odl_route_db_text(odl_ls* ls, const char* mes_nl, uint32_t n_mes, const char* prefixes_nl,
                         uint32_t n, int flags);
+/* Prefix entries may end in "@area" (the entry's area; default: the first
+ * area by name) and then "#n" (PrefixEntry.minNexthop = n: addBestPaths
+ * drops a route with fewer next hops, SpfSolver.cpp:976-1000,
+ * getMinNextHopThreshold :694-710).
+ * odl_route_db_multi_text: the same over several areas, one LinkState each
+ * (their area names, odl_create's `area`, distinct): createRouteForPrefix's
+ * per-area loop (SpfSolver.cpp:229-250, 360-442: entries reachable in their
+ * own area; per area the forwarding type / algorithm of its best entries;
+ * the next hops of the areas at the shortest IGP metric, UCMP weights
+ * summed, KSP2 next hops added), node labels of every area's databases
+ * (:490-598) and adjacency labels of every area (:603-631). Next-hop lines
+ * carry a last field: the next hop's area. Errors: odl_last_error(areas[0]). */
+char* odl_route_db_multi_text(odl_ls* const* areas, uint32_t n_areas, const char* mes_nl,
+                              uint32_t n_mes, const char* prefixes_nl, uint32_t n, int flags);
 
 /* odl_route_db_text's databases as one binary buffer (no text formatting or
  * parsing on either side; every string stored once). *out is malloc'd (free

@@ -413,8 +413,10 @@ int odl_path_a_in_b(const char* a_nl, uint32_t na, const char* b_nl, uint32_t nb
 
 namespace {
 // the prefix lines of odl_route_db_text / _bin -> PrefixRoutes, then the build
+// (over `areas` when given, else h's LinkState alone)
 std::vector<std::optional<odl::RouteDb>> buildDbs(odl_ls* h, const std::vector<std::string>& mes,
-                                                  const char* prefixes_nl, uint32_t n, int flags) {
+                                                  const char* prefixes_nl, uint32_t n, int flags,
+                                                  const std::vector<odl::LinkState*>* areas = nullptr) {
     auto field = [](const std::string& s, size_t& pos, char sep) {
       const size_t e = s.find(sep, pos);
       std::string out = s.substr(pos, e == std::string::npos ? std::string::npos : e - pos);
@@ -430,6 +432,17 @@ std::vector<std::optional<odl::RouteDb>> buildDbs(odl_ls* h, const std::vector<s
       std::stringstream es(ln.substr(t + 1));
       for (std::string x; std::getline(es, x, ',');) {
         if (x.empty()) continue;
+        // optional suffixes: "#minNexthop", then "@area" before it
+        std::optional<int64_t> minNh;
+        std::string area;
+        if (const size_t hsh = x.rfind('#'); hsh != std::string::npos) {
+          minNh = std::stoll(x.substr(hsh + 1));
+          x.resize(hsh);
+        }
+        if (const size_t at = x.rfind('@'); at != std::string::npos) {
+          area = x.substr(at + 1);
+          x.resize(at);
+        }
         // node:fwd:algo:weight[:prepend] -- a node name holding ':' or ','
         // would shift the fields: this text ABI rejects it (the C++ API
         // takes any name)
@@ -450,6 +463,8 @@ std::vector<std::optional<odl::RouteDb>> buildDbs(odl_ls* h, const std::vector<s
         if (e.fwdType < 0 || e.fwdType > 1 || e.algo < 0 || e.algo > 3 || e.weight < 0)
           throw std::invalid_argument("prefix entry out of range: " + x);
         if (!pl.empty()) e.prependLabel = std::stoi(pl);
+        e.area = area;
+        e.minNexthop = minNh;
         pr.entries.push_back(std::move(e));
       }
       prefixes.push_back(std::move(pr));
@@ -458,7 +473,7 @@ std::vector<std::optional<odl::RouteDb>> buildDbs(odl_ls* h, const std::vector<s
     opt.nodeSegmentLabels = flags & 1;
     opt.adjacencyLabels = flags & 2;
     opt.ucmp = flags & 4;
-    odl::SpfSolver solver(h->ls);
+    odl::SpfSolver solver = areas ? odl::SpfSolver(*areas) : odl::SpfSolver(h->ls);
     const auto t0 = std::chrono::steady_clock::now();
     auto dbs = solver.buildRouteDbs(mes, prefixes, opt);
     if (getenv("ODL_SPF_TIMING"))
@@ -469,44 +484,66 @@ std::vector<std::optional<odl::RouteDb>> buildDbs(odl_ls* h, const std::vector<s
 }
 }  // namespace
 
+namespace {
+std::string routeDbText(const std::vector<std::string>& mes,
+                        const std::vector<std::optional<odl::RouteDb>>& dbs, bool withArea) {
+  std::ostringstream os;
+  for (size_t i = 0; i < mes.size(); ++i) {
+    const auto& me = mes[i];
+    if (!dbs[i]) {
+      os << me << "\tNONE\n";
+      continue;
+    }
+    // fields are tab-separated, records newline-separated: names holding
+    // either cannot be written unambiguously by this text ABI
+    auto plain = [](const std::string& f) {
+      if (f.find_first_of("\t\n") != std::string::npos)
+        throw std::invalid_argument("name with a tab or newline in the route text: " + f);
+    };
+    plain(me);
+    auto put = [&](const char* kind, const std::string& key, const std::vector<odl::NextHop>& nhs) {
+      for (const auto& x : nhs) {
+        plain(x.ifName);
+        plain(x.neighbor);
+        os << me << '\t' << kind << '\t' << key << '\t' << x.ifName << '\t' << x.neighbor << '\t'
+           << x.metric << '\t' << (int)x.op << '\t';
+        for (size_t j = 0; j < x.labels.size(); ++j) os << (j ? "," : "") << x.labels[j];
+        os << '\t' << x.weight;
+        if (withArea) os << '\t' << x.area;
+        os << '\n';
+      }
+    };
+    for (const auto& kv : dbs[i]->unicast) {
+      os << me << "\tR\t" << kv.first << '\t' << kv.second.igpCost << '\t';
+      if (kv.second.weight) os << *kv.second.weight; else os << '-';
+      os << '\n';
+      put("U", kv.first, kv.second.nextHops);
+    }
+    for (const auto& kv : dbs[i]->mpls) put("M", std::to_string(kv.first), kv.second);
+  }
+  return os.str();
+}
+}  // namespace
+
 char* odl_route_db_text(odl_ls* h, const char* mes_nl, uint32_t n_mes, const char* prefixes_nl,
                         uint32_t n, int flags) {
   return guard(h, [&]() -> char* {
     const auto mes = splitNl(mes_nl, n_mes);
-    const auto dbs = buildDbs(h, mes, prefixes_nl, n, flags);
-    std::ostringstream os;
-    for (size_t i = 0; i < mes.size(); ++i) {
-      const auto& me = mes[i];
-      if (!dbs[i]) {
-        os << me << "\tNONE\n";
-        continue;
-      }
-      // fields are tab-separated, records newline-separated: names holding
-      // either cannot be written unambiguously by this text ABI
-      auto plain = [](const std::string& f) {
-        if (f.find_first_of("\t\n") != std::string::npos)
-          throw std::invalid_argument("name with a tab or newline in the route text: " + f);
-      };
-      plain(me);
-      auto put = [&](const char* kind, const std::string& key, const std::vector<odl::NextHop>& nhs) {
-        for (const auto& x : nhs) {
-          plain(x.ifName);
-          plain(x.neighbor);
-          os << me << '\t' << kind << '\t' << key << '\t' << x.ifName << '\t' << x.neighbor << '\t'
-             << x.metric << '\t' << (int)x.op << '\t';
-          for (size_t j = 0; j < x.labels.size(); ++j) os << (j ? "," : "") << x.labels[j];
-          os << '\t' << x.weight << '\n';
-        }
-      };
-      for (const auto& kv : dbs[i]->unicast) {
-        os << me << "\tR\t" << kv.first << '\t' << kv.second.igpCost << '\t';
-        if (kv.second.weight) os << *kv.second.weight; else os << '-';
-        os << '\n';
-        put("U", kv.first, kv.second.nextHops);
-      }
-      for (const auto& kv : dbs[i]->mpls) put("M", std::to_string(kv.first), kv.second);
+    return dup(routeDbText(mes, buildDbs(h, mes, prefixes_nl, n, flags), false));
+  }, (char*)nullptr);
+}
+
+char* odl_route_db_multi_text(odl_ls* const* areas, uint32_t n_areas, const char* mes_nl,
+                              uint32_t n_mes, const char* prefixes_nl, uint32_t n, int flags) {
+  if (!areas || n_areas == 0 || !areas[0]) return nullptr;
+  return guard(areas[0], [&]() -> char* {
+    std::vector<odl::LinkState*> ls;
+    for (uint32_t i = 0; i < n_areas; ++i) {
+      if (!areas[i]) throw std::invalid_argument("null area handle");
+      ls.push_back(&areas[i]->ls);
     }
-    return dup(os.str());
+    const auto mes = splitNl(mes_nl, n_mes);
+    return dup(routeDbText(mes, buildDbs(areas[0], mes, prefixes_nl, n, flags, &ls), true));
   }, (char*)nullptr);
 }
 

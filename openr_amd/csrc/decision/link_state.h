@@ -355,6 +355,7 @@ class LinkState {
   LinkState(const LinkState&) = delete;
   LinkState& operator=(const LinkState&) = delete;
 
+  const std::string& area() const { return area_; }
   LinkStateChange updateAdjacencyDatabase(const AdjacencyDatabase& db);
   LinkStateChange deleteAdjacencyDatabase(const std::string& node);
   // A batch of databases in order (Decision's debounced batch,

@@ -10,12 +10,28 @@
 namespace odl {
 
 bool NextHop::operator<(const NextHop& o) const {
-  return std::tie(ifName, neighbor, metric, op, labels, weight) <
-         std::tie(o.ifName, o.neighbor, o.metric, o.op, o.labels, o.weight);
+  return std::tie(ifName, neighbor, metric, op, labels, weight, area) <
+         std::tie(o.ifName, o.neighbor, o.metric, o.op, o.labels, o.weight, o.area);
 }
 bool NextHop::operator==(const NextHop& o) const {
-  return std::tie(ifName, neighbor, metric, op, labels, weight) ==
-         std::tie(o.ifName, o.neighbor, o.metric, o.op, o.labels, o.weight);
+  return std::tie(ifName, neighbor, metric, op, labels, weight, area) ==
+         std::tie(o.ifName, o.neighbor, o.metric, o.op, o.labels, o.weight, o.area);
+}
+
+namespace {
+LinkState& firstArea(const std::vector<LinkState*>& areas) {
+  if (areas.empty()) throw std::invalid_argument("SpfSolver: no area");
+  return **std::min_element(areas.begin(), areas.end(),
+                            [](const LinkState* a, const LinkState* b) { return a->area() < b->area(); });
+}
+}  // namespace
+
+SpfSolver::SpfSolver(const std::vector<LinkState*>& areas) : ls_(firstArea(areas)) {
+  for (LinkState* a : areas) areas_.emplace_back(a->area(), a);
+  std::sort(areas_.begin(), areas_.end());
+  for (size_t i = 1; i < areas_.size(); ++i)
+    if (areas_[i].first == areas_[i - 1].first)
+      throw std::invalid_argument("SpfSolver: area " + areas_[i].first + " twice");
 }
 
 namespace {
@@ -25,8 +41,8 @@ void sortUnique(std::vector<NextHop>& v) {
 }
 }  // namespace
 
-int32_t SpfSolver::nodeLabel(const std::string& node) const {
-  const auto& dbs = ls_.getAdjacencyDatabases();
+int32_t SpfSolver::nodeLabel(const LinkState& ls, const std::string& node) {
+  const auto& dbs = ls.getAdjacencyDatabases();
   auto it = dbs.find(node);
   return it == dbs.end() ? 0 : it->second.nodeLabel;
 }
@@ -63,15 +79,25 @@ MinCostNextHops SpfSolver::nextHopsWithMetric(const SpfResult& spf,
 }
 
 std::vector<NextHop> SpfSolver::nextHopsThrift(
-    const std::string& me, const std::vector<std::string>& dsts, bool perDestination,
-    const MinCostNextHops& m, std::optional<int32_t> swapLabel,
-    const std::map<std::string, const PrefixEntry*>& entries, const NodeUcmpResult* ucmp) {
-  std::set<std::string> dstSet(dsts.begin(), dsts.end());
-  const std::vector<std::string> loop =
-      perDestination ? std::vector<std::string>(dstSet.begin(), dstSet.end())
-                     : std::vector<std::string>{std::string()};
+    size_t ai, const std::string& me, const std::vector<NodeArea>& dsts, bool perDestination,
+    const MinCostNextHops& m, std::optional<int32_t> swapLabel, const Entries& entries,
+    const NodeUcmpResult* ucmp) {
+  const std::string& area = areas_[ai].first;
+  const LinkState& ls = *areas_[ai].second;
+  std::set<std::string> dstSet;  // every destination node, any area
+  for (const auto& d : dsts) dstSet.insert(d.first);
+  // perDestination: the (node, area) pairs of this area (:1189-1194)
+  std::vector<std::string> loop;
+  if (perDestination) {
+    std::set<std::string> mine;
+    for (const auto& d : dsts)
+      if (d.second.empty() || d.second == area) mine.insert(d.first);
+    loop.assign(mine.begin(), mine.end());
+  } else {
+    loop.push_back(std::string());
+  }
   std::vector<NextHop> out;
-  for (const auto& link : ls_.linksFromNode(me)) {
+  for (const auto& link : ls.linksFromNode(me)) {
     const std::string& nbr = link->otherNode(me);
     for (const auto& dst : loop) {
       auto it = m.viaNode.find({nbr, dst});
@@ -85,6 +111,7 @@ std::vector<NextHop> SpfSolver::nextHopsThrift(
       nh.ifName = link->ifaceFrom(me);
       nh.neighbor = nbr;
       nh.metric = toThriftMetric(over);
+      nh.area = area;
       if (swapLabel) {
         if (dstSet.count(nbr)) {
           nh.op = MplsOp::kPhp;
@@ -97,13 +124,13 @@ std::vector<NextHop> SpfSolver::nextHopsThrift(
         // SR_MPLS towards dst: prepend label, then dst's node label unless
         // dst is the neighbour (:1231-1261); an invalid label drops the hop
         std::vector<int32_t> push;
-        const PrefixEntry* e = entries.at(dst);
+        const PrefixEntry* e = entries.at({dst, area});
         if (e->prependLabel) {
           push.push_back(*e->prependLabel);
           if (!isMplsLabelValid(push.back())) continue;
         }
         if (dst != nbr) {
-          push.push_back(nodeLabel(dst));
+          push.push_back(nodeLabel(ls, dst));
           if (!isMplsLabelValid(push.back())) continue;
         }
         if (!push.empty()) {
@@ -128,7 +155,9 @@ std::vector<NextHop> SpfSolver::ecmpRoute(const std::string& me,
     return {};  // self-originated: no route
   auto m = nextHopsWithMetric(me, announcers, false);
   if (m.viaNode.empty()) return {};
-  return nextHopsThrift(me, announcers, false, m, std::nullopt, {}, nullptr);
+  std::vector<NodeArea> d;
+  for (const auto& n : announcers) d.emplace_back(n, ls_.area());
+  return nextHopsThrift(lsIndex(), me, d, false, m, std::nullopt, {}, nullptr);
 }
 
 std::vector<NextHop> SpfSolver::nodeLabelRoute(const std::string& me, const std::string& dst) {
@@ -140,26 +169,32 @@ std::vector<NextHop> SpfSolver::nodeLabelRoute(const std::string& me, const std:
   if (dst == me) return {};  // POP_AND_LOOKUP, not an SPF product
   auto m = nextHopsWithMetric(mine, {dst}, false);
   if (m.viaNode.empty()) return {};
-  return nextHopsThrift(me, {dst}, false, m, nodeLabel(dst), {}, nullptr);
+  return nextHopsThrift(lsIndex(), me, {{dst, ls_.area()}}, false, m, nodeLabel(dst), {}, nullptr);
 }
 
 std::vector<NextHop> SpfSolver::ksp2Route(const std::string& me,
                                           const std::vector<std::string>& announcers) {
-  return ksp2Paths(me, announcers, {});
+  std::set<NodeArea> best;
+  for (const auto& n : announcers) best.emplace(n, ls_.area());
+  return ksp2Paths(lsIndex(), me, best, {});
 }
 
-std::vector<NextHop> SpfSolver::ksp2Paths(const std::string& me,
-                                          const std::vector<std::string>& announcers,
-                                          const std::map<std::string, const PrefixEntry*>& entries) {
-  // selectBestPathsKsp2 (SpfSolver.cpp:847-973), one area
+std::vector<NextHop> SpfSolver::ksp2Paths(size_t ai, const std::string& me,
+                                          const std::set<NodeArea>& best, const Entries& entries) {
+  // selectBestPathsKsp2 (SpfSolver.cpp:847-973) in area ai: k = 1 paths to
+  // every best node (any area's entry, but not ourselves in this area),
+  // k = 2 paths to the best nodes of this area not covering a k = 1 path
+  const std::string& area = areas_[ai].first;
+  LinkState& ls = *areas_[ai].second;
   std::vector<Path> paths;
-  for (const auto& node : announcers) {
-    if (node == me) continue;
-    for (const auto& p : ls_.getKthPaths(me, node, 1)) paths.push_back(p);
+  for (const auto& [node, a] : best) {
+    if (node == me && a == area) continue;
+    for (const auto& p : ls.getKthPaths(me, node, 1)) paths.push_back(p);
   }
   const size_t firstPaths = paths.size();
-  for (const auto& node : announcers) {
-    for (const auto& p : ls_.getKthPaths(me, node, 2)) {
+  for (const auto& [node, a] : best) {
+    if (a != area) continue;
+    for (const auto& p : ls.getKthPaths(me, node, 2)) {
       bool covered = false;
       for (size_t i = 0; i < firstPaths && !covered; ++i)
         covered = LinkState::pathAInPathB(paths[i], p);
@@ -175,19 +210,22 @@ std::vector<NextHop> SpfSolver::ksp2Paths(const std::string& me,
     for (const auto& l : p) {
       cost += l->metricFrom(at);
       at = l->otherNode(at);
-      const int32_t lbl = nodeLabel(at);
+      const int32_t lbl = nodeLabel(ls, at);
       stack.insert(stack.begin(), lbl);
       valid &= isMplsLabelValid(lbl);
     }
     if (!valid) continue;
     stack.pop_back();  // PHP: the first hop's label
-    auto e = entries.find(at);
+    // the last node's entry in this area (the reference's
+    // prefixEntries.at({lastNode, area}); absent: no prepend label)
+    auto e = entries.find({at, area});
     if (e != entries.end() && e->second->prependLabel)
       stack.insert(stack.begin(), *e->second->prependLabel);  // bottom of stack
     NextHop nh;
     nh.ifName = p.front()->ifaceFrom(me);
     nh.neighbor = p.front()->otherNode(me);
     nh.metric = toThriftMetric(cost);
+    nh.area = area;
     if (!stack.empty()) {
       nh.op = MplsOp::kPush;
       nh.labels = std::move(stack);
@@ -200,92 +238,159 @@ std::vector<NextHop> SpfSolver::ksp2Paths(const std::string& me,
 
 std::optional<UnicastRoute> SpfSolver::prefixRoute(const std::string& me, const PrefixRoute& pr,
                                                    const RouteOptions& opt) {
-  return prefixRoute(me, pr, opt, ls_.getSpfResult(me));
+  std::vector<const SpfResult*> mines;
+  for (auto& a : areas_) mines.push_back(&a.second->getSpfResult(me));
+  return prefixRoute(me, pr, opt, mines);
 }
 
 std::optional<UnicastRoute> SpfSolver::prefixRoute(const std::string& me, const PrefixRoute& pr,
-                                                   const RouteOptions& opt, const SpfResult& mine) {
-  // entries of reachable announcers only (:225-253)
-  std::map<std::string, const PrefixEntry*> entries;
-  for (const auto& e : pr.entries)
-    if (mine.count(e.node)) entries.emplace(e.node, &e);
+                                                   const RouteOptions& opt,
+                                                   const std::vector<const SpfResult*>& mines) {
+  auto areaIx = [&](const std::string& a) -> size_t {
+    for (size_t i = 0; i < areas_.size(); ++i)
+      if (areas_[i].first == a) return i;
+    // the reference reads areaLinkStates.at(area) (maybeFilterDrainedNodes)
+    throw std::invalid_argument("prefix entry of unknown area " + a);
+  };
+  // (node, area) entries of reachable announcers only: an entry is dropped
+  // when its node is not reached in its own area (:225-253)
+  Entries entries;
+  for (const auto& e : pr.entries) {
+    const std::string& a = e.area.empty() ? areas_[0].first : e.area;
+    if (mines[areaIx(a)]->count(e.node)) entries.emplace(NodeArea{e.node, a}, &e);
+  }
   if (entries.empty()) return std::nullopt;
   bool selfPrepend = true;
-  if (auto s = entries.find(me); s != entries.end()) selfPrepend = s->second->prependLabel.has_value();
-  // every reachable announcer is a best route; drained (overloaded)
-  // announcers drop out unless all are drained (maybeFilterDrainedNodes :709-731)
-  std::vector<std::string> best;
+  for (const auto& [na, e] : entries)
+    if (na.first == me) selfPrepend &= e->prependLabel.has_value();
+  // every reachable announcer is a best route (selectBestRoutes' non-BGP
+  // branch, :666-672); drained announcers drop out unless all are drained
+  // (maybeFilterDrainedNodes :709-731)
+  std::set<NodeArea> best;
   for (const auto& kv : entries)
-    if (!ls_.isNodeOverloaded(kv.first)) best.push_back(kv.first);
+    if (!areas_[areaIx(kv.first.second)].second->isNodeOverloaded(kv.first.first)) best.insert(kv.first);
   if (best.empty())
-    for (const auto& kv : entries) best.push_back(kv.first);
-  const bool hasMe = std::find(best.begin(), best.end(), me) != best.end();
+    for (const auto& kv : entries) best.insert(kv.first);
+  auto hasNode = [&](const std::string& n) {
+    for (const auto& na : best)
+      if (na.first == n) return true;
+    return false;
+  };
+  const bool hasMe = hasNode(me);
   if (hasMe && !selfPrepend) return std::nullopt;  // :333-337
-  // forwarding type and algorithm: the minimum over the best entries
+  // per area (default route computation rules, :1288-1317): forwarding type
+  // and algorithm = the minimum over the area's best entries
   // (getPrefixForwardingTypeAndAlgorithm, LsdbUtil.cpp:379-413)
-  int fwdType = 1, algo = 3;
-  for (const auto& n : best) {
-    fwdType = std::min(fwdType, entries.at(n)->fwdType);
-    algo = std::min(algo, entries.at(n)->algo);
-  }
-  UnicastRoute route;
+  std::set<NextHop> total, ksp;
+  std::optional<int64_t> ucmpWeight;
   Metric shortest = std::numeric_limits<Metric>::max();
-  if (algo == 1) {
-    // KSP2_ED_ECMP needs SR_MPLS (:860-870)
-    if (fwdType == 1) route.nextHops = ksp2Paths(me, best, entries);
-  } else {
-    // selectBestPathsSpf (:772-845)
-    const bool perDestination = fwdType == 1;
-    std::vector<std::string> filtered = best;
-    if (hasMe && perDestination && entries.at(me)->prependLabel)
-      filtered.erase(std::find(filtered.begin(), filtered.end(), me));
-    const MinCostNextHops m = nextHopsWithMetric(mine, filtered, perDestination);
-    shortest = m.shortest;
-    if (!m.viaNode.empty()) {
-      // getNodeUcmpResult (:1091-1161): weights of the best announcers at the
-      // best metric; one without a weight turns UCMP off
-      std::optional<NodeUcmpResult> ucmp;
-      if (opt.ucmp && (algo == 2 || algo == 3)) {
-        std::unordered_map<std::string, int64_t> weights;
-        bool ok = true;
-        for (const auto& n : best) {
-          auto it = mine.find(n);
-          if (it == mine.end() || it->second.metric() != m.shortest) continue;
-          if (entries.at(n)->weight == 0) {
-            ok = false;
+  for (size_t ai = 0; ai < areas_.size(); ++ai) {
+    const std::string& area = areas_[ai].first;
+    const SpfResult& mine = *mines[ai];
+    bool any = false;
+    int fwdType = 1, algo = 3;
+    for (const auto& na : best) {
+      if (na.second != area) continue;
+      const PrefixEntry* e = entries.at(na);
+      fwdType = any ? std::min(fwdType, e->fwdType) : e->fwdType;
+      algo = any ? std::min(algo, e->algo) : e->algo;
+      any = true;
+    }
+    if (!any) continue;
+    if (algo == 1) {
+      // KSP2_ED_ECMP needs SR_MPLS (:860-870)
+      if (fwdType == 1) {
+        auto nhs = ksp2Paths(ai, me, best, entries);
+        ksp.insert(nhs.begin(), nhs.end());
+      }
+    } else {
+      // selectBestPathsSpf (:772-845): destinations = the best nodes of every
+      // area, looked up in this area's SPF
+      const bool perDestination = fwdType == 1;
+      std::set<NodeArea> filtered = best;
+      if (hasMe && perDestination)
+        for (const auto& [na, e] : entries)
+          if (na.first == me && e->prependLabel) {
+            filtered.erase(na);
             break;
           }
-          weights.emplace(n, entries.at(n)->weight);
+      std::vector<std::string> dsts;
+      for (const auto& na : filtered) dsts.push_back(na.first);
+      const MinCostNextHops m = nextHopsWithMetric(mine, dsts, perDestination);
+      std::vector<NextHop> nhs;
+      std::optional<int64_t> weight;
+      if (!m.viaNode.empty()) {
+        // getNodeUcmpResult (:1091-1161): weights of this area's best
+        // announcers at the best metric; one without a weight turns UCMP off
+        std::optional<NodeUcmpResult> ucmp;
+        if (opt.ucmp && (algo == 2 || algo == 3)) {
+          std::unordered_map<std::string, int64_t> weights;
+          bool ok = true;
+          for (const auto& na : best) {
+            if (na.second != area) continue;
+            auto it = mine.find(na.first);
+            if (it == mine.end() || it->second.metric() != m.shortest) continue;
+            if (entries.at(na)->weight == 0) {
+              ok = false;
+              break;
+            }
+            weights.emplace(na.first, entries.at(na)->weight);
+          }
+          if (ok) {
+            auto res = areas_[ai].second->resolveUcmpWeights(mine, weights, (UcmpAlgo)algo);
+            auto it = res.find(me);
+            if (it != res.end()) ucmp = std::move(it->second);
+          }
         }
-        if (ok) {
-          auto res = ls_.resolveUcmpWeights(mine, weights, (UcmpAlgo)algo);
-          auto it = res.find(me);
-          if (it != res.end()) ucmp = std::move(it->second);
-        }
+        if (ucmp) weight = ucmp->weight();
+        std::vector<NodeArea> bestv(best.begin(), best.end());
+        nhs = nextHopsThrift(ai, me, bestv, perDestination, m, std::nullopt, entries,
+                             ucmp ? &*ucmp : nullptr);
       }
-      if (ucmp) route.weight = ucmp->weight();
-      route.nextHops = nextHopsThrift(me, best, perDestination, m, std::nullopt, entries,
-                                      ucmp ? &*ucmp : nullptr);
+      // only the areas at the shortest IGP metric contribute (:392-407)
+      if (shortest >= m.shortest) {
+        if (shortest > m.shortest) {
+          shortest = m.shortest;
+          total.clear();
+          ucmpWeight.reset();
+        }
+        total.insert(nhs.begin(), nhs.end());
+        if (!ucmpWeight) ucmpWeight = weight;
+        else if (weight) *ucmpWeight += *weight;
+      }
     }
+    total.insert(ksp.begin(), ksp.end());  // KSP2 next hops merged (:436-437)
   }
-  // addBestPaths (:976-1041): no next hop, no route
-  if (route.nextHops.empty()) return std::nullopt;
+  // addBestPaths (:976-1041): no next hop, no route; minNexthop = the largest
+  // over the best entries (getMinNextHopThreshold :694-710)
+  if (total.empty()) return std::nullopt;
+  std::optional<int64_t> minNh;
+  for (const auto& na : best) {
+    const auto& mn = entries.at(na)->minNexthop;
+    if (mn && (!minNh || *mn > *minNh)) minNh = mn;
+  }
+  if (minNh && *minNh > (int64_t)total.size()) return std::nullopt;
+  UnicastRoute route;
+  route.nextHops.assign(total.begin(), total.end());
   route.igpCost = (uint32_t)shortest;
+  route.weight = ucmpWeight;
   return route;
 }
 
 std::optional<RouteDb> SpfSolver::buildRouteDb(const std::string& me,
                                                const std::vector<PrefixRoute>& prefixes,
                                                const RouteOptions& opt) {
-  const auto& dbs = ls_.getAdjacencyDatabases();
-  if (!dbs.count(me)) return std::nullopt;
+  bool exists = false;  // :463-471: `me` in some area's link state
+  for (const auto& a : areas_) exists |= a.second->getAdjacencyDatabases().count(me) > 0;
+  if (!exists) return std::nullopt;
   RouteDb db;
-  // The SP prefixes read only the memoised SPF of `me` (and const link
-  // state): they are built on host threads. A prefix with a KSP2 entry runs
-  // getKthPaths, which fills a memo, so those are built on this thread.
-  // `mine` is looked up (and memoised) here, on the calling thread; the
-  // host threads below only read it
-  const SpfResult& mine = ls_.getSpfResult(me);
+  // The SP prefixes read only the memoised SPF of `me` in each area (and
+  // const link state): they are built on host threads. A prefix with a KSP2
+  // entry runs getKthPaths, which fills a memo, so those are built on this
+  // thread. The results are looked up (and memoised) here, on the calling
+  // thread; the host threads below only read them
+  std::vector<const SpfResult*> mines;
+  for (auto& a : areas_) mines.push_back(&a.second->getSpfResult(me));
   std::vector<std::optional<UnicastRoute>> routes(prefixes.size());
   std::vector<uint32_t> sp, ksp;
   for (uint32_t i = 0; i < prefixes.size(); ++i) {
@@ -294,61 +399,74 @@ std::optional<RouteDb> SpfSolver::buildRouteDb(const std::string& me,
     (k ? ksp : sp).push_back(i);
   }
   parallelFor((uint32_t)sp.size(), [&](uint32_t lo, uint32_t hi) {
-    for (uint32_t j = lo; j < hi; ++j) routes[sp[j]] = prefixRoute(me, prefixes[sp[j]], opt, mine);
+    for (uint32_t j = lo; j < hi; ++j) routes[sp[j]] = prefixRoute(me, prefixes[sp[j]], opt, mines);
   }, 256);
-  for (const uint32_t i : ksp) routes[i] = prefixRoute(me, prefixes[i], opt);
+  for (const uint32_t i : ksp) routes[i] = prefixRoute(me, prefixes[i], opt, mines);
   for (uint32_t i = 0; i < prefixes.size(); ++i) {
     if (!routes[i]) continue;
     if (!db.unicast.emplace(prefixes[i].prefix, std::move(*routes[i])).second)
       throw std::invalid_argument("duplicate prefix " + prefixes[i].prefix);
   }
-  // node-label routes (:501-598): on a label collision the smallest node name
-  // keeps it (the reference's `iter->second.first < nodeName` rule, in any
-  // order); an unreachable node leaves no route and takes nothing over
+  // node-label routes (:501-598), every area's databases in area order: on a
+  // label collision the smallest node name keeps it (the reference's
+  // `iter->second.first < nodeName` rule, in any order; the same node in two
+  // areas: the later area); an unreachable node leaves no route and takes
+  // nothing over
   if (opt.nodeSegmentLabels) {
-    std::vector<std::string> names;
-    names.reserve(dbs.size());
-    for (const auto& kv : dbs) names.push_back(kv.first);
-    std::sort(names.begin(), names.end());
-    // candidate routes of every labelled node, on host threads
-    std::vector<std::vector<NextHop>> cand(names.size());
-    parallelFor((uint32_t)names.size(), [&](uint32_t lo, uint32_t hi) {
-      for (uint32_t j = lo; j < hi; ++j) {
-        const int32_t top = dbs.at(names[j]).nodeLabel;
-        if (top != 0 && isMplsLabelValid(top) && names[j] != me)
-          cand[j] = nodeLabelRoute(me, names[j], mine);
-      }
-    }, 256);
     std::map<int32_t, std::pair<std::string, std::vector<NextHop>>> labelToNode;
-    for (size_t j = 0; j < names.size(); ++j) {
-      const std::string& node = names[j];
-      const int32_t top = dbs.at(node).nodeLabel;
-      if (top == 0 || !isMplsLabelValid(top)) continue;
-      auto it = labelToNode.find(top);
-      if (it != labelToNode.end() && it->second.first < node) continue;
-      if (node == me) {
-        NextHop pop;
-        pop.op = MplsOp::kPopAndLookup;
-        labelToNode[top] = {me, {pop}};
-        continue;
+    for (size_t ai = 0; ai < areas_.size(); ++ai) {
+      const LinkState& ls = *areas_[ai].second;
+      const auto& dbs = ls.getAdjacencyDatabases();
+      std::vector<std::string> names;
+      names.reserve(dbs.size());
+      for (const auto& kv : dbs) names.push_back(kv.first);
+      std::sort(names.begin(), names.end());
+      // candidate routes of every labelled node, on host threads
+      std::vector<std::vector<NextHop>> cand(names.size());
+      parallelFor((uint32_t)names.size(), [&](uint32_t lo, uint32_t hi) {
+        for (uint32_t j = lo; j < hi; ++j) {
+          const int32_t top = dbs.at(names[j]).nodeLabel;
+          if (top == 0 || !isMplsLabelValid(top) || names[j] == me) continue;
+          auto m = nextHopsWithMetric(*mines[ai], {names[j]}, false);
+          if (!m.viaNode.empty())
+            cand[j] = nextHopsThrift(ai, me, {{names[j], areas_[ai].first}}, false, m, top, {}, nullptr);
+        }
+      }, 256);
+      for (size_t j = 0; j < names.size(); ++j) {
+        const std::string& node = names[j];
+        const int32_t top = dbs.at(node).nodeLabel;
+        if (top == 0 || !isMplsLabelValid(top)) continue;
+        auto it = labelToNode.find(top);
+        if (it != labelToNode.end() && it->second.first < node) continue;
+        if (node == me) {
+          NextHop pop;
+          pop.op = MplsOp::kPopAndLookup;
+          pop.area = areas_[ai].first;
+          labelToNode[top] = {me, {pop}};
+          continue;
+        }
+        if (cand[j].empty()) continue;
+        labelToNode[top] = {node, std::move(cand[j])};
       }
-      if (cand[j].empty()) continue;
-      labelToNode[top] = {node, std::move(cand[j])};
     }
     for (auto& kv : labelToNode) db.mpls.emplace(kv.first, std::move(kv.second.second));
   }
-  // adjacency-label routes (:603-631): PHP over each of our links (up or not)
+  // adjacency-label routes (:603-631): PHP over each of our links (up or
+  // not), every area
   if (opt.adjacencyLabels) {
-    for (const auto& link : ls_.linksFromNode(me)) {
-      const int32_t top = link->adjLabelFrom(me);
-      if (top == 0 || !isMplsLabelValid(top)) continue;
-      NextHop nh;
-      nh.ifName = link->ifaceFrom(me);
-      nh.neighbor = link->otherNode(me);
-      nh.metric = toThriftMetric(link->metricFrom(me));
-      nh.op = MplsOp::kPhp;
-      if (!db.mpls.emplace(top, std::vector<NextHop>{nh}).second)
-        throw std::invalid_argument("duplicate MPLS label " + std::to_string(top));
+    for (const auto& [area, ls] : areas_) {
+      for (const auto& link : ls->linksFromNode(me)) {
+        const int32_t top = link->adjLabelFrom(me);
+        if (top == 0 || !isMplsLabelValid(top)) continue;
+        NextHop nh;
+        nh.ifName = link->ifaceFrom(me);
+        nh.neighbor = link->otherNode(me);
+        nh.metric = toThriftMetric(link->metricFrom(me));
+        nh.op = MplsOp::kPhp;
+        nh.area = area;
+        if (!db.mpls.emplace(top, std::vector<NextHop>{nh}).second)
+          throw std::invalid_argument("duplicate MPLS label " + std::to_string(top));
+      }
     }
   }
   return db;
@@ -357,11 +475,21 @@ std::optional<RouteDb> SpfSolver::buildRouteDb(const std::string& me,
 std::vector<std::optional<RouteDb>> SpfSolver::buildRouteDbs(
     const std::vector<std::string>& mes, const std::vector<PrefixRoute>& prefixes,
     const RouteOptions& opt) {
+  std::vector<std::optional<RouteDb>> out;
+  out.reserve(mes.size());
+  if (areas_.size() > 1) {  // one batched launch per area, then the builds
+    for (auto& a : areas_) {
+      std::vector<std::string> roots;
+      for (const auto& me : mes)
+        if (a.second->getAdjacencyDatabases().count(me)) roots.push_back(me);
+      a.second->prefetchSpf(roots, true);
+    }
+    for (const auto& me : mes) out.push_back(buildRouteDb(me, prefixes, opt));
+    return out;
+  }
   std::vector<std::string> roots;
   for (const auto& me : mes)
     if (ls_.getAdjacencyDatabases().count(me)) roots.push_back(me);
-  std::vector<std::optional<RouteDb>> out;
-  out.reserve(mes.size());
   const size_t V = ls_.numNodes();
   if (roots.size() < LinkState::kSweepMinRoots || 2 * roots.size() < V) {
     ls_.prefetchSpf(roots, true);

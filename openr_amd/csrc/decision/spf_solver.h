@@ -6,14 +6,20 @@
 //   selectBestPathsSpf      openr/decision/SpfSolver.cpp:772-845 (UCMP too)
 //   selectBestPathsKsp2     openr/decision/SpfSolver.cpp:847-973
 //   createRouteForPrefix / buildRouteDb  SpfSolver.cpp:197-646
-// RIB policy (BGP metric vectors, prefix-metric best-route selection,
-// minNexthop, static routes, multi-area merge) is outside the SPF path and
-// not restated here.
+// Several areas (one LinkState each): createRouteForPrefix's per-area loop
+// (:229-250, :360-442: the shortest areas' next hops merged, UCMP weights
+// summed, KSP2 next hops added), the node-label loop over every area's
+// databases (:490-598) and the adjacency labels of every area (:603-631);
+// addBestPaths' minNexthop threshold (:976-1000 with
+// getMinNextHopThreshold :694-710). RIB policy beyond that (BGP metric
+// vectors, prefix-metric best-route selection, SR policies, static routes)
+// is outside the SPF path and not restated here.
 #pragma once
 
 #include <cstdint>
 #include <map>
 #include <optional>
+#include <set>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -35,6 +41,7 @@ struct NextHop {
   MplsOp op = MplsOp::kNone;
   std::vector<int32_t> labels;  // SWAP: {label}; PUSH: stack, bottom first
   int32_t weight = 0;           // UCMP next-hop weight, 0 = ECMP
+  std::string area;             // the area whose link the next hop leaves on
   bool operator<(const NextHop& o) const;
   bool operator==(const NextHop& o) const;
 };
@@ -56,6 +63,8 @@ struct PrefixEntry {
   int algo = 0;
   int64_t weight = 0;
   std::optional<int32_t> prependLabel;
+  std::string area;                  // "" = the solver's first area
+  std::optional<int64_t> minNexthop;  // PrefixEntry.minNexthop (Types.thrift)
 };
 struct PrefixRoute {
   std::string prefix;
@@ -93,7 +102,10 @@ struct MinCostNextHops {
 
 class SpfSolver {
  public:
-  explicit SpfSolver(LinkState& ls) : ls_(ls) {}
+  explicit SpfSolver(LinkState& ls) : ls_(ls), areas_{{ls.area(), &ls}} {}
+  // one LinkState per area (LinkState::area() names it); ls_ = the first by
+  // name (the single-area helpers below use it)
+  explicit SpfSolver(const std::vector<LinkState*>& areas);
 
   // getNextHopsWithMetric (SpfSolver.cpp:1043-1089)
   MinCostNextHops nextHopsWithMetric(const std::string& me, const std::vector<std::string>& dsts,
@@ -112,12 +124,14 @@ class SpfSolver {
   // KSP2_ED_ECMP route (SR-MPLS label stacks) over `announcers` (entries
   // without prepend labels)
   std::vector<NextHop> ksp2Route(const std::string& me, const std::vector<std::string>& announcers);
-  // createRouteForPrefix (SpfSolver.cpp:197-458), one area, non-BGP
+  // createRouteForPrefix (SpfSolver.cpp:197-458), every area, non-BGP
   std::optional<UnicastRoute> prefixRoute(const std::string& me, const PrefixRoute& pr,
                                           const RouteOptions& opt);
-  // over `me`'s SPF result (`mine`): what buildRouteDb runs on host threads
+  // over `me`'s SPF result in each area (`mines`, areas_ order): what
+  // buildRouteDb runs on host threads
   std::optional<UnicastRoute> prefixRoute(const std::string& me, const PrefixRoute& pr,
-                                          const RouteOptions& opt, const SpfResult& mine);
+                                          const RouteOptions& opt,
+                                          const std::vector<const SpfResult*>& mines);
   // SpfSolver::buildRouteDb (SpfSolver.cpp:460-646), one area: unicast routes
   // of `prefixes`, MPLS node-label routes of every node (POP_AND_LOOKUP for
   // our own label, PHP / SWAP towards the others, :501-598) and
@@ -134,16 +148,26 @@ class SpfSolver {
                                                     const RouteOptions& opt = RouteOptions{});
 
  private:
-  // getNextHopsThrift (SpfSolver.cpp:1163-1285)
-  std::vector<NextHop> nextHopsThrift(const std::string& me, const std::vector<std::string>& dsts,
-                                      bool perDestination, const MinCostNextHops& m,
-                                      std::optional<int32_t> swapLabel,
-                                      const std::map<std::string, const PrefixEntry*>& entries,
-                                      const NodeUcmpResult* ucmp);
-  std::vector<NextHop> ksp2Paths(const std::string& me, const std::vector<std::string>& announcers,
-                                 const std::map<std::string, const PrefixEntry*>& entries);
-  int32_t nodeLabel(const std::string& node) const;
+  using NodeArea = std::pair<std::string, std::string>;
+  using Entries = std::map<NodeArea, const PrefixEntry*>;
+  // getNextHopsThrift (SpfSolver.cpp:1163-1285) over area `ai`'s links;
+  // dsts = (node, area) pairs, perDestination reads those of this area
+  std::vector<NextHop> nextHopsThrift(size_t ai, const std::string& me,
+                                      const std::vector<NodeArea>& dsts, bool perDestination,
+                                      const MinCostNextHops& m, std::optional<int32_t> swapLabel,
+                                      const Entries& entries, const NodeUcmpResult* ucmp);
+  // selectBestPathsKsp2 (SpfSolver.cpp:847-973) in area `ai`
+  std::vector<NextHop> ksp2Paths(size_t ai, const std::string& me, const std::set<NodeArea>& best,
+                                 const Entries& entries);
+  static int32_t nodeLabel(const LinkState& ls, const std::string& node);
+  size_t lsIndex() const {
+    for (size_t i = 0; i < areas_.size(); ++i)
+      if (areas_[i].second == &ls_) return i;
+    return 0;
+  }
+  int32_t nodeLabel(const std::string& node) const { return nodeLabel(ls_, node); }
   LinkState& ls_;
+  std::vector<std::pair<std::string, LinkState*>> areas_;  // by area name
 };
 
 }  // namespace odl

@@ -552,14 +552,16 @@ struct DistDecr {
   const L_* L;
   __device__ uint32_t operator()(uint32_t u) const {
     const volatile uint32_t* keys = L->keys;
-    for (uint32_t h = dslot(u);; ++h) {
+    uint32_t h = dslot(u);
+    for (uint32_t p = 0; p < L_::kMap; ++p, ++h) {  // (the map never fills: kFill)
       const uint32_t k = keys[h & (L_::kMap - 1u)];
       if (k == u + 1u) {
         const uint32_t v = ((const volatile uint32_t*)L->vals)[h & (L_::kMap - 1u)];
         return (v & kAffFlag) ? ((const volatile uint32_t*)L->dp)[v & ~kAffFlag] : D[u];
       }
-      if (k == 0u) return D[u];
+      if (k == 0u) break;
     }
+    return D[u];
   }
 };
 
@@ -588,11 +590,13 @@ __global__ void __launch_bounds__(256) ksp_hint_kernel(DevGraph g, uint32_t src,
 template <class L_>
 __device__ __forceinline__ uint32_t map_find(const L_& L, uint32_t u) {  // slot, kInf: absent
   const volatile uint32_t* keys = L.keys;
-  for (uint32_t h = dslot(u);; ++h) {
+  uint32_t h = dslot(u);
+  for (uint32_t p = 0; p < L_::kMap; ++p, ++h) {
     const uint32_t k = keys[h & (L_::kMap - 1u)];
     if (k == u + 1u) return h & (L_::kMap - 1u);
     if (k == 0u) return kInf;
   }
+  return kInf;
 }
 // index of u in A, kInf: not affected
 template <class L_>
@@ -606,6 +610,7 @@ __device__ __forceinline__ uint32_t aff_ix(const L_& L, uint32_t u) {
 template <class L_>
 __device__ __forceinline__ uint32_t map_insert(L_& L, uint32_t u) {
   volatile uint32_t* keys = L.keys;
+  if (((volatile uint32_t&)L.ovf)) return kInf;  // past the budget: the run is abandoned
   uint32_t h = dslot(u);
   for (uint32_t p = 0; p < L_::kMap; ++p, ++h) {
     const uint32_t sl = h & (L_::kMap - 1u);
@@ -615,7 +620,7 @@ __device__ __forceinline__ uint32_t map_insert(L_& L, uint32_t u) {
     }
     const uint32_t old = atomicCAS(&L.keys[sl], 0u, u + 1u);
     if (old == 0u) {
-      if (atomicAdd(&L.nkeys, 1u) >= L_::kFill) L.ovf = 1u;
+      if (atomicAdd(&L.nkeys, 1u) >= L_::kFill) L.ovf = 1u;  // <= kFill + 63 keys: empty slots stay
       return sl;
     }
     if (old == u + 1u) return sl;

@@ -110,6 +110,68 @@ def _parse_spf(t: str) -> Dict[str, Tuple[int, tuple, tuple]]:
     return out
 
 
+_FWDS = {"ip": 0, "sr_mpls": 1}
+_ALGOS = {"ecmp": 0, "ksp2": 1, "ucmp_adj": 2, "ucmp_prefix": 3}
+_TXT_OPS = {"0": "", "1": "PHP", "2": "SWAP", "3": "PUSH", "4": "POP"}
+
+
+def _prefix_lines(prefixes) -> List[str]:
+    """{prefix: [(node, fwd, algo, weight, prepend[, area[, min_nexthop]])]}
+    -> the text ABI's "prefix\tnode:fwd:algo:weight:prepend[@area][#n],..." lines"""
+    lines = []
+    for p, ents in prefixes.items():
+        es = []
+        for ent in ents:
+            node, fwd, algo, weight, prepend = ent[:5]
+            area = ent[5] if len(ent) > 5 else None
+            mn = ent[6] if len(ent) > 6 else None
+            x = (f"{node}:{_FWDS[fwd]}:{_ALGOS[algo]}:{int(weight)}:"
+                 f"{'' if prepend is None else int(prepend)}")
+            if area:
+                x += f"@{area}"
+            if mn is not None:
+                x += f"#{int(mn)}"
+            es.append(x)
+        lines.append(f"{p}\t{','.join(es)}")
+    return lines
+
+
+def _parse_route_text(t: str, mes, with_area: bool):
+    out = {me: {"routes": {}} for me in mes}
+    for ln in t.splitlines():
+        f = ln.split("\t")
+        me, kind = f[0], f[1]
+        if kind == "NONE":
+            out[me] = None
+        elif kind == "R":
+            out[me]["routes"][f[2]] = (int(f[3]), None if f[4] == "-" else int(f[4]))
+        else:
+            key, ifn, nbr, metric, op, labels, w = f[2:9]
+            nh = (ifn, nbr, int(metric), _TXT_OPS[op], tuple(int(x) for x in labels.split(",") if x),
+                  int(w))
+            if with_area:
+                nh += (f[9],)
+            out[me].setdefault((kind, key), set()).add(nh)
+    return out
+
+
+def route_dbs_multi(areas: Sequence["LinkState"], mes: Sequence[str], prefixes,
+                    node_labels: bool = True, adj_labels: bool = True, ucmp: bool = False):
+    """SpfSolver::buildRouteDb over several areas (odl_route_db_multi_text):
+    one LinkState per area; prefix entries may carry (.., area, min_nexthop).
+    Same result shape as LinkState.route_dbs(binary=False) with the next
+    hop's area as a 7th tuple field."""
+    L = N.decision()
+    hs = (C.c_void_p * len(areas))(*[a._h for a in areas])
+    lines = _prefix_lines(prefixes)
+    flags = int(node_labels) | (2 if adj_labels else 0) | (4 if ucmp else 0)
+    p = L.odl_route_db_multi_text(hs, len(areas), "\n".join(mes).encode(), len(mes),
+                                  "\n".join(lines).encode(), len(lines), flags)
+    if not p:
+        raise LinkStateError(areas[0]._err())
+    return _parse_route_text(areas[0]._take(p), mes, with_area=True)
+
+
 class LinkState:
     """odl::LinkState over the MI355X SPF engine (device `device`)."""
 
@@ -201,36 +263,14 @@ class LinkState:
         (kind, key): set of (ifName, neighbor, metric, op, labels, weight)}}
         with kind 'U' (prefix) or 'M' (MPLS label) and op 'PHP' | 'SWAP' |
         'PUSH' | 'POP' | ''."""
-        fwds = {"ip": 0, "sr_mpls": 1}
-        algos = {"ecmp": 0, "ksp2": 1, "ucmp_adj": 2, "ucmp_prefix": 3}
-        lines = []
-        for p, ents in prefixes.items():
-            es = []
-            for (node, fwd, algo, weight, prepend) in ents:
-                es.append(f"{node}:{fwds[fwd]}:{algos[algo]}:{int(weight)}:"
-                          f"{'' if prepend is None else int(prepend)}")
-            lines.append(f"{p}\t{','.join(es)}")
+        lines = _prefix_lines(prefixes)
         flags = int(node_labels) | (2 if adj_labels else 0) | (4 if ucmp else 0)
         if binary:  # odl_route_db_bin: records + a string table, no text
             return decode_route_db_bin(self.route_db_bin_raw(mes, lines, flags))
         t = self._take(self._L.odl_route_db_text(
             self._h, "\n".join(mes).encode(), len(mes), "\n".join(lines).encode(),
             len(lines), flags))
-        ops = {"0": "", "1": "PHP", "2": "SWAP", "3": "PUSH", "4": "POP"}
-        out = {me: {"routes": {}} for me in mes}
-        for ln in t.splitlines():
-            f = ln.split("\t")
-            me, kind = f[0], f[1]
-            if kind == "NONE":
-                out[me] = None
-            elif kind == "R":
-                out[me]["routes"][f[2]] = (int(f[3]), None if f[4] == "-" else int(f[4]))
-            else:
-                key, ifn, nbr, metric, op, labels, w = f[2:]
-                out[me].setdefault((kind, key), set()).add(
-                    (ifn, nbr, int(metric), ops[op],
-                     tuple(int(x) for x in labels.split(",") if x), int(w)))
-        return out
+        return _parse_route_text(t, mes, with_area=False)
 
     def route_db_bin_raw(self, mes: Sequence[str], prefix_lines: Sequence[str], flags: int) -> bytes:
         """odl_route_db_bin as raw bytes (prefix_lines in the text ABI's

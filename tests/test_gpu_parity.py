@@ -141,7 +141,11 @@ def test_ksp2_decremental_equals_full_reruns(seed, unit, monkeypatch):
                 reruns = int(np.count_nonzero(stt & N.OSPF_KSP_RERUN))
                 took = s1["decremental"] - s0["decremental"]
                 sent = s1["full_reruns"] - s0["full_reruns"]
-                assert took + sent == reruns and (reruns == 0 or took > 0), (took, sent, reruns)
+                assert took + sent == reruns, (took, sent, reruns)
+                # unit metric: ECMP DAGs, small affected sets; weighted SPF
+                # DAGs are near-trees, where a cut link takes its subtree
+                # (those runs may all take the full reruns)
+                assert not unit or reruns == 0 or took > 0, (took, sent, reruns)
         finally:
             eng.close()
 

@@ -1,0 +1,139 @@
+"""Several areas and minNexthop in odl::SpfSolver (VERDICT r04 missing #3):
+createRouteForPrefix's per-area loop (openr/decision/SpfSolver.cpp:229-250,
+360-442), the node-label loop over every area (:490-598), adjacency labels
+of every area (:603-631) and addBestPaths' minNexthop threshold (:976-1000,
+getMinNextHopThreshold :694-710). Expectations transcribed from the
+reference's DecisionTestFixture.MultiAreaBestPathCalculation
+(openr/decision/tests/DecisionTest.cpp:5702-5836) and the minNexthop part of
+ParallelAdjRingTopologyFixture.Ksp2EdEcmp (:3899-3951). GPU-free
+(odl_set_host_spf); the route build is host code either way."""
+import sys
+import os
+
+import pytest
+
+from openr_amd.adjdb import AdjDb, AdjDbStream, create_adjacency
+from openr_amd.linkstate import LinkState, route_dbs_multi
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+
+A, B = "test_area_name", "B"  # kTestingAreaName (openr/common/Util.h:45)
+ADDR = {1: "::ffff:10.1.1.1/128", 2: "::ffff:10.2.2.2/128", 3: "::ffff:10.3.3.3/128",
+        4: "::ffff:10.4.4.4/128"}
+
+
+def _adj(other, ifn, oif, metric, label):
+    return create_adjacency(other, ifn, oif, metric, label=label)
+
+
+# DecisionTest.cpp:47-103 (createAdjacency(node, if, remoteIf, v6, v4, metric 10, label))
+adj12 = _adj("2", "1/2", "2/1", 10, 100002)
+adj13 = _adj("3", "1/3", "3/1", 10, 100003)
+adj21 = _adj("1", "2/1", "1/2", 10, 100001)
+adj24 = _adj("4", "2/4", "4/2", 10, 100004)
+adj31 = _adj("1", "3/1", "1/3", 10, 100001)
+adj34 = _adj("4", "3/4", "4/3", 10, 100004)
+adj42 = _adj("2", "4/2", "2/4", 10, 100002)
+adj43 = _adj("3", "4/3", "3/4", 10, 100003)
+
+
+def ls(area, dbs):
+    p = LinkState(area=area)
+    p.set_host_spf(True)
+    p.apply(AdjDbStream.from_dbs(dbs))
+    return p
+
+
+def U(routes, me, prefix):
+    return routes[me].get(("U", prefix))
+
+
+def test_multi_area_best_path_calculation():
+    # area A: 1-2-4 (createAdjValue(node, 1, adjs, false, label = node))
+    la = ls(A, [AdjDb("1", [adj12], 1), AdjDb("2", [adj21, adj24], 2), AdjDb("4", [adj42], 4)])
+    # area B: 1-3-4
+    lb = ls(B, [AdjDb("1", [adj13], 1), AdjDb("3", [adj31, adj34], 3), AdjDb("4", [adj43], 4)])
+    pfx = {ADDR[1]: [("1", "ip", "ecmp", 0, None, A)], ADDR[2]: [("2", "ip", "ecmp", 0, None, A)],
+           ADDR[3]: [("3", "ip", "ecmp", 0, None, B)], ADDR[4]: [("4", "ip", "ecmp", 0, None, B)]}
+    r = route_dbs_multi([la, lb], ["1", "2", "3", "4"], pfx)
+    # (ifName, neighbor, metric, op, labels, weight, area)
+    assert set(r["1"]["routes"]) == {ADDR[2], ADDR[3], ADDR[4]}
+    assert U(r, "1", ADDR[2]) == {("1/2", "2", 10, "", (), 0, A)}
+    assert U(r, "1", ADDR[3]) == {("1/3", "3", 10, "", (), 0, B)}
+    assert U(r, "1", ADDR[4]) == {("1/3", "3", 20, "", (), 0, B)}  # only in area B
+    assert set(r["2"]["routes"]) == {ADDR[1]}                     # 2 sees area A only
+    assert U(r, "2", ADDR[1]) == {("2/1", "1", 10, "", (), 0, A)}
+    assert set(r["3"]["routes"]) == {ADDR[4]}
+    assert U(r, "3", ADDR[4]) == {("3/4", "4", 10, "", (), 0, B)}
+    assert set(r["4"]["routes"]) == {ADDR[1], ADDR[2], ADDR[3]}
+    assert U(r, "4", ADDR[2]) == {("4/2", "2", 10, "", (), 0, A)}
+    assert U(r, "4", ADDR[3]) == {("4/3", "3", 10, "", (), 0, B)}
+    assert U(r, "4", ADDR[1]) == {("4/2", "2", 20, "", (), 0, A)}
+    # "1" originates addr1 into B too: 3 reaches it in B, 4 through both
+    # areas at the same metric (next hops of both areas merged)
+    pfx[ADDR[1]].append(("1", "ip", "ecmp", 0, None, B))
+    r = route_dbs_multi([la, lb], ["3", "4"], pfx)
+    assert U(r, "3", ADDR[1]) == {("3/1", "1", 10, "", (), 0, B)}
+    assert U(r, "4", ADDR[1]) == {("4/3", "3", 20, "", (), 0, B), ("4/2", "2", 20, "", (), 0, A)}
+    # node labels of both areas' databases: 1's routes to labels 2, 3, 4 and
+    # its own POP; adjacency labels of both areas' links
+    r = route_dbs_multi([la, lb], ["1"], pfx)
+    assert r["1"][("M", "2")] == {("1/2", "2", 10, "PHP", (), 0, A)}
+    assert r["1"][("M", "3")] == {("1/3", "3", 10, "PHP", (), 0, B)}
+    # node 4 and node 1 are in both areas: the later area by name ("B" <
+    # "test_area_name") gives the route
+    assert r["1"][("M", "4")] == {("1/2", "2", 20, "SWAP", (4,), 0, A)}
+    assert r["1"][("M", "1")] == {("", "", 0, "POP", (), 0, A)}
+    assert r["1"][("M", "100002")] == {("1/2", "2", 10, "PHP", (), 0, A)}
+    assert r["1"][("M", "100003")] == {("1/3", "3", 10, "PHP", (), 0, B)}
+    # a node in no area: the reference's nullopt
+    assert route_dbs_multi([la, lb], ["9"], pfx)["9"] is None
+
+
+def test_multi_area_shorter_area_wins_and_ucmp_weights_sum():
+    """Only the areas at the shortest IGP metric contribute (:392-407)."""
+    la = ls(A, [AdjDb("1", [adj12], 1), AdjDb("2", [adj21, adj24], 2), AdjDb("4", [adj42], 4)])
+    lb = ls(B, [AdjDb("1", [create_adjacency("3", "1/3", "3/1", 3)], 1),
+                AdjDb("3", [create_adjacency("1", "3/1", "1/3", 3),
+                            create_adjacency("4", "3/4", "4/3", 3)], 3),
+                AdjDb("4", [create_adjacency("3", "4/3", "3/4", 3)], 4)])
+    pfx = {ADDR[4]: [("4", "ip", "ecmp", 0, None, A), ("4", "ip", "ecmp", 0, None, B)]}
+    r = route_dbs_multi([la, lb], ["1"], pfx)
+    assert U(r, "1", ADDR[4]) == {("1/3", "3", 6, "", (), 0, B)}
+    assert r["1"]["routes"][ADDR[4]] == (6, None)
+
+
+def test_min_nexthop_threshold():
+    """ParallelAdjRingTopologyFixture (DecisionTest.cpp:3899-3951): node 4
+    announces an SR_MPLS KSP2_ED_ECMP prefix with minNexthop 4 -> no route at
+    1 (two edge-disjoint next hops); with 2 -> adj12_2 and adj13_1 with label
+    4; node 3 announcing it too with minNexthop 4 -> the threshold is the
+    largest, 4, and the route goes again."""
+    from make_golden import pring
+    dbs = [AdjDb(d["name"], [create_adjacency(a["other"], a["if_name"], a["other_if"],
+                                              a["metric"], label=a["label"],
+                                              overloaded=a["overloaded"]) for a in d["adjs"]],
+                 d["node_label"]) for d in pring()]
+    p = ls("0", dbs)
+    bgp = "2401:db00::1/128"
+
+    def route(entries):
+        return p.route_dbs(["1"], {bgp: entries}, binary=False)["1"].get(("U", bgp))
+
+    assert route([("4", "sr_mpls", "ksp2", 0, None, None, 4)]) is None
+    want = {("2/2", "2", 22, "PUSH", (4,), 0), ("3/1", "3", 22, "PUSH", (4,), 0)}
+    assert route([("4", "sr_mpls", "ksp2", 0, None, None, 2)]) == want
+    assert route([("4", "sr_mpls", "ksp2", 0, None, None, 2),
+                  ("3", "sr_mpls", "ksp2", 0, None, None, 4)]) is None
+    assert route([("4", "sr_mpls", "ksp2", 0, None, None, 2),
+                  ("3", "sr_mpls", "ksp2", 0, None, None, 3)]) is not None
+    # the binary route-DB ABI applies the same threshold
+    assert bgp not in p.route_dbs(["1"], {bgp: [("4", "sr_mpls", "ksp2", 0, None, None, 4)]})["1"]["routes"]
+
+
+def test_unknown_area_entry_raises():
+    la = ls(A, [AdjDb("1", [adj12], 1), AdjDb("2", [adj21], 2)])
+    lb = ls(B, [AdjDb("1", [adj13], 1), AdjDb("3", [adj31], 3)])
+    from openr_amd.linkstate import LinkStateError
+    with pytest.raises(LinkStateError):
+        route_dbs_multi([la, lb], ["1"], {ADDR[2]: [("2", "ip", "ecmp", 0, None, "C")]})
