@@ -104,6 +104,9 @@ void odl_incremental_stats(const odl_ls* ls, uint64_t* out3);
  * them}: a [LINK UP] / [LINK DOWN] between known nodes (LinkState.cpp:632-657)
  * takes no snapshot and no load. */
 void odl_topology_stats(const odl_ls* ls, uint64_t* out4);
+/* nodes added or removed in place (their rows inserted / erased and the ids
+ * above them renumbered, no whole snapshot; the device graph reloads) */
+uint64_t odl_node_patches(const odl_ls* ls);
 uint32_t odl_num_nodes(const odl_ls* ls);
 uint32_t odl_num_links(const odl_ls* ls);
 

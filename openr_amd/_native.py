@@ -50,7 +50,7 @@ DECISION_SYMBOLS = [
     "odl_kth_paths_text", "odl_links_text", "odl_link_keys_text", "odl_metric_a_to_b", "odl_is_overloaded",
     "odl_spf_runs", "odl_set_incremental", "odl_set_host_spf", "odl_incremental_stats", "odl_topology_stats", "odl_num_nodes", "odl_num_links", "odl_spf_digests", "odl_spf_prefetch",
     "odl_ksp2_text", "odl_route_text", "odl_route_db_text", "odl_route_db_bin", "odl_free_buf", "odl_path_a_in_b", "odl_ucmp_text", "odl_csr_size", "odl_csr_export", "odl_node_name", "odl_node_id",
-    "odl_apply_kvs", "odl_apply_publication", "odl_route_db_multi_text", "odl_adjdbs_decode", "odl_adjdbs_stream", "odl_adjdbs_error", "odl_adjdbs_free",
+    "odl_apply_kvs", "odl_apply_publication", "odl_node_patches", "odl_route_db_multi_text", "odl_adjdbs_decode", "odl_adjdbs_stream", "odl_adjdbs_error", "odl_adjdbs_free",
 ]
 
 
@@ -262,6 +262,8 @@ def decision() -> C.CDLL:
         L.odl_set_incremental.restype = None
         L.odl_route_db_multi_text.argtypes = [vp, u32, cp, u32, cp, u32, i32]
         L.odl_route_db_multi_text.restype = C.POINTER(C.c_char)
+        L.odl_node_patches.argtypes = [vp]
+        L.odl_node_patches.restype = u64
         L.odl_apply_kvs.argtypes = [vp, u32, vp, vp, vp, u32, vp, cp, vp]
         L.odl_apply_kvs.restype = i32
         L.odl_apply_publication.argtypes = [vp, vp, u64, cp, vp, u32, vp]

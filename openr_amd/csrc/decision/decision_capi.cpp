@@ -300,6 +300,7 @@ void odl_topology_stats(const odl_ls* h, uint64_t* out4) {
   out4[2] = st.link_patches;
   out4[3] = st.rows_patched;
 }
+uint64_t odl_node_patches(const odl_ls* h) { return h ? h->ls.topologyStats().node_patches : 0; }
 uint32_t odl_num_nodes(const odl_ls* h) { return h ? (uint32_t)h->ls.numNodes() : 0; }
 uint32_t odl_num_links(const odl_ls* h) { return h ? (uint32_t)h->ls.numLinks() : 0; }
 

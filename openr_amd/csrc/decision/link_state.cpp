@@ -394,8 +394,20 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db) 
     if (!deltas.empty() || !nodeDeltas.empty()) patchGraph(deltas, nodeDeltas);
     return ch;
   }
-  // a link or node added / removed (node ids may move), or a metric leaving
-  // the engine contract: the CSR is snapshotted again
+  // a node added while the snapshot is current: its (empty) row enters in
+  // place, then the links it formed (peers that already advertised it)
+  // patch their rows; the device graph reloads on its next use
+  if (!known && snapVersion_ == version_ && keepsContract && !getenv("ODL_NO_LINK_PATCH")) {
+    if (ch.topologyChanged) clearMemo();
+    engineVersion_ = 0;
+    const auto& nm = csr_->names;
+    const uint32_t k = (uint32_t)(std::lower_bound(nm.begin(), nm.end(), me) - nm.begin());
+    csrInsertNode(k, me, db.isOverloaded);
+    patchStructure(ch.addedLinks, {});
+    return ch;
+  }
+  // a metric leaving the engine contract, or a change without a current
+  // snapshot: the CSR is snapshotted again
   if (ch.topologyChanged) {
     invalidate();
   } else {
@@ -541,19 +553,35 @@ LinkStateChange LinkState::deleteAdjacencyDatabase(const std::string& node) {
   LinkStateChange ch;
   auto db = adjDbs_.find(node);
   if (db == adjDbs_.end()) return ch;
+  // in place when the snapshot is current: the node's links leave their
+  // rows (patchStructure), then its empty row leaves (ids above it move)
+  const bool inPlace = snapVersion_ == version_ && !hostMetric_ && csr_->ids.count(node) &&
+                       !getenv("ODL_NO_LINK_PATCH");
+  std::vector<LinkPtr> removed;
   auto lm = linkMap_.find(node);
   if (lm != linkMap_.end()) {
     for (const auto& l : lm->second) {
       if (!linkMap_.at(l->otherNode(node)).erase(l) || !shardOf(*l).erase(l))
         throw std::logic_error("inconsistent link map");
+      removed.push_back(l);
     }
     linkMap_.erase(lm);
     nodeOverloads_.erase(node);
   }
   adjDbs_.erase(db);
   adjIndex_.erase(node);
-  invalidate();
   ch.topologyChanged = true;
+  if (!inPlace) {
+    invalidate();
+    return ch;
+  }
+  clearMemo();  // LinkState.cpp:751-754
+  engineVersion_ = 0;  // the node count changes: the device graph reloads
+  const uint32_t k = csr_->ids.at(node);
+  patchStructure({}, removed);
+  csrEraseNode(k);
+  ++version_;
+  snapVersion_ = version_;
   return ch;
 }
 
@@ -1445,13 +1473,7 @@ void LinkState::patchGraph(const std::vector<LinkDelta>& links,
 void LinkState::patchStructure(const std::vector<LinkPtr>& added,
                                const std::vector<LinkPtr>& removed) {
   dropSweep();  // its rows describe the graph before the patch
-  // a kept memoised result reads this snapshot's ranks lazily: give it its own
-  // (results handed to the reaper are no readers; only the live memo is)
-  bool kept = false;
-  for (const auto* m : {&memoMetric_, &memoHops_})
-    for (const auto& kv : *m) kept |= kv.second.rows() && kv.second.rows()->csr == csr_;
-  if (kept) csr_ = std::make_shared<Csr>(*csr_);
-  Csr& c = *csr_;
+  Csr& c = csrForWrite();
   const uint32_t V = (uint32_t)c.names.size();
   std::vector<uint32_t> rows;
   for (const auto* set : {&added, &removed})
@@ -1586,6 +1608,52 @@ void LinkState::patchStructure(const std::vector<LinkPtr>& added,
   ++version_;
   snapVersion_ = version_;
   if (inSync) patchEngineRows(rows);
+}
+
+LinkState::Csr& LinkState::csrForWrite() {
+  // a kept memoised result reads this snapshot's ranks lazily: give it its own
+  // (results handed to the reaper are no readers; only the live memo is)
+  bool kept = false;
+  for (const auto* m : {&memoMetric_, &memoHops_})
+    for (const auto& kv : *m) kept |= kv.second.rows() && kv.second.rows()->csr == csr_;
+  if (kept) csr_ = std::make_shared<Csr>(*csr_);
+  return *csr_;
+}
+
+void LinkState::csrInsertNode(uint32_t k, const std::string& name, bool overloaded) {
+  Csr& c = csrForWrite();
+  const uint32_t V = (uint32_t)c.names.size();
+  if (k > V) throw std::logic_error("csrInsertNode: position");
+  c.names.insert(c.names.begin() + k, name);
+  for (auto& kv : c.ids)
+    if (kv.second >= k) ++kv.second;
+  c.ids.emplace(name, k);
+  c.rowPtr.insert(c.rowPtr.begin() + k + 1, c.rowPtr[k]);  // an empty row k
+  parallelFor((uint32_t)c.col.size(), [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t e = lo; e < hi; ++e)
+      if (c.col[e] >= k && c.col[e] != kInf) ++c.col[e];
+  }, 1u << 16);
+  c.noTransit.insert(c.noTransit.begin() + k, overloaded ? 1 : 0);
+  c.rowMax.insert(c.rowMax.begin() + k, 0);
+  ++topoStats_.node_patches;
+}
+
+void LinkState::csrEraseNode(uint32_t k) {
+  Csr& c = csrForWrite();
+  if (k >= c.names.size() || c.rowPtr[k] != c.rowPtr[k + 1])
+    throw std::logic_error("csrEraseNode: row not empty");
+  c.ids.erase(c.names[k]);
+  for (auto& kv : c.ids)
+    if (kv.second > k) --kv.second;
+  c.names.erase(c.names.begin() + k);
+  c.rowPtr.erase(c.rowPtr.begin() + k + 1);
+  parallelFor((uint32_t)c.col.size(), [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t e = lo; e < hi; ++e)
+      if (c.col[e] > k && c.col[e] != kInf) --c.col[e];
+  }, 1u << 16);
+  c.noTransit.erase(c.noTransit.begin() + k);
+  c.rowMax.erase(c.rowMax.begin() + k);
+  ++topoStats_.node_patches;
 }
 
 void LinkState::patchEngineRows(const std::vector<uint32_t>& rows) {

@@ -472,6 +472,7 @@ class LinkState {
     uint64_t loads = 0;         // whole device graph loads
     uint64_t link_patches = 0;  // updates patched in place with links added / removed
     uint64_t rows_patched = 0;  // CSR rows rebuilt by them
+    uint64_t node_patches = 0;  // nodes added / removed in place (ids renumbered)
   };
   const TopologyStats& topologyStats() const { return topoStats_; }
 
@@ -520,6 +521,12 @@ class LinkState {
   void patchGraph(const std::vector<LinkDelta>& links, const std::vector<std::string>& nodes);
   // links of the rows in `rows` to the engine (ospf_update_rows), or a reload
   void patchEngineRows(const std::vector<uint32_t>& rows);
+  // a node enters / leaves the snapshot in place (node id = name rank: ids
+  // from k on move by one); its row is empty (links: patchStructure). The
+  // device graph reloads on its next use (the node count changed).
+  void csrInsertNode(uint32_t k, const std::string& name, bool overloaded);
+  void csrEraseNode(uint32_t k);
+  Csr& csrForWrite();  // copy-on-write when a kept memoised result reads it
 
   std::string area_;
   int device_;

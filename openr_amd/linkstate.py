@@ -386,6 +386,11 @@ class LinkState:
         self._L.odl_incremental_stats(self._h, out)
         return {"patches": int(out[0]), "kept": int(out[1]), "dropped": int(out[2])}
 
+    @property
+    def node_patches(self) -> int:
+        """nodes added / removed in place (odl_node_patches)"""
+        return int(self._L.odl_node_patches(self._h))
+
     def topology_stats(self) -> Dict[str, int]:
         """{snapshots, loads, link_patches, rows_patched}: links added /
         removed between known nodes patch the CSR and the device graph in

@@ -165,3 +165,62 @@ def parallel_link_ranks_after_insert(host=False):
         for d in names[1:4]:
             assert p.kth_paths("n5", d, 2) == o.kth_paths("n5", d, 2), (step, d)
     assert p.topology_stats()["snapshots"] == s0["snapshots"]
+
+
+def node_remove_add_random_graphs(seed, unit, host=False, n=40):
+    """A node's database withdrawn (deleteAdjacencyDatabase: its links leave
+    its peers' rows, its row leaves, ids above it move down), then restored
+    (its links form again with peers that still advertise it); a brand-new
+    node joining with links to known nodes; all in place on the host
+    snapshot (LinkState.cpp:584-600 new node, :730-756 delete)."""
+    from openr_amd.adjdb import AdjDb
+    st, names = random_stream(1300 + seed, n=n, p=0.15, unit=unit)
+    o, p = both(st, host)
+    rng = np.random.default_rng(seed)
+    dbs = {d.name: d for d in st.to_dbs()}
+    check(o, p, names, rng)
+    s0 = p.topology_stats()
+    np0 = p.node_patches
+    events = 0
+    live = list(names)
+    for step in range(6):
+        a = live[int(rng.integers(len(live)))]
+        apply_both(o, p, [AdjDb(a, delete=True)])  # the node leaves
+        live.remove(a)
+        events += 1
+        check(o, p, live, rng)
+        assert p.spf_runs == o.spf_runs, ("delete", step)
+        if step % 2 == 0:  # KSP2 without it
+            s_, d_ = live[int(rng.integers(len(live)))], live[int(rng.integers(len(live)))]
+            for kk in (1, 2):
+                assert p.kth_paths(s_, d_, kk) == o.kth_paths(s_, d_, kk)
+        apply_both(o, p, [dbs[a]])  # and comes back
+        live.append(a)
+        events += 1
+        check(o, p, live, rng)
+        assert p.spf_runs == o.spf_runs, ("restore", step)
+    # new nodes whose peers advertise them first (links form at once), with
+    # names sorting before, between and after the others
+    for step, nm in enumerate(["a-new", "r5-new", "zz-new"]):
+        peers = rng.choice(live, 3, replace=False).tolist()
+        mine = []
+        for q in peers:
+            m1 = 1 if unit else int(rng.integers(1, 20))
+            m2 = 1 if unit else int(rng.integers(1, 20))
+            dbs[q].adjs.append(create_adjacency(nm, f"{q}-{nm}", f"{nm}-{q}", m1))
+            mine.append(create_adjacency(q, f"{nm}-{q}", f"{q}-{nm}", m2))
+        apply_both(o, p, [dbs[q] for q in peers])
+        dbs[nm] = AdjDb(nm, mine, 1000 + step)
+        apply_both(o, p, [dbs[nm]])
+        live.append(nm)
+        events += 1
+        check(o, p, live, rng)
+        assert p.spf_runs == o.spf_runs, ("new node", step)
+    s1 = p.topology_stats()
+    assert s1["snapshots"] == s0["snapshots"], (s0, s1)  # no whole snapshot
+    assert p.node_patches - np0 == events
+    ids = p.node_names()
+    assert sorted(ids) == ids and set(ids) == set(live)
+    assert np.array_equal(p.all_sources_digests(), o.fast_digests(ids, True, threads=8))
+    check(o, p, live, rng, all_digests=True)
+    return s0, s1

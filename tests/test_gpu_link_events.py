@@ -113,3 +113,13 @@ def test_f10k_link_down_up_sweep_in_place():
             assert p.spf_text(r) == o.spf_text(r), r
     s1 = p.topology_stats()
     assert s1["snapshots"] == s0["snapshots"] and s1["loads"] == s0["loads"], (s0, s1)
+
+
+@pytest.mark.parametrize("seed", range(2))
+@pytest.mark.parametrize("unit", [False, True])
+def test_node_remove_add_in_place(seed, unit):
+    """Nodes withdrawn, restored and added in place on the host snapshot; the
+    engine reloads the renumbered graph (one device load per event), results
+    == the oracle after every event."""
+    s0, s1 = LE.node_remove_add_random_graphs(seed, unit)
+    assert s1["loads"] > s0["loads"]

@@ -40,3 +40,9 @@ def test_host_spf_switch_never_opens_the_engine():
     p.ksp2_text(names[0], names[1:6])
     assert p.topology_stats()["loads"] == 0
     assert p.sweep_stats()["sweeps"] == 0
+
+
+@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("unit", [False, True])
+def test_node_remove_add_in_place_host(seed, unit):
+    LE.node_remove_add_random_graphs(seed, unit, host=True)
