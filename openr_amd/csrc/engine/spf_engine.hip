@@ -1195,6 +1195,9 @@ int ospf_close(ospf_ctx* c) {
     if (e) hipEventDestroy(e);
   if (c->d_cover) hipFree(c->d_cover);
   if (c->lv_aux) hipStreamDestroy(c->lv_aux);
+  for (auto& kv : c->sweep_pool) hipFree(kv.second);
+  for (hipStream_t st : c->stream_pool) hipStreamDestroy(st);
+  for (hipEvent_t e : c->event_pool) hipEventDestroy(e);
   delete c;
   return OSPF_OK;
 }

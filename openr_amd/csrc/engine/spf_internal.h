@@ -19,6 +19,13 @@ struct ospf_ctx {
   std::string err;
   uint64_t spf_runs = 0;
   uint64_t ksp_decr_stats[3] = {0, 0, 0};  // ospf_ksp2_stats
+  // device blocks, streams and events of destroyed sweeps, taken again by the
+  // next sweep (a graph patch drops the sweep; its successor reuses ~100 GB
+  // of F100k rows instead of hipFree + hipMalloc, and its streams' scratch)
+  std::multimap<size_t, void*> sweep_pool;
+  size_t sweep_pool_bytes = 0;
+  std::vector<hipStream_t> stream_pool;
+  std::vector<hipEvent_t> event_pool;
   // graph
   bool loaded = false;
   ospf_graph_info info{};

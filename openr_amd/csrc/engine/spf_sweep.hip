@@ -158,6 +158,7 @@ struct ospf_sweep {
   std::vector<const uint32_t*> row_dist, row_nh;
   std::vector<uint32_t> row_w;
   std::vector<void*> allocs;            // device allocations
+  std::vector<size_t> alloc_bytes;      // their sizes (returned to the ctx's pool)
   uint64_t device_bytes = 0;
   ospf_digest* dig_all = nullptr;       // every digest a run writes
   uint32_t n_dig = 0;
@@ -204,12 +205,31 @@ int sfail(ospf_sweep* s, int code, const std::string& m) {
 template <class T>
 int dalloc(ospf_sweep* s, T** p, size_t count) {
   void* q = nullptr;
-  const size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
-  hipError_t e = hipMalloc(&q, bytes);
-  if (e != hipSuccess)
-    return sfail(s, OSPF_E_NOMEM, "sweep: hipMalloc " + std::to_string(bytes) + " B: " +
-                                      hipGetErrorString(e));
+  const size_t want = std::max<size_t>(count, 1) * sizeof(T);
+  // a block of a destroyed sweep, at most 1/8 larger (+ 1 MB), else new
+  ospf_ctx* c = s->c;
+  size_t bytes = (want + 255) & ~(size_t)255;
+  auto it = c->sweep_pool.lower_bound(bytes);
+  if (it != c->sweep_pool.end() && it->first <= bytes + bytes / 8 + (1u << 20)) {
+    q = it->second;
+    bytes = it->first;
+    c->sweep_pool_bytes -= bytes;
+    c->sweep_pool.erase(it);
+  } else {
+    hipError_t e = hipMalloc(&q, bytes);
+    if (e != hipSuccess && !c->sweep_pool.empty()) {  // the pool's blocks back to the device
+      (void)hipGetLastError();
+      for (auto& kv : c->sweep_pool) (void)hipFree(kv.second);
+      c->sweep_pool.clear();
+      c->sweep_pool_bytes = 0;
+      e = hipMalloc(&q, bytes);
+    }
+    if (e != hipSuccess)
+      return sfail(s, OSPF_E_NOMEM, "sweep: hipMalloc " + std::to_string(bytes) + " B: " +
+                                        hipGetErrorString(e));
+  }
   s->allocs.push_back(q);
+  s->alloc_bytes.push_back(bytes);
   s->device_bytes += bytes;
   *p = (T*)q;
   return OSPF_OK;
@@ -225,14 +245,24 @@ int upload(ospf_sweep* s, T** p, const std::vector<T>& h) {
 
 int new_stream(ospf_sweep* s) {
   hipStream_t st;
-  SCHK(s, hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  if (!s->c->stream_pool.empty()) {
+    st = s->c->stream_pool.back();
+    s->c->stream_pool.pop_back();
+  } else {
+    SCHK(s, hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  }
   s->streams.push_back(st);
   return (int)s->streams.size() - 1;
 }
 
 int new_event(ospf_sweep* s) {
   hipEvent_t e;
-  SCHK(s, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (!s->c->event_pool.empty()) {
+    e = s->c->event_pool.back();
+    s->c->event_pool.pop_back();
+  } else {
+    SCHK(s, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
   s->events.push_back(e);
   return (int)s->events.size() - 1;
 }
@@ -2066,6 +2096,7 @@ int plan_wmulti(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     blocks = std::max(1u, blocks / 2);
   }
   s->allocs.push_back(scratch);
+  s->alloc_bytes.push_back(per * blocks);
   s->device_bytes += per * blocks;
   std::vector<uint32_t> wset;
   for (uint32_t r : own_c) wset.push_back(f.words(r));
@@ -2323,18 +2354,33 @@ void release(ospf_sweep* s) {
     if (st) hipStreamSynchronize(st);
   if (s->exec) hipGraphExecDestroy(s->exec);
   if (s->graph) hipGraphDestroy(s->graph);
-  for (void* p : s->allocs) hipFree(p);
-  for (hipEvent_t e : s->events) hipEventDestroy(e);
+  // blocks, streams (with their scratch) and events go to the ctx's pools
+  // for the next sweep (ospf_close frees them)
+  constexpr size_t kPoolCap = 160ull << 30;
+  for (size_t i = 0; i < s->allocs.size(); ++i) {
+    if (s->c && i < s->alloc_bytes.size() && s->c->sweep_pool_bytes + s->alloc_bytes[i] <= kPoolCap) {
+      s->c->sweep_pool.emplace(s->alloc_bytes[i], s->allocs[i]);
+      s->c->sweep_pool_bytes += s->alloc_bytes[i];
+    } else {
+      hipFree(s->allocs[i]);
+    }
+  }
+  for (hipEvent_t e : s->events)
+    if (e) (s->c ? (void)s->c->event_pool.push_back(e) : (void)hipEventDestroy(e));
   for (hipEvent_t e : s->ev_done)
     if (e) hipEventDestroy(e);
   if (s->ev_in) hipEventDestroy(s->ev_in);
   if (s->ev_out) hipEventDestroy(s->ev_out);
   for (hipStream_t st : s->streams) {
     if (!st) continue;
-    if (s->c) release_stream_scratch(s->c, st);
-    hipStreamDestroy(st);
+    if (s->c) {
+      s->c->stream_pool.push_back(st);
+    } else {
+      hipStreamDestroy(st);
+    }
   }
   s->allocs.clear();
+  s->alloc_bytes.clear();
   s->streams.clear();
 }
 
@@ -2375,6 +2421,15 @@ int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
     delete s;
     c->err = m;
     return rc;
+  };
+  const bool tm = getenv("OSPF_SWEEP_TIMING") != nullptr;
+  auto t0 = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (!tm) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "sweep_create %s %.2f ms\n", what,
+            std::chrono::duration<double, std::milli>(t - t0).count());
+    t0 = t;
   };
   if (hipSetDevice(c->device) != hipSuccess) return bail(fail(c, OSPF_E_DEVICE, "hipSetDevice"));
   if (new_stream(s) < 0 || new_event(s) < 0) return bail(OSPF_E_DEVICE);
@@ -2427,6 +2482,7 @@ int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
     if (rc) return bail(rc);
   }
   s->mode = mode;
+  lap("partition + leaf set + cover prepare");
   int rc = OSPF_OK;
   switch (mode) {
     case OSPF_SWEEP_DERIVE: rc = plan_derive(s, f, mine); break;
@@ -2437,11 +2493,13 @@ int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
     default: rc = plan_batch(s, f, mine, !unit); break;
   }
   if (rc) return bail(rc);
+  lap("plan");
   if (upload(s, &s->d_own_slot, s->own_slot)) return bail(OSPF_E_NOMEM);
   s->ev_done.assign(s->streams.size(), nullptr);
   for (size_t i = 1; i < s->streams.size(); ++i)
     if (hipEventCreateWithFlags(&s->ev_done[i], hipEventDisableTiming) != hipSuccess)
       return bail(fail(c, OSPF_E_DEVICE, "hipEventCreate"));
+  lap("slots + events");
   if (defer) {  // the caller's first ospf_sweep_run is the first run
     *out = s;
     return OSPF_OK;

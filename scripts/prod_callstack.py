@@ -117,9 +117,18 @@ def main():
         _, wall, _ = timed(lambda: p.apply(ev))
         out[f"{tag}_event_apply_ms"] = round(wall, 3)
         stack(p, args.me, f"{tag}_after_event")
-        # [LINK DOWN] / [LINK UP] (LinkState.cpp:632-657): the rack withdraws
+        # the metric back to 1: the graph is unit-metric again (one metric-3
+        # link makes the whole graph weighted -- the weighted sweep path --
+        # which r04's link events measured by accident)
+        db.adjs[0].metric = 1
+        _, wall, _ = timed(lambda: p.apply(AdjDbStream.from_dbs([db])))
+        out[f"{tag}_metric_revert_apply_ms"] = round(wall, 3)
+        # [LINK DOWN] / [LINK UP] (LinkState.cpp:632-657): a rack withdraws
         # its adjacency to its pod's first fabric switch, then restores it;
         # each: apply, getSpfResult(me), and a whole all-sources re-sweep
+        db = [d for d in st.to_dbs() if d.name == "3-901-0"][0]
+        _, wall, _ = timed(lambda: p.prefetch_all())
+        out[f"{tag}_all_sources_sweep_before_link_events_ms"] = round(wall, 3)
         t0 = p.topology_stats()
         adj = db.adjs.pop(0)
         for kind in ("link_down", "link_up"):
@@ -138,6 +147,23 @@ def main():
                   f"{out[f'{tag}_{kind}_all_sources_sweep_ms']} ms", file=sys.stderr, flush=True)
         t1 = p.topology_stats()
         out[f"{tag}_link_events_topology_stats"] = {k: t1[k] - t0[k] for k in t1}
+        # a steady re-sweep of the same graph version (the sweep is resident)
+        # and [NODE DOWN] / [NODE UP]: a rack's database deleted and restored
+        # (in place on the host snapshot; the device graph reloads)
+        from openr_amd.adjdb import AdjDb
+        rack = [d for d in st.to_dbs() if d.name == "3-902-7"][0]
+        for kind, ev in (("node_down", AdjDbStream.from_dbs([AdjDb(rack.name, delete=True)])),
+                         ("node_up", AdjDbStream.from_dbs([rack]))):
+            _, wall, _ = timed(lambda: p.apply(ev))
+            out[f"{tag}_{kind}_apply_ms"] = round(wall, 3)
+            _, wall, cap = timed(lambda: p.prefetch([args.me]))
+            out[f"{tag}_{kind}_getSpfResult_ms"] = round(wall, 3)
+            _, wall, _ = timed(lambda: p.prefetch_all())
+            out[f"{tag}_{kind}_all_sources_sweep_ms"] = round(wall, 3)
+            print(f"{tag} {kind}: apply {out[f'{tag}_{kind}_apply_ms']} ms, getSpfResult "
+                  f"{out[f'{tag}_{kind}_getSpfResult_ms']} ms, sweep "
+                  f"{out[f'{tag}_{kind}_all_sources_sweep_ms']} ms", file=sys.stderr, flush=True)
+        out[f"{tag}_node_patches"] = p.node_patches
         del p
     if not args.no_cpu:
         from oracle import Oracle  # CPU restatement, same root
