@@ -1184,6 +1184,11 @@ int ospf_open(int device, ospf_ctx** out) {
 int ospf_close(ospf_ctx* c) {
   if (!c) return OSPF_E_INVAL;
   hipSetDevice(c->device);
+  // sweeps still alive: their resources back (to the pools freed below) and
+  // detached from this context
+  for (ospf_sweep* s : std::vector<ospf_sweep*>(c->live_sweeps))
+    if (c->release_sweep) c->release_sweep(s);
+  c->live_sweeps.clear();
   if (c->d_graph) hipFree(c->d_graph);
   for (auto& kv : c->scratch)
     if (kv.second.p) hipFree(kv.second.p);
@@ -1817,6 +1822,20 @@ int ospf_nh_derive_twin_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, ui
                             const ospf_digest* d_lev_digest, const uint32_t* d_twin_class,
                             const uint32_t* d_twin_rep, const uint32_t* d_twin_second,
                             uint32_t* d_nh, ospf_digest* d_digest, void* stream) {
+  return ospf_int::nh_derive_twin_launch(c, d_roots, n, nh_words, max_root_neighbors, d_lev,
+                                         lev_pitch, d_lev_pos, d_lev_digest, d_twin_class,
+                                         d_twin_rep, d_twin_second, d_nh, d_digest, nullptr, stream);
+}
+
+}  // extern "C"
+
+namespace ospf_int {
+int nh_derive_twin_launch(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t nh_words,
+                          uint32_t max_root_neighbors, const uint8_t* d_lev, uint32_t lev_pitch,
+                          const uint32_t* d_lev_pos, const ospf_digest* d_lev_digest,
+                          const uint32_t* d_twin_class, const uint32_t* d_twin_rep,
+                          const uint32_t* d_twin_second, uint32_t* d_nh, ospf_digest* d_digest,
+                          uint32_t* d_dist, void* stream) {
   if (!c) return OSPF_E_INVAL;
   if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
   if (n == 0) return OSPF_OK;
@@ -1845,11 +1864,15 @@ int ospf_nh_derive_twin_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, ui
   a.nh = d_nh;
   a.digest = d_digest;
   a.err = c->d_err;
+  a.dist = d_dist;
   if (const char* e = getenv("OSPF_TWIN_CTILES")) a.ctiles = (uint32_t)std::max(1, atoi(e));
   hipError_t e = ospf::launch_nh_derive_twin(c->g, a, s);
   if (e != hipSuccess) return hip_fail(c, e, "launch_nh_derive_twin");
   return OSPF_OK;
 }
+}  // namespace ospf_int
+
+extern "C" {
 
 // Twin levels (spf_twin.hip): level + dist rows of roots from the
 // representative rows of their neighbours' twin classes (no traversal).

@@ -26,6 +26,11 @@ struct ospf_ctx {
   size_t sweep_pool_bytes = 0;
   std::vector<hipStream_t> stream_pool;
   std::vector<hipEvent_t> event_pool;
+  // sweeps created on this context and not yet destroyed: ospf_close
+  // releases them first (a sweep destroyed after its context -- a caller's
+  // GC order -- then frees only itself)
+  std::vector<struct ospf_sweep*> live_sweeps;
+  void (*release_sweep)(struct ospf_sweep*) = nullptr;
   // graph
   bool loaded = false;
   ospf_graph_info info{};
@@ -117,6 +122,14 @@ int twin_lv_build(ospf_ctx* c, const std::vector<uint32_t>& roots, const std::ve
                   const std::vector<uint32_t>& rep, TwinLvHost& out);
 // queue a planned twin-levels launch (device copies of the plan's arrays)
 int twin_lv_launch(ospf_ctx* c, const ospf::TwinLvPlan& p, void* stream);
+// ospf_nh_derive_twin_dev + the roots' own dist rows (d_dist at d_lev_pos;
+// null: not written)
+int nh_derive_twin_launch(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t nh_words,
+                          uint32_t max_root_neighbors, const uint8_t* d_lev, uint32_t lev_pitch,
+                          const uint32_t* d_lev_pos, const ospf_digest* d_lev_digest,
+                          const uint32_t* d_twin_class, const uint32_t* d_twin_rep,
+                          const uint32_t* d_twin_second, uint32_t* d_nh, ospf_digest* d_digest,
+                          uint32_t* d_dist, void* stream);
 
 // Host plan of the cover closure (spf_cover.hip closure_kernel) for the
 // closure roots `roots` (node ids, non-seed cover nodes; dc row i = roots[i])

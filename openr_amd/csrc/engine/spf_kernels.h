@@ -515,6 +515,10 @@ struct TwinArgs {
   ospf_digest* digest;    // [n] (zeroed by the caller) or null
   uint32_t* err;          // + bit 256: a root with more than kTwinMaxC classes
   uint32_t tiles, ctiles, chunks;
+  // the roots' own dist rows at dist + pos[root] * V from their own level
+  // bytes, beside the next-hop rows (the sweep's twin levels then write level
+  // rows only: their dist rows leave the serial prefix); null: not written
+  uint32_t* dist;
   // twin_levels_kernel: the roots' own rows at pos[root]
 };
 hipError_t launch_nh_derive_twin(const DevGraph& g, const TwinArgs& a, hipStream_t s);
@@ -632,7 +636,7 @@ struct TraceArgs {
   uint32_t* heavy;          // [n] queued run indices
   uint32_t* heavy_ctr;      // [2] {queued, taken}, zeroed by the caller
   // decremental reruns (launch_ksp_decr): rows = the source's dist row
-  const uint32_t* tc;       // [V] hint: link of each node's first support (launch_ksp_hint)
+  const uint32_t* tc;       // [V] hint: link of each node's last support (launch_ksp_hint)
   uint32_t* fb;             // [n] runs left to the full masked reruns
   uint32_t* ctr;            // [8] {next run, fallbacks, runs decided, affected nodes, heavy
                             //  queued / taken, A overflows, hash overflows}, zeroed
@@ -640,7 +644,7 @@ struct TraceArgs {
 };
 hipError_t launch_ksp_trace(bool lev, const DevGraph& g, const TraceArgs& t, hipStream_t s);
 // KSP2 k = 2 by decremental SSSP (spf_ksp2.hip): hint[v] = the link id of
-// v's first usable in-link (u, v) in row order with u transit (or the
+// v's last usable in-link (u, v) in row order with u transit (or the
 // source) and dist(u) + w(u -> v) == dist(v) in the source's dist row
 hipError_t launch_ksp_hint(const DevGraph& g, uint32_t src, const uint32_t* dist, uint32_t* hint,
                            hipStream_t s);

@@ -515,7 +515,7 @@ __global__ void __launch_bounds__(1024) ksp_heavy_kernel(DevGraph g, TraceArgs t
 // w(u -> v) == dist(v) -- survives with u unaffected. The affected set A is
 // the fixed point of lost supports: an ignored link loses its tight
 // directions, an affected node loses its tight out-links. Each node has a
-// hint, the link of its first support (ksp_hint_kernel); a lost support that
+// hint, the link of its last support (ksp_hint_kernel); a lost support that
 // is not a node's hint changes nothing while the hint stands, so a node gets
 // an LDS entry only once its hint is lost: then its surviving supports are
 // counted once (tails unaffected, or affected and not yet expanded -- those
@@ -565,7 +565,12 @@ struct DistDecr {
   }
 };
 
-// hint[v] = link id of v's first support in row order (kInf: none)
+// hint[v] = link id of v's last support in row order (kInf: none). The
+// last, not the first: a k = 1 trace takes each node's first candidate in
+// row order (traceOnePath's pathLinks order), so the first supports are the
+// ones the ignored links cut -- with them as hints every plane-0 fabric
+// switch of F100k would lose its hint to a rack's k = 1 path through spine
+// 1-0-0, with the last ones none does.
 __global__ void __launch_bounds__(256) ksp_hint_kernel(DevGraph g, uint32_t src,
                                                        const uint32_t* __restrict__ D,
                                                        uint32_t* __restrict__ hint) {
@@ -581,7 +586,6 @@ __global__ void __launch_bounds__(256) ksp_hint_kernel(DevGraph g, uint32_t src,
       if (du == kInf || (uint64_t)du + g.rw[e] != dv) continue;
       if (u != src && ((g.nt_bits[u >> 5] >> (u & 31u)) & 1u)) continue;
       h = g.link_id[e];
-      break;
     }
   }
   hint[v] = h;

@@ -938,6 +938,14 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     s->step_comp += lv.comp;
     s->units.push_back(lv);
   }
+  // the twin next-hop launches write their roots' dist rows (from the level
+  // rows they read anyway), off the serial prefix (OSPF_TWIN_DIST_IN_LEVELS:
+  // the twin levels write them, as before)
+  const bool nh_dist = twin_lv && !getenv("OSPF_TWIN_DIST_IN_LEVELS");
+  std::vector<uint8_t> twin_nh(V, 0);
+  for (const auto& k : cls)
+    if (k.twin)
+      for (uint32_t r : k.roots) twin_nh[r] = 1;
   for (uint32_t k = 0; k < S; ++k) {
     const uint32_t i0 = dgo[sg[k]], n = dgo[sg[k + 1]] - i0;
     std::vector<uint32_t> gk, rk(drv.begin() + i0, drv.begin() + i0 + n);
@@ -945,6 +953,10 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     // the stage's plan, built once on the host (spf_twin.hip twin_levels_kernel)
     ospf_int::TwinLvHost h;
     if ((rc = ospf_int::twin_lv_build(c, rk, gk, pos, tw.cls, tw.rep, h))) return sfail(s, rc, c->err);
+    // roots whose twin next-hop launch writes their dist rows: level rows only here
+    if (nh_dist)
+      for (auto& ri : h.rinfo)
+        if (twin_nh[ri.x]) ri.z |= 0x80000000u;
     ospf::TwinLvPlan plan{};
     uint32_t *d_grp2, *d_grow, *d_nbo, *d_nbl;
     uint4* d_rinfo;
@@ -970,10 +982,14 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     u.stream = 0;
     u.record = ev_s[k];
     u.n_roots = n;
-    // dist rows written (level rows are intermediate)
-    u.comp = (uint64_t)n * 4ull * V;
+    // the unit: the dist rows it writes + its level rows (read by the
+    // leaves); the step counts only the dist rows (level rows are
+    // intermediate)
+    uint64_t nd_rows = 0;
+    for (const auto& ri : h.rinfo) nd_rows += (ri.z >> 31) ? 0u : 1u;
+    u.comp = nd_rows * 4ull * V + (uint64_t)n * V;
     u.fn = [=](hipStream_t st) { return ospf_int::twin_lv_launch(c, plan, st); };
-    s->step_comp += u.comp;
+    s->step_comp += nd_rows * 4ull * V;
     s->units.push_back(u);
   }
   const int ev_cov = nd ? ev_t : ev_a;
@@ -1010,14 +1026,15 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
         u.wait = {ev_s[q]};
         u.n_roots = a1 - a0;
         u.W = W;
-        u.comp = (uint64_t)(a1 - a0) * 4ull * V * W;
+        u.comp = (uint64_t)(a1 - a0) * 4ull * V * (W + (nh_dist ? 1u : 0u));
         const uint32_t *tc = d_tcls, *tr = d_trep, *ts = d_tsec, *rr = d_roots + a0;
         const uint32_t m = a1 - a0;
         uint32_t* nhq = nh + (size_t)a0 * V * W;
         ospf_digest* dq = dg + a0;
+        uint32_t* dd = nh_dist ? dist : nullptr;
         u.fn = [=](hipStream_t strm) {
-          return ospf_nh_derive_twin_dev(c, rr, m, W, cap, lev, pitch, d_pos, ldg, tc, tr, ts, nhq,
-                                         dq, strm);
+          return ospf_int::nh_derive_twin_launch(c, rr, m, W, cap, lev, pitch, d_pos, ldg, tc, tr, ts,
+                                                 nhq, dq, dd, strm);
         };
         s->step_comp += u.comp;
         side.push_back(std::move(u));
@@ -1082,12 +1099,13 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     if (u.wait[0] == ev_b && nd) u.wait.push_back(ev_cov);
     u.n_roots = n;
     u.W = W;
-    u.comp = (uint64_t)n * 4ull * V * W;
+    u.comp = (uint64_t)n * 4ull * V * (W + (k.twin && nh_dist ? 1u : 0u));
     if (k.twin) {
       const uint32_t *tc = d_tcls, *tr = d_trep, *ts = d_tsec;
+      uint32_t* dd = nh_dist ? dist : nullptr;
       u.fn = [=](hipStream_t strm) {
-        return ospf_nh_derive_twin_dev(c, d_roots, n, W, cap, lev, pitch, d_pos, ldg, tc, tr, ts,
-                                       nh, dg, strm);
+        return ospf_int::nh_derive_twin_launch(c, d_roots, n, W, cap, lev, pitch, d_pos, ldg, tc, tr,
+                                               ts, nh, dg, dd, strm);
       };
     } else {
       u.fn = [=](hipStream_t strm) {
@@ -2379,9 +2397,16 @@ void release(ospf_sweep* s) {
       hipStreamDestroy(st);
     }
   }
+  // idempotent: a sweep released by ospf_close is released again (a no-op)
+  // by its own destroy
   s->allocs.clear();
   s->alloc_bytes.clear();
   s->streams.clear();
+  s->events.clear();
+  s->ev_done.clear();
+  s->ev_in = s->ev_out = nullptr;
+  s->exec = nullptr;
+  s->graph = nullptr;
 }
 
 }  // namespace
@@ -2408,6 +2433,11 @@ int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
   ospf_sweep* s = new (std::nothrow) ospf_sweep();
   if (!s) return OSPF_E_NOMEM;
   s->c = c;
+  c->live_sweeps.push_back(s);
+  c->release_sweep = [](ospf_sweep* x) {  // ospf_close: release now, detach
+    release(x);
+    x->c = nullptr;
+  };
   s->opts = *o;
   s->gen = c->graph_gen;
   s->V = c->info.n_nodes;
@@ -2417,6 +2447,8 @@ int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
   s->row_w.assign(V, 0);
   auto bail = [&](int rc) {
     const std::string m = s->err.empty() ? std::string(ospf_last_error(c)) : s->err;
+    auto& lsw = c->live_sweeps;
+    lsw.erase(std::remove(lsw.begin(), lsw.end(), s), lsw.end());
     release(s);
     delete s;
     c->err = m;
@@ -2539,6 +2571,10 @@ int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
 
 int ospf_sweep_destroy(ospf_sweep* s) {
   if (!s) return OSPF_E_INVAL;
+  if (s->c) {
+    auto& ls = s->c->live_sweeps;
+    ls.erase(std::remove(ls.begin(), ls.end(), s), ls.end());
+  }
   release(s);
   delete s;
   return OSPF_OK;

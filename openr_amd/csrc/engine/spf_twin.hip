@@ -320,6 +320,26 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
     __builtin_amdgcn_wave_barrier();
     const size_t dst0 = ((size_t)i * V + tv0) * W;
     const uint32_t tn = tv0 < V ? min(1024u, V - tv0) : 0u;
+    if (a.dist && tn) {  // dist row = own level - 1 (0x7F: unreached), 1 KB per store
+      uint32_t* drow = a.dist + (size_t)own * V + tv0;
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const uint32_t Lw = s_Lb[wave][x * 64 + lane], n0 = (uint32_t)x * 256u + 4u * lane;
+        uint32_t dv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t l = (Lw >> (8 * q)) & 0xFFu;
+          dv[q] = l < 0x7Fu ? l - 1u : kInf;
+        }
+        if (n0 + 4u <= tn && (V & 3u) == 0) {
+          store_row16(reinterpret_cast<uint4*>(drow + n0), make_uint4(dv[0], dv[1], dv[2], dv[3]));
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (n0 + q < tn) drow[n0 + q] = dv[q];
+        }
+      }
+    }
     if (tn == 1024u && (dst0 & 3u) == 0) {
 #pragma unroll
       for (int x = 0; x < 4 * W; ++x)
@@ -496,7 +516,7 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
           bh[j] += kd[q] * (uint64_t)l;
         }
       }
-      if (a.dist) {
+      if (a.dist && !(s_umask[j] >> 31)) {  // bit 31: the root's next-hop launch writes it
         uint32_t* drow = a.dist + (size_t)own * V + v0;
         if (vec) {
           store_row16(drow, make_uint4(dv[0], dv[1], dv[2], dv[3]));

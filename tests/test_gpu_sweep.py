@@ -335,7 +335,10 @@ def test_sweep_poison_and_profile(mode):
         prof = sw.profile(2)
         assert prof[0]["name"] == "levels" if mode == "derive" else prof[0]["name"].startswith("lds_w")
         assert all(p["ms_median"] > 0 and p["compulsory_bytes"] > 0 for p in prof)
-        assert sw.step_compulsory_bytes == sum(p["compulsory_bytes"] for p in prof)
+        # a unit's bytes may include intermediate rows it writes for a later
+        # unit (twin level rows when its dist rows are fused into the twin
+        # next-hop unit); the step counts outputs only
+        assert 0 < sw.step_compulsory_bytes <= sum(p["compulsory_bytes"] for p in prof)
         sw.close()
     finally:
         eng.close()
