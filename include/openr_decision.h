@@ -107,6 +107,10 @@ void odl_topology_stats(const odl_ls* ls, uint64_t* out4);
 /* nodes added or removed in place (their rows inserted / erased and the ids
  * above them renumbered, no whole snapshot; the device graph reloads) */
 uint64_t odl_node_patches(const odl_ls* ls);
+/* multi-device LinkState (odl_create_multi): out4 = {root batches split
+ * across the device slots, their per-slot launches, KSP2 prefetches split
+ * across the slots (destinations of one source), their per-slot runs} */
+void odl_shard_stats(const odl_ls* ls, uint64_t* out4);
 uint32_t odl_num_nodes(const odl_ls* ls);
 uint32_t odl_num_links(const odl_ls* ls);
 

@@ -615,6 +615,13 @@ int ospf_sweep_copy_rows(ospf_sweep* sw, const uint32_t* roots, uint32_t n, uint
  * after one untimed one; fills min(cap, n_launches) records. The sweep must
  * have run once. */
 int ospf_sweep_profile(ospf_sweep* sw, uint32_t reps, ospf_sweep_launch* out, uint32_t cap);
+/* Diagnostic: the memset nodes of the sweep's captured HIP graph (none
+ * unless OSPF_ZERO_MEMSET=1 routes the engine's zeroing through
+ * hipMemsetAsync): how many (n_memset), how many whose destination range is
+ * not inside a live device allocation (n_dead), how many inside the
+ * sweep's own blocks (n_own). */
+int ospf_sweep_graph_memsets(const ospf_sweep* sw, uint32_t* n_memset, uint32_t* n_dead,
+                             uint32_t* n_own);
 
 /* ---------------------------------------------------------------- devices
  * Several devices of one node behind one handle (SURVEY.md §8(b) ospf_open

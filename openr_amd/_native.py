@@ -38,7 +38,7 @@ ENGINE_SYMBOLS = [
     "ospf_sweep_create", "ospf_sweep_destroy", "ospf_sweep_last_error", "ospf_sweep_get_info",
     "ospf_sweep_roots", "ospf_sweep_run", "ospf_sweep_digests", "ospf_sweep_digests_host",
     "ospf_sweep_poison",
-    "ospf_sweep_row", "ospf_sweep_copy_rows", "ospf_sweep_profile",
+    "ospf_sweep_row", "ospf_sweep_copy_rows", "ospf_sweep_profile", "ospf_sweep_graph_memsets",
     "ospf_multi_open", "ospf_multi_close", "ospf_multi_last_error", "ospf_multi_size",
     "ospf_multi_ctx", "ospf_multi_load_graph", "ospf_msweep_create", "ospf_msweep_destroy",
     "ospf_msweep_run", "ospf_msweep_digests", "ospf_msweep_part", "ospf_msweep_owner",
@@ -50,7 +50,7 @@ DECISION_SYMBOLS = [
     "odl_kth_paths_text", "odl_links_text", "odl_link_keys_text", "odl_metric_a_to_b", "odl_is_overloaded",
     "odl_spf_runs", "odl_set_incremental", "odl_set_host_spf", "odl_incremental_stats", "odl_topology_stats", "odl_num_nodes", "odl_num_links", "odl_spf_digests", "odl_spf_prefetch",
     "odl_ksp2_text", "odl_route_text", "odl_route_db_text", "odl_route_db_bin", "odl_free_buf", "odl_path_a_in_b", "odl_ucmp_text", "odl_csr_size", "odl_csr_export", "odl_node_name", "odl_node_id",
-    "odl_apply_kvs", "odl_apply_publication", "odl_node_patches", "odl_route_db_multi_text", "odl_adjdbs_decode", "odl_adjdbs_stream", "odl_adjdbs_error", "odl_adjdbs_free",
+    "odl_apply_kvs", "odl_apply_publication", "odl_node_patches", "odl_shard_stats", "odl_route_db_multi_text", "odl_adjdbs_decode", "odl_adjdbs_stream", "odl_adjdbs_error", "odl_adjdbs_free",
 ]
 
 
@@ -197,6 +197,7 @@ def engine() -> C.CDLL:
         L.ospf_sweep_row.argtypes = [vp, u32, C.POINTER(vp), C.POINTER(vp), C.POINTER(u32)]
         L.ospf_sweep_copy_rows.argtypes = [vp, vp, u32, u32, vp, vp]
         L.ospf_sweep_profile.argtypes = [vp, u32, vp, u32]
+        L.ospf_sweep_graph_memsets.argtypes = [vp, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32)]
         L.ospf_multi_open.argtypes = [vp, u32, C.POINTER(vp)]
         L.ospf_multi_close.argtypes = [vp]
         L.ospf_multi_last_error.argtypes = [vp]
@@ -263,6 +264,8 @@ def decision() -> C.CDLL:
         L.odl_route_db_multi_text.argtypes = [vp, u32, cp, u32, cp, u32, i32]
         L.odl_route_db_multi_text.restype = C.POINTER(C.c_char)
         L.odl_node_patches.argtypes = [vp]
+        L.odl_shard_stats.argtypes = [vp, vp]
+        L.odl_shard_stats.restype = None
         L.odl_node_patches.restype = u64
         L.odl_apply_kvs.argtypes = [vp, u32, vp, vp, vp, u32, vp, cp, vp]
         L.odl_apply_kvs.restype = i32

@@ -301,6 +301,14 @@ void odl_topology_stats(const odl_ls* h, uint64_t* out4) {
   out4[3] = st.rows_patched;
 }
 uint64_t odl_node_patches(const odl_ls* h) { return h ? h->ls.topologyStats().node_patches : 0; }
+void odl_shard_stats(const odl_ls* h, uint64_t* out4) {
+  if (!h || !out4) return;
+  const auto& st = h->ls.shardStats();
+  out4[0] = st.spf_batches;
+  out4[1] = st.spf_launches;
+  out4[2] = st.ksp2_runs;
+  out4[3] = st.ksp2_launches;
+}
 uint32_t odl_num_nodes(const odl_ls* h) { return h ? (uint32_t)h->ls.numNodes() : 0; }
 uint32_t odl_num_links(const odl_ls* h) { return h ? (uint32_t)h->ls.numLinks() : 0; }
 

@@ -895,6 +895,36 @@ uint32_t LinkState::nhWordsFor(uint32_t root) const {
   return std::max<uint32_t>(1, (n + 31) / 32);
 }
 
+std::vector<ospf_ctx*> LinkState::slots() const {
+  std::vector<ospf_ctx*> out;
+  if (multi_) {
+    for (uint32_t i = 0, n = ospf_multi_size(multi_); i < n; ++i) out.push_back(ospf_multi_ctx(multi_, i));
+  } else if (engine_) {
+    out.push_back(engine_);
+  }
+  return out;
+}
+
+int LinkState::batchOn(ospf_ctx* c, const uint32_t* roots, uint32_t n, bool useLinkMetric,
+                       uint32_t flags, uint32_t W, uint32_t* dist, uint32_t* nh) const {
+  if (!useLinkMetric) flags |= OSPF_HOP_COUNT;
+  return ospf_sssp_batch(c, roots, n, nullptr, flags, W, dist, nh, nullptr);
+}
+
+// Run fn(slot, ctx) for every slot, slot 0 on the calling thread; the first
+// failure (rc, slot) is returned after every thread joined.
+static std::pair<int, size_t> onSlots(const std::vector<ospf_ctx*>& cs,
+                                      const std::function<int(size_t, ospf_ctx*)>& fn) {
+  std::vector<int> rc(cs.size(), OSPF_OK);
+  std::vector<std::thread> th;
+  for (size_t i = 1; i < cs.size(); ++i) th.emplace_back([&, i] { rc[i] = fn(i, cs[i]); });
+  rc[0] = fn(0, cs[0]);
+  for (auto& t : th) t.join();
+  for (size_t i = 0; i < cs.size(); ++i)
+    if (rc[i] != OSPF_OK) return {rc[i], i};
+  return {OSPF_OK, 0};
+}
+
 void LinkState::runBatch(const std::vector<uint32_t>& roots,
                          const std::vector<std::vector<uint32_t>>* ign, bool useLinkMetric,
                          uint32_t flags, uint32_t W, std::vector<uint32_t>* dist,
@@ -1103,10 +1133,27 @@ void LinkState::prefetchSpf(const std::vector<std::string>& roots, bool useLinkM
       std::vector<uint32_t> part(ids.begin() + c0, ids.begin() + std::min(ids.size(), c0 + chunk));
       std::vector<uint32_t> dist, nh;
       const auto t0 = std::chrono::steady_clock::now();
-      if (fromSweep)
+      const std::vector<ospf_ctx*> cs = fromSweep ? std::vector<ospf_ctx*>{} : (ensureEngine(), slots());
+      if (fromSweep) {
         sweepRows(part, W, dist, nh);
-      else
+      } else if (cs.size() > 1 && part.size() >= cs.size()) {
+        // split across the device slots: contiguous slices, rows in place
+        const size_t m = part.size(), ns = cs.size();
+        dist.assign(m * V, kInf);
+        nh.assign(m * V * W, 0);
+        const auto [rc, bad] = onSlots(cs, [&](size_t i, ospf_ctx* c) {
+          const size_t a = m * i / ns, b = m * (i + 1) / ns;
+          return b > a ? batchOn(c, part.data() + a, (uint32_t)(b - a), useLinkMetric,
+                                 OSPF_WANT_DIST | OSPF_WANT_NH, W, dist.data() + a * V,
+                                 nh.data() + a * V * W)
+                       : OSPF_OK;
+        });
+        if (rc != OSPF_OK) throw EngineError(rc, ospf_last_error(cs[bad]));
+        ++shardStats_.spf_batches;
+        shardStats_.spf_launches += ns;
+      } else {
         runBatch(part, nullptr, useLinkMetric, OSPF_WANT_DIST | OSPF_WANT_NH, W, &dist, &nh, nullptr);
+      }
       const auto t1 = std::chrono::steady_clock::now();
       for (size_t i = 0; i < part.size(); ++i) {
         auto rows = std::make_shared<SpfRows>();
@@ -1326,16 +1373,33 @@ void LinkState::prefetchKsp2(const std::string& src, const std::vector<std::stri
   if (const char* x = getenv("ODL_KSP_CAP")) kCap = std::max(2, std::min(2048, atoi(x)));
   const size_t n = ids.size();
   std::vector<uint32_t> k1(n * kCap), k2(n * kCap), status(n);
-  ospf_ksp2 a{};
-  a.src = sid->second;
-  a.dsts = ids.data();
-  a.n = (uint32_t)n;
-  a.path_cap = kCap;
-  a.k1 = k1.data();
-  a.k2 = k2.data();
-  a.status = status.data();
-  int rc = ospf_ksp2_run(engine_, &a);
-  if (rc != OSPF_OK) throw EngineError(rc, ospf_last_error(engine_));
+  auto runOn = [&](ospf_ctx* c, size_t a0, size_t a1) {
+    ospf_ksp2 a{};
+    a.src = sid->second;
+    a.dsts = ids.data() + a0;
+    a.n = (uint32_t)(a1 - a0);
+    a.path_cap = kCap;
+    a.k1 = k1.data() + a0 * kCap;
+    a.k2 = k2.data() + a0 * kCap;
+    a.status = status.data() + a0;
+    return a1 > a0 ? ospf_ksp2_run(c, &a) : OSPF_OK;
+  };
+  const std::vector<ospf_ctx*> cs = slots();
+  if (cs.size() > 1 && n >= cs.size()) {
+    // destinations of one source split across the device slots (SURVEY
+    // §8(e)): each slot runs the source's SPF, its k = 1 traces and its
+    // destinations' reruns; records land in place in k1 / k2 / status
+    const size_t ns = cs.size();
+    const auto [rc, bad] = onSlots(cs, [&](size_t i, ospf_ctx* c) {
+      return runOn(c, n * i / ns, n * (i + 1) / ns);
+    });
+    if (rc != OSPF_OK) throw EngineError(rc, ospf_last_error(cs[bad]));
+    ++shardStats_.ksp2_runs;
+    shardStats_.ksp2_launches += ns;
+  } else {
+    const int rc = runOn(engine_, 0, n);
+    if (rc != OSPF_OK) throw EngineError(rc, ospf_last_error(engine_));
+  }
   auto decode = [&](const uint32_t* rec) {
     std::vector<Path> paths(rec[0]);
     for (uint32_t p = 0, q = 1; p < rec[0]; ++p) {

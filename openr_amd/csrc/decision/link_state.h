@@ -476,6 +476,18 @@ class LinkState {
   };
   const TopologyStats& topologyStats() const { return topoStats_; }
 
+  // Root batches (prefetchSpf outside a sweep: a KSP2 source, LFA-style
+  // neighbour batches) and KSP2 destinations split across the device slots
+  // of a multi-device LinkState; one host thread per slot, the
+  // records land in the caller's host arrays (Decision consumes them there).
+  struct ShardStats {
+    uint64_t spf_batches = 0;   // batches split across slots
+    uint64_t spf_launches = 0;  // per-slot launches of them
+    uint64_t ksp2_runs = 0;     // KSP2 prefetches split across slots
+    uint64_t ksp2_launches = 0; // per-slot ospf_ksp2_run calls of them
+  };
+  const ShardStats& shardStats() const { return shardStats_; }
+
  private:
   LinkPtr makeLink(const std::string& node, const Adjacency& adj) const;
   void addLink(const LinkPtr& l);
@@ -494,6 +506,11 @@ class LinkState {
   void runBatch(const std::vector<uint32_t>& roots, const std::vector<std::vector<uint32_t>>* ign,
                 bool useLinkMetric, uint32_t flags, uint32_t W, std::vector<uint32_t>* dist,
                 std::vector<uint32_t>* nh, std::vector<ospf_digest>* dig);
+  // the engine's device slots (slot 0 = engine_; after ensureEngine)
+  std::vector<ospf_ctx*> slots() const;
+  // runBatch's launch on one slot into dist / nh rows at the given offsets
+  int batchOn(ospf_ctx* c, const uint32_t* roots, uint32_t n, bool useLinkMetric, uint32_t flags,
+              uint32_t W, uint32_t* dist, uint32_t* nh) const;
   std::optional<Path> trace(const SpfRows& run, uint32_t src, uint32_t x,
                             std::unordered_set<const Link*>& seen) const;
   std::vector<Path> tracePaths(const SpfRows& run, uint32_t src, uint32_t dst) const;
@@ -543,6 +560,7 @@ class LinkState {
   uint64_t snapVersion_ = 0;
   std::shared_ptr<Csr> csr_ = std::make_shared<Csr>();
   TopologyStats topoStats_;
+  ShardStats shardStats_;
   bool hostMetric_ = false;   // snapshot outside the engine's metric contract
   bool hostOnly_ = false;     // setHostSpf: no engine at all
   bool hostRun(bool useLinkMetric) const { return hostOnly_ || (useLinkMetric && hostMetric_); }

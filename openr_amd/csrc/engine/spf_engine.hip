@@ -55,7 +55,7 @@ char* stream_scratch(ospf_ctx* c, void* stream, size_t need, int* rc, int slot) 
 }
 
 void release_stream_scratch(ospf_ctx* c, void* stream) {
-  for (int slot = 0; slot < 4; ++slot) {
+  for (int slot = 0; slot < 5; ++slot) {
     auto it = c->scratch.find((char*)stream + slot);
     if (it == c->scratch.end()) continue;
     if (it->second.p) hipFree(it->second.p);
@@ -534,6 +534,8 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
   t.budget = unit && !getenv("OSPF_KSP_NOHEAVY") ? kTraceBudget : 0u;
   if (const char* x = getenv("OSPF_KSP_BUDGET"))  // test knob: send runs to the heavy kernel
     if (t.budget) t.budget = (uint32_t)std::max(1, atoi(x));
+  t.look = 16;  // (OSPF_KSP_LOOK: A/B knob, 0 = no lookahead)
+  if (const char* x = getenv("OSPF_KSP_LOOK")) t.look = (uint32_t)std::max(0, atoi(x));
   t.heavy = (uint32_t*)((char*)d_dead + align_up((size_t)tchunk * dw * 4ull, 256));
   t.heavy_ctr = t.heavy + tchunk;
   hipError_t e = hipSuccess;
@@ -706,21 +708,30 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
   };
   if (getenv("OSPF_KSP_NODECR")) return full_reruns(k->dsts, n, d_ign, d_cnt, k->status, k->k2);
   // decremental reruns (spf_ksp2.hip): the source's row + per-run lost
-  // supports; the runs past its budgets through full_reruns, compacted
+  // supports. Runs whose ignore list is past its budget are known before it
+  // starts (presplit): their full reruns go on `s` while the decremental
+  // kernels run on ksp_aux; the runs it gives up on follow them, compacted.
   {
     const size_t dwb = align_up((size_t)dw * 4ull, 256);
-    const uint32_t nblk = std::max<uint32_t>(1, ospf::ksp_decr_blocks_per_cu() * (uint32_t)c->n_cu);
+    uint32_t bpc = ospf::ksp_decr_blocks_per_cu();
+    if (const char* x = getenv("OSPF_KSP_DECR_BPC")) bpc = std::max(1u, std::min(bpc, (uint32_t)atoi(x)));
+    const uint32_t nblk = std::max<uint32_t>(1, bpc * (uint32_t)c->n_cu);
     const uint32_t hblk = 2u * (uint32_t)c->n_cu;  // ksp_decr_heavy_kernel: 2 per CU
     const size_t sz_tc = align_up(V * 4ull, 256), sz_fb = align_up(n * 4ull, 256), sz_ctr = 256,
                  sz_dd = dwb * std::max(nblk, hblk);
-    char* dp = stream_scratch(c, s, sz_tc + 2 * sz_fb + sz_ctr + sz_dd, &rc, 2);
+    // heavy runs' pruning (unit metric): level order + per-block good bits
+    const bool prune = t_k1.budget && !getenv("OSPF_KSP_NOPRUNE");
+    const size_t sz_ord = prune ? align_up(V * 4ull, 256) + align_up(2 * 257 * 4ull, 256) : 0,
+                 sz_good = prune ? dwb * hblk + (size_t)hblk * ospf::kGoodBig * 4ull : 0;
+    char* dp = stream_scratch(c, s, sz_tc + 3 * sz_fb + sz_ctr + sz_dd + sz_ord + sz_good, &rc, 2);
     if (rc) return rc;
     uint32_t* d_tc = (uint32_t*)dp;
     uint32_t* d_fb = (uint32_t*)(dp + sz_tc);
     uint32_t* d_hq = (uint32_t*)(dp + sz_tc + sz_fb);
-    uint32_t* d_ctr = (uint32_t*)(dp + sz_tc + 2 * sz_fb);
-    uint32_t* d_dd = (uint32_t*)(dp + sz_tc + 2 * sz_fb + sz_ctr);
-    HIPCHK(c, ospf::zero_async(d_ctr, 32, s));
+    uint32_t* d_pre = (uint32_t*)(dp + sz_tc + 2 * sz_fb);
+    uint32_t* d_ctr = (uint32_t*)(dp + sz_tc + 3 * sz_fb);
+    uint32_t* d_dd = (uint32_t*)(dp + sz_tc + 3 * sz_fb + sz_ctr);
+    HIPCHK(c, ospf::zero_async(d_ctr, 128, s));
     e = ospf::launch_ksp_hint(c->g, src, d_dist1, d_tc, s);
     if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_hint");
     ospf::TraceArgs td = t_k1;
@@ -742,43 +753,100 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
     td.heavy = d_hq;
     td.heavy_ctr = d_ctr + 4;
     td.err = c->d_err;
-    e = ospf::launch_ksp_decr(c->g, td, nblk, s);
+    if (prune) {
+      char* q = dp + sz_tc + 3 * sz_fb + sz_ctr + sz_dd;
+      uint32_t* d_ord = (uint32_t*)q;
+      uint32_t* d_off = (uint32_t*)(q + align_up(V * 4ull, 256));
+      e = ospf::launch_ksp_levels(d_dist1, V, d_ord, d_off, d_off + 257, s);
+      if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_levels");
+      td.ord = d_ord;
+      td.lvl_off = d_off;
+      td.nlvl = 256;
+      td.good = (uint32_t*)(q + sz_ord);
+      td.big = (uint32_t*)(q + sz_ord + dwb * hblk);
+    }
+    // (presplit count in ctr[12])
+    uint32_t npre = 0;
+    const bool split = getenv("OSPF_KSP_NOSPLIT") == nullptr;
+    if (split) {
+      e = ospf::launch_ksp_presplit(td, d_pre, d_ctr + 12, s);
+      if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_presplit");
+      HIPCHK(c, hipMemcpyAsync(&npre, d_ctr + 12, 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(c, hipStreamSynchronize(s));
+    }
+    td.skip_ign = split ? 1u : 0u;
+    hipStream_t ks = s;
+    if (npre) {
+      if (!c->ksp_aux) HIPCHK(c, hipStreamCreateWithFlags(&c->ksp_aux, hipStreamNonBlocking));
+      for (hipEvent_t& x : c->ksp_ev)
+        if (!x) HIPCHK(c, hipEventCreateWithFlags(&x, hipEventDisableTiming));
+      HIPCHK(c, hipEventRecord(c->ksp_ev[0], s));
+      HIPCHK(c, hipStreamWaitEvent(c->ksp_aux, c->ksp_ev[0], 0));
+      ks = c->ksp_aux;
+    }
+    e = ospf::launch_ksp_decr(c->g, td, nblk, ks);
     if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_decr");
     if (td.budget) {
-      e = ospf::launch_ksp_decr_heavy(c->g, td, hblk, s);
+      e = ospf::launch_ksp_decr_heavy(c->g, td, hblk, ks);
       if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_decr_heavy");
     }
-    uint32_t ctr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    HIPCHK(c, hipMemcpyAsync(ctr, d_ctr, 32, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipStreamSynchronize(s));
-    if (getenv("OSPF_KSP_DEBUG"))
-      fprintf(stderr, "ksp2 decr: runs %u decided %u fallbacks %u (A %u, map %u) heavy %u affected %u\n",
-              n, ctr[2], ctr[1], ctr[6], ctr[7], ctr[4], ctr[3]);
+    // a list of runs through full_reruns on s: compacted (dsts, status,
+    // ignore sets, counts) into scratch slot `slot`, records scattered back
+    auto rerun_list = [&](const uint32_t* d_list, uint32_t nl, int slot) -> int {
+      const size_t sz_fd = align_up(nl * 4ull, 256), sz_fr = align_up((size_t)nl * cap * 4ull, 256);
+      int rc2 = OSPF_OK;
+      char* fp = stream_scratch(c, s, 3 * sz_fd + 2 * sz_fr, &rc2, slot);
+      if (rc2) return rc2;
+      uint32_t* f_dsts = (uint32_t*)fp;
+      uint32_t* f_status = (uint32_t*)(fp + sz_fd);
+      uint32_t* f_cnt = (uint32_t*)(fp + 2 * sz_fd);
+      uint32_t* f_ign = (uint32_t*)(fp + 3 * sz_fd);
+      uint32_t* f_k2 = (uint32_t*)(fp + 3 * sz_fd + sz_fr);
+      hipError_t e2;
+      if ((e2 = ospf::launch_rows_gather(f_dsts, k->dsts, d_list, nl, 1, true, s)) != hipSuccess ||
+          (e2 = ospf::launch_rows_gather(f_status, k->status, d_list, nl, 1, true, s)) != hipSuccess ||
+          (e2 = ospf::launch_rows_gather(f_cnt, d_cnt, d_list, nl, 1, true, s)) != hipSuccess ||
+          (e2 = ospf::launch_rows_gather(f_ign, d_ign, d_list, nl, cap, true, s)) != hipSuccess)
+        return hip_fail(c, e2, "launch_rows_gather");
+      rc2 = full_reruns(f_dsts, nl, f_ign, f_cnt, f_status, f_k2);
+      if (rc2) return rc2;
+      if ((e2 = ospf::launch_rows_gather(k->status, f_status, d_list, nl, 1, false, s)) != hipSuccess ||
+          (e2 = ospf::launch_rows_gather(k->k2, f_k2, d_list, nl, cap, false, s)) != hipSuccess)
+        return hip_fail(c, e2, "launch_rows_gather");
+      return OSPF_OK;
+    };
+    if (npre) {  // beside the decremental kernels
+      rc = rerun_list(d_pre, npre, 3);
+      if (rc) return rc;
+    }
+    uint32_t ctr[32] = {};
+    HIPCHK(c, hipMemcpyAsync(ctr, d_ctr, 128, hipMemcpyDeviceToHost, ks));
+    HIPCHK(c, hipStreamSynchronize(ks));
+    if (ks != s) {
+      HIPCHK(c, hipEventRecord(c->ksp_ev[1], ks));
+      HIPCHK(c, hipStreamWaitEvent(s, c->ksp_ev[1], 0));
+    }
+    if (getenv("OSPF_KSP_DEBUG")) {
+      uint64_t clk[8];
+      memcpy(clk, ctr + 16, sizeof(clk));
+      // wave-ms: wall-clock ms (100 MHz) summed over the waves / blocks
+      auto wm = [](uint64_t x) { return (double)x / 1e5; };
+      fprintf(stderr,
+              "ksp2 decr: runs %u presplit %u decided %u fallbacks %u (A %u, map %u, ign %u, hash %u, edges %u) "
+              "heavy %u affected %u; wave-ms prep %.1f step3 %.1f trace %.1f fb-prep %.1f; heavy "
+              "block-ms prep %.1f trace %.1f\n",
+              n, npre, ctr[2], ctr[1], ctr[6], ctr[7], ctr[8], ctr[9], ctr[10], ctr[4], ctr[3], wm(clk[0]),
+              wm(clk[1]), wm(clk[2]), wm(clk[3]), wm(clk[4]), wm(clk[5]));
+    }
     c->ksp_decr_stats[0] += ctr[2];
-    c->ksp_decr_stats[1] += ctr[1];
+    c->ksp_decr_stats[1] += ctr[1] + npre;
     c->ksp_decr_stats[2] += ctr[3];
     const uint32_t nfb = ctr[1];
-    c->spf_runs += n - nfb;  // (full_reruns counts its own)
-    if (nfb == 0) return OSPF_OK;
-    // compact the fallbacks: dsts, status, ignore sets, counts; k2 records back
-    const size_t sz_fd = align_up(nfb * 4ull, 256), sz_fr = align_up((size_t)nfb * cap * 4ull, 256);
-    char* fp = stream_scratch(c, s, 3 * sz_fd + 2 * sz_fr, &rc, 3);
-    if (rc) return rc;
-    uint32_t* f_dsts = (uint32_t*)fp;
-    uint32_t* f_status = (uint32_t*)(fp + sz_fd);
-    uint32_t* f_cnt = (uint32_t*)(fp + 2 * sz_fd);
-    uint32_t* f_ign = (uint32_t*)(fp + 3 * sz_fd);
-    uint32_t* f_k2 = (uint32_t*)(fp + 3 * sz_fd + sz_fr);
-    if ((e = ospf::launch_rows_gather(f_dsts, k->dsts, d_fb, nfb, 1, true, s)) != hipSuccess ||
-        (e = ospf::launch_rows_gather(f_status, k->status, d_fb, nfb, 1, true, s)) != hipSuccess ||
-        (e = ospf::launch_rows_gather(f_cnt, d_cnt, d_fb, nfb, 1, true, s)) != hipSuccess ||
-        (e = ospf::launch_rows_gather(f_ign, d_ign, d_fb, nfb, cap, true, s)) != hipSuccess)
-      return hip_fail(c, e, "launch_rows_gather");
-    rc = full_reruns(f_dsts, nfb, f_ign, f_cnt, f_status, f_k2);
-    if (rc) return rc;
-    if ((e = ospf::launch_rows_gather(k->status, f_status, d_fb, nfb, 1, false, s)) != hipSuccess ||
-        (e = ospf::launch_rows_gather(k->k2, f_k2, d_fb, nfb, cap, false, s)) != hipSuccess)
-      return hip_fail(c, e, "launch_rows_gather");
+    c->spf_runs += n - nfb - npre;  // (full_reruns counts its own)
+    if (nfb) {
+      rc = rerun_list(d_fb, nfb, 4);
+      if (rc) return rc;
+    }
   }
   return OSPF_OK;
 }
@@ -1196,6 +1264,9 @@ int ospf_close(ospf_ctx* c) {
   if (c->d_err) hipFree(c->d_err);
   for (hipEvent_t e : c->ev) hipEventDestroy(e);
   if (c->aux) hipStreamDestroy(c->aux);
+  if (c->ksp_aux) hipStreamDestroy(c->ksp_aux);
+  for (hipEvent_t e : c->ksp_ev)
+    if (e) hipEventDestroy(e);
   for (hipEvent_t e : c->lv_ev)
     if (e) hipEventDestroy(e);
   if (c->d_cover) hipFree(c->d_cover);

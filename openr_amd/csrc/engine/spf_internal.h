@@ -63,6 +63,9 @@ struct ospf_ctx {
   uint32_t* d_err = nullptr;
   // KSP2: traces run on an engine stream, overlapping later reruns
   hipStream_t aux = nullptr;
+  // KSP2: the decremental kernels beside the pre-split runs' full reruns
+  hipStream_t ksp_aux = nullptr;
+  hipEvent_t ksp_ev[2] = {nullptr, nullptr};
   // derive phase 1: rows kernels of one round beside the next round's levels
   hipStream_t lv_aux = nullptr;
   hipEvent_t lv_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // traversed[2], rows done[2]

@@ -633,6 +633,8 @@ struct TraceArgs {
   uint32_t* dead;           // [n][dead_words] dead-node bits, zeroed by the caller
   uint32_t dead_words;      // (V + 31) / 32
   uint32_t budget;          // DFS steps before a run goes to the heavy kernel (0 = none)
+  uint32_t look;            // lookahead: predecessors with rows <= look entries are probed
+  uint32_t skip_ign;        // ksp_decr: skip runs the presplit sent to the full reruns
   uint32_t* heavy;          // [n] queued run indices
   uint32_t* heavy_ctr;      // [2] {queued, taken}, zeroed by the caller
   // decremental reruns (launch_ksp_decr): rows = the source's dist row
@@ -641,7 +643,19 @@ struct TraceArgs {
   uint32_t* ctr;            // [8] {next run, fallbacks, runs decided, affected nodes, heavy
                             //  queued / taken, A overflows, hash overflows}, zeroed
   uint32_t* err;            // the engine's device error word
+  // heavy decremental runs: the source's nodes by level (unit metric,
+  // levels < nlvl; launch_ksp_levels) and per-block scratch for the good set
+  const uint32_t* ord;      // [V] node ids, level-major
+  const uint32_t* lvl_off;  // [nlvl + 1]
+  uint32_t nlvl;            // 0: no level order (no pruning)
+  uint32_t* good;           // [blocks][dead_words]
+  uint32_t* big;            // [blocks][kGoodBig] long-row nodes of a level
 };
+// the nodes of the source's dist row by level: ord[V], off[257] (levels
+// 0..255; farther nodes are left out), cnt: 257 words of scratch
+hipError_t launch_ksp_levels(const uint32_t* dist, uint32_t V, uint32_t* ord, uint32_t* off,
+                             uint32_t* cnt, hipStream_t s);
+constexpr uint32_t kGoodBig = 4096;
 hipError_t launch_ksp_trace(bool lev, const DevGraph& g, const TraceArgs& t, hipStream_t s);
 // KSP2 k = 2 by decremental SSSP (spf_ksp2.hip): hint[v] = the link id of
 // v's last usable in-link (u, v) in row order with u transit (or the
@@ -654,6 +668,9 @@ hipError_t launch_ksp_hint(const DevGraph& g, uint32_t src, const uint32_t* dist
 // for the full masked reruns. t.dead: [blocks][dead_words], zeroed.
 hipError_t launch_ksp_decr(const DevGraph& g, const TraceArgs& t, uint32_t blocks, hipStream_t s);
 uint32_t ksp_decr_blocks_per_cu();
+// runs past the decremental kernel's ignore-list budget (the ones it would
+// send to the full reruns at once): their indices into list, *count of them
+hipError_t launch_ksp_presplit(const TraceArgs& t, uint32_t* list, uint32_t* count, hipStream_t s);
 // the runs ksp_decr queued as heavy (t.heavy / t.heavy_ctr): 16 waves each;
 // t.dead: [blocks][dead_words]; t.err: the engine's error word
 hipError_t launch_ksp_decr_heavy(const DevGraph& g, const TraceArgs& t, uint32_t blocks,
@@ -674,8 +691,14 @@ hipError_t launch_fill32(uint32_t* a, size_t n, uint32_t v, hipStream_t s);
 // nodes of a captured sweep graph replayed right after a caller's memset on
 // the same stream were seen writing pointer-like values into digest slots
 // (ROCm 7.2, gfx950; scripts/debug/replay_parity.py), kernel nodes never.
+// OSPF_ZERO_MEMSET=1 restores hipMemsetAsync (the round-4 behaviour), for
+// the A/B of scripts/debug/memset_nodes.py.
+inline bool zero_by_memset() {
+  static const bool m = getenv("OSPF_ZERO_MEMSET") != nullptr;
+  return m;
+}
 inline hipError_t zero_async(void* p, size_t bytes, hipStream_t s) {
-  if (bytes & 3u) return hipMemsetAsync(p, 0, bytes, s);
+  if ((bytes & 3u) || zero_by_memset()) return hipMemsetAsync(p, 0, bytes, s);
   return launch_fill32(static_cast<uint32_t*>(p), bytes / 4u, 0u, s);
 }
 hipError_t launch_shift_add(uint32_t* a, uint32_t n, uint32_t from, uint32_t thresh, uint32_t d,

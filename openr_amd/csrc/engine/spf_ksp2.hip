@@ -27,7 +27,7 @@
 //    links into dead nodes instead of claiming them, so the visited set holds
 //    just the links of the paths found (an LDS hash) and each node is
 //    explored in failure at most once per (src, dst, k).
-//  * lookahead. A candidate predecessor with a short row (<= kLook entries)
+//  * lookahead. A candidate predecessor with a short row (<= t.look entries, 16 by default)
 //    is entered only if it has an open pathLink itself (unclaimed, into a
 //    node not dead, or src); otherwise it would fail at once, so it is marked
 //    dead without the descent.
@@ -54,7 +54,6 @@ constexpr uint32_t kWaves = kBlock / kWave;
 constexpr uint32_t kStack = 256;      // links per path
 constexpr uint32_t kHash = 2048;      // visited-set slots (power of 2)
 constexpr uint32_t kSteps = 1u << 22; // DFS steps per run (termination guard)
-constexpr uint32_t kLook = 16;        // lookahead row length limit
 
 __device__ __forceinline__ bool in_sorted(const uint32_t* a, uint32_t n, uint32_t x) {
   uint32_t lo = 0, hi = n;
@@ -142,9 +141,10 @@ struct Tracer {
     __hip_atomic_fetch_or(&dead[u >> 5], 1u << (u & 31u), __ATOMIC_RELAXED,
                           __HIP_MEMORY_SCOPE_WORKGROUP);
   }
-  // pathLinks entry e of row v, not claimed, predecessor not dead?
-  __device__ bool cand(uint32_t v, uint32_t dv, uint32_t e, uint32_t& du) const {
-    const uint32_t cx = g.colx[e];
+  // pathLinks entry e of row v, not claimed, predecessor cx not dead? (no
+  // lookahead: see alive)
+  __device__ bool cand0(uint32_t v, uint32_t dv, uint32_t e, uint32_t& du, uint32_t& cx) const {
+    cx = g.colx[e];
     if (cx & kDown) return false;
     if (cx == v) return false;
     du = dist(cx);
@@ -155,11 +155,41 @@ struct Tracer {
     const uint32_t lid = g.link_id[e];
     if (nign && in_sorted(ign, nign, lid)) return false;
     if (cx == src) return !claimed(lid);
-    if (is_dead(cx) || claimed(lid)) return false;
-    // one level of lookahead on short rows: a predecessor without an open
-    // pathLink of its own fails at once when entered, i.e. it is dead
+    return !is_dead(cx) && !claimed(lid);
+  }
+  // one level of lookahead by the whole wave (wave-uniform x != src, du =
+  // dist(x)): a predecessor whose short row (<= t.look entries) holds no
+  // open pathLink of its own fails at once when entered, i.e. it is dead
+  __device__ bool alive(uint32_t x, uint32_t du) const {
+    const uint32_t b2 = g.row_ptr[x], e2end = g.row_ptr[x + 1];
+    if (e2end - b2 > t.look) return true;
+    bool ok = false;
+    for (uint32_t e2 = b2 + lane; e2 < e2end; e2 += kWave) {
+      const uint32_t c2 = g.colx[e2];
+      if ((c2 & kDown) || c2 == x) continue;
+      const uint32_t d2 = dist(c2);
+      if (d2 == kInf || (uint64_t)d2 + (t.unit ? 1u : g.rw[e2]) != du) continue;
+      if (c2 != src && ((g.nt_bits[c2 >> 5] >> (c2 & 31u)) & 1u)) continue;
+      const uint32_t l2 = g.link_id[e2];
+      if (nign && in_sorted(ign, nign, l2)) continue;
+      if (c2 != src && is_dead(c2)) continue;
+      if (!claimed(l2)) ok = true;
+    }
+    if (__ballot(ok)) return true;
+    if (lane == 0) mark_dead(x);
+    return false;
+  }
+  // cand0 plus this lane's own sequential lookahead (the 16-wave kernel's
+  // candidate gathering)
+  __device__ bool cand(uint32_t v, uint32_t dv, uint32_t e, uint32_t& du) const {
+    uint32_t cx = 0;
+    if (!cand0(v, dv, e, du, cx)) return false;
+    return cx == src || look_lane(cx, du);
+  }
+  // this lane's lookahead of its own predecessor cx != src (see alive)
+  __device__ bool look_lane(uint32_t cx, uint32_t du) const {
     const uint32_t b2 = g.row_ptr[cx], e2end = g.row_ptr[cx + 1];
-    if (e2end - b2 > kLook) return true;
+    if (e2end - b2 > t.look) return true;
     for (uint32_t e2 = b2; e2 < e2end; ++e2) {
       const uint32_t c2 = g.colx[e2];
       if ((c2 & kDown) || c2 == cx) continue;
@@ -174,31 +204,45 @@ struct Tracer {
     mark_dead(cx);
     return false;
   }
-  // smallest candidate key (du << 32 | e) >= lo among v's pathLinks, ~0 = none
+  // smallest candidate key (du << 32 | e) >= lo among v's pathLinks, ~0 =
+  // none. The cheap checks run on every lane; the lookahead (alive) only for
+  // the candidates in order until one passes, by the whole wave.
   __device__ uint64_t next_cand(uint32_t v, uint32_t dv, uint64_t lo) const {
     const uint32_t beg = g.row_ptr[v], end = g.row_ptr[v + 1];
     if (t.unit) {  // every candidate has du = dv - 1: row order
       const uint32_t e0 = lo ? max(beg, (uint32_t)lo) : beg;
       for (uint32_t base = e0; base < end; base += kWave) {
         const uint32_t e = base + lane;
-        uint32_t du = 0;
-        const bool ok = e < end && cand(v, dv, e, du);
-        const uint64_t bal = __ballot(ok);
-        if (bal) {
-          const uint32_t eb = base + (uint32_t)(__ffsll((unsigned long long)bal) - 1);
-          return ((uint64_t)(dv - 1u) << 32) | eb;
-        }
+        uint32_t du = 0, cx = 0;
+        const bool ok = e < end && cand0(v, dv, e, du, cx);
+        uint64_t bal = __ballot(ok);
+        if (!bal) continue;
+        // the first candidate by the whole wave; when it is dead, the rest of
+        // the chunk each by its own lane at once (a failing search's chunks
+        // are mostly dead ends: all of them pruned in one pass)
+        const int j = __ffsll((unsigned long long)bal) - 1;
+        const uint32_t xj = (uint32_t)__shfl((int)cx, j, kWave);
+        if (xj == src || alive(xj, dv - 1u)) return ((uint64_t)(dv - 1u) << 32) | (base + (uint32_t)j);
+        const bool ok2 = ok && lane != (uint32_t)j && (cx == src || look_lane(cx, dv - 1u));
+        bal = __ballot(ok2);
+        if (bal) return ((uint64_t)(dv - 1u) << 32) | (base + (uint32_t)(__ffsll((unsigned long long)bal) - 1));
       }
       return ~0ull;
     }
-    uint64_t best = ~0ull;
-    for (uint32_t e = beg + lane; e < end; e += kWave) {
-      uint32_t du = 0;
-      if (!cand(v, dv, e, du)) continue;
-      const uint64_t key = ((uint64_t)du << 32) | e;
-      if (key >= lo && key < best) best = key;
+    for (;;) {
+      uint64_t best = ~0ull;
+      for (uint32_t e = beg + lane; e < end; e += kWave) {
+        uint32_t du = 0, cx = 0;
+        if (!cand0(v, dv, e, du, cx)) continue;
+        const uint64_t key = ((uint64_t)du << 32) | e;
+        if (key >= lo && key < best) best = key;
+      }
+      best = wave_min64(best);
+      if (best == ~0ull) return best;
+      const uint32_t x = g.colx[(uint32_t)best];
+      if (x == src || alive(x, (uint32_t)(best >> 32))) return best;
+      lo = best + 1ull;  // x is dead now: the next key
     }
-    return wave_min64(best);
   }
   // an unclaimed pathLink out of src is left (a node x with dist(x) ==
   // metric(src -> x)); a path to src ends with one
@@ -376,12 +420,17 @@ struct HeavyLds {
   uint64_t cand[kHeavyWaves];
   int32_t res[kHeavyWaves];
   uint32_t ctl[4];
+  uint32_t nbig;
+};
+// heavy_trace's pruning hook (every thread of the block calls it): none
+struct NoPrune {
+  __device__ void operator()() const {}
 };
 // the 16-wave trace of run i, resuming from its record; `hs` = the block's
 // claim hash (kHash slots), every wave of the block calls it
-template <class DS>
+template <class DS, class Prune = NoPrune>
 __device__ void heavy_trace(const DevGraph& g, const TraceArgs& t, uint32_t i, Tracer<DS, kHash>& tr,
-                            uint32_t* hs, HeavyLds& H) {
+                            uint32_t* hs, HeavyLds& H, const Prune& prune = Prune{}) {
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   uint32_t* out = t.out + (size_t)i * t.stride;
   for (uint32_t k = threadIdx.x; k < kHash; k += blockDim.x) hs[k] = 0u;
@@ -398,6 +447,7 @@ __device__ void heavy_trace(const DevGraph& g, const TraceArgs& t, uint32_t i, T
     }
   }
   __syncthreads();
+  prune();  // (the claims of the paths found so far)
   bool ovf = false;
   uint32_t steps = 0;
   for (;;) {  // one traceOnePath per iteration
@@ -407,7 +457,10 @@ __device__ void heavy_trace(const DevGraph& g, const TraceArgs& t, uint32_t i, T
     uint64_t lo = 0;
     int winner = -1;
     bool stop = false;
-    for (;;) {  // dst's candidates, 16 at a time
+    for (uint32_t round = 0;; ++round) {  // dst's candidates, 16 at a time
+      // a long failing search: prune again with the claims of now (nodes
+      // that lost their last way to src since the last pruning)
+      if (round == 4) prune();
       if (wv == 0) {  // the next (up to) 16 candidates of dst in row order
         uint32_t m = 0;
         const uint32_t dv = tr.dist(tr.dst);
@@ -530,9 +583,13 @@ __global__ void __launch_bounds__(1024) ksp_heavy_kernel(DevGraph g, TraceArgs t
 constexpr uint32_t kAffFlag = 0x80000000u;
 __device__ __forceinline__ uint32_t dslot(uint32_t u) { return (u * 0x9E3779B1u) >> 20; }
 
-template <uint32_t MAP, uint32_t AFF, uint32_t IGN, uint32_t HS>
+template <uint32_t MAP, uint32_t AFF, uint32_t IGN, uint32_t HS, uint32_t EDGE>
 struct DecrLdsT {
   static constexpr uint32_t kMap = MAP, kFill = MAP / 4u * 3u, kAff = AFF, kIgn = IGN, kHS = HS;
+  // out-links the affected nodes' expansion may scan before the run is given
+  // up (a run that cuts a plane off scans the plane's spine rows: the full
+  // masked rerun, 64 runs per traversal, does that for less)
+  static constexpr uint32_t kEdge = EDGE;
   uint32_t keys[MAP];  // node + 1 (0: empty)
   uint32_t vals[MAP];  // supports left (hint lost), or kAffFlag | index in aff
   uint32_t aff[AFF];
@@ -542,9 +599,10 @@ struct DecrLdsT {
   uint32_t stack[kStack];
   uint32_t pend[64];   // nodes whose hint was just lost (their supports to count)
   uint32_t nkeys, naff, ovf, run, npend;
+  uint64_t t3;         // wall clock at step (3) (phase timing, t.ctr[16..])
 };
-using DecrSmall = DecrLdsT<512, 192, 256, 512>;     // ~10 KB: ~16 runs per CU in flight
-using DecrHeavy = DecrLdsT<4096, 1024, 1024, kHash>;
+using DecrSmall = DecrLdsT<512, 192, 256, 512, 8192>;  // ~10 KB: ~16 runs per CU in flight
+using DecrHeavy = DecrLdsT<4096, 1024, 1024, kHash, 1u << 30>;
 
 template <class L_>
 struct DistDecr {
@@ -574,21 +632,31 @@ struct DistDecr {
 __global__ void __launch_bounds__(256) ksp_hint_kernel(DevGraph g, uint32_t src,
                                                        const uint32_t* __restrict__ D,
                                                        uint32_t* __restrict__ hint) {
-  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  // one wave per node: a spine's row (1,781 entries at F100k) takes 28
+  // coalesced steps, not 1,781 dependent ones of a single lane
+  const uint32_t v = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63u;
   if (v >= g.V) return;
   const uint32_t dv = D[v];
   uint32_t h = kInf;
   if (dv != kInf && v != src) {
-    for (uint32_t e = g.row_ptr[v]; e < g.row_ptr[v + 1]; ++e) {
-      const uint32_t u = g.colx[e];
-      if ((u & kDown) || u == v) continue;
-      const uint32_t du = D[u];
-      if (du == kInf || (uint64_t)du + g.rw[e] != dv) continue;
-      if (u != src && ((g.nt_bits[u >> 5] >> (u & 31u)) & 1u)) continue;
-      h = g.link_id[e];
+    const uint32_t beg = g.row_ptr[v], end = g.row_ptr[v + 1];
+    for (uint32_t b = beg; b < end; b += kWave) {
+      const uint32_t e = b + lane;
+      bool ok = false;
+      if (e < end) {
+        const uint32_t u = g.colx[e];
+        if (!(u & kDown) && u != v) {
+          const uint32_t du = D[u];
+          ok = du != kInf && (uint64_t)du + g.rw[e] == dv &&
+               (u == src || !((g.nt_bits[u >> 5] >> (u & 31u)) & 1u));
+        }
+      }
+      const uint64_t bal = __ballot(ok);
+      if (bal) h = g.link_id[b + 63u - (uint32_t)__clzll((long long)bal)];
     }
   }
-  hint[v] = h;
+  if (lane == 0) hint[v] = h;
 }
 
 template <class L_>
@@ -655,7 +723,10 @@ __device__ bool decr_prepare(L_& L, const DevGraph& g, const TraceArgs& t, uint3
   auto ignored = [&](uint32_t lid) { return nign && in_sorted(L.ign, nign, lid); };
   const uint32_t* gign = t.ign + (size_t)i * t.stride;
   nign = min(t.ign_cnt[i], t.stride);
-  if (nign > L_::kIgn) return false;
+  if (nign > L_::kIgn) {
+    if (lane == 0) atomicAdd(&t.ctr[8], 1u);
+    return false;
+  }
   for (uint32_t k = lane; k < L_::kMap; k += kWave) {
     L.keys[k] = 0u;
     L.vals[k] = 0u;
@@ -762,6 +833,7 @@ __device__ bool decr_prepare(L_& L, const DevGraph& g, const TraceArgs& t, uint3
     settle_pending(0u);
   }
   // (2) affected nodes in order lose their tight out-links
+  uint32_t scanned = 0;
   for (uint32_t q = 0;; ++q) {
     const uint32_t nq = ((volatile uint32_t&)L.naff);
     if (((volatile uint32_t&)L.ovf) || q >= min(nq, L_::kAff)) break;
@@ -769,6 +841,14 @@ __device__ bool decr_prepare(L_& L, const DevGraph& g, const TraceArgs& t, uint3
     if (!transit(v)) continue;
     const uint32_t dv = D[v];
     const uint32_t beg = g.row_ptr[v], end = g.row_ptr[v + 1];
+    scanned += end - beg;
+    if (scanned > L_::kEdge) {
+      if (lane == 0) {
+        L.ovf = 1u;
+        atomicAdd(&t.ctr[10], 1u);
+      }
+      break;
+    }
     for (uint32_t e0 = beg; e0 < end; e0 += kWave) {
       const uint32_t e = e0 + lane;
       bool go = false;
@@ -785,10 +865,12 @@ __device__ bool decr_prepare(L_& L, const DevGraph& g, const TraceArgs& t, uint3
     }
   }
   if (((volatile uint32_t&)L.ovf)) {
-    if (lane == 0) atomicAdd(&t.ctr[((volatile uint32_t&)L.naff) > L_::kAff ? 6 : 7], 1u);
+    if (lane == 0 && scanned <= L_::kEdge)
+      atomicAdd(&t.ctr[((volatile uint32_t&)L.naff) > L_::kAff ? 6 : 7], 1u);
     return false;
   }
   na = ((volatile uint32_t&)L.naff);
+  if (lane == 0) L.t3 = wall_clock64();
   // (3) masked distances of A: boundary terms, then rounds over A's own links
   bool inner = false;
   for (uint32_t q = 0; q < na; ++q) {
@@ -864,11 +946,22 @@ __global__ void __launch_bounds__(64) ksp_decr_kernel(DevGraph g, TraceArgs t) {
       if (lane == 0) out[0] = 0u;
       continue;
     }
+    if (t.skip_ign && t.ign_cnt[i] > DecrSmall::kIgn) continue;  // presplit: the full reruns'
     auto fallback = [&]() {
       if (lane == 0) t.fb[atomicAdd(&t.ctr[1], 1u)] = i;
     };
     uint32_t nign = 0, na = 0;
-    if (!decr_prepare(L, g, t, i, lane, nign, na)) {
+    const uint64_t c0 = wall_clock64();
+    if (lane == 0) L.t3 = 0;
+    const bool prep = decr_prepare(L, g, t, i, lane, nign, na);
+    const uint64_t c1 = wall_clock64();
+    if (lane == 0) {  // phase clocks: steps (0)-(2), step (3), trace; [19] the fallbacks' prepare
+      uint64_t* clk = reinterpret_cast<uint64_t*>(t.ctr + 16);
+      const uint64_t t3 = L.t3 ? L.t3 : c1;
+      atomicAdd((unsigned long long*)&clk[prep ? 0 : 3], (unsigned long long)(t3 - c0));
+      if (prep) atomicAdd((unsigned long long*)&clk[1], (unsigned long long)(c1 - t3));
+    }
+    if (!prep) {
       fallback();
       continue;
     }
@@ -908,7 +1001,10 @@ __global__ void __launch_bounds__(64) ksp_decr_kernel(DevGraph g, TraceArgs t) {
       if (r < 0 || !tr.emit(out, stk, depth, w, npaths, nclaim)) ovf = true;
       if (t.budget) steps = 0;
     }
+    if (lane == 0)
+      atomicAdd((unsigned long long*)(t.ctr + 16) + 2, (unsigned long long)(wall_clock64() - c1));
     if (tier) {
+      if (lane == 0) atomicAdd(&t.ctr[9], 1u);
       fallback();
       continue;
     }
@@ -922,6 +1018,137 @@ __global__ void __launch_bounds__(64) ksp_decr_kernel(DevGraph g, TraceArgs t) {
     }
     tr.finish(out, npaths, ovf, tr.hs);
   }
+}
+
+// The good set of a heavy decremental run: the nodes that still reach src
+// over tight, unignored, unclaimed links through transit nodes -- the only
+// predecessors a trace can complete through. Pulled level by level over the
+// source's level order (the run's affected nodes at their masked levels),
+// then every other node is marked dead: a failing search over a spine's
+// thousands of fabric switches ends at once instead of visiting each. Dead
+// marks are facts (claims only grow), so pruning never changes a path.
+struct GoodPrune {
+  const DevGraph& g;
+  const TraceArgs& t;
+  Tracer<DistDecr<DecrHeavy>, kHash>& tr;
+  const DecrHeavy& L;
+  HeavyLds& H;
+  uint32_t* gb;   // V bits
+  uint32_t* big;  // kGoodBig node ids
+  __device__ bool good(uint32_t u) const {
+    const uint32_t w = __hip_atomic_load(&gb[u >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return (w >> (u & 31u)) & 1u;
+  }
+  __device__ void set_good(uint32_t u) const {
+    __hip_atomic_fetch_or(&gb[u >> 5], 1u << (u & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  // entry e of v's row: a usable pathLink from a good predecessor at level d - 1
+  __device__ bool link_ok(uint32_t v, uint32_t d, uint32_t e) const {
+    const uint32_t u = g.colx[e];
+    if ((u & kDown) || u == v || !good(u)) return false;
+    if (tr.dist(u) + 1u != d) return false;  // unit metric: tight
+    const uint32_t lid = g.link_id[e];
+    if (tr.nign && in_sorted(tr.ign, tr.nign, lid)) return false;
+    return !tr.claimed(lid);
+  }
+  __device__ void operator()() const {
+    const uint32_t tid = threadIdx.x, nthr = blockDim.x;
+    const uint32_t wv = tid >> 6, lane = tid & 63u, nw = nthr >> 6;
+    const uint32_t dmax = tr.dist(tr.dst);
+    if (t.nlvl == 0 || dmax == kInf || dmax >= t.nlvl) return;
+    const uint32_t words = (g.V + 31u) / 32u;
+    const uint32_t na = ((volatile uint32_t&)L.naff) < DecrHeavy::kAff ? ((volatile uint32_t&)L.naff) : 0u;
+    for (uint32_t w = tid; w < words; w += nthr) gb[w] = 0u;
+    __syncthreads();
+    if (tid == 0) set_good(tr.src);
+    for (uint32_t d = 1; d < dmax; ++d) {
+      if (tid == 0) H.nbig = 0u;
+      __syncthreads();
+      const uint32_t b0 = t.lvl_off[d], b1 = t.lvl_off[d + 1];
+      for (uint32_t k = b0 + tid; k < b1 + na; k += nthr) {
+        uint32_t v;
+        if (k < b1) {
+          v = t.ord[k];
+          if (aff_ix(L, v) != kInf) continue;  // affected: at its masked level
+        } else {
+          const uint32_t q = k - b1;
+          if (((const volatile uint32_t*)L.dp)[q] != d) continue;
+          v = ((const volatile uint32_t*)L.aff)[q];
+        }
+        if ((g.nt_bits[v >> 5] >> (v & 31u)) & 1u) continue;  // never a predecessor
+        const uint32_t beg = g.row_ptr[v], end = g.row_ptr[v + 1];
+        if (end - beg > 256u) {  // a spine's row: one wave below
+          const uint32_t j = atomicAdd(&H.nbig, 1u);
+          if (j < kGoodBig) big[j] = v;
+          else set_good(v);  // (no room: kept, i.e. not pruned)
+          continue;
+        }
+        for (uint32_t e = beg; e < end; ++e)
+          if (link_ok(v, d, e)) {
+            set_good(v);
+            break;
+          }
+      }
+      __syncthreads();
+      const uint32_t nb = min(((volatile uint32_t&)H.nbig), kGoodBig);
+      for (uint32_t j = wv; j < nb; j += nw) {
+        const uint32_t v = big[j];
+        const uint32_t beg = g.row_ptr[v], end = g.row_ptr[v + 1];
+        for (uint32_t e0 = beg; e0 < end; e0 += kWave) {
+          const uint32_t e = e0 + lane;
+          if (__ballot(e < end && link_ok(v, d, e))) {
+            if (lane == 0) set_good(v);
+            break;
+          }
+        }
+      }
+      __syncthreads();
+    }
+    for (uint32_t w = tid; w < words; w += nthr) {
+      const uint32_t x = ~__hip_atomic_load(&gb[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (x) __hip_atomic_fetch_or(&tr.dead[w], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __syncthreads();
+  }
+};
+
+__global__ void __launch_bounds__(256) lvl_hist_kernel(const uint32_t* __restrict__ D, uint32_t V,
+                                                       uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t h[256];
+  h[threadIdx.x] = 0u;
+  __syncthreads();
+  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v < V && D[v] < 256u) atomicAdd(&h[D[v]], 1u);
+  __syncthreads();
+  if (h[threadIdx.x]) atomicAdd(&cnt[threadIdx.x], h[threadIdx.x]);
+}
+// one block: off[d] = sum of cnt[< d]; cnt becomes the scatter cursor
+__global__ void __launch_bounds__(256) lvl_scan_kernel(uint32_t* cnt, uint32_t* off) {
+  if (threadIdx.x == 0) {
+    uint32_t a = 0;
+    for (uint32_t d = 0; d < 256u; ++d) {
+      off[d] = a;
+      const uint32_t c = cnt[d];
+      cnt[d] = a;
+      a += c;
+    }
+    off[256] = a;
+  }
+}
+__global__ void __launch_bounds__(256) lvl_scatter_kernel(const uint32_t* __restrict__ D, uint32_t V,
+                                                          uint32_t* __restrict__ cur,
+                                                          uint32_t* __restrict__ ord) {
+  __shared__ uint32_t h[256], base[256];
+  h[threadIdx.x] = 0u;
+  __syncthreads();
+  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t d = v < V ? D[v] : kInf;
+  uint32_t r = 0;
+  if (d < 256u) r = atomicAdd(&h[d], 1u);
+  __syncthreads();
+  if (h[threadIdx.x]) base[threadIdx.x] = atomicAdd(&cur[threadIdx.x], h[threadIdx.x]);
+  __syncthreads();
+  if (d < 256u) ord[base[d] + r] = v;
 }
 
 // Heavy decremental runs: the block's first wave recomputes the run's
@@ -944,6 +1171,7 @@ __global__ void __launch_bounds__(1024) ksp_decr_heavy_kernel(DevGraph g, TraceA
     __syncthreads();
     if (i == kInf) return;
     uint32_t nign = 0, na = 0;
+    const uint64_t c0 = wall_clock64();
     if (wv == 0) {
       const bool ok = decr_prepare(L, g, t, i, lane, nign, na);
       if (lane == 0) {
@@ -958,10 +1186,30 @@ __global__ void __launch_bounds__(1024) ksp_decr_heavy_kernel(DevGraph g, TraceA
       if (threadIdx.x == 0) t.status[i] |= OSPF_KSP_OVF2;
       continue;
     }
+    const uint64_t c1 = wall_clock64();
     Tracer<DistDecr<DecrHeavy>, kHash> tr{g, t, i, lane, t.src, t.dsts[i], L.ign, nign, L.hash, dead,
                                           DistDecr<DecrHeavy>{t.rows, &L}};
-    heavy_trace(g, t, i, tr, L.hash, H);
+    if (t.good) {
+      const GoodPrune pr{g, t, tr, L, H, t.good + (size_t)blockIdx.x * t.dead_words,
+                         t.big + (size_t)blockIdx.x * kGoodBig};
+      heavy_trace(g, t, i, tr, L.hash, H, pr);
+    } else {
+      heavy_trace(g, t, i, tr, L.hash, H);
+    }
+    if (threadIdx.x == 0) {  // [20] prepare, [21] trace of the heavy runs
+      uint64_t* clk = reinterpret_cast<uint64_t*>(t.ctr + 16);
+      atomicAdd((unsigned long long*)&clk[4], (unsigned long long)(c1 - c0));
+      atomicAdd((unsigned long long*)&clk[5], (unsigned long long)(wall_clock64() - c1));
+    }
   }
+}
+
+__global__ void ksp_presplit_kernel(TraceArgs t, uint32_t* list, uint32_t* count) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= t.n) return;
+  const uint32_t st = t.status[i];
+  if ((st & OSPF_KSP_RERUN) && !(st & OSPF_KSP_OVF1) && t.ign_cnt[i] > DecrSmall::kIgn)
+    list[atomicAdd(count, 1u)] = i;
 }
 
 __global__ void rows_gather_kernel(uint32_t* a, const uint32_t* b, const uint32_t* idx, uint32_t n,
@@ -1011,12 +1259,29 @@ hipError_t launch_ksp_trace(bool lev, const DevGraph& g, const TraceArgs& t, hip
 
 hipError_t launch_ksp_hint(const DevGraph& g, uint32_t src, const uint32_t* dist, uint32_t* hint,
                            hipStream_t s) {
-  hipLaunchKernelGGL(ksp_hint_kernel, dim3((g.V + 255) / 256), dim3(256), 0, s, g, src, dist, hint);
+  hipLaunchKernelGGL(ksp_hint_kernel, dim3((g.V + 3) / 4), dim3(256), 0, s, g, src, dist, hint);
   return hipGetLastError();
 }
 
 uint32_t ksp_decr_blocks_per_cu() {
   return std::min<uint32_t>(16u, (160u * 1024u) / (uint32_t)sizeof(DecrSmall));
+}
+
+hipError_t launch_ksp_levels(const uint32_t* dist, uint32_t V, uint32_t* ord, uint32_t* off,
+                             uint32_t* cnt, hipStream_t s) {
+  const hipError_t e = launch_fill32(cnt, 257, 0u, s);
+  if (e != hipSuccess) return e;
+  const dim3 grid((V + 255) / 256);
+  hipLaunchKernelGGL(lvl_hist_kernel, grid, dim3(256), 0, s, dist, V, cnt);
+  hipLaunchKernelGGL(lvl_scan_kernel, dim3(1), dim3(256), 0, s, cnt, off);
+  hipLaunchKernelGGL(lvl_scatter_kernel, grid, dim3(256), 0, s, dist, V, cnt, ord);
+  return hipGetLastError();
+}
+
+hipError_t launch_ksp_presplit(const TraceArgs& t, uint32_t* list, uint32_t* count, hipStream_t s) {
+  if (t.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(ksp_presplit_kernel, dim3((t.n + 255) / 256), dim3(256), 0, s, t, list, count);
+  return hipGetLastError();
 }
 
 hipError_t launch_ksp_decr(const DevGraph& g, const TraceArgs& t, uint32_t blocks, hipStream_t s) {

@@ -2656,11 +2656,50 @@ int ospf_sweep_poison(ospf_sweep* s, void* stream) {
   if (!s) return OSPF_E_INVAL;
   SCHK(s, hipSetDevice(s->c->device));
   // a kernel, not hipMemsetAsync: see ospf::zero_async
-  SCHK(s, ospf::launch_fill32((uint32_t*)s->dig_all, (size_t)std::max(1u, s->n_dig) * 6u,
-                              0xFFFFFFFFu, (hipStream_t)stream));
-  for (auto& a : s->dig_aux)
-    SCHK(s, ospf::launch_fill32((uint32_t*)a.first, std::max<size_t>(1, a.second) * 6u, 0xFFFFFFFFu,
-                                (hipStream_t)stream));
+  auto fill = [&](void* p, size_t words) {
+    return ospf::zero_by_memset() ? hipMemsetAsync(p, 0xFF, words * 4u, (hipStream_t)stream)
+                                  : ospf::launch_fill32((uint32_t*)p, words, 0xFFFFFFFFu,
+                                                        (hipStream_t)stream);
+  };
+  SCHK(s, fill(s->dig_all, (size_t)std::max(1u, s->n_dig) * 6u));
+  for (auto& a : s->dig_aux) SCHK(s, fill(a.first, std::max<size_t>(1, a.second) * 6u));
+  return OSPF_OK;
+}
+
+int ospf_sweep_graph_memsets(const ospf_sweep* s, uint32_t* n_memset, uint32_t* n_dead,
+                             uint32_t* n_own) {
+  if (!s || !n_memset || !n_dead || !n_own) return OSPF_E_INVAL;
+  *n_memset = *n_dead = *n_own = 0;
+  if (!s->graph) return OSPF_OK;
+  size_t nn = 0;
+  if (hipGraphGetNodes(s->graph, nullptr, &nn) != hipSuccess) return OSPF_E_DEVICE;
+  std::vector<hipGraphNode_t> nodes(nn);
+  if (nn && hipGraphGetNodes(s->graph, nodes.data(), &nn) != hipSuccess) return OSPF_E_DEVICE;
+  for (hipGraphNode_t g : nodes) {
+    hipGraphNodeType ty;
+    if (hipGraphNodeGetType(g, &ty) != hipSuccess) return OSPF_E_DEVICE;
+    if (ty != hipGraphNodeTypeMemset) continue;
+    hipMemsetParams p{};
+    if (hipGraphMemsetNodeGetParams(g, &p) != hipSuccess) return OSPF_E_DEVICE;
+    ++*n_memset;
+    const char* dst = static_cast<const char*>(p.dst);
+    const size_t bytes = (size_t)p.elementSize * p.width * std::max<size_t>(1, p.height);
+    // live allocation around [dst, dst + bytes)?
+    hipDeviceptr_t base = nullptr;
+    size_t sz = 0;
+    if (hipMemGetAddressRange(&base, &sz, (hipDeviceptr_t)dst) != hipSuccess ||
+        dst + bytes > static_cast<const char*>(base) + sz) {
+      ++*n_dead;
+      (void)hipGetLastError();
+    }
+    for (size_t i = 0; i < s->allocs.size() && i < s->alloc_bytes.size(); ++i) {
+      const char* a = static_cast<const char*>(s->allocs[i]);
+      if (dst >= a && dst + bytes <= a + s->alloc_bytes[i]) {
+        ++*n_own;
+        break;
+      }
+    }
+  }
   return OSPF_OK;
 }
 

@@ -385,6 +385,14 @@ class Sweep:
                      ms_median=float(a.ms_median), ms_min=float(a.ms_min))
                 for a in arr[: self.n_launches]]
 
+    def graph_memsets(self):
+        """Diagnostic: the captured graph's memset nodes -> (count, with a
+        destination outside every live allocation, inside the sweep's own
+        blocks); see ospf_sweep_graph_memsets."""
+        a, b, c = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        self._check(self._L.ospf_sweep_graph_memsets(self._h, C.byref(a), C.byref(b), C.byref(c)))
+        return int(a.value), int(b.value), int(c.value)
+
 
 class Multi:
     """Several devices behind one handle (ospf_multi_*): the graph replicated,

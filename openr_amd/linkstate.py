@@ -391,6 +391,14 @@ class LinkState:
         """nodes added / removed in place (odl_node_patches)"""
         return int(self._L.odl_node_patches(self._h))
 
+    def shard_stats(self) -> Dict[str, int]:
+        """multi-device LinkState: root batches / KSP2 prefetches split across
+        the device slots and their per-slot launches (odl_shard_stats)"""
+        out = (C.c_uint64 * 4)()
+        self._L.odl_shard_stats(self._h, out)
+        return {"spf_batches": int(out[0]), "spf_launches": int(out[1]),
+                "ksp2_runs": int(out[2]), "ksp2_launches": int(out[3])}
+
     def topology_stats(self) -> Dict[str, int]:
         """{snapshots, loads, link_patches, rows_patched}: links added /
         removed between known nodes patch the CSR and the device graph in

@@ -39,6 +39,10 @@ def one(topo, mode, hip_graph, reps, part_of):
         sw._check(sw._L.ospf_sweep_digests_host(sw._h, d.ctypes.data))
         return d[: sw.n_roots].copy()
     first = digs()
+    if hip_graph:
+        nm, nd, no = sw.graph_memsets()
+        print(f"captured memset nodes {nm}: dst outside every live allocation {nd}, "
+              f"inside the sweep's own blocks {no}", flush=True)
     s = torch.cuda.current_stream()
     if not os.environ.get("RP_NOPOISON"):
         sw.poison(s.cuda_stream)
@@ -81,7 +85,8 @@ def main():
         return
     envs = {"base": ({}, 1), "graphoff": ({}, 0), "seednonh": ({"OSPF_SEED_NONH": "1"}, 1),
             "closurenonh": ({"OSPF_CLOSURE_NONH": "1"}, 1),
-            "zerok": ({"OSPF_ZERO_KERNEL": "1"}, 1), "nopoison": ({"RP_NOPOISON": "1"}, 1)}
+            "zerok": ({"OSPF_ZERO_KERNEL": "1"}, 1),
+            "memset": ({"OSPF_ZERO_MEMSET": "1"}, 1), "memsetoff": ({"OSPF_ZERO_MEMSET": "1"}, 0), "nopoison": ({"RP_NOPOISON": "1"}, 1)}
     for v in a.variants.split(","):
         e, g = envs[v]
         env = dict(os.environ, **e)

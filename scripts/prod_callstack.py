@@ -56,6 +56,10 @@ class Stderr:
         self.text = self.f.read()
         self.f.close()
 
+    def laps(self):
+        """OSPF_SWEEP_TIMING's ospf_sweep_create phases -> {phase: ms}"""
+        return {k: float(v) for k, v in re.findall(r"sweep_create (.+?) ([0-9.]+) ms", self.text)}
+
     def values(self, key):
         return [float(x) for x in re.findall(key + r"=([0-9.]+)", self.text)]
 
@@ -127,8 +131,9 @@ def main():
         # its adjacency to its pod's first fabric switch, then restores it;
         # each: apply, getSpfResult(me), and a whole all-sources re-sweep
         db = [d for d in st.to_dbs() if d.name == "3-901-0"][0]
-        _, wall, _ = timed(lambda: p.prefetch_all())
+        _, wall, cap = timed(lambda: p.prefetch_all())
         out[f"{tag}_all_sources_sweep_before_link_events_ms"] = round(wall, 3)
+        out[f"{tag}_all_sources_sweep_before_link_events_create"] = cap.laps()
         t0 = p.topology_stats()
         adj = db.adjs.pop(0)
         for kind in ("link_down", "link_up"):
@@ -140,8 +145,9 @@ def main():
             _, wall, cap = timed(lambda: p.prefetch([args.me]))
             out[f"{tag}_{kind}_getSpfResult_ms"] = round(wall, 3)
             out[f"{tag}_{kind}_engine_ms"] = sum(cap.values("engine_ms"))
-            _, wall, _ = timed(lambda: p.prefetch_all())
+            _, wall, cap = timed(lambda: p.prefetch_all())
             out[f"{tag}_{kind}_all_sources_sweep_ms"] = round(wall, 3)
+            out[f"{tag}_{kind}_all_sources_sweep_create"] = cap.laps()
             print(f"{tag} {kind}: apply {out[f'{tag}_{kind}_apply_ms']} ms, getSpfResult "
                   f"{out[f'{tag}_{kind}_getSpfResult_ms']} ms, sweep "
                   f"{out[f'{tag}_{kind}_all_sources_sweep_ms']} ms", file=sys.stderr, flush=True)
@@ -158,8 +164,9 @@ def main():
             out[f"{tag}_{kind}_apply_ms"] = round(wall, 3)
             _, wall, cap = timed(lambda: p.prefetch([args.me]))
             out[f"{tag}_{kind}_getSpfResult_ms"] = round(wall, 3)
-            _, wall, _ = timed(lambda: p.prefetch_all())
+            _, wall, cap = timed(lambda: p.prefetch_all())
             out[f"{tag}_{kind}_all_sources_sweep_ms"] = round(wall, 3)
+            out[f"{tag}_{kind}_all_sources_sweep_create"] = cap.laps()
             print(f"{tag} {kind}: apply {out[f'{tag}_{kind}_apply_ms']} ms, getSpfResult "
                   f"{out[f'{tag}_{kind}_getSpfResult_ms']} ms, sweep "
                   f"{out[f'{tag}_{kind}_all_sources_sweep_ms']} ms", file=sys.stderr, flush=True)
