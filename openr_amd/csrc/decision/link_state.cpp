@@ -1454,11 +1454,15 @@ void LinkState::applyIncremental(const std::vector<LinkDelta>& links,
     }
     return false;
   };
+  // the dropped results go to the reaper thread, as clearMemo's do (a
+  // route build's result holds ~100k materialised entries at F100k)
+  auto dead = std::make_unique<MemoReaper::Dead>();
   for (int mode = 0; mode < 2; ++mode) {
     auto& memo = mode == 0 ? memoMetric_ : memoHops_;
+    auto& to = mode == 0 ? dead->a : dead->b;
     for (auto it = memo.begin(); it != memo.end();) {
       if (affected(it->first, it->second, mode == 1)) {
-        it = memo.erase(it);
+        to.insert(memo.extract(it++));
         ++incStats_.dropped;
       } else {
         ++it;
@@ -1466,7 +1470,14 @@ void LinkState::applyIncremental(const std::vector<LinkDelta>& links,
       }
     }
   }
-  memoKsp_.clear();  // KSP2 masked reruns are not tracked
+  dead->k.swap(memoKsp_);  // KSP2 masked reruns are not tracked
+  if (!reaper_) {
+    try {
+      reaper_ = std::make_unique<MemoReaper>();
+    } catch (const std::system_error&) {  // no thread to spare: freed here
+    }
+  }
+  if (reaper_) reaper_->push(std::move(dead));
   patchGraph(links, nodes);
 }
 

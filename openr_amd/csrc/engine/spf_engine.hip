@@ -723,7 +723,8 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
     const bool prune = t_k1.budget && !getenv("OSPF_KSP_NOPRUNE");
     const size_t sz_ord = prune ? align_up(V * 4ull, 256) + align_up(2 * 257 * 4ull, 256) : 0,
                  sz_good = prune ? dwb * hblk + (size_t)hblk * ospf::kGoodBig * 4ull : 0;
-    char* dp = stream_scratch(c, s, sz_tc + 3 * sz_fb + sz_ctr + sz_dd + sz_ord + sz_good, &rc, 2);
+    const size_t sz_pb = align_up((n + 31) / 32 * 4ull, 256);
+    char* dp = stream_scratch(c, s, sz_tc + 3 * sz_fb + sz_ctr + sz_dd + sz_ord + sz_good + sz_pb, &rc, 2);
     if (rc) return rc;
     uint32_t* d_tc = (uint32_t*)dp;
     uint32_t* d_fb = (uint32_t*)(dp + sz_tc);
@@ -769,12 +770,15 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
     uint32_t npre = 0;
     const bool split = getenv("OSPF_KSP_NOSPLIT") == nullptr;
     if (split) {
-      e = ospf::launch_ksp_presplit(td, d_pre, d_ctr + 12, s);
+      td.src_cut = 16;  // (OSPF_KSP_SRCCUT: A/B knob, 0 = off)
+      if (const char* x = getenv("OSPF_KSP_SRCCUT")) td.src_cut = (uint32_t)std::max(0, atoi(x));
+      td.pre_bits = (uint32_t*)(dp + sz_tc + 3 * sz_fb + sz_ctr + sz_dd + sz_ord + sz_good);
+      HIPCHK(c, ospf::zero_async(td.pre_bits, (n + 31) / 32 * 4ull, s));
+      e = ospf::launch_ksp_presplit(c->g, td, d_pre, d_ctr + 12, s);
       if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_presplit");
       HIPCHK(c, hipMemcpyAsync(&npre, d_ctr + 12, 4, hipMemcpyDeviceToHost, s));
       HIPCHK(c, hipStreamSynchronize(s));
     }
-    td.skip_ign = split ? 1u : 0u;
     hipStream_t ks = s;
     if (npre) {
       if (!c->ksp_aux) HIPCHK(c, hipStreamCreateWithFlags(&c->ksp_aux, hipStreamNonBlocking));

@@ -634,7 +634,8 @@ struct TraceArgs {
   uint32_t dead_words;      // (V + 31) / 32
   uint32_t budget;          // DFS steps before a run goes to the heavy kernel (0 = none)
   uint32_t look;            // lookahead: predecessors with rows <= look entries are probed
-  uint32_t skip_ign;        // ksp_decr: skip runs the presplit sent to the full reruns
+  uint32_t src_cut;         // presplit: runs ignoring more of the source's links (0: off)
+  uint32_t* pre_bits;       // [n / 32] runs the presplit sent to the full reruns (ksp_decr skips them)
   uint32_t* heavy;          // [n] queued run indices
   uint32_t* heavy_ctr;      // [2] {queued, taken}, zeroed by the caller
   // decremental reruns (launch_ksp_decr): rows = the source's dist row
@@ -670,7 +671,8 @@ hipError_t launch_ksp_decr(const DevGraph& g, const TraceArgs& t, uint32_t block
 uint32_t ksp_decr_blocks_per_cu();
 // runs past the decremental kernel's ignore-list budget (the ones it would
 // send to the full reruns at once): their indices into list, *count of them
-hipError_t launch_ksp_presplit(const TraceArgs& t, uint32_t* list, uint32_t* count, hipStream_t s);
+hipError_t launch_ksp_presplit(const DevGraph& g, const TraceArgs& t, uint32_t* list, uint32_t* count,
+                               hipStream_t s);
 // the runs ksp_decr queued as heavy (t.heavy / t.heavy_ctr): 16 waves each;
 // t.dead: [blocks][dead_words]; t.err: the engine's error word
 hipError_t launch_ksp_decr_heavy(const DevGraph& g, const TraceArgs& t, uint32_t blocks,

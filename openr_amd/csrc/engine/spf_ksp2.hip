@@ -375,19 +375,22 @@ __device__ bool trace_setup(const DevGraph& g, const TraceArgs& t, uint32_t i, u
 // one wave per run; a run that spends more than t.budget DFS steps (unit
 // metric) without finding a path -- a long failing search -- is queued for
 // ksp_heavy_kernel, which resumes it with 16 waves
-template <bool LEV>
+// HS: claim-hash slots per wave. With the 16-wave kernel behind it (unit
+// metric) a 1,024-slot hash (20 KB per block: 7 blocks per CU, VGPR-bound)
+// and runs past its claims go there; otherwise kHash slots.
+template <bool LEV, uint32_t HS>
 __global__ void __launch_bounds__(256) ksp_trace_kernel(DevGraph g, TraceArgs t) {
   __shared__ uint32_t s_stack[kWaves][kStack];
-  __shared__ uint32_t s_hash[kWaves][kHash];
+  __shared__ uint32_t s_hash[kWaves][HS];
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint32_t i = blockIdx.x * kWaves + wv;
   if (i >= t.n) return;
   volatile uint32_t* stk = s_stack[wv];
-  Tracer<decltype(dist_src<LEV>(g, t, i))> tr{g, t, i, lane, t.src, t.dsts[i], nullptr, 0,
-                                              s_hash[wv], t.dead + (size_t)i * t.dead_words,
-                                              dist_src<LEV>(g, t, i)};
+  Tracer<decltype(dist_src<LEV>(g, t, i)), HS> tr{g, t, i, lane, t.src, t.dsts[i], nullptr, 0,
+                                                  s_hash[wv], t.dead + (size_t)i * t.dead_words,
+                                                  dist_src<LEV>(g, t, i)};
   if (!trace_setup(g, t, i, lane, tr)) return;
-  for (uint32_t k = lane; k < kHash; k += kWave) tr.hs[k] = 0u;
+  for (uint32_t k = lane; k < HS; k += kWave) tr.hs[k] = 0u;
   uint32_t* out = t.out + (size_t)i * t.stride;
   uint32_t npaths = 0, w = 1, steps = 0, nclaim = 0;
   bool ovf = false;
@@ -397,7 +400,10 @@ __global__ void __launch_bounds__(256) ksp_trace_kernel(DevGraph g, TraceArgs t)
     uint32_t depth = 0;
     const int r = tr.dfs(stk, depth, 0, steps, budget);
     if (r == 0) break;
-    if (r == -1 && t.budget) {  // heavy: the paths so far stay in the record
+    // heavy: a long failing search, or more claimed links than this hash
+    // holds; the paths so far stay in the record
+    if ((r == -1 && t.budget) ||
+        (r == 1 && t.budget && HS < kHash && nclaim + depth > tr.kHM && w + 1u + depth <= t.stride)) {
       if (lane == 0) t.heavy[atomicAdd(&t.heavy_ctr[0], 1u)] = i;
       return;
     }
@@ -601,7 +607,7 @@ struct DecrLdsT {
   uint32_t nkeys, naff, ovf, run, npend;
   uint64_t t3;         // wall clock at step (3) (phase timing, t.ctr[16..])
 };
-using DecrSmall = DecrLdsT<512, 192, 256, 512, 8192>;  // ~10 KB: ~16 runs per CU in flight
+using DecrSmall = DecrLdsT<512, 192, 256, 512, 4096>;  // ~10 KB: ~16 runs per CU in flight
 using DecrHeavy = DecrLdsT<4096, 1024, 1024, kHash, 1u << 30>;
 
 template <class L_>
@@ -946,7 +952,7 @@ __global__ void __launch_bounds__(64) ksp_decr_kernel(DevGraph g, TraceArgs t) {
       if (lane == 0) out[0] = 0u;
       continue;
     }
-    if (t.skip_ign && t.ign_cnt[i] > DecrSmall::kIgn) continue;  // presplit: the full reruns'
+    if (t.pre_bits && ((t.pre_bits[i >> 5] >> (i & 31u)) & 1u)) continue;  // presplit: the full reruns'
     auto fallback = [&]() {
       if (lane == 0) t.fb[atomicAdd(&t.ctr[1], 1u)] = i;
     };
@@ -1204,12 +1210,34 @@ __global__ void __launch_bounds__(1024) ksp_decr_heavy_kernel(DevGraph g, TraceA
   }
 }
 
-__global__ void ksp_presplit_kernel(TraceArgs t, uint32_t* list, uint32_t* count) {
+// Runs for the full reruns from the start: ignore lists past the
+// decremental kernel's, and ignore sets holding more than t.src_cut of the
+// source's own links (a destination whose k = 1 paths leave through most of
+// the source's links -- F100k: a plane-0 fabric switch from 2-0-0 -- cuts
+// whole planes off: its affected set is the plane, past every budget)
+__global__ void ksp_presplit_kernel(DevGraph g, TraceArgs t, uint32_t* list, uint32_t* count) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= t.n) return;
   const uint32_t st = t.status[i];
-  if ((st & OSPF_KSP_RERUN) && !(st & OSPF_KSP_OVF1) && t.ign_cnt[i] > DecrSmall::kIgn)
+  if (!(st & OSPF_KSP_RERUN) || (st & OSPF_KSP_OVF1)) return;
+  const uint32_t nign = t.ign_cnt[i];
+  bool split = nign > DecrSmall::kIgn;
+  if (!split && t.src_cut) {
+    const uint32_t* ign = t.ign + (size_t)i * t.stride;
+    uint32_t at_src = 0;
+    for (uint32_t k = 0; k < nign && at_src <= t.src_cut; ++k) {
+      const uint32_t l = ign[k];
+      if (l >= g.n_lid) continue;
+      const uint32_t e0 = g.link_e[2u * l], e1 = g.link_e[2u * l + 1u];
+      if (e0 == kInf || e1 == kInf) continue;
+      if ((g.colx[e0] & ~kDown) == t.src || (g.colx[e1] & ~kDown) == t.src) ++at_src;
+    }
+    split = at_src > t.src_cut;
+  }
+  if (split) {
     list[atomicAdd(count, 1u)] = i;
+    atomicOr(&t.pre_bits[i >> 5], 1u << (i & 31u));
+  }
 }
 
 __global__ void rows_gather_kernel(uint32_t* a, const uint32_t* b, const uint32_t* idx, uint32_t n,
@@ -1242,10 +1270,17 @@ hipError_t launch_or_bits(uint32_t* st, uint32_t n, uint32_t bits, hipStream_t s
 hipError_t launch_ksp_trace(bool lev, const DevGraph& g, const TraceArgs& t, hipStream_t s) {
   if (t.n == 0) return hipSuccess;
   const dim3 grid((t.n + kWaves - 1) / kWaves);
-  if (lev)
-    hipLaunchKernelGGL(ksp_trace_kernel<true>, grid, dim3(kBlock), 0, s, g, t);
+  // the small hash when the 16-wave kernel takes the overflow and a k = 1
+  // record's sort (finish: stride words of the hash) fits
+  const bool small = t.budget && t.stride <= 1024u;
+  if (lev && small)
+    hipLaunchKernelGGL((ksp_trace_kernel<true, 1024>), grid, dim3(kBlock), 0, s, g, t);
+  else if (lev)
+    hipLaunchKernelGGL((ksp_trace_kernel<true, kHash>), grid, dim3(kBlock), 0, s, g, t);
+  else if (small)
+    hipLaunchKernelGGL((ksp_trace_kernel<false, 1024>), grid, dim3(kBlock), 0, s, g, t);
   else
-    hipLaunchKernelGGL(ksp_trace_kernel<false>, grid, dim3(kBlock), 0, s, g, t);
+    hipLaunchKernelGGL((ksp_trace_kernel<false, kHash>), grid, dim3(kBlock), 0, s, g, t);
   if (t.budget) {  // heavy runs queued by the pass above (counters zeroed by the caller)
     const dim3 hg(std::min<uint32_t>(512u, t.n));  // 2 per CU
     if (lev)
@@ -1278,9 +1313,10 @@ hipError_t launch_ksp_levels(const uint32_t* dist, uint32_t V, uint32_t* ord, ui
   return hipGetLastError();
 }
 
-hipError_t launch_ksp_presplit(const TraceArgs& t, uint32_t* list, uint32_t* count, hipStream_t s) {
+hipError_t launch_ksp_presplit(const DevGraph& g, const TraceArgs& t, uint32_t* list, uint32_t* count,
+                               hipStream_t s) {
   if (t.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(ksp_presplit_kernel, dim3((t.n + 255) / 256), dim3(256), 0, s, t, list, count);
+  hipLaunchKernelGGL(ksp_presplit_kernel, dim3((t.n + 255) / 256), dim3(256), 0, s, g, t, list, count);
   return hipGetLastError();
 }
 

@@ -61,7 +61,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-lfa", action="store_true", help="KSP2 launches only (PMC passes)")
     ap.add_argument("--iso-reps", type=int, default=3)
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r04", "ksp2_pmc.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r05", "ksp2_pmc.json"),
                     help="measured HBM bytes per KSP2 launch (scripts/pmc_sum.py)")
     args = ap.parse_args()
 
@@ -162,7 +162,15 @@ def main():
             b_.synchronize()
             ms.append(a_.elapsed_time(b_))
         return float(np.median(ms[1:]))
+    st0 = eng.ksp2_stats()
     ksp_ms = timed(ksp)
+    st1 = eng.ksp2_stats()
+    # per launch: k = 2 runs by the decremental kernel / sent to the full
+    # masked reruns (64 per multi-source traversal)
+    launches = args.iso_reps + 1
+    decr_runs = (st1["decremental"] - st0["decremental"]) // launches
+    full_runs = (st1["full_reruns"] - st0["full_reruns"]) // launches
+    affected = (st1["affected"] - st0["affected"]) // launches
     lfa_ms = timed(lfa_runs) if lfa_bufs else 0.0
     status = st.cpu().numpy().view(np.uint32)
     reruns = int(np.count_nonzero(status & N.OSPF_KSP_RERUN))
@@ -231,9 +239,11 @@ def main():
                          f"trace, the masked runSpf and the k = 2 trace), {threads} threads, "
                          f"{ct:.2f}s"}
     # compulsory bytes of this rank's KSP2 launch: one neighbour-id + offset
-    # scan for the source's SPF and one per 64 masked reruns (they run 64 per
-    # multi-source traversal), plus the path-record words actually written
-    # (count, then length + link ids per path, for k = 1 and k = 2)
+    # scan for the source's SPF and one per 64 full masked reruns (they run
+    # 64 per multi-source traversal), plus the path-record words actually
+    # written (count, then length + link ids per path, for k = 1 and k = 2);
+    # a decremental rerun's own reads (its affected nodes' rows) are not
+    # counted
     k1h = k1.cpu().numpy().view(np.uint32)
     k2h = k2.cpu().numpy().view(np.uint32)
 
@@ -249,7 +259,7 @@ def main():
     words = sum(rec_words(k1h[i]) + rec_words(k2h[i]) for i in range(n))
     scan = 4 * E + 4 * (V + 1)
     reruns_mine = int(np.count_nonzero(status & N.OSPF_KSP_RERUN))
-    comp = (1 + -(-reruns_mine // 64)) * scan + 4 * words
+    comp = (1 + -(-full_runs // 64)) * scan + 4 * words
     traffic = None
     if os.path.exists(args.pmc_json):
         try:
@@ -286,9 +296,12 @@ def main():
                                    "trace)", "compulsory_bytes": int(comp),
                          "avg_launch_ms": round(ksp_ms, 3), "destinations_per_launch": n,
                          "masked_reruns": reruns_mine, "alg_equiv_GBs": round(alg, 1),
+                         "reruns_decremental": decr_runs, "reruns_full": full_runs,
+                         "affected_nodes": affected,
                          "note": "achieved = compulsory bytes of rank 0's KSP2 launch (one "
                                  "neighbour-id + offset scan for the source SPF and per 64 "
-                                 "masked reruns, plus the path-record words written) / its "
+                                 "full masked reruns, plus the path-record words written; "
+                                 "decremental reruns' own reads not counted) / its "
                                  "isolated time (HIP events on its stream); alg_equiv_GBs = "
                                  "the SURVEY 8(d) per-run model (destinations x (8E + 8V + 4)), "
                                  "which the shared traversals beat: not a roofline fraction"},
