@@ -54,6 +54,7 @@ constexpr uint32_t kWaves = kBlock / kWave;
 constexpr uint32_t kStack = 256;      // links per path
 constexpr uint32_t kHash = 2048;      // visited-set slots (power of 2)
 constexpr uint32_t kSteps = 1u << 22; // DFS steps per run (termination guard)
+constexpr uint32_t kIgLog = 13, kIgBits = 1u << kIgLog;  // ignore-list filter bits per wave
 
 __device__ __forceinline__ bool in_sorted(const uint32_t* a, uint32_t n, uint32_t x) {
   uint32_t lo = 0, hi = n;
@@ -109,6 +110,32 @@ struct Tracer {
   volatile uint32_t* hs;  // claimed links (the paths found), kHash slots
   uint32_t* dead;
   DS ds;
+  // LDS filter of the ignore list when it lives in global memory (kIgBits
+  // bits: a clear bit answers "not ignored" without the list's binary search)
+  uint32_t* igb = nullptr;
+
+  __device__ bool ignored(uint32_t lid) const {
+    if (!nign) return false;
+    if (igb) {
+      const uint32_t h = igbit(lid);
+      if (!((((volatile uint32_t*)igb)[h >> 5] >> (h & 31u)) & 1u)) return false;
+    }
+    return in_sorted(ign, nign, lid);
+  }
+  __device__ static uint32_t igbit(uint32_t lid) { return (lid * 0x9E3779B1u) >> (32 - kIgLog); }
+  // the filter of the current ignore list (every lane of the wave)
+  __device__ void build_igb() const {
+    if (!igb) return;
+    for (uint32_t k = lane; k < kIgBits / 32u; k += kWave) igb[k] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t k = lane; k < nign; k += kWave) {
+      const uint32_t h = igbit(ign[k]);
+      atomicOr(&igb[h >> 5], 1u << (h & 31u));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+  }
 
   __device__ uint32_t dist(uint32_t u) const { return ds(u); }
   __device__ static uint32_t hslot(uint32_t lid) {
@@ -153,7 +180,7 @@ struct Tracer {
     if ((uint64_t)du + w != dv) return false;
     if (cx != src && ((g.nt_bits[cx >> 5] >> (cx & 31u)) & 1u)) return false;
     const uint32_t lid = g.link_id[e];
-    if (nign && in_sorted(ign, nign, lid)) return false;
+    if (ignored(lid)) return false;
     if (cx == src) return !claimed(lid);
     return !is_dead(cx) && !claimed(lid);
   }
@@ -171,7 +198,7 @@ struct Tracer {
       if (d2 == kInf || (uint64_t)d2 + (t.unit ? 1u : g.rw[e2]) != du) continue;
       if (c2 != src && ((g.nt_bits[c2 >> 5] >> (c2 & 31u)) & 1u)) continue;
       const uint32_t l2 = g.link_id[e2];
-      if (nign && in_sorted(ign, nign, l2)) continue;
+      if (ignored(l2)) continue;
       if (c2 != src && is_dead(c2)) continue;
       if (!claimed(l2)) ok = true;
     }
@@ -197,7 +224,7 @@ struct Tracer {
       if (d2 == kInf || (uint64_t)d2 + (t.unit ? 1u : g.rw[e2]) != du) continue;
       if (c2 != src && ((g.nt_bits[c2 >> 5] >> (c2 & 31u)) & 1u)) continue;
       const uint32_t l2 = g.link_id[e2];
-      if (nign && in_sorted(ign, nign, l2)) continue;
+      if (ignored(l2)) continue;
       if (c2 != src && is_dead(c2)) continue;
       if (!claimed(l2)) return true;
     }
@@ -255,7 +282,7 @@ struct Tracer {
       const uint32_t w = t.unit ? 1u : g.w[e];
       if (dist(cx) != w) continue;
       const uint32_t lid = g.link_id[e];
-      if (nign && in_sorted(ign, nign, lid)) continue;
+      if (ignored(lid)) continue;
       if (!claimed(lid)) any = true;
     }
     return __ballot(any) != 0ull;
@@ -357,6 +384,7 @@ __device__ bool trace_setup(const DevGraph& g, const TraceArgs& t, uint32_t i, u
     }
     tr.ign = t.ign + (size_t)i * t.stride;
     tr.nign = min(t.ign_cnt[i], t.stride);
+    tr.build_igb();
   }
   if (tr.dst == tr.src || tr.dist(tr.dst) == kInf) {  // LinkState.cpp:808-809: no paths
     if (lane == 0) out[0] = 0u;
@@ -382,13 +410,14 @@ template <bool LEV, uint32_t HS>
 __global__ void __launch_bounds__(256) ksp_trace_kernel(DevGraph g, TraceArgs t) {
   __shared__ uint32_t s_stack[kWaves][kStack];
   __shared__ uint32_t s_hash[kWaves][HS];
+  __shared__ uint32_t s_igb[kWaves][kIgBits / 32u];
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint32_t i = blockIdx.x * kWaves + wv;
   if (i >= t.n) return;
   volatile uint32_t* stk = s_stack[wv];
   Tracer<decltype(dist_src<LEV>(g, t, i)), HS> tr{g, t, i, lane, t.src, t.dsts[i], nullptr, 0,
                                                   s_hash[wv], t.dead + (size_t)i * t.dead_words,
-                                                  dist_src<LEV>(g, t, i)};
+                                                  dist_src<LEV>(g, t, i), s_igb[wv]};
   if (!trace_setup(g, t, i, lane, tr)) return;
   for (uint32_t k = lane; k < HS; k += kWave) tr.hs[k] = 0u;
   uint32_t* out = t.out + (size_t)i * t.stride;
@@ -547,6 +576,7 @@ template <bool LEV>
 __global__ void __launch_bounds__(1024) ksp_heavy_kernel(DevGraph g, TraceArgs t) {
   __shared__ uint32_t s_hash[kHash];
   __shared__ HeavyLds H;
+  __shared__ uint32_t s_igb[kHeavyWaves][kIgBits / 32u];  // each wave's own filter
   const uint32_t lane = threadIdx.x & 63u;
   for (;;) {
     if (threadIdx.x == 0) {
@@ -560,7 +590,7 @@ __global__ void __launch_bounds__(1024) ksp_heavy_kernel(DevGraph g, TraceArgs t
     if (i == kInf) return;
     Tracer<decltype(dist_src<LEV>(g, t, i))> tr{g, t, i, lane, t.src, t.dsts[i], nullptr, 0, s_hash,
                                                 t.dead + (size_t)i * t.dead_words,
-                                                dist_src<LEV>(g, t, i)};
+                                                dist_src<LEV>(g, t, i), s_igb[threadIdx.x >> 6]};
     trace_setup(g, t, i, lane, tr);  // (a queued run always has work)
     heavy_trace(g, t, i, tr, s_hash, H);
   }
@@ -1054,7 +1084,7 @@ struct GoodPrune {
     if ((u & kDown) || u == v || !good(u)) return false;
     if (tr.dist(u) + 1u != d) return false;  // unit metric: tight
     const uint32_t lid = g.link_id[e];
-    if (tr.nign && in_sorted(tr.ign, tr.nign, lid)) return false;
+    if (tr.ignored(lid)) return false;
     return !tr.claimed(lid);
   }
   __device__ void operator()() const {
