@@ -161,7 +161,7 @@ __device__ bool twin_setup(const DevGraph& g, const TwinArgs& a, uint32_t i, uin
 template <int W>
 __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, TwinArgs a) {
   __shared__ TwinTab T;
-  __shared__ unsigned long long s_h, s_r, s_sd;
+  __shared__ unsigned long long s_h;
   __shared__ uint64_t s_wk[1u << kComboC];
   __shared__ uint32_t s_Lb[kWaves][256];  // own level bytes of each wave's tile
   extern __shared__ uint32_t s_stage[];  // [4 waves][1024 nodes][W]
@@ -171,7 +171,7 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
   const uint32_t NT = a.n * a.chunks, T8 = NT / 8u * 8u, b = blockIdx.x;
   const uint32_t item = b < T8 ? (b % 8u) * (T8 / 8u) + b / 8u : b;
   const uint32_t i = item / a.chunks, ci = item % a.chunks;
-  if (tid == 0) s_h = s_r = s_sd = 0ull;
+  if (tid == 0) s_h = 0ull;
   if (!twin_setup(g, a, i, W, T)) return;
   const uint32_t K = min(T.K, (uint32_t)(32 * W)), own = T.own, nc = T.nc;
   // an unpatched word is the OR of the tight classes' masks: with <= 6
@@ -192,8 +192,7 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
   __syncthreads();
   const uint32_t t0 = ci * a.ctiles, t1 = min(a.tiles, t0 + a.ctiles);
   uint32_t* st = s_stage + wave * 1024u * W;
-  uint64_t h = 0, dsum = 0;  // (dsum, dreach: the distance part when this launch writes the dist row)
-  uint32_t dreach = 0;
+  uint64_t h = 0;
   // the own and class rows of the wave's next tile are loaded before this
   // tile is computed and stored (up to 1 + 3 classes prefetched)
   constexpr uint32_t kPre = 3;
@@ -331,12 +330,6 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
         for (int q = 0; q < 4; ++q) {
           const uint32_t l = (Lw >> (8 * q)) & 0xFFu;
           dv[q] = l < 0x7Fu ? l - 1u : kInf;
-          // the digest's distance part (twin_levels leaves it to this launch)
-          if (a.digest && l < 0x7Fu && n0 + q < tn) {
-            dreach += 1u;
-            dsum += l - 1u;
-            h += g.dkey[2ull * (tv0 + n0 + q)] * (uint64_t)l;
-          }
         }
         if (n0 + 4u <= tn && (V & 3u) == 0) {
           store_row16(reinterpret_cast<uint4*>(drow + n0), make_uint4(dv[0], dv[1], dv[2], dv[3]));
@@ -379,30 +372,19 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
     __builtin_amdgcn_wave_barrier();  // the slice is rewritten by the next tile
   }
   if (a.digest) {
-    uint64_t r64 = dreach;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      h += shfl_xor64(h, o);
-      r64 += shfl_xor64(r64, o);
-      dsum += shfl_xor64(dsum, o);
-    }
-    if (lane == 0) {
-      if (h) atomicAdd(&s_h, (unsigned long long)h);
-      if (r64) atomicAdd(&s_r, (unsigned long long)r64);
-      if (dsum) atomicAdd(&s_sd, (unsigned long long)dsum);
-    }
+    for (int o = 32; o > 0; o >>= 1) h += shfl_xor64(h, o);
+    if (lane == 0 && h) atomicAdd(&s_h, (unsigned long long)h);
     __syncthreads();
     if (tid == 0) {
       ospf_digest* dg = a.digest + i;
-      unsigned long long hh = s_h, rr = s_r, ss = s_sd;
-      if (ci == 0 && !a.dist) {  // the distance part came with the level row
+      unsigned long long hh = s_h;
+      if (ci == 0) {
         const ospf_digest ld = a.lev_digest[own];
-        rr += ld.reached;
-        ss += ld.sum_dist;
+        atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)ld.reached);
+        atomicAdd((unsigned long long*)&dg->sum_dist, (unsigned long long)ld.sum_dist);
         hh += ld.hash;
       }
-      if (rr) atomicAdd((unsigned long long*)&dg->reached, rr);
-      if (ss) atomicAdd((unsigned long long*)&dg->sum_dist, ss);
       if (hh) atomicAdd((unsigned long long*)&dg->hash, hh);
     }
   }
@@ -464,9 +446,6 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
     nu += urow[u] != kInf ? 1u : 0u;
   }
   __syncthreads();
-  // digest keys only for a group with a root whose distance part is here
-  bool need_kd = false;
-  for (uint32_t j = 0; j < ng; ++j) need_kd |= !(s_umask[j] >> 31);
   const uint32_t nchunks = (a.pitch + 255u) / 256u;
   const uint32_t cb = (uint32_t)((uint64_t)part * nchunks / a.parts);
   const uint32_t ce = (uint32_t)((uint64_t)(part + 1) * nchunks / a.parts);
@@ -479,7 +458,7 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
       x[u] = (u < nu && ok) ? *reinterpret_cast<const uint32_t*>(a.lev + (size_t)urow[u] * a.pitch + v0)
                             : 0x7F7F7F7Fu;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) kd[q] = need_kd && ok && v0 + q < V ? g.dkey[2ull * (v0 + q)] : 0ull;
+    for (int q = 0; q < 4; ++q) kd[q] = ok && v0 + q < V ? g.dkey[2ull * (v0 + q)] : 0ull;
   };
   uint32_t br[kTwinLvG], cur[kTwinLvG];
   uint64_t bs[kTwinLvG], bh[kTwinLvG];
@@ -527,10 +506,6 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
       __builtin_nontemporal_store(L, reinterpret_cast<uint32_t*>(a.lev + (size_t)own * a.pitch + v0));
       if (v0 >= V) continue;
       uint32_t dv[4];
-      // bit 31: the root's next-hop launch writes its dist row and the
-      // digest's distance part
-      const bool fused = (__builtin_amdgcn_readfirstlane(s_umask[j]) >> 31) != 0u;
-      if (fused) continue;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint32_t l = (L >> (8 * q)) & 0xFFu;
@@ -541,7 +516,7 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
           bh[j] += kd[q] * (uint64_t)l;
         }
       }
-      if (a.dist) {
+      if (a.dist && !(s_umask[j] >> 31)) {  // bit 31: the root's next-hop launch writes it
         uint32_t* drow = a.dist + (size_t)own * V + v0;
         if (vec) {
           store_row16(drow, make_uint4(dv[0], dv[1], dv[2], dv[3]));
