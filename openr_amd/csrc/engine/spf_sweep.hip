@@ -20,6 +20,8 @@
 #include <new>
 #include <numeric>
 #include <string>
+#include <system_error>
+#include <thread>
 #include <vector>
 
 #include <rccl/rccl.h>
@@ -69,6 +71,30 @@ struct Facts {
   }
   uint32_t words(uint32_t v) const { return std::max(1u, (nbrs(v) + 31) / 32); }
 };
+
+// fn(lo, hi) over [0, n) on up to 16 host threads (the plan's per-node
+// loops; serial when threads are unavailable)
+template <class F>
+void par_for(uint32_t n, F fn, uint32_t grain = 2048) {
+  const uint32_t hw = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  const uint32_t T = std::min(hw, (n + grain - 1) / grain);
+  if (T <= 1) {
+    fn(0u, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  uint32_t done = 0;
+  try {
+    for (uint32_t t = 1; t < T; ++t) {
+      th.emplace_back(fn, (uint32_t)((uint64_t)n * t / T), (uint32_t)((uint64_t)n * (t + 1) / T));
+      done = t;
+    }
+  } catch (const std::system_error&) {  // no more threads: the rest here
+    fn((uint32_t)((uint64_t)n * (done + 1) / T), n);
+  }
+  fn(0u, (uint32_t)((uint64_t)n / T));
+  for (auto& x : th) x.join();
+}
 
 // stable order of `v` by key(v)
 template <class K>
@@ -303,7 +329,9 @@ uint32_t usable_slots(const ospf_ctx* c, uint32_t r) {
 // groups of <= kLeafMaxG; returns the group offsets.
 std::vector<uint32_t> leaf_groups(const ospf_ctx* c, const Facts& f, std::vector<uint32_t>& roots) {
   std::vector<uint32_t> use(roots.size());
-  for (size_t i = 0; i < roots.size(); ++i) use[i] = usable_slots(c, roots[i]);
+  par_for((uint32_t)roots.size(), [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t i = lo; i < hi; ++i) use[i] = usable_slots(c, roots[i]);
+  });
   std::vector<uint32_t> ord(roots.size());
   std::iota(ord.begin(), ord.end(), 0u);
   auto same_nbrs = [&](uint32_t a, uint32_t b) {
@@ -349,31 +377,53 @@ Twins twin_classes(const ospf_ctx* c) {
   const uint32_t V = c->info.n_nodes;
   std::vector<uint32_t> off(V + 1, 0), lst;
   std::vector<uint64_t> key(V);
-  lst.reserve(c->h_dn.size());
-  for (uint32_t u = 0; u < V; ++u) {
-    off[u] = (uint32_t)lst.size();
-    const size_t b = lst.size();
+  // each node's usable distinct neighbours (sorted, unique): counted, then
+  // written and hashed, both on host threads
+  auto nbrs_of = [&](uint32_t u, uint32_t* out) {  // -> count (out may be null)
+    uint32_t m = 0, prev = 0xFFFFFFFFu;
+    bool sorted = true;
     for (uint32_t e = c->h_prow[u]; e < c->h_prow[u + 1]; ++e) {
       const uint32_t x = c->h_pcolx[e];
-      if ((x & 0x80000000u) || x == u) continue;
-      lst.push_back(x);
+      if ((x & 0x80000000u) || x == u || x == prev) continue;
+      sorted &= prev == 0xFFFFFFFFu || x > prev;
+      if (out) out[m] = x;
+      prev = x;
+      ++m;
     }
-    std::sort(lst.begin() + b, lst.end());
-    lst.erase(std::unique(lst.begin() + b, lst.end()), lst.end());
-    const bool tr = !((c->h_nt[u >> 5] >> (u & 31)) & 1u);
-    uint64_t h = tr ? 0x9E3779B97F4A7C15ull : 0xC2B2AE3D27D4EB4Full;
-    for (size_t i = b; i < lst.size(); ++i) h = ospf::digest_mix(h ^ lst[i]) + i - b;
-    key[u] = h;
-  }
-  off[V] = (uint32_t)lst.size();
+    if (out && !sorted) {  // (rows are sorted by neighbour id; kept exact either way)
+      std::sort(out, out + m);
+      m = (uint32_t)(std::unique(out, out + m) - out);
+    }
+    return m;
+  };
+  std::vector<uint32_t> cnt(V);
+  par_for(V, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t u = lo; u < hi; ++u) cnt[u] = nbrs_of(u, nullptr);
+  });
+  for (uint32_t u = 0; u < V; ++u) off[u + 1] = off[u] + cnt[u];
+  lst.resize(off[V]);
+  par_for(V, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t u = lo; u < hi; ++u) {
+      const uint32_t m = nbrs_of(u, lst.data() + off[u]);
+      for (uint32_t i = m; i < cnt[u]; ++i) lst[off[u] + i] = 0xFFFFFFFFu;  // (dups of an unsorted row)
+      cnt[u] = m;
+      const bool tr = !((c->h_nt[u >> 5] >> (u & 31)) & 1u);
+      uint64_t h = tr ? 0x9E3779B97F4A7C15ull : 0xC2B2AE3D27D4EB4Full;
+      for (uint32_t i = 0; i < m; ++i) h = ospf::digest_mix(h ^ lst[off[u] + i]) + i;
+      key[u] = h;
+    }
+  });
   auto same = [&](uint32_t a, uint32_t b) {
     const bool ta = !((c->h_nt[a >> 5] >> (a & 31)) & 1u), tb = !((c->h_nt[b >> 5] >> (b & 31)) & 1u);
-    return ta == tb && off[a + 1] - off[a] == off[b + 1] - off[b] &&
-           std::equal(lst.begin() + off[a], lst.begin() + off[a + 1], lst.begin() + off[b]);
+    return ta == tb && cnt[a] == cnt[b] &&
+           std::equal(lst.begin() + off[a], lst.begin() + off[a] + cnt[a], lst.begin() + off[b]);
   };
+  // nodes by (key, id): the stable order by key
+  std::vector<std::pair<uint64_t, uint32_t>> kv(V);
+  for (uint32_t u = 0; u < V; ++u) kv[u] = {key[u], u};
+  std::sort(kv.begin(), kv.end());
   std::vector<uint32_t> ord(V);
-  std::iota(ord.begin(), ord.end(), 0u);
-  std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
+  for (uint32_t u = 0; u < V; ++u) ord[u] = kv[u].second;
   Twins t;
   t.cls.assign(V, kNone);
   for (size_t i = 0; i < V;) {
@@ -664,13 +714,28 @@ int hub_build(ospf_ctx* c, const Facts& f, const std::vector<uint32_t>& roots, u
 // (C) one next-hop launch per width class of cover roots, roots ordered by
 //     their largest neighbour (their neighbours' level rows stay in L2 / MALL),
 //     on their own streams beside (B).
+// OSPF_SWEEP_TIMING: host phases of a plan on stderr
+struct PlanLaps {
+  bool on = getenv("OSPF_SWEEP_TIMING") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void operator()(const char* what) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    fprintf(stderr, "sweep_create plan/%s %.2f ms\n", what,
+            std::chrono::duration<double, std::milli>(n - t).count());
+    t = n;
+  }
+};
+
 int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine) {
   ospf_ctx* c = s->c;
   const uint32_t V = s->V;
   const uint32_t hop = s->opts.flags & OSPF_HOP_COUNT;
+  PlanLaps lap;
   std::vector<uint8_t> leaf;
   if (!getenv("OSPF_SWEEP_NOLEAF")) leaf = leaf_set(f);
   else leaf.assign(V, 0);
+  lap("leaf set");
   std::vector<uint32_t> own_l, own_c;
   for (uint32_t r : mine) (leaf[r] ? own_l : own_c).push_back(r);
   // leaves whose rows the cover roots' next hops read
@@ -704,19 +769,38 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   // twin classes: a class of <= 4-word roots whose usable transit
   // neighbours span few classes reads one row per class (spf_twin.hip), and
   // so can a cover row (twin levels)
+  lap("closure + width classes");
   Twins tw;
   if (!getenv("OSPF_SWEEP_NOTWIN")) tw = twin_classes(c);
-  // classes of r's usable transit neighbours (sorted, unique); false past kTwinMaxC
+  lap("twin classes");
+  // classes of r's usable transit neighbours (sorted, unique); false past
+  // kTwinMaxC. Every node's, once, on host threads: [V][kTwinMaxC + 1] slots
+  // and a count (kTwinMaxC + 1: more)
+  constexpr uint32_t kCS = ospf::kTwinMaxC + 1;
+  std::vector<uint32_t> ccls, ccnt;
+  if (!tw.cls.empty()) {
+    ccls.resize((size_t)V * kCS);
+    ccnt.resize(V);
+    par_for(V, [&](uint32_t lo, uint32_t hi) {
+      std::vector<uint32_t> b;
+      for (uint32_t r = lo; r < hi; ++r) {
+        b.clear();
+        for (uint32_t e = c->h_prow[r]; e < c->h_prow[r + 1]; ++e) {
+          const uint32_t x = c->h_pcolx[e];
+          if ((x & 0x80000000u) || x == r || ((c->h_nt[x >> 5] >> (x & 31)) & 1u)) continue;
+          b.push_back(tw.cls[x]);
+        }
+        std::sort(b.begin(), b.end());
+        b.erase(std::unique(b.begin(), b.end()), b.end());
+        const uint32_t m = std::min<uint32_t>((uint32_t)b.size(), kCS);
+        std::copy(b.begin(), b.begin() + m, ccls.begin() + (size_t)r * kCS);
+        ccnt[r] = m;
+      }
+    }, 512);
+  }
   std::vector<uint32_t> cs;
   auto classes_of = [&](uint32_t r) {
-    cs.clear();
-    for (uint32_t e = c->h_prow[r]; e < c->h_prow[r + 1]; ++e) {
-      const uint32_t x = c->h_pcolx[e];
-      if ((x & 0x80000000u) || x == r || ((c->h_nt[x >> 5] >> (x & 31)) & 1u)) continue;
-      cs.push_back(tw.cls[x]);
-    }
-    std::sort(cs.begin(), cs.end());
-    cs.erase(std::unique(cs.begin(), cs.end()), cs.end());
+    cs.assign(ccls.begin() + (size_t)r * kCS, ccls.begin() + (size_t)r * kCS + ccnt[r]);
     return cs.size() <= ospf::kTwinMaxC;
   };
   auto twin_ok = [&](const std::vector<uint32_t>& roots) {
@@ -735,6 +819,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     if (k.reads_leaf && !k.twin) all_leaf_rows = true;
   }
   all_leaf_rows |= tw.cls.empty() || getenv("OSPF_SWEEP_ALL_LEAF_ROWS") != nullptr;
+  lap("twin width classes");
   std::vector<uint32_t> need_l = own_l;
   need_l.insert(need_l.end(), extra_l.begin(), extra_l.end());
   // cover rows: own cover roots + every non-leaf neighbour of a needed root
@@ -790,6 +875,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   // rows are read, the representatives go first in a launch of their own,
   // so the next hops of the cover roots start while the other leaves' rows
   // are written
+  lap("cover rows + twin levels set");
   std::vector<uint32_t> reps, rest;
   for (uint32_t x : need_l) {
     const bool first = twin_lv ? seed[x] != 0 : (!all_leaf_rows && tw.rep[tw.cls[x]] == x);
@@ -797,6 +883,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   }
   std::vector<uint32_t> grp_r = leaf_groups(c, f, reps);
   std::vector<uint32_t> grp = leaf_groups(c, f, rest);
+  lap("leaf groups");
   need_l = reps;
   need_l.insert(need_l.end(), rest.begin(), rest.end());
   const uint32_t nR = (uint32_t)reps.size(), nL = (uint32_t)need_l.size();
@@ -878,6 +965,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       lsg[k] = k == S ? ngr0 : x;
     }
   }
+  lap("rows + stages");
   uint32_t rows = nc + nd;
   for (uint32_t i = 0; i < nL; ++i)
     if (pos[need_l[i]] == kNone) pos[need_l[i]] = rows++;
@@ -902,6 +990,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     std::vector<uint32_t> lout(std::max(drop_rest ? nL - nR : 0u, twin_lv ? nR : 0u), kNone);
     if ((rc = upload(s, &d_lout, lout))) return rc;
   }
+  lap("allocations + uploads");
   uint32_t *d_tcls = nullptr, *d_trep = nullptr, *d_tsec = nullptr;
   bool any_twin = nd > 0;
   for (auto& k : cls) any_twin |= k.twin;
@@ -995,6 +1084,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   const int ev_cov = nd ? ev_t : ev_a;
   // (C) cover classes: digest slots 0 .. |own_c|
   uint32_t slot = 0;
+  lap("twin levels units");
   std::vector<ospf_sweep::Unit> side, after;
   for (size_t i = 0; i < cls.size(); ++i) {
     Cls& k = cls[i];
@@ -1116,6 +1206,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     (u.wait[0] == ev_b || u.wait[0] == ev_r ? after : side).push_back(std::move(u));
   }
   for (auto& x : side) s->units.push_back(std::move(x));
+  lap("cover next-hop units");
   // (B) leaves: digest slots after the cover roots'; representatives first
   if (nL) {
     uint32_t kmax = 1;
@@ -1217,6 +1308,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       s->units.push_back(std::move(u));
     }
   }
+  lap("next-hop + leaf units");
   // an event no launch records stands for the one before it
   auto alias = [&](int from, int to) {
     for (auto& u : after)
