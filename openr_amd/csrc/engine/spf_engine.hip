@@ -870,6 +870,14 @@ int twin_lv_build(ospf_ctx* c, const std::vector<uint32_t>& roots, const std::ve
   if (out.grp.front() != 0 || out.grp.back() != n)
     return fail(c, OSPF_E_INVAL, "twin levels: group offsets must run 0 .. n");
   out.nbo.assign(1, 0u);
+  out.nbo.reserve(n + 1);
+  out.rinfo.reserve(n);
+  {
+    size_t ent = 0;
+    for (uint32_t r : roots)
+      if (r < V) ent += c->h_prow[r + 1] - c->h_prow[r];
+    out.nbl.reserve(ent);
+  }
   std::vector<uint32_t> rows;  // this root's class rows
   for (size_t gi = 0; gi + 1 < out.grp.size(); ++gi) {
     const uint32_t g0 = out.grp[gi], g1 = out.grp[gi + 1];

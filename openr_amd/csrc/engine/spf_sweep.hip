@@ -96,6 +96,36 @@ void par_for(uint32_t n, F fn, uint32_t grain = 2048) {
   for (auto& x : th) x.join();
 }
 
+// stable sort on host threads: chunks stable-sorted in parallel, then merged
+// pairwise (left run first: stable)
+template <class T, class Less>
+void par_stable_sort(std::vector<T>& v, Less less) {
+  const uint32_t n = (uint32_t)v.size();
+  const uint32_t hw = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  uint32_t C = 1;
+  while (C * 2 <= hw && n / (C * 2) >= 4096u) C *= 2;
+  if (C == 1) {
+    std::stable_sort(v.begin(), v.end(), less);
+    return;
+  }
+  std::vector<uint32_t> b(C + 1);
+  for (uint32_t k = 0; k <= C; ++k) b[k] = (uint32_t)((uint64_t)n * k / C);
+  par_for(C, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t k = lo; k < hi; ++k) std::stable_sort(v.begin() + b[k], v.begin() + b[k + 1], less);
+  }, 1);
+  std::vector<T> tmp(n);
+  for (uint32_t w = 1; w < C; w *= 2) {
+    const uint32_t pairs = C / (2 * w);
+    par_for(pairs, [&](uint32_t lo, uint32_t hi) {
+      for (uint32_t q = lo; q < hi; ++q) {
+        const uint32_t a0 = b[2 * q * w], a1 = b[2 * q * w + w], a2 = b[2 * q * w + 2 * w];
+        std::merge(v.begin() + a0, v.begin() + a1, v.begin() + a1, v.begin() + a2, tmp.begin() + a0, less);
+      }
+    }, 1);
+    v.swap(tmp);
+  }
+}
+
 // stable order of `v` by key(v)
 template <class K>
 void locality_order(std::vector<uint32_t>& v, K key) {
@@ -339,7 +369,7 @@ std::vector<uint32_t> leaf_groups(const ospf_ctx* c, const Facts& f, std::vector
            std::equal(f.dn->begin() + (*f.dn_off)[a], f.dn->begin() + (*f.dn_off)[a + 1],
                       f.dn->begin() + (*f.dn_off)[b]);
   };
-  std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
+  par_stable_sort(ord, [&](uint32_t x, uint32_t y) {
     const uint32_t a = roots[x], b = roots[y];
     if (f.nbrs(a) != f.nbrs(b)) return f.first(a) != f.first(b) ? f.first(a) < f.first(b)
                                                                  : f.nbrs(a) < f.nbrs(b);
@@ -421,7 +451,9 @@ Twins twin_classes(const ospf_ctx* c) {
   // nodes by (key, id): the stable order by key
   std::vector<std::pair<uint64_t, uint32_t>> kv(V);
   for (uint32_t u = 0; u < V; ++u) kv[u] = {key[u], u};
-  std::sort(kv.begin(), kv.end());
+  par_stable_sort(kv, [](const std::pair<uint64_t, uint32_t>& x, const std::pair<uint64_t, uint32_t>& y) {
+    return x < y;
+  });
   std::vector<uint32_t> ord(V);
   for (uint32_t u = 0; u < V; ++u) ord[u] = kv[u].second;
   Twins t;
@@ -478,18 +510,28 @@ int wide_plan_build(ospf_ctx* c, const Facts& f, const std::vector<uint32_t>& ro
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t r = roots[i];
     if (pos[r] == kNone) return fail(c, OSPF_E_RANGE, "wide plan: a root without a level row");
+    if (f.nbrs(r) > 32u * W || f.nbrs(r) > 2048u) return fail(c, OSPF_E_RANGE, "wide plan: too many neighbours");
     h.own.push_back(pos[r]);
-    const uint32_t* dn = f.dn->data() + (*f.dn_off)[r];
-    const uint32_t K = f.nbrs(r);
-    if (K > 32u * W || K > 2048u) return fail(c, OSPF_E_RANGE, "wide plan: too many neighbours");
-    for (uint32_t e = c->h_prow[r]; e < c->h_prow[r + 1]; ++e) {
-      const uint32_t x = c->h_pcolx[e];
-      if ((x & 0x80000000u) || x == r) continue;
-      const uint32_t k = (uint32_t)(std::lower_bound(dn, dn + K, x) - dn);
-      h.keep[(size_t)i * W + (k >> 5)] |= 1u << (k & 31u);
-    }
-    if (i == 0 || i - h.run.back() >= 64u || !same(roots[h.run.back()], r)) h.run.push_back(i);
   }
+  // each root's usable slots, on host threads (rows ascend by neighbour id:
+  // a cursor over the distinct neighbours, a search only if one is missed)
+  par_for(n, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t i = lo; i < hi; ++i) {
+      const uint32_t r = roots[i];
+      const uint32_t* dn = f.dn->data() + (*f.dn_off)[r];
+      const uint32_t K = f.nbrs(r);
+      uint32_t k = 0;
+      for (uint32_t e = c->h_prow[r]; e < c->h_prow[r + 1]; ++e) {
+        const uint32_t x = c->h_pcolx[e];
+        if ((x & 0x80000000u) || x == r) continue;
+        while (k < K && dn[k] < x) ++k;
+        if (k >= K || dn[k] != x) k = (uint32_t)(std::lower_bound(dn, dn + K, x) - dn);
+        h.keep[(size_t)i * W + (k >> 5)] |= 1u << (k & 31u);
+      }
+    }
+  }, 16);
+  for (uint32_t i = 0; i < n; ++i)
+    if (i == 0 || i - h.run.back() >= 64u || !same(roots[h.run.back()], roots[i])) h.run.push_back(i);
   h.run.push_back(n);
   h.soff.push_back(0u);
   for (size_t q = 0; q + 1 < h.run.size(); ++q) {
@@ -784,14 +826,15 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     par_for(V, [&](uint32_t lo, uint32_t hi) {
       std::vector<uint32_t> b;
       for (uint32_t r = lo; r < hi; ++r) {
+        // distinct classes, sorted; stops at kCS of them (more is "too many")
         b.clear();
-        for (uint32_t e = c->h_prow[r]; e < c->h_prow[r + 1]; ++e) {
+        for (uint32_t e = c->h_prow[r]; e < c->h_prow[r + 1] && b.size() < kCS; ++e) {
           const uint32_t x = c->h_pcolx[e];
           if ((x & 0x80000000u) || x == r || ((c->h_nt[x >> 5] >> (x & 31)) & 1u)) continue;
-          b.push_back(tw.cls[x]);
+          const uint32_t k = tw.cls[x];
+          const auto it = std::lower_bound(b.begin(), b.end(), k);
+          if (it == b.end() || *it != k) b.insert(it, k);
         }
-        std::sort(b.begin(), b.end());
-        b.erase(std::unique(b.begin(), b.end()), b.end());
         const uint32_t m = std::min<uint32_t>((uint32_t)b.size(), kCS);
         std::copy(b.begin(), b.begin() + m, ccls.begin() + (size_t)r * kCS);
         ccnt[r] = m;
