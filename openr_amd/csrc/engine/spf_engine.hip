@@ -557,11 +557,14 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
   // 3: masked reruns + k = 2 over a set of runs (all of them, or the ones the
   // decremental kernel left): the multi-source BFS with per-run ignore masks
   // (unit metric) or per-run rows
+  // the stream of the full reruns: the caller's, or a high-priority one
+  // while the decremental kernels run beside them (run_ksp2's presplit)
+  hipStream_t fs = s;
   auto full_reruns = [&](const uint32_t* R_dsts, uint32_t R_n, const uint32_t* R_ign,
                          const uint32_t* R_cnt, uint32_t* R_status, uint32_t* R_k2) -> int {
     ospf::TraceArgs t = t_k1;
-    const uint32_t total_vb = (R_n + 63) / 64;  // this set's virtual batches (<= the carve's)
-    HIPCHK(c, hipMemsetD32Async(d_roots, (int)src, ms ? R_n : chunk, s));
+    const uint32_t total_vb = (R_n + 63) / 64;  // this set's virtual batches (<= the carve'fs)
+    HIPCHK(c, hipMemsetD32Async(d_roots, (int)src, ms ? R_n : chunk, fs));
     if (ms) {
       if (!c->aux) HIPCHK(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
       while (c->ev.size() < 2 * (size_t)slots + 1) {
@@ -606,23 +609,23 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
         const size_t zero = (char*)(a.igb + (size_t)a.nb * igw) - st;
         a.igm = (uint64_t*)(st + align_up(zero, 256));
         a.lev = lev;
-        HIPCHK(c, ospf::zero_async(st, zero, s));
-        if (r >= slots) HIPCHK(c, hipStreamWaitEvent(s, ev_tr[slot], 0));  // slot's trace done
-        HIPCHK(c, ospf::zero_async(lev, (size_t)a.nb * V * 64ull, s));
-        e = ospf::launch_ksp_masks(c->g, a, R_ign, R_cnt, cap, s);
+        HIPCHK(c, ospf::zero_async(st, zero, fs));
+        if (r >= slots) HIPCHK(c, hipStreamWaitEvent(fs, ev_tr[slot], 0));  // slot's trace done
+        HIPCHK(c, ospf::zero_async(lev, (size_t)a.nb * V * 64ull, fs));
+        e = ospf::launch_ksp_masks(c->g, a, R_ign, R_cnt, cap, fs);
         if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_masks");
         uint32_t d = std::max<uint32_t>(2, c->depth_bound);
         // test knob: start with fewer levels (exercises the continuation below)
         if (const char* x = getenv("OSPF_KSP_D0")) d = std::max(2, std::min((int)d, atoi(x)));
-        e = ospf::launch_msbfs_ksp(c->g, a, 1, d, s);
+        e = ospf::launch_msbfs_ksp(c->g, a, 1, d, fs);
         if (e != hipSuccess) return hip_fail(c, e, "launch_msbfs_ksp");
         // masked runs may be deeper than the graph's bound: continue while any
         // batch still has a frontier (levels up to 253: lev bytes hold dist + 1)
         std::vector<uint32_t> deep;
         for (;;) {
           found.resize((size_t)a.nb * lmax);
-          HIPCHK(c, hipMemcpyAsync(found.data(), a.found, found.size() * 4ull, hipMemcpyDeviceToHost, s));
-          HIPCHK(c, hipStreamSynchronize(s));
+          HIPCHK(c, hipMemcpyAsync(found.data(), a.found, found.size() * 4ull, hipMemcpyDeviceToHost, fs));
+          HIPCHK(c, hipStreamSynchronize(fs));
           deep.clear();
           for (uint32_t j = 0; j < a.nb; ++j)
             if (found[(size_t)j * lmax + d]) deep.push_back(j);
@@ -630,17 +633,17 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
           if (d >= 254) {  // these runs keep OVF2: their levels stop at 254
             for (uint32_t j : deep) {
               const uint32_t r0 = (vb0 + j) * 64u;
-              e = ospf::launch_or_bits(R_status + r0, std::min(64u, R_n - r0), OSPF_KSP_OVF2, s);
+              e = ospf::launch_or_bits(R_status + r0, std::min(64u, R_n - r0), OSPF_KSP_OVF2, fs);
               if (e != hipSuccess) return hip_fail(c, e, "launch_or_bits");
             }
             break;
           }
           const uint32_t d1 = std::min<uint32_t>(d + 8, 254);
-          e = ospf::launch_msbfs_ksp(c->g, a, d, d1, s);
+          e = ospf::launch_msbfs_ksp(c->g, a, d, d1, fs);
           if (e != hipSuccess) return hip_fail(c, e, "launch_msbfs_ksp");
           d = d1;
         }
-        HIPCHK(c, hipEventRecord(ev_bfs[slot], s));
+        HIPCHK(c, hipEventRecord(ev_bfs[slot], fs));
         HIPCHK(c, hipStreamWaitEvent(c->aux, ev_bfs[slot], 0));
         const uint32_t r0 = vb0 * 64u;
         ospf::TraceArgs t2 = t;
@@ -665,12 +668,12 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
         HIPCHK(c, hipEventRecord(ev_tr[slot], c->aux));
       }
       HIPCHK(c, hipEventRecord(ev_end, c->aux));
-      HIPCHK(c, hipStreamWaitEvent(s, ev_end, 0));
+      HIPCHK(c, hipStreamWaitEvent(fs, ev_end, 0));
       c->spf_runs += R_n;
     } else {
       uint32_t* d_rows = (uint32_t*)st;
       uint32_t* d_off = (uint32_t*)(st + align_up((size_t)chunk * V * 4ull, 256));
-      e = ospf::launch_iota(d_off, chunk, cap, s);
+      e = ospf::launch_iota(d_off, chunk, cap, fs);
       if (e != hipSuccess) return hip_fail(c, e, "launch_iota");
       for (uint32_t r0 = 0; r0 < R_n; r0 += chunk) {
         const uint32_t nc = std::min(chunk, R_n - r0);
@@ -684,7 +687,7 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
         b.nh_words = W;
         b.max_root_neighbors = nn;
         b.d_dist = d_rows;
-        rc = ospf_run_batch_dev(c, &b, s);
+        rc = ospf_run_batch_dev(c, &b, fs);
         if (rc) return rc;
         ospf::TraceArgs t2 = t;
         t2.dsts = R_dsts + r0;
@@ -698,9 +701,9 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
         t2.cnt_out = nullptr;
         t2.status = R_status + r0;
         t2.k = 2;
-        HIPCHK(c, ospf::zero_async(d_dead, (size_t)t2.n * dw * 4ull, s));
-        HIPCHK(c, ospf::zero_async(t2.heavy_ctr, 8, s));
-        e = ospf::launch_ksp_trace(false, c->g, t2, s);
+        HIPCHK(c, ospf::zero_async(d_dead, (size_t)t2.n * dw * 4ull, fs));
+        HIPCHK(c, ospf::zero_async(t2.heavy_ctr, 8, fs));
+        e = ospf::launch_ksp_trace(false, c->g, t2, fs);
         if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_trace k2");
       }
     }
@@ -715,7 +718,11 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
     const size_t dwb = align_up((size_t)dw * 4ull, 256);
     uint32_t bpc = ospf::ksp_decr_blocks_per_cu();
     if (const char* x = getenv("OSPF_KSP_DECR_BPC")) bpc = std::max(1u, std::min(bpc, (uint32_t)atoi(x)));
-    const uint32_t nblk = std::max<uint32_t>(1, bpc * (uint32_t)c->n_cu);
+    // (OSPF_KSP_DECR_R: runs per block instead of persistent blocks)
+    uint32_t decr_r = 0;
+    if (const char* x = getenv("OSPF_KSP_DECR_R")) decr_r = (uint32_t)std::max(0, atoi(x));
+    const uint32_t nblk = decr_r ? std::max(1u, (n + decr_r - 1) / decr_r)
+                                 : std::max<uint32_t>(1, bpc * (uint32_t)c->n_cu);
     const uint32_t hblk = 2u * (uint32_t)c->n_cu;  // ksp_decr_heavy_kernel: 2 per CU
     const size_t sz_tc = align_up(V * 4ull, 256), sz_fb = align_up(n * 4ull, 256), sz_ctr = 256,
                  sz_dd = dwb * std::max(nblk, hblk);
@@ -754,6 +761,7 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
     td.heavy = d_hq;
     td.heavy_ctr = d_ctr + 4;
     td.err = c->d_err;
+    td.decr_runs = decr_r;
     if (prune) {
       char* q = dp + sz_tc + 3 * sz_fb + sz_ctr + sz_dd;
       uint32_t* d_ord = (uint32_t*)q;
@@ -780,13 +788,26 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
       HIPCHK(c, hipStreamSynchronize(s));
     }
     hipStream_t ks = s;
+    // with presplit runs: the decremental kernels on a low-priority stream,
+    // the full reruns (the launch's critical path) on a high-priority one
+    // (OSPF_KSP_NOPRIO: the caller's stream for them)
+    const bool prio = getenv("OSPF_KSP_NOPRIO") == nullptr;
     if (npre) {
-      if (!c->ksp_aux) HIPCHK(c, hipStreamCreateWithFlags(&c->ksp_aux, hipStreamNonBlocking));
+      if (!c->ksp_aux || !c->ksp_hi) {
+        int lo = 0, hi = 0;
+        HIPCHK(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+        if (!c->ksp_aux) HIPCHK(c, hipStreamCreateWithPriority(&c->ksp_aux, hipStreamNonBlocking, lo));
+        if (!c->ksp_hi) HIPCHK(c, hipStreamCreateWithPriority(&c->ksp_hi, hipStreamNonBlocking, hi));
+      }
       for (hipEvent_t& x : c->ksp_ev)
         if (!x) HIPCHK(c, hipEventCreateWithFlags(&x, hipEventDisableTiming));
       HIPCHK(c, hipEventRecord(c->ksp_ev[0], s));
       HIPCHK(c, hipStreamWaitEvent(c->ksp_aux, c->ksp_ev[0], 0));
       ks = c->ksp_aux;
+      if (prio) {
+        HIPCHK(c, hipStreamWaitEvent(c->ksp_hi, c->ksp_ev[0], 0));
+        fs = c->ksp_hi;
+      }
     }
     e = ospf::launch_ksp_decr(c->g, td, nblk, ks);
     if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_decr");
@@ -807,15 +828,15 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
       uint32_t* f_ign = (uint32_t*)(fp + 3 * sz_fd);
       uint32_t* f_k2 = (uint32_t*)(fp + 3 * sz_fd + sz_fr);
       hipError_t e2;
-      if ((e2 = ospf::launch_rows_gather(f_dsts, k->dsts, d_list, nl, 1, true, s)) != hipSuccess ||
-          (e2 = ospf::launch_rows_gather(f_status, k->status, d_list, nl, 1, true, s)) != hipSuccess ||
-          (e2 = ospf::launch_rows_gather(f_cnt, d_cnt, d_list, nl, 1, true, s)) != hipSuccess ||
-          (e2 = ospf::launch_rows_gather(f_ign, d_ign, d_list, nl, cap, true, s)) != hipSuccess)
+      if ((e2 = ospf::launch_rows_gather(f_dsts, k->dsts, d_list, nl, 1, true, fs)) != hipSuccess ||
+          (e2 = ospf::launch_rows_gather(f_status, k->status, d_list, nl, 1, true, fs)) != hipSuccess ||
+          (e2 = ospf::launch_rows_gather(f_cnt, d_cnt, d_list, nl, 1, true, fs)) != hipSuccess ||
+          (e2 = ospf::launch_rows_gather(f_ign, d_ign, d_list, nl, cap, true, fs)) != hipSuccess)
         return hip_fail(c, e2, "launch_rows_gather");
       rc2 = full_reruns(f_dsts, nl, f_ign, f_cnt, f_status, f_k2);
       if (rc2) return rc2;
-      if ((e2 = ospf::launch_rows_gather(k->status, f_status, d_list, nl, 1, false, s)) != hipSuccess ||
-          (e2 = ospf::launch_rows_gather(k->k2, f_k2, d_list, nl, cap, false, s)) != hipSuccess)
+      if ((e2 = ospf::launch_rows_gather(k->status, f_status, d_list, nl, 1, false, fs)) != hipSuccess ||
+          (e2 = ospf::launch_rows_gather(k->k2, f_k2, d_list, nl, cap, false, fs)) != hipSuccess)
         return hip_fail(c, e2, "launch_rows_gather");
       return OSPF_OK;
     };
@@ -828,7 +849,7 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
     HIPCHK(c, hipStreamSynchronize(ks));
     if (ks != s) {
       HIPCHK(c, hipEventRecord(c->ksp_ev[1], ks));
-      HIPCHK(c, hipStreamWaitEvent(s, c->ksp_ev[1], 0));
+      HIPCHK(c, hipStreamWaitEvent(fs, c->ksp_ev[1], 0));
     }
     if (getenv("OSPF_KSP_DEBUG")) {
       uint64_t clk[8];
@@ -850,6 +871,10 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
     if (nfb) {
       rc = rerun_list(d_fb, nfb, 4);
       if (rc) return rc;
+    }
+    if (fs != s) {  // the caller's stream after the full reruns (and, through them, ks)
+      HIPCHK(c, hipEventRecord(c->ksp_ev[2], fs));
+      HIPCHK(c, hipStreamWaitEvent(s, c->ksp_ev[2], 0));
     }
   }
   return OSPF_OK;
@@ -1277,6 +1302,7 @@ int ospf_close(ospf_ctx* c) {
   for (hipEvent_t e : c->ev) hipEventDestroy(e);
   if (c->aux) hipStreamDestroy(c->aux);
   if (c->ksp_aux) hipStreamDestroy(c->ksp_aux);
+  if (c->ksp_hi) hipStreamDestroy(c->ksp_hi);
   for (hipEvent_t e : c->ksp_ev)
     if (e) hipEventDestroy(e);
   for (hipEvent_t e : c->lv_ev)

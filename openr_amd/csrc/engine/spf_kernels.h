@@ -635,6 +635,7 @@ struct TraceArgs {
   uint32_t budget;          // DFS steps before a run goes to the heavy kernel (0 = none)
   uint32_t look;            // lookahead: predecessors with rows <= look entries are probed
   uint32_t src_cut;         // presplit: runs ignoring more of the source's links (0: off)
+  uint32_t decr_runs;       // ksp_decr: runs per block (0: persistent blocks)
   uint32_t* pre_bits;       // [n / 32] runs the presplit sent to the full reruns (ksp_decr skips them)
   uint32_t* heavy;          // [n] queued run indices
   uint32_t* heavy_ctr;      // [2] {queued, taken}, zeroed by the caller

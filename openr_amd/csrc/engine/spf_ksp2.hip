@@ -967,7 +967,9 @@ __global__ void __launch_bounds__(64) ksp_decr_kernel(DevGraph g, TraceArgs t) {
   const uint32_t lane = threadIdx.x;
   const uint32_t src = t.src;
   uint32_t* dead = t.dead + (size_t)blockIdx.x * t.dead_words;
-  for (;;) {
+  // persistent (decr_runs 0: until the runs are taken), or decr_runs runs per
+  // block so a higher-priority stream's blocks get the CUs as blocks retire
+  for (uint32_t it = 0; t.decr_runs == 0 || it < t.decr_runs; ++it) {
     if (lane == 0) L.run = atomicAdd(&t.ctr[0], 1u);
     __builtin_amdgcn_wave_barrier();
     const uint32_t i = ((volatile uint32_t&)L.run);
