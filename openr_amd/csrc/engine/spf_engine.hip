@@ -888,60 +888,93 @@ int twin_lv_build(ospf_ctx* c, const std::vector<uint32_t>& roots, const std::ve
                   const std::vector<uint32_t>& pos, const std::vector<uint32_t>& cls,
                   const std::vector<uint32_t>& rep, TwinLvHost& out) {
   const uint32_t V = c->info.n_nodes, n = (uint32_t)roots.size();
+  constexpr uint32_t kNo = 0xFFFFFFFFu;
   out = TwinLvHost{};
   out.grp = groups;
   if (out.grp.empty())
     for (uint32_t i = 0; i <= n; ++i) out.grp.push_back(i);
   if (out.grp.front() != 0 || out.grp.back() != n)
     return fail(c, OSPF_E_INVAL, "twin levels: group offsets must run 0 .. n");
-  out.nbo.assign(1, 0u);
-  out.nbo.reserve(n + 1);
-  out.rinfo.reserve(n);
-  {
-    size_t ent = 0;
-    for (uint32_t r : roots)
-      if (r < V) ent += c->h_prow[r + 1] - c->h_prow[r];
-    out.nbl.reserve(ent);
-  }
-  std::vector<uint32_t> rows;  // this root's class rows
-  for (size_t gi = 0; gi + 1 < out.grp.size(); ++gi) {
-    const uint32_t g0 = out.grp[gi], g1 = out.grp[gi + 1];
-    if (g1 < g0 || g1 - g0 > ospf::kTwinLvG)
+  const uint32_t ng = (uint32_t)out.grp.size() - 1;
+  for (uint32_t gi = 0; gi < ng; ++gi)
+    if (out.grp[gi + 1] < out.grp[gi] || out.grp[gi + 1] - out.grp[gi] > ospf::kTwinLvG)
       return fail(c, OSPF_E_RANGE, "twin levels: a group of more than 8 roots");
-    std::vector<uint32_t> urow;
-    for (uint32_t i = g0; i < g1; ++i) {
+  // two passes on host threads: each root's neighbour-list length, then per
+  // group the lists, class rows and masks at their offsets
+  std::atomic<int> bad{0};  // 1 no row, 2 no class row, 3 > 128 neighbours, 4 > 16 class rows
+  auto flag = [&](int e) {
+    int z = 0;
+    bad.compare_exchange_strong(z, e);
+  };
+  std::vector<uint32_t> nn(n);
+  par_for(n, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t i = lo; i < hi; ++i) {
       const uint32_t r = roots[i];
-      if (r >= V || pos[r] == 0xFFFFFFFFu) return fail(c, OSPF_E_RANGE, "twin levels: a root without a row");
-      rows.clear();
-      const size_t nb0 = out.nbl.size();
+      if (r >= V || pos[r] == kNo) {
+        flag(1);
+        nn[i] = 0;
+        continue;
+      }
+      uint32_t m = 0, prev = kNo;
       for (uint32_t e = c->h_prow[r]; e < c->h_prow[r + 1]; ++e) {
         const uint32_t x = c->h_pcolx[e];
-        if ((x & 0x80000000u) || x == r) continue;
-        if (out.nbl.size() == nb0 || out.nbl.back() != x) out.nbl.push_back(x);  // rows ascend
-        if ((c->h_nt[x >> 5] >> (x & 31)) & 1u) continue;  // overloaded: reaches only itself
-        const uint32_t k = cls[x];
-        const uint32_t row = k < rep.size() && rep[k] < V ? pos[rep[k]] : 0xFFFFFFFFu;
-        if (row == 0xFFFFFFFFu) return fail(c, OSPF_E_RANGE, "twin levels: a class row is missing");
-        rows.push_back(row);
+        if ((x & 0x80000000u) || x == r || x == prev) continue;  // rows ascend
+        prev = x;
+        ++m;
       }
-      if (out.nbl.size() - nb0 > 128)
-        return fail(c, OSPF_E_RANGE, "twin levels: more than 128 usable neighbours");
-      out.nbo.push_back((uint32_t)out.nbl.size());
-      uint32_t mask = 0;
-      for (uint32_t row : rows) {
-        uint32_t u = 0;
-        while (u < urow.size() && urow[u] != row) ++u;
-        if (u == urow.size()) {
-          if (u == ospf::kTwinMaxC)
-            return fail(c, OSPF_E_RANGE, "twin levels: more than 16 class rows in a group");
-          urow.push_back(row);
-        }
-        mask |= 1u << u;
-      }
-      out.rinfo.push_back(make_uint4(r, pos[r], mask, (uint32_t)nb0));
+      if (m > 128) flag(3);
+      nn[i] = m;
     }
-    urow.resize(ospf::kTwinMaxC, 0xFFFFFFFFu);
-    out.grow.insert(out.grow.end(), urow.begin(), urow.end());
+  });
+  out.nbo.assign(n + 1, 0u);
+  for (uint32_t i = 0; i < n; ++i) out.nbo[i + 1] = out.nbo[i] + nn[i];
+  out.nbl.resize(out.nbo[n]);
+  out.rinfo.resize(n);
+  out.grow.assign((size_t)ng * ospf::kTwinMaxC, kNo);
+  if (!bad.load())
+    par_for(ng, [&](uint32_t glo, uint32_t ghi) {
+      std::vector<uint32_t> rows;  // a root's class rows
+      for (uint32_t gi = glo; gi < ghi; ++gi) {
+        uint32_t* urow = out.grow.data() + (size_t)gi * ospf::kTwinMaxC;
+        uint32_t nu = 0;
+        for (uint32_t i = out.grp[gi]; i < out.grp[gi + 1]; ++i) {
+          const uint32_t r = roots[i];
+          rows.clear();
+          uint32_t w = out.nbo[i], prev = kNo;
+          for (uint32_t e = c->h_prow[r]; e < c->h_prow[r + 1]; ++e) {
+            const uint32_t x = c->h_pcolx[e];
+            if ((x & 0x80000000u) || x == r) continue;
+            if (x != prev) out.nbl[w++] = x;
+            prev = x;
+            if ((c->h_nt[x >> 5] >> (x & 31)) & 1u) continue;  // overloaded: reaches only itself
+            const uint32_t k = cls[x];
+            const uint32_t row = k < rep.size() && rep[k] < V ? pos[rep[k]] : kNo;
+            if (row == kNo) flag(2);
+            rows.push_back(row);
+          }
+          uint32_t mask = 0;
+          for (uint32_t row : rows) {
+            uint32_t u = 0;
+            while (u < nu && urow[u] != row) ++u;
+            if (u == nu) {
+              if (u == ospf::kTwinMaxC) {
+                flag(4);
+                break;
+              }
+              urow[nu++] = row;
+            }
+            mask |= 1u << u;
+          }
+          out.rinfo[i] = make_uint4(r, pos[r], mask, out.nbo[i]);
+        }
+      }
+    }, 64);
+  switch (bad.load()) {
+    case 1: return fail(c, OSPF_E_RANGE, "twin levels: a root without a row");
+    case 2: return fail(c, OSPF_E_RANGE, "twin levels: a class row is missing");
+    case 3: return fail(c, OSPF_E_RANGE, "twin levels: more than 128 usable neighbours");
+    case 4: return fail(c, OSPF_E_RANGE, "twin levels: more than 16 class rows in a group");
+    default: break;
   }
   return OSPF_OK;
 }

@@ -5,8 +5,12 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <atomic>
 #include <map>
 #include <string>
+#include <system_error>
+#include <thread>
 #include <vector>
 
 #include "spf_kernels.h"
@@ -98,6 +102,36 @@ struct ospf_ctx {
 };
 
 namespace ospf_int {
+
+// fn(lo, hi) over [0, n) on up to 16 host threads, chunks of `grain` taken
+// dynamically (a fabric's spines, first by name, have 20x the rows of the
+// rest: static slices left one thread with most of the work); serial when
+// threads are unavailable
+template <class F>
+void par_for(uint32_t n, F fn, uint32_t grain = 512) {
+  const uint32_t hw = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  const uint32_t T = std::min(hw, (n + grain - 1) / grain);
+  if (T <= 1) {
+    fn(0u, n);
+    return;
+  }
+  std::atomic<uint32_t> next{0};
+  auto work = [&]() {
+    for (;;) {
+      const uint32_t lo = next.fetch_add(grain);
+      if (lo >= n) return;
+      fn(lo, std::min(n, lo + grain));
+    }
+  };
+  std::vector<std::thread> th;
+  try {
+    for (uint32_t t = 1; t < T; ++t) th.emplace_back(work);
+  } catch (const std::system_error&) {  // fewer threads: the rest share the work
+  }
+  work();
+  for (auto& x : th) x.join();
+}
+
 
 int fail(ospf_ctx* c, int code, const std::string& msg);
 int hip_fail(ospf_ctx* c, hipError_t e, const char* what);

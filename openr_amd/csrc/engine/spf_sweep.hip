@@ -20,6 +20,7 @@
 #include <new>
 #include <numeric>
 #include <string>
+#include <atomic>
 #include <system_error>
 #include <thread>
 #include <vector>
@@ -72,32 +73,10 @@ struct Facts {
   uint32_t words(uint32_t v) const { return std::max(1u, (nbrs(v) + 31) / 32); }
 };
 
-// fn(lo, hi) over [0, n) on up to 16 host threads (the plan's per-node
-// loops; serial when threads are unavailable)
-template <class F>
-void par_for(uint32_t n, F fn, uint32_t grain = 2048) {
-  const uint32_t hw = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-  const uint32_t T = std::min(hw, (n + grain - 1) / grain);
-  if (T <= 1) {
-    fn(0u, n);
-    return;
-  }
-  std::vector<std::thread> th;
-  uint32_t done = 0;
-  try {
-    for (uint32_t t = 1; t < T; ++t) {
-      th.emplace_back(fn, (uint32_t)((uint64_t)n * t / T), (uint32_t)((uint64_t)n * (t + 1) / T));
-      done = t;
-    }
-  } catch (const std::system_error&) {  // no more threads: the rest here
-    fn((uint32_t)((uint64_t)n * (done + 1) / T), n);
-  }
-  fn(0u, (uint32_t)((uint64_t)n / T));
-  for (auto& x : th) x.join();
-}
-
 // stable sort on host threads: chunks stable-sorted in parallel, then merged
 // pairwise (left run first: stable)
+using ospf_int::par_for;
+
 template <class T, class Less>
 void par_stable_sort(std::vector<T>& v, Less less) {
   const uint32_t n = (uint32_t)v.size();
@@ -438,8 +417,10 @@ Twins twin_classes(const ospf_ctx* c) {
       for (uint32_t i = m; i < cnt[u]; ++i) lst[off[u] + i] = 0xFFFFFFFFu;  // (dups of an unsorted row)
       cnt[u] = m;
       const bool tr = !((c->h_nt[u >> 5] >> (u & 31)) & 1u);
+      // (independent mixes, summed: no dependent chain through a spine's row;
+      // a hash only -- classes are split by exact equality below)
       uint64_t h = tr ? 0x9E3779B97F4A7C15ull : 0xC2B2AE3D27D4EB4Full;
-      for (uint32_t i = 0; i < m; ++i) h = ospf::digest_mix(h ^ lst[off[u] + i]) + i;
+      for (uint32_t i = 0; i < m; ++i) h += ospf::digest_mix(lst[off[u] + i] ^ (i * 0x9E3779B97F4A7C15ull));
       key[u] = h;
     }
   });
