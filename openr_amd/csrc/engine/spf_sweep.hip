@@ -755,6 +755,8 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   const uint32_t V = s->V;
   const uint32_t hop = s->opts.flags & OSPF_HOP_COUNT;
   PlanLaps lap;
+  double leaf_tail = 0.0;
+  if (const char* x = getenv("OSPF_SWEEP_LEAF_TAIL")) leaf_tail = std::max(0.0, std::min(0.9, atof(x)));
   std::vector<uint8_t> leaf;
   if (!getenv("OSPF_SWEEP_NOLEAF")) leaf = leaf_set(f);
   else leaf.assign(V, 0);
@@ -900,9 +902,14 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   // so the next hops of the cover roots start while the other leaves' rows
   // are written
   lap("cover rows + twin levels set");
+  // (OSPF_SWEEP_MERGE_REPS: the BFS'd leaf representatives' next hops in
+  // their groups' leaf launch -- rows re-derived there, identical -- instead
+  // of a launch of their own that reads each one's neighbour rows alone)
+  const bool merge_reps = twin_lv && getenv("OSPF_SWEEP_MERGE_REPS") != nullptr;
   std::vector<uint32_t> reps, rest;
   for (uint32_t x : need_l) {
-    const bool first = twin_lv ? seed[x] != 0 : (!all_leaf_rows && tw.rep[tw.cls[x]] == x);
+    const bool first = twin_lv ? (seed[x] != 0 && !merge_reps)
+                               : (!all_leaf_rows && tw.rep[tw.cls[x]] == x);
     (first ? reps : rest).push_back(x);
   }
   std::vector<uint32_t> grp_r = leaf_groups(c, f, reps);
@@ -1297,6 +1304,55 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
         const uint32_t ngq = g1 - g0;
         u.fn = [=](hipStream_t strm) {
           return ospf_leaf_derive2_dev(c, dl, n, d_gq, ngq, kmax, lev, pitch, d_pos, lo, dist, nh,
+                                       dg2, strm);
+        };
+        s->step_comp += u.comp;
+        s->units.push_back(std::move(u));
+      }
+    } else if (nL > nR && leaf_tail > 0.0 && twin_lv && ngr >= 2) {
+      // the leaves in two launches on the main stream: the second waits for
+      // the largest cover next-hop launch, which so gets the GPU's share
+      // before it and no longer finishes alone after the leaves
+      // (OSPF_SWEEP_LEAF_TAIL = the second launch's share of the groups)
+      int big = -1;
+      for (size_t x = 0; x < s->units.size(); ++x)
+        if (s->units[x].name.rfind("derive_cap", 0) == 0 && s->units[x].record < 0 &&
+            (big < 0 || s->units[x].comp > s->units[big].comp))
+          big = (int)x;
+      const uint32_t gs = std::min(ngr - 1, std::max(1u, ngr - (uint32_t)(ngr * leaf_tail)));
+      int ev_tn = -1;
+      if (big >= 0) {
+        ev_tn = new_event(s);
+        if (ev_tn < 0) return ev_tn;
+        s->units[big].record = ev_tn;
+      }
+      std::vector<uint32_t> gq;
+      for (uint32_t g = gs; g <= ngr; ++g) gq.push_back(grp[g] - grp[gs]);
+      uint32_t* d_gq;
+      if ((rc = upload(s, &d_gq, gq))) return rc;
+      const uint32_t* lo = drop_rest ? d_lout : nullptr;
+      for (int part = 0; part < 2; ++part) {
+        ospf_sweep::Unit u;
+        u.name = part ? "leaf_tail" : "leaf";
+        u.kernel = "ospf_leaf_derive2_dev (leaf_derive_kernel: level + dist + next-hop rows of leaf "
+                   "roots from their neighbours' level rows)";
+        u.stream = 0;
+        const uint32_t i0 = part ? grp[gs] : 0u, i1 = part ? grp[ngr] : grp[gs];
+        const uint32_t n = i1 - i0, ngq = part ? ngr - gs : gs;
+        if (part) {
+          if (ev_tn >= 0) u.wait = {ev_tn};
+          u.record = ev_b;
+        }
+        u.n_roots = n;
+        u.W = 1;
+        u.comp = (uint64_t)n * 8ull * V;
+        const uint32_t* dl = d_l + nR + i0;
+        uint32_t* nh = lnh + (size_t)(nR + i0) * V;
+        ospf_digest* dg2 = dg + nR + i0;
+        const uint32_t* lo2 = lo ? lo + i0 : nullptr;
+        const uint32_t* gp = part ? d_gq : d_grp;
+        u.fn = [=](hipStream_t strm) {
+          return ospf_leaf_derive2_dev(c, dl, n, gp, ngq, kmax, lev, pitch, d_pos, lo2, dist, nh,
                                        dg2, strm);
         };
         s->step_comp += u.comp;
