@@ -397,6 +397,10 @@ __device__ __forceinline__ uint32_t bmin7(uint32_t a, uint32_t b) {
   const uint32_t m = (ge << 1) - (ge >> 7);  // 0xFF in the bytes where a >= b
   return (b & m) | (a & ~m);
 }
+// bit 7 of each byte: the 7-bit bytes of x and y are equal
+__device__ __forceinline__ uint32_t beq7(uint32_t x, uint32_t y) {
+  return ~((x ^ y) + 0x7F7F7F7Fu) & 0x80808080u;
+}
 
 // Level + dist rows of a root from its neighbour classes (twin Bellman).
 // dist(r, v) = 1 + min over the classes of the representative's row R_j(v)
@@ -460,13 +464,18 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
 #pragma unroll
     for (int q = 0; q < 4; ++q) kd[q] = ok && v0 + q < V ? g.dkey[2ull * (v0 + q)] : 0ull;
   };
-  uint32_t br[kTwinLvG], cur[kTwinLvG];
-  uint64_t bs[kTwinLvG], bh[kTwinLvG];
+  // distance part of each root's digest, per lane: reached, sum of dist
+  // (u32: <= V / 64 nodes x 125 per lane), sum of dkey * level split in
+  // sum(dkey_lo * level) (u64, one v_mad_u64_u32 a node) and
+  // sum(dkey_hi * level) mod 2^32 (the hash is mod 2^64)
+  uint32_t br[kTwinLvG], cur[kTwinLvG], bs[kTwinLvG], bhh[kTwinLvG];
+  uint64_t bl[kTwinLvG];
 #pragma unroll
   for (uint32_t j = 0; j < kTwinLvG; ++j) {
     br[j] = 0u;
     cur[j] = 0u;
-    bs[j] = bh[j] = 0ull;
+    bs[j] = bhh[j] = 0u;
+    bl[j] = 0ull;
   }
   const bool vec = (V & 3u) == 0;
   uint32_t xn[kTwinMaxC];
@@ -505,18 +514,28 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
       const uint32_t own = s_own[j];
       __builtin_nontemporal_store(L, reinterpret_cast<uint32_t*>(a.lev + (size_t)own * a.pitch + v0));
       if (v0 >= V) continue;
-      uint32_t dv[4];
+      // SWAR over the 4 nodes: reached bytes (< 0x7F, node < V), their
+      // levels summed, and the hash terms of the levels
+      uint32_t vb = ~beq7(L, 0x7F7F7F7Fu) & 0x80808080u;
+      if (V - v0 < 4u) vb &= (1u << (8u * (V - v0))) - 1u;
+      const uint32_t Lv = L & ((vb >> 7) * 0xFFu);
+      const uint32_t nv = (uint32_t)__builtin_popcount(vb);
+      const uint32_t t2 = (Lv & 0x00FF00FFu) + ((Lv >> 8) & 0x00FF00FFu);
+      br[j] += nv;
+      bs[j] += (t2 & 0xFFFFu) + (t2 >> 16) - nv;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const uint32_t l = (L >> (8 * q)) & 0xFFu;
-        dv[q] = l < 0x7Fu ? l - 1u : kInf;
-        if (l < 0x7Fu && v0 + q < V) {
-          br[j] += 1u;
-          bs[j] += l - 1u;
-          bh[j] += kd[q] * (uint64_t)l;
-        }
+        const uint32_t l = (Lv >> (8 * q)) & 0xFFu;
+        bl[j] += (uint64_t)(uint32_t)kd[q] * l;
+        bhh[j] += (uint32_t)(kd[q] >> 32) * l;
       }
       if (a.dist && !(s_umask[j] >> 31)) {  // bit 31: the root's next-hop launch writes it
+        uint32_t dv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t l = (L >> (8 * q)) & 0xFFu;
+          dv[q] = l < 0x7Fu ? l - 1u : kInf;
+        }
         uint32_t* drow = a.dist + (size_t)own * V + v0;
         if (vec) {
           store_row16(drow, make_uint4(dv[0], dv[1], dv[2], dv[3]));
@@ -531,17 +550,17 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
   if (!a.lev_digest) return;
 #pragma unroll
   for (uint32_t j = 0; j < kTwinLvG; ++j) {
-    uint64_t r64 = br[j];
+    uint64_t r64 = br[j], s64 = bs[j], h64 = bl[j] + ((uint64_t)bhh[j] << 32);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       r64 += shfl_xor64(r64, o);
-      bs[j] += shfl_xor64(bs[j], o);
-      bh[j] += shfl_xor64(bh[j], o);
+      s64 += shfl_xor64(s64, o);
+      h64 += shfl_xor64(h64, o);
     }
     if (lane == 0) {
       s_d[wave][j][0] = r64;
-      s_d[wave][j][1] = bs[j];
-      s_d[wave][j][2] = bh[j];
+      s_d[wave][j][1] = s64;
+      s_d[wave][j][2] = h64;
     }
   }
   __syncthreads();
