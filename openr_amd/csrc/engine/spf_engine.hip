@@ -841,6 +841,20 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
       return OSPF_OK;
     };
     if (npre) {  // beside the decremental kernels
+      // OSPF_KSP_PRESORT=1: longest ignore lists (most k = 1 paths) first
+      // (measured 21.3 vs 21.1 ms as found: off)
+      const char* ps = getenv("OSPF_KSP_PRESORT");
+      if (ps && atoi(ps) != 0) {
+        std::vector<uint32_t> pre(npre), cnt(n);
+        HIPCHK(c, hipMemcpyAsync(pre.data(), d_pre, npre * 4ull, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(cnt.data(), d_cnt, n * 4ull, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        std::stable_sort(pre.begin(), pre.end(), [&](uint32_t a, uint32_t b) {
+          return cnt[a] != cnt[b] ? cnt[a] > cnt[b] : a < b;
+        });
+        HIPCHK(c, hipMemcpyAsync(d_pre, pre.data(), npre * 4ull, hipMemcpyHostToDevice, fs));
+        HIPCHK(c, hipStreamSynchronize(fs));
+      }
       rc = rerun_list(d_pre, npre, 3);
       if (rc) return rc;
     }
