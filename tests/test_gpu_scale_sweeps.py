@@ -229,3 +229,59 @@ def test_m1m_wmulti_sweep_part():
     note("triangle + tight last hops")
     sw.close()
     eng.close()
+
+
+
+@pytest.mark.timeout(900)
+def test_f100k_weighted_sweep_whole_rows_vs_scipy():
+    """Whole dist + next-hop rows of the weighted F100k (metrics 1..64)
+    all-sources sweep (cover SPF + derived leaves) against an independent
+    solver: scipy's Dijkstra from the root and from each of its neighbours,
+    next hops = the neighbours n with w(r, n) + dist(n, v) == dist(r, v)
+    (LinkState.cpp:885-901; every node is transit here). Racks, fabric
+    switches and a spine (56 next-hop words); the reference-shaped runSpf
+    text takes minutes per root at this size with metrics."""
+    from scipy.sparse import csr_matrix
+    from scipy.sparse.csgraph import dijkstra
+    st = T.fabric(pods=1781, planes=8, weighted_seed=7)
+    ls = LinkState()
+    ls.apply(st)
+    csr = ls.csr()
+    names = ls.node_names()
+    V = len(names)
+    eng = Engine()
+    eng.load(csr)
+    sw = Sweep(eng)
+    sw.run()
+    eng.sync()
+    note(f"weighted F100k sweep ({sw.mode})")
+    rp, col = csr["row_ptr"].astype(np.int64), csr["col"].astype(np.int64)
+    up = csr["edge_up"] != 0
+    row = np.repeat(np.arange(V), np.diff(rp))
+    # parallel links: the smallest metric per (row, neighbour)
+    key = row[up] * V + col[up]
+    order = np.lexsort((csr["metric"][up], key))
+    first = np.ones(order.size, bool)
+    first[1:] = key[order][1:] != key[order][:-1]
+    sel = order[first]
+    G = csr_matrix((csr["metric"][up][sel].astype(np.float64), (row[up][sel], col[up][sel])), shape=(V, V))
+    for r in [names.index(x) for x in ("3-2-2", "3-1200-40", "2-17-3", "2-1500-0", "1-5-30")]:
+        nb = np.unique(col[rp[r]:rp[r + 1]])
+        nb = nb[nb != r]
+        W = eng.nh_words(int(r))
+        dist, nh = sw.rows(np.array([r], np.uint32), W)
+        D = dijkstra(G, indices=np.concatenate([[r], nb]))
+        d0 = np.where(np.isinf(D[0]), 0xFFFFFFFF, D[0]).astype(np.uint64)
+        assert np.array_equal(dist[0].astype(np.uint64), d0), names[r]
+        want = np.zeros((V, W), np.uint32)
+        for k, n in enumerate(nb):
+            wr = G[r, n]
+            if wr == 0:
+                continue  # no up link to n
+            tight = np.isfinite(D[0]) & (wr + D[1 + k] == D[0])
+            tight[r] = False
+            want[tight, k >> 5] |= np.uint32(1 << (k & 31))
+        assert np.array_equal(nh[0], want), names[r]
+        note(f"weighted F100k whole rows of {names[r]} == scipy Dijkstra")
+    sw.close()
+    eng.close()
