@@ -635,6 +635,7 @@ struct DecrLdsT {
   uint32_t stack[kStack];
   uint32_t pend[64];   // nodes whose hint was just lost (their supports to count)
   uint32_t nkeys, naff, ovf, run, npend;
+  uint32_t why;        // a failed prepare: 0 an LDS budget, 1 the edge budget, 2 the ignore list
   uint64_t t3;         // wall clock at step (3) (phase timing, t.ctr[16..])
 };
 using DecrSmall = DecrLdsT<512, 192, 256, 512, 4096>;  // ~10 KB: ~16 runs per CU in flight
@@ -760,9 +761,13 @@ __device__ bool decr_prepare(L_& L, const DevGraph& g, const TraceArgs& t, uint3
   const uint32_t* gign = t.ign + (size_t)i * t.stride;
   nign = min(t.ign_cnt[i], t.stride);
   if (nign > L_::kIgn) {
-    if (lane == 0) atomicAdd(&t.ctr[8], 1u);
+    if (lane == 0) {
+      atomicAdd(&t.ctr[8], 1u);
+      L.why = 2u;
+    }
     return false;
   }
+  if (lane == 0) L.why = 0u;
   for (uint32_t k = lane; k < L_::kMap; k += kWave) {
     L.keys[k] = 0u;
     L.vals[k] = 0u;
@@ -881,6 +886,7 @@ __device__ bool decr_prepare(L_& L, const DevGraph& g, const TraceArgs& t, uint3
     if (scanned > L_::kEdge) {
       if (lane == 0) {
         L.ovf = 1u;
+        L.why = 1u;
         atomicAdd(&t.ctr[10], 1u);
       }
       break;
@@ -1000,7 +1006,18 @@ __global__ void __launch_bounds__(64) ksp_decr_kernel(DevGraph g, TraceArgs t) {
       if (prep) atomicAdd((unsigned long long*)&clk[1], (unsigned long long)(c1 - t3));
     }
     if (!prep) {
-      fallback();
+      // past an LDS budget (affected set, map, pending nodes): the 16-wave
+      // kernel redoes it with 4-8x budgets and traces it from the start; past
+      // the edge budget or the ignore list: the full reruns
+      if (t.budget && ((volatile uint32_t&)L.why) == 0u) {
+        if (lane == 0) {
+          out[0] = 0u;
+          atomicAdd(&t.ctr[2], 1u);  // (decided there; un-counted if it falls back)
+          t.heavy[atomicAdd(&t.heavy_ctr[0], 1u)] = i;
+        }
+      } else {
+        fallback();
+      }
       continue;
     }
     const uint32_t dst = t.dsts[i];
@@ -1214,16 +1231,16 @@ __global__ void __launch_bounds__(1024) ksp_decr_heavy_kernel(DevGraph g, TraceA
       const bool ok = decr_prepare(L, g, t, i, lane, nign, na);
       if (lane == 0) {
         H.ctl[3] = ok ? nign : kInf;
-        if (!ok) atomicOr(&t.err[0], 2048u);  // cannot happen: it fit before
+        if (!ok) {  // past these budgets too: the full reruns
+          t.fb[atomicAdd(&t.ctr[1], 1u)] = i;
+          atomicSub(&t.ctr[2], 1u);
+        }
       }
     }
     for (uint32_t k = threadIdx.x; k < t.dead_words; k += blockDim.x) dead[k] = 0u;
     __syncthreads();
     nign = H.ctl[3];
-    if (nign == kInf) {
-      if (threadIdx.x == 0) t.status[i] |= OSPF_KSP_OVF2;
-      continue;
-    }
+    if (nign == kInf) continue;
     const uint64_t c1 = wall_clock64();
     Tracer<DistDecr<DecrHeavy>, kHash> tr{g, t, i, lane, t.src, t.dsts[i], L.ign, nign, L.hash, dead,
                                           DistDecr<DecrHeavy>{t.rows, &L}};
