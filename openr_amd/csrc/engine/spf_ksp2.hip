@@ -1006,10 +1006,13 @@ __global__ void __launch_bounds__(64) ksp_decr_kernel(DevGraph g, TraceArgs t) {
       if (prep) atomicAdd((unsigned long long*)&clk[1], (unsigned long long)(c1 - t3));
     }
     if (!prep) {
-      // past an LDS budget (affected set, map, pending nodes): the 16-wave
-      // kernel redoes it with 4-8x budgets and traces it from the start; past
-      // the edge budget or the ignore list: the full reruns
-      if (t.budget && ((volatile uint32_t&)L.why) == 0u) {
+      // past the map or pending-node budget: the 16-wave kernel redoes it
+      // with 8x budgets and traces it from the start; past the affected-set,
+      // edge or ignore-list budget (a large change, whose single-wave
+      // prepare there would be slow: OSPF_KSP_SRCCUT=0 at F100k sends 7 such
+      // runs and takes 58 ms): the full reruns
+      if (t.budget && ((volatile uint32_t&)L.why) == 0u &&
+          ((volatile uint32_t&)L.naff) <= DecrSmall::kAff) {
         if (lane == 0) {
           out[0] = 0u;
           atomicAdd(&t.ctr[2], 1u);  // (decided there; un-counted if it falls back)
