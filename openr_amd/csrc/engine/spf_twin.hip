@@ -419,6 +419,7 @@ __device__ __forceinline__ uint32_t beq7(uint32_t x, uint32_t y) {
 // neighbours' positions (each root's sorted neighbour list walked by a
 // cursor) and stores 256 B of level row + 1 KB of dist row per instruction.
 // The distance part of each root's digest is stored (not added).
+template <bool PRE>
 __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvPlan a) {
   __shared__ uint32_t s_nb[kTwinLvG][kMaxK];  // usable neighbours (ascending), per root
   __shared__ uint32_t s_nnb[kTwinLvG], s_root[kTwinLvG], s_own[kTwinLvG], s_umask[kTwinLvG];
@@ -478,18 +479,24 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
     bl[j] = 0ull;
   }
   const bool vec = (V & 3u) == 0;
-  uint32_t xn[kTwinMaxC];
+  // PRE: the next chunk's rows loaded before this one is used (24 more
+  // registers: 3 waves per SIMD instead of 4)
+  uint32_t xn[PRE ? kTwinMaxC : 1];
   uint64_t kdn[4];
-  load_x(cb + wave, xn, kdn);
+  if constexpr (PRE) load_x(cb + wave, xn, kdn);
   for (uint32_t c = cb + wave; c < ce; c += kWaves) {
     const uint32_t c0 = c * 256u, v0 = c0 + 4u * lane;
     uint32_t x[kTwinMaxC];
     uint64_t kd[4];
+    if constexpr (PRE) {
 #pragma unroll
-    for (uint32_t u = 0; u < kTwinMaxC; ++u) x[u] = xn[u];
+      for (uint32_t u = 0; u < kTwinMaxC; ++u) x[u] = xn[u];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) kd[q] = kdn[q];
-    load_x(c + kWaves, xn, kdn);
+      for (int q = 0; q < 4; ++q) kd[q] = kdn[q];
+      load_x(c + kWaves, xn, kdn);
+    } else {
+      load_x(c, x, kd);
+    }
     if (v0 >= a.pitch) continue;  // no wave-level work below (cursors are per wave: see skip)
 #pragma unroll
     for (uint32_t j = 0; j < kTwinLvG; ++j) {
@@ -617,7 +624,12 @@ hipError_t launch_twin_levels(const DevGraph& g, const TwinLvPlan& a0, hipStream
   if (a.lev_digest)
     hipLaunchKernelGGL(twin_zero_kernel, dim3((a.n + 255u) / 256u), dim3(256), 0, s, a.rinfo, a.n,
                        a.lev_digest);
-  hipLaunchKernelGGL(twin_levels_kernel, dim3(a.ngroups * a.parts), dim3(kBlock), 0, s, g, a);
+  // (OSPF_TWIN_PREFETCH=1: the software-pipelined variant, 3 waves per SIMD)
+  static const bool pre = getenv("OSPF_TWIN_PREFETCH") != nullptr;
+  if (pre)
+    hipLaunchKernelGGL(twin_levels_kernel<true>, dim3(a.ngroups * a.parts), dim3(kBlock), 0, s, g, a);
+  else
+    hipLaunchKernelGGL(twin_levels_kernel<false>, dim3(a.ngroups * a.parts), dim3(kBlock), 0, s, g, a);
   return hipGetLastError();
 }
 }  // namespace ospf
