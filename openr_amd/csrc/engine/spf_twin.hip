@@ -619,8 +619,12 @@ hipError_t launch_twin_levels(const DevGraph& g, const TwinLvPlan& a0, hipStream
   TwinLvPlan a = a0;
   // parts of the chunk range per group: ~4096 blocks, >= 8 chunks each
   const uint32_t nchunks = (a.pitch + 255u) / 256u;
+  static const uint32_t want = [] {
+    const char* e = getenv("OSPF_TWIN_LV_BLOCKS");
+    return e ? (uint32_t)std::max(1, atoi(e)) : 4096u;
+  }();
   if (!a.parts)
-    a.parts = std::max(1u, std::min(std::max(1u, nchunks / 8u), 4096u / std::max(1u, a.ngroups)));
+    a.parts = std::max(1u, std::min(std::max(1u, nchunks / 8u), want / std::max(1u, a.ngroups)));
   if (a.lev_digest)
     hipLaunchKernelGGL(twin_zero_kernel, dim3((a.n + 255u) / 256u), dim3(256), 0, s, a.rinfo, a.n,
                        a.lev_digest);
