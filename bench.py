@@ -240,6 +240,12 @@ def main():
     ap.add_argument("--dist-parity", type=int, default=0,
                     help="N>1: rank 0 checks the gathered digests of the last timed step "
                          "for this many roots against the CPU restatement")
+    ap.add_argument("--no-probe", action="store_true",
+                    help="sweeps: skip the store-bandwidth probe beside the roofline")
+    ap.add_argument("--ab", default="",
+                    help='sweeps: in-process A/B of engine env knobs, e.g. "OSPF_LEAF_CTILES=20;'
+                         'OSPF_LEAF_GROUP_MAJOR=1" (variants ";"-separated, settings ",")')
+    ap.add_argument("--ab-rounds", type=int, default=3)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -584,6 +590,7 @@ def sweep_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, 
                       if tr else None})
     dom = max(units, key=lambda u: u["isolated_launch_ms"])
     step_s = dt / args.steps
+    probe = store_probe(eng, V, dom, args) if not args.no_probe else None
     roofline = {
         "bound": "hbm", "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": dom["frac"], "traffic": dom["traffic"], "kernel": dom["kernel"],
@@ -601,6 +608,12 @@ def sweep_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, 
                 "sweep's compulsory bytes / ms_per_step. traffic = measured HBM bytes per launch "
                 "(rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/<round>/pmc_traffic.json)",
     }
+    if probe:
+        roofline["store_probe"] = probe
+        best = max(probe.get("stream_GBs") or 0.0, probe.get("rows_chunk_GBs") or 0.0,
+                   probe.get("rows_group_GBs") or 0.0)
+        if best > 0:
+            roofline["frac_of_box_store_rate"] = round(dom["achieved"] / best, 4)
     cfg = {"mode": sw.mode, "hip_graph": sw.hip_graph, "roots_this_rank": n,
            "rows_this_rank": sw.n_rows, "device_bytes": sw.device_bytes,
            "closure_over_roots": round(sw.n_rows / max(1, n), 4),
@@ -627,6 +640,8 @@ def sweep_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, 
         "total_ms": round((t3 - t1) * 1e3, 1),
         "note": "a new graph version: ospf_sweep_create(OSPF_SWEEP_DEFER) + the first (eager, "
                 "no HIP graph) run, as odl::LinkState::prefetchAllSources pays it"}
+    if args.ab:
+        roofline["ab"] = ab_sweeps(args, eng, mode, part, n_parts, main_s, step_digest, sw_roots)
     if K > 1:  # one part per rank of a K x N partition: the parts' roots, not V
         tot = n
         if dist_on:
@@ -649,6 +664,78 @@ def sweep_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, 
                trav_edges=trav * args.steps)
     if dist_on:
         torch.distributed.destroy_process_group()
+
+
+def store_probe(eng, V: int, dom: dict, args):
+    """The box's own HBM store rate beside the dominant launch
+    (ospf_probe_store, HIP events): the same bytes as the dominant launch's
+    dist + next-hop rows -- `rows` = its roots -- written (0) in address
+    order, (1) in the leaf launch's block shape, chunk-major, (2) the same
+    group-major. A slow box shows in all three; a code regression only in
+    the launch's own time."""
+    if V % 4 or dom["roots_per_launch"] <= 0:
+        return None
+    rows = int(dom["roots_per_launch"])
+    out = {"bytes": 2 * rows * V * 4, "rows": rows, "group": 48, "ctiles": 6,
+           "note": "ospf_probe_store: 16-B non-temporal stores of 2 x rows x V u32 (the dominant "
+                   "launch's dist + next-hop rows), median of 3 HIP-event-timed launches after one "
+                   "untimed; rows_* = blocks of 48 rows x 6 tiles of 1,024 nodes, the leaf "
+                   "launch's shape"}
+    for pat in ("stream", "rows_chunk", "rows_group"):
+        try:
+            ms = float(np.median(eng.probe_store(pat, V, rows, 48, 6, reps=3)))
+        except Exception as e:  # noqa: BLE001 -- evidence only (e.g. no room beside the sweep)
+            out[pat + "_error"] = str(e)
+            continue
+        out[pat + "_ms"] = round(ms, 3)
+        out[pat + "_GBs"] = round(out["bytes"] / (ms / 1e3) / 1e9, 1)
+    return out
+
+
+def ab_sweeps(args, eng, mode, part, n_parts, main_s, base_digest, roots):
+    """In-process A/B of engine knobs (env variables read when a sweep is
+    created / captured): `--ab "A=1;B=2,C=3"` times the base sweep and each
+    variant, interleaved over --ab-rounds rounds, each `--steps` replays,
+    and checks every variant's digests against the base run's timed step."""
+    variants = [""] + [v for v in args.ab.split(";") if v.strip()]
+    res = {v or "base": [] for v in variants}
+    parity = {}
+    for _ in range(args.ab_rounds):
+        for v in variants:
+            saved = {}
+            for kv in filter(None, v.split(",")):
+                k, val = kv.split("=", 1)
+                saved[k] = os.environ.get(k)
+                os.environ[k] = val
+            try:
+                sw = eng.sweep(mode=mode, part=part, n_parts=n_parts, hip_graph=args.graph != "off")
+                for _w in range(2):
+                    sw.run(main_s.cuda_stream)
+                torch.cuda.synchronize()
+                sw.poison(main_s.cuda_stream)
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                for _s in range(args.steps):
+                    sw.run(main_s.cuda_stream)
+                torch.cuda.synchronize()
+                res[v or "base"].append((time.perf_counter() - t) / args.steps * 1e3)
+                eng.sync(main_s.cuda_stream)
+                g = torch.zeros((max(1, sw.n_roots), 3), dtype=torch.int64, device=main_s.device)
+                sw.digests_dev(g.data_ptr(), main_s.cuda_stream)
+                d = g.cpu().numpy().view(np.uint64)
+                ok = all(np.array_equal(d[j], base_digest[int(r)]) for j, r in enumerate(sw.roots)
+                         if int(r) in base_digest)
+                parity[v or "base"] = parity.get(v or "base", True) and bool(ok)
+                sw.close()
+            finally:
+                for k, old in saved.items():
+                    if old is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = old
+    return [{"env": k, "ms_per_step": [round(x, 3) for x in ms],
+             "ms_median": round(float(np.median(ms)), 3), "digests_equal_base": parity.get(k)}
+            for k, ms in res.items()]
 
 
 def parity_sample(csr, V: int, k: int = 256):

@@ -57,6 +57,10 @@ typedef struct oadj_change {
   int32_t link_attributes_changed;
   int32_t node_label_changed;
   int32_t n_added_links;
+  /* odl_apply_kvs / odl_apply_publication: 1 when this key's value failed to
+   * decode; the key was skipped and the rest applied (Decision::
+   * updateKeyInLsdb catches and logs it, Decision.cpp:742-806) */
+  int32_t decode_error;
 } oadj_change;
 
 #ifdef __cplusplus

@@ -78,10 +78,18 @@ int odl_apply_kvs(odl_ls* ls, uint32_t n, const char* const* keys, const uint8_t
                   const char* my_node, oadj_change* changes);
 /* Same from a whole compact-thrift thrift::Publication (KvStore.thrift:270-
  * 320) in `buf`: keyVals in wire order, then expiredKeys. n_changes_out (may
- * be NULL) = number of records; changes (may be NULL) holds up to
- * max_changes of them. */
+ * be NULL) = number of records. When `changes` is not NULL and the records
+ * do not fit max_changes, nothing is applied and ODL_E_SMALL is returned with
+ * *n_changes_out set (call again with room for them). A publication whose
+ * area field is set and differs from this LinkState's area is rejected
+ * (Decision::processPublication picks the LinkState by the area,
+ * Decision.cpp:847-854; the caller routes it). */
+#define ODL_E_SMALL (-2)
 int odl_apply_publication(odl_ls* ls, const uint8_t* buf, uint64_t len, const char* my_node,
                           oadj_change* changes, uint32_t max_changes, uint32_t* n_changes_out);
+/* The last value odl_apply_kvs / odl_apply_publication could not decode
+ * ("" when none; owned by ls) and the number of such values so far. */
+const char* odl_last_decode_error(const odl_ls* ls, uint64_t* n_errors);
 /* Decode n compact-thrift AdjacencyDatabase values into a columnar stream
  * (include/openr_adjdb.h; adj_only_used_by_other filled, db_delete all 0),
  * owned by *out until odl_adjdbs_free. NULL on malformed input, with the

@@ -665,6 +665,21 @@ int ospf_msweep_owner(const ospf_msweep* ms, uint32_t root, uint32_t* slot);
  * (LinkState.cpp:843). */
 uint64_t ospf_spf_runs(const ospf_ctx* ctx);
 
+/* Box calibration (no reference counterpart: measurement).
+ * The HBM store rate of this device, timed with HIP events: 2 * rows * V * 4
+ * bytes written with 16-B non-temporal stores per launch, `reps` timed
+ * launches after one untimed one, ms_out[reps]. pattern 0 = one buffer in
+ * address order; 1 = two [rows][V] u32 arrays written the way the leaf
+ * launch writes its dist and next-hop rows (blocks of `group` rows x
+ * `ctiles` 1,024-node tiles, chunk-major); 2 = the same blocks group-major.
+ * Allocates (and frees) its own buffer: OSPF_E_NOMEM when it does not fit.
+ * V must be a multiple of 4. */
+#define OSPF_PROBE_STREAM 0u
+#define OSPF_PROBE_ROWS_CHUNK 1u
+#define OSPF_PROBE_ROWS_GROUP 2u
+int ospf_probe_store(ospf_ctx* ctx, uint32_t pattern, uint32_t V, uint32_t rows, uint32_t group,
+                     uint32_t ctiles, uint32_t reps, float* ms_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -42,7 +42,7 @@ ENGINE_SYMBOLS = [
     "ospf_multi_open", "ospf_multi_close", "ospf_multi_last_error", "ospf_multi_size",
     "ospf_multi_ctx", "ospf_multi_load_graph", "ospf_msweep_create", "ospf_msweep_destroy",
     "ospf_msweep_run", "ospf_msweep_digests", "ospf_msweep_part", "ospf_msweep_owner",
-    "ospf_msweep_gather_backend",
+    "ospf_msweep_gather_backend", "ospf_probe_store",
 ]
 DECISION_SYMBOLS = [
     "odl_create", "odl_create_multi", "odl_all_sources_prefetch", "odl_all_sources_digests",
@@ -51,6 +51,7 @@ DECISION_SYMBOLS = [
     "odl_spf_runs", "odl_set_incremental", "odl_set_host_spf", "odl_incremental_stats", "odl_topology_stats", "odl_num_nodes", "odl_num_links", "odl_spf_digests", "odl_spf_prefetch",
     "odl_ksp2_text", "odl_route_text", "odl_route_db_text", "odl_route_db_bin", "odl_free_buf", "odl_path_a_in_b", "odl_ucmp_text", "odl_csr_size", "odl_csr_export", "odl_node_name", "odl_node_id",
     "odl_apply_kvs", "odl_apply_publication", "odl_node_patches", "odl_shard_stats", "odl_route_db_multi_text", "odl_adjdbs_decode", "odl_adjdbs_stream", "odl_adjdbs_error", "odl_adjdbs_free",
+    "odl_last_decode_error",
 ]
 
 
@@ -216,6 +217,7 @@ def engine() -> C.CDLL:
         L.ospf_msweep_owner.argtypes = [vp, u32, C.POINTER(u32)]
         L.ospf_msweep_gather_backend.argtypes = [vp]
         L.ospf_msweep_gather_backend.restype = u32
+        L.ospf_probe_store.argtypes = [vp, u32, u32, u32, u32, u32, u32, vp]
         _engine = L
     return _engine
 
@@ -279,6 +281,8 @@ def decision() -> C.CDLL:
         L.odl_adjdbs_error.restype = cp
         L.odl_adjdbs_free.argtypes = [vp]
         L.odl_adjdbs_free.restype = None
+        L.odl_last_decode_error.argtypes = [vp, C.POINTER(u64)]
+        L.odl_last_decode_error.restype = cp
         L.odl_set_host_spf.argtypes = [vp, i32]
         L.odl_set_host_spf.restype = None
         L.odl_incremental_stats.argtypes = [vp, vp]

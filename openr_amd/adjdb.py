@@ -75,6 +75,7 @@ class oadj_change(C.Structure):  # noqa: N801
         ("link_attributes_changed", C.c_int32),
         ("node_label_changed", C.c_int32),
         ("n_added_links", C.c_int32),
+        ("decode_error", C.c_int32),
     ]
 
 

@@ -23,7 +23,7 @@ ENGINE_SRC = [os.path.join(PKG, "csrc", "engine", f)
               for f in ("spf_kernels.hip", "spf_bfs.hip", "spf_msbfs.hip", "spf_ksp2.hip",
                         "spf_dial.hip", "spf_wdial.hip", "spf_wderive.hip", "spf_levels.hip",
                         "spf_cover.hip", "spf_msdist.hip", "spf_update.hip", "spf_leaf.hip", "spf_twin.hip", "spf_small.hip",
-                        "spf_engine.hip",
+                        "spf_probe.hip", "spf_engine.hip",
                         "spf_sweep.hip")]
 DECISION_SRC = [os.path.join(PKG, "csrc", "decision", f)
                 for f in ("link_state.cpp", "spf_solver.cpp", "adjdb_thrift.cpp", "decision_capi.cpp")]

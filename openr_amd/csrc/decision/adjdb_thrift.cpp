@@ -65,6 +65,16 @@ struct Reader {
   [[noreturn]] void bad(const char* what) const {
     throw std::runtime_error(std::string("compact thrift: ") + what);
   }
+  // one level of struct / list / set / map nesting while skipping: bounded,
+  // so a value of nested containers cannot run the decoding thread's stack out
+  static constexpr int kMaxDepth = 64;
+  struct Nest {
+    Reader& r;
+    explicit Nest(Reader& x) : r(x) {
+      if (++r.depth > kMaxDepth) r.bad("nesting too deep");
+    }
+    ~Nest() { --r.depth; }
+  };
   uint8_t byte() {
     if (p >= end) bad("truncated");
     return *p++;
@@ -140,6 +150,7 @@ struct Reader {
         return;
       case kList:
       case kSet: {
+        Nest nest(*this);
         uint8_t et;
         uint64_t n;
         list_header(et, n);
@@ -147,9 +158,11 @@ struct Reader {
         return;
       }
       case kMap: {
+        Nest nest(*this);
         const uint64_t n = varint();
         if (!n) return;
         const uint8_t kv = byte();
+        if (n > (uint64_t)(end - p)) bad("map size past the end");  // >= 1 byte per entry
         for (uint64_t i = 0; i < n; ++i) {
           skip_elem(kv >> 4);
           skip_elem(kv & 0x0F);
@@ -157,11 +170,10 @@ struct Reader {
         return;
       }
       case kStruct: {
-        if (++depth > 64) bad("nesting too deep");
+        Nest nest(*this);
         int16_t last = 0, id;
         uint8_t t;
         while (field(last, id, t)) skip(t);
-        --depth;
         return;
       }
       default:
@@ -299,10 +311,19 @@ std::vector<LinkStateChange> LinkState::applyKvs(const std::vector<KvIn>& kvs,
   for (uint32_t i = 0; i < kvs.size(); ++i)
     if (kvs[i].hasValue && kvs[i].key.substr(0, kAdj.size()) == kAdj) which.push_back(i);
   std::vector<AdjacencyDatabase> dbs(which.size());
+  // a value that fails to decode skips its own key only (updateKeyInLsdb
+  // catches the deserialization error, logs it and returns, Decision.cpp:742-806)
+  std::vector<std::string> errs(which.size());
   parallelFor((uint32_t)which.size(), [&](uint32_t lo, uint32_t hi) {
     for (uint32_t k = lo; k < hi; ++k) {
       const KvIn& kv = kvs[which[k]];
-      thrift_compact::decodeAdjacencyDatabase((const uint8_t*)kv.value.data(), kv.value.size(), dbs[k]);
+      try {
+        thrift_compact::decodeAdjacencyDatabase((const uint8_t*)kv.value.data(), kv.value.size(),
+                                                dbs[k]);
+      } catch (const std::exception& e) {
+        errs[k] = "key " + std::string(kv.key) + ": " + e.what();
+        continue;
+      }
       if (myNodeName) {  // filterUnuseableAdjacency (Decision.cpp:568-600)
         auto& adjs = dbs[k].adjacencies;
         adjs.erase(std::remove_if(adjs.begin(), adjs.end(),
@@ -314,8 +335,21 @@ std::vector<LinkStateChange> LinkState::applyKvs(const std::vector<KvIn>& kvs,
     }
   }, 64);
   std::vector<LinkStateChange> out(kvs.size() + expired.size());
-  const auto chs = updateAdjacencyDatabases(dbs);
-  for (size_t k = 0; k < which.size(); ++k) out[which[k]] = chs[k];
+  std::vector<AdjacencyDatabase> good;
+  std::vector<uint32_t> goodAt;
+  good.reserve(dbs.size());
+  for (size_t k = 0; k < which.size(); ++k) {
+    if (!errs[k].empty()) {
+      out[which[k]].decodeError = true;
+      lastDecodeError_ = errs[k];
+      ++decodeErrors_;
+      continue;
+    }
+    good.push_back(std::move(dbs[k]));
+    goodAt.push_back(which[k]);
+  }
+  const auto chs = updateAdjacencyDatabases(good);
+  for (size_t k = 0; k < goodAt.size(); ++k) out[goodAt[k]] = chs[k];
   for (size_t j = 0; j < expired.size(); ++j)
     if (expired[j].substr(0, kAdj.size()) == kAdj)
       out[kvs.size() + j] = deleteAdjacencyDatabase(nodeNameFromKey(expired[j]));

@@ -78,6 +78,11 @@ void pathsText(std::ostringstream& os, const std::vector<odl::Path>& paths) {
   }
 }
 
+oadj_change changeRecord(const odl::LinkStateChange& c) {
+  return oadj_change{c.topologyChanged, c.linkAttributesChanged, c.nodeLabelChanged,
+                     (int32_t)c.addedLinks.size(), c.decodeError};
+}
+
 template <class F>
 auto guard(odl_ls* h, F&& f, decltype(f()) bad) -> decltype(f()) {
   if (!h) return bad;
@@ -159,8 +164,7 @@ int odl_apply(odl_ls* h, const oadj_stream* s, uint32_t first, uint32_t count,
                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
       const auto chs = h->ls.updateAdjacencyDatabases(dbs);
       for (uint32_t k = 0; changes && k < count; ++k)
-        changes[k] = oadj_change{chs[k].topologyChanged, chs[k].linkAttributesChanged,
-                                 chs[k].nodeLabelChanged, (int32_t)chs[k].addedLinks.size()};
+        changes[k] = changeRecord(chs[k]);
       return 0;
     }
     for (uint32_t k = 0; k < count; ++k) {
@@ -189,8 +193,7 @@ int odl_apply(odl_ls* h, const oadj_stream* s, uint32_t first, uint32_t count,
         ch = h->ls.updateAdjacencyDatabase(db);
       }
       if (changes)
-        changes[k] = oadj_change{ch.topologyChanged, ch.linkAttributesChanged,
-                                 ch.nodeLabelChanged, (int32_t)ch.addedLinks.size()};
+        changes[k] = changeRecord(ch);
     }
     return 0;
   }, -1);
@@ -256,9 +259,7 @@ int odl_apply_kvs(odl_ls* h, uint32_t n, const char* const* keys, const uint8_t*
     std::vector<std::string_view> exp(expired, expired + n_expired);
     const std::string me = my_node ? my_node : "";
     const auto chs = h->ls.applyKvs(kvs, exp, my_node ? &me : nullptr);
-    for (size_t k = 0; changes && k < chs.size(); ++k)
-      changes[k] = oadj_change{chs[k].topologyChanged, chs[k].linkAttributesChanged,
-                               chs[k].nodeLabelChanged, (int32_t)chs[k].addedLinks.size()};
+    for (size_t k = 0; changes && k < chs.size(); ++k) changes[k] = changeRecord(chs[k]);
     return 0;
   }, -1);
 }
@@ -269,17 +270,25 @@ int odl_apply_publication(odl_ls* h, const uint8_t* buf, uint64_t len, const cha
     if (!buf && len) throw std::invalid_argument("null publication buffer");
     odl::PublicationView pv;
     odl::thrift_compact::parsePublication(buf, (size_t)len, pv);
+    if (!pv.area.empty() && pv.area != h->ls.area())
+      throw std::invalid_argument("publication of area '" + std::string(pv.area) +
+                                  "' given to the LinkState of area '" + h->ls.area() + "'");
+    const size_t nrec = pv.keyVals.size() + pv.expiredKeys.size();
+    if (n_changes_out) *n_changes_out = (uint32_t)nrec;
+    if (changes && nrec > max_changes) return ODL_E_SMALL;  // nothing applied
     std::vector<odl::LinkState::KvIn> kvs(pv.keyVals.size());
     for (size_t i = 0; i < kvs.size(); ++i)
       kvs[i] = odl::LinkState::KvIn{pv.keyVals[i].key, pv.keyVals[i].value, pv.keyVals[i].hasValue};
     const std::string me = my_node ? my_node : "";
     const auto chs = h->ls.applyKvs(kvs, pv.expiredKeys, my_node ? &me : nullptr);
-    if (n_changes_out) *n_changes_out = (uint32_t)chs.size();
-    for (size_t k = 0; changes && k < chs.size() && k < max_changes; ++k)
-      changes[k] = oadj_change{chs[k].topologyChanged, chs[k].linkAttributesChanged,
-                               chs[k].nodeLabelChanged, (int32_t)chs[k].addedLinks.size()};
+    for (size_t k = 0; changes && k < chs.size(); ++k) changes[k] = changeRecord(chs[k]);
     return 0;
   }, -1);
+}
+
+const char* odl_last_decode_error(const odl_ls* h, uint64_t* n_errors) {
+  if (n_errors) *n_errors = h ? h->ls.decodeErrors() : 0;
+  return h ? h->ls.lastDecodeError().c_str() : "";
 }
 
 void odl_set_host_spf(odl_ls* h, int on) {

@@ -332,6 +332,9 @@ struct LinkStateChange {
   bool linkAttributesChanged = false;
   bool nodeLabelChanged = false;
   std::vector<LinkPtr> addedLinks;
+  // applyKvs: the key's value did not decode; the key was skipped, as
+  // Decision::updateKeyInLsdb catches, logs and skips it (Decision.cpp:803-806)
+  bool decodeError = false;
 };
 
 // Raised for engine failures (no device, engine error). Graphs outside the
@@ -370,7 +373,9 @@ class LinkState {
   // :743-765), TTL-only values and other keys skipped -- then every expired
   // "adj:" key deleted (deleteKeyFromLsdb, :812-826). myNodeName (may be
   // null) turns on filterUnuseableAdjacency (:568-600). One change record
-  // per key-value, then per expired key (empty for skipped ones).
+  // per key-value, then per expired key (empty for skipped ones). A value
+  // that fails to decode skips only its own key (decodeError set, the reason
+  // in lastDecodeError()); the rest of the publication is applied.
   struct KvIn {
     std::string_view key, value;
     bool hasValue = false;
@@ -378,6 +383,9 @@ class LinkState {
   std::vector<LinkStateChange> applyKvs(const std::vector<KvIn>& kvs,
                                         const std::vector<std::string_view>& expired,
                                         const std::string* myNodeName);
+  // the last decode failure of applyKvs ("" when none) and how many so far
+  const std::string& lastDecodeError() const { return lastDecodeError_; }
+  uint64_t decodeErrors() const { return decodeErrors_; }
 
   const LinkSet& linksFromNode(const std::string& node) const;
   bool isNodeOverloaded(const std::string& node) const;
@@ -546,6 +554,8 @@ class LinkState {
   Csr& csrForWrite();  // copy-on-write when a kept memoised result reads it
 
   std::string area_;
+  std::string lastDecodeError_;
+  uint64_t decodeErrors_ = 0;
   int device_;
   std::vector<int> devices_;
   ospf_multi* multi_ = nullptr;  // devices_.size() > 1: owns engine_ (its slot 0)

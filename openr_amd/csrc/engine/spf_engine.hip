@@ -30,13 +30,33 @@ int hip_fail(ospf_ctx* c, hipError_t e, const char* what) {
   return fail(c, OSPF_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }
 
+void pool_release(ospf_ctx* c) {
+  for (auto& kv : c->sweep_pool) (void)hipFree(kv.second);
+  c->sweep_pool.clear();
+  c->sweep_pool_bytes = 0;
+}
+
+hipError_t dev_malloc(ospf_ctx* c, void** p, size_t bytes) {
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess && c && !c->sweep_pool.empty()) {  // the pooled blocks back first
+    (void)hipGetLastError();
+    pool_release(c);
+    e = hipMalloc(p, bytes);
+  }
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    *p = nullptr;
+  }
+  return e;
+}
+
 static int ensure(ospf_ctx* c, void** p, size_t* have, size_t need) {
   if (*have >= need) return OSPF_OK;
   const size_t want = std::max(need, *have * 3 / 2);
   if (*p) hipFree(*p);
   *p = nullptr;
   *have = 0;
-  hipError_t e = hipMalloc(p, want);
+  hipError_t e = dev_malloc(c, p, want);
   if (e != hipSuccess) {
     *p = nullptr;
     return fail(c, OSPF_E_NOMEM, std::string("hipMalloc scratch: ") + hipGetErrorString(e));
@@ -1356,7 +1376,7 @@ int ospf_close(ospf_ctx* c) {
     if (e) hipEventDestroy(e);
   if (c->d_cover) hipFree(c->d_cover);
   if (c->lv_aux) hipStreamDestroy(c->lv_aux);
-  for (auto& kv : c->sweep_pool) hipFree(kv.second);
+  pool_release(c);
   for (hipStream_t st : c->stream_pool) hipStreamDestroy(st);
   for (hipEvent_t e : c->event_pool) hipEventDestroy(e);
   delete c;
@@ -1524,7 +1544,7 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
     c->d_graph = nullptr;
     c->loaded = false;
   }
-  hipError_t he = hipMalloc(&c->d_graph, tot);
+  hipError_t he = dev_malloc(c, &c->d_graph, tot);
   if (he != hipSuccess) {
     c->d_graph = nullptr;
     return fail(c, OSPF_E_NOMEM, std::string("hipMalloc graph: ") + hipGetErrorString(he));
@@ -2072,7 +2092,7 @@ int ospf_twin_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n,
   void* buf = nullptr;
   const size_t b0 = h.grp.size() * 4, b1 = h.grow.size() * 4, b2 = h.rinfo.size() * 16,
                b3 = h.nbo.size() * 4, b4 = std::max<size_t>(4, h.nbl.size() * 4);
-  HIPCHK(c, hipMalloc(&buf, b0 + b1 + b2 + b3 + b4 + 64));
+  HIPCHK(c, dev_malloc(c, (void**)&buf, b0 + b1 + b2 + b3 + b4 + 64));
   char* p = (char*)buf;
   ospf::TwinLvPlan a{};
   a.n = n;
@@ -2145,6 +2165,7 @@ int ospf_leaf_derive2_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n,
   a.digest = d_digest;
   a.err = c->d_err;
   if (const char* e = getenv("OSPF_LEAF_CTILES")) a.ctiles = (uint32_t)std::max(1, atoi(e));
+  if (const char* e = getenv("OSPF_LEAF_GROUP_MAJOR")) a.group_major = atoi(e) ? 1u : 0u;
   hipError_t e = ospf::launch_leaf_derive(c->g, a, max_root_neighbors ? max_root_neighbors : 32u, s);
   if (e != hipSuccess) return hip_fail(c, e, "launch_leaf_derive");
   c->spf_runs += n;
@@ -2437,7 +2458,7 @@ int ospf_cover_prepare(ospf_ctx* c, const uint8_t* leaf) {
   HIPCHK(c, hipSetDevice(c->device));
   if (c->d_cover) HIPCHK(c, hipFree(c->d_cover));
   c->d_cover = nullptr;
-  HIPCHK(c, hipMalloc(&c->d_cover, bytes));
+  HIPCHK(c, dev_malloc(c, &c->d_cover, bytes));
   char* base = (char*)c->d_cover;
   HIPCHK(c, hipMemcpy(base + o_cix, cix.data(), V * 4ull, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(base + o_crow, crow.data(), crow.size() * 4ull, hipMemcpyHostToDevice));

@@ -134,6 +134,11 @@ void par_for(uint32_t n, F fn, uint32_t grain = 512) {
 
 
 int fail(ospf_ctx* c, int code, const std::string& msg);
+// hipMalloc on the context's device; when it fails and destroyed sweeps'
+// blocks are pooled (sweep_pool), the pool is freed and the allocation tried
+// once more (the pool is never counted as used memory)
+hipError_t dev_malloc(ospf_ctx* c, void** p, size_t bytes);
+void pool_release(ospf_ctx* c);
 int hip_fail(ospf_ctx* c, hipError_t e, const char* what);
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // the scratch of `stream`, grown to `need` bytes (a grown buffer replaces the

@@ -562,6 +562,8 @@ struct LeafArgs {
   ospf_digest* digest;    // [n] (zeroed by the caller) or null
   uint32_t* err;
   uint32_t tiles, ctiles; // 1,024-node tiles of the rows, tiles per block
+  uint32_t chunks;        // blocks per group (set by the launcher)
+  uint32_t group_major;   // block order: 0 = chunk-major (a chunk of every group), 1 = group-major
 };
 hipError_t launch_leaf_derive(const DevGraph& g, const LeafArgs& a, uint32_t kmax, hipStream_t s);
 

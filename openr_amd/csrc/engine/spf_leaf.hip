@@ -67,7 +67,8 @@ __global__ void __launch_bounds__(kBlock) leaf_derive_kernel(DevGraph g, LeafArg
   __shared__ uint64_t s_wk[256];
   __shared__ uint32_t s_ok;
   const uint32_t V = g.V, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const uint32_t gr = blockIdx.x % a.ngroups, ci = blockIdx.x / a.ngroups;
+  const uint32_t gr = a.group_major ? blockIdx.x / a.chunks : blockIdx.x % a.ngroups;
+  const uint32_t ci = a.group_major ? blockIdx.x % a.chunks : blockIdx.x / a.ngroups;
   const uint32_t i0 = a.grp ? a.grp[gr] : gr;
   const uint32_t ng = a.grp ? min(kLeafMaxG, a.grp[gr + 1] - i0) : 1u;
   if (tid < ng) {
@@ -283,6 +284,7 @@ hipError_t launch_leaf_derive(const DevGraph& g, const LeafArgs& a0, uint32_t km
     a.ctiles = (a.tiles + chunks - 1) / chunks;
   }
   const uint32_t chunks = (a.tiles + a.ctiles - 1) / a.ctiles;
+  a.chunks = chunks;
   const dim3 grid(a.ngroups * chunks);
   if (kmax <= 8)
     hipLaunchKernelGGL(leaf_derive_kernel<8>, grid, dim3(kBlock), 0, s, g, a);

@@ -251,14 +251,7 @@ int dalloc(ospf_sweep* s, T** p, size_t count) {
     c->sweep_pool_bytes -= bytes;
     c->sweep_pool.erase(it);
   } else {
-    hipError_t e = hipMalloc(&q, bytes);
-    if (e != hipSuccess && !c->sweep_pool.empty()) {  // the pool's blocks back to the device
-      (void)hipGetLastError();
-      for (auto& kv : c->sweep_pool) (void)hipFree(kv.second);
-      c->sweep_pool.clear();
-      c->sweep_pool_bytes = 0;
-      e = hipMalloc(&q, bytes);
-    }
+    const hipError_t e = ospf_int::dev_malloc(c, &q, bytes);  // frees the pool on failure
     if (e != hipSuccess)
       return sfail(s, OSPF_E_NOMEM, "sweep: hipMalloc " + std::to_string(bytes) + " B: " +
                                         hipGetErrorString(e));
@@ -268,6 +261,18 @@ int dalloc(ospf_sweep* s, T** p, size_t count) {
   s->device_bytes += bytes;
   *p = (T*)q;
   return OSPF_OK;
+}
+
+// dalloc without an error message (a caller that retries smaller)
+template <class T>
+int dalloc_try(ospf_sweep* s, T** p, size_t count) {
+  const std::string keep = s->err, keep_c = s->c ? s->c->err : std::string();
+  const int rc = dalloc(s, p, count);
+  if (rc) {
+    s->err = keep;
+    if (s->c) s->c->err = keep_c;
+  }
+  return rc;
 }
 
 template <class T>
@@ -2271,23 +2276,23 @@ int plan_wmulti(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   // the scratch also fits what the device has left (other parts' sweeps,
   // smaller devices), with a 1 GB margin; fewer blocks when an allocation
   // still fails
+  // (destroyed sweeps' pooled blocks count as free: the allocation takes
+  // from the pool or frees it)
   {
     size_t fr = 0, tot = 0;
-    if (hipMemGetInfo(&fr, &tot) == hipSuccess)
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
+      fr += c->sweep_pool_bytes;
       budget = std::min<size_t>(budget, fr > (1ull << 30) ? fr - (1ull << 30) : per);
+    }
   }
   uint32_t blocks = std::min<uint32_t>(std::max(1u, ngroups), 2u * (uint32_t)c->n_cu);
   blocks = std::max<uint32_t>(1, std::min<uint32_t>(blocks, (uint32_t)(budget / per)));
   if (const char* e = getenv("OSPF_MSD_BLOCKS")) blocks = std::max(1, std::min((int)blocks, atoi(e)));
   for (;;) {
-    if (hipMalloc((void**)&scratch, per * blocks) == hipSuccess) break;
-    (void)hipGetLastError();
+    if (dalloc_try(s, &scratch, per * blocks / sizeof(uint32_t)) == OSPF_OK) break;
     if (blocks == 1) return sfail(s, OSPF_E_NOMEM, "wmulti: no room for one traversal's scratch");
     blocks = std::max(1u, blocks / 2);
   }
-  s->allocs.push_back(scratch);
-  s->alloc_bytes.push_back(per * blocks);
-  s->device_bytes += per * blocks;
   std::vector<uint32_t> wset;
   for (uint32_t r : own_c) wset.push_back(f.words(r));
   std::sort(wset.begin(), wset.end());

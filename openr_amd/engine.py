@@ -295,6 +295,17 @@ class Engine:
     def sweep(self, **kw) -> "Sweep":
         return Sweep(self, **kw)
 
+    PROBES = {"stream": 0, "rows_chunk": 1, "rows_group": 2}
+
+    def probe_store(self, pattern: str, V: int, rows: int, group: int = 48, ctiles: int = 6,
+                    reps: int = 3) -> np.ndarray:
+        """ospf_probe_store: ms per launch writing 2 * rows * V * 4 bytes with
+        16-B non-temporal stores (box calibration for the roofline)."""
+        out = np.zeros(reps, np.float32)
+        self._check(self._L.ospf_probe_store(self._h, self.PROBES[pattern], V, rows, group,
+                                             ctiles, reps, out.ctypes.data))
+        return out
+
 
 class Sweep:
     """All-sources sweep (ospf_sweep_*): runSpf for every node of the graph,

@@ -361,18 +361,35 @@ class LinkState:
         if self._L.odl_apply_kvs(self._h, n, keys, vals, lens, ne, exp,
                                  my_node.encode() if my_node is not None else None, ch) != 0:
             raise LinkStateError(self._err())
+        self.decode_errors = [i for i in range(n + ne) if ch[i].decode_error]
         return changes_to_list(ch, n + ne)
 
     def apply_publication(self, buf: bytes, my_node: Optional[str] = None):
-        """A whole compact-thrift thrift::Publication (odl_apply_publication)."""
+        """A whole compact-thrift thrift::Publication (odl_apply_publication).
+        Values that fail to decode skip their own key only: their record
+        indices are left in self.decode_errors, the reason in
+        last_decode_error()."""
         nout = C.c_uint32(0)
-        cap = 1 << 20
-        ch = change_array(cap)
-        if self._L.odl_apply_publication(self._h, buf, len(buf),
-                                         my_node.encode() if my_node is not None else None,
-                                         ch, cap, C.byref(nout)) != 0:
-            raise LinkStateError(self._err())
-        return changes_to_list(ch, min(int(nout.value), cap))
+        cap = 64
+        me = my_node.encode() if my_node is not None else None
+        while True:
+            ch = change_array(cap)
+            rc = self._L.odl_apply_publication(self._h, buf, len(buf), me, ch, cap, C.byref(nout))
+            if rc == -2 and int(nout.value) > cap:  # ODL_E_SMALL: nothing applied
+                cap = int(nout.value)
+                continue
+            if rc != 0:
+                raise LinkStateError(self._err())
+            break
+        n = int(nout.value)
+        self.decode_errors = [i for i in range(n) if ch[i].decode_error]
+        return changes_to_list(ch, n)
+
+    def last_decode_error(self):
+        """(message of the last value that failed to decode or "", count so far)."""
+        k = C.c_uint64(0)
+        msg = self._L.odl_last_decode_error(self._h, C.byref(k))
+        return (msg or b"").decode(), int(k.value)
 
     def set_host_spf(self, on: bool = True) -> None:
         """Run every SPF / KSP2 / digest of this LinkState on the host with the

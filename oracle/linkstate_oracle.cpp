@@ -284,7 +284,7 @@ class Graph {
   }
 
   oadj_change update(const AdjDb& db) {
-    oadj_change ch{0, 0, 0, 0};
+    oadj_change ch{0, 0, 0, 0, 0};
     const std::string& me = db.name;
     AdjDb prior = std::move(dbs[me]);
     dbs[me] = db;
@@ -360,7 +360,7 @@ class Graph {
   }
 
   oadj_change remove(const std::string& me) {
-    oadj_change ch{0, 0, 0, 0};
+    oadj_change ch{0, 0, 0, 0, 0};
     auto it = dbs.find(me);
     if (it == dbs.end()) return ch;
     auto bn = byNode.find(me);

@@ -199,3 +199,77 @@ def test_large_publication_decodes_on_threads():
     assert a.link_keys() == b.link_keys()
     assert a.num_nodes() == b.num_nodes() == len(dbs)
     assert a.spf_text("2-0-0") == b.spf_text("2-0-0")
+
+
+def test_corrupt_value_skips_only_its_key():
+    """updateKeyInLsdb catches a value that fails to deserialize, logs it and
+    skips that key (Decision.cpp:742-806): the other keys of the publication
+    are applied and its expired keys deleted."""
+    st, names = random_stream(91, n=40, p=0.15)
+    dbs = st.to_dbs()
+    p = host_ls()
+    p.apply(st)
+    # an update of node 3, a truncated value for node 4, node 6 updated, node 8 expired
+    d3, d6 = dbs[3], dbs[6]
+    d3.adjs = d3.adjs[1:]
+    d6.node_label = 4242
+    bad = TC.adjacency_database(dbs[4])[:5]
+    kv = [(f"adj:{d3.name}", TC.value(TC.adjacency_database(d3))),
+          (f"adj:{dbs[4].name}", TC.value(bad)),
+          (f"adj:{d6.name}", TC.value(TC.adjacency_database(d6)))]
+    pub = TC.publication(kv, expired=[f"adj:{dbs[8].name}"], area="0")
+    ch = p.apply_publication(pub)
+    assert p.decode_errors == [1]
+    msg, n = p.last_decode_error()
+    assert n == 1 and dbs[4].name in msg
+    o = Oracle()
+    o.apply(st)
+    och = o.apply(AdjDbStream.from_dbs([d3, d6, AdjDb(dbs[8].name, delete=True)]))
+    assert ch[0] == och[0] and ch[2] == och[1] and ch[3] == och[2]
+    assert ch[1] == (False, False, False, 0)
+    assert p.num_nodes() == o_nodes(names, dbs[8].name)
+    for r in names:
+        if r != dbs[8].name:
+            assert p.spf_text(r) == o.spf_text(r), r
+
+
+def o_nodes(names, deleted):
+    return len([n for n in names if n != deleted])
+
+
+def test_deeply_nested_values_raise_not_crash():
+    """skip() bounds the nesting of lists / sets / maps as well as structs: a
+    long run of 0x19 bytes (a one-element list of lists ...) in an unknown
+    field is a decode error, not a stack overflow."""
+    head = bytes([0x18, 0x01, ord("a")])          # 1: "a"
+    nested_lists = head + bytes([0x59]) + bytes([0x19]) * 200000 + bytes([0x00])  # 6: list
+    nested_maps = head + bytes([0x5B]) + bytes([0x01, 0xBB]) * 100000 + bytes([0x00])  # 6: map
+    nested_structs = head + bytes([0x5C]) + bytes([0x1C]) * 100000 + bytes([0x00])
+    for v in (nested_lists, nested_maps, nested_structs):
+        with pytest.raises(ValueError):
+            decode_adjdbs([v])
+    # through a publication: the key is skipped, the call succeeds
+    p = host_ls()
+    pub = TC.publication([("adj:a", TC.value(nested_lists))])
+    assert p.apply_publication(pub) == [(False, False, False, 0)]
+    assert p.decode_errors == [0]
+    # moderate nesting (< 64 levels) in an unknown field still decodes
+    ok = head + bytes([0x59]) + bytes([0x19]) * 30 + bytes([0x13, 0x05]) + bytes([0x00])
+    assert decode_adjdbs([ok]).to_dbs()[0].name == "a"
+
+
+def test_publication_area_and_record_count():
+    """A publication of another area is refused (Decision routes it to that
+    area's LinkState, Decision.cpp:847-854); more change records than the
+    first buffer holds: the wrapper asks again (nothing applied the first
+    time), so every record of a large publication comes back."""
+    st, names = random_stream(5, n=120, p=0.05)
+    p = host_ls()
+    pub = TC.publication([(k, TC.value(v)) for k, v in _kv_of(st.to_dbs())], area="other")
+    with pytest.raises(LinkStateError, match="area"):
+        p.apply_publication(pub)
+    assert p.num_nodes() == 0
+    pub = TC.publication([(k, TC.value(v)) for k, v in _kv_of(st.to_dbs())], area="0")
+    ch = p.apply_publication(pub)
+    assert len(ch) == len(names) > 64
+    assert p.num_nodes() == len(names)
