@@ -58,6 +58,33 @@ char* odl_link_keys_text(odl_ls* ls);
 int64_t odl_metric_a_to_b(odl_ls* ls, const char* a, const char* b, int use_link_metric);
 int odl_is_overloaded(odl_ls* ls, const char* node);
 uint64_t odl_spf_runs(const odl_ls* ls);
+/* The path's fb303 counters: decision.spf_runs COUNT
+ * (LinkState.cpp:843); decision.spf_ms (:909), ucmp_ms (:1029) and
+ * route_build_ms (SpfSolver.cpp:640-644) are AVG stats, kept here as a sum
+ * and a sample count; ucmp_runs COUNT (:926). Plus the device errors the
+ * LinkState survived (it then runs on its host path; degraded = 1). */
+typedef struct odl_counters {
+  uint64_t spf_runs;
+  uint64_t spf_ms_samples;
+  double spf_ms_sum;
+  uint64_t ucmp_runs;
+  double ucmp_ms_sum;
+  uint64_t route_build_runs;
+  double route_build_ms_sum;
+  uint64_t engine_errors;
+  uint32_t engine_degraded;
+} odl_counters;
+void odl_get_counters(const odl_ls* ls, odl_counters* out);
+/* The last engine error the LinkState degraded on ("" when none). */
+const char* odl_last_engine_error(const odl_ls* ls);
+/* Test hook: the after-th engine call from now fails with OSPF_E_DEVICE
+ * (ospf_inject_error); the LinkState must degrade to its host path. */
+int odl_inject_engine_error(odl_ls* ls, uint32_t after);
+/* Degrade to the host path on device errors (default 1; 0: the call fails
+ * with the engine's error instead). A LinkState whose engine never opened
+ * (no device) always fails: there is no silent CPU path. ODL_STRICT_ENGINE
+ * in the environment sets 0 at creation. */
+void odl_set_degrade(odl_ls* ls, int on);
 /* Incremental mode (off by default; odl::LinkState::setIncremental): keep the
  * memoised SPF of roots a metric / up / overload-only update cannot affect.
  * Stats: {patches applied, results kept, results dropped}. */

@@ -665,6 +665,13 @@ int ospf_msweep_owner(const ospf_msweep* ms, uint32_t root, uint32_t* slot);
  * (LinkState.cpp:843). */
 uint64_t ospf_spf_runs(const ospf_ctx* ctx);
 
+/* Test hook (fault injection): the after_calls-th call from now of
+ * ospf_load_graph / ospf_sssp_batch / ospf_ksp2_run / ospf_sweep_create /
+ * ospf_sweep_run / ospf_sweep_copy_rows on this context fails with
+ * OSPF_E_DEVICE and does nothing (0 = off). Lets the caller's handling of a
+ * device error be tested without a faulting GPU. */
+int ospf_inject_error(ospf_ctx* ctx, uint32_t after_calls);
+
 /* Box calibration (no reference counterpart: measurement).
  * The HBM store rate of this device, timed with HIP events: 2 * rows * V * 4
  * bytes written with 16-B non-temporal stores per launch, `reps` timed

@@ -42,7 +42,7 @@ ENGINE_SYMBOLS = [
     "ospf_multi_open", "ospf_multi_close", "ospf_multi_last_error", "ospf_multi_size",
     "ospf_multi_ctx", "ospf_multi_load_graph", "ospf_msweep_create", "ospf_msweep_destroy",
     "ospf_msweep_run", "ospf_msweep_digests", "ospf_msweep_part", "ospf_msweep_owner",
-    "ospf_msweep_gather_backend", "ospf_probe_store",
+    "ospf_msweep_gather_backend", "ospf_probe_store", "ospf_inject_error",
 ]
 DECISION_SYMBOLS = [
     "odl_create", "odl_create_multi", "odl_all_sources_prefetch", "odl_all_sources_digests",
@@ -51,7 +51,8 @@ DECISION_SYMBOLS = [
     "odl_spf_runs", "odl_set_incremental", "odl_set_host_spf", "odl_incremental_stats", "odl_topology_stats", "odl_num_nodes", "odl_num_links", "odl_spf_digests", "odl_spf_prefetch",
     "odl_ksp2_text", "odl_route_text", "odl_route_db_text", "odl_route_db_bin", "odl_free_buf", "odl_path_a_in_b", "odl_ucmp_text", "odl_csr_size", "odl_csr_export", "odl_node_name", "odl_node_id",
     "odl_apply_kvs", "odl_apply_publication", "odl_node_patches", "odl_shard_stats", "odl_route_db_multi_text", "odl_adjdbs_decode", "odl_adjdbs_stream", "odl_adjdbs_error", "odl_adjdbs_free",
-    "odl_last_decode_error",
+    "odl_last_decode_error", "odl_get_counters", "odl_last_engine_error", "odl_inject_engine_error",
+    "odl_set_degrade",
 ]
 
 
@@ -121,6 +122,13 @@ class ospf_sweep_launch(C.Structure):  # noqa: N801
     _fields_ = [("name", C.c_char * 32), ("kernel", C.c_char * 112), ("n_roots", u32),
                 ("nh_words", u32), ("compulsory_bytes", u64), ("ms_median", C.c_double),
                 ("ms_min", C.c_double)]
+
+
+class odl_counters(C.Structure):  # noqa: N801
+    _fields_ = [("spf_runs", u64), ("spf_ms_samples", u64), ("spf_ms_sum", C.c_double),
+                ("ucmp_runs", u64), ("ucmp_ms_sum", C.c_double), ("route_build_runs", u64),
+                ("route_build_ms_sum", C.c_double), ("engine_errors", u64),
+                ("engine_degraded", u32)]
 
 
 class ospf_graph_info(C.Structure):  # noqa: N801
@@ -218,6 +226,7 @@ def engine() -> C.CDLL:
         L.ospf_msweep_gather_backend.argtypes = [vp]
         L.ospf_msweep_gather_backend.restype = u32
         L.ospf_probe_store.argtypes = [vp, u32, u32, u32, u32, u32, u32, vp]
+        L.ospf_inject_error.argtypes = [vp, u32]
         _engine = L
     return _engine
 
@@ -283,6 +292,14 @@ def decision() -> C.CDLL:
         L.odl_adjdbs_free.restype = None
         L.odl_last_decode_error.argtypes = [vp, C.POINTER(u64)]
         L.odl_last_decode_error.restype = cp
+        L.odl_get_counters.argtypes = [vp, vp]
+        L.odl_get_counters.restype = None
+        L.odl_last_engine_error.argtypes = [vp]
+        L.odl_last_engine_error.restype = cp
+        L.odl_inject_engine_error.argtypes = [vp, u32]
+        L.odl_inject_engine_error.restype = i32
+        L.odl_set_degrade.argtypes = [vp, i32]
+        L.odl_set_degrade.restype = None
         L.odl_set_host_spf.argtypes = [vp, i32]
         L.odl_set_host_spf.restype = None
         L.odl_incremental_stats.argtypes = [vp, vp]

@@ -241,6 +241,25 @@ int odl_is_overloaded(odl_ls* h, const char* node) {
   return h ? (h->ls.isNodeOverloaded(node) ? 1 : 0) : -1;
 }
 uint64_t odl_spf_runs(const odl_ls* h) { return h ? h->ls.spfRuns() : 0; }
+void odl_get_counters(const odl_ls* h, odl_counters* out) {
+  if (!h || !out) return;
+  const auto c = h->ls.counters();
+  *out = odl_counters{c.spf_runs, c.spf_ms_samples, c.spf_ms_sum, c.ucmp_runs, c.ucmp_ms_sum,
+                      c.route_build_runs, c.route_build_ms_sum, h->ls.engineErrors(),
+                      h->ls.degraded() ? 1u : 0u};
+}
+const char* odl_last_engine_error(const odl_ls* h) {
+  return h ? h->ls.lastEngineError().c_str() : "";
+}
+void odl_set_degrade(odl_ls* h, int on) {
+  if (h) h->ls.setDegradeOnError(on != 0);
+}
+int odl_inject_engine_error(odl_ls* h, uint32_t after) {
+  return guard(h, [&]() -> int {
+    h->ls.injectEngineError(after);
+    return 0;
+  }, -1);
+}
 void odl_set_incremental(odl_ls* h, int on) {
   if (h) h->ls.setIncremental(on != 0);
 }

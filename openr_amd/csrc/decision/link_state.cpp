@@ -182,12 +182,14 @@ std::string Link::key() const {
 LinkState::LinkState(std::string area, int device)
     : area_(std::move(area)), device_(device), devices_{device} {
   hostOnly_ = getenv("ODL_HOST_SPF") != nullptr;
+  degradeOnError_ = getenv("ODL_STRICT_ENGINE") == nullptr;
 }
 
 LinkState::LinkState(std::string area, std::vector<int> devices)
     : area_(std::move(area)), device_(devices.empty() ? 0 : devices[0]), devices_(std::move(devices)) {
   if (devices_.empty()) throw std::invalid_argument("LinkState: no device");
   hostOnly_ = getenv("ODL_HOST_SPF") != nullptr;
+  degradeOnError_ = getenv("ODL_STRICT_ENGINE") == nullptr;
 }
 
 LinkState::~LinkState() {
@@ -739,6 +741,91 @@ uint32_t LinkState::linkIdOf(const Link& l) const {
   return lid;
 }
 
+// ---- device errors: degrade to the host path
+template <class F>
+decltype(auto) LinkState::guarded(F&& f) {
+  if (guardDepth_) return f();  // an inner entry point: the outermost one handles it
+  struct Depth {
+    int& d;
+    explicit Depth(int& x) : d(x) { ++d; }
+    ~Depth() { --d; }
+  };
+  const uint64_t runs0 = spfRuns_;
+  const size_t memo0 = memoMetric_.size() + memoHops_.size();
+  // decision.spf_ms (LinkState.cpp:844,906-909): the call's time, charged to
+  // the logical runs it made
+  struct Timer {
+    LinkState& ls;
+    uint64_t runs0;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    ~Timer() {
+      if (ls.spfRuns_ <= runs0) return;
+      ls.counters_.spf_ms_samples += ls.spfRuns_ - runs0;
+      ls.counters_.spf_ms_sum +=
+          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+  } timer{*this, runs0};
+  try {
+    Depth dp(guardDepth_);
+    return f();
+  } catch (const EngineError& e) {
+    if (!degradeOnError_ || !engineOpened_) throw;
+    onEngineError(e);
+  }
+  // runs memoised before the failure were made (and stay); the retry counts
+  // its own
+  spfRuns_ = runs0 + (memoMetric_.size() + memoHops_.size() - memo0);
+  Depth dp(guardDepth_);
+  return f();
+}
+
+void LinkState::onEngineError(const std::exception& e) {
+  ++engineErrors_;
+  lastEngineError_ = e.what();
+  fprintf(stderr, "odl::LinkState(%s): engine error, continuing on the host path: %s\n",
+          area_.c_str(), e.what());
+  dropSweep();
+  if (multi_) ospf_multi_close(multi_);
+  else if (engine_) ospf_close(engine_);
+  multi_ = nullptr;
+  engine_ = nullptr;
+  engineVersion_ = 0;
+  hostOnly_ = true;
+  degraded_ = true;
+}
+
+void LinkState::injectEngineError(uint32_t after) {
+  injectAfter_ = after;
+  if (engine_) {
+    ospf_inject_error(engine_, after);
+    injectAfter_ = 0;
+  }
+}
+
+const SpfResult& LinkState::getSpfResult(const std::string& node, bool useLinkMetric) {
+  return guarded([&]() -> const SpfResult& { return getSpfResultImpl(node, useLinkMetric); });
+}
+void LinkState::prefetchSpf(const std::vector<std::string>& roots, bool useLinkMetric) {
+  guarded([&] { prefetchSpfImpl(roots, useLinkMetric); });
+}
+std::vector<ospf_digest> LinkState::spfDigests(const std::vector<std::string>& roots,
+                                               bool useLinkMetric) {
+  return guarded([&] { return spfDigestsImpl(roots, useLinkMetric); });
+}
+void LinkState::prefetchAllSources(bool useLinkMetric) {
+  guarded([&] { prefetchAllSourcesImpl(useLinkMetric); });
+}
+std::vector<ospf_digest> LinkState::allSourcesDigests(bool useLinkMetric) {
+  return guarded([&] { return allSourcesDigestsImpl(useLinkMetric); });
+}
+const std::vector<Path>& LinkState::getKthPaths(const std::string& src, const std::string& dst,
+                                                size_t k) {
+  return guarded([&]() -> const std::vector<Path>& { return getKthPathsImpl(src, dst, k); });
+}
+void LinkState::prefetchKsp2(const std::string& src, const std::vector<std::string>& dsts) {
+  guarded([&] { prefetchKsp2Impl(src, dsts); });
+}
+
 void LinkState::ensureEngine() {
   snapshot();
   if (!engine_) {
@@ -753,6 +840,11 @@ void LinkState::ensureEngine() {
       engine_ = nullptr;
       multi_ = nullptr;
       throw EngineError(rc, "ospf_open failed (no MI355X device / HIP runtime?)");
+    }
+    engineOpened_ = true;
+    if (injectAfter_) {
+      ospf_inject_error(engine_, injectAfter_);
+      injectAfter_ = 0;
     }
   }
   if (engineVersion_ != snapVersion_) {
@@ -790,7 +882,7 @@ bool LinkState::sweepHas(bool useLinkMetric) const {
          snapVersion_ == version_;
 }
 
-void LinkState::prefetchAllSources(bool useLinkMetric) {
+void LinkState::prefetchAllSourcesImpl(bool useLinkMetric) {
   snapshot();
   if (sweepHas(useLinkMetric)) return;
   if (hostRun(useLinkMetric)) {  // outside the engine contract: the reference algorithm
@@ -861,7 +953,7 @@ void LinkState::sweepRows(const std::vector<uint32_t>& roots, uint32_t W,
   sweepStats_.rows_copied += roots.size();
 }
 
-std::vector<ospf_digest> LinkState::allSourcesDigests(bool useLinkMetric) {
+std::vector<ospf_digest> LinkState::allSourcesDigestsImpl(bool useLinkMetric) {
   snapshot();
   const size_t V = csr_->names.size();
   if (hostRun(useLinkMetric)) return spfDigests(csr_->names, useLinkMetric);
@@ -912,13 +1004,21 @@ int LinkState::batchOn(ospf_ctx* c, const uint32_t* roots, uint32_t n, bool useL
 }
 
 // Run fn(slot, ctx) for every slot, slot 0 on the calling thread; the first
-// failure (rc, slot) is returned after every thread joined.
+// failure (rc, slot) is returned after every thread joined. A slot whose
+// thread cannot be created runs on the calling thread too.
 static std::pair<int, size_t> onSlots(const std::vector<ospf_ctx*>& cs,
                                       const std::function<int(size_t, ospf_ctx*)>& fn) {
   std::vector<int> rc(cs.size(), OSPF_OK);
   std::vector<std::thread> th;
-  for (size_t i = 1; i < cs.size(); ++i) th.emplace_back([&, i] { rc[i] = fn(i, cs[i]); });
-  rc[0] = fn(0, cs[0]);
+  std::vector<size_t> here{0};
+  for (size_t i = 1; i < cs.size(); ++i) {
+    try {
+      th.emplace_back([&, i] { rc[i] = fn(i, cs[i]); });
+    } catch (const std::system_error&) {
+      here.push_back(i);
+    }
+  }
+  for (size_t i : here) rc[i] = fn(i, cs[i]);
   for (auto& t : th) t.join();
   for (size_t i = 0; i < cs.size(); ++i)
     if (rc[i] != OSPF_OK) return {rc[i], i};
@@ -1089,7 +1189,7 @@ std::vector<uint32_t> LinkState::nbrsOf(uint32_t root) const {
   return out;
 }
 
-const SpfResult& LinkState::getSpfResult(const std::string& node, bool useLinkMetric) {
+const SpfResult& LinkState::getSpfResultImpl(const std::string& node, bool useLinkMetric) {
   auto& memo = useLinkMetric ? memoMetric_ : memoHops_;
   auto it = memo.find(node);
   if (it != memo.end()) return it->second;
@@ -1097,7 +1197,7 @@ const SpfResult& LinkState::getSpfResult(const std::string& node, bool useLinkMe
   return memo.at(node);
 }
 
-void LinkState::prefetchSpf(const std::vector<std::string>& roots, bool useLinkMetric) {
+void LinkState::prefetchSpfImpl(const std::vector<std::string>& roots, bool useLinkMetric) {
   auto& memo = useLinkMetric ? memoMetric_ : memoHops_;
   snapshot();
   std::unordered_map<uint32_t, std::vector<uint32_t>> byW;  // W -> roots
@@ -1176,8 +1276,8 @@ void LinkState::prefetchSpf(const std::vector<std::string>& roots, bool useLinkM
   }
 }
 
-std::vector<ospf_digest> LinkState::spfDigests(const std::vector<std::string>& roots,
-                                               bool useLinkMetric) {
+std::vector<ospf_digest> LinkState::spfDigestsImpl(const std::vector<std::string>& roots,
+                                                   bool useLinkMetric) {
   snapshot();
   std::vector<ospf_digest> out(roots.size(), ospf_digest{0, 0, 0});
   std::vector<uint32_t> ids;
@@ -1268,8 +1368,8 @@ static std::string kspKey(const std::string& s, const std::string& d, size_t k) 
   return key;
 }
 
-const std::vector<Path>& LinkState::getKthPaths(const std::string& src, const std::string& dst,
-                                                size_t k) {
+const std::vector<Path>& LinkState::getKthPathsImpl(const std::string& src, const std::string& dst,
+                                                    size_t k) {
   if (k < 1) throw std::invalid_argument("k must be >= 1");
   const std::string key = kspKey(src, dst, k);
   auto it = memoKsp_.find(key);
@@ -1342,7 +1442,7 @@ const std::vector<Path>& LinkState::getKthPaths(const std::string& src, const st
   return memoKsp_.emplace(key, std::move(paths)).first->second;
 }
 
-void LinkState::prefetchKsp2(const std::string& src, const std::vector<std::string>& dsts) {
+void LinkState::prefetchKsp2Impl(const std::string& src, const std::vector<std::string>& dsts) {
   snapshot();
   if (hostRun(true)) {
     for (const auto& d : dsts) getKthPaths(src, d, 2);
@@ -1770,6 +1870,16 @@ void NodeUcmpResult::normalizeNextHopWeights() {
 UcmpResult LinkState::resolveUcmpWeights(
     const SpfResult& spfGraph, const std::unordered_map<std::string, int64_t>& leafNodeToWeights,
     UcmpAlgo algo, bool useLinkMetric) const {
+  // decision.ucmp_runs / ucmp_ms (LinkState.cpp:926,1025-1029)
+  struct Timer {
+    Counters& c;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    ~Timer() {
+      ++c.ucmp_runs;
+      c.ucmp_ms_sum +=
+          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+  } timer{counters_};
   UcmpResult out;
   // DijkstraQ<DijkstraQUcmpNode> (LinkState.h:573-645): entries still queued,
   // by name; pop order (metric, name). A popped node leaves the map, so a later

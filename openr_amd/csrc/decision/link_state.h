@@ -439,6 +439,48 @@ class LinkState {
 
   uint64_t spfRuns() const { return spfRuns_; }
 
+  // ---- device errors (degrade, never abort Decision) ----
+  // An engine call that fails (any OSPF_E_* other than an out-of-contract
+  // input, which the host path already takes) does not escape: the LinkState
+  // records it, releases the engine and switches to its host path
+  // (runSpfHost, the reference algorithm -- product code, not the oracle) for
+  // every later SPF / KSP2 / digest, and the failed call is answered there.
+  // setHostSpf(false) re-enables the engine. The reference instead ends in
+  // XLOG(FATAL) when an exception leaves the Decision fiber
+  // (Decision.cpp:240-250).
+  // fb303 counters of the path (LinkState.cpp:843,909,926,1029;
+  // SpfSolver.cpp:640-644): decision.spf_runs COUNT, decision.spf_ms /
+  // ucmp_ms / route_build_ms AVG -- kept as sums and sample counts (AVG =
+  // sum / samples). A batched engine call is charged to its logical runs.
+  struct Counters {
+    uint64_t spf_runs = 0, spf_ms_samples = 0;
+    double spf_ms_sum = 0;
+    uint64_t ucmp_runs = 0;
+    double ucmp_ms_sum = 0;
+    uint64_t route_build_runs = 0;
+    double route_build_ms_sum = 0;
+  };
+  Counters counters() const {
+    Counters c = counters_;
+    c.spf_runs = spfRuns_;
+    return c;
+  }
+  void addRouteBuild(double ms) {
+    ++counters_.route_build_runs;
+    counters_.route_build_ms_sum += ms;
+  }
+  uint64_t engineErrors() const { return engineErrors_; }
+  const std::string& lastEngineError() const { return lastEngineError_; }
+  // test hook: the after-th engine call from now fails with OSPF_E_DEVICE
+  // (ospf_inject_error; applied when the engine opens)
+  void injectEngineError(uint32_t after);
+  // degrade on device errors (default on; off: the EngineError escapes, as
+  // before). A LinkState whose engine never opened (no device) always
+  // throws: there is no silent CPU path for a box without a GPU. The
+  // environment variable ODL_STRICT_ENGINE turns it off at construction (the
+  // test suite sets it, so a GPU test cannot pass on the host path).
+  void setDegradeOnError(bool on) { degradeOnError_ = on; }
+
   // ---- incremental mode (off by default) ----
   // The reference drops every memoised SPF on a topology change
   // (LinkState.cpp:751-754). With incremental mode on, an update that only
@@ -470,7 +512,11 @@ class LinkState {
   // algorithm), the engine never opened: a GPU-free run of the whole ingest /
   // patch / memo logic (sanitizer builds, link-event sequences on the CPU).
   // Also set by the environment variable ODL_HOST_SPF at construction.
-  void setHostSpf(bool on) { hostOnly_ = on; }
+  void setHostSpf(bool on) {
+    hostOnly_ = on;
+    if (!on) degraded_ = false;
+  }
+  bool degraded() const { return degraded_; }
   bool hostSpf() const { return hostOnly_; }
   // Links added or removed between known nodes ([LINK UP] / [LINK DOWN],
   // LinkState.cpp:632-657) patch the snapshot and the device graph in place
@@ -573,6 +619,26 @@ class LinkState {
   ShardStats shardStats_;
   bool hostMetric_ = false;   // snapshot outside the engine's metric contract
   bool hostOnly_ = false;     // setHostSpf: no engine at all
+  bool degraded_ = false;     // hostOnly_ set by a device error
+  bool degradeOnError_ = true;
+  bool engineOpened_ = false;  // an engine context was opened once
+  int guardDepth_ = 0;        // nesting of the public entry points (guarded)
+  uint64_t engineErrors_ = 0;
+  std::string lastEngineError_;
+  uint32_t injectAfter_ = 0;  // test hook, handed to the engine when it opens
+  mutable Counters counters_;  // spf_runs lives in spfRuns_
+  // run f; an EngineError escaping the outermost public entry point degrades
+  // the LinkState to its host path and runs f again there
+  template <class F>
+  decltype(auto) guarded(F&& f);
+  void onEngineError(const std::exception& e);
+  const SpfResult& getSpfResultImpl(const std::string& node, bool useLinkMetric);
+  void prefetchSpfImpl(const std::vector<std::string>& roots, bool useLinkMetric);
+  std::vector<ospf_digest> spfDigestsImpl(const std::vector<std::string>& roots, bool useLinkMetric);
+  void prefetchAllSourcesImpl(bool useLinkMetric);
+  std::vector<ospf_digest> allSourcesDigestsImpl(bool useLinkMetric);
+  const std::vector<Path>& getKthPathsImpl(const std::string& src, const std::string& dst, size_t k);
+  void prefetchKsp2Impl(const std::string& src, const std::vector<std::string>& dsts);
   bool hostRun(bool useLinkMetric) const { return hostOnly_ || (useLinkMetric && hostMetric_); }
   uint64_t distBound_ = 0;    // >= every simple-path metric sum of the snapshot
   uint64_t spfRuns_ = 0;

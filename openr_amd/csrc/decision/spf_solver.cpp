@@ -2,6 +2,7 @@
 #include "spf_solver.h"
 
 #include <algorithm>
+#include <chrono>
 #include <limits>
 #include <set>
 #include <stdexcept>
@@ -380,9 +381,22 @@ std::optional<UnicastRoute> SpfSolver::prefixRoute(const std::string& me, const 
 std::optional<RouteDb> SpfSolver::buildRouteDb(const std::string& me,
                                                const std::vector<PrefixRoute>& prefixes,
                                                const RouteOptions& opt) {
+  // decision.route_build_ms (SpfSolver.cpp:460-462,640-644), on this
+  // solver's own LinkState
+  struct Timer {
+    LinkState& ls;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    bool on = false;
+    ~Timer() {
+      if (on)
+        ls.addRouteBuild(
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+  } timer{ls_};
   bool exists = false;  // :463-471: `me` in some area's link state
   for (const auto& a : areas_) exists |= a.second->getAdjacencyDatabases().count(me) > 0;
   if (!exists) return std::nullopt;
+  timer.on = true;
   RouteDb db;
   // The SP prefixes read only the memoised SPF of `me` in each area (and
   // const link state): they are built on host threads. A prefix with a KSP2

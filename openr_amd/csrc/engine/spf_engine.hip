@@ -30,6 +30,12 @@ int hip_fail(ospf_ctx* c, hipError_t e, const char* what) {
   return fail(c, OSPF_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }
 
+bool injected(ospf_ctx* c) {
+  if (!c || !c->inject_after || --c->inject_after) return false;
+  fail(c, OSPF_E_DEVICE, "injected device error (ospf_inject_error)");
+  return true;
+}
+
 void pool_release(ospf_ctx* c) {
   for (auto& kv : c->sweep_pool) (void)hipFree(kv.second);
   c->sweep_pool.clear();
@@ -1385,10 +1391,17 @@ int ospf_close(ospf_ctx* c) {
 
 const char* ospf_last_error(const ospf_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
+int ospf_inject_error(ospf_ctx* c, uint32_t after_calls) {
+  if (!c) return OSPF_E_INVAL;
+  c->inject_after = after_calls;
+  return OSPF_OK;
+}
+
 uint64_t ospf_spf_runs(const ospf_ctx* c) { return c ? c->spf_runs : 0; }
 
 int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   if (!c || !csr) return OSPF_E_INVAL;
+  if (injected(c)) return OSPF_E_DEVICE;
   const uint32_t V = csr->n_nodes, E = csr->n_edges;
   if (V == 0 || V >= 0x80000000u) return fail(c, OSPF_E_INVAL, "n_nodes out of range");
   if (!csr->row_ptr || (E && (!csr->col || !csr->metric || !csr->link_id || !csr->twin ||
@@ -2515,6 +2528,7 @@ int ospf_sssp_batch(ospf_ctx* c, const uint32_t* roots, uint32_t n_roots, const 
                     uint32_t flags, uint32_t nh_words, uint32_t* dist_out, uint32_t* nh_out,
                     ospf_digest* digest_out) {
   if (!c) return OSPF_E_INVAL;
+  if (injected(c)) return OSPF_E_DEVICE;
   if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
   if (n_roots == 0) return OSPF_OK;
   if (!roots) return fail(c, OSPF_E_INVAL, "null roots");
@@ -2611,6 +2625,7 @@ int ospf_ksp2_stats(const ospf_ctx* c, uint64_t* out) {
 
 int ospf_ksp2_run(ospf_ctx* c, const ospf_ksp2* k) {
   if (!c || !k) return OSPF_E_INVAL;
+  if (injected(c)) return OSPF_E_DEVICE;
   if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
   if (k->n == 0) return OSPF_OK;
   if (!k->dsts || !k->k1 || !k->k2 || !k->status) return fail(c, OSPF_E_INVAL, "null KSP2 buffer");

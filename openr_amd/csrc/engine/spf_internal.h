@@ -22,6 +22,7 @@ struct ospf_ctx {
   int n_cu = 256;
   std::string err;
   uint64_t spf_runs = 0;
+  uint32_t inject_after = 0;  // ospf_inject_error: calls until the injected failure (0 = off)
   uint64_t ksp_decr_stats[3] = {0, 0, 0};  // ospf_ksp2_stats
   // device blocks, streams and events of destroyed sweeps, taken again by the
   // next sweep (a graph patch drops the sweep; its successor reuses ~100 GB
@@ -139,6 +140,9 @@ int fail(ospf_ctx* c, int code, const std::string& msg);
 // once more (the pool is never counted as used memory)
 hipError_t dev_malloc(ospf_ctx* c, void** p, size_t bytes);
 void pool_release(ospf_ctx* c);
+// ospf_inject_error's hook at an entry point: true (and the error recorded)
+// when this call is the one to fail
+bool injected(ospf_ctx* c);
 int hip_fail(ospf_ctx* c, hipError_t e, const char* what);
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // the scratch of `stream`, grown to `need` bytes (a grown buffer replaces the

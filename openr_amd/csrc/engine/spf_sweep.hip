@@ -2593,6 +2593,7 @@ extern "C" {
 int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
   if (!c || !o || !out) return OSPF_E_INVAL;
   *out = nullptr;
+  if (ospf_int::injected(c)) return OSPF_E_DEVICE;
   if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
   if (c->mask.on) return fail(c, OSPF_E_INVAL, "sweep: links are masked (ospf_links_unmask)");
   const uint32_t parts = std::max(1u, o->n_parts);
@@ -2786,6 +2787,7 @@ int ospf_sweep_roots(const ospf_sweep* s, uint32_t* roots) {
 int ospf_sweep_run(ospf_sweep* s, void* stream) {
   if (!s) return OSPF_E_INVAL;
   ospf_ctx* c = s->c;
+  if (ospf_int::injected(c)) return sfail(s, OSPF_E_DEVICE, c->err);
   if (c->graph_gen != s->gen || c->mask.on)
     return sfail(s, OSPF_E_NOGRAPH, "sweep: the graph changed since the sweep was created");
   SCHK(s, hipSetDevice(c->device));
@@ -2893,6 +2895,7 @@ int ospf_sweep_row(const ospf_sweep* s, uint32_t root, const uint32_t** d_dist,
 int ospf_sweep_copy_rows(ospf_sweep* s, const uint32_t* roots, uint32_t n, uint32_t nh_words,
                          uint32_t* dist_out, uint32_t* nh_out) {
   if (!s || (n && !roots)) return OSPF_E_INVAL;
+  if (ospf_int::injected(s->c)) return sfail(s, OSPF_E_DEVICE, s->c->err);
   if (!s->ran) return sfail(s, OSPF_E_INVAL, "sweep: rows before the first run");
   const uint32_t V = s->V;
   for (uint32_t i = 0; i < n; ++i) {

@@ -385,6 +385,26 @@ class LinkState:
         self.decode_errors = [i for i in range(n) if ch[i].decode_error]
         return changes_to_list(ch, n)
 
+    def counters(self) -> dict:
+        """The path's fb303 counters (odl_get_counters): decision.spf_runs,
+        spf_ms / ucmp_ms / route_build_ms as sums + sample counts (AVG =
+        sum / samples), ucmp_runs, and the device errors survived."""
+        c = N.odl_counters()
+        self._L.odl_get_counters(self._h, C.byref(c))
+        return {k: getattr(c, k) for k, _ in c._fields_}
+
+    def set_degrade(self, on: bool = True) -> None:
+        """Degrade to the host path on device errors (odl_set_degrade)."""
+        self._L.odl_set_degrade(self._h, int(on))
+
+    def last_engine_error(self) -> str:
+        return (self._L.odl_last_engine_error(self._h) or b"").decode()
+
+    def inject_engine_error(self, after: int = 1) -> None:
+        """Test hook: the after-th engine call from now fails (OSPF_E_DEVICE)."""
+        if self._L.odl_inject_engine_error(self._h, after) != 0:
+            raise LinkStateError(self._err())
+
     def last_decode_error(self):
         """(message of the last value that failed to decode or "", count so far)."""
         k = C.c_uint64(0)

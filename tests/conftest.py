@@ -5,6 +5,12 @@ import sys
 # both torch device buffers and libopenr_spf_hip in the test process.
 import torch  # noqa: F401,E402
 
+# A LinkState degrades to its host path on a device error;
+# in the test suite it must not: a GPU test that passed on the host path
+# would not be evidence for the engine. test_gpu_degrade.py turns it back on
+# for the LinkStates it tests.
+os.environ["ODL_STRICT_ENGINE"] = "1"
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))

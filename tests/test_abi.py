@@ -40,3 +40,21 @@ def test_engine_library_is_gfx950():
         assert b"gfx950" in data
     else:
         assert "gfx950" in out
+
+
+def test_no_device_is_an_error_not_a_host_fallback():
+    """Degrading to the host path is for device errors of an engine that ran
+    (SURVEY.md §5); a LinkState on a box with no GPU must fail loudly, even
+    with degrading on, so no result can silently come from the CPU."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from graphs import random_stream
+    from openr_amd.linkstate import LinkState, LinkStateError
+    st, names = random_stream(1)
+    p = LinkState()
+    p.set_degrade(True)
+    p.apply(st)
+    with pytest.raises(LinkStateError):
+        p.spf_text(names[0])
+    assert p.counters()["engine_degraded"] == 0
