@@ -192,10 +192,14 @@ int odl_path_a_in_b(const char* a_nl, uint32_t na, const char* b_nl, uint32_t nb
  * entry = "node:fwd:algo:weight[:prepend]" (a thrift::PrefixEntry: fwd 0 IP /
  * 1 SR_MPLS; algo 0 SP_ECMP, 1 KSP2_ED_ECMP, 2 SP_UCMP_ADJ_WEIGHT_PROPAGATION,
  * 3 SP_UCMP_PREFIX_WEIGHT_PROPAGATION; weight 0 = unset; optional prepend
- * label). flags: 1 node-segment labels, 2 adjacency labels, 4 UCMP (the
- * SpfSolver constructor switches). Text, one line each, next hops sorted:
+ * label; then optionally "%pp/sp/d" = PrefixMetrics path_preference /
+ * source_preference / distance, and "!bgp" or "!bgpmv" = PrefixType::BGP
+ * without / with a metric vector). flags: 1 node-segment labels, 2 adjacency
+ * labels, 4 UCMP, 8 enableBestRouteSelection (the SpfSolver constructor
+ * switches, SpfSolver.h:108-118). Text, one line each, next hops sorted:
  *   me \t NONE                       (`me` unknown: the reference's nullopt)
  *   me \t R \t prefix \t igpCost(u32) \t ucmpWeight | -
+ *        [flag 8: \t best node@area \t selected node@area,...]
  *   me \t U \t prefix \t ifName \t neighbor \t metric(i32) \t op \t labels \t weight
  *   me \t M \t label  \t ifName \t neighbor \t metric(i32) \t op \t labels \t weight
  * op: 0 none, 1 PHP, 2 SWAP, 3 PUSH, 4 POP_AND_LOOKUP; labels comma-separated

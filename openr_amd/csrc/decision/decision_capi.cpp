@@ -469,9 +469,12 @@ std::vector<std::optional<odl::RouteDb>> buildDbs(odl_ls* h, const std::vector<s
       std::stringstream es(ln.substr(t + 1));
       for (std::string x; std::getline(es, x, ',');) {
         if (x.empty()) continue;
-        // optional suffixes: "#minNexthop", then "@area" before it
+        // optional suffixes, in this order: "%pp/sp/d" (PrefixMetrics),
+        // "!bgp" / "!bgpmv" (PrefixType::BGP without / with a metric
+        // vector), "@area", "#minNexthop"
         std::optional<int64_t> minNh;
-        std::string area;
+        std::string area, type;
+        int32_t met[3] = {0, 0, 0};
         if (const size_t hsh = x.rfind('#'); hsh != std::string::npos) {
           minNh = std::stoll(x.substr(hsh + 1));
           x.resize(hsh);
@@ -479,6 +482,17 @@ std::vector<std::optional<odl::RouteDb>> buildDbs(odl_ls* h, const std::vector<s
         if (const size_t at = x.rfind('@'); at != std::string::npos) {
           area = x.substr(at + 1);
           x.resize(at);
+        }
+        if (const size_t bang = x.rfind('!'); bang != std::string::npos) {
+          type = x.substr(bang + 1);
+          x.resize(bang);
+          if (type != "bgp" && type != "bgpmv")
+            throw std::invalid_argument("prefix entry type must be bgp or bgpmv: " + type);
+        }
+        if (const size_t pc = x.rfind('%'); pc != std::string::npos) {
+          size_t q = pc + 1;
+          for (int k = 0; k < 3; ++k) met[k] = std::stoi(field(x, q, '/'));
+          x.resize(pc);
         }
         // node:fwd:algo:weight[:prepend] -- a node name holding ':' or ','
         // would shift the fields: this text ABI rejects it (the C++ API
@@ -502,6 +516,11 @@ std::vector<std::optional<odl::RouteDb>> buildDbs(odl_ls* h, const std::vector<s
         if (!pl.empty()) e.prependLabel = std::stoi(pl);
         e.area = area;
         e.minNexthop = minNh;
+        e.pathPreference = met[0];
+        e.sourcePreference = met[1];
+        e.distance = met[2];
+        e.bgp = !type.empty();
+        e.hasMv = type == "bgpmv";
         pr.entries.push_back(std::move(e));
       }
       prefixes.push_back(std::move(pr));
@@ -510,6 +529,7 @@ std::vector<std::optional<odl::RouteDb>> buildDbs(odl_ls* h, const std::vector<s
     opt.nodeSegmentLabels = flags & 1;
     opt.adjacencyLabels = flags & 2;
     opt.ucmp = flags & 4;
+    opt.bestRouteSelection = flags & 8;
     odl::SpfSolver solver = areas ? odl::SpfSolver(*areas) : odl::SpfSolver(h->ls);
     const auto t0 = std::chrono::steady_clock::now();
     auto dbs = solver.buildRouteDbs(mes, prefixes, opt);
@@ -523,7 +543,8 @@ std::vector<std::optional<odl::RouteDb>> buildDbs(odl_ls* h, const std::vector<s
 
 namespace {
 std::string routeDbText(const std::vector<std::string>& mes,
-                        const std::vector<std::optional<odl::RouteDb>>& dbs, bool withArea) {
+                        const std::vector<std::optional<odl::RouteDb>>& dbs, bool withArea,
+                        bool withBest = false) {
   std::ostringstream os;
   for (size_t i = 0; i < mes.size(); ++i) {
     const auto& me = mes[i];
@@ -553,6 +574,11 @@ std::string routeDbText(const std::vector<std::string>& mes,
     for (const auto& kv : dbs[i]->unicast) {
       os << me << "\tR\t" << kv.first << '\t' << kv.second.igpCost << '\t';
       if (kv.second.weight) os << *kv.second.weight; else os << '-';
+      if (withBest) {  // the best-route selection: best node@area, then every selected one
+        os << '\t' << kv.second.best.first << '@' << kv.second.best.second << '\t';
+        size_t j = 0;
+        for (const auto& na : kv.second.selected) os << (j++ ? "," : "") << na.first << '@' << na.second;
+      }
       os << '\n';
       put("U", kv.first, kv.second.nextHops);
     }
@@ -566,7 +592,7 @@ char* odl_route_db_text(odl_ls* h, const char* mes_nl, uint32_t n_mes, const cha
                         uint32_t n, int flags) {
   return guard(h, [&]() -> char* {
     const auto mes = splitNl(mes_nl, n_mes);
-    return dup(routeDbText(mes, buildDbs(h, mes, prefixes_nl, n, flags), false));
+    return dup(routeDbText(mes, buildDbs(h, mes, prefixes_nl, n, flags), false, flags & 8));
   }, (char*)nullptr);
 }
 
@@ -580,7 +606,7 @@ char* odl_route_db_multi_text(odl_ls* const* areas, uint32_t n_areas, const char
       ls.push_back(&areas[i]->ls);
     }
     const auto mes = splitNl(mes_nl, n_mes);
-    return dup(routeDbText(mes, buildDbs(areas[0], mes, prefixes_nl, n, flags, &ls), true));
+    return dup(routeDbText(mes, buildDbs(areas[0], mes, prefixes_nl, n, flags, &ls), true, flags & 8));
   }, (char*)nullptr);
 }
 

@@ -261,17 +261,41 @@ std::optional<UnicastRoute> SpfSolver::prefixRoute(const std::string& me, const 
     if (mines[areaIx(a)]->count(e.node)) entries.emplace(NodeArea{e.node, a}, &e);
   }
   if (entries.empty()) return std::nullopt;
-  bool selfPrepend = true;
-  for (const auto& [na, e] : entries)
+  bool selfPrepend = true, hasBgp = false, hasNonBgp = false, missingMv = false;
+  for (const auto& [na, e] : entries) {
     if (na.first == me) selfPrepend &= e->prependLabel.has_value();
-  // every reachable announcer is a best route (selectBestRoutes' non-BGP
-  // branch, :666-672); drained announcers drop out unless all are drained
-  // (maybeFilterDrainedNodes :709-731)
+    hasBgp |= e->bgp;
+    hasNonBgp |= !e->bgp;
+    missingMv |= e->bgp && !e->hasMv;
+  }
+  // selectBestRoutes (:650-674)
+  std::set<NodeArea> all;
+  NodeArea bestNa;
+  if (opt.bestRouteSelection) {
+    all = selectShortestDistanceRoutes(entries);
+    bestNa = *all.begin();  // selectBestNodeArea (LsdbUtil.cpp:758-769): me if selected
+    for (const auto& na : all)
+      if (na.first == me) {
+        bestNa = na;
+        break;
+      }
+  } else {
+    // mixed BGP / other types, or a BGP entry without a metric vector: the
+    // prefix is skipped (decision.skipped_unicast_route, :282-300)
+    if (hasBgp && (hasNonBgp || missingMv)) return std::nullopt;
+    if (hasBgp)
+      throw std::invalid_argument("prefix " + pr.prefix + ": BGP metric-vector best-path "
+                                  "selection (runBestPathSelectionBgp) is not restated");
+    for (const auto& kv : entries) all.insert(kv.first);  // every announcer (:666-672)
+    bestNa = *all.begin();
+  }
+  // maybeFilterDrainedNodes (:709-731): drained announcers drop out unless
+  // all are drained; the reference's bestNodeArea update there compares the
+  // filtered copy with itself (:723-727), so the best entry stays as selected
   std::set<NodeArea> best;
-  for (const auto& kv : entries)
-    if (!areas_[areaIx(kv.first.second)].second->isNodeOverloaded(kv.first.first)) best.insert(kv.first);
-  if (best.empty())
-    for (const auto& kv : entries) best.insert(kv.first);
+  for (const auto& na : all)
+    if (!areas_[areaIx(na.second)].second->isNodeOverloaded(na.first)) best.insert(na);
+  if (best.empty()) best = all;
   auto hasNode = [&](const std::string& n) {
     for (const auto& na : best)
       if (na.first == n) return true;
@@ -375,7 +399,39 @@ std::optional<UnicastRoute> SpfSolver::prefixRoute(const std::string& me, const 
   route.nextHops.assign(total.begin(), total.end());
   route.igpCost = (uint32_t)shortest;
   route.weight = ucmpWeight;
+  route.selected = best;
+  route.best = bestNa;
   return route;
+}
+
+// selectRoutes(prefixEntries, SHORTEST_DISTANCE) (LsdbUtil.cpp:837-880 +
+// selectShortestDistance :772-793): the entries with the highest
+// (path_preference, source_preference), then the smallest distance among them
+std::set<SpfSolver::NodeArea> SpfSolver::selectShortestDistanceRoutes(const Entries& entries) {
+  std::pair<int32_t, int32_t> top{std::numeric_limits<int32_t>::min(),
+                                  std::numeric_limits<int32_t>::min()};
+  std::set<NodeArea> tied;
+  for (const auto& [na, e] : entries) {
+    const std::pair<int32_t, int32_t> t{e->pathPreference, e->sourcePreference};
+    if (t < top) continue;
+    if (t > top) {
+      top = t;
+      tied.clear();
+    }
+    tied.insert(na);
+  }
+  std::set<NodeArea> out;
+  int32_t shortest = std::numeric_limits<int32_t>::max();
+  for (const auto& na : tied) {
+    const int32_t d = entries.at(na)->distance;
+    if (d > shortest) continue;
+    if (d < shortest) {
+      shortest = d;
+      out.clear();
+    }
+    out.insert(na);
+  }
+  return out;
 }
 
 std::optional<RouteDb> SpfSolver::buildRouteDb(const std::string& me,

@@ -11,9 +11,14 @@
 // summed, KSP2 next hops added), the node-label loop over every area's
 // databases (:490-598) and the adjacency labels of every area (:603-631);
 // addBestPaths' minNexthop threshold (:976-1000 with
-// getMinNextHopThreshold :694-710). RIB policy beyond that (BGP metric
-// vectors, prefix-metric best-route selection, SR policies, static routes)
-// is outside the SPF path and not restated here.
+// getMinNextHopThreshold :694-710). Best-route selection: with
+// enableBestRouteSelection the announcers are picked by their prefix metrics
+// (selectRoutes(SHORTEST_DISTANCE) + selectBestNodeArea, LsdbUtil.cpp:758-880;
+// SpfSolver.cpp:658-663), otherwise every reachable announcer is best
+// (:666-672) and a prefix announced as BGP together with another type, or by
+// a BGP entry without a metric vector, gets no route (:272-300). RIB policy
+// beyond that (BGP metric-vector comparison, SR policies, static routes) is
+// outside the SPF path and not restated here.
 #pragma once
 
 #include <cstdint>
@@ -54,9 +59,11 @@ inline bool isMplsLabelValid(int32_t l) { return (l & 0xfff00000) == 0 && l != 0
 // reads: forwarding type (0 IP, 1 SR_MPLS) and algorithm (0 SP_ECMP,
 // 1 KSP2_ED_ECMP, 2 SP_UCMP_ADJ_WEIGHT_PROPAGATION, 3
 // SP_UCMP_PREFIX_WEIGHT_PROPAGATION; OpenrConfig.thrift:18-50), UCMP weight
-// (0 = unset) and prepend label. Prefix metrics / BGP metric vectors are RIB
-// policy outside the SPF path: every reachable announcer is a best route
-// (selectBestRoutes' non-BGP branch, SpfSolver.cpp:666-672).
+// (0 = unset), prepend label, the prefix metrics best-route selection reads
+// (PrefixMetrics, Types.thrift:328-370: path_preference and
+// source_preference prefer-higher, distance prefer-lower; IDL defaults 0) and
+// the origin type as far as selectBestRoutes reads it (BGP or not, and
+// whether a BGP entry carries a metric vector).
 struct PrefixEntry {
   std::string node;
   int fwdType = 0;
@@ -65,6 +72,9 @@ struct PrefixEntry {
   std::optional<int32_t> prependLabel;
   std::string area;                  // "" = the solver's first area
   std::optional<int64_t> minNexthop;  // PrefixEntry.minNexthop (Types.thrift)
+  int32_t pathPreference = 0, sourcePreference = 0, distance = 0;
+  bool bgp = false;   // PrefixType::BGP
+  bool hasMv = false; // a BGP entry's metric vector (mv) is set
 };
 struct PrefixRoute {
   std::string prefix;
@@ -77,6 +87,11 @@ struct UnicastRoute {
   std::vector<NextHop> nextHops;
   uint32_t igpCost = 0;
   std::optional<int64_t> weight;
+  // RouteSelectionResult (bestRoutesCache_, SpfSolver.cpp:315): every
+  // selected announcer and the best one (whose entry the RibUnicastEntry
+  // carries, :1032-1041)
+  std::set<std::pair<std::string, std::string>> selected;
+  std::pair<std::string, std::string> best;
 };
 
 // DecisionRouteDb (SpfSolver.h:80-98): routes by prefix and by MPLS label,
@@ -91,6 +106,7 @@ struct RouteOptions {
   bool nodeSegmentLabels = true;
   bool adjacencyLabels = true;
   bool ucmp = false;
+  bool bestRouteSelection = false;  // enableBestRouteSelection (SpfSolver.h:113)
 };
 
 struct MinCostNextHops {
@@ -160,6 +176,7 @@ class SpfSolver {
   std::vector<NextHop> ksp2Paths(size_t ai, const std::string& me, const std::set<NodeArea>& best,
                                  const Entries& entries);
   static int32_t nodeLabel(const LinkState& ls, const std::string& node);
+  static std::set<NodeArea> selectShortestDistanceRoutes(const Entries& entries);
   size_t lsIndex() const {
     for (size_t i = 0; i < areas_.size(); ++i)
       if (areas_[i].second == &ls_) return i;

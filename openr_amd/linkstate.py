@@ -116,8 +116,11 @@ _TXT_OPS = {"0": "", "1": "PHP", "2": "SWAP", "3": "PUSH", "4": "POP"}
 
 
 def _prefix_lines(prefixes) -> List[str]:
-    """{prefix: [(node, fwd, algo, weight, prepend[, area[, min_nexthop]])]}
-    -> the text ABI's "prefix\tnode:fwd:algo:weight:prepend[@area][#n],..." lines"""
+    """{prefix: [(node, fwd, algo, weight, prepend[, area[, min_nexthop[,
+    metrics[, type]]]])]} -> the text ABI's
+    "prefix\tnode:fwd:algo:weight:prepend[%pp/sp/d][!type][@area][#n],..."
+    lines (metrics = (path_preference, source_preference, distance), type
+    None | "bgp" | "bgpmv")"""
     lines = []
     for p, ents in prefixes.items():
         es = []
@@ -125,8 +128,14 @@ def _prefix_lines(prefixes) -> List[str]:
             node, fwd, algo, weight, prepend = ent[:5]
             area = ent[5] if len(ent) > 5 else None
             mn = ent[6] if len(ent) > 6 else None
+            met = ent[7] if len(ent) > 7 else None
+            typ = ent[8] if len(ent) > 8 else None
             x = (f"{node}:{_FWDS[fwd]}:{_ALGOS[algo]}:{int(weight)}:"
                  f"{'' if prepend is None else int(prepend)}")
+            if met is not None:
+                x += "%" + "/".join(str(int(v)) for v in met)
+            if typ:
+                x += f"!{typ}"
             if area:
                 x += f"@{area}"
             if mn is not None:
@@ -145,6 +154,9 @@ def _parse_route_text(t: str, mes, with_area: bool):
             out[me] = None
         elif kind == "R":
             out[me]["routes"][f[2]] = (int(f[3]), None if f[4] == "-" else int(f[4]))
+            if len(f) > 6:  # best-route selection on: (best, selected) as (node, area)
+                sel = tuple(tuple(x.rsplit("@", 1)) for x in f[6].split(",") if x)
+                out[me].setdefault("best", {})[f[2]] = (tuple(f[5].rsplit("@", 1)), sel)
         else:
             key, ifn, nbr, metric, op, labels, w = f[2:9]
             nh = (ifn, nbr, int(metric), _TXT_OPS[op], tuple(int(x) for x in labels.split(",") if x),
@@ -156,7 +168,8 @@ def _parse_route_text(t: str, mes, with_area: bool):
 
 
 def route_dbs_multi(areas: Sequence["LinkState"], mes: Sequence[str], prefixes,
-                    node_labels: bool = True, adj_labels: bool = True, ucmp: bool = False):
+                    node_labels: bool = True, adj_labels: bool = True, ucmp: bool = False,
+                    best_route_selection: bool = False):
     """SpfSolver::buildRouteDb over several areas (odl_route_db_multi_text):
     one LinkState per area; prefix entries may carry (.., area, min_nexthop).
     Same result shape as LinkState.route_dbs(binary=False) with the next
@@ -164,7 +177,8 @@ def route_dbs_multi(areas: Sequence["LinkState"], mes: Sequence[str], prefixes,
     L = N.decision()
     hs = (C.c_void_p * len(areas))(*[a._h for a in areas])
     lines = _prefix_lines(prefixes)
-    flags = int(node_labels) | (2 if adj_labels else 0) | (4 if ucmp else 0)
+    flags = int(node_labels) | (2 if adj_labels else 0) | (4 if ucmp else 0) | \
+        (8 if best_route_selection else 0)
     p = L.odl_route_db_multi_text(hs, len(areas), "\n".join(mes).encode(), len(mes),
                                   "\n".join(lines).encode(), len(lines), flags)
     if not p:
@@ -252,7 +266,7 @@ class LinkState:
 
     def route_dbs(self, mes: Sequence[str], prefixes: Dict[str, Sequence],
                   node_labels: bool = True, adj_labels: bool = True, ucmp: bool = False,
-                  binary: bool = True):
+                  binary: bool = True, best_route_selection: bool = False):
         """SpfSolver::buildRouteDb (odl::SpfSolver, C++) for every node in
         `mes`, over SPF results from one batched engine launch.
 
@@ -264,8 +278,9 @@ class LinkState:
         with kind 'U' (prefix) or 'M' (MPLS label) and op 'PHP' | 'SWAP' |
         'PUSH' | 'POP' | ''."""
         lines = _prefix_lines(prefixes)
-        flags = int(node_labels) | (2 if adj_labels else 0) | (4 if ucmp else 0)
-        if binary:  # odl_route_db_bin: records + a string table, no text
+        flags = int(node_labels) | (2 if adj_labels else 0) | (4 if ucmp else 0) | \
+            (8 if best_route_selection else 0)
+        if binary and not best_route_selection:  # odl_route_db_bin: records + strings, no text
             return decode_route_db_bin(self.route_db_bin_raw(mes, lines, flags))
         t = self._take(self._L.odl_route_db_text(
             self._h, "\n".join(mes).encode(), len(mes), "\n".join(lines).encode(),

@@ -868,6 +868,59 @@ fixtures.append(dict(
     ])])]))
 
 
+# Decision.BestRouteSelection (DecisionTest.cpp:1240-1384): SpfSolver with
+# enableBestRouteSelection; 2 <-> 1 <-> 3 (adj12, adj13, adj21, adj31 of
+# :46-106: metric 10); addr1 announced by 2 (DEFAULT) and 3 (BGP, no metric
+# vector -- the type plays no part in best-route selection), createMetrics(pp,
+# sp, d) (LsdbUtil.cpp:556-562). Entry = [node, fwd, algo, weight, prepend,
+# area, minNexthop, (pp, sp, d), type].
+_b1 = [db(1, [dadj(1, 2), dadj(1, 3)], 1), db(2, [dadj(2, 1)], 2), db(3, [dadj(3, 1)], 3)]
+_bopt = dict(best_route_selection=True)
+
+
+def _be(node, fwd, met, typ=None):
+    return [str(node), fwd, "ecmp", 0, None, None, None, list(met), typ]
+
+
+fixtures.append(dict(
+    name="decision_best_route_selection",
+    source="openr/decision/tests/DecisionTest.cpp:1240-1384",
+    steps=[dict(dbs=_b1, checks=[
+        # Case 1 (:1291-1320): node 1 ECMP towards {2, 3}; best routes {2, 3},
+        # best node 2
+        route_map([1], {ADDR[1]: [_be(2, "ip", (200, 0, 0)), _be(3, "ip", (200, 0, 0), "bgp")]},
+                  opts=_bopt, expect_counts={"1": [1, None]},
+                  expect={f"1|U|{ADDR[1]}": [H("1/2", 2, 10), H("1/3", 3, 10)]},
+                  expect_best={f"1|{ADDR[1]}": ["2", ["2", "3"]]}),
+        # Case 2 (:1322-1352): node 2's source preference 100 -> only node 2
+        route_map([1], {ADDR[1]: [_be(2, "ip", (200, 100, 0)), _be(3, "ip", (200, 0, 0), "bgp")]},
+                  opts=_bopt, expect_counts={"1": [1, None]},
+                  expect={f"1|U|{ADDR[1]}": [H("1/2", 2, 10)]},
+                  expect_best={f"1|{ADDR[1]}": ["2", ["2"]]}),
+        # Case 3 (:1354-1383): the forwarding type comes from the best entry:
+        # node 2 SR_MPLS (preferred), node 3 IP; from node 3: PUSH 2 via 1
+        route_map([3], {ADDR[1]: [_be(2, "sr_mpls", (200, 100, 0)),
+                                  _be(3, "ip", (200, 0, 0), "bgp")]},
+                  opts=_bopt, expect_counts={"3": [1, None]},
+                  expect={f"3|U|{ADDR[1]}": [H("3/1", 1, 20, "PUSH", [2])]}),
+    ])]))
+
+# EnableBestRouteSelectionFixture.PrefixWithMixedTypeRoutes
+# (DecisionTest.cpp:7203-7290): 10.1.0.0/16 announced by 2 as BGP (with a
+# metric vector, empty) and by 3 as RIB: skipped (decision.skipped_unicast_
+# route) unless best-route selection is on.
+_mix = {"10.1.0.0/16": [[ "2", "ip", "ecmp", 0, None, None, None, None, "bgpmv"],
+                        ["3", "ip", "ecmp", 0, None, None, None, None, None]]}
+fixtures.append(dict(
+    name="decision_best_route_selection_mixed_types",
+    source="openr/decision/tests/DecisionTest.cpp:7203-7290",
+    steps=[dict(dbs=_b1, checks=[
+        route_map([1], _mix, opts=dict(best_route_selection=False),
+                  expect_counts={"1": [0, None]}, expect_absent=["1|U|10.1.0.0/16"]),
+        route_map([1], _mix, opts=_bopt, expect_counts={"1": [1, None]}),
+    ])]))
+
+
 def main():
     for fx in fixtures:
         with open(os.path.join(HERE, fx["name"] + ".json"), "w") as f:

@@ -132,9 +132,11 @@ class RouteBuilder:
     Next hop = (ifName, neighbor, metric i32, op, labels, weight)."""
 
     def __init__(self, ls, dbs: Dict[str, dict], ucmp: bool = False,
-                 node_labels: bool = True, adj_labels: bool = True):
+                 node_labels: bool = True, adj_labels: bool = True,
+                 best_route_selection: bool = False, area: str = "0"):
         self.ls, self.dbs, self.ucmp = ls, dbs, ucmp
         self.node_labels, self.adj_labels = node_labels, adj_labels
+        self.best_sel, self.area = best_route_selection, area
         self._spf = {}
 
     def spf(self, me):
@@ -239,7 +241,28 @@ class RouteBuilder:
         if not entries:
             return None
         self_prepend = entries[me][4] is not None if me in entries else True
-        best = sorted(n for n in entries if not self.ls.is_overloaded(n)) or sorted(entries)
+        # selectBestRoutes (SpfSolver.cpp:650-674)
+        if self.best_sel:
+            # selectRoutes(SHORTEST_DISTANCE) (LsdbUtil.cpp:772-793,837-880):
+            # highest (path_preference, source_preference), then lowest distance
+            def met(n):
+                e = entries[n]
+                return tuple(e[7]) if len(e) > 7 and e[7] is not None else (0, 0, 0)
+            top = max(met(n)[:2] for n in entries)
+            tied = [n for n in entries if met(n)[:2] == top]
+            dmin = min(met(n)[2] for n in tied)
+            sel = sorted(n for n in tied if met(n)[2] == dmin)
+            best_node = me if me in sel else sel[0]  # selectBestNodeArea (:758-769)
+        else:
+            typ = {n: (e[8] if len(e) > 8 else None) for n, e in entries.items()}
+            if any(typ.values()) and (not all(typ.values()) or "bgp" in typ.values()):
+                return None  # mixed BGP / other, or BGP without mv (:282-300)
+            assert not any(typ.values()), "BGP metric-vector selection is not restated"
+            sel = sorted(entries)
+            best_node = sel[0]
+        # maybeFilterDrainedNodes (:709-731): the best entry stays as selected
+        best = sorted(n for n in sel if not self.ls.is_overloaded(n)) or sel
+        self.last_best = ((best_node, self.area), tuple((n, self.area) for n in best))
         if me in best and not self_prepend:
             return None
         fwd = min({"ip": 0, "sr_mpls": 1}[entries[n][1]] for n in best)
@@ -286,6 +309,8 @@ class RouteBuilder:
             if r is not None:
                 out["routes"][p] = r[0]
                 out[("U", p)] = r[1]
+                if self.best_sel:
+                    out.setdefault("best", {})[p] = self.last_best
         if self.node_labels:
             label_to = {}
             for node in sorted(self.dbs):
@@ -351,6 +376,11 @@ def check_route_map(c, dbs_of: Callable[[str], dict], where: str):
         node, kind, key = k.split("|", 2)
         got = dbs_of(node)[(kind, key)]
         assert {h[2] for h in got} == {m}, f"{where}: {k} metrics {got}"
+    for k, (b, sel) in c.get("expect_best", {}).items():
+        node, key = k.split("|", 1)  # bestRoutesCache_: best node, every selected node
+        got = dbs_of(node)["best"][key]
+        assert got[0][0] == b and sorted(x[0] for x in got[1]) == sorted(sel), \
+            f"{where}: {k} best {got}"
     for k, w in c.get("expect_weight", {}).items():
         node, key = k.split("|", 1)
         assert dbs_of(node)["routes"][key][1] == w, \

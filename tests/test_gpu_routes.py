@@ -90,3 +90,29 @@ def test_route_dbs_without_labels():
     for me in names:
         assert got[me] == rb.build(me, prefixes)
         assert not any(k[0] == "M" for k in got[me] if k != "routes")
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_best_route_selection_matches_restatement(seed):
+    """enableBestRouteSelection (SpfSolver.cpp:658-663; selectRoutes
+    SHORTEST_DISTANCE + selectBestNodeArea, LsdbUtil.cpp:758-880) on random
+    multi-announcer prefixes with random prefix metrics and origin types:
+    the product's routes and best-route results equal the restatement's."""
+    dbs, names, prefixes = random_routing_case(100 + seed)
+    rng = np.random.default_rng(seed)
+    for ents in prefixes.values():
+        for e in ents:
+            met = [int(rng.integers(0, 3)) * 100, int(rng.integers(0, 2)) * 50,
+                   int(rng.integers(0, 3))]
+            e += [None, None, met, [None, "bgp", "bgpmv"][int(rng.integers(0, 3))]]
+    stream = AdjDbStream.from_dbs(dbs)
+    o, p = OracleLS(), LinkState()
+    assert o.apply(stream) == p.apply(stream)
+    cur = {d.name: dataclasses.asdict(d) for d in dbs}
+    rb = RouteBuilder(o, cur, best_route_selection=True)
+    got = p.route_dbs(names, prefixes, best_route_selection=True)
+    n_best = 0
+    for me in names:
+        assert got[me] == rb.build(me, prefixes), me
+        n_best += len((got[me] or {}).get("best", {}))
+    assert n_best > len(names)

@@ -168,3 +168,21 @@ def test_bulk_ingest_matches_oracle():
             ol = [tuple(ln.split("\t")) for ln in o.links_text(nm).splitlines()]
             pl = [(k, str(m), "1" if up else "0") for k, m, up in _links(p, nm)]
             assert ol == pl, nm
+
+
+def _host_product():
+    p = LinkState()
+    p.set_host_spf(True)  # the product's C++ LinkState + SpfSolver, SPF on the host path
+    return p
+
+
+ROUTE_FIXTURES = [f for f in FIXTURES if "route" in f["name"] or "mpls" in f["name"]]
+
+
+@pytest.mark.parametrize("fx", ROUTE_FIXTURES, ids=[f["name"] for f in ROUTE_FIXTURES])
+def test_route_fixtures_through_product_host_spf(fx):
+    """The reference's route fixtures (incl. Decision.BestRouteSelection and
+    the mixed-type case, DecisionTest.cpp:1240-1384,7203-7290) through the
+    C++ odl::SpfSolver on the host SPF path; -m gpu runs the same on the
+    engine (test_gpu_parity.py::test_reference_fixture_on_gpu)."""
+    assert run_fixture(fx, _host_product) > 0

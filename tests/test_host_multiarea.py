@@ -5,8 +5,10 @@ of every area (:603-631) and addBestPaths' minNexthop threshold (:976-1000,
 getMinNextHopThreshold :694-710). Expectations transcribed from the
 reference's DecisionTestFixture.MultiAreaBestPathCalculation
 (openr/decision/tests/DecisionTest.cpp:5702-5836) and the minNexthop part of
-ParallelAdjRingTopologyFixture.Ksp2EdEcmp (:3899-3951). GPU-free
-(odl_set_host_spf); the route build is host code either way."""
+ParallelAdjRingTopologyFixture.Ksp2EdEcmp (:3899-3951). Each test runs twice:
+GPU-free (odl_set_host_spf) and, under -m gpu, with every SPF on the engine
+(the route build is host code, the SPF results it reads
+are the engine's)."""
 import sys
 import os
 
@@ -37,9 +39,19 @@ adj42 = _adj("2", "4/2", "2/4", 10, 100002)
 adj43 = _adj("3", "4/3", "3/4", 10, 100003)
 
 
+MODE = {"spf": "host"}
+
+
+@pytest.fixture(autouse=True, params=["host", pytest.param("gpu", marks=pytest.mark.gpu)])
+def spf_mode(request):
+    MODE["spf"] = request.param
+    yield request.param
+    MODE["spf"] = "host"
+
+
 def ls(area, dbs):
     p = LinkState(area=area)
-    p.set_host_spf(True)
+    p.set_host_spf(MODE["spf"] == "host")
     p.apply(AdjDbStream.from_dbs(dbs))
     return p
 
