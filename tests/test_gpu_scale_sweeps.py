@@ -232,6 +232,77 @@ def test_m1m_wmulti_sweep_part():
 
 
 
+def text_fields_of_row(names, nbrs, dist, nh):
+    """{name: (metric, sorted next-hop names)} of one root's engine rows: the
+    first two fields of the getSpfResult text (DESIGN.md §Result text)."""
+    out = {}
+    inf = np.uint32(0xFFFFFFFF)
+    for v in np.nonzero(dist != inf)[0].tolist():
+        hops = []
+        for w in range(nh.shape[1]):
+            x = int(nh[v, w])
+            while x:
+                b = (x & -x).bit_length() - 1
+                hops.append(names[int(nbrs[32 * w + b])])
+                x &= x - 1
+        out[names[v]] = (int(dist[v]), tuple(sorted(hops)))
+    return out
+
+
+@pytest.mark.timeout(1200)
+def test_m1m_wderive_sweep_part():
+    """The M1M path bench.py --topology mesh1m measures:
+    the middle part of the 122-part all-sources partition on the weighted
+    derive sweep (sweep:wderive -- per-root Dial for the part's cover roots,
+    leaf rows derived from their neighbours' rows). 64 roots' digests == the
+    CSR-Dijkstra restatement; every node's metric and next-hop set of 2 roots
+    (a leaf and a cover root) == the reference-shaped runSpf text
+    (LinkState.cpp:836-911); triangle + tight-last-hop checks on 4 rows."""
+    from oracle import parse_spf_text
+    st = T.mesh(1_000_000, seed=42)
+    o, p = Oracle(), LinkState()
+    assert o.apply(st) == p.apply(st)
+    names = p.node_names()
+    csr = p.csr()
+    note("ingested")
+    eng = Engine()
+    eng.load(csr)
+    sw = Sweep(eng, part=61, n_parts=122, mode="wderive", hip_graph=False)
+    assert sw.mode == "wderive"
+    n = sw.n_roots
+    assert 7000 < n < 9500, n
+    sw.run()
+    eng.sync()
+    d = np.zeros((n, 3), np.uint64)
+    sw._check(sw._L.ospf_sweep_digests_host(sw._h, d.ctypes.data))
+    got = dict(zip(sw.roots.tolist(), d))
+    note(f"wderive part: {n} roots, {sw.n_rows} rows")
+    roots = np.sort(sw.roots)
+    rng = np.random.default_rng(5)
+    pick = np.sort(rng.choice(roots, 64, replace=False))
+    want = o.fast_digests([names[i] for i in pick], True, threads=16)
+    bad = [names[r] for j, r in enumerate(pick) if not np.array_equal(got[int(r)], want[j])]
+    assert not bad, (len(bad), bad[:8])
+    note("64 roots == CSR-Dijkstra")
+    # a leaf root (<= 32 neighbours, derived) and the widest root of the part
+    deg = np.array([eng.root_neighbors(int(r)).size for r in roots])
+    two = [int(roots[int(np.argmin(deg))]), int(roots[int(np.argmax(deg))])]
+    for r in two:
+        W = max(1, eng.nh_words(r))
+        dist, nh = sw.rows(np.array([r], np.uint32), W)
+        mine = text_fields_of_row(names, eng.root_neighbors(r), dist[0], nh[0])
+        ref = {k: (v[0], tuple(sorted(v[1]))) for k, v in
+               parse_spf_text(o.spf_text(names[r])).items()}
+        assert mine == ref, names[r]
+        note(f"{names[r]}: {len(mine)} nodes' metric + next hops == reference-shaped runSpf")
+    for r in pick[:4].tolist():
+        dist, _ = sw.rows(np.array([r], np.uint32), max(1, eng.nh_words(r)))
+        triangle_and_tight(csr, r, dist[0])
+    note("triangle + tight last hops")
+    sw.close()
+    eng.close()
+
+
 @pytest.mark.timeout(900)
 def test_f100k_weighted_sweep_whole_rows_vs_scipy():
     """Whole dist + next-hop rows of the weighted F100k (metrics 1..64)
