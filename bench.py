@@ -676,14 +676,17 @@ def store_probe(eng, V: int, dom: dict, args):
     if V % 4 or dom["roots_per_launch"] <= 0:
         return None
     rows = int(dom["roots_per_launch"])
-    out = {"bytes": 2 * rows * V * 4, "rows": rows, "group": 48, "ctiles": 6,
-           "note": "ospf_probe_store: 16-B non-temporal stores of 2 x rows x V u32 (the dominant "
-                   "launch's dist + next-hop rows), median of 3 HIP-event-timed launches after one "
+    P = (V + 31) // 32 * 32 if os.environ.get("OSPF_SWEEP_ROW_PITCH", "") != "V" else V
+    out = {"bytes": 2 * rows * P * 4, "rows": rows, "row_pitch_words": P, "group": 48,
+           "ctiles": 6,
+           "note": "ospf_probe_store: 16-B non-temporal stores of 2 x rows x pitch u32 (the dominant "
+                   "launch's dist + next-hop rows at the sweep's row pitch: V rounded up to 32 "
+                   "words, 128-B aligned rows), median of 3 HIP-event-timed launches after one "
                    "untimed; rows_* = blocks of 48 rows x 6 tiles of 1,024 nodes, the leaf "
                    "launch's shape"}
     for pat in ("stream", "rows_chunk", "rows_group"):
         try:
-            ms = float(np.median(eng.probe_store(pat, V, rows, 48, 6, reps=3)))
+            ms = float(np.median(eng.probe_store(pat, P, rows, 48, 6, reps=3)))
         except Exception as e:  # noqa: BLE001 -- evidence only (e.g. no room beside the sweep)
             out[pat + "_error"] = str(e)
             continue

@@ -678,12 +678,15 @@ int ospf_inject_error(ospf_ctx* ctx, uint32_t after_calls);
  * launches after one untimed one, ms_out[reps]. pattern 0 = one buffer in
  * address order; 1 = two [rows][V] u32 arrays written the way the leaf
  * launch writes its dist and next-hop rows (blocks of `group` rows x
- * `ctiles` 1,024-node tiles, chunk-major); 2 = the same blocks group-major.
+ * `ctiles` 1,024-node tiles, chunk-major); 2 = the same blocks group-major;
+ * 3 = persistent blocks (`ctiles` per CU) taking (group, tile) items in
+ * group-major order (the chip walks the rows in order).
  * Allocates (and frees) its own buffer: OSPF_E_NOMEM when it does not fit.
  * V must be a multiple of 4. */
 #define OSPF_PROBE_STREAM 0u
 #define OSPF_PROBE_ROWS_CHUNK 1u
 #define OSPF_PROBE_ROWS_GROUP 2u
+#define OSPF_PROBE_ROWS_WALK 3u
 int ospf_probe_store(ospf_ctx* ctx, uint32_t pattern, uint32_t V, uint32_t rows, uint32_t group,
                      uint32_t ctiles, uint32_t reps, float* ms_out);
 

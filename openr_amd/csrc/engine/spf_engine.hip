@@ -1824,6 +1824,15 @@ int ospf_sync(ospf_ctx* c, void* stream) {
 int ospf_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t flags,
                     uint32_t* d_dist, uint8_t* d_lev, uint32_t lev_pitch,
                     ospf_digest* d_lev_digest, void* stream) {
+  return ospf_int::levels_dev(c, d_roots, n, flags, d_dist, 0, d_lev, lev_pitch, d_lev_digest,
+                              stream);
+}
+}  // extern "C"
+
+namespace ospf_int {
+int levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t flags,
+               uint32_t* d_dist, uint32_t dist_pitch, uint8_t* d_lev, uint32_t lev_pitch,
+               ospf_digest* d_lev_digest, void* stream) {
   if (!c) return OSPF_E_INVAL;
   if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
   if (n == 0) return OSPF_OK;
@@ -1866,6 +1875,7 @@ int ospf_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t f
     a.masked = 0;
     if (const char* e = getenv("OSPF_LV_MASKED")) a.masked = (uint32_t)atoi(e);
     a.dist = d_dist;
+    a.dpitch = dist_pitch;
     a.levrow = d_lev;
     a.lev_pitch = lev_pitch;
     a.digest = d_lev_digest;
@@ -1923,6 +1933,8 @@ int ospf_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t f
   HIPCHK(c, hipSetDevice(c->device));
   uint32_t push_div = 8;
   if (const char* e = getenv("OSPF_MS_PUSH_DIV")) push_div = (uint32_t)std::max(0, atoi(e));
+  if (dist_pitch && dist_pitch != V)
+    return fail(c, OSPF_E_INVAL, "levels (OSPF_LV64): dist rows of pitch V only");
   ospf::MsArgs a{};
   a.roots = d_roots;
   a.n = n;
@@ -1965,6 +1977,9 @@ int ospf_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t f
   c->spf_runs += n;
   return OSPF_OK;
 }
+}  // namespace ospf_int
+
+extern "C" {
 
 int ospf_nh_derive_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t nh_words,
                        uint32_t max_root_neighbors, const uint8_t* d_lev, uint32_t lev_pitch,
@@ -2024,7 +2039,8 @@ int nh_derive_twin_launch(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint
                           const uint32_t* d_lev_pos, const ospf_digest* d_lev_digest,
                           const uint32_t* d_twin_class, const uint32_t* d_twin_rep,
                           const uint32_t* d_twin_second, uint32_t* d_nh, ospf_digest* d_digest,
-                          uint32_t* d_dist, void* stream) {
+                          uint32_t* d_dist, void* stream, uint32_t dist_pitch,
+                          uint32_t nh_pitch) {
   if (!c) return OSPF_E_INVAL;
   if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
   if (n == 0) return OSPF_OK;
@@ -2054,6 +2070,10 @@ int nh_derive_twin_launch(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint
   a.digest = d_digest;
   a.err = c->d_err;
   a.dist = d_dist;
+  a.dpitch = dist_pitch;
+  a.npitch = nh_pitch;
+  if (nh_pitch && (nh_pitch < c->info.n_nodes * nh_words || nh_pitch % 4u))
+    return fail(c, OSPF_E_INVAL, "twin derive: next-hop row pitch < V * nh_words");
   if (const char* e = getenv("OSPF_TWIN_CTILES")) a.ctiles = (uint32_t)std::max(1, atoi(e));
   hipError_t e = ospf::launch_nh_derive_twin(c->g, a, s);
   if (e != hipSuccess) return hip_fail(c, e, "launch_nh_derive_twin");
@@ -2151,6 +2171,17 @@ int ospf_leaf_derive2_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n,
                           uint32_t max_root_neighbors, uint8_t* d_lev, uint32_t lev_pitch,
                           const uint32_t* d_pos, const uint32_t* d_lev_out, uint32_t* d_dist,
                           uint32_t* d_nh, ospf_digest* d_digest, void* stream) {
+  return ospf_int::leaf_derive(c, d_roots, n, d_groups, n_groups, max_root_neighbors, d_lev,
+                               lev_pitch, d_pos, d_lev_out, d_dist, 0, d_nh, 0, d_digest, stream);
+}
+}  // extern "C"
+
+namespace ospf_int {
+int leaf_derive(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, const uint32_t* d_groups,
+                uint32_t n_groups, uint32_t max_root_neighbors, uint8_t* d_lev,
+                uint32_t lev_pitch, const uint32_t* d_pos, const uint32_t* d_lev_out,
+                uint32_t* d_dist, uint32_t dist_pitch, uint32_t* d_nh, uint32_t nh_pitch,
+                ospf_digest* d_digest, void* stream) {
   if (!c) return OSPF_E_INVAL;
   if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
   if (n == 0) return OSPF_OK;
@@ -2179,11 +2210,16 @@ int ospf_leaf_derive2_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n,
   a.err = c->d_err;
   if (const char* e = getenv("OSPF_LEAF_CTILES")) a.ctiles = (uint32_t)std::max(1, atoi(e));
   if (const char* e = getenv("OSPF_LEAF_GROUP_MAJOR")) a.group_major = atoi(e) ? 1u : 0u;
+  a.dpitch = dist_pitch;
+  a.npitch = nh_pitch;
   hipError_t e = ospf::launch_leaf_derive(c->g, a, max_root_neighbors ? max_root_neighbors : 32u, s);
   if (e != hipSuccess) return hip_fail(c, e, "launch_leaf_derive");
   c->spf_runs += n;
   return OSPF_OK;
 }
+}  // namespace ospf_int
+
+extern "C" {
 
 // Small-graph sweep (spf_small.hip): waves per block that fit the LDS (0 =
 // the graph does not fit, or the run is outside the kernel's contract).

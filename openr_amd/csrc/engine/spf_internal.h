@@ -175,7 +175,18 @@ int nh_derive_twin_launch(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint
                           const uint32_t* d_lev_pos, const ospf_digest* d_lev_digest,
                           const uint32_t* d_twin_class, const uint32_t* d_twin_rep,
                           const uint32_t* d_twin_second, uint32_t* d_nh, ospf_digest* d_digest,
-                          uint32_t* d_dist, void* stream);
+                          uint32_t* d_dist, void* stream, uint32_t dist_pitch = 0,
+                          uint32_t nh_pitch = 0);
+// ospf_levels_dev / ospf_leaf_derive2_dev with row pitches (words; 0 = V)
+// for the dist and next-hop rows: the sweep keeps its rows 128-B aligned
+int levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t flags,
+               uint32_t* d_dist, uint32_t dist_pitch, uint8_t* d_lev, uint32_t lev_pitch,
+               ospf_digest* d_lev_digest, void* stream);
+int leaf_derive(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, const uint32_t* d_groups,
+                uint32_t n_groups, uint32_t max_root_neighbors, uint8_t* d_lev,
+                uint32_t lev_pitch, const uint32_t* d_pos, const uint32_t* d_lev_out,
+                uint32_t* d_dist, uint32_t dist_pitch, uint32_t* d_nh, uint32_t nh_pitch,
+                ospf_digest* d_digest, void* stream);
 
 // Host plan of the cover closure (spf_cover.hip closure_kernel) for the
 // closure roots `roots` (node ids, non-seed cover nodes; dc row i = roots[i])

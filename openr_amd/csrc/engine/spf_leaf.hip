@@ -136,7 +136,8 @@ __global__ void __launch_bounds__(kBlock) leaf_derive_kernel(DevGraph g, LeafArg
   uint32_t tab[KM];
 #pragma unroll
   for (int k = 0; k < KM; ++k) tab[k] = s_tab[k];
-  const bool vec = (V & 3u) == 0;
+  const uint32_t dpitch = a.dpitch ? a.dpitch : V, npitch = a.npitch ? a.npitch : V;
+  const bool vec = (V & 3u) == 0 && (dpitch & 3u) == 0 && (npitch & 3u) == 0;
   uint32_t br = 0;
   uint64_t bs = 0, bh = 0;
   const uint32_t t0 = ci * a.ctiles, t1 = min(a.tiles, t0 + a.ctiles);
@@ -232,8 +233,8 @@ __global__ void __launch_bounds__(kBlock) leaf_derive_kernel(DevGraph g, LeafArg
       if (lrow != kInf)
         __builtin_nontemporal_store(Lj, reinterpret_cast<uint32_t*>(a.lev + (size_t)lrow * a.pitch + v0));
       if (v0 >= V) continue;
-      uint32_t* nrow = a.nh + (size_t)(i0 + j) * V + v0;
-      uint32_t* drow = a.dist ? a.dist + (size_t)own * V + v0 : nullptr;
+      uint32_t* nrow = a.nh + (size_t)(i0 + j) * npitch + v0;
+      uint32_t* drow = a.dist ? a.dist + (size_t)own * dpitch + v0 : nullptr;
       if (vec) {
         store_row16(nrow, make_uint4(wj[0], wj[1], wj[2], wj[3]));
         if (drow) store_row16(drow, make_uint4(dj[0], dj[1], dj[2], dj[3]));

@@ -462,7 +462,7 @@ __global__ void __launch_bounds__(256) lv_rows_kernel(DevGraph g, LvArgs a) {
         }
       }
       if (a.dist) {
-        uint32_t* row = a.dist + (size_t)(base + r) * V + vq;
+        uint32_t* row = a.dist + (size_t)(base + r) * (a.dpitch ? a.dpitch : V) + vq;
         if (vec) {
           store_row16(row, make_uint4(dv[0], dv[1], dv[2], dv[3]));
         } else {

@@ -15,6 +15,9 @@
 //   2 ROWS_GROUP   the same blocks, group-major (consecutive blocks = one
 //                  group's chunks): the rows in flight at once span a few
 //                  groups instead of one chunk of every group
+//   3 ROWS_WALK    persistent blocks (ctiles per CU), items = (group, tile)
+//                  group-major, grid-stride: the whole chip walks the rows in
+//                  order, a few groups in flight
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -54,13 +57,34 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// persistent blocks, items = (group of `group` rows, one 1,024-node tile),
+// group-major, handed out grid-stride: the chip's in-flight writes stay in a
+// window of a few groups' rows (the whole chip walks the rows in order)
+__global__ void __launch_bounds__(256)
+    probe_rows_walk_kernel(uint32_t* a, uint32_t* b, uint32_t V, uint32_t rows, uint32_t group,
+                           uint32_t ngroups, uint32_t tiles, uint32_t val) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint4 v = make_uint4(val, val ^ 1u, val ^ 2u, val ^ 3u);
+  const uint64_t items = (uint64_t)ngroups * tiles;
+  for (uint64_t it = blockIdx.x; it < items; it += gridDim.x) {
+    const uint32_t gr = (uint32_t)(it / tiles), t = (uint32_t)(it % tiles);
+    const uint32_t r0 = gr * group, nr = min(group, rows - r0);
+    const uint32_t v0 = t * 1024u + wave * 256u + 4u * lane;
+    if (v0 >= V) continue;
+    for (uint32_t j = 0; j < nr; ++j) {
+      store_row16(a + (size_t)(r0 + j) * V + v0, v);
+      store_row16(b + (size_t)(r0 + j) * V + v0, v);
+    }
+  }
+}
+
 }  // namespace
 }  // namespace ospf
 
 int ospf_probe_store(ospf_ctx* c, uint32_t pattern, uint32_t V, uint32_t rows, uint32_t group,
                      uint32_t ctiles, uint32_t reps, float* ms_out) {
   if (!c || !ms_out || reps == 0) return OSPF_E_INVAL;
-  if (pattern > 2) return ospf_int::fail(c, OSPF_E_INVAL, "probe: pattern 0..2");
+  if (pattern > 3) return ospf_int::fail(c, OSPF_E_INVAL, "probe: pattern 0..3");
   if (V == 0 || (V & 3u) || rows == 0 || group == 0)
     return ospf_int::fail(c, OSPF_E_INVAL, "probe: V a positive multiple of 4, rows, group > 0");
   const size_t row_bytes = (size_t)V * 4u, half = row_bytes * rows;
@@ -92,6 +116,11 @@ int ospf_probe_store(ospf_ctx* c, uint32_t pattern, uint32_t V, uint32_t rows, u
       const size_t n16 = 2 * half / 16u;
       hipLaunchKernelGGL(ospf::probe_stream_kernel, dim3(c->n_cu * 8u), dim3(256), 0, s,
                          reinterpret_cast<uint4*>(buf), n16, 0x5A5A0000u + i);
+    } else if (pattern == 3) {
+      hipLaunchKernelGGL(ospf::probe_rows_walk_kernel, dim3(c->n_cu * (ctiles ? ctiles : 8u)),
+                         dim3(256), 0, s, reinterpret_cast<uint32_t*>(buf),
+                         reinterpret_cast<uint32_t*>(buf + half), V, rows, group, ngroups, tiles,
+                         0x5A5A0000u + i);
     } else {
       hipLaunchKernelGGL(ospf::probe_rows_kernel, dim3(ngroups * chunks), dim3(256), 0, s,
                          reinterpret_cast<uint32_t*>(buf), reinterpret_cast<uint32_t*>(buf + half),

@@ -307,6 +307,16 @@ int new_event(ospf_sweep* s) {
   return (int)s->events.size() - 1;
 }
 
+// Row pitch (u32 words) of the sweep's dist / one-word next-hop rows: V
+// rounded up to 32 words (128-B aligned rows) when V is a multiple of 4 (the
+// 16-B store path); OSPF_SWEEP_ROW_PITCH=V keeps the packed pitch (A/B knob)
+uint32_t row_pitch(uint32_t V) {
+  if (V & 3u) return V;
+  if (const char* e = getenv("OSPF_SWEEP_ROW_PITCH"))
+    if (e[0] == 'V') return V;
+  return (V + 31u) / 32u * 32u;
+}
+
 // CSR bytes one distance-only scan reads: neighbour ids + row offsets
 uint64_t scan_bytes(const ospf_ctx* c, bool weighted) {
   return (uint64_t)(weighted ? 8 : 4) * c->info.n_edges + 4ull * (c->info.n_nodes + 1);
@@ -1005,17 +1015,22 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   uint32_t rows = nc + nd;
   for (uint32_t i = 0; i < nL; ++i)
     if (pos[need_l[i]] == kNone) pos[need_l[i]] = rows++;
-  const uint32_t pitch = (V + 15) / 16 * 16;
+  // level rows (bytes), dist and leaf next-hop rows 128-B aligned (pitch a multiple of 32
+  // words): every 1-KB wave store of the row writers then covers whole lines
+  // (ospf_probe_store, leaf-shaped rows at V = 100,024: 7.0 TB/s aligned
+  // against 5.8 TB/s at the 400,096-B pitch; profiles/r06/a3_*)
+  const uint32_t DP = row_pitch(V);
+  const uint32_t pitch = DP == V ? (V + 15) / 16 * 16 : (V + 127) / 128 * 128;
   uint32_t *d_clo = nullptr, *d_pos, *dist, *d_l = nullptr, *lnh = nullptr;
   uint32_t *d_grp_r = nullptr, *d_grp = nullptr, *d_lout = nullptr;
   uint8_t* lev;
   ospf_digest* ldg;
   int rc;
   if ((rc = upload(s, &d_pos, pos)) || (rc = dalloc(s, &lev, (size_t)rows * pitch)) ||
-      (rc = dalloc(s, &dist, (size_t)rows * V)) || (rc = dalloc(s, &ldg, std::max(1u, nc + nd))))
+      (rc = dalloc(s, &dist, (size_t)rows * DP)) || (rc = dalloc(s, &ldg, std::max(1u, nc + nd))))
     return rc;
   if (nc && (rc = upload(s, &d_clo, clo))) return rc;
-  if (nL && ((rc = upload(s, &d_l, need_l)) || (rc = dalloc(s, &lnh, (size_t)nL * V))))
+  if (nL && ((rc = upload(s, &d_l, need_l)) || (rc = dalloc(s, &lnh, (size_t)nL * DP))))
     return rc;
   if (nR && (rc = upload(s, &d_grp_r, grp_r))) return rc;
   if (nL > nR && (rc = upload(s, &d_grp, grp))) return rc;
@@ -1058,7 +1073,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     lv.n_roots = nc;
     lv.comp = (uint64_t)nc * 4ull * V + ((nc + 127) / 128) * scan_bytes(c, false);
     lv.fn = [=](hipStream_t st) {
-      return ospf_levels_dev(c, d_clo, nc, hop, dist, lev, pitch, ldg, st);
+      return ospf_int::levels_dev(c, d_clo, nc, hop, dist, DP, lev, pitch, ldg, st);
     };
     s->step_comp += lv.comp;
     s->units.push_back(lv);
@@ -1099,6 +1114,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     plan.lev = lev;
     plan.pitch = pitch;
     plan.dist = dist;
+    plan.dpitch = DP;
     plan.lev_digest = ldg;
     ospf_sweep::Unit u;
     u.name = S > 1 ? "twin_levels_s" + std::to_string(k) : std::string("twin_levels");
@@ -1130,10 +1146,13 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       });
     const uint32_t n = (uint32_t)k.roots.size(), W = k.W, cap = std::min(k.cap, 2048u);
     uint32_t *d_roots, *nh;
-    if ((rc = upload(s, &d_roots, k.roots)) || (rc = dalloc(s, &nh, (size_t)n * V * W))) return rc;
+    // twin classes' next-hop rows 128-B aligned too (nh_derive_twin_kernel
+    // stores each 1,024-node tile's W words as one run)
+    const uint32_t NPW = k.twin ? row_pitch(V * W) : V * W;
+    if ((rc = upload(s, &d_roots, k.roots)) || (rc = dalloc(s, &nh, (size_t)n * NPW))) return rc;
     ospf_digest* dg = s->dig_all + slot;
     for (uint32_t j = 0; j < n; ++j)
-      own(s, k.roots[j], slot + j, dist + (size_t)pos[k.roots[j]] * V, nh + (size_t)j * V * W, W);
+      own(s, k.roots[j], slot + j, dist + (size_t)pos[k.roots[j]] * DP, nh + (size_t)j * NPW, W);
     slot += n;
     const int st = new_stream(s);
     if (st < 0) return st;
@@ -1155,12 +1174,12 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
         u.comp = (uint64_t)(a1 - a0) * 4ull * V * (W + (nh_dist ? 1u : 0u));
         const uint32_t *tc = d_tcls, *tr = d_trep, *ts = d_tsec, *rr = d_roots + a0;
         const uint32_t m = a1 - a0;
-        uint32_t* nhq = nh + (size_t)a0 * V * W;
+        uint32_t* nhq = nh + (size_t)a0 * NPW;
         ospf_digest* dq = dg + a0;
         uint32_t* dd = nh_dist ? dist : nullptr;
         u.fn = [=](hipStream_t strm) {
           return ospf_int::nh_derive_twin_launch(c, rr, m, W, cap, lev, pitch, d_pos, ldg, tc, tr, ts,
-                                                 nhq, dq, dd, strm);
+                                                 nhq, dq, dd, strm, DP, NPW);
         };
         s->step_comp += u.comp;
         side.push_back(std::move(u));
@@ -1231,7 +1250,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       uint32_t* dd = nh_dist ? dist : nullptr;
       u.fn = [=](hipStream_t strm) {
         return ospf_int::nh_derive_twin_launch(c, d_roots, n, W, cap, lev, pitch, d_pos, ldg, tc, tr,
-                                               ts, nh, dg, dd, strm);
+                                               ts, nh, dg, dd, strm, DP, NPW);
       };
     } else {
       u.fn = [=](hipStream_t strm) {
@@ -1249,7 +1268,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     for (uint32_t r : need_l) kmax = std::max(kmax, f.nbrs(r));
     for (uint32_t j = 0; j < nL; ++j)
       if (in_l[need_l[j]])
-        own(s, need_l[j], slot + j, dist + (size_t)pos[need_l[j]] * V, lnh + (size_t)j * V, 1);
+        own(s, need_l[j], slot + j, dist + (size_t)pos[need_l[j]] * DP, lnh + (size_t)j * DP, 1);
     ospf_digest* dg = s->dig_all + slot;
     const uint32_t ngr_r = nR ? (uint32_t)grp_r.size() - 1 : 0u;
     const uint32_t ngr = nL > nR ? (uint32_t)grp.size() - 1 : 0u;
@@ -1275,8 +1294,8 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       const uint32_t* lo = twin_lv ? d_lout : nullptr;
       uint32_t* dd = twin_lv ? nullptr : dist;
       u.fn = [=](hipStream_t strm) {
-        return ospf_leaf_derive2_dev(c, d_l, nR, d_grp_r, ngr_r, kmax, lev, pitch, d_pos, lo, dd,
-                                     lnh, dg, strm);
+        return ospf_int::leaf_derive(c, d_l, nR, d_grp_r, ngr_r, kmax, lev, pitch, d_pos, lo, dd, DP,
+                                     lnh, DP, dg, strm);
       };
       s->step_comp += u.comp;
       s->units.push_back(std::move(u));
@@ -1303,13 +1322,13 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
         u.W = 1;
         u.comp = (uint64_t)n * 8ull * V;
         const uint32_t* dl = d_l + nR + i0;
-        uint32_t* nh = lnh + (size_t)(nR + i0) * V;
+        uint32_t* nh = lnh + (size_t)(nR + i0) * DP;
         ospf_digest* dg2 = dg + nR + i0;
         const uint32_t* lo = drop_rest ? d_lout : nullptr;
         const uint32_t ngq = g1 - g0;
         u.fn = [=](hipStream_t strm) {
-          return ospf_leaf_derive2_dev(c, dl, n, d_gq, ngq, kmax, lev, pitch, d_pos, lo, dist, nh,
-                                       dg2, strm);
+          return ospf_int::leaf_derive(c, dl, n, d_gq, ngq, kmax, lev, pitch, d_pos, lo, dist, DP, nh,
+                                       DP, dg2, strm);
         };
         s->step_comp += u.comp;
         s->units.push_back(std::move(u));
@@ -1352,13 +1371,13 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
         u.W = 1;
         u.comp = (uint64_t)n * 8ull * V;
         const uint32_t* dl = d_l + nR + i0;
-        uint32_t* nh = lnh + (size_t)(nR + i0) * V;
+        uint32_t* nh = lnh + (size_t)(nR + i0) * DP;
         ospf_digest* dg2 = dg + nR + i0;
         const uint32_t* lo2 = lo ? lo + i0 : nullptr;
         const uint32_t* gp = part ? d_gq : d_grp;
         u.fn = [=](hipStream_t strm) {
-          return ospf_leaf_derive2_dev(c, dl, n, gp, ngq, kmax, lev, pitch, d_pos, lo2, dist, nh,
-                                       dg2, strm);
+          return ospf_int::leaf_derive(c, dl, n, gp, ngq, kmax, lev, pitch, d_pos, lo2, dist, DP, nh,
+                                       DP, dg2, strm);
         };
         s->step_comp += u.comp;
         s->units.push_back(std::move(u));
@@ -1382,11 +1401,11 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       u.W = 1;
       u.comp = (uint64_t)n * 8ull * V;
       const uint32_t* dl = d_l + nR;
-      uint32_t* nh = lnh + (size_t)nR * V;
+      uint32_t* nh = lnh + (size_t)nR * DP;
       ospf_digest* dg2 = dg + nR;
       const uint32_t* lo = drop_rest ? d_lout : nullptr;
       u.fn = [=](hipStream_t strm) {
-        return ospf_leaf_derive2_dev(c, dl, n, d_grp, ngr, kmax, lev, pitch, d_pos, lo, dist, nh,
+        return ospf_int::leaf_derive(c, dl, n, d_grp, ngr, kmax, lev, pitch, d_pos, lo, dist, DP, nh, DP,
                                      dg2, strm);
       };
       s->step_comp += u.comp;

@@ -318,10 +318,10 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
       }
     }
     __builtin_amdgcn_wave_barrier();
-    const size_t dst0 = ((size_t)i * V + tv0) * W;
+    const size_t dst0 = (size_t)i * (a.npitch ? a.npitch : (size_t)V * W) + (size_t)tv0 * W;
     const uint32_t tn = tv0 < V ? min(1024u, V - tv0) : 0u;
     if (a.dist && tn) {  // dist row = own level - 1 (0x7F: unreached), 1 KB per store
-      uint32_t* drow = a.dist + (size_t)own * V + tv0;
+      uint32_t* drow = a.dist + (size_t)own * (a.dpitch ? a.dpitch : V) + tv0;
 #pragma unroll
       for (int x = 0; x < 4; ++x) {
         const uint32_t Lw = s_Lb[wave][x * 64 + lane], n0 = (uint32_t)x * 256u + 4u * lane;
@@ -543,7 +543,7 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
           const uint32_t l = (L >> (8 * q)) & 0xFFu;
           dv[q] = l < 0x7Fu ? l - 1u : kInf;
         }
-        uint32_t* drow = a.dist + (size_t)own * V + v0;
+        uint32_t* drow = a.dist + (size_t)own * (a.dpitch ? a.dpitch : V) + v0;
         if (vec) {
           store_row16(drow, make_uint4(dv[0], dv[1], dv[2], dv[3]));
         } else {

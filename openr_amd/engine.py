@@ -295,7 +295,7 @@ class Engine:
     def sweep(self, **kw) -> "Sweep":
         return Sweep(self, **kw)
 
-    PROBES = {"stream": 0, "rows_chunk": 1, "rows_group": 2}
+    PROBES = {"stream": 0, "rows_chunk": 1, "rows_group": 2, "rows_walk": 3}
 
     def probe_store(self, pattern: str, V: int, rows: int, group: int = 48, ctiles: int = 6,
                     reps: int = 3) -> np.ndarray:

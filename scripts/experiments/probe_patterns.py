@@ -14,9 +14,12 @@ def run(p, g, ct):
          "GBs": round(2 * rows * V * 4 / ms / 1e6, 1)}
     print(json.dumps(r), flush=True)
     out.append(r)
+pats = sys.argv[1].split(",") if len(sys.argv) > 1 else ["rows_chunk", "rows_group"]
+groups = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 2, 4, 8, 16, 48, 64]
+cts = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [1, 2, 6, 20, 98]
 run("stream", 48, 6)
-for g in (1, 2, 4, 8, 16, 48, 64):
-    for ct in (1, 2, 6, 20, 98):
-        for p in ("rows_chunk", "rows_group"):
+for g in groups:
+    for ct in cts:
+        for p in pats:
             run(p, g, ct)
 run("stream", 48, 6)
