@@ -1535,8 +1535,10 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
     }
   }
   const size_t sz_didx = didx.size() * 2ull;
-  // node keys alone, padded to 16 nodes (derive: a lane's 16 nodes in 8 loads)
-  std::vector<uint64_t> dkn((V + 15) / 16 * 16, 0ull);
+  // node keys alone, zero padded past V: a lane's 16 nodes in 8 loads, and
+  // kernels that walk level rows to their pitch (V rounded up to 128 in the
+  // sweeps) read up to 128 keys past V
+  std::vector<uint64_t> dkn((V + 127) / 128 * 128 + 128, 0ull);
   for (uint32_t u = 0; u < V; ++u) dkn[u] = dkey[2ull * u + 1];
   const size_t sz_kn = dkn.size() * 8ull;
   size_t off[14], tot = 0;

@@ -391,6 +391,225 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
 }
 
 
+// The same derivation with lane = 4 nodes (wave = 256 nodes): a tile's
+// words staged per wave in 1 KB x W of LDS (12 KB a block at W = 3, against
+// 48 KB for 1,024-node wave tiles), 4 x W word registers instead of 16 x W,
+// so LDS and registers no longer cap the waves per SIMD; loads are one 4-B
+// piece of the own and each class row per lane (256 B per wave instruction),
+// stores W 1-KB runs of next-hop words and one 1-KB run of dist per chunk.
+template <int W, int PD>
+__global__ void __launch_bounds__(kBlock) nh_twin4_kernel(DevGraph g, TwinArgs a) {
+  __shared__ TwinTab T;
+  __shared__ unsigned long long s_h;
+  __shared__ uint64_t s_wk[1u << kComboC];
+  __shared__ uint32_t s_L[kWaves][64];           // own level bytes of each wave's chunk
+  __shared__ uint32_t s_st[kWaves][256 * W];     // [node][word] of each wave's chunk
+  const uint32_t V = g.V, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t NT = a.n * a.chunks, T8 = NT / 8u * 8u, b = blockIdx.x;
+  const uint32_t item = b < T8 ? (b % 8u) * (T8 / 8u) + b / 8u : b;
+  const uint32_t i = item / a.chunks, ci = item % a.chunks;
+  if (tid == 0) s_h = 0ull;
+  if (!twin_setup(g, a, i, W, T)) return;
+  const uint32_t K = min(T.K, (uint32_t)(32 * W)), own = T.own, nc = T.nc;
+  const bool ctab = a.digest && nc <= kComboC;
+  if (ctab && tid < (1u << nc)) {
+    uint64_t ws = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      uint32_t m = 0;
+      for (uint32_t j = 0; j < nc; ++j)
+        if ((tid >> j) & 1u) m |= T.cmask[j][w];
+      if (m) ws += digest_word_key(w, m);
+    }
+    s_wk[tid] = ws;
+  }
+  __syncthreads();
+  const uint32_t c_beg = ci * a.ctiles * 4u;
+  const uint32_t c_end = min((a.pitch + 255u) / 256u, (ci * a.ctiles + a.ctiles) * 4u);
+  uint32_t* st = s_st[wave];
+  const uint32_t dpitch = a.dpitch ? a.dpitch : V;
+  const size_t npitch = a.npitch ? a.npitch : (size_t)V * W;
+  const bool vec = (V & 3u) == 0 && (dpitch & 3u) == 0 && (npitch & 3u) == 0;
+  uint64_t h = 0;
+  constexpr uint32_t kPre = 3;
+  auto load_c = [&](uint32_t c, uint32_t& L, uint32_t* R) {
+    const uint32_t v0 = c * 256u + 4u * lane;
+    const uint32_t vs = (c < c_end && v0 < a.pitch) ? v0 : 0u;
+    L = *reinterpret_cast<const uint32_t*>(a.lev + (size_t)own * a.pitch + vs);
+#pragma unroll
+    for (uint32_t j = 0; j < kPre; ++j)
+      R[j] = j < nc ? *reinterpret_cast<const uint32_t*>(a.lev + (size_t)T.crow[j] * a.pitch + vs)
+                    : 0x7F7F7F7Fu;
+  };
+  // PD chunks of loads in flight per wave (a ring of prefetched rows)
+  uint32_t Ln[PD], Rn[PD][kPre];
+#pragma unroll
+  for (int d = 0; d < PD; ++d) load_c(c_beg + wave + d * kWaves, Ln[d], Rn[d]);
+  for (uint32_t c = c_beg + wave; c < c_end; c += kWaves) {
+    const uint32_t c0 = c * 256u, v0 = c0 + 4u * lane;
+    const bool live = v0 < a.pitch;
+    const uint32_t vs = live ? v0 : 0u;
+    const uint32_t L = Ln[0];
+    uint32_t Rp[kPre];
+#pragma unroll
+    for (uint32_t j = 0; j < kPre; ++j) Rp[j] = Rn[0][j];
+#pragma unroll
+    for (int d = 0; d + 1 < PD; ++d) {
+      Ln[d] = Ln[d + 1];
+#pragma unroll
+      for (uint32_t j = 0; j < kPre; ++j) Rn[d][j] = Rn[d + 1][j];
+    }
+    load_c(c + PD * kWaves, Ln[PD - 1], Rn[PD - 1]);
+    uint32_t lm1 = 0;
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      const uint32_t l = (L >> (8 * bb)) & 0xFFu;
+      lm1 |= (l >= 2u && l < 0x7Fu ? l - 1u : 0u) << (8 * bb);
+    }
+    lm1 |= 0x80808080u;
+    uint32_t word[W][4], cbp = 0u;  // cbp: tight-class bits, a byte per node
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) word[w][n] = 0u;
+    for (uint32_t j = 0; j < nc; ++j) {
+      uint32_t R = 0x7F7F7F7Fu;
+      if (j < kPre) {
+#pragma unroll
+        for (uint32_t q = 0; q < kPre; ++q)
+          if (q == j) R = Rp[q];
+      } else {
+        R = *reinterpret_cast<const uint32_t*>(a.lev + (size_t)T.crow[j] * a.pitch + vs);
+      }
+      const uint32_t z = live ? (lm1 - R) & 0x80808080u : 0u;
+      if (ctab) cbp |= ((z >> 7) & 0x01010101u) << j;
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb) {
+        const uint32_t sel = 0u - ((z >> (8 * bb + 7)) & 1u);
+#pragma unroll
+        for (int w = 0; w < W; ++w) word[w][bb] |= sel & T.cmask[j][w];
+      }
+    }
+    // stage [node][word]: the lane's 4 nodes are 4 W consecutive words
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+      uint32_t v4[4];
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) {
+        const int f = 4 * x + cc;
+        v4[cc] = word[f % W][f / W];
+      }
+      reinterpret_cast<uint4*>(st + 4u * W * lane)[x] = make_uint4(v4[0], v4[1], v4[2], v4[3]);
+    }
+    s_L[wave][lane] = L;
+    // digest terms of the unpatched words (the patches below add their deltas)
+    if (a.digest && live) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint64_t ws = 0;
+        if (ctab) {
+          ws = s_wk[(cbp >> (8 * q)) & 0xFFu];
+        } else {
+#pragma unroll
+          for (int w = 0; w < W; ++w)
+            if (word[w][q]) ws += digest_word_key(w, word[w][q]);
+        }
+        h += g.dkn[v0 + q] * ws;  // zero past V
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // members' own positions in this chunk, a lane per neighbour
+    {
+      uint32_t lo = 0, hi = K;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (T.nb[mid] < c0) lo = mid + 1; else hi = mid;
+      }
+      uint32_t end = lo;
+      hi = K;
+      while (end < hi) {
+        const uint32_t mid = (end + hi) >> 1;
+        if (T.nb[mid] < c0 + 256u) end = mid + 1; else hi = mid;
+      }
+      for (uint32_t k = lo + lane; k < end; k += 64u) {
+        const uint32_t sk = T.cid[k];
+        if (sk == kInf) continue;
+        const uint32_t n = T.nb[k], o = n - c0;
+        const uint32_t Lo = (s_L[wave][o >> 2] >> (8u * (o & 3u))) & 0xFFu;
+        uint32_t nw[W], ow[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) nw[w] = ow[w] = st[o * W + w];
+        if (sk != 0x100u && n == T.crep[sk]) {  // re-test the class against X
+          const bool tight = Lo >= 2u && Lo < 0x7Fu && T.cx[sk] + 1u == Lo;
+#pragma unroll
+          for (int w = 0; w < W; ++w) nw[w] = (nw[w] & ~T.cmask[sk][w]) | (tight ? T.cmask[sk][w] : 0u);
+        }
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+          if ((uint32_t)w == (k >> 5)) {
+            const uint32_t bit = 1u << (k & 31u);
+            nw[w] = (nw[w] & ~bit) | (Lo == 2u ? bit : 0u);
+          }
+#pragma unroll
+        for (int w = 0; w < W; ++w) st[o * W + w] = nw[w];
+        if (a.digest && n < V) {
+          uint64_t d = 0;
+#pragma unroll
+          for (int w = 0; w < W; ++w)
+            d += (nw[w] ? digest_word_key(w, nw[w]) : 0ull) - (ow[w] ? digest_word_key(w, ow[w]) : 0ull);
+          h += g.dkn[n] * d;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t tn = c0 < V ? min(256u, V - c0) : 0u;
+    if (a.dist && tn) {  // dist row = own level - 1 (0x7F: unreached)
+      uint32_t dv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t l = (L >> (8 * q)) & 0xFFu;
+        dv[q] = l < 0x7Fu ? l - 1u : kInf;
+      }
+      uint32_t* drow = a.dist + (size_t)own * dpitch + c0;
+      const uint32_t n0 = 4u * lane;
+      if (vec && n0 + 4u <= tn) {
+        store_row16(drow + n0, make_uint4(dv[0], dv[1], dv[2], dv[3]));
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (n0 + q < tn) drow[n0 + q] = dv[q];
+      }
+    }
+    const size_t dst0 = (size_t)i * npitch + (size_t)c0 * W;
+    if (tn == 256u && vec) {
+#pragma unroll
+      for (int x = 0; x < W; ++x)
+        store_row16(reinterpret_cast<uint4*>(a.nh + dst0) + x * 64 + lane,
+                    reinterpret_cast<const uint4*>(st)[x * 64 + lane]);
+    } else {
+      for (uint32_t x = lane; x < tn * W; x += 64u) a.nh[dst0 + x] = st[x];
+    }
+    __builtin_amdgcn_wave_barrier();  // the slice is rewritten by the next chunk
+  }
+  if (a.digest) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) h += shfl_xor64(h, o);
+    if (lane == 0 && h) atomicAdd(&s_h, (unsigned long long)h);
+    __syncthreads();
+    if (tid == 0) {
+      ospf_digest* dg = a.digest + i;
+      unsigned long long hh = s_h;
+      if (ci == 0) {
+        const ospf_digest ld = a.lev_digest[own];
+        atomicAdd((unsigned long long*)&dg->reached, (unsigned long long)ld.reached);
+        atomicAdd((unsigned long long*)&dg->sum_dist, (unsigned long long)ld.sum_dist);
+        hh += ld.hash;
+      }
+      if (hh) atomicAdd((unsigned long long*)&dg->hash, hh);
+    }
+  }
+}
+
 // byte-wise min of 7-bit bytes: bit 7 of (a | 0x80) - b is set iff a >= b
 __device__ __forceinline__ uint32_t bmin7(uint32_t a, uint32_t b) {
   const uint32_t ge = ((a | 0x80808080u) - b) & 0x80808080u;
@@ -601,6 +820,24 @@ hipError_t launch_nh_derive_twin(const DevGraph& g, const TwinArgs& a0, hipStrea
   a.ctiles = std::max(1u, std::min(a.tiles, a.ctiles));
   a.chunks = (a.tiles + a.ctiles - 1) / a.ctiles;
   const dim3 grid(a.n * a.chunks);
+  // lane = 4 nodes (nh_twin4_kernel) unless OSPF_TWIN_NH16=1 (lane = 16 nodes)
+  const bool nh16 = getenv("OSPF_TWIN_NH16") != nullptr;  // read per launch: in-process A/B
+  if (!nh16) {
+    // prefetch depth (chunks of loads in flight per wave): OSPF_TWIN4_PD 1 / 2
+    const char* pe = getenv("OSPF_TWIN4_PD");
+    const bool pd2 = !pe || atoi(pe) >= 2;
+#define OSPF_TWIN4(WW)                                                                        \
+  if (pd2) hipLaunchKernelGGL((nh_twin4_kernel<WW, 2>), grid, dim3(kBlock), 0, s, g, a);     \
+  else hipLaunchKernelGGL((nh_twin4_kernel<WW, 1>), grid, dim3(kBlock), 0, s, g, a);
+    switch (a.W) {
+      case 1: OSPF_TWIN4(1) break;
+      case 2: OSPF_TWIN4(2) break;
+      case 3: OSPF_TWIN4(3) break;
+      default: OSPF_TWIN4(4) break;
+    }
+#undef OSPF_TWIN4
+    return hipGetLastError();
+  }
   const size_t lds = (size_t)kWaves * 1024u * a.W * 4u;
   switch (a.W) {
     case 1: hipLaunchKernelGGL(nh_derive_twin_kernel<1>, grid, dim3(kBlock), lds, s, g, a); break;

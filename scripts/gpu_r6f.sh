@@ -6,7 +6,7 @@ timeout -k 10 700 python -u -m pytest -x -q --timeout 300 --timeout-method threa
   tests/test_gpu_sweep.py tests/test_gpu_derive.py tests/test_gpu_multi.py > $OUT/tests.log 2>&1 \
   || { tail -n 40 $OUT/tests.log; exit 1; }
 tail -n 2 $OUT/tests.log
-timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 --ab "OSPF_SWEEP_ROW_PITCH=V" \
+timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 --ab "${AB:-OSPF_SWEEP_ROW_PITCH=V}" \
   > $OUT/bench.json 2> $OUT/bench.err || { tail -n 30 $OUT/bench.err; exit 1; }
 python - <<PY
 import json
