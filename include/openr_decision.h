@@ -5,7 +5,8 @@
  *
  * The C++ class (openr_amd/csrc/decision/link_state.h, namespace odl) keeps
  * the reference's public surface and semantics:
- *   updateAdjacencyDatabase  LinkState.cpp:584-726 -> odl_apply
+ *   updateAdjacencyDatabase  LinkState.cpp:584-726 -> odl_apply (odl_apply_hold: TTLs)
+ *   decrementHolds, hasHolds LinkState.cpp:520-548 -> odl_decrement_holds, odl_has_holds
  *   deleteAdjacencyDatabase  LinkState.cpp:728-746 -> odl_apply (db_delete=1)
  *   linksFromNode            LinkState.cpp:477-485 -> odl_links_text
  *   isNodeOverloaded         LinkState.cpp:515-518 -> odl_is_overloaded
@@ -48,6 +49,19 @@ void odl_free(char* p);
 /* Apply stream records [first, first+count) in order; changes[count] out. */
 int odl_apply(odl_ls* ls, const oadj_stream* s, uint32_t first, uint32_t count,
               oadj_change* changes);
+/* Same with updateAdjacencyDatabase's hold TTLs (LinkState.cpp:585-700,
+ * HoldableValue LinkState.cpp:48-117): a new link stays down for hold_up_ttl
+ * odl_decrement_holds calls; a metric / overload change is held back
+ * hold_up_ttl calls when it brings the link up (metric decrease, overload
+ * cleared), hold_down_ttl otherwise. Decision itself passes 0
+ * (Decision.cpp:756), which is odl_apply. */
+int odl_apply_hold(odl_ls* ls, const oadj_stream* s, uint32_t first, uint32_t count,
+                   oadj_change* changes, uint64_t hold_up_ttl, uint64_t hold_down_ttl);
+/* LinkState::decrementHolds (LinkState.cpp:520-535): 1 when a hold expired
+ * (topology changed, memoised results dropped), 0 when none did, < 0 error.
+ * odl_has_holds (:537-548): 1 while any hold is on. */
+int odl_decrement_holds(odl_ls* ls);
+int odl_has_holds(const odl_ls* ls);
 
 char* odl_spf_text(odl_ls* ls, const char* root, int use_link_metric);
 char* odl_kth_paths_text(odl_ls* ls, const char* src, const char* dst, int k);

@@ -46,7 +46,7 @@ ENGINE_SYMBOLS = [
 ]
 DECISION_SYMBOLS = [
     "odl_create", "odl_create_multi", "odl_all_sources_prefetch", "odl_all_sources_digests",
-    "odl_sweep_stats", "odl_destroy", "odl_last_error", "odl_free", "odl_apply", "odl_spf_text",
+    "odl_sweep_stats", "odl_destroy", "odl_last_error", "odl_free", "odl_apply", "odl_apply_hold", "odl_decrement_holds", "odl_has_holds", "odl_spf_text",
     "odl_kth_paths_text", "odl_links_text", "odl_link_keys_text", "odl_metric_a_to_b", "odl_is_overloaded",
     "odl_spf_runs", "odl_set_incremental", "odl_set_host_spf", "odl_incremental_stats", "odl_topology_stats", "odl_num_nodes", "odl_num_links", "odl_spf_digests", "odl_spf_prefetch",
     "odl_ksp2_text", "odl_route_text", "odl_route_db_text", "odl_route_db_bin", "odl_free_buf", "odl_path_a_in_b", "odl_ucmp_text", "odl_csr_size", "odl_csr_export", "odl_node_name", "odl_node_id",
@@ -247,6 +247,9 @@ def decision() -> C.CDLL:
         L.odl_last_error.restype = cp
         L.odl_free.argtypes = [vp]
         L.odl_apply.argtypes = [vp, vp, u32, u32, vp]
+        L.odl_apply_hold.argtypes = [vp, vp, u32, u32, vp, u64, u64]
+        L.odl_decrement_holds.argtypes = [vp]
+        L.odl_has_holds.argtypes = [vp]
         for f in ("odl_spf_text", "odl_kth_paths_text", "odl_links_text", "odl_ksp2_text",
                   "odl_route_text", "odl_route_db_text", "odl_ucmp_text",
                   "odl_link_keys_text"):

@@ -128,6 +128,11 @@ void odl_free(char* p) { std::free(p); }
 
 int odl_apply(odl_ls* h, const oadj_stream* s, uint32_t first, uint32_t count,
               oadj_change* changes) {
+  return odl_apply_hold(h, s, first, count, changes, 0, 0);
+}
+
+int odl_apply_hold(odl_ls* h, const oadj_stream* s, uint32_t first, uint32_t count,
+                   oadj_change* changes, uint64_t hold_up_ttl, uint64_t hold_down_ttl) {
   return guard(h, [&]() -> int {
     if (!s) throw std::invalid_argument("null stream");
     bool deletes = false;
@@ -162,7 +167,7 @@ int odl_apply(odl_ls* h, const oadj_stream* s, uint32_t first, uint32_t count,
       if (getenv("ODL_SPF_TIMING"))
         std::fprintf(stderr, "ODL_INGEST build_dbs_ms=%.1f\n",
                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
-      const auto chs = h->ls.updateAdjacencyDatabases(dbs);
+      const auto chs = h->ls.updateAdjacencyDatabases(dbs, hold_up_ttl, hold_down_ttl);
       for (uint32_t k = 0; changes && k < count; ++k)
         changes[k] = changeRecord(chs[k]);
       return 0;
@@ -190,7 +195,7 @@ int odl_apply(odl_ls* h, const oadj_stream* s, uint32_t first, uint32_t count,
           x.weight = s->adj_weight[a];
           db.adjacencies.push_back(std::move(x));
         }
-        ch = h->ls.updateAdjacencyDatabase(db);
+        ch = h->ls.updateAdjacencyDatabase(db, hold_up_ttl, hold_down_ttl);
       }
       if (changes)
         changes[k] = changeRecord(ch);
@@ -236,6 +241,11 @@ int64_t odl_metric_a_to_b(odl_ls* h, const char* a, const char* b, int use_link_
     return m ? (int64_t)*m : -1;
   }, (int64_t)-2);
 }
+
+int odl_decrement_holds(odl_ls* h) {
+  return guard(h, [&]() -> int { return h->ls.decrementHolds().topologyChanged ? 1 : 0; }, -1);
+}
+int odl_has_holds(const odl_ls* h) { return h ? (h->ls.hasHolds() ? 1 : 0) : -1; }
 
 int odl_is_overloaded(odl_ls* h, const char* node) {
   return h ? (h->ls.isNodeOverloaded(node) ? 1 : 0) : -1;

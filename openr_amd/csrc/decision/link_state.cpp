@@ -124,7 +124,7 @@ Link::Link(const std::string& n1, const Adjacency& a1, const std::string& n2, co
     end_[i].node = *nn[i];
     end_[i].iface = adj[i]->ifName;
     end_[i].metric = (Metric)(int64_t)adj[i]->metric;  // i32 -> u64 as the reference
-    end_[i].overload = adj[i]->isOverloaded;
+    end_[i].overload = (bool)adj[i]->isOverloaded;
     end_[i].adjLabel = adj[i]->adjLabel;
     end_[i].weight = adj[i]->weight;
   }
@@ -144,21 +144,31 @@ const std::string& Link::otherNode(const std::string& n) const {
   throw std::invalid_argument(n);
 }
 const std::string& Link::ifaceFrom(const std::string& n) const { return endOf(n).iface; }
-Metric Link::metricFrom(const std::string& n) const { return endOf(n).metric; }
-bool Link::overloadFrom(const std::string& n) const { return endOf(n).overload; }
+Metric Link::metricFrom(const std::string& n) const { return endOf(n).metric.value(); }
+bool Link::overloadFrom(const std::string& n) const { return endOf(n).overload.value(); }
 int32_t Link::adjLabelFrom(const std::string& n) const { return endOf(n).adjLabel; }
 int64_t Link::weightFrom(const std::string& n) const { return endOf(n).weight; }
 
-bool Link::setMetricFrom(const std::string& n, Metric m) {
-  End& e = endOf(n);
-  if (e.metric == m) return false;
-  e.metric = m;
-  return true;
+bool Link::setMetricFrom(const std::string& n, Metric m, Metric holdUpTtl, Metric holdDownTtl) {
+  return endOf(n).metric.updateValue(m, holdUpTtl, holdDownTtl);
 }
-bool Link::setOverloadFrom(const std::string& n, bool ov) {
+bool Link::setOverloadFrom(const std::string& n, bool ov, Metric holdUpTtl, Metric holdDownTtl) {
   const bool wasUp = isUp();
-  endOf(n).overload = ov;
+  endOf(n).overload.updateValue(ov, holdUpTtl, holdDownTtl);
   return wasUp != isUp();
+}
+bool Link::decrementHolds() {
+  bool expired = false;
+  if (holdUpTtl_ != 0) expired |= --holdUpTtl_ == 0;
+  for (End& e : end_) {
+    expired |= e.metric.decrementTtl();
+    expired |= e.overload.decrementTtl();
+  }
+  return expired;
+}
+bool Link::hasHolds() const {
+  return holdUpTtl_ != 0 || end_[0].metric.hasHold() || end_[1].metric.hasHold() ||
+         end_[0].overload.hasHold() || end_[1].overload.hasHold();
 }
 void Link::setAdjLabelFrom(const std::string& n, int32_t l) { endOf(n).adjLabel = l; }
 void Link::setWeightFrom(const std::string& n, int64_t w) { endOf(n).weight = w; }
@@ -207,7 +217,28 @@ const LinkSet& LinkState::linksFromNode(const std::string& node) const {
 
 bool LinkState::isNodeOverloaded(const std::string& node) const {
   auto it = nodeOverloads_.find(node);
-  return it != nodeOverloads_.end() && it->second;
+  return it != nodeOverloads_.end() && it->second.value();
+}
+
+LinkStateChange LinkState::decrementHolds() {
+  LinkStateChange ch;
+  for (auto& shard : allLinks_)
+    for (const auto& l : shard) ch.topologyChanged |= l->decrementHolds();
+  for (auto& kv : nodeOverloads_) ch.topologyChanged |= kv.second.decrementTtl();
+  // an expired hold changes what the snapshot holds (metrics, up state, node
+  // overload): the memo is dropped (LinkState.cpp:530-533) and the CSR taken
+  // again
+  if (ch.topologyChanged) invalidate();
+  return ch;
+}
+
+bool LinkState::hasHolds() const {
+  for (const auto& shard : allLinks_)
+    for (const auto& l : shard)
+      if (l->hasHolds()) return true;
+  for (const auto& kv : nodeOverloads_)
+    if (kv.second.hasHold()) return true;
+  return false;
 }
 
 LinkPtr LinkState::makeLink(const std::string& node, const Adjacency& adj) const {
@@ -269,7 +300,8 @@ void LinkState::invalidate() {
   clearMemo();
 }
 
-LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db) {
+LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db, Metric holdUpTtl,
+                                                   Metric holdDownTtl) {
   LinkStateChange ch;
   const std::string me = db.thisNodeName;
   const bool known = adjDbs_.count(me) > 0;
@@ -297,10 +329,10 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db) 
   auto ov = nodeOverloads_.find(me);
   if (ov == nodeOverloads_.end()) {
     nodeOverloads_.emplace(me, db.isOverloaded);  // a new node is not a change
-  } else if (ov->second != db.isOverloaded) {
-    ov->second = db.isOverloaded;
-    ch.topologyChanged = true;
-    nodeDeltas.push_back(me);
+  } else {
+    const bool was = ov->second.value();
+    ch.topologyChanged |= ov->second.updateValue(db.isOverloaded, holdUpTtl, holdDownTtl);
+    if (ov->second.value() != was) nodeDeltas.push_back(me);
   }
   ch.nodeLabelChanged = priorLabel != db.nodeLabel;
 
@@ -312,6 +344,7 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db) 
                          (i == after.size() || before[j]->orderedBefore(*after[i]));
     if (takeNew) {
       structural = true;
+      after[i]->setHoldUpTtl(holdUpTtl);
       ch.topologyChanged |= after[i]->isUp();
       addLink(after[i]);
       ch.addedLinks.push_back(after[i]);
@@ -330,9 +363,10 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db) 
         deltas.push_back(LinkDelta{before[j], kept.isUp(), kept.metricFrom(kept.lowNode()),
                                    kept.metricFrom(kept.highNode())});
       if (fresh.metricFrom(me) != kept.metricFrom(me))
-        ch.topologyChanged |= kept.setMetricFrom(me, fresh.metricFrom(me));
+        ch.topologyChanged |= kept.setMetricFrom(me, fresh.metricFrom(me), holdUpTtl, holdDownTtl);
       if (fresh.overloadFrom(me) != kept.overloadFrom(me))
-        ch.topologyChanged |= kept.setOverloadFrom(me, fresh.overloadFrom(me));
+        ch.topologyChanged |=
+            kept.setOverloadFrom(me, fresh.overloadFrom(me), holdUpTtl, holdDownTtl);
       if (fresh.adjLabelFrom(me) != kept.adjLabelFrom(me)) {
         kept.setAdjLabelFrom(me, fresh.adjLabelFrom(me));
         ch.linkAttributesChanged = true;
@@ -427,11 +461,14 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db) 
 // indexes are only read), then every node's LinkSet filled in parallel with
 // its links in the sequential insertion order (creation order), so each
 // unordered_set ends up with the same buckets and iteration order.
-std::vector<LinkStateChange> LinkState::updateAdjacencyDatabases(std::vector<AdjacencyDatabase>& dbs) {
+std::vector<LinkStateChange> LinkState::updateAdjacencyDatabases(std::vector<AdjacencyDatabase>& dbs,
+                                                                Metric holdUpTtl,
+                                                                Metric holdDownTtl) {
   const auto tIn = std::chrono::steady_clock::now();
   const uint32_t n = (uint32_t)dbs.size();
   std::vector<LinkStateChange> out(n);
-  bool bulk = n >= 64 && !getenv("ODL_NO_BULK_INGEST");
+  // (the bulk path makes links without holds)
+  bool bulk = n >= 64 && holdUpTtl == 0 && !getenv("ODL_NO_BULK_INGEST");
   std::unordered_map<std::string, uint32_t> posOf;
   if (bulk) {
     posOf.reserve(n);
@@ -439,7 +476,7 @@ std::vector<LinkStateChange> LinkState::updateAdjacencyDatabases(std::vector<Adj
       bulk = !adjDbs_.count(dbs[i].thisNodeName) && posOf.emplace(dbs[i].thisNodeName, i).second;
   }
   if (!bulk) {
-    for (uint32_t i = 0; i < n; ++i) out[i] = updateAdjacencyDatabase(dbs[i]);
+    for (uint32_t i = 0; i < n; ++i) out[i] = updateAdjacencyDatabase(dbs[i], holdUpTtl, holdDownTtl);
     return out;
   }
   using Clock = std::chrono::steady_clock;

@@ -28,6 +28,7 @@
 #include <optional>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <string_view>
 #include <unordered_map>
 #include <unordered_set>
@@ -90,6 +91,54 @@ struct AdjacencyDatabase {
   std::vector<Adjacency> adjacencies;
 };
 
+// A value whose change can be held back for a number of decrementHolds()
+// calls (HoldableValue, LinkState.h:26-62 / LinkState.cpp:48-117): ordered
+// FIB programming. A change "bringing up" (overload true -> false, a metric
+// decrease) is held holdUpTtl calls, any other holdDownTtl; value() is the
+// held value meanwhile. A second change while a hold is on drops the hold.
+template <class T>
+class HoldableValue {
+ public:
+  explicit HoldableValue(T v) : val_(v) {}
+  void operator=(T v) {
+    val_ = v;
+    held_.reset();
+    ttl_ = 0;
+  }
+  const T& value() const { return held_ ? *held_ : val_; }
+  bool hasHold() const { return held_.has_value(); }
+  // true when a hold expired (the value changed)
+  bool decrementTtl() {
+    if (held_ && --ttl_ == 0) {
+      held_.reset();
+      return true;
+    }
+    return false;
+  }
+  // true when the change is effective now (no hold taken)
+  bool updateValue(T v, Metric holdUpTtl, Metric holdDownTtl) {
+    if (v == val_) return false;
+    if (hasHold()) {  // a change on top of a hold: the fast update
+      held_.reset();
+      ttl_ = 0;
+    } else {
+      ttl_ = bringsUp(v) ? holdUpTtl : holdDownTtl;
+      if (ttl_ != 0) held_ = val_;
+    }
+    val_ = v;
+    return !hasHold();
+  }
+
+ private:
+  bool bringsUp(T v) const {
+    if constexpr (std::is_same_v<T, bool>) return val_ && !v;  // overload cleared
+    else return v < val_;                                       // metric decreased
+  }
+  T val_;
+  std::optional<T> held_;
+  Metric ttl_ = 0;
+};
+
 // One undirected link (LinkState.h:80-182).
 class Link {
  public:
@@ -101,11 +150,20 @@ class Link {
   bool overloadFrom(const std::string& n) const;
   int32_t adjLabelFrom(const std::string& n) const;
   int64_t weightFrom(const std::string& n) const;
-  bool isUp() const { return !end_[0].overload && !end_[1].overload; }
+  bool isUp() const {
+    return holdUpTtl_ == 0 && !end_[0].overload.value() && !end_[1].overload.value();
+  }
 
   // attribute updates from node n; return value per LinkState.cpp:284-330
-  bool setMetricFrom(const std::string& n, Metric m);
-  bool setOverloadFrom(const std::string& n, bool ov);  // true iff isUp() flipped
+  // (hold TTLs: LinkState.cpp:313-360)
+  bool setMetricFrom(const std::string& n, Metric m, Metric holdUpTtl = 0, Metric holdDownTtl = 0);
+  // true iff isUp() flipped
+  bool setOverloadFrom(const std::string& n, bool ov, Metric holdUpTtl = 0, Metric holdDownTtl = 0);
+  // a new link is held down for holdUpTtl decrementHolds() calls
+  // (LinkState.cpp:237-263)
+  void setHoldUpTtl(Metric ttl) { holdUpTtl_ = ttl; }
+  bool decrementHolds();  // true when a hold expired
+  bool hasHolds() const;
   void setAdjLabelFrom(const std::string& n, int32_t l);
   void setWeightFrom(const std::string& n, int64_t w);
 
@@ -121,19 +179,20 @@ class Link {
   mutable uint32_t snapLid = 0xFFFFFFFFu;
   mutable uint32_t snapEnd[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};  // snapshot node ids of the ends
   int endIndex(const std::string& n) const { return end_[0].node == n ? 0 : 1; }
-  Metric metricOfEnd(int i) const { return end_[i].metric; }
+  Metric metricOfEnd(int i) const { return end_[i].metric.value(); }
 
  private:
   struct End {
     std::string node, iface;
-    Metric metric = 1;
-    bool overload = false;
+    HoldableValue<Metric> metric{1};
+    HoldableValue<bool> overload{false};
     int32_t adjLabel = 0;
     int64_t weight = 0;
   };
   End& endOf(const std::string& n);
   const End& endOf(const std::string& n) const;
   End end_[2];
+  Metric holdUpTtl_ = 0;
   uint8_t lo_ = 0;  // end_[lo_] is the lower (node, iface) pair, end_[lo_ ^ 1] the higher
   static size_t hashOf(const End& lo, const End& hi);
 };
@@ -359,14 +418,23 @@ class LinkState {
   LinkState& operator=(const LinkState&) = delete;
 
   const std::string& area() const { return area_; }
-  LinkStateChange updateAdjacencyDatabase(const AdjacencyDatabase& db);
+  // holdUpTtl / holdDownTtl: LinkState::updateAdjacencyDatabase's hold TTLs
+  // (LinkState.cpp:585-700; Decision passes 0, Decision.cpp:756)
+  LinkStateChange updateAdjacencyDatabase(const AdjacencyDatabase& db, Metric holdUpTtl = 0,
+                                          Metric holdDownTtl = 0);
+  // one step of every hold (LinkState.cpp:520-548): topologyChanged when one
+  // expired (the memo is dropped then); hasHolds: any hold left
+  LinkStateChange decrementHolds();
+  bool hasHolds() const;
   LinkStateChange deleteAdjacencyDatabase(const std::string& node);
   // A batch of databases in order (Decision's debounced batch,
   // Decision.cpp:731-765; the initial sync delivers the whole area): the same
   // state and change records as updateAdjacencyDatabase on each in turn. A
   // batch of nodes not yet known (no name twice) is built with host threads.
   // The databases are moved from.
-  std::vector<LinkStateChange> updateAdjacencyDatabases(std::vector<AdjacencyDatabase>& dbs);
+  std::vector<LinkStateChange> updateAdjacencyDatabases(std::vector<AdjacencyDatabase>& dbs,
+                                                        Metric holdUpTtl = 0,
+                                                        Metric holdDownTtl = 0);
   // Decision::processPublication's LinkState part (Decision.cpp:846-870):
   // every key-value in order -- an "adj:" key with a value decoded from
   // compact thrift (on host threads) and applied (updateKeyInLsdb,
@@ -651,7 +719,7 @@ class LinkState {
   static constexpr uint32_t kLinkShards = 16;
   std::array<LinkSet, kLinkShards> allLinks_;
   LinkSet& shardOf(const Link& l) { return allLinks_[(l.hash >> 7) % kLinkShards]; }
-  std::unordered_map<std::string, bool> nodeOverloads_;
+  std::unordered_map<std::string, HoldableValue<bool>> nodeOverloads_;
   std::unordered_map<std::string, AdjacencyDatabase> adjDbs_;
   // per node: (otherNodeName, ifName, otherIfName) -> adjacency position; the
   // views point into adjDbs_[node]'s own strings and are rebuilt with it

@@ -222,13 +222,36 @@ class LinkState:
         return s
 
     # ------------------------------------------------------------ ingest
-    def apply(self, stream: AdjDbStream, first: int = 0, count: Optional[int] = None):
+    def apply(self, stream: AdjDbStream, first: int = 0, count: Optional[int] = None,
+              hold_up_ttl: int = 0, hold_down_ttl: int = 0):
+        """updateAdjacencyDatabase per record (LinkState.cpp:584-726), with its
+        hold TTLs (0: Decision's own call, Decision.cpp:756)."""
         count = stream.n_dbs - first if count is None else count
         ch = change_array(count)
-        if self._L.odl_apply(self._h, C.addressof(stream.struct), first, count,
-                             C.addressof(ch)) != 0:
+        if hold_up_ttl or hold_down_ttl:
+            rc = self._L.odl_apply_hold(self._h, C.addressof(stream.struct), first, count,
+                                        C.addressof(ch), hold_up_ttl, hold_down_ttl)
+        else:
+            rc = self._L.odl_apply(self._h, C.addressof(stream.struct), first, count,
+                                   C.addressof(ch))
+        if rc != 0:
             raise LinkStateError(self._err())
         return changes_to_list(ch, count)
+
+    def decrement_holds(self) -> bool:
+        """LinkState::decrementHolds (LinkState.cpp:520-535): True when a hold
+        expired (topology changed)."""
+        rc = self._L.odl_decrement_holds(self._h)
+        if rc < 0:
+            raise LinkStateError(self._err())
+        return bool(rc)
+
+    decrementHolds = decrement_holds
+
+    def has_holds(self) -> bool:
+        return self._L.odl_has_holds(self._h) == 1
+
+    hasHolds = has_holds
 
     updateAdjacencyDatabases = apply
 
