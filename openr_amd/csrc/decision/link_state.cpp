@@ -203,6 +203,7 @@ LinkState::LinkState(std::string area, std::vector<int> devices)
 }
 
 LinkState::~LinkState() {
+  joinOpen();
   reaper_.reset();  // drains the dropped memos, joins the thread
   dropSweep();
   if (multi_) ospf_multi_close(multi_);
@@ -585,6 +586,7 @@ std::vector<LinkStateChange> LinkState::updateAdjacencyDatabases(std::vector<Adj
   // one version step per database, as in turn (a new node is structural)
   version_ += n - (anyTopo ? 1u : 0u);
   if (anyTopo) invalidate();
+  startOpen();
   return out;
 }
 
@@ -648,9 +650,11 @@ const LinkState::Csr& LinkState::snapshot() {
   Csr c;
   c.names.reserve(adjDbs_.size());
   for (const auto& kv : adjDbs_) c.names.push_back(kv.first);
-  std::sort(c.names.begin(), c.names.end());
+  parallelSort(c.names);
+  lap("names sorted");
   c.ids.reserve(c.names.size() * 2);
   for (uint32_t i = 0; i < c.names.size(); ++i) c.ids.emplace(c.names[i], i);
+  lap("names");
   const uint32_t V = (uint32_t)c.names.size();
   c.rowPtr.assign(V + 1, 0);
   c.noTransit.assign(V, 0);
@@ -675,7 +679,7 @@ const LinkState::Csr& LinkState::snapshot() {
         Ent e;
         e.end = (uint8_t)l->endIndex(un);
         l->snapEnd[e.end] = u;
-        if (e.end == 0 && l->otherNode(un) == un) l->snapEnd[1] = u;  // a self-loop
+        if (e.end == 0 && l->selfLoop()) l->snapEnd[1] = u;
         const Metric m = l->metricOfEnd(e.end);
         e.v = kInf;  // the other end's id: written by its own row
         e.rank = rank++;
@@ -688,7 +692,7 @@ const LinkState::Csr& LinkState::snapshot() {
         rowMax[u] = std::max<uint64_t>(rowMax[u], inRange ? m : 0);
         e.up = l->isUp() ? 1 : 0;
         // the lower end by name = by id sees the link first in id order
-        e.low = (l->lowNode() == un) ? 1 : 0;
+        e.low = (e.end == l->lowIndex() || l->selfLoop()) ? 1 : 0;
         e.link = &l;
         nf += e.low;
         row.push_back(e);
@@ -863,8 +867,59 @@ void LinkState::prefetchKsp2(const std::string& src, const std::vector<std::stri
   guarded([&] { prefetchKsp2Impl(src, dsts); });
 }
 
+void LinkState::startOpen() {
+  if (hostOnly_ || engine_ || opener_.joinable() || devices_.size() != 1 ||
+      getenv("ODL_NO_PREOPEN"))
+    return;
+  try {
+    opener_ = std::thread([this, dev = device_] {
+      ospf_ctx* c = nullptr;
+      if (ospf_open(dev, &c) != OSPF_OK) return;
+      // one link, one root: the batch path's kernels loaded and run once
+      const uint32_t rp[3] = {0, 1, 2}, col[2] = {1, 0}, one[2] = {1, 1}, lid[2] = {0, 0},
+                     twin[2] = {1, 0};
+      const uint8_t up[2] = {1, 1};
+      ospf_csr g{};
+      g.n_nodes = 2;
+      g.n_edges = 2;
+      g.row_ptr = rp;
+      g.col = col;
+      g.metric = one;
+      g.link_id = lid;
+      g.twin = twin;
+      g.edge_up = up;
+      uint32_t root = 0, dist[2], nh[2];
+      if (ospf_load_graph(c, &g, 0) != OSPF_OK ||
+          ospf_sssp_batch(c, &root, 1, nullptr, OSPF_WANT_DIST | OSPF_WANT_NH, 1, dist, nh,
+                          nullptr) != OSPF_OK) {
+        ospf_close(c);
+        return;
+      }
+      openerCtx_ = c;
+    });
+  } catch (const std::system_error&) {  // no thread: the engine opens on first use
+  }
+}
+
+void LinkState::joinOpen() {
+  if (!opener_.joinable()) return;
+  opener_.join();
+  if (!openerCtx_) return;  // failed: ensureEngine opens (and reports) as before
+  if (engine_ || hostOnly_) {
+    ospf_close(openerCtx_);
+  } else {
+    engine_ = openerCtx_;
+    engineOpened_ = true;
+    engineVersion_ = 0;  // the warm-up graph: the snapshot loads on first use
+  }
+  openerCtx_ = nullptr;
+}
+
 void LinkState::ensureEngine() {
   snapshot();
+  joinOpen();
+  const auto t0 = std::chrono::steady_clock::now();
+  const bool opening = !engine_, loading = engineVersion_ != snapVersion_;
   if (!engine_) {
     int rc = OSPF_OK;
     if (devices_.size() > 1) {
@@ -879,11 +934,12 @@ void LinkState::ensureEngine() {
       throw EngineError(rc, "ospf_open failed (no MI355X device / HIP runtime?)");
     }
     engineOpened_ = true;
-    if (injectAfter_) {
-      ospf_inject_error(engine_, injectAfter_);
-      injectAfter_ = 0;
-    }
   }
+  if (injectAfter_) {
+    ospf_inject_error(engine_, injectAfter_);
+    injectAfter_ = 0;
+  }
+  const auto tOpen = std::chrono::steady_clock::now();
   if (engineVersion_ != snapVersion_) {
     dropSweep();
     ospf_csr g{};
@@ -904,6 +960,10 @@ void LinkState::ensureEngine() {
     ++topoStats_.loads;
     engineVersion_ = snapVersion_;
   }
+  if ((opening || loading) && getenv("ODL_SPF_TIMING"))
+    fprintf(stderr, "ensure_engine open=%d load=%d open_ms=%.3f load_ms=%.3f\n", opening, loading,
+            std::chrono::duration<double, std::milli>(tOpen - t0).count(),
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tOpen).count());
 }
 
 void LinkState::dropSweep() {

@@ -75,6 +75,30 @@ void parallelFor(uint32_t n, F&& f, uint32_t chunk = 512) {
   if (err) std::rethrow_exception(err);
 }
 
+// std::sort of v on up to 8 host threads: sorted slices merged pairwise
+template <class T>
+void parallelSort(std::vector<T>& v) {
+  const size_t n = v.size();
+  uint32_t C = 1;
+  const uint32_t hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  while (C * 2 <= hw && n / (C * 2) >= 8192) C *= 2;
+  if (C == 1) {
+    std::sort(v.begin(), v.end());
+    return;
+  }
+  std::vector<size_t> b(C + 1);
+  for (uint32_t k = 0; k <= C; ++k) b[k] = n * k / C;
+  parallelFor(C, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t k = lo; k < hi; ++k) std::sort(v.begin() + b[k], v.begin() + b[k + 1]);
+  }, 1);
+  for (uint32_t w = 1; w < C; w *= 2)
+    parallelFor(C / (2 * w), [&](uint32_t lo, uint32_t hi) {
+      for (uint32_t q = lo; q < hi; ++q)
+        std::inplace_merge(v.begin() + b[2 * q * w], v.begin() + b[2 * q * w + w],
+                           v.begin() + b[2 * q * w + 2 * w]);
+    }, 1);
+}
+
 struct Adjacency {
   std::string otherNodeName, ifName, otherIfName;
   int32_t metric = 1;
@@ -179,6 +203,8 @@ class Link {
   mutable uint32_t snapLid = 0xFFFFFFFFu;
   mutable uint32_t snapEnd[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};  // snapshot node ids of the ends
   int endIndex(const std::string& n) const { return end_[0].node == n ? 0 : 1; }
+  int lowIndex() const { return lo_; }
+  bool selfLoop() const { return end_[0].node == end_[1].node; }
   Metric metricOfEnd(int i) const { return end_[i].metric.value(); }
 
  private:
@@ -737,6 +763,14 @@ class LinkState {
   // frees dropped memos on one background thread (clearMemo); joined by the
   // destructor
   std::unique_ptr<struct MemoReaper> reaper_;
+  // the engine opened on a host thread while a bulk ingest's caller goes on
+  // (Decision opens its device at start; here the first bulk ingest does):
+  // the HIP runtime's start and the kernels' code objects are loaded by a
+  // tiny warm-up run, off the first getSpfResult's path. ensureEngine joins.
+  std::thread opener_;
+  ospf_ctx* openerCtx_ = nullptr;
+  void startOpen();
+  void joinOpen();
 };
 
 }  // namespace odl

@@ -8,6 +8,9 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
+#include <mutex>
+#include <functional>
 #include <cstdio>
 #include <map>
 #include <unordered_map>
@@ -586,8 +589,12 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
   // the stream of the full reruns: the caller's, or a high-priority one
   // while the decremental kernels run beside them (run_ksp2's presplit)
   hipStream_t fs = s;
+  // after_first: called once the first round's traversal is done on fs (the
+  // host waits for it anyway): the presplit runs' first round gets the GPU
+  // alone, the decremental kernels are launched beside the later rounds
   auto full_reruns = [&](const uint32_t* R_dsts, uint32_t R_n, const uint32_t* R_ign,
-                         const uint32_t* R_cnt, uint32_t* R_status, uint32_t* R_k2) -> int {
+                         const uint32_t* R_cnt, uint32_t* R_status, uint32_t* R_k2,
+                         const std::function<int()>& after_first = nullptr) -> int {
     ospf::TraceArgs t = t_k1;
     const uint32_t total_vb = (R_n + 63) / 64;  // this set's virtual batches (<= the carve'fs)
     HIPCHK(c, hipMemsetD32Async(d_roots, (int)src, ms ? R_n : chunk, fs));
@@ -671,6 +678,10 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
         }
         HIPCHK(c, hipEventRecord(ev_bfs[slot], fs));
         HIPCHK(c, hipStreamWaitEvent(c->aux, ev_bfs[slot], 0));
+        if (r == 0 && after_first) {
+          const int rc3 = after_first();
+          if (rc3) return rc3;
+        }
         const uint32_t r0 = vb0 * 64u;
         ospf::TraceArgs t2 = t;
         t2.dsts = R_dsts + r0;
@@ -788,6 +799,8 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
     td.heavy_ctr = d_ctr + 4;
     td.err = c->d_err;
     td.decr_runs = decr_r;
+    // (OSPF_KSP_MAP_FB=1: a run past the map budget to the full reruns)
+    if (const char* x = getenv("OSPF_KSP_MAP_FB")) td.map_fb = atoi(x) ? 1u : 0u;
     if (prune) {
       char* q = dp + sz_tc + 3 * sz_fb + sz_ctr + sz_dd;
       uint32_t* d_ord = (uint32_t*)q;
@@ -835,15 +848,39 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
         fs = c->ksp_hi;
       }
     }
-    e = ospf::launch_ksp_decr(c->g, td, nblk, ks);
-    if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_decr");
-    if (td.budget) {
-      e = ospf::launch_ksp_decr_heavy(c->g, td, hblk, ks);
-      if (e != hipSuccess) return hip_fail(c, e, "launch_ksp_decr_heavy");
+    // OSPF_KSP_DEBUG=2: a log of the heavy runs (run, start, traced, end)
+    unsigned long long* d_hlog = nullptr;
+    const char* kdbg = getenv("OSPF_KSP_DEBUG");
+    if (kdbg && atoi(kdbg) >= 2 && td.budget) {
+      HIPCHK(c, dev_malloc(c, (void**)&d_hlog, 4ull * 65536 * 8));
+      td.hlog = d_hlog;
     }
+    // the decremental kernels: queued before the presplit runs, beside them
+    // (OSPF_KSP_DECR_AFTER=1: after their first traversal round -- measured
+    // slower, 22.9 vs 20.4 ms per F100k launch: the presplit chain is not
+    // the longer one once it shares the chip)
+    bool decr_queued = false;
+    auto launch_decr = [&]() -> int {
+      if (decr_queued) return OSPF_OK;
+      decr_queued = true;
+      if (ks != s) {  // (the first round's traversal done: ordered on fs)
+        HIPCHK(c, hipEventRecord(c->ksp_ev[0], fs));
+        HIPCHK(c, hipStreamWaitEvent(ks, c->ksp_ev[0], 0));
+      }
+      hipError_t e3 = ospf::launch_ksp_decr(c->g, td, nblk, ks);
+      if (e3 != hipSuccess) return hip_fail(c, e3, "launch_ksp_decr");
+      if (td.budget) {
+        e3 = ospf::launch_ksp_decr_heavy(c->g, td, hblk, ks);
+        if (e3 != hipSuccess) return hip_fail(c, e3, "launch_ksp_decr_heavy");
+      }
+      return OSPF_OK;
+    };
+    const bool decr_first = !npre || getenv("OSPF_KSP_DECR_AFTER") == nullptr;
+    if (decr_first && (rc = launch_decr())) return rc;
     // a list of runs through full_reruns on s: compacted (dsts, status,
     // ignore sets, counts) into scratch slot `slot`, records scattered back
-    auto rerun_list = [&](const uint32_t* d_list, uint32_t nl, int slot) -> int {
+    auto rerun_list = [&](const uint32_t* d_list, uint32_t nl, int slot,
+                          const std::function<int()>& after_first = nullptr) -> int {
       const size_t sz_fd = align_up(nl * 4ull, 256), sz_fr = align_up((size_t)nl * cap * 4ull, 256);
       int rc2 = OSPF_OK;
       char* fp = stream_scratch(c, s, 3 * sz_fd + 2 * sz_fr, &rc2, slot);
@@ -859,7 +896,7 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
           (e2 = ospf::launch_rows_gather(f_cnt, d_cnt, d_list, nl, 1, true, fs)) != hipSuccess ||
           (e2 = ospf::launch_rows_gather(f_ign, d_ign, d_list, nl, cap, true, fs)) != hipSuccess)
         return hip_fail(c, e2, "launch_rows_gather");
-      rc2 = full_reruns(f_dsts, nl, f_ign, f_cnt, f_status, f_k2);
+      rc2 = full_reruns(f_dsts, nl, f_ign, f_cnt, f_status, f_k2, after_first);
       if (rc2) return rc2;
       if ((e2 = ospf::launch_rows_gather(k->status, f_status, d_list, nl, 1, false, fs)) != hipSuccess ||
           (e2 = ospf::launch_rows_gather(k->k2, f_k2, d_list, nl, cap, false, fs)) != hipSuccess)
@@ -881,15 +918,34 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
         HIPCHK(c, hipMemcpyAsync(d_pre, pre.data(), npre * 4ull, hipMemcpyHostToDevice, fs));
         HIPCHK(c, hipStreamSynchronize(fs));
       }
-      rc = rerun_list(d_pre, npre, 3);
+      rc = rerun_list(d_pre, npre, 3, launch_decr);
       if (rc) return rc;
     }
+    if ((rc = launch_decr())) return rc;  // (no round called it)
     uint32_t ctr[32] = {};
     HIPCHK(c, hipMemcpyAsync(ctr, d_ctr, 128, hipMemcpyDeviceToHost, ks));
     HIPCHK(c, hipStreamSynchronize(ks));
     if (ks != s) {
       HIPCHK(c, hipEventRecord(c->ksp_ev[1], ks));
       HIPCHK(c, hipStreamWaitEvent(fs, c->ksp_ev[1], 0));
+    }
+    if (d_hlog) {
+      const uint32_t nh = std::min(ctr[11], 65536u);
+      std::vector<unsigned long long> hl(4ull * nh);
+      HIPCHK(c, hipMemcpy(hl.data(), d_hlog, hl.size() * 8, hipMemcpyDeviceToHost));
+      (void)hipFree(d_hlog);
+      unsigned long long t0 = ~0ull;
+      for (uint32_t q = 0; q < nh; ++q) t0 = std::min(t0, hl[4 * q + 1]);
+      std::vector<uint32_t> ord(nh);
+      for (uint32_t q = 0; q < nh; ++q) ord[q] = q;
+      std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) {
+        return hl[4 * a + 3] - hl[4 * a + 1] > hl[4 * b + 3] - hl[4 * b + 1];
+      });
+      for (uint32_t x = 0; x < std::min(nh, 12u); ++x) {
+        const unsigned long long* l = &hl[4ull * ord[x]];
+        fprintf(stderr, "ksp2 heavy run %llu (dst %u): start +%.3f ms, prep %.3f, trace %.3f ms\n", l[0],
+                k->dsts ? 0u : 0u, (l[1] - t0) / 1e5, (l[2] - l[1]) / 1e5, (l[3] - l[2]) / 1e5);
+      }
     }
     if (getenv("OSPF_KSP_DEBUG")) {
       uint64_t clk[8];
@@ -899,9 +955,10 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
       fprintf(stderr,
               "ksp2 decr: runs %u presplit %u decided %u fallbacks %u (A %u, map %u, ign %u, hash %u, edges %u) "
               "heavy %u affected %u; wave-ms prep %.1f step3 %.1f trace %.1f fb-prep %.1f; heavy "
-              "block-ms prep %.1f trace %.1f\n",
+              "block-ms prep %.1f trace %.1f; longest heavy run %.2f ms (run %u), %llu over 1 ms\n",
               n, npre, ctr[2], ctr[1], ctr[6], ctr[7], ctr[8], ctr[9], ctr[10], ctr[4], ctr[3], wm(clk[0]),
-              wm(clk[1]), wm(clk[2]), wm(clk[3]), wm(clk[4]), wm(clk[5]));
+              wm(clk[1]), wm(clk[2]), wm(clk[3]), wm(clk[4]), wm(clk[5]), wm(clk[6] >> 24),
+              (uint32_t)(clk[6] & 0xFFFFFFu), (unsigned long long)clk[7]);
     }
     c->ksp_decr_stats[0] += ctr[2];
     c->ksp_decr_stats[1] += ctr[1] + npre;
@@ -1402,6 +1459,16 @@ uint64_t ospf_spf_runs(const ospf_ctx* c) { return c ? c->spf_runs : 0; }
 int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   if (!c || !csr) return OSPF_E_INVAL;
   if (injected(c)) return OSPF_E_DEVICE;
+  // OSPF_SWEEP_TIMING: host phases of the load on stderr
+  const bool tm = getenv("OSPF_SWEEP_TIMING") != nullptr;
+  auto tl = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (!tm) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "sweep_create load/%s %.2f ms\n", what,
+            std::chrono::duration<double, std::milli>(now - tl).count());
+    tl = now;
+  };
   const uint32_t V = csr->n_nodes, E = csr->n_edges;
   if (V == 0 || V >= 0x80000000u) return fail(c, OSPF_E_INVAL, "n_nodes out of range");
   if (!csr->row_ptr || (E && (!csr->col || !csr->metric || !csr->link_id || !csr->twin ||
@@ -1410,46 +1477,92 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   if (csr->row_ptr[0] != 0 || csr->row_ptr[V] != E)
     return fail(c, OSPF_E_INVAL, "row_ptr must start at 0 and end at n_edges");
 
+  // validation, flagged entries and distinct-neighbour counts per node on
+  // host threads (chunks of 512 nodes: whole words of the no-transit bits)
   std::vector<uint32_t> colx(E), rw(E), nt((V + 31) / 32, 0u), dn_off(V + 1, 0u);
-  std::vector<uint32_t> dn;
-  dn.reserve(E);
   uint32_t max_deg = 0, max_metric = 0, max_dn = 0, n_links = 0;
   uint64_t dist_bound = 0;
   bool unit = true;
-  for (uint32_t u = 0; u < V; ++u) {
-    const uint32_t b = csr->row_ptr[u], e1 = csr->row_ptr[u + 1];
-    uint32_t row_max = 0;
-    if (e1 < b || e1 > E) return fail(c, OSPF_E_INVAL, "row_ptr not monotone");
-    max_deg = std::max(max_deg, e1 - b);
-    dn_off[u] = (uint32_t)dn.size();
-    for (uint32_t e = b; e < e1; ++e) {
-      const uint32_t v = csr->col[e];
-      if (v >= V) return fail(c, OSPF_E_INVAL, "col out of range");
-      if (e > b && csr->col[e - 1] > v) return fail(c, OSPF_E_INVAL, "rows must be sorted by col");
-      const uint32_t t = csr->twin[e];
-      if (t >= E || csr->twin[t] != e || csr->col[t] != u || t < csr->row_ptr[v] ||
-          t >= csr->row_ptr[v + 1] || csr->link_id[t] != csr->link_id[e])
-        return fail(c, OSPF_E_INVAL, "twin/link_id inconsistent");
-      if (csr->edge_up[e] != csr->edge_up[t])
-        return fail(c, OSPF_E_INVAL, "edge_up must match on both directions of a link");
-      const bool up = csr->edge_up[e] != 0;
-      colx[e] = v | (up ? 0u : 0x80000000u);
-      rw[e] = csr->metric[t];
-      if (up) {
-        if (csr->metric[e] == 0)
-          return fail(c, OSPF_E_RANGE, "metric 0 on a usable link is outside the engine contract");
-        max_metric = std::max(max_metric, csr->metric[e]);
-        row_max = std::max(row_max, csr->metric[e]);
-        unit &= csr->metric[e] == 1;
+  std::mutex red_mu;
+  int bad_rc = OSPF_OK;
+  const char* bad_msg = nullptr;
+  ospf_int::par_for(V, [&](uint32_t lo, uint32_t hi) {
+    uint32_t l_deg = 0, l_metric = 0, l_dn = 0, l_links = 0;
+    uint64_t l_bound = 0;
+    bool l_unit = true;
+    int rc = OSPF_OK;
+    const char* msg = nullptr;
+    auto bad = [&](int code, const char* m) {
+      rc = code;
+      msg = m;
+    };
+    for (uint32_t u = lo; u < hi && rc == OSPF_OK; ++u) {
+      const uint32_t b = csr->row_ptr[u], e1 = csr->row_ptr[u + 1];
+      uint32_t row_max = 0, ndn = 0;
+      if (e1 < b || e1 > E) {
+        bad(OSPF_E_INVAL, "row_ptr not monotone");
+        break;
       }
-      if (e < t) ++n_links;
-      if (v != u && (e == b || csr->col[e - 1] != v)) dn.push_back(v);
+      l_deg = std::max(l_deg, e1 - b);
+      for (uint32_t e = b; e < e1; ++e) {
+        const uint32_t v = csr->col[e];
+        if (v >= V) { bad(OSPF_E_INVAL, "col out of range"); break; }
+        if (e > b && csr->col[e - 1] > v) { bad(OSPF_E_INVAL, "rows must be sorted by col"); break; }
+        const uint32_t t = csr->twin[e];
+        if (t >= E || csr->twin[t] != e || csr->col[t] != u || t < csr->row_ptr[v] ||
+            t >= csr->row_ptr[v + 1] || csr->link_id[t] != csr->link_id[e]) {
+          bad(OSPF_E_INVAL, "twin/link_id inconsistent");
+          break;
+        }
+        if (csr->edge_up[e] != csr->edge_up[t]) {
+          bad(OSPF_E_INVAL, "edge_up must match on both directions of a link");
+          break;
+        }
+        const bool up = csr->edge_up[e] != 0;
+        colx[e] = v | (up ? 0u : 0x80000000u);
+        rw[e] = csr->metric[t];
+        if (up) {
+          if (csr->metric[e] == 0) {
+            bad(OSPF_E_RANGE, "metric 0 on a usable link is outside the engine contract");
+            break;
+          }
+          l_metric = std::max(l_metric, csr->metric[e]);
+          row_max = std::max(row_max, csr->metric[e]);
+          l_unit &= csr->metric[e] == 1;
+        }
+        if (e < t) ++l_links;
+        if (v != u && (e == b || csr->col[e - 1] != v)) ++ndn;
+      }
+      dn_off[u + 1] = ndn;
+      l_dn = std::max(l_dn, ndn);
+      l_bound += row_max;
+      if (csr->no_transit && csr->no_transit[u]) nt[u >> 5] |= 1u << (u & 31);
     }
-    max_dn = std::max<uint32_t>(max_dn, (uint32_t)dn.size() - dn_off[u]);
-    dist_bound += row_max;
-    if (csr->no_transit && csr->no_transit[u]) nt[u >> 5] |= 1u << (u & 31);
-  }
-  dn_off[V] = (uint32_t)dn.size();
+    std::lock_guard<std::mutex> g(red_mu);
+    max_deg = std::max(max_deg, l_deg);
+    max_metric = std::max(max_metric, l_metric);
+    max_dn = std::max(max_dn, l_dn);
+    n_links += l_links;
+    dist_bound += l_bound;
+    unit &= l_unit;
+    if (rc != OSPF_OK && bad_rc == OSPF_OK) {
+      bad_rc = rc;
+      bad_msg = msg;
+    }
+  });
+  if (bad_rc != OSPF_OK) return fail(c, bad_rc, bad_msg);
+  for (uint32_t u = 0; u < V; ++u) dn_off[u + 1] += dn_off[u];
+  std::vector<uint32_t> dn(dn_off[V]);
+  ospf_int::par_for(V, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t u = lo; u < hi; ++u) {
+      uint32_t k = dn_off[u];
+      for (uint32_t e = csr->row_ptr[u], b = e; e < csr->row_ptr[u + 1]; ++e) {
+        const uint32_t v = csr->col[e];
+        if (v != u && (e == b || csr->col[e - 1] != v)) dn[k++] = v;
+      }
+    }
+  });
+  lap("validate + distinct neighbours");
   if (max_dn > OSPF_MAX_ROOT_NEIGHBORS)
     return fail(c, OSPF_E_RANGE, "a node has more distinct neighbours than OSPF_MAX_ROOT_NEIGHBORS");
 
@@ -1464,26 +1577,39 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   // link_rank given: a parallel group (same neighbour) is ordered by the
   // twin entry's rank = the link's position in linksFromNode(neighbour), the
   // order pathLinks lists links of one predecessor in (LinkState.cpp:885-901)
-  std::vector<uint32_t> ord;
   uint32_t max_lid = 0;
-  for (uint32_t u = 0; u < V; ++u) {
-    const uint32_t b = csr->row_ptr[u], n = csr->row_ptr[u + 1] - b, pb = prow[u];
-    ord.resize(n);
-    for (uint32_t k = 0; k < n; ++k) ord[k] = b + k;
-    if (csr->link_rank)
-      std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
-        if (csr->col[x] != csr->col[y]) return csr->col[x] < csr->col[y];
-        return csr->link_rank[csr->twin[x]] < csr->link_rank[csr->twin[y]];
-      });
-    for (uint32_t k = 0; k < n; ++k) {
-      const uint32_t e = ord[k];
-      pcolx[pb + k] = colx[e];
-      pw[pb + k] = csr->metric[e];
-      prw[pb + k] = rw[e];
-      plink[pb + k] = csr->link_id[e];
-      max_lid = std::max(max_lid, csr->link_id[e]);
+  ospf_int::par_for(V, [&](uint32_t lo, uint32_t hi) {
+    std::vector<uint32_t> ord;
+    uint32_t l_lid = 0;
+    for (uint32_t u = lo; u < hi; ++u) {
+      const uint32_t b = csr->row_ptr[u], n = csr->row_ptr[u + 1] - b, pb = prow[u];
+      ord.resize(n);
+      for (uint32_t k = 0; k < n; ++k) ord[k] = b + k;
+      // rows are sorted by neighbour: only a run of parallel links (equal
+      // neighbours) is reordered, by its twins' ranks
+      if (csr->link_rank)
+        for (uint32_t k = 0; k < n;) {
+          uint32_t k1 = k + 1;
+          while (k1 < n && csr->col[b + k1] == csr->col[b + k]) ++k1;
+          if (k1 - k > 1)
+            std::stable_sort(ord.begin() + k, ord.begin() + k1, [&](uint32_t x, uint32_t y) {
+              return csr->link_rank[csr->twin[x]] < csr->link_rank[csr->twin[y]];
+            });
+          k = k1;
+        }
+      for (uint32_t k = 0; k < n; ++k) {
+        const uint32_t e = ord[k];
+        pcolx[pb + k] = colx[e];
+        pw[pb + k] = csr->metric[e];
+        prw[pb + k] = rw[e];
+        plink[pb + k] = csr->link_id[e];
+        l_lid = std::max(l_lid, csr->link_id[e]);
+      }
     }
-  }
+    std::lock_guard<std::mutex> g(red_mu);
+    max_lid = std::max(max_lid, l_lid);
+  });
+  lap("padded rows + parallel-link order");
   // entries of each link id (KSP2 ignore masks); ids above 2^28 disable them
   const uint32_t n_lid = (E && max_lid < (1u << 28)) ? max_lid + 1 : 0;
   // Reserves for structural patches (ospf_update_rows, links added / removed
@@ -1509,31 +1635,38 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
                sz_big = std::max<size_t>(big.size(), 1) * 4ull, sz_key = V * 16ull,
                sz_le = link_e.size() * 4ull;
   std::vector<uint64_t> dkey(2ull * V);  // digest key tables (row digest kernel)
-  for (uint32_t u = 0; u < V; ++u) {
-    dkey[2ull * u] = ospf::digest_dist_key(u);
-    dkey[2ull * u + 1] = ospf::digest_node_key(u);
-  }
+  ospf_int::par_for(V, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t u = lo; u < hi; ++u) {
+      dkey[2ull * u] = ospf::digest_dist_key(u);
+      dkey[2ull * u + 1] = ospf::digest_node_key(u);
+    }
+  });
   // packed {colx, w | rw << 16} entries when every metric fits 16 bits
   bool ew_ok = true;
   for (uint32_t e = 0; e < Ep && ew_ok; ++e) ew_ok = pw[e] <= 0xFFFFu && prw[e] <= 0xFFFFu;
   std::vector<uint32_t> pew(ew_ok ? 2ull * Ep : 2, 0u);
-  for (uint32_t e = 0; e < Ep && ew_ok; ++e) {
-    pew[2ull * e] = pcolx[e];
-    pew[2ull * e + 1] = pw[e] | (prw[e] << 16);
-  }
+  if (ew_ok)
+    ospf_int::par_for(Ep, [&](uint32_t lo, uint32_t hi) {
+      for (uint32_t e = lo; e < hi; ++e) {
+        pew[2ull * e] = pcolx[e];
+        pew[2ull * e + 1] = pw[e] | (prw[e] << 16);
+      }
+    }, 1u << 16);
   const size_t sz_ew = pew.size() * 4ull;
   // distinct-neighbour index per padded entry (rows are sorted by neighbour)
   std::vector<uint16_t> didx(std::max<uint32_t>(Ep, 1), 0xFFFFu);
-  for (uint32_t u = 0; u < V; ++u) {
-    uint32_t k = 0, prev = 0xFFFFFFFFu;
-    for (uint32_t e = prow[u]; e < prow[u + 1]; ++e) {
-      const uint32_t v = pcolx[e] & 0x7FFFFFFFu;
-      if (plink[e] == 0xFFFFFFFFu || v == u) continue;  // padding, self-loop
-      if (prev != 0xFFFFFFFFu && v != prev) ++k;
-      prev = v;
-      didx[e] = (uint16_t)k;
+  ospf_int::par_for(V, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t u = lo; u < hi; ++u) {
+      uint32_t k = 0, prev = 0xFFFFFFFFu;
+      for (uint32_t e = prow[u]; e < prow[u + 1]; ++e) {
+        const uint32_t v = pcolx[e] & 0x7FFFFFFFu;
+        if (plink[e] == 0xFFFFFFFFu || v == u) continue;  // padding, self-loop
+        if (prev != 0xFFFFFFFFu && v != prev) ++k;
+        prev = v;
+        didx[e] = (uint16_t)k;
+      }
     }
-  }
+  });
   const size_t sz_didx = didx.size() * 2ull;
   // node keys alone, zero padded past V: a lane's 16 nodes in 8 loads, and
   // kernels that walk level rows to their pitch (V rounded up to 128 in the
@@ -1541,6 +1674,7 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   std::vector<uint64_t> dkn((V + 127) / 128 * 128 + 128, 0ull);
   for (uint32_t u = 0; u < V; ++u) dkn[u] = dkey[2ull * u + 1];
   const size_t sz_kn = dkn.size() * 8ull;
+  lap("link entries, digest keys, packed entries, didx");
   size_t off[14], tot = 0;
   const size_t szs[14] = {sz_row, sz_e,     sz_e,  sz_e,   sz_e,  sz_nt,  sz_dnoff,
                           sz_dn,  sz_big,   sz_key, sz_le, sz_ew, sz_didx, sz_kn};
@@ -1570,6 +1704,7 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
                           link_e.data(), pew.data(), didx.data(), dkn.data()};
   for (int i = 0; i < 14; ++i)
     if (szs[i] && srcs[i]) HIPCHK(c, hipMemcpy(base + off[i], srcs[i], szs[i], hipMemcpyHostToDevice));
+  lap("device allocation + copies");
   c->g.V = V;
   c->g.E = Ep;
   c->g.row_ptr = (const uint32_t*)(base + off[0]);
@@ -1606,8 +1741,15 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   c->h_nt = std::move(nt);
   c->h_link_e = std::move(link_e);
   c->non_unit = 0;
-  for (uint32_t e = 0; e < Ep; ++e)
-    if (!(c->h_pcolx[e] & 0x80000000u) && c->h_pw[e] != 1) ++c->non_unit;
+  {
+    std::atomic<uint64_t> nu{0};
+    ospf_int::par_for(Ep, [&](uint32_t lo, uint32_t hi) {
+      uint64_t k = 0;
+      for (uint32_t e = lo; e < hi; ++e) k += !(c->h_pcolx[e] & 0x80000000u) && c->h_pw[e] != 1;
+      nu += k;
+    }, 1u << 16);
+    c->non_unit = nu.load();
+  }
   c->info.n_nodes = V;
   c->info.n_edges = E;
   c->info.n_links = n_links;
@@ -1619,12 +1761,15 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   c->info.device_bytes = tot;
   c->dist_bound = dist_bound;
   c->h_rowmax.assign(V, 0u);
-  for (uint32_t u = 0; u < V; ++u)
-    for (uint32_t e = c->h_prow[u]; e < c->h_prow[u + 1]; ++e)
-      if (!(c->h_pcolx[e] & 0x80000000u)) c->h_rowmax[u] = std::max(c->h_rowmax[u], c->h_pw[e]);
+  ospf_int::par_for(V, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t u = lo; u < hi; ++u)
+      for (uint32_t e = c->h_prow[u]; e < c->h_prow[u + 1]; ++e)
+        if (!(c->h_pcolx[e] & 0x80000000u)) c->h_rowmax[u] = std::max(c->h_rowmax[u], c->h_pw[e]);
+  });
   c->mask = ospf_ctx::Mask{};
   c->loaded = true;
   ++c->graph_gen;
+  lap("depth bound + host shadows");
   return OSPF_OK;
 }
 
@@ -2074,7 +2219,8 @@ int nh_derive_twin_launch(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint
   a.dist = d_dist;
   a.dpitch = dist_pitch;
   a.npitch = nh_pitch;
-  if (nh_pitch && (nh_pitch < c->info.n_nodes * nh_words || nh_pitch % 4u))
+  // (a pitch that is not a multiple of 4 words takes the kernels' 4-B stores)
+  if (nh_pitch && nh_pitch < c->info.n_nodes * nh_words)
     return fail(c, OSPF_E_INVAL, "twin derive: next-hop row pitch < V * nh_words");
   if (const char* e = getenv("OSPF_TWIN_CTILES")) a.ctiles = (uint32_t)std::max(1, atoi(e));
   hipError_t e = ospf::launch_nh_derive_twin(c->g, a, s);

@@ -649,6 +649,8 @@ struct TraceArgs {
   uint32_t* pre_bits;       // [n / 32] runs the presplit sent to the full reruns (ksp_decr skips them)
   uint32_t* heavy;          // [n] queued run indices
   uint32_t* heavy_ctr;      // [2] {queued, taken}, zeroed by the caller
+  unsigned long long* hlog; // debug (OSPF_KSP_DEBUG=2): [n][4] {run, start, traced, end} clocks of heavy runs
+  uint32_t map_fb;          // runs past the decremental map budget: 1 = the full reruns, 0 = the heavy kernel
   // decremental reruns (launch_ksp_decr): rows = the source's dist row
   const uint32_t* tc;       // [V] hint: link of each node's last support (launch_ksp_hint)
   uint32_t* fb;             // [n] runs left to the full masked reruns

@@ -1011,7 +1011,7 @@ __global__ void __launch_bounds__(64) ksp_decr_kernel(DevGraph g, TraceArgs t) {
       // edge or ignore-list budget (a large change, whose single-wave
       // prepare there would be slow: OSPF_KSP_SRCCUT=0 at F100k sends 7 such
       // runs and takes 58 ms): the full reruns
-      if (t.budget && ((volatile uint32_t&)L.why) == 0u &&
+      if (t.budget && !t.map_fb && ((volatile uint32_t&)L.why) == 0u &&
           ((volatile uint32_t&)L.naff) <= DecrSmall::kAff) {
         if (lane == 0) {
           out[0] = 0u;
@@ -1256,8 +1256,19 @@ __global__ void __launch_bounds__(1024) ksp_decr_heavy_kernel(DevGraph g, TraceA
     }
     if (threadIdx.x == 0) {  // [20] prepare, [21] trace of the heavy runs
       uint64_t* clk = reinterpret_cast<uint64_t*>(t.ctr + 16);
+      const uint64_t c2 = wall_clock64();
       atomicAdd((unsigned long long*)&clk[4], (unsigned long long)(c1 - c0));
-      atomicAdd((unsigned long long*)&clk[5], (unsigned long long)(wall_clock64() - c1));
+      atomicAdd((unsigned long long*)&clk[5], (unsigned long long)(c2 - c1));
+      // [22] the longest heavy run (time << 24 | run), [23] runs over 1 ms
+      atomicMax((unsigned long long*)&clk[6], (unsigned long long)(((c2 - c0) << 24) | (i & 0xFFFFFFu)));
+      if (c2 - c0 > 100000ull) atomicAdd((unsigned long long*)&clk[7], 1ull);
+      if (t.hlog) {
+        unsigned long long* l = t.hlog + 4ull * (atomicAdd(&t.ctr[11], 1u) & 0xFFFFu);
+        l[0] = i;
+        l[1] = c0;
+        l[2] = c1;
+        l[3] = c2;
+      }
     }
   }
 }

@@ -108,7 +108,7 @@ for st in $STEPS; do
            if [ $rc -eq 0 ]; then
              ND=$(python -c "import json; print(json.load(open('$OUT/kpmc1.json'))['roofline']['destinations_per_launch'])")
              python scripts/pmc_sum.py "$OUT/kpmc1" "$OUT/kpmc2" --launches 3 --match "ospf::" --extra destinations_per_launch=$ND > "$OUT/ksp2_pmc.json" &&
-             mkdir -p profiles/r05 && cp "$OUT/ksp2_pmc.json" profiles/r05/ksp2_pmc.json &&
+             mkdir -p profiles/r06 && cp "$OUT/ksp2_pmc.json" profiles/r06/ksp2_pmc.json &&
              timeout -k 10 600 python scripts/bench_ksp2.py > "$OUT/ksp2.json" 2> "$OUT/ksp2.err"; rc=$?
              head -c 600 "$OUT/ksp2.json"; tail -3 "$OUT/ksp2.err"
            fi;;

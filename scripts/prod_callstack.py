@@ -30,6 +30,8 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ["ODL_SPF_TIMING"] = "1"
+os.environ.setdefault("OSPF_SWEEP_TIMING", "1")  # sweep + graph-load phases
+os.environ.setdefault("ODL_SNAP_TIMING", "1")    # CSR snapshot phases
 
 import torch  # noqa: E402,F401  (one HIP runtime for torch and the engine)
 
@@ -60,6 +62,10 @@ class Stderr:
         """OSPF_SWEEP_TIMING's ospf_sweep_create phases -> {phase: ms}"""
         return {k: float(v) for k, v in re.findall(r"sweep_create (.+?) ([0-9.]+) ms", self.text)}
 
+    def snap_laps(self):
+        """ODL_SNAP_TIMING's CSR snapshot phases -> {phase: ms}"""
+        return {k: float(v) for k, v in re.findall(r"snapshot (.+?) ([0-9.]+) ms", self.text)}
+
     def values(self, key):
         return [float(x) for x in re.findall(key + r"=([0-9.]+)", self.text)]
 
@@ -72,7 +78,20 @@ def timed(fn):
     return out, wall, cap
 
 
+def progress(msg):
+    """a line on the real stderr (fd 2 may be captured by Stderr)"""
+    with open("/proc/self/fd/%d" % PROGRESS_FD, "a") as f:
+        f.write(f"[{time.strftime('%H:%M:%S')}] {msg}\n")
+
+
+PROGRESS_FD = os.dup(2)
+
+
 def main():
+    import faulthandler
+    trace = os.environ.get("PROD_TRACE_FILE")
+    if trace:  # where a stalled step is, every 60 s
+        faulthandler.dump_traceback_later(60, repeat=True, file=open(trace, "w"))
     ap = argparse.ArgumentParser()
     ap.add_argument("--pods", type=int, default=1781)
     ap.add_argument("--me", default="3-0-0")
@@ -83,10 +102,18 @@ def main():
     out = {"topology": f"fabric pods={args.pods} planes=8 (unit metric)", "me": args.me}
 
     def stack(p, me, label):
+        progress(f"{label}: getSpfResult")
         _, wall, cap = timed(lambda: p.prefetch([me]))
         rec = {"getSpfResult_wall_ms": round(wall, 3),
                "engine_ms": sum(cap.values("engine_ms")),
                "build_result_ms": sum(cap.values("build_result_ms"))}
+        if cap.laps():  # ospf_load_graph phases (a cold call loads the graph)
+            rec["engine_laps"] = cap.laps()
+        if cap.snap_laps():
+            rec["snapshot_laps"] = cap.snap_laps()
+        for k in ("open_ms", "load_ms"):  # ensureEngine (ODL_SPF_TIMING)
+            if cap.values(k):
+                rec["ensure_engine_" + k] = sum(cap.values(k))
         names = p.node_names()
         prefixes = {f"lo-{n}": [[n, "ip", "ecmp", 0, None]] for n in names}
         lines = [f"{pfx}\t{ents[0][0]}:0:0:0:" for pfx, ents in prefixes.items()]
@@ -105,6 +132,7 @@ def main():
         print(f"{label}: {rec}", file=sys.stderr, flush=True)
 
     for incremental in (False, True):
+        progress(f"ingest incremental={incremental}")
         p = LinkState()
         p.set_incremental(incremental)
         t = time.perf_counter()
@@ -160,6 +188,7 @@ def main():
         rack = [d for d in st.to_dbs() if d.name == "3-902-7"][0]
         for kind, ev in (("node_down", AdjDbStream.from_dbs([AdjDb(rack.name, delete=True)])),
                          ("node_up", AdjDbStream.from_dbs([rack]))):
+            progress(f"{tag} {kind}")
             _, wall, _ = timed(lambda: p.apply(ev))
             out[f"{tag}_{kind}_apply_ms"] = round(wall, 3)
             _, wall, cap = timed(lambda: p.prefetch([args.me]))

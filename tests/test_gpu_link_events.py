@@ -15,7 +15,7 @@ from graphs import drained_fabric
 from link_events import apply_both, both, withdraw
 from oracle import Oracle  # noqa: F401
 from openr_amd import topology as T
-from openr_amd.adjdb import AdjDbStream, create_adjacency
+from openr_amd.adjdb import AdjDb, AdjDbStream, create_adjacency
 from openr_amd.engine import Engine
 from openr_amd.linkstate import LinkState
 
@@ -113,6 +113,29 @@ def test_f10k_link_down_up_sweep_in_place():
             assert p.spf_text(r) == o.spf_text(r), r
     s1 = p.topology_stats()
     assert s1["snapshots"] == s0["snapshots"] and s1["loads"] == s0["loads"], (s0, s1)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("pods", [64, 173])
+def test_fabric_node_down_up_sweep(pods):
+    """[NODE DOWN] / [NODE UP] of a rack on a fabric: the node count leaves
+    the multiples of 4 (unaligned row pitches in the derive sweep: round 6's
+    prod_callstack found its twin next-hop launch refusing them) and comes
+    back; the all-sources digests after each event equal the CSR-Dijkstra
+    restatement's for every root, on the engine (ODL_STRICT_ENGINE: no host
+    fallback)."""
+    st = drained_fabric(pods, 8, seed=5, drain=0.01, down=0.005)
+    o, p = both(st)
+    p.prefetch_all()
+    dbs = {d.name: d for d in st.to_dbs()}
+    rack = "3-7-5"
+    for ev in ([AdjDb(rack, delete=True)], [dbs[rack]]):
+        apply_both(o, p, ev)
+        names = p.node_names()
+        assert p.all_sources_digests().tolist() == o.fast_digests(names, True, threads=16).tolist()
+        assert p.spf_text("3-0-0") == o.spf_text("3-0-0")
+    assert p.sweep_stats()["mode"] == "derive"
+    assert not p.counters()["engine_degraded"]
 
 
 @pytest.mark.parametrize("seed", range(2))
