@@ -222,7 +222,7 @@ def main():
                     help="sweep order within a width class: grouped by smallest neighbour "
                          "(multi-source batches share frontiers), the random permutation, or "
                          "auto = grouped for single-word classes only")
-    ap.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles", "r05"))
+    ap.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles", "r06"))
     ap.add_argument("--iso-reps", type=int, default=3,
                     help="isolated launches per class for the roofline (after the timed steps)")
     ap.add_argument("--class-only", type=int, default=0,

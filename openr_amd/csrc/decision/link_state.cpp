@@ -760,6 +760,7 @@ const LinkState::Csr& LinkState::snapshot() {
       }
     }
   });
+  lap("rows sorted");
   parallelFor(V, [&](uint32_t lo, uint32_t hi) {
     for (size_t e = c.rowPtr[lo]; e < c.rowPtr[hi]; ++e) {
       const uint32_t lid = c.linkId[e];

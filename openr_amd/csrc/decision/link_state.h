@@ -21,6 +21,7 @@
 #include <atomic>
 #include <cstdint>
 #include <exception>
+#include <functional>
 #include <iterator>
 #include <memory>
 #include <mutex>
@@ -88,15 +89,25 @@ void parallelSort(std::vector<T>& v) {
   }
   std::vector<size_t> b(C + 1);
   for (uint32_t k = 0; k <= C; ++k) b[k] = n * k / C;
-  parallelFor(C, [&](uint32_t lo, uint32_t hi) {
-    for (uint32_t k = lo; k < hi; ++k) std::sort(v.begin() + b[k], v.begin() + b[k + 1]);
-  }, 1);
+  // fn(k) for k < m, one thread each (the calling thread runs k = 0)
+  auto each = [](uint32_t m, const std::function<void(uint32_t)>& fn) {
+    std::vector<std::thread> th;
+    for (uint32_t k = 1; k < m; ++k) {
+      try {
+        th.emplace_back(fn, k);
+      } catch (const std::system_error&) {
+        fn(k);
+      }
+    }
+    fn(0);
+    for (auto& t : th) t.join();
+  };
+  each(C, [&](uint32_t k) { std::sort(v.begin() + b[k], v.begin() + b[k + 1]); });
   for (uint32_t w = 1; w < C; w *= 2)
-    parallelFor(C / (2 * w), [&](uint32_t lo, uint32_t hi) {
-      for (uint32_t q = lo; q < hi; ++q)
-        std::inplace_merge(v.begin() + b[2 * q * w], v.begin() + b[2 * q * w + w],
-                           v.begin() + b[2 * q * w + 2 * w]);
-    }, 1);
+    each(C / (2 * w), [&](uint32_t q) {
+      std::inplace_merge(v.begin() + b[2 * q * w], v.begin() + b[2 * q * w + w],
+                         v.begin() + b[2 * q * w + 2 * w]);
+    });
 }
 
 struct Adjacency {
