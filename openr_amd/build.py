@@ -31,7 +31,7 @@ ENGINE_SO = os.path.join(LIB, "libopenr_spf_hip.so")
 DECISION_SO = os.path.join(LIB, "libopenr_decision.so")
 HEADERS = [os.path.join(ROOT, "include", h)
            for h in ("openr_spf.h", "openr_decision.h", "openr_adjdb.h")] + \
-    [os.path.join(PKG, "csrc", "engine", h) for h in ("spf_kernels.h", "spf_internal.h")]
+    [os.path.join(PKG, "csrc", "engine", h) for h in ("spf_kernels.h", "spf_internal.h", "host_pool.h")]
 DECISION_HEADERS = HEADERS + \
     [os.path.join(PKG, "csrc", "decision", h) for h in ("link_state.h", "spf_solver.h", "adjdb_thrift.h")]
 

@@ -36,6 +36,7 @@
 #include <vector>
 
 #include "../../../include/openr_adjdb.h"
+#include "../engine/host_pool.h"
 #include "../../../include/openr_spf.h"
 
 namespace odl {
@@ -46,13 +47,16 @@ using Metric = uint64_t;
 // (rows differ in length by 1000x: spines vs racks). The first exception a
 // chunk throws is rethrown on the calling thread after every thread joined.
 template <class F>
-void parallelFor(uint32_t n, F&& f, uint32_t chunk = 512) {
+void parallelFor(uint32_t n, F&& f, uint32_t chunk = 64) {
   const uint32_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   const uint32_t nt = std::max(1u, std::min(hw, n / (4 * chunk)));
   if (nt == 1) {
     f(0u, n);
     return;
   }
+  // the persistent pool (host_pool.h); threads of its own when it is busy
+  if (host_pool::Pool::get().run(n, chunk, nt, [&](uint32_t lo, uint32_t hi) { f(lo, hi); }))
+    return;
   std::atomic<uint32_t> next{0};
   std::exception_ptr err;
   std::atomic<bool> failed{false};
@@ -91,6 +95,10 @@ void parallelSort(std::vector<T>& v) {
   for (uint32_t k = 0; k <= C; ++k) b[k] = n * k / C;
   // fn(k) for k < m, one thread each (the calling thread runs k = 0)
   auto each = [](uint32_t m, const std::function<void(uint32_t)>& fn) {
+    if (host_pool::Pool::get().run(m, 1, m, [&](uint32_t lo, uint32_t hi) {
+          for (uint32_t k = lo; k < hi; ++k) fn(k);
+        }))
+      return;
     std::vector<std::thread> th;
     for (uint32_t k = 1; k < m; ++k) {
       try {

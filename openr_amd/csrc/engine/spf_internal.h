@@ -13,6 +13,7 @@
 #include <thread>
 #include <vector>
 
+#include "host_pool.h"
 #include "spf_kernels.h"
 
 struct ospf_ctx {
@@ -106,16 +107,21 @@ namespace ospf_int {
 
 // fn(lo, hi) over [0, n) on up to 16 host threads, chunks of `grain` taken
 // dynamically (a fabric's spines, first by name, have 20x the rows of the
-// rest: static slices left one thread with most of the work); serial when
-// threads are unavailable
+// rest: static slices left one thread with most of the work, and so did
+// 512-node chunks -- the 288 spines' 513 k entries in one); serial when
+// threads are unavailable. Chunks start at multiples of `grain` (64: whole
+// words of per-node bitmaps).
 template <class F>
-void par_for(uint32_t n, F fn, uint32_t grain = 512) {
+void par_for(uint32_t n, F fn, uint32_t grain = 64) {
   const uint32_t hw = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
   const uint32_t T = std::min(hw, (n + grain - 1) / grain);
   if (T <= 1) {
     fn(0u, n);
     return;
   }
+  // the persistent pool (host_pool.h); threads of its own when it is busy
+  if (host_pool::Pool::get().run(n, grain, T, [&](uint32_t lo, uint32_t hi) { fn(lo, hi); }))
+    return;
   std::atomic<uint32_t> next{0};
   auto work = [&]() {
     for (;;) {

@@ -163,11 +163,14 @@ std::vector<uint32_t> partition(const Facts& f, uint32_t parts, uint32_t p) {
 // independent set of the candidates under that priority (what Luby rounds
 // with a fixed priority also produce). Links of any state count.
 std::vector<uint8_t> leaf_set(const Facts& f, uint32_t max_nbrs = 32) {
-  std::vector<uint32_t> cand;
+  // candidates in (distinct neighbours, id) order: a counting sort
+  std::vector<uint32_t> cnt(max_nbrs + 2, 0u);
   for (uint32_t v = 0; v < f.V; ++v)
-    if (f.nbrs(v) <= max_nbrs) cand.push_back(v);
-  std::stable_sort(cand.begin(), cand.end(),
-                   [&](uint32_t a, uint32_t b) { return f.nbrs(a) < f.nbrs(b); });
+    if (f.nbrs(v) <= max_nbrs) ++cnt[f.nbrs(v) + 1];
+  for (uint32_t k = 1; k < cnt.size(); ++k) cnt[k] += cnt[k - 1];
+  std::vector<uint32_t> cand(cnt.back());
+  for (uint32_t v = 0; v < f.V; ++v)
+    if (f.nbrs(v) <= max_nbrs) cand[cnt[f.nbrs(v)]++] = v;
   std::vector<uint8_t> leaf(f.V, 0), blocked(f.V, 0);
   for (uint32_t v : cand) {
     if (blocked[v]) continue;
@@ -837,7 +840,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
         std::copy(b.begin(), b.begin() + m, ccls.begin() + (size_t)r * kCS);
         ccnt[r] = m;
       }
-    }, 512);
+    }, 64);
   }
   std::vector<uint32_t> cs;
   auto classes_of = [&](uint32_t r) {
