@@ -547,10 +547,20 @@ int ospf_links_unmask(ospf_ctx* ctx);
  * once per graph version (odl::LinkState; ospf_msweep_create, which starts
  * every device's first run together) pays one run instead of two. */
 #define OSPF_SWEEP_DEFER 0x100u
+/* opts.flags, with OSPF_SWEEP_DEFER: the first run starts inside
+ * ospf_sweep_create -- each launch unit of the plan's serial prefix (derive
+ * mode: the seed BFS and the twin levels) is queued as soon as it is planned,
+ * ordered after the null stream's prior work, so the device works on it while
+ * the host plans the rest; the first ospf_sweep_run queues the remaining
+ * units and joins the caller's stream. For a caller that runs the sweep right
+ * after creating it on an unchanged graph (odl::LinkState's re-sweep after a
+ * topology change). */
+#define OSPF_SWEEP_EARLY_START 0x200u
 
 typedef struct ospf_sweep ospf_sweep;
 typedef struct ospf_sweep_opts {
-  uint32_t flags;      /* 0 (link metrics) or OSPF_HOP_COUNT, | OSPF_SWEEP_DEFER */
+  uint32_t flags;      /* 0 (link metrics) or OSPF_HOP_COUNT, | OSPF_SWEEP_DEFER
+                          (| OSPF_SWEEP_EARLY_START) */
   uint32_t mode;       /* OSPF_SWEEP_* */
   uint32_t part;       /* this part of the root partition ... */
   uint32_t n_parts;    /* ... over n_parts (0 or 1: every node) */

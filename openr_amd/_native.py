@@ -24,6 +24,7 @@ OSPF_WANT_DIST = 0x2
 OSPF_WANT_NH = 0x4
 OSPF_WANT_DIGEST = 0x8
 OSPF_SWEEP_DEFER = 0x100
+OSPF_SWEEP_EARLY_START = 0x200
 
 ENGINE_SYMBOLS = [
     "ospf_open", "ospf_close", "ospf_last_error", "ospf_load_graph", "ospf_graph_info_get",

@@ -1008,6 +1008,8 @@ void LinkState::prefetchAllSourcesImpl(bool useLinkMetric) {
     ospf_sweep_get_info(ospf_msweep_part(msweep_, 0), &info);
     sweepStats_.devices = ospf_multi_size(multi_);
   } else {
+    // the serial prefix of the run starts while the plan is still built
+    o.flags |= OSPF_SWEEP_EARLY_START;
     rc = ospf_sweep_create(engine_, &o, &sweep_);
     bool runErr = false;  // ospf_sweep_run reports through the sweep's own error
     if (rc == OSPF_OK) runErr = (rc = ospf_sweep_run(sweep_, nullptr)) != OSPF_OK;

@@ -80,13 +80,13 @@ void parallelFor(uint32_t n, F&& f, uint32_t chunk = 64) {
   if (err) std::rethrow_exception(err);
 }
 
-// std::sort of v on up to 8 host threads: sorted slices merged pairwise
+// std::sort of v on up to 16 host threads: sorted slices merged pairwise
 template <class T>
 void parallelSort(std::vector<T>& v) {
   const size_t n = v.size();
   uint32_t C = 1;
-  const uint32_t hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
-  while (C * 2 <= hw && n / (C * 2) >= 8192) C *= 2;
+  const uint32_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  while (C * 2 <= hw && n / (C * 2) >= 4096) C *= 2;
   if (C == 1) {
     std::sort(v.begin(), v.end());
     return;

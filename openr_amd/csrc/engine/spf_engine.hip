@@ -1619,11 +1619,22 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   auto reserve = [](size_t used) { return used + std::max<size_t>(1024, used / 32); };
   const size_t cap_e = align_up(reserve(Ep), 4), cap_dn = reserve(dn.size()),
                cap_lid = n_lid ? reserve(n_lid) : 0;
+  // [2 lid] = the link's first entry, [2 lid + 1] = its second (none: ~0):
+  // the smallest and largest entry of each id, on host threads
   std::vector<uint32_t> link_e(std::max<size_t>(2ull * n_lid, 2), 0xFFFFFFFFu);
-  for (uint32_t e = 0; e < Ep && n_lid; ++e) {
-    if (plink[e] == 0xFFFFFFFFu) continue;
-    uint32_t* le = &link_e[2ull * plink[e]];
-    if (le[0] == 0xFFFFFFFFu) le[0] = e; else le[1] = e;
+  if (n_lid) {
+    for (size_t l = 0; l < n_lid; ++l) link_e[2 * l + 1] = 0u;
+    ospf_int::par_for(Ep, [&](uint32_t lo, uint32_t hi) {
+      for (uint32_t e = lo; e < hi; ++e) {
+        if (plink[e] == 0xFFFFFFFFu) continue;
+        uint32_t* le = &link_e[2ull * plink[e]];
+        __atomic_fetch_min(le, e, __ATOMIC_RELAXED);
+        __atomic_fetch_max(le + 1, e, __ATOMIC_RELAXED);
+      }
+    }, 1u << 14);
+    for (size_t l = 0; l < n_lid; ++l)
+      if (link_e[2 * l + 1] == link_e[2 * l] || link_e[2 * l] == 0xFFFFFFFFu)
+        link_e[2 * l + 1] = 0xFFFFFFFFu;  // one entry (or none)
   }
 
   // device layout: one allocation, 256-B aligned sub-buffers

@@ -223,6 +223,10 @@ struct ospf_sweep {
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
   bool ran = false;
+  // OSPF_SWEEP_EARLY_START: units [0, started) of the first run already
+  // queued by the plan (after ev_in on the null stream and events[0])
+  bool early = false, early_on = false;
+  size_t started = 0;
 };
 
 namespace {
@@ -232,6 +236,8 @@ int sfail(ospf_sweep* s, int code, const std::string& m) {
   if (s->c) s->c->err = m;
   return code;
 }
+
+int start_early(ospf_sweep* s);  // (below: OSPF_SWEEP_EARLY_START)
 
 #define SCHK(sw, call)                                                               \
   do {                                                                               \
@@ -1139,6 +1145,8 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   const int ev_cov = nd ? ev_t : ev_a;
   // (C) cover classes: digest slots 0 .. |own_c|
   uint32_t slot = 0;
+  // OSPF_SWEEP_EARLY_START: the serial prefix starts now, the host plans on
+  if ((rc = start_early(s))) return rc;
   lap("twin levels units");
   std::vector<ospf_sweep::Unit> side, after;
   for (size_t i = 0; i < cls.size(); ++i) {
@@ -2537,16 +2545,44 @@ int plan_wderive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& min
 
 // queue one run's launches; the run starts when `origin` (the main stream)
 // reaches this point and ends when main has waited for every other stream
+// one unit of a run on its stream: its waits, the launch, its event
+int launch_unit(ospf_sweep* s, ospf_sweep::Unit& u) {
+  hipStream_t st = s->streams[u.stream];
+  for (int e : u.wait)
+    if (!(e == 0 && u.stream == 0)) SCHK(s, hipStreamWaitEvent(st, s->events[e], 0));
+  const int rc = u.fn(st);
+  if (rc != OSPF_OK) return sfail(s, rc, std::string(u.name) + ": " + ospf_last_error(s->c));
+  if (u.record >= 0) SCHK(s, hipEventRecord(s->events[u.record], st));
+  return OSPF_OK;
+}
+
+// OSPF_SWEEP_EARLY_START: queue the units planned so far (the first run's
+// start: after the null stream's prior work, as run_eager orders it)
+int start_early(ospf_sweep* s) {
+  if (!s->early) return OSPF_OK;
+  if (!s->early_on) {
+    SCHK(s, hipEventRecord(s->ev_in, nullptr));
+    SCHK(s, hipStreamWaitEvent(s->streams[0], s->ev_in, 0));
+    SCHK(s, hipEventRecord(s->events[0], s->streams[0]));
+    s->early_on = true;
+  }
+  for (; s->started < s->units.size(); ++s->started) {
+    const int rc = launch_unit(s, s->units[s->started]);
+    if (rc) return rc;
+  }
+  return OSPF_OK;
+}
+
 int enqueue(ospf_sweep* s) {
   hipStream_t main = s->streams[0];
-  SCHK(s, hipEventRecord(s->events[0], main));
-  for (auto& u : s->units) {
-    hipStream_t st = s->streams[u.stream];
-    for (int e : u.wait)
-      if (!(e == 0 && u.stream == 0)) SCHK(s, hipStreamWaitEvent(st, s->events[e], 0));
-    const int rc = u.fn(st);
-    if (rc != OSPF_OK) return sfail(s, rc, std::string(u.name) + ": " + ospf_last_error(s->c));
-    if (u.record >= 0) SCHK(s, hipEventRecord(s->events[u.record], st));
+  // (units an early start queued are skipped, once)
+  const size_t first = s->early_on ? s->started : 0;
+  if (!s->early_on) SCHK(s, hipEventRecord(s->events[0], main));
+  s->early_on = false;
+  s->started = 0;
+  for (size_t i = first; i < s->units.size(); ++i) {
+    const int rc = launch_unit(s, s->units[i]);
+    if (rc) return rc;
   }
   for (size_t i = 1; i < s->streams.size(); ++i) {
     SCHK(s, hipEventRecord(s->ev_done[i], s->streams[i]));
@@ -2556,8 +2592,10 @@ int enqueue(ospf_sweep* s) {
 }
 
 int run_eager(ospf_sweep* s, hipStream_t caller) {
-  SCHK(s, hipEventRecord(s->ev_in, caller));
-  SCHK(s, hipStreamWaitEvent(s->streams[0], s->ev_in, 0));
+  if (!s->early_on) {  // (an early start ordered it after the null stream)
+    SCHK(s, hipEventRecord(s->ev_in, caller));
+    SCHK(s, hipStreamWaitEvent(s->streams[0], s->ev_in, 0));
+  }
   const int rc = enqueue(s);
   if (rc) return rc;
   SCHK(s, hipEventRecord(s->ev_out, s->streams[0]));
@@ -2621,9 +2659,12 @@ int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
   const uint32_t parts = std::max(1u, o->n_parts);
   if (o->part >= parts) return fail(c, OSPF_E_INVAL, "sweep: part >= n_parts");
   if (o->mode > OSPF_SWEEP_WMULTI) return fail(c, OSPF_E_INVAL, "sweep: unknown mode");
-  if (o->flags & ~(OSPF_HOP_COUNT | OSPF_SWEEP_DEFER))
-    return fail(c, OSPF_E_INVAL, "sweep: flags = 0 or OSPF_HOP_COUNT, | OSPF_SWEEP_DEFER");
+  if (o->flags & ~(OSPF_HOP_COUNT | OSPF_SWEEP_DEFER | OSPF_SWEEP_EARLY_START))
+    return fail(c, OSPF_E_INVAL,
+                "sweep: flags = 0 or OSPF_HOP_COUNT, | OSPF_SWEEP_DEFER (| OSPF_SWEEP_EARLY_START)");
   const bool defer = (o->flags & OSPF_SWEEP_DEFER) != 0;
+  if ((o->flags & OSPF_SWEEP_EARLY_START) && !defer)
+    return fail(c, OSPF_E_INVAL, "sweep: OSPF_SWEEP_EARLY_START needs OSPF_SWEEP_DEFER");
   if (defer && o->hip_graph)
     return fail(c, OSPF_E_INVAL, "sweep: OSPF_SWEEP_DEFER needs hip_graph = 0 (the capture "
                                  "follows the first run)");
@@ -2639,6 +2680,7 @@ int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
     x->c = nullptr;
   };
   s->opts = *o;
+  s->early = (o->flags & OSPF_SWEEP_EARLY_START) && !getenv("OSPF_SWEEP_NO_EARLY");
   s->gen = c->graph_gen;
   s->V = c->info.n_nodes;
   const uint32_t V = s->V;

@@ -315,7 +315,7 @@ class Sweep:
 
     def __init__(self, engine: "Engine", *, hop_count: bool = False, mode: str = "auto",
                  part: int = 0, n_parts: int = 1, hip_graph: bool = True, defer: bool = False,
-                 _handle=None):
+                 early_start: bool = False, _handle=None):
         self._L = N.engine()
         self.engine = engine
         if _handle is not None:  # a part of an ospf_msweep (owned by it)
@@ -323,8 +323,12 @@ class Sweep:
         else:
             # defer: no eager run at create (hip_graph must be off): the
             # first run() is the first run (OSPF_SWEEP_DEFER)
+            # early_start (with defer): the first run's serial prefix is
+            # queued while the plan is built (OSPF_SWEEP_EARLY_START)
             o = N.ospf_sweep_opts((N.OSPF_HOP_COUNT if hop_count else 0) |
-                                  (N.OSPF_SWEEP_DEFER if defer else 0), N.SWEEP_MODES[mode],
+                                  (N.OSPF_SWEEP_DEFER if defer else 0) |
+                                  (N.OSPF_SWEEP_EARLY_START if early_start else 0),
+                                  N.SWEEP_MODES[mode],
                                   part, n_parts, int(hip_graph and not defer))
             h = C.c_void_p()
             rc = self._L.ospf_sweep_create(engine._h, C.byref(o), C.byref(h))

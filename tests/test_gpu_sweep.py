@@ -123,6 +123,33 @@ def test_sweep_fabric_with_drains_vs_oracle():
         eng.close()
 
 
+@pytest.mark.parametrize("hop", [False, True])
+def test_sweep_early_start_equals_eager(hop):
+    """OSPF_SWEEP_EARLY_START (the first run's serial prefix queued while the
+    plan is built, odl::LinkState's re-sweep): digests and rows == a sweep
+    created and run the plain way, on a drained fabric in derive mode."""
+    st = drained_fabric(24, 4, seed=9)
+    ls, csr, eng = engine_for(st)
+    try:
+        base = Sweep(eng, mode="derive", hop_count=hop)
+        base.run()
+        want = sweep_digests(base)
+        base.close()
+        def same(got):
+            return sorted(got) == sorted(want) and all(np.array_equal(got[r], want[r]) for r in want)
+
+        for _ in range(2):  # (the second: pooled blocks, streams and events)
+            sw = Sweep(eng, mode="derive", hop_count=hop, hip_graph=False, defer=True,
+                       early_start=True)
+            sw.run()
+            assert same(sweep_digests(sw))
+            sw.run()  # a later run of the same sweep: the plain eager path
+            assert same(sweep_digests(sw))
+            sw.close()
+    finally:
+        eng.close()
+
+
 def test_sweep_weighted_fabric_cover_path():
     st = T.fabric(pods=8, planes=4, weighted_seed=7)
     ls, csr, eng = engine_for(st)
