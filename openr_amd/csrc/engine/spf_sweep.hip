@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <memory>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -104,6 +105,21 @@ void par_stable_sort(std::vector<T>& v, Less less) {
     v.swap(tmp);
   }
 }
+
+// OSPF_SWEEP_TIMING: sub-phases of a plan phase on stderr
+struct SubLaps {
+  const char* phase;
+  bool on = getenv("OSPF_SWEEP_TIMING") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  explicit SubLaps(const char* p) : phase(p) {}
+  void operator()(const char* what) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    fprintf(stderr, "sweep_create plan/%s/%s %.2f ms\n", phase, what,
+            std::chrono::duration<double, std::milli>(n - t).count());
+    t = n;
+  }
+};
 
 // stable order of `v` by key(v)
 template <class K>
@@ -361,6 +377,7 @@ uint32_t usable_slots(const ospf_ctx* c, uint32_t r) {
 // neighbours + usable links: the racks of a pod) are adjacent, cut into
 // groups of <= kLeafMaxG; returns the group offsets.
 std::vector<uint32_t> leaf_groups(const ospf_ctx* c, const Facts& f, std::vector<uint32_t>& roots) {
+  SubLaps lap("leaf groups");
   std::vector<uint32_t> use(roots.size());
   par_for((uint32_t)roots.size(), [&](uint32_t lo, uint32_t hi) {
     for (uint32_t i = lo; i < hi; ++i) use[i] = usable_slots(c, roots[i]);
@@ -384,6 +401,7 @@ std::vector<uint32_t> leaf_groups(const ospf_ctx* c, const Facts& f, std::vector
     if (cmp) return cmp < 0;
     return use[x] < use[y];
   });
+  lap("sort");
   std::vector<uint32_t> out(roots.size()), uo(roots.size());
   for (size_t i = 0; i < ord.size(); ++i) {
     out[i] = roots[ord[i]];
@@ -407,8 +425,9 @@ struct Twins {
   std::vector<uint32_t> cls, rep, sec;
 };
 Twins twin_classes(const ospf_ctx* c) {
+  SubLaps lap("twin classes");
   const uint32_t V = c->info.n_nodes;
-  std::vector<uint32_t> off(V + 1, 0), lst;
+  std::vector<uint32_t> off(V + 1, 0);
   std::vector<uint64_t> key(V);
   // each node's usable distinct neighbours (sorted, unique): counted, then
   // written and hashed, both on host threads
@@ -434,10 +453,13 @@ Twins twin_classes(const ospf_ctx* c) {
     for (uint32_t u = lo; u < hi; ++u) cnt[u] = nbrs_of(u, nullptr);
   });
   for (uint32_t u = 0; u < V; ++u) off[u + 1] = off[u] + cnt[u];
-  lst.resize(off[V]);
+  // (uninitialized: every slot is written below; a zero fill of ~10 MB of
+  // fresh pages cost more than the pass)
+  std::unique_ptr<uint32_t[]> lst_buf(new uint32_t[std::max<uint32_t>(off[V], 1)]);
+  uint32_t* const lst = lst_buf.get();
   par_for(V, [&](uint32_t lo, uint32_t hi) {
     for (uint32_t u = lo; u < hi; ++u) {
-      const uint32_t m = nbrs_of(u, lst.data() + off[u]);
+      const uint32_t m = nbrs_of(u, lst + off[u]);
       for (uint32_t i = m; i < cnt[u]; ++i) lst[off[u] + i] = 0xFFFFFFFFu;  // (dups of an unsorted row)
       cnt[u] = m;
       const bool tr = !((c->h_nt[u >> 5] >> (u & 31)) & 1u);
@@ -448,10 +470,11 @@ Twins twin_classes(const ospf_ctx* c) {
       key[u] = h;
     }
   });
+  lap("lists + keys");
   auto same = [&](uint32_t a, uint32_t b) {
     const bool ta = !((c->h_nt[a >> 5] >> (a & 31)) & 1u), tb = !((c->h_nt[b >> 5] >> (b & 31)) & 1u);
     return ta == tb && cnt[a] == cnt[b] &&
-           std::equal(lst.begin() + off[a], lst.begin() + off[a] + cnt[a], lst.begin() + off[b]);
+           std::equal(lst + off[a], lst + off[a] + cnt[a], lst + off[b]);
   };
   // nodes by (key, id): the stable order by key
   std::vector<std::pair<uint64_t, uint32_t>> kv(V);
@@ -461,6 +484,7 @@ Twins twin_classes(const ospf_ctx* c) {
   });
   std::vector<uint32_t> ord(V);
   for (uint32_t u = 0; u < V; ++u) ord[u] = kv[u].second;
+  lap("key sort");
   Twins t;
   t.cls.assign(V, kNone);
   for (size_t i = 0; i < V;) {
@@ -482,6 +506,7 @@ Twins twin_classes(const ospf_ctx* c) {
     }
     i = j;
   }
+  lap("classes");
   // representative = smallest member, second = the next one
   for (uint32_t u = 0; u < V; ++u) {
     const uint32_t id = t.cls[u];
@@ -794,6 +819,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   std::vector<uint32_t> extra_l;
   for (uint32_t v : nb_c)
     if (leaf[v] && !in_l[v]) extra_l.push_back(v);
+  lap("closure");
   // cover classes by capacity, roots by largest neighbour
   std::vector<uint32_t> caps;
   for (uint32_t r : own_c) caps.push_back(f.cap(r));
@@ -818,7 +844,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   // twin classes: a class of <= 4-word roots whose usable transit
   // neighbours span few classes reads one row per class (spf_twin.hip), and
   // so can a cover row (twin levels)
-  lap("closure + width classes");
+  lap("width classes");
   Twins tw;
   if (!getenv("OSPF_SWEEP_NOTWIN")) tw = twin_classes(c);
   lap("twin classes");
