@@ -29,3 +29,9 @@ print({k: (v[0], round(v[1], 2)) for k, v in agg.items()})
 for r in seg:
     if r["k"] in ("ksp_trace_kernel", "ksp_heavy_kernel", "msbfs_init_kernel"):
         print(f'{r["k"]:20s} {(r["s"] - t0) / 1e6:8.2f} {(r["e"] - t0) / 1e6:8.2f} grid {r["Grid_Size_X"]}')
+# every kernel of the call: start / end / duration (ms from the call's start), queue
+print("all kernels:")
+for r in seg:
+    q = r.get("Queue_Id") or r.get("Stream_Id") or "?"
+    print(f'{(r["s"] - t0) / 1e6:8.3f} {(r["e"] - t0) / 1e6:8.3f} {(r["e"] - r["s"]) / 1e6:7.3f} q{q} {r["k"]}')
+print("end", round((max(r["e"] for r in seg) - t0) / 1e6, 3))
