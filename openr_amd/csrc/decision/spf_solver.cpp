@@ -3,6 +3,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <limits>
 #include <set>
 #include <stdexcept>
@@ -239,8 +241,17 @@ std::vector<NextHop> SpfSolver::ksp2Paths(size_t ai, const std::string& me,
 
 std::optional<UnicastRoute> SpfSolver::prefixRoute(const std::string& me, const PrefixRoute& pr,
                                                    const RouteOptions& opt) {
+  const bool tm = getenv("ODL_ROUTE_TIMING") != nullptr;
+  auto tl = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (!tm) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "route_build %s %.2f ms\n", what, std::chrono::duration<double, std::milli>(t - tl).count());
+    tl = t;
+  };
   std::vector<const SpfResult*> mines;
   for (auto& a : areas_) mines.push_back(&a.second->getSpfResult(me));
+  lap("spf results");
   return prefixRoute(me, pr, opt, mines);
 }
 
@@ -459,8 +470,17 @@ std::optional<RouteDb> SpfSolver::buildRouteDb(const std::string& me,
   // entry runs getKthPaths, which fills a memo, so those are built on this
   // thread. The results are looked up (and memoised) here, on the calling
   // thread; the host threads below only read them
+  const bool tm = getenv("ODL_ROUTE_TIMING") != nullptr;
+  auto tl = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (!tm) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "route_build %s %.2f ms\n", what, std::chrono::duration<double, std::milli>(t - tl).count());
+    tl = t;
+  };
   std::vector<const SpfResult*> mines;
   for (auto& a : areas_) mines.push_back(&a.second->getSpfResult(me));
+  lap("spf results");
   std::vector<std::optional<UnicastRoute>> routes(prefixes.size());
   std::vector<uint32_t> sp, ksp;
   for (uint32_t i = 0; i < prefixes.size(); ++i) {
@@ -472,11 +492,27 @@ std::optional<RouteDb> SpfSolver::buildRouteDb(const std::string& me,
     for (uint32_t j = lo; j < hi; ++j) routes[sp[j]] = prefixRoute(me, prefixes[sp[j]], opt, mines);
   }, 256);
   for (const uint32_t i : ksp) routes[i] = prefixRoute(me, prefixes[i], opt, mines);
-  for (uint32_t i = 0; i < prefixes.size(); ++i) {
-    if (!routes[i]) continue;
-    if (!db.unicast.emplace(prefixes[i].prefix, std::move(*routes[i])).second)
+  lap("prefix routes");
+  // into the ordered map in key order: each insert at the end (a hint), not
+  // a tree search per prefix
+  std::vector<uint32_t> byKey;
+  byKey.reserve(prefixes.size());
+  for (uint32_t i = 0; i < prefixes.size(); ++i)
+    if (routes[i]) byKey.push_back(i);
+  bool ascending = true;
+  for (size_t j = 1; j < byKey.size() && ascending; ++j)
+    ascending = prefixes[byKey[j - 1]].prefix < prefixes[byKey[j]].prefix;
+  if (!ascending)
+    std::stable_sort(byKey.begin(), byKey.end(), [&](uint32_t a, uint32_t b) {
+      return prefixes[a].prefix < prefixes[b].prefix;
+    });
+  for (size_t j = 0; j < byKey.size(); ++j) {
+    const uint32_t i = byKey[j];
+    if (j && prefixes[byKey[j - 1]].prefix == prefixes[i].prefix)
       throw std::invalid_argument("duplicate prefix " + prefixes[i].prefix);
+    db.unicast.emplace_hint(db.unicast.end(), prefixes[i].prefix, std::move(*routes[i]));
   }
+  lap("unicast map");
   // node-label routes (:501-598), every area's databases in area order: on a
   // label collision the smallest node name keeps it (the reference's
   // `iter->second.first < nodeName` rule, in any order; the same node in two
@@ -490,37 +526,65 @@ std::optional<RouteDb> SpfSolver::buildRouteDb(const std::string& me,
       std::vector<std::string> names;
       names.reserve(dbs.size());
       for (const auto& kv : dbs) names.push_back(kv.first);
-      std::sort(names.begin(), names.end());
+      parallelSort(names);
+      std::vector<int32_t> tops(names.size());
+      parallelFor((uint32_t)names.size(), [&](uint32_t lo, uint32_t hi) {
+        for (uint32_t j = lo; j < hi; ++j) tops[j] = dbs.at(names[j]).nodeLabel;
+      }, 1024);
+      lap("labels: names");
       // candidate routes of every labelled node, on host threads
       std::vector<std::vector<NextHop>> cand(names.size());
       parallelFor((uint32_t)names.size(), [&](uint32_t lo, uint32_t hi) {
         for (uint32_t j = lo; j < hi; ++j) {
-          const int32_t top = dbs.at(names[j]).nodeLabel;
+          const int32_t top = tops[j];
           if (top == 0 || !isMplsLabelValid(top) || names[j] == me) continue;
           auto m = nextHopsWithMetric(*mines[ai], {names[j]}, false);
           if (!m.viaNode.empty())
             cand[j] = nextHopsThrift(ai, me, {{names[j], areas_[ai].first}}, false, m, top, {}, nullptr);
         }
       }, 256);
+      lap("labels: candidates");
+      // the area's labelled nodes that can take their label (a route, or me)
+      // by (label, name): the smallest name of each label first
+      std::vector<std::pair<int32_t, uint32_t>> lab;
+      lab.reserve(names.size());
       for (size_t j = 0; j < names.size(); ++j) {
-        const std::string& node = names[j];
-        const int32_t top = dbs.at(node).nodeLabel;
+        const int32_t top = tops[j];
         if (top == 0 || !isMplsLabelValid(top)) continue;
-        auto it = labelToNode.find(top);
-        if (it != labelToNode.end() && it->second.first < node) continue;
+        if (names[j] != me && cand[j].empty()) continue;  // unreachable: takes nothing over
+        lab.emplace_back(top, (uint32_t)j);
+      }
+      std::sort(lab.begin(), lab.end());
+      for (size_t q = 0; q < lab.size(); ++q) {
+        if (q && lab[q - 1].first == lab[q].first) continue;  // a larger name of this label
+        const int32_t top = lab[q].first;
+        const std::string& node = names[lab[q].second];
+        auto it = labelToNode.lower_bound(top);
+        const bool have = it != labelToNode.end() && it->first == top;
+        // an earlier area's holder keeps it when its name is smaller (the same
+        // node in two areas: the later area)
+        if (have && it->second.first < node) continue;
+        std::vector<NextHop> nhs;
         if (node == me) {
           NextHop pop;
           pop.op = MplsOp::kPopAndLookup;
           pop.area = areas_[ai].first;
-          labelToNode[top] = {me, {pop}};
+          nhs.push_back(std::move(pop));
+        } else {
+          nhs = std::move(cand[lab[q].second]);
+        }
+        if (areas_.size() == 1) {  // one area: no holder to compare with later
+          db.mpls.emplace_hint(db.mpls.end(), top, std::move(nhs));
           continue;
         }
-        if (cand[j].empty()) continue;
-        labelToNode[top] = {node, std::move(cand[j])};
+        if (have) it->second = {node, std::move(nhs)};
+        else labelToNode.emplace_hint(it, top, std::make_pair(node, std::move(nhs)));
       }
     }
-    for (auto& kv : labelToNode) db.mpls.emplace(kv.first, std::move(kv.second.second));
+    lap("labels: collisions");
+    for (auto& kv : labelToNode) db.mpls.emplace_hint(db.mpls.end(), kv.first, std::move(kv.second.second));
   }
+  lap("node labels");
   // adjacency-label routes (:603-631): PHP over each of our links (up or
   // not), every area
   if (opt.adjacencyLabels) {
