@@ -480,6 +480,7 @@ std::vector<LinkStateChange> LinkState::updateAdjacencyDatabases(std::vector<Adj
     for (uint32_t i = 0; i < n; ++i) out[i] = updateAdjacencyDatabase(dbs[i], holdUpTtl, holdDownTtl);
     return out;
   }
+
   using Clock = std::chrono::steady_clock;
   const bool timing = getenv("ODL_SPF_TIMING") != nullptr;
   Clock::time_point tp[6];
@@ -586,7 +587,10 @@ std::vector<LinkStateChange> LinkState::updateAdjacencyDatabases(std::vector<Adj
   // one version step per database, as in turn (a new node is structural)
   version_ += n - (anyTopo ? 1u : 0u);
   if (anyTopo) invalidate();
-  startOpen();
+  // (after the ingest, not beside it: the HIP runtime's start beside the
+  // ingest's page-fault-heavy host work slowed the ingest by ~150-290 ms
+  // at F100k, more than it saved the first getSpfResult, c9 vs c5)
+  startOpen(adjDbs_.size());
   return out;
 }
 
@@ -868,31 +872,36 @@ void LinkState::prefetchKsp2(const std::string& src, const std::vector<std::stri
   guarded([&] { prefetchKsp2Impl(src, dsts); });
 }
 
-void LinkState::startOpen() {
+void LinkState::startOpen(size_t nodes) {
   if (hostOnly_ || engine_ || opener_.joinable() || devices_.size() != 1 ||
       getenv("ODL_NO_PREOPEN"))
     return;
+  // the warm-up: one link, one root (a warm-up graph as large as the
+  // ingested one -- a hypercube, to size the batch path's buffers too -- cost
+  // more on the first getSpfResult's path than the ~14 ms it saved there)
+  (void)nodes;
+  constexpr uint32_t V = 2;
   try {
     opener_ = std::thread([this, dev = device_] {
       ospf_ctx* c = nullptr;
       if (ospf_open(dev, &c) != OSPF_OK) return;
-      // one link, one root: the batch path's kernels loaded and run once
-      const uint32_t rp[3] = {0, 1, 2}, col[2] = {1, 0}, one[2] = {1, 1}, lid[2] = {0, 0},
-                     twin[2] = {1, 0};
-      const uint8_t up[2] = {1, 1};
+      const std::vector<uint32_t> rp{0, 1, 2}, col{1, 0}, one{1, 1}, lid{0, 0}, twin{1, 0};
+      const std::vector<uint8_t> up{1, 1};
+      const uint32_t E = 2;
       ospf_csr g{};
-      g.n_nodes = 2;
-      g.n_edges = 2;
-      g.row_ptr = rp;
-      g.col = col;
-      g.metric = one;
-      g.link_id = lid;
-      g.twin = twin;
-      g.edge_up = up;
-      uint32_t root = 0, dist[2], nh[2];
+      g.n_nodes = V;
+      g.n_edges = E;
+      g.row_ptr = rp.data();
+      g.col = col.data();
+      g.metric = one.data();
+      g.link_id = lid.data();
+      g.twin = twin.data();
+      g.edge_up = up.data();
+      uint32_t root = 0;
+      std::vector<uint32_t> dist(V), nh(V);
       if (ospf_load_graph(c, &g, 0) != OSPF_OK ||
-          ospf_sssp_batch(c, &root, 1, nullptr, OSPF_WANT_DIST | OSPF_WANT_NH, 1, dist, nh,
-                          nullptr) != OSPF_OK) {
+          ospf_sssp_batch(c, &root, 1, nullptr, OSPF_WANT_DIST | OSPF_WANT_NH, 1, dist.data(),
+                          nh.data(), nullptr) != OSPF_OK) {
         ospf_close(c);
         return;
       }

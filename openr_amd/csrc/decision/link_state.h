@@ -782,13 +782,13 @@ class LinkState {
   // frees dropped memos on one background thread (clearMemo); joined by the
   // destructor
   std::unique_ptr<struct MemoReaper> reaper_;
-  // the engine opened on a host thread while a bulk ingest's caller goes on
-  // (Decision opens its device at start; here the first bulk ingest does):
+  // the engine opened on a host thread beside a bulk ingest (Decision opens
+  // its device at start; here the first bulk ingest does):
   // the HIP runtime's start and the kernels' code objects are loaded by a
   // tiny warm-up run, off the first getSpfResult's path. ensureEngine joins.
   std::thread opener_;
   ospf_ctx* openerCtx_ = nullptr;
-  void startOpen();
+  void startOpen(size_t nodes);  // nodes: the warm-up graph's size
   void joinOpen();
 };
 
