@@ -27,6 +27,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "spf_kernels.h"
 
@@ -57,7 +58,7 @@ __device__ __forceinline__ uint32_t beq7(uint32_t x, uint32_t y) {
   return ~((x ^ y) + 0x7F7F7F7Fu) & 0x80808080u;
 }
 
-template <int KM>
+template <int KM, int PD>
 __global__ void __launch_bounds__(kBlock) leaf_derive_kernel(DevGraph g, LeafArgs a) {
   __shared__ uint32_t s_root[kLeafMaxG], s_own[kLeafMaxG], s_use[kLeafMaxG], s_lrow[kLeafMaxG];
   __shared__ uint32_t s_rb[kLeafMaxG], s_re[kLeafMaxG];
@@ -141,8 +142,8 @@ __global__ void __launch_bounds__(kBlock) leaf_derive_kernel(DevGraph g, LeafArg
   uint32_t br = 0;
   uint64_t bs = 0, bh = 0;
   const uint32_t t0 = ci * a.ctiles, t1 = min(a.tiles, t0 + a.ctiles);
-  // the neighbour words of the next tile are loaded before this tile's
-  // stores are issued (one tile of loads in flight per wave)
+  // the neighbour words of the next PD tiles are loaded before this tile's
+  // stores are issued (PD tiles of loads in flight per wave)
   auto load_x = [&](uint32_t t, uint32_t* x) {
     const uint32_t v0 = t * 1024u + wave * 256u + 4u * lane;
     const bool ok = t < t1 && v0 < a.pitch;
@@ -153,14 +154,19 @@ __global__ void __launch_bounds__(kBlock) leaf_derive_kernel(DevGraph g, LeafArg
                   : kNoRow;
     }
   };
-  uint32_t xn[KM];
-  load_x(t0, xn);
+  uint32_t xn[PD][KM];
+#pragma unroll
+  for (int d = 0; d < PD; ++d) load_x(t0 + d, xn[d]);
   for (uint32_t t = t0; t < t1; ++t) {
     const uint32_t v0 = t * 1024u + wave * 256u + 4u * lane;
     uint32_t x[KM];
 #pragma unroll
-    for (int k = 0; k < KM; ++k) x[k] = xn[k];
-    load_x(t + 1, xn);
+    for (int k = 0; k < KM; ++k) x[k] = xn[0][k];
+#pragma unroll
+    for (int d = 0; d + 1 < PD; ++d)
+#pragma unroll
+      for (int k = 0; k < KM; ++k) xn[d][k] = xn[d + 1][k];
+    load_x(t + PD, xn[PD - 1]);
     if (v0 >= a.pitch) continue;
     uint32_t m = kNoRow;
 #pragma unroll
@@ -287,12 +293,19 @@ hipError_t launch_leaf_derive(const DevGraph& g, const LeafArgs& a0, uint32_t km
   const uint32_t chunks = (a.tiles + a.ctiles - 1) / a.ctiles;
   a.chunks = chunks;
   const dim3 grid(a.ngroups * chunks);
-  if (kmax <= 8)
-    hipLaunchKernelGGL(leaf_derive_kernel<8>, grid, dim3(kBlock), 0, s, g, a);
-  else if (kmax <= 16)
-    hipLaunchKernelGGL(leaf_derive_kernel<16>, grid, dim3(kBlock), 0, s, g, a);
-  else
-    hipLaunchKernelGGL(leaf_derive_kernel<32>, grid, dim3(kBlock), 0, s, g, a);
+  // two tiles of neighbour loads in flight (OSPF_LEAF_PD=1: one; read per
+  // launch for in-process A/B: 19.61 vs 19.71 ms per F100k sweep,
+  // profiles/r06/i1_leaf_prefetch_ab.txt)
+  const char* pe = getenv("OSPF_LEAF_PD");
+  const bool pd2 = !pe || atoi(pe) >= 2;
+  if (kmax <= 8) {
+    if (pd2) hipLaunchKernelGGL((leaf_derive_kernel<8, 2>), grid, dim3(kBlock), 0, s, g, a);
+    else hipLaunchKernelGGL((leaf_derive_kernel<8, 1>), grid, dim3(kBlock), 0, s, g, a);
+  } else if (kmax <= 16) {
+    hipLaunchKernelGGL((leaf_derive_kernel<16, 1>), grid, dim3(kBlock), 0, s, g, a);
+  } else {
+    hipLaunchKernelGGL((leaf_derive_kernel<32, 1>), grid, dim3(kBlock), 0, s, g, a);
+  }
   return hipGetLastError();
 }
 
