@@ -592,12 +592,15 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
   // after_first: called once the first round's traversal is done on fs (the
   // host waits for it anyway): the presplit runs' first round gets the GPU
   // alone, the decremental kernels are launched beside the later rounds
+  // before_last(R_n): called once before the last round is queued; it may
+  // append runs to the R_* arrays (their capacity) and raise R_n
   auto full_reruns = [&](const uint32_t* R_dsts, uint32_t R_n, const uint32_t* R_ign,
                          const uint32_t* R_cnt, uint32_t* R_status, uint32_t* R_k2,
-                         const std::function<int()>& after_first = nullptr) -> int {
+                         const std::function<int()>& after_first = nullptr,
+                         const std::function<int(uint32_t&)>& before_last = nullptr) -> int {
     ospf::TraceArgs t = t_k1;
-    const uint32_t total_vb = (R_n + 63) / 64;  // this set's virtual batches (<= the carve'fs)
-    HIPCHK(c, hipMemsetD32Async(d_roots, (int)src, ms ? R_n : chunk, fs));
+    uint32_t total_vb = (R_n + 63) / 64;  // this set's virtual batches (<= the carve'fs)
+    HIPCHK(c, hipMemsetD32Async(d_roots, (int)src, ms ? (before_last ? n : R_n) : chunk, fs));
     if (ms) {
       if (!c->aux) HIPCHK(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
       while (c->ev.size() < 2 * (size_t)slots + 1) {
@@ -610,7 +613,14 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
       hipEvent_t ev_end = c->ev[2 * slots];
       char* ring = st + per_vb * nb_max;
       std::vector<uint32_t> found;
+      bool last_called = false;
       for (uint32_t r = 0, vb0 = 0; vb0 < total_vb; ++r, vb0 += nb_max) {
+        if (before_last && !last_called && vb0 + nb_max >= total_vb) {
+          last_called = true;
+          const int rc3 = before_last(R_n);
+          if (rc3) return rc3;
+          total_vb = (R_n + 63) / 64;
+        }
         const uint32_t slot = r % slots;
         uint8_t* lev = (uint8_t*)(ring + (size_t)slot * (sz_lev + sz_sdead));
         uint32_t* dead = (uint32_t*)(ring + (size_t)slot * (sz_lev + sz_sdead) + sz_lev);
@@ -642,6 +652,9 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
         const size_t zero = (char*)(a.igb + (size_t)a.nb * igw) - st;
         a.igm = (uint64_t*)(st + align_up(zero, 256));
         a.lev = lev;
+        // a batch stops once all its destinations are reached
+        // (OSPF_KSP_FULL_DEPTH: every level, as before)
+        a.kdst = getenv("OSPF_KSP_FULL_DEPTH") ? nullptr : R_dsts;
         HIPCHK(c, ospf::zero_async(st, zero, fs));
         if (r >= slots) HIPCHK(c, hipStreamWaitEvent(fs, ev_tr[slot], 0));  // slot's trace done
         HIPCHK(c, ospf::zero_async(lev, (size_t)a.nb * V * 64ull, fs));
@@ -869,6 +882,10 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
       }
       hipError_t e3 = ospf::launch_ksp_decr(c->g, td, nblk, ks);
       if (e3 != hipSuccess) return hip_fail(c, e3, "launch_ksp_decr");
+      if (npre) {  // the decremental kernel's fallback count (ctr[13]), then its event
+        HIPCHK(c, hipMemcpyAsync(d_ctr + 13, d_ctr + 1, 4, hipMemcpyDeviceToDevice, ks));
+        HIPCHK(c, hipEventRecord(c->ksp_ev[3], ks));
+      }
       if (td.budget) {
         e3 = ospf::launch_ksp_decr_heavy(c->g, td, hblk, ks);
         if (e3 != hipSuccess) return hip_fail(c, e3, "launch_ksp_decr_heavy");
@@ -879,9 +896,17 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
     if (decr_first && (rc = launch_decr())) return rc;
     // a list of runs through full_reruns on s: compacted (dsts, status,
     // ignore sets, counts) into scratch slot `slot`, records scattered back
+    // fold: before the last round, runs of a second list (the decremental
+    // kernel's fallbacks) join it -- fold(d_list2, n2) returns the list and
+    // how many (<= extra); they are gathered behind the first list's and
+    // scattered back with it
+    const uint32_t* fold_list = nullptr;
+    uint32_t folded = 0;
     auto rerun_list = [&](const uint32_t* d_list, uint32_t nl, int slot,
-                          const std::function<int()>& after_first = nullptr) -> int {
-      const size_t sz_fd = align_up(nl * 4ull, 256), sz_fr = align_up((size_t)nl * cap * 4ull, 256);
+                          const std::function<int()>& after_first = nullptr, uint32_t extra = 0,
+                          const std::function<int(const uint32_t**, uint32_t*)>& fold = nullptr) -> int {
+      const uint32_t cap_n = nl + extra;
+      const size_t sz_fd = align_up(cap_n * 4ull, 256), sz_fr = align_up((size_t)cap_n * cap * 4ull, 256);
       int rc2 = OSPF_OK;
       char* fp = stream_scratch(c, s, 3 * sz_fd + 2 * sz_fr, &rc2, slot);
       if (rc2) return rc2;
@@ -890,17 +915,43 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
       uint32_t* f_cnt = (uint32_t*)(fp + 2 * sz_fd);
       uint32_t* f_ign = (uint32_t*)(fp + 3 * sz_fd);
       uint32_t* f_k2 = (uint32_t*)(fp + 3 * sz_fd + sz_fr);
-      hipError_t e2;
-      if ((e2 = ospf::launch_rows_gather(f_dsts, k->dsts, d_list, nl, 1, true, fs)) != hipSuccess ||
-          (e2 = ospf::launch_rows_gather(f_status, k->status, d_list, nl, 1, true, fs)) != hipSuccess ||
-          (e2 = ospf::launch_rows_gather(f_cnt, d_cnt, d_list, nl, 1, true, fs)) != hipSuccess ||
-          (e2 = ospf::launch_rows_gather(f_ign, d_ign, d_list, nl, cap, true, fs)) != hipSuccess)
-        return hip_fail(c, e2, "launch_rows_gather");
-      rc2 = full_reruns(f_dsts, nl, f_ign, f_cnt, f_status, f_k2, after_first);
+      auto gather = [&](uint32_t at, const uint32_t* list, uint32_t m) -> int {
+        hipError_t e2;
+        if ((e2 = ospf::launch_rows_gather(f_dsts + at, k->dsts, list, m, 1, true, fs)) != hipSuccess ||
+            (e2 = ospf::launch_rows_gather(f_status + at, k->status, list, m, 1, true, fs)) != hipSuccess ||
+            (e2 = ospf::launch_rows_gather(f_cnt + at, d_cnt, list, m, 1, true, fs)) != hipSuccess ||
+            (e2 = ospf::launch_rows_gather(f_ign + (size_t)at * cap, d_ign, list, m, cap, true, fs)) !=
+                hipSuccess)
+          return hip_fail(c, e2, "launch_rows_gather");
+        return OSPF_OK;
+      };
+      auto scatter = [&](uint32_t at, const uint32_t* list, uint32_t m) -> int {
+        hipError_t e2;
+        if ((e2 = ospf::launch_rows_gather(k->status, f_status + at, list, m, 1, false, fs)) != hipSuccess ||
+            (e2 = ospf::launch_rows_gather(k->k2, f_k2 + (size_t)at * cap, list, m, cap, false, fs)) !=
+                hipSuccess)
+          return hip_fail(c, e2, "launch_rows_gather");
+        return OSPF_OK;
+      };
+      if ((rc2 = gather(0, d_list, nl))) return rc2;
+      const uint32_t* l2 = nullptr;
+      uint32_t n2 = 0;
+      std::function<int(uint32_t&)> before_last;
+      if (fold)
+        before_last = [&](uint32_t& Rn) -> int {
+          int rc4 = fold(&l2, &n2);
+          if (rc4) return rc4;
+          n2 = std::min(n2, extra);
+          if (n2 && (rc4 = gather(Rn, l2, n2))) return rc4;
+          Rn += n2;
+          return OSPF_OK;
+        };
+      rc2 = full_reruns(f_dsts, nl, f_ign, f_cnt, f_status, f_k2, after_first, before_last);
       if (rc2) return rc2;
-      if ((e2 = ospf::launch_rows_gather(k->status, f_status, d_list, nl, 1, false, fs)) != hipSuccess ||
-          (e2 = ospf::launch_rows_gather(k->k2, f_k2, d_list, nl, cap, false, fs)) != hipSuccess)
-        return hip_fail(c, e2, "launch_rows_gather");
+      if ((rc2 = scatter(0, d_list, nl))) return rc2;
+      if (n2 && (rc2 = scatter(nl, l2, n2))) return rc2;
+      fold_list = l2;
+      folded = n2;
       return OSPF_OK;
     };
     if (npre) {  // beside the decremental kernels
@@ -918,7 +969,22 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
         HIPCHK(c, hipMemcpyAsync(d_pre, pre.data(), npre * 4ull, hipMemcpyHostToDevice, fs));
         HIPCHK(c, hipStreamSynchronize(fs));
       }
-      rc = rerun_list(d_pre, npre, 3, launch_decr);
+      // the decremental kernel's fallbacks join the last presplit round when
+      // that kernel is done by then (OSPF_KSP_NOFOLD: a round of their own
+      // after it, as before)
+      const bool fold_on = !getenv("OSPF_KSP_NOFOLD");
+      auto fold = [&](const uint32_t** l, uint32_t* m) -> int {
+        *l = d_fb;
+        *m = 0;
+        if (!decr_queued || hipEventQuery(c->ksp_ev[3]) != hipSuccess) return OSPF_OK;
+        uint32_t cnt = 0;
+        HIPCHK(c, hipMemcpy(&cnt, d_ctr + 13, 4, hipMemcpyDeviceToHost));
+        *m = cnt;
+        return OSPF_OK;
+      };
+      constexpr uint32_t kFold = 256;  // fallbacks a presplit round takes
+      rc = fold_on ? rerun_list(d_pre, npre, 3, launch_decr, kFold, fold)
+                   : rerun_list(d_pre, npre, 3, launch_decr);
       if (rc) return rc;
     }
     if ((rc = launch_decr())) return rc;  // (no round called it)
@@ -965,8 +1031,9 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
     c->ksp_decr_stats[2] += ctr[3];
     const uint32_t nfb = ctr[1];
     c->spf_runs += n - nfb - npre;  // (full_reruns counts its own)
-    if (nfb) {
-      rc = rerun_list(d_fb, nfb, 4);
+    const uint32_t nfold = fold_list == d_fb ? std::min(folded, nfb) : 0u;
+    if (nfb > nfold) {  // the fallbacks no presplit round took
+      rc = rerun_list(d_fb + nfold, nfb - nfold, 4);
       if (rc) return rc;
     }
     if (fs != s) {  // the caller's stream after the full reruns (and, through them, ks)

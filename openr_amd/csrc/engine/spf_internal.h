@@ -71,7 +71,7 @@ struct ospf_ctx {
   hipStream_t aux = nullptr;
   // KSP2: the decremental kernels beside the pre-split runs' full reruns
   hipStream_t ksp_aux = nullptr, ksp_hi = nullptr;  // low / high priority
-  hipEvent_t ksp_ev[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t ksp_ev[4] = {nullptr, nullptr, nullptr, nullptr};
   // derive phase 1: rows kernels of one round beside the next round's levels
   hipStream_t lv_aux = nullptr;
   hipEvent_t lv_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // traversed[2], rows done[2]

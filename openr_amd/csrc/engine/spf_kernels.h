@@ -231,6 +231,10 @@ struct MsArgs {
   uint32_t* igb;          // [nb][igw]
   uint64_t* igm;          // [nb][E]
   uint32_t igw;
+  // KSP2 reruns: destination of each run (by run index), or null. A batch
+  // whose every run has reached its destination stops after that level (the
+  // k = 2 trace reads only levels below the destination's)
+  const uint32_t* kdst;
   uint8_t* levrow;        // derive phase 1 (kp -1): [n][lev_pitch] dist + 1 per (run, node)
   uint32_t lev_pitch;     //   bytes per level row (multiple of 16, >= V; padding zeroed)
 };

@@ -2051,6 +2051,22 @@ hipError_t launch_nh_interleave(const uint32_t* nhs, uint32_t* nh, uint32_t n, u
   return hipGetLastError();
 }
 
+namespace {
+// KSP2 reruns: a batch stops after level d once every run has reached its
+// destination (found[d + 1] cleared: the next level kernels return at once)
+__global__ void __launch_bounds__(64) ksp_done_kernel(MsArgs a, uint32_t V, uint32_t d) {
+  const uint32_t vbl = blockIdx.x, r = threadIdx.x;
+  if (!a.found[vbl * a.lmax + d + 1]) return;  // block-uniform
+  const uint32_t run = (a.vb0 + vbl) * a.R + r;  // (npass 1)
+  bool ok = true;
+  if (run < a.n) {
+    const uint32_t dst = a.kdst[run];
+    ok = dst < V && ((a.seen[(size_t)vbl * V + dst] >> r) & 1ull);
+  }
+  if (__all(ok) && r == 0) a.found[vbl * a.lmax + d + 1] = 0u;
+}
+}  // namespace
+
 hipError_t launch_msbfs_ksp(const DevGraph& g, const MsArgs& a, uint32_t d0, uint32_t d1,
                             hipStream_t s) {
   if (d0 <= 1) {
@@ -2064,6 +2080,8 @@ hipError_t launch_msbfs_ksp(const DevGraph& g, const MsArgs& a, uint32_t d0, uin
     hipLaunchKernelGGL(msbfs_level_kernel<0>, dim3(a.nb * (chunks + bigblocks)), dim3(kBlock), 0, s,
                        g, a, d);
     hipLaunchKernelGGL(msbfs_settle_kernel<0>, dim3(a.nb * chunks), dim3(kBlock), 0, s, g, a, d);
+    if (a.kdst && a.npass == 1 && a.R == 64)
+      hipLaunchKernelGGL(ksp_done_kernel, dim3(a.nb), dim3(64), 0, s, a, g.V, d);
   }
   return hipGetLastError();
 }
