@@ -812,7 +812,11 @@ int run_ksp2(ospf_ctx* c, const ospf_ksp2* k, hipStream_t s) {
     td.heavy_ctr = d_ctr + 4;
     td.err = c->d_err;
     td.decr_runs = decr_r;
-    // (OSPF_KSP_MAP_FB=1: a run past the map budget to the full reruns)
+    // a run past the map budget goes to the full reruns (with presplit runs
+    // it joins their last round) instead of the 16-wave kernel, whose
+    // single slow run (F100k: 10.8 ms) had ended the launch: 20.17 -> 20.04
+    // ms (profiles/r06/h1_ksp2_order_ab.txt; OSPF_KSP_MAP_FB=0 restores it)
+    td.map_fb = 1u;
     if (const char* x = getenv("OSPF_KSP_MAP_FB")) td.map_fb = atoi(x) ? 1u : 0u;
     if (prune) {
       char* q = dp + sz_tc + 3 * sz_fb + sz_ctr + sz_dd;
