@@ -1557,7 +1557,9 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   std::mutex red_mu;
   int bad_rc = OSPF_OK;
   const char* bad_msg = nullptr;
-  ospf_int::par_for(V, [&](uint32_t lo, uint32_t hi) {
+  // (chunks by entries, starting at multiples of 32 nodes: whole words of
+  // the no-transit bits)
+  ospf_int::par_for_rows(V, csr->row_ptr, [&](uint32_t lo, uint32_t hi) {
     uint32_t l_deg = 0, l_metric = 0, l_dn = 0, l_links = 0;
     uint64_t l_bound = 0;
     bool l_unit = true;
@@ -1620,11 +1622,11 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
       bad_rc = rc;
       bad_msg = msg;
     }
-  });
+  }, 8192, 32);
   if (bad_rc != OSPF_OK) return fail(c, bad_rc, bad_msg);
   for (uint32_t u = 0; u < V; ++u) dn_off[u + 1] += dn_off[u];
   std::vector<uint32_t> dn(dn_off[V]);
-  ospf_int::par_for(V, [&](uint32_t lo, uint32_t hi) {
+  ospf_int::par_for_rows(V, csr->row_ptr, [&](uint32_t lo, uint32_t hi) {
     for (uint32_t u = lo; u < hi; ++u) {
       uint32_t k = dn_off[u];
       for (uint32_t e = csr->row_ptr[u], b = e; e < csr->row_ptr[u + 1]; ++e) {
@@ -1649,7 +1651,7 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   // twin entry's rank = the link's position in linksFromNode(neighbour), the
   // order pathLinks lists links of one predecessor in (LinkState.cpp:885-901)
   uint32_t max_lid = 0;
-  ospf_int::par_for(V, [&](uint32_t lo, uint32_t hi) {
+  ospf_int::par_for_rows(V, csr->row_ptr, [&](uint32_t lo, uint32_t hi) {
     std::vector<uint32_t> ord;
     uint32_t l_lid = 0;
     for (uint32_t u = lo; u < hi; ++u) {
@@ -1737,7 +1739,7 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   const size_t sz_ew = pew.size() * 4ull;
   // distinct-neighbour index per padded entry (rows are sorted by neighbour)
   std::vector<uint16_t> didx(std::max<uint32_t>(Ep, 1), 0xFFFFu);
-  ospf_int::par_for(V, [&](uint32_t lo, uint32_t hi) {
+  ospf_int::par_for_rows(V, prow.data(), [&](uint32_t lo, uint32_t hi) {
     for (uint32_t u = lo; u < hi; ++u) {
       uint32_t k = 0, prev = 0xFFFFFFFFu;
       for (uint32_t e = prow[u]; e < prow[u + 1]; ++e) {
@@ -1843,7 +1845,7 @@ int ospf_load_graph(ospf_ctx* c, const ospf_csr* csr, uint64_t version) {
   c->info.device_bytes = tot;
   c->dist_bound = dist_bound;
   c->h_rowmax.assign(V, 0u);
-  ospf_int::par_for(V, [&](uint32_t lo, uint32_t hi) {
+  ospf_int::par_for_rows(V, c->h_prow.data(), [&](uint32_t lo, uint32_t hi) {
     for (uint32_t u = lo; u < hi; ++u)
       for (uint32_t e = c->h_prow[u]; e < c->h_prow[u + 1]; ++e)
         if (!(c->h_pcolx[e] & 0x80000000u)) c->h_rowmax[u] = std::max(c->h_rowmax[u], c->h_pw[e]);

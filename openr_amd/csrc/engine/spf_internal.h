@@ -140,6 +140,36 @@ void par_for(uint32_t n, F fn, uint32_t grain = 64) {
 }
 
 
+// fn(lo, hi) over items [0, n) in chunks of about `target` units of work,
+// item i weighing off[i + 1] - off[i] (a row's entries), and of at most 256
+// items: a fabric's spines (1,781 entries each, first by name) spread over
+// many chunks instead of loading one, and the light rows share few chunks
+// (one atomic claim each). Chunk starts are multiples of `align`.
+template <class F>
+void par_for_rows(uint32_t n, const uint32_t* off, F fn, uint32_t target = 8192, uint32_t align = 1) {
+  if (!n) return;
+  const uint64_t total = (uint64_t)off[n] - off[0];
+  const uint32_t want = (uint32_t)std::min<uint64_t>(n, std::max<uint64_t>(1, total / std::max(1u, target)));
+  std::vector<uint32_t> cut{0u};
+  for (uint32_t k = 1; k < want; ++k) {
+    const uint64_t at = off[0] + total * k / want;
+    uint32_t i = (uint32_t)(std::lower_bound(off, off + n, (uint32_t)at) - off);
+    i = i / align * align;
+    if (i > cut.back() && i < n) cut.push_back(i);
+  }
+  cut.push_back(n);
+  std::vector<uint32_t> all;
+  for (size_t k = 0; k + 1 < cut.size(); ++k) {
+    all.push_back(cut[k]);
+    const uint32_t step = std::max<uint32_t>(align, 256u / align * align);
+    for (uint32_t x = cut[k] + step; x < cut[k + 1]; x += step) all.push_back(x);
+  }
+  all.push_back(n);
+  par_for((uint32_t)all.size() - 1, [&](uint32_t clo, uint32_t chi) {
+    for (uint32_t k = clo; k < chi; ++k) fn(all[k], all[k + 1]);
+  }, 1);
+}
+
 int fail(ospf_ctx* c, int code, const std::string& msg);
 // hipMalloc on the context's device; when it fails and destroyed sweeps'
 // blocks are pooled (sweep_pool), the pool is freed and the allocation tried
