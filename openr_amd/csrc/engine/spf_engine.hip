@@ -2413,7 +2413,7 @@ int leaf_derive(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, const uint32_t
                 uint32_t n_groups, uint32_t max_root_neighbors, uint8_t* d_lev,
                 uint32_t lev_pitch, const uint32_t* d_pos, const uint32_t* d_lev_out,
                 uint32_t* d_dist, uint32_t dist_pitch, uint32_t* d_nh, uint32_t nh_pitch,
-                ospf_digest* d_digest, void* stream) {
+                ospf_digest* d_digest, void* stream, int group_major) {
   if (!c) return OSPF_E_INVAL;
   if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
   if (n == 0) return OSPF_OK;
@@ -2441,6 +2441,7 @@ int leaf_derive(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, const uint32_t
   a.digest = d_digest;
   a.err = c->d_err;
   if (const char* e = getenv("OSPF_LEAF_CTILES")) a.ctiles = (uint32_t)std::max(1, atoi(e));
+  if (group_major >= 0) a.group_major = group_major ? 1u : 0u;  // the sweep's choice
   if (const char* e = getenv("OSPF_LEAF_GROUP_MAJOR")) a.group_major = atoi(e) ? 1u : 0u;
   a.dpitch = dist_pitch;
   a.npitch = nh_pitch;

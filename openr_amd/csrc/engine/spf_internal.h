@@ -222,7 +222,7 @@ int leaf_derive(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, const uint32_t
                 uint32_t n_groups, uint32_t max_root_neighbors, uint8_t* d_lev,
                 uint32_t lev_pitch, const uint32_t* d_pos, const uint32_t* d_lev_out,
                 uint32_t* d_dist, uint32_t dist_pitch, uint32_t* d_nh, uint32_t nh_pitch,
-                ospf_digest* d_digest, void* stream);
+                ospf_digest* d_digest, void* stream, int group_major = -1);
 
 // Host plan of the cover closure (spf_cover.hip closure_kernel) for the
 // closure roots `roots` (node ids, non-seed cover nodes; dc row i = roots[i])

@@ -245,6 +245,11 @@ struct ospf_sweep {
   // queued by the plan (after ev_in on the null stream and events[0])
   bool early = false, early_on = false;
   size_t started = 0;
+  // block order of the leaf launch (0 chunk-major, 1 group-major): picked at
+  // create by timing both -- which order stores faster depends on where the
+  // allocation's rows fall in the memory channels (the probe's two patterns
+  // swap places from one allocation to the next)
+  int leaf_order = 0;
 };
 
 namespace {
@@ -1443,9 +1448,10 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       uint32_t* nh = lnh + (size_t)nR * DP;
       ospf_digest* dg2 = dg + nR;
       const uint32_t* lo = drop_rest ? d_lout : nullptr;
+      ospf_sweep* sw = s;
       u.fn = [=](hipStream_t strm) {
         return ospf_int::leaf_derive(c, dl, n, d_grp, ngr, kmax, lev, pitch, d_pos, lo, dist, DP, nh, DP,
-                                     dg2, strm);
+                                     dg2, strm, sw->leaf_order);
       };
       s->step_comp += u.comp;
       s->units.push_back(std::move(u));
@@ -2631,6 +2637,42 @@ int run_eager(ospf_sweep* s, hipStream_t caller) {
   return OSPF_OK;
 }
 
+// The leaf launch (derive mode) timed in both block orders on the rows of
+// the eager run (its own digests are zeroed by the launch, rows rewritten
+// identically), the faster kept for the HIP graph and every later run.
+// OSPF_LEAF_GROUP_MAJOR fixes the order; OSPF_LEAF_NO_AUTO keeps chunk-major.
+int pick_leaf_order(ospf_sweep* s) {
+  if (getenv("OSPF_LEAF_GROUP_MAJOR") || getenv("OSPF_LEAF_NO_AUTO")) return OSPF_OK;
+  ospf_sweep::Unit* u = nullptr;
+  for (auto& x : s->units)
+    if (x.name == "leaf") u = &x;
+  if (!u || u->n_roots < 4096) return OSPF_OK;
+  hipStream_t st = s->streams[u->stream];
+  hipEvent_t a, b;
+  SCHK(s, hipEventCreate(&a));
+  SCHK(s, hipEventCreate(&b));
+  float best[2] = {1e30f, 1e30f};
+  int rc = OSPF_OK;
+  for (int rep = 0; rep < 2 && rc == OSPF_OK; ++rep)
+    for (int ord = 0; ord < 2 && rc == OSPF_OK; ++ord) {
+      s->leaf_order = ord;
+      if (hipEventRecord(a, st) != hipSuccess) rc = OSPF_E_DEVICE;
+      if (rc == OSPF_OK) rc = u->fn(st);
+      if (rc == OSPF_OK && (hipEventRecord(b, st) != hipSuccess || hipEventSynchronize(b) != hipSuccess))
+        rc = OSPF_E_DEVICE;
+      float t = 0;
+      if (rc == OSPF_OK && hipEventElapsedTime(&t, a, b) == hipSuccess) best[ord] = std::min(best[ord], t);
+    }
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+  if (rc) return sfail(s, rc, "sweep: leaf order probe: " + std::string(ospf_last_error(s->c)));
+  s->leaf_order = best[1] < best[0] ? 1 : 0;
+  if (getenv("OSPF_SWEEP_TIMING"))
+    fprintf(stderr, "sweep_create leaf order %s (chunk-major %.3f ms, group-major %.3f ms)\n",
+            s->leaf_order ? "group-major" : "chunk-major", best[0], best[1]);
+  return ospf_sync(s->c, st);
+}
+
 void release(ospf_sweep* s) {
   if (s->c) hipSetDevice(s->c->device);
   for (hipStream_t st : s->streams)
@@ -2814,6 +2856,7 @@ int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
     return bail(fail(c, OSPF_E_DEVICE, "sweep: first run failed"));
   if ((rc = ospf_sync(c, s->streams[0]))) return bail(rc);
   s->ran = true;
+  if ((rc = pick_leaf_order(s))) return bail(rc);
   if (o->hip_graph) {
     hipStream_t m = s->streams[0];
     hipGraph_t g = nullptr;
