@@ -397,7 +397,7 @@ __global__ void __launch_bounds__(kBlock) nh_derive_twin_kernel(DevGraph g, Twin
 // so LDS and registers no longer cap the waves per SIMD; loads are one 4-B
 // piece of the own and each class row per lane (256 B per wave instruction),
 // stores W 1-KB runs of next-hop words and one 1-KB run of dist per chunk.
-template <int W, int PD>
+template <int W, int PD, bool KD>
 __global__ void __launch_bounds__(kBlock) nh_twin4_kernel(DevGraph g, TwinArgs a) {
   __shared__ TwinTab T;
   __shared__ unsigned long long s_h;
@@ -432,7 +432,9 @@ __global__ void __launch_bounds__(kBlock) nh_twin4_kernel(DevGraph g, TwinArgs a
   const bool vec = (V & 3u) == 0 && (dpitch & 3u) == 0 && (npitch & 3u) == 0;
   uint64_t h = 0;
   constexpr uint32_t kPre = 3;
-  auto load_c = [&](uint32_t c, uint32_t& L, uint32_t* R) {
+  // KD: the 4 nodes' digest keys ride in the same ring (their L2 latency
+  // was exposed at the digest terms of every chunk)
+  auto load_c = [&](uint32_t c, uint32_t& L, uint32_t* R, uint4* K) {
     const uint32_t v0 = c * 256u + 4u * lane;
     const uint32_t vs = (c < c_end && v0 < a.pitch) ? v0 : 0u;
     L = *reinterpret_cast<const uint32_t*>(a.lev + (size_t)own * a.pitch + vs);
@@ -440,11 +442,18 @@ __global__ void __launch_bounds__(kBlock) nh_twin4_kernel(DevGraph g, TwinArgs a
     for (uint32_t j = 0; j < kPre; ++j)
       R[j] = j < nc ? *reinterpret_cast<const uint32_t*>(a.lev + (size_t)T.crow[j] * a.pitch + vs)
                     : 0x7F7F7F7Fu;
+    if constexpr (KD) {  // (zero padded past V up to the level pitch)
+      if (a.digest) {
+        K[0] = reinterpret_cast<const uint4*>(g.dkn + vs)[0];
+        K[1] = reinterpret_cast<const uint4*>(g.dkn + vs)[1];
+      }
+    }
   };
   // PD chunks of loads in flight per wave (a ring of prefetched rows)
   uint32_t Ln[PD], Rn[PD][kPre];
+  uint4 Kn[PD][KD ? 2 : 1];
 #pragma unroll
-  for (int d = 0; d < PD; ++d) load_c(c_beg + wave + d * kWaves, Ln[d], Rn[d]);
+  for (int d = 0; d < PD; ++d) load_c(c_beg + wave + d * kWaves, Ln[d], Rn[d], Kn[d]);
   for (uint32_t c = c_beg + wave; c < c_end; c += kWaves) {
     const uint32_t c0 = c * 256u, v0 = c0 + 4u * lane;
     const bool live = v0 < a.pitch;
@@ -453,13 +462,24 @@ __global__ void __launch_bounds__(kBlock) nh_twin4_kernel(DevGraph g, TwinArgs a
     uint32_t Rp[kPre];
 #pragma unroll
     for (uint32_t j = 0; j < kPre; ++j) Rp[j] = Rn[0][j];
+    uint64_t kd4[4] = {0ull, 0ull, 0ull, 0ull};
+    if constexpr (KD) {
+      kd4[0] = ((uint64_t)Kn[0][0].y << 32) | Kn[0][0].x;
+      kd4[1] = ((uint64_t)Kn[0][0].w << 32) | Kn[0][0].z;
+      kd4[2] = ((uint64_t)Kn[0][1].y << 32) | Kn[0][1].x;
+      kd4[3] = ((uint64_t)Kn[0][1].w << 32) | Kn[0][1].z;
+    }
 #pragma unroll
     for (int d = 0; d + 1 < PD; ++d) {
       Ln[d] = Ln[d + 1];
 #pragma unroll
       for (uint32_t j = 0; j < kPre; ++j) Rn[d][j] = Rn[d + 1][j];
+      if constexpr (KD) {
+        Kn[d][0] = Kn[d + 1][0];
+        Kn[d][1] = Kn[d + 1][1];
+      }
     }
-    load_c(c + PD * kWaves, Ln[PD - 1], Rn[PD - 1]);
+    load_c(c + PD * kWaves, Ln[PD - 1], Rn[PD - 1], Kn[PD - 1]);
     uint32_t lm1 = 0;
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb) {
@@ -514,7 +534,7 @@ __global__ void __launch_bounds__(kBlock) nh_twin4_kernel(DevGraph g, TwinArgs a
           for (int w = 0; w < W; ++w)
             if (word[w][q]) ws += digest_word_key(w, word[w][q]);
         }
-        h += g.dkn[v0 + q] * ws;  // zero past V
+        h += (KD ? kd4[q] : g.dkn[v0 + q]) * ws;  // zero past V
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -823,12 +843,18 @@ hipError_t launch_nh_derive_twin(const DevGraph& g, const TwinArgs& a0, hipStrea
   // lane = 4 nodes (nh_twin4_kernel) unless OSPF_TWIN_NH16=1 (lane = 16 nodes)
   const bool nh16 = getenv("OSPF_TWIN_NH16") != nullptr;  // read per launch: in-process A/B
   if (!nh16) {
-    // prefetch depth (chunks of loads in flight per wave): OSPF_TWIN4_PD 1 / 2
+    // prefetch depth (chunks of loads in flight per wave): OSPF_TWIN4_PD 1 / 2;
+    // the digest keys prefetched with the rows (OSPF_TWIN4_KD=0: loaded at
+    // the digest terms; 20.10 -> 19.82 ms per F100k sweep in one process,
+    // profiles/r06/k2_twin4_key_prefetch_ab.txt)
     const char* pe = getenv("OSPF_TWIN4_PD");
     const bool pd2 = !pe || atoi(pe) >= 2;
-#define OSPF_TWIN4(WW)                                                                        \
-  if (pd2) hipLaunchKernelGGL((nh_twin4_kernel<WW, 2>), grid, dim3(kBlock), 0, s, g, a);     \
-  else hipLaunchKernelGGL((nh_twin4_kernel<WW, 1>), grid, dim3(kBlock), 0, s, g, a);
+    const char* ke = getenv("OSPF_TWIN4_KD");
+    const bool kd = pd2 && (!ke || atoi(ke) != 0);
+#define OSPF_TWIN4(WW)                                                                          \
+  if (kd) hipLaunchKernelGGL((nh_twin4_kernel<WW, 2, true>), grid, dim3(kBlock), 0, s, g, a);  \
+  else if (pd2) hipLaunchKernelGGL((nh_twin4_kernel<WW, 2, false>), grid, dim3(kBlock), 0, s, g, a); \
+  else hipLaunchKernelGGL((nh_twin4_kernel<WW, 1, false>), grid, dim3(kBlock), 0, s, g, a);
     switch (a.W) {
       case 1: OSPF_TWIN4(1) break;
       case 2: OSPF_TWIN4(2) break;
