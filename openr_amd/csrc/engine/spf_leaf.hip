@@ -58,7 +58,7 @@ __device__ __forceinline__ uint32_t beq7(uint32_t x, uint32_t y) {
   return ~((x ^ y) + 0x7F7F7F7Fu) & 0x80808080u;
 }
 
-template <int KM, int PD>
+template <int KM, int PD, bool KD = false>
 __global__ void __launch_bounds__(kBlock) leaf_derive_kernel(DevGraph g, LeafArgs a) {
   __shared__ uint32_t s_root[kLeafMaxG], s_own[kLeafMaxG], s_use[kLeafMaxG], s_lrow[kLeafMaxG];
   __shared__ uint32_t s_rb[kLeafMaxG], s_re[kLeafMaxG];
@@ -154,9 +154,20 @@ __global__ void __launch_bounds__(kBlock) leaf_derive_kernel(DevGraph g, LeafArg
                   : kNoRow;
     }
   };
+  // KD: the tile's digest keys (dkey: {dist key, node key} per node, 64 B a
+  // lane) one tile ahead, with the neighbour words
+  auto load_k = [&](uint32_t t, uint4* k4) {
+    const uint32_t v0 = t * 1024u + wave * 256u + 4u * lane;
+    const bool ok = a.digest && t < t1 && v0 + 4u <= V;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      k4[q] = ok ? reinterpret_cast<const uint4*>(g.dkey + 2ull * v0)[q] : make_uint4(0u, 0u, 0u, 0u);
+  };
   uint32_t xn[PD][KM];
+  uint4 kn[KD ? 4 : 1];
 #pragma unroll
   for (int d = 0; d < PD; ++d) load_x(t0 + d, xn[d]);
+  if constexpr (KD) load_k(t0, kn);
   for (uint32_t t = t0; t < t1; ++t) {
     const uint32_t v0 = t * 1024u + wave * 256u + 4u * lane;
     uint32_t x[KM];
@@ -167,6 +178,17 @@ __global__ void __launch_bounds__(kBlock) leaf_derive_kernel(DevGraph g, LeafArg
 #pragma unroll
       for (int k = 0; k < KM; ++k) xn[d][k] = xn[d + 1][k];
     load_x(t + PD, xn[PD - 1]);
+    uint64_t kdist[4] = {0ull, 0ull, 0ull, 0ull}, knode[4] = {0ull, 0ull, 0ull, 0ull};
+    bool kok = false;
+    if constexpr (KD) {
+      kok = v0 + 4u <= V;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        kdist[q] = ((uint64_t)kn[q].y << 32) | kn[q].x;
+        knode[q] = ((uint64_t)kn[q].w << 32) | kn[q].z;
+      }
+      load_k(t + 1, kn);
+    }
     if (v0 >= a.pitch) continue;
     uint32_t m = kNoRow;
 #pragma unroll
@@ -210,7 +232,9 @@ __global__ void __launch_bounds__(kBlock) leaf_derive_kernel(DevGraph g, LeafArg
         if (v >= V || dv[b] == kInf) continue;
         const uint64_t wk = small ? s_wk[word[b] & 0xFFu]
                                   : (word[b] ? digest_word_key(0, word[b]) : 0ull);
-        hterm[b] = g.dkey[2ull * v] * (uint64_t)(dv[b] + 1u) + g.dkn[v] * wk;
+        const uint64_t kdv = (KD && kok) ? kdist[b] : g.dkey[2ull * v];
+        const uint64_t knv = (KD && kok) ? knode[b] : g.dkn[v];
+        hterm[b] = kdv * (uint64_t)(dv[b] + 1u) + knv * wk;
         br += 1u;
         bs += dv[b];
         bh += hterm[b];
@@ -298,8 +322,14 @@ hipError_t launch_leaf_derive(const DevGraph& g, const LeafArgs& a0, uint32_t km
   // profiles/r06/i1_leaf_prefetch_ab.txt)
   const char* pe = getenv("OSPF_LEAF_PD");
   const bool pd2 = !pe || atoi(pe) >= 2;
+  // the tile's digest keys one tile ahead with the neighbour words
+  // (OSPF_LEAF_KD=0: loaded at the digest terms; 20.26 -> 19.48 ms per F100k
+  // sweep in one process, profiles/r06/k3_leaf_key_prefetch_ab.txt)
+  const char* ke = getenv("OSPF_LEAF_KD");
+  const bool kd = !ke || atoi(ke) != 0;
   if (kmax <= 8) {
-    if (pd2) hipLaunchKernelGGL((leaf_derive_kernel<8, 2>), grid, dim3(kBlock), 0, s, g, a);
+    if (pd2 && kd) hipLaunchKernelGGL((leaf_derive_kernel<8, 2, true>), grid, dim3(kBlock), 0, s, g, a);
+    else if (pd2) hipLaunchKernelGGL((leaf_derive_kernel<8, 2>), grid, dim3(kBlock), 0, s, g, a);
     else hipLaunchKernelGGL((leaf_derive_kernel<8, 1>), grid, dim3(kBlock), 0, s, g, a);
   } else if (kmax <= 16) {
     hipLaunchKernelGGL((leaf_derive_kernel<16, 1>), grid, dim3(kBlock), 0, s, g, a);
