@@ -271,6 +271,7 @@ struct WidePlan {
   uint32_t* nh;           // [n][V][W]
   ospf_digest* digest;    // [n] (zeroed by the launcher) or null
   uint32_t tiles, ctiles, chunks;  // set by the launcher (ctiles 0: its choice)
+  uint32_t late_keys;     // set by the launcher: OSPF_WIDE_LATE_KEYS (A/B)
 };
 hipError_t launch_wide_plan(const DevGraph& g, const WidePlan& p, hipStream_t s);
 

@@ -1805,6 +1805,16 @@ __global__ void __launch_bounds__(256) nh_wide_plan_kernel(DevGraph g, WidePlan 
       const uint32_t row = pk[m] < 0x80000000u ? pk[m] : s_own[0];  // a valid row, masked below
       xk[m] = *reinterpret_cast<const uint4*>(d.lev + (size_t)row * d.pitch + v0);
     }
+    // this wave's 4 nodes: their digest keys and every root's own levels,
+    // issued with the slot loads (their latency was exposed after the barrier)
+    const uint32_t nq = v0 + 4u * wave;
+    uint64_t kn[4] = {0ull, 0ull, 0ull, 0ull};
+    uint32_t Lmine = 0u;
+    if (nq < V && !d.late_keys) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) kn[b] = d.digest ? g.dkn[nq + b] : 0ull;  // zero past V
+      Lmine = lane < ng ? *reinterpret_cast<const uint32_t*>(d.lev + (size_t)s_own[lane] * d.pitch + nq) : 0u;
+    }
 #pragma unroll
     for (uint32_t m = 0; m < kDeriveTab / kBlock; ++m) {
       const uint32_t k = tid + m * kBlock, p = pk[m];
@@ -1826,14 +1836,13 @@ __global__ void __launch_bounds__(256) nh_wide_plan_kernel(DevGraph g, WidePlan 
       bw[3] = x.w;
     }
     __syncthreads();
-    const uint32_t nq = v0 + 4u * wave;  // this wave's 4 nodes
-    if (nq >= V) continue;                // wave-uniform (the next barrier is reached by all)
-    uint64_t kn[4];
+    if (nq >= V) continue;  // wave-uniform (the next barrier is reached by all)
+    if (d.late_keys) {
 #pragma unroll
-    for (int b = 0; b < 4; ++b) kn[b] = d.digest ? g.dkn[nq + b] : 0ull;  // zero past V
-    // every root's own levels at the 4 nodes in one trip: lane j holds root j's
-    const uint32_t Lmine =
-        lane < ng ? *reinterpret_cast<const uint32_t*>(d.lev + (size_t)s_own[lane] * d.pitch + nq) : 0u;
+      for (int b = 0; b < 4; ++b) kn[b] = d.digest ? g.dkn[nq + b] : 0ull;
+      Lmine = lane < ng ? *reinterpret_cast<const uint32_t*>(d.lev + (size_t)s_own[lane] * d.pitch + nq) : 0u;
+    }
+    // (Lmine: lane j holds root j's own levels at the 4 nodes)
     uint32_t word[4] = {0u, 0u, 0u, 0u}, Lp = 0xFFFFFFFFu;
     // the word key of each node's masked word, kept while the next root's
     // masked word is the same (the roots of a run mostly store equal words)
@@ -2170,6 +2179,9 @@ hipError_t launch_nh_derive(const DevGraph& g, const DeriveArgs& d0, hipStream_t
 hipError_t launch_wide_plan(const DevGraph& g, const WidePlan& p0, hipStream_t s) {
   WidePlan p = p0;
   if (p.n == 0) return hipSuccess;
+  // digest keys and own levels issued with the slot loads (OSPF_WIDE_LATE_KEYS:
+  // after the tile's barrier, as before; read per launch for in-process A/B)
+  p.late_keys = getenv("OSPF_WIDE_LATE_KEYS") ? 1u : 0u;
   if (p.W < 1 || p.W > 64 || p.pitch % kW3Tile) return hipErrorInvalidValue;
   p.tiles = (g.V + kW3Tile - 1) / kW3Tile;
   // ~4096 blocks; a chunk of >= 7 tiles covers a 128-B line of every row
