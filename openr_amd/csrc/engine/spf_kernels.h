@@ -272,6 +272,7 @@ struct WidePlan {
   ospf_digest* digest;    // [n] (zeroed by the launcher) or null
   uint32_t tiles, ctiles, chunks;  // set by the launcher (ctiles 0: its choice)
   uint32_t late_keys;     // set by the launcher: OSPF_WIDE_LATE_KEYS (A/B)
+  uint32_t st16;          // set by the launcher: records staged, 16-B stores (A/B)
 };
 hipError_t launch_wide_plan(const DevGraph& g, const WidePlan& p, hipStream_t s);
 

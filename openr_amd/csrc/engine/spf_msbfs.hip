@@ -1769,6 +1769,7 @@ __global__ void __launch_bounds__(256) nh_wide_plan_kernel(DevGraph g, WidePlan 
   __shared__ uint32_t s_pos[kDeriveTab];  // the run's slot table
   __shared__ uint32_t s_own[kWideG];
   __shared__ unsigned long long s_h[kWideG];
+  __shared__ uint4 s_rec[4][64];          // st16: a wave's 4 node records (4 W words)
   extern __shared__ uint32_t s_dyn[];     // keep [G][W], then the staged bytes [K][kW3Pitch]
   const uint32_t V = g.V, W = d.W, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint32_t NB = d.nruns * d.chunks, NB8 = NB / 8u * 8u, bb = blockIdx.x;
@@ -1843,6 +1844,11 @@ __global__ void __launch_bounds__(256) nh_wide_plan_kernel(DevGraph g, WidePlan 
       Lmine = lane < ng ? *reinterpret_cast<const uint32_t*>(d.lev + (size_t)s_own[lane] * d.pitch + nq) : 0u;
     }
     // (Lmine: lane j holds root j's own levels at the 4 nodes)
+    // st16 (wave-uniform): the 4 records (4 W words, 7 whole 128-B lines at
+    // W = 56) staged in LDS and stored as W 16-B pieces by one instruction,
+    // instead of 4 stores of W words whose 128-B lines straddle them
+    const bool st16 = d.st16 && (W & 3u) == 0 && nq + 4u <= V;
+    uint32_t* rec = reinterpret_cast<uint32_t*>(s_rec[wave]);
     uint32_t word[4] = {0u, 0u, 0u, 0u}, Lp = 0xFFFFFFFFu;
     // the word key of each node's masked word, kept while the next root's
     // masked word is the same (the roots of a run mostly store equal words)
@@ -1880,7 +1886,11 @@ __global__ void __launch_bounds__(256) nh_wide_plan_kernel(DevGraph g, WidePlan 
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         const uint32_t ow = word[b] & keep;
-        if (lane < W && nq + b < V) __builtin_nontemporal_store(ow, dst + (size_t)b * W);
+        if (st16) {
+          if (lane < W) rec[(size_t)b * W + lane] = ow;
+        } else if (lane < W && nq + b < V) {
+          __builtin_nontemporal_store(ow, dst + (size_t)b * W);
+        }
         if (d.digest && ow) {
           if (ow != kw_word[b]) {
             kw_word[b] = ow;
@@ -1888,6 +1898,11 @@ __global__ void __launch_bounds__(256) nh_wide_plan_kernel(DevGraph g, WidePlan 
           }
           h += kn[b] * kw_key[b];
         }
+      }
+      if (st16) {
+        __builtin_amdgcn_wave_barrier();
+        if (lane < W) store_row16(reinterpret_cast<uint4*>(dst - lane) + lane, s_rec[wave][lane]);
+        __builtin_amdgcn_wave_barrier();  // the records are rewritten by the next root
       }
       // few lanes hold a non-zero word: their terms go straight to the root's sum
       if (d.digest && h) atomicAdd(&s_h[j], (unsigned long long)h);
@@ -2182,6 +2197,11 @@ hipError_t launch_wide_plan(const DevGraph& g, const WidePlan& p0, hipStream_t s
   // digest keys and own levels issued with the slot loads (OSPF_WIDE_LATE_KEYS:
   // after the tile's barrier, as before; read per launch for in-process A/B)
   p.late_keys = getenv("OSPF_WIDE_LATE_KEYS") ? 1u : 0u;
+  // records staged in LDS, 16-B stores (OSPF_WIDE_ST16=0: 4 word stores per
+  // wave and root, as before; read per launch): 19.74 -> 19.21 ms per F100k
+  // sweep in one process, profiles/r06/l1_twin_levels_ab.txt (box 3)
+  const char* se = getenv("OSPF_WIDE_ST16");
+  p.st16 = (!se || atoi(se) != 0) ? 1u : 0u;
   if (p.W < 1 || p.W > 64 || p.pitch % kW3Tile) return hipErrorInvalidValue;
   p.tiles = (g.V + kW3Tile - 1) / kW3Tile;
   // ~4096 blocks; a chunk of >= 7 tiles covers a 128-B line of every row

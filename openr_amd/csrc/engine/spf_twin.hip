@@ -658,8 +658,16 @@ __device__ __forceinline__ uint32_t beq7(uint32_t x, uint32_t y) {
 // neighbours' positions (each root's sorted neighbour list walked by a
 // cursor) and stores 256 B of level row + 1 KB of dist row per instruction.
 // The distance part of each root's digest is stored (not added).
-template <bool PRE>
+// OPT bit 1 (CUR, the default): each root's next neighbour position cached
+// in a register, so the cursor tests read LDS only when a neighbour is due
+// (18.73 -> 18.53 ms per F100k sweep in one process, profiles/r06/
+// l1_twin_levels_ab.txt); bit 2 (NOHASH): diagnostic only -- the level-hash
+// terms and their key loads skipped (digests then differ): -0.3 ms, what the
+// hash costs. (Its terms as v_dot2_u32_u16 of level bytes and 16-bit key
+// pieces were exact but no faster: the launch waits on loads, not the VALU.)
+template <bool PRE, int OPT = 1>
 __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvPlan a) {
+  constexpr bool CUR = (OPT & 1) != 0, NOHASH = (OPT & 2) != 0;
   __shared__ uint32_t s_nb[kTwinLvG][kMaxK];  // usable neighbours (ascending), per root
   __shared__ uint32_t s_nnb[kTwinLvG], s_root[kTwinLvG], s_own[kTwinLvG], s_umask[kTwinLvG];
   __shared__ unsigned long long s_d[kWaves][kTwinLvG][3];
@@ -702,7 +710,7 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
       x[u] = (u < nu && ok) ? *reinterpret_cast<const uint32_t*>(a.lev + (size_t)urow[u] * a.pitch + v0)
                             : 0x7F7F7F7Fu;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) kd[q] = ok && v0 + q < V ? g.dkey[2ull * (v0 + q)] : 0ull;
+    for (int q = 0; q < 4; ++q) kd[q] = !NOHASH && ok && v0 + q < V ? g.dkey[2ull * (v0 + q)] : 0ull;
   };
   // distance part of each root's digest, per lane: reached, sum of dist
   // (u32: <= V / 64 nodes x 125 per lane), sum of dkey * level split in
@@ -716,6 +724,11 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
     cur[j] = 0u;
     bs[j] = bhh[j] = 0u;
     bl[j] = 0ull;
+  }
+  uint32_t nx[CUR ? kTwinLvG : 1];  // CUR: s_nb[j][cur[j]], kInf past the list
+  if constexpr (CUR) {
+#pragma unroll
+    for (uint32_t j = 0; j < kTwinLvG; ++j) nx[j] = (j < ng && s_nnb[j]) ? s_nb[j][0] : kInf;
   }
   const bool vec = (V & 3u) == 0;
   // PRE: the next chunk's rows loaded before this one is used (24 more
@@ -750,10 +763,23 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
       // neighbours in this chunk: level 2 (the list is ascending; chunks of a
       // wave ascend, so the cursor skips the other waves' chunks)
       const uint32_t nn = s_nnb[j];
-      while (cur[j] < nn && s_nb[j][cur[j]] < c0) ++cur[j];
-      while (cur[j] < nn && s_nb[j][cur[j]] < c0 + 256u) {
-        const uint32_t n = s_nb[j][cur[j]++], o = n - v0;
-        if (o < 4u) L = (L & ~(0xFFu << (8u * o))) | (2u << (8u * o));
+      if constexpr (CUR) {
+        while (nx[j] < c0) {
+          ++cur[j];
+          nx[j] = cur[j] < nn ? s_nb[j][cur[j]] : kInf;
+        }
+        while (nx[j] < c0 + 256u) {
+          const uint32_t o = nx[j] - v0;
+          if (o < 4u) L = (L & ~(0xFFu << (8u * o))) | (2u << (8u * o));
+          ++cur[j];
+          nx[j] = cur[j] < nn ? s_nb[j][cur[j]] : kInf;
+        }
+      } else {
+        while (cur[j] < nn && s_nb[j][cur[j]] < c0) ++cur[j];
+        while (cur[j] < nn && s_nb[j][cur[j]] < c0 + 256u) {
+          const uint32_t n = s_nb[j][cur[j]++], o = n - v0;
+          if (o < 4u) L = (L & ~(0xFFu << (8u * o))) | (2u << (8u * o));
+        }
       }
       const uint32_t off = s_root[j] - v0;
       if (off < 4u) L = (L & ~(0xFFu << (8u * off))) | (1u << (8u * off));
@@ -769,11 +795,13 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
       const uint32_t t2 = (Lv & 0x00FF00FFu) + ((Lv >> 8) & 0x00FF00FFu);
       br[j] += nv;
       bs[j] += (t2 & 0xFFFFu) + (t2 >> 16) - nv;
+      if constexpr (!NOHASH) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t l = (Lv >> (8 * q)) & 0xFFu;
-        bl[j] += (uint64_t)(uint32_t)kd[q] * l;
-        bhh[j] += (uint32_t)(kd[q] >> 32) * l;
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t l = (Lv >> (8 * q)) & 0xFFu;
+          bl[j] += (uint64_t)(uint32_t)kd[q] * l;
+          bhh[j] += (uint32_t)(kd[q] >> 32) * l;
+        }
       }
       if (a.dist && !(s_umask[j] >> 31)) {  // bit 31: the root's next-hop launch writes it
         uint32_t dv[4];
@@ -880,23 +908,31 @@ namespace ospf {
 hipError_t launch_twin_levels(const DevGraph& g, const TwinLvPlan& a0, hipStream_t s) {
   if (a0.n == 0) return hipSuccess;
   TwinLvPlan a = a0;
-  // parts of the chunk range per group: ~4096 blocks, >= 8 chunks each
+  // parts of the chunk range per group: ~2048 blocks, >= 8 chunks each
   const uint32_t nchunks = (a.pitch + 255u) / 256u;
-  static const uint32_t want = [] {
-    const char* e = getenv("OSPF_TWIN_LV_BLOCKS");
-    return e ? (uint32_t)std::max(1, atoi(e)) : 4096u;
-  }();
+  const char* be = getenv("OSPF_TWIN_LV_BLOCKS");  // read per launch: in-process A/B
+  const uint32_t want = be ? (uint32_t)std::max(1, atoi(be)) : 2048u;  // (4096: +0.05 ms at F100k)
   if (!a.parts)
     a.parts = std::max(1u, std::min(std::max(1u, nchunks / 8u), want / std::max(1u, a.ngroups)));
   if (a.lev_digest)
     hipLaunchKernelGGL(twin_zero_kernel, dim3((a.n + 255u) / 256u), dim3(256), 0, s, a.rinfo, a.n,
                        a.lev_digest);
-  // (OSPF_TWIN_PREFETCH=1: the software-pipelined variant, 3 waves per SIMD)
-  static const bool pre = getenv("OSPF_TWIN_PREFETCH") != nullptr;
+  // (OSPF_TWIN_PREFETCH=1: the software-pipelined variant, 3 waves per SIMD;
+  // OSPF_TWIN_LV_OPT: the OPT bits above, default 1; both read per launch)
+  const bool pre = getenv("OSPF_TWIN_PREFETCH") != nullptr;
+  const char* oe = getenv("OSPF_TWIN_LV_OPT");
+  const int opt = oe ? atoi(oe) & 3 : 1;
+  const dim3 grid(a.ngroups * a.parts);
   if (pre)
-    hipLaunchKernelGGL(twin_levels_kernel<true>, dim3(a.ngroups * a.parts), dim3(kBlock), 0, s, g, a);
+    hipLaunchKernelGGL((twin_levels_kernel<true, 1>), grid, dim3(kBlock), 0, s, g, a);
+  else if (opt == 0)
+    hipLaunchKernelGGL((twin_levels_kernel<false, 0>), grid, dim3(kBlock), 0, s, g, a);
+  else if (opt == 2)
+    hipLaunchKernelGGL((twin_levels_kernel<false, 2>), grid, dim3(kBlock), 0, s, g, a);
+  else if (opt == 3)
+    hipLaunchKernelGGL((twin_levels_kernel<false, 3>), grid, dim3(kBlock), 0, s, g, a);
   else
-    hipLaunchKernelGGL(twin_levels_kernel<false>, dim3(a.ngroups * a.parts), dim3(kBlock), 0, s, g, a);
+    hipLaunchKernelGGL((twin_levels_kernel<false, 1>), grid, dim3(kBlock), 0, s, g, a);
   return hipGetLastError();
 }
 }  // namespace ospf
