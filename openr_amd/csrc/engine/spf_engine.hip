@@ -1064,9 +1064,11 @@ int twin_lv_build(ospf_ctx* c, const std::vector<uint32_t>& roots, const std::ve
   if (out.grp.front() != 0 || out.grp.back() != n)
     return fail(c, OSPF_E_INVAL, "twin levels: group offsets must run 0 .. n");
   const uint32_t ng = (uint32_t)out.grp.size() - 1;
-  for (uint32_t gi = 0; gi < ng; ++gi)
+  for (uint32_t gi = 0; gi < ng; ++gi) {
     if (out.grp[gi + 1] < out.grp[gi] || out.grp[gi + 1] - out.grp[gi] > ospf::kTwinLvG)
       return fail(c, OSPF_E_RANGE, "twin levels: a group of more than 8 roots");
+    out.gmax = std::max(out.gmax, out.grp[gi + 1] - out.grp[gi]);
+  }
   // two passes on host threads: each root's neighbour-list length, then per
   // group the lists, class rows and masks at their offsets
   std::atomic<int> bad{0};  // 1 no row, 2 no class row, 3 > 128 neighbours, 4 > 16 class rows
@@ -2362,6 +2364,7 @@ int ospf_twin_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n,
   ospf::TwinLvPlan a{};
   a.n = n;
   a.ngroups = (uint32_t)h.grp.size() - 1;
+  a.gsz = h.gmax;
   a.rinfo = (const uint4*)p;
   HIPCHK(c, hipMemcpy(p, h.rinfo.data(), b2, hipMemcpyHostToDevice));
   p += b2;

@@ -198,6 +198,7 @@ void release_stream_scratch(ospf_ctx* c, void* stream);
 struct TwinLvHost {
   std::vector<uint32_t> grp, grow, nbo, nbl;
   std::vector<uint4> rinfo;
+  uint32_t gmax = 0;  // largest group
 };
 int twin_lv_build(ospf_ctx* c, const std::vector<uint32_t>& roots, const std::vector<uint32_t>& groups,
                   const std::vector<uint32_t>& pos, const std::vector<uint32_t>& cls,

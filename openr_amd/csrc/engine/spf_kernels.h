@@ -538,6 +538,7 @@ hipError_t launch_nh_derive_twin(const DevGraph& g, const TwinArgs& a, hipStream
 constexpr uint32_t kTwinLvG = 8;
 struct TwinLvPlan {
   uint32_t n, ngroups;
+  uint32_t gsz;           // largest group (0: kTwinLvG); <= 4 takes the 4-root kernel
   const uint32_t* grp;    // [ngroups + 1] root offsets
   const uint32_t* grow;   // [ngroups][kTwinMaxC] class rows (level-row positions; kInf unused)
   const uint4* rinfo;     // [n] {root, own row, mask over the group's class rows, nbl offset}

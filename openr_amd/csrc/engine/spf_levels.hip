@@ -106,11 +106,13 @@ __device__ __forceinline__ void set_lev(const LvArgs& a, const WB& b, uint32_t v
 }
 
 // ---------------------------------------------------------------- init
-// One wave per root: level 0 (the root) and level 1 (its usable neighbours).
-// Roots of a batch may share nodes: atomics.
+// One block per root: level 0 (the root) and level 1 (its usable
+// neighbours), the row strided over the block (a spine's 1,781 entries in 7
+// steps of returning atomics instead of a wave's 28: 0.12 ms at F100k for the
+// launch, bound by its spine roots). Roots of a batch may share nodes: atomics.
 __global__ void __launch_bounds__(256) lv_init_kernel(DevGraph g, LvArgs a) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t slot = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t slot = blockIdx.x;
   const uint32_t vbl = slot / kRoots, bit = slot % kRoots;
   if (vbl >= a.nb) return;
   const WB b(a, vbl, g.V);
@@ -118,7 +120,7 @@ __global__ void __launch_bounds__(256) lv_init_kernel(DevGraph g, LvArgs a) {
   if (rix >= a.n) return;
   const uint32_t V = g.V, s = a.roots[rix];
   if (s >= V) {
-    if (lane == 0) atomicOr(a.err, 64u);
+    if (tid == 0) atomicOr(a.err, 64u);
     return;
   }
   const uint32_t wi = bit >> 6;
@@ -132,14 +134,14 @@ __global__ void __launch_bounds__(256) lv_init_kernel(DevGraph g, LvArgs a) {
   auto or_word = [&](uint4* p, uint32_t v) {
     return atomicOr(reinterpret_cast<unsigned long long*>(p + v) + wi, bm);
   };
-  if (lane == 0) {
+  if (tid == 0) {
     or_word(b.seen, s);
     lev_put(s, 1u);
   }
   uint4* f1 = b.front(a, 1);
   bool any = false;
   uint32_t mass = 0;
-  for (uint32_t e = g.row_ptr[s] + lane; e < g.row_ptr[s + 1]; e += kWave) {
+  for (uint32_t e = g.row_ptr[s] + tid; e < g.row_ptr[s + 1]; e += kBlock) {
     const uint32_t cx = g.colx[e];
     if ((cx & kDown) || cx == s) continue;
     or_word(b.seen, cx);
@@ -505,7 +507,7 @@ __global__ void __launch_bounds__(256) lv_rows_kernel(DevGraph g, LvArgs a) {
 }  // namespace
 
 hipError_t launch_levels128_traverse(const DevGraph& g, const LvArgs& a, hipStream_t s) {
-  const uint32_t init_blocks = (a.nb * kRoots + kWaves - 1) / kWaves;
+  const uint32_t init_blocks = a.nb * kRoots;
   hipLaunchKernelGGL(lv_init_kernel, dim3(init_blocks), dim3(kBlock), 0, s, g, a);
   const uint32_t chunks = (g.V + kBlock - 1) / kBlock;
   const uint32_t bigblocks = (g.nbig + kWaves - 1) / kWaves;

@@ -989,8 +989,11 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
   for (uint32_t i = 0; i < nc; ++i) pos[clo[i]] = i;
   for (uint32_t i = 0; i < nd; ++i) pos[drv[i]] = nc + i;
   // twin-levels groups: <= 8 consecutive derived rows (a pod's fabric
-  // switches) reading <= kTwinMaxC class rows together
+  // switches) reading <= kTwinMaxC class rows together (OSPF_TWIN_LV_G=4:
+  // <= 4 rows, the launch's 4-root kernel with half the per-root registers)
   std::vector<uint32_t> dgo{0u};
+  const char* tge = getenv("OSPF_TWIN_LV_G");
+  const uint32_t tlg = tge && atoi(tge) == 4 ? 4u : ospf::kTwinLvG;
   if (nd) {
     std::vector<uint32_t> cl;
     for (uint32_t i = 0; i < nd; ++i) {
@@ -999,7 +1002,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       u.insert(u.end(), cs.begin(), cs.end());
       std::sort(u.begin(), u.end());
       u.erase(std::unique(u.begin(), u.end()), u.end());
-      if (i > dgo.back() && (i - dgo.back() >= 8u || u.size() > ospf::kTwinMaxC)) {
+      if (i > dgo.back() && (i - dgo.back() >= tlg || u.size() > ospf::kTwinMaxC)) {
         dgo.push_back(i);
         u = cs;
       }
@@ -1148,6 +1151,7 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
       return rc;
     plan.n = n;
     plan.ngroups = (uint32_t)h.grp.size() - 1;
+    plan.gsz = h.gmax;
     plan.grp = d_grp2;
     plan.grow = d_grow;
     plan.rinfo = d_rinfo;

@@ -665,19 +665,19 @@ __device__ __forceinline__ uint32_t beq7(uint32_t x, uint32_t y) {
 // terms and their key loads skipped (digests then differ): -0.3 ms, what the
 // hash costs. (Its terms as v_dot2_u32_u16 of level bytes and 16-bit key
 // pieces were exact but no faster: the launch waits on loads, not the VALU.)
-template <bool PRE, int OPT = 1>
+template <bool PRE, int OPT = 1, uint32_t G = kTwinLvG>
 __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvPlan a) {
   constexpr bool CUR = (OPT & 1) != 0, NOHASH = (OPT & 2) != 0;
-  __shared__ uint32_t s_nb[kTwinLvG][kMaxK];  // usable neighbours (ascending), per root
-  __shared__ uint32_t s_nnb[kTwinLvG], s_root[kTwinLvG], s_own[kTwinLvG], s_umask[kTwinLvG];
-  __shared__ unsigned long long s_d[kWaves][kTwinLvG][3];
+  __shared__ uint32_t s_nb[G][kMaxK];  // usable neighbours (ascending), per root
+  __shared__ uint32_t s_nnb[G], s_root[G], s_own[G], s_umask[G];
+  __shared__ unsigned long long s_d[kWaves][G][3];
   const uint32_t V = g.V, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   // block = (group, part of the chunk range); XCD-aware order over the items
   const uint32_t NB = a.ngroups * a.parts, B8 = NB / 8u * 8u, b = blockIdx.x;
   const uint32_t item = b < B8 ? (b % 8u) * (B8 / 8u) + b / 8u : b;
   const uint32_t gi = item / a.parts, part = item % a.parts;
   const uint32_t i0 = a.grp[gi];
-  const uint32_t ng = min(kTwinLvG, a.grp[gi + 1] - i0);
+  const uint32_t ng = min(G, a.grp[gi + 1] - i0);
   if (tid < ng) {
     const uint4 ri = a.rinfo[i0 + tid];
     s_root[tid] = ri.x;
@@ -716,19 +716,19 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
   // (u32: <= V / 64 nodes x 125 per lane), sum of dkey * level split in
   // sum(dkey_lo * level) (u64, one v_mad_u64_u32 a node) and
   // sum(dkey_hi * level) mod 2^32 (the hash is mod 2^64)
-  uint32_t br[kTwinLvG], cur[kTwinLvG], bs[kTwinLvG], bhh[kTwinLvG];
-  uint64_t bl[kTwinLvG];
+  uint32_t br[G], cur[G], bs[G], bhh[G];
+  uint64_t bl[G];
 #pragma unroll
-  for (uint32_t j = 0; j < kTwinLvG; ++j) {
+  for (uint32_t j = 0; j < G; ++j) {
     br[j] = 0u;
     cur[j] = 0u;
     bs[j] = bhh[j] = 0u;
     bl[j] = 0ull;
   }
-  uint32_t nx[CUR ? kTwinLvG : 1];  // CUR: s_nb[j][cur[j]], kInf past the list
+  uint32_t nx[CUR ? G : 1];  // CUR: s_nb[j][cur[j]], kInf past the list
   if constexpr (CUR) {
 #pragma unroll
-    for (uint32_t j = 0; j < kTwinLvG; ++j) nx[j] = (j < ng && s_nnb[j]) ? s_nb[j][0] : kInf;
+    for (uint32_t j = 0; j < G; ++j) nx[j] = (j < ng && s_nnb[j]) ? s_nb[j][0] : kInf;
   }
   const bool vec = (V & 3u) == 0;
   // PRE: the next chunk's rows loaded before this one is used (24 more
@@ -751,7 +751,7 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
     }
     if (v0 >= a.pitch) continue;  // no wave-level work below (cursors are per wave: see skip)
 #pragma unroll
-    for (uint32_t j = 0; j < kTwinLvG; ++j) {
+    for (uint32_t j = 0; j < G; ++j) {
       if (j >= ng) break;
       // the root's class rows (a scalar mask: untaken rows cost a branch)
       const uint32_t mask = __builtin_amdgcn_readfirstlane(s_umask[j]);
@@ -823,7 +823,7 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
   }
   if (!a.lev_digest) return;
 #pragma unroll
-  for (uint32_t j = 0; j < kTwinLvG; ++j) {
+  for (uint32_t j = 0; j < G; ++j) {
     uint64_t r64 = br[j], s64 = bs[j], h64 = bl[j] + ((uint64_t)bhh[j] << 32);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -923,16 +923,24 @@ hipError_t launch_twin_levels(const DevGraph& g, const TwinLvPlan& a0, hipStream
   const char* oe = getenv("OSPF_TWIN_LV_OPT");
   const int opt = oe ? atoi(oe) & 3 : 1;
   const dim3 grid(a.ngroups * a.parts);
-  if (pre)
-    hipLaunchKernelGGL((twin_levels_kernel<true, 1>), grid, dim3(kBlock), 0, s, g, a);
-  else if (opt == 0)
-    hipLaunchKernelGGL((twin_levels_kernel<false, 0>), grid, dim3(kBlock), 0, s, g, a);
-  else if (opt == 2)
-    hipLaunchKernelGGL((twin_levels_kernel<false, 2>), grid, dim3(kBlock), 0, s, g, a);
-  else if (opt == 3)
-    hipLaunchKernelGGL((twin_levels_kernel<false, 3>), grid, dim3(kBlock), 0, s, g, a);
-  else
-    hipLaunchKernelGGL((twin_levels_kernel<false, 1>), grid, dim3(kBlock), 0, s, g, a);
+  // groups of <= 4 roots (OSPF_TWIN_LV_G=4 at plan time): the 4-root kernel
+#define OSPF_TWIN_LV(GG)                                                                 \
+  if (pre)                                                                               \
+    hipLaunchKernelGGL((twin_levels_kernel<true, 1, GG>), grid, dim3(kBlock), 0, s, g, a);  \
+  else if (opt == 0)                                                                     \
+    hipLaunchKernelGGL((twin_levels_kernel<false, 0, GG>), grid, dim3(kBlock), 0, s, g, a); \
+  else if (opt == 2)                                                                     \
+    hipLaunchKernelGGL((twin_levels_kernel<false, 2, GG>), grid, dim3(kBlock), 0, s, g, a); \
+  else if (opt == 3)                                                                     \
+    hipLaunchKernelGGL((twin_levels_kernel<false, 3, GG>), grid, dim3(kBlock), 0, s, g, a); \
+  else                                                                                   \
+    hipLaunchKernelGGL((twin_levels_kernel<false, 1, GG>), grid, dim3(kBlock), 0, s, g, a);
+  if (a.gsz && a.gsz <= 4u) {
+    OSPF_TWIN_LV(4u)
+  } else {
+    OSPF_TWIN_LV(kTwinLvG)
+  }
+#undef OSPF_TWIN_LV
   return hipGetLastError();
 }
 }  // namespace ospf
