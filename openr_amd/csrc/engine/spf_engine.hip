@@ -2065,7 +2065,7 @@ int ospf_levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t f
 namespace ospf_int {
 int levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t flags,
                uint32_t* d_dist, uint32_t dist_pitch, uint8_t* d_lev, uint32_t lev_pitch,
-               ospf_digest* d_lev_digest, void* stream) {
+               ospf_digest* d_lev_digest, void* stream, uint32_t depth_cap, uint32_t* d_maxd) {
   if (!c) return OSPF_E_INVAL;
   if (!c->loaded) return fail(c, OSPF_E_NOGRAPH, "no graph loaded");
   if (n == 0) return OSPF_OK;
@@ -2102,7 +2102,8 @@ int levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t flags,
     a.roots = d_roots;
     a.n = n;
     a.lmax = lmax;
-    a.dbound = c->depth_bound;
+    a.dbound = depth_cap ? std::min(depth_cap, c->depth_bound) : c->depth_bound;
+    a.maxd = d_maxd;
     a.push_div = 16;
     if (const char* e = getenv("OSPF_MS_PUSH_DIV")) a.push_div = (uint32_t)std::max(0, atoi(e));
     a.masked = 0;

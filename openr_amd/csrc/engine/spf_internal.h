@@ -216,9 +216,13 @@ int nh_derive_twin_launch(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint
                           uint32_t nh_pitch = 0);
 // ospf_levels_dev / ospf_leaf_derive2_dev with row pitches (words; 0 = V)
 // for the dist and next-hop rows: the sweep keeps its rows 128-B aligned
+// (depth_cap: levels launched 1 .. min(cap, depth bound) when non-zero -- a
+// sweep's seed BFS at the depth its first run reached; d_maxd: that depth,
+// atomicMax'ed by the rows kernel)
 int levels_dev(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, uint32_t flags,
                uint32_t* d_dist, uint32_t dist_pitch, uint8_t* d_lev, uint32_t lev_pitch,
-               ospf_digest* d_lev_digest, void* stream);
+               ospf_digest* d_lev_digest, void* stream, uint32_t depth_cap = 0,
+               uint32_t* d_maxd = nullptr);
 int leaf_derive(ospf_ctx* c, const uint32_t* d_roots, uint32_t n, const uint32_t* d_groups,
                 uint32_t n_groups, uint32_t max_root_neighbors, uint8_t* d_lev,
                 uint32_t lev_pitch, const uint32_t* d_pos, const uint32_t* d_lev_out,

@@ -299,6 +299,7 @@ struct LvArgs {
   uint32_t lev_pitch;
   ospf_digest* digest;      // [n] distance parts (zeroed by the caller) or null
   uint32_t* err;            // bit 8: depth bound too small, 64: bad root
+  uint32_t* maxd;           // optional: max over batches of the deepest non-empty level
 };
 // a round = init + levels (traverse), then the rows kernel; rounds of
 // different state buffers may overlap (rows of round k beside the levels of

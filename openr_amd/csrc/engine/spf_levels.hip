@@ -389,7 +389,15 @@ __global__ void __launch_bounds__(256) lv_rows_kernel(DevGraph g, LvArgs a) {
   const WB b(a, vbl, g.V);
   const uint32_t V = g.V, tid = threadIdx.x, q = tid & 63u, rg = tid >> 6;
   const uint32_t vb0 = (blockIdx.x / per) * 512u;
-  if (vb0 == 0 && h == 0 && tid == 0 && a.found[vbl * a.lmax + a.dbound + 1]) atomicOr(a.err, 8u);
+  if (vb0 == 0 && h == 0 && tid == 0) {
+    if (a.found[vbl * a.lmax + a.dbound + 1]) atomicOr(a.err, 8u);
+    if (a.maxd) {  // the deepest non-empty level (a sweep caps its captured launches there)
+      uint32_t dm = 0;
+      for (uint32_t d = 1; d <= a.dbound + 1; ++d)
+        if (a.found[vbl * a.lmax + d]) dm = d;
+      atomicMax(a.maxd, dm);
+    }
+  }
   const uint32_t base = b.rix0 + 64u * h;  // first root of this half
   if (base >= a.n) return;                  // block-uniform
   const uint32_t nr = min(64u, a.n - base);

@@ -2199,7 +2199,7 @@ hipError_t launch_wide_plan(const DevGraph& g, const WidePlan& p0, hipStream_t s
   p.late_keys = getenv("OSPF_WIDE_LATE_KEYS") ? 1u : 0u;
   // records staged in LDS, 16-B stores (OSPF_WIDE_ST16=0: 4 word stores per
   // wave and root, as before; read per launch): 19.74 -> 19.21 ms per F100k
-  // sweep in one process, profiles/r06/l1_twin_levels_ab.txt (box 3)
+  // sweep in one process, profiles/r06/l1_late_kernel_ab.txt (box 3)
   const char* se = getenv("OSPF_WIDE_ST16");
   p.st16 = (!se || atoi(se) != 0) ? 1u : 0u;
   if (p.W < 1 || p.W > 64 || p.pitch % kW3Tile) return hipErrorInvalidValue;

@@ -250,6 +250,10 @@ struct ospf_sweep {
   // allocation's rows fall in the memory channels (the probe's two patterns
   // swap places from one allocation to the next)
   int leaf_order = 0;
+  // the seed BFS's deepest level in the first run (device word), and the
+  // level launches the HIP graph captures (0: the graph's transit-depth bound)
+  uint32_t* d_lv_maxd = nullptr;
+  uint32_t lv_cap = 0;
 };
 
 namespace {
@@ -1117,8 +1121,10 @@ int plan_derive(ospf_sweep* s, const Facts& f, const std::vector<uint32_t>& mine
     lv.record = ev_a;
     lv.n_roots = nc;
     lv.comp = (uint64_t)nc * 4ull * V + ((nc + 127) / 128) * scan_bytes(c, false);
+    if ((rc = upload(s, &s->d_lv_maxd, std::vector<uint32_t>{0u}))) return rc;
     lv.fn = [=](hipStream_t st) {
-      return ospf_int::levels_dev(c, d_clo, nc, hop, dist, DP, lev, pitch, ldg, st);
+      return ospf_int::levels_dev(c, d_clo, nc, hop, dist, DP, lev, pitch, ldg, st, s->lv_cap,
+                                  s->d_lv_maxd);
     };
     s->step_comp += lv.comp;
     s->units.push_back(lv);
@@ -2861,6 +2867,17 @@ int ospf_sweep_create(ospf_ctx* c, const ospf_sweep_opts* o, ospf_sweep** out) {
   if ((rc = ospf_sync(c, s->streams[0]))) return bail(rc);
   s->ran = true;
   if ((rc = pick_leaf_order(s))) return bail(rc);
+  // the graph's seed BFS launches levels 1 .. the depth the eager run reached
+  // (deterministic for this graph version; a deeper level would set error
+  // bit 8 in the rows kernel) instead of the transit-depth bound (10 at
+  // F100k, where the seeds' BFS ends at 4: 14 empty level launches).
+  // OSPF_SWEEP_FULL_DEPTH keeps the bound.
+  if (s->d_lv_maxd && !getenv("OSPF_SWEEP_FULL_DEPTH")) {
+    uint32_t dm = 0;
+    if (hipMemcpy(&dm, s->d_lv_maxd, 4, hipMemcpyDeviceToHost) != hipSuccess)
+      return bail(fail(c, OSPF_E_DEVICE, "sweep: seed BFS depth readback"));
+    if (dm >= 1 && dm < c->depth_bound) s->lv_cap = dm;
+  }
   if (o->hip_graph) {
     hipStream_t m = s->streams[0];
     hipGraph_t g = nullptr;

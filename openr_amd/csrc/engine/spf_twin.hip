@@ -661,7 +661,7 @@ __device__ __forceinline__ uint32_t beq7(uint32_t x, uint32_t y) {
 // OPT bit 1 (CUR, the default): each root's next neighbour position cached
 // in a register, so the cursor tests read LDS only when a neighbour is due
 // (18.73 -> 18.53 ms per F100k sweep in one process, profiles/r06/
-// l1_twin_levels_ab.txt); bit 2 (NOHASH): diagnostic only -- the level-hash
+// l1_late_kernel_ab.txt); bit 2 (NOHASH): diagnostic only -- the level-hash
 // terms and their key loads skipped (digests then differ): -0.3 ms, what the
 // hash costs. (Its terms as v_dot2_u32_u16 of level bytes and 16-bit key
 // pieces were exact but no faster: the launch waits on loads, not the VALU.)
