@@ -652,9 +652,40 @@ const LinkState::Csr& LinkState::snapshot() {
   };
   ++topoStats_.snapshots;
   Csr c;
-  c.names.reserve(adjDbs_.size());
-  for (const auto& kv : adjDbs_) c.names.push_back(kv.first);
-  parallelSort(c.names);
+  {
+    // sorted by (first 8 bytes big-endian, then the whole name): 16-B keys
+    // move and compare as integers (the string sort's merges had moved and
+    // compared strings); the order is the names' byte-wise order either way
+    struct NameKey {
+      uint64_t k;
+      const std::string* s;
+      bool operator<(const NameKey& o) const { return k != o.k ? k < o.k : *s < *o.s; }
+    };
+    // the map's buckets walked on threads (its nodes are scattered on the
+    // heap: a serial walk was ~14 ms of cache misses at 100k nodes)
+    constexpr uint32_t kParts = 64;
+    const size_t nbk = adjDbs_.bucket_count();
+    std::vector<std::vector<NameKey>> part(kParts);
+    parallelFor(kParts, [&](uint32_t lo, uint32_t hi) {
+      for (uint32_t p = lo; p < hi; ++p) {
+        auto& out = part[p];
+        for (size_t b = nbk * p / kParts; b < nbk * (p + 1) / kParts; ++b)
+          for (auto it = adjDbs_.begin(b); it != adjDbs_.end(b); ++it) {
+            const std::string& n = it->first;
+            uint64_t k = 0;
+            for (size_t i = 0; i < std::min<size_t>(8, n.size()); ++i)
+              k |= (uint64_t)(uint8_t)n[i] << (56 - 8 * i);
+            out.push_back({k, &n});
+          }
+      }
+    }, 1);
+    std::vector<NameKey> keyed;
+    keyed.reserve(adjDbs_.size());
+    for (auto& v : part) keyed.insert(keyed.end(), v.begin(), v.end());
+    parallelSort(keyed);
+    c.names.reserve(keyed.size());
+    for (const auto& x : keyed) c.names.push_back(*x.s);
+  }
   lap("names sorted");
   c.ids.reserve(c.names.size() * 2);
   for (uint32_t i = 0; i < c.names.size(); ++i) c.ids.emplace(c.names[i], i);

@@ -665,9 +665,14 @@ __device__ __forceinline__ uint32_t beq7(uint32_t x, uint32_t y) {
 // terms and their key loads skipped (digests then differ): -0.3 ms, what the
 // hash costs. (Its terms as v_dot2_u32_u16 of level bytes and 16-bit key
 // pieces were exact but no faster: the launch waits on loads, not the VALU.)
-template <bool PRE, int OPT = 1, uint32_t G = kTwinLvG>
+// RW: each wave takes G / 4 of the group's roots over every chunk of the
+// block's range (loading only its roots' class rows) instead of every root
+// over a quarter of the chunks: a quarter of the per-root registers, so more
+// waves per SIMD hide the row and key loads' latency.
+template <bool PRE, int OPT = 1, uint32_t G = kTwinLvG, bool RW = false>
 __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvPlan a) {
   constexpr bool CUR = (OPT & 1) != 0, NOHASH = (OPT & 2) != 0;
+  constexpr uint32_t NR = RW ? G / kWaves : G;  // roots per wave
   __shared__ uint32_t s_nb[G][kMaxK];  // usable neighbours (ascending), per root
   __shared__ uint32_t s_nnb[G], s_root[G], s_own[G], s_umask[G];
   __shared__ unsigned long long s_d[kWaves][G][3];
@@ -678,6 +683,7 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
   const uint32_t gi = item / a.parts, part = item % a.parts;
   const uint32_t i0 = a.grp[gi];
   const uint32_t ng = min(G, a.grp[gi + 1] - i0);
+  if (RW && tid < kWaves * G * 3) (&s_d[0][0][0])[tid] = 0ull;  // owners write theirs
   if (tid < ng) {
     const uint4 ri = a.rinfo[i0 + tid];
     s_root[tid] = ri.x;
@@ -701,14 +707,24 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
   const uint32_t nchunks = (a.pitch + 255u) / 256u;
   const uint32_t cb = (uint32_t)((uint64_t)part * nchunks / a.parts);
   const uint32_t ce = (uint32_t)((uint64_t)(part + 1) * nchunks / a.parts);
+  const uint32_t j0 = RW ? wave * NR : 0u;  // this wave's first root
+  uint32_t lmask = ~0u;  // class rows this wave loads
+  if constexpr (RW) {
+    lmask = 0u;
+#pragma unroll
+    for (uint32_t jj = 0; jj < NR; ++jj)
+      if (j0 + jj < ng) lmask |= s_umask[j0 + jj];
+    lmask = __builtin_amdgcn_readfirstlane(lmask);
+  }
   // the next chunk's rows and distance keys are loaded before this one is used
   auto load_x = [&](uint32_t c, uint32_t* x, uint64_t* kd) {
     const uint32_t v0 = c * 256u + 4u * lane;
     const bool ok = c < ce && v0 < a.pitch;
 #pragma unroll
     for (uint32_t u = 0; u < kTwinMaxC; ++u)
-      x[u] = (u < nu && ok) ? *reinterpret_cast<const uint32_t*>(a.lev + (size_t)urow[u] * a.pitch + v0)
-                            : 0x7F7F7F7Fu;
+      x[u] = (u < nu && ok && ((lmask >> u) & 1u))
+                 ? *reinterpret_cast<const uint32_t*>(a.lev + (size_t)urow[u] * a.pitch + v0)
+                 : 0x7F7F7F7Fu;
 #pragma unroll
     for (int q = 0; q < 4; ++q) kd[q] = !NOHASH && ok && v0 + q < V ? g.dkey[2ull * (v0 + q)] : 0ull;
   };
@@ -716,27 +732,29 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
   // (u32: <= V / 64 nodes x 125 per lane), sum of dkey * level split in
   // sum(dkey_lo * level) (u64, one v_mad_u64_u32 a node) and
   // sum(dkey_hi * level) mod 2^32 (the hash is mod 2^64)
-  uint32_t br[G], cur[G], bs[G], bhh[G];
-  uint64_t bl[G];
+  uint32_t br[NR], cur[NR], bs[NR], bhh[NR];
+  uint64_t bl[NR];
 #pragma unroll
-  for (uint32_t j = 0; j < G; ++j) {
+  for (uint32_t j = 0; j < NR; ++j) {
     br[j] = 0u;
     cur[j] = 0u;
     bs[j] = bhh[j] = 0u;
     bl[j] = 0ull;
   }
-  uint32_t nx[CUR ? G : 1];  // CUR: s_nb[j][cur[j]], kInf past the list
+  uint32_t nx[CUR ? NR : 1];  // CUR: s_nb[j][cur[j]], kInf past the list
   if constexpr (CUR) {
 #pragma unroll
-    for (uint32_t j = 0; j < G; ++j) nx[j] = (j < ng && s_nnb[j]) ? s_nb[j][0] : kInf;
+    for (uint32_t j = 0; j < NR; ++j) nx[j] = (j0 + j < ng && s_nnb[j0 + j]) ? s_nb[j0 + j][0] : kInf;
   }
   const bool vec = (V & 3u) == 0;
   // PRE: the next chunk's rows loaded before this one is used (24 more
   // registers: 3 waves per SIMD instead of 4)
   uint32_t xn[PRE ? kTwinMaxC : 1];
   uint64_t kdn[4];
-  if constexpr (PRE) load_x(cb + wave, xn, kdn);
-  for (uint32_t c = cb + wave; c < ce; c += kWaves) {
+  constexpr uint32_t cstep = RW ? 1u : kWaves;
+  const uint32_t cfirst = RW ? cb : cb + wave;
+  if constexpr (PRE) load_x(cfirst, xn, kdn);
+  for (uint32_t c = cfirst; c < ce; c += cstep) {
     const uint32_t c0 = c * 256u, v0 = c0 + 4u * lane;
     uint32_t x[kTwinMaxC];
     uint64_t kd[4];
@@ -745,16 +763,17 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
       for (uint32_t u = 0; u < kTwinMaxC; ++u) x[u] = xn[u];
 #pragma unroll
       for (int q = 0; q < 4; ++q) kd[q] = kdn[q];
-      load_x(c + kWaves, xn, kdn);
+      load_x(c + cstep, xn, kdn);
     } else {
       load_x(c, x, kd);
     }
     if (v0 >= a.pitch) continue;  // no wave-level work below (cursors are per wave: see skip)
 #pragma unroll
-    for (uint32_t j = 0; j < G; ++j) {
-      if (j >= ng) break;
+    for (uint32_t j = 0; j < NR; ++j) {
+      const uint32_t jr = j0 + j;  // the root's index in the group
+      if (jr >= ng) break;
       // the root's class rows (a scalar mask: untaken rows cost a branch)
-      const uint32_t mask = __builtin_amdgcn_readfirstlane(s_umask[j]);
+      const uint32_t mask = __builtin_amdgcn_readfirstlane(s_umask[jr]);
       uint32_t m = 0x7F7F7F7Fu;
 #pragma unroll
       for (uint32_t u = 0; u < kTwinMaxC; ++u)
@@ -762,28 +781,28 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
       uint32_t L = (m + 0x01010101u) - (((m + 0x01010101u) & 0x80808080u) >> 7);
       // neighbours in this chunk: level 2 (the list is ascending; chunks of a
       // wave ascend, so the cursor skips the other waves' chunks)
-      const uint32_t nn = s_nnb[j];
+      const uint32_t nn = s_nnb[jr];
       if constexpr (CUR) {
         while (nx[j] < c0) {
           ++cur[j];
-          nx[j] = cur[j] < nn ? s_nb[j][cur[j]] : kInf;
+          nx[j] = cur[j] < nn ? s_nb[jr][cur[j]] : kInf;
         }
         while (nx[j] < c0 + 256u) {
           const uint32_t o = nx[j] - v0;
           if (o < 4u) L = (L & ~(0xFFu << (8u * o))) | (2u << (8u * o));
           ++cur[j];
-          nx[j] = cur[j] < nn ? s_nb[j][cur[j]] : kInf;
+          nx[j] = cur[j] < nn ? s_nb[jr][cur[j]] : kInf;
         }
       } else {
-        while (cur[j] < nn && s_nb[j][cur[j]] < c0) ++cur[j];
-        while (cur[j] < nn && s_nb[j][cur[j]] < c0 + 256u) {
-          const uint32_t n = s_nb[j][cur[j]++], o = n - v0;
+        while (cur[j] < nn && s_nb[jr][cur[j]] < c0) ++cur[j];
+        while (cur[j] < nn && s_nb[jr][cur[j]] < c0 + 256u) {
+          const uint32_t n = s_nb[jr][cur[j]++], o = n - v0;
           if (o < 4u) L = (L & ~(0xFFu << (8u * o))) | (2u << (8u * o));
         }
       }
-      const uint32_t off = s_root[j] - v0;
+      const uint32_t off = s_root[jr] - v0;
       if (off < 4u) L = (L & ~(0xFFu << (8u * off))) | (1u << (8u * off));
-      const uint32_t own = s_own[j];
+      const uint32_t own = s_own[jr];
       __builtin_nontemporal_store(L, reinterpret_cast<uint32_t*>(a.lev + (size_t)own * a.pitch + v0));
       if (v0 >= V) continue;
       // SWAR over the 4 nodes: reached bytes (< 0x7F, node < V), their
@@ -803,7 +822,7 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
           bhh[j] += (uint32_t)(kd[q] >> 32) * l;
         }
       }
-      if (a.dist && !(s_umask[j] >> 31)) {  // bit 31: the root's next-hop launch writes it
+      if (a.dist && !(s_umask[jr] >> 31)) {  // bit 31: the root's next-hop launch writes it
         uint32_t dv[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -823,7 +842,7 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
   }
   if (!a.lev_digest) return;
 #pragma unroll
-  for (uint32_t j = 0; j < G; ++j) {
+  for (uint32_t j = 0; j < NR; ++j) {
     uint64_t r64 = br[j], s64 = bs[j], h64 = bl[j] + ((uint64_t)bhh[j] << 32);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -831,10 +850,10 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
       s64 += shfl_xor64(s64, o);
       h64 += shfl_xor64(h64, o);
     }
-    if (lane == 0) {
-      s_d[wave][j][0] = r64;
-      s_d[wave][j][1] = s64;
-      s_d[wave][j][2] = h64;
+    if (lane == 0 && j0 + j < G) {
+      s_d[wave][j0 + j][0] = r64;
+      s_d[wave][j0 + j][1] = s64;
+      s_d[wave][j0 + j][2] = h64;
     }
   }
   __syncthreads();
@@ -935,7 +954,14 @@ hipError_t launch_twin_levels(const DevGraph& g, const TwinLvPlan& a0, hipStream
     hipLaunchKernelGGL((twin_levels_kernel<false, 3, GG>), grid, dim3(kBlock), 0, s, g, a); \
   else                                                                                   \
     hipLaunchKernelGGL((twin_levels_kernel<false, 1, GG>), grid, dim3(kBlock), 0, s, g, a);
-  if (a.gsz && a.gsz <= 4u) {
+  // OSPF_TWIN_LV_RW=1: two roots a wave over every chunk (RW above)
+  const char* rwe = getenv("OSPF_TWIN_LV_RW");
+  const int rw = rwe ? atoi(rwe) : 0;
+  if (rw == 1 && !pre && opt == 1 && !(a.gsz && a.gsz <= 4u)) {
+    hipLaunchKernelGGL((twin_levels_kernel<false, 1, kTwinLvG, true>), grid, dim3(kBlock), 0, s, g, a);
+  } else if (rw == 2 && !(a.gsz && a.gsz <= 4u)) {
+    hipLaunchKernelGGL((twin_levels_kernel<true, 1, kTwinLvG, true>), grid, dim3(kBlock), 0, s, g, a);
+  } else if (a.gsz && a.gsz <= 4u) {
     OSPF_TWIN_LV(4u)
   } else {
     OSPF_TWIN_LV(kTwinLvG)
