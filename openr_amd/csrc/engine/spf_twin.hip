@@ -864,10 +864,14 @@ __global__ void __launch_bounds__(kBlock) twin_levels_kernel(DevGraph g, TwinLvP
       d.sum_dist += s_d[w][tid][1];
       d.hash += s_d[w][tid][2];
     }
-    ospf_digest* o = a.lev_digest + s_own[tid];  // zeroed by twin_zero_kernel
-    atomicAdd((unsigned long long*)&o->reached, (unsigned long long)d.reached);
-    atomicAdd((unsigned long long*)&o->sum_dist, (unsigned long long)d.sum_dist);
-    atomicAdd((unsigned long long*)&o->hash, (unsigned long long)d.hash);
+    ospf_digest* o = a.lev_digest + s_own[tid];
+    if (a.parts == 1) {  // the root's only block: stored (no zeroing launch before)
+      *o = d;
+    } else {  // zeroed by twin_zero_kernel
+      atomicAdd((unsigned long long*)&o->reached, (unsigned long long)d.reached);
+      atomicAdd((unsigned long long*)&o->sum_dist, (unsigned long long)d.sum_dist);
+      atomicAdd((unsigned long long*)&o->hash, (unsigned long long)d.hash);
+    }
   }
 }
 
@@ -933,7 +937,8 @@ hipError_t launch_twin_levels(const DevGraph& g, const TwinLvPlan& a0, hipStream
   const uint32_t want = be ? (uint32_t)std::max(1, atoi(be)) : 2048u;  // (4096: +0.05 ms at F100k)
   if (!a.parts)
     a.parts = std::max(1u, std::min(std::max(1u, nchunks / 8u), want / std::max(1u, a.ngroups)));
-  if (a.lev_digest)
+  // (one part per group: each root's digest is stored by its block, no zeroing)
+  if (a.lev_digest && a.parts > 1)
     hipLaunchKernelGGL(twin_zero_kernel, dim3((a.n + 255u) / 256u), dim3(256), 0, s, a.rinfo, a.n,
                        a.lev_digest);
   // (OSPF_TWIN_PREFETCH=1: the software-pipelined variant, 3 waves per SIMD;
