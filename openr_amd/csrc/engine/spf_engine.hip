@@ -49,8 +49,16 @@ hipError_t dev_malloc(ospf_ctx* c, void** p, size_t bytes) {
   hipError_t e = hipMalloc(p, bytes);
   if (e != hipSuccess && c && !c->sweep_pool.empty()) {  // the pooled blocks back first
     (void)hipGetLastError();
+    // a rare, slow path (hipFree of pooled row blocks): said on stderr, so a
+    // stall in a caller's timing can be traced to it
+    const auto t0 = std::chrono::steady_clock::now();
+    const size_t nb = c->sweep_pool.size(), pb = c->sweep_pool_bytes;
     pool_release(c);
     e = hipMalloc(p, bytes);
+    fprintf(stderr, "ospf: hipMalloc of %zu B failed: released %zu pooled sweep blocks (%.2f GB) in %.1f ms, retry %s\n",
+            bytes, nb, pb / 1e9,
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
+            e == hipSuccess ? "ok" : "failed");
   }
   if (e != hipSuccess) {
     (void)hipGetLastError();
