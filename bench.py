@@ -590,7 +590,6 @@ def sweep_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, 
                       if tr else None})
     dom = max(units, key=lambda u: u["isolated_launch_ms"])
     step_s = dt / args.steps
-    probe = store_probe(eng, V, dom, args) if not args.no_probe else None
     roofline = {
         "bound": "hbm", "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": dom["frac"], "traffic": dom["traffic"], "kernel": dom["kernel"],
@@ -608,12 +607,6 @@ def sweep_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, 
                 "sweep's compulsory bytes / ms_per_step. traffic = measured HBM bytes per launch "
                 "(rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/<round>/pmc_traffic.json)",
     }
-    if probe:
-        roofline["store_probe"] = probe
-        best = max(probe.get("stream_GBs") or 0.0, probe.get("rows_chunk_GBs") or 0.0,
-                   probe.get("rows_group_GBs") or 0.0)
-        if best > 0:
-            roofline["frac_of_box_store_rate"] = round(dom["achieved"] / best, 4)
     cfg = {"mode": sw.mode, "hip_graph": sw.hip_graph, "roots_this_rank": n,
            "rows_this_rank": sw.n_rows, "device_bytes": sw.device_bytes,
            "closure_over_roots": round(sw.n_rows / max(1, n), 4),
@@ -640,6 +633,16 @@ def sweep_main(args, eng, csr, names, stream, desc, V, E, world, rank, dist_on, 
         "total_ms": round((t3 - t1) * 1e3, 1),
         "note": "a new graph version: ospf_sweep_create(OSPF_SWEEP_DEFER) + the first (eager, "
                 "no HIP graph) run, as odl::LinkState::prefetchAllSources pays it"}
+    # the store probe after the first-sweep record: its 67 GB buffer freed just
+    # before that record had stalled the deferred sweep's first allocation by
+    # ~3.7 s on some boxes (profiles/r06/f4_first_run_check)
+    probe = store_probe(eng, V, dom, args) if not args.no_probe else None
+    if probe:
+        roofline["store_probe"] = probe
+        best = max(probe.get("stream_GBs") or 0.0, probe.get("rows_chunk_GBs") or 0.0,
+                   probe.get("rows_group_GBs") or 0.0)
+        if best > 0:
+            roofline["frac_of_box_store_rate"] = round(dom["achieved"] / best, 4)
     if args.ab:
         roofline["ab"] = ab_sweeps(args, eng, mode, part, n_parts, main_s, step_digest, sw_roots)
     if K > 1:  # one part per rank of a K x N partition: the parts' roots, not V
