@@ -529,6 +529,7 @@ struct TwinArgs {
   uint32_t* dist;
   uint32_t dpitch;        // 0: V
   uint32_t npitch;        // next-hop row pitch in words (0: V * W)
+  uint32_t bsearch;       // set by the launcher: OSPF_TWIN4_BSEARCH (A/B)
   // twin_levels_kernel: the roots' own rows at pos[root]
 };
 hipError_t launch_nh_derive_twin(const DevGraph& g, const TwinArgs& a, hipStream_t s);

@@ -431,6 +431,9 @@ __global__ void __launch_bounds__(kBlock) nh_twin4_kernel(DevGraph g, TwinArgs a
   const size_t npitch = a.npitch ? a.npitch : (size_t)V * W;
   const bool vec = (V & 3u) == 0 && (dpitch & 3u) == 0 && (npitch & 3u) == 0;
   uint64_t h = 0;
+  // members' positions: a cursor over the ascending neighbour list (the
+  // wave's chunks ascend), its next position cached in a register
+  uint32_t ncur = 0, nnx = K ? T.nb[0] : kInf;
   constexpr uint32_t kPre = 3;
   // KD: the 4 nodes' digest keys ride in the same ring (their L2 latency
   // was exposed at the digest terms of every chunk)
@@ -540,16 +543,31 @@ __global__ void __launch_bounds__(kBlock) nh_twin4_kernel(DevGraph g, TwinArgs a
     __builtin_amdgcn_wave_barrier();
     // members' own positions in this chunk, a lane per neighbour
     {
-      uint32_t lo = 0, hi = K;
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (T.nb[mid] < c0) lo = mid + 1; else hi = mid;
-      }
-      uint32_t end = lo;
-      hi = K;
-      while (end < hi) {
-        const uint32_t mid = (end + hi) >> 1;
-        if (T.nb[mid] < c0 + 256u) end = mid + 1; else hi = mid;
+      uint32_t lo, end;
+      if (a.bsearch) {
+        uint32_t hi = K;
+        lo = 0;
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (T.nb[mid] < c0) lo = mid + 1; else hi = mid;
+        }
+        end = lo;
+        hi = K;
+        while (end < hi) {
+          const uint32_t mid = (end + hi) >> 1;
+          if (T.nb[mid] < c0 + 256u) end = mid + 1; else hi = mid;
+        }
+      } else {
+        while (nnx < c0) {
+          ++ncur;
+          nnx = ncur < K ? T.nb[ncur] : kInf;
+        }
+        lo = ncur;
+        while (nnx < c0 + 256u) {
+          ++ncur;
+          nnx = ncur < K ? T.nb[ncur] : kInf;
+        }
+        end = ncur;
       }
       for (uint32_t k = lo + lane; k < end; k += 64u) {
         const uint32_t sk = T.cid[k];
@@ -886,6 +904,8 @@ hipError_t launch_nh_derive_twin(const DevGraph& g, const TwinArgs& a0, hipStrea
   TwinArgs a = a0;
   if (a.n == 0) return hipSuccess;
   if (a.W == 0 || a.W > 4) return hipErrorInvalidValue;
+  // members' positions by binary search per chunk (OSPF_TWIN4_BSEARCH; read per launch)
+  a.bsearch = getenv("OSPF_TWIN4_BSEARCH") ? 1u : 0u;
   a.tiles = (g.V + 1023u) / 1024u;
   if (!a.ctiles) a.ctiles = a.tiles;  // one block per root: the slot setup once
   a.ctiles = std::max(1u, std::min(a.tiles, a.ctiles));
